@@ -1,0 +1,81 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if REPO not in sys.path:
+    sys.path.insert(0, REPO)
+sys.dont_write_bytecode = True
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI)")
+    config.addinivalue_line("markers", "ref: needs /root/reference (build container only)")
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return os.path.join(REPO, "tests", "golden")
+
+
+@pytest.fixture(scope="session")
+def golden_core(golden_dir):
+    import numpy as np
+    return dict(np.load(os.path.join(golden_dir, "golden_core.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_analyzers(golden_dir):
+    import numpy as np
+    return dict(np.load(os.path.join(golden_dir, "golden_analyzers.npz")))
+
+
+@pytest.fixture(scope="session")
+def golden_torch(golden_dir):
+    import numpy as np
+    return dict(np.load(os.path.join(golden_dir, "golden_torch.npz")))
+
+
+@pytest.fixture(scope="session")
+def kat(golden_dir):
+    import json
+    with open(os.path.join(golden_dir, "kat.json")) as f:
+        return json.load(f)
+
+
+def analyzer_case(an, i):
+    """Unpack analyzer case i from golden_analyzers.npz."""
+    nb = int(an["a%d_nb" % i])
+    keys = [str(k) for k in an["a%d_enc_keys" % i]]
+    vals = an["a%d_enc_vals" % i]
+    encs = {}
+    for k, v in zip(keys, vals):
+        bw, flags = k.split("_")
+        encs[(int(bw), int(flags[0]), int(flags[1]), int(flags[2]))] = tuple(v)
+    return dict(scheme=int(an["a%d_scheme" % i]), percentile=float(an["a%d_percentile" % i]),
+                batches=[an["a%d_b%d" % (i, k)] for k in range(nb)], encs=encs,
+                xleft=an["a%d_xleft" % i], pdf=an["a%d_pdf" % i])
+
+
+def per_channel_case(core, i):
+    p = "pc%d_" % i
+    return dict(x=core[p + "x"], outer=int(core[p + "outer"]), C=int(core[p + "C"]), K=int(core[p + "K"]),
+                encs=core[p + "encs"], table=core[p + "table"], y=core[p + "y"])
+
+
+def bits(a):
+    """Bit pattern view for bit-exact comparisons (NaN payloads compared as NaN-ness)."""
+    import numpy as np
+    a = np.asarray(a, dtype=np.float32)
+    b = a.view(np.uint32).copy()
+    b[np.isnan(a)] = 0x7FC00000
+    return b

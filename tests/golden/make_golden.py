@@ -1,0 +1,280 @@
+"""Generate the committed golden fixtures of tests/golden from the REFERENCE itself.
+
+Run in the build container only (it needs /root/reference):
+
+    python tests/golden/make_golden.py
+
+Sources of truth, in order:
+  * oracle/_ref/libdlq_ref.so -- the reference DlQuantization C++ compiled in place from
+    /root/reference (oracle/build_ref.sh). Produces every integer encoding, QDQ output,
+    histogram/PDF and analyzer encoding stored here.
+  * the reference's own known-answer tests (values copied with file:line into kat.json).
+  * the reference's Python (aimet_torch.v1.quantsim_straight_through_grad,
+    aimet_torch.v1.adaround.adaround_loss), imported read-only with bytecode writing off,
+    for the STE mask and the AdaRound round-loss/beta.
+  * torch CPU float32 ops in exactly the sequence of AimetTensorQuantizer.cpp:236-299 for the
+    per-channel encoding tables (that is what the reference executes on that path).
+
+The fixtures are data (inputs + expected outputs); no reference source text is stored.
+"""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+REF_ROOT = os.environ.get("AIMET_REFERENCE", "/root/reference")
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from oracle import ref as R  # noqa: E402
+
+EDGE = np.array([0.0, -0.0, np.nan, np.inf, -np.inf, 1e30, -1e30, 1e-40, -1e-40, 0.5, -0.5, 1.5, -2.5],
+                dtype=np.float32)
+
+
+def per_tensor_cases(rng):
+    xs, encs = [], []
+    for t in range(40):
+        x = (rng.standard_normal(2048) * rng.uniform(0.01, 30) + rng.uniform(-3, 3)).astype(np.float32)
+        x[:EDGE.size] = EDGE
+        mn, mx = sorted(rng.uniform(-8, 8, 2))
+        bw = int([8, 8, 8, 4, 16, 31, 32][t % 7])
+        if t % 5 == 0:
+            mn = -mx            # strict-symmetric detection branch (TensorQuantizationSim.cpp:70-73)
+        if t % 9 == 0:
+            mn = 0.0            # ReLU-like encodings
+        if t % 13 == 0:
+            mx = mn             # gated min == max
+        xs.append(x)
+        encs.append((mn, mx, bw))
+    # ties: values exactly on .5 quantization boundaries of a 1/255 grid
+    e = R.fill_encoding_info(8, -1.0, 1.0)
+    k = np.arange(-300, 300, dtype=np.float64)
+    xs.append(((k + 0.5) * e.delta).astype(np.float32)[:2048] if k.size >= 2048 else
+              np.resize(((k + 0.5) * e.delta).astype(np.float32), 2048))
+    encs.append((-1.0, 1.0, 8))
+    return np.stack(xs), np.array(encs, dtype=np.float64)
+
+
+def torch_channel_table(encs):
+    """AimetTensorQuantizer.cpp:236-299, CPU torch float32 ops, literally."""
+    C = len(encs)
+    ev = torch.tensor([e[0] for e in encs] + [e[1] for e in encs], dtype=torch.float32).view(2, C)
+    emin, emax = ev[0], ev[1]
+    steps = 2 ** int(encs[0][4]) - 1
+    if encs[0][0] == -encs[0][1]:
+        steps -= 1
+    zero = torch.zeros(1)
+    emin = torch.minimum(emin, zero)
+    emax = torch.maximum(emax, zero)
+    emax = torch.maximum(emax, emin + 1e-5)
+    delta = (emax - emin) / float(steps)
+    off = torch.round(emin / delta)
+    return torch.stack([emin, emax, delta, off]).numpy()
+
+
+def per_channel_cases(rng):
+    out = []
+    shapes = [(1, 64, 27), (1, 16, 9), (1, 3, 1), (2, 8, 33), (1, 300, 4), (4, 5, 6)]   # (outer, C, K)
+    for si, (outer, C, K) in enumerate(shapes):
+        x = (rng.standard_normal(outer * C * K) * rng.uniform(0.1, 3)).astype(np.float32)
+        x[:min(EDGE.size, x.size)] = EDGE[:min(EDGE.size, x.size)]
+        bw = 8 if si % 2 == 0 else 4
+        sym = si % 3 == 0
+        encs = []
+        for c in range(C):
+            a = R.Analyzer(0)
+            a.update(rng.standard_normal(64).astype(np.float32) * (c + 1) / C)
+            e = a.compute(bw, sym, False, False)
+            encs.append(e.as_tuple())
+        table = torch_channel_table(encs)
+        y = R.qdq_per_channel(x, C, K, table)
+        out.append(dict(x=x, outer=outer, C=C, K=K, encs=np.array(encs), table=table, y=y))
+    return out
+
+
+def analyzer_cases(rng):
+    cases = []
+    flagsets = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]
+    for scheme, ncase in ((0, 6), (1, 6), (3, 5), (4, 3)):
+        for t in range(ncase):
+            nb = 3
+            batches = []
+            for k in range(nb):
+                n = int(rng.integers(500, 1500))
+                x = (rng.standard_normal(n) * rng.uniform(0.05, 5) + rng.uniform(-2, 2)).astype(np.float32)
+                if t == 1:
+                    x = np.maximum(x, 0)                     # ReLU output: min == 0
+                if t == 2 and k == 0:
+                    x[:] = 0                                 # all-zero first batch (math_functions.cpp:254-259)
+                if t == 3:
+                    x[:7] = EDGE[2:9]                        # nan/inf/huge/denormal
+                batches.append(x)
+            a = R.Analyzer(scheme)
+            pct = 99.0 if (scheme == 3 and t % 2) else 100.0
+            if scheme == 3:
+                a.set_percentile(pct)
+            for x in batches:
+                a.update(x)
+            encs = {}
+            for bw in (8, 4, 16):
+                for fl in flagsets:
+                    encs["%d_%d%d%d" % ((bw,) + fl)] = a.compute(bw, *fl).as_tuple()
+            xl, pdf = a.histogram() if scheme != 0 else (np.zeros(0), np.zeros(0))
+            cases.append(dict(scheme=scheme, percentile=pct, batches=batches, encs=encs, xleft=xl, pdf=pdf))
+    return cases
+
+
+def tfe_kat_data():
+    exe = os.path.join(tempfile.mkdtemp(), "gen")
+    subprocess.run(["g++", "-O2", "-o", exe, os.path.join(HERE, "gen_mt19937_normal.cpp")], check=True)
+    path = exe + ".f32"
+    subprocess.run([exe, path], check=True)
+    return np.fromfile(path, dtype=np.float32)
+
+
+def reference_python():
+    """Import the reference's pure-Python STE and AdaRound-loss modules (read-only)."""
+    for p in ("TrainingExtensions/torch/src/python", "TrainingExtensions/common/src/python"):
+        sys.path.insert(0, os.path.join(REF_ROOT, p))
+    import aimet_torch.v1.quantsim_straight_through_grad as ste  # noqa
+    from aimet_torch.v1.adaround.adaround_loss import AdaroundLoss, AdaroundHyperParameters  # noqa
+    return ste, AdaroundLoss, AdaroundHyperParameters
+
+
+def main():
+    rng = np.random.default_rng(20251015)
+    R.lib()
+
+    # ---- per-tensor QDQ / quantize-only / encoding math -------------------------------
+    xs, encs = per_tensor_cases(rng)
+    qdq = np.stack([R.qdq_per_tensor(x, e[0], e[1], int(e[2])) for x, e in zip(xs, encs)])
+    q_u = np.stack([R.quantize_per_tensor(x, e[0], e[1], int(e[2]), False) for x, e in zip(xs, encs)])
+    q_s = np.stack([R.quantize_per_tensor(x, e[0], e[1], int(e[2]), True) for x, e in zip(xs, encs)])
+    fei = np.array([R.fill_encoding_info(int(e[2]), e[0], e[1]).as_tuple() for e in encs])
+
+    gce_in, gce_out = [], []
+    for _ in range(200):
+        mn, mx = rng.uniform(-50, 50, 2)
+        if rng.uniform() < 0.2:
+            mn = 0.0
+        if rng.uniform() < 0.1:
+            mx = np.inf
+        if rng.uniform() < 0.1:
+            mn = -np.inf
+        bw = int(rng.choice([4, 8, 16, 32]))
+        for sym, strict, un in [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]:
+            gce_in.append((bw, mn, mx, sym, strict, un))
+            gce_out.append(R.get_computed_encodings(bw, mn, mx, sym, strict, un).as_tuple())
+
+    pc = per_channel_cases(rng)
+    core = dict(pt_x=xs, pt_enc=encs, pt_qdq=qdq, pt_q_unsigned=q_u, pt_q_signed=q_s, pt_fill=fei,
+                gce_in=np.array(gce_in, dtype=np.float64), gce_out=np.array(gce_out, dtype=np.float64))
+    for i, c in enumerate(pc):
+        for k, v in c.items():
+            core["pc%d_%s" % (i, k)] = np.asarray(v)
+    core["pc_count"] = np.array(len(pc))
+    np.savez_compressed(os.path.join(HERE, "golden_core.npz"), **core)
+
+    # ---- analyzers (TF, TF-E, percentile, MSE) ------------------------------------------
+    an = {}
+    cases = analyzer_cases(rng)
+    for i, c in enumerate(cases):
+        an["a%d_scheme" % i] = np.array(c["scheme"])
+        an["a%d_percentile" % i] = np.array(c["percentile"], dtype=np.float32)
+        an["a%d_nb" % i] = np.array(len(c["batches"]))
+        for k, b in enumerate(c["batches"]):
+            an["a%d_b%d" % (i, k)] = b
+        an["a%d_xleft" % i] = c["xleft"]
+        an["a%d_pdf" % i] = c["pdf"]
+        keys = sorted(c["encs"])
+        an["a%d_enc_keys" % i] = np.array(keys)
+        an["a%d_enc_vals" % i] = np.array([c["encs"][k] for k in keys], dtype=np.float64)
+    an["count"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(HERE, "golden_analyzers.npz"), **an)
+
+    # ---- KATs from the reference test-suites ----------------------------------------------
+    kdata = tfe_kat_data()
+    a = R.Analyzer(1)
+    a.update(kdata)
+    kenc = a.compute(8, False, False, False)
+    kqdq = R.qdq_per_tensor(np.full(4, 5.0, np.float32), kenc.min, kenc.max, 8)[0]
+
+    ste, AdaroundLoss, AdaroundHyperParameters = reference_python()
+    g = torch.Generator().manual_seed(3)
+    sx = torch.randn(6, 5, generator=g) * 2
+    sg = torch.randn(6, 5, generator=g)
+    mins = torch.tensor([-1.0, -0.5, -2.0, -1.5, 0.0, -0.25]).tolist()
+    maxs = torch.tensor([1.0, 0.5, 2.0, 0.75, 1.0, 3.0]).tolist()
+    ste_pc = ste.compute_dloss_by_dx(sx, sg, mins, maxs, ch_axis=0)
+    ste_pt = ste.compute_dloss_by_dx(sx, sg, -1.25, 0.8, ch_axis=0)
+    np.savez_compressed(os.path.join(HERE, "golden_torch.npz"), ste_x=sx.numpy(), ste_g=sg.numpy(),
+                        ste_mins=np.array(mins, np.float32), ste_maxs=np.array(maxs, np.float32),
+                        ste_pc=ste_pc.numpy(), ste_pt=ste_pt.numpy(), tfe_kat_x=kdata)
+
+    np.random.seed(0)
+    alpha = torch.from_numpy(np.random.rand(1, 3, 12, 12))
+    hp = AdaroundHyperParameters(num_iterations=10000, reg_param=0.01, beta_range=(20, 2), warm_start=0.2)
+    rl = float(AdaroundLoss.compute_round_loss(alpha, hp, 8000))
+    beta = float(AdaroundLoss._compute_beta(10000, 8000, (20, 2), 0.2))
+
+    kat = {
+        "_sources": "values quoted from the reference test-suites (file:line per entry) plus the reference "
+                    "C++/Python re-run in the build container (make_golden.py)",
+        "qdq_sanity": {"src": "DlQuantization/test/TestTensorQuantizationSim.cpp:51-75",
+                       "x": [-0.5, -0.25, 0.0, 0.25, 0.5, 0.75], "min": -0.46, "max": 0.72, "bw": 8,
+                       "expected": [-0.45811754, -0.2498823, 0.0, 0.2498823, 0.49976459, 0.72188222],
+                       "tol": "EXPECT_FLOAT_EQ (4 ulp)"},
+        "qdq_gated_min": {"src": "TestTensorQuantizationSim.cpp:77-104", "x": [-0.5, -0.25, 0.0, 0.25, 0.5, 0.75],
+                          "min": 0.5, "max": 1.0, "bw": 8,
+                          "expected": [0.0, 0.0, 0.0, 0.25098041, 0.49803925, 0.74901962]},
+        "qdq_gated_equal": {"src": "TestTensorQuantizationSim.cpp:106-132",
+                            "x": [-0.5, -0.25, 0.0, 0.25, 0.5, 0.75], "min": 0.5, "max": 0.5, "bw": 8,
+                            "expected": [0.0, 0.0, 0.0, 0.24901962, 0.5, 0.5]},
+        "qdq_gated_max": {"src": "TestTensorQuantizationSim.cpp:134-159", "x": [-0.5, -0.25, 0.0, 0.25, 0.5, 0.75],
+                          "min": -0.5, "max": -0.1, "bw": 8,
+                          "expected": [-0.5, -0.24901962, 0.0, 0.0, 0.0, 0.0]},
+        "quantize_unsigned": {"src": "TestTensorQuantizationSim.cpp:161-185",
+                              "x": [-0.5, -0.25, 0.0, 0.25, 0.5, 0.75], "min": -0.46, "max": 0.72, "bw": 8,
+                              "shift": False, "expected": [0, 45, 99, 153, 207, 255]},
+        "quantize_signed": {"src": "TestTensorQuantizationSim.cpp:212-236",
+                            "x": [-0.5, -0.25, 0.0, 0.25, 0.5, 0.75], "min": -0.46, "max": 0.72, "bw": 8,
+                            "shift": True, "expected": [-128, -83, -29, 25, 79, 127]},
+        "tfe_normal": {"src": "DlQuantization/test/TestTensorQuantizer.cpp:89-134 (data: golden_torch.npz tfe_kat_x)",
+                       "expected_min": -6.52711, "expected_max": 8.88412, "expected_qdq5": 5.0162, "tol": 0.001,
+                       "ref_encoding": list(kenc.as_tuple()), "ref_qdq5": float(kqdq)},
+        "tfe_all_zero": {"src": "DlQuantization/test/TestTfEnhancedEncodingAnalyzer.cpp:176-196",
+                         "n": 6000, "expected_min": -1.00392, "expected_max": 0.996078, "expected_offset": -128,
+                         "tol": 0.0001},
+        "per_channel_symmetric": {
+            "src": "TrainingExtensions/torch/test/python/test_per_channel_quantization.py:66-102",
+            "encodings": [[-3.84, 3.81, 0.03, -128, 8]] * 3 + [[-6.4, 6.35, 0.05, -128, 8]],
+            "x": [[-7, -5, -3, 0, .1, 2.5]] * 4,
+            "expected": [[-3.84, -3.84, -3, 0, .089999996, 2.49]] * 3 + [[-6.4, -5, -3, 0, .1, 2.5]],
+            "atol": 1e-5},
+        "per_channel_asymmetric": {
+            "src": "TrainingExtensions/torch/test/python/test_per_channel_quantization.py:104-141",
+            "encodings": [[-2.9999934, 1.9999956, 0.0196078, -153, 8]] * 3 + [[-5.995262, 2.404693, 0.032941, -182, 8]],
+            "x": [[-7, -5, -3, 0, .1, 2.5]] * 4,
+            "expected": [[-3.0, -3.0, -3.0, 0, .098, 2.0]] * 3 + [[-5.9953, -5.0070, -2.9976, 0, .09888, 2.4047]],
+            "atol": 1e-4},
+        "adaround_round_loss": {"src": "TrainingExtensions/torch/test/python/test_adaround_loss.py:83-100",
+                                "seed": 0, "shape": [1, 3, 12, 12], "reg_param": 0.01, "beta_range": [20, 2],
+                                "warm_start": 0.2, "num_iterations": 10000, "cur_iter": 8000,
+                                "expected": 4.266156963161077, "places": 5, "ref_value": rl},
+        "adaround_beta": {"src": "TrainingExtensions/torch/test/python/test_adaround_loss.py:102-110",
+                          "expected": 4.636038969321072, "ref_value": beta},
+    }
+    with open(os.path.join(HERE, "kat.json"), "w") as f:
+        json.dump(kat, f, indent=1)
+    print("golden fixtures written to", HERE)
+
+
+if __name__ == "__main__":
+    main()
