@@ -1,0 +1,136 @@
+"""ctypes binding of libaimet_amd.so (include/aimet_amd.h).
+
+The library is the only compute path: there is no CPU or PyTorch fallback. If it is missing or
+fails to load, every entry point raises immediately (`NativeLibraryError`).
+"""
+import ctypes
+import os
+import subprocess
+
+import torch  # noqa: F401  -- load torch's HIP runtime first so libaimet_amd binds to the same one
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libaimet_amd.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+AIMET_OK = 0
+AIMET_ERR_INVALID_ARGUMENT = -1
+AIMET_ERR_RUNTIME = -2
+AIMET_ERR_HIP = -3
+
+
+class NativeLibraryError(RuntimeError):
+    """libaimet_amd.so is missing or unusable; aimet_amd has no fallback path."""
+
+
+class HipError(RuntimeError):
+    """A HIP runtime call inside libaimet_amd failed."""
+
+
+class TfEncodingC(ctypes.Structure):
+    _fields_ = [("min", ctypes.c_double), ("max", ctypes.c_double), ("delta", ctypes.c_double),
+                ("offset", ctypes.c_double), ("bw", ctypes.c_int32)]
+
+
+_fp = ctypes.POINTER(ctypes.c_float)
+_dp = ctypes.POINTER(ctypes.c_double)
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_int = ctypes.c_int
+_enc_p = ctypes.POINTER(TfEncodingC)
+
+# name -> argtypes (restype is int status unless listed in _RESTYPES)
+_PROTOTYPES = {
+    "aimet_last_error": [],
+    "aimet_version": [],
+    "aimet_device_count": [],
+    "aimet_get_computed_encodings": [_i32, ctypes.c_double, ctypes.c_double, _int, _int, _int, _enc_p],
+    "aimet_fill_encoding_info": [_i32, ctypes.c_double, ctypes.c_double, _enc_p],
+    "aimet_compute_partial_encoding": [_i32, _enc_p, _int, _int, _int],
+    "aimet_encoding_from_minmax": [ctypes.c_double, ctypes.c_double, _i32, _int, _int, _int, _enc_p],
+    "aimet_encoding_from_histogram": [_int, _int, _int, ctypes.c_float, ctypes.c_double, _dp, ctypes.c_float, _i32,
+                                      _int, _int, _int, _enc_p],
+    "aimet_qdq_per_tensor": [_vp, _vp, _i64, _enc_p, _int, ctypes.c_uint64, _vp],
+    "aimet_quantize_per_tensor": [_vp, _vp, _i64, _enc_p, _int, _int, ctypes.c_uint64, _vp],
+    "aimet_per_channel_table": [_enc_p, _i64, _vp, _vp],
+    "aimet_make_delta_offset": [_enc_p, _i64, _vp, _vp],
+    "aimet_qdq_per_channel": [_vp, _vp, _i64, _i64, _i64, _vp, _int, ctypes.c_uint64, _vp],
+    "aimet_ste_backward": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp],
+    "aimet_ste_backward_per_tensor": [_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, _vp],
+    "aimet_tq_create": [_int, _i64, _int, ctypes.POINTER(_vp)],
+    "aimet_tq_destroy": [_vp],
+    "aimet_tq_reset_encoding_stats": [_vp, _vp],
+    "aimet_tq_set_percentile_value": [_vp, ctypes.c_float],
+    "aimet_tq_get_percentile_value": [_vp, _fp],
+    "aimet_tq_update_stats": [_vp, _vp, _i64, _i64, _i64, _vp],
+    "aimet_tq_batch_minmax": [_vp, _vp, _i64, _i64, _i64, _vp],
+    "aimet_tq_fold_minmax": [_vp, _vp],
+    "aimet_tq_batch_histogram": [_vp, _vp, _i64, _i64, _i64, _vp],
+    "aimet_tq_fold_histogram": [_vp, _i64, _vp],
+    "aimet_tq_minmax_buffer": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_i64)],
+    "aimet_tq_counts_buffer": [_vp, ctypes.POINTER(_vp), ctypes.POINTER(_i64)],
+    "aimet_tq_bind_exchange": [_vp, _vp, _vp],
+    "aimet_tq_mark_stats_updated": [_vp],
+    "aimet_tq_get_encoding": [_vp, ctypes.c_uint32, _int, _int, _int, _enc_p, ctypes.POINTER(_int), _vp],
+    "aimet_tq_get_stats_histogram": [_vp, _i64, _dp, _dp, ctypes.POINTER(_int), _vp],
+    "aimet_tq_num_channels": [_vp, ctypes.POINTER(_i64)],
+    "aimet_tq_quant_scheme": [_vp, ctypes.POINTER(_int)],
+    "aimet_adaround_forward": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _int, _vp],
+    "aimet_adaround_backward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, ctypes.c_float,
+                                ctypes.c_float, _vp, _vp],
+}
+_RESTYPES = {"aimet_last_error": ctypes.c_char_p, "aimet_version": ctypes.c_char_p}
+
+EXPORTED_SYMBOLS = tuple(_PROTOTYPES)
+
+_lib = None
+_load_error = None
+
+
+def build(verbose=False):
+    """Compile libaimet_amd.so for gfx950 with hipcc (make -C aimet_amd/csrc)."""
+    jobs = str(min(16, os.cpu_count() or 4))
+    subprocess.run(["make", "-s", "-j", jobs, "-C", CSRC], check=True,
+                   stdout=None if verbose else subprocess.DEVNULL)
+
+
+def load():
+    """Return the loaded library or raise NativeLibraryError (never falls back)."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise _load_error
+    if not os.path.exists(LIB_PATH):
+        _load_error = NativeLibraryError(
+            "aimet_amd: %s not found. Build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(hipcc --offload-arch=gfx950). There is no CPU fallback." % LIB_PATH)
+        raise _load_error
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:
+        _load_error = NativeLibraryError("aimet_amd: cannot load %s: %s" % (LIB_PATH, e))
+        raise _load_error from e
+    for name, args in _PROTOTYPES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    """Map a C-ABI status to the exception the reference's pybind layer would raise."""
+    if rc == AIMET_OK:
+        return
+    msg = load().aimet_last_error().decode(errors="replace")
+    if rc == AIMET_ERR_INVALID_ARGUMENT:
+        raise ValueError(msg)
+    if rc == AIMET_ERR_HIP:
+        raise HipError(msg)
+    raise RuntimeError(msg)
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args))

@@ -1,0 +1,116 @@
+// capi.cpp -- error state, device checks and the host encoding-math entry points of the C-ABI.
+#include <string>
+
+#include "encodings.hpp"
+
+namespace aimet_amd
+{
+
+namespace
+{
+thread_local std::string g_last_error;
+}
+
+void set_last_error(const std::string& msg)
+{
+    g_last_error = msg;
+}
+
+void require_device_ptr(const void* p, const char* what)
+{
+    if (p == nullptr)
+        throw InvalidArgument(std::string(what) + " pointer is null");
+    hipPointerAttribute_t attr;
+    hipError_t e = hipPointerGetAttributes(&attr, p);
+    if (e != hipSuccess)
+    {
+        (void) hipGetLastError();   // clear the sticky error of the failed query
+        throw InvalidArgument(std::string(what) +
+                              " is not device memory: aimet_amd has no CPU path (move the tensor to an MI355X)");
+    }
+    if (attr.type != hipMemoryTypeDevice && attr.type != hipMemoryTypeManaged)
+        throw InvalidArgument(std::string(what) +
+                              " is not device memory: aimet_amd has no CPU path (move the tensor to an MI355X)");
+}
+
+}   // namespace aimet_amd
+
+using namespace aimet_amd;
+
+extern "C" {
+
+const char* aimet_last_error(void)
+{
+    return g_last_error.c_str();
+}
+
+const char* aimet_version(void)
+{
+    return "aimet_amd 0.1.0 gfx950";
+}
+
+int aimet_device_count(void)
+{
+    int n  = 0;
+    int rc = guarded([&] { AIMET_HIP_CHECK(hipGetDeviceCount(&n)); });
+    return rc == AIMET_OK ? n : rc;
+}
+
+int aimet_get_computed_encodings(int32_t bw, double mn, double mx, int sym, int strict, int unsign,
+                                 aimet_tf_encoding* out)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(out != nullptr, "output is null");
+        *out = computed_encoding((int32_t) (uint8_t) bw, mn, mx, sym != 0, strict != 0, unsign != 0);
+    });
+}
+
+int aimet_fill_encoding_info(int32_t bw, double mn, double mx, aimet_tf_encoding* out)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(out != nullptr, "output is null");
+        *out = fill_encoding_info(bw, mn, mx);
+    });
+}
+
+int aimet_compute_partial_encoding(int32_t bw, aimet_tf_encoding* enc, int sym, int unsign, int strict)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(enc != nullptr, "encoding is null");
+        std::string err;
+        aimet_tf_encoding e = *enc;
+        if (!partial_encoding((int32_t) (uint8_t) bw, e, sym != 0, unsign != 0, strict != 0, err))
+        {
+            if (err.find("Cannot determine") != std::string::npos)
+                throw RuntimeError(err);
+            throw InvalidArgument(err);
+        }
+        *enc = e;
+    });
+}
+
+int aimet_encoding_from_minmax(double acc_min, double acc_max, int32_t bw, int sym, int strict, int unsign,
+                               aimet_tf_encoding* out)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(out != nullptr, "output is null");
+        *out = tf_encoding(acc_min, acc_max, (int32_t) (uint8_t) bw, sym != 0, strict != 0, unsign != 0);
+    });
+}
+
+int aimet_encoding_from_histogram(int scheme, int initialized, int stats_updated, float hist_min, double bucket_size,
+                                  const double* pdf, float percentile, int32_t bw, int sym, int strict, int unsign,
+                                  aimet_tf_encoding* out)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(out != nullptr, "output is null");
+        AIMET_REQUIRE(scheme == AIMET_QUANTIZATION_TF_ENHANCED || scheme == AIMET_QUANTIZATION_PERCENTILE ||
+                          scheme == AIMET_QUANTIZATION_MSE,
+                      "histogram encodings exist for TF-Enhanced, percentile and MSE only");
+        AIMET_REQUIRE(!initialized || pdf != nullptr, "pdf is null");
+        *out = histogram_encoding(scheme, initialized != 0, stats_updated != 0, hist_min, bucket_size, pdf, percentile,
+                                  (int32_t) (uint8_t) bw, sym != 0, strict != 0, unsign != 0);
+    });
+}
+
+}   // extern "C"

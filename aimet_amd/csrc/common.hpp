@@ -1,0 +1,189 @@
+// common.hpp -- shared host/device helpers of the MI355X DlQuantization core.
+//
+// Numerics contract: every kernel reproduces the reference CPU arithmetic of
+// DlQuantization bit for bit. That rules out fast-math: the library is compiled with
+// -ffp-contract=off and correctly-rounded fp32 division (the reference GPU build used
+// --use_fast_math, which is why its GPU output never matched its own CPU output).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+#include "aimet_amd.h"
+
+namespace aimet_amd
+{
+
+constexpr int kPdfSize     = 512;   // math_functions.hpp:80 PDF_SIZE
+constexpr int kBlock       = 256;   // 4 waves of 64
+constexpr int kMaxStreamBlocks = 2048;  // 256 CUs x 8 resident blocks (grid-stride beyond)
+
+// ------------------------------------------------------------------------------------------
+// Error plumbing: C++ exceptions are turned into status codes at the C-ABI.
+// ------------------------------------------------------------------------------------------
+struct InvalidArgument : std::invalid_argument
+{
+    using std::invalid_argument::invalid_argument;
+};
+struct RuntimeError : std::runtime_error
+{
+    using std::runtime_error::runtime_error;
+};
+struct HipError : std::runtime_error
+{
+    using std::runtime_error::runtime_error;
+};
+
+void set_last_error(const std::string& msg);
+
+#define AIMET_HIP_CHECK(expr)                                                                            \
+    do                                                                                                   \
+    {                                                                                                    \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess)                                                                            \
+            throw ::aimet_amd::HipError(std::string(#expr) + ": " + hipGetErrorString(e_) + " (" +      \
+                                        __FILE__ + ":" + std::to_string(__LINE__) + ")");                \
+    } while (0)
+
+#define AIMET_LAUNCH_CHECK() AIMET_HIP_CHECK(hipGetLastError())
+
+#define AIMET_REQUIRE(cond, msg)                                                                         \
+    do                                                                                                   \
+    {                                                                                                    \
+        if (!(cond))                                                                                     \
+            throw ::aimet_amd::InvalidArgument(msg);                                                     \
+    } while (0)
+
+template <class F>
+int guarded(F&& f)
+{
+    try
+    {
+        f();
+        return AIMET_OK;
+    }
+    catch (const InvalidArgument& e)
+    {
+        set_last_error(e.what());
+        return AIMET_ERR_INVALID_ARGUMENT;
+    }
+    catch (const HipError& e)
+    {
+        set_last_error(e.what());
+        return AIMET_ERR_HIP;
+    }
+    catch (const std::exception& e)
+    {
+        set_last_error(e.what());
+        return AIMET_ERR_RUNTIME;
+    }
+    catch (...)
+    {
+        set_last_error("unknown error");
+        return AIMET_ERR_RUNTIME;
+    }
+}
+
+inline hipStream_t as_stream(void* s)
+{
+    return reinterpret_cast<hipStream_t>(s);
+}
+
+// Reject host pointers: there is no CPU compute path in this library.
+void require_device_ptr(const void* p, const char* what);
+
+inline int64_t ceil_div(int64_t a, int64_t b)
+{
+    return (a + b - 1) / b;
+}
+
+inline int stream_blocks(int64_t work_items, int64_t items_per_block)
+{
+    int64_t b = ceil_div(work_items, items_per_block);
+    if (b < 1)
+        b = 1;
+    if (b > kMaxStreamBlocks)
+        b = kMaxStreamBlocks;
+    return (int) b;
+}
+
+// ------------------------------------------------------------------------------------------
+// Fast 32-bit division by a runtime-invariant divisor (dividends < 2^31).
+// ------------------------------------------------------------------------------------------
+struct FastDiv
+{
+    uint32_t d, mul, shr;
+    FastDiv() = default;
+    explicit FastDiv(uint32_t divisor) : d(divisor), mul(0), shr(0)
+    {
+        if (d > 1)
+        {
+            uint32_t l = 32 - __builtin_clz(d - 1);   // ceil(log2(d))
+            uint32_t p = 31 + l;
+            mul        = (uint32_t) (((1ull << p) + d - 1) / d);
+            shr        = p - 32;
+        }
+    }
+    __device__ __forceinline__ uint32_t div(uint32_t n) const
+    {
+        return d == 1 ? n : (__umulhi(n, mul) >> shr);
+    }
+};
+
+// ------------------------------------------------------------------------------------------
+// Reference element arithmetic (trim_functions.cpp:140-171, x86-64 glibc semantics).
+// ------------------------------------------------------------------------------------------
+
+// glibc fminf/fmaxf (x86-64): a NaN operand yields the other operand; otherwise
+// minss/maxss, i.e. the SECOND operand on ties (matters for +-0).
+__device__ __forceinline__ float glibc_fminf(float x, float y)
+{
+    return (x < y || __builtin_isnan(y)) ? x : y;
+}
+__device__ __forceinline__ float glibc_fmaxf(float x, float y)
+{
+    return (x > y || __builtin_isnan(y)) ? x : y;
+}
+
+struct QdqParams
+{
+    float min, max, delta, offset;
+};
+
+// quantizeValueCpu (ROUND_NEAREST): round(clamp(x)/delta - offset), half away from zero.
+__device__ __forceinline__ float quantize_nearest(float x, const QdqParams& p)
+{
+    float o = glibc_fmaxf(glibc_fminf(x, p.max), p.min);
+    o       = o / p.delta - p.offset;
+    return __builtin_roundf(o);
+}
+
+// ROUND_STOCHASTIC: floor(v + U[0,1)). The reference draws rand() (CPU) or curand seeded by
+// clock() (GPU) -- neither reproducible, so only the distribution is specified.
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx)
+{
+    uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+    z          = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z          = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    return (float) (uint32_t) (z >> 40) * (1.0f / 16777216.0f);
+}
+
+__device__ __forceinline__ float quantize_stochastic(float x, const QdqParams& p, uint64_t seed, uint64_t idx)
+{
+    float o = glibc_fmaxf(glibc_fminf(x, p.max), p.min);
+    o       = o / p.delta - p.offset;
+    return __builtin_floorf(o + uniform01(seed, idx));
+}
+
+// dequantizeValueCpu
+__device__ __forceinline__ float dequantize(float q, const QdqParams& p)
+{
+    return p.delta * (q + p.offset);
+}
+
+}   // namespace aimet_amd

@@ -1,0 +1,488 @@
+// encodings.cpp -- host-side encoding math of the DlQuantization analyzers.
+//
+// These are O(512) computations per channel on statistics already reduced on the device
+// (stats.hip). They reproduce the reference arithmetic exactly, including its float/double
+// mix (the analyzers are instantiated with DTYPE = float) and libstdc++'s std::min/std::max
+// tie rules; the file is compiled with -ffp-contract=off like the reference (x86-64, no FMA).
+//
+//   getComputedEncodings           quantization_utils.cpp:58-143
+//   gateMinMax / fillEncodingInfo  quantization_utils.cpp:145-156, TensorQuantizationSim.cpp:62-92
+//   partial encodings              quantization_utils.cpp:158-228, TensorQuantizer.cpp:323-341
+//   TF                             TfEncodingAnalyzer.cpp:80-101
+//   TF-Enhanced                    TfEnhancedEncodingAnalyzer.cpp:78-392
+//   Percentile                     PercentileEncodingAnalyzer.cpp:78-190, math_functions.cpp:404-439
+//   MSE                            MseEncodingAnalyzer.cpp:79-264
+#include "encodings.hpp"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <limits>
+#include <numeric>
+#include <utility>
+
+namespace aimet_amd
+{
+
+namespace
+{
+constexpr double kGateEps  = 1e-5;   // quantization_utils.hpp:51 EPSILON
+constexpr double kMinRange = 0.01;   // TfEncodingAnalyzer.h:81 / TfEnhancedEncodingAnalyzer.h:105
+constexpr float kGammaTfe  = 3.0f;   // TfEnhancedEncodingAnalyzer.h:102 (DTYPE)
+constexpr float kFltLowest = std::numeric_limits<float>::lowest();
+constexpr float kFltMax    = std::numeric_limits<float>::max();
+
+inline double sq(double v)
+{
+    return v * v;   // std::pow(v, 2) folds to v*v in the reference build (-O3)
+}
+
+aimet_tf_encoding make_enc(double mn, double mx, double d, double o, int32_t bw)
+{
+    aimet_tf_encoding e;
+    e.min    = mn;
+    e.max    = mx;
+    e.delta  = d;
+    e.offset = o;
+    e.bw     = bw;
+    return e;
+}
+
+}   // namespace
+
+aimet_tf_encoding computed_encoding(int32_t bw, double mn, double mx, bool sym, bool strict, bool unsign)
+{
+    double steps = std::pow(2.0, bw) - 1;
+    if (sym && strict)
+        steps -= 1;
+    if (std::isinf(mn))
+        mn = kFltLowest;
+    if (std::isinf(mx))
+        mx = kFltMax;
+    aimet_tf_encoding e = make_enc(0, 0, 0, 0, bw);
+    if (sym && (mn < 0.0 || !unsign))
+    {
+        double absmax        = std::max(std::abs(mx), std::abs(mn));
+        unsigned int posSteps = (unsigned int) std::floor(steps / 2);
+        e.delta              = absmax / posSteps;
+        e.offset             = -std::ceil(steps / 2);
+        e.min                = std::max(e.offset * e.delta, (double) kFltLowest);
+        e.max                = std::min(e.delta * posSteps, (double) kFltMax);
+        return e;
+    }
+    e.delta = (mx - mn) / steps;
+    if (!(mn < 0 && mx > 0))
+    {
+        // one end is zero: 0 is already on the grid
+        e.offset = std::round(mn / e.delta);
+        e.min    = mn;
+        e.max    = mx;
+        return e;
+    }
+    double zeroCode = std::round(-mn / e.delta);
+    zeroCode        = std::min(steps, std::max(0.0, zeroCode));
+    e.offset        = -zeroCode;
+    double lo       = e.delta * e.offset;
+    e.min           = (lo >= (double) kFltLowest && lo <= (double) kFltMax) ? lo : (double) kFltLowest;
+    e.max           = mx - mn + e.min;
+    if (e.max > (double) kFltMax)
+        e.max = kFltMax;
+    return e;
+}
+
+void gate_min_max(double& mn, double& mx)
+{
+    mn = std::min(mn, 0.0);
+    mx = std::max(mx, 0.0);
+    mx = std::max(mx, mn + kGateEps);
+}
+
+aimet_tf_encoding fill_encoding_info(int32_t bw, double mn, double mx)
+{
+    gate_min_max(mn, mx);
+    double steps = std::pow(2.0, (uint8_t) bw) - 1;
+    if (mn == -mx)
+        steps -= 1;   // strict symmetric: 2^bw - 2 steps
+    double delta  = (mx - mn) / steps;
+    double offset = std::round(mn / delta);
+    double lo     = offset * delta;
+    return make_enc(lo, delta * steps + lo, delta, offset, (uint8_t) bw);
+}
+
+bool partial_encoding(int32_t bw, aimet_tf_encoding& e, bool sym, bool unsign, bool strict, std::string& err)
+{
+    if (e.min == 0 && e.max == 0)
+    {
+        // computeMinMaxRangeFromDeltaOffset
+        if (e.bw == 0)
+            return err = "Encodings must have a valid non-zero bitwidth", false;
+        if (e.delta == 0 && e.offset > 0)
+            return err = "Encoding must have a valid non-zero delta/offset if min and max are zero", false;
+        double steps = std::pow(2.0, (uint8_t) bw) - 1;
+        if (sym && strict)
+            steps -= 1;
+        e.min = e.offset * e.delta;
+        if (sym && (e.min < 0.0 || !unsign))
+            e.max = e.delta * std::floor(steps / 2);
+        else
+            e.max = e.delta * steps + e.min;
+        if (e.max - e.min < kGateEps)
+            gate_min_max(e.min, e.max);
+        return true;
+    }
+    if (e.delta == 0)
+    {
+        // computeDeltaAndOffsetFromMinMax
+        if (e.bw == 0)
+            return err = "Encodings must have a valid non-zero bitwidth", false;
+        if (e.delta != 0 && e.offset != 0)
+            return err = "Encoding delta and offset must be zero to use this function", false;
+        double mn = e.min, mx = e.max;
+        e         = computed_encoding((uint8_t) bw, mn, mx, sym, strict, unsign);
+        e.min     = mn;
+        e.max     = mx;
+        return true;
+    }
+    err = "Cannot determine how to compute partial encoding";
+    return false;
+}
+
+void per_channel_table_host(const aimet_tf_encoding* encs, int64_t C, float* table)
+{
+    // AimetTensorQuantizer.cpp:262-299 executed as float32 torch ops on the CPU:
+    // minimum/maximum propagate NaN, scalars are rounded to float, at::round is half-to-even.
+    auto tmin = [](float a, float b) { return (std::isnan(a) || std::isnan(b)) ? NAN : (a < b ? a : b); };
+    auto tmax = [](float a, float b) { return (std::isnan(a) || std::isnan(b)) ? NAN : (a > b ? a : b); };
+    double steps = std::pow(2.0, encs[0].bw) - 1;
+    if (encs[0].min == -encs[0].max)
+        steps -= 1;
+    const float fsteps = (float) steps;
+    const float eps    = (float) 1e-5;
+    for (int64_t c = 0; c < C; ++c)
+    {
+        float mn = tmin((float) encs[c].min, 0.0f);
+        float mx = tmax((float) encs[c].max, 0.0f);
+        mx       = tmax(mx, mn + eps);
+        float d  = (mx - mn) / fsteps;
+        table[c]         = mn;
+        table[C + c]     = mx;
+        table[2 * C + c] = d;
+        table[3 * C + c] = std::nearbyint(mn / d);
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Histogram analyzers. `HistView` is the reconstructed PDF of one channel:
+// xLeft[i] = (double)hist_min + (double)i * bucket_size (InitializePdf, signed branch).
+// ---------------------------------------------------------------------------------------------
+namespace
+{
+
+struct HistView
+{
+    float hist_min;
+    double bucket;
+    const double* pdf;
+    double xl(int i) const
+    {
+        return (double) hist_min + (double) i * bucket;
+    }
+};
+
+// findOriginalRange<float> (== TfEnhanced::_findRangeOfAggregateStats)
+std::pair<float, float> observed_range(const HistView& h)
+{
+    float lo = (float) h.xl(0), hi = (float) h.xl(kPdfSize - 1);
+    int first = -1, last = -1;
+    for (int i = 0; i < kPdfSize; ++i)
+        if (h.pdf[i] > 0)
+        {
+            first = i;
+            break;
+        }
+    for (int i = kPdfSize - 1; i > 0; --i)
+        if (h.pdf[i] > 0)
+        {
+            last = i;
+            break;
+        }
+    if (first >= 0)
+        lo = (float) h.xl(first);
+    if (last >= 0)
+        hi = (float) h.xl(last);
+    lo = std::min(lo, 0.0f);
+    hi = std::max(hi, 0.0f);
+    hi = std::max(hi, lo + (float) kMinRange);
+    return {lo, hi};
+}
+
+aimet_tf_encoding unseen_or_zero(bool stats_updated, int32_t bw, float steps)
+{
+    // "we have seen all zero data": a [-1, 1] encoding (TfEnhancedEncodingAnalyzer.cpp:86-99)
+    if (!stats_updated)
+        return make_enc(0, 0, 0, 0, 0);
+    int isteps   = (int) steps;
+    double delta = (1.0 - (-1.0)) / isteps;
+    double off   = std::floor(-1.0 / delta);
+    double lo    = off * delta;
+    return make_enc(lo, lo + isteps * delta, delta, off, bw);
+}
+
+// ---- TF-Enhanced --------------------------------------------------------------------------
+struct Candidate
+{
+    float delta;
+    int offset;
+};
+
+double tfe_cost(const HistView& h, int32_t bw, float delta, int offset)
+{
+    const float lo       = delta * offset;
+    const float steps    = (float) (std::pow(2.0, bw) - 1);
+    const float hi       = delta * (offset + steps);
+    const float start    = (float) h.xl(0);
+    const double step    = h.xl(1) - h.xl(0);
+    auto index           = [&](float v) {
+        int i = (int) std::floor((v - start) / step);
+        return std::min(std::max(0, i), kPdfSize - 1);
+    };
+    const int iLo = index(lo), iHi = index(hi);
+    auto mid      = [&](int i) { return start + i * step + step / 2; };   // double
+    const float loMid = (float) (start + (iLo * step) + step / 2);
+    const float hiMid = (float) (start + (iHi * step) + step / 2);
+
+    double satLo = 0, satHi = 0, quant = 0;
+    for (int i = 0; i < iLo; ++i)
+        satLo += h.pdf[i] * sq(mid(i) - loMid);
+    for (int i = iHi; i < kPdfSize; ++i)
+        satHi += h.pdf[i] * sq(mid(i) - hiMid);
+    for (int i = iLo; i < iHi; ++i)
+    {
+        float v   = (float) mid(i);
+        int q     = (int) std::round(v / delta - offset);
+        float deq = delta * (q + offset);
+        quant += h.pdf[i] * sq((double) (v - deq));
+    }
+    double cost = kGammaTfe * (satLo + satHi) + quant;
+    return std::min(cost, std::numeric_limits<double>::max());
+}
+
+bool tfe_clamp_candidate(float obsLo, float obsHi, float steps, float& delta, int& offset)
+{
+    float lo = std::max(delta * offset, kFltLowest);
+    float hi = std::min(delta * (offset + steps), kFltMax);
+    if (lo < obsLo && hi > obsHi)
+        return false;
+    lo = std::max(obsLo, lo);
+    hi = std::min(obsHi, hi);
+    if (lo == hi)
+        return false;
+    delta  = (float) (((double) hi - lo) / steps);
+    offset = (int) std::round(lo / delta);
+    return true;
+}
+
+void tfe_candidates_asym(float obsLo, float obsHi, float steps, std::vector<Candidate>& out)
+{
+    const float d0 = (float) (((double) obsHi - (double) obsLo) / steps);
+    const int o0   = (int) std::round(obsLo / d0);
+    obsLo          = std::max(d0 * o0, kFltLowest);
+    obsHi          = std::min(d0 * (o0 + steps), kFltMax);
+    // 17 deltas f*d0, f = 1/16 .. 17/16 (float accumulator, double compare), x 21 offsets
+    for (float f = 1.0 / 16; f <= 1 + 1.0 / 16; f += 1.0 / 16)
+        for (int i = 0; i <= 20; ++i)
+        {
+            float d = f * d0;
+            int o   = (int) (-steps + steps / 20.0 * i);
+            if (tfe_clamp_candidate(obsLo, obsHi, steps, d, o))
+                out.push_back({d, o});
+        }
+    out.push_back({d0, o0});
+}
+
+void tfe_candidates_sym(float lo, float hi, float steps, bool unsign, std::vector<Candidate>& out)
+{
+    float dmax = 0.0f;
+    int off    = 0;
+    if (lo == 0.0 && unsign)
+        dmax = hi / steps;
+    else
+    {
+        float absmax = std::max(std::abs(hi), std::abs(lo));
+        dmax         = (float) (absmax / (steps / 2.0));
+        off          = (int) std::floor(-steps / 2);
+    }
+    for (float f = 1.0 / 100; f <= 1 + 1.0 / 100; f += 1.0 / 100)
+        out.push_back({f * dmax, off});
+}
+
+aimet_tf_encoding tfe_encoding(const HistView& h, int32_t bw, bool sym, bool strict, bool unsign)
+{
+    auto range  = observed_range(h);
+    float steps = (float) (std::pow(2.0, bw) - 1);
+    std::vector<Candidate> cands;
+    cands.reserve(400);
+    if (sym)
+    {
+        if (strict)
+            steps -= 1;
+        tfe_candidates_sym(range.first, range.second, steps, unsign, cands);
+    }
+    else
+        tfe_candidates_asym(range.first, range.second, steps, cands);
+
+    float bestDelta = -1;
+    int bestOffset  = -1;
+    double best     = std::numeric_limits<double>::max();
+    for (const auto& c: cands)
+    {
+        double cost = tfe_cost(h, bw, c.delta, c.offset);
+        if (cost < best)
+        {
+            best       = cost;
+            bestDelta  = c.delta;
+            bestOffset = c.offset;
+        }
+    }
+    float lo = std::max(bestDelta * bestOffset, kFltLowest);
+    float hi = std::min(bestDelta * (bestOffset + steps), kFltMax);
+    return make_enc(lo, hi, bestDelta, bestOffset, bw);
+}
+
+// ---- Percentile ---------------------------------------------------------------------------
+std::pair<float, float> percentile_range(const HistView& h, float percentile)
+{
+    auto range = observed_range(h);
+    if (percentile == 100.0f)
+        return range;
+    const float width = (float) (h.xl(1) - h.xl(0));
+    float pLo         = (float) h.xl(0);
+    float pHi         = (float) h.xl(kPdfSize - 1) + width;
+    double cdf[kPdfSize];
+    std::partial_sum(h.pdf, h.pdf + kPdfSize, cdf);
+    const float left = 1 - percentile / 100;
+    for (int i = 0; i < kPdfSize; ++i)
+        if (cdf[i] >= left)
+        {
+            pLo = (float) h.xl(i);
+            break;
+        }
+    const float right = percentile / 100;
+    for (int i = kPdfSize - 1; i >= 0; --i)
+        if (cdf[i] < right && h.xl(i) < range.second)
+        {
+            pHi = (float) (h.xl(i) + width);
+            break;
+        }
+    if (pLo == pHi)
+        pHi += width;
+    return {pLo, pHi};
+}
+
+// ---- MSE ----------------------------------------------------------------------------------
+float mse_cost(int32_t bw, const std::vector<std::pair<float, float>>& centers, float cLo, float cHi, bool sym,
+               bool strict, bool unsign)
+{
+    aimet_tf_encoding e = computed_encoding(bw, cLo, cHi, sym, strict, unsign);
+    float err           = 0;
+    for (const auto& bc: centers)
+    {
+        float v       = bc.first;
+        float clamped = std::max(cLo, std::min(v, cHi));
+        int q         = (int) std::round(clamped / e.delta - e.offset);
+        float deq     = e.delta * (q + e.offset);
+        err += bc.second * sq((double) (v - deq));
+    }
+    return err;
+}
+
+std::pair<float, float> mse_range(const HistView& h, int32_t bw, bool sym, bool strict, bool unsign)
+{
+    const float width = (float) (h.xl(1) - h.xl(0));
+    const float hMin  = (float) h.xl(0);
+    const float hMax  = (float) h.xl(kPdfSize - 1) + width;
+    auto range        = observed_range(h);
+    const float lo    = range.first;
+    const float hi    = range.second + width;
+
+    std::vector<float> edges {lo};
+    for (float e = hMin; e <= hMax; e += width)
+        if (e >= lo && e <= hi)
+            edges.push_back(e);
+
+    std::vector<float> mins, maxs;
+    for (float e: edges)
+    {
+        if (e < 0)
+            mins.push_back(e);
+        else if (e > 0)
+            maxs.push_back(e);
+    }
+    mins.push_back(0);
+    maxs.push_back(0);
+
+    const float start = (float) h.xl(0);
+    const float step  = (float) (h.xl(1) - h.xl(0));
+    const int nc      = (int) edges.size() - 1;
+    std::vector<std::pair<float, float>> centers(std::max(nc, 0));
+    for (int i = 0; i < nc; ++i)
+    {
+        centers[i].first = (i == 0) ? lo + width / 2 : centers[i - 1].first + width;
+        int idx          = (int) std::floor((centers[i].first - start) / step);
+        idx              = std::min(std::max(0, idx), kPdfSize - 1);
+        centers[i].second = (float) h.pdf[idx];
+    }
+
+    float bestErr = std::numeric_limits<float>::max();
+    std::pair<float, float> best(lo, hi);
+    const size_t total = mins.size() * maxs.size() - 1;   // the trailing {0, 0} is not a candidate
+    for (size_t t = 0; t < total; ++t)
+    {
+        float cLo = mins[t / maxs.size()], cHi = maxs[t % maxs.size()];
+        float err = mse_cost(bw, centers, cLo, cHi, sym, strict, unsign);
+        if (err < bestErr)
+        {
+            bestErr = err;
+            best    = {cLo, cHi};
+        }
+    }
+    return best;
+}
+
+}   // namespace
+
+aimet_tf_encoding tf_encoding(double accMin, double accMax, int32_t bw, bool sym, bool strict, bool unsign)
+{
+    double lo = std::min(0.0, accMin);
+    double hi = std::max(0.0, accMax);
+    hi        = std::max(hi, lo + kMinRange);
+    return computed_encoding(bw, lo, hi, sym, strict, unsign);
+}
+
+aimet_tf_encoding histogram_encoding(int scheme, bool initialized, bool stats_updated, float hist_min,
+                                     double bucket_size, const double* pdf, float percentile, int32_t bw, bool sym,
+                                     bool strict, bool unsign)
+{
+    float steps = (float) (std::pow(2.0, bw) - 1);
+    if (scheme != AIMET_QUANTIZATION_TF_ENHANCED && sym && strict)
+        steps -= 1;   // percentile / MSE reduce before the zero-data check
+    if (!initialized)
+        return unseen_or_zero(stats_updated, bw, steps);
+    HistView h {hist_min, bucket_size, pdf};
+    if (scheme == AIMET_QUANTIZATION_TF_ENHANCED)
+        return tfe_encoding(h, bw, sym, strict, unsign);
+    std::pair<float, float> r = scheme == AIMET_QUANTIZATION_PERCENTILE ? percentile_range(h, percentile)
+                                                                         : mse_range(h, bw, sym, strict, unsign);
+    float lo = std::min(r.first, 0.0f);
+    float hi = std::max(r.second, 0.0f);
+    return computed_encoding(bw, lo, hi, sym, strict, unsign);
+}
+
+void histogram_xleft(float hist_min, double bucket_size, double* xleft)
+{
+    HistView h {hist_min, bucket_size, nullptr};
+    for (int i = 0; i < kPdfSize; ++i)
+        xleft[i] = h.xl(i);
+}
+
+}   // namespace aimet_amd

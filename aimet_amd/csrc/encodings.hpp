@@ -1,0 +1,24 @@
+// encodings.hpp -- host-side encoding math (see encodings.cpp for the reference map).
+#pragma once
+
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+
+namespace aimet_amd
+{
+
+aimet_tf_encoding computed_encoding(int32_t bw, double mn, double mx, bool sym, bool strict, bool unsign);
+void gate_min_max(double& mn, double& mx);
+aimet_tf_encoding fill_encoding_info(int32_t bw, double mn, double mx);
+bool partial_encoding(int32_t bw, aimet_tf_encoding& e, bool sym, bool unsign, bool strict, std::string& err);
+void per_channel_table_host(const aimet_tf_encoding* encs, int64_t C, float* table);
+
+aimet_tf_encoding tf_encoding(double accMin, double accMax, int32_t bw, bool sym, bool strict, bool unsign);
+aimet_tf_encoding histogram_encoding(int scheme, bool initialized, bool stats_updated, float hist_min,
+                                     double bucket_size, const double* pdf, float percentile, int32_t bw, bool sym,
+                                     bool strict, bool unsign);
+void histogram_xleft(float hist_min, double bucket_size, double* xleft);
+
+}   // namespace aimet_amd

@@ -1,0 +1,407 @@
+// quantizer.cpp -- aimet_tensor_quantizer: the AimetTensorQuantizer / TensorQuantizer object of the
+// reference (AimetTensorQuantizer.cpp:79-315, TensorQuantizer.cpp:49-343) with its analyzer state
+// held in HBM. One object carries the analyzers of all channels of a tensor (the reference
+// allocates one C++ analyzer per channel and loops over channels in Python).
+#include <algorithm>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "encodings.hpp"
+#include "tq_state.hpp"
+
+using namespace aimet_amd;
+
+struct aimet_tensor_quantizer
+{
+    int scheme       = AIMET_QUANTIZATION_TF;
+    int64_t C        = 1;
+    int device       = 0;
+    float percentile = 100.0f;   // PercentileEncodingAnalyzer.h:100
+    bool stats_updated = false;  // AimetTensorQuantizer::_isEncodingValid / analyzer _statsUpdated
+    bool hist        = false;    // histogram-based analyzer (TF-E, percentile, MSE)
+    void* arena      = nullptr;
+    size_t arena_bytes = 0;
+    TqDevice d {};
+};
+
+namespace
+{
+
+struct DeviceGuard
+{
+    int prev = -1;
+    explicit DeviceGuard(int dev)
+    {
+        AIMET_HIP_CHECK(hipGetDevice(&prev));
+        if (prev != dev)
+            AIMET_HIP_CHECK(hipSetDevice(dev));
+    }
+    ~DeviceGuard()
+    {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0)
+            (void) hipSetDevice(prev);
+    }
+};
+
+size_t align256(size_t b)
+{
+    return (b + 255) & ~size_t(255);
+}
+
+void layout(aimet_tensor_quantizer* q, bool assign)
+{
+    const int64_t C = q->C;
+    size_t off      = 0;
+    char* base      = static_cast<char*>(q->arena);
+    auto take       = [&](size_t bytes) -> void* {
+        void* p = assign ? base + off : nullptr;
+        off += align256(bytes);
+        return p;
+    };
+    q->d.minmax      = (float*) take(sizeof(float) * 2 * C);
+    q->d.partials    = (float*) take(sizeof(float) * 2 * kMinmaxParts);
+    q->d.acc         = (double*) take(sizeof(double) * 2 * C);
+    q->d.pdf_init    = (int32_t*) take(sizeof(int32_t) * C);
+    q->d.iterations  = (int32_t*) take(sizeof(int32_t) * C);
+    q->d.hist_min    = (float*) take(sizeof(float) * C);
+    q->d.bucket_size = (double*) take(sizeof(double) * C);
+    q->d.bin_bucket  = (float*) take(sizeof(float) * C);
+    q->d.bin_offset  = (float*) take(sizeof(float) * C);
+    if (q->hist)
+    {
+        q->d.pdf    = (double*) take(sizeof(double) * kPdfSize * C);
+        q->d.counts = (unsigned long long*) take(sizeof(unsigned long long) * kPdfSize * C);
+    }
+    else
+    {
+        q->d.pdf    = nullptr;
+        q->d.counts = nullptr;
+    }
+    q->arena_bytes = off;
+}
+
+bool in_arena(const aimet_tensor_quantizer* q, const void* p)
+{
+    auto b = static_cast<const char*>(q->arena), c = static_cast<const char*>(p);
+    return c >= b && c < b + q->arena_bytes;
+}
+
+void reset_device_state(aimet_tensor_quantizer* q, hipStream_t s)
+{
+    AIMET_HIP_CHECK(hipMemsetAsync(q->arena, 0, q->arena_bytes, s));
+    // exchange buffers bound outside the arena (aimet_tq_bind_exchange)
+    if (q->d.minmax && !in_arena(q, q->d.minmax))
+        AIMET_HIP_CHECK(hipMemsetAsync(q->d.minmax, 0, sizeof(float) * 2 * q->C, s));
+    if (q->d.counts && !in_arena(q, q->d.counts))
+        AIMET_HIP_CHECK(hipMemsetAsync(q->d.counts, 0, sizeof(unsigned long long) * kPdfSize * q->C, s));
+    launch_reset_state(q->d, q->C, q->hist, s);
+}
+
+void check_shape(aimet_tensor_quantizer* q, int64_t outer, int64_t C, int64_t K)
+{
+    AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
+    AIMET_REQUIRE(outer >= 0 && K >= 0, "invalid tensor shape");
+    AIMET_REQUIRE(C == q->C, "channel count of the tensor (" + std::to_string(C) +
+                                 ") does not match the quantizer (" + std::to_string(q->C) + ")");
+}
+
+template <class T>
+std::vector<T> d2h(const T* dev, size_t n)
+{
+    std::vector<T> h(n);
+    if (n)
+        AIMET_HIP_CHECK(hipMemcpy(h.data(), dev, sizeof(T) * n, hipMemcpyDeviceToHost));
+    return h;
+}
+
+template <class F>
+void parallel_channels(int64_t C, F&& f)
+{
+    unsigned hw   = std::max(1u, std::thread::hardware_concurrency());
+    int64_t nthr  = std::min<int64_t>({(int64_t) hw, 16, (C + 63) / 64});
+    if (nthr <= 1)
+    {
+        for (int64_t c = 0; c < C; ++c)
+            f(c);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (int64_t t = 0; t < nthr; ++t)
+        th.emplace_back([&, t] {
+            for (int64_t c = t; c < C; c += nthr)
+                f(c);
+        });
+    for (auto& x: th)
+        x.join();
+}
+
+}   // namespace
+
+extern "C" {
+
+int aimet_tq_create(int scheme, int64_t num_channels, int device, aimet_tensor_quantizer** out)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(out != nullptr, "output handle is null");
+        AIMET_REQUIRE(num_channels >= 1, "num_channels must be >= 1");
+        if (scheme == AIMET_QUANTIZATION_RANGE_LEARNING)   // QuantizerFactory.cpp:93-96
+            scheme = AIMET_QUANTIZATION_TF;
+        if (scheme == AIMET_QUANTIZATION_ENTROPY)
+            throw RuntimeError("QUANTIZATION_ENTROPY is not implemented by the MI355X core (SURVEY §8(f) row 3)");
+        AIMET_REQUIRE(scheme >= AIMET_QUANTIZATION_TF && scheme <= AIMET_QUANTIZATION_MSE, "Unknown quant scheme");
+        DeviceGuard g(device);
+        auto* q   = new aimet_tensor_quantizer();
+        q->scheme = scheme;
+        q->C      = num_channels;
+        q->device = device;
+        q->hist   = scheme != AIMET_QUANTIZATION_TF;
+        layout(q, false);
+        hipError_t e = hipMalloc(&q->arena, q->arena_bytes);
+        if (e != hipSuccess)
+        {
+            delete q;
+            throw HipError(std::string("hipMalloc(tensor quantizer state): ") + hipGetErrorString(e));
+        }
+        layout(q, true);
+        reset_device_state(q, nullptr);
+        AIMET_HIP_CHECK(hipStreamSynchronize(nullptr));
+        *out = q;
+    });
+}
+
+int aimet_tq_destroy(aimet_tensor_quantizer* q)
+{
+    return guarded([&] {
+        if (!q)
+            return;
+        if (q->arena)
+        {
+            DeviceGuard g(q->device);
+            // callers may still have work queued on any stream that uses this state
+            AIMET_HIP_CHECK(hipDeviceSynchronize());
+            AIMET_HIP_CHECK(hipFree(q->arena));
+        }
+        delete q;
+    });
+}
+
+int aimet_tq_reset_encoding_stats(aimet_tensor_quantizer* q, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
+        DeviceGuard g(q->device);
+        reset_device_state(q, as_stream(stream));
+        q->stats_updated = false;
+        q->percentile    = 100.0f;   // a fresh analyzer (AimetTensorQuantizer.cpp:89-96)
+    });
+}
+
+int aimet_tq_set_percentile_value(aimet_tensor_quantizer* q, float p)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
+        if (q->scheme == AIMET_QUANTIZATION_PERCENTILE)   // only for the percentile scheme
+        {
+            // PercentileEncodingAnalyzer.cpp setPercentileValue: valid range (0, 100]? The reference
+            // asserts 50 <= p <= 100 in Python (v1/quantsim.py:1009) and not in C++.
+            q->percentile = p;
+        }
+    });
+}
+
+int aimet_tq_get_percentile_value(aimet_tensor_quantizer* q, float* p)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr && p != nullptr, "null argument");
+        if (q->scheme != AIMET_QUANTIZATION_PERCENTILE)
+            throw RuntimeError("Percentile Value only exists in case of percentile quant scheme.");
+        *p = q->percentile;
+    });
+}
+
+int aimet_tq_batch_minmax(aimet_tensor_quantizer* q, const float* x, int64_t outer, int64_t C, int64_t K,
+                          void* stream)
+{
+    return guarded([&] {
+        check_shape(q, outer, C, K);
+        if (outer * K > 0)
+            require_device_ptr(x, "input");
+        DeviceGuard g(q->device);
+        launch_batch_minmax(q->d, x, outer, C, K, q->hist ? 1 : 0, as_stream(stream));
+        q->stats_updated = true;
+    });
+}
+
+int aimet_tq_fold_minmax(aimet_tensor_quantizer* q, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
+        DeviceGuard g(q->device);
+        launch_fold_minmax(q->d, q->C, !q->hist, as_stream(stream));
+    });
+}
+
+int aimet_tq_batch_histogram(aimet_tensor_quantizer* q, const float* x, int64_t outer, int64_t C, int64_t K,
+                             void* stream)
+{
+    return guarded([&] {
+        check_shape(q, outer, C, K);
+        if (!q->hist)
+            return;
+        if (outer * K > 0)
+            require_device_ptr(x, "input");
+        DeviceGuard g(q->device);
+        launch_batch_histogram(q->d, x, outer, C, K, as_stream(stream));
+    });
+}
+
+int aimet_tq_fold_histogram(aimet_tensor_quantizer* q, int64_t count, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
+        AIMET_REQUIRE(count >= 0, "negative element count");
+        if (!q->hist)
+            return;
+        DeviceGuard g(q->device);
+        launch_fold_histogram(q->d, q->C, count, as_stream(stream));
+    });
+}
+
+int aimet_tq_update_stats(aimet_tensor_quantizer* q, const float* x, int64_t outer, int64_t C, int64_t K,
+                          void* stream)
+{
+    return guarded([&] {
+        check_shape(q, outer, C, K);
+        if (outer * K > 0)
+            require_device_ptr(x, "input");
+        DeviceGuard g(q->device);
+        hipStream_t s = as_stream(stream);
+        launch_batch_minmax(q->d, x, outer, C, K, q->hist ? 1 : 0, s);
+        launch_fold_minmax(q->d, q->C, !q->hist, s);
+        if (q->hist)
+        {
+            launch_batch_histogram(q->d, x, outer, C, K, s);
+            launch_fold_histogram(q->d, q->C, outer * K, s);
+        }
+        q->stats_updated = true;
+    });
+}
+
+int aimet_tq_minmax_buffer(aimet_tensor_quantizer* q, float** dev, int64_t* n)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q && dev && n, "null argument");
+        *dev = q->d.minmax;
+        *n   = 2 * q->C;
+    });
+}
+
+int aimet_tq_counts_buffer(aimet_tensor_quantizer* q, uint64_t** dev, int64_t* n)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q && dev && n, "null argument");
+        *dev = reinterpret_cast<uint64_t*>(q->d.counts);
+        *n   = q->hist ? (int64_t) kPdfSize * q->C : 0;
+    });
+}
+
+int aimet_tq_bind_exchange(aimet_tensor_quantizer* q, float* minmax, uint64_t* counts)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
+        require_device_ptr(minmax, "minmax exchange buffer");
+        if (q->hist)
+        {
+            require_device_ptr(counts, "counts exchange buffer");
+            q->d.counts = reinterpret_cast<unsigned long long*>(counts);
+        }
+        q->d.minmax = minmax;
+    });
+}
+
+int aimet_tq_mark_stats_updated(aimet_tensor_quantizer* q)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
+        q->stats_updated = true;
+    });
+}
+
+int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int sym, int strict, int unsign,
+                          aimet_tf_encoding* out, int* valid, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr && out != nullptr, "null argument");
+        const int64_t C = q->C;
+        std::memset(out, 0, sizeof(aimet_tf_encoding) * C);
+        if (valid)
+            *valid = q->stats_updated ? 1 : 0;
+        if (!q->stats_updated)
+            return;   // AimetTensorQuantizer.cpp:185-189: encoding left default, valid = false
+        DeviceGuard g(q->device);
+        AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+        const int32_t b = (int32_t) (uint8_t) bw;   // computeEncoding(uint8_t bw, ...)
+        if (!q->hist)
+        {
+            auto acc = d2h(q->d.acc, 2 * C);
+            parallel_channels(C, [&](int64_t c) {
+                out[c] = tf_encoding(acc[2 * c], acc[2 * c + 1], b, sym, strict, unsign);
+            });
+            return;
+        }
+        auto init  = d2h(q->d.pdf_init, C);
+        auto hmin  = d2h(q->d.hist_min, C);
+        auto bsz   = d2h(q->d.bucket_size, C);
+        auto pdf   = d2h(q->d.pdf, (size_t) kPdfSize * C);
+        parallel_channels(C, [&](int64_t c) {
+            out[c] = histogram_encoding(q->scheme, init[c] != 0, true, hmin[c], bsz[c], pdf.data() + kPdfSize * c,
+                                        q->percentile, b, sym, strict, unsign);
+        });
+    });
+}
+
+int aimet_tq_get_stats_histogram(aimet_tensor_quantizer* q, int64_t channel, double* xleft, double* pdf, int* n,
+                                 void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q != nullptr && xleft != nullptr && pdf != nullptr && n != nullptr, "null argument");
+        AIMET_REQUIRE(channel >= 0 && channel < q->C, "channel out of range");
+        if (!q->hist)
+            throw RuntimeError("the TF encoding analyzer keeps no histogram (TfEncodingAnalyzer.cpp:53-57)");
+        DeviceGuard g(q->device);
+        AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+        int32_t init = 0;
+        AIMET_HIP_CHECK(hipMemcpy(&init, q->d.pdf_init + channel, sizeof(int32_t), hipMemcpyDeviceToHost));
+        *n = 0;
+        if (!init)
+            return;
+        float hmin = 0;
+        double bs  = 0;
+        AIMET_HIP_CHECK(hipMemcpy(&hmin, q->d.hist_min + channel, sizeof(float), hipMemcpyDeviceToHost));
+        AIMET_HIP_CHECK(hipMemcpy(&bs, q->d.bucket_size + channel, sizeof(double), hipMemcpyDeviceToHost));
+        AIMET_HIP_CHECK(hipMemcpy(pdf, q->d.pdf + kPdfSize * channel, sizeof(double) * kPdfSize,
+                                  hipMemcpyDeviceToHost));
+        histogram_xleft(hmin, bs, xleft);
+        *n = kPdfSize;
+    });
+}
+
+int aimet_tq_num_channels(aimet_tensor_quantizer* q, int64_t* c)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q && c, "null argument");
+        *c = q->C;
+    });
+}
+
+int aimet_tq_quant_scheme(aimet_tensor_quantizer* q, int* s)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q && s, "null argument");
+        *s = q->scheme;
+    });
+}
+
+}   // extern "C"

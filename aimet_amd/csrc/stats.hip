@@ -1,0 +1,478 @@
+// stats.hip -- encoding-statistics kernels (TF min/max; TF-E / percentile / MSE histograms).
+//
+// Reference: math_functions.cu:52-64 (two thrust reductions, each ending in a blocking D2H),
+// :125-211 (a private 512-bin histogram per THREAD in a <=32 MiB global scratch, reduced by ONE
+// 512-thread block, then a blocking cudaMemcpy), math_functions.cpp:207-288 (range init and PDF
+// averaging on the host). Per-channel statistics were gathered by a Python loop over channels
+// (v1/tensor_quantizer.py:567-570), one select().contiguous() copy + one analyzer per channel.
+//
+// MI355X design:
+//   * min/max: one fused pass, 16-B loads, wave64 shuffle + LDS block reduction, per-block
+//     partials combined by one small block (no atomics: deterministic).
+//   * histogram: LDS-privatised 512-bin histograms (one per wave, ds_add_u32), a register counter
+//     for exact zeros (ReLU outputs put ~half of all elements into one bin), then one 64-bit
+//     global atomic per non-empty bin per workgroup.
+//   * range init and the double-precision PDF running average run on the device, so an
+//     updateStats call is 2-4 stream-ordered launches with no host synchronisation.
+//   * per-channel: all channels in one launch, one workgroup per channel.
+// Arithmetic follows the reference CPU code bit for bit (DTYPE = float; see common.hpp).
+#include "tq_state.hpp"
+
+#include <cfloat>
+
+namespace aimet_amd
+{
+
+namespace
+{
+
+constexpr int kWaves = kBlock / 64;
+
+__device__ __forceinline__ float wave_min(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v = fminf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-wide min/max; result valid in thread 0. NaNs never enter (fminf/fmaxf drop them),
+// matching GetMin_cpu/GetMax_cpu (std::min/std::max skip NaN, math_functions.cpp:327-347).
+// The sign of a zero extremum is immaterial downstream (TfEncodingAnalyzer.cpp:87-88 and
+// InitializePdf produce identical results for +0 and -0).
+__device__ __forceinline__ void block_minmax(float& mn, float& mx)
+{
+    __shared__ float smn[kWaves], smx[kWaves];
+    mn       = wave_min(mn);
+    mx       = wave_max(mx);
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 0)
+    {
+        smn[w] = mn;
+        smx[w] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+#pragma unroll
+        for (int i = 1; i < kWaves; ++i)
+        {
+            mn = fminf(mn, smn[i]);
+            mx = fmaxf(mx, smx[i]);
+        }
+    }
+}
+
+__device__ __forceinline__ void accum4(const float4& v, float& mn, float& mx)
+{
+    mn = fminf(fminf(mn, v.x), fminf(v.y, fminf(v.z, v.w)));
+    mx = fmaxf(fmaxf(mx, v.x), fmaxf(v.y, fmaxf(v.z, v.w)));
+}
+
+// ---- per-tensor min/max: partials[block] = {-min, max} --------------------------------------
+__global__ __launch_bounds__(kBlock) void minmax_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
+                                                               float2* __restrict__ partials,
+                                                               const int32_t* __restrict__ pdf_init, int skip_if_init)
+{
+    if (skip_if_init && pdf_init[0])
+        return;
+    float mn = INFINITY, mx = -INFINITY;
+    if (vec)
+    {
+        const float4* x4     = reinterpret_cast<const float4*>(x);
+        int64_t nvec         = n / 4;
+        const int64_t stride = (int64_t) gridDim.x * kBlock * 4;
+        for (int64_t b = (int64_t) blockIdx.x * kBlock * 4 + threadIdx.x; b < nvec; b += stride)
+        {
+            float4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (b + u * kBlock < nvec)
+                    v[u] = x4[b + u * kBlock];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (b + u * kBlock < nvec)
+                    accum4(v[u], mn, mx);
+        }
+        for (int64_t i = nvec * 4 + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n;
+             i += (int64_t) gridDim.x * kBlock)
+        {
+            mn = fminf(mn, x[i]);
+            mx = fmaxf(mx, x[i]);
+        }
+    }
+    else
+    {
+        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
+        {
+            mn = fminf(mn, x[i]);
+            mx = fmaxf(mx, x[i]);
+        }
+    }
+    block_minmax(mn, mx);
+    if (threadIdx.x == 0)
+        partials[blockIdx.x] = make_float2(-mn, mx);
+}
+
+// Combine per-block partials {-min, max} into minmax[0].
+__global__ __launch_bounds__(kBlock) void minmax_combine_max_kernel(const float2* __restrict__ partials, int nparts,
+                                                                    float2* __restrict__ minmax,
+                                                                    const int32_t* __restrict__ pdf_init,
+                                                                    int skip_if_init)
+{
+    if (skip_if_init && pdf_init[0])
+        return;
+    float a = -INFINITY, b = -INFINITY;
+    for (int i = threadIdx.x; i < nparts; i += kBlock)
+    {
+        a = fmaxf(a, partials[i].x);
+        b = fmaxf(b, partials[i].y);
+    }
+    float na = -a;            // min over -(partials.x) == global min
+    block_minmax(na, b);      // na: block min of mins, b: block max of maxes
+    if (threadIdx.x == 0)
+        minmax[0] = make_float2(-na, b);
+}
+
+// ---- per-channel min/max: one workgroup per channel of [outer][C][K] -----------------------
+__global__ __launch_bounds__(kBlock) void minmax_channel_kernel(const float* __restrict__ x, int64_t outer, int64_t C,
+                                                                int64_t K, int vec, float2* __restrict__ minmax,
+                                                                const int32_t* __restrict__ pdf_init,
+                                                                int skip_if_init)
+{
+    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+    {
+        if (skip_if_init && pdf_init[c])
+            continue;
+        float mn = INFINITY, mx = -INFINITY;
+        for (int64_t o = 0; o < outer; ++o)
+        {
+            const float* row = x + (o * C + c) * K;
+            if (vec)
+            {
+                const float4* r4 = reinterpret_cast<const float4*>(row);
+                for (int64_t k = threadIdx.x; k < K / 4; k += kBlock)
+                    accum4(r4[k], mn, mx);
+            }
+            else
+            {
+                for (int64_t k = threadIdx.x; k < K; k += kBlock)
+                {
+                    mn = fminf(mn, row[k]);
+                    mx = fmaxf(mx, row[k]);
+                }
+            }
+        }
+        block_minmax(mn, mx);
+        if (threadIdx.x == 0)
+            minmax[c] = make_float2(-mn, mx);
+        __syncthreads();
+    }
+}
+
+// ---- fold: TF running min/max, or PDF range initialisation --------------------------------
+// InitializePdf<float>(pdf, min, max, signed=true), math_functions.cpp:207-241.
+__device__ void initialize_pdf(const TqDevice& d, int64_t c, float min_val, float max_val)
+{
+    if (min_val == max_val)
+        max_val = (max_val < min_val + 0.01f) ? min_val + 0.01f : max_val;
+    float center = (max_val + min_val) / 2.0f;
+    float lo     = center - 3.0f * (center - min_val);
+    float hi     = center + 3.0f * (max_val - center);
+    min_val      = (-FLT_MAX < lo) ? lo : -FLT_MAX;   // std::max(lowest, lo)
+    max_val      = (hi < FLT_MAX) ? hi : FLT_MAX;     // std::min(max, hi)
+    double bs    = ((double) max_val - (double) min_val) / kPdfSize;
+    double x0    = (double) min_val + (double) 0 * bs;
+    double x1    = (double) min_val + (double) 1 * bs;
+    float bucket = (float) (x1 - x0);                 // UpdatePdf:264
+    float mv     = (float) x0;                        // UpdatePdf:265 (signed)
+    d.hist_min[c]    = min_val;
+    d.bucket_size[c] = bs;
+    d.bin_bucket[c]  = bucket;
+    d.bin_offset[c]  = mv / bucket;                   // UpdatePdf:267
+    d.iterations[c]  = 0;                             // pdf[] is zero since the last reset
+    d.pdf_init[c]    = 1;
+}
+
+__global__ __launch_bounds__(kBlock) void fold_minmax_kernel(TqDevice d, int64_t C, int tf_scheme)
+{
+    int64_t c = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (c >= C)
+        return;
+    float2 m  = reinterpret_cast<const float2*>(d.minmax)[c];
+    float mn  = -m.x, mx = m.y;
+    if (tf_scheme)
+    {
+        // TfEncodingAnalyzer.cpp:63-71 (std::min/std::max in double)
+        double cmin = (double) mn, cmax = (double) mx;
+        double2* acc = reinterpret_cast<double2*>(d.acc);
+        double2 a    = acc[c];
+        a.x          = (cmin < a.x) ? cmin : a.x;
+        a.y          = (a.y < cmax) ? cmax : a.y;
+        acc[c]       = a;
+    }
+    else if (!d.pdf_init[c])
+    {
+        // UpdatePdf:254-259: an all-zero tensor does not initialise the PDF (batch ignored)
+        if (mn == 0 && mx == 0)
+            return;
+        initialize_pdf(d, c, mn, mx);
+    }
+}
+
+// ---- histogram ----------------------------------------------------------------------------
+// GetHistogram_cpu, math_functions.cpp:367-384: index = round(x / bucket - offset) in float,
+// out-of-range (and NaN) dropped.
+struct Binner
+{
+    float bucket, offset;
+    __device__ __forceinline__ int bin(float x) const
+    {
+        float r = __builtin_roundf(x / bucket - offset);
+        return (r >= 0.0f && r < (float) kPdfSize) ? (int) r : -1;
+    }
+};
+
+// per-tensor: many workgroups over one tensor, atomics into counts[0][:]
+__global__ __launch_bounds__(kBlock) void histogram_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
+                                                                  TqDevice d)
+{
+    if (!d.pdf_init[0])
+        return;
+    __shared__ uint32_t lds[kWaves][kPdfSize];
+    Binner bn {d.bin_bucket[0], d.bin_offset[0]};
+    const int w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < kWaves * kPdfSize; i += kBlock)
+        (&lds[0][0])[i] = 0;
+    __syncthreads();
+    const int zbin = bn.bin(0.0f);
+    uint32_t zc    = 0;
+    auto add = [&](float v) {
+        if (v == 0.0f)
+        {
+            ++zc;
+            return;
+        }
+        int b = bn.bin(v);
+        if (b >= 0)
+            atomicAdd(&lds[w][b], 1u);
+    };
+    int64_t done = 0;
+    if (vec)
+    {
+        const float4* x4     = reinterpret_cast<const float4*>(x);
+        int64_t nv           = n / 4;
+        const int64_t stride = (int64_t) gridDim.x * kBlock * 2;
+        for (int64_t b = (int64_t) blockIdx.x * kBlock * 2 + threadIdx.x; b < nv; b += stride)
+        {
+            float4 v0 = x4[b];
+            float4 v1 = (b + kBlock < nv) ? x4[b + kBlock] : make_float4(NAN, NAN, NAN, NAN);
+            add(v0.x);
+            add(v0.y);
+            add(v0.z);
+            add(v0.w);
+            add(v1.x);   // NaN padding is dropped by the binner
+            add(v1.y);
+            add(v1.z);
+            add(v1.w);
+        }
+        done = nv * 4;
+    }
+    for (int64_t i = done + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
+        add(x[i]);
+    zc = wave_sum(zc);
+    if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
+        atomicAdd(&lds[w][zbin], zc);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kPdfSize; b += kBlock)
+    {
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < kWaves; ++i)
+            s += lds[i][b];
+        if (s)
+            atomicAdd(&d.counts[b], (unsigned long long) s);
+    }
+}
+
+// per-channel: one workgroup per channel, counts written directly
+__global__ __launch_bounds__(kBlock) void histogram_channel_kernel(const float* __restrict__ x, int64_t outer,
+                                                                   int64_t C, int64_t K, int vec, TqDevice d)
+{
+    __shared__ uint32_t lds[kWaves][kPdfSize];
+    const int w = threadIdx.x >> 6;
+    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+    {
+        if (!d.pdf_init[c])
+            continue;
+        Binner bn {d.bin_bucket[c], d.bin_offset[c]};
+        for (int i = threadIdx.x; i < kWaves * kPdfSize; i += kBlock)
+            (&lds[0][0])[i] = 0;
+        __syncthreads();
+        const int zbin = bn.bin(0.0f);
+        uint32_t zc    = 0;
+        auto add = [&](float v) {
+            if (v == 0.0f)
+            {
+                ++zc;
+                return;
+            }
+            int b = bn.bin(v);
+            if (b >= 0)
+                atomicAdd(&lds[w][b], 1u);
+        };
+        for (int64_t o = 0; o < outer; ++o)
+        {
+            const float* row = x + (o * C + c) * K;
+            if (vec)
+            {
+                const float4* r4 = reinterpret_cast<const float4*>(row);
+                for (int64_t k = threadIdx.x; k < K / 4; k += kBlock)
+                {
+                    float4 v = r4[k];
+                    add(v.x);
+                    add(v.y);
+                    add(v.z);
+                    add(v.w);
+                }
+            }
+            else
+            {
+                for (int64_t k = threadIdx.x; k < K; k += kBlock)
+                    add(row[k]);
+            }
+        }
+        zc = wave_sum(zc);
+        if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
+            atomicAdd(&lds[w][zbin], zc);
+        __syncthreads();
+        for (int b = threadIdx.x; b < kPdfSize; b += kBlock)
+        {
+            uint32_t s = 0;
+#pragma unroll
+            for (int i = 0; i < kWaves; ++i)
+                s += lds[i][b];
+            d.counts[c * kPdfSize + b] = s;
+        }
+        __syncthreads();
+    }
+}
+
+// UpdatePdf:277-287 -- pdf = (pdf * it + count / N) / (it + 1), double, per bin.
+__global__ __launch_bounds__(kPdfSize) void fold_histogram_kernel(TqDevice d, int64_t C, int64_t count)
+{
+    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+    {
+        if (!d.pdf_init[c])
+            continue;
+        int it          = d.iterations[c];
+        int64_t idx     = c * kPdfSize + threadIdx.x;
+        double prob     = (double) d.counts[idx] / (double) count;
+        d.pdf[idx]      = (d.pdf[idx] * it + prob) / (it + 1);
+        d.counts[idx]   = 0;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            d.iterations[c] = it + 1;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void reset_acc_kernel(double* acc, int64_t C)
+{
+    int64_t c = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (c < C)
+    {
+        acc[2 * c]     = DBL_MAX;    // TfEncodingAnalyzer.h:88
+        acc[2 * c + 1] = -DBL_MAX;   // TfEncodingAnalyzer.h:89
+    }
+}
+
+inline int grid_for_channels(int64_t C)
+{
+    return (int) (C < 65536 ? C : 65536);
+}
+
+}   // namespace
+
+void launch_batch_minmax(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, int skip_if_init,
+                         hipStream_t s)
+{
+    bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    if (C == 1)
+    {
+        int64_t n  = outer * K;
+        int blocks = stream_blocks(n, (int64_t) kBlock * 16);
+        if (blocks > kMinmaxParts)
+            blocks = kMinmaxParts;
+        minmax_tensor_kernel<<<blocks, kBlock, 0, s>>>(x, n, al ? 1 : 0, reinterpret_cast<float2*>(d.partials),
+                                                       d.pdf_init, skip_if_init);
+        AIMET_LAUNCH_CHECK();
+        minmax_combine_max_kernel<<<1, kBlock, 0, s>>>(reinterpret_cast<const float2*>(d.partials), blocks,
+                                                       reinterpret_cast<float2*>(d.minmax), d.pdf_init, skip_if_init);
+        AIMET_LAUNCH_CHECK();
+    }
+    else
+    {
+        int vec = (al && K % 4 == 0) ? 1 : 0;
+        minmax_channel_kernel<<<grid_for_channels(C), kBlock, 0, s>>>(x, outer, C, K, vec,
+                                                                      reinterpret_cast<float2*>(d.minmax), d.pdf_init,
+                                                                      skip_if_init);
+        AIMET_LAUNCH_CHECK();
+    }
+}
+
+void launch_fold_minmax(const TqDevice& d, int64_t C, bool tf_scheme, hipStream_t s)
+{
+    fold_minmax_kernel<<<(int) ceil_div(C, kBlock), kBlock, 0, s>>>(d, C, tf_scheme ? 1 : 0);
+    AIMET_LAUNCH_CHECK();
+}
+
+void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, hipStream_t s)
+{
+    bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
+    if (C == 1)
+    {
+        int64_t n  = outer * K;
+        // enough workgroups to fill the chip, few enough that the per-bin global atomics stay
+        // a small fraction of the pass (<= 512 x 512 64-bit adds)
+        int blocks = stream_blocks(n, (int64_t) kBlock * 32);
+        if (blocks > 512)
+            blocks = 512;
+        histogram_tensor_kernel<<<blocks, kBlock, 0, s>>>(x, n, al ? 1 : 0, d);
+    }
+    else
+    {
+        int vec = (al && K % 4 == 0) ? 1 : 0;
+        histogram_channel_kernel<<<grid_for_channels(C), kBlock, 0, s>>>(x, outer, C, K, vec, d);
+    }
+    AIMET_LAUNCH_CHECK();
+}
+
+void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStream_t s)
+{
+    fold_histogram_kernel<<<grid_for_channels(C), kPdfSize, 0, s>>>(d, C, count);
+    AIMET_LAUNCH_CHECK();
+}
+
+void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s)
+{
+    (void) hist;
+    reset_acc_kernel<<<(int) ceil_div(C, kBlock), kBlock, 0, s>>>(d.acc, C);
+    AIMET_LAUNCH_CHECK();
+}
+
+}   // namespace aimet_amd

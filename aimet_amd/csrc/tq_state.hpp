@@ -1,0 +1,42 @@
+// tq_state.hpp -- device-resident statistics of one aimet_tensor_quantizer (C channels).
+//
+// The reference keeps statistics on the host (TfEncodingAnalyzer::_accumulatedStats, PDF in a
+// std::vector) and synchronises the device 1-3x per updateStats (thrust D2H + histogram memcpy,
+// math_functions.cu:52-64,174-211). Here every field lives in HBM and updateStats is a chain
+// of stream-ordered kernels with no host round trip; only getEncoding reads them back.
+#pragma once
+
+#include "common.hpp"
+
+namespace aimet_amd
+{
+
+struct TqDevice
+{
+    // phase-1 output, exchanged between ranks with all_reduce(MAX): {-min, max} per channel
+    float* minmax;          // [C][2]
+    float* partials;        // [kMinmaxParts][2]   (C == 1: per-block partial {-min, max})
+    // TF analyzer (TfEncodingAnalyzer.h:86-91), double
+    double* acc;            // [C][2] {min, max}
+    // PDF (math_functions.hpp:70-77) of histogram analyzers
+    int32_t* pdf_init;      // [C] xLeft.size() != 0
+    int32_t* iterations;    // [C]
+    float* hist_min;        // [C] min_val of InitializePdf (xLeft[i] = min_val + i*bucket_size)
+    double* bucket_size;    // [C]
+    float* bin_bucket;      // [C] (float)(xLeft[1]-xLeft[0])      UpdatePdf:264
+    float* bin_offset;      // [C] (float)xLeft[0] / bin_bucket    UpdatePdf:265-268
+    double* pdf;            // [C][512]
+    unsigned long long* counts;   // [C][512] histogram of the current batch
+};
+
+constexpr int kMinmaxParts = 1024;   // grid of the per-tensor min/max pass
+
+// stats.hip
+void launch_batch_minmax(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, int skip_if_init,
+                         hipStream_t s);
+void launch_fold_minmax(const TqDevice& d, int64_t C, bool tf_scheme, hipStream_t s);
+void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, hipStream_t s);
+void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStream_t s);
+void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s);
+
+}   // namespace aimet_amd

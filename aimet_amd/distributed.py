@@ -1,0 +1,93 @@
+"""Calibration (compute_encodings statistics) sharded per sample across ranks.
+
+The reference forbids multi-GPU calibration (Docs/api_docs/torch_multi_gpu.rst:32) and runs
+each quantizer's statistics on one device. Here every rank reduces its shard of the batch on its
+own GPU and the ranks exchange only the reduced statistics, packed for ALL quantizers of the
+batch into one buffer per phase:
+
+  1. batch min/max          -> packed float32 {-min, max}   -> ONE all_reduce(MAX)
+  2. fold: TF running min/max; histogram schemes fix the 512-bucket PDF range on the first batch
+     from the GLOBAL min/max (so every rank bins identically)
+  3. batch histogram        -> packed int64 counts            -> ONE all_reduce(SUM)
+  4. fold: PDF running average with the GLOBAL element count
+
+Every rank ends with statistics identical to one device processing the whole batch (integer
+counts are order-independent; the double PDF recurrence sees the same inputs), hence identical
+encodings. Collectives run over torch.distributed ("nccl" = RCCL over xGMI on MI355X; "gloo" on
+CPU in the tests). Messages are tiny (8 B x C and 4 KiB x C per quantizer) and latency-bound, so
+the packing (2 collectives per batch instead of 2 per quantizer) is what matters.
+
+Quantizers are duck-typed: anything with ``num_channels``, ``uses_histogram``,
+``bind_exchange``, ``batch_minmax``, ``fold_minmax``, ``batch_histogram``, ``fold_histogram``.
+``AimetTensorQuantizer`` implements them on the gfx950 kernels.
+"""
+import torch
+import torch.distributed as dist
+
+PDF_SIZE = 512
+
+
+class PackedExchange:
+    """Packed exchange buffers for a fixed list of quantizers (bound once, reused every batch)."""
+
+    def __init__(self, quantizers, device):
+        self.quantizers = list(quantizers)
+        chans = [q.num_channels for q in self.quantizers]
+        self.minmax = torch.zeros(2 * sum(chans), dtype=torch.float32, device=device)
+        hist_ch = sum(c for q, c in zip(self.quantizers, chans) if q.uses_histogram)
+        self.counts = torch.zeros(PDF_SIZE * hist_ch, dtype=torch.int64, device=device)
+        m = h = 0
+        for q, c in zip(self.quantizers, chans):
+            mm = self.minmax[m:m + 2 * c]
+            cc = self.counts[h:h + PDF_SIZE * c] if q.uses_histogram else None
+            q.bind_exchange(mm, cc)
+            m += 2 * c
+            if q.uses_histogram:
+                h += PDF_SIZE * c
+
+
+def _world(group):
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def global_counts(local_counts, device, group=None):
+    """Per-quantizer element counts summed over ranks (one tiny collective)."""
+    t = torch.tensor(local_counts, dtype=torch.int64, device=device)
+    if _world(group) > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return t.tolist()
+
+
+def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange=None):
+    """One calibration batch: every rank passes ITS shard of each quantizer's tensor.
+
+    Equivalent to ``q.updateStats(whole_batch_tensor)`` on one device for every quantizer."""
+    if not quantizers:
+        return exchange
+    device = tensors[0].device
+    if exchange is None or exchange.quantizers != list(quantizers):
+        exchange = PackedExchange(quantizers, device)
+    ch_axes = ch_axes or [0] * len(quantizers)
+    world = _world(group)
+
+    for q, t, ax in zip(quantizers, tensors, ch_axes):
+        q.batch_minmax(t, ax)
+    if world > 1:
+        # {-min, max}: a single MAX reduces both ends exactly
+        dist.all_reduce(exchange.minmax, op=dist.ReduceOp.MAX, group=group)
+    for q in quantizers:
+        q.fold_minmax()
+
+    hist = [(q, t, ax) for q, t, ax in zip(quantizers, tensors, ch_axes) if q.uses_histogram]
+    if hist:
+        for q, t, ax in hist:
+            q.batch_histogram(t, ax)
+        local = [t.numel() // q.num_channels for q, t, _ in hist]
+        if world > 1:
+            dist.all_reduce(exchange.counts, op=dist.ReduceOp.SUM, group=group)
+            counts = global_counts(local, device, group)
+        else:
+            counts = local
+        for (q, _, _), n in zip(hist, counts):
+            q.fold_histogram(n)
+    return exchange

@@ -1,0 +1,390 @@
+"""Static-grid tensor quantizers and their autograd functions on the MI355X core.
+
+Mirrors the aimet_torch v1 surface that owns ``AimetTensorQuantizer`` objects
+(TrainingExtensions/torch/src/python/aimet_torch/v1/tensor_quantizer.py) and the STE gradient
+(v1/quantsim_straight_through_grad.py:66-118): same class names, properties and methods, same
+encoding/validity behaviour. MI355X-first changes:
+
+* a per-channel quantizer holds ONE native object with C analyzers (one stats launch per
+  tensor instead of C Python-level ``select().contiguous()`` + ``updateStats`` calls);
+* per-channel QDQ tables are built once per encoding change and kept in HBM;
+* the STE backward is one fused kernel (``grad * (min <= x <= max)``) instead of 3-4 torch
+  kernels plus a host->device copy of the per-channel bounds on every backward.
+"""
+import enum
+import io
+
+import torch
+
+from aimet_amd import _native
+from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding
+from aimet_amd.tensor_quantizer import (AimetTensorQuantizer, _require_gpu, _stream, per_channel_view,
+                                        qdq_per_channel_table)
+
+
+class QuantScheme(enum.Enum):
+    """aimet_common/defs.py:50-71."""
+    post_training_tf = 1
+    post_training_tf_enhanced = 2
+    training_range_learning_with_tf_init = 3
+    training_range_learning_with_tf_enhanced_init = 4
+    training_range_learning = 5
+    post_training_percentile = 6
+
+
+class QuantizationDataType(enum.Enum):
+    """aimet_common/defs.py:309-314."""
+    undefined = 0
+    int = 1
+    float = 2
+
+
+MAP_QUANT_SCHEME_TO_PYMO = {   # aimet_common/defs.py:70-78
+    QuantScheme.post_training_tf: QuantizationMode.QUANTIZATION_TF,
+    QuantScheme.post_training_tf_enhanced: QuantizationMode.QUANTIZATION_TF_ENHANCED,
+    QuantScheme.training_range_learning_with_tf_init: QuantizationMode.QUANTIZATION_TF,
+    QuantScheme.training_range_learning_with_tf_enhanced_init: QuantizationMode.QUANTIZATION_TF_ENHANCED,
+    QuantScheme.post_training_percentile: QuantizationMode.QUANTIZATION_PERCENTILE,
+}
+MAP_ROUND_MODE_TO_PYMO = {"nearest": RoundingMode.ROUND_NEAREST,   # aimet_common/defs.py:79-80
+                          "stochastic": RoundingMode.ROUND_STOCHASTIC}
+
+
+def _pymo_mode(quant_scheme):
+    if isinstance(quant_scheme, QuantScheme):
+        return MAP_QUANT_SCHEME_TO_PYMO[quant_scheme]
+    return QuantizationMode(int(quant_scheme))
+
+
+def _round_mode(rm):
+    if isinstance(rm, str):
+        return MAP_ROUND_MODE_TO_PYMO[rm]
+    return RoundingMode(int(rm))
+
+
+class StaticGridTensorQuantizer:
+    """v1/tensor_quantizer.py:132-401."""
+
+    def __init__(self, bitwidth, round_mode, quant_scheme, use_symmetric_encodings, enabled_by_default,
+                 data_type=QuantizationDataType.int):
+        self.round_mode = _round_mode(round_mode)
+        self._quant_scheme = quant_scheme
+        self.use_symmetric_encodings = use_symmetric_encodings
+        self.use_strict_symmetric = False
+        self.use_unsigned_symmetric = False
+        self.is_unsigned_symmetric = False
+        self.bitwidth = bitwidth
+        self.enabled = enabled_by_default
+        self.data_type = data_type
+        self.is_const = False
+        self._encoding_min_max_fixed_vals = None
+        self._is_encoding_frozen = False
+        self._encoding = None
+        self._cppOp = None
+
+    def __str__(self):
+        s = io.StringIO()
+        s.write("StaticGrid TensorQuantizer:\n")
+        s.write("    quant-scheme:{}, round_mode={}, bitwidth={}, enabled={}\n".format(
+            self._quant_scheme, self.round_mode, self.bitwidth, self.enabled))
+        if self._encoding:
+            for e in self._encoding:
+                s.write("    min:{}, max={}, delta={}, offset={}\n".format(e.min, e.max, e.delta, e.offset))
+        else:
+            s.write("    no encoding\n")
+        return s.getvalue()
+
+    @property
+    def quant_scheme(self):
+        return self._quant_scheme
+
+    @quant_scheme.setter
+    def quant_scheme(self, quant_scheme):
+        self._quant_scheme = quant_scheme
+        self._make_op()
+
+    @property
+    def is_encoding_frozen(self):
+        return self._is_encoding_frozen
+
+    @property
+    def channel_axis(self):
+        return None
+
+    @property
+    def encoding_min_max_fixed_vals(self):
+        return self._encoding_min_max_fixed_vals
+
+    @encoding_min_max_fixed_vals.setter
+    def encoding_min_max_fixed_vals(self, vals):
+        if not (isinstance(vals, tuple) and len(vals) == 2 and vals[0] < vals[1]):
+            raise AssertionError("Min max vals must be a tuple of two increasing values")
+        if self.quant_scheme != QuantScheme.post_training_tf:
+            self.quant_scheme = QuantScheme.post_training_tf
+        self._encoding_min_max_fixed_vals = vals
+
+    def _make_op(self):
+        raise NotImplementedError
+
+    def _encodings_from_op(self):
+        """(encodings, valid) from the native analyzers."""
+        raise NotImplementedError
+
+    def compute_encoding(self):
+        """v1/tensor_quantizer.py:280-321."""
+        if not self.enabled or self._is_encoding_frozen:
+            return
+        if self.bitwidth == 32:
+            self._encoding = None
+            return
+        if self.data_type == QuantizationDataType.float:
+            if self.bitwidth == 16:
+                self._encoding = None
+            elif self.bitwidth == 8:
+                self._encoding = [TfEncoding()]
+            else:
+                raise ValueError("Only bitwidths [8, 16] allowed for float data type, not ", str(self.bitwidth))
+            return
+        encodings, valid = self._encodings_from_op()
+        self._encoding = []
+        if not valid:
+            self.enabled = False
+        else:
+            self._encoding = encodings
+        self.is_unsigned_symmetric = (self.use_symmetric_encodings and self.use_unsigned_symmetric and
+                                      all(e.min >= 0 and e.max >= 0 for e in self._encoding))
+
+    def quantize_dequantize(self, tensor, round_mode):
+        return QuantizeDequantize.apply(tensor, self, _round_mode(round_mode))
+
+    def quantize(self, tensor, round_mode):
+        return Quantize.apply(tensor, self, _round_mode(round_mode))
+
+    def reset_encoding_stats(self):
+        if not self._is_encoding_frozen:
+            self._op().resetEncodingStats()
+            self._encoding = None
+
+    def get_stats_histogram(self):
+        if self._quant_scheme != QuantScheme.post_training_tf_enhanced:
+            raise RuntimeError("get_stats_histogram() can be invoked only when quantization scheme is TF-Enhanced.")
+        if not self._encoding:
+            raise RuntimeError("get_stats_histogram() can be invoked only when encoding is computed.")
+        op = self._op()
+        return [op.getStatsHistogram(c) for c in range(op.num_channels)]
+
+    def freeze_encoding(self):
+        if not self._encoding:
+            raise RuntimeError("Encoding can be frozen only when it is not None.")
+        self._is_encoding_frozen = True
+
+    def set_percentile_value(self, percentile_value):
+        self._op().setPercentileValue(percentile_value)
+
+    def _op(self) -> AimetTensorQuantizer:
+        return self._cppOp[0]
+
+
+class StaticGridPerTensorQuantizer(StaticGridTensorQuantizer):
+    """v1/tensor_quantizer.py:403-481."""
+
+    def __init__(self, bitwidth, round_mode, quant_scheme, use_symmetric_encodings, enabled_by_default,
+                 data_type=QuantizationDataType.int):
+        super().__init__(bitwidth, round_mode, quant_scheme, use_symmetric_encodings, enabled_by_default, data_type)
+        self._make_op()
+
+    def _make_op(self):
+        self._cppOp = [AimetTensorQuantizer(_pymo_mode(self._quant_scheme))]
+
+    @property
+    def encoding(self):
+        return self._encoding[0] if self._encoding else None
+
+    @encoding.setter
+    def encoding(self, encoding):
+        if self._is_encoding_frozen:
+            raise RuntimeError("Encoding can be set only when it is not frozen.")
+        if isinstance(encoding, list) and len(encoding) == 1:
+            self._encoding = encoding
+        else:
+            self._encoding = [encoding]
+
+    def update_encoding_stats(self, tensor):
+        """v1/tensor_quantizer.py:452-481."""
+        if not self.enabled or self._is_encoding_frozen or self.bitwidth == 32:
+            return
+        if self.data_type == QuantizationDataType.float:
+            raise NotImplementedError("float (fp8/fp16) quantization is outside the MI355X integer QDQ core")
+        if self.encoding_min_max_fixed_vals is not None:
+            tensor = torch.tensor(list(self.encoding_min_max_fixed_vals), device=tensor.device)
+        if tensor.dtype in (torch.float16, torch.bfloat16):
+            tensor = tensor.to(torch.float32)
+        self._op().updateStats(tensor, tensor.is_cuda)
+
+    def _encodings_from_op(self):
+        enc, valid = self._op().getEncoding(self.bitwidth, self.use_symmetric_encodings, self.use_strict_symmetric,
+                                            self.use_unsigned_symmetric)
+        return [enc], valid
+
+
+class StaticGridPerChannelQuantizer(StaticGridTensorQuantizer):
+    """v1/tensor_quantizer.py:483-571."""
+
+    def __init__(self, bitwidth, round_mode, quant_scheme, use_symmetric_encodings, num_channels,
+                 enabled_by_default, ch_axis=0, data_type=QuantizationDataType.int):
+        super().__init__(bitwidth, round_mode, quant_scheme, use_symmetric_encodings, enabled_by_default, data_type)
+        self._num_channels = int(num_channels)
+        self._ch_axis = ch_axis
+        self._make_op()
+
+    def _make_op(self):
+        self._cppOp = [AimetTensorQuantizer(_pymo_mode(self._quant_scheme), num_channels=self._num_channels)]
+
+    @property
+    def encoding(self):
+        return self._encoding
+
+    @encoding.setter
+    def encoding(self, encoding):
+        if self._is_encoding_frozen:
+            raise RuntimeError("Encoding can be set only when it is not frozen.")
+        self._encoding = encoding
+
+    @property
+    def channel_axis(self):
+        return self._ch_axis
+
+    def update_encoding_stats(self, tensor):
+        """v1/tensor_quantizer.py:535-571, all channels in one launch."""
+        if not self.enabled or self._is_encoding_frozen or self.bitwidth == 32:
+            return
+        if self.data_type == QuantizationDataType.float:
+            raise NotImplementedError("float (fp8/fp16) quantization is outside the MI355X integer QDQ core")
+        if tensor.dtype in (torch.float16, torch.bfloat16):
+            tensor = tensor.to(torch.float32)
+        if self.encoding_min_max_fixed_vals is not None:
+            # every channel analyzer sees the same 2-element tensor (v1/tensor_quantizer.py:556-561)
+            fixed = torch.tensor(list(self.encoding_min_max_fixed_vals), device=tensor.device)
+            tensor = fixed.view(1, 2).expand(self._num_channels, 2).contiguous()
+            self._op().updateStatsPerChannel(tensor, 0)
+            return
+        self._op().updateStatsPerChannel(tensor, self._ch_axis)
+
+    def _encodings_from_op(self):
+        return self._op()._get_encodings(self.bitwidth, self.use_symmetric_encodings, self.use_strict_symmetric,
+                                         self.use_unsigned_symmetric)
+
+    def channel_table(self, device):
+        return self._op().channelTable(self._encoding, device)
+
+
+# ---------------------------------------------------------------------------------------------
+# autograd
+# ---------------------------------------------------------------------------------------------
+def compute_dloss_by_dx(x, grad, encoding_min, encoding_max, ch_axis=0):
+    """quantsim_straight_through_grad.py:91-118 as one kernel: grad * (min <= x <= max).
+
+    encoding_min/max: python floats (per-tensor) or sequences / float32 tensors of C values."""
+    _require_gpu(x, True, "x")
+    _require_gpu(grad, True, "grad")
+    x = x.contiguous()
+    grad = grad.contiguous()
+    out = torch.empty_like(grad)
+    if isinstance(encoding_min, (int, float)) or (torch.is_tensor(encoding_min) and encoding_min.numel() == 1):
+        mn = float(encoding_min)
+        mx = float(encoding_max)
+        # torch.tensor(python float) is float32: the comparison bounds are rounded to float
+        with torch.cuda.device(x.device):
+            _native.call("aimet_ste_backward_per_tensor", x.data_ptr(), grad.data_ptr(), out.data_ptr(), x.numel(),
+                         mn, mx, _stream(x))
+        return out
+    mins = torch.as_tensor(encoding_min, dtype=torch.float32).to(x.device).contiguous()
+    maxs = torch.as_tensor(encoding_max, dtype=torch.float32).to(x.device).contiguous()
+    outer, C, K = per_channel_view(x.shape, ch_axis)
+    if mins.numel() != C:
+        raise ValueError("expected %d per-channel bounds, got %d" % (C, mins.numel()))
+    with torch.cuda.device(x.device):
+        _native.call("aimet_ste_backward", x.data_ptr(), grad.data_ptr(), out.data_ptr(), outer, C, K,
+                     mins.data_ptr(), maxs.data_ptr(), _stream(x))
+    return out
+
+
+def _ste_bounds(tq, device):
+    """float32 per-channel STE bounds = the raw encoding min/max (the QDQ table holds the gated
+    ones), cached until any encoding changes (the reference re-uploads them every backward,
+    quantsim_straight_through_grad.py:75-76)."""
+    key = (id(tq._encoding), TfEncoding._version, device)
+    cache = getattr(tq, "_ste_cache", None)
+    if cache is None or cache[0] != key:
+        mins = torch.tensor([e.min for e in tq._encoding], dtype=torch.float32, device=device)
+        maxs = torch.tensor([e.max for e in tq._encoding], dtype=torch.float32, device=device)
+        tq._ste_cache = (key, mins, maxs)
+    return tq._ste_cache[1], tq._ste_cache[2]
+
+
+class QuantizeDequantize(torch.autograd.Function):
+    """v1/tensor_quantizer.py:1098-1213."""
+
+    @staticmethod
+    def forward(ctx, tensor, tensor_quantizer, round_mode):
+        tq = tensor_quantizer
+        ctx.tensor_quantizer = tq
+        if not tq.enabled or tq.bitwidth == 32:
+            return tensor
+        if tq.data_type == QuantizationDataType.float:
+            if tq.bitwidth == 16:
+                out = tensor.half().float()
+                ctx.save_for_backward(tensor)
+                return out
+            raise NotImplementedError("fp8 quantization is outside the MI355X integer QDQ core")
+        dtype = tensor.dtype
+        t = tensor.to(torch.float32)
+        if isinstance(tq, StaticGridPerChannelQuantizer):
+            t = t.contiguous()
+            outer, C, K = per_channel_view(t.shape, tq.channel_axis)
+            table = tq.channel_table(t.device)
+            out = qdq_per_channel_table(t, table, outer, C, K, round_mode)
+        else:
+            out = AimetTensorQuantizer.quantize_dequantize_tensor(t, tq.encoding, round_mode)
+        ctx.save_for_backward(tensor)
+        return out.to(dtype)
+
+    @staticmethod
+    def backward(ctx, grad):
+        tq = ctx.tensor_quantizer
+        if tq.enabled and tq.data_type == QuantizationDataType.int and tq.bitwidth != 32:
+            (x,) = ctx.saved_tensors
+            dtype = grad.dtype
+            xf = x.to(torch.float32)
+            gf = grad.to(torch.float32)
+            if isinstance(tq, StaticGridPerChannelQuantizer):
+                mins, maxs = _ste_bounds(tq, x.device)
+                g = compute_dloss_by_dx(xf, gf, mins, maxs, tq.channel_axis)
+            else:
+                g = compute_dloss_by_dx(xf, gf, tq.encoding.min, tq.encoding.max)
+            return g.to(dtype), None, None
+        return grad, None, None
+
+
+class Quantize(torch.autograd.Function):
+    """v1/tensor_quantizer.py:1216-1264 (quantize-only, STE gradient)."""
+
+    @staticmethod
+    def forward(ctx, tensor, tensor_quantizer, round_mode):
+        tq = tensor_quantizer
+        ctx.tensor_quantizer = tq
+        shift_to_signed = not (tq.use_symmetric_encodings and tq.use_unsigned_symmetric)
+        if isinstance(tq, StaticGridPerChannelQuantizer):
+            outs = []
+            for c, enc in enumerate(tq.encoding):
+                sl = tensor.select(tq.channel_axis, c).contiguous()
+                outs.append(tq._op().quantize(sl, enc, round_mode, True, shift_to_signed))
+            out = torch.stack(outs, dim=tq.channel_axis)
+        else:
+            out = tq._op().quantize(tensor.to(torch.float32), tq.encoding, round_mode, True, shift_to_signed)
+        ctx.save_for_backward(tensor)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad):
+        return QuantizeDequantize.backward(ctx, grad)

@@ -1,0 +1,325 @@
+"""Drop-in for the ``AimetTensorQuantizer`` torch extension
+(TrainingExtensions/torch/src/AimetTensorQuantizer.cpp:79-331).
+
+Same class name, method names and argument meaning. Differences, all MI355X-first:
+
+* statistics stay in HBM (no host synchronisation in ``updateStats``);
+* kernels run on torch's *current* HIP stream of the tensor's device (the reference used the
+  legacy default stream);
+* one object may hold the analyzers of C channels (``num_channels``), updated in one launch by
+  ``updateStatsPerChannel`` -- the reference needed C objects and a Python loop;
+* there is no CPU path: CPU tensors / ``use_cuda=False`` raise ``RuntimeError``.
+"""
+import ctypes
+import itertools
+
+import torch
+
+from aimet_amd import _native
+from aimet_amd._native import TfEncodingC
+from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding, encodings_to_c
+
+_seed_counter = itertools.count(1)
+
+
+def _stream(t: torch.Tensor) -> int:
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _require_gpu(t: torch.Tensor, use_cuda: bool = True, what: str = "input"):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("%s must be a torch.Tensor" % what)
+    if not t.is_cuda or not use_cuda:
+        raise RuntimeError("aimet_amd: %s must be a HIP (cuda) tensor with use_cuda=True; the MI355X core has no "
+                           "CPU path" % what)
+    if t.dtype != torch.float32:
+        raise TypeError("aimet_amd: %s must be float32 (got %s); upcast as the reference callers do "
+                        "(v1/tensor_quantizer.py:1124)" % (what, t.dtype))
+
+
+def per_channel_view(shape, ch_axis):
+    """[outer][C][K] triple of a tensor quantized along ch_axis (v1/tensor_quantizer.py:1150-1153)."""
+    sizes = list(shape)
+    if ch_axis < 0:
+        ch_axis += len(sizes)
+    outer = 1
+    for s in sizes[:ch_axis]:
+        outer *= s
+    K = 1
+    for s in sizes[ch_axis + 1:]:
+        K *= s
+    return outer, sizes[ch_axis], K
+
+
+class PerChannelTable:
+    """Device table [4][C] {min, max, delta, offset} built once per encoding change
+    (AimetTensorQuantizer.cpp:262-299 rebuilt and re-uploaded it on every call)."""
+
+    def __init__(self):
+        self._key = None
+        self.table = None
+
+    def get(self, encodings, device):
+        key = (id(encodings), len(encodings), TfEncoding._version, device)
+        if self._key != key or self.table is None:
+            C = len(encodings)
+            table = torch.empty((4, C), dtype=torch.float32, device=device)
+            _native.call("aimet_per_channel_table", encodings_to_c(encodings), C, table.data_ptr(),
+                         torch.cuda.current_stream(device).cuda_stream)
+            self.table, self._key = table, key
+        return self.table
+
+
+class AimetTensorQuantizer:
+    """AimetTensorQuantizer(quant_scheme[, num_channels]) -- AimetTensorQuantizer.cpp:82-87."""
+
+    def __init__(self, quant_scheme, num_channels: int = 1, device=None):
+        self._scheme = QuantizationMode(int(quant_scheme))
+        self._num_channels = int(num_channels)
+        self._device = device
+        self._handle = None
+        self._is_encoding_valid = False
+        self._pc_table = PerChannelTable()
+        self._pending_percentile = None
+
+    # -- lifetime ------------------------------------------------------------------------------
+    def _ensure(self, device: torch.device):
+        idx = device.index if device.index is not None else torch.cuda.current_device()
+        if self._handle is not None and self._device == idx:
+            return self._handle
+        if self._handle is not None:
+            # statistics live on one device; moving devices starts from empty statistics
+            self._release()
+        h = ctypes.c_void_p()
+        _native.call("aimet_tq_create", int(self._scheme), self._num_channels, idx, ctypes.byref(h))
+        self._handle, self._device = h, idx
+        if self._pending_percentile is not None:
+            _native.call("aimet_tq_set_percentile_value", self._handle, float(self._pending_percentile))
+        return h
+
+    def _release(self):
+        if self._handle is not None:
+            try:
+                _native.call("aimet_tq_destroy", self._handle)
+            finally:
+                self._handle = None
+
+    def __del__(self):
+        try:
+            self._release()
+        except Exception:  # interpreter shutdown
+            pass
+
+    def __getstate__(self):
+        raise TypeError("AimetTensorQuantizer holds device state and is not picklable "
+                        "(the reference drops it in StaticGridTensorQuantizer.__getstate__)")
+
+    @property
+    def num_channels(self):
+        return self._num_channels
+
+    @property
+    def quant_scheme(self):
+        return self._scheme
+
+    # -- statistics --------------------------------------------------------------------------
+    def resetEncodingStats(self):
+        """AimetTensorQuantizer.cpp:89-96."""
+        self._is_encoding_valid = False
+        self._pending_percentile = None
+        if self._handle is not None:
+            with torch.cuda.device(self._device):
+                _native.call("aimet_tq_reset_encoding_stats", self._handle,
+                             torch.cuda.current_stream(self._device).cuda_stream)
+
+    def updateStats(self, tensor: torch.Tensor, use_cuda: bool = True):
+        """AimetTensorQuantizer.cpp:98-127 (per-tensor; the whole tensor feeds one analyzer)."""
+        if self._num_channels != 1:
+            raise ValueError("updateStats on a %d-channel quantizer: use updateStatsPerChannel" % self._num_channels)
+        _require_gpu(tensor, use_cuda)
+        t = tensor if tensor.is_contiguous() else tensor.contiguous()
+        h = self._ensure(t.device)
+        with torch.cuda.device(t.device):
+            _native.call("aimet_tq_update_stats", h, t.data_ptr(), 1, 1, t.numel(), _stream(t))
+        self._is_encoding_valid = True
+
+    def updateStatsPerChannel(self, tensor: torch.Tensor, ch_axis: int = 0, use_cuda: bool = True):
+        """All C channel analyzers in one pass: replaces the loop of
+        v1/tensor_quantizer.py:567-570 (select(ch_axis, c).contiguous() + updateStats per channel)."""
+        _require_gpu(tensor, use_cuda)
+        t = tensor if tensor.is_contiguous() else tensor.contiguous()
+        outer, C, K = per_channel_view(t.shape, ch_axis)
+        if C != self._num_channels:
+            raise ValueError("tensor has %d channels along axis %d, quantizer has %d" % (C, ch_axis,
+                                                                                         self._num_channels))
+        h = self._ensure(t.device)
+        with torch.cuda.device(t.device):
+            _native.call("aimet_tq_update_stats", h, t.data_ptr(), outer, C, K, _stream(t))
+        self._is_encoding_valid = True
+
+    # -- phased statistics (sharded calibration, aimet_amd.distributed) ------------------------
+    @property
+    def uses_histogram(self):
+        return self._scheme != QuantizationMode.QUANTIZATION_TF
+
+    def _view(self, tensor, ch_axis):
+        _require_gpu(tensor)
+        t = tensor if tensor.is_contiguous() else tensor.contiguous()
+        if self._num_channels == 1:
+            return t, (1, 1, t.numel())
+        outer, C, K = per_channel_view(t.shape, ch_axis)
+        if C != self._num_channels:
+            raise ValueError("tensor has %d channels, quantizer has %d" % (C, self._num_channels))
+        return t, (outer, C, K)
+
+    def bind_exchange(self, minmax: torch.Tensor, counts: torch.Tensor = None):
+        """Keep this quantizer's exchanged statistics in slices of caller-owned packed buffers:
+        minmax float32[2*C], counts int64[512*C] (zeroed)."""
+        h = self._ensure(minmax.device)
+        _native.call("aimet_tq_bind_exchange", h, minmax.data_ptr(),
+                     counts.data_ptr() if counts is not None else None)
+        self._bound = (minmax, counts)   # keep the memory alive
+
+    def batch_minmax(self, tensor, ch_axis=0):
+        t, (outer, C, K) = self._view(tensor, ch_axis)
+        h = self._ensure(t.device)
+        _native.call("aimet_tq_batch_minmax", h, t.data_ptr(), outer, C, K, _stream(t))
+        self._is_encoding_valid = True
+
+    def fold_minmax(self):
+        _native.call("aimet_tq_fold_minmax", self._handle, torch.cuda.current_stream(self._device).cuda_stream)
+
+    def batch_histogram(self, tensor, ch_axis=0):
+        t, (outer, C, K) = self._view(tensor, ch_axis)
+        _native.call("aimet_tq_batch_histogram", self._ensure(t.device), t.data_ptr(), outer, C, K, _stream(t))
+
+    def fold_histogram(self, count_per_channel: int):
+        _native.call("aimet_tq_fold_histogram", self._handle, int(count_per_channel),
+                     torch.cuda.current_stream(self._device).cuda_stream)
+
+    def getEncoding(self, bitwidth, use_symmetric_encodings, use_strict_symmetric, use_unsigned_symmetric):
+        """AimetTensorQuantizer.cpp:180-192 -> (TfEncoding, is_valid). Per-channel objects return a
+        list of C encodings."""
+        encs, valid = self._get_encodings(bitwidth, use_symmetric_encodings, use_strict_symmetric,
+                                          use_unsigned_symmetric)
+        if self._num_channels == 1:
+            return encs[0], valid
+        return encs, valid
+
+    def _get_encodings(self, bw, sym, strict, unsign):
+        C = self._num_channels
+        if self._handle is None or not self._is_encoding_valid:
+            return [TfEncoding() for _ in range(C)], False
+        out = (TfEncodingC * C)()
+        valid = ctypes.c_int(0)
+        with torch.cuda.device(self._device):
+            _native.call("aimet_tq_get_encoding", self._handle, int(bw), int(bool(sym)), int(bool(strict)),
+                         int(bool(unsign)), out, ctypes.byref(valid),
+                         torch.cuda.current_stream(self._device).cuda_stream)
+        return [TfEncoding.from_c(out[i]) for i in range(C)], bool(valid.value)
+
+    def getStatsHistogram(self, channel: int = 0):
+        """AimetTensorQuantizer.cpp:194-198 -> list of (xLeft, pdf)."""
+        import numpy as np
+        if self._handle is None:
+            if self._scheme == QuantizationMode.QUANTIZATION_TF:
+                raise RuntimeError("the TF encoding analyzer keeps no histogram (TfEncodingAnalyzer.cpp:53-57)")
+            return []
+        xl = np.zeros(512, dtype=np.float64)
+        pdf = np.zeros(512, dtype=np.float64)
+        n = ctypes.c_int(0)
+        with torch.cuda.device(self._device):
+            _native.call("aimet_tq_get_stats_histogram", self._handle, int(channel),
+                         xl.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                         pdf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(n),
+                         torch.cuda.current_stream(self._device).cuda_stream)
+        return [(float(xl[i]), float(pdf[i])) for i in range(n.value)]
+
+    def setPercentileValue(self, percentile: float):
+        """AimetTensorQuantizer.cpp:200-207 (percentile scheme only)."""
+        if self._scheme != QuantizationMode.QUANTIZATION_PERCENTILE:
+            return
+        self._pending_percentile = float(percentile)
+        if self._handle is not None:
+            _native.call("aimet_tq_set_percentile_value", self._handle, float(percentile))
+
+    def getPercentileValue(self) -> float:
+        if self._scheme != QuantizationMode.QUANTIZATION_PERCENTILE:
+            raise RuntimeError("Percentile Value only exists in case of percentile quant scheme.")
+        return 100.0 if self._pending_percentile is None else self._pending_percentile
+
+    # -- quantize-dequantize -----------------------------------------------------------------
+    @staticmethod
+    def quantize_dequantize_tensor(tensor, encoding, round_mode=RoundingMode.ROUND_NEAREST, out=None):
+        _require_gpu(tensor)
+        t = tensor.contiguous(memory_format=_suggest_memory_format(tensor))
+        if out is None:
+            out = torch.empty_like(t)
+        seed = next(_seed_counter) if int(round_mode) == RoundingMode.ROUND_STOCHASTIC else 0
+        with torch.cuda.device(t.device):
+            _native.call("aimet_qdq_per_tensor", t.data_ptr(), out.data_ptr(), t.numel(), encoding.to_c(),
+                         int(round_mode), seed, _stream(t))
+        return out
+
+    def quantizeDequantize(self, tensor, encoding, round_mode, use_cuda=True):
+        """AimetTensorQuantizer.cpp:129-155: new output tensor, uses encoding.min/max/bw."""
+        _require_gpu(tensor, use_cuda)
+        t = tensor.contiguous(memory_format=_suggest_memory_format(tensor))
+        return AimetTensorQuantizer.quantize_dequantize_tensor(t, encoding, round_mode)
+
+    def quantize(self, tensor, encoding, round_mode, use_cuda=True, shift_to_signed=False):
+        """AimetTensorQuantizer.cpp:157-178: float tensor of integer codes."""
+        _require_gpu(tensor, use_cuda)
+        t = tensor.contiguous(memory_format=_suggest_memory_format(tensor))
+        out = torch.empty_like(t)
+        seed = next(_seed_counter) if int(round_mode) == RoundingMode.ROUND_STOCHASTIC else 0
+        with torch.cuda.device(t.device):
+            _native.call("aimet_quantize_per_tensor", t.data_ptr(), out.data_ptr(), t.numel(), encoding.to_c(),
+                         int(round_mode), int(bool(shift_to_signed)), seed, _stream(t))
+        return out
+
+    def makeDeltaOffsetTensor(self, device, encodings):
+        """AimetTensorQuantizer.cpp:209-231 -> (delta[C], offset[C]) float32 on `device`."""
+        device = torch.device(device)
+        C = len(encodings)
+        if device.type != "cuda":
+            raise RuntimeError("aimet_amd: makeDeltaOffsetTensor needs a HIP device")
+        table = torch.empty((2, C), dtype=torch.float32, device=device)
+        with torch.cuda.device(device):
+            _native.call("aimet_make_delta_offset", encodings_to_c(encodings), C, table.data_ptr(),
+                         torch.cuda.current_stream(device).cuda_stream)
+        return table[0], table[1]
+
+    def channelTable(self, encodings, device):
+        """Device table [4][C] for per-channel QDQ/STE, cached until any encoding changes."""
+        return self._pc_table.get(encodings, torch.device(device))
+
+    def quantizeDequantizePerChannel(self, tensor, encodings, num_channel, num_element, num_element_per_channel,
+                                     round_mode, use_cuda=True):
+        """AimetTensorQuantizer.cpp:233-307 (numChannel, numElement, numElementPerChannel)."""
+        _require_gpu(tensor, use_cuda)
+        t = tensor.contiguous()
+        C, N, K = int(num_channel), int(num_element), int(num_element_per_channel)
+        if len(encodings) != C:
+            raise ValueError("expected %d encodings, got %d" % (C, len(encodings)))
+        if C * K == 0 or N % (C * K) != 0 or N != t.numel():
+            raise ValueError("inconsistent per-channel shape: numElement=%d numChannel=%d "
+                             "numElementPerChannel=%d" % (N, C, K))
+        table = self.channelTable(encodings, t.device)
+        return qdq_per_channel_table(t, table, N // (C * K), C, K, round_mode)
+
+
+def qdq_per_channel_table(t, table, outer, C, K, round_mode=RoundingMode.ROUND_NEAREST, out=None):
+    if out is None:
+        out = torch.empty_like(t)
+    seed = next(_seed_counter) if int(round_mode) == RoundingMode.ROUND_STOCHASTIC else 0
+    with torch.cuda.device(t.device):
+        _native.call("aimet_qdq_per_channel", t.data_ptr(), out.data_ptr(), outer, C, K, table.data_ptr(),
+                     int(round_mode), seed, _stream(t))
+    return out
+
+
+def _suggest_memory_format(t):
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last) and not t.is_contiguous():
+        return torch.channels_last
+    return torch.contiguous_format

@@ -1,0 +1,243 @@
+"""bench.py -- fake-quant throughput of the MI355X quantization-simulation core.
+
+Workload (BASELINE.json configs[1]): ResNet-50 W8A8 fake-quant forward, synthetic 224x224 batch of
+256 per GPU, i.e. every tensor QuantizationSimModel quantize-dequantizes in one forward:
+  * the model input + the 54 conv/fc outputs, per-tensor 8-bit (2.884 G elements), and
+  * the 54 conv/fc weights, per-channel (axis 0) symmetric 8-bit (25.5 M elements, 27,560 channels).
+Activations come from one real fp32 forward of a random-init ResNet-50 (seed 0) on U(0,1) images
+(seed 1234 + rank) and stay resident in HBM; a "step" quantize-dequantizes all of them once.
+Encodings are computed first (TF-Enhanced activations, TF-Enhanced per-channel weights =
+QuantizationSimModel's default scheme) and that compute_encodings wall-clock is reported too.
+
+Multi-GPU: one process per GPU (torch.distributed, RCCL). Each rank runs its own batch (weak
+scaling, no data-path collective); calibration is sharded per sample across ranks with one RCCL
+exchange of the packed statistics per batch (aimet_amd.distributed).
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+BYTES_QDQ = 8            # fp32 read + fp32 write per element
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=256)
+    p.add_argument("--calib-batches", type=int, default=1,
+                   help="calibration batches for the compute_encodings timing")
+    p.add_argument("--cpu-sample-images", type=int, default=32,
+                   help="images of each activation tensor (plus all weights) timed on the CPU oracle")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--profile-steps", action="store_true", help="short run for rocprofv3")
+    return p.parse_args()
+
+
+def setup_dist(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    return rank, world, torch.device("cuda", local)
+
+
+def collect_tensors(model, x):
+    """Run the fp32 forward once; keep the model input and every conv/fc output resident."""
+    acts = [("input", x)]
+    hooks = []
+    for name, mod in model.named_modules():
+        if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear)):
+            hooks.append(mod.register_forward_hook(
+                lambda m, i, o, name=name: acts.append((name, o.detach().contiguous()))))
+    with torch.no_grad():
+        model(x)
+    for h in hooks:
+        h.remove()
+    weights = [(name, mod.weight.detach().contiguous()) for name, mod in model.named_modules()
+               if isinstance(mod, (torch.nn.Conv2d, torch.nn.Linear))]
+    return acts, weights
+
+
+def compute_encodings(acts, weights, world):
+    """compute_encodings as QuantizationSimModel does it for this workload (v1/quantsim.py:425-449):
+    TF-Enhanced stats for every activation, TF-Enhanced per-channel symmetric for every weight."""
+    from aimet_amd import distributed as D
+    from aimet_amd.libpymo import QuantizationMode
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    aq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in acts]
+    wq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=w.shape[0])
+          for _, w in weights]
+    if world > 1:
+        D.sharded_update_stats(aq, [t for _, t in acts])
+    else:
+        for q, (_, t) in zip(aq, acts):
+            q.updateStats(t, True)
+    for q, (_, w) in zip(wq, weights):
+        q.updateStatsPerChannel(w, 0, True)
+    act_enc = [q.getEncoding(8, False, False, False)[0] for q in aq]
+    w_enc = [q.getEncoding(8, True, False, False)[0] for q in wq]
+    torch.cuda.synchronize()
+    return act_enc, w_enc, time.perf_counter() - t0, aq, wq
+
+
+def cpu_baseline(acts, weights, act_enc, w_enc, images):
+    """The CPU restatement of the reference (oracle/, single thread) on a bounded sample."""
+    from oracle import oracle as O
+    xs, ws = [], []
+    for (name, t), e in zip(acts, act_enc):
+        xs.append((t[:images].cpu().numpy().ravel(), e))
+    for (name, w), encs in zip(weights, w_enc):
+        ws.append((w.cpu().numpy().ravel(), w.shape[0], w[0].numel(),
+                   O.per_channel_table([e.to_tuple() for e in encs])))
+    n = sum(x.size for x, _ in xs) + sum(w.size for w, _, _, _ in ws)
+    t0 = time.perf_counter()
+    for x, e in xs:
+        O.qdq_per_tensor(x, e.min, e.max, 8)
+    for w, C, K, tab in ws:
+        O.qdq_per_channel(w, C, K, tab)
+    dt = time.perf_counter() - t0
+    return n / dt / 1e9, n, dt
+
+
+def main():
+    args = parse()
+    rank, world, dev = setup_dist(args)
+    import aimet_amd
+    from aimet_amd import _native
+    from aimet_amd._native import TfEncodingC
+    from workloads.resnet import resnet50
+
+    lib = aimet_amd.native_library()
+    torch.manual_seed(1234 + rank)
+    model = resnet50(seed=0, device=dev)
+    x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=torch.Generator(device=dev).manual_seed(1234 + rank))
+    acts, weights = collect_tensors(model, x)
+    del model
+    torch.cuda.empty_cache()
+
+    act_enc, w_enc, enc_seconds, aq, wq = compute_encodings(acts, weights, world)
+
+    # ---- the step: every QDQ of one QuantSim forward, pre-bound C-ABI calls --------------------
+    stream = torch.cuda.current_stream(dev)
+    sptr = ctypes.c_void_p(stream.cuda_stream)
+    act_calls, w_calls = [], []
+    outs = []
+    for (name, t), e in zip(acts, act_enc):
+        o = torch.empty_like(t)
+        outs.append(o)
+        act_calls.append((ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(o.data_ptr()), t.numel(), e.to_c()))
+    for ((name, w), encs), q in zip(zip(weights, w_enc), wq):
+        o = torch.empty_like(w)
+        outs.append(o)
+        table = q.channelTable(encs, dev)
+        outs.append(table)
+        w_calls.append((ctypes.c_void_p(w.data_ptr()), ctypes.c_void_p(o.data_ptr()), 1, w.shape[0], w[0].numel(),
+                        ctypes.c_void_p(table.data_ptr())))
+    n_act = sum(c[2] for c in act_calls)
+    n_w = sum(c[2] * c[3] * c[4] for c in w_calls)
+    n_step = n_act + n_w
+    qdq_t = lib.aimet_qdq_per_tensor
+    qdq_c = lib.aimet_qdq_per_channel
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in act_calls]
+
+    def step(timed_kernels=False):
+        for i, (a, o, n, e) in enumerate(act_calls):
+            if timed_kernels:
+                ev[i][0].record(stream)
+            rc = qdq_t(a, o, n, ctypes.byref(e), 0, 0, sptr)
+            if timed_kernels:
+                ev[i][1].record(stream)
+            if rc:
+                _native.check(rc)
+        for (a, o, outer, C, K, tab) in w_calls:
+            rc = qdq_c(a, o, outer, C, K, tab, 0, 0, sptr)
+            if rc:
+                _native.check(rc)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    kernel_ms = 0.0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed_kernels=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # per-launch kernel durations of the last timed step (events on the launch stream)
+    kernel_ms = sum(s.elapsed_time(e) for s, e in ev)
+    if world > 1:
+        tt = torch.tensor([dt, enc_seconds], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt, enc_seconds = float(tt[0]), float(tt[1])
+
+    ms_per_step = dt / args.steps * 1e3
+    value = n_step * world * args.steps / dt / 1e9
+    achieved = n_act * BYTES_QDQ / (kernel_ms / 1e3) / 1e9
+    result = {
+        "metric": "fake-quant Gelem/s (ResNet-50 W8A8 QuantSim forward QDQ; + compute_encodings wall-clock)",
+        "value": round(value, 3),
+        "unit": "Gelem/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: U(0,1) 224x224 images (seed 1234+rank), activations of a random-init ResNet-50 (seed 0)",
+        "config": {"workload": "resnet50_w8a8_per_channel_fake_quant_fwd", "global_batch": args.batch * world,
+                   "per_gpu_batch": args.batch, "act_elems_per_step": n_act, "weight_elems_per_step": n_w,
+                   "act_quantizers": len(act_calls), "weight_quantizers": len(w_calls),
+                   "weight_channels": int(sum(c[3] for c in w_calls)), "parallelism": "dp%d" % world,
+                   "compute_encodings_s": round(enc_seconds, 4),
+                   "compute_encodings_scheme": "tf_enhanced act per-tensor + tf_enhanced weight per-channel sym"},
+        "roofline": {"bound": "hbm", "kernel": "qdq_per_tensor (tensor_vec_kernel)",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
+                     "bytes_per_elem": BYTES_QDQ, "kernel_ms_per_step": round(kernel_ms, 4)},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        gel, n, secs = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images)
+        result["cpu_baseline"] = {"value": round(gel, 4), "unit": "Gelem/s", "cores": 1, "kind": "port",
+                                  "sample": "first %d images of each activation tensor + all weights (%d elems, "
+                                            "%.1f s), oracle/dlq_oracle.c single-threaded on the host"
+                                            % (args.cpu_sample_images, n, secs)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

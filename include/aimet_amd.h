@@ -1,0 +1,210 @@
+/*
+ * aimet_amd.h -- C-ABI of the MI355X-native DlQuantization hot path.
+ *
+ * This is the drop-in boundary that replaces the two pybind11 modules aimet_torch binds for
+ * quantization simulation:
+ *   - AimetTensorQuantizer          TrainingExtensions/torch/src/AimetTensorQuantizer.cpp:318-331
+ *   - _libpymo (quantization subset) ModelOptimizations/PyModelOptimizations/PyModelOptimizations.cpp:147-261
+ * Every entry point below names the reference interface it replaces (file:line, relative to the
+ * reference repository root). Plain pointers and sizes only: no torch or pybind types cross it.
+ *
+ * Conventions
+ *   - All float tensors are fp32 *device* pointers (HBM of an MI355X, gfx950) unless the name says
+ *     _host. There is no CPU compute path: a host pointer is an error (the product fails loudly).
+ *   - `stream` is a hipStream_t (nullptr = the legacy default stream). Every call is asynchronous on
+ *     that stream unless documented otherwise; results stay device-resident until a get_* call.
+ *   - Per-channel tensors are viewed as [outer][C][K] (channel = (i / K) % C), the reference's
+ *     (numChannel, numElement, numElementPerChannel) triple (trim_functions.cpp:607-630).
+ *   - Element counts are int64 (the reference uses int; results are identical below 2^31).
+ *   - Return value: AIMET_OK (0) or a negative status; aimet_last_error() then holds the message.
+ *     AIMET_ERR_INVALID_ARGUMENT mirrors std::invalid_argument (Python ValueError),
+ *     AIMET_ERR_RUNTIME mirrors std::runtime_error (Python RuntimeError).
+ */
+#ifndef AIMET_AMD_H
+#define AIMET_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AIMET_OK 0
+#define AIMET_ERR_INVALID_ARGUMENT (-1)
+#define AIMET_ERR_RUNTIME (-2)
+#define AIMET_ERR_HIP (-3)
+
+/* Quantization.hpp:84-106 QuantizationMode */
+enum aimet_quantization_mode {
+    AIMET_QUANTIZATION_TF = 0,
+    AIMET_QUANTIZATION_TF_ENHANCED = 1,
+    AIMET_QUANTIZATION_RANGE_LEARNING = 2,
+    AIMET_QUANTIZATION_PERCENTILE = 3,
+    AIMET_QUANTIZATION_MSE = 4,
+    AIMET_QUANTIZATION_ENTROPY = 5
+};
+
+/* Quantization.hpp:140-144 RoundingMode */
+enum aimet_rounding_mode { AIMET_ROUND_NEAREST = 0, AIMET_ROUND_STOCHASTIC = 1 };
+
+/* Quantization.hpp:113-120 TfEncoding */
+typedef struct aimet_tf_encoding {
+    double min;
+    double max;
+    double delta;
+    double offset;
+    int32_t bw;
+} aimet_tf_encoding;
+
+/* Thread-local message of the last failing call. */
+const char* aimet_last_error(void);
+/* Library version string ("aimet_amd <semver> gfx950"). */
+const char* aimet_version(void);
+/* Number of gfx950 devices visible; negative status on HIP failure. */
+int aimet_device_count(void);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Encoding math (host, exact reference arithmetic)                                            */
+/* ------------------------------------------------------------------------------------------ */
+
+/* quantization_utils.cpp:58-143 getComputedEncodings */
+int aimet_get_computed_encodings(int32_t bw, double min, double max, int use_symmetric, int use_strict_symmetric,
+                                 int use_unsigned_symmetric, aimet_tf_encoding* out);
+/* TensorQuantizationSim.cpp:62-92 fillEncodingInfo (gate, strict-symmetric detection, delta/offset) */
+int aimet_fill_encoding_info(int32_t bw, double min, double max, aimet_tf_encoding* out);
+/* TensorQuantizer.cpp:323-341 computePartialEncoding (in/out `enc`) */
+int aimet_compute_partial_encoding(int32_t bw, aimet_tf_encoding* enc, int use_symmetric,
+                                   int use_unsigned_symmetric, int use_strict_symmetric);
+
+/* Host-side encoding analyzers applied to statistics already reduced (e.g. read back, or merged
+ * from another process). They are what aimet_tq_get_encoding runs per channel.
+ *   TF:        TfEncodingAnalyzer.cpp:80-101 from the running {min, max}
+ *   histogram: TfEnhanced / Percentile / Mse computeEncoding from a PDF whose bucket edges are
+ *              xLeft[i] = hist_min + i * bucket_size (InitializePdf, math_functions.cpp:207-241);
+ *              initialized = 0 reproduces the "no histogram yet" branches. */
+int aimet_encoding_from_minmax(double acc_min, double acc_max, int32_t bw, int use_symmetric,
+                               int use_strict_symmetric, int use_unsigned_symmetric, aimet_tf_encoding* out);
+int aimet_encoding_from_histogram(int quant_scheme, int initialized, int stats_updated, float hist_min,
+                                  double bucket_size, const double* pdf_host, float percentile, int32_t bw,
+                                  int use_symmetric, int use_strict_symmetric, int use_unsigned_symmetric,
+                                  aimet_tf_encoding* out);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Quantize-dequantize kernels                                                                 */
+/* ------------------------------------------------------------------------------------------ */
+
+/* AimetTensorQuantizer.cpp:129-155 quantizeDequantize -> TensorQuantizationSim.cpp:96-114 ->
+ * trim_functions.cu:46-60. Uses enc->min/max/bw only (fillEncodingInfo is applied here).
+ * `seed` is used by AIMET_ROUND_STOCHASTIC only. in == out is allowed. */
+int aimet_qdq_per_tensor(const float* in, float* out, int64_t n, const aimet_tf_encoding* enc, int round_mode,
+                         uint64_t seed, void* stream);
+
+/* AimetTensorQuantizer.cpp:157-178 quantize -> trim_functions.cu:62-76 (float output holding integer
+ * codes, shifted by 2^(bw-1) when shift_to_signed). */
+int aimet_quantize_per_tensor(const float* in, float* out, int64_t n, const aimet_tf_encoding* enc, int round_mode,
+                              int shift_to_signed, uint64_t seed, void* stream);
+
+/* AimetTensorQuantizer.cpp:233-299 (gateMinMaxTensor / computeDeltaTensor / computeOffsetTensor):
+ * builds the device table [4][C] = {min, max, delta, offset} (fp32, torch rounding semantics) from
+ * `encs_host[C]`. The table depends only on the encodings: build it once per encoding change and
+ * reuse it for every forward (the reference re-uploads it on every call). */
+int aimet_per_channel_table(const aimet_tf_encoding* encs_host, int64_t C, float* table_dev, void* stream);
+
+/* AimetTensorQuantizer.cpp:209-231 makeDeltaOffsetTensor: table_dev [2][C] = {(float)delta, (float)offset}. */
+int aimet_make_delta_offset(const aimet_tf_encoding* encs_host, int64_t C, float* table_dev, void* stream);
+
+/* AimetTensorQuantizer.cpp:233-307 quantizeDequantizePerChannel -> trim_functions.cu:78-92 with the
+ * table from aimet_per_channel_table. N = outer*C*K elements. */
+int aimet_qdq_per_channel(const float* in, float* out, int64_t outer, int64_t C, int64_t K, const float* table_dev,
+                          int round_mode, uint64_t seed, void* stream);
+
+/* quantsim_straight_through_grad.py:91-118 compute_dloss_by_dx: grad_in = grad * (min <= x <= max).
+ * Per-tensor: C == 1, mins/maxs are one float each (device). */
+int aimet_ste_backward(const float* x, const float* grad, float* grad_in, int64_t outer, int64_t C, int64_t K,
+                       const float* mins_dev, const float* maxs_dev, void* stream);
+/* Per-tensor STE with host scalars (the common activation case). */
+int aimet_ste_backward_per_tensor(const float* x, const float* grad, float* grad_in, int64_t n, float enc_min,
+                                  float enc_max, void* stream);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Tensor quantizer: device-resident encoding statistics (AimetTensorQuantizer / TensorQuantizer) */
+/* ------------------------------------------------------------------------------------------ */
+
+typedef struct aimet_tensor_quantizer aimet_tensor_quantizer;
+
+/* AimetTensorQuantizer.cpp:82-87 ctor(QuantizationMode); num_channels analyzers are held together
+ * (the reference builds one AimetTensorQuantizer per channel, v1/tensor_quantizer.py:525).
+ * QUANTIZATION_RANGE_LEARNING maps to TF (QuantizerFactory.cpp:93-96). `device` = HIP ordinal. */
+int aimet_tq_create(int quant_scheme, int64_t num_channels, int device, aimet_tensor_quantizer** out);
+int aimet_tq_destroy(aimet_tensor_quantizer* q);
+/* AimetTensorQuantizer.cpp:89-96 resetEncodingStats (synchronous w.r.t. `stream`). */
+int aimet_tq_reset_encoding_stats(aimet_tensor_quantizer* q, void* stream);
+/* AimetTensorQuantizer.cpp:200-207 setPercentileValue (percentile scheme only). */
+int aimet_tq_set_percentile_value(aimet_tensor_quantizer* q, float percentile);
+int aimet_tq_get_percentile_value(aimet_tensor_quantizer* q, float* percentile);
+
+/* AimetTensorQuantizer.cpp:98-127 updateStats -> TfEncodingAnalyzer.cpp:59-72 / UpdatePdf
+ * (math_functions.cpp:243-288). x is [outer][C][K] with C == num_channels (per-tensor: outer=1,
+ * C=1, K=n). All channels are reduced in one pass; no host synchronisation. */
+int aimet_tq_update_stats(aimet_tensor_quantizer* q, const float* x, int64_t outer, int64_t C, int64_t K,
+                          void* stream);
+
+/* The same update split into phases, so a caller can exchange statistics between ranks
+ * (sharded calibration):
+ *   1. batch_minmax  -> q's device buffer of C pairs {-min, max} (float)   [all_reduce MAX]
+ *   2. fold_minmax   -> TF: running min/max; histogram schemes: PDF range on first batch
+ *   3. batch_histogram -> q's device buffer of C x 512 uint64 counts      [all_reduce SUM]
+ *   4. fold_histogram(count_per_channel) -> PDF running average with the global element count */
+int aimet_tq_batch_minmax(aimet_tensor_quantizer* q, const float* x, int64_t outer, int64_t C, int64_t K,
+                          void* stream);
+int aimet_tq_fold_minmax(aimet_tensor_quantizer* q, void* stream);
+int aimet_tq_batch_histogram(aimet_tensor_quantizer* q, const float* x, int64_t outer, int64_t C, int64_t K,
+                             void* stream);
+int aimet_tq_fold_histogram(aimet_tensor_quantizer* q, int64_t count_per_channel, void* stream);
+/* Device buffers exchanged between phases (owned by q). */
+int aimet_tq_minmax_buffer(aimet_tensor_quantizer* q, float** dev, int64_t* num_floats);
+int aimet_tq_counts_buffer(aimet_tensor_quantizer* q, uint64_t** dev, int64_t* num_counts);
+/* Place the two exchange buffers in caller-owned device memory (e.g. one slice of a packed buffer
+ * covering every quantizer, so one collective exchanges all of them). minmax_dev: 2*C floats,
+ * counts_dev: 512*C uint64 (zeroed by the caller; histogram schemes only, may be NULL for TF).
+ * The memory must outlive q or a later rebind. */
+int aimet_tq_bind_exchange(aimet_tensor_quantizer* q, float* minmax_dev, uint64_t* counts_dev);
+/* Marks statistics as updated without touching data (a rank whose shard was empty). */
+int aimet_tq_mark_stats_updated(aimet_tensor_quantizer* q);
+
+/* AimetTensorQuantizer.cpp:180-192 getEncoding -> IQuantizationEncodingAnalyzer::computeEncoding.
+ * Synchronises `stream`. out[num_channels]; *valid mirrors _isEncodingValid. */
+int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int use_symmetric, int use_strict_symmetric,
+                          int use_unsigned_symmetric, aimet_tf_encoding* out, int* valid, void* stream);
+
+/* AimetTensorQuantizer.cpp:194-198 getStatsHistogram (histogram schemes): xleft/pdf[512] of
+ * `channel`; *n = 0 when no histogram exists yet. Synchronises `stream`. */
+int aimet_tq_get_stats_histogram(aimet_tensor_quantizer* q, int64_t channel, double* xleft, double* pdf, int* n,
+                                 void* stream);
+
+int aimet_tq_num_channels(aimet_tensor_quantizer* q, int64_t* num_channels);
+int aimet_tq_quant_scheme(aimet_tensor_quantizer* q, int* quant_scheme);
+
+/* ------------------------------------------------------------------------------------------ */
+/* AdaRound soft rounding (v1/adaround/adaround_wrapper.py:124-149, adaround_loss.py:83-133)     */
+/* ------------------------------------------------------------------------------------------ */
+
+/* Wq = (clamp(floor(W/delta) + h(alpha) - offset, 0, 2^bw-1) + offset) * delta,
+ * h = clamp(sigmoid(alpha)*(zeta-gamma)+gamma, 0, 1) (soft) or (alpha >= 0) (hard).
+ * delta/offset broadcast along the channel axis of [outer][C][K] (per-tensor: C == 1). */
+int aimet_adaround_forward(const float* w, const float* alpha, float* wq, int64_t outer, int64_t C, int64_t K,
+                           const float* delta_dev, const float* offset_dev, int32_t bw, int use_soft_rounding,
+                           void* stream);
+/* dL/dalpha of the forward above (clamp pass-through masks as torch autograd) plus, when
+ * reg_param != 0, the round-loss gradient reg*d/dalpha sum(1-|2h-1|^beta), and the round loss
+ * itself accumulated into round_loss_dev[0] (fp32, atomically; caller zeroes it). */
+int aimet_adaround_backward(const float* w, const float* alpha, const float* grad_wq, float* grad_alpha,
+                            int64_t outer, int64_t C, int64_t K, const float* delta_dev, const float* offset_dev,
+                            int32_t bw, float reg_param, float beta, float* round_loss_dev, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIMET_AMD_H */

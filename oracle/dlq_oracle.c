@@ -266,6 +266,8 @@ typedef struct {
     int iterations;
     double xLeft[PDF_SIZE];
     double pdf[PDF_SIZE];
+    float hist_min;       /* InitializePdf's min_val after widening: xLeft[i] = hist_min + i*bucket_size */
+    double bucket_size;
 } orc_pdf; /* math_functions.hpp:70-77 */
 
 /* math_functions.cpp:207-241 InitializePdf<float> */
@@ -292,6 +294,8 @@ void orc_initialize_pdf(orc_pdf* p, float min_val, float max_val, int signed_val
     memset(p->pdf, 0, sizeof(p->pdf));
     p->iterations = 0;
     p->initialized = 1;
+    p->hist_min = min_val;
+    p->bucket_size = bucket_size;
 }
 
 /* math_functions.cpp:367-384 GetHistogram_cpu. Out-of-range/NaN indices (x86 cvttss2si
@@ -753,6 +757,19 @@ int orc_analyzer_histogram(const orc_analyzer* a, double* xleft, double* pdf)
     memcpy(xleft, a->pdf.xLeft, sizeof(a->pdf.xLeft));
     memcpy(pdf, a->pdf.pdf, sizeof(a->pdf.pdf));
     return PDF_SIZE;
+}
+
+/* Reduced statistics, as the HIP path keeps them (tests of the host-side encoding math) */
+void orc_analyzer_stats(const orc_analyzer* a, int* stats_updated, double* acc_min, double* acc_max,
+                        int* initialized, float* hist_min, double* bucket_size, int* iterations)
+{
+    *stats_updated = a->stats_updated;
+    *acc_min = a->acc_min;
+    *acc_max = a->acc_max;
+    *initialized = a->pdf.initialized;
+    *hist_min = a->pdf.hist_min;
+    *bucket_size = a->pdf.bucket_size;
+    *iterations = a->pdf.iterations;
 }
 
 /* Direct PDF access for tests of the sharded path */

@@ -71,6 +71,8 @@ def lib():
         L.orc_analyzer_compute.restype = Encoding
         L.orc_analyzer_compute.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.orc_analyzer_histogram.argtypes = [ctypes.c_void_p, dp, dp]
+        L.orc_analyzer_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), dp, dp,
+                                         ctypes.POINTER(ctypes.c_int), fp, dp, ctypes.POINTER(ctypes.c_int)]
         L.orc_analyzer_pdf.restype = ctypes.c_void_p
         L.orc_analyzer_pdf.argtypes = [ctypes.c_void_p]
         L.orc_update_pdf_from_counts.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), i64]
@@ -193,6 +195,19 @@ class Analyzer:
 
     def compute(self, bw, sym=False, strict=False, unsign=False) -> Encoding:
         return lib().orc_analyzer_compute(self._buf, int(bw), int(sym), int(strict), int(unsign))
+
+    def stats(self):
+        """Reduced statistics: dict(stats_updated, acc_min, acc_max, initialized, hist_min, bucket_size,
+        iterations, pdf)."""
+        su, ini, it = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        amin, amax, bs = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        hm = ctypes.c_float()
+        lib().orc_analyzer_stats(self._buf, ctypes.byref(su), ctypes.byref(amin), ctypes.byref(amax),
+                                 ctypes.byref(ini), ctypes.byref(hm), ctypes.byref(bs), ctypes.byref(it))
+        _, pdf = self.histogram()
+        return dict(stats_updated=su.value, acc_min=amin.value, acc_max=amax.value, initialized=ini.value,
+                    hist_min=hm.value, bucket_size=bs.value, iterations=it.value,
+                    pdf=pdf if ini.value else np.zeros(PDF_SIZE))
 
     def histogram(self):
         xl = np.zeros(PDF_SIZE, dtype=np.float64)

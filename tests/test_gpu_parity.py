@@ -1,0 +1,314 @@
+"""Parity of the HIP path (through the C-ABI) with the reference: golden vectors of the reference
+C++ (bit-exact), the reference test-suites' KATs, the CPU oracle on seeded inputs, and at full
+size size-independent properties. Needs an MI355X."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import analyzer_case, bits, gpu_available, per_channel_case
+from oracle import oracle as O
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+from aimet_amd import AimetTensorQuantizer  # noqa: E402
+from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding  # noqa: E402
+
+DEV = "cuda"
+NEAREST = RoundingMode.ROUND_NEAREST
+FLAGS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]
+
+
+def enc_of(mn, mx, bw, delta=0.0, offset=0.0):
+    e = TfEncoding()
+    e.min, e.max, e.bw, e.delta, e.offset = mn, mx, bw, delta, offset
+    return e
+
+
+def gpu(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(DEV)
+
+
+def host(t):
+    return t.detach().cpu().numpy()
+
+
+# ------------------------------------------------------------------------------------------
+# QDQ / quantize-only
+# ------------------------------------------------------------------------------------------
+def test_kat_qdq(kat):
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+    for name in ("qdq_sanity", "qdq_gated_min", "qdq_gated_equal", "qdq_gated_max"):
+        k = kat[name]
+        y = host(q.quantizeDequantize(gpu(k["x"]), enc_of(k["min"], k["max"], k["bw"]), NEAREST, True))
+        np.testing.assert_array_max_ulp(y, np.array(k["expected"], np.float32), maxulp=4)
+        np.testing.assert_array_equal(bits(y), bits(O.qdq_per_tensor(k["x"], k["min"], k["max"], k["bw"])))
+    for name in ("quantize_unsigned", "quantize_signed"):
+        k = kat[name]
+        y = host(q.quantize(gpu(k["x"]), enc_of(k["min"], k["max"], k["bw"]), NEAREST, True, k["shift"]))
+        np.testing.assert_array_equal(y, np.array(k["expected"], np.float32))
+
+
+def test_golden_qdq_per_tensor_bit_exact(golden_core):
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+    for i, (x, e) in enumerate(zip(golden_core["pt_x"], golden_core["pt_enc"])):
+        enc = enc_of(e[0], e[1], int(e[2]))
+        xd = gpu(x)
+        np.testing.assert_array_equal(bits(host(q.quantizeDequantize(xd, enc, NEAREST, True))),
+                                      bits(golden_core["pt_qdq"][i]), err_msg="case %d" % i)
+        np.testing.assert_array_equal(bits(host(q.quantize(xd, enc, NEAREST, True, False))),
+                                      bits(golden_core["pt_q_unsigned"][i]))
+        np.testing.assert_array_equal(bits(host(q.quantize(xd, enc, NEAREST, True, True))),
+                                      bits(golden_core["pt_q_signed"][i]))
+        # unaligned / ragged views take the scalar path: same bits
+        y = host(q.quantizeDequantize(xd[1:], enc, NEAREST, True))
+        np.testing.assert_array_equal(bits(y), bits(golden_core["pt_qdq"][i][1:]))
+
+
+def test_golden_qdq_per_channel_bit_exact(golden_core):
+    for i in range(int(golden_core["pc_count"])):
+        c = per_channel_case(golden_core, i)
+        encs = [enc_of(*e[:2], int(e[4]), e[2], e[3]) for e in c["encs"]]
+        q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+        table = q.channelTable(encs, torch.device(DEV))
+        np.testing.assert_array_equal(bits(host(table)), bits(c["table"]))
+        N = c["x"].size
+        y = q.quantizeDequantizePerChannel(gpu(c["x"]), encs, c["C"], N, c["K"], NEAREST, True)
+        np.testing.assert_array_equal(bits(host(y)), bits(c["y"]), err_msg="case %d" % i)
+
+
+def test_kat_per_channel(kat):
+    for name in ("per_channel_symmetric", "per_channel_asymmetric"):
+        k = kat[name]
+        x = np.array(k["x"], np.float32)
+        encs = [enc_of(e[0], e[1], int(e[4]), e[2], e[3]) for e in k["encodings"]]
+        q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+        y = host(q.quantizeDequantizePerChannel(gpu(x), encs, 4, x.size, x.shape[1], NEAREST, True))
+        np.testing.assert_allclose(y, np.array(k["expected"], np.float32), atol=k["atol"])
+
+
+@pytest.mark.parametrize("shape,axis", [((64, 3, 7, 7), 0), ((256, 64, 3, 3), 0), ((32, 16, 3, 3), 1),
+                                        ((1000, 2048), 0), ((7, 5, 3), 2)])
+def test_per_channel_vs_oracle_random(shape, axis):
+    rng = np.random.default_rng(hash(shape) % 1000)
+    x = (rng.standard_normal(shape) * 0.1).astype(np.float32)
+    C = shape[axis]
+    encs = []
+    for c in range(C):
+        lo, hi = sorted(rng.uniform(-0.3, 0.3, 2))
+        encs.append(enc_of(lo, hi, 8))
+    from aimet_amd.tensor_quantizer import per_channel_view, qdq_per_channel_table
+    outer, C_, K = per_channel_view(shape, axis)
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+    table = q.channelTable(encs, torch.device(DEV))
+    y = host(qdq_per_channel_table(gpu(x), table, outer, C_, K))
+    otab = O.per_channel_table([e.to_tuple() for e in encs])
+    want = O.qdq_per_channel(x.ravel(), C_, K, otab).reshape(shape)
+    np.testing.assert_array_equal(bits(y), bits(want))
+
+
+def test_qdq_full_size_bit_exact_and_properties():
+    """ResNet-50 bs256 conv1 output size (256x64x112x112 = 205M elements): bit-exact vs the
+    oracle, idempotent, on the quantization grid."""
+    g = torch.Generator(device=DEV).manual_seed(0)
+    x = torch.randn(256, 64, 112, 112, device=DEV, generator=g) * 2.0
+    enc = enc_of(-3.1, 5.7, 8)
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+    y = q.quantizeDequantize(x, enc, NEAREST, True)
+    want = O.qdq_per_tensor(host(x).ravel(), enc.min, enc.max, 8)
+    np.testing.assert_array_equal(bits(host(y).ravel()), bits(want))
+    y2 = q.quantizeDequantize(y, enc, NEAREST, True)
+    assert torch.equal(y, y2)
+    codes = q.quantize(x, enc, NEAREST, True, False)
+    assert float(codes.min()) >= 0 and float(codes.max()) <= 255
+    assert torch.equal(codes, torch.round(codes))
+
+
+def test_stochastic_rounding_is_unbiased():
+    x = torch.full((1 << 22,), 0.3, device=DEV)
+    enc = enc_of(-1.0, 1.0, 8)
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+    e = O.fill_encoding_info(8, -1.0, 1.0)
+    y = q.quantizeDequantize(x, enc, RoundingMode.ROUND_STOCHASTIC, True)
+    lo = np.float32(e.delta) * (np.floor(np.float32(0.3) / np.float32(e.delta) - np.float32(e.offset)) +
+                                np.float32(e.offset))
+    vals = torch.unique(y).cpu().numpy()
+    assert len(vals) == 2 and abs(vals[0] - lo) < 1e-6
+    assert abs(float(y.mean()) - 0.3) < 2e-4
+
+
+# ------------------------------------------------------------------------------------------
+# statistics + encodings
+# ------------------------------------------------------------------------------------------
+def test_golden_analyzers_bit_exact(golden_analyzers):
+    n = int(golden_analyzers["count"])
+    for i in range(n):
+        c = analyzer_case(golden_analyzers, i)
+        q = AimetTensorQuantizer(QuantizationMode(c["scheme"]))
+        if c["scheme"] == QuantizationMode.QUANTIZATION_PERCENTILE:
+            q.setPercentileValue(c["percentile"])
+        for b in c["batches"]:
+            q.updateStats(gpu(b), True)
+        for (bw, sym, strict, un), want in c["encs"].items():
+            got, valid = q.getEncoding(bw, sym, strict, un)
+            assert valid
+            assert got.to_tuple() == tuple(want[:4]) + (int(want[4]),), (i, c["scheme"], bw, sym, strict, un)
+        if c["scheme"] != QuantizationMode.QUANTIZATION_TF:
+            h = q.getStatsHistogram()
+            if len(c["xleft"]):
+                np.testing.assert_array_equal(np.array([t[0] for t in h]), c["xleft"])
+                np.testing.assert_array_equal(np.array([t[1] for t in h]), c["pdf"])
+
+
+def test_kat_tfe(kat, golden_torch):
+    k = kat["tfe_normal"]
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED)
+    q.updateStats(gpu(golden_torch["tfe_kat_x"]), True)
+    e, valid = q.getEncoding(8, False, False, False)
+    assert valid and e.to_tuple() == tuple(k["ref_encoding"])
+    y = host(q.quantizeDequantize(gpu(np.full(8, 5.0)), e, NEAREST, True))
+    assert float(y[0]) == k["ref_qdq5"]
+    z = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED)
+    z.updateStats(torch.zeros(6000, device=DEV), True)
+    e, _ = z.getEncoding(8, False, False, False)
+    kz = kat["tfe_all_zero"]
+    assert abs(e.min - kz["expected_min"]) < kz["tol"] and e.offset == kz["expected_offset"]
+
+
+def test_invalid_without_stats():
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED)
+    _, valid = q.getEncoding(8, False, False, False)
+    assert not valid
+    q.updateStats(torch.randn(100, device=DEV), True)
+    q.resetEncodingStats()
+    _, valid = q.getEncoding(8, False, False, False)
+    assert not valid
+
+
+@pytest.mark.parametrize("scheme", [QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
+                                    QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE])
+@pytest.mark.parametrize("shape,axis", [((64, 3, 7, 7), 0), ((96, 32, 3, 3), 0), ((16, 24, 3, 3), 1),
+                                        ((40, 130), 0)])
+def test_per_channel_stats_vs_per_channel_oracle(scheme, shape, axis):
+    """One batched launch == C independent reference analyzers over select(axis, c).contiguous()."""
+    rng = np.random.default_rng(7)
+    C = shape[axis]
+    q = AimetTensorQuantizer(scheme, num_channels=C)
+    if scheme == QuantizationMode.QUANTIZATION_PERCENTILE:
+        q.setPercentileValue(99.5)
+    orcs = [O.Analyzer(int(scheme)) for _ in range(C)]
+    for batch in range(2):
+        x = (rng.standard_normal(shape) * rng.uniform(0.01, 2)).astype(np.float32)
+        x[(slice(None),) * axis + (1,)] = 0.0          # one all-zero channel
+        if batch == 1:
+            x = np.maximum(x, 0)
+        q.updateStatsPerChannel(gpu(x), axis, True)
+        for c in range(C):
+            orcs[c].update(np.ascontiguousarray(np.take(x, c, axis=axis)))
+        if scheme == QuantizationMode.QUANTIZATION_PERCENTILE:
+            for o in orcs:
+                o.set_percentile(99.5)
+    for fl in FLAGS[:2] if scheme == QuantizationMode.QUANTIZATION_MSE else FLAGS:
+        encs, valid = q.getEncoding(8, *fl)
+        assert valid
+        for c in range(C):
+            assert encs[c].to_tuple() == orcs[c].compute(8, *fl).as_tuple(), (c, fl)
+
+
+def test_minmax_and_histogram_full_size():
+    """Stats of a 205M-element activation: TF encoding == oracle over the whole tensor, TF-E PDF
+    == oracle PDF (bit-exact) and sums to the in-range fraction."""
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = torch.relu(torch.randn(256, 64, 112, 112, device=DEV, generator=g) * 1.5 + 0.2)
+    xh = host(x).ravel()
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+    q.updateStats(x, True)
+    o = O.Analyzer(O.QUANTIZATION_TF)
+    o.update(xh)
+    assert q.getEncoding(8, False, False, False)[0].to_tuple() == o.compute(8).as_tuple()
+    qe = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED)
+    qe.updateStats(x, True)
+    oe = O.Analyzer(O.QUANTIZATION_TF_ENHANCED)
+    oe.update(xh)
+    h = qe.getStatsHistogram()
+    xl, pdf = oe.histogram()
+    np.testing.assert_array_equal(np.array([t[1] for t in h]), pdf)
+    np.testing.assert_array_equal(np.array([t[0] for t in h]), xl)
+    assert qe.getEncoding(8, False, False, False)[0].to_tuple() == oe.compute(8).as_tuple()
+
+
+# ------------------------------------------------------------------------------------------
+# STE / autograd
+# ------------------------------------------------------------------------------------------
+def test_ste_golden(golden_torch):
+    from aimet_amd.quantizers import compute_dloss_by_dx
+    x, g = gpu(golden_torch["ste_x"]), gpu(golden_torch["ste_g"])
+    got = compute_dloss_by_dx(x, g, golden_torch["ste_mins"].tolist(), golden_torch["ste_maxs"].tolist(), 0)
+    np.testing.assert_array_equal(bits(host(got)), bits(golden_torch["ste_pc"]))
+    got = compute_dloss_by_dx(x, g, -1.25, 0.8)
+    np.testing.assert_array_equal(bits(host(got)), bits(golden_torch["ste_pt"]))
+
+
+def test_quantize_dequantize_autograd_per_tensor_and_channel():
+    from aimet_amd.quantizers import QuantScheme, StaticGridPerChannelQuantizer, StaticGridPerTensorQuantizer
+    torch.manual_seed(0)
+    x = torch.randn(8, 16, 5, 5, device=DEV, requires_grad=True)
+    tq = StaticGridPerTensorQuantizer(8, "nearest", QuantScheme.post_training_tf, False, True)
+    tq.update_encoding_stats(x.detach() * 0.5)
+    tq.compute_encoding()
+    y = tq.quantize_dequantize(x, NEAREST)
+    y.backward(torch.ones_like(y))
+    mn, mx = np.float32(tq.encoding.min), np.float32(tq.encoding.max)
+    xh = host(x)
+    np.testing.assert_array_equal(host(x.grad), ((xh >= mn) & (xh <= mx)).astype(np.float32))
+    np.testing.assert_array_equal(bits(host(y)), bits(O.qdq_per_tensor(xh, tq.encoding.min, tq.encoding.max, 8)))
+
+    w = torch.randn(16, 8, 3, 3, device=DEV, requires_grad=True)
+    pq = StaticGridPerChannelQuantizer(8, "nearest", QuantScheme.post_training_tf_enhanced, True, 16, True)
+    pq.update_encoding_stats(w.detach())
+    pq.compute_encoding()
+    assert len(pq.encoding) == 16
+    yw = pq.quantize_dequantize(w, NEAREST)
+    yw.sum().backward()
+    wh = host(w)
+    for c in range(16):
+        o = O.Analyzer(O.QUANTIZATION_TF_ENHANCED)
+        o.update(wh[c].ravel())
+        assert pq.encoding[c].to_tuple() == o.compute(8, True, False, False).as_tuple()
+        lo, hi = np.float32(pq.encoding[c].min), np.float32(pq.encoding[c].max)
+        np.testing.assert_array_equal(host(w.grad)[c], ((wh[c] >= lo) & (wh[c] <= hi)).astype(np.float32))
+
+
+# ------------------------------------------------------------------------------------------
+# AdaRound
+# ------------------------------------------------------------------------------------------
+def _torch_adaround(w, alpha, delta, offset, bw, reg, beta):
+    """v1/adaround/adaround_wrapper.py:124-149 + adaround_loss.py:83-110 in float32 torch autograd."""
+    alpha = alpha.clone().requires_grad_(True)
+    t = torch.floor(w / delta)
+    h = torch.clamp(torch.sigmoid(alpha) * (1.1 - (-0.1)) + (-0.1), 0, 1)
+    q = torch.clamp(t + h - offset, 0, 2 ** bw - 1)
+    wq = (q + offset) * delta
+    return wq, alpha, h
+
+
+def test_adaround_forward_backward_vs_torch(kat):
+    from aimet_amd.adaround import AdaroundFunction, round_loss_and_grad
+    torch.manual_seed(0)
+    w = torch.randn(32, 16, 3, 3, device=DEV) * 0.1
+    delta = (torch.rand(32, device=DEV) * 0.01 + 0.001).view(32, 1, 1, 1)
+    offset = torch.full((32, 1, 1, 1), -128.0, device=DEV)
+    alpha = torch.randn_like(w)
+    wq_ref, a_ref, h_ref = _torch_adaround(w, alpha, delta, offset, 8, 0.0, 2.0)
+    g = torch.randn_like(w)
+    (wq_ref * g).sum().backward()
+    a = alpha.clone().requires_grad_(True)
+    wq = AdaroundFunction.apply(w, a, delta.view(-1), offset.view(-1), 8, 0)
+    torch.testing.assert_close(wq, wq_ref.detach(), rtol=0, atol=1e-6)
+    (wq * g).sum().backward()
+    torch.testing.assert_close(a.grad, a_ref.grad, rtol=1e-5, atol=1e-6)
+    # round loss KAT (test_adaround_loss.py:83-100): float32 alpha, tolerance 1e-5 (places=5)
+    k = kat["adaround_round_loss"]
+    np.random.seed(k["seed"])
+    al = torch.from_numpy(np.random.rand(*k["shape"]).astype(np.float32)).to(DEV)
+    loss, _ = round_loss_and_grad(al, k["reg_param"], kat["adaround_beta"]["expected"])
+    assert abs(float(loss) - k["expected"]) < 1e-4
