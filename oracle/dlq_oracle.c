@@ -772,5 +772,25 @@ void orc_analyzer_stats(const orc_analyzer* a, int* stats_updated, double* acc_m
     *iterations = a->pdf.iterations;
 }
 
+/* Fold a batch's (already exchanged) min/max into the analyzer: TF running min/max, or the PDF
+ * range on the first non-zero batch -- the same step UpdatePdf / TfEncodingAnalyzer::updateStats
+ * take after GetMin/GetMax (math_functions.cpp:249-260, TfEncodingAnalyzer.cpp:63-71).
+ * Returns 1 when a histogram update must follow (PDF initialised). */
+int orc_analyzer_fold_minmax(orc_analyzer* a, float mn, float mx)
+{
+    a->stats_updated = 1;
+    if (a->scheme == QUANTIZATION_TF) {
+        a->acc_min = dmin_(a->acc_min, (double) mn);
+        a->acc_max = dmax_(a->acc_max, (double) mx);
+        return 0;
+    }
+    if (!a->pdf.initialized) {
+        if (mn == 0 && mx == 0)
+            return 0;
+        orc_initialize_pdf(&a->pdf, mn, mx, 1);
+    }
+    return 1;
+}
+
 /* Direct PDF access for tests of the sharded path */
 orc_pdf* orc_analyzer_pdf(orc_analyzer* a) { return &a->pdf; }

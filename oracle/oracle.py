@@ -73,6 +73,7 @@ def lib():
         L.orc_analyzer_histogram.argtypes = [ctypes.c_void_p, dp, dp]
         L.orc_analyzer_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), dp, dp,
                                          ctypes.POINTER(ctypes.c_int), fp, dp, ctypes.POINTER(ctypes.c_int)]
+        L.orc_analyzer_fold_minmax.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float]
         L.orc_analyzer_pdf.restype = ctypes.c_void_p
         L.orc_analyzer_pdf.argtypes = [ctypes.c_void_p]
         L.orc_update_pdf_from_counts.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), i64]
@@ -192,6 +193,10 @@ class Analyzer:
 
     def set_percentile(self, p):
         lib().orc_analyzer_set_percentile(self._buf, float(p))
+
+    def fold_minmax(self, mn, mx):
+        """Apply an exchanged batch min/max; True when a histogram update must follow."""
+        return bool(lib().orc_analyzer_fold_minmax(self._buf, float(mn), float(mx)))
 
     def compute(self, bw, sym=False, strict=False, unsign=False) -> Encoding:
         return lib().orc_analyzer_compute(self._buf, int(bw), int(sym), int(strict), int(unsign))

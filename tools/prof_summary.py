@@ -1,0 +1,60 @@
+"""Summarise a rocprofv3 kernel trace (+ optional FETCH_SIZE / WRITE_SIZE PMC passes) of bench.py.
+
+usage: python tools/prof_summary.py <trace_dir> [<pmc_fetch_dir> <pmc_write_dir>] [--steps N]
+Prints per-kernel totals over the timed steps and, with PMC data, the HBM bytes per step of the
+per-tensor QDQ kernel corrected as MI355X_MICROARCH.md §HBM prescribes (FETCH_SIZE x 2 on gfx950,
+WRITE_SIZE as is; both in KiB).
+"""
+import collections
+import csv
+import glob
+import os
+import sys
+
+QDQ = "tensor_vec_kernel"
+
+
+def trace_rows(d):
+    f = glob.glob(os.path.join(d, "*kernel_trace.csv"))[0]
+    rows = list(csv.DictReader(open(f)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    return rows
+
+
+def pmc(d, name):
+    f = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    return [(r["Kernel_Name"], float(r["Counter_Value"])) for r in csv.DictReader(open(f)) if r["Counter_Name"] == name]
+
+
+def main():
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    per_step = 55
+    rows = trace_rows(args[0])
+    qi = [i for i, r in enumerate(rows) if QDQ in r["Kernel_Name"]]
+    # skip warmup: use the last 5 steps of QDQ dispatches
+    nsteps = len(qi) // per_step
+    first = qi[(nsteps - min(nsteps, 5)) * per_step]
+    ai = [i for i, r in enumerate(rows) if "aimet_amd" in r["Kernel_Name"]]
+    seg = rows[first:ai[-1] + 1]
+    steps = min(nsteps, 5)
+    agg = collections.defaultdict(lambda: [0, 0])
+    for r in seg:
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0][-60:]
+        agg[k][0] += 1
+        agg[k][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    span = int(seg[-1]["End_Timestamp"]) - int(seg[0]["Start_Timestamp"])
+    print("timed steps analysed: %d, span %.3f ms/step" % (steps, span / 1e6 / steps))
+    for k, (c, d) in sorted(agg.items(), key=lambda x: -x[1][1]):
+        print("  %-62s calls/step %5.1f  ms/step %.4f" % (k, c / steps, d / 1e6 / steps))
+    q_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg if QDQ in r["Kernel_Name"]) / steps
+    print("per-tensor QDQ kernel time/step: %.4f ms" % (q_ns / 1e6))
+    if len(args) >= 3:
+        f = [v for n, v in pmc(args[1], "FETCH_SIZE") if QDQ in n][-per_step:]
+        w = [v for n, v in pmc(args[2], "WRITE_SIZE") if QDQ in n][-per_step:]
+        fb, wb = sum(f) * 1024 * 2, sum(w) * 1024
+        print("per-tensor QDQ HBM traffic/step: fetch %.4f GB (FETCH_SIZE x2), write %.4f GB, total %.4f GB"
+              % (fb / 1e9, wb / 1e9, (fb + wb) / 1e9))
+
+
+if __name__ == "__main__":
+    main()
