@@ -32,6 +32,9 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_QDQ = 8            # fp32 read + fp32 write per element
+# HBM bytes per step of the activation QDQ launches from the rocprofv3 PMC passes
+# (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), profiles/r01/bench_summary_*.txt
+TRAFFIC_GB = 23.075
 
 
 def parse():
@@ -45,7 +48,7 @@ def parse():
     p.add_argument("--cpu-sample-images", type=int, default=32,
                    help="images of each activation tensor (plus all weights) timed on the CPU oracle")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--profile-steps", action="store_true", help="short run for rocprofv3")
+    p.add_argument("--eager", action="store_true", help="launch every QDQ from Python instead of HIP graphs")
     return p.parse_args()
 
 
@@ -162,21 +165,51 @@ def main():
     qdq_t = lib.aimet_qdq_per_tensor
     qdq_c = lib.aimet_qdq_per_channel
 
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in act_calls]
+    def launch_acts(sp):
+        for (a, o, n, e) in act_calls:
+            rc = qdq_t(a, o, n, ctypes.byref(e), 0, 0, sp)
+            if rc:
+                _native.check(rc)
 
-    def step(timed_kernels=False):
-        for i, (a, o, n, e) in enumerate(act_calls):
-            if timed_kernels:
-                ev[i][0].record(stream)
-            rc = qdq_t(a, o, n, ctypes.byref(e), 0, 0, sptr)
-            if timed_kernels:
-                ev[i][1].record(stream)
-            if rc:
-                _native.check(rc)
+    def launch_weights(sp):
         for (a, o, outer, C, K, tab) in w_calls:
-            rc = qdq_c(a, o, outer, C, K, tab, 0, 0, sptr)
+            rc = qdq_c(a, o, outer, C, K, tab, 0, 0, sp)
             if rc:
                 _native.check(rc)
+
+    # The step is captured once into two HIP graphs (activation QDQs, weight QDQs) and replayed:
+    # 109 launches per step would otherwise cost ~8 us of host launch each.
+    use_graph = not args.eager
+    if use_graph:
+        cap = torch.cuda.Stream(dev)
+        g_act, g_w = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        cap.wait_stream(stream)
+        with torch.cuda.stream(cap):
+            launch_acts(ctypes.c_void_p(cap.cuda_stream))   # warm (outside capture)
+            launch_weights(ctypes.c_void_p(cap.cuda_stream))
+        stream.wait_stream(cap)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g_act, stream=cap):
+            launch_acts(ctypes.c_void_p(cap.cuda_stream))
+        with torch.cuda.graph(g_w, stream=cap):
+            launch_weights(ctypes.c_void_p(cap.cuda_stream))
+        torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            ev[i][0].record(stream)
+        if use_graph:
+            g_act.replay()
+        else:
+            launch_acts(sptr)
+        if i is not None:
+            ev[i][1].record(stream)
+        if use_graph:
+            g_w.replay()
+        else:
+            launch_weights(sptr)
 
     for _ in range(args.warmup):
         step()
@@ -184,17 +217,17 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    kernel_ms = 0.0
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed_kernels=True)
+    for i in range(args.steps):
+        step(i)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    # per-launch kernel durations of the last timed step (events on the launch stream)
-    kernel_ms = sum(s.elapsed_time(e) for s, e in ev)
+    # HIP events on the launch stream bracket the activation QDQ launches of every timed step
+    act_ms = [s.elapsed_time(e) for s, e in ev]
+    kernel_ms = sum(act_ms) / len(act_ms)
     if world > 1:
         tt = torch.tensor([dt, enc_seconds], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -216,7 +249,7 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: U(0,1) 224x224 images (seed 1234+rank), activations of a random-init ResNet-50 (seed 0)",
-        "config": {"workload": "resnet50_w8a8_per_channel_fake_quant_fwd", "global_batch": args.batch * world,
+        "config": {"workload": "resnet50_w8a8_per_channel_fake_quant_fwd", "launch": "hipgraph" if use_graph else "eager", "global_batch": args.batch * world,
                    "per_gpu_batch": args.batch, "act_elems_per_step": n_act, "weight_elems_per_step": n_w,
                    "act_quantizers": len(act_calls), "weight_quantizers": len(w_calls),
                    "weight_channels": int(sum(c[3] for c in w_calls)), "parallelism": "dp%d" % world,
@@ -224,8 +257,12 @@ def main():
                    "compute_encodings_scheme": "tf_enhanced act per-tensor + tf_enhanced weight per-channel sym"},
         "roofline": {"bound": "hbm", "kernel": "qdq_per_tensor (tensor_vec_kernel)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": None,
-                     "bytes_per_elem": BYTES_QDQ, "kernel_ms_per_step": round(kernel_ms, 4)},
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": TRAFFIC_GB,
+                     "bytes_per_elem": BYTES_QDQ, "launches_per_step": len(act_calls),
+                     "avg_launch_us": round(kernel_ms * 1e3 / len(act_calls), 2),
+                     "act_qdq_ms_per_step": round(kernel_ms, 4),
+                     "timing": "HIP events on the launch stream around the %d activation QDQ launches of each "
+                               "timed step (%s)" % (len(act_calls), "graph replay" if use_graph else "eager")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         gel, n, secs = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images)
