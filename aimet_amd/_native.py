@@ -40,6 +40,11 @@ _i32 = ctypes.c_int32
 _int = ctypes.c_int
 _enc_p = ctypes.POINTER(TfEncodingC)
 
+
+class ChannelDescC(ctypes.Structure):
+    _fields_ = [("in_", ctypes.c_void_p), ("out", ctypes.c_void_p), ("outer", ctypes.c_int64),
+                ("C", ctypes.c_int64), ("K", ctypes.c_int64), ("table", ctypes.c_void_p)]
+
 # name -> argtypes (restype is int status unless listed in _RESTYPES)
 _PROTOTYPES = {
     "aimet_last_error": [],
@@ -56,6 +61,9 @@ _PROTOTYPES = {
     "aimet_per_channel_table": [_enc_p, _i64, _vp, _vp],
     "aimet_make_delta_offset": [_enc_p, _i64, _vp, _vp],
     "aimet_qdq_per_channel": [_vp, _vp, _i64, _i64, _i64, _vp, _int, ctypes.c_uint64, _vp],
+    "aimet_qdq_channel_plan_create": [ctypes.POINTER(ChannelDescC), _i64, _int, ctypes.POINTER(_vp)],
+    "aimet_qdq_channel_plan_run": [_vp, _int, ctypes.c_uint64, _vp],
+    "aimet_qdq_channel_plan_destroy": [_vp],
     "aimet_ste_backward": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp],
     "aimet_ste_backward_per_tensor": [_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, _vp],
     "aimet_tq_create": [_int, _i64, _int, ctypes.POINTER(_vp)],
@@ -76,6 +84,8 @@ _PROTOTYPES = {
     "aimet_tq_get_stats_histogram": [_vp, _i64, _dp, _dp, ctypes.POINTER(_int), _vp],
     "aimet_tq_num_channels": [_vp, ctypes.POINTER(_i64)],
     "aimet_tq_quant_scheme": [_vp, ctypes.POINTER(_int)],
+    "aimet_lg_forward": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_float, _vp],
+    "aimet_lg_backward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_float, _vp],
     "aimet_adaround_forward": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _int, _vp],
     "aimet_adaround_backward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, ctypes.c_float,
                                 ctypes.c_float, _vp, _vp],

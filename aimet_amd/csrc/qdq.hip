@@ -232,6 +232,61 @@ __global__ __launch_bounds__(kBlock) void ste_channel_vec_kernel(const f4* __res
     store_stream(r, gi + i);
 }
 
+// ---------------------------------------------------------------------------------------
+// Batched per-channel QDQ (one launch for many tensors)
+// ---------------------------------------------------------------------------------------
+struct BatchDesc
+{
+    const float* in;
+    float* out;
+    const float* table;
+    ChannelMap map;
+    uint32_t n;           // elements
+    uint32_t vec;         // 16-B vector path (K % 4 == 0, aligned)
+    uint32_t block0;      // first workgroup of this tensor in the flattened grid
+    uint32_t pad;
+};
+
+template <bool STOCHASTIC>
+__global__ __launch_bounds__(kBlock) void channel_batch_kernel(const BatchDesc* __restrict__ descs, int count,
+                                                               uint64_t seed)
+{
+    // find the tensor of this workgroup (block0 is increasing): scalar binary search
+    int lo = 0, hi = count - 1;
+    const uint32_t b = blockIdx.x;
+    while (lo < hi)
+    {
+        int mid = (lo + hi + 1) >> 1;
+        if (descs[mid].block0 <= b)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    const BatchDesc& d = descs[lo];
+    const uint32_t t   = (b - d.block0) * kBlock + threadIdx.x;
+    if (d.vec)
+    {
+        if (t >= d.n / 4)
+            return;
+        f4 v        = load_stream(reinterpret_cast<const f4*>(d.in) + t);
+        QdqParams p = load_params(d.table, d.map.C, d.map.channel(t * 4));
+        uint64_t e  = ((uint64_t) lo << 40) + (uint64_t) t * 4;
+        f4 r;
+        r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0);
+        r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1);
+        r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2);
+        r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3);
+        store_stream(r, reinterpret_cast<f4*>(d.out) + t);
+    }
+    else
+    {
+        if (t >= d.n)
+            return;
+        QdqParams p = load_params(d.table, d.map.C, d.map.channel(t));
+        d.out[t]    = apply<Op::QDQ, STOCHASTIC>(d.in[t], p, 0.f, seed, ((uint64_t) lo << 40) + t);
+    }
+}
+
 inline bool aligned16(const void* a, const void* b, const void* c = nullptr)
 {
     return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(c)) & 15) ==
@@ -257,7 +312,99 @@ QdqParams tensor_params(const aimet_tf_encoding& enc)
 
 using namespace aimet_amd;
 
+struct aimet_qdq_plan
+{
+    int device          = 0;
+    int count           = 0;
+    uint32_t blocks     = 0;
+    BatchDesc* descs    = nullptr;   // device
+};
+
 extern "C" {
+
+int aimet_qdq_channel_plan_create(const aimet_qdq_channel_desc* descs, int64_t count, int device, aimet_qdq_plan** out)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(out != nullptr && descs != nullptr && count > 0, "empty plan");
+        AIMET_REQUIRE(count < (1 << 20), "too many tensors in one plan");
+        std::vector<BatchDesc> h((size_t) count);
+        uint64_t blocks = 0;
+        for (int64_t i = 0; i < count; ++i)
+        {
+            const auto& d = descs[i];
+            AIMET_REQUIRE(d.outer >= 0 && d.C > 0 && d.K >= 0, "invalid per-channel shape");
+            int64_t n = d.outer * d.C * d.K;
+            AIMET_REQUIRE(n < (int64_t(1) << 31), "batched per-channel QDQ needs < 2^31 elements per tensor");
+            if (n > 0)
+            {
+                require_device_ptr(d.in, "input");
+                require_device_ptr(d.out, "output");
+                require_device_ptr(d.table, "table");
+            }
+            BatchDesc& b = h[(size_t) i];
+            b.in         = d.in;
+            b.out        = d.out;
+            b.table      = d.table;
+            b.map        = ChannelMap {FastDiv((uint32_t) (d.K > 0 ? d.K : 1)), FastDiv((uint32_t) d.C), (uint32_t) d.C};
+            b.n          = (uint32_t) n;
+            b.vec        = (d.K % 4 == 0 && aligned16(d.in, d.out)) ? 1u : 0u;
+            b.block0     = (uint32_t) blocks;
+            b.pad        = 0;
+            blocks += (uint64_t) ceil_div(b.vec ? n / 4 : n, kBlock);
+        }
+        AIMET_REQUIRE(blocks < (uint64_t(1) << 31), "plan too large");
+        auto* plan   = new aimet_qdq_plan();
+        plan->device = device;
+        plan->count  = (int) count;
+        plan->blocks = (uint32_t) blocks;
+        int prev     = 0;
+        AIMET_HIP_CHECK(hipGetDevice(&prev));
+        AIMET_HIP_CHECK(hipSetDevice(device));
+        hipError_t e = hipMalloc(&plan->descs, sizeof(BatchDesc) * count);
+        if (e == hipSuccess)
+            e = hipMemcpy(plan->descs, h.data(), sizeof(BatchDesc) * count, hipMemcpyHostToDevice);
+        (void) hipSetDevice(prev);
+        if (e != hipSuccess)
+        {
+            if (plan->descs)
+                (void) hipFree(plan->descs);
+            delete plan;
+            throw HipError(std::string("plan upload: ") + hipGetErrorString(e));
+        }
+        *out = plan;
+    });
+}
+
+int aimet_qdq_channel_plan_run(aimet_qdq_plan* plan, int round_mode, uint64_t seed, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(plan != nullptr, "plan is null");
+        AIMET_REQUIRE(round_mode == AIMET_ROUND_NEAREST || round_mode == AIMET_ROUND_STOCHASTIC,
+                      "Unknown rounding mode.");
+        if (plan->blocks == 0)
+            return;
+        hipStream_t s = as_stream(stream);
+        if (round_mode == AIMET_ROUND_STOCHASTIC)
+            channel_batch_kernel<true><<<plan->blocks, kBlock, 0, s>>>(plan->descs, plan->count, seed);
+        else
+            channel_batch_kernel<false><<<plan->blocks, kBlock, 0, s>>>(plan->descs, plan->count, seed);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_qdq_channel_plan_destroy(aimet_qdq_plan* plan)
+{
+    return guarded([&] {
+        if (!plan)
+            return;
+        if (plan->descs)
+        {
+            AIMET_HIP_CHECK(hipDeviceSynchronize());
+            AIMET_HIP_CHECK(hipFree(plan->descs));
+        }
+        delete plan;
+    });
+}
 
 int aimet_qdq_per_tensor(const float* in, float* out, int64_t n, const aimet_tf_encoding* enc, int round_mode,
                          uint64_t seed, void* stream)

@@ -323,3 +323,46 @@ def _suggest_memory_format(t):
     if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last) and not t.is_contiguous():
         return torch.channels_last
     return torch.contiguous_format
+
+
+class ChannelQdqPlan:
+    """Every per-channel parameter QDQ of a forward in ONE launch (aimet_qdq_channel_plan_*).
+
+    entries: list of (input, output, ch_axis, table) with device fp32 tensors and [4][C] tables
+    from ``AimetTensorQuantizer.channelTable``. The tensors must stay alive (and not move) while
+    the plan is used; the plan is graph-capturable."""
+
+    def __init__(self, entries):
+        from aimet_amd._native import ChannelDescC
+        if not entries:
+            raise ValueError("empty plan")
+        descs = (ChannelDescC * len(entries))()
+        self._keep = []
+        device = None
+        for i, (x, y, ax, table) in enumerate(entries):
+            _require_gpu(x)
+            _require_gpu(y, True, "output")
+            if not (x.is_contiguous() and y.is_contiguous() and x.shape == y.shape):
+                raise ValueError("plan tensors must be contiguous and of equal shape")
+            outer, C, K = per_channel_view(x.shape, ax)
+            descs[i] = ChannelDescC(x.data_ptr(), y.data_ptr(), outer, C, K, table.data_ptr())
+            self._keep += [x, y, table]
+            device = x.device
+        self.device = device
+        h = ctypes.c_void_p()
+        _native.call("aimet_qdq_channel_plan_create", descs, len(entries), device.index, ctypes.byref(h))
+        self._handle = h
+
+    def run(self, round_mode=RoundingMode.ROUND_NEAREST, stream=None):
+        seed = next(_seed_counter) if int(round_mode) == RoundingMode.ROUND_STOCHASTIC else 0
+        s = stream if stream is not None else torch.cuda.current_stream(self.device).cuda_stream
+        _native.call("aimet_qdq_channel_plan_run", self._handle, int(round_mode), seed, s)
+
+    def __del__(self):
+        h = getattr(self, "_handle", None)
+        if h is not None:
+            try:
+                _native.call("aimet_qdq_channel_plan_destroy", h)
+            except Exception:
+                pass
+            self._handle = None

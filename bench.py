@@ -49,6 +49,8 @@ def parse():
                    help="images of each activation tensor (plus all weights) timed on the CPU oracle")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--eager", action="store_true", help="launch every QDQ from Python instead of HIP graphs")
+    p.add_argument("--per-weight-launches", action="store_true",
+                   help="one per-channel QDQ launch per weight instead of the batched plan")
     return p.parse_args()
 
 
@@ -147,10 +149,10 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sptr = ctypes.c_void_p(stream.cuda_stream)
     act_calls, w_calls = [], []
-    outs = []
+    outs, act_outs = [], []
     for (name, t), e in zip(acts, act_enc):
         o = torch.empty_like(t)
-        outs.append(o)
+        act_outs.append(o)
         act_calls.append((ctypes.c_void_p(t.data_ptr()), ctypes.c_void_p(o.data_ptr()), t.numel(), e.to_c()))
     for ((name, w), encs), q in zip(zip(weights, w_enc), wq):
         o = torch.empty_like(w)
@@ -171,7 +173,18 @@ def main():
             if rc:
                 _native.check(rc)
 
+    # all 54 parameter QDQs of the forward in ONE launch (aimet_qdq_channel_plan_*)
+    from aimet_amd.tensor_quantizer import ChannelQdqPlan
+    plan = ChannelQdqPlan([(w, outs[2 * i], 0, outs[2 * i + 1]) for i, (_, w) in enumerate(weights)]) \
+        if not args.per_weight_launches else None
+    plan_run = lib.aimet_qdq_channel_plan_run
+
     def launch_weights(sp):
+        if plan is not None:
+            rc = plan_run(plan._handle, 0, 0, sp)
+            if rc:
+                _native.check(rc)
+            return
         for (a, o, outer, C, K, tab) in w_calls:
             rc = qdq_c(a, o, outer, C, K, tab, 0, 0, sp)
             if rc:
@@ -249,7 +262,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: U(0,1) 224x224 images (seed 1234+rank), activations of a random-init ResNet-50 (seed 0)",
-        "config": {"workload": "resnet50_w8a8_per_channel_fake_quant_fwd", "launch": "hipgraph" if use_graph else "eager", "global_batch": args.batch * world,
+        "config": {"workload": "resnet50_w8a8_per_channel_fake_quant_fwd", "launch": "hipgraph" if use_graph else "eager",
+                   "weight_qdq": "per-weight launches" if plan is None else "one batched launch", "global_batch": args.batch * world,
                    "per_gpu_batch": args.batch, "act_elems_per_step": n_act, "weight_elems_per_step": n_w,
                    "act_quantizers": len(act_calls), "weight_quantizers": len(w_calls),
                    "weight_channels": int(sum(c[3] for c in w_calls)), "parallelism": "dp%d" % world,

@@ -119,6 +119,22 @@ int aimet_make_delta_offset(const aimet_tf_encoding* encs_host, int64_t C, float
 int aimet_qdq_per_channel(const float* in, float* out, int64_t outer, int64_t C, int64_t K, const float* table_dev,
                           int round_mode, uint64_t seed, void* stream);
 
+/* Batched per-channel QDQ: every parameter quantizer of a model forward in ONE launch (the
+ * reference loops over parameters in Python, one kernel + one table upload each:
+ * v1/qc_quantize_op.py:753-798 -> AimetTensorQuantizer.cpp:233-307). A plan holds the device
+ * copy of the descriptors; run it once per forward (graph-capturable). */
+typedef struct aimet_qdq_channel_desc {
+    const float* in;      /* [outer][C][K] fp32, device */
+    float* out;           /* same shape, device (may equal in) */
+    int64_t outer, C, K;
+    const float* table;   /* [4][C] from aimet_per_channel_table */
+} aimet_qdq_channel_desc;
+typedef struct aimet_qdq_plan aimet_qdq_plan;
+int aimet_qdq_channel_plan_create(const aimet_qdq_channel_desc* descs_host, int64_t count, int device,
+                                  aimet_qdq_plan** out);
+int aimet_qdq_channel_plan_run(aimet_qdq_plan* plan, int round_mode, uint64_t seed, void* stream);
+int aimet_qdq_channel_plan_destroy(aimet_qdq_plan* plan);
+
 /* quantsim_straight_through_grad.py:91-118 compute_dloss_by_dx: grad_in = grad * (min <= x <= max).
  * Per-tensor: C == 1, mins/maxs are one float each (device). */
 int aimet_ste_backward(const float* x, const float* grad, float* grad_in, int64_t outer, int64_t C, int64_t K,
@@ -185,6 +201,21 @@ int aimet_tq_get_stats_histogram(aimet_tensor_quantizer* q, int64_t channel, dou
 
 int aimet_tq_num_channels(aimet_tensor_quantizer* q, int64_t* num_channels);
 int aimet_tq_quant_scheme(aimet_tensor_quantizer* q, int* quant_scheme);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Range-learning (LearnedGrid) QAT: quantsim_straight_through_grad.py:191-328,                  */
+/* QuantizeDequantizeFunc v1/tensor_quantizer.py:896-986                                         */
+/* ------------------------------------------------------------------------------------------ */
+
+/* y = (clamp(round_half_even(x/delta) - offset, 0, num_steps) + offset) * delta, delta/offset per
+ * channel of [outer][C][K] (C == 1: per-tensor), float32 device vectors. */
+int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t K, const float* delta_dev,
+                     const float* offset_dev, float num_steps, void* stream);
+/* grad_x = mask * grad (grad_x may be NULL) and per-channel sums_dev[C][3] =
+ * { sum((x_quant+offset)*grad), sum(mask*(x/delta)*grad), sum(!mask*grad) } from which the
+ * encoding-min/max gradients are assembled (asymmetric_gradients / symmetric_gradients). */
+int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* sums_dev, int64_t outer, int64_t C,
+                      int64_t K, const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* AdaRound soft rounding (v1/adaround/adaround_wrapper.py:124-149, adaround_loss.py:83-133)     */

@@ -1,0 +1,87 @@
+"""TEST INFRASTRUCTURE ONLY: float32 torch restatements of the reference's Python-side arithmetic
+on the path (only tests/ import this):
+
+* learned-grid forward / gradients -- quantsim_straight_through_grad.py:121-328
+  (pinned against the reference module itself: tests/golden/golden_lg.npz, make_golden.py)
+* AdaRound soft rounding -- adaround_wrapper.py:124-149, adaround_loss.py:83-110
+  (pinned by the reference KATs in tests/golden/kat.json)
+"""
+import math
+
+import torch
+
+
+def _bcast(tensor, v, ch_axis):
+    if v.numel() == 1:
+        return v.reshape(())
+    shape = tuple(d if a == ch_axis else 1 for a, d in enumerate(tensor.shape))
+    return v.view(shape)
+
+
+def lg_encodings(bw, emin, emax, sym, strict, unsigned):
+    """quantsim_straight_through_grad.py:121-160 get_computed_encodings."""
+    steps = 2 ** bw - 1
+    if sym and strict:
+        steps -= 1
+    half = steps / 2
+    steps_t = torch.full_like(emin, steps)
+    if sym and not unsigned:
+        delta = emax / torch.full_like(emin, math.floor(half))
+        offset = -torch.full_like(emin, math.ceil(half))
+    else:
+        delta = (emax - emin) / steps_t
+        if sym:
+            offset = emin / delta
+        else:
+            b0 = torch.round(-emin / delta)
+            b0 = torch.min(steps_t, torch.max(torch.full_like(emin, 0.), b0))
+            offset = -b0
+    return delta, offset, steps_t
+
+
+def lg_forward(x, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0):
+    """calculate_forward_pass (:191-249), float32: returns (y, mask, x_quant, delta_b, offset_b, steps)."""
+    delta, offset, steps = lg_encodings(bw, emin, emax, sym, strict, unsigned)
+    delta_b, offset_b = _bcast(x, delta, ch_axis), _bcast(x, offset, ch_axis)
+    zero = torch.zeros_like(steps)
+    x_round = torch.round(x / delta_b) - offset_b
+    x_quant = x_round.clamp(zero[0], steps[0])
+    y = (x_quant + offset_b) * delta_b
+    mask = x_round.ge(zero[0]) * x_round.le(steps[0])
+    return y, mask, x_quant, delta_b, offset_b, steps[0]
+
+
+def lg_gradients(x, grad, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0):
+    """(grad_x, grad_min, grad_max): QuantizeDequantizeFunc.backward + asymmetric/symmetric_gradients."""
+    y, mask, x_quant, delta, offset, steps = lg_forward(x, emin, emax, bw, sym, strict, unsigned, ch_axis)
+    grad_x = mask * grad
+    dims = list(range(x.dim()))
+    if emin.numel() > 1:
+        dims.pop(ch_axis)
+    if sym:
+        gmax = ((x_quant + offset) * grad).sum(dim=dims) - (mask * (x / delta) * grad).sum(dim=dims)
+        gmax = gmax / torch.div(steps, 2, rounding_mode="floor")
+        return grad_x, (-gmax).view_as(emin), gmax.view_as(emax)
+    grad_xq = delta * grad
+    grad_scale = (x_quant + offset - x * mask / delta) * grad
+    grad_offset = grad_xq * (~mask)
+    t1 = grad_scale.sum(dim=dims) / steps
+    t2 = steps / (emax - emin) ** 2 * grad_offset.sum(dim=dims)
+    return grad_x, (-t1 + emax * t2).view_as(emin), (t1 - emin * t2).view_as(emax)
+
+
+ZETA, GAMMA = 1.1, -0.1   # aimet_common/defs.py:302-306
+
+
+def adaround_forward(w, alpha, delta, offset, bw):
+    """AdaroundWrapper.apply_adaround (adaround_wrapper.py:124-149), soft rounding."""
+    t = torch.floor(w / delta)
+    h = torch.clamp(torch.sigmoid(alpha) * (ZETA - GAMMA) + GAMMA, 0, 1)
+    q = torch.clamp(t + h - offset, 0, 2 ** bw - 1)
+    return (q + offset) * delta
+
+
+def adaround_round_loss(alpha, reg, beta):
+    """AdaroundLoss.compute_round_loss after warm start (adaround_loss.py:97-110)."""
+    h = torch.clamp(torch.sigmoid(alpha) * (ZETA - GAMMA) + GAMMA, 0, 1)
+    return reg * torch.add(1, -(torch.add(2 * h, -1).abs()).pow(beta)).sum()

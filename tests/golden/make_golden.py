@@ -218,6 +218,35 @@ def main():
                         ste_mins=np.array(mins, np.float32), ste_maxs=np.array(maxs, np.float32),
                         ste_pc=ste_pc.numpy(), ste_pt=ste_pt.numpy(), tfe_kat_x=kdata)
 
+    # learned-grid forward/backward straight from the reference module (float32)
+    from types import SimpleNamespace
+    lg = {}
+    cases = [((4, 6, 5, 5), 1, 8, False), ((4, 6, 5, 5), 1, 8, True), ((8, 16, 3, 3), 8, 4, True),
+             ((16, 8, 3, 3), 16, 8, False), ((300,), 1, 8, False)]
+    gl = torch.Generator().manual_seed(9)
+    for i, (shape, C, bw, sym) in enumerate(cases):
+        x = torch.randn(shape, generator=gl) * 1.5
+        grad = torch.randn(shape, generator=gl)
+        if C == 1:
+            emin = torch.tensor([-2.0]) if not sym else torch.tensor([-2.5])
+            emax = torch.tensor([2.5])
+        else:
+            emax = torch.rand(C, generator=gl) + 0.5
+            emin = -emax if sym else -(torch.rand(C, generator=gl) + 0.3)
+        emin = emin.clone().requires_grad_(True)
+        emax = emax.clone().requires_grad_(True)
+        tq = SimpleNamespace(bitwidth=bw, use_symmetric_encodings=sym, is_unsigned_symmetric=False,
+                             use_strict_symmetric=False, channel_axis=0)
+        y, ir = ste.calculate_forward_pass(x, tq, emin, emax)
+        gmin, gmax = ste.calculate_gradients(x, grad, ir, 0)
+        lg["c%d_x" % i], lg["c%d_grad" % i] = x.numpy(), grad.numpy()
+        lg["c%d_emin" % i], lg["c%d_emax" % i] = emin.detach().numpy(), emax.detach().numpy()
+        lg["c%d_cfg" % i] = np.array([bw, int(sym)])
+        lg["c%d_y" % i], lg["c%d_gx" % i] = y.detach().numpy(), (ir.mask_tensor * grad).numpy()
+        lg["c%d_gmin" % i], lg["c%d_gmax" % i] = gmin.detach().numpy(), gmax.detach().numpy()
+    lg["count"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(HERE, "golden_lg.npz"), **lg)
+
     np.random.seed(0)
     alpha = torch.from_numpy(np.random.rand(1, 3, 12, 12))
     hp = AdaroundHyperParameters(num_iterations=10000, reg_param=0.01, beta_range=(20, 2), warm_start=0.2)

@@ -282,13 +282,10 @@ def test_quantize_dequantize_autograd_per_tensor_and_channel():
 # AdaRound
 # ------------------------------------------------------------------------------------------
 def _torch_adaround(w, alpha, delta, offset, bw, reg, beta):
-    """v1/adaround/adaround_wrapper.py:124-149 + adaround_loss.py:83-110 in float32 torch autograd."""
+    """oracle/torch_ref.adaround_forward under torch autograd (float32)."""
+    from oracle import torch_ref as T
     alpha = alpha.clone().requires_grad_(True)
-    t = torch.floor(w / delta)
-    h = torch.clamp(torch.sigmoid(alpha) * (1.1 - (-0.1)) + (-0.1), 0, 1)
-    q = torch.clamp(t + h - offset, 0, 2 ** bw - 1)
-    wq = (q + offset) * delta
-    return wq, alpha, h
+    return T.adaround_forward(w, alpha, delta, offset, bw), alpha, None
 
 
 def test_adaround_forward_backward_vs_torch(kat):
@@ -312,3 +309,65 @@ def test_adaround_forward_backward_vs_torch(kat):
     al = torch.from_numpy(np.random.rand(*k["shape"]).astype(np.float32)).to(DEV)
     loss, _ = round_loss_and_grad(al, k["reg_param"], kat["adaround_beta"]["expected"])
     assert abs(float(loss) - k["expected"]) < 1e-4
+
+
+def test_channel_plan_equals_individual_launches():
+    """All parameter QDQs in one launch == one launch per tensor (incl. K % 4 != 0, axis 1)."""
+    from aimet_amd.tensor_quantizer import ChannelQdqPlan, per_channel_view, qdq_per_channel_table
+    torch.manual_seed(5)
+    shapes = [((64, 3, 7, 7), 0), ((256, 64, 1, 1), 0), ((128, 128, 3, 3), 0), ((1000, 2048), 0),
+              ((32, 16, 3, 3), 1), ((5,), 0)]
+    entries, wants = [], []
+    for shape, ax in shapes:
+        w = torch.randn(shape, device=DEV) * 0.05
+        C = shape[ax]
+        encs = [enc_of(-0.1 - 0.001 * c, 0.12 + 0.001 * c, 8) for c in range(C)]
+        q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF)
+        table = q.channelTable(encs, torch.device(DEV)).clone()
+        outer, C_, K = per_channel_view(shape, ax)
+        wants.append(qdq_per_channel_table(w, table, outer, C_, K))
+        entries.append((w, torch.empty_like(w), ax, table))
+    plan = ChannelQdqPlan(entries)
+    plan.run()
+    for (w, y, ax, t), want in zip(entries, wants):
+        assert torch.equal(y, want)
+
+
+@pytest.mark.parametrize("case", range(5))
+def test_learned_grid_vs_reference_golden(golden_dir, case):
+    """Fused learned-grid fwd/bwd vs the reference module's outputs (golden_lg.npz): y and grad_x
+    bit-exact, encoding gradients to fp32 summation tolerance (rtol 1e-4)."""
+    import os
+    from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
+    g = dict(np.load(os.path.join(golden_dir, "golden_lg.npz")))
+    i = case
+    x = gpu(g["c%d_x" % i]).requires_grad_(True)
+    grad = gpu(g["c%d_grad" % i])
+    emin = gpu(g["c%d_emin" % i]).requires_grad_(True)
+    emax = gpu(g["c%d_emax" % i]).requires_grad_(True)
+    bw, sym = (int(v) for v in g["c%d_cfg" % i])
+    y = LearnedGridQuantizeDequantize.apply(x, emin, emax, bw, bool(sym), False, False, 0)
+    np.testing.assert_array_equal(bits(host(y)), bits(g["c%d_y" % i]))
+    y.backward(grad)
+    np.testing.assert_array_equal(bits(host(x.grad)), bits(g["c%d_gx" % i]))
+    np.testing.assert_allclose(host(emin.grad), g["c%d_gmin" % i], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(host(emax.grad), g["c%d_gmax" % i], rtol=1e-4, atol=1e-5)
+
+
+def test_learned_grid_large_vs_torch_ref():
+    """Llama-like weight (4096 x 4096, per-channel 4-bit symmetric): kernel vs torch restatement."""
+    from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
+    from oracle import torch_ref as T
+    torch.manual_seed(2)
+    w = (torch.randn(4096, 4096, device=DEV) * 0.02).requires_grad_(True)
+    emax = (w.detach().abs().amax(dim=1) * 0.9).requires_grad_(True)
+    emin = (-emax.detach()).clone().requires_grad_(True)
+    grad = torch.randn_like(w)
+    y = LearnedGridQuantizeDequantize.apply(w, emin, emax, 4, True, False, False, 0)
+    yr = T.lg_forward(w.detach(), emin.detach(), emax.detach(), 4, True)[0]
+    assert torch.equal(y, yr)
+    y.backward(grad)
+    gx, gmin, gmax = T.lg_gradients(w.detach(), grad, emin.detach(), emax.detach(), 4, True)
+    assert torch.equal(w.grad, gx)
+    torch.testing.assert_close(emax.grad, gmax, rtol=2e-4, atol=1e-4)
+    torch.testing.assert_close(emin.grad, gmin, rtol=2e-4, atol=1e-4)

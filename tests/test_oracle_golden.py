@@ -141,3 +141,31 @@ def test_oracle_vs_compiled_reference_random():
             b.update(x)
         for fl in [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]:
             assert a.compute(8, *fl).as_tuple() == b.compute(8, *fl).as_tuple()
+
+
+def test_torch_ref_learned_grid_vs_reference_python(golden_dir):
+    """oracle/torch_ref.py (learned-grid restatement) == the reference module's own outputs."""
+    import os
+    import torch
+    from oracle import torch_ref as T
+    g = dict(np.load(os.path.join(golden_dir, "golden_lg.npz")))
+    for i in range(int(g["count"])):
+        x, grad = torch.from_numpy(g["c%d_x" % i]), torch.from_numpy(g["c%d_grad" % i])
+        emin, emax = torch.from_numpy(g["c%d_emin" % i]), torch.from_numpy(g["c%d_emax" % i])
+        bw, sym = (int(v) for v in g["c%d_cfg" % i])
+        y = T.lg_forward(x, emin, emax, bw, bool(sym))[0]
+        np.testing.assert_array_equal(bits(y.numpy()), bits(g["c%d_y" % i]))
+        gx, gmin, gmax = T.lg_gradients(x, grad, emin, emax, bw, bool(sym))
+        np.testing.assert_array_equal(bits(gx.numpy()), bits(g["c%d_gx" % i]))
+        np.testing.assert_allclose(gmin.numpy(), g["c%d_gmin" % i], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(gmax.numpy(), g["c%d_gmax" % i], rtol=1e-6, atol=1e-6)
+
+
+def test_torch_ref_adaround_round_loss_kat(kat):
+    import torch
+    from oracle import torch_ref as T
+    k = kat["adaround_round_loss"]
+    np.random.seed(k["seed"])
+    alpha = torch.from_numpy(np.random.rand(*k["shape"]))
+    loss = T.adaround_round_loss(alpha, k["reg_param"], kat["adaround_beta"]["expected"])
+    assert abs(float(loss) - k["expected"]) < 10 ** -k["places"]
