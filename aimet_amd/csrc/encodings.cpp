@@ -13,6 +13,7 @@
 //   Percentile                     PercentileEncodingAnalyzer.cpp:78-190, math_functions.cpp:404-439
 //   MSE                            MseEncodingAnalyzer.cpp:79-264
 #include "encodings.hpp"
+#include "tfe_core.hpp"
 
 #include <algorithm>
 #include <cfloat>
@@ -28,7 +29,6 @@ namespace
 {
 constexpr double kGateEps  = 1e-5;   // quantization_utils.hpp:51 EPSILON
 constexpr double kMinRange = 0.01;   // TfEncodingAnalyzer.h:81 / TfEnhancedEncodingAnalyzer.h:105
-constexpr float kGammaTfe  = 3.0f;   // TfEnhancedEncodingAnalyzer.h:102 (DTYPE)
 constexpr float kFltLowest = std::numeric_limits<float>::lowest();
 constexpr float kFltMax    = std::numeric_limits<float>::max();
 
@@ -228,125 +228,50 @@ aimet_tf_encoding unseen_or_zero(bool stats_updated, int32_t bw, float steps)
     return make_enc(lo, lo + isteps * delta, delta, off, bw);
 }
 
-// ---- TF-Enhanced --------------------------------------------------------------------------
-struct Candidate
-{
-    float delta;
-    int offset;
-};
-
-double tfe_cost(const HistView& h, int32_t bw, float delta, int offset)
-{
-    const float lo       = delta * offset;
-    const float steps    = (float) (std::pow(2.0, bw) - 1);
-    const float hi       = delta * (offset + steps);
-    const float start    = (float) h.xl(0);
-    const double step    = h.xl(1) - h.xl(0);
-    auto index           = [&](float v) {
-        int i = (int) std::floor((v - start) / step);
-        return std::min(std::max(0, i), kPdfSize - 1);
-    };
-    const int iLo = index(lo), iHi = index(hi);
-    auto mid      = [&](int i) { return start + i * step + step / 2; };   // double
-    const float loMid = (float) (start + (iLo * step) + step / 2);
-    const float hiMid = (float) (start + (iHi * step) + step / 2);
-
-    double satLo = 0, satHi = 0, quant = 0;
-    for (int i = 0; i < iLo; ++i)
-        satLo += h.pdf[i] * sq(mid(i) - loMid);
-    for (int i = iHi; i < kPdfSize; ++i)
-        satHi += h.pdf[i] * sq(mid(i) - hiMid);
-    for (int i = iLo; i < iHi; ++i)
-    {
-        float v   = (float) mid(i);
-        int q     = (int) std::round(v / delta - offset);
-        float deq = delta * (q + offset);
-        quant += h.pdf[i] * sq((double) (v - deq));
-    }
-    double cost = kGammaTfe * (satLo + satHi) + quant;
-    return std::min(cost, std::numeric_limits<double>::max());
-}
-
-bool tfe_clamp_candidate(float obsLo, float obsHi, float steps, float& delta, int& offset)
-{
-    float lo = std::max(delta * offset, kFltLowest);
-    float hi = std::min(delta * (offset + steps), kFltMax);
-    if (lo < obsLo && hi > obsHi)
-        return false;
-    lo = std::max(obsLo, lo);
-    hi = std::min(obsHi, hi);
-    if (lo == hi)
-        return false;
-    delta  = (float) (((double) hi - lo) / steps);
-    offset = (int) std::round(lo / delta);
-    return true;
-}
-
-void tfe_candidates_asym(float obsLo, float obsHi, float steps, std::vector<Candidate>& out)
-{
-    const float d0 = (float) (((double) obsHi - (double) obsLo) / steps);
-    const int o0   = (int) std::round(obsLo / d0);
-    obsLo          = std::max(d0 * o0, kFltLowest);
-    obsHi          = std::min(d0 * (o0 + steps), kFltMax);
-    // 17 deltas f*d0, f = 1/16 .. 17/16 (float accumulator, double compare), x 21 offsets
-    for (float f = 1.0 / 16; f <= 1 + 1.0 / 16; f += 1.0 / 16)
-        for (int i = 0; i <= 20; ++i)
-        {
-            float d = f * d0;
-            int o   = (int) (-steps + steps / 20.0 * i);
-            if (tfe_clamp_candidate(obsLo, obsHi, steps, d, o))
-                out.push_back({d, o});
-        }
-    out.push_back({d0, o0});
-}
-
-void tfe_candidates_sym(float lo, float hi, float steps, bool unsign, std::vector<Candidate>& out)
-{
-    float dmax = 0.0f;
-    int off    = 0;
-    if (lo == 0.0 && unsign)
-        dmax = hi / steps;
-    else
-    {
-        float absmax = std::max(std::abs(hi), std::abs(lo));
-        dmax         = (float) (absmax / (steps / 2.0));
-        off          = (int) std::floor(-steps / 2);
-    }
-    for (float f = 1.0 / 100; f <= 1 + 1.0 / 100; f += 1.0 / 100)
-        out.push_back({f * dmax, off});
-}
-
+// ---- TF-Enhanced (tfe_core.hpp: shared with the device search in tfe_search.hip) ---------
 aimet_tf_encoding tfe_encoding(const HistView& h, int32_t bw, bool sym, bool strict, bool unsign)
 {
-    auto range  = observed_range(h);
-    float steps = (float) (std::pow(2.0, bw) - 1);
-    std::vector<Candidate> cands;
-    cands.reserve(400);
+    int first = -1, last = -1;
+    for (int i = 0; i < kPdfSize; ++i)
+        if (h.pdf[i] > 0)
+        {
+            first = i;
+            break;
+        }
+    for (int i = kPdfSize - 1; i > 0; --i)
+        if (h.pdf[i] > 0)
+        {
+            last = i;
+            break;
+        }
+    tfe::Hist th {h.hist_min, h.bucket, h.pdf};
+    float lo, hi;
+    tfe::observed_range(th, first, last, lo, hi);
+    tfe::Setup st = tfe::setup(lo, hi, bw, sym, strict, unsign);
+    float fseq[tfe::kSymF + 8];
     if (sym)
-    {
-        if (strict)
-            steps -= 1;
-        tfe_candidates_sym(range.first, range.second, steps, unsign, cands);
-    }
+        tfe::fseq_sym(fseq);
     else
-        tfe_candidates_asym(range.first, range.second, steps, cands);
-
+        tfe::fseq_asym(fseq);
     float bestDelta = -1;
     int bestOffset  = -1;
     double best     = std::numeric_limits<double>::max();
-    for (const auto& c: cands)
+    for (int t = 0; t < st.ncand; ++t)
     {
-        double cost = tfe_cost(h, bw, c.delta, c.offset);
-        if (cost < best)
+        float d;
+        int o;
+        if (!tfe::candidate(st, fseq, t, d, o))
+            continue;
+        double c = tfe::cost(th, bw, d, o);
+        if (c < best)
         {
-            best       = cost;
-            bestDelta  = c.delta;
-            bestOffset = c.offset;
+            best       = c;
+            bestDelta  = d;
+            bestOffset = o;
         }
     }
-    float lo = std::max(bestDelta * bestOffset, kFltLowest);
-    float hi = std::min(bestDelta * (bestOffset + steps), kFltMax);
-    return make_enc(lo, hi, bestDelta, bestOffset, bw);
+    tfe::Result r = tfe::finish(st, bestDelta, bestOffset);
+    return make_enc(r.min, r.max, r.delta, r.offset, bw);
 }
 
 // ---- Percentile ---------------------------------------------------------------------------

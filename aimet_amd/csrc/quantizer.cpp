@@ -73,11 +73,13 @@ void layout(aimet_tensor_quantizer* q, bool assign)
     {
         q->d.pdf    = (double*) take(sizeof(double) * kPdfSize * C);
         q->d.counts = (unsigned long long*) take(sizeof(unsigned long long) * kPdfSize * C);
+        q->d.enc    = (aimet_tf_encoding*) take(sizeof(aimet_tf_encoding) * C);
     }
     else
     {
         q->d.pdf    = nullptr;
         q->d.counts = nullptr;
+        q->d.enc    = nullptr;
     }
     q->arena_bytes = off;
 }
@@ -349,6 +351,15 @@ int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int sym, int s
             parallel_channels(C, [&](int64_t c) {
                 out[c] = tf_encoding(acc[2 * c], acc[2 * c + 1], b, sym, strict, unsign);
             });
+            return;
+        }
+        if (q->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
+        {
+            // candidate search on the device (tfe_search.hip), only the encodings come back
+            launch_tfe_search(q->d, C, b, sym, strict, unsign, true, q->d.enc, as_stream(stream));
+            AIMET_HIP_CHECK(hipMemcpyAsync(out, q->d.enc, sizeof(aimet_tf_encoding) * C, hipMemcpyDeviceToHost,
+                                           as_stream(stream)));
+            AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
             return;
         }
         auto init  = d2h(q->d.pdf_init, C);

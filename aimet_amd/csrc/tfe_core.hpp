@@ -1,0 +1,220 @@
+// tfe_core.hpp -- TF-Enhanced encoding search, one source for the host (encodings.cpp) and the
+// device (tfe_search.hip): TfEnhancedEncodingAnalyzer.cpp:115-392 with DTYPE = float.
+//
+// Every expression keeps the reference's evaluation types (float vs double), std::min/std::max
+// tie rules and std::round (half away from zero); pow(v, 2) is v*v as the reference build
+// (-O3) folds it. Compiled with -ffp-contract=off on both sides, IEEE fp32/fp64 division.
+#pragma once
+
+#include <cfloat>
+#include <cmath>
+
+#if defined(__HIPCC__)
+#define AIMET_HD __host__ __device__
+#else
+#define AIMET_HD
+#endif
+
+namespace aimet_amd
+{
+namespace tfe
+{
+
+constexpr int kBins        = 512;
+constexpr float kGamma     = 3.0f;     // TfEnhancedEncodingAnalyzer.h:102 (DTYPE)
+constexpr float kMinRangeF = (float) 0.01;
+constexpr int kAsymF       = 17;       // deltas f = 1/16 .. 17/16
+constexpr int kAsymO       = 21;       // offsets i = 0 .. 20
+constexpr int kSymF        = 101;      // deltas f = 1/100 .. 101/100
+constexpr int kMaxCand     = kAsymF * kAsymO + 1;
+
+template <class T>
+AIMET_HD inline T smin(T a, T b)
+{
+    return (b < a) ? b : a;   // std::min
+}
+template <class T>
+AIMET_HD inline T smax(T a, T b)
+{
+    return (a < b) ? b : a;   // std::max
+}
+
+// PDF of one channel: xLeft[i] = (double)hist_min + (double)i * bucket (InitializePdf)
+struct Hist
+{
+    float hist_min;
+    double bucket;
+    const double* pdf;
+    AIMET_HD double xl(int i) const
+    {
+        return (double) hist_min + (double) i * bucket;
+    }
+};
+
+// _findRangeOfAggregateStats (:255-291) given the first / last non-empty bins (-1: none;
+// `last` only scans i > 0 like the reference loop).
+AIMET_HD inline void observed_range(const Hist& h, int first, int last, float& lo, float& hi)
+{
+    lo = (float) h.xl(0);
+    hi = (float) h.xl(kBins - 1);
+    if (first >= 0)
+        lo = (float) h.xl(first);
+    if (last >= 0)
+        hi = (float) h.xl(last);
+    lo = smin(lo, 0.0f);
+    hi = smax(hi, 0.0f);
+    hi = smax(hi, lo + kMinRangeF);
+}
+
+// f sequences of the candidate loops: float accumulator, double comparison (data independent)
+AIMET_HD inline int fseq_asym(float* f)
+{
+    int n = 0;
+    for (float v = 1.0 / 16; v <= 1 + 1.0 / 16; v += 1.0 / 16)
+        f[n++] = v;
+    return n;
+}
+AIMET_HD inline int fseq_sym(float* f)
+{
+    int n = 0;
+    for (float v = 1.0 / 100; v <= 1 + 1.0 / 100; v += 1.0 / 100)
+        f[n++] = v;
+    return n;
+}
+
+// _clampToObservedMinMax (:144-170)
+AIMET_HD inline bool clamp_candidate(float obsLo, float obsHi, float steps, float& delta, int& offset)
+{
+    float lo = smax(delta * offset, -FLT_MAX);
+    float hi = smin(delta * (offset + steps), FLT_MAX);
+    if (lo < obsLo && hi > obsHi)
+        return false;
+    lo = smax(obsLo, lo);
+    hi = smin(obsHi, hi);
+    if (lo == hi)
+        return false;
+    delta  = (float) (((double) hi - lo) / steps);
+    offset = (int) roundf(lo / delta);
+    return true;
+}
+
+// Search parameters of one channel, derived from the observed range.
+struct Setup
+{
+    bool sym;
+    float steps;        // numSteps (strict-reduced for symmetric strict)
+    // asymmetric
+    float obsLo, obsHi, d0;
+    int o0;
+    // symmetric
+    float dmax;
+    int symOffset;
+    int ncand;
+};
+
+AIMET_HD inline Setup setup(float lo, float hi, int bw, bool sym, bool strict, bool unsign)
+{
+    Setup s {};
+    s.sym   = sym;
+    s.steps = (float) (ldexp(1.0, bw) - 1);   // pow(2, bw) - 1, exact
+    if (sym)
+    {
+        if (strict)
+            s.steps -= 1;
+        if ((lo == 0.0) && unsign)
+        {
+            s.dmax      = hi / s.steps;
+            s.symOffset = 0;
+        }
+        else
+        {
+            float absmax = smax(fabsf(hi), fabsf(lo));
+            s.dmax       = (float) (absmax / (s.steps / 2.0));
+            s.symOffset  = (int) floorf(-s.steps / 2);
+        }
+        s.ncand = kSymF;
+    }
+    else
+    {
+        s.d0    = (float) (((double) hi - (double) lo) / s.steps);
+        s.o0    = (int) roundf(lo / s.d0);
+        s.obsLo = smax(s.d0 * s.o0, -FLT_MAX);
+        s.obsHi = smin(s.d0 * (s.o0 + s.steps), FLT_MAX);
+        s.ncand = kAsymF * kAsymO + 1;
+    }
+    return s;
+}
+
+// Candidate t in the reference's order; false when _clampToObservedMinMax drops it.
+AIMET_HD inline bool candidate(const Setup& s, const float* fseq, int t, float& delta, int& offset)
+{
+    if (s.sym)
+    {
+        delta  = fseq[t] * s.dmax;
+        offset = s.symOffset;
+        return true;
+    }
+    if (t == kAsymF * kAsymO)
+    {
+        delta  = s.d0;
+        offset = s.o0;
+        return true;
+    }
+    int k  = t / kAsymO, i = t % kAsymO;
+    delta  = fseq[k] * s.d0;
+    offset = (int) (-s.steps + s.steps / 20.0 * i);
+    return clamp_candidate(s.obsLo, s.obsHi, s.steps, delta, offset);
+}
+
+// _quantAndSatCost (:293-355)
+AIMET_HD inline double cost(const Hist& h, int bw, float delta, int offset)
+{
+    const float lo     = delta * offset;
+    const float steps  = (float) (ldexp(1.0, bw) - 1);
+    const float hi     = delta * (offset + steps);
+    const float start  = (float) h.xl(0);
+    const double step  = h.xl(1) - h.xl(0);
+    int iLo            = (int) floor((lo - start) / step);
+    iLo                = smin(smax(0, iLo), kBins - 1);
+    int iHi            = (int) floor((hi - start) / step);
+    iHi                = smin(smax(0, iHi), kBins - 1);
+    const float loMid  = (float) (start + (iLo * step) + step / 2);
+    const float hiMid  = (float) (start + (iHi * step) + step / 2);
+    double satLo = 0, satHi = 0, quant = 0;
+    for (int i = 0; i < iLo; ++i)
+    {
+        double d = (start + i * step + step / 2) - loMid;
+        satLo += h.pdf[i] * (d * d);
+    }
+    for (int i = iHi; i < kBins; ++i)
+    {
+        double d = (start + i * step + step / 2) - hiMid;
+        satHi += h.pdf[i] * (d * d);
+    }
+    for (int i = iLo; i < iHi; ++i)
+    {
+        float v   = (float) (start + i * step + step / 2);
+        int q     = (int) roundf(v / delta - offset);
+        float deq = delta * (q + offset);
+        double d  = (double) (v - deq);
+        quant += h.pdf[i] * (d * d);
+    }
+    double c = kGamma * (satLo + satHi) + quant;
+    return smin(c, DBL_MAX);
+}
+
+struct Result
+{
+    double min, max, delta, offset;
+};
+
+// getComputedEncodings (:357-392) tail from the best candidate
+AIMET_HD inline Result finish(const Setup& s, float bestDelta, int bestOffset)
+{
+    float lo = smax(bestDelta * bestOffset, -FLT_MAX);
+    float hi = smin(bestDelta * (bestOffset + s.steps), FLT_MAX);
+    return Result {lo, hi, bestDelta, (double) bestOffset};
+}
+
+}   // namespace tfe
+}   // namespace aimet_amd

@@ -27,6 +27,7 @@ struct TqDevice
     float* bin_offset;      // [C] (float)xLeft[0] / bin_bucket    UpdatePdf:265-268
     double* pdf;            // [C][512]
     unsigned long long* counts;   // [C][512] histogram of the current batch
+    aimet_tf_encoding* enc; // [C] device-computed encodings (TF-Enhanced search)
 };
 
 constexpr int kMinmaxParts = 1024;   // grid of the per-tensor min/max pass
@@ -38,5 +39,8 @@ void launch_fold_minmax(const TqDevice& d, int64_t C, bool tf_scheme, hipStream_
 void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, hipStream_t s);
 void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStream_t s);
 void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s);
+// tfe_search.hip
+void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, bool stats_updated,
+                       aimet_tf_encoding* out, hipStream_t s);
 
 }   // namespace aimet_amd

@@ -214,6 +214,33 @@ def test_per_channel_stats_vs_per_channel_oracle(scheme, shape, axis):
             assert encs[c].to_tuple() == orcs[c].compute(8, *fl).as_tuple(), (c, fl)
 
 
+def test_tfe_device_search_many_channels():
+    """Device TF-Enhanced search (tfe_search.hip, one workgroup per channel) == the oracle's
+    host search for 600 channels of varied shape, every flag set and bit-width."""
+    rng = np.random.default_rng(21)
+    C, K = 600, 96
+    scale = rng.uniform(1e-3, 30, (C, 1))
+    shift = rng.uniform(-3, 3, (C, 1))
+    x = rng.standard_t(3, (C, K)) * scale + shift * scale
+    x[5] = 0.0
+    x[7] = np.abs(x[7])
+    x[9, :] = 2.5                                   # constant channel
+    x = x.astype(np.float32)
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=C)
+    q.updateStatsPerChannel(gpu(x), 0, True)
+    orcs = []
+    for c in range(C):
+        o = O.Analyzer(O.QUANTIZATION_TF_ENHANCED)
+        o.update(x[c])
+        orcs.append(o)
+    for bw in (4, 8, 16):
+        for fl in FLAGS:
+            encs, valid = q.getEncoding(bw, *fl)
+            assert valid
+            for c in range(C):
+                assert encs[c].to_tuple() == orcs[c].compute(bw, *fl).as_tuple(), (c, bw, fl)
+
+
 def test_minmax_and_histogram_full_size():
     """Stats of a 205M-element activation: TF encoding == oracle over the whole tensor, TF-E PDF
     == oracle PDF (bit-exact) and sums to the in-range fraction."""
