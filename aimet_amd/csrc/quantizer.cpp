@@ -331,45 +331,117 @@ int aimet_tq_mark_stats_updated(aimet_tensor_quantizer* q)
     });
 }
 
+namespace
+{
+
+bool device_search(const aimet_tensor_quantizer* q)
+{
+    return q->hist && q->scheme == AIMET_QUANTIZATION_TF_ENHANCED;
+}
+
+// getEncoding, part 1: enqueue the device-side search (TF-Enhanced) on the stream.
+void launch_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict, int unsign, hipStream_t s)
+{
+    if (device_search(q))
+        launch_tfe_search(q->d, q->C, b, sym, strict, unsign, s);
+}
+
+// getEncoding, part 2 (stream already synchronised): read back and finish on the host.
+void collect_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict, int unsign, aimet_tf_encoding* out)
+{
+    const int64_t C = q->C;
+    if (!q->hist)
+    {
+        auto acc = d2h(q->d.acc, 2 * C);
+        parallel_channels(C, [&](int64_t c) {
+            out[c] = tf_encoding(acc[2 * c], acc[2 * c + 1], b, sym, strict, unsign);
+        });
+        return;
+    }
+    if (device_search(q))
+    {
+        // candidate search ran on the device (tfe_search.hip): only the encodings come back
+        AIMET_HIP_CHECK(hipMemcpy(out, q->d.enc, sizeof(aimet_tf_encoding) * C, hipMemcpyDeviceToHost));
+        return;
+    }
+    auto init = d2h(q->d.pdf_init, C);
+    auto hmin = d2h(q->d.hist_min, C);
+    auto bsz  = d2h(q->d.bucket_size, C);
+    auto pdf  = d2h(q->d.pdf, (size_t) kPdfSize * C);
+    parallel_channels(C, [&](int64_t c) {
+        out[c] = histogram_encoding(q->scheme, init[c] != 0, true, hmin[c], bsz[c], pdf.data() + kPdfSize * c,
+                                    q->percentile, b, sym, strict, unsign);
+    });
+}
+
+}   // namespace
+
 int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int sym, int strict, int unsign,
                           aimet_tf_encoding* out, int* valid, void* stream)
 {
     return guarded([&] {
         AIMET_REQUIRE(q != nullptr && out != nullptr, "null argument");
-        const int64_t C = q->C;
-        std::memset(out, 0, sizeof(aimet_tf_encoding) * C);
+        std::memset(out, 0, sizeof(aimet_tf_encoding) * q->C);
         if (valid)
             *valid = q->stats_updated ? 1 : 0;
         if (!q->stats_updated)
             return;   // AimetTensorQuantizer.cpp:185-189: encoding left default, valid = false
         DeviceGuard g(q->device);
-        AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
         const int32_t b = (int32_t) (uint8_t) bw;   // computeEncoding(uint8_t bw, ...)
-        if (!q->hist)
+        launch_encoding(q, b, sym, strict, unsign, as_stream(stream));
+        AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+        collect_encoding(q, b, sym, strict, unsign, out);
+    });
+}
+
+int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym, int strict,
+                           int unsign, aimet_tf_encoding* out, int* valid, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(qs != nullptr && out != nullptr && nq >= 0, "null argument");
+        int64_t total = 0;
+        for (int64_t i = 0; i < nq; ++i)
         {
-            auto acc = d2h(q->d.acc, 2 * C);
-            parallel_channels(C, [&](int64_t c) {
-                out[c] = tf_encoding(acc[2 * c], acc[2 * c + 1], b, sym, strict, unsign);
-            });
-            return;
+            AIMET_REQUIRE(qs[i] != nullptr, "null quantizer");
+            AIMET_REQUIRE(qs[i]->device == qs[0]->device, "quantizers of one batched getEncoding share a device");
+            total += qs[i]->C;
         }
-        if (q->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
+        std::memset(out, 0, sizeof(aimet_tf_encoding) * total);
+        if (nq == 0)
+            return;
+        DeviceGuard g(qs[0]->device);
+        const int32_t b = (int32_t) (uint8_t) bw;
+        // every TF-Enhanced search in ONE launch (one workgroup per channel of every quantizer),
+        // results back in one copy; the other schemes read back their statistics per quantizer
+        std::vector<const TqDevice*> ds;
+        std::vector<int64_t> Cs, offs;
+        int64_t off = 0, tfe_total = 0;
+        for (int64_t i = 0; i < nq; ++i)
         {
-            // candidate search on the device (tfe_search.hip), only the encodings come back
-            launch_tfe_search(q->d, C, b, sym, strict, unsign, true, q->d.enc, as_stream(stream));
-            AIMET_HIP_CHECK(hipMemcpyAsync(out, q->d.enc, sizeof(aimet_tf_encoding) * C, hipMemcpyDeviceToHost,
-                                           as_stream(stream)));
-            AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
-            return;
+            if (valid)
+                valid[i] = qs[i]->stats_updated ? 1 : 0;
+            if (qs[i]->stats_updated && device_search(qs[i]))
+            {
+                ds.push_back(&qs[i]->d);
+                Cs.push_back(qs[i]->C);
+                offs.push_back(off);
+                tfe_total += qs[i]->C;
+            }
+            off += qs[i]->C;
         }
-        auto init  = d2h(q->d.pdf_init, C);
-        auto hmin  = d2h(q->d.hist_min, C);
-        auto bsz   = d2h(q->d.bucket_size, C);
-        auto pdf   = d2h(q->d.pdf, (size_t) kPdfSize * C);
-        parallel_channels(C, [&](int64_t c) {
-            out[c] = histogram_encoding(q->scheme, init[c] != 0, true, hmin[c], bsz[c], pdf.data() + kPdfSize * c,
-                                        q->percentile, b, sym, strict, unsign);
-        });
+        std::vector<aimet_tf_encoding> tfe(tfe_total);
+        launch_tfe_search_many(ds.data(), Cs.data(), (int) ds.size(), b, sym, strict, unsign, tfe.data(),
+                               as_stream(stream));
+        for (size_t k = 0, src = 0; k < ds.size(); src += Cs[k], ++k)
+            std::memcpy(out + offs[k], tfe.data() + src, sizeof(aimet_tf_encoding) * Cs[k]);
+        AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+        off = 0;
+        for (int64_t i = 0; i < nq; ++i)
+        {
+            if (qs[i]->stats_updated && !device_search(qs[i]))
+                collect_encoding(qs[i], b, sym, strict, unsign, out + off);
+            off += qs[i]->C;
+        }
     });
 }
 

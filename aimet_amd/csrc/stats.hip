@@ -26,7 +26,10 @@ namespace aimet_amd
 namespace
 {
 
-constexpr int kWaves = kBlock / 64;
+constexpr int kWaves      = kBlock / 64;
+constexpr int kHistUnroll = 4;
+constexpr int kHistGrid   = 2048;   // 8 workgroups per CU: enough 16-B loads in flight for HBM
+typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float wave_min(float v)
 {
@@ -274,21 +277,27 @@ __global__ __launch_bounds__(kBlock) void histogram_tensor_kernel(const float* _
     int64_t done = 0;
     if (vec)
     {
-        const float4* x4     = reinterpret_cast<const float4*>(x);
-        int64_t nv           = n / 4;
-        const int64_t stride = (int64_t) gridDim.x * kBlock * 2;
-        for (int64_t b = (int64_t) blockIdx.x * kBlock * 2 + threadIdx.x; b < nv; b += stride)
+        // 4 x 16-B streaming loads in flight per lane (tools/hist_variants.hip: 5.6-5.8 TB/s)
+        const f4* x4         = reinterpret_cast<const f4*>(x);
+        const int64_t nv     = n / 4;
+        const int64_t stride = (int64_t) gridDim.x * kBlock * kHistUnroll;
+        for (int64_t base = (int64_t) blockIdx.x * kBlock * kHistUnroll + threadIdx.x; base < nv; base += stride)
         {
-            float4 v0 = x4[b];
-            float4 v1 = (b + kBlock < nv) ? x4[b + kBlock] : make_float4(NAN, NAN, NAN, NAN);
-            add(v0.x);
-            add(v0.y);
-            add(v0.z);
-            add(v0.w);
-            add(v1.x);   // NaN padding is dropped by the binner
-            add(v1.y);
-            add(v1.z);
-            add(v1.w);
+            f4 v[kHistUnroll];
+#pragma unroll
+            for (int u = 0; u < kHistUnroll; ++u)
+            {
+                int64_t i = base + (int64_t) u * kBlock;
+                v[u]      = i < nv ? __builtin_nontemporal_load(x4 + i) : f4 {NAN, NAN, NAN, NAN};
+            }
+#pragma unroll
+            for (int u = 0; u < kHistUnroll; ++u)
+            {
+                add(v[u].x);   // NaN padding is dropped by the binner
+                add(v[u].y);
+                add(v[u].z);
+                add(v[u].w);
+            }
         }
         done = nv * 4;
     }
@@ -447,11 +456,11 @@ void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, in
     if (C == 1)
     {
         int64_t n  = outer * K;
-        // enough workgroups to fill the chip, few enough that the per-bin global atomics stay
-        // a small fraction of the pass (<= 512 x 512 64-bit adds)
-        int blocks = stream_blocks(n, (int64_t) kBlock * 32);
-        if (blocks > 512)
-            blocks = 512;
+        // enough workgroups to keep HBM busy (8 per CU), few enough that the per-bin global atomics
+        // stay a small fraction of the pass (<= 2048 x 512 64-bit adds, spread over 32 lines)
+        int blocks = stream_blocks(n, (int64_t) kBlock * kHistUnroll * 4 * 4);
+        if (blocks > kHistGrid)
+            blocks = kHistGrid;
         histogram_tensor_kernel<<<blocks, kBlock, 0, s>>>(x, n, al ? 1 : 0, d);
     }
     else

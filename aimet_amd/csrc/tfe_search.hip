@@ -10,6 +10,8 @@
 #include "tfe_core.hpp"
 #include "tq_state.hpp"
 
+#include <vector>
+
 namespace aimet_amd
 {
 namespace
@@ -34,9 +36,19 @@ __device__ __forceinline__ bool better(const Best& a, const Best& b)
     return (a.cost < b.cost) || (a.cost == b.cost && a.idx < b.idx);
 }
 
-__global__ __launch_bounds__(kBlock) void tfe_search_kernel(TqDevice d, int64_t C, int bw, int sym, int strict,
-                                                            int unsign, int stats_updated,
-                                                            aimet_tf_encoding* __restrict__ out)
+// One quantizer's statistics and output; a batched getEncoding passes one job per quantizer.
+struct TfeJob
+{
+    const int32_t* pdf_init;
+    const float* hist_min;
+    const double* bucket_size;
+    const double* pdf;
+    aimet_tf_encoding* out;
+    int64_t start;   // first global channel of this job
+};
+
+__global__ __launch_bounds__(kBlock) void tfe_search_kernel(TfeJob one, const TfeJob* __restrict__ jobs, int njobs,
+                                                            int64_t total, int bw, int sym, int strict, int unsign)
 {
     __shared__ double pdf[tfe::kBins];
     __shared__ float fseq[tfe::kSymF + 8];
@@ -49,28 +61,41 @@ __global__ __launch_bounds__(kBlock) void tfe_search_kernel(TqDevice d, int64_t 
         else
             tfe::fseq_asym(fseq);
     }
-    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+    for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
     {
-        if (!d.pdf_init[c])
+        TfeJob j = one;
+        if (jobs)
+        {
+            int lo = 0, hi = njobs - 1;   // last job with start <= g
+            while (lo < hi)
+            {
+                int mid = (lo + hi + 1) >> 1;
+                if (jobs[mid].start <= g)
+                    lo = mid;
+                else
+                    hi = mid - 1;
+            }
+            j = jobs[lo];
+        }
+        const int64_t c = g - j.start;
+        if (!j.pdf_init[c])
         {
             if (threadIdx.x == 0)
             {
-                aimet_tf_encoding e {0, 0, 0, 0, 0};
-                if (stats_updated)   // all-zero data seen (TfEnhancedEncodingAnalyzer.cpp:86-99)
-                {
-                    int isteps = (int) (float) (ldexp(1.0, bw) - 1);
-                    e.delta    = (1.0 - (-1.0)) / isteps;
-                    e.offset   = floor(-1.0 / e.delta);
-                    e.min      = e.offset * e.delta;
-                    e.max      = e.min + isteps * e.delta;
-                    e.bw       = bw;
-                }
-                out[c] = e;
+                // statistics updated but all data zero (TfEnhancedEncodingAnalyzer.cpp:86-99)
+                int isteps = (int) (float) (ldexp(1.0, bw) - 1);
+                aimet_tf_encoding e;
+                e.delta    = (1.0 - (-1.0)) / isteps;
+                e.offset   = floor(-1.0 / e.delta);
+                e.min      = e.offset * e.delta;
+                e.max      = e.min + isteps * e.delta;
+                e.bw       = bw;
+                j.out[c]   = e;
             }
             continue;
         }
         for (int i = threadIdx.x; i < tfe::kBins; i += kBlock)
-            pdf[i] = d.pdf[c * tfe::kBins + i];
+            pdf[i] = j.pdf[c * tfe::kBins + i];
         if (threadIdx.x == 0)
         {
             first = tfe::kBins;
@@ -85,7 +110,7 @@ __global__ __launch_bounds__(kBlock) void tfe_search_kernel(TqDevice d, int64_t 
                     atomicMax(&last, i);
             }
         __syncthreads();
-        tfe::Hist h {d.hist_min[c], d.bucket_size[c], pdf};
+        tfe::Hist h {j.hist_min[c], j.bucket_size[c], pdf};
         float lo, hi;
         tfe::observed_range(h, first < tfe::kBins ? first : -1, last, lo, hi);
         tfe::Setup st = tfe::setup(lo, hi, bw, sym != 0, strict != 0, unsign != 0);
@@ -126,20 +151,58 @@ __global__ __launch_bounds__(kBlock) void tfe_search_kernel(TqDevice d, int64_t 
             float bd = b.idx >= 0 ? b.delta : -1.0f;
             int bo   = b.idx >= 0 ? b.offset : -1;
             tfe::Result r = tfe::finish(st, bd, bo);
-            out[c]        = aimet_tf_encoding {r.min, r.max, r.delta, r.offset, bw};
+            j.out[c]      = aimet_tf_encoding {r.min, r.max, r.delta, r.offset, bw};
         }
         __syncthreads();
     }
 }
 
+TfeJob job_of(const TqDevice& d, int64_t start)
+{
+    return TfeJob {d.pdf_init, d.hist_min, d.bucket_size, d.pdf, d.enc, start};
+}
+
+int grid_of(int64_t total)
+{
+    return (int) (total < 65536 ? total : 65536);
+}
+
 }   // namespace
 
-void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, bool stats_updated,
-                       aimet_tf_encoding* out, hipStream_t s)
+void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s)
 {
-    int grid = (int) (C < 65536 ? C : 65536);
-    tfe_search_kernel<<<grid, kBlock, 0, s>>>(d, C, bw, sym, strict, unsign, stats_updated, out);
+    tfe_search_kernel<<<grid_of(C), kBlock, 0, s>>>(job_of(d, 0), nullptr, 0, C, bw, sym, strict, unsign);
     AIMET_LAUNCH_CHECK();
+}
+
+void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
+                            bool unsign, aimet_tf_encoding* host_out, hipStream_t s)
+{
+    if (n == 0)
+        return;
+    std::vector<TfeJob> jobs(n);
+    int64_t total = 0;
+    for (int i = 0; i < n; ++i)
+    {
+        jobs[i] = job_of(*ds[i], total);
+        total += Cs[i];
+    }
+    // one stream-ordered scratch block: the job table, then every quantizer's encodings
+    // back to back so that a single copy brings them all to the host
+    const size_t jobs_bytes = (sizeof(TfeJob) * n + 255) & ~size_t(255);
+    char* scratch           = nullptr;
+    AIMET_HIP_CHECK(hipMallocAsync((void**) &scratch, jobs_bytes + sizeof(aimet_tf_encoding) * total, s));
+    aimet_tf_encoding* dout = reinterpret_cast<aimet_tf_encoding*>(scratch + jobs_bytes);
+    for (int i = 0; i < n; ++i)
+        jobs[i].out = dout + jobs[i].start;
+    TfeJob* djobs = reinterpret_cast<TfeJob*>(scratch);
+    AIMET_HIP_CHECK(hipMemcpyAsync(djobs, jobs.data(), sizeof(TfeJob) * n, hipMemcpyHostToDevice, s));
+    tfe_search_kernel<<<grid_of(total), kBlock, 0, s>>>(jobs[0], djobs, n, total, bw, sym, strict, unsign);
+    AIMET_LAUNCH_CHECK();
+    AIMET_HIP_CHECK(hipMemcpyAsync(host_out, dout, sizeof(aimet_tf_encoding) * total, hipMemcpyDeviceToHost, s));
+    AIMET_HIP_CHECK(hipFreeAsync(scratch, s));
+    // `jobs` (pageable source) and host_out must be complete before returning
+    AIMET_HIP_CHECK(hipStreamSynchronize(s));
 }
 
 }   // namespace aimet_amd

@@ -40,7 +40,11 @@ void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, in
 void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStream_t s);
 void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s);
 // tfe_search.hip
-void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, bool stats_updated,
-                       aimet_tf_encoding* out, hipStream_t s);
+// d.enc[c] <- TF-Enhanced encoding of channel c (statistics updated; see aimet_tq_get_encoding)
+void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
+// the same for n quantizers in one launch; host_out <- their encodings concatenated
+// (sum of Cs). Synchronises s.
+void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
+                            bool unsign, aimet_tf_encoding* host_out, hipStream_t s);
 
 }   // namespace aimet_amd

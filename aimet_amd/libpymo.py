@@ -53,23 +53,24 @@ for _e in (ComputationMode, QuantizationMode, LayerInOut, RoundingMode):
     globals().update(_e.__members__)
 
 
-class TfEncoding:
+class TfEncoding(TfEncodingC):
     """``DlQuantization::TfEncoding`` (Quantization.hpp:113-120); default-constructed to zeros.
 
+    The object IS the C struct the library reads and writes (no conversion at the boundary), so
+    a per-channel getEncoding of 27,560 channels materialises its list in one C-level pass.
     Every field assignment bumps a process-wide version number, so device-side caches built from
     encodings (per-channel QDQ tables) can tell in O(1) that any encoding changed.
     """
-    __slots__ = ("min", "max", "delta", "offset", "bw")
     _version = 0
 
-    def __init__(self):
-        for f in ("min", "max", "delta", "offset"):
-            object.__setattr__(self, f, 0.0)
-        object.__setattr__(self, "bw", 0)
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        TfEncoding._version += 1
 
     def __setattr__(self, name, value):
-        value = int(value) if name == "bw" else float(value)
-        object.__setattr__(self, name, value)
+        if name == "bw":
+            value = int(value)
+        super().__setattr__(name, value)
         TfEncoding._version += 1
 
     def __repr__(self):
@@ -77,7 +78,7 @@ class TfEncoding:
             self.min, self.max, self.delta, self.offset, self.bw)
 
     def __eq__(self, other):
-        return isinstance(other, TfEncoding) and self.to_tuple() == other.to_tuple()
+        return isinstance(other, TfEncodingC) and self.to_tuple() == TfEncoding.to_tuple(other)
 
     __hash__ = None
 
@@ -85,32 +86,24 @@ class TfEncoding:
         return (self.min, self.max, self.delta, self.offset, self.bw)
 
     def to_c(self) -> TfEncodingC:
-        return TfEncodingC(self.min, self.max, self.delta, self.offset, int(self.bw))
+        return self
 
     @staticmethod
     def from_c(c: TfEncodingC) -> "TfEncoding":
-        e = TfEncoding()
-        object.__setattr__(e, "min", c.min)
-        object.__setattr__(e, "max", c.max)
-        object.__setattr__(e, "delta", c.delta)
-        object.__setattr__(e, "offset", c.offset)
-        object.__setattr__(e, "bw", int(c.bw))
         TfEncoding._version += 1
-        return e
+        return TfEncoding.from_buffer_copy(c)
 
-    def __getstate__(self):
-        return self.to_tuple()
-
-    def __setstate__(self, state):
-        for f, v in zip(("min", "max", "delta", "offset", "bw"), state):
-            object.__setattr__(self, f, v)
+    @staticmethod
+    def array(n: int):
+        """A C array of n zero encodings; ``list(arr)`` gives TfEncoding views into it."""
+        TfEncoding._version += 1
+        return (TfEncoding * n)()
 
 
 def encodings_to_c(encodings):
-    arr = (TfEncodingC * len(encodings))()
-    for i, e in enumerate(encodings):
-        arr[i] = e.to_c()
-    return arr
+    """Contiguous C copy of a sequence of TfEncoding (one C-level pass)."""
+    n = len(encodings)
+    return (TfEncodingC * n).from_buffer_copy(b"".join(map(bytes, encodings))) if n else (TfEncodingC * 0)()
 
 
 def getComputedEncodings(bw, min_val, max_val, use_symmetric, use_strict_symmetric, use_unsigned_symmetric):

@@ -210,13 +210,48 @@ class AimetTensorQuantizer:
         C = self._num_channels
         if self._handle is None or not self._is_encoding_valid:
             return [TfEncoding() for _ in range(C)], False
-        out = (TfEncodingC * C)()
+        out = TfEncoding.array(C)
         valid = ctypes.c_int(0)
         with torch.cuda.device(self._device):
             _native.call("aimet_tq_get_encoding", self._handle, int(bw), int(bool(sym)), int(bool(strict)),
                          int(bool(unsign)), out, ctypes.byref(valid),
                          torch.cuda.current_stream(self._device).cuda_stream)
-        return [TfEncoding.from_c(out[i]) for i in range(C)], bool(valid.value)
+        return list(out), bool(valid.value)
+
+    @staticmethod
+    def getEncodings(quantizers, bitwidth, use_symmetric_encodings, use_strict_symmetric,
+                     use_unsigned_symmetric):
+        """getEncoding of many quantizers with ONE stream synchronisation (every device-side
+        encoding search is enqueued first): the per-quantizer loop of
+        QuantizationSimModel.compute_encodings (v1/quantsim.py:425-449), batched.
+        Returns [(encoding or list of encodings, is_valid)] in input order."""
+        quantizers = list(quantizers)
+        live = [q for q in quantizers if q._handle is not None and q._is_encoding_valid]
+        results = {}
+        if live:
+            dev = live[0]._device
+            total = sum(q._num_channels for q in live)
+            out = TfEncoding.array(total)
+            valid = (ctypes.c_int * len(live))()
+            handles = (ctypes.c_void_p * len(live))(*[q._handle for q in live])
+            with torch.cuda.device(dev):
+                _native.call("aimet_tq_get_encodings", handles, len(live), int(bitwidth),
+                             int(bool(use_symmetric_encodings)), int(bool(use_strict_symmetric)),
+                             int(bool(use_unsigned_symmetric)), out, valid, torch.cuda.current_stream(dev).cuda_stream)
+            encs = list(out)
+            off = 0
+            for i, q in enumerate(live):
+                C = q._num_channels
+                results[id(q)] = (encs[off] if C == 1 else encs[off:off + C], bool(valid[i]))
+                off += C
+        res = []
+        for q in quantizers:
+            if id(q) in results:
+                res.append(results[id(q)])
+            else:
+                e = [TfEncoding() for _ in range(q._num_channels)]
+                res.append((e[0] if q._num_channels == 1 else e, False))
+        return res
 
     def getStatsHistogram(self, channel: int = 0):
         """AimetTensorQuantizer.cpp:194-198 -> list of (xLeft, pdf)."""

@@ -102,8 +102,9 @@ def compute_encodings(acts, weights, world):
             q.updateStats(t, True)
     for q, (_, w) in zip(wq, weights):
         q.updateStatsPerChannel(w, 0, True)
-    act_enc = [q.getEncoding(8, False, False, False)[0] for q in aq]
-    w_enc = [q.getEncoding(8, True, False, False)[0] for q in wq]
+    # getEncoding of every quantizer, batched: one device search launch + one sync per flag set
+    act_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(aq, 8, False, False, False)]
+    w_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(wq, 8, True, False, False)]
     torch.cuda.synchronize()
     return act_enc, w_enc, time.perf_counter() - t0, aq, wq
 

@@ -193,6 +193,13 @@ int aimet_tq_mark_stats_updated(aimet_tensor_quantizer* q);
  * Synchronises `stream`. out[num_channels]; *valid mirrors _isEncodingValid. */
 int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int use_symmetric, int use_strict_symmetric,
                           int use_unsigned_symmetric, aimet_tf_encoding* out, int* valid, void* stream);
+/* getEncoding of nq quantizers (one device) with one stream synchronisation: every device-side
+ * search is enqueued first (QuantizationSimModel.compute_encodings' per-quantizer loop,
+ * v1/quantsim.py:425-449, batched). out = the quantizers' encodings concatenated
+ * (sum of num_channels); valid[nq]. */
+int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int use_symmetric,
+                           int use_strict_symmetric, int use_unsigned_symmetric, aimet_tf_encoding* out, int* valid,
+                           void* stream);
 
 /* AimetTensorQuantizer.cpp:194-198 getStatsHistogram (histogram schemes): xleft/pdf[512] of
  * `channel`; *n = 0 when no histogram exists yet. Synchronises `stream`. */

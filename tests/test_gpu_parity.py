@@ -241,6 +241,39 @@ def test_tfe_device_search_many_channels():
                 assert encs[c].to_tuple() == orcs[c].compute(bw, *fl).as_tuple(), (c, bw, fl)
 
 
+def test_get_encodings_batched_equals_individual():
+    """AimetTensorQuantizer.getEncodings (one device search launch + one sync for all quantizers)
+    == getEncoding of each, for every scheme, per-tensor and per-channel, with and without stats."""
+    rng = np.random.default_rng(3)
+    qs = []
+    for scheme in (QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
+                   QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE):
+        for C in (1, 7):
+            q = AimetTensorQuantizer(scheme, num_channels=C)
+            if scheme == QuantizationMode.QUANTIZATION_PERCENTILE:
+                q.setPercentileValue(99.0)
+            x = (rng.standard_normal((C, 300)) * rng.uniform(0.1, 4)).astype(np.float32)
+            if C == 1:
+                q.updateStats(gpu(x), True)
+            else:
+                q.updateStatsPerChannel(gpu(x), 0, True)
+            qs.append(q)
+    qs.append(AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED))      # no stats
+    qs.append(AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=3))
+    z = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=4)
+    z.updateStatsPerChannel(torch.zeros(4, 50, device=DEV), 0, True)                 # all-zero data
+    qs.append(z)
+    for fl in FLAGS:
+        batched = AimetTensorQuantizer.getEncodings(qs, 8, *fl)
+        for q, (e, v) in zip(qs, batched):
+            e1, v1 = q.getEncoding(8, *fl)
+            assert v == v1
+            if isinstance(e1, list):
+                assert [a.to_tuple() for a in e] == [a.to_tuple() for a in e1]
+            else:
+                assert e.to_tuple() == e1.to_tuple()
+
+
 def test_minmax_and_histogram_full_size():
     """Stats of a 205M-element activation: TF encoding == oracle over the whole tensor, TF-E PDF
     == oracle PDF (bit-exact) and sums to the in-range fraction."""

@@ -1,0 +1,323 @@
+// hist_variants.hip -- microbenchmark of the 512-bin histogram pass (UpdatePdf's GetHistogram) on
+// gfx950 (tuning tool for stats.hip). Build:
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off \
+//         -fhip-fp32-correctly-rounded-divide-sqrt -I include -I aimet_amd/csrc tools/hist_variants.hip -o tools/hist_variants
+// Two inputs of n floats (default 205,520,896 = 256x64x112x112, ResNet-50's largest activation):
+// relu(N(0,1)*1.5+0.2) (about half exact zeros) and N(0,1)*2 (no zeros). Every variant's counts
+// are checked against the first variant bit for bit; median GB/s (4 B/elem) over interleaved rounds.
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include <hip/hip_runtime.h>
+
+#define CK(x)                                                                                                  \
+    do                                                                                                         \
+    {                                                                                                          \
+        hipError_t e = (x);                                                                                    \
+        if (e != hipSuccess)                                                                                   \
+        {                                                                                                      \
+            printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__);                                   \
+            exit(1);                                                                                           \
+        }                                                                                                      \
+    } while (0)
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int kBins = 512;
+
+struct Binner
+{
+    float bucket, offset;
+    __device__ __forceinline__ int bin(float x) const
+    {
+        float r = __builtin_roundf(x / bucket - offset);
+        return (r >= 0.0f && r < (float) kBins) ? (int) r : -1;
+    }
+};
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// COPIES: LDS histograms per block (1 = shared by the block, BLOCK/64 = one per wave)
+template <int BLOCK, int UNROLL, int COPIES, bool NT, bool ZSKIP>
+__global__ __launch_bounds__(BLOCK) void hist_var(const float* __restrict__ x, int64_t n, Binner bn,
+                                                  unsigned long long* __restrict__ counts)
+{
+    __shared__ uint32_t lds[COPIES][kBins];
+    const int copy = (threadIdx.x >> 6) % COPIES;
+    for (int i = threadIdx.x; i < COPIES * kBins; i += BLOCK)
+        (&lds[0][0])[i] = 0;
+    __syncthreads();
+    const int zbin = bn.bin(0.0f);
+    uint32_t zc    = 0;
+    auto add = [&](float v) {
+        if (ZSKIP && v == 0.0f)
+        {
+            ++zc;
+            return;
+        }
+        int b = bn.bin(v);
+        if (b >= 0)
+            atomicAdd(&lds[copy][b], 1u);
+    };
+    const f4* x4         = reinterpret_cast<const f4*>(x);
+    const int64_t nv     = n / 4;
+    const int64_t stride = (int64_t) gridDim.x * BLOCK * UNROLL;
+    for (int64_t base = (int64_t) blockIdx.x * BLOCK * UNROLL + threadIdx.x; base < nv; base += stride)
+    {
+        f4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            int64_t i = base + (int64_t) u * BLOCK;
+            if (i < nv)
+                v[u] = NT ? __builtin_nontemporal_load(x4 + i) : x4[i];
+            else
+                v[u] = f4 {NAN, NAN, NAN, NAN};
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            add(v[u].x);
+            add(v[u].y);
+            add(v[u].z);
+            add(v[u].w);
+        }
+    }
+    for (int64_t i = nv * 4 + (int64_t) blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t) gridDim.x * BLOCK)
+        add(x[i]);
+    if (ZSKIP)
+    {
+        zc = wave_sum(zc);
+        if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
+            atomicAdd(&lds[copy][zbin], zc);
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBins; b += BLOCK)
+    {
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < COPIES; ++i)
+            s += lds[i][b];
+        if (s)
+            atomicAdd(&counts[b], (unsigned long long) s);
+    }
+}
+
+// min/max partials (stats.hip minmax_tensor_kernel shape)
+template <int BLOCK, int UNROLL, bool NT>
+__global__ __launch_bounds__(BLOCK) void minmax_var(const float* __restrict__ x, int64_t n, float2* __restrict__ part)
+{
+    const f4* x4         = reinterpret_cast<const f4*>(x);
+    const int64_t nv     = n / 4;
+    const int64_t stride = (int64_t) gridDim.x * BLOCK * UNROLL;
+    float mn = INFINITY, mx = -INFINITY;
+    for (int64_t base = (int64_t) blockIdx.x * BLOCK * UNROLL + threadIdx.x; base < nv; base += stride)
+    {
+        f4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            int64_t i = base + (int64_t) u * BLOCK;
+            v[u]      = i < nv ? (NT ? __builtin_nontemporal_load(x4 + i) : x4[i]) : f4 {NAN, NAN, NAN, NAN};
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            mn = fminf(fminf(mn, v[u].x), fminf(v[u].y, fminf(v[u].z, v[u].w)));
+            mx = fmaxf(fmaxf(mx, v[u].x), fmaxf(v[u].y, fmaxf(v[u].z, v[u].w)));
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+    {
+        mn = fminf(mn, __shfl_xor(mn, o, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    }
+    __shared__ float smn[BLOCK / 64], smx[BLOCK / 64];
+    if ((threadIdx.x & 63) == 0)
+    {
+        smn[threadIdx.x >> 6] = mn;
+        smx[threadIdx.x >> 6] = mx;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0)
+    {
+        for (int i = 1; i < BLOCK / 64; ++i)
+        {
+            mn = fminf(mn, smn[i]);
+            mx = fmaxf(mx, smx[i]);
+        }
+        part[blockIdx.x] = make_float2(-mn, mx);
+    }
+}
+
+template <int BLOCK, int UNROLL, bool NT, int GRID>
+void launch_minmax(const float* x, int64_t n, Binner, unsigned long long* c, hipStream_t s)
+{
+    int64_t need = (n / 4 + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
+    int g        = (int) std::max<int64_t>(1, std::min<int64_t>(need, GRID));
+    minmax_var<BLOCK, UNROLL, NT><<<g, BLOCK, 0, s>>>(x, n, (float2*) c);
+}
+
+// read-only ceiling: sum of the input (same load pattern)
+template <int BLOCK, int UNROLL>
+__global__ __launch_bounds__(BLOCK) void read_var(const float* __restrict__ x, int64_t n, float* __restrict__ out)
+{
+    const f4* x4         = reinterpret_cast<const f4*>(x);
+    const int64_t nv     = n / 4;
+    const int64_t stride = (int64_t) gridDim.x * BLOCK * UNROLL;
+    float s              = 0;
+    for (int64_t base = (int64_t) blockIdx.x * BLOCK * UNROLL + threadIdx.x; base < nv; base += stride)
+    {
+        f4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            int64_t i = base + (int64_t) u * BLOCK;
+            v[u]      = i < nv ? __builtin_nontemporal_load(x4 + i) : f4 {0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            s += v[u].x + v[u].y + v[u].z + v[u].w;
+    }
+    if (s == 1234.5f)
+        out[0] = s;
+}
+
+__global__ void gen_kernel(float* x, int64_t n, int relu, uint32_t seed)
+{
+    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t) gridDim.x * blockDim.x)
+    {
+        uint64_t h = (uint64_t) i * 0x9E3779B97F4A7C15ull + seed;
+        h ^= h >> 31;
+        h *= 0xBF58476D1CE4E5B9ull;
+        h ^= h >> 29;
+        float u1 = ((h & 0xFFFFFF) + 1) / 16777217.0f, u2 = ((h >> 24) & 0xFFFFFF) / 16777216.0f;
+        float z  = sqrtf(-2.0f * logf(u1)) * cosf(6.2831853f * u2);
+        x[i]     = relu ? fmaxf(z * 1.5f + 0.2f, 0.0f) : z * 2.0f;
+    }
+}
+
+struct Variant
+{
+    const char* name;
+    void (*launch)(const float*, int64_t, Binner, unsigned long long*, hipStream_t);
+    bool check;
+    std::vector<float> ms;
+};
+
+template <int BLOCK, int UNROLL, int COPIES, bool NT, bool ZSKIP, int GRID>
+void launch_hist(const float* x, int64_t n, Binner bn, unsigned long long* c, hipStream_t s)
+{
+    int64_t need = (n / 4 + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
+    int g        = (int) std::max<int64_t>(1, std::min<int64_t>(need, GRID));
+    hist_var<BLOCK, UNROLL, COPIES, NT, ZSKIP><<<g, BLOCK, 0, s>>>(x, n, bn, c);
+}
+
+template <int BLOCK, int UNROLL, int GRID>
+void launch_read(const float* x, int64_t n, Binner, unsigned long long* c, hipStream_t s)
+{
+    read_var<BLOCK, UNROLL><<<GRID, BLOCK, 0, s>>>(x, n, (float*) c);
+}
+
+// InitializePdf's range (math_functions.cpp:207-241) for min/max -> UpdatePdf's bucket/offset
+Binner binner_for(float mn, float mx)
+{
+    float center = (mx + mn) / 2.0f;
+    float lo = center - 3.0f * (center - mn), hi = center + 3.0f * (mx - center);
+    double bs    = ((double) hi - (double) lo) / kBins;
+    float bucket = (float) (((double) lo + bs) - (double) lo);
+    return Binner {bucket, (float) (double) lo / bucket};
+}
+
+int main(int argc, char** argv)
+{
+    int64_t n  = argc > 1 ? atoll(argv[1]) : 205520896;
+    int rounds = argc > 2 ? atoi(argv[2]) : 9;
+    float* x;
+    unsigned long long *cnt, *ref;
+    CK(hipMalloc(&x, n * 4));
+    CK(hipMalloc(&cnt, 4096 * 8 * 2));
+    CK(hipMalloc(&ref, kBins * 8));
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    std::vector<Variant> vs = {
+        {"read-only ceiling b256 u4 g4096", launch_read<256, 4, 4096>, false, {}},
+        {"minmax b256 u4 g1024 (current)", launch_minmax<256, 4, false, 1024>, false, {}},
+        {"minmax b256 u4 g1024 nt", launch_minmax<256, 4, true, 1024>, false, {}},
+        {"minmax b256 u4 g2048 nt", launch_minmax<256, 4, true, 2048>, false, {}},
+        {"minmax b256 u2 g4096 nt", launch_minmax<256, 2, true, 4096>, false, {}},
+        {"minmax b512 u4 g1024 nt", launch_minmax<512, 4, true, 1024>, false, {}},
+        {"hist b256 u2 c4 g512 (current)", launch_hist<256, 2, 4, false, true, 512>, true, {}},
+        {"hist b256 u2 c4 g1024", launch_hist<256, 2, 4, false, true, 1024>, true, {}},
+        {"hist b256 u2 c4 g2048", launch_hist<256, 2, 4, false, true, 2048>, true, {}},
+        {"hist b256 u4 c4 g2048", launch_hist<256, 4, 4, false, true, 2048>, true, {}},
+        {"hist b256 u4 c4 g2048 nt", launch_hist<256, 4, 4, true, true, 2048>, true, {}},
+        {"hist b256 u4 c4 g4096 nt", launch_hist<256, 4, 4, true, true, 4096>, true, {}},
+        {"hist b256 u2 c4 g4096 nt", launch_hist<256, 2, 4, true, true, 4096>, true, {}},
+        {"hist b256 u4 c1 g2048 nt", launch_hist<256, 4, 1, true, true, 2048>, true, {}},
+        {"hist b256 u4 c2 g2048 nt", launch_hist<256, 4, 2, true, true, 2048>, true, {}},
+        {"hist b512 u4 c8 g1024 nt", launch_hist<512, 4, 8, true, true, 1024>, true, {}},
+        {"hist b512 u2 c8 g2048 nt", launch_hist<512, 2, 8, true, true, 2048>, true, {}},
+        {"hist b1024 u2 c16 g1024 nt", launch_hist<1024, 2, 16, true, true, 1024>, true, {}},
+        {"hist b256 u4 c4 g2048 nt nozskip", launch_hist<256, 4, 4, true, false, 2048>, true, {}},
+        {"hist b256 u8 c4 g2048 nt", launch_hist<256, 8, 4, true, true, 2048>, true, {}},
+        {"hist b256 u4 c4 g8192 nt", launch_hist<256, 4, 4, true, true, 8192>, true, {}},
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const char* dname[2] = {"relu(N(0,1)*1.5+0.2)", "N(0,1)*2"};
+    for (int dist = 0; dist < 2; ++dist)
+    {
+        gen_kernel<<<4096, 256, 0, s>>>(x, n, dist == 0, 1234);
+        CK(hipStreamSynchronize(s));
+        Binner bn = dist == 0 ? binner_for(0.0f, 9.0f) : binner_for(-11.0f, 11.0f);
+        CK(hipMemsetAsync(ref, 0, kBins * 8, s));
+        launch_hist<256, 2, 4, false, true, 512>(x, n, bn, ref, s);
+        std::vector<unsigned long long> href(kBins), hc(kBins);
+        CK(hipMemcpy(href.data(), ref, kBins * 8, hipMemcpyDeviceToHost));
+        unsigned long long tot = 0;
+        for (auto v: href)
+            tot += v;
+        for (auto& v: vs)
+        {
+            v.ms.clear();
+            CK(hipMemsetAsync(cnt, 0, kBins * 8, s));
+            v.launch(x, n, bn, cnt, s);
+            CK(hipMemcpy(hc.data(), cnt, kBins * 8, hipMemcpyDeviceToHost));
+            if (v.check && memcmp(hc.data(), href.data(), kBins * 8) != 0)
+                printf("MISMATCH in %s\n", v.name);
+        }
+        for (int r = 0; r < rounds; ++r)
+            for (auto& v: vs)
+            {
+                CK(hipMemsetAsync(cnt, 0, kBins * 8, s));
+                CK(hipEventRecord(e0, s));
+                v.launch(x, n, bn, cnt, s);
+                CK(hipEventRecord(e1, s));
+                CK(hipEventSynchronize(e1));
+                float ms;
+                CK(hipEventElapsedTime(&ms, e0, e1));
+                v.ms.push_back(ms);
+            }
+        printf("== %s, n=%lld, in-range %llu\n", dname[dist], (long long) n, tot);
+        for (auto& v: vs)
+        {
+            std::sort(v.ms.begin(), v.ms.end());
+            float med = v.ms[v.ms.size() / 2];
+            printf("%-40s %8.3f ms  %7.1f GB/s\n", v.name, med, n * 4.0 / (med * 1e-3) / 1e9);
+        }
+    }
+    return 0;
+}
