@@ -253,6 +253,22 @@ aimet_tf_encoding tfe_encoding(const HistView& h, int32_t bw, bool sym, bool str
         tfe::fseq_sym(fseq);
     else
         tfe::fseq_asym(fseq);
+    // the per-channel bin tables every candidate shares (tfe_core.hpp, as the device builds them)
+    double cd[tfe::kBins];
+    float cf[tfe::kBins];
+    short nz[tfe::kBins];
+    const float start = tfe::bins_start(th);
+    const double step = tfe::bins_step(th);
+    const bool skip   = tfe::bins_skip_empty(th);
+    int nnz           = 0;
+    for (int i = 0; i < tfe::kBins; ++i)
+    {
+        cd[i] = tfe::bin_centre(start, step, i);
+        cf[i] = (float) cd[i];
+        if (h.pdf[i] > 0 || !skip)
+            nz[nnz++] = (short) i;
+    }
+    const tfe::Bins B {start, step, h.pdf, cd, cf, nz, nnz};
     float bestDelta = -1;
     int bestOffset  = -1;
     double best     = std::numeric_limits<double>::max();
@@ -262,7 +278,7 @@ aimet_tf_encoding tfe_encoding(const HistView& h, int32_t bw, bool sym, bool str
         int o;
         if (!tfe::candidate(st, fseq, t, d, o))
             continue;
-        double c = tfe::cost(th, bw, d, o);
+        double c = tfe::cost(B, bw, d, o);
         if (c < best)
         {
             best       = c;

@@ -96,20 +96,20 @@ __global__ __launch_bounds__(kBlock) void minmax_tensor_kernel(const float* __re
     float mn = INFINITY, mx = -INFINITY;
     if (vec)
     {
-        const float4* x4     = reinterpret_cast<const float4*>(x);
+        // streaming 16-B loads, 4 in flight per lane (tools/hist_variants.hip: 6.8 TB/s)
+        const f4* x4         = reinterpret_cast<const f4*>(x);
         int64_t nvec         = n / 4;
         const int64_t stride = (int64_t) gridDim.x * kBlock * 4;
         for (int64_t b = (int64_t) blockIdx.x * kBlock * 4 + threadIdx.x; b < nvec; b += stride)
         {
-            float4 v[4];
+            f4 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)   // NaN padding is ignored by fminf/fmaxf
+                v[u] = b + u * kBlock < nvec ? __builtin_nontemporal_load(x4 + b + u * kBlock)
+                                             : f4 {NAN, NAN, NAN, NAN};
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (b + u * kBlock < nvec)
-                    v[u] = x4[b + u * kBlock];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (b + u * kBlock < nvec)
-                    accum4(v[u], mn, mx);
+                accum4(make_float4(v[u].x, v[u].y, v[u].z, v[u].w), mn, mx);
         }
         for (int64_t i = nvec * 4 + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n;
              i += (int64_t) gridDim.x * kBlock)

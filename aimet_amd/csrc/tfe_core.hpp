@@ -166,38 +166,78 @@ AIMET_HD inline bool candidate(const Setup& s, const float* fseq, int t, float& 
     return clamp_candidate(s.obsLo, s.obsHi, s.steps, delta, offset);
 }
 
-// _quantAndSatCost (:293-355)
-AIMET_HD inline double cost(const Hist& h, int bw, float delta, int offset)
+// Per-channel precomputation shared by every candidate of _quantAndSatCost (:293-355):
+//   cd[i] = start + i*step + step/2 (double, the bin centre as the reference evaluates it)
+//   cf[i] = (float) cd[i]            (loMid / hiMid / the quantised value v)
+//   nz[0..nnz) = the bins the cost loops must visit, ascending.
+// A bin whose pdf is 0 adds exactly +0.0 to its sum as long as its squared distance is finite,
+// so such bins are skipped when the histogram range is bounded (|x| <= 1e30 keeps every
+// distance finite); otherwise every bin is visited, as in the reference.
+struct Bins
 {
-    const float lo     = delta * offset;
-    const float steps  = (float) (ldexp(1.0, bw) - 1);
-    const float hi     = delta * (offset + steps);
-    const float start  = (float) h.xl(0);
-    const double step  = h.xl(1) - h.xl(0);
-    int iLo            = (int) floor((lo - start) / step);
-    iLo                = smin(smax(0, iLo), kBins - 1);
-    int iHi            = (int) floor((hi - start) / step);
-    iHi                = smin(smax(0, iHi), kBins - 1);
-    const float loMid  = (float) (start + (iLo * step) + step / 2);
-    const float hiMid  = (float) (start + (iHi * step) + step / 2);
+    float start;
+    double step;
+    const double* pdf;
+    const double* cd;
+    const float* cf;
+    const short* nz;
+    int nnz;
+};
+
+AIMET_HD inline float bins_start(const Hist& h)
+{
+    return (float) h.xl(0);
+}
+AIMET_HD inline double bins_step(const Hist& h)
+{
+    return h.xl(1) - h.xl(0);
+}
+AIMET_HD inline double bin_centre(float start, double step, int i)
+{
+    return start + i * step + step / 2;
+}
+AIMET_HD inline bool bins_skip_empty(const Hist& h)
+{
+    double a = h.xl(0), b = h.xl(kBins - 1) + (h.xl(1) - h.xl(0));
+    return a >= -1e30 && a <= 1e30 && b >= -1e30 && b <= 1e30;
+}
+
+// _quantAndSatCost (:293-355) over the prepared bins. The three sums keep the reference's
+// ascending order; a bin can belong to more than one of them exactly as in the reference loops.
+AIMET_HD inline double cost(const Bins& B, int bw, float delta, int offset)
+{
+    const float lo    = delta * offset;
+    const float steps = (float) (ldexp(1.0, bw) - 1);
+    const float hi    = delta * (offset + steps);
+    int iLo           = (int) floor((lo - B.start) / B.step);
+    iLo               = smin(smax(0, iLo), kBins - 1);
+    int iHi           = (int) floor((hi - B.start) / B.step);
+    iHi               = smin(smax(0, iHi), kBins - 1);
+    const float loMid = B.cf[iLo];
+    const float hiMid = B.cf[iHi];
     double satLo = 0, satHi = 0, quant = 0;
-    for (int i = 0; i < iLo; ++i)
+    for (int k = 0; k < B.nnz; ++k)
     {
-        double d = (start + i * step + step / 2) - loMid;
-        satLo += h.pdf[i] * (d * d);
-    }
-    for (int i = iHi; i < kBins; ++i)
-    {
-        double d = (start + i * step + step / 2) - hiMid;
-        satHi += h.pdf[i] * (d * d);
-    }
-    for (int i = iLo; i < iHi; ++i)
-    {
-        float v   = (float) (start + i * step + step / 2);
-        int q     = (int) roundf(v / delta - offset);
-        float deq = delta * (q + offset);
-        double d  = (double) (v - deq);
-        quant += h.pdf[i] * (d * d);
+        const int i    = B.nz[k];
+        const double p = B.pdf[i];
+        if (i < iLo)
+        {
+            double d = B.cd[i] - loMid;
+            satLo += p * (d * d);
+        }
+        if (i >= iHi)
+        {
+            double d = B.cd[i] - hiMid;
+            satHi += p * (d * d);
+        }
+        if (i >= iLo && i < iHi)
+        {
+            float v   = B.cf[i];
+            int q     = (int) roundf(v / delta - offset);
+            float deq = delta * (q + offset);
+            double d  = (double) (v - deq);
+            quant += p * (d * d);
+        }
     }
     double c = kGamma * (satLo + satHi) + quant;
     return smin(c, DBL_MAX);

@@ -10,6 +10,7 @@
 #include "tfe_core.hpp"
 #include "tq_state.hpp"
 
+#include <mutex>
 #include <vector>
 
 namespace aimet_amd
@@ -47,13 +48,18 @@ struct TfeJob
     int64_t start;   // first global channel of this job
 };
 
-__global__ __launch_bounds__(kBlock) void tfe_search_kernel(TfeJob one, const TfeJob* __restrict__ jobs, int njobs,
-                                                            int64_t total, int bw, int sym, int strict, int unsign)
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void tfe_search_kernel(TfeJob one, const TfeJob* __restrict__ jobs, int njobs,
+                                                           int64_t total, int bw, int sym, int strict, int unsign)
 {
+    constexpr int kW = BLOCK / 64;
     __shared__ double pdf[tfe::kBins];
+    __shared__ double cd[tfe::kBins];
+    __shared__ float cf[tfe::kBins];
+    __shared__ short nz[tfe::kBins];
     __shared__ float fseq[tfe::kSymF + 8];
-    __shared__ int first, last;
-    __shared__ Best wbest[kBlock / 64];
+    __shared__ int first, last, nnz;
+    __shared__ Best wbest[kW];
     if (threadIdx.x == 0)
     {
         if (sym)
@@ -61,6 +67,7 @@ __global__ __launch_bounds__(kBlock) void tfe_search_kernel(TfeJob one, const Tf
         else
             tfe::fseq_asym(fseq);
     }
+    const int lane = threadIdx.x & 63;
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
     {
         TfeJob j = one;
@@ -94,42 +101,68 @@ __global__ __launch_bounds__(kBlock) void tfe_search_kernel(TfeJob one, const Tf
             }
             continue;
         }
-        for (int i = threadIdx.x; i < tfe::kBins; i += kBlock)
-            pdf[i] = j.pdf[c * tfe::kBins + i];
-        if (threadIdx.x == 0)
+        tfe::Hist h {j.hist_min[c], j.bucket_size[c], nullptr};
+        const float start = tfe::bins_start(h);
+        const double step = tfe::bins_step(h);
+        for (int i = threadIdx.x; i < tfe::kBins; i += BLOCK)
         {
-            first = tfe::kBins;
-            last  = -1;
+            pdf[i]   = j.pdf[c * tfe::kBins + i];
+            double m = tfe::bin_centre(start, step, i);
+            cd[i]    = m;
+            cf[i]    = (float) m;
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < tfe::kBins; i += kBlock)
-            if (pdf[i] > 0)
+        if (threadIdx.x < 64)
+        {
+            // ascending compaction of the bins the cost must visit + first/last non-empty bins
+            const bool skip = tfe::bins_skip_empty(h);
+            int base = 0, fst = -1, lst = -1;
+            for (int i0 = 0; i0 < tfe::kBins; i0 += 64)
             {
-                atomicMin(&first, i);
-                if (i > 0)
-                    atomicMax(&last, i);
+                const int i          = i0 + lane;
+                const bool occupied  = pdf[i] > 0;
+                const bool visit     = occupied || !skip;
+                unsigned long long m = __ballot(visit);
+                unsigned long long o = __ballot(occupied);
+                if (visit)
+                    nz[base + __popcll(m & ((1ull << lane) - 1))] = (short) i;
+                base += __popcll(m);
+                if (o)
+                {
+                    if (fst < 0)
+                        fst = i0 + __ffsll((long long) o) - 1;
+                    lst = i0 + 63 - __clzll(o);
+                }
             }
+            if (lane == 0)
+            {
+                nnz   = base;
+                first = fst;
+                last  = lst > 0 ? lst : -1;   // the reference's backward scan stops before bin 0
+            }
+        }
         __syncthreads();
-        tfe::Hist h {j.hist_min[c], j.bucket_size[c], pdf};
+        h.pdf = pdf;
         float lo, hi;
-        tfe::observed_range(h, first < tfe::kBins ? first : -1, last, lo, hi);
+        tfe::observed_range(h, first, last, lo, hi);
         tfe::Setup st = tfe::setup(lo, hi, bw, sym != 0, strict != 0, unsign != 0);
+        const tfe::Bins B {start, step, pdf, cd, cf, nz, nnz};
 
         Best b {0.0, -1, -1.0f, -1};
-        for (int t = threadIdx.x; t < st.ncand; t += kBlock)
+        for (int t = threadIdx.x; t < st.ncand; t += BLOCK)
         {
             float dl;
             int o;
             if (!tfe::candidate(st, fseq, t, dl, o))
                 continue;
-            double cst = tfe::cost(h, bw, dl, o);
+            double cst = tfe::cost(B, bw, dl, o);
             if (!(cst < DBL_MAX))
                 continue;
             Best me {cst, t, dl, o};
             if (better(me, b))
                 b = me;
         }
-        // wave argmin
+        // wave argmin, then across waves
         for (int k = 32; k > 0; k >>= 1)
         {
             Best o;
@@ -140,12 +173,12 @@ __global__ __launch_bounds__(kBlock) void tfe_search_kernel(TfeJob one, const Tf
             if (better(o, b))
                 b = o;
         }
-        if ((threadIdx.x & 63) == 0)
+        if (lane == 0)
             wbest[threadIdx.x >> 6] = b;
         __syncthreads();
         if (threadIdx.x == 0)
         {
-            for (int w = 1; w < kBlock / 64; ++w)
+            for (int w = 1; w < kW; ++w)
                 if (better(wbest[w], b))
                     b = wbest[w];
             float bd = b.idx >= 0 ? b.delta : -1.0f;
@@ -157,22 +190,43 @@ __global__ __launch_bounds__(kBlock) void tfe_search_kernel(TfeJob one, const Tf
     }
 }
 
+// one candidate per lane: 101 symmetric candidates -> 2 waves, 358 asymmetric -> 6 waves
+void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t total, int bw, bool sym, bool strict,
+                   bool unsign, hipStream_t s)
+{
+    const int grid = (int) (total < 65536 ? total : 65536);
+    if (sym)
+        tfe_search_kernel<128><<<grid, 128, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign);
+    else
+        tfe_search_kernel<384><<<grid, 384, 0, s>>>(one, jobs, njobs, total, bw, 0, strict, unsign);
+    AIMET_LAUNCH_CHECK();
+}
+
 TfeJob job_of(const TqDevice& d, int64_t start)
 {
     return TfeJob {d.pdf_init, d.hist_min, d.bucket_size, d.pdf, d.enc, start};
 }
 
-int grid_of(int64_t total)
+// Grow-only device scratch per device for batched searches (job table + results); held under
+// the lock until the call has synchronised, so concurrent callers never share it.
+struct Scratch
 {
-    return (int) (total < 65536 ? total : 65536);
+    std::mutex m;
+    char* p[64]   = {};
+    size_t cap[64] = {};
+};
+Scratch& scratch_state()
+{
+    static Scratch s;
+    return s;
 }
+
 
 }   // namespace
 
 void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s)
 {
-    tfe_search_kernel<<<grid_of(C), kBlock, 0, s>>>(job_of(d, 0), nullptr, 0, C, bw, sym, strict, unsign);
-    AIMET_LAUNCH_CHECK();
+    launch_kernel(job_of(d, 0), nullptr, 0, C, bw, sym, strict, unsign, s);
 }
 
 void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
@@ -190,17 +244,30 @@ void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n,
     // one stream-ordered scratch block: the job table, then every quantizer's encodings
     // back to back so that a single copy brings them all to the host
     const size_t jobs_bytes = (sizeof(TfeJob) * n + 255) & ~size_t(255);
-    char* scratch           = nullptr;
-    AIMET_HIP_CHECK(hipMallocAsync((void**) &scratch, jobs_bytes + sizeof(aimet_tf_encoding) * total, s));
+    const size_t need       = jobs_bytes + sizeof(aimet_tf_encoding) * total;
+    int dev                 = 0;
+    AIMET_HIP_CHECK(hipGetDevice(&dev));
+    AIMET_REQUIRE(dev >= 0 && dev < 64, "device id out of range");
+    Scratch& st = scratch_state();
+    std::lock_guard<std::mutex> lock(st.m);
+    if (st.cap[dev] < need)
+    {
+        AIMET_HIP_CHECK(hipStreamSynchronize(s));
+        if (st.p[dev])
+            AIMET_HIP_CHECK(hipFree(st.p[dev]));
+        st.p[dev]   = nullptr;
+        st.cap[dev] = 0;
+        AIMET_HIP_CHECK(hipMalloc((void**) &st.p[dev], need));
+        st.cap[dev] = need;
+    }
+    char* scratch = st.p[dev];
     aimet_tf_encoding* dout = reinterpret_cast<aimet_tf_encoding*>(scratch + jobs_bytes);
     for (int i = 0; i < n; ++i)
         jobs[i].out = dout + jobs[i].start;
     TfeJob* djobs = reinterpret_cast<TfeJob*>(scratch);
     AIMET_HIP_CHECK(hipMemcpyAsync(djobs, jobs.data(), sizeof(TfeJob) * n, hipMemcpyHostToDevice, s));
-    tfe_search_kernel<<<grid_of(total), kBlock, 0, s>>>(jobs[0], djobs, n, total, bw, sym, strict, unsign);
-    AIMET_LAUNCH_CHECK();
+    launch_kernel(jobs[0], djobs, n, total, bw, sym, strict, unsign, s);
     AIMET_HIP_CHECK(hipMemcpyAsync(host_out, dout, sizeof(aimet_tf_encoding) * total, hipMemcpyDeviceToHost, s));
-    AIMET_HIP_CHECK(hipFreeAsync(scratch, s));
     // `jobs` (pageable source) and host_out must be complete before returning
     AIMET_HIP_CHECK(hipStreamSynchronize(s));
 }

@@ -141,3 +141,29 @@ def test_libpymo_surface():
         libpymo.GetSVDInstance()
     enc = libpymo.getComputedEncodings(8, -1.0, 2.0, False, False, False)
     assert enc.to_tuple() == O.get_computed_encodings(8, -1.0, 2.0).as_tuple()
+
+
+def test_host_tfe_search_vs_oracle_sparse_and_extreme():
+    """The TF-Enhanced search over prepared bins (tfe_core.hpp, shared with the device kernel:
+    empty bins skipped when the range is bounded) == the oracle's full loops, on sparse PDFs,
+    ranges near FLT_MAX (no skipping), constant and one-sided data, every flag set and width."""
+    rng = np.random.default_rng(17)
+    cases = []
+    for k in (3, 40, 700):
+        cases.append(rng.standard_normal(k) * rng.uniform(0.01, 5) + rng.uniform(-2, 2))
+    cases.append(np.abs(rng.standard_normal(100)) * 3)
+    cases.append(np.full(50, 2.5))
+    cases.append(rng.standard_normal(200) * 3e36)
+    cases.append(rng.standard_normal(200) * 2e29)
+    cases.append(np.concatenate([rng.standard_normal(100), [1e5]]))
+    for x in cases:
+        a = O.Analyzer(O.QUANTIZATION_TF_ENHANCED)
+        a.update(x.astype(np.float32))
+        st = a.stats()
+        pdf = np.ascontiguousarray(st["pdf"], dtype=np.float64)
+        for bw in (4, 8, 16):
+            for fl in [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]:
+                got = _enc("aimet_encoding_from_histogram", O.QUANTIZATION_TF_ENHANCED, st["initialized"],
+                           st["stats_updated"], st["hist_min"], st["bucket_size"],
+                           pdf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), 100.0, bw, *fl)
+                assert got == a.compute(bw, *fl).as_tuple(), (x[:3], bw, fl)

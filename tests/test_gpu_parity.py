@@ -225,6 +225,9 @@ def test_tfe_device_search_many_channels():
     x[5] = 0.0
     x[7] = np.abs(x[7])
     x[9, :] = 2.5                                   # constant channel
+    x[11] = rng.standard_normal(K) * 3e36           # range near FLT_MAX: every bin visited
+    x[13, :3] = 7.0                                 # nearly empty PDF
+    x[13, 3:] = 0.0
     x = x.astype(np.float32)
     q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=C)
     q.updateStatsPerChannel(gpu(x), 0, True)
