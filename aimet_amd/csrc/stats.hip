@@ -29,6 +29,7 @@ namespace
 constexpr int kWaves      = kBlock / 64;
 constexpr int kHistUnroll = 4;
 constexpr int kHistGrid   = 2048;   // 8 workgroups per CU: enough 16-B loads in flight for HBM
+constexpr int64_t kHistLargeN = int64_t(1) << 27;
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float wave_min(float v)
@@ -251,15 +252,17 @@ struct Binner
 };
 
 // per-tensor: many workgroups over one tensor, atomics into counts[0][:]
-__global__ __launch_bounds__(kBlock) void histogram_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
-                                                                  TqDevice d)
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void histogram_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
+                                                                 TqDevice d)
 {
+    constexpr int kWaves = BLOCK / 64;
     if (!d.pdf_init[0])
         return;
     __shared__ uint32_t lds[kWaves][kPdfSize];
     Binner bn {d.bin_bucket[0], d.bin_offset[0]};
     const int w = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < kWaves * kPdfSize; i += kBlock)
+    for (int i = threadIdx.x; i < kWaves * kPdfSize; i += BLOCK)
         (&lds[0][0])[i] = 0;
     __syncthreads();
     const int zbin = bn.bin(0.0f);
@@ -280,14 +283,14 @@ __global__ __launch_bounds__(kBlock) void histogram_tensor_kernel(const float* _
         // 4 x 16-B streaming loads in flight per lane (tools/hist_variants.hip: 5.6-5.8 TB/s)
         const f4* x4         = reinterpret_cast<const f4*>(x);
         const int64_t nv     = n / 4;
-        const int64_t stride = (int64_t) gridDim.x * kBlock * kHistUnroll;
-        for (int64_t base = (int64_t) blockIdx.x * kBlock * kHistUnroll + threadIdx.x; base < nv; base += stride)
+        const int64_t stride = (int64_t) gridDim.x * BLOCK * kHistUnroll;
+        for (int64_t base = (int64_t) blockIdx.x * BLOCK * kHistUnroll + threadIdx.x; base < nv; base += stride)
         {
             f4 v[kHistUnroll];
 #pragma unroll
             for (int u = 0; u < kHistUnroll; ++u)
             {
-                int64_t i = base + (int64_t) u * kBlock;
+                int64_t i = base + (int64_t) u * BLOCK;
                 v[u]      = i < nv ? __builtin_nontemporal_load(x4 + i) : f4 {NAN, NAN, NAN, NAN};
             }
 #pragma unroll
@@ -301,13 +304,13 @@ __global__ __launch_bounds__(kBlock) void histogram_tensor_kernel(const float* _
         }
         done = nv * 4;
     }
-    for (int64_t i = done + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
+    for (int64_t i = done + (int64_t) blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t) gridDim.x * BLOCK)
         add(x[i]);
     zc = wave_sum(zc);
     if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
         atomicAdd(&lds[w][zbin], zc);
     __syncthreads();
-    for (int b = threadIdx.x; b < kPdfSize; b += kBlock)
+    for (int b = threadIdx.x; b < kPdfSize; b += BLOCK)
     {
         uint32_t s = 0;
 #pragma unroll
@@ -456,12 +459,19 @@ void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, in
     if (C == 1)
     {
         int64_t n  = outer * K;
-        // enough workgroups to keep HBM busy (8 per CU), few enough that the per-bin global atomics
-        // stay a small fraction of the pass (<= 2048 x 512 64-bit adds, spread over 32 lines)
-        int blocks = stream_blocks(n, (int64_t) kBlock * kHistUnroll * 4 * 4);
-        if (blocks > kHistGrid)
-            blocks = kHistGrid;
-        histogram_tensor_kernel<<<blocks, kBlock, 0, s>>>(x, n, al ? 1 : 0, d);
+        // tools/hist_variants.hip: large tensors stream best with 8 x 256-lane workgroups per CU;
+        // below that the fixed per-workgroup cost (LDS clear + 512-bin flush into the global
+        // counters) dominates, and one 1024-lane workgroup per CU (16 wave-private copies) wins
+        if (n >= kHistLargeN)
+        {
+            int blocks = stream_blocks(n, (int64_t) 256 * kHistUnroll * 4 * 4);
+            histogram_tensor_kernel<256><<<blocks < kHistGrid ? blocks : kHistGrid, 256, 0, s>>>(x, n, al ? 1 : 0, d);
+        }
+        else
+        {
+            int blocks = stream_blocks(n, (int64_t) 1024 * kHistUnroll * 4 * 2);
+            histogram_tensor_kernel<1024><<<blocks < 256 ? blocks : 256, 1024, 0, s>>>(x, n, al ? 1 : 0, d);
+        }
     }
     else
     {

@@ -48,7 +48,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 }
 
 // COPIES: LDS histograms per block (1 = shared by the block, BLOCK/64 = one per wave)
-template <int BLOCK, int UNROLL, int COPIES, bool NT, bool ZSKIP>
+template <int BLOCK, int UNROLL, int COPIES, bool NT, bool ZSKIP, bool PART = false>
 __global__ __launch_bounds__(BLOCK) void hist_var(const float* __restrict__ x, int64_t n, Binner bn,
                                                   unsigned long long* __restrict__ counts)
 {
@@ -108,9 +108,199 @@ __global__ __launch_bounds__(BLOCK) void hist_var(const float* __restrict__ x, i
 #pragma unroll
         for (int i = 0; i < COPIES; ++i)
             s += lds[i][b];
+        if (PART)
+            reinterpret_cast<uint32_t*>(counts + 1024)[(int64_t) blockIdx.x * kBins + b] = s;
+        else if (s)
+            atomicAdd(&counts[b], (unsigned long long) s);
+    }
+}
+
+// replicated global counts: block b adds into replica (b % R); the last block to finish (atomic
+// ticket) folds the R replicas into counts and re-zeroes them -- no second launch, R-fold less
+// contention on the 512 global counters
+template <int BLOCK, int UNROLL, int COPIES, int R>
+__global__ __launch_bounds__(BLOCK) void hist_rep(const float* __restrict__ x, int64_t n, Binner bn,
+                                                  unsigned long long* __restrict__ counts)
+{
+    __shared__ uint32_t lds[COPIES][kBins];
+    __shared__ int is_last;
+    unsigned long long* rep = counts + 1024;              // [R][512], zero on entry
+    unsigned int* ticket    = reinterpret_cast<unsigned int*>(counts + 1024 + R * kBins);
+    const int copy = (threadIdx.x >> 6) % COPIES;
+    for (int i = threadIdx.x; i < COPIES * kBins; i += BLOCK)
+        (&lds[0][0])[i] = 0;
+    __syncthreads();
+    const int zbin = bn.bin(0.0f);
+    uint32_t zc    = 0;
+    auto add = [&](float v) {
+        if (v == 0.0f)
+        {
+            ++zc;
+            return;
+        }
+        int b = bn.bin(v);
+        if (b >= 0)
+            atomicAdd(&lds[copy][b], 1u);
+    };
+    const f4* x4         = reinterpret_cast<const f4*>(x);
+    const int64_t nv     = n / 4;
+    const int64_t stride = (int64_t) gridDim.x * BLOCK * UNROLL;
+    for (int64_t base = (int64_t) blockIdx.x * BLOCK * UNROLL + threadIdx.x; base < nv; base += stride)
+    {
+        f4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            int64_t i = base + (int64_t) u * BLOCK;
+            v[u]      = i < nv ? __builtin_nontemporal_load(x4 + i) : f4 {NAN, NAN, NAN, NAN};
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            add(v[u].x);
+            add(v[u].y);
+            add(v[u].z);
+            add(v[u].w);
+        }
+    }
+    for (int64_t i = nv * 4 + (int64_t) blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t) gridDim.x * BLOCK)
+        add(x[i]);
+    zc = wave_sum(zc);
+    if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
+        atomicAdd(&lds[copy][zbin], zc);
+    __syncthreads();
+    unsigned long long* mine = rep + (blockIdx.x % R) * kBins;
+    for (int b = threadIdx.x; b < kBins; b += BLOCK)
+    {
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < COPIES; ++i)
+            s += lds[i][b];
+        if (s)
+            atomicAdd(&mine[b], (unsigned long long) s);
+    }
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0)
+        is_last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (is_last)
+    {
+        __threadfence();
+        for (int b = threadIdx.x; b < kBins; b += BLOCK)
+        {
+            unsigned long long s = 0;
+            for (int r = 0; r < R; ++r)
+                s += atomicExch(&rep[r * kBins + b], 0ull);
+            if (s)
+                counts[b] += s;
+        }
+        if (threadIdx.x == 0)
+            *ticket = 0;
+    }
+}
+
+template <int BLOCK, int UNROLL, int COPIES, int R, int GRID>
+void launch_rep(const float* x, int64_t n, Binner bn, unsigned long long* c, hipStream_t s)
+{
+    int64_t need = (n / 4 + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
+    int g        = (int) std::max<int64_t>(1, std::min<int64_t>(need, GRID));
+    hist_rep<BLOCK, UNROLL, COPIES, R><<<g, BLOCK, 0, s>>>(x, n, bn, c);
+}
+
+// sum per-block partial rows [nrows][512] into counts (64-bit): 2-D grid of row slices
+__global__ __launch_bounds__(256) void reduce_parts(const uint32_t* __restrict__ part, int nrows,
+                                                    unsigned long long* __restrict__ counts)
+{
+    const int rows_per = (nrows + gridDim.x - 1) / gridDim.x;
+    const int r0 = blockIdx.x * rows_per, r1 = min(nrows, r0 + rows_per);
+    for (int b = threadIdx.x; b < kBins; b += 256)
+    {
+        unsigned long long s = 0;
+        for (int r = r0; r < r1; ++r)
+            s += part[(int64_t) r * kBins + b];
+        if (s)
+            atomicAdd(&counts[b], s);
+    }
+}
+
+template <int BLOCK, int UNROLL, int GRID>
+void launch_part(const float* x, int64_t n, Binner bn, unsigned long long* c, hipStream_t s)
+{
+    int64_t need = (n / 4 + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
+    int g        = (int) std::max<int64_t>(1, std::min<int64_t>(need, GRID));
+    hist_var<BLOCK, UNROLL, BLOCK / 64, true, true, true><<<g, BLOCK, 0, s>>>(x, n, bn, c);
+    reduce_parts<<<std::min(g, 64), 256, 0, s>>>(reinterpret_cast<const uint32_t*>(c + 1024), g, c);
+}
+
+// run-length variant: each lane keeps (bin, count) of its current run and only touches LDS when
+// the bin changes (hot bins of peaked distributions stop serialising the LDS atomics)
+template <int BLOCK, int UNROLL, int COPIES>
+__global__ __launch_bounds__(BLOCK) void hist_rl(const float* __restrict__ x, int64_t n, Binner bn,
+                                                 unsigned long long* __restrict__ counts)
+{
+    __shared__ uint32_t lds[COPIES][kBins];
+    const int copy = (threadIdx.x >> 6) % COPIES;
+    for (int i = threadIdx.x; i < COPIES * kBins; i += BLOCK)
+        (&lds[0][0])[i] = 0;
+    __syncthreads();
+    int cur = -1;
+    uint32_t cnt = 0;
+    auto add = [&](float v) {
+        int b = bn.bin(v);
+        if (b == cur)
+            ++cnt;
+        else
+        {
+            if (cur >= 0)
+                atomicAdd(&lds[copy][cur], cnt);
+            cur = b;
+            cnt = 1;
+        }
+    };
+    const f4* x4         = reinterpret_cast<const f4*>(x);
+    const int64_t nv     = n / 4;
+    const int64_t stride = (int64_t) gridDim.x * BLOCK * UNROLL;
+    for (int64_t base = (int64_t) blockIdx.x * BLOCK * UNROLL + threadIdx.x; base < nv; base += stride)
+    {
+        f4 v[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            int64_t i = base + (int64_t) u * BLOCK;
+            v[u]      = i < nv ? __builtin_nontemporal_load(x4 + i) : f4 {NAN, NAN, NAN, NAN};
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            add(v[u].x);
+            add(v[u].y);
+            add(v[u].z);
+            add(v[u].w);
+        }
+    }
+    for (int64_t i = nv * 4 + (int64_t) blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t) gridDim.x * BLOCK)
+        add(x[i]);
+    if (cur >= 0)
+        atomicAdd(&lds[copy][cur], cnt);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBins; b += BLOCK)
+    {
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < COPIES; ++i)
+            s += lds[i][b];
         if (s)
             atomicAdd(&counts[b], (unsigned long long) s);
     }
+}
+
+template <int BLOCK, int UNROLL, int COPIES, int GRID>
+void launch_rl(const float* x, int64_t n, Binner bn, unsigned long long* c, hipStream_t s)
+{
+    int64_t need = (n / 4 + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
+    int g        = (int) std::max<int64_t>(1, std::min<int64_t>(need, GRID));
+    hist_rl<BLOCK, UNROLL, COPIES><<<g, BLOCK, 0, s>>>(x, n, bn, c);
 }
 
 // min/max partials (stats.hip minmax_tensor_kernel shape)
@@ -247,42 +437,36 @@ int main(int argc, char** argv)
     float* x;
     unsigned long long *cnt, *ref;
     CK(hipMalloc(&x, n * 4));
-    CK(hipMalloc(&cnt, 4096 * 8 * 2));
+    CK(hipMalloc(&cnt, 1024 * 8 + 8192 * 512 * 4));
     CK(hipMalloc(&ref, kBins * 8));
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    CK(hipMemset(cnt, 0, 1024 * 8 + 8192 * 512 * 4));
     std::vector<Variant> vs = {
         {"read-only ceiling b256 u4 g4096", launch_read<256, 4, 4096>, false, {}},
-        {"minmax b256 u4 g1024 (current)", launch_minmax<256, 4, false, 1024>, false, {}},
-        {"minmax b256 u4 g1024 nt", launch_minmax<256, 4, true, 1024>, false, {}},
-        {"minmax b256 u4 g2048 nt", launch_minmax<256, 4, true, 2048>, false, {}},
-        {"minmax b256 u2 g4096 nt", launch_minmax<256, 2, true, 4096>, false, {}},
-        {"minmax b512 u4 g1024 nt", launch_minmax<512, 4, true, 1024>, false, {}},
-        {"hist b256 u2 c4 g512 (current)", launch_hist<256, 2, 4, false, true, 512>, true, {}},
-        {"hist b256 u2 c4 g1024", launch_hist<256, 2, 4, false, true, 1024>, true, {}},
-        {"hist b256 u2 c4 g2048", launch_hist<256, 2, 4, false, true, 2048>, true, {}},
-        {"hist b256 u4 c4 g2048", launch_hist<256, 4, 4, false, true, 2048>, true, {}},
-        {"hist b256 u4 c4 g2048 nt", launch_hist<256, 4, 4, true, true, 2048>, true, {}},
-        {"hist b256 u4 c4 g4096 nt", launch_hist<256, 4, 4, true, true, 4096>, true, {}},
-        {"hist b256 u2 c4 g4096 nt", launch_hist<256, 2, 4, true, true, 4096>, true, {}},
-        {"hist b256 u4 c1 g2048 nt", launch_hist<256, 4, 1, true, true, 2048>, true, {}},
-        {"hist b256 u4 c2 g2048 nt", launch_hist<256, 4, 2, true, true, 2048>, true, {}},
-        {"hist b512 u4 c8 g1024 nt", launch_hist<512, 4, 8, true, true, 1024>, true, {}},
-        {"hist b512 u2 c8 g2048 nt", launch_hist<512, 2, 8, true, true, 2048>, true, {}},
-        {"hist b1024 u2 c16 g1024 nt", launch_hist<1024, 2, 16, true, true, 1024>, true, {}},
-        {"hist b256 u4 c4 g2048 nt nozskip", launch_hist<256, 4, 4, true, false, 2048>, true, {}},
-        {"hist b256 u8 c4 g2048 nt", launch_hist<256, 8, 4, true, true, 2048>, true, {}},
-        {"hist b256 u4 c4 g8192 nt", launch_hist<256, 4, 4, true, true, 8192>, true, {}},
+        {"hist b256 u4 c4 g2048 nt (current)", launch_hist<256, 4, 4, true, true, 2048>, true, {}},
+        {"hist b256 u4 c4 g1024 nt", launch_hist<256, 4, 4, true, true, 1024>, true, {}},
+        {"hist b256 u4 c4 g512 nt", launch_hist<256, 4, 4, true, true, 512>, true, {}},
+        {"hist b512 u4 c8 g512 nt", launch_hist<512, 4, 8, true, true, 512>, true, {}},
+        {"hist b1024 u2 c16 g256 nt", launch_hist<1024, 2, 16, true, true, 256>, true, {}},
+        {"hist b1024 u4 c16 g256 nt", launch_hist<1024, 4, 16, true, true, 256>, true, {}},
+        {"part b256 u4 g1024", launch_part<256, 4, 1024>, true, {}},
+        {"part b256 u4 g512", launch_part<256, 4, 512>, true, {}},
+        {"part b512 u4 g512", launch_part<512, 4, 512>, true, {}},
+        {"part b1024 u2 g256", launch_part<1024, 2, 256>, true, {}},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    const char* dname[2] = {"relu(N(0,1)*1.5+0.2)", "N(0,1)*2"};
-    for (int dist = 0; dist < 2; ++dist)
+    const char* dname[4] = {"relu(N(0,1)*1.5+0.2)", "N(0,1)*2", "N(0,1)*2, range +-30 (outliers)", "relu, range 0..40 (outliers)"};
+    for (int dist = 0; dist < 4; ++dist)
     {
-        gen_kernel<<<4096, 256, 0, s>>>(x, n, dist == 0, 1234);
+        gen_kernel<<<4096, 256, 0, s>>>(x, n, dist == 0 || dist == 3, 1234);
         CK(hipStreamSynchronize(s));
-        Binner bn = dist == 0 ? binner_for(0.0f, 9.0f) : binner_for(-11.0f, 11.0f);
+        Binner bn = dist == 0 ? binner_for(0.0f, 9.0f)
+                    : dist == 1 ? binner_for(-11.0f, 11.0f)
+                    : dist == 2 ? binner_for(-30.0f, 30.0f)
+                                : binner_for(0.0f, 40.0f);
         CK(hipMemsetAsync(ref, 0, kBins * 8, s));
         launch_hist<256, 2, 4, false, true, 512>(x, n, bn, ref, s);
         std::vector<unsigned long long> href(kBins), hc(kBins);
@@ -293,7 +477,7 @@ int main(int argc, char** argv)
         for (auto& v: vs)
         {
             v.ms.clear();
-            CK(hipMemsetAsync(cnt, 0, kBins * 8, s));
+            CK(hipMemsetAsync(cnt, 0, 1024 * 8 + 33 * kBins * 8, s));
             v.launch(x, n, bn, cnt, s);
             CK(hipMemcpy(hc.data(), cnt, kBins * 8, hipMemcpyDeviceToHost));
             if (v.check && memcmp(hc.data(), href.data(), kBins * 8) != 0)
@@ -302,7 +486,7 @@ int main(int argc, char** argv)
         for (int r = 0; r < rounds; ++r)
             for (auto& v: vs)
             {
-                CK(hipMemsetAsync(cnt, 0, kBins * 8, s));
+                CK(hipMemsetAsync(cnt, 0, 1024 * 8 + 33 * kBins * 8, s));
                 CK(hipEventRecord(e0, s));
                 v.launch(x, n, bn, cnt, s);
                 CK(hipEventRecord(e1, s));

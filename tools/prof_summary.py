@@ -48,6 +48,19 @@ def main():
         print("  %-62s calls/step %5.1f  ms/step %.4f" % (k, c / steps, d / 1e6 / steps))
     q_ns = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in seg if QDQ in r["Kernel_Name"]) / steps
     print("per-tensor QDQ kernel time/step: %.4f ms" % (q_ns / 1e6))
+    # calibration (compute_encodings) = every aimet kernel before the first QDQ dispatch
+    cal = [r for r in rows[:qi[0]] if "aimet_amd" in r["Kernel_Name"]]
+    if cal:
+        cagg = collections.defaultdict(lambda: [0, 0])
+        for r in cal:
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").replace("aimet_amd::", "")
+            k = k.replace("void ", "").split("(")[0][-60:]
+            cagg[k][0] += 1
+            cagg[k][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        tot = sum(d for _, d in cagg.values())
+        print("compute_encodings kernels (before the first QDQ step): %.3f ms GPU time" % (tot / 1e6))
+        for k, (c, d) in sorted(cagg.items(), key=lambda x: -x[1][1]):
+            print("  %-62s calls %5d  total ms %.4f  avg us %.1f" % (k, c, d / 1e6, d / 1e3 / c))
     if len(args) >= 3:
         f = [v for n, v in pmc(args[1], "FETCH_SIZE") if QDQ in n][-per_step:]
         w = [v for n, v in pmc(args[2], "WRITE_SIZE") if QDQ in n][-per_step:]
