@@ -388,3 +388,31 @@ class Quantize(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         return QuantizeDequantize.backward(ctx, grad)
+
+
+# ---------------------------------------------------------------------------------------------
+# batched compute_encoding (QuantizationSimModel.compute_encodings' per-quantizer loop)
+# ---------------------------------------------------------------------------------------------
+def compute_encodings_batched(quantizers):
+    """``q.compute_encoding()`` for every quantizer (v1/tensor_quantizer.py:280-321 semantics) with
+    one native call -- one device search launch + one stream sync -- per distinct
+    (bitwidth, symmetric, strict, unsigned) setting instead of one sync per quantizer."""
+    groups = {}
+    for q in quantizers:
+        if not q.enabled or q._is_encoding_frozen or q.bitwidth == 32 or \
+                q.data_type == QuantizationDataType.float:
+            q.compute_encoding()           # the non-native branches
+            continue
+        key = (int(q.bitwidth), bool(q.use_symmetric_encodings), bool(q.use_strict_symmetric),
+               bool(q.use_unsigned_symmetric), str(q._op()._device))
+        groups.setdefault(key, []).append(q)
+    for (bw, sym, strict, unsign, _), qs in groups.items():
+        results = AimetTensorQuantizer.getEncodings([q._op() for q in qs], bw, sym, strict, unsign)
+        for q, (enc, valid) in zip(qs, results):
+            q._encoding = []
+            if not valid:
+                q.enabled = False
+            else:
+                q._encoding = enc if isinstance(enc, list) else [enc]
+            q.is_unsigned_symmetric = (q.use_symmetric_encodings and q.use_unsigned_symmetric and
+                                       all(e.min >= 0 and e.max >= 0 for e in q._encoding))

@@ -1,0 +1,248 @@
+"""QuantizationSimModel for the MI355X core: wraps a model's quantizable layers, calibrates them
+(compute_encodings) and exports / loads encodings.
+
+Mirrors aimet_torch/v1/quantsim.py (QuantizationSimModel :170-1043, compute_encodings :381-449,
+_export_encodings_to_files :940-1043, load_encodings :1696-1838) for the hot path of §8: the
+calibration loop (ANALYSIS mode: every quantizer's updateStats on the device, no host sync), the
+encoding computation (batched: one device search launch + one sync per setting instead of one
+per quantizer) and the ACTIVE fake-quant forward.
+
+Deliberately narrower than the reference (SURVEY §8 marks the rest out of scope):
+  * the quantizable layers are the modules of `quantizable_types` (default: conv / conv-transpose /
+    linear), each with an output quantizer, a weight quantizer (bias unquantized) and an input
+    quantizer enabled for the first layer only -- the reference's default config
+    (aimet_common/quantsim_config/default_config.json) without connected-graph supergroups;
+  * `config_file` accepts the defaults section of that JSON schema (params is_symmetric,
+    strict_symmetric, unsigned_symmetric, per_channel_quantization) as a path or a dict;
+  * export writes the PyTorch-named `<prefix>_torch.encodings` file; the ONNX-named
+    `<prefix>.encodings` needs an ONNX export of the model, which is outside this core.
+"""
+import contextlib
+import copy
+import json
+import os
+from typing import Any, Callable, Dict, Optional, Union
+
+import torch
+from torch import nn
+
+from aimet_amd.qc_quantize_op import (QUANTIZER_TYPE_INPUT, QUANTIZER_TYPE_OUTPUT, QcQuantizeOpMode,
+                                      QcQuantizeWrapper, StaticGridQuantWrapper)
+from aimet_amd.quantizers import QuantizationDataType, QuantScheme, compute_encodings_batched
+
+ENCODING_VERSION = "0.6.1"
+DEFAULT_QUANTIZABLE_TYPES = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d, nn.ConvTranspose2d,
+                             nn.ConvTranspose3d, nn.Linear)
+
+_SCHEME_NAMES = {"tf": QuantScheme.post_training_tf, "tf_enhanced": QuantScheme.post_training_tf_enhanced,
+                 "percentile": QuantScheme.post_training_percentile}
+
+
+def _truthy(v):
+    return v if isinstance(v, bool) else str(v) == "True"
+
+
+def _load_config(config_file) -> Dict:
+    cfg = {"param_symmetric": True, "act_symmetric": False, "strict_symmetric": False,
+           "unsigned_symmetric": False, "per_channel_quantization": False}
+    if config_file is None:
+        return cfg
+    if isinstance(config_file, (str, os.PathLike)):
+        with open(config_file) as f:
+            config_file = json.load(f)
+    d = config_file.get("defaults", {})
+    if "is_symmetric" in d.get("params", {}):
+        cfg["param_symmetric"] = _truthy(d["params"]["is_symmetric"])
+    if "is_symmetric" in d.get("ops", {}):
+        cfg["act_symmetric"] = _truthy(d["ops"]["is_symmetric"])
+    for k in ("strict_symmetric", "unsigned_symmetric", "per_channel_quantization"):
+        if k in d:
+            cfg[k] = _truthy(d[k])
+    return cfg
+
+
+@contextlib.contextmanager
+def _eval_mode(model):
+    was = model.training
+    model.eval()
+    try:
+        yield
+    finally:
+        model.train(was)
+
+
+class QuantizationSimModel:
+    """v1/quantsim.py:170."""
+
+    def __init__(self, model: nn.Module, dummy_input=None,
+                 quant_scheme: Union[str, QuantScheme] = QuantScheme.post_training_tf_enhanced,
+                 rounding_mode: str = "nearest", default_output_bw: int = 8, default_param_bw: int = 8,
+                 in_place: bool = False, config_file=None,
+                 default_data_type: QuantizationDataType = QuantizationDataType.int,
+                 quantizable_types=DEFAULT_QUANTIZABLE_TYPES):
+        if isinstance(quant_scheme, str):
+            quant_scheme = _SCHEME_NAMES[quant_scheme]
+        if default_data_type != QuantizationDataType.int:
+            raise NotImplementedError("float (fp8/fp16) quantization is outside the MI355X integer QDQ core")
+        self.model = model if in_place else copy.deepcopy(model)
+        self._quant_scheme = quant_scheme
+        self._rounding_mode = rounding_mode
+        self._default_output_bw = default_output_bw
+        self._default_param_bw = default_param_bw
+        self._percentile_value = 100
+        self._cfg = _load_config(config_file)
+        self._excluded_layer_names = []
+        first = True
+        for parent_name, parent in list(self.model.named_modules()):
+            for child_name, child in list(parent.named_children()):
+                if isinstance(child, quantizable_types) and not isinstance(child, QcQuantizeWrapper):
+                    w = StaticGridQuantWrapper(child, default_param_bw, default_output_bw, rounding_mode,
+                                               quant_scheme, is_output_quantized=True,
+                                               is_symmetric=self._cfg["act_symmetric"])
+                    for pname, pq in w.param_quantizers.items():
+                        pq.use_symmetric_encodings = self._cfg["param_symmetric"]
+                        if pname == "bias":
+                            pq.enabled = False
+                    if self._cfg["per_channel_quantization"]:
+                        w.enable_per_channel_quantization()
+                    for q in self._quantizers_of(w):
+                        q.use_strict_symmetric = self._cfg["strict_symmetric"]
+                        q.use_unsigned_symmetric = self._cfg["unsigned_symmetric"]
+                    if first:
+                        w.enable_input_quantizers(True)   # model_input: is_input_quantized
+                        first = False
+                    setattr(parent, child_name, w)
+        if dummy_input is not None:
+            self._run_passthrough(dummy_input)
+
+    # -- helpers --------------------------------------------------------------------------------
+    @staticmethod
+    def _quantizers_of(w):
+        return list(w.input_quantizers) + list(w.param_quantizers.values()) + list(w.output_quantizers)
+
+    def quant_wrappers(self):
+        for name, m in self.model.named_modules():
+            if isinstance(m, QcQuantizeWrapper):
+                yield name, m
+
+    def _run_passthrough(self, dummy_input):
+        """Checks the wrapped model runs on the dummy input (no statistics are collected)."""
+        for _, w in self.quant_wrappers():
+            w.set_mode(QcQuantizeOpMode.PASSTHROUGH)
+        with _eval_mode(self.model), torch.no_grad():
+            if isinstance(dummy_input, (list, tuple)):
+                self.model(*dummy_input)
+            else:
+                self.model(dummy_input)
+
+    def set_percentile_value(self, percentile_value: float):
+        """v1/quantsim.py:361-372."""
+        if self._quant_scheme != QuantScheme.post_training_percentile:
+            raise ValueError("set_percentile_value() can only be called with the percentile quant scheme")
+        self._percentile_value = percentile_value
+
+    # -- calibration ------------------------------------------------------------------------------
+    def compute_encodings(self, forward_pass_callback: Callable[[nn.Module, Any], Any],
+                          forward_pass_callback_args: Any = None):
+        """v1/quantsim.py:381-449: reset, ANALYSIS forward(s), encodings, ACTIVE."""
+        for _, w in self.quant_wrappers():
+            w.reset_encodings()
+            w.set_mode(QcQuantizeOpMode.ANALYSIS)
+            if self._quant_scheme == QuantScheme.post_training_percentile:
+                w.set_percentile_value(self._percentile_value)
+        with _eval_mode(self.model), torch.no_grad():
+            forward_pass_callback(self.model, forward_pass_callback_args)
+        # every activation / param quantizer of the model in one batched native call per setting
+        quantizers = [q for _, w in self.quant_wrappers() for q in self._quantizers_of(w)]
+        compute_encodings_batched(quantizers)
+        for _, w in self.quant_wrappers():
+            w.set_mode(QcQuantizeOpMode.ACTIVE)
+
+    def __call__(self, *args, **kwargs):
+        return self.model(*args, **kwargs)
+
+    # -- export / import --------------------------------------------------------------------------
+    def get_encodings_dict(self) -> Dict:
+        """The `<prefix>_torch.encodings` content (v1/quantsim.py:884-938, 1031-1043)."""
+        activation, params = {}, {}
+        for name, w in self.quant_wrappers():
+            for kind, encs in ((QUANTIZER_TYPE_INPUT, w.export_input_encodings()),
+                               (QUANTIZER_TYPE_OUTPUT, w.export_output_encodings())):
+                for i, e in enumerate(encs):
+                    if e is not None:
+                        activation.setdefault(name, {}).setdefault(kind, {})[str(i)] = e[0]
+            for pname, e in w.export_param_encodings().items():
+                if e is not None:
+                    params["%s.%s" % (name, pname)] = e
+        return {"version": ENCODING_VERSION, "activation_encodings": activation, "param_encodings": params,
+                "excluded_layers": list(self._excluded_layer_names),
+                "quantizer_args": self.quant_args}
+
+    @property
+    def quant_args(self) -> Dict:
+        """v1/quantsim.py quant_args: the settings the encodings were made with."""
+        return {"activation_bitwidth": self._default_output_bw, "param_bitwidth": self._default_param_bw,
+                "dtype": "int", "is_symmetric": self._cfg["param_symmetric"],
+                "per_channel_quantization": self._cfg["per_channel_quantization"],
+                "quant_scheme": self._quant_scheme.name, "strict_symmetric": self._cfg["strict_symmetric"],
+                "unsigned_symmetric": self._cfg["unsigned_symmetric"]}
+
+    def export(self, path: str, filename_prefix: str, dummy_input=None):
+        """Writes `<path>/<prefix>_torch.encodings` (JSON) and the model state dict
+        (`<prefix>.pth`, weights unquantized as in v1/quantsim.py:455-520)."""
+        os.makedirs(path, exist_ok=True)
+        enc_path = os.path.join(path, filename_prefix + "_torch.encodings")
+        with open(enc_path, "w") as f:
+            json.dump(self.get_encodings_dict(), f, sort_keys=True, indent=4)
+        torch.save(self._original_state_dict(), os.path.join(path, filename_prefix + ".pth"))
+        return enc_path
+
+    def _original_state_dict(self):
+        sd = self.model.state_dict()
+        return {k.replace("._module_to_wrap", ""): v for k, v in sd.items()}
+
+    def load_encodings(self, encodings: Union[Dict, str, os.PathLike], strict: bool = True, partial: bool = True,
+                       requires_grad: Optional[bool] = None, allow_overwrite: bool = True):
+        """v1/quantsim.py:1696-1838."""
+        if isinstance(encodings, (str, os.PathLike)):
+            with open(encodings) as f:
+                encodings = json.load(f)
+        if "param_encodings" not in encodings:
+            param_encodings, activation_encodings = encodings, {}
+        else:
+            param_encodings = encodings.get("param_encodings", {})
+            activation_encodings = encodings.get("activation_encodings", {})
+        if not param_encodings and not activation_encodings:
+            raise RuntimeError("the encodings contain neither parameter nor activation encodings")
+        if strict:
+            keys = set(param_encodings) | set(activation_encodings)
+            model_keys = {n.replace("._module_to_wrap", "") for n, _ in self.model.named_modules()} | \
+                         {n.replace("._module_to_wrap", "") for n, _ in self.model.named_parameters()}
+            missing = keys - model_keys
+            if missing:
+                raise RuntimeError("Encoding dictionary contains modules/parameters that doesn't exist in the "
+                                   "model: " + ", ".join(sorted(missing)))
+        for name, w in self.quant_wrappers():
+            penc = {p: param_encodings["%s.%s" % (name, p)] for p in w.param_quantizers
+                    if "%s.%s" % (name, p) in param_encodings}
+            try:
+                w.import_param_encodings(penc, strict, partial, requires_grad, allow_overwrite)
+                entry = activation_encodings.get(name, {})
+                w.import_input_encodings(entry.get(QUANTIZER_TYPE_INPUT, {}), strict, partial, requires_grad,
+                                         allow_overwrite)
+                w.import_output_encodings(entry.get(QUANTIZER_TYPE_OUTPUT, {}), strict, partial, requires_grad,
+                                          allow_overwrite)
+            except RuntimeError as e:
+                raise RuntimeError("Encoding import failed for module: %s.\n%s" % (name, e)) from e
+        for _, w in self.quant_wrappers():
+            w.set_mode(QcQuantizeOpMode.ACTIVE)
+
+    def load_and_freeze_encodings(self, encoding_path: str, ignore_when_quantizer_disabled: bool = False):
+        self.load_encodings(encoding_path, strict=not ignore_when_quantizer_disabled, partial=True,
+                            requires_grad=False, allow_overwrite=False)
+
+
+def load_encodings_to_sim(quant_sim_model: QuantizationSimModel, pytorch_encoding_path: str):
+    """v1/quantsim.py:2278."""
+    quant_sim_model.load_encodings(pytorch_encoding_path, strict=True, partial=False, requires_grad=None,
+                                   allow_overwrite=None)
