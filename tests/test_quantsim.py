@@ -236,7 +236,9 @@ def test_qat_step_gates_parameter_gradients():
     sim = QuantizationSimModel(net, quant_scheme="tf_enhanced", config_file=PER_CHANNEL_CFG)
     sim.compute_encodings(lambda m, d: [m(x) for x in d], _calib(4))
     sim.model.train()
-    x = _calib(5, 1)[0]
+    # SteGatingFuncForParameters runs in the backward of the wrapper inputs (as in the reference),
+    # so the first layer's gating needs an input that requires grad
+    x = _calib(5, 1)[0].requires_grad_(True)
     loss = sim(x).square().mean()
     loss.backward()
     for name, w in sim.quant_wrappers():
