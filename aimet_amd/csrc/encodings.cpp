@@ -13,6 +13,7 @@
 //   Percentile                     PercentileEncodingAnalyzer.cpp:78-190, math_functions.cpp:404-439
 //   MSE                            MseEncodingAnalyzer.cpp:79-264
 #include "encodings.hpp"
+#include "mse_core.hpp"
 #include "tfe_core.hpp"
 
 #include <algorithm>
@@ -29,8 +30,6 @@ namespace
 {
 constexpr double kGateEps  = 1e-5;   // quantization_utils.hpp:51 EPSILON
 constexpr double kMinRange = 0.01;   // TfEncodingAnalyzer.h:81 / TfEnhancedEncodingAnalyzer.h:105
-constexpr float kFltLowest = std::numeric_limits<float>::lowest();
-constexpr float kFltMax    = std::numeric_limits<float>::max();
 
 inline double sq(double v)
 {
@@ -52,42 +51,7 @@ aimet_tf_encoding make_enc(double mn, double mx, double d, double o, int32_t bw)
 
 aimet_tf_encoding computed_encoding(int32_t bw, double mn, double mx, bool sym, bool strict, bool unsign)
 {
-    double steps = std::pow(2.0, bw) - 1;
-    if (sym && strict)
-        steps -= 1;
-    if (std::isinf(mn))
-        mn = kFltLowest;
-    if (std::isinf(mx))
-        mx = kFltMax;
-    aimet_tf_encoding e = make_enc(0, 0, 0, 0, bw);
-    if (sym && (mn < 0.0 || !unsign))
-    {
-        double absmax        = std::max(std::abs(mx), std::abs(mn));
-        unsigned int posSteps = (unsigned int) std::floor(steps / 2);
-        e.delta              = absmax / posSteps;
-        e.offset             = -std::ceil(steps / 2);
-        e.min                = std::max(e.offset * e.delta, (double) kFltLowest);
-        e.max                = std::min(e.delta * posSteps, (double) kFltMax);
-        return e;
-    }
-    e.delta = (mx - mn) / steps;
-    if (!(mn < 0 && mx > 0))
-    {
-        // one end is zero: 0 is already on the grid
-        e.offset = std::round(mn / e.delta);
-        e.min    = mn;
-        e.max    = mx;
-        return e;
-    }
-    double zeroCode = std::round(-mn / e.delta);
-    zeroCode        = std::min(steps, std::max(0.0, zeroCode));
-    e.offset        = -zeroCode;
-    double lo       = e.delta * e.offset;
-    e.min           = (lo >= (double) kFltLowest && lo <= (double) kFltMax) ? lo : (double) kFltLowest;
-    e.max           = mx - mn + e.min;
-    if (e.max > (double) kFltMax)
-        e.max = kFltMax;
-    return e;
+    return mse::computed_encoding(bw, mn, mx, sym, strict, unsign);   // shared with the device (mse_core.hpp)
 }
 
 void gate_min_max(double& mn, double& mx)
@@ -320,67 +284,21 @@ std::pair<float, float> percentile_range(const HistView& h, float percentile)
     return {pLo, pHi};
 }
 
-// ---- MSE ----------------------------------------------------------------------------------
-float mse_cost(int32_t bw, const std::vector<std::pair<float, float>>& centers, float cLo, float cHi, bool sym,
-               bool strict, bool unsign)
-{
-    aimet_tf_encoding e = computed_encoding(bw, cLo, cHi, sym, strict, unsign);
-    float err           = 0;
-    for (const auto& bc: centers)
-    {
-        float v       = bc.first;
-        float clamped = std::max(cLo, std::min(v, cHi));
-        int q         = (int) std::round(clamped / e.delta - e.offset);
-        float deq     = e.delta * (q + e.offset);
-        err += bc.second * sq((double) (v - deq));
-    }
-    return err;
-}
-
+// ---- MSE (mse_core.hpp: shared with the device search in mse_search.hip) -------------------
 std::pair<float, float> mse_range(const HistView& h, int32_t bw, bool sym, bool strict, bool unsign)
 {
-    const float width = (float) (h.xl(1) - h.xl(0));
-    const float hMin  = (float) h.xl(0);
-    const float hMax  = (float) h.xl(kPdfSize - 1) + width;
-    auto range        = observed_range(h);
-    const float lo    = range.first;
-    const float hi    = range.second + width;
-
-    std::vector<float> edges {lo};
-    for (float e = hMin; e <= hMax; e += width)
-        if (e >= lo && e <= hi)
-            edges.push_back(e);
-
-    std::vector<float> mins, maxs;
-    for (float e: edges)
-    {
-        if (e < 0)
-            mins.push_back(e);
-        else if (e > 0)
-            maxs.push_back(e);
-    }
-    mins.push_back(0);
-    maxs.push_back(0);
-
-    const float start = (float) h.xl(0);
-    const float step  = (float) (h.xl(1) - h.xl(0));
-    const int nc      = (int) edges.size() - 1;
-    std::vector<std::pair<float, float>> centers(std::max(nc, 0));
-    for (int i = 0; i < nc; ++i)
-    {
-        centers[i].first = (i == 0) ? lo + width / 2 : centers[i - 1].first + width;
-        int idx          = (int) std::floor((centers[i].first - start) / step);
-        idx              = std::min(std::max(0, idx), kPdfSize - 1);
-        centers[i].second = (float) h.pdf[idx];
-    }
-
+    tfe::Hist th {h.hist_min, h.bucket, h.pdf};
+    int first, last;
+    tfe::first_last(h.pdf, first, last);
+    float mins[mse::kMaxEdges + 1], maxs[mse::kMaxEdges + 1], cv[mse::kMaxEdges], cw[mse::kMaxEdges];
+    mse::Setup st = mse::setup(th, first, last, mins, maxs, cv, cw);
     float bestErr = std::numeric_limits<float>::max();
-    std::pair<float, float> best(lo, hi);
-    const size_t total = mins.size() * maxs.size() - 1;   // the trailing {0, 0} is not a candidate
-    for (size_t t = 0; t < total; ++t)
+    std::pair<float, float> best(st.lo, st.hi);
+    for (long long t = 0; t < st.total; ++t)
     {
-        float cLo = mins[t / maxs.size()], cHi = maxs[t % maxs.size()];
-        float err = mse_cost(bw, centers, cLo, cHi, sym, strict, unsign);
+        float cLo, cHi;
+        mse::candidate(st, mins, maxs, t, cLo, cHi);
+        float err = mse::cost(bw, cv, cw, st.nc, cLo, cHi, sym, strict, unsign);
         if (err < bestErr)
         {
             bestErr = err;

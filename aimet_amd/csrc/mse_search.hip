@@ -1,0 +1,195 @@
+// mse_search.hip -- MSE encoding search on the device.
+//
+// Reference: MseEncodingAnalyzer::computeEncoding (MseEncodingAnalyzer.cpp:79-264) evaluates
+// every (min edge, max edge) pair of the observed range -- up to ~257^2 candidates x 512 bin
+// centres -- on the host, one channel at a time (10.5 ms per tensor). Here: a 2-D grid
+// (channel, candidate slice); each workgroup rebuilds the channel's candidate grid in LDS (one
+// lane, ~1k serial float ops exactly as the reference loops), evaluates its slice with one
+// candidate per lane, and keeps the first minimum; a second launch folds the slices in candidate
+// order. Arithmetic: mse_core.hpp, shared with the host path (bit-exact).
+#include "mse_core.hpp"
+#include "tq_state.hpp"
+
+namespace aimet_amd
+{
+namespace
+{
+
+struct MsePart
+{
+    float err;
+    int idx;   // candidate index, -1: none selected in this slice
+    float lo, hi;
+    float obs_lo, obs_hi;   // the search range: result when no candidate is ever selected
+};
+
+__device__ __forceinline__ bool better(float e, long long t, float be, long long bt)
+{
+    if (t < 0)
+        return false;
+    if (bt < 0)
+        return true;
+    return (e < be) || (e == be && t < bt);
+}
+
+__global__ __launch_bounds__(kBlock) void mse_search_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
+                                                            int strict, int unsign)
+{
+    __shared__ double pdf[tfe::kBins];
+    __shared__ float mins[mse::kMaxEdges + 1], maxs[mse::kMaxEdges + 1], cv[mse::kMaxEdges], cw[mse::kMaxEdges];
+    __shared__ mse::Setup st;
+    __shared__ int first, last;
+    __shared__ float werr[kBlock / 64];
+    __shared__ long long widx[kBlock / 64];
+    __shared__ float wlo[kBlock / 64], whi[kBlock / 64];
+    const int lane = threadIdx.x & 63;
+    MsePart* parts = reinterpret_cast<MsePart*>(d.search_part);
+    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+    {
+        const int y = blockIdx.y;
+        if (!d.pdf_init[c])
+            continue;   // mse_finish_kernel writes the all-zero-data encoding
+        for (int i = threadIdx.x; i < tfe::kBins; i += kBlock)
+            pdf[i] = d.pdf[c * tfe::kBins + i];
+        __syncthreads();
+        if (threadIdx.x < 64)
+        {
+            int fst = -1, lst = -1;
+            for (int i0 = 0; i0 < tfe::kBins; i0 += 64)
+            {
+                unsigned long long o = __ballot(pdf[i0 + lane] > 0);
+                if (o)
+                {
+                    if (fst < 0)
+                        fst = i0 + __ffsll((long long) o) - 1;
+                    lst = i0 + 63 - __clzll(o);
+                }
+            }
+            if (lane == 0)
+            {
+                first = fst;
+                last  = lst > 0 ? lst : -1;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            tfe::Hist h {d.hist_min[c], d.bucket_size[c], pdf};
+            st = mse::setup(h, first, last, mins, maxs, cv, cw);
+        }
+        __syncthreads();
+        const long long chunk = (st.total + splits - 1) / splits;
+        const long long t0 = (long long) y * chunk;
+        const long long t1 = t0 + chunk < st.total ? t0 + chunk : st.total;
+        float be = 0, blo = 0, bhi = 0;
+        long long bt = -1;
+        for (long long t = t0 + threadIdx.x; t < t1; t += kBlock)
+        {
+            float cLo, cHi;
+            mse::candidate(st, mins, maxs, t, cLo, cHi);
+            float err = mse::cost(bw, cv, cw, st.nc, cLo, cHi, sym != 0, strict != 0, unsign != 0);
+            if (!(err < FLT_MAX))
+                continue;   // `err < bestErr` with bestErr = FLT_MAX never selects it
+            if (better(err, t, be, bt))
+            {
+                be  = err;
+                bt  = t;
+                blo = cLo;
+                bhi = cHi;
+            }
+        }
+        for (int k = 32; k > 0; k >>= 1)
+        {
+            float oe       = __shfl_xor(be, k, 64);
+            long long ot   = __shfl_xor(bt, k, 64);
+            float olo      = __shfl_xor(blo, k, 64);
+            float ohi      = __shfl_xor(bhi, k, 64);
+            if (better(oe, ot, be, bt))
+            {
+                be  = oe;
+                bt  = ot;
+                blo = olo;
+                bhi = ohi;
+            }
+        }
+        if (lane == 0)
+        {
+            werr[threadIdx.x >> 6] = be;
+            widx[threadIdx.x >> 6] = bt;
+            wlo[threadIdx.x >> 6]  = blo;
+            whi[threadIdx.x >> 6]  = bhi;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+        {
+            for (int w = 1; w < kBlock / 64; ++w)
+                if (better(werr[w], widx[w], be, bt))
+                {
+                    be  = werr[w];
+                    bt  = widx[w];
+                    blo = wlo[w];
+                    bhi = whi[w];
+                }
+            parts[c * splits + y] = MsePart {be, bt >= 0 ? (int) bt : -1, blo, bhi, st.lo, st.hi};
+        }
+        __syncthreads();
+    }
+}
+
+// fold the slices of every channel (in candidate order) and write the encodings
+__global__ __launch_bounds__(kBlock) void mse_finish_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
+                                                            int strict, int unsign)
+{
+    const int64_t c = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (c >= C)
+        return;
+    if (!d.pdf_init[c])
+    {
+        // statistics updated but no histogram (all data zero): MseEncodingAnalyzer.cpp:86-99,
+        // numSteps reduced first for strict symmetric
+        float steps = (float) (ldexp(1.0, bw) - 1);
+        if (sym && strict)
+            steps -= 1;
+        int isteps = (int) steps;
+        aimet_tf_encoding e;
+        e.delta  = (1.0 - (-1.0)) / isteps;
+        e.offset = floor(-1.0 / e.delta);
+        e.min    = e.offset * e.delta;
+        e.max    = e.min + isteps * e.delta;
+        e.bw     = bw;
+        d.enc[c] = e;
+        return;
+    }
+    const MsePart* parts = reinterpret_cast<const MsePart*>(d.search_part) + c * splits;
+    float be = 0, blo = parts[0].obs_lo, bhi = parts[0].obs_hi;
+    long long bt = -1;
+    for (int y = 0; y < splits; ++y)
+        if (better(parts[y].err, parts[y].idx, be, bt))
+        {
+            be  = parts[y].err;
+            bt  = parts[y].idx;
+            blo = parts[y].lo;
+            bhi = parts[y].hi;
+        }
+    d.enc[c] = mse::finish(bw, blo, bhi, sym != 0, strict != 0, unsign != 0);
+}
+
+}   // namespace
+
+size_t mse_part_bytes(int64_t C)
+{
+    return sizeof(MsePart) * (size_t) (C > kMseMaxSplits ? C : kMseMaxSplits);
+}
+
+void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s)
+{
+    // slices per channel: fill the chip when there are few channels (per-tensor: 128 workgroups)
+    const int splits = C >= kMseMaxSplits ? 1 : (int) (kMseMaxSplits / C);
+    dim3 grid((unsigned) (C < 65536 ? C : 65536), (unsigned) splits);
+    mse_search_kernel<<<grid, kBlock, 0, s>>>(d, C, splits, bw, sym, strict, unsign);
+    AIMET_LAUNCH_CHECK();
+    mse_finish_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(d, C, splits, bw, sym, strict, unsign);
+    AIMET_LAUNCH_CHECK();
+}
+
+}   // namespace aimet_amd

@@ -74,12 +74,14 @@ void layout(aimet_tensor_quantizer* q, bool assign)
         q->d.pdf    = (double*) take(sizeof(double) * kPdfSize * C);
         q->d.counts = (unsigned long long*) take(sizeof(unsigned long long) * kPdfSize * C);
         q->d.enc    = (aimet_tf_encoding*) take(sizeof(aimet_tf_encoding) * C);
+        q->d.search_part = q->scheme == AIMET_QUANTIZATION_MSE ? take(mse_part_bytes(C)) : nullptr;
     }
     else
     {
-        q->d.pdf    = nullptr;
-        q->d.counts = nullptr;
-        q->d.enc    = nullptr;
+        q->d.pdf         = nullptr;
+        q->d.counts      = nullptr;
+        q->d.enc         = nullptr;
+        q->d.search_part = nullptr;
     }
     q->arena_bytes = off;
 }
@@ -336,14 +338,18 @@ namespace
 
 bool device_search(const aimet_tensor_quantizer* q)
 {
-    return q->hist && q->scheme == AIMET_QUANTIZATION_TF_ENHANCED;
+    return q->hist && (q->scheme == AIMET_QUANTIZATION_TF_ENHANCED || q->scheme == AIMET_QUANTIZATION_MSE);
 }
 
 // getEncoding, part 1: enqueue the device-side search (TF-Enhanced) on the stream.
 void launch_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict, int unsign, hipStream_t s)
 {
-    if (device_search(q))
+    if (!device_search(q))
+        return;
+    if (q->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
         launch_tfe_search(q->d, q->C, b, sym, strict, unsign, s);
+    else
+        launch_mse_search(q->d, q->C, b, sym, strict, unsign, s);
 }
 
 // getEncoding, part 2 (stream already synchronised): read back and finish on the host.
@@ -360,7 +366,8 @@ void collect_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict,
     }
     if (device_search(q))
     {
-        // candidate search ran on the device (tfe_search.hip): only the encodings come back
+        // candidate search ran on the device (tfe_search.hip / mse_search.hip): only the
+        // encodings come back
         AIMET_HIP_CHECK(hipMemcpy(out, q->d.enc, sizeof(aimet_tf_encoding) * C, hipMemcpyDeviceToHost));
         return;
     }
@@ -420,7 +427,7 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
         {
             if (valid)
                 valid[i] = qs[i]->stats_updated ? 1 : 0;
-            if (qs[i]->stats_updated && device_search(qs[i]))
+            if (qs[i]->stats_updated && qs[i]->hist && qs[i]->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
             {
                 ds.push_back(&qs[i]->d);
                 Cs.push_back(qs[i]->C);
@@ -429,6 +436,9 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
             }
             off += qs[i]->C;
         }
+        for (int64_t i = 0; i < nq; ++i)   // the other device searches (MSE), enqueued before the sync
+            if (qs[i]->stats_updated && device_search(qs[i]) && qs[i]->scheme != AIMET_QUANTIZATION_TF_ENHANCED)
+                launch_encoding(qs[i], b, sym, strict, unsign, as_stream(stream));
         std::vector<aimet_tf_encoding> tfe(tfe_total);
         launch_tfe_search_many(ds.data(), Cs.data(), (int) ds.size(), b, sym, strict, unsign, tfe.data(),
                                as_stream(stream));
@@ -438,7 +448,7 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
         off = 0;
         for (int64_t i = 0; i < nq; ++i)
         {
-            if (qs[i]->stats_updated && !device_search(qs[i]))
+            if (qs[i]->stats_updated && !(qs[i]->hist && qs[i]->scheme == AIMET_QUANTIZATION_TF_ENHANCED))
                 collect_encoding(qs[i], b, sym, strict, unsign, out + off);
             off += qs[i]->C;
         }

@@ -66,6 +66,24 @@ AIMET_HD inline void observed_range(const Hist& h, int first, int last, float& l
     hi = smax(hi, lo + kMinRangeF);
 }
 
+// first non-empty bin and last non-empty bin with i > 0 (-1: none), serial form
+AIMET_HD inline void first_last(const double* pdf, int& first, int& last)
+{
+    first = last = -1;
+    for (int i = 0; i < kBins; ++i)
+        if (pdf[i] > 0)
+        {
+            first = i;
+            break;
+        }
+    for (int i = kBins - 1; i > 0; --i)
+        if (pdf[i] > 0)
+        {
+            last = i;
+            break;
+        }
+}
+
 // f sequences of the candidate loops: float accumulator, double comparison (data independent)
 AIMET_HD inline int fseq_asym(float* f)
 {

@@ -27,10 +27,12 @@ struct TqDevice
     float* bin_offset;      // [C] (float)xLeft[0] / bin_bucket    UpdatePdf:265-268
     double* pdf;            // [C][512]
     unsigned long long* counts;   // [C][512] histogram of the current batch
-    aimet_tf_encoding* enc; // [C] device-computed encodings (TF-Enhanced search)
+    aimet_tf_encoding* enc; // [C] device-computed encodings (TF-Enhanced / MSE search)
+    void* search_part;      // MSE search slices (mse_part_bytes(C))
 };
 
-constexpr int kMinmaxParts = 1024;   // grid of the per-tensor min/max pass
+constexpr int kMinmaxParts  = 1024;   // grid of the per-tensor min/max pass
+constexpr int kMseMaxSplits = 128;    // candidate slices of a per-tensor MSE search
 
 // stats.hip
 void launch_batch_minmax(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, int skip_if_init,
@@ -42,6 +44,9 @@ void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s);
 // tfe_search.hip
 // d.enc[c] <- TF-Enhanced encoding of channel c (statistics updated; see aimet_tq_get_encoding)
 void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
+// mse_search.hip: d.enc[c] <- MSE encoding of channel c (statistics updated)
+size_t mse_part_bytes(int64_t C);
+void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
 // the same for n quantizers in one launch; host_out <- their encodings concatenated
 // (sum of Cs). Synchronises s.
 void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,

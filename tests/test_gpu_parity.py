@@ -214,11 +214,14 @@ def test_per_channel_stats_vs_per_channel_oracle(scheme, shape, axis):
             assert encs[c].to_tuple() == orcs[c].compute(8, *fl).as_tuple(), (c, fl)
 
 
-def test_tfe_device_search_many_channels():
-    """Device TF-Enhanced search (tfe_search.hip, one workgroup per channel) == the oracle's
-    host search for 600 channels of varied shape, every flag set and bit-width."""
+@pytest.mark.parametrize("scheme,C,bws", [(QuantizationMode.QUANTIZATION_TF_ENHANCED, 600, (4, 8, 16)),
+                                          (QuantizationMode.QUANTIZATION_MSE, 160, (8, 4))])
+def test_device_search_many_channels(scheme, C, bws):
+    """Device encoding searches (tfe_search.hip: one workgroup per channel; mse_search.hip:
+    channel x candidate-slice grid) == the oracle's host searches, for channels of varied shape,
+    every flag set and several bit-widths."""
     rng = np.random.default_rng(21)
-    C, K = 600, 96
+    K = 96
     scale = rng.uniform(1e-3, 30, (C, 1))
     shift = rng.uniform(-3, 3, (C, 1))
     x = rng.standard_t(3, (C, K)) * scale + shift * scale
@@ -229,19 +232,32 @@ def test_tfe_device_search_many_channels():
     x[13, :3] = 7.0                                 # nearly empty PDF
     x[13, 3:] = 0.0
     x = x.astype(np.float32)
-    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=C)
+    q = AimetTensorQuantizer(scheme, num_channels=C)
     q.updateStatsPerChannel(gpu(x), 0, True)
     orcs = []
     for c in range(C):
-        o = O.Analyzer(O.QUANTIZATION_TF_ENHANCED)
+        o = O.Analyzer(int(scheme))
         o.update(x[c])
         orcs.append(o)
-    for bw in (4, 8, 16):
+    for bw in bws:
         for fl in FLAGS:
             encs, valid = q.getEncoding(bw, *fl)
             assert valid
             for c in range(C):
                 assert encs[c].to_tuple() == orcs[c].compute(bw, *fl).as_tuple(), (c, bw, fl)
+
+
+def test_mse_device_search_per_tensor_large():
+    """Per-tensor MSE (all 128 candidate slices of one channel) on a dense 16M-element histogram
+    == the oracle."""
+    g = torch.Generator(device=DEV).manual_seed(9)
+    x = torch.randn(1 << 24, device=DEV, generator=g) * 2 + 0.5
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_MSE)
+    q.updateStats(x, True)
+    o = O.Analyzer(O.QUANTIZATION_MSE)
+    o.update(host(x))
+    for fl in FLAGS:
+        assert q.getEncoding(8, *fl)[0].to_tuple() == o.compute(8, *fl).as_tuple(), fl
 
 
 def test_get_encodings_batched_equals_individual():
