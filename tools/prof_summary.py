@@ -67,6 +67,22 @@ def main():
         fb, wb = sum(f) * 1024 * 2, sum(w) * 1024
         print("per-tensor QDQ HBM traffic/step: fetch %.4f GB (FETCH_SIZE x2), write %.4f GB, total %.4f GB"
               % (fb / 1e9, wb / 1e9, (fb + wb) / 1e9))
+        # calibration kernels: every dispatch before the first QDQ one (one compute_encodings)
+        fa, wa = pmc(args[1], "FETCH_SIZE"), pmc(args[2], "WRITE_SIZE")
+        cut_f = next(i for i, (n, _) in enumerate(fa) if QDQ in n)
+        cut_w = next(i for i, (n, _) in enumerate(wa) if QDQ in n)
+        cf, cw = collections.defaultdict(float), collections.defaultdict(float)
+        for n, v in fa[:cut_f]:
+            if "aimet_amd" in n:
+                cf[n.replace("(anonymous namespace)::", "").replace("aimet_amd::", "").replace("void ", "")
+                   .split("(")[0]] += v * 1024 * 2
+        for n, v in wa[:cut_w]:
+            if "aimet_amd" in n:
+                cw[n.replace("(anonymous namespace)::", "").replace("aimet_amd::", "").replace("void ", "")
+                   .split("(")[0]] += v * 1024
+        print("compute_encodings HBM traffic per kernel (FETCH_SIZE x2 + WRITE_SIZE):")
+        for k in sorted(cf, key=lambda k: -cf[k]):
+            print("  %-62s fetch %.4f GB  write %.4f GB" % (k, cf[k] / 1e9, cw.get(k, 0) / 1e9))
 
 
 if __name__ == "__main__":
