@@ -18,6 +18,7 @@ namespace
 constexpr float kGamma = -0.1f;
 // python: (ZETA - GAMMA) = 1.2000000000000002 -> float32 scalar 1.2f in the torch op
 constexpr float kZmG = (float) (1.1 - (-0.1));
+constexpr int kAdaBwdGrid = 8192;   // 32 workgroups per CU; bounds the round-loss atomics
 
 struct AdaChannel
 {
@@ -32,33 +33,99 @@ struct AdaChannel
     }
 };
 
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// sigmoid with the hardware exp2 (v_exp_f32, ~1 ulp) and an IEEE reciprocal: within 2 ulp of
+// torch's 1/(1+expf(-a)); h enters Wq additively inside floor/clamp, so Wq stays within the
+// tests' 1e-6 absolute tolerance, and dL/dalpha within 1e-5 relative.
 __device__ __forceinline__ float sigmoidf(float a)
 {
-    return 1.0f / (1.0f + expf(-a));
+    return 1.0f / (1.0f + __expf(-a));
+}
+
+// |x|^beta for x in [0, 1] (the rounding-loss power): exp2(beta * log2 x) on the hardware
+// transcendental unit; the reference's (torch) powf differs by a few ulp
+__device__ __forceinline__ float pow01(float ax, float beta)
+{
+    return ax > 0.0f ? exp2f(beta * __log2f(ax)) : (beta == 0.0f ? 1.0f : 0.0f);
+}
+
+struct AdaParams
+{
+    float qmax, reg, beta;
+    int soft;
+};
+
+__device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, const AdaParams& p)
+{
+    float t = __builtin_floorf(w / d);   // IEEE division: floor() is sensitive to the last ulp
+    float h;
+    if (p.soft)
+    {
+        float pre = sigmoidf(a) * kZmG + kGamma;
+        h         = fminf(fmaxf(pre, 0.0f), 1.0f);
+    }
+    else
+        h = a >= 0.0f ? 1.0f : 0.0f;
+    float q = fminf(fmaxf(t + h - o, 0.0f), p.qmax);
+    return (q + o) * d;
+}
+
+// dL/dalpha of Wq (clamp pass-through masks as torch autograd) + the rounding-loss gradient
+__device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, float o, const AdaParams& p, float& loss)
+{
+    float t   = __builtin_floorf(w / d);
+    float sg  = sigmoidf(a);
+    float pre = sg * kZmG + kGamma;
+    float h   = fminf(fmaxf(pre, 0.0f), 1.0f);
+    float u   = t + h - o;
+    // d wq / d h = delta inside the clamp window (torch clamp_backward: min <= x <= max)
+    float gh = (u >= 0.0f && u <= p.qmax) ? g * d : 0.0f;
+    if (p.reg != 0.0f)
+    {
+        float x  = 2.0f * h - 1.0f;
+        float ax = fabsf(x);
+        float pw = pow01(ax, p.beta);
+        loss += 1.0f - pw;
+        // d/dh [reg * (1 - |2h-1|^beta)] = -reg * beta * |x|^(beta-1) * sign(x) * 2
+        float dp = (ax > 0.0f) ? p.beta * (pw / ax) * (x > 0.0f ? 1.0f : -1.0f) : 0.0f;
+        gh += -p.reg * dp * 2.0f;
+    }
+    // h = clamp(pre, 0, 1); pre = sigmoid(a) * (zeta - gamma) + gamma
+    float gpre = (pre >= 0.0f && pre <= 1.0f) ? gh : 0.0f;
+    return gpre * kZmG * (1.0f - sg) * sg;
+}
+
+// 16-B streaming form: four consecutive elements share a channel (K % 4 == 0 or C == 1);
+// one quad per lane, one tile per workgroup (the QDQ kernels' measured-best shape)
+__global__ __launch_bounds__(kBlock) void adaround_fwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
+                                                                  f4* __restrict__ wq, uint32_t nq, AdaChannel map,
+                                                                  const float* __restrict__ delta,
+                                                                  const float* __restrict__ offset, AdaParams p)
+{
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nq)
+        return;
+    const uint32_t c = map.channel(4 * i);
+    const float d = delta[c], o = offset[c];
+    f4 wv = __builtin_nontemporal_load(w + i), av = __builtin_nontemporal_load(alpha + i), r;
+    r.x = ada_fwd(wv.x, av.x, d, o, p);
+    r.y = ada_fwd(wv.y, av.y, d, o, p);
+    r.z = ada_fwd(wv.z, av.z, d, o, p);
+    r.w = ada_fwd(wv.w, av.w, d, o, p);
+    __builtin_nontemporal_store(r, wq + i);
 }
 
 __global__ __launch_bounds__(kBlock) void adaround_fwd_kernel(const float* __restrict__ w,
                                                               const float* __restrict__ alpha, float* __restrict__ wq,
                                                               uint32_t n, AdaChannel map,
                                                               const float* __restrict__ delta,
-                                                              const float* __restrict__ offset, float qmax, int soft)
+                                                              const float* __restrict__ offset, AdaParams p)
 {
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
     {
         uint32_t c = map.channel(i);
-        float d = delta[c], o = offset[c];
-        float t = __builtin_floorf(w[i] / d);
-        float a = alpha[i];
-        float h;
-        if (soft)
-        {
-            float pre = sigmoidf(a) * kZmG + kGamma;
-            h         = fminf(fmaxf(pre, 0.0f), 1.0f);
-        }
-        else
-            h = a >= 0.0f ? 1.0f : 0.0f;
-        float q = fminf(fmaxf(t + h - o, 0.0f), qmax);
-        wq[i]   = (q + o) * d;
+        wq[i]      = ada_fwd(w[i], alpha[i], delta[c], offset[c], p);
     }
 }
 
@@ -79,47 +146,60 @@ __device__ __forceinline__ float block_sum(float v)
     return r;
 }
 
+// backward: grid-stride over quads (bounded grid: one round-loss atomic per workgroup)
+__global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
+                                                                  const f4* __restrict__ g, f4* __restrict__ ga,
+                                                                  uint32_t nq, AdaChannel map,
+                                                                  const float* __restrict__ delta,
+                                                                  const float* __restrict__ offset, AdaParams p,
+                                                                  float* __restrict__ round_loss)
+{
+    float loss = 0.0f;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nq; i += gridDim.x * kBlock)
+    {
+        const uint32_t c = map.channel(4 * i);
+        const float d = delta[c], o = offset[c];
+        f4 wv = __builtin_nontemporal_load(w + i), av = __builtin_nontemporal_load(alpha + i);
+        f4 gv = __builtin_nontemporal_load(g + i), r;
+        r.x = ada_bwd(wv.x, av.x, gv.x, d, o, p, loss);
+        r.y = ada_bwd(wv.y, av.y, gv.y, d, o, p, loss);
+        r.z = ada_bwd(wv.z, av.z, gv.z, d, o, p, loss);
+        r.w = ada_bwd(wv.w, av.w, gv.w, d, o, p, loss);
+        __builtin_nontemporal_store(r, ga + i);
+    }
+    if (p.reg != 0.0f && round_loss)
+    {
+        float s = block_sum(loss);
+        if (threadIdx.x == 0)
+            atomicAdd(round_loss, p.reg * s);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __restrict__ w,
                                                               const float* __restrict__ alpha,
                                                               const float* __restrict__ g, float* __restrict__ ga,
                                                               uint32_t n, AdaChannel map,
                                                               const float* __restrict__ delta,
-                                                              const float* __restrict__ offset, float qmax, float reg,
-                                                              float beta, float* __restrict__ round_loss)
+                                                              const float* __restrict__ offset, AdaParams p,
+                                                              float* __restrict__ round_loss)
 {
     float loss = 0.0f;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
     {
         uint32_t c = map.channel(i);
-        float d = delta[c], o = offset[c];
-        float t   = __builtin_floorf(w[i] / d);
-        float a   = alpha[i];
-        float sg  = sigmoidf(a);
-        float pre = sg * kZmG + kGamma;
-        float h   = fminf(fmaxf(pre, 0.0f), 1.0f);
-        float u   = t + h - o;
-        // d wq / d h = delta inside the clamp window (torch clamp_backward: min <= x <= max)
-        float gh = (u >= 0.0f && u <= qmax) ? g[i] * d : 0.0f;
-        if (reg != 0.0f)
-        {
-            float x  = 2.0f * h - 1.0f;
-            float ax = fabsf(x);
-            float p  = powf(ax, beta);
-            loss += 1.0f - p;
-            // d/dh [reg * (1 - |2h-1|^beta)] = -reg * beta * |x|^(beta-1) * sign(x) * 2
-            float dp = (ax > 0.0f) ? beta * powf(ax, beta - 1.0f) * (x > 0.0f ? 1.0f : -1.0f) : 0.0f;
-            gh += -reg * dp * 2.0f;
-        }
-        // h = clamp(pre, 0, 1); pre = sigmoid(a) * (zeta - gamma) + gamma
-        float gpre = (pre >= 0.0f && pre <= 1.0f) ? gh : 0.0f;
-        ga[i]      = gpre * kZmG * (1.0f - sg) * sg;
+        ga[i]      = ada_bwd(w[i], alpha[i], g[i], delta[c], offset[c], p, loss);
     }
-    if (reg != 0.0f && round_loss)
+    if (p.reg != 0.0f && round_loss)
     {
         float s = block_sum(loss);
         if (threadIdx.x == 0)
-            atomicAdd(round_loss, reg * s);
+            atomicAdd(round_loss, p.reg * s);
     }
+}
+
+bool aligned16(const void* p)
+{
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0;
 }
 
 }   // namespace
@@ -144,9 +224,17 @@ int aimet_adaround_forward(const float* w, const float* alpha, float* wq, int64_
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        float qmax = (float) ((1ull << bw) - 1);
-        adaround_fwd_kernel<<<stream_blocks(n, kBlock), kBlock, 0, as_stream(stream)>>>(
-            w, alpha, wq, (uint32_t) n, map, delta, offset, qmax, soft);
+        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, soft};
+        if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(wq))
+        {
+            uint32_t nq = (uint32_t) (n / 4);
+            adaround_fwd_vec_kernel<<<ceil_div(nq, kBlock), kBlock, 0, as_stream(stream)>>>(
+                reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<f4*>(wq), nq,
+                map, delta, offset, p);
+        }
+        else
+            adaround_fwd_kernel<<<stream_blocks(n, kBlock), kBlock, 0, as_stream(stream)>>>(
+                w, alpha, wq, (uint32_t) n, map, delta, offset, p);
         AIMET_LAUNCH_CHECK();
     });
 }
@@ -168,9 +256,20 @@ int aimet_adaround_backward(const float* w, const float* alpha, const float* g, 
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        float qmax = (float) ((1ull << bw) - 1);
-        adaround_bwd_kernel<<<stream_blocks(n, kBlock), kBlock, 0, as_stream(stream)>>>(
-            w, alpha, g, ga, (uint32_t) n, map, delta, offset, qmax, reg, beta, round_loss);
+        AdaParams p {(float) ((1ull << bw) - 1), reg, beta, 1};
+        if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(g) &&
+            aligned16(ga))
+        {
+            uint32_t nq = (uint32_t) (n / 4);
+            int64_t blocks = ceil_div(nq, kBlock);
+            adaround_bwd_vec_kernel<<<(unsigned) (blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid), kBlock, 0,
+                                      as_stream(stream)>>>(
+                reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),
+                reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss);
+        }
+        else
+            adaround_bwd_kernel<<<stream_blocks(n, kBlock), kBlock, 0, as_stream(stream)>>>(
+                w, alpha, g, ga, (uint32_t) n, map, delta, offset, p, round_loss);
         AIMET_LAUNCH_CHECK();
     });
 }

@@ -390,6 +390,36 @@ def test_adaround_forward_backward_vs_torch(kat):
     assert abs(float(loss) - k["expected"]) < 1e-4
 
 
+@pytest.mark.parametrize("beta", [2.0, 7.5, 20.0])
+@pytest.mark.parametrize("shape", [(64, 32, 3, 3), (48, 3, 3, 3)])   # 16-B path / scalar path
+def test_adaround_backward_with_round_loss_vs_torch(beta, shape):
+    """Fused backward with the rounding loss (reg != 0): dL/dalpha and the loss itself vs torch
+    autograd of the reference formulas (adaround_wrapper.py:124-149 + adaround_loss.py:97-110).
+    Tolerances: loss rtol 1e-4 (fp32 sum order), gradient rtol 1e-4 / atol 1e-7 (hardware
+    exp2/log2 in the kernel vs libm in torch)."""
+    from aimet_amd.adaround import AdaroundFunction
+    from oracle import torch_ref as T
+    torch.manual_seed(1)
+    C = shape[0]
+    w = torch.randn(*shape, device=DEV) * 0.1
+    delta = (torch.rand(C, device=DEV) * 0.01 + 0.001).view(C, 1, 1, 1)
+    offset = torch.full((C, 1, 1, 1), -128.0, device=DEV)
+    alpha = torch.randn_like(w) * 2
+    g = torch.randn_like(w)
+    reg = 0.01
+    a_ref = alpha.clone().requires_grad_(True)
+    wq_ref = T.adaround_forward(w, a_ref, delta, offset, 8)
+    loss_ref = T.adaround_round_loss(a_ref, reg, beta)
+    ((wq_ref * g).sum() + loss_ref).backward()
+    a = alpha.clone().requires_grad_(True)
+    loss = torch.zeros(1, device=DEV)
+    wq = AdaroundFunction.apply(w, a, delta.view(-1), offset.view(-1), 8, 0, True, reg, beta, loss)
+    (wq * g).sum().backward()
+    torch.testing.assert_close(wq, wq_ref.detach(), rtol=0, atol=1e-6)
+    torch.testing.assert_close(a.grad, a_ref.grad, rtol=1e-4, atol=1e-7)
+    assert abs(float(loss) - float(loss_ref)) <= 1e-4 * abs(float(loss_ref))
+
+
 def test_channel_plan_equals_individual_launches():
     """All parameter QDQs in one launch == one launch per tensor (incl. K % 4 != 0, axis 1)."""
     from aimet_amd.tensor_quantizer import ChannelQdqPlan, per_channel_view, qdq_per_channel_table
