@@ -200,6 +200,58 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
     }
 }
 
+// per-channel, 16-B form (K % 4 == 0, aligned): a (channel, slice) grid; with one slice the sums
+// are stored (deterministic), with several (few channels: fill the chip) they are added atomically
+// into the zeroed sums.
+__global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __restrict__ x, const f4* __restrict__ g,
+                                                                    f4* __restrict__ gx, int64_t outer, int64_t C,
+                                                                    int64_t K4, FastDiv divK4,
+                                                                    const float* __restrict__ delta,
+                                                                    const float* __restrict__ offset, float steps,
+                                                                    float* __restrict__ sums)
+{
+    const int splits = gridDim.y;
+    const int64_t Q  = outer * K4;
+    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+    {
+        const float dl = delta[c], o = offset[c];
+        Sums s {0, 0, 0};
+        for (int64_t j = (int64_t) blockIdx.y * kBlock + threadIdx.x; j < Q; j += (int64_t) splits * kBlock)
+        {
+            const int64_t r = outer == 1 ? 0 : divK4.div((uint32_t) j);
+            const int64_t i = (r * C + c) * K4 + (j - r * K4);
+            f4 a = __builtin_nontemporal_load(x + i);
+            f4 b = __builtin_nontemporal_load(g + i);
+            float r0, r1, r2, r3;
+            lg_bwd_elem(a.x, b.x, dl, o, steps, r0, s);
+            lg_bwd_elem(a.y, b.y, dl, o, steps, r1, s);
+            lg_bwd_elem(a.z, b.z, dl, o, steps, r2, s);
+            lg_bwd_elem(a.w, b.w, dl, o, steps, r3, s);
+            if (gx)
+            {
+                f4 rv = {r0, r1, r2, r3};
+                __builtin_nontemporal_store(rv, gx + i);
+            }
+        }
+        Sums t = block_reduce(s);
+        if (threadIdx.x == 0)
+        {
+            if (splits == 1)
+            {
+                sums[3 * c + 0] = t.a;
+                sums[3 * c + 1] = t.b;
+                sums[3 * c + 2] = t.d;
+            }
+            else
+            {
+                atomicAdd(&sums[3 * c + 0], t.a);
+                atomicAdd(&sums[3 * c + 1], t.b);
+                atomicAdd(&sums[3 * c + 2], t.d);
+            }
+        }
+    }
+}
+
 }   // namespace
 }   // namespace aimet_amd
 
@@ -253,6 +305,21 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
                          reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
             lg_bwd_tensor_kernel<<<stream_blocks(n, (int64_t) kBlock * 16), kBlock, 0, s>>>(
                 x, grad, grad_x, n, delta, offset, num_steps, sums, vec ? 1 : 0);
+        }
+        else if (K % 4 == 0 && outer * (K / 4) < (int64_t(1) << 32) &&
+                 ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
+                   reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0)
+        {
+            // >= 2048 workgroups in flight: slice channels when there are fewer than that
+            const int64_t K4  = K / 4;
+            int64_t splits    = C >= 2048 ? 1 : (2048 + C - 1) / C;
+            const int64_t per = ceil_div(outer * K4, kBlock);   // enough quads for every slice
+            if (splits > per)
+                splits = per > 0 ? per : 1;
+            dim3 grid((unsigned) (C < 65536 ? C : 65536), (unsigned) splits);
+            lg_bwd_channel_vec_kernel<<<grid, kBlock, 0, s>>>(
+                reinterpret_cast<const f4*>(x), reinterpret_cast<const f4*>(grad), reinterpret_cast<f4*>(grad_x),
+                outer, C, K4, FastDiv((uint32_t) (K4 > 0 ? K4 : 1)), delta, offset, num_steps, sums);
         }
         else
         {

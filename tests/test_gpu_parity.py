@@ -463,20 +463,24 @@ def test_learned_grid_vs_reference_golden(golden_dir, case):
     np.testing.assert_allclose(host(emax.grad), g["c%d_gmax" % i], rtol=1e-4, atol=1e-5)
 
 
-def test_learned_grid_large_vs_torch_ref():
-    """Llama-like weight (4096 x 4096, per-channel 4-bit symmetric): kernel vs torch restatement."""
+@pytest.mark.parametrize("shape,sym", [((4096, 4096), True), ((8, 1 << 20), False), ((96, 3, 7), True)])
+def test_learned_grid_large_vs_torch_ref(shape, sym):
+    """Llama-like weight (4096 x 4096, per-channel 4-bit symmetric; one workgroup per channel),
+    few long channels (channel x slice grid, atomic sums) and K % 4 != 0 (scalar path): kernel vs
+    the torch restatement. grad_x bit-exact; encoding gradients rtol 2e-4 (fp32 sum order)."""
     from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
     from oracle import torch_ref as T
     torch.manual_seed(2)
-    w = (torch.randn(4096, 4096, device=DEV) * 0.02).requires_grad_(True)
-    emax = (w.detach().abs().amax(dim=1) * 0.9).requires_grad_(True)
-    emin = (-emax.detach()).clone().requires_grad_(True)
+    w = (torch.randn(*shape, device=DEV) * 0.02).requires_grad_(True)
+    red = tuple(range(1, w.dim()))
+    emax = (w.detach().abs().amax(dim=red) * 0.9).requires_grad_(True)
+    emin = (-emax.detach() * (1.0 if sym else 0.7)).clone().requires_grad_(True)
     grad = torch.randn_like(w)
-    y = LearnedGridQuantizeDequantize.apply(w, emin, emax, 4, True, False, False, 0)
-    yr = T.lg_forward(w.detach(), emin.detach(), emax.detach(), 4, True)[0]
+    y = LearnedGridQuantizeDequantize.apply(w, emin, emax, 4, sym, False, False, 0)
+    yr = T.lg_forward(w.detach(), emin.detach(), emax.detach(), 4, sym)[0]
     assert torch.equal(y, yr)
     y.backward(grad)
-    gx, gmin, gmax = T.lg_gradients(w.detach(), grad, emin.detach(), emax.detach(), 4, True)
+    gx, gmin, gmax = T.lg_gradients(w.detach(), grad, emin.detach(), emax.detach(), 4, sym)
     assert torch.equal(w.grad, gx)
     torch.testing.assert_close(emax.grad, gmax, rtol=2e-4, atol=1e-4)
     torch.testing.assert_close(emin.grad, gmin, rtol=2e-4, atol=1e-4)
