@@ -66,6 +66,10 @@ _PROTOTYPES = {
     "aimet_qdq_channel_plan_destroy": [_vp],
     "aimet_ste_backward": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp],
     "aimet_ste_backward_per_tensor": [_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, _vp],
+    "aimet_qdq_per_tensor_16": [_vp, _vp, _i64, _int, _enc_p, _int, ctypes.c_uint64, _vp],
+    "aimet_qdq_per_channel_16": [_vp, _vp, _i64, _i64, _i64, _int, _vp, _int, ctypes.c_uint64, _vp],
+    "aimet_ste_backward_16": [_vp, _vp, _vp, _i64, _i64, _i64, _int, _vp, _vp, ctypes.c_float, ctypes.c_float,
+                              _vp],
     "aimet_tq_create": [_int, _i64, _int, ctypes.POINTER(_vp)],
     "aimet_tq_destroy": [_vp],
     "aimet_tq_reset_encoding_stats": [_vp, _vp],

@@ -18,7 +18,7 @@ import torch
 
 from aimet_amd import _native
 from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding
-from aimet_amd.tensor_quantizer import (AimetTensorQuantizer, _require_gpu, _stream, per_channel_view,
+from aimet_amd.tensor_quantizer import (IO_DTYPES, AimetTensorQuantizer, _require_gpu, _stream, per_channel_view,
                                         qdq_per_channel_table)
 
 
@@ -285,10 +285,14 @@ def compute_dloss_by_dx(x, grad, encoding_min, encoding_max, ch_axis=0):
     """quantsim_straight_through_grad.py:91-118 as one kernel: grad * (min <= x <= max).
 
     encoding_min/max: python floats (per-tensor) or sequences / float32 tensors of C values."""
-    _require_gpu(x, True, "x")
-    _require_gpu(grad, True, "grad")
+    _require_gpu(x, True, "x", allow_16bit=True)
+    _require_gpu(grad, True, "grad", allow_16bit=True)
     x = x.contiguous()
     grad = grad.contiguous()
+    if x.dtype in IO_DTYPES and grad.dtype == x.dtype:
+        return _ste_16(x, grad, encoding_min, encoding_max, ch_axis)
+    if x.dtype != torch.float32 or grad.dtype != torch.float32:
+        return compute_dloss_by_dx(x.float(), grad.float(), encoding_min, encoding_max, ch_axis).to(grad.dtype)
     out = torch.empty_like(grad)
     if isinstance(encoding_min, (int, float)) or (torch.is_tensor(encoding_min) and encoding_min.numel() == 1):
         mn = float(encoding_min)
@@ -306,6 +310,25 @@ def compute_dloss_by_dx(x, grad, encoding_min, encoding_max, ch_axis=0):
     with torch.cuda.device(x.device):
         _native.call("aimet_ste_backward", x.data_ptr(), grad.data_ptr(), out.data_ptr(), outer, C, K,
                      mins.data_ptr(), maxs.data_ptr(), _stream(x))
+    return out
+
+
+def _ste_16(x, grad, encoding_min, encoding_max, ch_axis):
+    """fp16 / bf16 STE in one pass (aimet_ste_backward_16): float(x) vs the float32 bounds."""
+    out = torch.empty_like(grad)
+    code = IO_DTYPES[x.dtype]
+    with torch.cuda.device(x.device):
+        if isinstance(encoding_min, (int, float)) or (torch.is_tensor(encoding_min) and encoding_min.numel() == 1):
+            _native.call("aimet_ste_backward_16", x.data_ptr(), grad.data_ptr(), out.data_ptr(), 1, 1, x.numel(), code,
+                         None, None, float(encoding_min), float(encoding_max), _stream(x))
+            return out
+        mins = torch.as_tensor(encoding_min, dtype=torch.float32).to(x.device).contiguous()
+        maxs = torch.as_tensor(encoding_max, dtype=torch.float32).to(x.device).contiguous()
+        outer, C, K = per_channel_view(x.shape, ch_axis)
+        if mins.numel() != C:
+            raise ValueError("expected %d per-channel bounds, got %d" % (C, mins.numel()))
+        _native.call("aimet_ste_backward_16", x.data_ptr(), grad.data_ptr(), out.data_ptr(), outer, C, K, code,
+                     mins.data_ptr(), maxs.data_ptr(), 0.0, 0.0, _stream(x))
     return out
 
 
@@ -338,7 +361,9 @@ class QuantizeDequantize(torch.autograd.Function):
                 return out
             raise NotImplementedError("fp8 quantization is outside the MI355X integer QDQ core")
         dtype = tensor.dtype
-        t = tensor.to(torch.float32)
+        # fp16 / bf16 go through the fused 16-bit I/O kernels (identical to the reference's
+        # upcast -> fp32 QDQ -> downcast, v1/tensor_quantizer.py:1116-1168); others upcast
+        t = tensor if dtype in IO_DTYPES else tensor.to(torch.float32)
         if isinstance(tq, StaticGridPerChannelQuantizer):
             t = t.contiguous()
             outer, C, K = per_channel_view(t.shape, tq.channel_axis)
@@ -355,8 +380,10 @@ class QuantizeDequantize(torch.autograd.Function):
         if tq.enabled and tq.data_type == QuantizationDataType.int and tq.bitwidth != 32:
             (x,) = ctx.saved_tensors
             dtype = grad.dtype
-            xf = x.to(torch.float32)
-            gf = grad.to(torch.float32)
+            if x.dtype == dtype and dtype in IO_DTYPES:
+                xf, gf = x, grad          # fused 16-bit STE
+            else:
+                xf, gf = x.to(torch.float32), grad.to(torch.float32)
             if isinstance(tq, StaticGridPerChannelQuantizer):
                 mins, maxs = _ste_bounds(tq, x.device)
                 g = compute_dloss_by_dx(xf, gf, mins, maxs, tq.channel_axis)

@@ -26,12 +26,14 @@ def _stream(t: torch.Tensor) -> int:
     return torch.cuda.current_stream(t.device).cuda_stream
 
 
-def _require_gpu(t: torch.Tensor, use_cuda: bool = True, what: str = "input"):
+def _require_gpu(t: torch.Tensor, use_cuda: bool = True, what: str = "input", allow_16bit: bool = False):
     if not isinstance(t, torch.Tensor):
         raise TypeError("%s must be a torch.Tensor" % what)
     if not t.is_cuda or not use_cuda:
         raise RuntimeError("aimet_amd: %s must be a HIP (cuda) tensor with use_cuda=True; the MI355X core has no "
                            "CPU path" % what)
+    if allow_16bit and t.dtype in (torch.float16, torch.bfloat16):
+        return
     if t.dtype != torch.float32:
         raise TypeError("aimet_amd: %s must be float32 (got %s); upcast as the reference callers do "
                         "(v1/tensor_quantizer.py:1124)" % (what, t.dtype))
@@ -286,14 +288,18 @@ class AimetTensorQuantizer:
     # -- quantize-dequantize -----------------------------------------------------------------
     @staticmethod
     def quantize_dequantize_tensor(tensor, encoding, round_mode=RoundingMode.ROUND_NEAREST, out=None):
-        _require_gpu(tensor)
+        _require_gpu(tensor, allow_16bit=True)
         t = tensor.contiguous(memory_format=_suggest_memory_format(tensor))
         if out is None:
             out = torch.empty_like(t)
         seed = next(_seed_counter) if int(round_mode) == RoundingMode.ROUND_STOCHASTIC else 0
         with torch.cuda.device(t.device):
-            _native.call("aimet_qdq_per_tensor", t.data_ptr(), out.data_ptr(), t.numel(), encoding.to_c(),
-                         int(round_mode), seed, _stream(t))
+            if t.dtype in IO_DTYPES:   # fp16 / bf16 I/O fused (aimet_qdq_per_tensor_16)
+                _native.call("aimet_qdq_per_tensor_16", t.data_ptr(), out.data_ptr(), t.numel(), IO_DTYPES[t.dtype],
+                             encoding.to_c(), int(round_mode), seed, _stream(t))
+            else:
+                _native.call("aimet_qdq_per_tensor", t.data_ptr(), out.data_ptr(), t.numel(), encoding.to_c(),
+                             int(round_mode), seed, _stream(t))
         return out
 
     def quantizeDequantize(self, tensor, encoding, round_mode, use_cuda=True):
@@ -344,13 +350,22 @@ class AimetTensorQuantizer:
         return qdq_per_channel_table(t, table, N // (C * K), C, K, round_mode)
 
 
+IO_DTYPES = {torch.float16: 1, torch.bfloat16: 2}   # aimet_*_16 io_dtype codes
+
+
 def qdq_per_channel_table(t, table, outer, C, K, round_mode=RoundingMode.ROUND_NEAREST, out=None):
+    """Per-channel QDQ of a contiguous fp32 / fp16 / bf16 tensor (16-bit I/O fused, see
+    aimet_qdq_per_channel_16), output in the input dtype."""
     if out is None:
         out = torch.empty_like(t)
     seed = next(_seed_counter) if int(round_mode) == RoundingMode.ROUND_STOCHASTIC else 0
     with torch.cuda.device(t.device):
-        _native.call("aimet_qdq_per_channel", t.data_ptr(), out.data_ptr(), outer, C, K, table.data_ptr(),
-                     int(round_mode), seed, _stream(t))
+        if t.dtype in IO_DTYPES:
+            _native.call("aimet_qdq_per_channel_16", t.data_ptr(), out.data_ptr(), outer, C, K, IO_DTYPES[t.dtype],
+                         table.data_ptr(), int(round_mode), seed, _stream(t))
+        else:
+            _native.call("aimet_qdq_per_channel", t.data_ptr(), out.data_ptr(), outer, C, K, table.data_ptr(),
+                         int(round_mode), seed, _stream(t))
     return out
 
 

@@ -143,6 +143,20 @@ int aimet_ste_backward(const float* x, const float* grad, float* grad_in, int64_
 int aimet_ste_backward_per_tensor(const float* x, const float* grad, float* grad_in, int64_t n, float enc_min,
                                   float enc_max, void* stream);
 
+/* fp16 / bf16 I/O (io_dtype 1 = float16, 2 = bfloat16): the reference upcasts to fp32, runs the fp32
+ * kernel and casts back (v1/tensor_quantizer.py:1116-1168, `.to(torch.float32)` ... `.to(dtype)`);
+ * these fuse the casts (2 B in + 2 B out per element) with results identical to that sequence
+ * (round-to-nearest-even downcast as torch). */
+int aimet_qdq_per_tensor_16(const void* in, void* out, int64_t n, int io_dtype, const aimet_tf_encoding* enc,
+                            int round_mode, uint64_t seed, void* stream);
+int aimet_qdq_per_channel_16(const void* in, void* out, int64_t outer, int64_t C, int64_t K, int io_dtype,
+                             const float* table_dev, int round_mode, uint64_t seed, void* stream);
+/* grad_in = grad * (min <= float(x) <= max) in the grad dtype (x, grad, grad_in share io_dtype);
+ * per-channel bounds mins_dev/maxs_dev[C], or per-tensor enc_min/enc_max when mins_dev is NULL. */
+int aimet_ste_backward_16(const void* x, const void* grad, void* grad_in, int64_t outer, int64_t C, int64_t K,
+                          int io_dtype, const float* mins_dev, const float* maxs_dev, float enc_min, float enc_max,
+                          void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Tensor quantizer: device-resident encoding statistics (AimetTensorQuantizer / TensorQuantizer) */
 /* ------------------------------------------------------------------------------------------ */

@@ -484,3 +484,82 @@ def test_learned_grid_large_vs_torch_ref(shape, sym):
     assert torch.equal(w.grad, gx)
     torch.testing.assert_close(emax.grad, gmax, rtol=2e-4, atol=1e-4)
     torch.testing.assert_close(emin.grad, gmin, rtol=2e-4, atol=1e-4)
+
+
+# ------------------------------------------------------------------------------------------
+# fp16 / bf16 I/O (fused casts) == the reference's upcast -> fp32 kernel -> downcast
+# ------------------------------------------------------------------------------------------
+def _bits16(t):
+    return t.view(torch.int16).cpu().numpy()
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+@pytest.mark.parametrize("rm", [0, 1])
+def test_16bit_io_qdq_equals_upcast_path(dtype, rm):
+    from aimet_amd import _native
+    from aimet_amd.tensor_quantizer import IO_DTYPES
+    g = torch.Generator(device=DEV).manual_seed(4)
+    code = IO_DTYPES[dtype]
+    stream = torch.cuda.current_stream().cuda_stream
+    for n, off in ((1 << 20, 0), (100003, 1), (7, 0)):
+        x = (torch.randn(n + off, device=DEV, generator=g) * 3).to(dtype)[off:]
+        if n > 16:
+            x[:6] = torch.tensor([float("nan"), float("inf"), -float("inf"), 0.0, -0.0, 1e-7], dtype=dtype)
+        enc = enc_of(-2.5, 4.0, 8)
+        out16 = torch.empty_like(x)
+        _native.call("aimet_qdq_per_tensor_16", x.data_ptr(), out16.data_ptr(), n, code, enc.to_c(), rm, 77, stream)
+        xf = x.float()
+        out32 = torch.empty_like(xf)
+        _native.call("aimet_qdq_per_tensor", xf.data_ptr(), out32.data_ptr(), n, enc.to_c(), rm, 77, stream)
+        np.testing.assert_array_equal(_bits16(out16), _bits16(out32.to(dtype)))
+    # per-channel: K % 8 == 0 (16-B path) and K % 8 != 0 (scalar path), axis 0 and 1
+    for shape, axis in (((64, 16, 3, 3), 0), ((40, 24), 0), ((6, 10, 5), 1)):
+        x = (torch.randn(*shape, device=DEV, generator=g) * 0.5).to(dtype)
+        C = shape[axis]
+        encs = [enc_of(-1.0 - 0.1 * c, 0.8 + 0.05 * c, 8) for c in range(C)]
+        q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF, num_channels=C)
+        table = q.channelTable(encs, torch.device(DEV))
+        from aimet_amd.tensor_quantizer import per_channel_view
+        outer, C, K = per_channel_view(x.shape, axis)
+        out16 = torch.empty_like(x)
+        _native.call("aimet_qdq_per_channel_16", x.data_ptr(), out16.data_ptr(), outer, C, K, code, table.data_ptr(),
+                     rm, 5, stream)
+        xf = x.float()
+        out32 = torch.empty_like(xf)
+        _native.call("aimet_qdq_per_channel", xf.data_ptr(), out32.data_ptr(), outer, C, K, table.data_ptr(), rm, 5,
+                     stream)
+        np.testing.assert_array_equal(_bits16(out16), _bits16(out32.to(dtype)), err_msg=str(shape))
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_16bit_io_ste_and_autograd(dtype):
+    from aimet_amd.quantizers import (QuantScheme, StaticGridPerChannelQuantizer, StaticGridPerTensorQuantizer,
+                                      compute_dloss_by_dx)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    x = (torch.randn(1 << 16, device=DEV, generator=g) * 3).to(dtype)
+    gr = torch.randn(1 << 16, device=DEV, generator=g).to(dtype)
+    got = compute_dloss_by_dx(x, gr, -2.0, 2.5)
+    want = compute_dloss_by_dx(x.float(), gr.float(), -2.0, 2.5).to(dtype)
+    np.testing.assert_array_equal(_bits16(got), _bits16(want))
+    w = (torch.randn(32, 16, 3, 3, device=DEV, generator=g) * 0.1).to(dtype)
+    gw = torch.randn_like(w)
+    mins = [-0.1 - 0.01 * c for c in range(32)]
+    maxs = [0.12 + 0.01 * c for c in range(32)]
+    got = compute_dloss_by_dx(w, gw, mins, maxs, 0)
+    want = compute_dloss_by_dx(w.float(), gw.float(), mins, maxs, 0).to(dtype)
+    np.testing.assert_array_equal(_bits16(got), _bits16(want))
+    # through the quantizer's autograd function: forward / backward == the upcast path
+    for tq in (StaticGridPerTensorQuantizer(8, "nearest", QuantScheme.post_training_tf, False, True),
+               StaticGridPerChannelQuantizer(8, "nearest", QuantScheme.post_training_tf, True, 32, True)):
+        src = w if isinstance(tq, StaticGridPerChannelQuantizer) else w.flatten()
+        tq.update_encoding_stats(src.float())
+        tq.compute_encoding()
+        a = src.clone().requires_grad_(True)
+        y = tq.quantize_dequantize(a, "nearest")
+        assert y.dtype == dtype
+        y.backward(torch.ones_like(y))
+        b = src.float().clone().requires_grad_(True)
+        y32 = tq.quantize_dequantize(b, "nearest")
+        y32.backward(torch.ones_like(y32))
+        np.testing.assert_array_equal(_bits16(y.detach()), _bits16(y32.detach().to(dtype)))
+        np.testing.assert_array_equal(_bits16(a.grad), _bits16(b.grad.to(dtype)))
