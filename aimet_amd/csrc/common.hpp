@@ -162,6 +162,32 @@ __device__ __forceinline__ float quantize_nearest(float x, const QdqParams& p)
     return __builtin_roundf(o);
 }
 
+// round(RN(RN(a / d) - off)) (half away from zero) without the IEEE division in the common case.
+// q = RN(a * rcp) with rcp = RN(1/d) is within 3.0001 ulp(|a/d|) of RN(a/d), so v = RN(q - off)
+// and the reference's v* = RN(RN(a/d) - off) differ by at most 6u(|q| + |off|) (u = 2^-24). Their
+// roundings can only differ if a half-integer lies within that distance of v; when v is farther
+// than 2^-21 (|q| + |off| + 1) (>= 8u(...)) from every half-integer, round(v) == round(v*).
+// Otherwise -- and for every non-finite intermediate -- the exact IEEE division decides. The
+// result is therefore bit-identical to the division form (and to the reference).
+__device__ __forceinline__ float round_div_sub(float a, float d, float rcp, float off)
+{
+    const float q    = a * rcp;
+    const float v    = q - off;
+    const float h    = v - __builtin_floorf(v);             // exact fractional part, [0, 1)
+    const float dist = __builtin_fabsf(h - 0.5f);
+    const float thr  = (__builtin_fabsf(q) + __builtin_fabsf(off) + 1.0f) * 4.76837158203125e-7f;   // 2^-21
+    if (dist > thr)                                          // false for NaN / inf
+        return __builtin_roundf(v);
+    return __builtin_roundf(a / d - off);
+}
+
+// quantize_nearest with a per-thread reciprocal of delta (see round_div_sub): identical results
+__device__ __forceinline__ float quantize_nearest_rcp(float x, const QdqParams& p, float rcp)
+{
+    float o = glibc_fmaxf(glibc_fminf(x, p.max), p.min);
+    return round_div_sub(o, p.delta, rcp, p.offset);
+}
+
 // ROUND_STOCHASTIC: floor(v + U[0,1)). The reference draws rand() (CPU) or curand seeded by
 // clock() (GPU) -- neither reproducible, so only the distribution is specified.
 __device__ __forceinline__ float uniform01(uint64_t seed, uint64_t idx)

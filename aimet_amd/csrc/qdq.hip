@@ -25,9 +25,10 @@ enum class Op
 };
 
 template <Op OP, bool STOCHASTIC>
-__device__ __forceinline__ float apply(float x, const QdqParams& p, float shift, uint64_t seed, uint64_t idx)
+__device__ __forceinline__ float apply(float x, const QdqParams& p, float shift, uint64_t seed, uint64_t idx,
+                                       float rcp)
 {
-    float q = STOCHASTIC ? quantize_stochastic(x, p, seed, idx) : quantize_nearest(x, p);
+    float q = STOCHASTIC ? quantize_stochastic(x, p, seed, idx) : quantize_nearest_rcp(x, p, rcp);
     if constexpr (OP == Op::QDQ)
         return dequantize(q, p);
     else
@@ -60,11 +61,12 @@ __global__ __launch_bounds__(kBlock) void tensor_vec_kernel(const f4* __restrict
         return;
     f4 v = load_stream(in + i);
     uint64_t e = (uint64_t) i * 4;
+    const float rcp = 1.0f / p.delta;
     f4 r;
-    r.x = apply<OP, STOCHASTIC>(v.x, p, shift, seed, e + 0);
-    r.y = apply<OP, STOCHASTIC>(v.y, p, shift, seed, e + 1);
-    r.z = apply<OP, STOCHASTIC>(v.z, p, shift, seed, e + 2);
-    r.w = apply<OP, STOCHASTIC>(v.w, p, shift, seed, e + 3);
+    r.x = apply<OP, STOCHASTIC>(v.x, p, shift, seed, e + 0, rcp);
+    r.y = apply<OP, STOCHASTIC>(v.y, p, shift, seed, e + 1, rcp);
+    r.z = apply<OP, STOCHASTIC>(v.z, p, shift, seed, e + 2, rcp);
+    r.w = apply<OP, STOCHASTIC>(v.w, p, shift, seed, e + 3, rcp);
     store_stream(r, out + i);
 }
 
@@ -74,8 +76,9 @@ __global__ __launch_bounds__(kBlock) void tensor_scalar_kernel(const float* __re
                                                                uint64_t seed)
 {
     const int64_t stride = (int64_t) gridDim.x * kBlock;
+    const float rcp      = 1.0f / p.delta;
     for (int64_t i = begin + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-        out[i] = apply<OP, STOCHASTIC>(in[i], p, shift, seed, (uint64_t) i);
+        out[i] = apply<OP, STOCHASTIC>(in[i], p, shift, seed, (uint64_t) i, rcp);
 }
 
 template <Op OP, bool STOCHASTIC>
@@ -135,11 +138,12 @@ __global__ __launch_bounds__(kBlock) void channel_vec_kernel(const f4* __restric
     f4 v        = load_stream(in + i);
     QdqParams p = load_params(table, map.C, map.channel(i * 4));
     uint64_t e  = (uint64_t) i * 4;
+    const float rcp = 1.0f / p.delta;
     f4 r;
-    r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0);
-    r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1);
-    r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2);
-    r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3);
+    r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0, rcp);
+    r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1, rcp);
+    r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2, rcp);
+    r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3, rcp);
     store_stream(r, out + i);
 }
 
@@ -151,8 +155,9 @@ __global__ __launch_bounds__(kBlock) void channel_scalar_kernel(const float* __r
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
     {
-        QdqParams p = load_params(table, map.C, map.channel(i));
-        out[i]      = apply<Op::QDQ, STOCHASTIC>(in[i], p, 0.f, seed, i);
+        QdqParams p     = load_params(table, map.C, map.channel(i));
+        const float rcp = 1.0f / p.delta;
+        out[i]          = apply<Op::QDQ, STOCHASTIC>(in[i], p, 0.f, seed, i, rcp);
     }
 }
 
@@ -167,8 +172,9 @@ __global__ __launch_bounds__(kBlock) void channel_scalar64_kernel(const float* _
     for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
     {
         uint32_t c  = (uint32_t) ((i / K) % C);
-        QdqParams p = load_params(table, (uint32_t) C, c);
-        out[i]      = apply<Op::QDQ, STOCHASTIC>(in[i], p, 0.f, seed, (uint64_t) i);
+        QdqParams p     = load_params(table, (uint32_t) C, c);
+        const float rcp = 1.0f / p.delta;
+        out[i]          = apply<Op::QDQ, STOCHASTIC>(in[i], p, 0.f, seed, (uint64_t) i, rcp);
     }
 }
 
@@ -271,19 +277,21 @@ __global__ __launch_bounds__(kBlock) void channel_batch_kernel(const BatchDesc* 
         f4 v        = load_stream(reinterpret_cast<const f4*>(d.in) + t);
         QdqParams p = load_params(d.table, d.map.C, d.map.channel(t * 4));
         uint64_t e  = ((uint64_t) lo << 40) + (uint64_t) t * 4;
+        const float rcp = 1.0f / p.delta;
         f4 r;
-        r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0);
-        r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1);
-        r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2);
-        r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3);
+        r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0, rcp);
+        r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1, rcp);
+        r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2, rcp);
+        r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3, rcp);
         store_stream(r, reinterpret_cast<f4*>(d.out) + t);
     }
     else
     {
         if (t >= d.n)
             return;
-        QdqParams p = load_params(d.table, d.map.C, d.map.channel(t));
-        d.out[t]    = apply<Op::QDQ, STOCHASTIC>(d.in[t], p, 0.f, seed, ((uint64_t) lo << 40) + t);
+        QdqParams p     = load_params(d.table, d.map.C, d.map.channel(t));
+        const float rcp = 1.0f / p.delta;
+        d.out[t]        = apply<Op::QDQ, STOCHASTIC>(d.in[t], p, 0.f, seed, ((uint64_t) lo << 40) + t, rcp);
     }
 }
 

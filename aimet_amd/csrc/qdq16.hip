@@ -52,9 +52,9 @@ __device__ __forceinline__ unsigned short from_f32(float f)
 }
 
 template <bool STOCHASTIC>
-__device__ __forceinline__ float qdq(float x, const QdqParams& p, uint64_t seed, uint64_t idx)
+__device__ __forceinline__ float qdq(float x, const QdqParams& p, uint64_t seed, uint64_t idx, float rcp)
 {
-    float q = STOCHASTIC ? quantize_stochastic(x, p, seed, idx) : quantize_nearest(x, p);
+    float q = STOCHASTIC ? quantize_stochastic(x, p, seed, idx) : quantize_nearest_rcp(x, p, rcp);
     return dequantize(q, p);
 }
 
@@ -88,9 +88,10 @@ __global__ __launch_bounds__(kBlock) void qdq16_vec_kernel(const u16x8* __restri
         p = table_params(table, map.C, map.channel((uint32_t) (i * 8)));
     u16x8 v = __builtin_nontemporal_load(in + i), r;
     const uint64_t e = (uint64_t) i * 8;
+    const float rcp  = 1.0f / p.delta;
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-        r[k] = from_f32<IO>(qdq<STOCHASTIC>(to_f32<IO>(v[k]), p, seed, e + k));
+        r[k] = from_f32<IO>(qdq<STOCHASTIC>(to_f32<IO>(v[k]), p, seed, e + k, rcp));
     __builtin_nontemporal_store(r, out + i);
 }
 
@@ -106,7 +107,7 @@ __global__ __launch_bounds__(kBlock) void qdq16_scalar_kernel(const unsigned sho
         QdqParams q = p;
         if constexpr (CH)
             q = table_params(table, (uint32_t) C, (uint32_t) ((i / K) % C));
-        out[i] = from_f32<IO>(qdq<STOCHASTIC>(to_f32<IO>(in[i]), q, seed, (uint64_t) i));
+        out[i] = from_f32<IO>(qdq<STOCHASTIC>(to_f32<IO>(in[i]), q, seed, (uint64_t) i, 1.0f / q.delta));
     }
 }
 

@@ -243,10 +243,12 @@ __global__ __launch_bounds__(kBlock) void fold_minmax_kernel(TqDevice d, int64_t
 // out-of-range (and NaN) dropped.
 struct Binner
 {
-    float bucket, offset;
+    float bucket, offset, rcp;
+    __device__ Binner(float b, float o) : bucket(b), offset(o), rcp(1.0f / b) {}
     __device__ __forceinline__ int bin(float x) const
     {
-        float r = __builtin_roundf(x / bucket - offset);
+        // == roundf(x / bucket - offset) bit for bit (round_div_sub, common.hpp)
+        float r = round_div_sub(x, bucket, rcp, offset);
         return (r >= 0.0f && r < (float) kPdfSize) ? (int) r : -1;
     }
 };

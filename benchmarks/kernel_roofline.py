@@ -125,6 +125,23 @@ def main():
     ms = timed(lambda: lib.aimet_quantize_per_tensor(P(x), P(y), N, ctypes.byref(enc), 0, 1, 0, sp), args.reps,
                stream)
     row("quantize_per_tensor", "a4", 8, ms, cpu_rate(lambda: O.quantize_per_tensor(xs, enc.min, enc.max, 8, True)))
+    # a3 / a5 with fp16 and bf16 I/O (casts fused: 4 B/elem) vs the reference's upcast-QDQ-downcast
+    for dt, code in ((torch.float16, 1), (torch.bfloat16, 2)):
+        x16, y16 = x.to(dt), torch.empty(N, dtype=dt, device=dev)
+        ms = timed(lambda: lib.aimet_qdq_per_tensor_16(P(x16), P(y16), N, code, ctypes.byref(enc), 0, 0, sp),
+                   args.reps, stream)
+
+        def three_pass():
+            xf = x16.to(torch.float32)
+            lib.aimet_qdq_per_tensor(P(xf), P(y), N, ctypes.byref(enc), 0, 0, sp)
+            return y.to(dt)
+        t_ms = timed(three_pass, 2, stream)
+        row("qdq_per_tensor %s I/O" % str(dt).split(".")[1], "a3", 4, ms, None, t_ms,
+            note="reference: .to(float32) -> fp32 QDQ -> .to(dtype)")
+        ms = timed(lambda: lib.aimet_qdq_per_channel_16(P(x16), P(y16), 1, C, K, code, P(table), 0, 0, sp),
+                   args.reps, stream)
+        row("qdq_per_channel %s I/O" % str(dt).split(".")[1], "a5", 4, ms)
+        del x16, y16
     # a5: per-channel QDQ
     ms = timed(lambda: lib.aimet_qdq_per_channel(P(x), P(y), 1, C, K, P(table), 0, 0, sp), args.reps, stream)
     Cs = max(1, M // K)
