@@ -168,7 +168,8 @@ __device__ __forceinline__ float quantize_nearest(float x, const QdqParams& p)
 // roundings can only differ if a half-integer lies within that distance of v; when v is farther
 // than 2^-21 (|q| + |off| + 1) (>= 8u(...)) from every half-integer, round(v) == round(v*).
 // Otherwise -- and for every non-finite intermediate -- the exact IEEE division decides. The
-// result is therefore bit-identical to the division form (and to the reference).
+// result is therefore bit-identical to the division form (and to the reference), signed zeros
+// included (see below).
 __device__ __forceinline__ float round_div_sub(float a, float d, float rcp, float off)
 {
     const float q    = a * rcp;
@@ -176,7 +177,9 @@ __device__ __forceinline__ float round_div_sub(float a, float d, float rcp, floa
     const float h    = v - __builtin_floorf(v);             // exact fractional part, [0, 1)
     const float dist = __builtin_fabsf(h - 0.5f);
     const float thr  = (__builtin_fabsf(q) + __builtin_fabsf(off) + 1.0f) * 4.76837158203125e-7f;   // 2^-21
-    if (dist > thr)                                          // false for NaN / inf
+    // A zero result also needs the sign of v*: with off == +-0 it is the sign of a (as for v);
+    // otherwise (v* = q* - off exactly) q' and q* may straddle off, so the division decides.
+    if (dist > thr && (off == 0.0f || __builtin_fabsf(v) >= 0.5f))   // false for NaN / inf
         return __builtin_roundf(v);
     return __builtin_roundf(a / d - off);
 }

@@ -563,3 +563,45 @@ def test_16bit_io_ste_and_autograd(dtype):
         y32.backward(torch.ones_like(y32))
         np.testing.assert_array_equal(_bits16(y.detach()), _bits16(y32.detach().to(dtype)))
         np.testing.assert_array_equal(_bits16(a.grad), _bits16(b.grad.to(dtype)))
+
+
+def test_qdq_and_histogram_near_rounding_boundaries():
+    """Inputs within a few ulp of every rounding boundary (x / delta - offset = k + 1/2): the
+    reciprocal fast path must defer to the IEEE division exactly there (bit-exact vs the oracle),
+    for QDQ (fp32 and bf16 I/O) and the histogram binning."""
+    rng = np.random.default_rng(31)
+    for bw, mn, mx in ((8, -3.1, 5.7), (4, -0.37, 0.9), (16, -1e-3, 2e-3), (8, 0.0, 6.0), (8, -1e4, 3e4)):
+        e = O.fill_encoding_info(bw, mn, mx)
+        d, o = np.float32(e.delta), np.float32(e.offset)
+        k = np.arange(0, 2 ** bw, max(1, 2 ** bw // 4096), dtype=np.float32)
+        base = ((k + np.float32(0.5) + o) * d).astype(np.float32)
+        xs = [base]
+        for s in (1, 2, 3):
+            xs.append(np.nextafter(base, np.float32(np.inf)))
+            xs.append(np.nextafter(base, np.float32(-np.inf)))
+            base = xs[-2]
+        x = np.concatenate(xs + [rng.uniform(mn, mx, 100000).astype(np.float32)]).astype(np.float32)
+        y = host(AimetTensorQuantizer.quantize_dequantize_tensor(gpu(x), enc_of(mn, mx, bw)))
+        np.testing.assert_array_equal(bits(y), bits(O.qdq_per_tensor(x, mn, mx, bw)), err_msg=str((bw, mn, mx)))
+        # quantize-only exposes the sign of a zero code (x / delta ~ offset): code-0 neighbourhood
+        z = ((o + np.float32(0.0)) * d).astype(np.float32)
+        zs = [np.nextafter(z, np.float32(np.inf) if s > 0 else np.float32(-np.inf)) for s in (1, -1)]
+        xz = np.concatenate([x, np.array([z] + zs, np.float32).ravel(),
+                             (z + rng.uniform(-1, 1, 1000).astype(np.float32) * d * np.float32(0.6))
+                             .astype(np.float32)])
+        qz = host(AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF).quantize(gpu(xz), enc_of(mn, mx, bw),
+                                                                                  NEAREST, True, False))
+        np.testing.assert_array_equal(bits(qz), bits(O.quantize_per_tensor(xz, mn, mx, bw, False)))
+        # histogram over the same values (bins = round(x / bucket - offset))
+        q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED)
+        a = O.Analyzer(O.QUANTIZATION_TF_ENHANCED)
+        q.updateStats(gpu(x), True)
+        a.update(x)
+        xl, _ = a.histogram()
+        bucket = np.float32(xl[1] - xl[0])
+        off = np.float32(np.float32(xl[0]) / bucket)
+        edges = ((np.arange(512, dtype=np.float32) + np.float32(0.5) + off) * bucket).astype(np.float32)
+        x2 = np.concatenate([edges, np.nextafter(edges, np.float32(np.inf)), np.nextafter(edges, np.float32(-np.inf))])
+        q.updateStats(gpu(x2), True)
+        a.update(x2)
+        np.testing.assert_array_equal(np.array([t[1] for t in q.getStatsHistogram()]), a.histogram()[1])
