@@ -2,6 +2,9 @@
 //
 // Reference: trim_functions.cu:46-92 (one element per thread, 512-thread blocks, fast-math
 // division, per-element global loads of the per-channel table, legacy default stream).
+// The per-element IEEE division stays (tools/qdq_variants.hip: the reciprocal fast path of
+// common.hpp measures 4% slower here -- this kernel is HBM-bound, the fast path's extra VGPRs and
+// branch cost more than the division; it pays off in the 16-bit and histogram kernels).
 // MI355X design: HBM-bound streaming (8 B/elem fwd, 12 B/elem STE) -> one 16-B vector per lane,
 // one tile per 256-thread workgroup (thousands of workgroups fill the 256 CUs), non-temporal
 // loads/stores (streamed once, kept out of L2/MALL), scalar encoding parameters in SGPRs,
@@ -25,10 +28,9 @@ enum class Op
 };
 
 template <Op OP, bool STOCHASTIC>
-__device__ __forceinline__ float apply(float x, const QdqParams& p, float shift, uint64_t seed, uint64_t idx,
-                                       float rcp)
+__device__ __forceinline__ float apply(float x, const QdqParams& p, float shift, uint64_t seed, uint64_t idx)
 {
-    float q = STOCHASTIC ? quantize_stochastic(x, p, seed, idx) : quantize_nearest_rcp(x, p, rcp);
+    float q = STOCHASTIC ? quantize_stochastic(x, p, seed, idx) : quantize_nearest(x, p);
     if constexpr (OP == Op::QDQ)
         return dequantize(q, p);
     else
@@ -61,12 +63,11 @@ __global__ __launch_bounds__(kBlock) void tensor_vec_kernel(const f4* __restrict
         return;
     f4 v = load_stream(in + i);
     uint64_t e = (uint64_t) i * 4;
-    const float rcp = 1.0f / p.delta;
     f4 r;
-    r.x = apply<OP, STOCHASTIC>(v.x, p, shift, seed, e + 0, rcp);
-    r.y = apply<OP, STOCHASTIC>(v.y, p, shift, seed, e + 1, rcp);
-    r.z = apply<OP, STOCHASTIC>(v.z, p, shift, seed, e + 2, rcp);
-    r.w = apply<OP, STOCHASTIC>(v.w, p, shift, seed, e + 3, rcp);
+    r.x = apply<OP, STOCHASTIC>(v.x, p, shift, seed, e + 0);
+    r.y = apply<OP, STOCHASTIC>(v.y, p, shift, seed, e + 1);
+    r.z = apply<OP, STOCHASTIC>(v.z, p, shift, seed, e + 2);
+    r.w = apply<OP, STOCHASTIC>(v.w, p, shift, seed, e + 3);
     store_stream(r, out + i);
 }
 
@@ -76,9 +77,8 @@ __global__ __launch_bounds__(kBlock) void tensor_scalar_kernel(const float* __re
                                                                uint64_t seed)
 {
     const int64_t stride = (int64_t) gridDim.x * kBlock;
-    const float rcp      = 1.0f / p.delta;
     for (int64_t i = begin + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
-        out[i] = apply<OP, STOCHASTIC>(in[i], p, shift, seed, (uint64_t) i, rcp);
+        out[i] = apply<OP, STOCHASTIC>(in[i], p, shift, seed, (uint64_t) i);
 }
 
 template <Op OP, bool STOCHASTIC>
@@ -138,12 +138,11 @@ __global__ __launch_bounds__(kBlock) void channel_vec_kernel(const f4* __restric
     f4 v        = load_stream(in + i);
     QdqParams p = load_params(table, map.C, map.channel(i * 4));
     uint64_t e  = (uint64_t) i * 4;
-    const float rcp = 1.0f / p.delta;
     f4 r;
-    r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0, rcp);
-    r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1, rcp);
-    r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2, rcp);
-    r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3, rcp);
+    r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0);
+    r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1);
+    r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2);
+    r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3);
     store_stream(r, out + i);
 }
 
@@ -155,9 +154,8 @@ __global__ __launch_bounds__(kBlock) void channel_scalar_kernel(const float* __r
     const uint32_t stride = gridDim.x * kBlock;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
     {
-        QdqParams p     = load_params(table, map.C, map.channel(i));
-        const float rcp = 1.0f / p.delta;
-        out[i]          = apply<Op::QDQ, STOCHASTIC>(in[i], p, 0.f, seed, i, rcp);
+        QdqParams p = load_params(table, map.C, map.channel(i));
+        out[i]      = apply<Op::QDQ, STOCHASTIC>(in[i], p, 0.f, seed, i);
     }
 }
 
@@ -172,9 +170,8 @@ __global__ __launch_bounds__(kBlock) void channel_scalar64_kernel(const float* _
     for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
     {
         uint32_t c  = (uint32_t) ((i / K) % C);
-        QdqParams p     = load_params(table, (uint32_t) C, c);
-        const float rcp = 1.0f / p.delta;
-        out[i]          = apply<Op::QDQ, STOCHASTIC>(in[i], p, 0.f, seed, (uint64_t) i, rcp);
+        QdqParams p = load_params(table, (uint32_t) C, c);
+        out[i]      = apply<Op::QDQ, STOCHASTIC>(in[i], p, 0.f, seed, (uint64_t) i);
     }
 }
 
@@ -277,21 +274,19 @@ __global__ __launch_bounds__(kBlock) void channel_batch_kernel(const BatchDesc* 
         f4 v        = load_stream(reinterpret_cast<const f4*>(d.in) + t);
         QdqParams p = load_params(d.table, d.map.C, d.map.channel(t * 4));
         uint64_t e  = ((uint64_t) lo << 40) + (uint64_t) t * 4;
-        const float rcp = 1.0f / p.delta;
         f4 r;
-        r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0, rcp);
-        r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1, rcp);
-        r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2, rcp);
-        r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3, rcp);
+        r.x = apply<Op::QDQ, STOCHASTIC>(v.x, p, 0.f, seed, e + 0);
+        r.y = apply<Op::QDQ, STOCHASTIC>(v.y, p, 0.f, seed, e + 1);
+        r.z = apply<Op::QDQ, STOCHASTIC>(v.z, p, 0.f, seed, e + 2);
+        r.w = apply<Op::QDQ, STOCHASTIC>(v.w, p, 0.f, seed, e + 3);
         store_stream(r, reinterpret_cast<f4*>(d.out) + t);
     }
     else
     {
         if (t >= d.n)
             return;
-        QdqParams p     = load_params(d.table, d.map.C, d.map.channel(t));
-        const float rcp = 1.0f / p.delta;
-        d.out[t]        = apply<Op::QDQ, STOCHASTIC>(d.in[t], p, 0.f, seed, ((uint64_t) lo << 40) + t, rcp);
+        QdqParams p = load_params(d.table, d.map.C, d.map.channel(t));
+        d.out[t]    = apply<Op::QDQ, STOCHASTIC>(d.in[t], p, 0.f, seed, ((uint64_t) lo << 40) + t);
     }
 }
 

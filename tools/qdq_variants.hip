@@ -74,8 +74,8 @@ __global__ __launch_bounds__(BLOCK) void qdq_var(const float4* __restrict__ in, 
     }
 }
 
-// one tile per block, no grid-stride loop
-template <int BLOCK, int UNROLL, bool NT = false>
+// one tile per block, no grid-stride loop (RCP: reciprocal fast path of common.hpp)
+template <int BLOCK, int UNROLL, bool NT = false, bool RCP = false>
 __global__ __launch_bounds__(BLOCK) void qdq_tile(const float4* __restrict__ in, float4* __restrict__ out, int64_t nvec,
                                                   QdqParams p)
 {
@@ -95,10 +95,21 @@ __global__ __launch_bounds__(BLOCK) void qdq_tile(const float4* __restrict__ in,
         if (base + u * BLOCK < nvec)
         {
             f4 r;
-            r.x = dequantize(quantize_nearest(v[u].x, p), p);
-            r.y = dequantize(quantize_nearest(v[u].y, p), p);
-            r.z = dequantize(quantize_nearest(v[u].z, p), p);
-            r.w = dequantize(quantize_nearest(v[u].w, p), p);
+            if (RCP)
+            {
+                const float rcp = 1.0f / p.delta;
+                r.x = dequantize(quantize_nearest_rcp(v[u].x, p, rcp), p);
+                r.y = dequantize(quantize_nearest_rcp(v[u].y, p, rcp), p);
+                r.z = dequantize(quantize_nearest_rcp(v[u].z, p, rcp), p);
+                r.w = dequantize(quantize_nearest_rcp(v[u].w, p, rcp), p);
+            }
+            else
+            {
+                r.x = dequantize(quantize_nearest(v[u].x, p), p);
+                r.y = dequantize(quantize_nearest(v[u].y, p), p);
+                r.z = dequantize(quantize_nearest(v[u].z, p), p);
+                r.w = dequantize(quantize_nearest(v[u].w, p), p);
+            }
             if (NT)
                 __builtin_nontemporal_store(r, reinterpret_cast<f4*>(out) + base + u * BLOCK);
             else
@@ -122,11 +133,11 @@ void launch_var(const float4* in, float4* out, int64_t nvec, QdqParams p, hipStr
     qdq_var<BLOCK, UNROLL, NTL, NTS, COPY><<<g, BLOCK, 0, s>>>(in, out, nvec, p);
 }
 
-template <int BLOCK, int UNROLL, bool NT = false>
+template <int BLOCK, int UNROLL, bool NT = false, bool RCP = false>
 void launch_tile(const float4* in, float4* out, int64_t nvec, QdqParams p, hipStream_t s)
 {
     int64_t g = (nvec + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
-    qdq_tile<BLOCK, UNROLL, NT><<<(int) g, BLOCK, 0, s>>>(in, out, nvec, p);
+    qdq_tile<BLOCK, UNROLL, NT, RCP><<<(int) g, BLOCK, 0, s>>>(in, out, nvec, p);
 }
 
 int main(int argc, char** argv)
@@ -148,31 +159,11 @@ int main(int argc, char** argv)
     CK(hipStreamCreate(&s));
 
     std::vector<Variant> vs = {
-        {"copy b256 u4 g2048", launch_var<256, 4, false, false, true, 2048>, true, {}},
         {"copy b256 u4 g2048 nt-ld+st", launch_var<256, 4, true, true, true, 2048>, true, {}},
-        {"qdq  b256 u4 g2048 (current)", launch_var<256, 4, false, false, false, 2048>, false, {}},
-        {"qdq  b256 u4 g2048 nt-load", launch_var<256, 4, true, false, false, 2048>, false, {}},
-        {"qdq  b256 u4 g2048 nt-store", launch_var<256, 4, false, true, false, 2048>, false, {}},
-        {"qdq  b256 u4 g2048 nt-ld+st", launch_var<256, 4, true, true, false, 2048>, false, {}},
-        {"qdq  b256 u8 g2048", launch_var<256, 8, false, false, false, 2048>, false, {}},
-        {"qdq  b256 u2 g2048", launch_var<256, 2, false, false, false, 2048>, false, {}},
-        {"qdq  b256 u4 g1024", launch_var<256, 4, false, false, false, 1024>, false, {}},
-        {"qdq  b256 u4 g4096", launch_var<256, 4, false, false, false, 4096>, false, {}},
-        {"qdq  b256 u4 g8192", launch_var<256, 4, false, false, false, 8192>, false, {}},
-        {"qdq  b512 u4 g1024", launch_var<512, 4, false, false, false, 1024>, false, {}},
-        {"qdq  b512 u2 g2048", launch_var<512, 2, false, false, false, 2048>, false, {}},
-        {"qdq  tile b256 u4", launch_tile<256, 4>, false, {}},
-        {"qdq  tile b256 u2", launch_tile<256, 2>, false, {}},
-        {"qdq  tile b512 u4", launch_tile<512, 4>, false, {}},
-        {"qdq  tile b256 u1 nt", launch_tile<256, 1, true>, false, {}},
-        {"qdq  tile b256 u2 nt", launch_tile<256, 2, true>, false, {}},
-        {"qdq  tile b256 u4 nt", launch_tile<256, 4, true>, false, {}},
-        {"qdq  tile b512 u2 nt", launch_tile<512, 2, true>, false, {}},
-        {"qdq  tile b1024 u1 nt", launch_tile<1024, 1, true>, false, {}},
-        {"qdq  b256 u4 g4096 nt", launch_var<256, 4, true, true, false, 4096>, false, {}},
-        {"qdq  b256 u4 g8192 nt", launch_var<256, 4, true, true, false, 8192>, false, {}},
-        {"qdq  b256 u2 g8192 nt", launch_var<256, 2, true, true, false, 8192>, false, {}},
-        {"qdq  b256 u2 g16384 nt", launch_var<256, 2, true, true, false, 16384>, false, {}},
+        {"qdq  tile b256 u1 nt (division)", launch_tile<256, 1, true>, false, {}},
+        {"qdq  tile b256 u1 nt rcp fast path", launch_tile<256, 1, true, true>, false, {}},
+        {"qdq  tile b256 u2 nt rcp fast path", launch_tile<256, 2, true, true>, false, {}},
+        {"qdq  tile b512 u1 nt rcp fast path", launch_tile<512, 1, true, true>, false, {}},
     };
     // reference output
     launch_var<256, 4, false, false, false, 2048>((const float4*) in, (float4*) ref, nvec, p, s);
