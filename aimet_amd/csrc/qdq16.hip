@@ -42,12 +42,10 @@ __device__ __forceinline__ unsigned short from_f32(float f)
         return __half_as_ushort(__float2half_rn(f));
     else
     {
-        // c10::BFloat16 round_to_nearest_even (c10/util/BFloat16.h)
-        if (f != f)
-            return 0x7FC0;
-        uint32_t u = __float_as_uint(f);
-        u += 0x7FFFu + ((u >> 16) & 1u);
-        return (unsigned short) (u >> 16);
+        // c10::BFloat16 round_to_nearest_even (c10/util/BFloat16.h): RNE = gfx950's
+        // v_cvt_pk_bf16_f32; torch maps every NaN to 0x7FC0
+        const unsigned short h = __builtin_bit_cast(unsigned short, (__bf16) f);
+        return f != f ? (unsigned short) 0x7FC0 : h;
     }
 }
 

@@ -15,6 +15,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include "common.hpp"   // round_div_sub (reciprocal fast path)
+
 #define CK(x)                                                                                                  \
     do                                                                                                         \
     {                                                                                                          \
@@ -39,6 +41,16 @@ struct Binner
     }
 };
 
+struct BinnerRcp
+{
+    float bucket, offset, rcp;
+    __device__ __forceinline__ int bin(float x) const
+    {
+        float r = aimet_amd::round_div_sub(x, bucket, rcp, offset);
+        return (r >= 0.0f && r < (float) kBins) ? (int) r : -1;
+    }
+};
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
 #pragma unroll
@@ -48,8 +60,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 }
 
 // COPIES: LDS histograms per block (1 = shared by the block, BLOCK/64 = one per wave)
-template <int BLOCK, int UNROLL, int COPIES, bool NT, bool ZSKIP, bool PART = false>
-__global__ __launch_bounds__(BLOCK) void hist_var(const float* __restrict__ x, int64_t n, Binner bn,
+template <int BLOCK, int UNROLL, int COPIES, bool NT, bool ZSKIP, bool PART = false, class B = Binner>
+__global__ __launch_bounds__(BLOCK) void hist_var(const float* __restrict__ x, int64_t n, B bn,
                                                   unsigned long long* __restrict__ counts)
 {
     __shared__ uint32_t lds[COPIES][kBins];
@@ -359,6 +371,15 @@ void launch_minmax(const float* x, int64_t n, Binner, unsigned long long* c, hip
     minmax_var<BLOCK, UNROLL, NT><<<g, BLOCK, 0, s>>>(x, n, (float2*) c);
 }
 
+template <int BLOCK, int UNROLL, int COPIES, int GRID>
+void launch_hist_rcp(const float* x, int64_t n, Binner bn, unsigned long long* c, hipStream_t s)
+{
+    int64_t need = (n / 4 + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
+    int g        = (int) std::max<int64_t>(1, std::min<int64_t>(need, GRID));
+    BinnerRcp br {bn.bucket, bn.offset, 1.0f / bn.bucket};
+    hist_var<BLOCK, UNROLL, COPIES, true, true, false, BinnerRcp><<<g, BLOCK, 0, s>>>(x, n, br, c);
+}
+
 // read-only ceiling: sum of the input (same load pattern)
 template <int BLOCK, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void read_var(const float* __restrict__ x, int64_t n, float* __restrict__ out)
@@ -444,16 +465,10 @@ int main(int argc, char** argv)
     CK(hipMemset(cnt, 0, 1024 * 8 + 8192 * 512 * 4));
     std::vector<Variant> vs = {
         {"read-only ceiling b256 u4 g4096", launch_read<256, 4, 4096>, false, {}},
-        {"hist b256 u4 c4 g2048 nt (current)", launch_hist<256, 4, 4, true, true, 2048>, true, {}},
-        {"hist b256 u4 c4 g1024 nt", launch_hist<256, 4, 4, true, true, 1024>, true, {}},
-        {"hist b256 u4 c4 g512 nt", launch_hist<256, 4, 4, true, true, 512>, true, {}},
-        {"hist b512 u4 c8 g512 nt", launch_hist<512, 4, 8, true, true, 512>, true, {}},
-        {"hist b1024 u2 c16 g256 nt", launch_hist<1024, 2, 16, true, true, 256>, true, {}},
-        {"hist b1024 u4 c16 g256 nt", launch_hist<1024, 4, 16, true, true, 256>, true, {}},
-        {"part b256 u4 g1024", launch_part<256, 4, 1024>, true, {}},
-        {"part b256 u4 g512", launch_part<256, 4, 512>, true, {}},
-        {"part b512 u4 g512", launch_part<512, 4, 512>, true, {}},
-        {"part b1024 u2 g256", launch_part<1024, 2, 256>, true, {}},
+        {"hist b256 u4 c4 g2048 nt (division)", launch_hist<256, 4, 4, true, true, 2048>, true, {}},
+        {"hist b256 u4 c4 g2048 nt (rcp fast path)", launch_hist_rcp<256, 4, 4, 2048>, true, {}},
+        {"hist b1024 u4 c16 g256 nt (division)", launch_hist<1024, 4, 16, true, true, 256>, true, {}},
+        {"hist b1024 u4 c16 g256 nt (rcp fast path)", launch_hist_rcp<1024, 4, 16, 256>, true, {}},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
