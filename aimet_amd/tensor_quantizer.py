@@ -11,6 +11,7 @@ Same class name, method names and argument meaning. Differences, all MI355X-firs
 * there is no CPU path: CPU tensors / ``use_cuda=False`` raise ``RuntimeError``.
 """
 import ctypes
+import gc
 import itertools
 
 import torch
@@ -240,12 +241,19 @@ class AimetTensorQuantizer:
                 _native.call("aimet_tq_get_encodings", handles, len(live), int(bitwidth),
                              int(bool(use_symmetric_encodings)), int(bool(use_strict_symmetric)),
                              int(bool(use_unsigned_symmetric)), out, valid, torch.cuda.current_stream(dev).cuda_stream)
-            encs = list(out)
-            off = 0
-            for i, q in enumerate(live):
-                C = q._num_channels
-                results[id(q)] = (encs[off] if C == 1 else encs[off:off + C], bool(valid[i]))
-                off += C
+            # tens of thousands of small objects: keep the cyclic GC from firing mid-list
+            gc_was_enabled = gc.isenabled()
+            gc.disable()
+            try:
+                encs = list(out)
+                off = 0
+                for i, q in enumerate(live):
+                    C = q._num_channels
+                    results[id(q)] = (encs[off] if C == 1 else encs[off:off + C], bool(valid[i]))
+                    off += C
+            finally:
+                if gc_was_enabled:
+                    gc.enable()
         res = []
         for q in quantizers:
             if id(q) in results:
