@@ -50,11 +50,22 @@ def _world(group):
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
+def _all_reduce(t, op, group):
+    """all_reduce in place; a device tensor over a gloo group (no RCCL: e.g. several ranks sharing
+    one GPU) is staged through host memory."""
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
 def global_counts(local_counts, device, group=None):
     """Per-quantizer element counts summed over ranks (one tiny collective)."""
     t = torch.tensor(local_counts, dtype=torch.int64, device=device)
     if _world(group) > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+        _all_reduce(t, dist.ReduceOp.SUM, group)
     return t.tolist()
 
 
@@ -74,7 +85,7 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
         q.batch_minmax(t, ax)
     if world > 1:
         # {-min, max}: a single MAX reduces both ends exactly
-        dist.all_reduce(exchange.minmax, op=dist.ReduceOp.MAX, group=group)
+        _all_reduce(exchange.minmax, dist.ReduceOp.MAX, group)
     for q in quantizers:
         q.fold_minmax()
 
@@ -84,7 +95,7 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
             q.batch_histogram(t, ax)
         local = [t.numel() // q.num_channels for q, t, _ in hist]
         if world > 1:
-            dist.all_reduce(exchange.counts, op=dist.ReduceOp.SUM, group=group)
+            _all_reduce(exchange.counts, dist.ReduceOp.SUM, group)
             counts = global_counts(local, device, group)
         else:
             counts = local

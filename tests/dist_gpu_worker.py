@@ -1,0 +1,88 @@
+"""Worker of tests/test_distributed_gpu.py (not collected by pytest): one rank of a sharded
+calibration on the GPU. Every rank uses cuda:0 (one-GPU box) and a gloo group (the exchange
+buffers are staged through host memory); the statistics are computed by the gfx950 kernels."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+from aimet_amd.distributed import sharded_update_stats  # noqa: E402
+from aimet_amd.libpymo import QuantizationMode  # noqa: E402
+from aimet_amd.tensor_quantizer import AimetTensorQuantizer  # noqa: E402
+
+SCHEMES = [QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
+           QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE]
+FLAGS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]
+
+
+def batches(n_batches=3, batch=8, seed=0):
+    """(activation [batch, 6, 5, 5], relu of it) per batch; batch 0 has an all-zero channel."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for b in range(n_batches):
+        act = (rng.standard_normal((batch, 6, 5, 5)) * (1 + b)).astype(np.float32)
+        if b == 0:
+            act[:, 2] = 0.0
+        out.append((act, np.maximum(act, 0)))
+    return out
+
+
+def make_quantizers():
+    qs = []
+    for s in SCHEMES:
+        qs.append(AimetTensorQuantizer(s))                     # per-tensor activation
+        qs.append(AimetTensorQuantizer(s, num_channels=6))     # per-channel (axis 1)
+    for q in qs:
+        if q.quant_scheme == QuantizationMode.QUANTIZATION_PERCENTILE:
+            q.setPercentileValue(99.0)
+    return qs
+
+
+def encodings(qs):
+    out = []
+    for q in qs:
+        for fl in FLAGS:
+            e, valid = q.getEncoding(8, *fl)
+            out.append([x.to_tuple() for x in (e if isinstance(e, list) else [e])] + [bool(valid)])
+    return out
+
+
+def main():
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    qs = make_quantizers()
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    ex = None
+    for act, relu in batches():
+        shard = slice(rank, None, world)      # per-sample sharding
+        tensors, axes = [], []
+        for i, q in enumerate(qs):
+            src = act if (i // 2) % 2 == 0 else relu
+            tensors.append(torch.from_numpy(np.ascontiguousarray(src[shard])).to(dev))
+            axes.append(1)
+        if world > 1:
+            ex = sharded_update_stats(qs, tensors, axes, exchange=ex)
+        else:
+            for q, t, ax in zip(qs, tensors, axes):
+                if q.num_channels == 1:
+                    q.updateStats(t, True)
+                else:
+                    q.updateStatsPerChannel(t, ax, True)
+    res = encodings(qs)
+    with open(os.environ["OUT"] + ".%d" % rank, "w") as f:
+        json.dump(res, f)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

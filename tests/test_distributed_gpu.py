@@ -1,0 +1,41 @@
+"""Sharded calibration on the GPU kernels (world size 2, both ranks on cuda:0 over gloo): every
+rank's encodings == one process seeing the whole batches, for TF / TF-E / percentile / MSE,
+per-tensor and per-channel. Ranks are separate child processes."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+WORKER = os.path.join(os.path.dirname(os.path.abspath(__file__)), "dist_gpu_worker.py")
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(world, out):
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), OUT=out)
+        procs.append(subprocess.Popen([sys.executable, WORKER], env=env))
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    return [json.load(open(out + ".%d" % r)) for r in range(world)]
+
+
+def test_sharded_calibration_equals_whole_batch_on_gpu(tmp_path):
+    whole, = _run(1, str(tmp_path / "whole"))
+    shards = _run(2, str(tmp_path / "shard"))
+    for r, res in enumerate(shards):
+        assert res == whole, "rank %d" % r
