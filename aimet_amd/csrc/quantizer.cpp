@@ -293,6 +293,89 @@ int aimet_tq_update_stats(aimet_tensor_quantizer* q, const float* x, int64_t out
     });
 }
 
+}   // extern "C"
+
+namespace
+{
+
+// jobs of a many-quantizer call: per-tensor quantizers of one device
+std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
+                                const int64_t* counts, int64_t count)
+{
+    AIMET_REQUIRE(qs != nullptr && count >= 0, "null argument");
+    std::vector<StatsJob> jobs((size_t) count);
+    for (int64_t i = 0; i < count; ++i)
+    {
+        aimet_tensor_quantizer* q = qs[i];
+        AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
+        AIMET_REQUIRE(q->C == 1, "the *_many entry points take per-tensor quantizers (num_channels == 1)");
+        AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one *_many call share a device");
+        StatsJob& j = jobs[(size_t) i];
+        j.x         = xs ? xs[i] : nullptr;
+        j.n         = ns ? ns[i] : 0;
+        AIMET_REQUIRE(j.n >= 0, "negative element count");
+        if (xs && j.n > 0)
+            require_device_ptr(j.x, "input");
+        j.count = counts ? counts[i] : j.n;
+        AIMET_REQUIRE(j.count >= 0, "negative element count");
+        j.d     = q->d;
+        j.hist  = q->hist ? 1 : 0;
+        j.vec   = (reinterpret_cast<uintptr_t>(j.x) & 15) == 0 ? 1 : 0;
+    }
+    return jobs;
+}
+
+int run_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns, const int64_t* counts,
+             int64_t count, int phases, bool marks_updated, void* stream)
+{
+    return guarded([&] {
+        auto jobs = make_jobs(qs, xs, ns, counts, count);
+        if (jobs.empty())
+            return;
+        DeviceGuard g(qs[0]->device);
+        launch_stats_many(jobs, phases, as_stream(stream));
+        if (marks_updated)
+            for (int64_t i = 0; i < count; ++i)
+                qs[i]->stats_updated = true;
+    });
+}
+
+}   // namespace
+
+extern "C" {
+
+int aimet_tq_update_stats_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
+                               int64_t count, void* stream)
+{
+    return run_many(qs, xs, ns, nullptr, count,
+                    kPhaseMinmax | kPhaseFoldMinmax | kPhaseHistogram | kPhaseFoldHistogram, true, stream);
+}
+
+int aimet_tq_batch_minmax_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
+                               int64_t count, void* stream)
+{
+    return run_many(qs, xs, ns, nullptr, count, kPhaseMinmax, true, stream);
+}
+
+int aimet_tq_fold_minmax_many(aimet_tensor_quantizer* const* qs, int64_t count, void* stream)
+{
+    return run_many(qs, nullptr, nullptr, nullptr, count, kPhaseFoldMinmax, false, stream);
+}
+
+int aimet_tq_batch_histogram_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
+                                  int64_t count, void* stream)
+{
+    return run_many(qs, xs, ns, nullptr, count, kPhaseHistogram, false, stream);
+}
+
+int aimet_tq_fold_histogram_many(aimet_tensor_quantizer* const* qs, const int64_t* counts, int64_t count,
+                                 void* stream)
+{
+    if (counts == nullptr && count > 0)
+        return guarded([] { AIMET_REQUIRE(false, "null element counts"); });
+    return run_many(qs, nullptr, nullptr, counts, count, kPhaseFoldHistogram, false, stream);
+}
+
 int aimet_tq_minmax_buffer(aimet_tensor_quantizer* q, float** dev, int64_t* n)
 {
     return guarded([&] {

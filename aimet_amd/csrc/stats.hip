@@ -18,7 +18,9 @@
 // Arithmetic follows the reference CPU code bit for bit (DTYPE = float; see common.hpp).
 #include "tq_state.hpp"
 
+#include <algorithm>
 #include <cfloat>
+#include <vector>
 
 namespace aimet_amd
 {
@@ -88,20 +90,18 @@ __device__ __forceinline__ void accum4(const float4& v, float& mn, float& mx)
 }
 
 // ---- per-tensor min/max: partials[block] = {-min, max} --------------------------------------
-__global__ __launch_bounds__(kBlock) void minmax_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
-                                                               float2* __restrict__ partials,
-                                                               const int32_t* __restrict__ pdf_init, int skip_if_init)
+// One workgroup's share (block `blk` of `nblk`) of the min/max pass over x[0, n).
+__device__ __forceinline__ void minmax_part(const float* __restrict__ x, int64_t n, int vec, int64_t blk,
+                                            int64_t nblk, float2* __restrict__ partials)
 {
-    if (skip_if_init && pdf_init[0])
-        return;
     float mn = INFINITY, mx = -INFINITY;
     if (vec)
     {
         // streaming 16-B loads, 4 in flight per lane (tools/hist_variants.hip: 6.8 TB/s)
         const f4* x4         = reinterpret_cast<const f4*>(x);
         int64_t nvec         = n / 4;
-        const int64_t stride = (int64_t) gridDim.x * kBlock * 4;
-        for (int64_t b = (int64_t) blockIdx.x * kBlock * 4 + threadIdx.x; b < nvec; b += stride)
+        const int64_t stride = nblk * kBlock * 4;
+        for (int64_t b = blk * kBlock * 4 + threadIdx.x; b < nvec; b += stride)
         {
             f4 v[4];
 #pragma unroll
@@ -112,8 +112,7 @@ __global__ __launch_bounds__(kBlock) void minmax_tensor_kernel(const float* __re
             for (int u = 0; u < 4; ++u)
                 accum4(make_float4(v[u].x, v[u].y, v[u].z, v[u].w), mn, mx);
         }
-        for (int64_t i = nvec * 4 + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n;
-             i += (int64_t) gridDim.x * kBlock)
+        for (int64_t i = nvec * 4 + blk * kBlock + threadIdx.x; i < n; i += nblk * kBlock)
         {
             mn = fminf(mn, x[i]);
             mx = fmaxf(mx, x[i]);
@@ -121,7 +120,7 @@ __global__ __launch_bounds__(kBlock) void minmax_tensor_kernel(const float* __re
     }
     else
     {
-        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
+        for (int64_t i = blk * kBlock + threadIdx.x; i < n; i += nblk * kBlock)
         {
             mn = fminf(mn, x[i]);
             mx = fmaxf(mx, x[i]);
@@ -129,7 +128,16 @@ __global__ __launch_bounds__(kBlock) void minmax_tensor_kernel(const float* __re
     }
     block_minmax(mn, mx);
     if (threadIdx.x == 0)
-        partials[blockIdx.x] = make_float2(-mn, mx);
+        partials[blk] = make_float2(-mn, mx);
+}
+
+__global__ __launch_bounds__(kBlock) void minmax_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
+                                                               float2* __restrict__ partials,
+                                                               const int32_t* __restrict__ pdf_init, int skip_if_init)
+{
+    if (skip_if_init && pdf_init[0])
+        return;
+    minmax_part(x, n, vec, blockIdx.x, gridDim.x, partials);
 }
 
 // Combine per-block partials {-min, max} into minmax[0].
@@ -212,16 +220,15 @@ __device__ void initialize_pdf(const TqDevice& d, int64_t c, float min_val, floa
     d.pdf_init[c]    = 1;
 }
 
-__global__ __launch_bounds__(kBlock) void fold_minmax_kernel(TqDevice d, int64_t C, int tf_scheme)
+// TfEncodingAnalyzer.cpp:63-71 (TF: running min/max in double) or UpdatePdf's first-batch range
+// initialisation (histogram schemes), for channel c from minmax[c] = {-min, max}
+__device__ __forceinline__ void fold_one(const TqDevice& d, int64_t c, bool tf_scheme)
 {
-    int64_t c = (int64_t) blockIdx.x * kBlock + threadIdx.x;
-    if (c >= C)
-        return;
-    float2 m  = reinterpret_cast<const float2*>(d.minmax)[c];
-    float mn  = -m.x, mx = m.y;
+    float2 m = reinterpret_cast<const float2*>(d.minmax)[c];
+    float mn = -m.x, mx = m.y;
     if (tf_scheme)
     {
-        // TfEncodingAnalyzer.cpp:63-71 (std::min/std::max in double)
+        // std::min/std::max in double
         double cmin = (double) mn, cmax = (double) mx;
         double2* acc = reinterpret_cast<double2*>(d.acc);
         double2 a    = acc[c];
@@ -236,6 +243,13 @@ __global__ __launch_bounds__(kBlock) void fold_minmax_kernel(TqDevice d, int64_t
             return;
         initialize_pdf(d, c, mn, mx);
     }
+}
+
+__global__ __launch_bounds__(kBlock) void fold_minmax_kernel(TqDevice d, int64_t C, int tf_scheme)
+{
+    int64_t c = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (c < C)
+        fold_one(d, c, tf_scheme != 0);
 }
 
 // ---- histogram ----------------------------------------------------------------------------
@@ -253,14 +267,13 @@ struct Binner
     }
 };
 
-// per-tensor: many workgroups over one tensor, atomics into counts[0][:]
+// per-tensor: many workgroups over one tensor, atomics into counts[0][:]. One workgroup's share
+// (block `blk` of `nblk`) of the pass over x[0, n).
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void histogram_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
-                                                                 TqDevice d)
+__device__ __forceinline__ void histogram_part(const float* __restrict__ x, int64_t n, int vec, int64_t blk,
+                                               int64_t nblk, const TqDevice& d)
 {
     constexpr int kWaves = BLOCK / 64;
-    if (!d.pdf_init[0])
-        return;
     __shared__ uint32_t lds[kWaves][kPdfSize];
     Binner bn {d.bin_bucket[0], d.bin_offset[0]};
     const int w = threadIdx.x >> 6;
@@ -285,8 +298,8 @@ __global__ __launch_bounds__(BLOCK) void histogram_tensor_kernel(const float* __
         // 4 x 16-B streaming loads in flight per lane (tools/hist_variants.hip: 5.6-5.8 TB/s)
         const f4* x4         = reinterpret_cast<const f4*>(x);
         const int64_t nv     = n / 4;
-        const int64_t stride = (int64_t) gridDim.x * BLOCK * kHistUnroll;
-        for (int64_t base = (int64_t) blockIdx.x * BLOCK * kHistUnroll + threadIdx.x; base < nv; base += stride)
+        const int64_t stride = nblk * BLOCK * kHistUnroll;
+        for (int64_t base = blk * BLOCK * kHistUnroll + threadIdx.x; base < nv; base += stride)
         {
             f4 v[kHistUnroll];
 #pragma unroll
@@ -306,7 +319,7 @@ __global__ __launch_bounds__(BLOCK) void histogram_tensor_kernel(const float* __
         }
         done = nv * 4;
     }
-    for (int64_t i = done + (int64_t) blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t) gridDim.x * BLOCK)
+    for (int64_t i = done + blk * BLOCK + threadIdx.x; i < n; i += nblk * BLOCK)
         add(x[i]);
     zc = wave_sum(zc);
     if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
@@ -321,6 +334,15 @@ __global__ __launch_bounds__(BLOCK) void histogram_tensor_kernel(const float* __
         if (s)
             atomicAdd(&d.counts[b], (unsigned long long) s);
     }
+}
+
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void histogram_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
+                                                                 TqDevice d)
+{
+    if (!d.pdf_init[0])
+        return;
+    histogram_part<BLOCK>(x, n, vec, blockIdx.x, gridDim.x, d);
 }
 
 // per-channel: one workgroup per channel, counts written directly
@@ -387,21 +409,28 @@ __global__ __launch_bounds__(kBlock) void histogram_channel_kernel(const float* 
 }
 
 // UpdatePdf:277-287 -- pdf = (pdf * it + count / N) / (it + 1), double, per bin.
+// UpdatePdf:280-287 for channel c (one 512-lane workgroup): pdf = (pdf*it + cnt/N)/(it+1) in
+// double; counts cleared for the next batch
+__device__ __forceinline__ void fold_hist_one(const TqDevice& d, int64_t c, int64_t count)
+{
+    int it        = d.iterations[c];
+    int64_t idx   = c * kPdfSize + threadIdx.x;
+    double prob   = (double) d.counts[idx] / (double) count;
+    d.pdf[idx]    = (d.pdf[idx] * it + prob) / (it + 1);
+    d.counts[idx] = 0;
+    __syncthreads();
+    if (threadIdx.x == 0)
+        d.iterations[c] = it + 1;
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(kPdfSize) void fold_histogram_kernel(TqDevice d, int64_t C, int64_t count)
 {
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
     {
         if (!d.pdf_init[c])
             continue;
-        int it          = d.iterations[c];
-        int64_t idx     = c * kPdfSize + threadIdx.x;
-        double prob     = (double) d.counts[idx] / (double) count;
-        d.pdf[idx]      = (d.pdf[idx] * it + prob) / (it + 1);
-        d.counts[idx]   = 0;
-        __syncthreads();
-        if (threadIdx.x == 0)
-            d.iterations[c] = it + 1;
-        __syncthreads();
+        fold_hist_one(d, c, count);
     }
 }
 
@@ -413,6 +442,79 @@ __global__ __launch_bounds__(kBlock) void reset_acc_kernel(double* acc, int64_t 
         acc[2 * c]     = DBL_MAX;    // TfEncodingAnalyzer.h:88
         acc[2 * c + 1] = -DBL_MAX;   // TfEncodingAnalyzer.h:89
     }
+}
+
+// ---- many per-tensor quantizers in one launch per phase ---------------------------------------
+// A calibration batch updates every activation quantizer of the model: per quantizer the single
+// launches are min/max + combine + fold + histogram + PDF fold (5 launches, ~5 us each); for
+// ViT-L's 99 quantizers that is ~500 launches per batch. Here each phase is ONE launch over all
+// quantizers: workgroup -> quantizer by a binary search over the quantizers' first workgroups.
+__device__ __forceinline__ int find_job(const StatsJob* __restrict__ jobs, int njobs, uint32_t b, bool hist)
+{
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi)
+    {
+        int mid        = (lo + hi + 1) >> 1;
+        uint32_t first = hist ? jobs[mid].h_block0 : jobs[mid].mm_block0;
+        if (first <= b)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
+{
+    const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, false)];
+    if (J.hist && J.d.pdf_init[0])
+        return;   // histogram schemes take min/max on the first (non-zero) batch only
+    minmax_part(J.x, J.n, J.vec, blockIdx.x - J.mm_block0, J.mm_blocks, reinterpret_cast<float2*>(J.d.partials));
+}
+
+// one workgroup per quantizer: partials -> minmax[0] = {-min, max}; optionally the fold
+__global__ __launch_bounds__(kBlock) void combine_many_kernel(const StatsJob* __restrict__ jobs, int fold)
+{
+    const StatsJob& J = jobs[blockIdx.x];
+    if (J.hist && J.d.pdf_init[0])
+        return;
+    const float2* partials = reinterpret_cast<const float2*>(J.d.partials);
+    float a = -INFINITY, b = -INFINITY;
+    for (uint32_t i = threadIdx.x; i < J.mm_blocks; i += kBlock)
+    {
+        a = fmaxf(a, partials[i].x);
+        b = fmaxf(b, partials[i].y);
+    }
+    float na = -a;
+    block_minmax(na, b);
+    if (threadIdx.x == 0)
+    {
+        reinterpret_cast<float2*>(J.d.minmax)[0] = make_float2(-na, b);
+        if (fold)
+            fold_one(J.d, 0, !J.hist);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void fold_minmax_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
+{
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j < njobs)
+        fold_one(jobs[j].d, 0, !jobs[j].hist);
+}
+
+__global__ __launch_bounds__(kBlock) void histogram_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
+{
+    const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, true)];
+    if (!J.hist || !J.d.pdf_init[0])
+        return;
+    histogram_part<kBlock>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
+}
+
+__global__ __launch_bounds__(kPdfSize) void fold_histogram_many_kernel(const StatsJob* __restrict__ jobs)
+{
+    const StatsJob& J = jobs[blockIdx.x];
+    if (J.hist && J.d.pdf_init[0])
+        fold_hist_one(J.d, 0, J.count);
 }
 
 inline int grid_for_channels(int64_t C)
@@ -487,6 +589,53 @@ void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStrea
 {
     fold_histogram_kernel<<<grid_for_channels(C), kPdfSize, 0, s>>>(d, C, count);
     AIMET_LAUNCH_CHECK();
+}
+
+void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
+{
+    if (jobs.empty())
+        return;
+    uint64_t mm = 0, hb = 0;
+    for (auto& j: jobs)
+    {
+        j.mm_block0 = (uint32_t) mm;
+        j.mm_blocks = (uint32_t) (j.n > 0 ? std::min<int64_t>(kMinmaxParts, ceil_div(j.n, (int64_t) kBlock * 16))
+                                          : 1);
+        j.h_block0  = (uint32_t) hb;
+        // ~32K elements per workgroup, at most 2048 workgroups per tensor
+        j.h_blocks  = (uint32_t) (j.hist ? std::max<int64_t>(1, std::min<int64_t>(kHistGrid, ceil_div(j.n, 32768)))
+                                         : 0);
+        mm += j.mm_blocks;
+        hb += j.h_blocks;
+    }
+    AIMET_REQUIRE(mm < (uint64_t(1) << 31) && hb < (uint64_t(1) << 31), "too many workgroups");
+    const int n = (int) jobs.size();
+    StatsJob* dj = nullptr;
+    AIMET_HIP_CHECK(hipMallocAsync((void**) &dj, sizeof(StatsJob) * n, s));
+    AIMET_HIP_CHECK(hipMemcpyAsync(dj, jobs.data(), sizeof(StatsJob) * n, hipMemcpyHostToDevice, s));
+    if (phases & kPhaseMinmax)
+    {
+        minmax_many_kernel<<<(unsigned) mm, kBlock, 0, s>>>(dj, n);
+        AIMET_LAUNCH_CHECK();
+        combine_many_kernel<<<n, kBlock, 0, s>>>(dj, (phases & kPhaseFoldMinmax) ? 1 : 0);
+        AIMET_LAUNCH_CHECK();
+    }
+    else if (phases & kPhaseFoldMinmax)
+    {
+        fold_minmax_many_kernel<<<(unsigned) ceil_div(n, kBlock), kBlock, 0, s>>>(dj, n);
+        AIMET_LAUNCH_CHECK();
+    }
+    if ((phases & kPhaseHistogram) && hb > 0)
+    {
+        histogram_many_kernel<<<(unsigned) hb, kBlock, 0, s>>>(dj, n);
+        AIMET_LAUNCH_CHECK();
+    }
+    if (phases & kPhaseFoldHistogram)
+    {
+        fold_histogram_many_kernel<<<n, kPdfSize, 0, s>>>(dj);
+        AIMET_LAUNCH_CHECK();
+    }
+    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
 }
 
 void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s)

@@ -8,6 +8,8 @@
 
 #include "common.hpp"
 
+#include <vector>
+
 namespace aimet_amd
 {
 
@@ -41,6 +43,24 @@ void launch_fold_minmax(const TqDevice& d, int64_t C, bool tf_scheme, hipStream_
 void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, hipStream_t s);
 void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStream_t s);
 void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s);
+// Many per-tensor quantizers (C == 1) in one launch per phase (stats.hip: launch_stats_many)
+struct StatsJob
+{
+    const float* x;
+    int64_t n;       // elements of this quantizer's tensor
+    int64_t count;   // element count of the PDF fold (the global count when sharded)
+    TqDevice d;
+    uint32_t mm_block0, mm_blocks, h_block0, h_blocks;   // filled by launch_stats_many
+    int32_t hist, vec;
+};
+enum StatsPhase
+{
+    kPhaseMinmax        = 1,   // min/max pass + combine into minmax[0]
+    kPhaseFoldMinmax    = 2,   // TF running min/max / PDF range initialisation
+    kPhaseHistogram     = 4,
+    kPhaseFoldHistogram = 8
+};
+void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s);
 // tfe_search.hip
 // d.enc[c] <- TF-Enhanced encoding of channel c (statistics updated; see aimet_tq_get_encoding)
 void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);

@@ -81,24 +81,45 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
     ch_axes = ch_axes or [0] * len(quantizers)
     world = _world(group)
 
-    for q, t, ax in zip(quantizers, tensors, ch_axes):
-        q.batch_minmax(t, ax)
+    # per-tensor AimetTensorQuantizers: one launch per phase for all of them (aimet_tq_*_many)
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    many = [i for i, q in enumerate(quantizers) if type(q) is AimetTensorQuantizer and q.num_channels == 1]
+    rest = [i for i in range(len(quantizers)) if i not in set(many)]
+    mq = [quantizers[i] for i in many]
+    mt = [tensors[i] for i in many]
+    hist_many = [i for i in many if quantizers[i].uses_histogram]
+
+    if mq:
+        AimetTensorQuantizer.batch_minmax_many(mq, mt)
+    for i in rest:
+        quantizers[i].batch_minmax(tensors[i], ch_axes[i])
     if world > 1:
         # {-min, max}: a single MAX reduces both ends exactly
         _all_reduce(exchange.minmax, dist.ReduceOp.MAX, group)
-    for q in quantizers:
-        q.fold_minmax()
+    if mq:
+        AimetTensorQuantizer.fold_minmax_many(mq)
+    for i in rest:
+        quantizers[i].fold_minmax()
 
-    hist = [(q, t, ax) for q, t, ax in zip(quantizers, tensors, ch_axes) if q.uses_histogram]
+    hist = [i for i in range(len(quantizers)) if quantizers[i].uses_histogram]
     if hist:
-        for q, t, ax in hist:
-            q.batch_histogram(t, ax)
-        local = [t.numel() // q.num_channels for q, t, _ in hist]
+        if hist_many:
+            AimetTensorQuantizer.batch_histogram_many([quantizers[i] for i in hist_many],
+                                                      [tensors[i] for i in hist_many])
+        for i in hist:
+            if i not in set(hist_many):
+                quantizers[i].batch_histogram(tensors[i], ch_axes[i])
+        local = [tensors[i].numel() // quantizers[i].num_channels for i in hist]
         if world > 1:
             _all_reduce(exchange.counts, dist.ReduceOp.SUM, group)
             counts = global_counts(local, device, group)
         else:
             counts = local
-        for (q, _, _), n in zip(hist, counts):
-            q.fold_histogram(n)
+        by_index = dict(zip(hist, counts))
+        if hist_many:
+            AimetTensorQuantizer.fold_histogram_many([quantizers[i] for i in hist_many],
+                                                     [by_index[i] for i in hist_many])
+        for i in hist:
+            if i not in set(hist_many):
+                quantizers[i].fold_histogram(by_index[i])
     return exchange

@@ -221,6 +221,59 @@ class AimetTensorQuantizer:
                          torch.cuda.current_stream(self._device).cuda_stream)
         return list(out), bool(valid.value)
 
+    # -- many per-tensor quantizers at once (aimet_tq_*_many: one launch per phase) ------------
+    @staticmethod
+    def _many(name, quantizers, tensors=None, counts=None):
+        qs = list(quantizers)
+        if not qs:
+            return
+        if any(q._num_channels != 1 for q in qs):
+            raise ValueError("the batched statistics entry points take per-tensor quantizers")
+        ts = None
+        if tensors is not None:
+            ts = [t if t.is_contiguous() else t.contiguous() for t in tensors]
+            for t in ts:
+                _require_gpu(t)
+            dev = ts[0].device
+            handles = [q._ensure(dev) for q in qs]
+        else:
+            dev = torch.device("cuda", qs[0]._device)
+            handles = [q._handle for q in qs]
+        n = len(qs)
+        args = [(ctypes.c_void_p * n)(*handles)]
+        if ts is not None:
+            args += [(ctypes.c_void_p * n)(*[t.data_ptr() for t in ts]),
+                     (ctypes.c_int64 * n)(*[t.numel() for t in ts])]
+        if counts is not None:
+            args.append((ctypes.c_int64 * n)(*[int(c) for c in counts]))
+        with torch.cuda.device(dev):
+            _native.call(name, *args, n, torch.cuda.current_stream(dev).cuda_stream)
+        if name in ("aimet_tq_update_stats_many", "aimet_tq_batch_minmax_many"):
+            for q in qs:
+                q._is_encoding_valid = True
+        return ts   # keep the contiguous copies alive until the caller synchronises
+
+    @staticmethod
+    def updateStatsMany(quantizers, tensors):
+        """updateStats(tensors[i]) for every (per-tensor) quantizer with one launch per phase."""
+        return AimetTensorQuantizer._many("aimet_tq_update_stats_many", quantizers, tensors)
+
+    @staticmethod
+    def batch_minmax_many(quantizers, tensors):
+        return AimetTensorQuantizer._many("aimet_tq_batch_minmax_many", quantizers, tensors)
+
+    @staticmethod
+    def fold_minmax_many(quantizers):
+        return AimetTensorQuantizer._many("aimet_tq_fold_minmax_many", quantizers)
+
+    @staticmethod
+    def batch_histogram_many(quantizers, tensors):
+        return AimetTensorQuantizer._many("aimet_tq_batch_histogram_many", quantizers, tensors)
+
+    @staticmethod
+    def fold_histogram_many(quantizers, counts):
+        return AimetTensorQuantizer._many("aimet_tq_fold_histogram_many", quantizers, counts=counts)
+
     @staticmethod
     def getEncodings(quantizers, bitwidth, use_symmetric_encodings, use_strict_symmetric,
                      use_unsigned_symmetric):

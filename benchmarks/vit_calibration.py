@@ -1,0 +1,144 @@
+"""Config 4 (BASELINE.json / SURVEY §8(d)): ViT-L/16 INT8 TF-Enhanced histogram calibration with
+the calibration batch sharded per sample across GPUs.
+
+  python benchmarks/vit_calibration.py                       # 1 GPU
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 \
+         benchmarks/vit_calibration.py                       # N GPUs (RCCL)
+
+256 images N(0,1) (seed 3), global batch 32 (8 calibration batches), each rank runs the forward
+on its 32/N images. Quantizers: one TF-Enhanced per-tensor activation quantizer per conv/linear
+output (+ the model input), as QuantizationSimModel places them for the default config. Per batch
+the ranks run the device statistics (min/max on the first batch, 512-bin histogram, PDF fold) and
+exchange them with ONE all_reduce(MAX) + ONE all_reduce(SUM) of the packed buffers
+(aimet_amd.distributed). Reported (rank 0, one JSON line):
+  * stats Gelem/s per GPU and aggregate (elements histogrammed / time of the statistics path,
+    forward excluded, HIP events + max over ranks),
+  * time inside the two collectives, forward time,
+  * encodings identical on every rank (all_gather of a digest) and, at N=1, bit-identical to the
+    CPU oracle fed the same tensors for the first --oracle-check quantizers.
+"""
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--images", type=int, default=256)
+    ap.add_argument("--batch", type=int, default=32, help="global calibration batch")
+    ap.add_argument("--oracle-check", type=int, default=3)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    from aimet_amd import distributed as D
+    from aimet_amd.libpymo import QuantizationMode
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    from workloads.vit import vit_l16
+
+    model = vit_l16(seed=0, device=dev)
+    layers = [m for m in model.modules() if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear))]
+    quantizers = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in range(len(layers) + 1)]
+    acts = []
+    hooks = [m.register_forward_hook(lambda mod, i, o: acts.append(o)) for m in layers]
+    per_rank = args.batch // world
+    g = torch.Generator().manual_seed(3)
+    images = torch.randn(args.images, 3, 224, 224, generator=g)       # the same 256 images on every rank
+    check = [] if (world > 1 or args.oracle_check <= 0) else [[] for _ in range(args.oracle_check)]
+
+    stream = torch.cuda.current_stream(dev)
+    t_fwd = t_stats = t_coll = 0.0
+    elems = 0
+    ex = None
+    for b0 in range(0, args.images, args.batch):
+        x = images[b0 + rank * per_rank: b0 + (rank + 1) * per_rank].to(dev)
+        acts.clear()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        with torch.no_grad():
+            model(x)
+        torch.cuda.synchronize()
+        t_fwd += time.perf_counter() - t0
+        tensors = [x] + [a.contiguous() for a in acts]
+        elems += sum(t.numel() for t in tensors)
+        for i, lst in enumerate(check):
+            lst.append(tensors[i].cpu().numpy().ravel())
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        ex = D.sharded_update_stats(quantizers, tensors, exchange=ex)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        t_stats += e0.elapsed_time(e1) / 1e3
+        # the collectives alone (same packed buffers, values already reduced: MAX / SUM of zeros
+        # would change them, so time a copy of each buffer)
+        if world > 1:
+            mm, cnt = ex.minmax.clone(), ex.counts.clone()
+            c0 = torch.cuda.Event(enable_timing=True)
+            c1 = torch.cuda.Event(enable_timing=True)
+            c0.record(stream)
+            dist.all_reduce(mm, op=dist.ReduceOp.MAX)
+            dist.all_reduce(cnt, op=dist.ReduceOp.SUM)
+            c1.record(stream)
+            torch.cuda.synchronize()
+            t_coll += c0.elapsed_time(c1) / 1e3
+    for h in hooks:
+        h.remove()
+    encs = AimetTensorQuantizer.getEncodings(quantizers, 8, False, False, False)
+    digest = hashlib.sha256(json.dumps([e.to_tuple() for e, _ in encs]).encode()).hexdigest()
+
+    same = True
+    if world > 1:
+        tt = torch.tensor([t_stats, t_fwd, t_coll], device=dev, dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        t_stats, t_fwd, t_coll = (float(v) for v in tt)
+        digests = [None] * world
+        dist.all_gather_object(digests, digest)
+        same = all(d == digest for d in digests)
+    oracle_ok = None
+    if check:
+        from oracle import oracle as O
+        oracle_ok = True
+        for i, chunks in enumerate(check):
+            a = O.Analyzer(O.QUANTIZATION_TF_ENHANCED)
+            for c in chunks:
+                a.update(c)
+            oracle_ok &= encs[i][0].to_tuple() == a.compute(8).as_tuple()
+
+    if rank == 0:
+        per_gpu = elems / t_stats / 1e9
+        print(json.dumps({
+            "metric": "TF-Enhanced calibration statistics Gelem/s (ViT-L/16, batch sharded)",
+            "value": round(per_gpu * world, 3), "unit": "Gelem/s", "n_gpus": world,
+            "per_gpu_gelem_s": round(per_gpu, 3), "elements_per_rank": elems,
+            "stats_s": round(t_stats, 4), "collectives_s": round(t_coll, 4), "forward_s": round(t_fwd, 3),
+            "quantizers": len(quantizers), "images": args.images, "global_batch": args.batch,
+            "act_elems_per_image": round(elems * world / args.images),
+            "encodings_identical_across_ranks": same, "encodings_equal_cpu_oracle": oracle_ok,
+            "oracle_checked_quantizers": len(check),
+            "data": "synthetic N(0,1) images (seed 3), random-init ViT-L/16 (seed 0)"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

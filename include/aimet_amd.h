@@ -203,6 +203,22 @@ int aimet_tq_bind_exchange(aimet_tensor_quantizer* q, float* minmax_dev, uint64_
 /* Marks statistics as updated without touching data (a rank whose shard was empty). */
 int aimet_tq_mark_stats_updated(aimet_tensor_quantizer* q);
 
+/* The statistics update of MANY per-tensor quantizers (num_channels == 1, one device) with one
+ * launch per phase instead of ~5 per quantizer: a calibration batch of QuantizationSimModel
+ * (v1/qc_quantize_op.py:837-897 calls updateStats once per activation quantizer). Equivalent to
+ * aimet_tq_update_stats(qs[i], xs[i], 1, 1, ns[i], stream) for every i. */
+int aimet_tq_update_stats_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
+                               int64_t count, void* stream);
+/* The phases of it for the sharded calibration (same semantics as the single-quantizer phases):
+ * min/max (+ exchange buffer), fold, histogram (+ counts buffer), PDF fold with counts[i]. */
+int aimet_tq_batch_minmax_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
+                               int64_t count, void* stream);
+int aimet_tq_fold_minmax_many(aimet_tensor_quantizer* const* qs, int64_t count, void* stream);
+int aimet_tq_batch_histogram_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
+                                  int64_t count, void* stream);
+int aimet_tq_fold_histogram_many(aimet_tensor_quantizer* const* qs, const int64_t* counts, int64_t count,
+                                 void* stream);
+
 /* AimetTensorQuantizer.cpp:180-192 getEncoding -> IQuantizationEncodingAnalyzer::computeEncoding.
  * Synchronises `stream`. out[num_channels]; *valid mirrors _isEncodingValid. */
 int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int use_symmetric, int use_strict_symmetric,

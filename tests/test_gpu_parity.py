@@ -605,3 +605,37 @@ def test_qdq_and_histogram_near_rounding_boundaries():
         q.updateStats(gpu(x2), True)
         a.update(x2)
         np.testing.assert_array_equal(np.array([t[1] for t in q.getStatsHistogram()]), a.histogram()[1])
+
+
+def test_update_stats_many_equals_individual():
+    """aimet_tq_update_stats_many (one launch per phase for all quantizers) == updateStats per
+    quantizer: every scheme, sizes from 1 element to 2^22 (unaligned views, an all-zero first
+    batch, NaN / inf), three batches, then encodings and histograms bit-identical."""
+    rng = np.random.default_rng(12)
+    schemes = [QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
+               QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE]
+    sizes = [1, 3, 1000, 4097, 65536, 1 << 22]
+    specs = [(s, n) for s in schemes for n in sizes]
+    a = [AimetTensorQuantizer(s) for s, _ in specs]
+    b = [AimetTensorQuantizer(s) for s, _ in specs]
+    for q in a + b:
+        if q.quant_scheme == QuantizationMode.QUANTIZATION_PERCENTILE:
+            q.setPercentileValue(99.5)
+    for batch in range(3):
+        ts = []
+        for i, (s, n) in enumerate(specs):
+            x = (rng.standard_normal(n + 1) * (1 + batch + i % 3)).astype(np.float32)
+            if batch == 0 and i % 5 == 0:
+                x[:] = 0.0
+            if n > 100 and batch == 1:
+                x[7], x[8] = np.nan, np.inf
+            ts.append(gpu(x)[1:])          # 4-byte offset: exercises the scalar path
+        AimetTensorQuantizer.updateStatsMany(a, ts)
+        for q, t in zip(b, ts):
+            q.updateStats(t, True)
+    for fl in FLAGS:
+        for qa, qb in zip(a, b):
+            assert qa.getEncoding(8, *fl)[0].to_tuple() == qb.getEncoding(8, *fl)[0].to_tuple()
+    for qa, qb in zip(a, b):
+        if qa.quant_scheme != QuantizationMode.QUANTIZATION_TF:
+            assert qa.getStatsHistogram() == qb.getStatsHistogram()
