@@ -149,6 +149,10 @@ __device__ __forceinline__ float glibc_fmaxf(float x, float y)
     return (x > y || __builtin_isnan(y)) ? x : y;
 }
 
+// upload.cpp: stream-ordered device copy of a small host table without blocking the host
+// (pinned staging ring); release with hipFreeAsync(ptr, s) after the consuming launches.
+void* upload_async(const void* src, size_t bytes, hipStream_t s);
+
 struct QdqParams
 {
     float min, max, delta, offset;

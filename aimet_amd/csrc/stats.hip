@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cstdlib>
 #include <vector>
 
 namespace aimet_amd
@@ -591,6 +592,15 @@ void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStrea
     AIMET_LAUNCH_CHECK();
 }
 
+static int64_t hist_elems_per_block()
+{
+    static int64_t v = [] {
+        const char* e = getenv("AIMET_TUNE_HIST_ELEMS");   // tuning experiments only
+        return e ? atoll(e) : (int64_t) 131072;
+    }();
+    return v;
+}
+
 void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
 {
     if (jobs.empty())
@@ -602,17 +612,15 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
         j.mm_blocks = (uint32_t) (j.n > 0 ? std::min<int64_t>(kMinmaxParts, ceil_div(j.n, (int64_t) kBlock * 16))
                                           : 1);
         j.h_block0  = (uint32_t) hb;
-        // ~32K elements per workgroup, at most 2048 workgroups per tensor
-        j.h_blocks  = (uint32_t) (j.hist ? std::max<int64_t>(1, std::min<int64_t>(kHistGrid, ceil_div(j.n, 32768)))
+        j.h_blocks  = (uint32_t) (j.hist ? std::max<int64_t>(1, std::min<int64_t>(kHistGrid,
+                                                                               ceil_div(j.n, hist_elems_per_block())))
                                          : 0);
         mm += j.mm_blocks;
         hb += j.h_blocks;
     }
     AIMET_REQUIRE(mm < (uint64_t(1) << 31) && hb < (uint64_t(1) << 31), "too many workgroups");
     const int n = (int) jobs.size();
-    StatsJob* dj = nullptr;
-    AIMET_HIP_CHECK(hipMallocAsync((void**) &dj, sizeof(StatsJob) * n, s));
-    AIMET_HIP_CHECK(hipMemcpyAsync(dj, jobs.data(), sizeof(StatsJob) * n, hipMemcpyHostToDevice, s));
+    auto* dj = static_cast<StatsJob*>(upload_async(jobs.data(), sizeof(StatsJob) * n, s));
     if (phases & kPhaseMinmax)
     {
         minmax_many_kernel<<<(unsigned) mm, kBlock, 0, s>>>(dj, n);
