@@ -84,10 +84,15 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
     # per-tensor AimetTensorQuantizers: one launch per phase for all of them (aimet_tq_*_many)
     from aimet_amd.tensor_quantizer import AimetTensorQuantizer
     many = [i for i, q in enumerate(quantizers) if type(q) is AimetTensorQuantizer and q.num_channels == 1]
-    rest = [i for i in range(len(quantizers)) if i not in set(many)]
+    many_set = set(many)
+    rest = [i for i in range(len(quantizers)) if i not in many_set]
     mq = [quantizers[i] for i in many]
     mt = [tensors[i] for i in many]
-    hist_many = [i for i in many if quantizers[i].uses_histogram]
+
+    if world == 1 and not rest:
+        # nothing to exchange: the fused single-pass update (4 launches for all quantizers)
+        AimetTensorQuantizer.updateStatsMany(mq, mt)
+        return exchange
 
     if mq:
         AimetTensorQuantizer.batch_minmax_many(mq, mt)
@@ -103,12 +108,13 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
 
     hist = [i for i in range(len(quantizers)) if quantizers[i].uses_histogram]
     if hist:
+        hist_many = [i for i in many if quantizers[i].uses_histogram]
+        hist_rest = [i for i in hist if i not in many_set]
         if hist_many:
             AimetTensorQuantizer.batch_histogram_many([quantizers[i] for i in hist_many],
                                                       [tensors[i] for i in hist_many])
-        for i in hist:
-            if i not in set(hist_many):
-                quantizers[i].batch_histogram(tensors[i], ch_axes[i])
+        for i in hist_rest:
+            quantizers[i].batch_histogram(tensors[i], ch_axes[i])
         local = [tensors[i].numel() // quantizers[i].num_channels for i in hist]
         if world > 1:
             _all_reduce(exchange.counts, dist.ReduceOp.SUM, group)
@@ -119,7 +125,6 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
         if hist_many:
             AimetTensorQuantizer.fold_histogram_many([quantizers[i] for i in hist_many],
                                                      [by_index[i] for i in hist_many])
-        for i in hist:
-            if i not in set(hist_many):
-                quantizers[i].fold_histogram(by_index[i])
+        for i in hist_rest:
+            quantizers[i].fold_histogram(by_index[i])
     return exchange

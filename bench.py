@@ -95,11 +95,9 @@ def compute_encodings(acts, weights, world):
     aq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in acts]
     wq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=w.shape[0])
           for _, w in weights]
-    if world > 1:
-        D.sharded_update_stats(aq, [t for _, t in acts])
-    else:
-        for q, (_, t) in zip(aq, acts):
-            q.updateStats(t, True)
+    # every activation quantizer's statistics in one launch per phase (aimet_tq_*_many);
+    # with N ranks each phase's packed statistics are exchanged once (aimet_amd.distributed)
+    D.sharded_update_stats(aq, [t for _, t in acts])
     for q, (_, w) in zip(wq, weights):
         q.updateStatsPerChannel(w, 0, True)
     # getEncoding of every quantizer, batched: one device search launch + one sync per flag set

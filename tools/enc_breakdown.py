@@ -31,9 +31,15 @@ def main():
         aq = [AimetTensorQuantizer(TFE) for _ in acts]
         wq = [AimetTensorQuantizer(TFE, num_channels=w.shape[0]) for _, w in weights]
         t0 = mark("create", t0)
-        for q, (_, a) in zip(aq, acts):
-            q.updateStats(a, True)
-        t0 = mark("act_update", t0)
+        if rep == 0:
+            for q, (_, a) in zip(aq, acts):
+                q.updateStats(a, True)
+            t0 = mark("act_update_each", t0)
+            for q in aq:
+                q.resetEncodingStats()
+            t0 = mark("reset", t0)
+        AimetTensorQuantizer.updateStatsMany(aq, [a for _, a in acts])
+        t0 = mark("act_update_many", t0)
         for q, (_, w) in zip(wq, weights):
             q.updateStatsPerChannel(w, 0, True)
         t0 = mark("w_update", t0)
