@@ -69,7 +69,7 @@ def global_counts(local_counts, device, group=None):
     return t.tolist()
 
 
-def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange=None):
+def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange=None, fused=True):
     """One calibration batch: every rank passes ITS shard of each quantizer's tensor.
 
     Equivalent to ``q.updateStats(whole_batch_tensor)`` on one device for every quantizer."""
@@ -89,7 +89,7 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
     mq = [quantizers[i] for i in many]
     mt = [tensors[i] for i in many]
 
-    if world == 1 and not rest:
+    if world == 1 and not rest and fused:
         # nothing to exchange: the fused single-pass update (4 launches for all quantizers)
         AimetTensorQuantizer.updateStatsMany(mq, mt)
         return exchange

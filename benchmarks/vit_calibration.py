@@ -11,8 +11,8 @@ output (+ the model input), as QuantizationSimModel places them for the default 
 the ranks run the device statistics (min/max on the first batch, 512-bin histogram, PDF fold) and
 exchange them with ONE all_reduce(MAX) + ONE all_reduce(SUM) of the packed buffers
 (aimet_amd.distributed). Reported (rank 0, one JSON line):
-  * stats Gelem/s per GPU and aggregate (elements histogrammed / time of the statistics path,
-    forward excluded, HIP events + max over ranks),
+  * stats Gelem/s per GPU and aggregate (elements histogrammed / wall time of the statistics
+    path between two device synchronisations, forward excluded, max over ranks),
   * time inside the two collectives, forward time,
   * encodings identical on every rank (all_gather of a digest) and, at N=1, bit-identical to the
     CPU oracle fed the same tensors for the first --oracle-check quantizers.
@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--images", type=int, default=256)
     ap.add_argument("--batch", type=int, default=32, help="global calibration batch")
     ap.add_argument("--oracle-check", type=int, default=3)
+    ap.add_argument("--phased", action="store_true", help="single rank: run the sharded phases anyway")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -64,6 +65,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     t_fwd = t_stats = t_coll = 0.0
+    per_batch = []
     elems = 0
     ex = None
     for b0 in range(0, args.images, args.batch):
@@ -82,13 +84,11 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        ex = D.sharded_update_stats(quantizers, tensors, exchange=ex)
-        e1.record(stream)
+        t0 = time.perf_counter()
+        ex = D.sharded_update_stats(quantizers, tensors, exchange=ex, fused=not args.phased)
         torch.cuda.synchronize()
-        t_stats += e0.elapsed_time(e1) / 1e3
+        per_batch.append(time.perf_counter() - t0)
+        t_stats += per_batch[-1]
         # the collectives alone (same packed buffers, values already reduced: MAX / SUM of zeros
         # would change them, so time a copy of each buffer)
         if world > 1:
@@ -130,7 +130,8 @@ def main():
             "metric": "TF-Enhanced calibration statistics Gelem/s (ViT-L/16, batch sharded)",
             "value": round(per_gpu * world, 3), "unit": "Gelem/s", "n_gpus": world,
             "per_gpu_gelem_s": round(per_gpu, 3), "elements_per_rank": elems,
-            "stats_s": round(t_stats, 4), "collectives_s": round(t_coll, 4), "forward_s": round(t_fwd, 3),
+            "stats_s": round(t_stats, 4), "stats_ms_per_batch": [round(v * 1e3, 3) for v in per_batch],
+            "collectives_s": round(t_coll, 4), "forward_s": round(t_fwd, 3),
             "quantizers": len(quantizers), "images": args.images, "global_batch": args.batch,
             "act_elems_per_image": round(elems * world / args.images),
             "encodings_identical_across_ranks": same, "encodings_equal_cpu_oracle": oracle_ok,
