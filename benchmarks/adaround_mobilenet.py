@@ -1,0 +1,166 @@
+"""Config 3 (BASELINE.json / SURVEY §8(d)): MobileNet-v2 W8 AdaRound on one GPU.
+
+For every conv / linear layer in order (53 layers): cache the layer's input from the model whose
+previous layers already carry their adarounded weights and the layer's output from the FP model
+over 1024 images U(0,1) (seed 7); then optimise the rounding with
+aimet_amd.adaround_optimizer (Adam on alpha, batch 32, 10k iterations, reg 0.01, beta 20->2,
+warm start 0.2, ReLU6 applied to both outputs when the layer feeds one); then write the
+hard-rounded weight. Weight encodings: 8-bit symmetric per-tensor TF-Enhanced (AIMET's AdaRound
+default) from the device analyzers.
+
+Reported (one JSON line): total AdaRound wall-clock, mean ms per iteration, and the soft-quant
+kernels' HBM rates: forward 12 B/elem (W, alpha -> Wq) and backward + rounding loss 16 B/elem
+(g, W, alpha -> g_alpha), measured with HIP events on every layer's weight; with --reference-iters
+the same loop using the reference's torch-op soft quantization + rounding loss
+(oracle/torch_ref.py) for comparison.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iterations", type=int, default=10000)
+    ap.add_argument("--images", type=int, default=1024)
+    ap.add_argument("--layers", type=int, default=0, help="only the first N layers (0 = all)")
+    ap.add_argument("--reference-iters", type=int, default=0,
+                    help="also time N iterations per layer of the torch-op reference loop")
+    args = ap.parse_args()
+
+    from aimet_amd.adaround import AdaroundFunction, compute_beta, init_alpha
+    from aimet_amd.adaround_optimizer import (AdaroundHyperParameters, AdaroundOptimizer, layer_forward,
+                                              recon_loss)
+    from aimet_amd.libpymo import QuantizationMode
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    from workloads.mobilenet_v2 import mobilenet_v2
+
+    dev = torch.device("cuda", 0)
+    fp = mobilenet_v2(seed=0, device=dev)
+    qm = mobilenet_v2(seed=0, device=dev)     # receives the adarounded weights layer by layer
+    images = torch.rand(args.images, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(dev)
+    names = [n for n, m in fp.named_modules() if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear))]
+    if args.layers:
+        names = names[:args.layers]
+    mods_fp, mods_q = dict(fp.named_modules()), dict(qm.named_modules())
+    # the activation following each layer (AIMET applies it to both outputs)
+    follow = {}
+    for pname, parent in fp.named_modules():
+        kids = list(parent.named_children())
+        for (a, m), (_, nxt) in zip(kids, kids[1:]):
+            if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear)) and isinstance(nxt, torch.nn.ReLU6):
+                follow[(pname + "." + a) if pname else a] = nxt
+
+    def cache(model, name, want_input):
+        out = []
+        mod = dict(model.named_modules())[name]
+        h = mod.register_forward_hook(lambda m, i, o: out.append((i[0] if want_input else o).detach()))
+        with torch.no_grad():
+            for b in range(0, images.shape[0], 128):
+                model(images[b:b + 128])
+        h.remove()
+        return torch.cat(out)
+
+    params = AdaroundHyperParameters(num_iterations=args.iterations)
+    gen = torch.Generator().manual_seed(0)
+    loss_buf = torch.zeros(1, device=dev)
+    t_opt = t_cache = t_ref = 0.0
+    kern = []   # (elements, fwd_ms, bwd_ms) per layer
+    for name in names:
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        inp = cache(qm, name, True)
+        out = cache(fp, name, False)
+        torch.cuda.synchronize()
+        t_cache += time.perf_counter() - t0
+        m = mods_q[name]
+        w = m.weight.detach()
+        q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED)
+        q.updateStats(w.contiguous().view(-1), True)
+        e, _ = q.getEncoding(8, True, False, False)
+        d = torch.tensor([e.delta], dtype=torch.float32, device=dev)
+        o = torch.tensor([e.offset], dtype=torch.float32, device=dev)
+        act = follow.get(name)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        alpha = AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, params, act, gen, loss_buf)
+        torch.cuda.synchronize()
+        t_opt += time.perf_counter() - t0
+        with torch.no_grad():
+            m.weight.copy_(AdaroundOptimizer.hard_rounded_weight(m, alpha, d, o, 8))
+        # soft-quant kernel rates on this weight (HIP events, 20 launches each)
+        g = torch.randn_like(w)
+        a = alpha.detach()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        from aimet_amd import _native
+        stream = torch.cuda.current_stream().cuda_stream
+        wq, ga = torch.empty_like(w), torch.empty_like(w)
+        e0.record()
+        for _ in range(20):
+            _native.call("aimet_adaround_forward", w.data_ptr(), a.data_ptr(), wq.data_ptr(), 1, 1, w.numel(),
+                         d.data_ptr(), o.data_ptr(), 8, 1, stream)
+        e1.record()
+        torch.cuda.synchronize()
+        fwd_ms = e0.elapsed_time(e1) / 20
+        e0.record()
+        for _ in range(20):
+            _native.call("aimet_adaround_backward", w.data_ptr(), a.data_ptr(), g.data_ptr(), ga.data_ptr(), 1, 1,
+                         w.numel(), d.data_ptr(), o.data_ptr(), 8, 0.01, 10.0, loss_buf.data_ptr(), stream)
+        e1.record()
+        torch.cuda.synchronize()
+        kern.append((w.numel(), fwd_ms, e0.elapsed_time(e1) / 20))
+        if args.reference_iters:
+            from oracle import torch_ref as T
+            a_ref = init_alpha(w, d)
+            opt = torch.optim.Adam([a_ref])
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for it in range(args.reference_iters):
+                idx = torch.randperm(inp.shape[0], generator=gen)[:32].to(dev)
+                x, target = inp.index_select(0, idx), out.index_select(0, idx)
+                opt.zero_grad()
+                wq_r = T.adaround_forward(w, a_ref, d, o, 8)
+                qo = layer_forward(m, x, wq_r)
+                if act is not None:
+                    qo, target = act(qo), act(target)
+                loss = recon_loss(qo, target)
+                if it >= params.num_iterations * params.warm_start:
+                    beta = compute_beta(params.num_iterations, it, params.beta_range, params.warm_start)
+                    loss = loss + T.adaround_round_loss(a_ref, params.reg_param, beta)
+                loss.backward()
+                opt.step()
+            torch.cuda.synchronize()
+            t_ref += time.perf_counter() - t0
+        del inp, out
+
+    iters = args.iterations * len(names)
+    elems = sum(k[0] for k in kern)
+    fwd_t = sum(k[1] for k in kern)
+    bwd_t = sum(k[2] for k in kern)
+    res = {
+        "metric": "AdaRound wall-clock (MobileNet-v2, W8, all layers)",
+        "value": round(t_opt, 3), "unit": "s", "higher_is_better": False, "n_gpus": 1,
+        "layers": len(names), "iterations_per_layer": args.iterations, "images": args.images,
+        "ms_per_iteration": round(t_opt / iters * 1e3, 4), "activation_caching_s": round(t_cache, 3),
+        "weights_elems": elems,
+        "softquant_fwd_GBps": round(elems * 12 / (fwd_t * 1e-3) / 1e9, 1),
+        "softquant_bwd_roundloss_GBps": round(elems * 16 / (bwd_t * 1e-3) / 1e9, 1),
+        "softquant_fwd_bwd_us_per_iteration_all_layers": round((fwd_t + bwd_t) * 1e3, 2),
+        "data": "synthetic U(0,1) images (seed 7), random-init MobileNet-v2 with folded BN (seed 0)",
+    }
+    if args.reference_iters:
+        res["reference_torch_ops_ms_per_iteration"] = round(t_ref / (args.reference_iters * len(names)) * 1e3, 4)
+        res["speedup_vs_reference_loop"] = round(res["reference_torch_ops_ms_per_iteration"] /
+                                                 res["ms_per_iteration"], 2)
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

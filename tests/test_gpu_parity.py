@@ -639,3 +639,45 @@ def test_update_stats_many_equals_individual():
     for qa, qb in zip(a, b):
         if qa.quant_scheme != QuantizationMode.QUANTIZATION_TF:
             assert qa.getStatsHistogram() == qb.getStatsHistogram()
+
+
+def test_adaround_optimizer_matches_reference_loop():
+    """AdaroundOptimizer (fused soft-quant + rounding-loss kernels) follows the reference's loop
+    (torch-op soft quantization + AdaroundLoss, adaround_optimizer.py:181-218) iteration for
+    iteration: same Adam trajectory of alpha within fp32 tolerance, same hard rounding."""
+    from aimet_amd.adaround import compute_beta, init_alpha
+    from aimet_amd.adaround_optimizer import (AdaroundHyperParameters, AdaroundOptimizer, layer_forward,
+                                              recon_loss)
+    from oracle import torch_ref as T
+    torch.manual_seed(3)
+    conv = torch.nn.Conv2d(16, 24, 3, padding=1).to(DEV)
+    inp = torch.randn(256, 16, 12, 12, device=DEV)
+    with torch.no_grad():
+        out = conv(inp) + 0.01 * torch.randn(256, 24, 12, 12, device=DEV)
+    w = conv.weight.detach()
+    d = (w.abs().amax(dim=(1, 2, 3)) / 127).contiguous()
+    o = torch.full((24,), -128.0, device=DEV)
+    params = AdaroundHyperParameters(num_iterations=120, warm_start=0.25)
+    act = torch.nn.ReLU6()
+    a_ours = AdaroundOptimizer.optimize_rounding(conv, inp, out, d, o, 8, 0, params, act,
+                                                 torch.Generator().manual_seed(5))
+    # the reference loop
+    a_ref = init_alpha(w, d.view(-1, 1, 1, 1))
+    opt = torch.optim.Adam([a_ref])
+    g = torch.Generator().manual_seed(5)
+    for it in range(params.num_iterations):
+        idx = torch.randperm(256, generator=g)[:32].to(DEV)
+        x, target = inp.index_select(0, idx), out.index_select(0, idx)
+        opt.zero_grad()
+        qo = layer_forward(conv, x, T.adaround_forward(w, a_ref, d.view(-1, 1, 1, 1), o.view(-1, 1, 1, 1), 8))
+        loss = recon_loss(act(qo), act(target))
+        if it >= params.num_iterations * params.warm_start:
+            beta = compute_beta(params.num_iterations, it, params.beta_range, params.warm_start)
+            loss = loss + T.adaround_round_loss(a_ref, params.reg_param, beta)
+        loss.backward()
+        opt.step()
+    torch.testing.assert_close(a_ours.detach(), a_ref.detach(), rtol=1e-3, atol=2e-4)
+    hard_ours = AdaroundOptimizer.hard_rounded_weight(conv, a_ours, d, o, 8)
+    hard_ref = T.adaround_forward(w, torch.where(a_ref.detach() >= 0, 100.0, -100.0), d.view(-1, 1, 1, 1),
+                                  o.view(-1, 1, 1, 1), 8)
+    assert (hard_ours != hard_ref).float().mean() < 1e-3
