@@ -16,10 +16,14 @@ the rounding loss as a separate autograd graph. The rounding-loss VALUE is accum
 from dataclasses import dataclass
 from typing import Callable, Optional, Tuple
 
+import ctypes
+
 import torch
 import torch.nn.functional as F
 
+from aimet_amd import _native
 from aimet_amd.adaround import AdaroundFunction, compute_beta, init_alpha
+from aimet_amd.tensor_quantizer import per_channel_view
 
 BATCH_SIZE = 32   # adaround_optimizer.py:58
 
@@ -54,6 +58,58 @@ def recon_loss(quant_out: torch.Tensor, orig_out: torch.Tensor) -> torch.Tensor:
     return (torch.norm(quant_out - orig_out, p="fro", dim=1) ** 2).mean()
 
 
+class _BoundSoftQuant:
+    """The per-iteration soft quantization of ONE layer with every kernel argument bound once
+    (weight, alpha, delta, offset and the Wq / grad-alpha buffers keep their addresses for the
+    whole optimisation): a forward and a backward are one direct library call each, no per-call
+    Python argument marshalling (the loop is launch-bound for MobileNet-sized weights)."""
+
+    def __init__(self, w, alpha, d, o, bitwidth, ch_axis, round_loss_out):
+        lib = _native.load()
+        self.fwd, self.bwd = lib.aimet_adaround_forward, lib.aimet_adaround_backward
+        self.w, self.alpha = w.contiguous(), alpha
+        outer, C, K = per_channel_view(self.w.shape, ch_axis) if d.numel() > 1 else (1, 1, self.w.numel())
+        self.shape = (outer, C, K)
+        self.d, self.o = d.contiguous(), o.contiguous()
+        self.bw = int(bitwidth)
+        self.loss = round_loss_out
+        P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
+        self.pw, self.pa = P(self.w), P(alpha)
+        self.pd, self.po = P(self.d), P(self.o)
+        self.pl = P(round_loss_out) if round_loss_out is not None else None
+        self.stream = ctypes.c_void_p(torch.cuda.current_stream(self.w.device).cuda_stream)
+        self.reg = self.beta = 0.0
+
+    def forward(self):
+        wq = torch.empty_like(self.w)    # fresh outputs: autograd may keep / steal them
+        rc = self.fwd(self.pw, self.pa, ctypes.c_void_p(wq.data_ptr()), *self.shape, self.pd, self.po, self.bw, 1,
+                      self.stream)
+        if rc:
+            _native.check(rc)
+        return wq
+
+    def backward(self, grad):
+        g = grad if grad.is_contiguous() else grad.contiguous()
+        ga = torch.empty_like(self.w)
+        rc = self.bwd(self.pw, self.pa, ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(ga.data_ptr()), *self.shape,
+                      self.pd, self.po, self.bw, ctypes.c_float(self.reg), ctypes.c_float(self.beta),
+                      self.pl if self.reg != 0.0 else None, self.stream)
+        if rc:
+            _native.check(rc)
+        return ga
+
+
+class _SoftQuantFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, alpha, bound):
+        ctx.bound = bound
+        return bound.forward()
+
+    @staticmethod
+    def backward(ctx, grad):
+        return ctx.bound.backward(grad), None
+
+
 class AdaroundOptimizer:
     """v1/adaround/adaround_optimizer.py."""
 
@@ -72,20 +128,25 @@ class AdaroundOptimizer:
         d = torch.as_tensor(delta, dtype=torch.float32, device=dev).reshape(-1)
         o = torch.as_tensor(offset, dtype=torch.float32, device=dev).reshape(-1)
         alpha = init_alpha(w, d.view(shape) if d.numel() > 1 else d)
-        optimizer = torch.optim.Adam([alpha])
+        # one Adam kernel per step (the reference's default multi-tensor Adam: same update rule)
+        try:
+            optimizer = torch.optim.Adam([alpha], fused=True)
+        except (RuntimeError, TypeError):
+            optimizer = torch.optim.Adam([alpha])
+        sq = _BoundSoftQuant(w, alpha, d, o, bitwidth, ch_axis, round_loss_out)
         n = inp_data.shape[0]
         warm = opt_params.num_iterations * opt_params.warm_start
         for it in range(opt_params.num_iterations):
-            idx = torch.randperm(n, generator=generator)[:BATCH_SIZE].to(dev)
+            idx = torch.randperm(n, generator=generator)[:BATCH_SIZE].to(dev, non_blocking=True)
             inp = inp_data.index_select(0, idx)
             target = out_data.index_select(0, idx)
             optimizer.zero_grad()
             if it < warm:
-                reg, beta = 0.0, 0.0
+                sq.reg, sq.beta = 0.0, 0.0
             else:
-                reg = opt_params.reg_param
-                beta = compute_beta(opt_params.num_iterations, it, opt_params.beta_range, opt_params.warm_start)
-            wq = AdaroundFunction.apply(w, alpha, d, o, bitwidth, ch_axis, True, reg, beta, round_loss_out)
+                sq.reg = opt_params.reg_param
+                sq.beta = compute_beta(opt_params.num_iterations, it, opt_params.beta_range, opt_params.warm_start)
+            wq = _SoftQuantFn.apply(alpha, sq)
             q_out = layer_forward(module, inp, wq)
             if act_func is not None:
                 q_out, target = act_func(q_out), act_func(target)
