@@ -1,0 +1,159 @@
+"""Config 5 (BASELINE.json / SURVEY §8(d)): Llama-3-8B W4A16 QAT with learned-grid (range
+learning) per-channel 4-bit symmetric weight quantizers, seq 2048, micro-batch 1 per GPU.
+
+  python benchmarks/llama_qat.py [--layers 32] [--impl fused|reference]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 benchmarks/llama_qat.py
+
+Every linear layer (q/k/v/o, gate/up/down, lm_head) quantize-dequantizes its fp32 master weight
+with learnable per-output-channel encoding_min / encoding_max (initialised from the TF analyzer),
+then runs its matmul in bf16 (torch.autocast); Adam (fused) updates weights and encodings.
+  --impl fused      aimet_amd's learned-grid kernels (one forward pass, one backward pass per weight)
+  --impl reference  the reference's torch-op QuantizeDequantizeFunc (v1/tensor_quantizer.py:896-986 over
+                    quantsim_straight_through_grad.py:121-347, restated in oracle/torch_ref.py)
+Unit of work = weight QDQ + STE elements per step (forward + backward over all linear weights).
+Synthetic data: random token ids, random-init weights N(0, 0.02) (seed 0).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+import torch.nn.functional as F
+from torch import nn
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+BITWIDTH = 4
+
+
+class RefLearnedGrid(torch.autograd.Function):
+    """The reference's QuantizeDequantizeFunc with symmetric per-channel encodings: forward saves
+    the mask and x_quant, backward = symmetric_gradients (quantsim_straight_through_grad.py)."""
+
+    @staticmethod
+    def forward(ctx, x, emin, emax):
+        from oracle import torch_ref as T
+        y, mask, x_quant, delta, offset, steps = T.lg_forward(x, emin, emax, BITWIDTH, True)
+        ctx.save_for_backward(x, mask, x_quant, delta, offset)
+        ctx.steps = steps
+        return y
+
+    @staticmethod
+    def backward(ctx, grad):
+        x, mask, x_quant, delta, offset = ctx.saved_tensors
+        grad_x = mask * grad
+        gmax = ((x_quant + offset) * grad).sum(dim=1) - (mask * (x / delta) * grad).sum(dim=1)
+        gmax = gmax / torch.div(ctx.steps, 2, rounding_mode="floor")
+        return grad_x, -gmax, gmax
+
+
+class QatLinear(nn.Module):
+    impl = "fused"
+
+    def __init__(self, fin, fout):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(fout, fin))
+        self.encoding_min = nn.Parameter(torch.empty(fout))
+        self.encoding_max = nn.Parameter(torch.empty(fout))
+
+    def forward(self, x):
+        if QatLinear.impl == "fused":
+            from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
+            wq = LearnedGridQuantizeDequantize.apply(self.weight, self.encoding_min, self.encoding_max, BITWIDTH, True,
+                                                     False, False, 0)
+        else:
+            wq = RefLearnedGrid.apply(self.weight, self.encoding_min, self.encoding_max)
+        return F.linear(x, wq)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=2048)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--impl", choices=["fused", "reference"], default="fused")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    from aimet_amd.libpymo import QuantizationMode
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    from workloads.llama import Llama
+
+    QatLinear.impl = args.impl
+    torch.manual_seed(0)
+    with torch.device(dev):
+        model = Llama(QatLinear, layers=args.layers)
+    qlin = [m for m in model.modules() if isinstance(m, QatLinear)]
+    with torch.no_grad():
+        g = torch.Generator(device=dev).manual_seed(0)
+        model.embed_tokens.weight.normal_(0, 0.02, generator=g)
+        for m in qlin:
+            m.weight.normal_(0, 0.02, generator=g)
+            # TF per-channel symmetric init of the learnable range (QuantSim compute_encodings)
+            q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF, num_channels=m.weight.shape[0])
+            q.updateStatsPerChannel(m.weight, 0, True)
+            encs, _ = q.getEncoding(BITWIDTH, True, False, False)
+            m.encoding_min.copy_(torch.tensor([e.min for e in encs], dtype=torch.float32))
+            m.encoding_max.copy_(torch.tensor([e.max for e in encs], dtype=torch.float32))
+    n_weights = sum(m.weight.numel() for m in qlin)
+    ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local]) if world > 1 else model
+    try:
+        opt = torch.optim.Adam(model.parameters(), lr=1e-5, fused=True)
+    except (RuntimeError, TypeError):
+        opt = torch.optim.Adam(model.parameters(), lr=1e-5)
+    vocab = model.lm_head.weight.shape[0]
+    gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+
+    def step():
+        ids = torch.randint(vocab, (1, args.seq + 1), device=dev, generator=gen)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            logits = ddp(ids[:, :-1])
+        loss = F.cross_entropy(logits.float().view(-1, vocab), ids[:, 1:].reshape(-1))
+        loss.backward()
+        opt.step()
+        opt.zero_grad(set_to_none=True)
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    if rank == 0:
+        ms = dt / args.steps * 1e3
+        print(json.dumps({
+            "metric": "Llama-3-8B W4A16 learned-grid QAT step (weight QDQ + STE elements / s)",
+            "value": round(2 * n_weights * world / (ms * 1e-3) / 1e9, 3), "unit": "Gelem/s", "n_gpus": world,
+            "impl": args.impl, "ms_per_step": round(ms, 2), "layers": args.layers, "seq_len": args.seq,
+            "micro_batch": 1, "quantized_weight_elems": n_weights, "final_loss": round(float(loss), 4),
+            "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1),
+            "data": "synthetic token ids, random-init weights N(0, 0.02) (seed 0)"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
