@@ -148,7 +148,7 @@ def main():
             "metric": "Llama-3-8B W4A16 learned-grid QAT step (weight QDQ + STE elements / s)",
             "value": round(2 * n_weights * world / (ms * 1e-3) / 1e9, 3), "unit": "Gelem/s", "n_gpus": world,
             "impl": args.impl, "ms_per_step": round(ms, 2), "layers": args.layers, "seq_len": args.seq,
-            "micro_batch": 1, "quantized_weight_elems": n_weights, "final_loss": round(float(loss), 4),
+            "micro_batch": 1, "quantized_weight_elems": n_weights, "final_loss": round(loss.item(), 4),
             "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1),
             "data": "synthetic token ids, random-init weights N(0, 0.02) (seed 0)"}), flush=True)
     if world > 1:
