@@ -56,6 +56,8 @@ _PROTOTYPES = {
     "aimet_encoding_from_minmax": [ctypes.c_double, ctypes.c_double, _i32, _int, _int, _int, _enc_p],
     "aimet_encoding_from_histogram": [_int, _int, _int, ctypes.c_float, ctypes.c_double, _dp, ctypes.c_float, _i32,
                                       _int, _int, _int, _enc_p],
+    "aimet_encoding_from_entropy_histogram": [_int, _int, ctypes.c_double, ctypes.c_double, _dp, _i32, _int, _int,
+                                              _int, _enc_p],
     "aimet_qdq_per_tensor": [_vp, _vp, _i64, _enc_p, _int, ctypes.c_uint64, _vp],
     "aimet_quantize_per_tensor": [_vp, _vp, _i64, _enc_p, _int, _int, ctypes.c_uint64, _vp],
     "aimet_per_channel_table": [_enc_p, _i64, _vp, _vp],
@@ -93,6 +95,7 @@ _PROTOTYPES = {
     "aimet_tq_get_encodings": [ctypes.POINTER(_vp), _i64, ctypes.c_uint32, _int, _int, _int, _enc_p,
                                ctypes.POINTER(_int), _vp],
     "aimet_tq_get_stats_histogram": [_vp, _i64, _dp, _dp, ctypes.POINTER(_int), _vp],
+    "aimet_tq_get_entropy_state": [_vp, _i64, _dp, _dp, ctypes.POINTER(_int), ctypes.POINTER(_int), _vp],
     "aimet_tq_num_channels": [_vp, ctypes.POINTER(_i64)],
     "aimet_tq_quant_scheme": [_vp, ctypes.POINTER(_int)],
     "aimet_lg_forward": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_float, _vp],

@@ -113,4 +113,16 @@ int aimet_encoding_from_histogram(int scheme, int initialized, int stats_updated
     });
 }
 
+int aimet_encoding_from_entropy_histogram(int has_histogram, int stats_updated, double tpp_min, double tpp_max,
+                                          const double* hist, int32_t bw, int sym, int strict, int unsign,
+                                          aimet_tf_encoding* out)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(out != nullptr, "output is null");
+        AIMET_REQUIRE(!has_histogram || hist != nullptr, "histogram is null");
+        *out = entropy_encoding(has_histogram != 0, stats_updated != 0, tpp_min, tpp_max, hist,
+                                (int32_t) (uint8_t) bw, sym != 0, strict != 0, unsign != 0);
+    });
+}
+
 }   // extern "C"

@@ -19,7 +19,8 @@ struct aimet_tensor_quantizer
     int device       = 0;
     float percentile = 100.0f;   // PercentileEncodingAnalyzer.h:100
     bool stats_updated = false;  // AimetTensorQuantizer::_isEncodingValid / analyzer _statsUpdated
-    bool hist        = false;    // histogram-based analyzer (TF-E, percentile, MSE)
+    bool hist        = false;    // histogram-based analyzer (TF-E, percentile, MSE, entropy)
+    StatsKind kind   = kKindTf;
     void* arena      = nullptr;
     size_t arena_bytes = 0;
     TqDevice d {};
@@ -69,6 +70,7 @@ void layout(aimet_tensor_quantizer* q, bool assign)
     q->d.bucket_size = (double*) take(sizeof(double) * C);
     q->d.bin_bucket  = (float*) take(sizeof(float) * C);
     q->d.bin_offset  = (float*) take(sizeof(float) * C);
+    q->d.active      = (int32_t*) take(sizeof(int32_t) * C);
     if (q->hist)
     {
         q->d.pdf    = (double*) take(sizeof(double) * kPdfSize * C);
@@ -152,15 +154,15 @@ int aimet_tq_create(int scheme, int64_t num_channels, int device, aimet_tensor_q
         AIMET_REQUIRE(num_channels >= 1, "num_channels must be >= 1");
         if (scheme == AIMET_QUANTIZATION_RANGE_LEARNING)   // QuantizerFactory.cpp:93-96
             scheme = AIMET_QUANTIZATION_TF;
-        if (scheme == AIMET_QUANTIZATION_ENTROPY)
-            throw RuntimeError("QUANTIZATION_ENTROPY is not implemented by the MI355X core (SURVEY §8(f) row 3)");
-        AIMET_REQUIRE(scheme >= AIMET_QUANTIZATION_TF && scheme <= AIMET_QUANTIZATION_MSE, "Unknown quant scheme");
+        AIMET_REQUIRE(scheme >= AIMET_QUANTIZATION_TF && scheme <= AIMET_QUANTIZATION_ENTROPY, "Unknown quant scheme");
         DeviceGuard g(device);
         auto* q   = new aimet_tensor_quantizer();
         q->scheme = scheme;
         q->C      = num_channels;
         q->device = device;
         q->hist   = scheme != AIMET_QUANTIZATION_TF;
+        q->kind   = scheme == AIMET_QUANTIZATION_TF ? kKindTf
+                    : scheme == AIMET_QUANTIZATION_ENTROPY ? kKindEntropy : kKindPdf;
         layout(q, false);
         hipError_t e = hipMalloc(&q->arena, q->arena_bytes);
         if (e != hipSuccess)
@@ -233,7 +235,7 @@ int aimet_tq_batch_minmax(aimet_tensor_quantizer* q, const float* x, int64_t out
         if (outer * K > 0)
             require_device_ptr(x, "input");
         DeviceGuard g(q->device);
-        launch_batch_minmax(q->d, x, outer, C, K, q->hist ? 1 : 0, as_stream(stream));
+        launch_batch_minmax(q->d, x, outer, C, K, q->kind == kKindPdf ? 1 : 0, as_stream(stream));
         q->stats_updated = true;
     });
 }
@@ -243,7 +245,7 @@ int aimet_tq_fold_minmax(aimet_tensor_quantizer* q, void* stream)
     return guarded([&] {
         AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
         DeviceGuard g(q->device);
-        launch_fold_minmax(q->d, q->C, !q->hist, as_stream(stream));
+        launch_fold_minmax(q->d, q->C, q->kind, as_stream(stream));
     });
 }
 
@@ -257,7 +259,7 @@ int aimet_tq_batch_histogram(aimet_tensor_quantizer* q, const float* x, int64_t 
         if (outer * K > 0)
             require_device_ptr(x, "input");
         DeviceGuard g(q->device);
-        launch_batch_histogram(q->d, x, outer, C, K, as_stream(stream));
+        launch_batch_histogram(q->d, x, outer, C, K, q->kind, as_stream(stream));
     });
 }
 
@@ -269,7 +271,7 @@ int aimet_tq_fold_histogram(aimet_tensor_quantizer* q, int64_t count, void* stre
         if (!q->hist)
             return;
         DeviceGuard g(q->device);
-        launch_fold_histogram(q->d, q->C, count, as_stream(stream));
+        launch_fold_histogram(q->d, q->C, count, q->kind, as_stream(stream));
     });
 }
 
@@ -282,12 +284,12 @@ int aimet_tq_update_stats(aimet_tensor_quantizer* q, const float* x, int64_t out
             require_device_ptr(x, "input");
         DeviceGuard g(q->device);
         hipStream_t s = as_stream(stream);
-        launch_batch_minmax(q->d, x, outer, C, K, q->hist ? 1 : 0, s);
-        launch_fold_minmax(q->d, q->C, !q->hist, s);
+        launch_batch_minmax(q->d, x, outer, C, K, q->kind == kKindPdf ? 1 : 0, s);
+        launch_fold_minmax(q->d, q->C, q->kind, s);
         if (q->hist)
         {
-            launch_batch_histogram(q->d, x, outer, C, K, s);
-            launch_fold_histogram(q->d, q->C, outer * K, s);
+            launch_batch_histogram(q->d, x, outer, C, K, q->kind, s);
+            launch_fold_histogram(q->d, q->C, outer * K, q->kind, s);
         }
         q->stats_updated = true;
     });
@@ -320,6 +322,7 @@ std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* 
         AIMET_REQUIRE(j.count >= 0, "negative element count");
         j.d     = q->d;
         j.hist  = q->hist ? 1 : 0;
+        j.ent   = q->kind == kKindEntropy ? 1 : 0;
         j.vec   = (reinterpret_cast<uintptr_t>(j.x) & 15) == 0 ? 1 : 0;
     }
     return jobs;
@@ -447,6 +450,18 @@ void collect_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict,
         });
         return;
     }
+    if (q->kind == kKindEntropy)
+    {
+        // TensorProfilingParams back (16 + 4 KiB per channel); the KL search runs on the host
+        auto init = d2h(q->d.pdf_init, C);
+        auto acc  = d2h(q->d.acc, 2 * C);
+        auto hist = d2h(q->d.pdf, (size_t) kPdfSize * C);
+        parallel_channels(C, [&](int64_t c) {
+            out[c] = entropy_encoding(init[c] != 0, true, acc[2 * c], acc[2 * c + 1], hist.data() + kPdfSize * c, b,
+                                      sym, strict, unsign);
+        });
+        return;
+    }
     if (device_search(q))
     {
         // candidate search ran on the device (tfe_search.hip / mse_search.hip): only the
@@ -546,6 +561,9 @@ int aimet_tq_get_stats_histogram(aimet_tensor_quantizer* q, int64_t channel, dou
         AIMET_REQUIRE(channel >= 0 && channel < q->C, "channel out of range");
         if (!q->hist)
             throw RuntimeError("the TF encoding analyzer keeps no histogram (TfEncodingAnalyzer.cpp:53-57)");
+        if (q->kind == kKindEntropy)   // EntropyEncodingAnalyzer.cpp:56-78 returns a malformed PDF
+            throw RuntimeError("getStatsHistogram is only defined for the PDF analyzers (TF-Enhanced, percentile, "
+                               "MSE); v1/tensor_quantizer.py:366 allows it for TF-Enhanced only");
         DeviceGuard g(q->device);
         AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
         int32_t init = 0;
@@ -561,6 +579,28 @@ int aimet_tq_get_stats_histogram(aimet_tensor_quantizer* q, int64_t channel, dou
                                   hipMemcpyDeviceToHost));
         histogram_xleft(hmin, bs, xleft);
         *n = kPdfSize;
+    });
+}
+
+int aimet_tq_get_entropy_state(aimet_tensor_quantizer* q, int64_t channel, double* minmax, double* hist,
+                               int* has_hist, int* iterations, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(q && minmax && hist && has_hist && iterations, "null argument");
+        AIMET_REQUIRE(channel >= 0 && channel < q->C, "channel out of range");
+        AIMET_REQUIRE(q->kind == kKindEntropy, "not an entropy quantizer");
+        DeviceGuard g(q->device);
+        AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
+        int32_t init = 0, it = 0;
+        AIMET_HIP_CHECK(hipMemcpy(&init, q->d.pdf_init + channel, sizeof(int32_t), hipMemcpyDeviceToHost));
+        AIMET_HIP_CHECK(hipMemcpy(&it, q->d.iterations + channel, sizeof(int32_t), hipMemcpyDeviceToHost));
+        AIMET_HIP_CHECK(hipMemcpy(minmax, q->d.acc + 2 * channel, 2 * sizeof(double), hipMemcpyDeviceToHost));
+        AIMET_HIP_CHECK(hipMemcpy(hist, q->d.pdf + kPdfSize * channel, kPdfSize * sizeof(double),
+                                  hipMemcpyDeviceToHost));
+        if (!init)   // a value-initialised TensorProfilingParams (the TF reset values live there)
+            minmax[0] = minmax[1] = 0.0;
+        *has_hist   = init;
+        *iterations = it;
     });
 }
 

@@ -16,6 +16,7 @@
 //     updateStats call is 2-4 stream-ordered launches with no host synchronisation.
 //   * per-channel: all channels in one launch, one workgroup per channel.
 // Arithmetic follows the reference CPU code bit for bit (DTYPE = float; see common.hpp).
+#include "entropy_core.hpp"
 #include "tq_state.hpp"
 
 #include <algorithm>
@@ -253,13 +254,112 @@ __global__ __launch_bounds__(kBlock) void fold_minmax_kernel(TqDevice d, int64_t
         fold_one(d, c, tf_scheme != 0);
 }
 
+// ---- entropy analyzer: TensorProfilingParams (math_functions.cpp:476-560) ---------------------
+// Per batch, for channel c and the (exchanged) batch min/max: an all-zero batch is skipped
+// (:482-487), the first batch fixes the range (:496-501), a batch outside the range widens it and
+// redistributes the 512 bins (:503-550), and the batch is binned with the float (binWidth, min)
+// of :552-558. Bin counts are integers (doubles < 2^53 in the reference), so the redistribution is
+// accumulated in 64-bit integers: exact and independent of the order of the adds. Any blockDim;
+// mnf / mxf must be uniform over the block.
+__device__ void ent_fold_one(const TqDevice& d, int64_t c, float mnf, float mxf)
+{
+    using entropy::get_bin;
+    using entropy::x86_d2u64;
+    __shared__ unsigned long long scaled[kPdfSize];
+    double minInput = mnf, maxInput = mxf;
+    if (minInput == 0 && maxInput == 0)
+    {
+        if (threadIdx.x == 0)
+            d.active[c] = 0;
+        return;
+    }
+    if (minInput == maxInput)
+    {
+        double t = minInput + (double) 0.01f;   // minInput + (DTYPE) 0.01
+        maxInput = (maxInput < t) ? t : maxInput;
+    }
+    double2* acc = reinterpret_cast<double2*>(d.acc);
+    double2 a    = acc[c];
+    if (!d.pdf_init[c])
+    {
+        a.x = minInput;
+        a.y = maxInput;
+    }
+    if (minInput < a.x || maxInput > a.y)
+    {
+        const double newMin = (a.x < minInput) ? a.x : minInput;    // std::min(minInput, tpp.min)
+        const double newMax = (maxInput < a.y) ? a.y : maxInput;    // std::max(maxInput, tpp.max)
+        const double dstW   = (newMax - newMin) / kPdfSize;
+        const double srcW   = (a.y - a.x) / kPdfSize;
+        const float dstWf = (float) dstW, newMinf = (float) newMin;
+        for (int i = threadIdx.x; i < kPdfSize; i += blockDim.x)
+            scaled[i] = 0;
+        __syncthreads();
+        double* hist = d.pdf + c * kPdfSize;
+        for (int i = threadIdx.x; i < kPdfSize; i += blockDim.x)
+        {
+            const double h = hist[i];
+            if (h == 0)
+                continue;
+            const double begin  = a.x + srcW * (double) i;
+            const uint64_t dbin = x86_d2u64((begin - newMin) / dstW);
+            const double dend   = newMin + dstW * (double) (dbin + 1);
+            double cnt          = __builtin_round((dend - begin) / srcW * h);
+            cnt                 = (h < cnt) ? h : cnt;
+            if (!(__builtin_fabs(cnt) < 9.0e15))   // non-finite ranges (inf inputs): see DESIGN.md
+                cnt = h;
+            atomicAdd(&scaled[get_bin(dstWf, newMinf, (float) begin)], (unsigned long long) (long long) cnt);
+            if (cnt < h)
+                atomicAdd(&scaled[get_bin(dstWf, newMinf, (float) (begin + dstW))],
+                          (unsigned long long) (long long) (h - cnt));
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < kPdfSize; i += blockDim.x)
+            hist[i] = (double) (long long) scaled[i];
+        a.x = newMin;
+        a.y = newMax;
+    }
+    __syncthreads();   // every lane has read acc / pdf_init
+    if (threadIdx.x == 0)
+    {
+        acc[c]          = a;
+        d.pdf_init[c]   = 1;
+        d.bin_bucket[c] = (float) ((a.y - a.x) / kPdfSize);   // float binWidth
+        d.bin_offset[c] = (float) a.x;                        // getBin's float minValue
+        d.active[c]     = 1;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void ent_fold_minmax_kernel(TqDevice d, int64_t C)
+{
+    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+    {
+        float2 m = reinterpret_cast<const float2*>(d.minmax)[c];
+        ent_fold_one(d, c, -m.x, m.y);
+        __syncthreads();
+    }
+}
+
+// histogram += this batch's counts; iterations++ (math_functions.cpp:554-559). Any blockDim.
+__device__ __forceinline__ void ent_fold_hist_one(const TqDevice& d, int64_t c)
+{
+    for (int i = threadIdx.x; i < kPdfSize; i += blockDim.x)
+    {
+        int64_t idx   = c * kPdfSize + i;
+        d.pdf[idx]    = d.pdf[idx] + (double) d.counts[idx];
+        d.counts[idx] = 0;
+    }
+    if (threadIdx.x == 0)
+        d.iterations[c] += 1;
+}
+
 // ---- histogram ----------------------------------------------------------------------------
 // GetHistogram_cpu, math_functions.cpp:367-384: index = round(x / bucket - offset) in float,
 // out-of-range (and NaN) dropped.
-struct Binner
+struct PdfBinner
 {
     float bucket, offset, rcp;
-    __device__ Binner(float b, float o) : bucket(b), offset(o), rcp(1.0f / b) {}
+    __device__ PdfBinner(float b, float o) : bucket(b), offset(o), rcp(1.0f / b) {}
     __device__ __forceinline__ int bin(float x) const
     {
         // == roundf(x / bucket - offset) bit for bit (round_div_sub, common.hpp)
@@ -268,15 +368,31 @@ struct Binner
     }
 };
 
+// The binner of channel c: the PDF's (TF-E / percentile / MSE) or the entropy analyzer's
+template <bool ENT>
+struct BinnerOf;
+template <>
+struct BinnerOf<false>
+{
+    typedef PdfBinner type;
+    __device__ static bool live(const TqDevice& d, int64_t c) { return d.pdf_init[c] != 0; }
+};
+template <>
+struct BinnerOf<true>
+{
+    typedef entropy::Binner type;
+    __device__ static bool live(const TqDevice& d, int64_t c) { return d.active[c] != 0; }
+};
+
 // per-tensor: many workgroups over one tensor, atomics into counts[0][:]. One workgroup's share
 // (block `blk` of `nblk`) of the pass over x[0, n).
-template <int BLOCK>
+template <int BLOCK, bool ENT>
 __device__ __forceinline__ void histogram_part(const float* __restrict__ x, int64_t n, int vec, int64_t blk,
                                                int64_t nblk, const TqDevice& d)
 {
     constexpr int kWaves = BLOCK / 64;
     __shared__ uint32_t lds[kWaves][kPdfSize];
-    Binner bn {d.bin_bucket[0], d.bin_offset[0]};
+    typename BinnerOf<ENT>::type bn {d.bin_bucket[0], d.bin_offset[0]};
     const int w = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < kWaves * kPdfSize; i += BLOCK)
         (&lds[0][0])[i] = 0;
@@ -312,7 +428,11 @@ __device__ __forceinline__ void histogram_part(const float* __restrict__ x, int6
 #pragma unroll
             for (int u = 0; u < kHistUnroll; ++u)
             {
-                add(v[u].x);   // NaN padding is dropped by the binner
+                // NaN padding is dropped by the PDF binner; the entropy binner counts NaN (last
+                // bin, as the reference), so there the padding is skipped explicitly
+                if (ENT && base + (int64_t) u * BLOCK >= nv)
+                    continue;
+                add(v[u].x);
                 add(v[u].y);
                 add(v[u].z);
                 add(v[u].w);
@@ -337,16 +457,17 @@ __device__ __forceinline__ void histogram_part(const float* __restrict__ x, int6
     }
 }
 
-template <int BLOCK>
+template <int BLOCK, bool ENT>
 __global__ __launch_bounds__(BLOCK) void histogram_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
                                                                  TqDevice d)
 {
-    if (!d.pdf_init[0])
+    if (!BinnerOf<ENT>::live(d, 0))
         return;
-    histogram_part<BLOCK>(x, n, vec, blockIdx.x, gridDim.x, d);
+    histogram_part<BLOCK, ENT>(x, n, vec, blockIdx.x, gridDim.x, d);
 }
 
 // per-channel: one workgroup per channel, counts written directly
+template <bool ENT>
 __global__ __launch_bounds__(kBlock) void histogram_channel_kernel(const float* __restrict__ x, int64_t outer,
                                                                    int64_t C, int64_t K, int vec, TqDevice d)
 {
@@ -354,9 +475,9 @@ __global__ __launch_bounds__(kBlock) void histogram_channel_kernel(const float* 
     const int w = threadIdx.x >> 6;
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
     {
-        if (!d.pdf_init[c])
+        if (!BinnerOf<ENT>::live(d, c))
             continue;
-        Binner bn {d.bin_bucket[c], d.bin_offset[c]};
+        typename BinnerOf<ENT>::type bn {d.bin_bucket[c], d.bin_offset[c]};
         for (int i = threadIdx.x; i < kWaves * kPdfSize; i += kBlock)
             (&lds[0][0])[i] = 0;
         __syncthreads();
@@ -435,6 +556,13 @@ __global__ __launch_bounds__(kPdfSize) void fold_histogram_kernel(TqDevice d, in
     }
 }
 
+__global__ __launch_bounds__(kPdfSize) void ent_fold_histogram_kernel(TqDevice d, int64_t C)
+{
+    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+        if (d.active[c])
+            ent_fold_hist_one(d, c);
+}
+
 __global__ __launch_bounds__(kBlock) void reset_acc_kernel(double* acc, int64_t C)
 {
     int64_t c = (int64_t) blockIdx.x * kBlock + threadIdx.x;
@@ -468,8 +596,8 @@ __device__ __forceinline__ int find_job(const StatsJob* __restrict__ jobs, int n
 __global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
 {
     const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, false)];
-    if (J.hist && J.d.pdf_init[0])
-        return;   // histogram schemes take min/max on the first (non-zero) batch only
+    if (J.hist && !J.ent && J.d.pdf_init[0])
+        return;   // PDF schemes take min/max on the first (non-zero) batch only
     minmax_part(J.x, J.n, J.vec, blockIdx.x - J.mm_block0, J.mm_blocks, reinterpret_cast<float2*>(J.d.partials));
 }
 
@@ -477,7 +605,7 @@ __global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __r
 __global__ __launch_bounds__(kBlock) void combine_many_kernel(const StatsJob* __restrict__ jobs, int fold)
 {
     const StatsJob& J = jobs[blockIdx.x];
-    if (J.hist && J.d.pdf_init[0])
+    if (J.hist && !J.ent && J.d.pdf_init[0])
         return;
     const float2* partials = reinterpret_cast<const float2*>(J.d.partials);
     float a = -INFINITY, b = -INFINITY;
@@ -488,33 +616,59 @@ __global__ __launch_bounds__(kBlock) void combine_many_kernel(const StatsJob* __
     }
     float na = -a;
     block_minmax(na, b);
+    __shared__ float2 res;
     if (threadIdx.x == 0)
     {
-        reinterpret_cast<float2*>(J.d.minmax)[0] = make_float2(-na, b);
-        if (fold)
+        res = make_float2(-na, b);
+        reinterpret_cast<float2*>(J.d.minmax)[0] = res;
+        if (fold && !J.ent)
             fold_one(J.d, 0, !J.hist);
+    }
+    if (fold && J.ent)
+    {
+        __syncthreads();
+        ent_fold_one(J.d, 0, -res.x, res.y);
     }
 }
 
-__global__ __launch_bounds__(kBlock) void fold_minmax_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
+// one workgroup per quantizer (the entropy fold redistributes 512 bins)
+__global__ __launch_bounds__(kBlock) void fold_minmax_many_kernel(const StatsJob* __restrict__ jobs)
 {
-    const int j = blockIdx.x * kBlock + threadIdx.x;
-    if (j < njobs)
-        fold_one(jobs[j].d, 0, !jobs[j].hist);
+    const StatsJob& J = jobs[blockIdx.x];
+    if (J.ent)
+    {
+        float2 m = reinterpret_cast<const float2*>(J.d.minmax)[0];
+        ent_fold_one(J.d, 0, -m.x, m.y);
+    }
+    else if (threadIdx.x == 0)
+        fold_one(J.d, 0, !J.hist);
 }
 
 __global__ __launch_bounds__(kBlock) void histogram_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
 {
     const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, true)];
-    if (!J.hist || !J.d.pdf_init[0])
+    if (!J.hist)
         return;
-    histogram_part<kBlock>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
+    if (J.ent)
+    {
+        if (J.d.active[0])
+            histogram_part<kBlock, true>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
+    }
+    else if (J.d.pdf_init[0])
+        histogram_part<kBlock, false>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
 }
 
 __global__ __launch_bounds__(kPdfSize) void fold_histogram_many_kernel(const StatsJob* __restrict__ jobs)
 {
     const StatsJob& J = jobs[blockIdx.x];
-    if (J.hist && J.d.pdf_init[0])
+    if (!J.hist)
+        return;
+    if (J.ent)
+    {
+        if (J.d.active[0])
+            ent_fold_hist_one(J.d, 0);
+    }
+    else if (J.d.pdf_init[0])
         fold_hist_one(J.d, 0, J.count);
 }
 
@@ -552,13 +706,17 @@ void launch_batch_minmax(const TqDevice& d, const float* x, int64_t outer, int64
     }
 }
 
-void launch_fold_minmax(const TqDevice& d, int64_t C, bool tf_scheme, hipStream_t s)
+void launch_fold_minmax(const TqDevice& d, int64_t C, StatsKind kind, hipStream_t s)
 {
-    fold_minmax_kernel<<<(int) ceil_div(C, kBlock), kBlock, 0, s>>>(d, C, tf_scheme ? 1 : 0);
+    if (kind == kKindEntropy)
+        ent_fold_minmax_kernel<<<grid_for_channels(C), kBlock, 0, s>>>(d, C);
+    else
+        fold_minmax_kernel<<<(int) ceil_div(C, kBlock), kBlock, 0, s>>>(d, C, kind == kKindTf ? 1 : 0);
     AIMET_LAUNCH_CHECK();
 }
 
-void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, hipStream_t s)
+template <bool ENT>
+static void batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, hipStream_t s)
 {
     bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     if (C == 1)
@@ -570,25 +728,40 @@ void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, in
         if (n >= kHistLargeN)
         {
             int blocks = stream_blocks(n, (int64_t) 256 * kHistUnroll * 4 * 4);
-            histogram_tensor_kernel<256><<<blocks < kHistGrid ? blocks : kHistGrid, 256, 0, s>>>(x, n, al ? 1 : 0, d);
+            histogram_tensor_kernel<256, ENT><<<blocks < kHistGrid ? blocks : kHistGrid, 256, 0, s>>>(x, n, al ? 1 : 0,
+                                                                                                     d);
         }
         else
         {
             int blocks = stream_blocks(n, (int64_t) 1024 * kHistUnroll * 4 * 2);
-            histogram_tensor_kernel<1024><<<blocks < 256 ? blocks : 256, 1024, 0, s>>>(x, n, al ? 1 : 0, d);
+            histogram_tensor_kernel<1024, ENT><<<blocks < 256 ? blocks : 256, 1024, 0, s>>>(x, n, al ? 1 : 0, d);
         }
     }
     else
     {
         int vec = (al && K % 4 == 0) ? 1 : 0;
-        histogram_channel_kernel<<<grid_for_channels(C), kBlock, 0, s>>>(x, outer, C, K, vec, d);
+        histogram_channel_kernel<ENT><<<grid_for_channels(C), kBlock, 0, s>>>(x, outer, C, K, vec, d);
     }
     AIMET_LAUNCH_CHECK();
 }
 
-void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStream_t s)
+void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, StatsKind kind,
+                            hipStream_t s)
 {
-    fold_histogram_kernel<<<grid_for_channels(C), kPdfSize, 0, s>>>(d, C, count);
+    if (kind == kKindEntropy)
+        batch_histogram<true>(d, x, outer, C, K, s);
+    else if (kind == kKindPdf)
+        batch_histogram<false>(d, x, outer, C, K, s);
+}
+
+void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, StatsKind kind, hipStream_t s)
+{
+    if (kind == kKindEntropy)
+        ent_fold_histogram_kernel<<<grid_for_channels(C), kPdfSize, 0, s>>>(d, C);
+    else if (kind == kKindPdf)
+        fold_histogram_kernel<<<grid_for_channels(C), kPdfSize, 0, s>>>(d, C, count);
+    else
+        return;
     AIMET_LAUNCH_CHECK();
 }
 
@@ -630,7 +803,7 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
     }
     else if (phases & kPhaseFoldMinmax)
     {
-        fold_minmax_many_kernel<<<(unsigned) ceil_div(n, kBlock), kBlock, 0, s>>>(dj, n);
+        fold_minmax_many_kernel<<<(unsigned) n, kBlock, 0, s>>>(dj);
         AIMET_LAUNCH_CHECK();
     }
     if ((phases & kPhaseHistogram) && hb > 0)

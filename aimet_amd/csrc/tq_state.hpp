@@ -29,8 +29,20 @@ struct TqDevice
     float* bin_offset;      // [C] (float)xLeft[0] / bin_bucket    UpdatePdf:265-268
     double* pdf;            // [C][512]
     unsigned long long* counts;   // [C][512] histogram of the current batch
+    // Entropy analyzer (TensorProfilingParams, math_functions.hpp:71-77) reuses: acc = {min, max},
+    // pdf_init = histogram allocated, pdf = the 512 bin counts (integers in double), iterations,
+    // bin_bucket / bin_offset = the float (binWidth, min) of the current batch, and
+    int32_t* active;        // [C] the current batch is binned (not all-zero, :482-487)
     aimet_tf_encoding* enc; // [C] device-computed encodings (TF-Enhanced / MSE search)
     void* search_part;      // MSE search slices (mse_part_bytes(C))
+};
+
+// statistics family of a quantizer's analyzer
+enum StatsKind
+{
+    kKindTf      = 0,   // running min/max (TF)
+    kKindPdf     = 1,   // PDF histogram, range fixed on the first batch (TF-E, percentile, MSE)
+    kKindEntropy = 2    // TensorProfilingParams histogram, range widened every batch (entropy)
 };
 
 constexpr int kMinmaxParts  = 1024;   // grid of the per-tensor min/max pass
@@ -39,9 +51,10 @@ constexpr int kMseMaxSplits = 128;    // candidate slices of a per-tensor MSE se
 // stats.hip
 void launch_batch_minmax(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, int skip_if_init,
                          hipStream_t s);
-void launch_fold_minmax(const TqDevice& d, int64_t C, bool tf_scheme, hipStream_t s);
-void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, hipStream_t s);
-void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, hipStream_t s);
+void launch_fold_minmax(const TqDevice& d, int64_t C, StatsKind kind, hipStream_t s);
+void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, StatsKind kind,
+                            hipStream_t s);
+void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, StatsKind kind, hipStream_t s);
 void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s);
 // Many per-tensor quantizers (C == 1) in one launch per phase (stats.hip: launch_stats_many)
 struct StatsJob
@@ -52,6 +65,7 @@ struct StatsJob
     TqDevice d;
     uint32_t mm_block0, mm_blocks, h_block0, h_blocks;   // filled by launch_stats_many
     int32_t hist, vec;
+    int32_t ent;     // entropy analyzer (hist == 1 too): min/max every batch, TensorProfilingParams
 };
 enum StatsPhase
 {

@@ -333,6 +333,24 @@ class AimetTensorQuantizer:
                          torch.cuda.current_stream(self._device).cuda_stream)
         return [(float(xl[i]), float(pdf[i])) for i in range(n.value)]
 
+    def entropy_state(self, channel: int = 0):
+        """The entropy analyzer's TensorProfilingParams (math_functions.hpp:71-77) of `channel`:
+        dict(has_hist, min, max, hist[512] bin counts, iterations)."""
+        import numpy as np
+        if self._scheme != QuantizationMode.QUANTIZATION_ENTROPY:
+            raise RuntimeError("entropy_state() exists for the entropy quant scheme only")
+        mm = np.zeros(2, dtype=np.float64)
+        hist = np.zeros(512, dtype=np.float64)
+        if self._handle is None:
+            return dict(has_hist=0, min=0.0, max=0.0, hist=hist, iterations=0)
+        has, it = ctypes.c_int(0), ctypes.c_int(0)
+        with torch.cuda.device(self._device):
+            _native.call("aimet_tq_get_entropy_state", self._handle, int(channel),
+                         mm.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                         hist.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(has), ctypes.byref(it),
+                         torch.cuda.current_stream(self._device).cuda_stream)
+        return dict(has_hist=has.value, min=float(mm[0]), max=float(mm[1]), hist=hist, iterations=it.value)
+
     def setPercentileValue(self, percentile: float):
         """AimetTensorQuantizer.cpp:200-207 (percentile scheme only)."""
         if self._scheme != QuantizationMode.QUANTIZATION_PERCENTILE:

@@ -89,6 +89,13 @@ int aimet_encoding_from_histogram(int quant_scheme, int initialized, int stats_u
                                   double bucket_size, const double* pdf_host, float percentile, int32_t bw,
                                   int use_symmetric, int use_strict_symmetric, int use_unsigned_symmetric,
                                   aimet_tf_encoding* out);
+/* EntropyEncodingAnalyzer.cpp:97-435 computeEncoding (KL-divergence search, 8-bit) from the
+ * analyzer's TensorProfilingParams (math_functions.hpp:71-77): the range {tpp_min, tpp_max} and the
+ * 512 bin counts `hist_host`; has_histogram = 0 reproduces the "no histogram yet" branch. */
+int aimet_encoding_from_entropy_histogram(int has_histogram, int stats_updated, double tpp_min, double tpp_max,
+                                          const double* hist_host, int32_t bw, int use_symmetric,
+                                          int use_strict_symmetric, int use_unsigned_symmetric,
+                                          aimet_tf_encoding* out);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Quantize-dequantize kernels                                                                 */
@@ -235,6 +242,10 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
  * `channel`; *n = 0 when no histogram exists yet. Synchronises `stream`. */
 int aimet_tq_get_stats_histogram(aimet_tensor_quantizer* q, int64_t channel, double* xleft, double* pdf, int* n,
                                  void* stream);
+/* The entropy analyzer's TensorProfilingParams of `channel` (math_functions.hpp:71-77): minmax[2] =
+ * {min, max}, hist[512] = bin counts, *has_histogram = histogram.size() != 0. Synchronises `stream`. */
+int aimet_tq_get_entropy_state(aimet_tensor_quantizer* q, int64_t channel, double* minmax_host, double* hist_host,
+                               int* has_histogram, int* iterations, void* stream);
 
 int aimet_tq_num_channels(aimet_tensor_quantizer* q, int64_t* num_channels);
 int aimet_tq_quant_scheme(aimet_tensor_quantizer* q, int* quant_scheme);

@@ -686,6 +686,265 @@ static orc_encoding mse_compute(const orc_pdf* p, int stats_updated, int bw, int
 }
 
 /* ------------------------------------------------------------------------- */
+/* Entropy analyzer: TensorProfilingParams histogram + KL-divergence range search              */
+/* (math_functions.cpp:470-641, EntropyEncodingAnalyzer.cpp:97-435)                            */
+/* ------------------------------------------------------------------------- */
+
+typedef struct {
+    double min, max;           /* TensorProfilingParams (math_functions.hpp:71-77) */
+    double hist[PDF_SIZE];
+    int has_hist;              /* histogram.size() != 0 */
+    int iterations;
+} orc_tpp;
+
+/* math_functions.cpp:470-474 getBin. The (size_t) conversion of a float is the x86-64 one gcc
+ * emits (NaN and values <= -1 land in the last bin, values >= 2^64 in bin 0), as in the
+ * reference build. */
+static size_t ent_get_bin(size_t nBins, float binWidth, float minValue, float value)
+{
+    if (binWidth == 0)
+        return 0;
+    size_t b = (size_t) ((value - minValue) / binWidth);
+    return (nBins - 1 < b) ? nBins - 1 : b;
+}
+
+/* math_functions.cpp:476-560 updateTensorHistogram_cpu */
+void orc_entropy_update(orc_tpp* t, const float* x, int64_t n)
+{
+    double minInput = (double) orc_get_min(x, n);
+    double maxInput = (double) orc_get_max(x, n);
+    if (minInput == 0 && maxInput == 0)
+        return;
+    if (minInput == maxInput)
+        maxInput = dmax_(maxInput, minInput + (double) 0.01f);
+    if (!t->has_hist) {
+        memset(t->hist, 0, sizeof(t->hist));
+        t->has_hist = 1;
+        t->min = minInput;
+        t->max = maxInput;
+    }
+    if (minInput < t->min || maxInput > t->max) {
+        double newMin = dmin_(minInput, t->min);
+        double newMax = dmax_(maxInput, t->max);
+        double destBinWidth = (newMax - newMin) / PDF_SIZE;
+        double srcBinWidth = (t->max - t->min) / PDF_SIZE;
+        double scaled[PDF_SIZE];
+        memset(scaled, 0, sizeof(scaled));
+        for (size_t i = 0; i < PDF_SIZE; ++i) {
+            if (t->hist[i] == 0)
+                continue;
+            double srcBinBegin = t->min + srcBinWidth * (double) i;
+            size_t destBin = (size_t) ((srcBinBegin - newMin) / destBinWidth);
+            double destBinEnd = newMin + destBinWidth * (double) (destBin + 1);
+            double dstBinCnt = dmin_(round((destBinEnd - srcBinBegin) / srcBinWidth * t->hist[i]), t->hist[i]);
+            scaled[ent_get_bin(PDF_SIZE, (float) destBinWidth, (float) newMin, (float) srcBinBegin)] += dstBinCnt;
+            if (dstBinCnt < t->hist[i])
+                scaled[ent_get_bin(PDF_SIZE, (float) destBinWidth, (float) newMin,
+                                   (float) (srcBinBegin + destBinWidth))] += t->hist[i] - dstBinCnt;
+        }
+        memcpy(t->hist, scaled, sizeof(scaled));
+        t->min = newMin;
+        t->max = newMax;
+    }
+    float binWidth = (float) ((t->max - t->min) / PDF_SIZE);
+    float fmin = (float) t->min;
+    for (int64_t i = 0; i < n; ++i)
+        t->hist[ent_get_bin(PDF_SIZE, binWidth, fmin, x[i])] += 1;
+    t->iterations++;
+}
+
+/* math_functions.cpp:562-641 rescaleHistogram (non-empty source) */
+static void ent_rescale(const double* src, double srcMin, double srcMax, double dstMin, double dstMax, double* dst)
+{
+    if (srcMin == dstMin && srcMax == dstMax) {
+        memcpy(dst, src, PDF_SIZE * sizeof(double));
+        return;
+    }
+    const size_t numBins = PDF_SIZE;
+    const double srcBinWidth = (srcMax - srcMin) / (double) numBins;
+    const double destBinWidth = (dstMax - dstMin) / (double) numBins;
+    memset(dst, 0, PDF_SIZE * sizeof(double));
+    for (size_t s = 0; s < numBins; s++) {
+        double v = src[s];
+        if (v == 0)
+            continue;
+        double sStart = srcMin + (double) s * srcBinWidth;
+        double sStop = srcMin + (double) (s + 1) * srcBinWidth;
+        double startF = floor((sStart - dstMin) / destBinWidth);
+        double stopF = ceil((sStop - dstMin) / destBinWidth);
+        size_t i0 = (size_t) dmax_(startF, 0.0);
+        size_t i1 = (size_t) dmax_(stopF, 0.0);
+        if (i0 >= numBins) i0 = numBins - 1;
+        if (i1 >= numBins) i1 = numBins - 1;
+        double rem = v;
+        for (size_t d = i0; d <= i1; d++) {
+            double dStart = dstMin + (double) d * destBinWidth;
+            double dStop = dstMin + (double) (d + 1) * destBinWidth;
+            double oStart = dmax_(sStart, dStart);
+            double oStop = dmin_(sStop, dStop);
+            double ratio = (oStop - oStart) / srcBinWidth;
+            ratio = ratio >= 0.0f ? ratio : 0.0f;
+            ratio = ratio <= 1.0f ? ratio : 1.0f;
+            double dist = round(ratio * v);
+            dist = dist <= rem ? dist : rem;
+            dst[d] += dist;
+            rem -= dist;
+        }
+    }
+}
+
+/* std::accumulate(first, last, 0.f): the running sum is a float */
+static double ent_accumulate_f(const double* p, size_t n)
+{
+    float acc = 0.f;
+    for (size_t i = 0; i < n; i++)
+        acc = (float) ((double) acc + p[i]);
+    return (double) acc;
+}
+
+/* EntropyEncodingAnalyzer.cpp:156-198 _conditionHistogram */
+static void ent_condition(double* h, size_t n)
+{
+    const double epsZero = 0.0001;
+    size_t numZeros = 0;
+    for (size_t i = 0; i < n; i++)
+        numZeros += (h[i] == 0.f);
+    if (numZeros == n)
+        return;
+    double epsNonZero = epsZero * (double) numZeros / (double) (n - numZeros);
+    if (epsNonZero >= 1.0)
+        return;
+    for (size_t i = 0; i < n; i++) {
+        int z = (h[i] == 0.f);
+        h[i] += epsZero * z;
+        h[i] -= epsNonZero * (1 - z);
+    }
+}
+
+/* EntropyEncodingAnalyzer.cpp:200-224 _computeKL */
+static double ent_kl(double* P, double* Q, size_t n)
+{
+    double sumP = ent_accumulate_f(P, n);
+    double sumQ = ent_accumulate_f(Q, n);
+    double divergence = 0;
+    for (size_t i = 0; i < n; i++) {
+        P[i] /= sumP;
+        Q[i] /= sumQ;
+        if (P[i] > 0 && Q[i] > 0)
+            divergence += P[i] * log(P[i] / Q[i]);
+    }
+    return divergence;
+}
+
+/* EntropyEncodingAnalyzer.cpp:226-435 _optimizeKL (the DTYPE=float tuple it returns) */
+static void ent_optimize_kl(const orc_tpp* t, int bw, int sym, int strict, int unsign, float* outMin, float* outMax)
+{
+    double histMin = t->min, histMax = t->max;
+    double hist[PDF_SIZE];
+    if (sym && ((histMin < 0.0) || (!unsign))) {
+        float absoluteMax = (float) dmax_(fabs(histMax), fabs(histMin));
+        float absoluteMin = -absoluteMax;
+        ent_rescale(t->hist, histMin, histMax, absoluteMin, absoluteMax, hist);
+        histMin = absoluteMin;
+        histMax = absoluteMax;
+    } else {
+        memcpy(hist, t->hist, sizeof(hist));
+    }
+    const size_t numBins = PDF_SIZE, numQ = 255;
+    if (bw != 8) {
+        *outMin = (float) histMin;
+        *outMax = (float) histMax;
+        return;
+    }
+    const double binWidth = (histMax - histMin) / (double) numBins;
+    double divOpt = INFINITY;
+    double thrMin = histMin, thrMax = histMax;
+    size_t start = 0, stop = numBins - 1;
+    double P[PDF_SIZE], Q[PDF_SIZE];
+    while ((stop - start + 1) >= numQ) {
+        const size_t win = stop - start + 1;
+        const double* hw = hist + start;
+        memset(P, 0, win * sizeof(double));
+        double leftSum = 0;
+        for (size_t i = 0; i <= start; i++)
+            leftSum += hist[i];
+        P[0] += leftSum;
+        for (size_t i = start + 1; i < stop; i++)
+            P[i - start] = hist[i];
+        double rightSum = 0;
+        for (size_t i = stop; i < numBins; i++)
+            rightSum += hist[i];
+        P[win - 1] += rightSum;
+        const double merged = (double) win / (double) numQ;
+        memset(Q, 0, win * sizeof(double));
+        for (size_t q = 0; q < numQ; q++) {
+            const size_t i0 = (size_t) ceil((double) q * merged);
+            const size_t i1 = (q < numQ - 1) ? (size_t) ceil((double) (q + 1) * merged) : win;
+            double sum = 0, norm = 0;
+            for (size_t i = i0; i < i1; i++) {
+                sum += hw[i];
+                norm += (hw[i] != 0);
+            }
+            if (norm != 0)
+                for (size_t i = i0; i < i1; i++)
+                    if (hw[i] != 0)
+                        Q[i] = sum / norm;
+        }
+        if (ent_accumulate_f(P, win) == 0 || ent_accumulate_f(Q, win) == 0)
+            break;
+        ent_condition(P, win);
+        ent_condition(Q, win);
+        double dv = ent_kl(P, Q, win);
+        if (dv < divOpt) {
+            divOpt = dv;
+            thrMin = histMin + (double) start * binWidth;
+            thrMax = histMin + (double) (stop + 1) * binWidth;
+        }
+        if (sym || strict) {
+            start++;
+            stop--;
+        } else {
+            double loss[3] = {hist[start] + hist[stop], hist[start] + hist[start + 1], hist[stop] + hist[stop - 1]};
+            int k = 0;
+            if (loss[1] < loss[k]) k = 1;
+            if (loss[2] < loss[k]) k = 2;
+            if ((k == 0 && (histMin + (double) (start + 1) * binWidth) > 0) ||
+                (k == 1 && (histMin + (double) (start + 2) * binWidth) > 0))
+                k = 2;
+            else if ((k == 0 && (histMin + (double) stop * binWidth) < 0) ||
+                     (k == 2 && (histMin + (double) (stop - 1) * binWidth) < 0))
+                k = 1;
+            if (k == 0) {
+                start++;
+                stop--;
+            } else if (k == 1) {
+                start += 2;
+            } else {
+                stop -= 2;
+            }
+        }
+    }
+    *outMin = (float) thrMin;
+    *outMax = (float) thrMax;
+}
+
+/* EntropyEncodingAnalyzer.cpp:97-148 computeEncoding */
+orc_encoding orc_entropy_compute(const orc_tpp* t, int stats_updated, int bw, int sym, int strict, int unsign)
+{
+    orc_encoding e = {0, 0, 0, 0, 0};
+    float numSteps = (float) (pow(2.0, (double) bw) - 1);
+    if (sym && strict)
+        numSteps -= 1;
+    if (!t->has_hist)
+        return stats_updated ? zero_data_encoding(bw, numSteps) : e;
+    float aMin, aMax;
+    ent_optimize_kl(t, bw, sym, strict, unsign, &aMin, &aMax);
+    aMin = fmin_(aMin, 0.0f);
+    aMax = fmax_(aMax, 0.0f);
+    return orc_get_computed_encodings(bw, aMin, aMax, sym, strict, unsign);
+}
+
+/* ------------------------------------------------------------------------- */
 /* Analyzer facade (IQuantizationEncodingAnalyzer<float>, QuantizerFactory.cpp:74-104)          */
 /* ------------------------------------------------------------------------- */
 
@@ -695,6 +954,7 @@ typedef struct {
     double acc_min, acc_max;   /* TfEncodingAnalyzer.h:86-91 */
     float percentile;          /* PercentileEncodingAnalyzer.h:100 */
     orc_pdf pdf;
+    orc_tpp tpp;               /* EntropyEncodingAnalyzer.h: _tensorProfilingParams */
 } orc_analyzer;
 
 size_t orc_analyzer_size(void) { return sizeof(orc_analyzer); }
@@ -704,8 +964,6 @@ int orc_analyzer_init(orc_analyzer* a, int scheme)
     memset(a, 0, sizeof(*a));
     if (scheme == QUANTIZATION_RANGE_LEARNING)   /* QuantizerFactory.cpp:93-96 */
         scheme = QUANTIZATION_TF;
-    if (scheme == QUANTIZATION_ENTROPY)
-        return -1;                                /* not restated */
     a->scheme = scheme;
     a->acc_min = DBL_MAX;
     a->acc_max = -DBL_MAX;
@@ -724,6 +982,8 @@ void orc_analyzer_update(orc_analyzer* a, const float* x, int64_t n)
         double cmax = (double) orc_get_max(x, n);
         a->acc_min = dmin_(a->acc_min, cmin);
         a->acc_max = dmax_(a->acc_max, cmax);
+    } else if (a->scheme == QUANTIZATION_ENTROPY) {
+        orc_entropy_update(&a->tpp, x, n);
     } else {
         orc_update_pdf(&a->pdf, x, n, 1);
     }
@@ -746,6 +1006,7 @@ orc_encoding orc_analyzer_compute(const orc_analyzer* a, int bw, int sym, int st
     case QUANTIZATION_PERCENTILE:
         return percentile_compute(&a->pdf, a->stats_updated, a->percentile, bw, sym, strict, unsign);
     case QUANTIZATION_MSE: return mse_compute(&a->pdf, a->stats_updated, bw, sym, strict, unsign);
+    case QUANTIZATION_ENTROPY: return orc_entropy_compute(&a->tpp, a->stats_updated, bw, sym, strict, unsign);
     default: { orc_encoding z = {0, 0, 0, 0, 0}; return z; }
     }
 }
@@ -791,6 +1052,9 @@ int orc_analyzer_fold_minmax(orc_analyzer* a, float mn, float mx)
     }
     return 1;
 }
+
+/* Entropy statistics (TensorProfilingParams) for tests of the device path */
+orc_tpp* orc_analyzer_tpp(orc_analyzer* a) { return &a->tpp; }
 
 /* Direct PDF access for tests of the sharded path */
 orc_pdf* orc_analyzer_pdf(orc_analyzer* a) { return &a->pdf; }

@@ -171,8 +171,14 @@ def histogram(x, bucket_size, pdf_offset, is_signed=True):
     return h
 
 
+class _Tpp(ctypes.Structure):
+    """orc_tpp (TensorProfilingParams, math_functions.hpp:71-77)."""
+    _fields_ = [("min", ctypes.c_double), ("max", ctypes.c_double), ("hist", ctypes.c_double * PDF_SIZE),
+                ("has_hist", ctypes.c_int), ("iterations", ctypes.c_int)]
+
+
 class Analyzer:
-    """IQuantizationEncodingAnalyzer<float> restated (TF, TF-E, percentile, MSE)."""
+    """IQuantizationEncodingAnalyzer<float> restated (TF, TF-E, percentile, MSE, entropy)."""
 
     def __init__(self, scheme):
         L = lib()
@@ -213,6 +219,14 @@ class Analyzer:
         return dict(stats_updated=su.value, acc_min=amin.value, acc_max=amax.value, initialized=ini.value,
                     hist_min=hm.value, bucket_size=bs.value, iterations=it.value,
                     pdf=pdf if ini.value else np.zeros(PDF_SIZE))
+
+    def entropy_state(self):
+        """TensorProfilingParams of the entropy analyzer: dict(has_hist, min, max, hist, iterations)."""
+        L = lib()
+        L.orc_analyzer_tpp.restype = ctypes.POINTER(_Tpp)
+        t = L.orc_analyzer_tpp(self._buf).contents
+        return dict(has_hist=t.has_hist, min=t.min, max=t.max, hist=np.array(t.hist[:], dtype=np.float64),
+                    iterations=t.iterations)
 
     def histogram(self):
         xl = np.zeros(PDF_SIZE, dtype=np.float64)

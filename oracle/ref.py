@@ -59,6 +59,11 @@ def lib():
         L.ref_analyzer_set_percentile.argtypes = [ctypes.c_void_p, ctypes.c_float]
         L.ref_analyzer_histogram.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]
+        L.ref_tpp_create.restype = ctypes.c_void_p
+        L.ref_tpp_destroy.argtypes = [ctypes.c_void_p]
+        L.ref_tpp_update.argtypes = [ctypes.c_void_p, fp, i64]
+        L.ref_tpp_get.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
         _lib = L
     return _lib
 
@@ -139,8 +144,35 @@ class Analyzer:
         return e
 
     def histogram(self):
+        if self.scheme == 5:
+            # EntropyEncodingAnalyzer::getStatsHistogram (EntropyEncodingAnalyzer.cpp:56-78) builds a
+            # 1024-entry PDF next to a ~513-entry xLeft (assert) -- never called on this path
+            raise NotImplementedError("getStatsHistogram is not defined for the entropy analyzer")
         xl = np.zeros(PDF_SIZE, dtype=np.float64)
         pdf = np.zeros(PDF_SIZE, dtype=np.float64)
         n = lib().ref_analyzer_histogram(self._p, xl.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
                                          pdf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
         return xl[:n], pdf[:n]
+
+
+class TensorProfilingParams:
+    """The entropy analyzer's histogram state updated by the reference updateTensorHistogram_cpu."""
+
+    def __init__(self):
+        self._p = lib().ref_tpp_create()
+
+    def __del__(self):
+        if getattr(self, "_p", None) and _lib is not None:
+            _lib.ref_tpp_destroy(self._p)
+            self._p = None
+
+    def update(self, x):
+        x = _f32(x)
+        lib().ref_tpp_update(self._p, _fp(x), x.size)
+
+    def state(self):
+        mn, mx, it = ctypes.c_double(), ctypes.c_double(), ctypes.c_int()
+        h = np.zeros(PDF_SIZE, dtype=np.float64)
+        n = lib().ref_tpp_get(self._p, ctypes.byref(mn), ctypes.byref(mx),
+                              h.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(it))
+        return dict(has_hist=int(n != 0), min=mn.value, max=mx.value, hist=h, iterations=it.value)

@@ -137,4 +137,34 @@ int ref_analyzer_histogram(void* a, double* xleft, double* pdf)
     return i;
 }
 
+// math_functions.cpp:476-560: the entropy analyzer's TensorProfilingParams, driven directly
+// (EntropyEncodingAnalyzer keeps its copy private)
+void* ref_tpp_create()
+{
+    auto* t       = new TensorProfilingParams();
+    t->min        = 0;
+    t->max        = 0;
+    t->iterations = 0;
+    return t;
+}
+void ref_tpp_destroy(void* t)
+{
+    delete static_cast<TensorProfilingParams*>(t);
+}
+void ref_tpp_update(void* t, const float* x, int64_t n)
+{
+    updateTensorHistogram_cpu(x, (int) n, *static_cast<TensorProfilingParams*>(t));
+}
+// returns histogram.size() (0 or 512)
+int ref_tpp_get(void* t, double* mn, double* mx, double* hist, int* iterations)
+{
+    auto* p     = static_cast<TensorProfilingParams*>(t);
+    *mn         = p->min;
+    *mx         = p->max;
+    *iterations = p->iterations;
+    for (size_t i = 0; i < p->histogram.size(); ++i)
+        hist[i] = p->histogram[i];
+    return (int) p->histogram.size();
+}
+
 }   // extern "C"

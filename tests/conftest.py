@@ -40,6 +40,26 @@ def golden_analyzers(golden_dir):
 
 
 @pytest.fixture(scope="session")
+def golden_entropy(golden_dir):
+    import numpy as np
+    return dict(np.load(os.path.join(golden_dir, "golden_entropy.npz")))
+
+
+def entropy_case(en, i):
+    """Unpack entropy case i of golden_entropy.npz: batches, reference TensorProfilingParams and
+    encodings {(bw, sym, strict, unsigned): (min, max, delta, offset, bw)}."""
+    nb = int(en["e%d_nb" % i])
+    encs = {}
+    for k, v in zip(en["e%d_enc_keys" % i], en["e%d_enc_vals" % i]):
+        bw, flags = str(k).split("_")
+        encs[(int(bw), int(flags[0]), int(flags[1]), int(flags[2]))] = tuple(v[:4]) + (int(v[4]),)
+    t = en["e%d_tpp" % i]
+    return dict(batches=[en["e%d_b%d" % (i, k)] for k in range(nb)], encs=encs,
+                tpp=dict(has_hist=int(t[0]), min=float(t[1]), max=float(t[2]), iterations=int(t[3]),
+                         hist=en["e%d_hist" % i]))
+
+
+@pytest.fixture(scope="session")
 def golden_torch(golden_dir):
     import numpy as np
     return dict(np.load(os.path.join(golden_dir, "golden_torch.npz")))

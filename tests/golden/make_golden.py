@@ -131,12 +131,88 @@ def analyzer_cases(rng):
     return cases
 
 
-def tfe_kat_data():
+def tfe_kat_data(count=6000):
     exe = os.path.join(tempfile.mkdtemp(), "gen")
     subprocess.run(["g++", "-O2", "-o", exe, os.path.join(HERE, "gen_mt19937_normal.cpp")], check=True)
     path = exe + ".f32"
-    subprocess.run([exe, path], check=True)
+    subprocess.run([exe, path, str(count)], check=True)
     return np.fromfile(path, dtype=np.float32)
+
+
+ENTROPY_FLAGS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1), (0, 1, 0)]
+
+
+def entropy_cases(rng):
+    """Entropy analyzer (EntropyEncodingAnalyzer.cpp + updateTensorHistogram_cpu): batch sequences
+    that initialise, widen (rescale) and skip the histogram. Per case: the TensorProfilingParams
+    after the last batch (reference updateTensorHistogram_cpu) and the analyzer's encodings."""
+    cases = []
+    for t in range(12):
+        nb = 5 if t in (6, 9) else 3
+        batches = []
+        for k in range(nb):
+            n = int(rng.integers(300, 3000)) if t != 7 else 20000
+            mu, s = rng.uniform(-2, 2), rng.uniform(0.05, 5) * (1 + k)      # ranges grow: rescales
+            x = (rng.standard_normal(n) * s + mu).astype(np.float32)
+            if t == 1:
+                x = np.maximum(x, 0)                                      # ReLU output
+            elif t == 2 and k != 1:
+                x[:] = 0                                                  # all-zero batches (skipped)
+            elif t == 3:
+                x[:5] = [np.nan, 1e30, -1e30, 1e-40, -1e-40]              # no inf: the reference asserts
+            elif t == 4 and k == 0:
+                x[:] = 1.25                                               # min == max (+0.01)
+            elif t == 5:
+                x = -np.abs(x)                                            # one-sided negative
+            elif t == 6:
+                x = (rng.laplace(0, 1, n) * rng.uniform(0.1, 10)).astype(np.float32)
+            elif t == 8:
+                x = (np.abs(x) + 3).astype(np.float32)                    # positive, away from 0
+            elif t == 9 and k % 2:
+                x = x[::-1].copy() * 0.01                                 # narrower batch: no rescale
+            elif t == 10:
+                x = np.round(x * 4).astype(np.float32) / 4                # values on a lattice
+            elif t == 11:
+                x[:] = rng.uniform(-1, 1) * np.float32(1e-3) * (1 + k)    # constant batches
+            batches.append(x.astype(np.float32))
+        cases.append(batches)
+    out = []
+    for batches in cases:
+        a, tpp = R.Analyzer(5), R.TensorProfilingParams()
+        for x in batches:
+            a.update(x)
+            tpp.update(x)
+        encs = {}
+        for bw in (8, 4, 16):
+            for fl in ENTROPY_FLAGS:
+                encs["%d_%d%d%d" % ((bw,) + fl)] = a.compute(bw, *fl).as_tuple()
+        out.append(dict(batches=batches, encs=encs, tpp=tpp.state()))
+    return out
+
+
+def entropy_golden():
+    """golden_entropy.npz: entropy analyzer cases + the TestEntropyEncodingAnalyzer KAT input."""
+    rng = np.random.default_rng(20251016)
+    en = {}
+    cases = entropy_cases(rng)
+    for i, c in enumerate(cases):
+        en["e%d_nb" % i] = np.array(len(c["batches"]))
+        for k, b in enumerate(c["batches"]):
+            en["e%d_b%d" % (i, k)] = b
+        st = c["tpp"]
+        en["e%d_tpp" % i] = np.array([st["has_hist"], st["min"], st["max"], st["iterations"]], dtype=np.float64)
+        en["e%d_hist" % i] = st["hist"]
+        keys = sorted(c["encs"])
+        en["e%d_enc_keys" % i] = np.array(keys)
+        en["e%d_enc_vals" % i] = np.array([c["encs"][k] for k in keys], dtype=np.float64)
+    en["count"] = np.array(len(cases))
+    kx = tfe_kat_data(100000)
+    a = R.Analyzer(5)
+    a.update(kx)
+    en["kat_x"] = kx
+    en["kat_enc_keys"] = np.array(["8_%d%d%d" % fl for fl in ENTROPY_FLAGS])
+    en["kat_enc_vals"] = np.array([a.compute(8, *fl).as_tuple() for fl in ENTROPY_FLAGS], dtype=np.float64)
+    np.savez_compressed(os.path.join(HERE, "golden_entropy.npz"), **en)
 
 
 def reference_python():
@@ -149,6 +225,9 @@ def reference_python():
 
 
 def main():
+    entropy_golden()
+    if "--entropy-only" in sys.argv:
+        return
     rng = np.random.default_rng(20251015)
     R.lib()
 

@@ -417,7 +417,7 @@ def test_adaround_backward_with_round_loss_vs_torch(beta, shape):
     (wq * g).sum().backward()
     torch.testing.assert_close(wq, wq_ref.detach(), rtol=0, atol=1e-6)
     torch.testing.assert_close(a.grad, a_ref.grad, rtol=1e-4, atol=1e-7)
-    assert abs(float(loss) - float(loss_ref)) <= 1e-4 * abs(float(loss_ref))
+    assert abs(loss.item() - loss_ref.item()) <= 1e-4 * abs(loss_ref.item())
 
 
 def test_channel_plan_equals_individual_launches():
