@@ -87,12 +87,12 @@ struct Binner
         if (zero_width)
             return 0;
         const float s   = x - lo;
-        float q         = s * rcp;
+        const float q   = s * rcp;
         const float fr  = __builtin_fabsf(q - __builtin_rintf(q));
         const float thr = (__builtin_fabsf(q) + 1.0f) * 9.5367431640625e-7f;   // 2^-20
-        if (!(fr > thr))
-            q = s / width;
-        return bin_of_quotient(q);
+        if (__builtin_expect(fr > thr, 1))   // q finite and off every integer
+            return (q > -1.0f && q < (float) kBins) ? (int) q : (q >= 18446744073709551616.0f ? 0 : kBins - 1);
+        return bin_of_quotient(s / width);
     }
 };
 #endif

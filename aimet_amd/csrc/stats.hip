@@ -422,16 +422,18 @@ __device__ __forceinline__ void histogram_part(const float* __restrict__ x, int6
 #pragma unroll
             for (int u = 0; u < kHistUnroll; ++u)
             {
+                // padding: NaN is dropped by the PDF binner; the entropy binner counts NaN (last
+                // bin, as the reference), so there the padding is zeros, taken back from the
+                // register zero counter
                 int64_t i = base + (int64_t) u * BLOCK;
-                v[u]      = i < nv ? __builtin_nontemporal_load(x4 + i) : f4 {NAN, NAN, NAN, NAN};
+                if (ENT && i >= nv)
+                    zc -= 4;
+                v[u] = i < nv ? __builtin_nontemporal_load(x4 + i)
+                              : (ENT ? f4 {0.f, 0.f, 0.f, 0.f} : f4 {NAN, NAN, NAN, NAN});
             }
 #pragma unroll
             for (int u = 0; u < kHistUnroll; ++u)
             {
-                // NaN padding is dropped by the PDF binner; the entropy binner counts NaN (last
-                // bin, as the reference), so there the padding is skipped explicitly
-                if (ENT && base + (int64_t) u * BLOCK >= nv)
-                    continue;
                 add(v[u].x);
                 add(v[u].y);
                 add(v[u].z);

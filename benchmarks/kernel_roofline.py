@@ -166,6 +166,16 @@ def main():
     ms = timed(lambda: q.batch_histogram(x), args.reps, stream)
     row("histogram 512 bins (stats pass 2)", "a8", 4, ms,
         cpu_rate(lambda: O.histogram(xs, np.float32(0.0469), np.float32(-150.0))))
+    # §8(f) row 3: entropy analyzer -- the histogram pass alone (binning with the range widened
+    # every batch) and a whole updateStats (min/max + widen + histogram + fold: two reads of x)
+    qe = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_ENTROPY)
+    qe.updateStats(x, True)
+    ms = timed(lambda: qe.batch_histogram(x), args.reps, stream)
+    row("entropy histogram 512 bins", "f3", 4, ms)
+    oe = O.Analyzer(O.QUANTIZATION_ENTROPY)
+    ms = timed(lambda: qe.updateStats(x, True), args.reps, stream)
+    row("entropy updateStats (4 launches)", "f3", 8, ms, cpu_rate(lambda: oe.update(xs)),
+        note="cpu = updateTensorHistogram_cpu restated (the reference GPU build copies to the host and runs it)")
     # a14: learned grid forward / backward vs the reference's torch ops
     steps = 255.0
     ms = timed(lambda: lib.aimet_lg_forward(P(x), P(y), 1, C, K, P(delta), P(offset), ctypes.c_float(steps), sp),
