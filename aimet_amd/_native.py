@@ -45,6 +45,33 @@ class ChannelDescC(ctypes.Structure):
     _fields_ = [("in_", ctypes.c_void_p), ("out", ctypes.c_void_p), ("outer", ctypes.c_int64),
                 ("C", ctypes.c_int64), ("K", ctypes.c_int64), ("table", ctypes.c_void_p)]
 
+AIMET_BCAST_MAX_DIMS = 16
+
+
+class BroadcastShapeInfoC(ctypes.Structure):
+    """aimet_broadcast_shape_info (onnx/src/QuantizeDequantizeUtils.hpp:166-178 BroadcastShapeInfo)."""
+    _fields_ = [("num_dims", ctypes.c_int64),
+                ("tensor_shape", ctypes.c_int64 * AIMET_BCAST_MAX_DIMS),
+                ("encoding_shape", ctypes.c_int64 * AIMET_BCAST_MAX_DIMS),
+                ("tensor_strides", ctypes.c_int64 * AIMET_BCAST_MAX_DIMS),
+                ("encoding_strides", ctypes.c_int64 * AIMET_BCAST_MAX_DIMS),
+                ("num_elements", ctypes.c_int64), ("num_encodings", ctypes.c_int64),
+                ("contiguous_blocks", ctypes.c_int)]
+
+
+class QcQuantizeInfoC(ctypes.Structure):
+    """aimet_qc_quantize_info (onnx/src/QcQuantizeInfo.h:46-73 + the TensorQuantizer settings)."""
+    _fields_ = [("op_mode", ctypes.c_int), ("enabled", ctypes.c_int), ("is_int_data_type", ctypes.c_int),
+                ("use_per_channel_mode", ctypes.c_int), ("channel_axis", ctypes.c_int),
+                ("block_axis", ctypes.c_int), ("block_size", ctypes.c_int),
+                ("use_symmetric_encoding", ctypes.c_int), ("use_strict_symmetric", ctypes.c_int),
+                ("use_unsigned_symmetric", ctypes.c_int), ("rounding_mode", ctypes.c_int),
+                ("num_encodings", ctypes.c_int64), ("encodings", ctypes.POINTER(TfEncodingC)),
+                ("quantizer", ctypes.c_void_p)]
+
+
+_i64p = ctypes.POINTER(ctypes.c_int64)
+
 # name -> argtypes (restype is int status unless listed in _RESTYPES)
 _PROTOTYPES = {
     "aimet_last_error": [],
@@ -56,6 +83,12 @@ _PROTOTYPES = {
     "aimet_encoding_from_minmax": [ctypes.c_double, ctypes.c_double, _i32, _int, _int, _int, _enc_p],
     "aimet_encoding_from_histogram": [_int, _int, _int, ctypes.c_float, ctypes.c_double, _dp, ctypes.c_float, _i32,
                                       _int, _int, _int, _enc_p],
+    "aimet_qdq_broadcast": [_vp, _vp, _i64, _i64, _i64p, _i64p, _vp, _vp, _vp, _vp, _vp],
+    "aimet_permute_tensor": [_vp, _vp, _i64, _i64, _i64p, _i64p, _vp],
+    "aimet_qdq_fp16": [_vp, _vp, _i64, _vp],
+    "aimet_broadcast_shape_info_init": [_i64p, _i64, _int, _int, _int, ctypes.POINTER(BroadcastShapeInfoC)],
+    "aimet_copy_to_contiguous_block_layout": [_vp, _vp, ctypes.POINTER(BroadcastShapeInfoC), _vp],
+    "aimet_qc_quantize_op_compute": [ctypes.POINTER(QcQuantizeInfoC), _vp, _vp, _i64p, _i64, _vp],
     "aimet_encoding_from_entropy_histogram": [_int, _int, ctypes.c_double, ctypes.c_double, _dp, _i32, _int, _int,
                                               _int, _enc_p],
     "aimet_qdq_per_tensor": [_vp, _vp, _i64, _enc_p, _int, ctypes.c_uint64, _vp],

@@ -1,0 +1,354 @@
+// broadcast.hip -- blockwise (broadcast) quantize-dequantize, the block-layout permutation of the
+// blockwise statistics, and the fp16 round trip of float quantizers.
+//
+// Reference:
+//   quantizeDequantizeBroadcast{Cpu,Gpu}  trim_functions.cpp:633-687, trim_functions.cu:96-122
+//   permuteTensor{CPU,GPU}                onnx/src/QuantizeDequantizeUtils.cpp:64-95 (+ .cu)
+//   quantizeDequantizeFp16{Cpu,Gpu}       onnx/src/AimetOpUtils.cpp:61-67, trim_functions.cu:135-148
+//
+// The reference walks every dimension of the broadcast view per element with 64-bit divisions
+// and int indices (wrapping at 2^31). Here the view is first collapsed on the host: size-1 dims
+// are dropped and neighbours that index the encodings the same way (both broadcast, or both
+// row-major over the encodings) are merged, so the usual LPBQ / blockwise weight layouts become
+// 2-3 dims. The kernel then does one 32-bit multiply-shift division per merged dim per 4
+// elements (16-B vectors whenever the innermost run allows), and gathers the per-element
+// encoding from the four float arrays (L1/L2-resident: E << N).
+#include "common.hpp"
+
+#include <vector>
+
+namespace aimet_amd
+{
+namespace
+{
+
+constexpr int kMaxMerged = 8;
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// A collapsed row-major view: dim d has `size`, tensor stride `tstride` (contiguous) and
+// encoding stride `estride` (0 along broadcast dims).
+struct View
+{
+    int nd;
+    int64_t size[kMaxMerged];
+    int64_t tstride[kMaxMerged];
+    int64_t estride[kMaxMerged];
+};
+
+// Host: the reference's (input strides, encoding / output strides) description of a contiguous
+// tensor of n elements -> collapsed view. Input strides must be those of a row-major tensor.
+View collapse(int64_t n, int64_t nd, const int64_t* tstr, const int64_t* estr)
+{
+    std::vector<int64_t> size(nd), ts(tstr, tstr + nd), es(estr, estr + nd);
+    for (int64_t d = 0; d < nd; ++d)
+    {
+        AIMET_REQUIRE(ts[d] > 0, "input strides must be positive");
+        int64_t outer = d == 0 ? n : ts[d - 1];
+        AIMET_REQUIRE(outer % ts[d] == 0, "input strides do not describe a contiguous row-major tensor");
+        size[d] = outer / ts[d];
+    }
+    AIMET_REQUIRE(nd == 0 || ts[nd - 1] == 1, "the innermost input stride must be 1");
+    // drop size-1 dims, then merge neighbours with estride[d] == estride[d+1] * size[d+1]
+    std::vector<int64_t> s2, t2, e2;
+    for (int64_t d = 0; d < nd; ++d)
+        if (size[d] != 1)
+        {
+            s2.push_back(size[d]);
+            t2.push_back(ts[d]);
+            e2.push_back(es[d]);
+        }
+    std::vector<int64_t> s3, t3, e3;
+    for (size_t d = 0; d < s2.size(); ++d)
+    {
+        if (!s3.empty() && e3.back() == e2[d] * s2[d])
+        {
+            s3.back() *= s2[d];
+            t3.back() = t2[d];
+            e3.back() = e2[d];
+            continue;
+        }
+        s3.push_back(s2[d]);
+        t3.push_back(t2[d]);
+        e3.push_back(e2[d]);
+    }
+    if (s3.empty())
+    {
+        s3.push_back(1);
+        t3.push_back(1);
+        e3.push_back(0);
+    }
+    AIMET_REQUIRE(s3.size() <= (size_t) kMaxMerged, "broadcast view has too many alternating dimensions");
+    View v {};
+    v.nd = (int) s3.size();
+    for (int d = 0; d < v.nd; ++d)
+    {
+        v.size[d]    = s3[d];
+        v.tstride[d] = t3[d];
+        v.estride[d] = e3[d];
+    }
+    return v;
+}
+
+// 32-bit index math (n < 2^31)
+struct View32
+{
+    int nd;
+    FastDiv div[kMaxMerged];       // by tstride
+    uint32_t tstride[kMaxMerged];
+    uint32_t estride[kMaxMerged];
+    __device__ __forceinline__ uint32_t index(uint32_t i) const
+    {
+        uint32_t e = 0, rem = i;
+#pragma unroll
+        for (int d = 0; d < kMaxMerged; ++d)
+        {
+            if (d >= nd)
+                break;
+            uint32_t q = div[d].div(rem);
+            rem -= q * tstride[d];
+            e += q * estride[d];
+        }
+        return e;
+    }
+};
+
+View32 to32(const View& v)
+{
+    View32 r {};
+    r.nd = v.nd;
+    for (int d = 0; d < v.nd; ++d)
+    {
+        r.div[d]     = FastDiv((uint32_t) v.tstride[d]);
+        r.tstride[d] = (uint32_t) v.tstride[d];
+        r.estride[d] = (uint32_t) v.estride[d];
+    }
+    return r;
+}
+
+__device__ __forceinline__ int64_t index64(const View& v, int64_t i)
+{
+    int64_t e = 0, rem = i;
+    for (int d = 0; d < v.nd; ++d)
+    {
+        int64_t q = rem / v.tstride[d];
+        rem -= q * v.tstride[d];
+        e += q * v.estride[d];
+    }
+    return e;
+}
+
+struct EncArrays
+{
+    const float* __restrict__ mn;
+    const float* __restrict__ mx;
+    const float* __restrict__ delta;
+    const float* __restrict__ offset;
+    __device__ __forceinline__ float qdq(float x, uint32_t e) const
+    {
+        QdqParams p {mn[e], mx[e], delta[e], offset[e]};
+        return dequantize(quantize_nearest(x, p), p);
+    }
+};
+
+// 4 consecutive elements per lane; the innermost merged dim has size % 4 == 0, so they share the
+// outer indices and their encodings are e0 + j * inner_estride.
+__global__ __launch_bounds__(kBlock) void bcast_vec_kernel(const f4* __restrict__ in, f4* __restrict__ out,
+                                                           uint32_t nvec, View32 v, uint32_t inner_es, EncArrays enc)
+{
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride)
+    {
+        f4 x        = __builtin_nontemporal_load(in + i);
+        uint32_t e0 = v.index(i * 4);
+        f4 r;
+        r.x = enc.qdq(x.x, e0);
+        r.y = enc.qdq(x.y, e0 + inner_es);
+        r.z = enc.qdq(x.z, e0 + 2 * inner_es);
+        r.w = enc.qdq(x.w, e0 + 3 * inner_es);
+        __builtin_nontemporal_store(r, out + i);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void bcast_scalar_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                              uint32_t n, View32 v, EncArrays enc)
+{
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        out[i] = enc.qdq(in[i], v.index(i));
+}
+
+__global__ __launch_bounds__(kBlock) void bcast_scalar64_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                                int64_t n, View v, EncArrays enc)
+{
+    const int64_t stride = (int64_t) gridDim.x * kBlock;
+    for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        out[i] = enc.qdq(in[i], (uint32_t) index64(v, i));
+}
+
+// permuteTensor: out[sum_d idx_d * ostride_d] = in[i] (the collapsed view's estride holds the
+// output strides)
+__global__ __launch_bounds__(kBlock) void permute_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                         uint32_t n, View32 v)
+{
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        out[v.index(i)] = in[i];
+}
+
+__global__ __launch_bounds__(kBlock) void permute64_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                           int64_t n, View v)
+{
+    const int64_t stride = (int64_t) gridDim.x * kBlock;
+    for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        out[index64(v, i)] = in[i];
+}
+
+// float -> half (round to nearest even, v_cvt_f16_f32) -> float
+__device__ __forceinline__ float fp16_rt(float x)
+{
+    return (float) (_Float16) x;
+}
+
+__global__ __launch_bounds__(kBlock) void fp16_vec_kernel(const f4* __restrict__ in, f4* __restrict__ out,
+                                                          int64_t nvec)
+{
+    const int64_t stride = (int64_t) gridDim.x * kBlock;
+    for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride)
+    {
+        f4 x = __builtin_nontemporal_load(in + i);
+        f4 r {fp16_rt(x.x), fp16_rt(x.y), fp16_rt(x.z), fp16_rt(x.w)};
+        __builtin_nontemporal_store(r, out + i);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void fp16_scalar_kernel(const float* __restrict__ in, float* __restrict__ out,
+                                                             int64_t begin, int64_t n)
+{
+    const int64_t stride = (int64_t) gridDim.x * kBlock;
+    for (int64_t i = begin + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += stride)
+        out[i] = fp16_rt(in[i]);
+}
+
+inline bool aligned16(const void* a, const void* b)
+{
+    return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+}
+
+}   // namespace
+
+void launch_qdq_broadcast(const float* in, float* out, int64_t n, int64_t nd, const int64_t* tstr, const int64_t* estr,
+                          const float* mn, const float* mx, const float* delta, const float* offset, hipStream_t s)
+{
+    if (n == 0)
+        return;
+    View v = collapse(n, nd, tstr, estr);
+    EncArrays enc {mn, mx, delta, offset};
+    if (n >= (int64_t(1) << 31))
+    {
+        bcast_scalar64_kernel<<<kMaxStreamBlocks, kBlock, 0, s>>>(in, out, n, v, enc);
+        AIMET_LAUNCH_CHECK();
+        return;
+    }
+    View32 v32 = to32(v);
+    if (v.size[v.nd - 1] % 4 == 0 && aligned16(in, out))
+    {
+        uint32_t nvec = (uint32_t) (n / 4);
+        bcast_vec_kernel<<<stream_blocks(nvec, kBlock), kBlock, 0, s>>>(
+            reinterpret_cast<const f4*>(in), reinterpret_cast<f4*>(out), nvec, v32, (uint32_t) v.estride[v.nd - 1], enc);
+    }
+    else
+        bcast_scalar_kernel<<<stream_blocks(n, kBlock), kBlock, 0, s>>>(in, out, (uint32_t) n, v32, enc);
+    AIMET_LAUNCH_CHECK();
+}
+
+void launch_permute(const float* in, float* out, int64_t n, int64_t nd, const int64_t* istr, const int64_t* ostr,
+                    hipStream_t s)
+{
+    if (n == 0)
+        return;
+    View v = collapse(n, nd, istr, ostr);
+    if (n >= (int64_t(1) << 31))
+        permute64_kernel<<<kMaxStreamBlocks, kBlock, 0, s>>>(in, out, n, v);
+    else
+        permute_kernel<<<stream_blocks(n, kBlock), kBlock, 0, s>>>(in, out, (uint32_t) n, to32(v));
+    AIMET_LAUNCH_CHECK();
+}
+
+void launch_qdq_fp16(const float* in, float* out, int64_t n, hipStream_t s)
+{
+    if (n == 0)
+        return;
+    int64_t done = 0;
+    if (aligned16(in, out))
+    {
+        int64_t nvec = n / 4;
+        if (nvec)
+        {
+            fp16_vec_kernel<<<stream_blocks(nvec, kBlock * 4), kBlock, 0, s>>>(reinterpret_cast<const f4*>(in),
+                                                                             reinterpret_cast<f4*>(out), nvec);
+            AIMET_LAUNCH_CHECK();
+        }
+        done = nvec * 4;
+    }
+    if (done < n)
+    {
+        fp16_scalar_kernel<<<stream_blocks(n - done, kBlock), kBlock, 0, s>>>(in, out, done, n);
+        AIMET_LAUNCH_CHECK();
+    }
+}
+
+}   // namespace aimet_amd
+
+extern "C" {
+
+int aimet_qdq_broadcast(const float* in, float* out, int64_t n, int64_t num_dims, const int64_t* input_strides,
+                        const int64_t* encoding_strides, const float* enc_min, const float* enc_max,
+                        const float* enc_delta, const float* enc_offset, void* stream)
+{
+    using namespace aimet_amd;
+    return guarded([&] {
+        AIMET_REQUIRE(n >= 0 && num_dims >= 0, "invalid broadcast shape");
+        if (n == 0)
+            return;
+        AIMET_REQUIRE(num_dims > 0 && input_strides && encoding_strides, "null strides");
+        require_device_ptr(in, "input");
+        require_device_ptr(out, "output");
+        require_device_ptr(enc_min, "encoding min");
+        require_device_ptr(enc_max, "encoding max");
+        require_device_ptr(enc_delta, "encoding delta");
+        require_device_ptr(enc_offset, "encoding offset");
+        launch_qdq_broadcast(in, out, n, num_dims, input_strides, encoding_strides, enc_min, enc_max, enc_delta,
+                             enc_offset, as_stream(stream));
+    });
+}
+
+int aimet_permute_tensor(const float* in, float* out, int64_t n, int64_t num_dims, const int64_t* input_strides,
+                         const int64_t* output_strides, void* stream)
+{
+    using namespace aimet_amd;
+    return guarded([&] {
+        AIMET_REQUIRE(n >= 0 && num_dims >= 0, "invalid tensor shape");
+        if (n == 0)
+            return;
+        AIMET_REQUIRE(num_dims > 0 && input_strides && output_strides, "null strides");
+        require_device_ptr(in, "input");
+        require_device_ptr(out, "output");
+        AIMET_REQUIRE(in != out, "permute cannot run in place");
+        launch_permute(in, out, n, num_dims, input_strides, output_strides, as_stream(stream));
+    });
+}
+
+int aimet_qdq_fp16(const float* in, float* out, int64_t n, void* stream)
+{
+    using namespace aimet_amd;
+    return guarded([&] {
+        AIMET_REQUIRE(n >= 0, "negative element count");
+        if (n == 0)
+            return;
+        require_device_ptr(in, "input");
+        require_device_ptr(out, "output");
+        launch_qdq_fp16(in, out, n, as_stream(stream));
+    });
+}
+
+}   // extern "C"

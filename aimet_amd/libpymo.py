@@ -178,11 +178,17 @@ class TensorQuantizer:
         self._unsigned = False
         self._valid_stats = False
         self._op = AimetTensorQuantizer(self._scheme)
+        self._channel = None   # bound to channel c of a shared device quantizer (onnx_op.QcQuantizeInfo)
+
+    def _bind(self, shared, channel):
+        """Read statistics from channel `channel` of `shared` (the analyzers of a QcQuantizeOp)."""
+        self._op, self._channel = shared, int(channel)
 
     def resetEncodingStats(self):
         self._valid_stats = False
         self.isEncodingValid = False
-        self._op.resetEncodingStats()
+        if self._channel is None:   # a bound quantizer shares its statistics with its op
+            self._op.resetEncodingStats()
 
     def updateStats(self, tensor, use_cuda=True):
         self._valid_stats = True
@@ -192,6 +198,8 @@ class TensorQuantizer:
         enc = TfEncoding()
         if self._valid_stats:
             enc, _ = self._op.getEncoding(bitwidth, use_symmetric_encoding, self._strict, self._unsigned)
+            if self._channel is not None:
+                enc = enc[self._channel] if isinstance(enc, list) else enc
             self.isEncodingValid = True
         return enc
 

@@ -176,6 +176,28 @@ def main():
     ms = timed(lambda: qe.updateStats(x, True), args.reps, stream)
     row("entropy updateStats (4 launches)", "f3", 8, ms, cpu_rate(lambda: oe.update(xs)),
         note="cpu = updateTensorHistogram_cpu restated (the reference GPU build copies to the host and runs it)")
+    # §8(f) row 4: blockwise (LPBQ-style) QDQ over a [C, K] weight with 64-element blocks along K
+    # (contiguous blocks: 2 merged dims) and over its transpose [K, C] (blocks strided: 3 dims),
+    # plus the fp16 round trip of float quantizers
+    from aimet_amd.onnx_op import BroadcastShapeInfo
+    Kb = N // C
+    for shape, ch, ba in (((C, Kb), 0, 1), ((Kb, C), 1, 0)):
+        info = BroadcastShapeInfo(shape, ch, ba, 64)
+        E = info.numEncodings
+        etab = torch.empty(4, E, device=dev)
+        etab[2].uniform_(0.01, 0.02)
+        etab[3].fill_(-8.0)
+        etab[0] = etab[2] * -8
+        etab[1] = etab[2] * 7
+        nd = info.numDims
+        ts = (ctypes.c_int64 * nd)(*info.tensorStrides)
+        es = (ctypes.c_int64 * nd)(*info.encodingStrides)
+        ms = timed(lambda: lib.aimet_qdq_broadcast(P(x), P(y), N, nd, ts, es, P(etab[0]), P(etab[1]), P(etab[2]),
+                                                   P(etab[3]), sp), args.reps, stream)
+        row("qdq_blockwise %s block 64" % ("x".join(map(str, shape))), "f4", 8, ms,
+            note="%d encodings, %s blocks" % (E, "contiguous" if info.hasContiguousBlocks() else "strided"))
+    ms = timed(lambda: lib.aimet_qdq_fp16(P(x), P(y), N, sp), args.reps, stream)
+    row("qdq_fp16 (float quantizer)", "f4", 8, ms)
     # a14: learned grid forward / backward vs the reference's torch ops
     steps = 255.0
     ms = timed(lambda: lib.aimet_lg_forward(P(x), P(y), 1, C, K, P(delta), P(offset), ctypes.c_float(steps), sp),

@@ -282,6 +282,78 @@ int aimet_adaround_backward(const float* w, const float* alpha, const float* gra
                             int64_t outer, int64_t C, int64_t K, const float* delta_dev, const float* offset_dev,
                             int32_t bw, float reg_param, float beta, float* round_loss_dev, void* stream);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Blockwise (broadcast) quantization and the ONNX QcQuantizeOp                                */
+/* ------------------------------------------------------------------------------------------ */
+
+/* trim_functions.cpp:633-687 quantizeDequantizeBroadcast (Quantization.hpp:150-215): the E
+ * encodings (device float arrays enc_*[E], used as given: no fillEncodingInfo) broadcast over a
+ * contiguous tensor of n elements viewed with num_dims dims; input_strides_host = its row-major
+ * strides, encoding_strides_host = the encodings' strides, 0 along broadcast dims. ROUND_NEAREST. */
+int aimet_qdq_broadcast(const float* in, float* out, int64_t n, int64_t num_dims, const int64_t* input_strides_host,
+                        const int64_t* encoding_strides_host, const float* enc_min, const float* enc_max,
+                        const float* enc_delta, const float* enc_offset, void* stream);
+/* onnx/src/QuantizeDequantizeUtils.cpp:64-95 permuteTensor: out[sum_d idx_d(i) * output_strides[d]] = in[i]. */
+int aimet_permute_tensor(const float* in, float* out, int64_t n, int64_t num_dims, const int64_t* input_strides_host,
+                         const int64_t* output_strides_host, void* stream);
+/* quantizeDequantizeFp16 (onnx/src/AimetOpUtils.cpp:61-67, trim_functions.cu:135-148): out = (float)(half) in,
+ * round to nearest even. */
+int aimet_qdq_fp16(const float* in, float* out, int64_t n, void* stream);
+
+#define AIMET_BCAST_MAX_DIMS 16
+/* onnx/src/QuantizeDequantizeUtils.hpp:166-178 BroadcastShapeInfo: the input viewed with the block
+ * axis split into (num_blocks, block_size) and the broadcastable encoding shape. */
+typedef struct aimet_broadcast_shape_info {
+    int64_t num_dims;
+    int64_t tensor_shape[AIMET_BCAST_MAX_DIMS];
+    int64_t encoding_shape[AIMET_BCAST_MAX_DIMS];
+    int64_t tensor_strides[AIMET_BCAST_MAX_DIMS];
+    int64_t encoding_strides[AIMET_BCAST_MAX_DIMS];
+    int64_t num_elements;
+    int64_t num_encodings;
+    int contiguous_blocks; /* hasContiguousBlocks() */
+} aimet_broadcast_shape_info;
+/* QuantizeDequantizeUtils.cpp:100-170 (channel_axis / block_axis < 0: none). Host only. */
+int aimet_broadcast_shape_info_init(const int64_t* input_shape, int64_t ndims, int channel_axis, int block_axis,
+                                    int block_size, aimet_broadcast_shape_info* out);
+/* QuantizeDequantizeUtils.cpp:173-213 copyToContiguousBlockLayout: every quantization block contiguous. */
+int aimet_copy_to_contiguous_block_layout(const float* in, float* out, const aimet_broadcast_shape_info* info,
+                                          void* stream);
+
+/* TensorQuantizerOpMode (TensorQuantizerOpFacade.h:48-54) */
+enum {
+    AIMET_OP_UPDATE_STATS = 0,
+    AIMET_OP_ONE_SHOT_QUANTIZE_DEQUANTIZE = 1,
+    AIMET_OP_QUANTIZE_DEQUANTIZE = 2,
+    AIMET_OP_PASS_THROUGH = 3
+};
+/* onnx/src/QcQuantizeInfo.h:46-73 with the TensorQuantizer settings its tensorQuantizerRef carry
+ * (TensorQuantizer.h: roundingMode, strict / unsigned symmetric). The reference holds one
+ * TensorQuantizer per encoding; here ONE aimet_tensor_quantizer with num_channels ==
+ * num_encodings (1 per-tensor) holds all their analyzers. `encodings` is the caller's host array,
+ * updated in place by oneShotQuantizeDequantize (min, max, offset, delta). */
+typedef struct aimet_qc_quantize_info {
+    int op_mode;
+    int enabled;
+    int is_int_data_type;
+    int use_per_channel_mode;
+    int channel_axis;
+    int block_axis;
+    int block_size;
+    int use_symmetric_encoding;
+    int use_strict_symmetric;
+    int use_unsigned_symmetric;
+    int rounding_mode;
+    int64_t num_encodings;
+    aimet_tf_encoding* encodings;
+    aimet_tensor_quantizer* quantizer;
+} aimet_qc_quantize_info;
+/* onnx/src/QcQuantizeOp.cpp:62-113 QcQuantizeOp::computeImpl on a contiguous fp32 device tensor
+ * of shape[ndims] (the ORT custom op's Compute; `stream` = the EP's compute stream). After a
+ * oneShotQuantizeDequantize the info switches to quantizeDequantize. */
+int aimet_qc_quantize_op_compute(aimet_qc_quantize_info* info, const float* in, float* out, const int64_t* shape,
+                                 int64_t ndims, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1058,3 +1058,44 @@ orc_tpp* orc_analyzer_tpp(orc_analyzer* a) { return &a->tpp; }
 
 /* Direct PDF access for tests of the sharded path */
 orc_pdf* orc_analyzer_pdf(orc_analyzer* a) { return &a->pdf; }
+
+/* ------------------------------------------------------------------------- */
+/* Blockwise (broadcast) QDQ and the block-layout permutation                  */
+/* ------------------------------------------------------------------------- */
+
+/* trim_functions.cpp:633-660 quantizeDequantizeBroadcastCpu (int index arithmetic as written) */
+void orc_qdq_broadcast(const float* in, float* out, int64_t n, int64_t nd, const int64_t* istr, const int64_t* estr,
+                       const float* emin, const float* emax, const float* edelta, const float* eoff)
+{
+    for (size_t i = 0; i < (size_t) n; i++) {
+        int e = 0;
+        int rem = (int) i;
+        for (int d = 0; d < nd; d++) {
+            int q = (int) (rem / istr[d]);
+            rem = (int) (rem - q * istr[d]);
+            e += (int) (estr[d] * q);
+        }
+        float v = quantize_value(in[i], emin[e], emax[e], edelta[e], eoff[e]);
+        out[i] = dequantize_value(v, edelta[e], eoff[e]);
+    }
+}
+
+/* onnx/src/QuantizeDequantizeUtils.cpp:64-95 permuteTensorCPU */
+void orc_permute(const float* in, float* out, int64_t n, int64_t nd, const int64_t* istr, const int64_t* ostr)
+{
+    int64_t chunk = n;
+    for (int64_t i = nd - 1; i >= 0; i--)
+        if (istr[i] != ostr[i]) {
+            chunk = istr[i];
+            break;
+        }
+    for (size_t i = 0; i < (size_t) n; i += (size_t) chunk) {
+        size_t o = 0, rem = i;
+        for (int d = 0; d < nd; d++) {
+            size_t q = rem / (size_t) istr[d];
+            rem = rem - q * (size_t) istr[d];
+            o += (size_t) ostr[d] * q;
+        }
+        memcpy(out + o, in + i, (size_t) chunk * sizeof(float));
+    }
+}

@@ -59,6 +59,9 @@ def lib():
                                               ctypes.c_int]
         L.orc_per_channel_table.argtypes = [ctypes.POINTER(Encoding), i64, fp]
         L.orc_qdq_per_channel.argtypes = [fp, fp, i64, i64, i64, fp]
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        L.orc_qdq_broadcast.argtypes = [fp, fp, i64, i64, i64p, i64p, fp, fp, fp, fp]
+        L.orc_permute.argtypes = [fp, fp, i64, i64, i64p, i64p]
         L.orc_ste_backward.argtypes = [fp, fp, fp, i64, i64, i64, fp, fp]
         L.orc_get_min.restype = ctypes.c_float
         L.orc_get_min.argtypes = [fp, i64]
@@ -151,6 +154,87 @@ def ste_backward(x, g, mins, maxs, C=1, K=1):
     out = np.empty_like(x)
     lib().orc_ste_backward(_fp(x), _fp(g), _fp(out), x.size, int(C), int(K), _fp(mins), _fp(maxs))
     return out
+
+
+def _i64a(v):
+    a = np.ascontiguousarray(v, dtype=np.int64)
+    return a, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
+
+
+def qdq_broadcast(x, input_strides, encoding_strides, emin, emax, edelta, eoffset):
+    """trim_functions.cpp:633-660 quantizeDequantizeBroadcastCpu (float encoding arrays, used as given)."""
+    x = _f32(x)
+    out = np.empty_like(x)
+    ist, ip = _i64a(input_strides)
+    est, ep = _i64a(encoding_strides)
+    arrs = [_f32(a) for a in (emin, emax, edelta, eoffset)]
+    lib().orc_qdq_broadcast(_fp(x), _fp(out), x.size, len(ist), ip, ep, *[_fp(a) for a in arrs])
+    return out
+
+
+def permute(x, input_strides, output_strides):
+    """QuantizeDequantizeUtils.cpp:64-95 permuteTensorCPU."""
+    x = _f32(x)
+    out = np.empty_like(x)
+    ist, ip = _i64a(input_strides)
+    ost, op = _i64a(output_strides)
+    lib().orc_permute(_fp(x), _fp(out), x.size, len(ist), ip, op)
+    return out
+
+
+def _row_major(shape):
+    st, s = [], 1
+    for d in reversed(shape):
+        st.append(s)
+        s *= d
+    return st[::-1]
+
+
+def broadcast_shape_info(input_shape, channel_axis, block_axis, block_size):
+    """QuantizeDequantizeUtils.cpp:100-170 BroadcastShapeInfo (+ hasContiguousBlocks)."""
+    tshape, eshape = [], []
+    for i, d in enumerate(input_shape):
+        if i == channel_axis:
+            tshape.append(d)
+            eshape.append(d)
+        elif i == block_axis:
+            if d % block_size != 0:
+                raise RuntimeError("Block dimension is not evenly divisible by block size.")
+            tshape += [d // block_size, block_size]
+            eshape += [d // block_size, 1]
+        else:
+            tshape.append(d)
+            eshape.append(1)
+    estr = [0 if (e == 1 and t != 1) else s for e, t, s in zip(eshape, tshape, _row_major(eshape))]
+    contiguous, prev = True, False
+    for t, e in zip(tshape, eshape):
+        if prev and t == e:
+            contiguous = False
+        prev = t != e
+    return dict(num_dims=len(tshape), tensor_shape=tshape, encoding_shape=eshape, tensor_strides=_row_major(tshape),
+                encoding_strides=estr, num_elements=int(np.prod(input_shape)) if len(input_shape) else 1,
+                num_encodings=int(np.prod(eshape)) if eshape else 1, contiguous_blocks=contiguous)
+
+
+def block_layout_strides(info):
+    """copyToContiguousBlockLayout's output strides (QuantizeDequantizeUtils.cpp:173-203)."""
+    nd, es, ts = info["num_dims"], info["encoding_strides"], info["tensor_shape"]
+    order = [i for i in range(nd) if es[i] != 0] + [i for i in range(nd) if es[i] == 0]
+    ost = [0] * nd
+    ost[order[-1]] = 1
+    for i in range(nd - 2, -1, -1):
+        ost[order[i]] = ost[order[i + 1]] * ts[order[i + 1]]
+    return ost
+
+
+def copy_to_contiguous_block_layout(x, info):
+    return permute(x, info["tensor_strides"], block_layout_strides(info))
+
+
+def qdq_fp16(x):
+    """quantizeDequantizeFp16Cpu (AimetOpUtils.cpp:61-67): float -> half (RNE) -> float."""
+    with np.errstate(over="ignore"):
+        return _f32(x).astype(np.float16).astype(np.float32)
 
 
 def get_min(x):

@@ -59,6 +59,8 @@ def lib():
         L.ref_analyzer_set_percentile.argtypes = [ctypes.c_void_p, ctypes.c_float]
         L.ref_analyzer_histogram.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_double),
                                              ctypes.POINTER(ctypes.c_double)]
+        i64p = ctypes.POINTER(ctypes.c_int64)
+        L.ref_qdq_broadcast.argtypes = [fp, fp, i64, i64, i64p, i64p, fp, fp, fp, fp]
         L.ref_tpp_create.restype = ctypes.c_void_p
         L.ref_tpp_destroy.argtypes = [ctypes.c_void_p]
         L.ref_tpp_update.argtypes = [ctypes.c_void_p, fp, i64]
@@ -109,6 +111,18 @@ def partial_encoding(bw, enc: Encoding, sym=False, unsign=False, strict=False) -
     if lib().ref_partial_encoding(int(bw), ctypes.byref(e), int(sym), int(unsign), int(strict)) != 0:
         raise RuntimeError("Cannot determine how to compute partial encoding")
     return e
+
+
+def qdq_broadcast(x, input_strides, encoding_strides, emin, emax, edelta, eoffset):
+    x = _f32(x)
+    out = np.empty_like(x)
+    ist = np.ascontiguousarray(input_strides, dtype=np.int64)
+    est = np.ascontiguousarray(encoding_strides, dtype=np.int64)
+    arrs = [_f32(a) for a in (emin, emax, edelta, eoffset)]
+    P = ctypes.POINTER(ctypes.c_int64)
+    lib().ref_qdq_broadcast(_fp(x), _fp(out), x.size, len(ist), ist.ctypes.data_as(P), est.ctypes.data_as(P),
+                            *[_fp(a) for a in arrs])
+    return out
 
 
 def get_min(x):

@@ -137,6 +137,13 @@ int ref_analyzer_histogram(void* a, double* xleft, double* pdf)
     return i;
 }
 
+// trim_functions.cpp:633-687 (CPU)
+void ref_qdq_broadcast(const float* in, float* out, int64_t n, int64_t nd, const int64_t* istr, const int64_t* estr,
+                       const float* mn, const float* mx, const float* delta, const float* offset)
+{
+    quantizeDequantizeBroadcast(in, out, n, nd, istr, estr, mn, mx, delta, offset, COMP_MODE_CPU, nullptr);
+}
+
 // math_functions.cpp:476-560: the entropy analyzer's TensorProfilingParams, driven directly
 // (EntropyEncodingAnalyzer keeps its copy private)
 void* ref_tpp_create()

@@ -224,10 +224,48 @@ def reference_python():
     return ste, AdaroundLoss, AdaroundHyperParameters
 
 
+BROADCAST_CASES = [   # (input shape, channel axis, block axis, block size)
+    ((2, 3, 4), 1, 0, 1), ((4, 2, 2), 2, 0, 2), ((4, 4), 0, 1, 2), ((10, 4, 10), 1, 0, 2),
+    ((16, 64), 0, 1, 16), ((64, 32), 1, 0, 8), ((8, 6, 3, 3), 0, 1, 3), ((3, 5, 7), -1, 2, 7),
+    ((4, 2, 2), 1, -1, 0), ((6, 2), 1, 0, 2), ((2, 6), 0, 1, 3), ((5, 12, 4), 2, 1, 4),
+]
+
+
+def broadcast_golden():
+    """golden_broadcast.npz: blockwise QDQ (quantizeDequantizeBroadcastCpu, trim_functions.cpp:633-660)
+    of random tensors under random per-block encodings, views from BroadcastShapeInfo."""
+    from oracle import oracle as O
+    rng = np.random.default_rng(20251017)
+    g = {}
+    for i, (shape, ch, ba, bs) in enumerate(BROADCAST_CASES):
+        info = O.broadcast_shape_info(shape, ch, ba, bs)
+        E = info["num_encodings"]
+        x = (rng.standard_normal(int(np.prod(shape))) * rng.uniform(0.5, 4)).astype(np.float32)
+        x[: min(4, x.size)] = EDGE[[2, 5, 7, 10]][: min(4, x.size)]     # nan, 1e30, denormal, -0.5
+        bw = 4 if i % 3 == 0 else 8
+        encs = []
+        for e in range(E):
+            lo, hi = -rng.uniform(0.1, 3), rng.uniform(0.1, 3)
+            sym = bool(e % 2)
+            encs.append(R.get_computed_encodings(bw, lo, hi, sym, False, False).as_tuple())
+        encs = np.array(encs, dtype=np.float64)
+        f = encs[:, :4].astype(np.float32)
+        y = R.qdq_broadcast(x, info["tensor_strides"], info["encoding_strides"], f[:, 0], f[:, 1], f[:, 2], f[:, 3])
+        g["b%d_cfg" % i] = np.array([ch, ba, bs], dtype=np.int64)
+        g["b%d_shape" % i] = np.array(shape, dtype=np.int64)
+        g["b%d_x" % i], g["b%d_encs" % i], g["b%d_y" % i] = x, encs, y
+    g["count"] = np.array(len(BROADCAST_CASES))
+    np.savez_compressed(os.path.join(HERE, "golden_broadcast.npz"), **g)
+
+
 def main():
+    if "--broadcast-only" in sys.argv:
+        broadcast_golden()
+        return
     entropy_golden()
     if "--entropy-only" in sys.argv:
         return
+    broadcast_golden()
     rng = np.random.default_rng(20251015)
     R.lib()
 
