@@ -150,22 +150,131 @@ struct EncArrays
     }
 };
 
-// 4 consecutive elements per lane; the innermost merged dim has size % 4 == 0, so they share the
-// outer indices and their encodings are e0 + j * inner_estride.
+// 4 consecutive elements per lane (the innermost merged dim has size % 4 == 0, so they share the
+// outer indices and their encodings are e0 + j * inner_estride), kUnroll vectors in flight per
+// lane: with LPBQ-sized tables (one encoding per 16-64 elements, tens of MB) the encoding loads
+// miss L2 and are as latency-bound as the data.
+//   MODE 0: inner_estride == 0 -- one encoding per vector (4 scalar loads)
+//   MODE 1: inner_estride == 1, e0 % 4 == 0 and 16-B aligned arrays -- 4 x 16-B vector loads
+//   MODE 2: anything else -- 16 scalar gathers
+constexpr int kUnroll = 4;
+
+template <int MODE>
 __global__ __launch_bounds__(kBlock) void bcast_vec_kernel(const f4* __restrict__ in, f4* __restrict__ out,
                                                            uint32_t nvec, View32 v, uint32_t inner_es, EncArrays enc)
 {
-    const uint32_t stride = gridDim.x * kBlock;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride)
+    const uint32_t stride = gridDim.x * kBlock * kUnroll;
+    for (uint32_t base = blockIdx.x * kBlock * kUnroll + threadIdx.x; base < nvec; base += stride)
     {
-        f4 x        = __builtin_nontemporal_load(in + i);
-        uint32_t e0 = v.index(i * 4);
-        f4 r;
-        r.x = enc.qdq(x.x, e0);
-        r.y = enc.qdq(x.y, e0 + inner_es);
-        r.z = enc.qdq(x.z, e0 + 2 * inner_es);
-        r.w = enc.qdq(x.w, e0 + 3 * inner_es);
-        __builtin_nontemporal_store(r, out + i);
+        f4 x[kUnroll];
+        uint32_t e0[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+        {
+            const uint32_t i = base + u * kBlock;
+            const uint32_t c = i < nvec ? i : nvec - 1;   // clamped (never stored)
+            x[u]             = __builtin_nontemporal_load(in + c);
+            e0[u]            = v.index(c * 4);
+        }
+        f4 mn[kUnroll], mx[kUnroll], dl[kUnroll], of[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+        {
+            const uint32_t e = e0[u];
+            if (MODE == 0)
+            {
+                const float a = enc.mn[e], b = enc.mx[e], d = enc.delta[e], o = enc.offset[e];
+                mn[u] = f4 {a, a, a, a};
+                mx[u] = f4 {b, b, b, b};
+                dl[u] = f4 {d, d, d, d};
+                of[u] = f4 {o, o, o, o};
+            }
+            else if (MODE == 1)
+            {
+                mn[u] = *reinterpret_cast<const f4*>(enc.mn + e);
+                mx[u] = *reinterpret_cast<const f4*>(enc.mx + e);
+                dl[u] = *reinterpret_cast<const f4*>(enc.delta + e);
+                of[u] = *reinterpret_cast<const f4*>(enc.offset + e);
+            }
+            else
+            {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                {
+                    const uint32_t ej = e + j * inner_es;
+                    mn[u][j]          = enc.mn[ej];
+                    mx[u][j]          = enc.mx[ej];
+                    dl[u][j]          = enc.delta[ej];
+                    of[u][j]          = enc.offset[ej];
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u)
+        {
+            const uint32_t i = base + u * kBlock;
+            if (i >= nvec)
+                break;
+            f4 r;
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+            {
+                QdqParams p {mn[u][j], mx[u][j], dl[u][j], of[u][j]};
+                r[j] = dequantize(quantize_nearest(x[u][j], p), p);
+            }
+            __builtin_nontemporal_store(r, out + i);
+        }
+    }
+}
+
+// Blocks strided along the outer dim -- the merged view [A][B][C] with encodings [A][C] (ONNX
+// MatMul weights [K, N] with blocks along K: channel axis 1, block axis 0). A lane owns 4
+// consecutive columns of one block and kRows of its B rows: the 4 x 16-B encoding loads are
+// reused kRows times and every row load is coalesced across the wave (lanes = columns).
+constexpr int kRows = 16;
+
+__global__ __launch_bounds__(kBlock) void bcast_colblock_kernel(const f4* __restrict__ in, f4* __restrict__ out,
+                                                                uint32_t A, uint32_t B, uint32_t C4, FastDiv divC4,
+                                                                FastDiv divRg, uint32_t nrg, EncArrays enc)
+{
+    const uint32_t items  = A * nrg * C4;
+    const uint32_t stride = gridDim.x * kBlock;
+    for (uint32_t it = blockIdx.x * kBlock + threadIdx.x; it < items; it += stride)
+    {
+        const uint32_t t  = divC4.div(it);
+        const uint32_t c4 = it - t * C4;
+        const uint32_t a  = divRg.div(t);
+        const uint32_t rg = t - a * nrg;
+        const uint32_t e  = (a * C4 + c4) * 4;
+        const f4 mn = *reinterpret_cast<const f4*>(enc.mn + e);
+        const f4 mx = *reinterpret_cast<const f4*>(enc.mx + e);
+        const f4 dl = *reinterpret_cast<const f4*>(enc.delta + e);
+        const f4 of = *reinterpret_cast<const f4*>(enc.offset + e);
+        const uint32_t b0   = rg * kRows;
+        const uint32_t rows = B - b0 < (uint32_t) kRows ? B - b0 : (uint32_t) kRows;
+        const uint32_t base = (a * B + b0) * C4 + c4;
+        for (uint32_t r0 = 0; r0 < rows; r0 += 4)
+        {
+            f4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (r0 + u < rows)
+                    x[u] = __builtin_nontemporal_load(in + base + (r0 + u) * C4);
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+            {
+                if (r0 + u >= rows)
+                    break;
+                f4 y;
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                {
+                    QdqParams p {mn[j], mx[j], dl[j], of[j]};
+                    y[j] = dequantize(quantize_nearest(x[u][j], p), p);
+                }
+                __builtin_nontemporal_store(y, out + base + (r0 + u) * C4);
+            }
+        }
     }
 }
 
@@ -252,9 +361,29 @@ void launch_qdq_broadcast(const float* in, float* out, int64_t n, int64_t nd, co
     View32 v32 = to32(v);
     if (v.size[v.nd - 1] % 4 == 0 && aligned16(in, out))
     {
-        uint32_t nvec = (uint32_t) (n / 4);
-        bcast_vec_kernel<<<stream_blocks(nvec, kBlock), kBlock, 0, s>>>(
-            reinterpret_cast<const f4*>(in), reinterpret_cast<f4*>(out), nvec, v32, (uint32_t) v.estride[v.nd - 1], enc);
+        const uint32_t nvec = (uint32_t) (n / 4);
+        const uint32_t ies  = (uint32_t) v.estride[v.nd - 1];
+        // MODE 1 needs every e0 = sum_d q_d * estride_d to be a multiple of 4: all estrides are
+        // (the innermost is 1 and its run is a multiple of 4 elements)
+        bool vec_tab = ies == 1 && aligned16(mn, mx) && aligned16(delta, offset);
+        for (int d = 0; d + 1 < v.nd; ++d)
+            vec_tab = vec_tab && v.estride[d] % 4 == 0;
+        const int blocks = stream_blocks(nvec, (int64_t) kBlock * kUnroll);
+        auto in4 = reinterpret_cast<const f4*>(in);
+        auto out4 = reinterpret_cast<f4*>(out);
+        if (vec_tab && v.nd == 3 && v.estride[1] == 0 && v.estride[0] == v.size[2])
+        {
+            const uint32_t A = (uint32_t) v.size[0], B = (uint32_t) v.size[1], C4 = (uint32_t) (v.size[2] / 4);
+            const uint32_t nrg = (B + kRows - 1) / kRows;
+            bcast_colblock_kernel<<<stream_blocks((int64_t) A * nrg * C4, kBlock), kBlock, 0, s>>>(
+                in4, out4, A, B, C4, FastDiv(C4), FastDiv(nrg), nrg, enc);
+        }
+        else if (ies == 0)
+            bcast_vec_kernel<0><<<blocks, kBlock, 0, s>>>(in4, out4, nvec, v32, ies, enc);
+        else if (vec_tab)
+            bcast_vec_kernel<1><<<blocks, kBlock, 0, s>>>(in4, out4, nvec, v32, ies, enc);
+        else
+            bcast_vec_kernel<2><<<blocks, kBlock, 0, s>>>(in4, out4, nvec, v32, ies, enc);
     }
     else
         bcast_scalar_kernel<<<stream_blocks(n, kBlock), kBlock, 0, s>>>(in, out, (uint32_t) n, v32, enc);

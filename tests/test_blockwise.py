@@ -221,6 +221,18 @@ def test_broadcast_qdq_large_vs_oracle():
         y = quantize_dequantize_broadcast(torch.from_numpy(x).cuda(), info, _encs_from(tab)).cpu().numpy()
         want = O.qdq_broadcast(x, info.tensorStrides, info.encodingStrides, tab[:, 0], tab[:, 1], tab[:, 2], tab[:, 3])
         np.testing.assert_array_equal(bits(y), bits(want), err_msg=str(shape))
+        # the same through the C-ABI with encoding arrays that are not 16-B aligned (gather path)
+        from aimet_amd import _native
+        buf = torch.zeros(4 * E + 1, device="cuda")
+        arrs = [buf[1 + k * E: 1 + (k + 1) * E] for k in range(4)]
+        for k in range(4):
+            arrs[k].copy_(torch.from_numpy(np.ascontiguousarray(tab[:, k])))
+        xt, yt = torch.from_numpy(x).cuda(), torch.empty(x.size, device="cuda")
+        nd = info.numDims
+        _native.call("aimet_qdq_broadcast", xt.data_ptr(), yt.data_ptr(), x.size, nd,
+                     (ctypes.c_int64 * nd)(*info.tensorStrides), (ctypes.c_int64 * nd)(*info.encodingStrides),
+                     *[a.data_ptr() for a in arrs], torch.cuda.current_stream().cuda_stream)
+        np.testing.assert_array_equal(bits(yt.cpu().numpy()), bits(want), err_msg=str(shape))
 
 
 @pytest.mark.gpu
