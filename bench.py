@@ -123,7 +123,17 @@ def cpu_baseline(acts, weights, act_enc, w_enc, images):
     for w, C, K, tab in ws:
         O.qdq_per_channel(w, C, K, tab)
     dt = time.perf_counter() - t0
-    return n / dt / 1e9, n, dt
+    # the OpenMP variant of the same loops on the box's CPU share
+    threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    t0 = time.perf_counter()
+    for x, e in xs:
+        O.qdq_per_tensor_omp(x, e.min, e.max, 8, threads)
+    for w, C, K, tab in ws:
+        O.qdq_per_channel_omp(w, C, K, tab, threads)
+    dt_omp = time.perf_counter() - t0
+    omp = {"value": round(n / dt_omp / 1e9, 4), "cores": threads, "nproc": os.cpu_count(),
+           "openmp": O.openmp_enabled()}
+    return n / dt / 1e9, n, dt, omp
 
 
 def main():
@@ -278,11 +288,12 @@ def main():
                                "timed step (%s)" % (len(act_calls), "graph replay" if use_graph else "eager")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        gel, n, secs = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images)
+        gel, n, secs, omp = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images)
         result["cpu_baseline"] = {"value": round(gel, 4), "unit": "Gelem/s", "cores": 1, "kind": "port",
                                   "sample": "first %d images of each activation tensor + all weights (%d elems, "
                                             "%.1f s), oracle/dlq_oracle.c single-threaded on the host"
-                                            % (args.cpu_sample_images, n, secs)}
+                                            % (args.cpu_sample_images, n, secs),
+                                  "omp": omp}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -227,6 +227,38 @@ void orc_qdq_per_channel(const float* in, float* out, int64_t C, int64_t N, int6
     }
 }
 
+/* OpenMP variants of the two QDQ loops (the cpu_baseline's multi-core figure):
+ * the same element arithmetic, iterations split statically over `threads` threads. */
+void orc_qdq_per_tensor_omp(const float* in, float* out, int64_t n, double enc_min, double enc_max, int bw,
+                            int threads)
+{
+    orc_encoding e = orc_fill_encoding_info(bw, enc_min, enc_max);
+    float mn = (float) e.min, mx = (float) e.max, d = (float) e.delta, off = (float) e.offset;
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int64_t i = 0; i < n; ++i)
+        out[i] = dequantize_value(quantize_value(in[i], mn, mx, d, off), d, off);
+}
+
+void orc_qdq_per_channel_omp(const float* in, float* out, int64_t C, int64_t N, int64_t K, const float* table,
+                             int threads)
+{
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int64_t i = 0; i < N; ++i) {
+        int64_t c = (i / K) % C;
+        float mn = table[c], mx = table[C + c], d = table[2 * C + c], off = table[3 * C + c];
+        out[i] = dequantize_value(quantize_value(in[i], mn, mx, d, off), d, off);
+    }
+}
+
+int orc_openmp_enabled(void)
+{
+#ifdef _OPENMP
+    return 1;
+#else
+    return 0;
+#endif
+}
+
 /* quantsim_straight_through_grad.py:91-118 compute_dloss_by_dx: grad * (min <= x <= max),
  * min/max are float32 tensors broadcast along ch_axis (C==1: per-tensor). Layout [outer][C][K]. */
 void orc_ste_backward(const float* x, const float* g, float* gin, int64_t N, int64_t C, int64_t K,

@@ -59,6 +59,9 @@ def lib():
                                               ctypes.c_int]
         L.orc_per_channel_table.argtypes = [ctypes.POINTER(Encoding), i64, fp]
         L.orc_qdq_per_channel.argtypes = [fp, fp, i64, i64, i64, fp]
+        L.orc_qdq_per_tensor_omp.argtypes = [fp, fp, i64, ctypes.c_double, ctypes.c_double, ctypes.c_int,
+                                             ctypes.c_int]
+        L.orc_qdq_per_channel_omp.argtypes = [fp, fp, i64, i64, i64, fp, ctypes.c_int]
         i64p = ctypes.POINTER(ctypes.c_int64)
         L.orc_qdq_broadcast.argtypes = [fp, fp, i64, i64, i64p, i64p, fp, fp, fp, fp]
         L.orc_permute.argtypes = [fp, fp, i64, i64, i64p, i64p]
@@ -138,6 +141,25 @@ def per_channel_table(encs):
     table = np.empty((4, C), dtype=np.float32)
     lib().orc_per_channel_table(arr, C, _fp(table))
     return table
+
+
+def qdq_per_tensor_omp(x, enc_min, enc_max, bw, threads):
+    x = _f32(x)
+    out = np.empty_like(x)
+    lib().orc_qdq_per_tensor_omp(_fp(x), _fp(out), x.size, float(enc_min), float(enc_max), int(bw), int(threads))
+    return out
+
+
+def qdq_per_channel_omp(x, C, K, table, threads):
+    x = _f32(x)
+    out = np.empty_like(x)
+    table = _f32(table)
+    lib().orc_qdq_per_channel_omp(_fp(x), _fp(out), int(C), x.size, int(K), _fp(table), int(threads))
+    return out
+
+
+def openmp_enabled():
+    return bool(lib().orc_openmp_enabled())
 
 
 def qdq_per_channel(x, C, K, table):
