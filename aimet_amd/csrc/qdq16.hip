@@ -13,6 +13,8 @@
 
 #include <hip/hip_fp16.h>
 
+#include <cstdlib>
+
 namespace aimet_amd
 {
 namespace
@@ -162,10 +164,74 @@ __global__ __launch_bounds__(kBlock) void ste16_scalar_kernel(const unsigned sho
     }
 }
 
+// ---- per-tensor ROUND_NEAREST via a 65,536-entry table ---------------------------------------------
+// A 16-bit input has 65,536 possible values, so a per-tensor nearest QDQ is a pure function of the
+// input bits: the table is built once per launch by the arithmetic above (so it is bit-identical to
+// it) and each persistent workgroup stages it in LDS (128 KiB of the CU's 160) and maps its share
+// of the tensor with one LDS read per element -- the arithmetic kernel is VALU-bound at ~20 ops per
+// element, the lookup is ~3.
+constexpr int kLutSize    = 65536;
+constexpr int kLutBlock   = 1024;
+constexpr int kLutUnroll  = 8;
+constexpr int64_t kLutMinN = int64_t(1) << 23;   // below: the table build is not amortised
+
+template <int IO>
+__global__ __launch_bounds__(kBlock) void qdq16_lut_build(QdqParams p, unsigned short* __restrict__ lut)
+{
+    const int b = blockIdx.x * kBlock + threadIdx.x;
+    if (b < kLutSize)
+        lut[b] = from_f32<IO>(qdq<false>(to_f32<IO>((unsigned short) b), p, 0, 0, 1.0f / p.delta));
+}
+
+__global__ __launch_bounds__(kLutBlock) void qdq16_lut_kernel(const u16x8* __restrict__ in, u16x8* __restrict__ out,
+                                                              int64_t nvec, const uint4* __restrict__ lut)
+{
+    __shared__ unsigned short tab[kLutSize];
+    uint4* t4 = reinterpret_cast<uint4*>(tab);
+#pragma unroll
+    for (int k = 0; k < kLutSize * 2 / 16 / kLutBlock; ++k)
+        t4[k * kLutBlock + threadIdx.x] = lut[k * kLutBlock + threadIdx.x];
+    __syncthreads();
+    constexpr int U      = kLutUnroll;   // 16-B loads in flight per lane: one workgroup per CU
+    const int64_t stride = (int64_t) gridDim.x * kLutBlock * U;
+    for (int64_t base = (int64_t) blockIdx.x * kLutBlock * U + threadIdx.x; base < nvec; base += stride)
+    {
+        u16x8 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const int64_t i = base + (int64_t) u * kLutBlock;
+            if (i < nvec)
+                v[u] = __builtin_nontemporal_load(in + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const int64_t i = base + (int64_t) u * kLutBlock;
+            if (i >= nvec)
+                break;
+            u16x8 r;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                r[k] = tab[v[u][k]];
+            __builtin_nontemporal_store(r, out + i);
+        }
+    }
+}
+
 bool aligned16(const void* a, const void* b, const void* c = nullptr)
 {
     return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(c)) & 15) ==
            0;
+}
+
+bool lut_enabled()
+{
+    static const bool on = [] {
+        const char* e = getenv("AIMET_QDQ16_LUT");   // A/B switch for measurements and tests
+        return !(e && e[0] == '0');
+    }();
+    return on;
 }
 
 // vector part over [0, nvec*8), scalar tail (per-tensor) or everything scalar (K % 8 != 0)
@@ -175,7 +241,23 @@ void launch_qdq16(const void* in, void* out, int64_t n, const QdqParams& p, int6
 {
     const bool vec_ok = aligned16(in, out) && (!CH || (K % 8 == 0 && n < (int64_t(1) << 32)));
     int64_t nvec      = vec_ok ? n / 8 : 0;
-    if (nvec > 0)
+    if (!CH && !STO && nvec > 0 && n >= kLutMinN && lut_enabled())
+    {
+        void* lut = nullptr;
+        AIMET_HIP_CHECK(hipMallocAsync(&lut, kLutSize * sizeof(unsigned short), s));
+        qdq16_lut_build<IO><<<kLutSize / kBlock, kBlock, 0, s>>>(p, static_cast<unsigned short*>(lut));
+        AIMET_LAUNCH_CHECK();
+        int dev = 0, cus = 0;
+        AIMET_HIP_CHECK(hipGetDevice(&dev));
+        AIMET_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        const int64_t want = ceil_div(nvec, (int64_t) kLutBlock * kLutUnroll);
+        const int grid     = (int) (want < cus ? want : cus);
+        qdq16_lut_kernel<<<grid, kLutBlock, 0, s>>>(reinterpret_cast<const u16x8*>(in), reinterpret_cast<u16x8*>(out),
+                                                    nvec, static_cast<const uint4*>(lut));
+        AIMET_LAUNCH_CHECK();
+        AIMET_HIP_CHECK(hipFreeAsync(lut, s));
+    }
+    else if (nvec > 0)
     {
         ChannelMap16 map {FastDiv((uint32_t) (CH ? K : 1)), FastDiv((uint32_t) (CH ? C : 1)), (uint32_t) C};
         qdq16_vec_kernel<IO, CH, STO><<<(unsigned) ceil_div(nvec, kBlock), kBlock, 0, s>>>(

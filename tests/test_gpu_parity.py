@@ -532,6 +532,27 @@ def test_16bit_io_qdq_equals_upcast_path(dtype, rm):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_16bit_io_qdq_table_path_all_bit_patterns(dtype):
+    """Large per-tensor nearest QDQ takes the 65,536-entry table path (qdq16.hip: qdq16_lut_kernel):
+    every 16-bit input pattern, tiled past the table threshold, equals upcast -> fp32 QDQ -> downcast."""
+    from aimet_amd import _native
+    from aimet_amd.tensor_quantizer import IO_DTYPES
+    code = IO_DTYPES[dtype]
+    stream = torch.cuda.current_stream().cuda_stream
+    n = (1 << 23) + 13
+    pat = torch.arange(65536, dtype=torch.int32, device=DEV).to(torch.int16).view(dtype)
+    x = pat.repeat(n // 65536 + 1)[:n].contiguous()
+    for lo, hi, bw in ((-2.5, 4.0, 8), (-1e-3, 7e4, 16), (0.0, 1.0, 4), (-6e4, 6e4, 8)):
+        enc = enc_of(lo, hi, bw)
+        out16 = torch.empty_like(x)
+        _native.call("aimet_qdq_per_tensor_16", x.data_ptr(), out16.data_ptr(), n, code, enc.to_c(), 0, 0, stream)
+        xf = x.float()
+        out32 = torch.empty_like(xf)
+        _native.call("aimet_qdq_per_tensor", xf.data_ptr(), out32.data_ptr(), n, enc.to_c(), 0, 0, stream)
+        np.testing.assert_array_equal(_bits16(out16), _bits16(out32.to(dtype)), err_msg=str((lo, hi, bw)))
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
 def test_16bit_io_ste_and_autograd(dtype):
     from aimet_amd.quantizers import (QuantScheme, StaticGridPerChannelQuantizer, StaticGridPerTensorQuantizer,
                                       compute_dloss_by_dx)
