@@ -35,12 +35,25 @@ struct AdaChannel
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-// sigmoid with the hardware exp2 (v_exp_f32, ~1 ulp) and an IEEE reciprocal: within 2 ulp of
-// torch's 1/(1+expf(-a)); h enters Wq additively inside floor/clamp, so Wq stays within the
-// tests' 1e-6 absolute tolerance, and dL/dalpha within 1e-5 relative.
+// sigmoid with the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32, ~1 ulp each): within a
+// few ulp of torch's 1/(1+expf(-a)); h enters Wq additively inside the clamp (no rounding after
+// it), so Wq stays within the tests' 1e-6 absolute tolerance, and dL/dalpha within 1e-5 relative.
 __device__ __forceinline__ float sigmoidf(float a)
 {
-    return 1.0f / (1.0f + __expf(-a));
+    return __builtin_amdgcn_rcpf(1.0f + __expf(-a));
+}
+
+// floor(w / d) exactly as the IEEE division gives it, from q = w * rcp (rcp = v_rcp_f32(d), within
+// 1 ulp): |q - RN(w/d)| <= 3.5 ulp(q) < 2^-21 (|q| + 1), so when q lies farther than that from
+// every integer both floors agree; otherwise (and for non-finite q) the division decides.
+__device__ __forceinline__ float floor_div(float w, float d, float rcp)
+{
+    const float q   = w * rcp;
+    const float f   = __builtin_floorf(q);
+    const float thr = (__builtin_fabsf(q) + 1.0f) * 4.76837158203125e-7f;   // 2^-21
+    if (q - f > thr && (f + 1.0f) - q > thr)
+        return f;
+    return __builtin_floorf(w / d);
 }
 
 // |x|^beta for x in [0, 1] (the rounding-loss power): exp2(beta * log2 x) on the hardware
@@ -56,9 +69,9 @@ struct AdaParams
     int soft;
 };
 
-__device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, const AdaParams& p)
+__device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, const AdaParams& p, float rcp)
 {
-    float t = __builtin_floorf(w / d);   // IEEE division: floor() is sensitive to the last ulp
+    float t = floor_div(w, d, rcp);   // == floor of the IEEE division (floor is sensitive to the last ulp)
     float h;
     if (p.soft)
     {
@@ -72,9 +85,10 @@ __device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, con
 }
 
 // dL/dalpha of Wq (clamp pass-through masks as torch autograd) + the rounding-loss gradient
-__device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, float o, const AdaParams& p, float& loss)
+__device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, float o, const AdaParams& p, float rcp,
+                                         float& loss)
 {
-    float t   = __builtin_floorf(w / d);
+    float t   = floor_div(w, d, rcp);
     float sg  = sigmoidf(a);
     float pre = sg * kZmG + kGamma;
     float h   = fminf(fmaxf(pre, 0.0f), 1.0f);
@@ -88,7 +102,7 @@ __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, flo
         float pw = pow01(ax, p.beta);
         loss += 1.0f - pw;
         // d/dh [reg * (1 - |2h-1|^beta)] = -reg * beta * |x|^(beta-1) * sign(x) * 2
-        float dp = (ax > 0.0f) ? p.beta * (pw / ax) * (x > 0.0f ? 1.0f : -1.0f) : 0.0f;
+        float dp = (ax > 0.0f) ? p.beta * (pw * __builtin_amdgcn_rcpf(ax)) * (x > 0.0f ? 1.0f : -1.0f) : 0.0f;
         gh += -p.reg * dp * 2.0f;
     }
     // h = clamp(pre, 0, 1); pre = sigmoid(a) * (zeta - gamma) + gamma
@@ -107,12 +121,12 @@ __global__ __launch_bounds__(kBlock) void adaround_fwd_vec_kernel(const f4* __re
     if (i >= nq)
         return;
     const uint32_t c = map.channel(4 * i);
-    const float d = delta[c], o = offset[c];
+    const float d = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(d);
     f4 wv = __builtin_nontemporal_load(w + i), av = __builtin_nontemporal_load(alpha + i), r;
-    r.x = ada_fwd(wv.x, av.x, d, o, p);
-    r.y = ada_fwd(wv.y, av.y, d, o, p);
-    r.z = ada_fwd(wv.z, av.z, d, o, p);
-    r.w = ada_fwd(wv.w, av.w, d, o, p);
+    r.x = ada_fwd(wv.x, av.x, d, o, p, rcp);
+    r.y = ada_fwd(wv.y, av.y, d, o, p, rcp);
+    r.z = ada_fwd(wv.z, av.z, d, o, p, rcp);
+    r.w = ada_fwd(wv.w, av.w, d, o, p, rcp);
     __builtin_nontemporal_store(r, wq + i);
 }
 
@@ -125,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void adaround_fwd_kernel(const float* __res
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
     {
         uint32_t c = map.channel(i);
-        wq[i]      = ada_fwd(w[i], alpha[i], delta[c], offset[c], p);
+        wq[i]      = ada_fwd(w[i], alpha[i], delta[c], offset[c], p, __builtin_amdgcn_rcpf(delta[c]));
     }
 }
 
@@ -155,17 +169,35 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
                                                                   float* __restrict__ round_loss)
 {
     float loss = 0.0f;
-    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nq; i += gridDim.x * kBlock)
+    constexpr int U       = 4;   // quads in flight per lane (3 x 16-B loads each)
+    const uint32_t stride = gridDim.x * kBlock * U;
+    for (uint32_t base = blockIdx.x * kBlock * U + threadIdx.x; base < nq; base += stride)
     {
-        const uint32_t c = map.channel(4 * i);
-        const float d = delta[c], o = offset[c];
-        f4 wv = __builtin_nontemporal_load(w + i), av = __builtin_nontemporal_load(alpha + i);
-        f4 gv = __builtin_nontemporal_load(g + i), r;
-        r.x = ada_bwd(wv.x, av.x, gv.x, d, o, p, loss);
-        r.y = ada_bwd(wv.y, av.y, gv.y, d, o, p, loss);
-        r.z = ada_bwd(wv.z, av.z, gv.z, d, o, p, loss);
-        r.w = ada_bwd(wv.w, av.w, gv.w, d, o, p, loss);
-        __builtin_nontemporal_store(r, ga + i);
+        f4 wv[U], av[U], gv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t i = base + u * kBlock;
+            const uint32_t j = i < nq ? i : nq - 1;   // clamped (never stored)
+            wv[u] = __builtin_nontemporal_load(w + j);
+            av[u] = __builtin_nontemporal_load(alpha + j);
+            gv[u] = __builtin_nontemporal_load(g + j);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t i = base + u * kBlock;
+            if (i >= nq)
+                break;
+            const uint32_t c = map.channel(4 * i);
+            const float d = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(d);
+            f4 r;
+            r.x = ada_bwd(wv[u].x, av[u].x, gv[u].x, d, o, p, rcp, loss);
+            r.y = ada_bwd(wv[u].y, av[u].y, gv[u].y, d, o, p, rcp, loss);
+            r.z = ada_bwd(wv[u].z, av[u].z, gv[u].z, d, o, p, rcp, loss);
+            r.w = ada_bwd(wv[u].w, av[u].w, gv[u].w, d, o, p, rcp, loss);
+            __builtin_nontemporal_store(r, ga + i);
+        }
     }
     if (p.reg != 0.0f && round_loss)
     {
@@ -187,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
     {
         uint32_t c = map.channel(i);
-        ga[i]      = ada_bwd(w[i], alpha[i], g[i], delta[c], offset[c], p, loss);
+        ga[i]      = ada_bwd(w[i], alpha[i], g[i], delta[c], offset[c], p, __builtin_amdgcn_rcpf(delta[c]), loss);
     }
     if (p.reg != 0.0f && round_loss)
     {
@@ -261,7 +293,7 @@ int aimet_adaround_backward(const float* w, const float* alpha, const float* g, 
             aligned16(ga))
         {
             uint32_t nq = (uint32_t) (n / 4);
-            int64_t blocks = ceil_div(nq, kBlock);
+            int64_t blocks = ceil_div(nq, kBlock * 4);
             adaround_bwd_vec_kernel<<<(unsigned) (blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid), kBlock, 0,
                                       as_stream(stream)>>>(
                 reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),

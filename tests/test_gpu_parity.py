@@ -420,6 +420,29 @@ def test_adaround_backward_with_round_loss_vs_torch(beta, shape):
     assert abs(loss.item() - loss_ref.item()) <= 1e-4 * abs(loss_ref.item())
 
 
+def test_adaround_hard_rounding_floor_exact_at_multiples():
+    """floor(W / delta) in the AdaRound kernels (reciprocal fast path, adaround.hip: floor_div) equals
+    torch's IEEE floor(W / delta) bit for bit, on weights at exact multiples of delta and 1-2 ulp
+    beside them; hard rounding makes Wq exact, so the comparison is equality."""
+    from aimet_amd.adaround import AdaroundFunction
+    torch.manual_seed(3)
+    C, K = 64, 1024
+    delta = (torch.rand(C, device=DEV) * 0.01 + 0.0005)
+    k = torch.randint(-140, 140, (C, K), device=DEV).float()
+    w = k * delta.view(C, 1)
+    for step in (0, 1, -1, 2, -2):
+        ws = w if step == 0 else torch.nextafter(w, w + step * float("inf"))
+        if abs(step) == 2:
+            ws = torch.nextafter(ws, ws + step * float("inf"))
+        offset = torch.full((C,), -128.0, device=DEV)
+        alpha = torch.randn(C, K, device=DEV)
+        with torch.no_grad():
+            wq = AdaroundFunction.apply(ws, alpha, delta, offset, 8, 0, False)
+            ref = (torch.clamp(torch.floor(ws / delta.view(C, 1)) + (alpha >= 0).float() - offset.view(C, 1), 0, 255)
+                   + offset.view(C, 1)) * delta.view(C, 1)
+        assert torch.equal(wq, ref), step
+
+
 def test_channel_plan_equals_individual_launches():
     """All parameter QDQs in one launch == one launch per tensor (incl. K % 4 != 0, axis 1)."""
     from aimet_amd.tensor_quantizer import ChannelQdqPlan, per_channel_view, qdq_per_channel_table
