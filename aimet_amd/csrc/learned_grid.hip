@@ -20,6 +20,7 @@ namespace
 {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
+constexpr int kLgUnroll = 4;
 
 struct LgChannel
 {
@@ -74,14 +75,31 @@ struct Sums
     float a, b, d;
 };
 
-__device__ __forceinline__ void lg_bwd_elem(float x, float g, float dl, float o, float steps, float& gx, Sums& s)
+// q = x / dl from the reciprocal (rcp = v_rcp_f32(dl), within 1 ulp): |q - RN(x/dl)| <= 3.5 ulp(q).
+// rint(q) equals rint of the IEEE quotient unless a half-integer lies within 2^-21 (|q| + 1) of q
+// (ties-to-even only acts exactly on half-integers); then -- and for non-finite q -- the division
+// decides. The returned quotient feeds only the tolerance-checked sum B.
+__device__ __forceinline__ float rint_div(float x, float dl, float rcp, float& q)
 {
-    float xr   = __builtin_rintf(x / dl) - o;
+    q               = x * rcp;
+    const float h   = q - __builtin_floorf(q);
+    const float thr = (__builtin_fabsf(q) + 1.0f) * 4.76837158203125e-7f;   // 2^-21
+    if (__builtin_fabsf(h - 0.5f) > thr)                                     // false for NaN / inf
+        return __builtin_rintf(q);
+    q = x / dl;
+    return __builtin_rintf(q);
+}
+
+__device__ __forceinline__ void lg_bwd_elem(float x, float g, float dl, float o, float steps, float rcp, float& gx,
+                                            Sums& s)
+{
+    float q;
+    float xr   = rint_div(x, dl, rcp, q) - o;
     bool mask  = (xr >= 0.0f) && (xr <= steps);
     float xq   = fminf(fmaxf(xr, 0.0f), steps);
     gx         = mask ? g : 0.0f * g;      // mask_tensor * grad (keeps -0 / NaN behaviour of a multiply)
     s.a += (xq + o) * g;
-    s.b += mask ? (x / dl) * g : 0.0f;
+    s.b += mask ? q * g : 0.0f;
     s.d += mask ? 0.0f : g;
 }
 
@@ -122,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
                                                                const float* __restrict__ offset, float steps,
                                                                float* __restrict__ sums, int vec)
 {
-    const float dl = delta[0], o = offset[0];
+    const float dl = delta[0], o = offset[0], rcp = __builtin_amdgcn_rcpf(dl);
     Sums s {0, 0, 0};
     if (vec)
     {
@@ -132,10 +150,10 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
             f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + i);
             f4 b = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + i);
             float r0, r1, r2, r3;
-            lg_bwd_elem(a.x, b.x, dl, o, steps, r0, s);
-            lg_bwd_elem(a.y, b.y, dl, o, steps, r1, s);
-            lg_bwd_elem(a.z, b.z, dl, o, steps, r2, s);
-            lg_bwd_elem(a.w, b.w, dl, o, steps, r3, s);
+            lg_bwd_elem(a.x, b.x, dl, o, steps, rcp, r0, s);
+            lg_bwd_elem(a.y, b.y, dl, o, steps, rcp, r1, s);
+            lg_bwd_elem(a.z, b.z, dl, o, steps, rcp, r2, s);
+            lg_bwd_elem(a.w, b.w, dl, o, steps, rcp, r3, s);
             f4 r = {r0, r1, r2, r3};
             if (gx)
                 __builtin_nontemporal_store(r, reinterpret_cast<f4*>(gx) + i);
@@ -143,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
         for (int64_t i = nv * 4 + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
         {
             float r;
-            lg_bwd_elem(x[i], g[i], dl, o, steps, r, s);
+            lg_bwd_elem(x[i], g[i], dl, o, steps, rcp, r, s);
             if (gx)
                 gx[i] = r;
         }
@@ -153,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
         for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
         {
             float r;
-            lg_bwd_elem(x[i], g[i], dl, o, steps, r, s);
+            lg_bwd_elem(x[i], g[i], dl, o, steps, rcp, r, s);
             if (gx)
                 gx[i] = r;
         }
@@ -177,7 +195,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
 {
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
     {
-        const float dl = delta[c], o = offset[c];
+        const float dl = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(dl);
         Sums s {0, 0, 0};
         for (int64_t r = 0; r < outer; ++r)
         {
@@ -185,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
             for (int64_t k = threadIdx.x; k < K; k += kBlock)
             {
                 float v;
-                lg_bwd_elem(x[base + k], g[base + k], dl, o, steps, v, s);
+                lg_bwd_elem(x[base + k], g[base + k], dl, o, steps, rcp, v, s);
                 if (gx)
                     gx[base + k] = v;
             }
@@ -214,23 +232,39 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
     const int64_t Q  = outer * K4;
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
     {
-        const float dl = delta[c], o = offset[c];
+        const float dl = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(dl);
         Sums s {0, 0, 0};
-        for (int64_t j = (int64_t) blockIdx.y * kBlock + threadIdx.x; j < Q; j += (int64_t) splits * kBlock)
+        // kLgUnroll quads (2 x 16-B loads each) in flight per lane
+        const int64_t step = (int64_t) splits * kBlock;
+        for (int64_t j0 = (int64_t) blockIdx.y * kBlock + threadIdx.x; j0 < Q; j0 += step * kLgUnroll)
         {
-            const int64_t r = outer == 1 ? 0 : divK4.div((uint32_t) j);
-            const int64_t i = (r * C + c) * K4 + (j - r * K4);
-            f4 a = __builtin_nontemporal_load(x + i);
-            f4 b = __builtin_nontemporal_load(g + i);
-            float r0, r1, r2, r3;
-            lg_bwd_elem(a.x, b.x, dl, o, steps, r0, s);
-            lg_bwd_elem(a.y, b.y, dl, o, steps, r1, s);
-            lg_bwd_elem(a.z, b.z, dl, o, steps, r2, s);
-            lg_bwd_elem(a.w, b.w, dl, o, steps, r3, s);
-            if (gx)
+            f4 a[kLgUnroll], b[kLgUnroll];
+            int64_t idx[kLgUnroll];
+#pragma unroll
+            for (int u = 0; u < kLgUnroll; ++u)
             {
-                f4 rv = {r0, r1, r2, r3};
-                __builtin_nontemporal_store(rv, gx + i);
+                const int64_t j = j0 + u * step;
+                const int64_t jj = j < Q ? j : Q - 1;   // clamped (neither summed nor stored)
+                const int64_t r  = outer == 1 ? 0 : divK4.div((uint32_t) jj);
+                idx[u]           = (r * C + c) * K4 + (jj - r * K4);
+                a[u]             = __builtin_nontemporal_load(x + idx[u]);
+                b[u]             = __builtin_nontemporal_load(g + idx[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < kLgUnroll; ++u)
+            {
+                if (j0 + u * step >= Q)
+                    break;
+                float r0, r1, r2, r3;
+                lg_bwd_elem(a[u].x, b[u].x, dl, o, steps, rcp, r0, s);
+                lg_bwd_elem(a[u].y, b[u].y, dl, o, steps, rcp, r1, s);
+                lg_bwd_elem(a[u].z, b[u].z, dl, o, steps, rcp, r2, s);
+                lg_bwd_elem(a[u].w, b[u].w, dl, o, steps, rcp, r3, s);
+                if (gx)
+                {
+                    f4 rv = {r0, r1, r2, r3};
+                    __builtin_nontemporal_store(rv, gx + idx[u]);
+                }
             }
         }
         Sums t = block_reduce(s);
@@ -250,6 +284,74 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
             }
         }
     }
+}
+
+// per-channel, tile form (K/4 a multiple of 256*U): workgroup b covers the U*256 consecutive quads
+// [b*U*256, (b+1)*U*256) of the flat tensor -- inside one row, so one channel -- in address order,
+// like the streaming QDQ kernels (the (channel, slice) grid above streams from as many places as
+// there are channels in flight). Per-workgroup sums go to partial[b][3]; lg_bwd_tile_fold adds them
+// per channel in a fixed order (deterministic).
+template <int U>
+__global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restrict__ x, const f4* __restrict__ g,
+                                                             f4* __restrict__ gx, FastDiv divK4, FastDiv divC,
+                                                             uint32_t C, const float* __restrict__ delta,
+                                                             const float* __restrict__ offset, float steps,
+                                                             float* __restrict__ partial)
+{
+    const uint32_t q0  = blockIdx.x * (uint32_t) (kBlock * U);
+    const uint32_t row = divK4.div(q0);
+    const uint32_t c   = row - divC.div(row) * C;
+    const float dl = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(dl);
+    f4 a[U], b[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+        a[u] = __builtin_nontemporal_load(x + q0 + u * kBlock + threadIdx.x);
+        b[u] = __builtin_nontemporal_load(g + q0 + u * kBlock + threadIdx.x);
+    }
+    Sums s {0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+    {
+        float r0, r1, r2, r3;
+        lg_bwd_elem(a[u].x, b[u].x, dl, o, steps, rcp, r0, s);
+        lg_bwd_elem(a[u].y, b[u].y, dl, o, steps, rcp, r1, s);
+        lg_bwd_elem(a[u].z, b[u].z, dl, o, steps, rcp, r2, s);
+        lg_bwd_elem(a[u].w, b[u].w, dl, o, steps, rcp, r3, s);
+        if (gx)
+        {
+            f4 rv = {r0, r1, r2, r3};
+            __builtin_nontemporal_store(rv, gx + q0 + u * kBlock + threadIdx.x);
+        }
+    }
+    Sums t = block_reduce(s);
+    if (threadIdx.x == 0)
+    {
+        partial[3 * blockIdx.x + 0] = t.a;
+        partial[3 * blockIdx.x + 1] = t.b;
+        partial[3 * blockIdx.x + 2] = t.d;
+    }
+}
+
+// sums[c] = sum over the rows r of channel c and their workgroups w (in that order)
+__global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restrict__ partial, float* __restrict__ sums,
+                                                           uint32_t outer, uint32_t C, uint32_t per_row)
+{
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= C)
+        return;
+    float a = 0, b = 0, d = 0;
+    for (uint32_t r = 0; r < outer; ++r)
+        for (uint32_t w = 0; w < per_row; ++w)
+        {
+            const float* p = partial + 3 * ((size_t) (r * C + c) * per_row + w);
+            a += p[0];
+            b += p[1];
+            d += p[2];
+        }
+    sums[3 * c + 0] = a;
+    sums[3 * c + 1] = b;
+    sums[3 * c + 2] = d;
 }
 
 }   // namespace
@@ -305,6 +407,35 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
                          reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
             lg_bwd_tensor_kernel<<<stream_blocks(n, (int64_t) kBlock * 16), kBlock, 0, s>>>(
                 x, grad, grad_x, n, delta, offset, num_steps, sums, vec ? 1 : 0);
+        }
+        else if (K % 1024 == 0 && n < (int64_t(1) << 31) && C < 65536 &&
+                 ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
+                   reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0)
+        {
+            const int64_t K4 = K / 4;
+            const int U      = K4 % (kBlock * 4) == 0 ? 4 : K4 % (kBlock * 2) == 0 ? 2 : 1;
+            const int64_t wg = n / 4 / (kBlock * U);
+            float* partial   = nullptr;
+            AIMET_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&partial), sizeof(float) * 3 * wg, s));
+            auto xv = reinterpret_cast<const f4*>(x);
+            auto gv = reinterpret_cast<const f4*>(grad);
+            auto ov = reinterpret_cast<f4*>(grad_x);
+            FastDiv dk((uint32_t) K4), dc((uint32_t) C);
+            if (U == 4)
+                lg_bwd_tile_kernel<4><<<(unsigned) wg, kBlock, 0, s>>>(xv, gv, ov, dk, dc, (uint32_t) C, delta, offset,
+                                                                       num_steps, partial);
+            else if (U == 2)
+                lg_bwd_tile_kernel<2><<<(unsigned) wg, kBlock, 0, s>>>(xv, gv, ov, dk, dc, (uint32_t) C, delta, offset,
+                                                                       num_steps, partial);
+            else
+                lg_bwd_tile_kernel<1><<<(unsigned) wg, kBlock, 0, s>>>(xv, gv, ov, dk, dc, (uint32_t) C, delta, offset,
+                                                                       num_steps, partial);
+            AIMET_LAUNCH_CHECK();
+            lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
+                partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)));
+            AIMET_LAUNCH_CHECK();
+            AIMET_HIP_CHECK(hipFreeAsync(partial, s));
+            return;
         }
         else if (K % 4 == 0 && outer * (K / 4) < (int64_t(1) << 32) &&
                  ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |

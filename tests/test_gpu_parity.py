@@ -1,6 +1,8 @@
 """Parity of the HIP path (through the C-ABI) with the reference: golden vectors of the reference
 C++ (bit-exact), the reference test-suites' KATs, the CPU oracle on seeded inputs, and at full
 size size-independent properties. Needs an MI355X."""
+import ctypes
+
 import numpy as np
 import pytest
 import torch
@@ -486,7 +488,8 @@ def test_learned_grid_vs_reference_golden(golden_dir, case):
     np.testing.assert_allclose(host(emax.grad), g["c%d_gmax" % i], rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("shape,sym", [((4096, 4096), True), ((8, 1 << 20), False), ((96, 3, 7), True)])
+@pytest.mark.parametrize("shape,sym", [((4096, 4096), True), ((8, 1 << 20), False), ((96, 3, 7), True),
+                                       ((1024, 14336), False)])
 def test_learned_grid_large_vs_torch_ref(shape, sym):
     """Llama-like weight (4096 x 4096, per-channel 4-bit symmetric; one workgroup per channel),
     few long channels (channel x slice grid, atomic sums) and K % 4 != 0 (scalar path): kernel vs
@@ -507,6 +510,36 @@ def test_learned_grid_large_vs_torch_ref(shape, sym):
     assert torch.equal(w.grad, gx)
     torch.testing.assert_close(emax.grad, gmax, rtol=2e-4, atol=1e-4)
     torch.testing.assert_close(emin.grad, gmin, rtol=2e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("outer,C,K", [(3, 5, 2048), (2, 7, 3072), (4, 3, 100)])
+def test_learned_grid_backward_sums_channel_axis_inner(outer, C, K):
+    """aimet_lg_backward on [outer][C][K] with outer > 1 (channel axis not first): grad_x exact and
+    the per-channel sums A = sum((x_q + o) g), B = sum(mask x/delta g), D = sum(!mask g) against
+    float64 numpy (rtol 1e-4: fp32 accumulation order). Covers the tile form (K % 1024 == 0, 4 and 2
+    quads per lane) and the channel form."""
+    from aimet_amd import _native
+    g0 = torch.Generator(device=DEV).manual_seed(outer * 100 + C)
+    x = torch.randn(outer, C, K, device=DEV, generator=g0) * 0.3
+    g = torch.randn(outer, C, K, device=DEV, generator=g0)
+    delta = torch.rand(C, device=DEV, generator=g0) * 0.01 + 0.002
+    offset = torch.full((C,), -8.0, device=DEV)
+    steps = 15.0
+    gx = torch.empty_like(x)
+    sums = torch.empty(3 * C, device=DEV)
+    _native.call("aimet_lg_backward", x.data_ptr(), g.data_ptr(), gx.data_ptr(), sums.data_ptr(), outer, C, K,
+                 delta.data_ptr(), offset.data_ptr(), ctypes.c_float(steps), torch.cuda.current_stream().cuda_stream)
+    d3, o3 = delta.view(1, C, 1), offset.view(1, C, 1)
+    xr = torch.round(x / d3) - o3
+    mask = (xr >= 0) & (xr <= steps)
+    assert torch.equal(gx, mask.float() * g)
+    xq = torch.clamp(xr, 0, steps)
+    xd, gd, md = x.double(), g.double(), mask.double()
+    A = ((xq.double() + o3.double()) * gd).sum(dim=(0, 2))
+    B = (md * (xd / d3.double()) * gd).sum(dim=(0, 2))
+    D = ((1 - md) * gd).sum(dim=(0, 2))
+    want = torch.stack([A, B, D], 1).reshape(-1).float()
+    torch.testing.assert_close(sums, want, rtol=1e-4, atol=1e-3)
 
 
 # ------------------------------------------------------------------------------------------
