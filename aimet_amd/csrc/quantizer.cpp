@@ -3,6 +3,7 @@
 // held in HBM. One object carries the analyzers of all channels of a tensor (the reference
 // allocates one C++ analyzer per channel and loops over channels in Python).
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -23,7 +24,15 @@ struct aimet_tensor_quantizer
     StatsKind kind   = kKindTf;
     void* arena      = nullptr;
     size_t arena_bytes = 0;
+    // quantizers made by aimet_tq_create_many share one allocation; the last one destroyed frees it
+    struct Slab* slab = nullptr;
     TqDevice d {};
+};
+
+struct Slab
+{
+    void* base = nullptr;
+    std::atomic<int64_t> refs {0};
 };
 
 namespace
@@ -143,27 +152,85 @@ void parallel_channels(int64_t C, F&& f)
         x.join();
 }
 
+aimet_tensor_quantizer* new_quantizer(int scheme, int64_t num_channels, int device)
+{
+    AIMET_REQUIRE(num_channels >= 1, "num_channels must be >= 1");
+    if (scheme == AIMET_QUANTIZATION_RANGE_LEARNING)   // QuantizerFactory.cpp:93-96
+        scheme = AIMET_QUANTIZATION_TF;
+    AIMET_REQUIRE(scheme >= AIMET_QUANTIZATION_TF && scheme <= AIMET_QUANTIZATION_ENTROPY, "Unknown quant scheme");
+    auto* q   = new aimet_tensor_quantizer();
+    q->scheme = scheme;
+    q->C      = num_channels;
+    q->device = device;
+    q->hist   = scheme != AIMET_QUANTIZATION_TF;
+    q->kind   = scheme == AIMET_QUANTIZATION_TF ? kKindTf : scheme == AIMET_QUANTIZATION_ENTROPY ? kKindEntropy : kKindPdf;
+    layout(q, false);
+    return q;
+}
+
 }   // namespace
 
 extern "C" {
+
+int aimet_tq_create_many(const int* schemes, const int64_t* num_channels, int64_t count, int device,
+                         aimet_tensor_quantizer** out)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(count >= 0, "negative quantizer count");
+        if (count == 0)
+            return;
+        AIMET_REQUIRE(schemes && num_channels && out, "null argument");
+        std::vector<aimet_tensor_quantizer*> qs;
+        std::vector<size_t> offs;
+        size_t total = 0;
+        try
+        {
+            for (int64_t i = 0; i < count; ++i)
+            {
+                qs.push_back(new_quantizer(schemes[i], num_channels[i], device));
+                offs.push_back(total);
+                total += align256(qs.back()->arena_bytes);
+            }
+        }
+        catch (...)
+        {
+            for (auto* q: qs)
+                delete q;
+            throw;
+        }
+        DeviceGuard g(device);
+        auto* sl     = new Slab();
+        hipError_t e = hipMalloc(&sl->base, total);
+        if (e != hipSuccess)
+        {
+            delete sl;
+            for (auto* q: qs)
+                delete q;
+            throw HipError(std::string("hipMalloc(tensor quantizer state): ") + hipGetErrorString(e));
+        }
+        sl->refs = count;
+        AIMET_HIP_CHECK(hipMemsetAsync(sl->base, 0, total, nullptr));
+        std::vector<ResetJob> resets;
+        for (int64_t i = 0; i < count; ++i)
+        {
+            aimet_tensor_quantizer* q = qs[(size_t) i];
+            q->arena = static_cast<char*>(sl->base) + offs[(size_t) i];
+            q->slab  = sl;
+            layout(q, true);
+            resets.push_back(ResetJob {q->d.acc, q->C});
+            out[i] = q;
+        }
+        launch_reset_state_many(resets, nullptr);
+        AIMET_HIP_CHECK(hipStreamSynchronize(nullptr));
+    });
+}
 
 int aimet_tq_create(int scheme, int64_t num_channels, int device, aimet_tensor_quantizer** out)
 {
     return guarded([&] {
         AIMET_REQUIRE(out != nullptr, "output handle is null");
-        AIMET_REQUIRE(num_channels >= 1, "num_channels must be >= 1");
-        if (scheme == AIMET_QUANTIZATION_RANGE_LEARNING)   // QuantizerFactory.cpp:93-96
-            scheme = AIMET_QUANTIZATION_TF;
-        AIMET_REQUIRE(scheme >= AIMET_QUANTIZATION_TF && scheme <= AIMET_QUANTIZATION_ENTROPY, "Unknown quant scheme");
+        auto* q = new_quantizer(scheme, num_channels, device);
         DeviceGuard g(device);
-        auto* q   = new aimet_tensor_quantizer();
-        q->scheme = scheme;
-        q->C      = num_channels;
-        q->device = device;
-        q->hist   = scheme != AIMET_QUANTIZATION_TF;
-        q->kind   = scheme == AIMET_QUANTIZATION_TF ? kKindTf
-                    : scheme == AIMET_QUANTIZATION_ENTROPY ? kKindEntropy : kKindPdf;
-        layout(q, false);
         hipError_t e = hipMalloc(&q->arena, q->arena_bytes);
         if (e != hipSuccess)
         {
@@ -182,7 +249,18 @@ int aimet_tq_destroy(aimet_tensor_quantizer* q)
     return guarded([&] {
         if (!q)
             return;
-        if (q->arena)
+        if (q->slab)
+        {
+            Slab* sl = q->slab;
+            if (--sl->refs == 0)
+            {
+                DeviceGuard g(q->device);
+                AIMET_HIP_CHECK(hipDeviceSynchronize());
+                AIMET_HIP_CHECK(hipFree(sl->base));
+                delete sl;
+            }
+        }
+        else if (q->arena)
         {
             DeviceGuard g(q->device);
             // callers may still have work queued on any stream that uses this state
@@ -377,6 +455,41 @@ int aimet_tq_fold_histogram_many(aimet_tensor_quantizer* const* qs, const int64_
     if (counts == nullptr && count > 0)
         return guarded([] { AIMET_REQUIRE(false, "null element counts"); });
     return run_many(qs, nullptr, nullptr, counts, count, kPhaseFoldHistogram, false, stream);
+}
+
+int aimet_tq_update_stats_channels_many(aimet_tensor_quantizer* const* qs, const float* const* xs,
+                                        const int64_t* outers, const int64_t* Cs, const int64_t* Ks, int64_t count,
+                                        void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(count >= 0, "negative quantizer count");
+        if (count == 0)
+            return;
+        AIMET_REQUIRE(qs && xs && outers && Cs && Ks, "null argument");
+        std::vector<ChannelJob> jobs;
+        jobs.reserve((size_t) count);
+        for (int64_t i = 0; i < count; ++i)
+        {
+            aimet_tensor_quantizer* q = qs[i];
+            check_shape(q, outers[i], Cs[i], Ks[i]);
+            AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one *_many call share a device");
+            if (outers[i] * Ks[i] > 0)
+                require_device_ptr(xs[i], "input");
+            ChannelJob j {};
+            j.x     = xs[i];
+            j.outer = outers[i];
+            j.C     = Cs[i];
+            j.K     = Ks[i];
+            j.d     = q->d;
+            j.kind  = (int32_t) q->kind;
+            j.vec   = ((reinterpret_cast<uintptr_t>(xs[i]) & 15) == 0 && Ks[i] % 4 == 0) ? 1 : 0;
+            jobs.push_back(j);
+        }
+        DeviceGuard g(qs[0]->device);
+        launch_channel_stats_many(jobs, as_stream(stream));
+        for (int64_t i = 0; i < count; ++i)
+            qs[i]->stats_updated = true;
+    });
 }
 
 int aimet_tq_minmax_buffer(aimet_tensor_quantizer* q, float** dev, int64_t* n)

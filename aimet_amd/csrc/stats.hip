@@ -575,6 +575,17 @@ __global__ __launch_bounds__(kBlock) void reset_acc_kernel(double* acc, int64_t 
     }
 }
 
+// one workgroup per quantizer
+__global__ __launch_bounds__(kBlock) void reset_acc_many_kernel(const ResetJob* __restrict__ jobs)
+{
+    const ResetJob J = jobs[blockIdx.x];
+    for (int64_t c = threadIdx.x; c < J.C; c += kBlock)
+    {
+        J.acc[2 * c]     = DBL_MAX;    // TfEncodingAnalyzer.h:88
+        J.acc[2 * c + 1] = -DBL_MAX;   // TfEncodingAnalyzer.h:89
+    }
+}
+
 // ---- many per-tensor quantizers in one launch per phase ---------------------------------------
 // A calibration batch updates every activation quantizer of the model: per quantizer the single
 // launches are min/max + combine + fold + histogram + PDF fold (5 launches, ~5 us each); for
@@ -672,6 +683,155 @@ __global__ __launch_bounds__(kPdfSize) void fold_histogram_many_kernel(const Sta
     }
     else if (J.d.pdf_init[0])
         fold_hist_one(J.d, 0, J.count);
+}
+
+// ---- many per-channel quantizers: updateStats in two launches ------------------------------
+// ResNet-50's 54 weight quantizers took 4-5 launches each (min/max, fold, histogram, fold, and
+// the PDF fold of every channel); a channel's fold depends only on its own statistics, so here
+// the workgroup that reduces channel c also folds it.
+__device__ __forceinline__ int find_channel_job(const ChannelJob* __restrict__ jobs, int njobs, uint32_t b)
+{
+    int lo = 0, hi = njobs - 1;
+    while (lo < hi)
+    {
+        int mid = (lo + hi + 1) >> 1;
+        if (jobs[mid].block0 <= b)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void channel_minmax(const ChannelJob& J, int64_t c, float& mn, float& mx)
+{
+    mn = INFINITY;
+    mx = -INFINITY;
+    for (int64_t o = 0; o < J.outer; ++o)
+    {
+        const float* row = J.x + (o * J.C + c) * J.K;
+        if (J.vec)
+        {
+            const float4* r4 = reinterpret_cast<const float4*>(row);
+            for (int64_t k = threadIdx.x; k < J.K / 4; k += kBlock)
+                accum4(r4[k], mn, mx);
+        }
+        else
+        {
+            for (int64_t k = threadIdx.x; k < J.K; k += kBlock)
+            {
+                mn = fminf(mn, row[k]);
+                mx = fmaxf(mx, row[k]);
+            }
+        }
+    }
+}
+
+// min/max of channel c + fold_one / ent_fold_one (fold_minmax_kernel, ent_fold_minmax_kernel)
+__global__ __launch_bounds__(kBlock) void channel_minmax_fold_many_kernel(const ChannelJob* __restrict__ jobs,
+                                                                          int njobs)
+{
+    const ChannelJob& J = jobs[find_channel_job(jobs, njobs, blockIdx.x)];
+    const int64_t c     = blockIdx.x - J.block0;
+    if (J.kind == kKindPdf && J.d.pdf_init[c])
+        return;   // PDF schemes take min/max on the first (non-zero) batch only
+    float mn, mx;
+    channel_minmax(J, c, mn, mx);
+    block_minmax(mn, mx);
+    __shared__ float2 res;
+    if (threadIdx.x == 0)
+    {
+        res = make_float2(-mn, mx);
+        reinterpret_cast<float2*>(J.d.minmax)[c] = res;
+        if (J.kind != kKindEntropy)
+            fold_one(J.d, c, J.kind == kKindTf);
+    }
+    if (J.kind == kKindEntropy)
+    {
+        __syncthreads();
+        ent_fold_one(J.d, c, -res.x, res.y);
+    }
+}
+
+// histogram of channel c + the PDF fold (fold_hist_one) / entropy accumulation (ent_fold_hist_one),
+// straight from the LDS counts
+template <bool ENT>
+__device__ __forceinline__ void channel_hist_fold(const ChannelJob& J, int64_t c)
+{
+    __shared__ uint32_t lds[kWaves][kPdfSize];
+    const TqDevice& d = J.d;
+    if (!BinnerOf<ENT>::live(d, c))
+        return;
+    const int w = threadIdx.x >> 6;
+    typename BinnerOf<ENT>::type bn {d.bin_bucket[c], d.bin_offset[c]};
+    for (int i = threadIdx.x; i < kWaves * kPdfSize; i += kBlock)
+        (&lds[0][0])[i] = 0;
+    __syncthreads();
+    const int zbin = bn.bin(0.0f);
+    uint32_t zc    = 0;
+    auto add = [&](float v) {
+        if (v == 0.0f)
+        {
+            ++zc;
+            return;
+        }
+        int b = bn.bin(v);
+        if (b >= 0)
+            atomicAdd(&lds[w][b], 1u);
+    };
+    for (int64_t o = 0; o < J.outer; ++o)
+    {
+        const float* row = J.x + (o * J.C + c) * J.K;
+        if (J.vec)
+        {
+            const float4* r4 = reinterpret_cast<const float4*>(row);
+            for (int64_t k = threadIdx.x; k < J.K / 4; k += kBlock)
+            {
+                float4 v = r4[k];
+                add(v.x);
+                add(v.y);
+                add(v.z);
+                add(v.w);
+            }
+        }
+        else
+        {
+            for (int64_t k = threadIdx.x; k < J.K; k += kBlock)
+                add(row[k]);
+        }
+    }
+    zc = wave_sum(zc);
+    if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
+        atomicAdd(&lds[w][zbin], zc);
+    __syncthreads();
+    const int it       = d.iterations[c];
+    const double count = (double) (J.outer * J.K);
+    for (int b = threadIdx.x; b < kPdfSize; b += kBlock)
+    {
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < kWaves; ++i)
+            s += lds[i][b];
+        const int64_t idx = c * kPdfSize + b;
+        if (ENT)
+            d.pdf[idx] = d.pdf[idx] + (double) s;                        // math_functions.cpp:554-559
+        else
+            d.pdf[idx] = (d.pdf[idx] * it + (double) s / count) / (it + 1);   // UpdatePdf:280-287
+    }
+    __syncthreads();   // every lane has read iterations[c]
+    if (threadIdx.x == 0)
+        d.iterations[c] = it + 1;
+}
+
+__global__ __launch_bounds__(kBlock) void channel_hist_fold_many_kernel(const ChannelJob* __restrict__ jobs,
+                                                                        int njobs)
+{
+    const ChannelJob& J = jobs[find_channel_job(jobs, njobs, blockIdx.x)];
+    const int64_t c     = blockIdx.x - J.block0;
+    if (J.kind == kKindEntropy)
+        channel_hist_fold<true>(J, c);
+    else if (J.kind == kKindPdf)
+        channel_hist_fold<false>(J, c);
 }
 
 inline int grid_for_channels(int64_t C)
@@ -818,6 +978,41 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
         fold_histogram_many_kernel<<<n, kPdfSize, 0, s>>>(dj);
         AIMET_LAUNCH_CHECK();
     }
+    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
+}
+
+void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s)
+{
+    if (jobs.empty())
+        return;
+    uint64_t blocks = 0;
+    bool any_hist   = false;
+    for (auto& j: jobs)
+    {
+        j.block0 = (uint32_t) blocks;
+        blocks += (uint64_t) j.C;
+        any_hist = any_hist || j.kind != kKindTf;
+    }
+    AIMET_REQUIRE(blocks < (uint64_t(1) << 31), "too many channels");
+    const int n = (int) jobs.size();
+    auto* dj    = static_cast<ChannelJob*>(upload_async(jobs.data(), sizeof(ChannelJob) * n, s));
+    channel_minmax_fold_many_kernel<<<(unsigned) blocks, kBlock, 0, s>>>(dj, n);
+    AIMET_LAUNCH_CHECK();
+    if (any_hist)
+    {
+        channel_hist_fold_many_kernel<<<(unsigned) blocks, kBlock, 0, s>>>(dj, n);
+        AIMET_LAUNCH_CHECK();
+    }
+    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
+}
+
+void launch_reset_state_many(const std::vector<ResetJob>& jobs, hipStream_t s)
+{
+    if (jobs.empty())
+        return;
+    auto* dj = static_cast<ResetJob*>(upload_async(jobs.data(), sizeof(ResetJob) * jobs.size(), s));
+    reset_acc_many_kernel<<<(unsigned) jobs.size(), kBlock, 0, s>>>(dj);
+    AIMET_LAUNCH_CHECK();
     AIMET_HIP_CHECK(hipFreeAsync(dj, s));
 }
 

@@ -56,6 +56,13 @@ void launch_batch_histogram(const TqDevice& d, const float* x, int64_t outer, in
                             hipStream_t s);
 void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, StatsKind kind, hipStream_t s);
 void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s);
+// the TF accumulators of many quantizers (aimet_tq_create_many) in one launch
+struct ResetJob
+{
+    double* acc;
+    int64_t C;
+};
+void launch_reset_state_many(const std::vector<ResetJob>& jobs, hipStream_t s);
 // Many per-tensor quantizers (C == 1) in one launch per phase (stats.hip: launch_stats_many)
 struct StatsJob
 {
@@ -75,6 +82,20 @@ enum StatsPhase
     kPhaseFoldHistogram = 8
 };
 void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s);
+// Many per-channel quantizers ([outer][C][K] tensors) with the whole updateStats (min/max, fold,
+// histogram, fold) in TWO launches: every channel of every quantizer is one workgroup, and the
+// fold of a channel needs only that channel's statistics, so it runs in the workgroup that
+// produced them (stats.hip: launch_channel_stats_many).
+struct ChannelJob
+{
+    const float* x;
+    int64_t outer, C, K;
+    TqDevice d;
+    uint32_t block0;   // first workgroup (filled by launch_channel_stats_many)
+    int32_t kind;      // StatsKind
+    int32_t vec;       // 16-B aligned rows
+};
+void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s);
 // tfe_search.hip
 // d.enc[c] <- TF-Enhanced encoding of channel c (statistics updated; see aimet_tq_get_encoding)
 void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);

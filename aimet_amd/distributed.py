@@ -32,6 +32,12 @@ class PackedExchange:
 
     def __init__(self, quantizers, device):
         self.quantizers = list(quantizers)
+        if torch.device(device).type == "cuda":
+            # device state of every native quantizer from one allocation (aimet_tq_create_many)
+            from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+            native = [q for q in self.quantizers if isinstance(q, AimetTensorQuantizer)]
+            if native:
+                AimetTensorQuantizer._ensure_many(native, torch.device(device))
         chans = [q.num_channels for q in self.quantizers]
         self.minmax = torch.zeros(2 * sum(chans), dtype=torch.float32, device=device)
         hist_ch = sum(c for q, c in zip(self.quantizers, chans) if q.uses_histogram)

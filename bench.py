@@ -43,11 +43,10 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--batch", type=int, default=256)
-    p.add_argument("--calib-batches", type=int, default=1,
-                   help="calibration batches for the compute_encodings timing")
     p.add_argument("--cpu-sample-images", type=int, default=32,
                    help="images of each activation tensor (plus all weights) timed on the CPU oracle")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--enc-reps", type=int, default=5, help="timed compute_encodings calls after the cold one")
     p.add_argument("--eager", action="store_true", help="launch every QDQ from Python instead of HIP graphs")
     p.add_argument("--per-weight-launches", action="store_true",
                    help="one per-channel QDQ launch per weight instead of the batched plan")
@@ -98,8 +97,8 @@ def compute_encodings(acts, weights, world):
     # every activation quantizer's statistics in one launch per phase (aimet_tq_*_many);
     # with N ranks each phase's packed statistics are exchanged once (aimet_amd.distributed)
     D.sharded_update_stats(aq, [t for _, t in acts])
-    for q, (_, w) in zip(wq, weights):
-        q.updateStatsPerChannel(w, 0, True)
+    # every weight quantizer's per-channel statistics in two launches (one workgroup per channel)
+    AimetTensorQuantizer.updateStatsPerChannelMany(wq, [w for _, w in weights])
     # getEncoding of every quantizer, batched: one device search launch + one sync per flag set
     act_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(aq, 8, False, False, False)]
     w_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(wq, 8, True, False, False)]
@@ -152,7 +151,16 @@ def main():
     del model
     torch.cuda.empty_cache()
 
-    act_enc, w_enc, enc_seconds, aq, wq = compute_encodings(acts, weights, world)
+    # compute_encodings wall-clock: the first call (cold: code objects load, pools grow) and the
+    # median of --enc-reps further calls on fresh quantizers (what a calibration costs in a warm
+    # process); the encodings of the last call are used
+    act_enc, w_enc, enc_cold, aq, wq = compute_encodings(acts, weights, world)
+    warm = []
+    for _ in range(args.enc_reps):
+        del aq, wq
+        act_enc, w_enc, secs, aq, wq = compute_encodings(acts, weights, world)
+        warm.append(secs)
+    enc_seconds = sorted(warm)[len(warm) // 2] if warm else enc_cold
 
     # ---- the step: every QDQ of one QuantSim forward, pre-bound C-ABI calls --------------------
     stream = torch.cuda.current_stream(dev)
@@ -251,9 +259,9 @@ def main():
     act_ms = [s.elapsed_time(e) for s, e in ev]
     kernel_ms = sum(act_ms) / len(act_ms)
     if world > 1:
-        tt = torch.tensor([dt, enc_seconds], device=dev, dtype=torch.float64)
+        tt = torch.tensor([dt, enc_seconds, enc_cold], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt, enc_seconds = float(tt[0]), float(tt[1])
+        dt, enc_seconds, enc_cold = float(tt[0]), float(tt[1]), float(tt[2])
 
     ms_per_step = dt / args.steps * 1e3
     value = n_step * world * args.steps / dt / 1e9
@@ -277,6 +285,9 @@ def main():
                    "act_quantizers": len(act_calls), "weight_quantizers": len(w_calls),
                    "weight_channels": int(sum(c[3] for c in w_calls)), "parallelism": "dp%d" % world,
                    "compute_encodings_s": round(enc_seconds, 4),
+                   "compute_encodings_cold_s": round(enc_cold, 4),
+                   "compute_encodings_timing": "median of %d calls after the first (cold) one, max over ranks"
+                                               % args.enc_reps,
                    "compute_encodings_scheme": "tf_enhanced act per-tensor + tf_enhanced weight per-channel sym"},
         "roofline": {"bound": "hbm", "kernel": "qdq_per_tensor (tensor_vec_kernel)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -175,6 +175,13 @@ typedef struct aimet_tensor_quantizer aimet_tensor_quantizer;
  * QUANTIZATION_RANGE_LEARNING maps to TF (QuantizerFactory.cpp:93-96). `device` = HIP ordinal. */
 int aimet_tq_create(int quant_scheme, int64_t num_channels, int device, aimet_tensor_quantizer** out);
 int aimet_tq_destroy(aimet_tensor_quantizer* q);
+/* count quantizers (schemes[i], num_channels[i]) on one device with ONE device allocation, one
+ * memset and one initialisation launch (a model's quantizers are created together by
+ * QuantizationSimModel; one aimet_tq_create each costs an allocation and a synchronisation).
+ * Each out[i] is destroyed with aimet_tq_destroy as usual; the shared allocation is released
+ * with the last of them. */
+int aimet_tq_create_many(const int* schemes, const int64_t* num_channels, int64_t count, int device,
+                         aimet_tensor_quantizer** out);
 /* AimetTensorQuantizer.cpp:89-96 resetEncodingStats (synchronous w.r.t. `stream`). */
 int aimet_tq_reset_encoding_stats(aimet_tensor_quantizer* q, void* stream);
 /* AimetTensorQuantizer.cpp:200-207 setPercentileValue (percentile scheme only). */
@@ -225,6 +232,14 @@ int aimet_tq_batch_histogram_many(aimet_tensor_quantizer* const* qs, const float
                                   int64_t count, void* stream);
 int aimet_tq_fold_histogram_many(aimet_tensor_quantizer* const* qs, const int64_t* counts, int64_t count,
                                  void* stream);
+/* updateStats of many quantizers of any channel count, each tensor viewed as [outers[i]][Cs[i]][Ks[i]]
+ * (Cs[i] == num_channels of qs[i]), in two launches with one workgroup per channel: the weight
+ * quantizers of a model (v1/tensor_quantizer.py:535-571 per weight, batched). Equivalent to
+ * aimet_tq_update_stats(qs[i], xs[i], outers[i], Cs[i], Ks[i], stream) for every i; meant for
+ * per-channel quantizers (one workgroup streams a whole per-tensor quantizer's tensor). */
+int aimet_tq_update_stats_channels_many(aimet_tensor_quantizer* const* qs, const float* const* xs,
+                                        const int64_t* outers, const int64_t* Cs, const int64_t* Ks, int64_t count,
+                                        void* stream);
 
 /* AimetTensorQuantizer.cpp:180-192 getEncoding -> IQuantizationEncodingAnalyzer::computeEncoding.
  * Synchronises `stream`. out[num_channels]; *valid mirrors _isEncodingValid. */

@@ -718,6 +718,73 @@ def test_update_stats_many_equals_individual():
             assert qa.getStatsHistogram() == qb.getStatsHistogram()
 
 
+def test_update_stats_channels_many_equals_individual():
+    """aimet_tq_update_stats_channels_many (min/max + fold, histogram + fold: two launches for
+    every channel of every quantizer) == updateStatsPerChannel per quantizer, for every scheme
+    incl. entropy, channel axes 0 and 1, ragged K, unaligned views, all-zero channels and first
+    batches, NaN / inf, three batches; then encodings, histograms and entropy state bit-identical,
+    and a few channels against the CPU oracle."""
+    rng = np.random.default_rng(31)
+    schemes = [QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
+               QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE,
+               QuantizationMode.QUANTIZATION_ENTROPY]
+    shapes = [((64, 3, 7, 7), 0), ((96, 32, 3, 3), 0), ((16, 24, 3, 3), 1), ((40, 130), 0), ((7, 1), 0),
+              ((3, 1000), 0)]
+    specs = [(s, sh, ax) for s in schemes for sh, ax in shapes]
+    a = [AimetTensorQuantizer(s, num_channels=sh[ax]) for s, sh, ax in specs]
+    b = [AimetTensorQuantizer(s, num_channels=sh[ax]) for s, sh, ax in specs]
+    for q in a + b:
+        if q.quant_scheme == QuantizationMode.QUANTIZATION_PERCENTILE:
+            q.setPercentileValue(99.5)
+    orc = {}
+    for batch in range(3):
+        ts = []
+        for i, (s, sh, ax) in enumerate(specs):
+            n = int(np.prod(sh))
+            xt = (rng.standard_normal(n) * (1 + batch + i % 3)).astype(np.float32)
+            if batch == 0 and i % 4 == 0:
+                xt[:] = 0.0
+            if n > 100 and batch == 1:
+                xt[7], xt[8] = np.nan, np.inf
+            xt = xt.reshape(sh)
+            xt[(slice(None),) * ax + (min(1, sh[ax] - 1),)] = 0.0   # an all-zero channel
+            if i % 2:   # odd specs: a 4-byte offset view (scalar path)
+                ts.append(gpu(np.concatenate([[0], xt.ravel()]))[1:].view(sh))
+            else:
+                ts.append(gpu(xt))
+            if s in (QuantizationMode.QUANTIZATION_TF_ENHANCED, QuantizationMode.QUANTIZATION_TF) and i % 3 == 0:
+                C = sh[ax]
+                oc = orc.setdefault(i, [O.Analyzer(int(s)) for _ in range(C)])
+                for c in range(C):
+                    oc[c].update(np.ascontiguousarray(np.take(xt, c, axis=ax)))
+        keep = AimetTensorQuantizer.updateStatsPerChannelMany(a, ts, [ax for _, _, ax in specs])
+        for q, t, (_, _, ax) in zip(b, ts, specs):
+            q.updateStatsPerChannel(t, ax, True)
+        torch.cuda.synchronize()
+        del keep
+    for fl in FLAGS:
+        for i, (qa, qb) in enumerate(zip(a, b)):
+            if qa.quant_scheme == QuantizationMode.QUANTIZATION_MSE and fl[1]:
+                continue
+            ea, va = qa.getEncoding(8, *fl)
+            eb, vb = qb.getEncoding(8, *fl)
+            assert va == vb
+            ta = np.array([e.to_tuple() for e in ea], np.float64)
+            tb = np.array([e.to_tuple() for e in eb], np.float64)
+            assert np.array_equal(ta.view(np.uint64), tb.view(np.uint64)), (i, fl)   # NaN-safe
+            if i in orc:
+                for c, o in enumerate(orc[i]):
+                    assert ea[c].to_tuple() == o.compute(8, *fl).as_tuple(), (i, c, fl)
+    for qa, qb in zip(a, b):
+        for c in range(qa.num_channels):
+            if qa.quant_scheme == QuantizationMode.QUANTIZATION_ENTROPY:
+                sa, sb = qa.entropy_state(c), qb.entropy_state(c)
+                assert sa.keys() == sb.keys()
+                assert all(np.array_equal(np.asarray(sa[k]), np.asarray(sb[k])) for k in sa), c
+            elif qa.quant_scheme != QuantizationMode.QUANTIZATION_TF:
+                assert qa.getStatsHistogram(c) == qb.getStatsHistogram(c)
+
+
 def test_adaround_optimizer_matches_reference_loop():
     """AdaroundOptimizer (fused soft-quant + rounding-loss kernels) follows the reference's loop
     (torch-op soft quantization + AdaroundLoss, adaround_optimizer.py:181-218) iteration for
@@ -758,3 +825,33 @@ def test_adaround_optimizer_matches_reference_loop():
     hard_ref = T.adaround_forward(w, torch.where(a_ref.detach() >= 0, 100.0, -100.0), d.view(-1, 1, 1, 1),
                                   o.view(-1, 1, 1, 1), 8)
     assert (hard_ours != hard_ref).float().mean() < 1e-3
+
+
+def test_create_many_shared_state_lifetime():
+    """aimet_tq_create_many: quantizers sharing one allocation behave like individually created
+    ones, and destroying some of them (the slab is freed with the last) leaves the others intact."""
+    import gc
+    rng = np.random.default_rng(5)
+    schemes = [QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
+               QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE,
+               QuantizationMode.QUANTIZATION_ENTROPY] * 2
+    xs = [gpu(rng.standard_normal(5000 + 17 * i).astype(np.float32) * (i + 1)) for i in range(len(schemes))]
+    shared = [AimetTensorQuantizer(s) for s in schemes]
+    shared[2].setPercentileValue(99.0)
+    AimetTensorQuantizer.updateStatsMany(shared, xs)
+    for i in (0, 3, 4, 8):
+        shared[i] = None
+    gc.collect()
+    for i, (s, x) in enumerate(zip(schemes, xs)):
+        if shared[i] is None:
+            continue
+        single = AimetTensorQuantizer(s)
+        if i == 2:
+            single.setPercentileValue(99.0)
+        single.updateStats(x, True)
+        shared[i].updateStats(x * 1.5, True)
+        single.updateStats(x * 1.5, True)
+        assert shared[i].getEncoding(8, False, False, False)[0] == single.getEncoding(8, False, False, False)[0], i
+    shared = None
+    gc.collect()
+    torch.cuda.synchronize()

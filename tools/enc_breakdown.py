@@ -40,9 +40,15 @@ def main():
             t0 = mark("reset", t0)
         AimetTensorQuantizer.updateStatsMany(aq, [a for _, a in acts])
         t0 = mark("act_update_many", t0)
-        for q, (_, w) in zip(wq, weights):
-            q.updateStatsPerChannel(w, 0, True)
-        t0 = mark("w_update", t0)
+        if rep == 0:
+            for q, (_, w) in zip(wq, weights):
+                q.updateStatsPerChannel(w, 0, True)
+            t0 = mark("w_update_each", t0)
+            for q in wq:
+                q.resetEncodingStats()
+            t0 = mark("w_reset", t0)
+        AimetTensorQuantizer.updateStatsPerChannelMany(wq, [w for _, w in weights])
+        t0 = mark("w_update_many", t0)
         if rep == 0:
             [q.getEncoding(8, False, False, False) for q in aq]
             t0 = mark("act_getenc_each", t0)
