@@ -657,7 +657,8 @@ __global__ __launch_bounds__(kBlock) void fold_minmax_many_kernel(const StatsJob
         fold_one(J.d, 0, !J.hist);
 }
 
-__global__ __launch_bounds__(kBlock) void histogram_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void histogram_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
 {
     const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, true)];
     if (!J.hist)
@@ -665,10 +666,10 @@ __global__ __launch_bounds__(kBlock) void histogram_many_kernel(const StatsJob* 
     if (J.ent)
     {
         if (J.d.active[0])
-            histogram_part<kBlock, true>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
+            histogram_part<BLOCK, true>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
     }
     else if (J.d.pdf_init[0])
-        histogram_part<kBlock, false>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
+        histogram_part<BLOCK, false>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
 }
 
 __global__ __launch_bounds__(kPdfSize) void fold_histogram_many_kernel(const StatsJob* __restrict__ jobs)
@@ -936,6 +937,17 @@ static int64_t hist_elems_per_block()
     return v;
 }
 
+static int hist_many_block()
+{
+    static int v = [] {
+        // tools/hist_many_tune.py (ResNet-50 bs256, 55 tensors): 512 lanes 5.48 TB/s, 256 lanes 5.33
+        const char* e = getenv("AIMET_TUNE_HIST_BLOCK");   // tuning experiments only
+        int b         = e ? atoi(e) : 512;
+        return (b == 256 || b == 1024) ? b : 512;
+    }();
+    return v;
+}
+
 void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
 {
     if (jobs.empty())
@@ -970,7 +982,13 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
     }
     if ((phases & kPhaseHistogram) && hb > 0)
     {
-        histogram_many_kernel<<<(unsigned) hb, kBlock, 0, s>>>(dj, n);
+        const int hbk = hist_many_block();
+        if (hbk == 1024)
+            histogram_many_kernel<1024><<<(unsigned) hb, 1024, 0, s>>>(dj, n);
+        else if (hbk == 256)
+            histogram_many_kernel<256><<<(unsigned) hb, 256, 0, s>>>(dj, n);
+        else
+            histogram_many_kernel<512><<<(unsigned) hb, 512, 0, s>>>(dj, n);
         AIMET_LAUNCH_CHECK();
     }
     if (phases & kPhaseFoldHistogram)

@@ -107,7 +107,10 @@ def compute_encodings(acts, weights, world):
 
 
 def cpu_baseline(acts, weights, act_enc, w_enc, images):
-    """The CPU restatement of the reference (oracle/, single thread) on a bounded sample."""
+    """The reference's CPU path on a bounded sample: oracle/_ref (the reference DlQuantization C++
+    compiled from its own sources, TensorQuantizationSim::quantizeDequantizeTensor and
+    quantizeDequantizePerChannel with COMP_MODE_CPU) when that library travelled with the tree,
+    and the in-repo C restatement (oracle/dlq_oracle.c, single thread + OpenMP) beside it."""
     from oracle import oracle as O
     xs, ws = [], []
     for (name, t), e in zip(acts, act_enc):
@@ -116,23 +119,61 @@ def cpu_baseline(acts, weights, act_enc, w_enc, images):
         ws.append((w.cpu().numpy().ravel(), w.shape[0], w[0].numel(),
                    O.per_channel_table([e.to_tuple() for e in encs])))
     n = sum(x.size for x, _ in xs) + sum(w.size for w, _, _, _ in ws)
-    t0 = time.perf_counter()
-    for x, e in xs:
-        O.qdq_per_tensor(x, e.min, e.max, 8)
-    for w, C, K, tab in ws:
-        O.qdq_per_channel(w, C, K, tab)
-    dt = time.perf_counter() - t0
+
+    def timed(qdq_t, qdq_c):
+        t0 = time.perf_counter()
+        for x, e in xs:
+            qdq_t(x, e)
+        for w, C, K, tab in ws:
+            qdq_c(w, C, K, tab)
+        return time.perf_counter() - t0
+
+    res = {"n": n}
+    res["port_s"] = timed(lambda x, e: O.qdq_per_tensor(x, e.min, e.max, 8), O.qdq_per_channel)
     # the OpenMP variant of the same loops on the box's CPU share
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
+    res["omp_s"] = timed(lambda x, e: O.qdq_per_tensor_omp(x, e.min, e.max, 8, threads),
+                         lambda w, C, K, tab: O.qdq_per_channel_omp(w, C, K, tab, threads))
+    res["omp_threads"] = threads
+    res["openmp"] = O.openmp_enabled()
+    ref_lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle", "_ref", "libdlq_ref.so")
+    Analyzer = O.Analyzer
+    if os.path.exists(ref_lib):
+        from oracle import ref as R
+        res["ref_s"] = timed(lambda x, e: R.qdq_per_tensor(x, e.min, e.max, 8), R.qdq_per_channel)
+        Analyzer = R.Analyzer
+    # compute_encodings on the CPU (the reference analyzers, TF-Enhanced): statistics + encoding of
+    # the activation sample (per-tensor) and of the first `wch` channels of every weight
+    # (per-channel, symmetric); projected to the full batch / all 27,560 channels by element and
+    # channel counts
+    TFE = 1
     t0 = time.perf_counter()
-    for x, e in xs:
-        O.qdq_per_tensor_omp(x, e.min, e.max, 8, threads)
-    for w, C, K, tab in ws:
-        O.qdq_per_channel_omp(w, C, K, tab, threads)
-    dt_omp = time.perf_counter() - t0
-    omp = {"value": round(n / dt_omp / 1e9, 4), "cores": threads, "nproc": os.cpu_count(),
-           "openmp": O.openmp_enabled()}
-    return n / dt / 1e9, n, dt, omp
+    for x, _ in xs:
+        a = Analyzer(TFE)
+        a.update(x)
+        a.compute(8)
+    act_s = time.perf_counter() - t0
+    wch, nch = 32, 0
+    t0 = time.perf_counter()
+    for w, C, K, _ in ws:
+        w2 = w.reshape(C, K)
+        for c in range(min(wch, C)):
+            a = Analyzer(TFE)
+            a.update(w2[c])
+            a.compute(8, True)
+            nch += 1
+    w_s = time.perf_counter() - t0
+    n_act_sample = sum(x.size for x, _ in xs)
+    n_act_full = sum(t.numel() for _, t in acts)
+    c_full = sum(C for _, C, _, _ in ws)
+    res["enc"] = {"sample_s": round(act_s + w_s, 3),
+                  "projected_full_s": round(act_s * n_act_full / n_act_sample + w_s * c_full / nch, 2),
+                  "sample": "TF-E statistics + encoding: the activation sample above (per-tensor) and the first %d "
+                            "channels of every weight (%d channels, per-channel symmetric); projected by element "
+                            "and channel counts to the full batch" % (wch, nch),
+                  "what": "reference analyzers (oracle/_ref)" if Analyzer is not O.Analyzer
+                          else "C restatement analyzers (oracle/dlq_oracle.c)"}
+    return res
 
 
 def main():
@@ -286,6 +327,11 @@ def main():
                    "weight_channels": int(sum(c[3] for c in w_calls)), "parallelism": "dp%d" % world,
                    "compute_encodings_s": round(enc_seconds, 4),
                    "compute_encodings_cold_s": round(enc_cold, 4),
+                   # two passes (min/max, histogram) of 4 B over every activation and weight element
+                   "compute_encodings_roofline": {
+                       "algorithmic_gb": round(8 * n_step / 1e9, 3),
+                       "achieved_gbps": round(8 * n_step / enc_seconds / 1e9, 1),
+                       "frac": round(8 * n_step / enc_seconds / 1e9 / HBM_PEAK_GBPS, 4)},
                    "compute_encodings_timing": "median of %d calls after the first (cold) one, max over ranks"
                                                % args.enc_reps,
                    "compute_encodings_scheme": "tf_enhanced act per-tensor + tf_enhanced weight per-channel sym"},
@@ -299,12 +345,25 @@ def main():
                                "timed step (%s)" % (len(act_calls), "graph replay" if use_graph else "eager")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        gel, n, secs, omp = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images)
-        result["cpu_baseline"] = {"value": round(gel, 4), "unit": "Gelem/s", "cores": 1, "kind": "port",
-                                  "sample": "first %d images of each activation tensor + all weights (%d elems, "
-                                            "%.1f s), oracle/dlq_oracle.c single-threaded on the host"
-                                            % (args.cpu_sample_images, n, secs),
-                                  "omp": omp}
+        cb = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images)
+        n = cb["n"]
+        sample = ("first %d images of each activation tensor + all weights (%d elems), per-tensor + per-channel "
+                  "QDQ with the bench's encodings, single-threaded on the host" % (args.cpu_sample_images, n))
+        port = {"value": round(n / cb["port_s"] / 1e9, 4), "cores": 1, "seconds": round(cb["port_s"], 3),
+                "what": "oracle/dlq_oracle.c (C restatement)"}
+        omp = {"value": round(n / cb["omp_s"] / 1e9, 4), "cores": cb["omp_threads"], "nproc": os.cpu_count(),
+               "openmp": cb["openmp"], "what": "oracle/dlq_oracle.c with OpenMP"}
+        if "ref_s" in cb:
+            result["cpu_baseline"] = {"value": round(n / cb["ref_s"] / 1e9, 4), "unit": "Gelem/s", "cores": 1,
+                                      "kind": "reference",
+                                      "sample": sample + "; oracle/_ref/libdlq_ref.so = the reference "
+                                                "DlQuantization CPU code compiled from its sources",
+                                      "seconds": round(cb["ref_s"], 3), "port": port, "omp": omp,
+                                      "compute_encodings": cb["enc"]}
+        else:
+            result["cpu_baseline"] = {"value": port["value"], "unit": "Gelem/s", "cores": 1, "kind": "port",
+                                      "sample": sample + "; " + port["what"], "seconds": port["seconds"],
+                                      "omp": omp, "compute_encodings": cb["enc"]}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -61,6 +61,10 @@ def main():
         print("rep %d: " % rep + "  ".join("%s %.2f ms" % (k, v * 1e3) for k, v in t.items()),
               "total %.2f ms" % (sum(t.values()) * 1e3), flush=True)
         del aq, wq
+    for rep in range(4):
+        *_, secs, aq, wq = bench.compute_encodings(acts, weights, 1)
+        del aq, wq
+        print("bench.compute_encodings rep %d: %.2f ms" % (rep, secs * 1e3), flush=True)
 
 
 if __name__ == "__main__":

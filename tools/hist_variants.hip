@@ -51,6 +51,27 @@ struct BinnerRcp
     }
 };
 
+// uniform-threshold fast path (stats.hip HistBinner): v = RN(RN(x*rcp) - off) is within
+// 6u(|q|+|off|) of the reference's RN(RN(x/bucket) - off); away from half-integers by more than
+// thr = (515 + 2|off|) 2^-21 (valid for |v| <= 513; beyond, both roundings are out of range)
+// round-half-away(v*) == rint(v). v_fract + one compare instead of floor/abs/abs/add/mul.
+struct BinnerFast
+{
+    float bucket, offset, rcp, thr;
+    __device__ __forceinline__ int bin(float x) const
+    {
+        const float v = x * rcp - offset;
+        const float h = __builtin_amdgcn_fractf(v);
+        if (__builtin_fabsf(h - 0.5f) > thr)
+        {
+            const int r = (int) __builtin_rintf(v);
+            return (unsigned) r < (unsigned) kBins ? r : -1;
+        }
+        float r = __builtin_roundf(x / bucket - offset);
+        return (r >= 0.0f && r < (float) kBins) ? (int) r : -1;
+    }
+};
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 {
 #pragma unroll
@@ -60,12 +81,12 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 }
 
 // COPIES: LDS histograms per block (1 = shared by the block, BLOCK/64 = one per wave)
-template <int BLOCK, int UNROLL, int COPIES, bool NT, bool ZSKIP, bool PART = false, class B = Binner>
+template <int BLOCK, int UNROLL, int COPIES, bool NT, bool ZSKIP, bool PART = false, class B = Binner, int LSH = 6>
 __global__ __launch_bounds__(BLOCK) void hist_var(const float* __restrict__ x, int64_t n, B bn,
                                                   unsigned long long* __restrict__ counts)
 {
     __shared__ uint32_t lds[COPIES][kBins];
-    const int copy = (threadIdx.x >> 6) % COPIES;
+    const int copy = (threadIdx.x >> LSH) % COPIES;
     for (int i = threadIdx.x; i < COPIES * kBins; i += BLOCK)
         (&lds[0][0])[i] = 0;
     __syncthreads();
@@ -380,6 +401,95 @@ void launch_hist_rcp(const float* x, int64_t n, Binner bn, unsigned long long* c
     hist_var<BLOCK, UNROLL, COPIES, true, true, false, BinnerRcp><<<g, BLOCK, 0, s>>>(x, n, br, c);
 }
 
+// software-pipelined: the next UNROLL float4 are in flight while the current ones are binned
+template <int BLOCK, int UNROLL, int COPIES, class B>
+__global__ __launch_bounds__(BLOCK) void hist_pipe(const float* __restrict__ x, int64_t n, B bn,
+                                                   unsigned long long* __restrict__ counts)
+{
+    __shared__ uint32_t lds[COPIES][kBins];
+    const int copy = (threadIdx.x >> 6) % COPIES;
+    for (int i = threadIdx.x; i < COPIES * kBins; i += BLOCK)
+        (&lds[0][0])[i] = 0;
+    __syncthreads();
+    const int zbin = bn.bin(0.0f);
+    uint32_t zc    = 0;
+    auto add = [&](float v) {
+        if (v == 0.0f)
+        {
+            ++zc;
+            return;
+        }
+        int b = bn.bin(v);
+        if (b >= 0)
+            atomicAdd(&lds[copy][b], 1u);
+    };
+    const f4* x4         = reinterpret_cast<const f4*>(x);
+    const int64_t nv     = n / 4;
+    const int64_t stride = (int64_t) gridDim.x * BLOCK * UNROLL;
+    int64_t base         = (int64_t) blockIdx.x * BLOCK * UNROLL + threadIdx.x;
+    f4 cur[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u)
+    {
+        int64_t i = base + (int64_t) u * BLOCK;
+        cur[u]    = i < nv ? __builtin_nontemporal_load(x4 + i) : f4 {NAN, NAN, NAN, NAN};
+    }
+    for (; base < nv; base += stride)
+    {
+        f4 nxt[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            int64_t i = base + stride + (int64_t) u * BLOCK;
+            nxt[u]    = i < nv ? __builtin_nontemporal_load(x4 + i) : f4 {NAN, NAN, NAN, NAN};
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+        {
+            add(cur[u].x);
+            add(cur[u].y);
+            add(cur[u].z);
+            add(cur[u].w);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+            cur[u] = nxt[u];
+    }
+    for (int64_t i = nv * 4 + (int64_t) blockIdx.x * BLOCK + threadIdx.x; i < n; i += (int64_t) gridDim.x * BLOCK)
+        add(x[i]);
+    zc = wave_sum(zc);
+    if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
+        atomicAdd(&lds[copy][zbin], zc);
+    __syncthreads();
+    for (int b = threadIdx.x; b < kBins; b += BLOCK)
+    {
+        uint32_t s = 0;
+#pragma unroll
+        for (int i = 0; i < COPIES; ++i)
+            s += lds[i][b];
+        if (s)
+            atomicAdd(&counts[b], (unsigned long long) s);
+    }
+}
+
+template <int BLOCK, int UNROLL, int COPIES, int GRID>
+void launch_hist_pipe(const float* x, int64_t n, Binner bn, unsigned long long* c, hipStream_t s)
+{
+    int64_t need = (n / 4 + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
+    int g        = (int) std::max<int64_t>(1, std::min<int64_t>(need, GRID));
+    BinnerRcp br {bn.bucket, bn.offset, 1.0f / bn.bucket};
+    hist_pipe<BLOCK, UNROLL, COPIES, BinnerRcp><<<g, BLOCK, 0, s>>>(x, n, br, c);
+}
+
+template <int BLOCK, int UNROLL, int COPIES, int GRID, int LSH>
+void launch_hist_fast(const float* x, int64_t n, Binner bn, unsigned long long* c, hipStream_t s)
+{
+    int64_t need = (n / 4 + BLOCK * UNROLL - 1) / (BLOCK * UNROLL);
+    int g        = (int) std::max<int64_t>(1, std::min<int64_t>(need, GRID));
+    BinnerFast bf {bn.bucket, bn.offset, 1.0f / bn.bucket, (515.0f + 2.0f * fabsf(bn.offset)) * 4.76837158203125e-7f};
+    hist_var<BLOCK, UNROLL, COPIES, true, true, false, BinnerFast, LSH><<<g, BLOCK, 0, s>>>(x, n, bf, c);
+}
+
 // read-only ceiling: sum of the input (same load pattern)
 template <int BLOCK, int UNROLL>
 __global__ __launch_bounds__(BLOCK) void read_var(const float* __restrict__ x, int64_t n, float* __restrict__ out)
@@ -469,6 +579,12 @@ int main(int argc, char** argv)
         {"hist b256 u4 c4 g2048 nt (rcp fast path)", launch_hist_rcp<256, 4, 4, 2048>, true, {}},
         {"hist b1024 u4 c16 g256 nt (division)", launch_hist<1024, 4, 16, true, true, 256>, true, {}},
         {"hist b1024 u4 c16 g256 nt (rcp fast path)", launch_hist_rcp<1024, 4, 16, 256>, true, {}},
+        {"hist b256 u4 c4 g2048 nt (uniform thr)", launch_hist_fast<256, 4, 4, 2048, 6>, true, {}},
+        {"hist b512 u4 c8 g1024 nt (uniform thr)", launch_hist_fast<512, 4, 8, 1024, 6>, true, {}},
+        {"hist b256 u2 c4 g2048 pipelined (rcp)", launch_hist_pipe<256, 2, 4, 2048>, true, {}},
+        {"hist b256 u4 c4 g2048 pipelined (rcp)", launch_hist_pipe<256, 4, 4, 2048>, true, {}},
+        {"hist b512 u2 c8 g1024 pipelined (rcp)", launch_hist_pipe<512, 2, 8, 1024>, true, {}},
+        {"hist b256 u2 c4 g1024 pipelined (rcp)", launch_hist_pipe<256, 2, 4, 1024>, true, {}},
     };
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
