@@ -37,9 +37,16 @@ __device__ __forceinline__ float to_f32(unsigned short u)
         return __uint_as_float((uint32_t) u << 16);
 }
 
-template <int IO>
+// MAYBE_NAN = false: the caller knows f is not NaN (a QDQ output with finite delta and offset is
+// delta * (integer + offset): finite or +-inf), so the bf16 NaN canonicalisation is skipped
+template <int IO, bool MAYBE_NAN = true>
 __device__ __forceinline__ unsigned short from_f32(float f)
 {
+    // The empty asm pins f as an fp32 VGPR value: without it the backend folds
+    // fptrunc(fmul(a, b)) into v_fma_mix{lo,hi}_f16(a, b, 0), which rounds the exact product
+    // straight to fp16 (no fp32 rounding first: differs from torch's two-step cast near fp16
+    // rounding boundaries) and adds +0 (turns a -0 result into +0).
+    asm volatile("" : "+v"(f));
     if constexpr (IO == IO_F16)
         return __half_as_ushort(__float2half_rn(f));
     else
@@ -47,14 +54,21 @@ __device__ __forceinline__ unsigned short from_f32(float f)
         // c10::BFloat16 round_to_nearest_even (c10/util/BFloat16.h): RNE = gfx950's
         // v_cvt_pk_bf16_f32; torch maps every NaN to 0x7FC0
         const unsigned short h = __builtin_bit_cast(unsigned short, (__bf16) f);
+        if constexpr (!MAYBE_NAN)
+            return h;
         return f != f ? (unsigned short) 0x7FC0 : h;
     }
 }
 
+// thr = qdq_round_thr(p, rcp) (common.hpp), hoisted by the callers out of their element loops
 template <bool STOCHASTIC>
-__device__ __forceinline__ float qdq(float x, const QdqParams& p, uint64_t seed, uint64_t idx, float rcp)
+__device__ __forceinline__ float qdq(float x, const QdqParams& p, uint64_t seed, uint64_t idx, float rcp, float thr)
 {
-    float q = STOCHASTIC ? quantize_stochastic(x, p, seed, idx) : quantize_nearest_rcp(x, p, rcp);
+    float q;
+    if constexpr (STOCHASTIC)
+        q = quantize_stochastic(x, p, seed, idx);
+    else
+        q = qdq_round_fast(glibc_fmaxf(glibc_fminf(x, p.max), p.min), p, rcp, thr);
     return dequantize(q, p);
 }
 
@@ -89,9 +103,19 @@ __global__ __launch_bounds__(kBlock) void qdq16_vec_kernel(const u16x8* __restri
     u16x8 v = __builtin_nontemporal_load(in + i), r;
     const uint64_t e = (uint64_t) i * 8;
     const float rcp  = 1.0f / p.delta;
+    const float thr  = qdq_round_thr(p, rcp);
+    if (__builtin_isfinite(p.delta) && __builtin_isfinite(p.offset))
+    {
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-        r[k] = from_f32<IO>(qdq<STOCHASTIC>(to_f32<IO>(v[k]), p, seed, e + k, rcp));
+        for (int k = 0; k < 8; ++k)
+            r[k] = from_f32<IO, false>(qdq<STOCHASTIC>(to_f32<IO>(v[k]), p, seed, e + k, rcp, thr));
+    }
+    else
+    {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            r[k] = from_f32<IO>(qdq<STOCHASTIC>(to_f32<IO>(v[k]), p, seed, e + k, rcp, thr));
+    }
     __builtin_nontemporal_store(r, out + i);
 }
 
@@ -107,7 +131,8 @@ __global__ __launch_bounds__(kBlock) void qdq16_scalar_kernel(const unsigned sho
         QdqParams q = p;
         if constexpr (CH)
             q = table_params(table, (uint32_t) C, (uint32_t) ((i / K) % C));
-        out[i] = from_f32<IO>(qdq<STOCHASTIC>(to_f32<IO>(in[i]), q, seed, (uint64_t) i, 1.0f / q.delta));
+        const float rcp = 1.0f / q.delta;
+        out[i] = from_f32<IO>(qdq<STOCHASTIC>(to_f32<IO>(in[i]), q, seed, (uint64_t) i, rcp, qdq_round_thr(q, rcp)));
     }
 }
 
@@ -164,74 +189,10 @@ __global__ __launch_bounds__(kBlock) void ste16_scalar_kernel(const unsigned sho
     }
 }
 
-// ---- per-tensor ROUND_NEAREST via a 65,536-entry table ---------------------------------------------
-// A 16-bit input has 65,536 possible values, so a per-tensor nearest QDQ is a pure function of the
-// input bits: the table is built once per launch by the arithmetic above (so it is bit-identical to
-// it) and each persistent workgroup stages it in LDS (128 KiB of the CU's 160) and maps its share
-// of the tensor with one LDS read per element -- the arithmetic kernel is VALU-bound at ~20 ops per
-// element, the lookup is ~3.
-constexpr int kLutSize    = 65536;
-constexpr int kLutBlock   = 1024;
-constexpr int kLutUnroll  = 8;
-constexpr int64_t kLutMinN = int64_t(1) << 23;   // below: the table build is not amortised
-
-template <int IO>
-__global__ __launch_bounds__(kBlock) void qdq16_lut_build(QdqParams p, unsigned short* __restrict__ lut)
-{
-    const int b = blockIdx.x * kBlock + threadIdx.x;
-    if (b < kLutSize)
-        lut[b] = from_f32<IO>(qdq<false>(to_f32<IO>((unsigned short) b), p, 0, 0, 1.0f / p.delta));
-}
-
-__global__ __launch_bounds__(kLutBlock) void qdq16_lut_kernel(const u16x8* __restrict__ in, u16x8* __restrict__ out,
-                                                              int64_t nvec, const uint4* __restrict__ lut)
-{
-    __shared__ unsigned short tab[kLutSize];
-    uint4* t4 = reinterpret_cast<uint4*>(tab);
-#pragma unroll
-    for (int k = 0; k < kLutSize * 2 / 16 / kLutBlock; ++k)
-        t4[k * kLutBlock + threadIdx.x] = lut[k * kLutBlock + threadIdx.x];
-    __syncthreads();
-    constexpr int U      = kLutUnroll;   // 16-B loads in flight per lane: one workgroup per CU
-    const int64_t stride = (int64_t) gridDim.x * kLutBlock * U;
-    for (int64_t base = (int64_t) blockIdx.x * kLutBlock * U + threadIdx.x; base < nvec; base += stride)
-    {
-        u16x8 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-        {
-            const int64_t i = base + (int64_t) u * kLutBlock;
-            if (i < nvec)
-                v[u] = __builtin_nontemporal_load(in + i);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-        {
-            const int64_t i = base + (int64_t) u * kLutBlock;
-            if (i >= nvec)
-                break;
-            u16x8 r;
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-                r[k] = tab[v[u][k]];
-            __builtin_nontemporal_store(r, out + i);
-        }
-    }
-}
-
 bool aligned16(const void* a, const void* b, const void* c = nullptr)
 {
     return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(c)) & 15) ==
            0;
-}
-
-bool lut_enabled()
-{
-    static const bool on = [] {
-        const char* e = getenv("AIMET_QDQ16_LUT");   // A/B switch for measurements and tests
-        return !(e && e[0] == '0');
-    }();
-    return on;
 }
 
 // vector part over [0, nvec*8), scalar tail (per-tensor) or everything scalar (K % 8 != 0)
@@ -241,23 +202,7 @@ void launch_qdq16(const void* in, void* out, int64_t n, const QdqParams& p, int6
 {
     const bool vec_ok = aligned16(in, out) && (!CH || (K % 8 == 0 && n < (int64_t(1) << 32)));
     int64_t nvec      = vec_ok ? n / 8 : 0;
-    if (!CH && !STO && nvec > 0 && n >= kLutMinN && lut_enabled())
-    {
-        void* lut = nullptr;
-        AIMET_HIP_CHECK(hipMallocAsync(&lut, kLutSize * sizeof(unsigned short), s));
-        qdq16_lut_build<IO><<<kLutSize / kBlock, kBlock, 0, s>>>(p, static_cast<unsigned short*>(lut));
-        AIMET_LAUNCH_CHECK();
-        int dev = 0, cus = 0;
-        AIMET_HIP_CHECK(hipGetDevice(&dev));
-        AIMET_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        const int64_t want = ceil_div(nvec, (int64_t) kLutBlock * kLutUnroll);
-        const int grid     = (int) (want < cus ? want : cus);
-        qdq16_lut_kernel<<<grid, kLutBlock, 0, s>>>(reinterpret_cast<const u16x8*>(in), reinterpret_cast<u16x8*>(out),
-                                                    nvec, static_cast<const uint4*>(lut));
-        AIMET_LAUNCH_CHECK();
-        AIMET_HIP_CHECK(hipFreeAsync(lut, s));
-    }
-    else if (nvec > 0)
+    if (nvec > 0)
     {
         ChannelMap16 map {FastDiv((uint32_t) (CH ? K : 1)), FastDiv((uint32_t) (CH ? C : 1)), (uint32_t) C};
         qdq16_vec_kernel<IO, CH, STO><<<(unsigned) ceil_div(nvec, kBlock), kBlock, 0, s>>>(

@@ -588,9 +588,9 @@ def test_16bit_io_qdq_equals_upcast_path(dtype, rm):
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
-def test_16bit_io_qdq_table_path_all_bit_patterns(dtype):
-    """Large per-tensor nearest QDQ takes the 65,536-entry table path (qdq16.hip: qdq16_lut_kernel):
-    every 16-bit input pattern, tiled past the table threshold, equals upcast -> fp32 QDQ -> downcast."""
+def test_16bit_io_qdq_per_tensor_all_bit_patterns(dtype):
+    """Per-tensor nearest QDQ with 16-bit I/O (qdq16_vec_kernel, hoisted rounding threshold): every
+    16-bit input pattern, tiled to a large tensor, equals upcast -> fp32 QDQ -> downcast."""
     from aimet_amd import _native
     from aimet_amd.tensor_quantizer import IO_DTYPES
     code = IO_DTYPES[dtype]
@@ -606,6 +606,40 @@ def test_16bit_io_qdq_table_path_all_bit_patterns(dtype):
         out32 = torch.empty_like(xf)
         _native.call("aimet_qdq_per_tensor", xf.data_ptr(), out32.data_ptr(), n, enc.to_c(), 0, 0, stream)
         np.testing.assert_array_equal(_bits16(out16), _bits16(out32.to(dtype)), err_msg=str((lo, hi, bw)))
+
+
+@pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
+def test_16bit_io_qdq_per_channel_all_bit_patterns(dtype):
+    """Per-channel 16-bit QDQ (qdq16_vec_kernel, hoisted rounding threshold): every 16-bit input
+    pattern in every channel, channels with dyadic deltas (exact half-integer quotients: the exact
+    division path), zero / non-zero offsets, tiny and huge ranges, non-finite encodings; equals
+    upcast -> fp32 per-channel QDQ (IEEE division) -> downcast bit for bit."""
+    from aimet_amd import _native
+    from aimet_amd.tensor_quantizer import IO_DTYPES
+    code = IO_DTYPES[dtype]
+    stream = torch.cuda.current_stream().cuda_stream
+    ranges = [(-1.0, 1.0, 8), (-0.5, 0.5, 4), (0.0, 1.0, 8), (-1e-3, 7e4, 16), (-6e4, 6e4, 8), (-3e-5, 3e-5, 8),
+              (-2.0, 2.0 * 127 / 128, 8), (-2.5, 4.0, 8), (-1e-30, 1e-30, 8), (0.0, 255.0, 8), (-8.0, 7.0, 4),
+              (float("-inf"), 1.0, 8), (-1.0, float("nan"), 8),
+              # 16-bit grids: products delta * (q + off) on fine grids, where rounding the fp32
+              # product to fp16 (torch's two-step cast) and rounding the exact product differ
+              (-0.37, 11.3, 16), (-123.4, 77.7, 16), (-3.3e4, 6.1e4, 16), (-0.0123, 0.0456, 16)]
+    encs = [enc_of(lo, hi, bw) for lo, hi, bw in ranges]
+    C = len(encs)
+    pat = torch.arange(65536, dtype=torch.int32, device=DEV).to(torch.int16).view(dtype)
+    x = pat.repeat(C).view(C, 65536).contiguous()
+    q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF, num_channels=C)
+    table = q.channelTable(encs, torch.device(DEV))
+    out16 = torch.empty_like(x)
+    _native.call("aimet_qdq_per_channel_16", x.data_ptr(), out16.data_ptr(), 1, C, 65536, code, table.data_ptr(),
+                 0, 0, stream)
+    xf = x.float()
+    out32 = torch.empty_like(xf)
+    _native.call("aimet_qdq_per_channel", xf.data_ptr(), out32.data_ptr(), 1, C, 65536, table.data_ptr(), 0, 0,
+                 stream)
+    got, want = _bits16(out16).reshape(C, -1), _bits16(out32.to(dtype)).reshape(C, -1)
+    for c in range(C):
+        np.testing.assert_array_equal(got[c], want[c], err_msg=str(ranges[c]))
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
