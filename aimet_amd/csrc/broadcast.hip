@@ -216,11 +216,24 @@ __global__ __launch_bounds__(kBlock) void bcast_vec_kernel(const f4* __restrict_
             if (i >= nvec)
                 break;
             f4 r;
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
+            if (MODE == 0)
             {
-                QdqParams p {mn[u][j], mx[u][j], dl[u][j], of[u][j]};
-                r[j] = dequantize(quantize_nearest(x[u][j], p), p);
+                // one encoding per vector: its reciprocal and rounding threshold serve 4 elements
+                // (qdq_round_fast, common.hpp: bit-identical to the division form)
+                const QdqParams p {mn[u][0], mx[u][0], dl[u][0], of[u][0]};
+                const float rcp = 1.0f / p.delta, thr = qdq_round_thr(p, rcp);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    r[j] = dequantize(qdq_round_fast(glibc_fmaxf(glibc_fminf(x[u][j], p.max), p.min), p, rcp, thr), p);
+            }
+            else
+            {
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                {
+                    QdqParams p {mn[u][j], mx[u][j], dl[u][j], of[u][j]};
+                    r[j] = dequantize(quantize_nearest(x[u][j], p), p);
+                }
             }
             __builtin_nontemporal_store(r, out + i);
         }
@@ -250,6 +263,14 @@ __global__ __launch_bounds__(kBlock) void bcast_colblock_kernel(const f4* __rest
         const f4 mx = *reinterpret_cast<const f4*>(enc.mx + e);
         const f4 dl = *reinterpret_cast<const f4*>(enc.delta + e);
         const f4 of = *reinterpret_cast<const f4*>(enc.offset + e);
+        // per-column reciprocal and rounding threshold, reused over the kRows rows (qdq_round_fast)
+        f4 rc, th;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+        {
+            rc[j] = 1.0f / dl[j];
+            th[j] = qdq_round_thr(QdqParams {mn[j], mx[j], dl[j], of[j]}, rc[j]);
+        }
         const uint32_t b0   = rg * kRows;
         const uint32_t rows = B - b0 < (uint32_t) kRows ? B - b0 : (uint32_t) kRows;
         const uint32_t base = (a * B + b0) * C4 + c4;
@@ -269,8 +290,9 @@ __global__ __launch_bounds__(kBlock) void bcast_colblock_kernel(const f4* __rest
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
                 {
-                    QdqParams p {mn[j], mx[j], dl[j], of[j]};
-                    y[j] = dequantize(quantize_nearest(x[u][j], p), p);
+                    const QdqParams p {mn[j], mx[j], dl[j], of[j]};
+                    y[j] = dequantize(qdq_round_fast(glibc_fmaxf(glibc_fminf(x[u][j], p.max), p.min), p, rc[j], th[j]),
+                                      p);
                 }
                 __builtin_nontemporal_store(y, out + base + (r0 + u) * C4);
             }
@@ -318,16 +340,17 @@ __device__ __forceinline__ float fp16_rt(float x)
     return (float) (_Float16) x;
 }
 
+// one float4 per lane, one 256-lane tile per workgroup (the tensor_vec_kernel form: 6.4 TB/s
+// where a 2048-workgroup grid-stride loop reached 5.2)
 __global__ __launch_bounds__(kBlock) void fp16_vec_kernel(const f4* __restrict__ in, f4* __restrict__ out,
                                                           int64_t nvec)
 {
-    const int64_t stride = (int64_t) gridDim.x * kBlock;
-    for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < nvec; i += stride)
-    {
-        f4 x = __builtin_nontemporal_load(in + i);
-        f4 r {fp16_rt(x.x), fp16_rt(x.y), fp16_rt(x.z), fp16_rt(x.w)};
-        __builtin_nontemporal_store(r, out + i);
-    }
+    const int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nvec)
+        return;
+    f4 x = __builtin_nontemporal_load(in + i);
+    f4 r {fp16_rt(x.x), fp16_rt(x.y), fp16_rt(x.z), fp16_rt(x.w)};
+    __builtin_nontemporal_store(r, out + i);
 }
 
 __global__ __launch_bounds__(kBlock) void fp16_scalar_kernel(const float* __restrict__ in, float* __restrict__ out,
@@ -368,14 +391,17 @@ void launch_qdq_broadcast(const float* in, float* out, int64_t n, int64_t nd, co
         bool vec_tab = ies == 1 && aligned16(mn, mx) && aligned16(delta, offset);
         for (int d = 0; d + 1 < v.nd; ++d)
             vec_tab = vec_tab && v.estride[d] % 4 == 0;
-        const int blocks = stream_blocks(nvec, (int64_t) kBlock * kUnroll);
+        // one tile (kBlock x kUnroll vectors) per workgroup: 6.4 TB/s on [4096 x 65536] with
+        // 64-blocks, where a 2048-workgroup grid-stride loop reached 5.7 (profiles/r01)
+        const int blocks = (int) ceil_div(nvec, (int64_t) kBlock * kUnroll);
         auto in4 = reinterpret_cast<const f4*>(in);
         auto out4 = reinterpret_cast<f4*>(out);
         if (vec_tab && v.nd == 3 && v.estride[1] == 0 && v.estride[0] == v.size[2])
         {
             const uint32_t A = (uint32_t) v.size[0], B = (uint32_t) v.size[1], C4 = (uint32_t) (v.size[2] / 4);
             const uint32_t nrg = (B + kRows - 1) / kRows;
-            bcast_colblock_kernel<<<stream_blocks((int64_t) A * nrg * C4, kBlock), kBlock, 0, s>>>(
+            const int64_t items = (int64_t) A * nrg * C4;
+            bcast_colblock_kernel<<<(int) ceil_div(items, kBlock), kBlock, 0, s>>>(
                 in4, out4, A, B, C4, FastDiv(C4), FastDiv(nrg), nrg, enc);
         }
         else if (ies == 0)
@@ -413,8 +439,9 @@ void launch_qdq_fp16(const float* in, float* out, int64_t n, hipStream_t s)
         int64_t nvec = n / 4;
         if (nvec)
         {
-            fp16_vec_kernel<<<stream_blocks(nvec, kBlock * 4), kBlock, 0, s>>>(reinterpret_cast<const f4*>(in),
-                                                                             reinterpret_cast<f4*>(out), nvec);
+            AIMET_REQUIRE(ceil_div(nvec, kBlock) < (int64_t(1) << 31), "tensor too large");
+            fp16_vec_kernel<<<(unsigned) ceil_div(nvec, kBlock), kBlock, 0, s>>>(reinterpret_cast<const f4*>(in),
+                                                                               reinterpret_cast<f4*>(out), nvec);
             AIMET_LAUNCH_CHECK();
         }
         done = nvec * 4;

@@ -237,6 +237,35 @@ def test_broadcast_qdq_large_vs_oracle():
 
 @pytest.mark.gpu
 @gpu
+def test_broadcast_qdq_rounding_ties_vs_oracle():
+    """Blockwise QDQ with a per-vector reciprocal (contiguous blocks) and per-column reciprocals
+    (strided blocks): dyadic deltas and inputs on exact half-integer quotients (the exact-division
+    fallback), zero and non-zero offsets, signed zeros, NaN / inf inputs; bit-exact vs the oracle."""
+    import torch
+    from aimet_amd.onnx_op import BroadcastShapeInfo, quantize_dequantize_broadcast
+    rng = np.random.default_rng(9)
+    for shape, ch, ba, bs in [((256, 512), 0, 1, 64), ((512, 256), 1, 0, 32)]:
+        info = BroadcastShapeInfo(shape, ch, ba, bs)
+        E = info.numEncodings
+        d = (2.0 ** rng.integers(-12, 2, E)).astype(np.float32)
+        off = rng.choice(np.array([-8, 0, -0.0, -3, -128], np.float32), E)
+        steps = rng.choice(np.array([15, 255], np.float32), E)
+        tab = np.stack([off * d, (off + steps) * d, d, off], 1).astype(np.float32)
+        n = int(np.prod(shape))
+        # each element's encoding index: a QDQ with min = max = index, delta 1, offset 0
+        ar = np.arange(E, dtype=np.float32)
+        eidx = O.qdq_broadcast(np.zeros(n, np.float32), info.tensorStrides, info.encodingStrides, ar, ar,
+                               np.ones(E, np.float32), np.zeros(E, np.float32)).astype(np.int64)
+        # multiples of delta/2 of every element's own encoding: exact half-integer quotients
+        x = (rng.integers(-600, 600, n) * 0.5 * d[eidx]).astype(np.float32)
+        x[:8] = [0.0, -0.0, np.nan, np.inf, -np.inf, 1e-30, -1e-30, 3.0]
+        y = quantize_dequantize_broadcast(torch.from_numpy(x).cuda(), info, _encs_from(tab)).cpu().numpy()
+        want = O.qdq_broadcast(x, info.tensorStrides, info.encodingStrides, tab[:, 0], tab[:, 1], tab[:, 2], tab[:, 3])
+        np.testing.assert_array_equal(bits(y), bits(want), err_msg=str(shape))
+
+
+@pytest.mark.gpu
+@gpu
 def test_block_permute_and_fp16_on_device():
     import torch
     from aimet_amd.onnx_op import BroadcastShapeInfo, copy_to_contiguous_block_layout, quantize_dequantize_fp16
