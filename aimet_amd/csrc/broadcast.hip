@@ -246,6 +246,7 @@ __global__ __launch_bounds__(kBlock) void bcast_vec_kernel(const f4* __restrict_
 // reused kRows times and every row load is coalesced across the wave (lanes = columns).
 constexpr int kRows = 16;
 
+template <int RB>
 __global__ __launch_bounds__(kBlock) void bcast_colblock_kernel(const f4* __restrict__ in, f4* __restrict__ out,
                                                                 uint32_t A, uint32_t B, uint32_t C4, FastDiv divC4,
                                                                 FastDiv divRg, uint32_t nrg, EncArrays enc)
@@ -274,15 +275,15 @@ __global__ __launch_bounds__(kBlock) void bcast_colblock_kernel(const f4* __rest
         const uint32_t b0   = rg * kRows;
         const uint32_t rows = B - b0 < (uint32_t) kRows ? B - b0 : (uint32_t) kRows;
         const uint32_t base = (a * B + b0) * C4 + c4;
-        for (uint32_t r0 = 0; r0 < rows; r0 += 4)
+        for (uint32_t r0 = 0; r0 < rows; r0 += RB)   // RB row loads in flight per lane
         {
-            f4 x[4];
+            f4 x[RB];
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < RB; ++u)
                 if (r0 + u < rows)
                     x[u] = __builtin_nontemporal_load(in + base + (r0 + u) * C4);
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
+            for (int u = 0; u < RB; ++u)
             {
                 if (r0 + u >= rows)
                     break;
@@ -401,8 +402,9 @@ void launch_qdq_broadcast(const float* in, float* out, int64_t n, int64_t nd, co
             const uint32_t A = (uint32_t) v.size[0], B = (uint32_t) v.size[1], C4 = (uint32_t) (v.size[2] / 4);
             const uint32_t nrg = (B + kRows - 1) / kRows;
             const int64_t items = (int64_t) A * nrg * C4;
-            bcast_colblock_kernel<<<(int) ceil_div(items, kBlock), kBlock, 0, s>>>(
-                in4, out4, A, B, C4, FastDiv(C4), FastDiv(nrg), nrg, enc);
+            // 8 row loads in flight per lane (measured: 4 -> 5.2 TB/s, 8 -> 5.4, 16 -> 5.0)
+            bcast_colblock_kernel<8><<<(int) ceil_div(items, kBlock), kBlock, 0, s>>>(in4, out4, A, B, C4, FastDiv(C4),
+                                                                                     FastDiv(nrg), nrg, enc);
         }
         else if (ies == 0)
             bcast_vec_kernel<0><<<blocks, kBlock, 0, s>>>(in4, out4, nvec, v32, ies, enc);
