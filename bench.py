@@ -34,7 +34,10 @@ HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level pa
 BYTES_QDQ = 8            # fp32 read + fp32 write per element
 # HBM bytes per step of the activation QDQ launches from the rocprofv3 PMC passes
 # (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), profiles/r01/bench_summary_*.txt
+# (measured at the default workload: 2,883,971,072 activation elements per step; other batch sizes
+# report null)
 TRAFFIC_GB = 23.075
+TRAFFIC_ELEMS = 2883971072
 
 
 def parse():
@@ -57,10 +60,18 @@ def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # AIMET_BENCH_BACKEND=gloo rehearses the N-rank path with several ranks sharing fewer GPUs
+    # (RCCL needs one GPU per rank); the statistics exchange then stages through host memory
+    backend = os.environ.get("AIMET_BENCH_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend, rank=rank, world_size=world)
     else:
         torch.cuda.set_device(local)
     return rank, world, torch.device("cuda", local)
@@ -300,7 +311,8 @@ def main():
     act_ms = [s.elapsed_time(e) for s, e in ev]
     kernel_ms = sum(act_ms) / len(act_ms)
     if world > 1:
-        tt = torch.tensor([dt, enc_seconds, enc_cold], device=dev, dtype=torch.float64)
+        tt = torch.tensor([dt, enc_seconds, enc_cold], dtype=torch.float64,
+                          device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt, enc_seconds, enc_cold = float(tt[0]), float(tt[1]), float(tt[2])
 
@@ -337,7 +349,7 @@ def main():
                    "compute_encodings_scheme": "tf_enhanced act per-tensor + tf_enhanced weight per-channel sym"},
         "roofline": {"bound": "hbm", "kernel": "qdq_per_tensor (tensor_vec_kernel)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": TRAFFIC_GB,
+                     "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": TRAFFIC_GB if n_act == TRAFFIC_ELEMS else None,
                      "bytes_per_elem": BYTES_QDQ, "launches_per_step": len(act_calls),
                      "avg_launch_us": round(kernel_ms * 1e3 / len(act_calls), 2),
                      "act_qdq_ms_per_step": round(kernel_ms, 4),
