@@ -132,10 +132,10 @@ std::vector<T> d2h(const T* dev, size_t n)
 }
 
 template <class F>
-void parallel_channels(int64_t C, F&& f)
+void parallel_channels(int64_t C, F&& f, int64_t grain = 64)   // grain: fewest tasks worth a thread
 {
     unsigned hw   = std::max(1u, std::thread::hardware_concurrency());
-    int64_t nthr  = std::min<int64_t>({(int64_t) hw, 16, (C + 63) / 64});
+    int64_t nthr  = std::min<int64_t>({(int64_t) hw, 16, (C + grain - 1) / grain});
     if (nthr <= 1)
     {
         for (int64_t c = 0; c < C; ++c)
@@ -551,45 +551,92 @@ void launch_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict, 
         launch_mse_search(q->d, q->C, b, sym, strict, unsign, s);
 }
 
-// getEncoding, part 2 (stream already synchronised): read back and finish on the host.
-void collect_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict, int unsign, aimet_tf_encoding* out)
+// getEncoding, part 2 (stream already synchronised): read back the statistics of a quantizer whose
+// encoding is finished on the host (TF, percentile, entropy); the device-searched ones (MSE) copy
+// their encodings straight into `out`.
+struct HostStats
+{
+    aimet_tensor_quantizer* q = nullptr;
+    aimet_tf_encoding* out    = nullptr;
+    std::vector<double> acc, bsz, pdf;
+    std::vector<int32_t> init;
+    std::vector<float> hmin;
+};
+
+bool fetch_stats(aimet_tensor_quantizer* q, aimet_tf_encoding* out, HostStats& h)
 {
     const int64_t C = q->C;
+    h.q   = q;
+    h.out = out;
     if (!q->hist)
     {
-        auto acc = d2h(q->d.acc, 2 * C);
-        parallel_channels(C, [&](int64_t c) {
-            out[c] = tf_encoding(acc[2 * c], acc[2 * c + 1], b, sym, strict, unsign);
-        });
-        return;
-    }
-    if (q->kind == kKindEntropy)
-    {
-        // TensorProfilingParams back (16 + 4 KiB per channel); the KL search runs on the host
-        auto init = d2h(q->d.pdf_init, C);
-        auto acc  = d2h(q->d.acc, 2 * C);
-        auto hist = d2h(q->d.pdf, (size_t) kPdfSize * C);
-        parallel_channels(C, [&](int64_t c) {
-            out[c] = entropy_encoding(init[c] != 0, true, acc[2 * c], acc[2 * c + 1], hist.data() + kPdfSize * c, b,
-                                      sym, strict, unsign);
-        });
-        return;
+        h.acc = d2h(q->d.acc, 2 * C);
+        return true;
     }
     if (device_search(q))
     {
         // candidate search ran on the device (tfe_search.hip / mse_search.hip): only the
         // encodings come back
         AIMET_HIP_CHECK(hipMemcpy(out, q->d.enc, sizeof(aimet_tf_encoding) * C, hipMemcpyDeviceToHost));
-        return;
+        return false;
     }
-    auto init = d2h(q->d.pdf_init, C);
-    auto hmin = d2h(q->d.hist_min, C);
-    auto bsz  = d2h(q->d.bucket_size, C);
-    auto pdf  = d2h(q->d.pdf, (size_t) kPdfSize * C);
-    parallel_channels(C, [&](int64_t c) {
-        out[c] = histogram_encoding(q->scheme, init[c] != 0, true, hmin[c], bsz[c], pdf.data() + kPdfSize * c,
-                                    q->percentile, b, sym, strict, unsign);
-    });
+    h.init = d2h(q->d.pdf_init, C);
+    h.pdf  = d2h(q->d.pdf, (size_t) kPdfSize * C);
+    if (q->kind == kKindEntropy)
+        h.acc = d2h(q->d.acc, 2 * C);   // TensorProfilingParams {min, max}; the KL search runs here
+    else
+    {
+        h.hmin = d2h(q->d.hist_min, C);
+        h.bsz  = d2h(q->d.bucket_size, C);
+    }
+    return true;
+}
+
+void host_encoding(const HostStats& h, int64_t c, int32_t b, int sym, int strict, int unsign)
+{
+    const aimet_tensor_quantizer* q = h.q;
+    if (!q->hist)
+        h.out[c] = tf_encoding(h.acc[2 * c], h.acc[2 * c + 1], b, sym, strict, unsign);
+    else if (q->kind == kKindEntropy)
+        h.out[c] = entropy_encoding(h.init[c] != 0, true, h.acc[2 * c], h.acc[2 * c + 1], h.pdf.data() + kPdfSize * c,
+                                    b, sym, strict, unsign);
+    else
+        h.out[c] = histogram_encoding(q->scheme, h.init[c] != 0, true, h.hmin[c], h.bsz[c], h.pdf.data() + kPdfSize * c,
+                                      q->percentile, b, sym, strict, unsign);
+}
+
+// the host-finished encodings of every (quantizer, channel) in one thread pool: the entropy KL
+// search is ~3 ms per channel, so a model's per-tensor entropy quantizers run in parallel too
+void collect_encodings(aimet_tensor_quantizer* const* qs, aimet_tf_encoding* const* outs, int64_t n, int32_t b,
+                       int sym, int strict, int unsign)
+{
+    std::vector<HostStats> hs;
+    hs.reserve((size_t) n);
+    for (int64_t i = 0; i < n; ++i)
+    {
+        HostStats h;
+        if (fetch_stats(qs[i], outs[i], h))
+            hs.push_back(std::move(h));
+    }
+    std::vector<std::pair<int32_t, int64_t>> tasks;
+    bool costly = false;   // the entropy KL search: ~3 ms per channel, worth a thread each
+    for (size_t k = 0; k < hs.size(); ++k)
+    {
+        costly = costly || hs[k].q->kind == kKindEntropy;
+        for (int64_t c = 0; c < hs[k].q->C; ++c)
+            tasks.emplace_back((int32_t) k, c);
+    }
+    parallel_channels(
+        (int64_t) tasks.size(),
+        [&](int64_t t) {
+            host_encoding(hs[(size_t) tasks[(size_t) t].first], tasks[(size_t) t].second, b, sym, strict, unsign);
+        },
+        costly ? 1 : 64);
+}
+
+void collect_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict, int unsign, aimet_tf_encoding* out)
+{
+    collect_encodings(&q, &out, 1, b, sym, strict, unsign);
 }
 
 }   // namespace
@@ -657,12 +704,18 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
             std::memcpy(out + offs[k], tfe.data() + src, sizeof(aimet_tf_encoding) * Cs[k]);
         AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
         off = 0;
+        std::vector<aimet_tensor_quantizer*> host_q;
+        std::vector<aimet_tf_encoding*> host_out;
         for (int64_t i = 0; i < nq; ++i)
         {
             if (qs[i]->stats_updated && !(qs[i]->hist && qs[i]->scheme == AIMET_QUANTIZATION_TF_ENHANCED))
-                collect_encoding(qs[i], b, sym, strict, unsign, out + off);
+            {
+                host_q.push_back(qs[i]);
+                host_out.push_back(out + off);
+            }
             off += qs[i]->C;
         }
+        collect_encodings(host_q.data(), host_out.data(), (int64_t) host_q.size(), b, sym, strict, unsign);
     });
 }
 

@@ -268,8 +268,9 @@ def test_get_encodings_batched_equals_individual():
     rng = np.random.default_rng(3)
     qs = []
     for scheme in (QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
-                   QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE):
-        for C in (1, 7):
+                   QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE,
+                   QuantizationMode.QUANTIZATION_ENTROPY):
+        for C in (1, 7, 1, 1):   # several per-tensor entropy quantizers: the host pool spans quantizers
             q = AimetTensorQuantizer(scheme, num_channels=C)
             if scheme == QuantizationMode.QUANTIZATION_PERCENTILE:
                 q.setPercentileValue(99.0)
