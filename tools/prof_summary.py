@@ -58,9 +58,13 @@ def main():
             cagg[k][0] += 1
             cagg[k][1] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         tot = sum(d for _, d in cagg.values())
-        print("compute_encodings kernels (before the first QDQ step): %.3f ms GPU time" % (tot / 1e6))
+        # bench.py runs compute_encodings 1 + --enc-reps times: one minmax_many launch per call
+        ncalls = max(1, sum(c for k, (c, _) in cagg.items() if k.startswith("minmax_many_kernel")))
+        print("compute_encodings kernels (before the first QDQ step): %d calls, %.3f ms GPU time per call"
+              % (ncalls, tot / 1e6 / ncalls))
         for k, (c, d) in sorted(cagg.items(), key=lambda x: -x[1][1]):
-            print("  %-62s calls %5d  total ms %.4f  avg us %.1f" % (k, c, d / 1e6, d / 1e3 / c))
+            print("  %-62s calls/call %4.1f  ms/call %.4f  avg us %.1f" % (k, c / ncalls, d / 1e6 / ncalls,
+                                                                         d / 1e3 / c))
     if len(args) >= 3:
         f = [v for n, v in pmc(args[1], "FETCH_SIZE") if QDQ in n][-per_step:]
         w = [v for n, v in pmc(args[2], "WRITE_SIZE") if QDQ in n][-per_step:]
@@ -80,9 +84,10 @@ def main():
             if "aimet_amd" in n:
                 cw[n.replace("(anonymous namespace)::", "").replace("aimet_amd::", "").replace("void ", "")
                    .split("(")[0]] += v * 1024
-        print("compute_encodings HBM traffic per kernel (FETCH_SIZE x2 + WRITE_SIZE):")
+        nc = max(1, sum(1 for n, _ in fa[:cut_f] if "minmax_many_kernel" in n))
+        print("compute_encodings HBM traffic per kernel per call (FETCH_SIZE x2 + WRITE_SIZE; %d calls):" % nc)
         for k in sorted(cf, key=lambda k: -cf[k]):
-            print("  %-62s fetch %.4f GB  write %.4f GB" % (k, cf[k] / 1e9, cw.get(k, 0) / 1e9))
+            print("  %-62s fetch %.4f GB  write %.4f GB" % (k, cf[k] / 1e9 / nc, cw.get(k, 0) / 1e9 / nc))
 
 
 if __name__ == "__main__":
