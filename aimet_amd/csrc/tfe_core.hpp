@@ -220,6 +220,25 @@ AIMET_HD inline bool bins_skip_empty(const Hist& h)
     return a >= -1e30 && a <= 1e30 && b >= -1e30 && b <= 1e30;
 }
 
+// (int) std::round(v / delta - offset) exactly as the reference evaluates it (float division,
+// half away from zero). On the device the IEEE division is taken only near half-integers: with
+// rcp = RN(1/delta) and thr >= 2^-21 (|v*rcp| + |offset| + 1) for every v of the loop, rint of
+// RN(RN(v*rcp) - offset) equals the reference's rounding whenever the fractional part is more
+// than thr away from 1/2 (the round_div_sub / qdq_round_fast argument, common.hpp); the int
+// conversion drops the sign of a zero code, so no sign test is needed.
+AIMET_HD inline int quant_code(float v, float delta, int offset, float rcp, float thr)
+{
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float x = v * rcp - (float) offset;
+    if (fabsf(__builtin_amdgcn_fractf(x) - 0.5f) > thr)   // false for NaN
+        return (int) __builtin_rintf(x);
+#else
+    (void) rcp;
+    (void) thr;
+#endif
+    return (int) roundf(v / delta - offset);
+}
+
 // _quantAndSatCost (:293-355) over the prepared bins. The three sums keep the reference's
 // ascending order; a bin can belong to more than one of them exactly as in the reference loops.
 AIMET_HD inline double cost(const Bins& B, int bw, float delta, int offset)
@@ -233,6 +252,10 @@ AIMET_HD inline double cost(const Bins& B, int bw, float delta, int offset)
     iHi               = smin(smax(0, iHi), kBins - 1);
     const float loMid = B.cf[iLo];
     const float hiMid = B.cf[iHi];
+    // every v of the quantisation loop lies in [cf[iLo], cf[iHi]] (bin centres ascend)
+    const float rcp = 1.0f / delta;
+    const float vmax = (loMid != loMid || hiMid != hiMid) ? NAN : smax(fabsf(loMid), fabsf(hiMid));   // NaN: exact path
+    const float thr  = (vmax * rcp + fabsf((float) offset) + 1.0f) * 4.76837158203125e-7f;
     double satLo = 0, satHi = 0, quant = 0;
     for (int k = 0; k < B.nnz; ++k)
     {
@@ -251,7 +274,7 @@ AIMET_HD inline double cost(const Bins& B, int bw, float delta, int offset)
         if (i >= iLo && i < iHi)
         {
             float v   = B.cf[i];
-            int q     = (int) roundf(v / delta - offset);
+            int q     = quant_code(v, delta, offset, rcp, thr);
             float deq = delta * (q + offset);
             double d  = (double) (v - deq);
             quant += p * (d * d);
