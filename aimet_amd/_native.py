@@ -140,6 +140,8 @@ _PROTOTYPES = {
     "aimet_adaround_forward": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _int, _vp],
     "aimet_adaround_backward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, ctypes.c_float,
                                 ctypes.c_float, _vp, _vp],
+    "aimet_adaround_backward_dev": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp],
+    "aimet_adaround_recon_grad": [_vp, _vp, _vp, _i64, _i64, _int, _vp],
 }
 _RESTYPES = {"aimet_last_error": ctypes.c_char_p, "aimet_version": ctypes.c_char_p}
 

@@ -166,8 +166,14 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
                                                                   uint32_t nq, AdaChannel map,
                                                                   const float* __restrict__ delta,
                                                                   const float* __restrict__ offset, AdaParams p,
-                                                                  float* __restrict__ round_loss)
+                                                                  float* __restrict__ round_loss,
+                                                                  const float* __restrict__ reg_beta)
 {
+    if (reg_beta)   // device-resident {reg, beta}: a HIP-graph replay per iteration
+    {
+        p.reg  = reg_beta[0];
+        p.beta = reg_beta[1];
+    }
     float loss = 0.0f;
     constexpr int U       = 4;   // quads in flight per lane (3 x 16-B loads each)
     const uint32_t stride = gridDim.x * kBlock * U;
@@ -213,8 +219,14 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
                                                               uint32_t n, AdaChannel map,
                                                               const float* __restrict__ delta,
                                                               const float* __restrict__ offset, AdaParams p,
-                                                              float* __restrict__ round_loss)
+                                                              float* __restrict__ round_loss,
+                                                              const float* __restrict__ reg_beta)
 {
+    if (reg_beta)
+    {
+        p.reg  = reg_beta[0];
+        p.beta = reg_beta[1];
+    }
     float loss = 0.0f;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
     {
@@ -232,6 +244,53 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
 bool aligned16(const void* p)
 {
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+}
+
+// ---- reconstruction-loss gradient (adaround_loss.py:70-80) ------------------------------------
+// loss = mean over (N, spatial) of ||act(q) - act(t)||^2 over dim 1, so
+// dloss/dq = scale * (act(q) - act(t)) * act'(q) with scale = 2 / (N * spatial): one elementwise
+// pass (12 B/elem) for the ~12 torch kernels of act / sub / norm / pow / mean and their backward.
+// act: 0 none, 1 ReLU (torch threshold_backward: x > 0), 2 ReLU6 (hardtanh(0, 6) backward:
+// 0 < x < 6).
+__device__ __forceinline__ float recon_g(float q, float t, float scale, int act)
+{
+    float a = q, b = t, m = 1.0f;
+    if (act == 1)
+    {
+        a = fmaxf(q, 0.0f);
+        b = fmaxf(t, 0.0f);
+        m = q > 0.0f ? 1.0f : 0.0f;
+    }
+    else if (act == 2)
+    {
+        a = fminf(fmaxf(q, 0.0f), 6.0f);
+        b = fminf(fmaxf(t, 0.0f), 6.0f);
+        m = (q > 0.0f && q < 6.0f) ? 1.0f : 0.0f;
+    }
+    return scale * (a - b) * m;
+}
+
+__global__ __launch_bounds__(kBlock) void recon_grad_vec_kernel(const f4* __restrict__ q, const f4* __restrict__ t,
+                                                                f4* __restrict__ g, int64_t nq, float scale, int act)
+{
+    const int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nq)
+        return;
+    const f4 a = __builtin_nontemporal_load(q + i), b = __builtin_nontemporal_load(t + i);
+    f4 r;
+    r.x = recon_g(a.x, b.x, scale, act);
+    r.y = recon_g(a.y, b.y, scale, act);
+    r.z = recon_g(a.z, b.z, scale, act);
+    r.w = recon_g(a.w, b.w, scale, act);
+    __builtin_nontemporal_store(r, g + i);
+}
+
+__global__ __launch_bounds__(kBlock) void recon_grad_kernel(const float* __restrict__ q, const float* __restrict__ t,
+                                                            float* __restrict__ g, int64_t begin, int64_t n,
+                                                            float scale, int act)
+{
+    for (int64_t i = begin + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
+        g[i] = recon_g(q[i], t[i], scale, act);
 }
 
 }   // namespace
@@ -271,9 +330,14 @@ int aimet_adaround_forward(const float* w, const float* alpha, float* wq, int64_
     });
 }
 
-int aimet_adaround_backward(const float* w, const float* alpha, const float* g, float* ga, int64_t outer, int64_t C,
-                            int64_t K, const float* delta, const float* offset, int32_t bw, float reg, float beta,
-                            float* round_loss, void* stream)
+}   // extern "C"
+
+namespace
+{
+
+int adaround_backward(const float* w, const float* alpha, const float* g, float* ga, int64_t outer, int64_t C,
+                      int64_t K, const float* delta, const float* offset, int32_t bw, float reg, float beta,
+                      const float* reg_beta, float* round_loss, void* stream)
 {
     return guarded([&] {
         AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
@@ -297,13 +361,75 @@ int aimet_adaround_backward(const float* w, const float* alpha, const float* g, 
             adaround_bwd_vec_kernel<<<(unsigned) (blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid), kBlock, 0,
                                       as_stream(stream)>>>(
                 reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),
-                reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss);
+                reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss, reg_beta);
         }
         else
             adaround_bwd_kernel<<<stream_blocks(n, kBlock), kBlock, 0, as_stream(stream)>>>(
-                w, alpha, g, ga, (uint32_t) n, map, delta, offset, p, round_loss);
+                w, alpha, g, ga, (uint32_t) n, map, delta, offset, p, round_loss, reg_beta);
         AIMET_LAUNCH_CHECK();
     });
+}
+
+}   // namespace
+
+extern "C" {
+
+int aimet_adaround_backward(const float* w, const float* alpha, const float* g, float* ga, int64_t outer, int64_t C,
+                            int64_t K, const float* delta, const float* offset, int32_t bw, float reg, float beta,
+                            float* round_loss, void* stream)
+{
+    return adaround_backward(w, alpha, g, ga, outer, C, K, delta, offset, bw, reg, beta, nullptr, round_loss, stream);
+}
+
+int aimet_adaround_recon_grad(const float* q, const float* t, float* g, int64_t n, int64_t reduced, int act,
+                              void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(n >= 0 && reduced > 0, "invalid shape");
+        AIMET_REQUIRE(act >= 0 && act <= 2, "act must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
+        if (n == 0)
+            return;
+        require_device_ptr(q, "quant_out");
+        require_device_ptr(t, "orig_out");
+        require_device_ptr(g, "grad");
+        AIMET_REQUIRE(n % reduced == 0, "element count is not a multiple of the reduced dimension");
+        // torch: mean over n / reduced values of the dim-1 squared norm; d/dq = 2 (a - b) / count
+        const float scale = (float) (2.0 / (double) (n / reduced));
+        hipStream_t s     = as_stream(stream);
+        int64_t done      = 0;
+        if (aligned16(q) && aligned16(t) && aligned16(g))
+        {
+            const int64_t nq = n / 4;
+            if (nq)
+            {
+                AIMET_REQUIRE(ceil_div(nq, kBlock) < (int64_t(1) << 31), "tensor too large");
+                recon_grad_vec_kernel<<<(unsigned) ceil_div(nq, kBlock), kBlock, 0, s>>>(
+                    reinterpret_cast<const f4*>(q), reinterpret_cast<const f4*>(t), reinterpret_cast<f4*>(g), nq,
+                    scale, act);
+                AIMET_LAUNCH_CHECK();
+            }
+            done = nq * 4;
+        }
+        if (done < n)
+        {
+            recon_grad_kernel<<<stream_blocks(n - done, kBlock), kBlock, 0, s>>>(q, t, g, done, n, scale, act);
+            AIMET_LAUNCH_CHECK();
+        }
+    });
+}
+
+int aimet_adaround_backward_dev(const float* w, const float* alpha, const float* g, float* ga, int64_t outer,
+                                int64_t C, int64_t K, const float* delta, const float* offset, int32_t bw,
+                                const float* reg_beta_dev, float* round_loss, void* stream)
+{
+    const int rc = guarded([&] {
+        AIMET_REQUIRE(reg_beta_dev != nullptr, "reg_beta_dev is null");
+        require_device_ptr(reg_beta_dev, "reg_beta");
+    });
+    if (rc != AIMET_OK)
+        return rc;
+    return adaround_backward(w, alpha, g, ga, outer, C, K, delta, offset, bw, 0.0f, 0.0f, reg_beta_dev, round_loss,
+                             stream);
 }
 
 }   // extern "C"

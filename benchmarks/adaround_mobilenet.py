@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--iterations", type=int, default=10000)
     ap.add_argument("--images", type=int, default=1024)
     ap.add_argument("--layers", type=int, default=0, help="only the first N layers (0 = all)")
+    ap.add_argument("--eager", action="store_true",
+                    help="launch every iteration from Python instead of replaying one captured HIP graph")
     ap.add_argument("--reference-iters", type=int, default=0,
                     help="also time N iterations per layer of the torch-op reference loop")
     args = ap.parse_args()
@@ -91,10 +93,12 @@ def main():
         act = follow.get(name)
         # untimed warm-up of this layer's shapes (MIOpen kernel selection, allocator) for both loops
         warm = AdaroundHyperParameters(num_iterations=5, warm_start=0.2)
-        AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, warm, act, torch.Generator().manual_seed(1))
+        AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, warm, act, torch.Generator().manual_seed(1),
+                                            use_graph=not args.eager)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        alpha = AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, params, act, gen, loss_buf)
+        alpha = AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, params, act, gen, loss_buf,
+                                                    use_graph=not args.eager)
         torch.cuda.synchronize()
         dt_ours = time.perf_counter() - t0
         t_opt += dt_ours
@@ -156,6 +160,7 @@ def main():
         "value": round(t_opt, 3), "unit": "s", "higher_is_better": False, "n_gpus": 1,
         "layers": len(names), "iterations_per_layer": args.iterations, "images": args.images,
         "ms_per_iteration": round(t_opt / iters * 1e3, 4), "activation_caching_s": round(t_cache, 3),
+        "loop": "eager" if args.eager else "hipgraph (one captured iteration replayed per iteration)",
         "weights_elems": elems,
         "softquant_fwd_GBps": round(elems * 12 / (fwd_t * 1e-3) / 1e9, 1),
         "softquant_bwd_roundloss_GBps": round(elems * 16 / (bwd_t * 1e-3) / 1e9, 1),

@@ -296,6 +296,18 @@ int aimet_adaround_forward(const float* w, const float* alpha, float* wq, int64_
 int aimet_adaround_backward(const float* w, const float* alpha, const float* grad_wq, float* grad_alpha,
                             int64_t outer, int64_t C, int64_t K, const float* delta_dev, const float* offset_dev,
                             int32_t bw, float reg_param, float beta, float* round_loss_dev, void* stream);
+/* The same with {reg_param, beta} read from device memory (reg_beta_dev[2]) when the kernel runs:
+ * the AdaRound iteration captured once in a HIP graph and replayed with the annealed beta of
+ * each iteration (adaround_optimizer.py:115-222's loop; aimet_amd.adaround_optimizer). */
+/* adaround_loss.py:70-80 compute_recon_loss + its autograd backward in one pass: grad[i] =
+ * d/dq of mean(||act(q) - act(t)||^2 over dim 1) = 2 (act(q) - act(t)) act'(q) / (n / reduced),
+ * where `reduced` is the size of dim 1 (channels / features) and act is 0 none, 1 ReLU,
+ * 2 ReLU6 (the layer's following activation, applied to both outputs as the reference does). */
+int aimet_adaround_recon_grad(const float* quant_out, const float* orig_out, float* grad, int64_t n, int64_t reduced,
+                              int act, void* stream);
+int aimet_adaround_backward_dev(const float* w, const float* alpha, const float* grad_wq, float* grad_alpha,
+                                int64_t outer, int64_t C, int64_t K, const float* delta_dev, const float* offset_dev,
+                                int32_t bw, const float* reg_beta_dev, float* round_loss_dev, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Blockwise (broadcast) quantization and the ONNX QcQuantizeOp                                */

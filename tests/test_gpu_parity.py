@@ -820,6 +820,24 @@ def test_update_stats_channels_many_equals_individual():
                 assert qa.getStatsHistogram(c) == qb.getStatsHistogram(c)
 
 
+@pytest.mark.parametrize("act", [None, torch.nn.ReLU(), torch.nn.ReLU6()])
+@pytest.mark.parametrize("shape", [(32, 24, 12, 12), (32, 1000), (3, 5, 7)])
+def test_recon_loss_backward_fused_vs_torch(act, shape):
+    """aimet_adaround_recon_grad (one pass) == the gradient of adaround_loss.py:70-80's
+    recon_loss(act(q), act(t)) through torch autograd, to fp32 rounding."""
+    from aimet_amd.adaround_optimizer import recon_loss, recon_loss_backward
+    g = torch.Generator(device=DEV).manual_seed(8)
+    q0 = torch.randn(*shape, device=DEV, generator=g) * 4
+    t = q0 + torch.randn(*shape, device=DEV, generator=g)
+    q0[0].view(-1)[:3] = torch.tensor([0.0, 6.0, -0.0], device=DEV)   # activation edges
+    qa = q0.clone().requires_grad_(True)
+    recon_loss_backward(qa, t, act)
+    qb = q0.clone().requires_grad_(True)
+    a, b = (act(qb), act(t)) if act is not None else (qb, t)
+    recon_loss(a, b).backward()
+    torch.testing.assert_close(qa.grad, qb.grad, rtol=2e-6, atol=1e-12)
+
+
 def test_adaround_optimizer_matches_reference_loop():
     """AdaroundOptimizer (fused soft-quant + rounding-loss kernels) follows the reference's loop
     (torch-op soft quantization + AdaroundLoss, adaround_optimizer.py:181-218) iteration for
@@ -838,8 +856,16 @@ def test_adaround_optimizer_matches_reference_loop():
     o = torch.full((24,), -128.0, device=DEV)
     params = AdaroundHyperParameters(num_iterations=120, warm_start=0.25)
     act = torch.nn.ReLU6()
+    loss_eager = torch.zeros(1, device=DEV)
     a_ours = AdaroundOptimizer.optimize_rounding(conv, inp, out, d, o, 8, 0, params, act,
-                                                 torch.Generator().manual_seed(5))
+                                                 torch.Generator().manual_seed(5), loss_eager, use_graph=False)
+    # the HIP-graph form (one captured iteration replayed): the same trajectory
+    loss_graph = torch.zeros(1, device=DEV)
+    a_graph = AdaroundOptimizer.optimize_rounding(conv, inp, out, d, o, 8, 0, params, act,
+                                                  torch.Generator().manual_seed(5), loss_graph, use_graph=True)
+    torch.testing.assert_close(a_graph.detach(), a_ours.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(loss_graph, loss_eager, rtol=1e-4, atol=1e-6)
+    assert float(loss_graph) > 0
     # the reference loop
     a_ref = init_alpha(w, d.view(-1, 1, 1, 1))
     opt = torch.optim.Adam([a_ref])
