@@ -37,6 +37,9 @@ TF_ENHANCED_OFFSET_FACTOR = 0
 TF_ENHANCED_STRIDE_FACTOR = 2
 
 _IGNORED_DTYPES = (torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64, torch.bool)
+# wrapped modules that never modify their inputs in place
+_INPUT_PRESERVING_TYPES = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d, nn.ConvTranspose2d,
+                           nn.ConvTranspose3d, nn.Linear)
 
 
 def tensor_quantizer_factory(bitwidth, round_mode, quant_scheme, use_symmetric_encodings, enabled_by_default,
@@ -282,8 +285,14 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
         """v1/qc_quantize_op.py:705-745."""
         quantized_inputs = self._quantize_activation(self.input_quantizers, list(inputs))
         shadow_params = self._quantize_dequantize_params()
-        quantized_inputs = SteGatingFuncForParameters.apply(self, *quantized_inputs)
-        quantized_inputs = [t.clone() if isinstance(t, torch.Tensor) else t for t in quantized_inputs]
+        if torch.is_grad_enabled() or not isinstance(self._module_to_wrap, _INPUT_PRESERVING_TYPES):
+            quantized_inputs = SteGatingFuncForParameters.apply(self, *quantized_inputs)
+            # the reference clones the custom Function's outputs (in-place ops on a view of them
+            # would corrupt the gradient)
+            quantized_inputs = [t.clone() if isinstance(t, torch.Tensor) else t for t in quantized_inputs]
+        # else: no autograd graph is recorded and conv / linear never write to their inputs, so the
+        # gating node is an identity and the clone (a full copy of every input activation: 23 GB
+        # per ResNet-50 bs256 forward) changes nothing
         wrapped_output = self._module_to_wrap(*quantized_inputs, **kwargs)
         self._restore_shadow_params(shadow_params)
         if not isinstance(wrapped_output, (list, tuple)):
