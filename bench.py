@@ -94,6 +94,16 @@ def collect_tensors(model, x):
     return acts, weights
 
 
+_SIDE = {}
+
+
+def _side_stream(dev):
+    """One non-blocking stream per device, created once (stream creation is not free)."""
+    if dev not in _SIDE:
+        _SIDE[dev] = torch.cuda.Stream(dev)
+    return _SIDE[dev]
+
+
 def compute_encodings(acts, weights, world):
     """compute_encodings as QuantizationSimModel does it for this workload (v1/quantsim.py:425-449):
     TF-Enhanced stats for every activation, TF-Enhanced per-channel symmetric for every weight."""
@@ -102,17 +112,23 @@ def compute_encodings(acts, weights, world):
     from aimet_amd.tensor_quantizer import AimetTensorQuantizer
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    dev = acts[0][1].device
     aq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in acts]
     wq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=w.shape[0])
           for _, w in weights]
+    # device state of all 109 quantizers from one allocation, before anything is enqueued
+    AimetTensorQuantizer._ensure_many(aq + wq, dev)
     # every activation quantizer's statistics in one launch per phase (aimet_tq_*_many);
     # with N ranks each phase's packed statistics are exchanged once (aimet_amd.distributed)
     D.sharded_update_stats(aq, [t for _, t in acts])
-    # every weight quantizer's per-channel statistics in two launches (one workgroup per channel)
-    AimetTensorQuantizer.updateStatsPerChannelMany(wq, [w for _, w in weights])
-    # getEncoding of every quantizer, batched: one device search launch + one sync per flag set
+    # the weights on a second stream (inputs resident since the synchronize above): their
+    # statistics (two launches, one workgroup per channel) and TF-E search run beside the
+    # activation passes, and the host builds the 27,560 weight encodings while those still stream
+    with torch.cuda.stream(_side_stream(dev)):
+        AimetTensorQuantizer.updateStatsPerChannelMany(wq, [w for _, w in weights])
+        # getEncoding of every quantizer, batched: one device search launch + one sync per flag set
+        w_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(wq, 8, True, False, False)]
     act_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(aq, 8, False, False, False)]
-    w_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(wq, 8, True, False, False)]
     torch.cuda.synchronize()
     return act_enc, w_enc, time.perf_counter() - t0, aq, wq
 
