@@ -1,0 +1,61 @@
+"""One calibration pass over tensors that are already resident in HBM: every quantizer's statistics
+and encodings with a handful of launches and two stream synchronisations.
+
+This is QuantizationSimModel.compute_encodings' work (v1/quantsim.py:381-449: updateStats of every
+activation quantizer for the batch, then getEncoding of every activation and parameter quantizer)
+for callers that hold the activations and parameters themselves (a captured forward, a serving
+stack, bench.py), scheduled for the MI355X:
+
+* activations: one launch per phase for all per-tensor quantizers (aimet_tq_*_many), sharded across
+  ranks with one packed collective per phase when a process group is given (aimet_amd.distributed);
+* parameters: on a second stream, per-channel statistics in two launches (one workgroup per
+  channel), the TF-Enhanced / MSE searches in one launch, and the host building the parameter
+  encodings while the activation passes still stream;
+* activation encodings: one search launch + one synchronisation.
+"""
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+
+from aimet_amd import distributed as D
+from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+
+_SIDE = {}
+
+
+def _side_stream(dev: torch.device) -> torch.cuda.Stream:
+    """One non-blocking stream per device, created once (stream creation is not free)."""
+    key = dev.index if dev.index is not None else torch.cuda.current_device()
+    if key not in _SIDE:
+        _SIDE[key] = torch.cuda.Stream(torch.device("cuda", key))
+    return _SIDE[key]
+
+
+def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], activations: Sequence[torch.Tensor],
+                               param_quantizers: Sequence[AimetTensorQuantizer], params: Sequence[torch.Tensor],
+                               act_settings: Tuple[int, bool, bool, bool] = (8, False, False, False),
+                               param_settings: Tuple[int, bool, bool, bool] = (8, True, False, False),
+                               param_ch_axes: Optional[Sequence[int]] = None, group=None
+                               ) -> Tuple[List, List]:
+    """Statistics + encodings of every quantizer for one batch.
+
+    act_quantizers[i] (per-tensor) sees activations[i] (this rank's shard when `group` spans several
+    ranks); param_quantizers[j] (per-tensor or per-channel along param_ch_axes[j]) sees params[j]
+    (replicated). *_settings = (bitwidth, symmetric, strict symmetric, unsigned symmetric).
+    Returns ([(encoding, valid)] of the activations, [(encodings, valid)] of the parameters)."""
+    if not activations and not params:
+        return [], []
+    dev = (activations[0] if activations else params[0]).device
+    torch.cuda.synchronize(dev)   # inputs produced on any stream are complete
+    AimetTensorQuantizer._ensure_many(list(act_quantizers) + list(param_quantizers), dev)
+    if act_quantizers:
+        D.sharded_update_stats(list(act_quantizers), list(activations), group=group)
+    p_res = []
+    if param_quantizers:
+        with torch.cuda.stream(_side_stream(dev)):
+            keep = AimetTensorQuantizer.updateStatsPerChannelMany(param_quantizers, params, param_ch_axes)
+            p_res = AimetTensorQuantizer.getEncodings(param_quantizers, *param_settings)   # syncs the side stream
+            del keep
+    a_res = AimetTensorQuantizer.getEncodings(act_quantizers, *act_settings) if act_quantizers else []
+    torch.cuda.synchronize(dev)
+    return a_res, p_res

@@ -94,42 +94,24 @@ def collect_tensors(model, x):
     return acts, weights
 
 
-_SIDE = {}
-
-
-def _side_stream(dev):
-    """One non-blocking stream per device, created once (stream creation is not free)."""
-    if dev not in _SIDE:
-        _SIDE[dev] = torch.cuda.Stream(dev)
-    return _SIDE[dev]
-
-
-def compute_encodings(acts, weights, world):
+def compute_encodings(acts, weights):
     """compute_encodings as QuantizationSimModel does it for this workload (v1/quantsim.py:425-449):
     TF-Enhanced stats for every activation, TF-Enhanced per-channel symmetric for every weight."""
-    from aimet_amd import distributed as D
+    from aimet_amd.calibration import compute_encodings_resident
     from aimet_amd.libpymo import QuantizationMode
     from aimet_amd.tensor_quantizer import AimetTensorQuantizer
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    dev = acts[0][1].device
     aq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in acts]
     wq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=w.shape[0])
           for _, w in weights]
-    # device state of all 109 quantizers from one allocation, before anything is enqueued
-    AimetTensorQuantizer._ensure_many(aq + wq, dev)
-    # every activation quantizer's statistics in one launch per phase (aimet_tq_*_many);
-    # with N ranks each phase's packed statistics are exchanged once (aimet_amd.distributed)
-    D.sharded_update_stats(aq, [t for _, t in acts])
-    # the weights on a second stream (inputs resident since the synchronize above): their
-    # statistics (two launches, one workgroup per channel) and TF-E search run beside the
-    # activation passes, and the host builds the 27,560 weight encodings while those still stream
-    with torch.cuda.stream(_side_stream(dev)):
-        AimetTensorQuantizer.updateStatsPerChannelMany(wq, [w for _, w in weights])
-        # getEncoding of every quantizer, batched: one device search launch + one sync per flag set
-        w_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(wq, 8, True, False, False)]
-    act_enc = [e for e, _ in AimetTensorQuantizer.getEncodings(aq, 8, False, False, False)]
-    torch.cuda.synchronize()
+    # activations (sharded across ranks, one packed collective per phase) and per-channel weights
+    # on a second stream: aimet_amd.calibration
+    a_res, w_res = compute_encodings_resident(aq, [t for _, t in acts], wq, [w for _, w in weights],
+                                              act_settings=(8, False, False, False),
+                                              param_settings=(8, True, False, False))
+    act_enc = [e for e, _ in a_res]
+    w_enc = [e for e, _ in w_res]
     return act_enc, w_enc, time.perf_counter() - t0, aq, wq
 
 
@@ -222,11 +204,11 @@ def main():
     # compute_encodings wall-clock: the first call (cold: code objects load, pools grow) and the
     # median of --enc-reps further calls on fresh quantizers (what a calibration costs in a warm
     # process); the encodings of the last call are used
-    act_enc, w_enc, enc_cold, aq, wq = compute_encodings(acts, weights, world)
+    act_enc, w_enc, enc_cold, aq, wq = compute_encodings(acts, weights)
     warm = []
     for _ in range(args.enc_reps):
         del aq, wq
-        act_enc, w_enc, secs, aq, wq = compute_encodings(acts, weights, world)
+        act_enc, w_enc, secs, aq, wq = compute_encodings(acts, weights)
         warm.append(secs)
     enc_seconds = sorted(warm)[len(warm) // 2] if warm else enc_cold
 

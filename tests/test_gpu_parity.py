@@ -916,3 +916,27 @@ def test_create_many_shared_state_lifetime():
     shared = None
     gc.collect()
     torch.cuda.synchronize()
+
+
+def test_compute_encodings_resident_equals_individual():
+    """aimet_amd.calibration.compute_encodings_resident (batched activation statistics, parameter
+    statistics + searches on a second stream) == updateStats / getEncoding quantizer by quantizer."""
+    from aimet_amd.calibration import compute_encodings_resident
+    g = torch.Generator(device=DEV).manual_seed(14)
+    acts = [torch.relu(torch.randn(n, device=DEV, generator=g) * (1 + i)) for i, n in
+            enumerate((1 << 20, 3000, 77777, 1 << 18))]
+    params = [torch.randn(c, k, device=DEV, generator=g) * 0.05 for c, k in ((64, 27), (128, 576), (10, 2048))]
+    TFE = QuantizationMode.QUANTIZATION_TF_ENHANCED
+    aq = [AimetTensorQuantizer(TFE) for _ in acts]
+    pq = [AimetTensorQuantizer(TFE, num_channels=p.shape[0]) for p in params]
+    a_res, p_res = compute_encodings_resident(aq, acts, pq, params)
+    for t, (e, v) in zip(acts, a_res):
+        q = AimetTensorQuantizer(TFE)
+        q.updateStats(t, True)
+        e1, v1 = q.getEncoding(8, False, False, False)
+        assert v and v1 and e.to_tuple() == e1.to_tuple()
+    for p, (es, v) in zip(params, p_res):
+        q = AimetTensorQuantizer(TFE, num_channels=p.shape[0])
+        q.updateStatsPerChannel(p, 0, True)
+        e1, v1 = q.getEncoding(8, True, False, False)
+        assert v and v1 and [e.to_tuple() for e in es] == [e.to_tuple() for e in e1]

@@ -62,7 +62,7 @@ def main():
               "total %.2f ms" % (sum(t.values()) * 1e3), flush=True)
         del aq, wq
     for rep in range(4):
-        *_, secs, aq, wq = bench.compute_encodings(acts, weights, 1)
+        *_, secs, aq, wq = bench.compute_encodings(acts, weights)
         del aq, wq
         print("bench.compute_encodings rep %d: %.2f ms" % (rep, secs * 1e3), flush=True)
 
