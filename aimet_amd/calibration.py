@@ -24,10 +24,14 @@ _SIDE = {}
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
-    """One non-blocking stream per device, created once (stream creation is not free)."""
+    """One high-priority stream per device, created once (stream creation is not free). The
+    parameters' short statistics launches and their compute-bound encoding search run on it: at high
+    priority their workgroups are dispatched ahead of the HBM-bound activation passes queued on the
+    main stream, so the parameter encodings are ready (and built on the host) while the activation
+    passes still stream."""
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(torch.device("cuda", key))
+        _SIDE[key] = torch.cuda.Stream(torch.device("cuda", key), priority=-1)
     return _SIDE[key]
 
 
@@ -48,14 +52,18 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
     dev = (activations[0] if activations else params[0]).device
     torch.cuda.synchronize(dev)   # inputs produced on any stream are complete
     AimetTensorQuantizer._ensure_many(list(act_quantizers) + list(param_quantizers), dev)
+    side = _side_stream(dev)
+    keep, p_res = None, []
+    if param_quantizers:
+        # enqueued first: the parameters' statistics take the CUs before the activation passes
+        with torch.cuda.stream(side):
+            keep = AimetTensorQuantizer.updateStatsPerChannelMany(param_quantizers, params, param_ch_axes)
     if act_quantizers:
         D.sharded_update_stats(list(act_quantizers), list(activations), group=group)
-    p_res = []
     if param_quantizers:
-        with torch.cuda.stream(_side_stream(dev)):
-            keep = AimetTensorQuantizer.updateStatsPerChannelMany(param_quantizers, params, param_ch_axes)
+        with torch.cuda.stream(side):
             p_res = AimetTensorQuantizer.getEncodings(param_quantizers, *param_settings)   # syncs the side stream
-            del keep
+        del keep
     a_res = AimetTensorQuantizer.getEncodings(act_quantizers, *act_settings) if act_quantizers else []
     torch.cuda.synchronize(dev)
     return a_res, p_res

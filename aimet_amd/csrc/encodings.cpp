@@ -220,21 +220,28 @@ aimet_tf_encoding tfe_encoding(const HistView& h, int32_t bw, bool sym, bool str
     else
         tfe::fseq_asym(fseq);
     // the per-channel bin tables every candidate shares (tfe_core.hpp, as the device builds them)
-    double cd[tfe::kBins];
     float cf[tfe::kBins];
-    short nz[tfe::kBins];
+    double pdf_c[tfe::kBins], cd_c[tfe::kBins];
+    float cf_c[tfe::kBins];
+    short pos[tfe::kBins];
     const float start = tfe::bins_start(th);
     const double step = tfe::bins_step(th);
     const bool skip   = tfe::bins_skip_empty(th);
     int nnz           = 0;
     for (int i = 0; i < tfe::kBins; ++i)
     {
-        cd[i] = tfe::bin_centre(start, step, i);
-        cf[i] = (float) cd[i];
+        const double cd = tfe::bin_centre(start, step, i);
+        cf[i]           = (float) cd;
+        pos[i]          = (short) nnz;
         if (h.pdf[i] > 0 || !skip)
-            nz[nnz++] = (short) i;
+        {
+            pdf_c[nnz] = h.pdf[i];
+            cd_c[nnz]  = cd;
+            cf_c[nnz]  = cf[i];
+            ++nnz;
+        }
     }
-    const tfe::Bins B {start, step, h.pdf, cd, cf, nz, nnz};
+    const tfe::Bins B {start, step, cf, pdf_c, cd_c, cf_c, pos, nnz};
     float bestDelta = -1;
     int bestOffset  = -1;
     double best     = std::numeric_limits<double>::max();
@@ -244,7 +251,7 @@ aimet_tf_encoding tfe_encoding(const HistView& h, int32_t bw, bool sym, bool str
         int o;
         if (!tfe::candidate(st, fseq, t, d, o))
             continue;
-        double c = tfe::cost(B, bw, d, o);
+        double c = sym ? tfe::cost<true>(B, bw, d, o) : tfe::cost<false>(B, bw, d, o);
         if (c < best)
         {
             best       = c;

@@ -187,7 +187,9 @@ AIMET_HD inline bool candidate(const Setup& s, const float* fseq, int t, float& 
 // Per-channel precomputation shared by every candidate of _quantAndSatCost (:293-355):
 //   cd[i] = start + i*step + step/2 (double, the bin centre as the reference evaluates it)
 //   cf[i] = (float) cd[i]            (loMid / hiMid / the quantised value v)
-//   nz[0..nnz) = the bins the cost loops must visit, ascending.
+// and, over the bins the cost loops must visit (ascending bin index, k = 0..nnz):
+//   pdf_c[k], cd_c[k], cf_c[k]       (the visited bins' pdf and centres, compacted)
+//   pos[i] = number of visited bins with index < i   (i = 0..kBins-1)
 // A bin whose pdf is 0 adds exactly +0.0 to its sum as long as its squared distance is finite,
 // so such bins are skipped when the histogram range is bounded (|x| <= 1e30 keeps every
 // distance finite); otherwise every bin is visited, as in the reference.
@@ -195,10 +197,11 @@ struct Bins
 {
     float start;
     double step;
-    const double* pdf;
-    const double* cd;
     const float* cf;
-    const short* nz;
+    const double* pdf_c;
+    const double* cd_c;
+    const float* cf_c;
+    const short* pos;
     int nnz;
 };
 
@@ -239,8 +242,13 @@ AIMET_HD inline int quant_code(float v, float delta, int offset, float rcp, floa
     return (int) roundf(v / delta - offset);
 }
 
-// _quantAndSatCost (:293-355) over the prepared bins. The three sums keep the reference's
-// ascending order; a bin can belong to more than one of them exactly as in the reference loops.
+// _quantAndSatCost (:293-355) over the prepared bins. The reference's three loops are kept as
+// three loops, each over its own contiguous range of visited bins (i < iLo, i >= iHi,
+// iLo <= i < iHi) in ascending order, so every sum adds the same terms in the same order; a bin
+// can belong to both saturation ranges exactly as in the reference. `split` picks between running
+// them as three loops (the lanes of a wave, one candidate each, run branch-free bodies: the
+// symmetric grid, whose candidates' ranges nest) or as one guarded loop; both give identical sums.
+template <bool split>
 AIMET_HD inline double cost(const Bins& B, int bw, float delta, int offset)
 {
     const float lo    = delta * offset;
@@ -256,29 +264,54 @@ AIMET_HD inline double cost(const Bins& B, int bw, float delta, int offset)
     const float rcp = 1.0f / delta;
     const float vmax = (loMid != loMid || hiMid != hiMid) ? NAN : smax(fabsf(loMid), fabsf(hiMid));   // NaN: exact path
     const float thr  = (vmax * rcp + fabsf((float) offset) + 1.0f) * 4.76837158203125e-7f;
+    const int kLo = B.pos[iLo];   // visited bins below iLo: k in [0, kLo)
+    const int kHi = B.pos[iHi];   // visited bins at or above iHi: k in [kHi, nnz)
     double satLo = 0, satHi = 0, quant = 0;
-    for (int k = 0; k < B.nnz; ++k)
+    if constexpr (!split)
     {
-        const int i    = B.nz[k];
-        const double p = B.pdf[i];
-        if (i < iLo)
+        // one pass with the three bodies guarded: the lanes of a wave share each bin's loads,
+        // which wins when their candidates' ranges differ widely (the asymmetric grid)
+        for (int k = 0; k < B.nnz; ++k)
         {
-            double d = B.cd[i] - loMid;
-            satLo += p * (d * d);
+            if (k < kLo)
+            {
+                double d = B.cd_c[k] - loMid;
+                satLo += B.pdf_c[k] * (d * d);
+            }
+            if (k >= kHi)
+            {
+                double d = B.cd_c[k] - hiMid;
+                satHi += B.pdf_c[k] * (d * d);
+            }
+            if (k >= kLo && k < kHi)
+            {
+                float v   = B.cf_c[k];
+                int q     = quant_code(v, delta, offset, rcp, thr);
+                float deq = delta * (q + offset);
+                double d  = (double) (v - deq);
+                quant += B.pdf_c[k] * (d * d);
+            }
         }
-        if (i >= iHi)
-        {
-            double d = B.cd[i] - hiMid;
-            satHi += p * (d * d);
-        }
-        if (i >= iLo && i < iHi)
-        {
-            float v   = B.cf[i];
-            int q     = quant_code(v, delta, offset, rcp, thr);
-            float deq = delta * (q + offset);
-            double d  = (double) (v - deq);
-            quant += p * (d * d);
-        }
+        double c = kGamma * (satLo + satHi) + quant;
+        return smin(c, DBL_MAX);
+    }
+    for (int k = 0; k < kLo; ++k)
+    {
+        double d = B.cd_c[k] - loMid;
+        satLo += B.pdf_c[k] * (d * d);
+    }
+    for (int k = kHi; k < B.nnz; ++k)
+    {
+        double d = B.cd_c[k] - hiMid;
+        satHi += B.pdf_c[k] * (d * d);
+    }
+    for (int k = kLo; k < kHi; ++k)   // empty unless iLo < iHi
+    {
+        float v   = B.cf_c[k];
+        int q     = quant_code(v, delta, offset, rcp, thr);
+        float deq = delta * (q + offset);
+        double d  = (double) (v - deq);
+        quant += B.pdf_c[k] * (d * d);
     }
     double c = kGamma * (satLo + satHi) + quant;
     return smin(c, DBL_MAX);

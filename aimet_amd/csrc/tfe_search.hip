@@ -49,14 +49,15 @@ struct TfeJob
 };
 
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK) void tfe_search_kernel(TfeJob one, const TfeJob* __restrict__ jobs, int njobs,
+__global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 6 : 7) void tfe_search_kernel(TfeJob one, const TfeJob* __restrict__ jobs, int njobs,
                                                            int64_t total, int bw, int sym, int strict, int unsign)
 {
     constexpr int kW = BLOCK / 64;
-    __shared__ double pdf[tfe::kBins];
-    __shared__ double cd[tfe::kBins];
+    __shared__ double pdf_c[tfe::kBins];
+    __shared__ double cd_c[tfe::kBins];
+    __shared__ float cf_c[tfe::kBins];
     __shared__ float cf[tfe::kBins];
-    __shared__ short nz[tfe::kBins];
+    __shared__ short pos[tfe::kBins];
     __shared__ float fseq[tfe::kSymF + 8];
     __shared__ int first, last, nnz;
     __shared__ Best wbest[kW];
@@ -104,28 +105,35 @@ __global__ __launch_bounds__(BLOCK) void tfe_search_kernel(TfeJob one, const Tfe
         tfe::Hist h {j.hist_min[c], j.bucket_size[c], nullptr};
         const float start = tfe::bins_start(h);
         const double step = tfe::bins_step(h);
-        for (int i = threadIdx.x; i < tfe::kBins; i += BLOCK)
-        {
-            pdf[i]   = j.pdf[c * tfe::kBins + i];
-            double m = tfe::bin_centre(start, step, i);
-            cd[i]    = m;
-            cf[i]    = (float) m;
-        }
+        for (int i = threadIdx.x; i < tfe::kBins; i += BLOCK)   // staged by every wave
+            pdf_c[i] = j.pdf[c * tfe::kBins + i];
         __syncthreads();
         if (threadIdx.x < 64)
         {
-            // ascending compaction of the bins the cost must visit + first/last non-empty bins
+            // ascending compaction of the bins the cost must visit (pdf and centres gathered
+            // into k order, pos[i] = visited bins below i) + first/last non-empty bins. In place:
+            // chunk r is read before any of its lanes writes, and every write goes to k <= i.
             const bool skip = tfe::bins_skip_empty(h);
+            const unsigned long long below = (1ull << lane) - 1;
             int base = 0, fst = -1, lst = -1;
             for (int i0 = 0; i0 < tfe::kBins; i0 += 64)
             {
                 const int i          = i0 + lane;
-                const bool occupied  = pdf[i] > 0;
+                const double pi      = pdf_c[i];
+                const double m_c     = tfe::bin_centre(start, step, i);
+                const bool occupied  = pi > 0;
                 const bool visit     = occupied || !skip;
                 unsigned long long m = __ballot(visit);
                 unsigned long long o = __ballot(occupied);
+                const int k          = base + __popcll(m & below);
+                cf[i]                = (float) m_c;
+                pos[i]               = (short) k;
                 if (visit)
-                    nz[base + __popcll(m & ((1ull << lane) - 1))] = (short) i;
+                {
+                    pdf_c[k] = pi;
+                    cd_c[k]  = m_c;
+                    cf_c[k]  = (float) m_c;
+                }
                 base += __popcll(m);
                 if (o)
                 {
@@ -142,11 +150,10 @@ __global__ __launch_bounds__(BLOCK) void tfe_search_kernel(TfeJob one, const Tfe
             }
         }
         __syncthreads();
-        h.pdf = pdf;
         float lo, hi;
         tfe::observed_range(h, first, last, lo, hi);
         tfe::Setup st = tfe::setup(lo, hi, bw, sym != 0, strict != 0, unsign != 0);
-        const tfe::Bins B {start, step, pdf, cd, cf, nz, nnz};
+        const tfe::Bins B {start, step, cf, pdf_c, cd_c, cf_c, pos, nnz};
 
         Best b {0.0, -1, -1.0f, -1};
         for (int t = threadIdx.x; t < st.ncand; t += BLOCK)
@@ -155,7 +162,7 @@ __global__ __launch_bounds__(BLOCK) void tfe_search_kernel(TfeJob one, const Tfe
             int o;
             if (!tfe::candidate(st, fseq, t, dl, o))
                 continue;
-            double cst = tfe::cost(B, bw, dl, o);
+            double cst = tfe::cost<BLOCK == 128>(B, bw, dl, o);
             if (!(cst < DBL_MAX))
                 continue;
             Best me {cst, t, dl, o};

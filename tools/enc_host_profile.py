@@ -32,11 +32,12 @@ def one(acts, weights, dev):
     mark("sync_in")
     AimetTensorQuantizer._ensure_many(aq + wq, dev)
     mark("create_many")
+    with torch.cuda.stream(CAL._side_stream(dev)):
+        keep = AimetTensorQuantizer.updateStatsPerChannelMany(wq, weights)
+    mark("w_update_launch")
     D.sharded_update_stats(aq, acts)
     mark("act_update_launch")
     with torch.cuda.stream(CAL._side_stream(dev)):
-        keep = AimetTensorQuantizer.updateStatsPerChannelMany(wq, weights)
-        mark("w_update_launch")
         p = AimetTensorQuantizer.getEncodings(wq, 8, True, False, False)
         mark("w_getencs(sync side)")
         del keep
