@@ -15,6 +15,7 @@
 //   Entropy                        EntropyEncodingAnalyzer.cpp:97-435, math_functions.cpp:562-641
 #include "encodings.hpp"
 #include "entropy_core.hpp"
+#include "entropy_kl.hpp"
 #include "mse_core.hpp"
 #include "tfe_core.hpp"
 
@@ -318,185 +319,37 @@ std::pair<float, float> mse_range(const HistView& h, int32_t bw, bool sym, bool 
 }
 
 // ---- Entropy: KL-divergence range search over the TensorProfilingParams histogram -------------
-// The search stays on the host: the argmin over windows compares sums of p*log(p/q) and the
-// reference's glibc log is what decides near-ties (the device log differs in the last ulp).
-// The reference's std::accumulate(..., 0.f) sums run in FLOAT; they are restated as such.
-double accumulate_f(const double* p, size_t n)
+// _optimizeKL (EntropyEncodingAnalyzer.cpp:226-435) with the arithmetic of entropy_kl.hpp (shared
+// with the device search, entropy_search.hip) and glibc's log, which is what decides near-ties.
+double glibc_log(double v)
 {
-    float acc = 0.f;
-    for (size_t i = 0; i < n; ++i)
-        acc = (float) ((double) acc + p[i]);
-    return acc;
+    return std::log(v);
 }
 
-// rescaleHistogram (math_functions.cpp:562-641), non-empty source
-void rescale_histogram(const double* src, double srcMin, double srcMax, double dstMin, double dstMax, double* dst)
-{
-    if (srcMin == dstMin && srcMax == dstMax)
-    {
-        std::copy(src, src + kPdfSize, dst);
-        return;
-    }
-    const size_t n      = kPdfSize;
-    const double srcW   = (srcMax - srcMin) / (double) n;
-    const double dstW   = (dstMax - dstMin) / (double) n;
-    std::fill(dst, dst + n, 0.0);
-    for (size_t b = 0; b < n; ++b)
-    {
-        const double v = src[b];
-        if (v == 0)
-            continue;
-        const double s0 = srcMin + (double) b * srcW;
-        const double s1 = srcMin + (double) (b + 1) * srcW;
-        size_t d0 = (size_t) entropy::x86_d2u64(std::max(std::floor((s0 - dstMin) / dstW), 0.0));
-        size_t d1 = (size_t) entropy::x86_d2u64(std::max(std::ceil((s1 - dstMin) / dstW), 0.0));
-        d0        = std::min(d0, n - 1);
-        d1        = std::min(d1, n - 1);
-        double rem = v;
-        for (size_t k = d0; k <= d1; ++k)
-        {
-            const double o0 = std::max(s0, dstMin + (double) k * dstW);
-            const double o1 = std::min(s1, dstMin + (double) (k + 1) * dstW);
-            double ratio    = (o1 - o0) / srcW;
-            ratio           = ratio >= 0.0f ? ratio : 0.0f;
-            ratio           = ratio <= 1.0f ? ratio : 1.0f;
-            double part     = std::round(ratio * v);
-            part            = part <= rem ? part : rem;
-            dst[k] += part;
-            rem -= part;
-        }
-    }
-}
-
-// _conditionHistogram (EntropyEncodingAnalyzer.cpp:156-198)
-void condition(double* h, size_t n)
-{
-    const double epsZero = 0.0001;
-    size_t zeros         = 0;
-    for (size_t i = 0; i < n; ++i)
-        zeros += (h[i] == 0.f);
-    if (zeros == n)
-        return;
-    const double epsNonZero = epsZero * (double) zeros / (double) (n - zeros);
-    if (epsNonZero >= 1.0)
-        return;
-    for (size_t i = 0; i < n; ++i)
-    {
-        const int z = (h[i] == 0.f);
-        h[i] += epsZero * z;
-        h[i] -= epsNonZero * (1 - z);
-    }
-}
-
-// _computeKL (EntropyEncodingAnalyzer.cpp:200-224); P and Q are normalised in place
-double kl_divergence(double* P, double* Q, size_t n)
-{
-    const double sP = accumulate_f(P, n), sQ = accumulate_f(Q, n);
-    double dv       = 0;
-    for (size_t i = 0; i < n; ++i)
-    {
-        P[i] /= sP;
-        Q[i] /= sQ;
-        if (P[i] > 0 && Q[i] > 0)
-            dv += P[i] * std::log(P[i] / Q[i]);
-    }
-    return dv;
-}
-
-// _optimizeKL (EntropyEncodingAnalyzer.cpp:226-435): shrink a window over the 512 bins -- both
-// ends at once for symmetric encodings, else the end(s) losing the least mass while keeping 0 in
-// range -- and keep the window whose 255-level requantization Q is closest to the saturated P.
 std::pair<float, float> kl_range(double tmin, double tmax, const double* tpp_hist, int32_t bw, bool sym, bool strict,
                                  bool unsign)
 {
-    double lo = tmin, hi = tmax;
     double hist[kPdfSize];
-    if (sym && (lo < 0.0 || !unsign))
-    {
-        const float amax = (float) std::max(std::fabs(hi), std::fabs(lo));
-        const float amin = -amax;
-        rescale_histogram(tpp_hist, lo, hi, amin, amax, hist);
-        lo = amin;
-        hi = amax;
-    }
-    else
-        std::copy(tpp_hist, tpp_hist + kPdfSize, hist);
-    constexpr size_t kN = kPdfSize, kLevels = 255;
+    double lo, hi;
+    entropy::kl_histogram(tmin, tmax, tpp_hist, sym, unsign, hist, lo, hi);
     if (bw != 8)
         return {(float) lo, (float) hi};
-    const double w = (hi - lo) / (double) kN;
-    double best    = std::numeric_limits<double>::infinity();
+    const double w = (hi - lo) / (double) kPdfSize;
+    short wa[entropy::kWindows], wb[entropy::kWindows];
+    const int n   = entropy::windows(hist, lo, w, sym || strict, wa, wb);
+    double best   = std::numeric_limits<double>::infinity();
     double bestLo = lo, bestHi = hi;
-    double P[kPdfSize], Q[kPdfSize];
-    size_t a = 0, b = kN - 1;   // window [a, b], inclusive
-    while (b - a + 1 >= kLevels)
+    for (int k = 0; k < n; ++k)
     {
-        const size_t win  = b - a + 1;
-        const double* hw  = hist + a;
-        double left = 0, right = 0;
-        for (size_t i = 0; i <= a; ++i)
-            left += hist[i];
-        for (size_t i = b; i < kN; ++i)
-            right += hist[i];
-        P[0] = 0;
-        for (size_t i = 1; i + 1 < win; ++i)
-            P[i] = hw[i];
-        P[win - 1] = 0;
-        P[0] += left;
-        P[win - 1] += right;
-        std::fill(Q, Q + win, 0.0);
-        const double merged = (double) win / (double) kLevels;
-        for (size_t q = 0; q < kLevels; ++q)
-        {
-            const size_t i0 = (size_t) std::ceil((double) q * merged);
-            const size_t i1 = q < kLevels - 1 ? (size_t) std::ceil((double) (q + 1) * merged) : win;
-            double sum = 0, norm = 0;
-            for (size_t i = i0; i < i1; ++i)
-            {
-                sum += hw[i];
-                norm += (hw[i] != 0);
-            }
-            if (norm != 0)
-                for (size_t i = i0; i < i1; ++i)
-                    if (hw[i] != 0)
-                        Q[i] = sum / norm;
-        }
-        if (accumulate_f(P, win) == 0 || accumulate_f(Q, win) == 0)
+        const entropy::WindowKl r = entropy::window_kl(hist, wa[k], wb[k], glibc_log);
+        if (r.brk)
             break;
-        condition(P, win);
-        condition(Q, win);
-        const double dv = kl_divergence(P, Q, win);
-        if (dv < best)
+        if (r.dv < best)
         {
-            best   = dv;
-            bestLo = lo + (double) a * w;
-            bestHi = lo + (double) (b + 1) * w;
+            best   = r.dv;
+            bestLo = lo + (double) wa[k] * w;
+            bestHi = lo + (double) (wb[k] + 1) * w;
         }
-        if (sym || strict)
-        {
-            ++a;
-            --b;
-            continue;
-        }
-        const double loss[3] = {hist[a] + hist[b], hist[a] + hist[a + 1], hist[b] + hist[b - 1]};
-        int k = 0;   // std::min_element: the first minimum
-        if (loss[1] < loss[k])
-            k = 1;
-        if (loss[2] < loss[k])
-            k = 2;
-        if ((k == 0 && lo + (double) (a + 1) * w > 0) || (k == 1 && lo + (double) (a + 2) * w > 0))
-            k = 2;   // keep 0 representable: only shrink from the right
-        else if ((k == 0 && lo + (double) b * w < 0) || (k == 2 && lo + (double) (b - 1) * w < 0))
-            k = 1;   // ... or only from the left
-        if (k == 0)
-        {
-            ++a;
-            --b;
-        }
-        else if (k == 1)
-            a += 2;
-        else
-            b -= 2;
     }
     return {(float) bestLo, (float) bestHi};
 }
@@ -512,8 +365,13 @@ aimet_tf_encoding entropy_encoding(bool has_hist, bool stats_updated, double tmi
     if (!has_hist)
         return unseen_or_zero(stats_updated, bw, steps);
     std::pair<float, float> r = kl_range(tmin, tmax, hist, bw, sym, strict, unsign);
-    float lo = std::min(r.first, 0.0f);
-    float hi = std::max(r.second, 0.0f);
+    return entropy_encoding_from_range(r.first, r.second, bw, sym, strict, unsign);
+}
+
+aimet_tf_encoding entropy_encoding_from_range(float kl_lo, float kl_hi, int32_t bw, bool sym, bool strict, bool unsign)
+{
+    float lo = std::min(kl_lo, 0.0f);
+    float hi = std::max(kl_hi, 0.0f);
     return computed_encoding(bw, lo, hi, sym, strict, unsign);
 }
 

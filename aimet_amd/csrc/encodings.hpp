@@ -22,6 +22,8 @@ aimet_tf_encoding histogram_encoding(int scheme, bool initialized, bool stats_up
 // EntropyEncodingAnalyzer::computeEncoding from the TensorProfilingParams (min, max, 512 counts)
 aimet_tf_encoding entropy_encoding(bool has_hist, bool stats_updated, double tmin, double tmax, const double* hist,
                                    int32_t bw, bool sym, bool strict, bool unsign);
+// the tail of entropy_encoding for a _optimizeKL range found elsewhere (entropy_search.hip)
+aimet_tf_encoding entropy_encoding_from_range(float kl_lo, float kl_hi, int32_t bw, bool sym, bool strict, bool unsign);
 void histogram_xleft(float hist_min, double bucket_size, double* xleft);
 
 }   // namespace aimet_amd

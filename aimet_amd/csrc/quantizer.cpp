@@ -540,9 +540,22 @@ bool device_search(const aimet_tensor_quantizer* q)
     return q->hist && (q->scheme == AIMET_QUANTIZATION_TF_ENHANCED || q->scheme == AIMET_QUANTIZATION_MSE);
 }
 
-// getEncoding, part 1: enqueue the device-side search (TF-Enhanced) on the stream.
+// the entropy KL search runs on the device for 8-bit encodings (the only width _optimizeKL
+// searches; other widths take the histogram range as it is)
+bool entropy_device(const aimet_tensor_quantizer* q, int32_t b)
+{
+    return q->kind == kKindEntropy && b == 8;
+}
+
+// getEncoding, part 1: enqueue the device-side search (TF-Enhanced, MSE, entropy) on the stream.
 void launch_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict, int unsign, hipStream_t s)
 {
+    if (entropy_device(q, b))
+    {
+        const TqDevice* d = &q->d;
+        launch_entropy_search_many(&d, &q->C, 1, sym != 0, strict != 0, unsign != 0, s);
+        return;
+    }
     if (!device_search(q))
         return;
     if (q->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
@@ -561,13 +574,29 @@ struct HostStats
     std::vector<double> acc, bsz, pdf;
     std::vector<int32_t> init;
     std::vector<float> hmin;
+    std::vector<EntropyRange> ent;   // device KL ranges (entropy, 8 bit)
+    bool host_search = false;        // some channel still needs the host KL search
 };
 
-bool fetch_stats(aimet_tensor_quantizer* q, aimet_tf_encoding* out, HostStats& h)
+bool fetch_stats(aimet_tensor_quantizer* q, int32_t b, aimet_tf_encoding* out, HostStats& h)
 {
     const int64_t C = q->C;
     h.q   = q;
     h.out = out;
+    if (entropy_device(q, b))
+    {
+        h.ent = d2h(entropy_ranges(q->d), C);
+        for (const EntropyRange& r: h.ent)
+            h.host_search = h.host_search || r.status == kEntHost;
+        if (h.host_search)
+        {
+            // near-ties (or non-finite ranges) on some channel: its statistics for the glibc search
+            h.init = d2h(q->d.pdf_init, C);
+            h.pdf  = d2h(q->d.pdf, (size_t) kPdfSize * C);
+            h.acc  = d2h(q->d.acc, 2 * C);
+        }
+        return true;
+    }
     if (!q->hist)
     {
         h.acc = d2h(q->d.acc, 2 * C);
@@ -597,6 +626,10 @@ void host_encoding(const HostStats& h, int64_t c, int32_t b, int sym, int strict
     const aimet_tensor_quantizer* q = h.q;
     if (!q->hist)
         h.out[c] = tf_encoding(h.acc[2 * c], h.acc[2 * c + 1], b, sym, strict, unsign);
+    else if (!h.ent.empty() && h.ent[(size_t) c].status != kEntHost)
+        h.out[c] = h.ent[(size_t) c].status == kEntFinal
+                       ? entropy_encoding_from_range(h.ent[(size_t) c].lo, h.ent[(size_t) c].hi, b, sym, strict, unsign)
+                       : entropy_encoding(false, true, 0.0, 0.0, nullptr, b, sym, strict, unsign);
     else if (q->kind == kKindEntropy)
         h.out[c] = entropy_encoding(h.init[c] != 0, true, h.acc[2 * c], h.acc[2 * c + 1], h.pdf.data() + kPdfSize * c,
                                     b, sym, strict, unsign);
@@ -615,14 +648,14 @@ void collect_encodings(aimet_tensor_quantizer* const* qs, aimet_tf_encoding* con
     for (int64_t i = 0; i < n; ++i)
     {
         HostStats h;
-        if (fetch_stats(qs[i], outs[i], h))
+        if (fetch_stats(qs[i], b, outs[i], h))
             hs.push_back(std::move(h));
     }
     std::vector<std::pair<int32_t, int64_t>> tasks;
-    bool costly = false;   // the entropy KL search: ~3 ms per channel, worth a thread each
+    bool costly = false;   // the host entropy KL search: ~3 ms per channel, worth a thread each
     for (size_t k = 0; k < hs.size(); ++k)
     {
-        costly = costly || hs[k].q->kind == kKindEntropy;
+        costly = costly || (hs[k].q->kind == kKindEntropy && (hs[k].ent.empty() || hs[k].host_search));
         for (int64_t c = 0; c < hs[k].q->C; ++c)
             tasks.emplace_back((int32_t) k, c);
     }
@@ -694,9 +727,22 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
             }
             off += qs[i]->C;
         }
-        for (int64_t i = 0; i < nq; ++i)   // the other device searches (MSE), enqueued before the sync
-            if (qs[i]->stats_updated && device_search(qs[i]) && qs[i]->scheme != AIMET_QUANTIZATION_TF_ENHANCED)
+        std::vector<const TqDevice*> ent;
+        std::vector<int64_t> entC;
+        for (int64_t i = 0; i < nq; ++i)   // the other device searches (MSE, entropy), enqueued before the sync
+        {
+            if (!qs[i]->stats_updated)
+                continue;
+            if (entropy_device(qs[i], b))
+            {
+                ent.push_back(&qs[i]->d);
+                entC.push_back(qs[i]->C);
+            }
+            else if (device_search(qs[i]) && qs[i]->scheme != AIMET_QUANTIZATION_TF_ENHANCED)
                 launch_encoding(qs[i], b, sym, strict, unsign, as_stream(stream));
+        }
+        launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0,
+                                   as_stream(stream));
         std::vector<aimet_tf_encoding> tfe(tfe_total);
         launch_tfe_search_many(ds.data(), Cs.data(), (int) ds.size(), b, sym, strict, unsign, tfe.data(),
                                as_stream(stream));

@@ -107,4 +107,26 @@ void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool stri
 void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
                             bool unsign, aimet_tf_encoding* host_out, hipStream_t s);
 
+// entropy_search.hip: the KL range of every channel of an 8-bit entropy getEncoding, written over
+// the first 16 B per channel of d.enc (the quantizer's encoding scratch, 40 B per channel)
+enum EntropyStatus
+{
+    kEntFinal  = 0,   // [lo, hi] is the reference's _optimizeKL range
+    kEntHost   = 1,   // near-tie or non-finite range: the host search decides (glibc log)
+    kEntNoHist = 2    // histogram never allocated: the unseen / all-zero encoding
+};
+struct EntropyRange
+{
+    float lo, hi;
+    int32_t status;
+    int32_t pad;
+};
+static_assert(sizeof(EntropyRange) <= sizeof(aimet_tf_encoding), "fits the encoding scratch");
+inline EntropyRange* entropy_ranges(const TqDevice& d)
+{
+    return reinterpret_cast<EntropyRange*>(d.enc);
+}
+void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, bool sym, bool strict, bool unsign,
+                                hipStream_t s);
+
 }   // namespace aimet_amd

@@ -2,13 +2,15 @@
 
 Reference: EntropyEncodingAnalyzer.cpp:80-435 over updateTensorHistogram_cpu /
 rescaleHistogram (math_functions.cpp:470-641). The reference GPU build copies every tensor to the
-host for this analyzer (math_functions.cpp:449-456); here min/max, the range widening and the
-512-bin histogram run on the device and only the KL search runs on the host.
+host for this analyzer (math_functions.cpp:449-456); here min/max, the range widening, the
+512-bin histogram and the KL search (entropy_search.hip, near-ties re-checked with glibc's log on
+the host) run on the device.
 
 CPU tests pin the oracle (oracle/dlq_oracle.c) to golden vectors of the reference C++ itself
 (tests/golden/golden_entropy.npz, make_golden.py) and to the property KATs of
 TestEntropyEncodingAnalyzer.cpp, and check the product's host KL search through the C-ABI.
-GPU tests run the device statistics through AimetTensorQuantizer: bit-exact state and encodings.
+GPU tests run the device statistics and searches through AimetTensorQuantizer: bit-exact state and
+encodings.
 """
 import ctypes
 
@@ -129,6 +131,41 @@ def test_host_entropy_encoding_golden(golden_entropy):
         z.update(np.zeros(10, np.float32))   # stats updated, histogram never initialised
         assert _host_encoding(empty, 8, *fl) == z.compute(8, *fl).as_tuple()
         assert _host_encoding(empty, 8, *fl, stats_updated=0) == (0.0, 0.0, 0.0, 0.0, 0)
+
+
+def _random_entropy_analyzers(seed, count):
+    """Oracle analyzers fed 1-4 random batches each (normal / uniform / one-sided / zero / Laplace)."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(count):
+        a = O.Analyzer(ENTROPY)
+        batches = []
+        for _ in range(int(rng.integers(1, 5))):
+            n = int(rng.integers(1, 4000))
+            kind = int(rng.integers(0, 5))
+            if kind == 0:
+                x = rng.normal(rng.uniform(-3, 3), rng.uniform(0.01, 5), n)
+            elif kind == 1:
+                x = rng.uniform(0, rng.uniform(0.1, 10), n)
+            elif kind == 2:
+                x = -rng.exponential(rng.uniform(0.1, 3), n)
+            elif kind == 3:
+                x = np.zeros(n)
+            else:
+                x = rng.laplace(0, 1, n) * rng.uniform(0.5, 20)
+            x = x.astype(np.float32)
+            a.update(x)
+            batches.append(x)
+        out.append((a, batches))
+    return out
+
+
+def test_host_entropy_encoding_random():
+    """The product's KL search (entropy_kl.hpp, streamed windows) vs the oracle's array form."""
+    for t, (a, _) in enumerate(_random_entropy_analyzers(31, 40)):
+        st = a.entropy_state()
+        for fl in FLAGS:
+            assert _host_encoding(st, 8, *fl) == a.compute(8, *fl).as_tuple(), (t, fl)
 
 
 # ---- GPU: device statistics ---------------------------------------------------------------------
@@ -252,3 +289,54 @@ def test_entropy_binning_at_bin_edges_large():
     _assert_state(q.entropy_state(), a.entropy_state(), "edges")
     for fl in FLAGS:
         assert _enc_tuple(q.getEncoding(8, *(bool(v) for v in fl))[0]) == a.compute(8, *fl).as_tuple()
+
+
+@pytest.mark.gpu
+@gpu
+def test_entropy_device_kl_search_random():
+    """The device KL search (entropy_search.hip) over 40 random statistics sequences, all flag
+    combinations, through the batched getEncodings (one launch for every quantizer) and the
+    per-quantizer getEncoding: bit-exact vs the oracle's glibc search."""
+    import torch
+    from aimet_amd.libpymo import QuantizationMode
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    cases = _random_entropy_analyzers(47, 40)
+    qs = []
+    for a, batches in cases:
+        q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_ENTROPY)
+        for x in batches:
+            q.updateStats(torch.from_numpy(x).cuda(), True)
+        qs.append(q)
+    for fl in FLAGS:
+        batched = AimetTensorQuantizer.getEncodings(qs, 8, *(bool(v) for v in fl))
+        for t, ((a, _), q, (e, valid)) in enumerate(zip(cases, qs, batched)):
+            want = a.compute(8, *fl).as_tuple()
+            assert valid and _enc_tuple(e) == want, (t, fl)
+            e1, _ = q.getEncoding(8, *(bool(v) for v in fl))
+            assert _enc_tuple(e1) == want, (t, fl)
+
+
+@pytest.mark.gpu
+@gpu
+def test_entropy_device_kl_search_per_channel_many():
+    """Per-channel entropy statistics of 3 weights (one workgroup per channel) and their KL
+    searches in one launch: every channel bit-exact vs an oracle analyzer of its slice."""
+    import torch
+    from aimet_amd.libpymo import QuantizationMode
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    rng = np.random.default_rng(12)
+    shapes = [(64, 27), (128, 576), (32, 2048)]
+    ws = [(rng.standard_normal(s) * rng.uniform(0.01, 0.2, (s[0], 1))).astype(np.float32) for s in shapes]
+    ws[1][5] = 0                                      # an all-zero channel
+    ws[2][:, ::3] = np.abs(ws[2][:, ::3])             # skewed channels
+    qs = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_ENTROPY, num_channels=s[0]) for s in shapes]
+    AimetTensorQuantizer.updateStatsPerChannelMany(qs, [torch.from_numpy(w).cuda() for w in ws])
+    torch.cuda.synchronize()
+    for fl in ((1, 0, 0), (0, 0, 0), (1, 1, 0)):
+        res = AimetTensorQuantizer.getEncodings(qs, 8, *(bool(v) for v in fl))
+        for w, (encs, valid) in zip(ws, res):
+            assert valid
+            for c in range(0, w.shape[0], 7):
+                a = O.Analyzer(ENTROPY)
+                a.update(w[c])
+                assert _enc_tuple(encs[c]) == a.compute(8, *fl).as_tuple(), (w.shape, c, fl)
