@@ -1,7 +1,8 @@
-"""Isolated timing of the TF-Enhanced device search (tfe_search_kernel) on ResNet-50's weights:
-27,560 channels, per-channel symmetric and asymmetric 8-bit, statistics computed once, then
-getEncodings repeated. Run under `rocprofv3 --kernel-trace --stats` for the kernel durations; the
-wall-clock per batched getEncodings (search + copy + host encodings) is printed. Tuning tool."""
+"""Isolated timing of the device encoding searches (TF-Enhanced tfe_search_kernel, MSE
+mse_search_kernel, entropy entropy_search_kernel) on ResNet-50's weights: 27,560 channels,
+per-channel symmetric and asymmetric 8-bit, statistics computed once, then getEncodings repeated.
+usage: tfe_search_time.py [TF_ENHANCED] [MSE] [ENTROPY]. Run under `rocprofv3 --kernel-trace --stats`
+for the kernel durations; the wall-clock per batched getEncodings (search + copy + host encodings) is printed. Tuning tool."""
 import os
 import sys
 import time
@@ -19,9 +20,16 @@ def main():
     torch.cuda.set_device(dev)
     model = resnet50(seed=0, device=dev)
     ws = [m.weight.detach().contiguous() for m in model.modules() if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear))]
-    qs = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=w.shape[0]) for w in ws]
-    AimetTensorQuantizer.updateStatsPerChannelMany(qs, ws)
-    torch.cuda.synchronize()
+    schemes = sys.argv[1:] or ["TF_ENHANCED"]
+    for scheme in schemes:
+        qs = [AimetTensorQuantizer(getattr(QuantizationMode, "QUANTIZATION_" + scheme), num_channels=w.shape[0])
+              for w in ws]
+        AimetTensorQuantizer.updateStatsPerChannelMany(qs, ws)
+        torch.cuda.synchronize()
+        run(scheme, qs, ws)
+
+
+def run(scheme, qs, ws):
     for sym in (True, False):
         AimetTensorQuantizer.getEncodings(qs, 8, sym, False, False)   # warm
         t = []
@@ -30,8 +38,9 @@ def main():
             AimetTensorQuantizer.getEncodings(qs, 8, sym, False, False)
             t.append(time.perf_counter() - t0)
         t.sort()
-        print("%s: %d channels, getEncodings median %.3f ms" % ("sym" if sym else "asym", sum(w.shape[0] for w in ws),
-                                                              t[len(t) // 2] * 1e3), flush=True)
+        print("%s %s: %d channels, getEncodings median %.3f ms" % (scheme, "sym" if sym else "asym",
+                                                                 sum(w.shape[0] for w in ws), t[len(t) // 2] * 1e3),
+              flush=True)
 
 
 if __name__ == "__main__":
