@@ -12,7 +12,8 @@ the ranks run the device statistics (min/max on the first batch, 512-bin histogr
 exchange them with ONE all_reduce(MAX) + ONE all_reduce(SUM) of the packed buffers
 (aimet_amd.distributed). Reported (rank 0, one JSON line):
   * stats Gelem/s per GPU and aggregate (elements histogrammed / wall time of the statistics
-    path between two device synchronisations, forward excluded, max over ranks),
+    path between two device synchronisations, forward excluded, max over ranks), in a process
+    warmed by one untimed statistics pass on throwaway quantizers (--cold: without it),
   * time inside the two collectives, forward time,
   * encodings identical on every rank (all_gather of a digest) and, at N=1, bit-identical to the
     CPU oracle fed the same tensors for the first --oracle-check quantizers.
@@ -38,6 +39,7 @@ def main():
     ap.add_argument("--batch", type=int, default=32, help="global calibration batch")
     ap.add_argument("--oracle-check", type=int, default=3)
     ap.add_argument("--phased", action="store_true", help="single rank: run the sharded phases anyway")
+    ap.add_argument("--cold", action="store_true", help="time the first batch in a cold process (no warm-up pass)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -81,6 +83,13 @@ def main():
         elems += sum(t.numel() for t in tensors)
         for i, lst in enumerate(check):
             lst.append(tensors[i].cpu().numpy().ravel())
+        if b0 == 0 and not args.cold:
+            # warm the process once (code objects of the statistics kernels, allocator pools) on
+            # throwaway quantizers: the timed calibration is what it costs in a warm process
+            warm = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in quantizers]
+            D.sharded_update_stats(warm, tensors, fused=not args.phased)
+            AimetTensorQuantizer.getEncodings(warm, 8, False, False, False)
+            del warm
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
