@@ -32,8 +32,9 @@ __device__ __forceinline__ bool better(float e, long long t, float be, long long
     return (e < be) || (e == be && t < bt);
 }
 
-__global__ __launch_bounds__(kBlock) void mse_search_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
-                                                            int strict, int unsign)
+// slice y (of `splits`) of channel c's candidate grid -> parts[c * splits + y]. Every lane of the
+// workgroup calls it with the same (c, y).
+__device__ void search_slice(const TqDevice& d, int64_t c, int y, int splits, int bw, int sym, int strict, int unsign)
 {
     __shared__ double pdf[tfe::kBins];
     __shared__ float mins[mse::kMaxEdges + 1], maxs[mse::kMaxEdges + 1], cv[mse::kMaxEdges], cw[mse::kMaxEdges];
@@ -44,11 +45,9 @@ __global__ __launch_bounds__(kBlock) void mse_search_kernel(TqDevice d, int64_t 
     __shared__ float wlo[kBlock / 64], whi[kBlock / 64];
     const int lane = threadIdx.x & 63;
     MsePart* parts = reinterpret_cast<MsePart*>(d.search_part);
-    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
     {
-        const int y = blockIdx.y;
         if (!d.pdf_init[c])
-            continue;   // mse_finish_kernel writes the all-zero-data encoding
+            return;   // the finish step writes the all-zero-data encoding
         for (int i = threadIdx.x; i < tfe::kBins; i += kBlock)
             pdf[i] = d.pdf[c * tfe::kBins + i];
         __syncthreads();
@@ -136,13 +135,51 @@ __global__ __launch_bounds__(kBlock) void mse_search_kernel(TqDevice d, int64_t 
     }
 }
 
-// fold the slices of every channel (in candidate order) and write the encodings
-__global__ __launch_bounds__(kBlock) void mse_finish_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
+__global__ __launch_bounds__(kBlock) void mse_search_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
                                                             int strict, int unsign)
 {
-    const int64_t c = (int64_t) blockIdx.x * kBlock + threadIdx.x;
-    if (c >= C)
-        return;
+    for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
+        search_slice(d, c, (int) blockIdx.y, splits, bw, sym, strict, unsign);
+}
+
+// many quantizers in one launch: work item g = (job, channel, slice), flattened in job order
+struct MseJob
+{
+    TqDevice d;
+    int64_t C;
+    int splits;
+    int64_t wstart;   // first work item (channel x slice) of this job
+    int64_t cstart;   // first channel of this job
+};
+
+__device__ __forceinline__ int job_of(const MseJob* jobs, int njobs, int64_t g, bool by_channel)
+{
+    int lo = 0, hi = njobs - 1;   // last job whose start <= g
+    while (lo < hi)
+    {
+        int mid = (lo + hi + 1) >> 1;
+        if ((by_channel ? jobs[mid].cstart : jobs[mid].wstart) <= g)
+            lo = mid;
+        else
+            hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kBlock) void mse_search_many_kernel(const MseJob* __restrict__ jobs, int njobs,
+                                                                 int64_t total, int bw, int sym, int strict, int unsign)
+{
+    for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
+    {
+        const MseJob& j      = jobs[job_of(jobs, njobs, g, false)];
+        const int64_t local  = g - j.wstart;
+        search_slice(j.d, local / j.splits, (int) (local % j.splits), j.splits, bw, sym, strict, unsign);
+    }
+}
+
+// fold the slices of every channel (in candidate order) and write the encodings
+__device__ void finish_channel(const TqDevice& d, int64_t c, int splits, int bw, int sym, int strict, int unsign)
+{
     if (!d.pdf_init[c])
     {
         // statistics updated but no histogram (all data zero): MseEncodingAnalyzer.cpp:86-99,
@@ -174,6 +211,24 @@ __global__ __launch_bounds__(kBlock) void mse_finish_kernel(TqDevice d, int64_t 
     d.enc[c] = mse::finish(bw, blo, bhi, sym != 0, strict != 0, unsign != 0);
 }
 
+__global__ __launch_bounds__(kBlock) void mse_finish_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
+                                                            int strict, int unsign)
+{
+    const int64_t c = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (c < C)
+        finish_channel(d, c, splits, bw, sym, strict, unsign);
+}
+
+__global__ __launch_bounds__(kBlock) void mse_finish_many_kernel(const MseJob* __restrict__ jobs, int njobs,
+                                                                 int64_t total, int bw, int sym, int strict, int unsign)
+{
+    const int64_t g = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (g >= total)
+        return;
+    const MseJob& j = jobs[job_of(jobs, njobs, g, true)];
+    finish_channel(j.d, g - j.cstart, j.splits, bw, sym, strict, unsign);
+}
+
 }   // namespace
 
 size_t mse_part_bytes(int64_t C)
@@ -181,10 +236,43 @@ size_t mse_part_bytes(int64_t C)
     return sizeof(MsePart) * (size_t) (C > kMseMaxSplits ? C : kMseMaxSplits);
 }
 
+namespace
+{
+// slices per channel: fill the chip when there are few channels (per-tensor: 128 workgroups);
+// the result does not depend on it (slices are folded in candidate order)
+int mse_splits(int64_t C)
+{
+    return C >= kMseMaxSplits ? 1 : (int) (kMseMaxSplits / C);
+}
+}   // namespace
+
+void launch_mse_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
+                            bool unsign, hipStream_t s)
+{
+    if (n == 0)
+        return;
+    std::vector<MseJob> jobs((size_t) n);
+    int64_t work = 0, chans = 0;
+    for (int i = 0; i < n; ++i)
+    {
+        const int splits = mse_splits(Cs[i]);
+        jobs[(size_t) i] = MseJob {*ds[i], Cs[i], splits, work, chans};
+        work += Cs[i] * splits;
+        chans += Cs[i];
+    }
+    auto* dj = static_cast<MseJob*>(upload_async(jobs.data(), sizeof(MseJob) * (size_t) n, s));
+    mse_search_many_kernel<<<(unsigned) (work < 65536 ? work : 65536), kBlock, 0, s>>>(
+        dj, n, work, bw, sym ? 1 : 0, strict ? 1 : 0, unsign ? 1 : 0);
+    AIMET_LAUNCH_CHECK();
+    mse_finish_many_kernel<<<(unsigned) ceil_div(chans, kBlock), kBlock, 0, s>>>(dj, n, chans, bw, sym ? 1 : 0,
+                                                                                 strict ? 1 : 0, unsign ? 1 : 0);
+    AIMET_LAUNCH_CHECK();
+    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
+}
+
 void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s)
 {
-    // slices per channel: fill the chip when there are few channels (per-tensor: 128 workgroups)
-    const int splits = C >= kMseMaxSplits ? 1 : (int) (kMseMaxSplits / C);
+    const int splits = mse_splits(C);
     dim3 grid((unsigned) (C < 65536 ? C : 65536), (unsigned) splits);
     mse_search_kernel<<<grid, kBlock, 0, s>>>(d, C, splits, bw, sym, strict, unsign);
     AIMET_LAUNCH_CHECK();

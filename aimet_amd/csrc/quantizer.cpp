@@ -727,8 +727,8 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
             }
             off += qs[i]->C;
         }
-        std::vector<const TqDevice*> ent;
-        std::vector<int64_t> entC;
+        std::vector<const TqDevice*> ent, mse;
+        std::vector<int64_t> entC, mseC;
         for (int64_t i = 0; i < nq; ++i)   // the other device searches (MSE, entropy), enqueued before the sync
         {
             if (!qs[i]->stats_updated)
@@ -738,9 +738,14 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
                 ent.push_back(&qs[i]->d);
                 entC.push_back(qs[i]->C);
             }
-            else if (device_search(qs[i]) && qs[i]->scheme != AIMET_QUANTIZATION_TF_ENHANCED)
-                launch_encoding(qs[i], b, sym, strict, unsign, as_stream(stream));
+            else if (qs[i]->hist && qs[i]->scheme == AIMET_QUANTIZATION_MSE)
+            {
+                mse.push_back(&qs[i]->d);
+                mseC.push_back(qs[i]->C);
+            }
         }
+        launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0,
+                               as_stream(stream));
         launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0,
                                    as_stream(stream));
         std::vector<aimet_tf_encoding> tfe(tfe_total);

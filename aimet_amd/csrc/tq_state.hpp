@@ -99,13 +99,16 @@ void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s);
 // tfe_search.hip
 // d.enc[c] <- TF-Enhanced encoding of channel c (statistics updated; see aimet_tq_get_encoding)
 void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
-// mse_search.hip: d.enc[c] <- MSE encoding of channel c (statistics updated)
-size_t mse_part_bytes(int64_t C);
-void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
 // the same for n quantizers in one launch; host_out <- their encodings concatenated
 // (sum of Cs). Synchronises s.
 void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
                             bool unsign, aimet_tf_encoding* host_out, hipStream_t s);
+// mse_search.hip: d.enc[c] <- MSE encoding of channel c (statistics updated)
+size_t mse_part_bytes(int64_t C);
+void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
+// the same for n quantizers in one launch (+ one fold launch)
+void launch_mse_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
+                            bool unsign, hipStream_t s);
 
 // entropy_search.hip: the KL range of every channel of an 8-bit entropy getEncoding, written over
 // the first 16 B per channel of d.enc (the quantizer's encoding scratch, 40 B per channel)
