@@ -337,11 +337,15 @@ std::pair<float, float> kl_range(double tmin, double tmax, const double* tpp_his
     const double w = (hi - lo) / (double) kPdfSize;
     short wa[entropy::kWindows], wb[entropy::kWindows];
     const int n   = entropy::windows(hist, lo, w, sym || strict, wa, wb);
+    double left[kPdfSize];
+    int zeros[kPdfSize + 1];
+    entropy::Prefix pre {left, zeros, false};
+    entropy::build_prefix(hist, left, zeros, pre.q_zero_rule);
     double best   = std::numeric_limits<double>::infinity();
     double bestLo = lo, bestHi = hi;
     for (int k = 0; k < n; ++k)
     {
-        const entropy::WindowKl r = entropy::window_kl(hist, wa[k], wb[k], glibc_log);
+        const entropy::WindowKl r = entropy::window_kl(hist, wa[k], wb[k], glibc_log, &pre);
         if (r.brk)
             break;
         if (r.dv < best)

@@ -203,35 +203,90 @@ struct WindowKl
     double mag;    // sum of |p * log(p / q)| (the device's near-tie tolerance scales with it)
 };
 
-// _computeKL (:200-224) of window [a, b] over `hist`, with `lg` the natural logarithm.
+// Per-histogram tables shared by every window (built once, in the reference's summation order):
+//   left[a]  = hist[0] + ... + hist[a]          (sequential double sum, as the window loop adds it)
+//   zeros[k] = number of zero bins in hist[0, k)
+//   q_zero_rule: every bin is 0 or in [1e-300, DBL_MAX] (bin counts always are). Then Q[i] == 0
+//   exactly when hw[i] == 0 (a non-empty level's sum / norm cannot underflow), so both zero
+//   counts of the conditioning are known before the window is streamed.
+struct Prefix
+{
+    const double* left;   // [kBins]
+    const int* zeros;     // [kBins + 1]
+    bool q_zero_rule;
+};
+
+AIMET_ENT_HD void build_prefix(const double* hist, double* left, int* zeros, bool& q_zero_rule)
+{
+    double l = 0;
+    int z    = 0;
+    bool ok  = true;
+    zeros[0] = 0;
+    for (int i = 0; i < kBins; ++i)
+    {
+        l += hist[i];
+        left[i] = l;
+        z += hist[i] == 0;
+        zeros[i + 1] = z;
+        ok = ok && (hist[i] == 0 || (hist[i] >= 1e-300 && hist[i] <= 1.7976931348623157e308));
+    }
+    q_zero_rule = ok;
+}
+
+// _computeKL (:200-224) of window [a, b] over `hist`, with `lg` the natural logarithm. With a
+// Prefix whose q_zero_rule holds, the accumulate() sums and the conditioned normalisers come
+// from one streamed pass instead of two (same operations, same order).
 template <class Log>
-AIMET_ENT_HD WindowKl window_kl(const double* hist, int a, int b, Log&& lg)
+AIMET_ENT_HD WindowKl window_kl(const double* hist, int a, int b, Log&& lg, const Prefix* pre = nullptr)
 {
     const int win = b - a + 1;
     double left = 0, right = 0;
-    for (int i = 0; i <= a; ++i)
-        left += hist[i];
+    if (pre)
+        left = pre->left[a];
+    else
+        for (int i = 0; i <= a; ++i)
+            left += hist[i];
     for (int i = b; i < kBins; ++i)
         right += hist[i];
-    // pass 1: accumulate(P), accumulate(Q) (float) and the zero counts of the conditioning
-    float aP = 0.f, aQ = 0.f;
-    uint64_t zP = 0, zQ = 0;
-    stream_pq(hist, a, b, left, right, [&](int, double p, double q) {
-        aP = (float) ((double) aP + p);
-        aQ = (float) ((double) aQ + q);
-        zP += (p == 0.f);
-        zQ += (q == 0.f);
-    });
-    if (aP == 0 || aQ == 0)
-        return WindowKl {true, 0.0, 0.0};
-    const Cond cP = cond_of(zP, (uint64_t) win), cQ = cond_of(zQ, (uint64_t) win);
-    // pass 2: the normalisers of the conditioned histograms (float accumulate)
-    float sP = 0.f, sQ = 0.f;
-    stream_pq(hist, a, b, left, right, [&](int, double p, double q) {
-        sP = (float) ((double) sP + cond_apply(cP, p));
-        sQ = (float) ((double) sQ + cond_apply(cQ, q));
-    });
-    // pass 3: the divergence, ascending
+    float aP = 0.f, aQ = 0.f, sP = 0.f, sQ = 0.f;
+    Cond cP, cQ;
+    if (pre && pre->q_zero_rule)
+    {
+        // P = {left, hist[a+1 .. b-1], right}, Q is zero exactly where hist[a .. b] is
+        const uint64_t zP = (uint64_t) (pre->zeros[b] - pre->zeros[a + 1]) + (left == 0.f) + (right == 0.f);
+        const uint64_t zQ = (uint64_t) (pre->zeros[b + 1] - pre->zeros[a]);
+        cP = cond_of(zP, (uint64_t) win);
+        cQ = cond_of(zQ, (uint64_t) win);
+        stream_pq(hist, a, b, left, right, [&](int, double p, double q) {
+            aP = (float) ((double) aP + p);
+            aQ = (float) ((double) aQ + q);
+            sP = (float) ((double) sP + cond_apply(cP, p));
+            sQ = (float) ((double) sQ + cond_apply(cQ, q));
+        });
+        if (aP == 0 || aQ == 0)
+            return WindowKl {true, 0.0, 0.0};
+    }
+    else
+    {
+        // pass 1: accumulate(P), accumulate(Q) (float) and the zero counts of the conditioning
+        uint64_t zP = 0, zQ = 0;
+        stream_pq(hist, a, b, left, right, [&](int, double p, double q) {
+            aP = (float) ((double) aP + p);
+            aQ = (float) ((double) aQ + q);
+            zP += (p == 0.f);
+            zQ += (q == 0.f);
+        });
+        if (aP == 0 || aQ == 0)
+            return WindowKl {true, 0.0, 0.0};
+        cP = cond_of(zP, (uint64_t) win);
+        cQ = cond_of(zQ, (uint64_t) win);
+        // pass 2: the normalisers of the conditioned histograms (float accumulate)
+        stream_pq(hist, a, b, left, right, [&](int, double p, double q) {
+            sP = (float) ((double) sP + cond_apply(cP, p));
+            sQ = (float) ((double) sQ + cond_apply(cQ, q));
+        });
+    }
+    // the divergence, ascending
     double dv = 0, mag = 0;
     const double dP = sP, dQ = sQ;
     stream_pq(hist, a, b, left, right, [&](int, double p, double q) {

@@ -43,8 +43,10 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
     __shared__ short wa[entropy::kWindows], wb[entropy::kWindows];
     __shared__ double dv[entropy::kWindows], mag[entropy::kWindows];
     __shared__ int brk[entropy::kWindows];
+    __shared__ double left[entropy::kBins];
+    __shared__ int zeros[entropy::kBins + 1];
     __shared__ double s_lo, s_hi;
-    __shared__ int s_n;
+    __shared__ int s_n, s_rule;
     const int t = threadIdx.x;
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
     {
@@ -78,11 +80,16 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
             s_lo = lo;
             s_hi = hi;
             s_n  = entropy::windows(hist, lo, (hi - lo) / (double) entropy::kBins, sym || strict, wa, wb);
+            bool rule;
+            entropy::build_prefix(hist, left, zeros, rule);
+            s_rule = rule ? 1 : 0;
         }
         __syncthreads();
         if (t < s_n)
         {
-            const entropy::WindowKl r = entropy::window_kl(hist, wa[t], wb[t], [](double v) { return log(v); });
+            const entropy::Prefix pre {left, zeros, s_rule != 0};
+            const entropy::WindowKl r =
+                entropy::window_kl(hist, wa[t], wb[t], [](double v) { return log(v); }, &pre);
             dv[t]  = r.dv;
             mag[t] = r.mag;
             brk[t] = r.brk ? 1 : 0;
