@@ -60,8 +60,20 @@ def main():
         tot = sum(d for _, d in cagg.values())
         # bench.py runs compute_encodings 1 + --enc-reps times: one minmax_many launch per call
         ncalls = max(1, sum(c for k, (c, _) in cagg.items() if k.startswith("minmax_many_kernel")))
-        print("compute_encodings kernels (before the first QDQ step): %d calls, %.3f ms GPU time per call"
-              % (ncalls, tot / 1e6 / ncalls))
+        # kernels of the parameter stream overlap the activation passes: also report the union of
+        # the busy intervals (the GPU time a call actually occupies)
+        iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in cal)
+        busy, cs, ce = 0, iv[0][0], iv[0][1]
+        for s0, e0 in iv[1:]:
+            if s0 > ce:
+                busy += ce - cs
+                cs, ce = s0, e0
+            else:
+                ce = max(ce, e0)
+        busy += ce - cs
+        print("compute_encodings kernels (before the first QDQ step): %d calls, %.3f ms summed kernel time per "
+              "call, %.3f ms GPU busy per call (union of overlapping kernels)"
+              % (ncalls, tot / 1e6 / ncalls, busy / 1e6 / ncalls))
         for k, (c, d) in sorted(cagg.items(), key=lambda x: -x[1][1]):
             print("  %-62s calls/call %4.1f  ms/call %.4f  avg us %.1f" % (k, c / ncalls, d / 1e6 / ncalls,
                                                                          d / 1e3 / c))
