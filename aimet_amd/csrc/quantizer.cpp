@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -31,7 +32,8 @@ struct aimet_tensor_quantizer
 
 struct Slab
 {
-    void* base = nullptr;
+    void* base   = nullptr;
+    size_t bytes = 0;
     std::atomic<int64_t> refs {0};
 };
 
@@ -152,6 +154,80 @@ void parallel_channels(int64_t C, F&& f, int64_t grain = 64)   // grain: fewest 
         x.join();
 }
 
+// Released quantizer state is cached for reuse (as torch's caching allocator does) instead of
+// hipDeviceSynchronize + hipFree at destruction: destroying a quantizer then never blocks the host
+// nor breaks a HIP graph being captured on another stream, and a calibration that creates a
+// model's quantizers again reuses the allocation. Work queued on any stream may still use a
+// released block, so it is handed out again only after a device synchronisation (by the creating
+// call, outside any capture). Blocks that do not fit are freed when an allocation misses.
+struct StateCache
+{
+    struct Block
+    {
+        int device;
+        void* p;
+        size_t bytes;
+    };
+    std::mutex m;
+    std::vector<Block> blocks;
+};
+StateCache& state_cache()
+{
+    static StateCache* c = new StateCache();   // never destroyed: blocks live until process exit
+    return *c;
+}
+
+// device memory for quantizer state on the current device (the caller holds a DeviceGuard)
+void* state_alloc(int device, size_t bytes)
+{
+    StateCache& c = state_cache();
+    void* p       = nullptr;
+    std::vector<void*> misfits;
+    {
+        std::lock_guard<std::mutex> lock(c.m);
+        size_t best = (size_t) -1;
+        for (size_t i = 0; i < c.blocks.size(); ++i)
+        {
+            const StateCache::Block& b = c.blocks[i];
+            if (b.device == device && b.bytes >= bytes && b.bytes <= 2 * bytes &&
+                (best == (size_t) -1 || b.bytes < c.blocks[best].bytes))
+                best = i;
+        }
+        if (best != (size_t) -1)
+        {
+            p = c.blocks[best].p;
+            c.blocks.erase(c.blocks.begin() + (std::ptrdiff_t) best);
+        }
+        else
+            for (size_t i = 0; i < c.blocks.size();)
+                if (c.blocks[i].device == device)
+                {
+                    misfits.push_back(c.blocks[i].p);
+                    c.blocks.erase(c.blocks.begin() + (std::ptrdiff_t) i);
+                }
+                else
+                    ++i;
+    }
+    if (p)
+    {
+        AIMET_HIP_CHECK(hipDeviceSynchronize());   // the previous owner's queued work is done
+        return p;
+    }
+    for (void* m: misfits)
+        AIMET_HIP_CHECK(hipFree(m));
+    hipError_t e = hipMalloc(&p, bytes);
+    if (e != hipSuccess)
+        throw HipError(std::string("hipMalloc(tensor quantizer state): ") + hipGetErrorString(e));
+    return p;
+}
+
+void state_release(int device, void* p, size_t bytes)
+{
+    StateCache& c = state_cache();
+    std::lock_guard<std::mutex> lock(c.m);
+    c.blocks.push_back(StateCache::Block {device, p, bytes});
+}
+
 aimet_tensor_quantizer* new_quantizer(int scheme, int64_t num_channels, int device)
 {
     AIMET_REQUIRE(num_channels >= 1, "num_channels must be >= 1");
@@ -199,16 +275,20 @@ int aimet_tq_create_many(const int* schemes, const int64_t* num_channels, int64_
             throw;
         }
         DeviceGuard g(device);
-        auto* sl     = new Slab();
-        hipError_t e = hipMalloc(&sl->base, total);
-        if (e != hipSuccess)
+        auto* sl = new Slab();
+        try
+        {
+            sl->base = state_alloc(device, total);
+        }
+        catch (...)
         {
             delete sl;
             for (auto* q: qs)
                 delete q;
-            throw HipError(std::string("hipMalloc(tensor quantizer state): ") + hipGetErrorString(e));
+            throw;
         }
-        sl->refs = count;
+        sl->bytes = total;
+        sl->refs  = count;
         AIMET_HIP_CHECK(hipMemsetAsync(sl->base, 0, total, nullptr));
         std::vector<ResetJob> resets;
         for (int64_t i = 0; i < count; ++i)
@@ -231,11 +311,14 @@ int aimet_tq_create(int scheme, int64_t num_channels, int device, aimet_tensor_q
         AIMET_REQUIRE(out != nullptr, "output handle is null");
         auto* q = new_quantizer(scheme, num_channels, device);
         DeviceGuard g(device);
-        hipError_t e = hipMalloc(&q->arena, q->arena_bytes);
-        if (e != hipSuccess)
+        try
+        {
+            q->arena = static_cast<char*>(state_alloc(device, q->arena_bytes));
+        }
+        catch (...)
         {
             delete q;
-            throw HipError(std::string("hipMalloc(tensor quantizer state): ") + hipGetErrorString(e));
+            throw;
         }
         layout(q, true);
         reset_device_state(q, nullptr);
@@ -249,24 +332,18 @@ int aimet_tq_destroy(aimet_tensor_quantizer* q)
     return guarded([&] {
         if (!q)
             return;
+        // the memory goes back to the state cache (no synchronisation here: see state_alloc)
         if (q->slab)
         {
             Slab* sl = q->slab;
             if (--sl->refs == 0)
             {
-                DeviceGuard g(q->device);
-                AIMET_HIP_CHECK(hipDeviceSynchronize());
-                AIMET_HIP_CHECK(hipFree(sl->base));
+                state_release(q->device, sl->base, sl->bytes);
                 delete sl;
             }
         }
         else if (q->arena)
-        {
-            DeviceGuard g(q->device);
-            // callers may still have work queued on any stream that uses this state
-            AIMET_HIP_CHECK(hipDeviceSynchronize());
-            AIMET_HIP_CHECK(hipFree(q->arena));
-        }
+            state_release(q->device, q->arena, q->arena_bytes);
         delete q;
     });
 }
