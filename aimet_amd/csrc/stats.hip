@@ -358,12 +358,25 @@ __device__ __forceinline__ void ent_fold_hist_one(const TqDevice& d, int64_t c)
 // out-of-range (and NaN) dropped.
 struct PdfBinner
 {
-    float bucket, offset, rcp;
-    __device__ PdfBinner(float b, float o) : bucket(b), offset(o), rcp(1.0f / b) {}
+    float bucket, offset, rcp, thr;
+    // thr: round_div_sub's threshold 2^-21 (|q| + |off| + 1) bounded once for every element whose
+    // bin can be in range (|v| <= 512, so |q| <= 512 + |off| + 1): hoisted out of the element loop.
+    // An element beyond that bound lies out of range whichever way it rounds, and a zero code's
+    // sign does not matter for a bin index, so the fast path needs no other test.
+    __device__ PdfBinner(float b, float o)
+        : bucket(b), offset(o), rcp(1.0f / b),
+          thr((2.0f * __builtin_fabsf(o) + 514.0f) * 4.76837158203125e-7f)
+    {
+    }
     __device__ __forceinline__ int bin(float x) const
     {
-        // == roundf(x / bucket - offset) bit for bit (round_div_sub, common.hpp)
-        float r = round_div_sub(x, bucket, rcp, offset);
+        // == roundf(x / bucket - offset) bit for bit (round_div_sub, common.hpp), in range
+        const float v = x * rcp - offset;
+        float r;
+        if (__builtin_fabsf(__builtin_amdgcn_fractf(v) - 0.5f) > thr)   // false for NaN
+            r = __builtin_rintf(v);
+        else
+            r = __builtin_roundf(x / bucket - offset);
         return (r >= 0.0f && r < (float) kPdfSize) ? (int) r : -1;
     }
 };
