@@ -125,6 +125,7 @@ _PROTOTYPES = {
     "aimet_tq_fold_minmax_many": [ctypes.POINTER(_vp), _i64, _vp],
     "aimet_tq_batch_histogram_many": [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64), _i64, _vp],
     "aimet_tq_fold_histogram_many": [ctypes.POINTER(_vp), ctypes.POINTER(_i64), _i64, _vp],
+    "aimet_tq_fold_histogram_many_dev": [ctypes.POINTER(_vp), _vp, _i64, _vp],
     "aimet_tq_create_many": [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(_i64), _i64, ctypes.c_int,
                              ctypes.POINTER(_vp)],
     "aimet_tq_update_stats_channels_many": [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64),

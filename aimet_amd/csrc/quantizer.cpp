@@ -457,7 +457,7 @@ namespace
 
 // jobs of a many-quantizer call: per-tensor quantizers of one device
 std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
-                                const int64_t* counts, int64_t count)
+                                const int64_t* counts, int64_t count, const int64_t* counts_dev = nullptr)
 {
     AIMET_REQUIRE(qs != nullptr && count >= 0, "null argument");
     std::vector<StatsJob> jobs((size_t) count);
@@ -475,6 +475,7 @@ std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* 
             require_device_ptr(j.x, "input");
         j.count = counts ? counts[i] : j.n;
         AIMET_REQUIRE(j.count >= 0, "negative element count");
+        j.count_dev = counts_dev ? counts_dev + i : nullptr;
         j.d     = q->d;
         j.hist  = q->hist ? 1 : 0;
         j.ent   = q->kind == kKindEntropy ? 1 : 0;
@@ -484,10 +485,12 @@ std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* 
 }
 
 int run_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns, const int64_t* counts,
-             int64_t count, int phases, bool marks_updated, void* stream)
+             int64_t count, int phases, bool marks_updated, void* stream, const int64_t* counts_dev = nullptr)
 {
     return guarded([&] {
-        auto jobs = make_jobs(qs, xs, ns, counts, count);
+        if (counts_dev)
+            require_device_ptr(counts_dev, "element counts");
+        auto jobs = make_jobs(qs, xs, ns, counts, count, counts_dev);
         if (jobs.empty())
             return;
         DeviceGuard g(qs[0]->device);
@@ -532,6 +535,14 @@ int aimet_tq_fold_histogram_many(aimet_tensor_quantizer* const* qs, const int64_
     if (counts == nullptr && count > 0)
         return guarded([] { AIMET_REQUIRE(false, "null element counts"); });
     return run_many(qs, nullptr, nullptr, counts, count, kPhaseFoldHistogram, false, stream);
+}
+
+int aimet_tq_fold_histogram_many_dev(aimet_tensor_quantizer* const* qs, const int64_t* counts_dev, int64_t count,
+                                     void* stream)
+{
+    if (counts_dev == nullptr && count > 0)
+        return guarded([] { AIMET_REQUIRE(false, "null element counts"); });
+    return run_many(qs, nullptr, nullptr, nullptr, count, kPhaseFoldHistogram, false, stream, counts_dev);
 }
 
 int aimet_tq_update_stats_channels_many(aimet_tensor_quantizer* const* qs, const float* const* xs,

@@ -696,7 +696,7 @@ __global__ __launch_bounds__(kPdfSize) void fold_histogram_many_kernel(const Sta
             ent_fold_hist_one(J.d, 0);
     }
     else if (J.d.pdf_init[0])
-        fold_hist_one(J.d, 0, J.count);
+        fold_hist_one(J.d, 0, J.count_dev ? *J.count_dev : J.count);
 }
 
 // ---- many per-channel quantizers: updateStats in two launches ------------------------------

@@ -69,6 +69,7 @@ struct StatsJob
     const float* x;
     int64_t n;       // elements of this quantizer's tensor
     int64_t count;   // element count of the PDF fold (the global count when sharded)
+    const int64_t* count_dev;   // when set: the count is read on the device (summed over ranks in HBM)
     TqDevice d;
     uint32_t mm_block0, mm_blocks, h_block0, h_blocks;   // filled by launch_stats_many
     int32_t hist, vec;

@@ -8,8 +8,10 @@ batch into one buffer per phase:
   1. batch min/max          -> packed float32 {-min, max}   -> ONE all_reduce(MAX)
   2. fold: TF running min/max; histogram schemes fix the 512-bucket PDF range on the first batch
      from the GLOBAL min/max (so every rank bins identically)
-  3. batch histogram        -> packed int64 counts            -> ONE all_reduce(SUM)
-  4. fold: PDF running average with the GLOBAL element count
+  3. batch histogram        -> packed int64 counts, followed by every histogram quantizer's local
+                               element count                 -> ONE all_reduce(SUM)
+  4. fold: PDF running average with the GLOBAL element count, read by the fold kernel from the
+     reduced buffer (no host round trip between the phases)
 
 Every rank ends with statistics identical to one device processing the whole batch (integer
 counts are order-independent; the double PDF recurrence sees the same inputs), hence identical
@@ -41,7 +43,11 @@ class PackedExchange:
         chans = [q.num_channels for q in self.quantizers]
         self.minmax = torch.zeros(2 * sum(chans), dtype=torch.float32, device=device)
         hist_ch = sum(c for q, c in zip(self.quantizers, chans) if q.uses_histogram)
-        self.counts = torch.zeros(PDF_SIZE * hist_ch, dtype=torch.int64, device=device)
+        n_hist = sum(1 for q in self.quantizers if q.uses_histogram)
+        # bin counts of every histogram channel, then one element count per histogram quantizer:
+        # the element counts ride the same SUM as the bins
+        self.counts = torch.zeros(PDF_SIZE * hist_ch + n_hist, dtype=torch.int64, device=device)
+        self.elem_counts = self.counts[PDF_SIZE * hist_ch:]
         m = h = 0
         for q, c in zip(self.quantizers, chans):
             mm = self.minmax[m:m + 2 * c]
@@ -65,14 +71,6 @@ def _all_reduce(t, op, group):
         t.copy_(h)
     else:
         dist.all_reduce(t, op=op, group=group)
-
-
-def global_counts(local_counts, device, group=None):
-    """Per-quantizer element counts summed over ranks (one tiny collective)."""
-    t = torch.tensor(local_counts, dtype=torch.int64, device=device)
-    if _world(group) > 1:
-        _all_reduce(t, dist.ReduceOp.SUM, group)
-    return t.tolist()
 
 
 def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange=None, fused=True):
@@ -122,15 +120,30 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
         for i in hist_rest:
             quantizers[i].batch_histogram(tensors[i], ch_axes[i])
         local = [tensors[i].numel() // quantizers[i].num_channels for i in hist]
+        # element counts, ordered as the histogram quantizers: the batched ones first (the fold
+        # kernel reads its slice of the reduced buffer), then the others
+        order = hist_many + hist_rest
+        by_pos = {i: k for k, i in enumerate(hist)}
         if world > 1:
+            host = torch.tensor([local[by_pos[i]] for i in order], dtype=torch.int64)
+            if exchange.elem_counts.is_cuda:
+                # a pinned staging buffer from torch's caching host allocator, which keeps it alive
+                # until the stream-ordered copy has run
+                exchange.elem_counts.copy_(host.pin_memory(), non_blocking=True)
+            else:
+                exchange.elem_counts.copy_(host)
             _all_reduce(exchange.counts, dist.ReduceOp.SUM, group)
-            counts = global_counts(local, device, group)
+            if hist_many:
+                AimetTensorQuantizer.fold_histogram_many([quantizers[i] for i in hist_many],
+                                                         exchange.elem_counts[:len(hist_many)])
+            if hist_rest:
+                rest_counts = exchange.elem_counts[len(hist_many):].tolist()
+                for i, c in zip(hist_rest, rest_counts):
+                    quantizers[i].fold_histogram(c)
         else:
-            counts = local
-        by_index = dict(zip(hist, counts))
-        if hist_many:
-            AimetTensorQuantizer.fold_histogram_many([quantizers[i] for i in hist_many],
-                                                     [by_index[i] for i in hist_many])
-        for i in hist_rest:
-            quantizers[i].fold_histogram(by_index[i])
+            if hist_many:
+                AimetTensorQuantizer.fold_histogram_many([quantizers[i] for i in hist_many],
+                                                         [local[by_pos[i]] for i in hist_many])
+            for i in hist_rest:
+                quantizers[i].fold_histogram(local[by_pos[i]])
     return exchange

@@ -323,6 +323,21 @@ class AimetTensorQuantizer:
 
     @staticmethod
     def fold_histogram_many(quantizers, counts):
+        """counts: per-quantizer element counts, a host sequence, or an int64 device tensor read by
+        the fold kernel itself (no host round trip: aimet_tq_fold_histogram_many_dev)."""
+        if isinstance(counts, torch.Tensor):
+            qs = list(quantizers)
+            if not qs:
+                return
+            if counts.dtype != torch.int64 or not counts.is_cuda or counts.numel() < len(qs) \
+                    or not counts.is_contiguous():
+                raise ValueError("device element counts: a contiguous int64 HIP tensor of >= %d entries" % len(qs))
+            dev = counts.device
+            n = len(qs)
+            with torch.cuda.device(dev):
+                _native.call("aimet_tq_fold_histogram_many_dev", (ctypes.c_void_p * n)(*[q._handle for q in qs]),
+                             counts.data_ptr(), n, torch.cuda.current_stream(dev).cuda_stream)
+            return
         return AimetTensorQuantizer._many("aimet_tq_fold_histogram_many", quantizers, counts=counts)
 
     @staticmethod

@@ -20,6 +20,8 @@ import ctypes
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -56,13 +58,77 @@ def parse():
     return p.parse_args()
 
 
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n):
+    """`bench.py --gpus N` without a launcher: start N copies of this script, one per GPU, with
+    RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, and wait for them. This parent never touches the
+    GPU (torch.cuda.device_count() does not initialise HIP on this image); it only counts devices.
+    Rank 0 writes the JSON line to the inherited stdout. If any rank fails, the others are stopped
+    and the parent exits with that rank's status."""
+    backend = os.environ.get("AIMET_BENCH_BACKEND", "nccl")
+    if backend == "nccl" and not os.environ.get("AIMET_BENCH_LAUNCH_CHECK"):
+        ndev = torch.cuda.device_count()
+        if ndev < n:
+            print("bench.py --gpus %d: only %d GPU(s) visible; RCCL needs one GPU per rank "
+                  "(AIMET_BENCH_BACKEND=gloo rehearses several ranks on fewer GPUs)" % (n, ndev), file=sys.stderr)
+            return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                print("bench.py: rank %d exited with %d; stopping the other ranks" % (procs.index(p), code),
+                      file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def launch_check(world, rank):
+    """AIMET_BENCH_LAUNCH_CHECK=1: form the process group exactly as the bench does (no GPU work)
+    and report what formed: the CPU test of the launcher (tests/test_bench_launch.py)."""
+    backend = os.environ.get("AIMET_BENCH_BACKEND", "nccl")
+    if os.environ["AIMET_BENCH_LAUNCH_CHECK"] == "fail%d" % rank:
+        sys.exit(3)   # the launcher's failure path (a rank dying before the group forms)
+    dist.init_process_group(backend, rank=rank, world_size=world)
+    t = torch.tensor([rank + 1], dtype=torch.int64)
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"launch_check": True, "n_gpus": dist.get_world_size(), "dist_backend": dist.get_backend(),
+                          "rank_sum": int(t.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def setup_dist(args):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher formed WORLD_SIZE=%d" % (args.gpus, world))
     # AIMET_BENCH_BACKEND=gloo rehearses the N-rank path with several ranks sharing fewer GPUs
     # (RCCL needs one GPU per rank); the statistics exchange then stages through host memory
     backend = os.environ.get("AIMET_BENCH_BACKEND", "nccl")
+    if backend == "nccl" and world > 1 and torch.cuda.device_count() < world:
+        raise SystemExit("bench.py: %d ranks over RCCL but only %d GPU(s) visible" % (world, torch.cuda.device_count()))
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
     if world > 1:
@@ -115,11 +181,15 @@ def compute_encodings(acts, weights):
     return act_enc, w_enc, time.perf_counter() - t0, aq, wq
 
 
-def cpu_baseline(acts, weights, act_enc, w_enc, images):
+def cpu_baseline(acts, weights, act_enc, w_enc, images, act_outs, w_outs):
     """The reference's CPU path on a bounded sample: oracle/_ref (the reference DlQuantization C++
     compiled from its own sources, TensorQuantizationSim::quantizeDequantizeTensor and
     quantizeDequantizePerChannel with COMP_MODE_CPU) when that library travelled with the tree,
-    and the in-repo C restatement (oracle/dlq_oracle.c, single thread + OpenMP) beside it."""
+    and the in-repo C restatement (oracle/dlq_oracle.c, single thread + OpenMP) beside it.
+
+    The outputs of the timed reference run are then compared bit for bit with the GPU outputs of
+    the same elements (act_outs / w_outs: the QDQ results of the last timed step), and the TF-E
+    encodings the reference analyzers compute for the sampled weight channels with the GPU's."""
     from oracle import oracle as O
     xs, ws = [], []
     for (name, t), e in zip(acts, act_enc):
@@ -129,32 +199,50 @@ def cpu_baseline(acts, weights, act_enc, w_enc, images):
                    O.per_channel_table([e.to_tuple() for e in encs])))
     n = sum(x.size for x, _ in xs) + sum(w.size for w, _, _, _ in ws)
 
-    def timed(qdq_t, qdq_c):
+    def timed(qdq_t, qdq_c, keep=None):
         t0 = time.perf_counter()
         for x, e in xs:
-            qdq_t(x, e)
+            y = qdq_t(x, e)
+            if keep is not None:
+                keep.append(y)
         for w, C, K, tab in ws:
-            qdq_c(w, C, K, tab)
+            y = qdq_c(w, C, K, tab)
+            if keep is not None:
+                keep.append(y)
         return time.perf_counter() - t0
 
     res = {"n": n}
-    res["port_s"] = timed(lambda x, e: O.qdq_per_tensor(x, e.min, e.max, 8), O.qdq_per_channel)
+    ref_lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle", "_ref", "libdlq_ref.so")
+    have_ref = os.path.exists(ref_lib)
+    outs = []
+    res["port_s"] = timed(lambda x, e: O.qdq_per_tensor(x, e.min, e.max, 8), O.qdq_per_channel,
+                          None if have_ref else outs)
     # the OpenMP variant of the same loops on the box's CPU share
     threads = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))))
     res["omp_s"] = timed(lambda x, e: O.qdq_per_tensor_omp(x, e.min, e.max, 8, threads),
                          lambda w, C, K, tab: O.qdq_per_channel_omp(w, C, K, tab, threads))
     res["omp_threads"] = threads
     res["openmp"] = O.openmp_enabled()
-    ref_lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "oracle", "_ref", "libdlq_ref.so")
     Analyzer = O.Analyzer
-    if os.path.exists(ref_lib):
+    if have_ref:
         from oracle import ref as R
-        res["ref_s"] = timed(lambda x, e: R.qdq_per_tensor(x, e.min, e.max, 8), R.qdq_per_channel)
+        res["ref_s"] = timed(lambda x, e: R.qdq_per_tensor(x, e.min, e.max, 8), R.qdq_per_channel, outs)
         Analyzer = R.Analyzer
+    # parity of the timed CPU outputs with the GPU's (bit patterns; NaN payloads canonicalised)
+    gpu = [o[:images] for o in act_outs] + list(w_outs)
+    mism = 0
+    for want, got in zip(outs, gpu):
+        a = np.asarray(want, np.float32).ravel()
+        b = got.detach().cpu().numpy().ravel()
+        ba, bb = a.view(np.uint32).copy(), b.view(np.uint32).copy()
+        ba[np.isnan(a)] = 0x7FC00000
+        bb[np.isnan(b)] = 0x7FC00000
+        mism += int(np.count_nonzero(ba != bb)) if a.size == b.size else max(a.size, b.size)
+    res["parity"] = {"parity_checked": len(outs) == len(gpu), "elements": n, "mismatches": mism,
+                     "against": "oracle/_ref (reference C++)" if have_ref else "oracle/dlq_oracle.c"}
     # compute_encodings on the CPU (the reference analyzers, TF-Enhanced): statistics + encoding of
     # the activation sample (per-tensor) and of the first `wch` channels of every weight
-    # (per-channel, symmetric); projected to the full batch / all 27,560 channels by element and
-    # channel counts
+    # (per-channel, symmetric). The whole-batch time is a PROJECTION by element and channel counts.
     TFE = 1
     t0 = time.perf_counter()
     for x, _ in xs:
@@ -162,31 +250,75 @@ def cpu_baseline(acts, weights, act_enc, w_enc, images):
         a.update(x)
         a.compute(8)
     act_s = time.perf_counter() - t0
-    wch, nch = 32, 0
+    wch, nch, enc_mism = 32, 0, 0
+    cpu_encs = []
     t0 = time.perf_counter()
     for w, C, K, _ in ws:
         w2 = w.reshape(C, K)
+        row = []
         for c in range(min(wch, C)):
             a = Analyzer(TFE)
             a.update(w2[c])
-            a.compute(8, True)
+            row.append(a.compute(8, True).as_tuple())
             nch += 1
+        cpu_encs.append(row)
     w_s = time.perf_counter() - t0
+    for row, encs in zip(cpu_encs, w_enc):
+        enc_mism += sum(1 for c, want in enumerate(row) if encs[c].to_tuple() != want)
     n_act_sample = sum(x.size for x, _ in xs)
     n_act_full = sum(t.numel() for _, t in acts)
     c_full = sum(C for _, C, _, _ in ws)
     res["enc"] = {"sample_s": round(act_s + w_s, 3),
                   "projected_full_s": round(act_s * n_act_full / n_act_sample + w_s * c_full / nch, 2),
+                  "projected": True,
                   "sample": "TF-E statistics + encoding: the activation sample above (per-tensor) and the first %d "
-                            "channels of every weight (%d channels, per-channel symmetric); projected by element "
-                            "and channel counts to the full batch" % (wch, nch),
+                            "channels of every weight (%d channels, per-channel symmetric); projected_full_s is a "
+                            "PROJECTION by element and channel counts to the full batch, not a measurement"
+                            % (wch, nch),
+                  "weight_channel_encodings_checked": nch, "weight_channel_encoding_mismatches": enc_mism,
                   "what": "reference analyzers (oracle/_ref)" if Analyzer is not O.Analyzer
                           else "C restatement analyzers (oracle/dlq_oracle.c)"}
     return res
 
 
+def time_exchange(dev, act_quantizers, reps=20):
+    """The two collectives of one sharded calibration batch (aimet_amd.distributed) at the packed
+    sizes this workload exchanges: {-min, max} of every activation quantizer (all_reduce MAX) and
+    512 int64 bin counts + 1 element count per histogram quantizer (all_reduce SUM). Median host
+    wall time of `reps` synchronised calls, max over ranks, in ms."""
+    from aimet_amd.distributed import _all_reduce
+    n_hist = sum(1 for q in act_quantizers if q.uses_histogram)
+    bufs = (("minmax_max", torch.zeros(2 * len(act_quantizers), dtype=torch.float32, device=dev), dist.ReduceOp.MAX),
+            ("counts_sum", torch.zeros(513 * n_hist, dtype=torch.int64, device=dev), dist.ReduceOp.SUM))
+    out = {}
+    for key, t, op in bufs:
+        ts = []
+        for i in range(reps + 3):
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            _all_reduce(t, op, None)
+            torch.cuda.synchronize()
+            if i >= 3:
+                ts.append(time.perf_counter() - t0)
+        out[key] = round(_max_over_ranks(sorted(ts)[len(ts) // 2], dev) * 1e3, 4)
+        out[key + "_bytes"] = t.numel() * t.element_size()
+    return out
+
+
+def _max_over_ranks(v, dev):
+    t = torch.tensor([v], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if world_env is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus))
+    if os.environ.get("AIMET_BENCH_LAUNCH_CHECK"):
+        return launch_check(int(world_env or 1), int(os.environ.get("RANK", "0")))
     rank, world, dev = setup_dist(args)
     import aimet_amd
     from aimet_amd import _native
@@ -355,7 +487,7 @@ def main():
                                "timed step (%s)" % (len(act_calls), "graph replay" if use_graph else "eager")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images)
+        cb = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images, act_outs, outs[0::2])
         n = cb["n"]
         sample = ("first %d images of each activation tensor + all weights (%d elems), per-tensor + per-channel "
                   "QDQ with the bench's encodings, single-threaded on the host" % (args.cpu_sample_images, n))
@@ -369,11 +501,25 @@ def main():
                                       "sample": sample + "; oracle/_ref/libdlq_ref.so = the reference "
                                                 "DlQuantization CPU code compiled from its sources",
                                       "seconds": round(cb["ref_s"], 3), "port": port, "omp": omp,
-                                      "compute_encodings": cb["enc"]}
+                                      "parity": cb["parity"], "compute_encodings": cb["enc"]}
         else:
             result["cpu_baseline"] = {"value": port["value"], "unit": "Gelem/s", "cores": 1, "kind": "port",
                                       "sample": sample + "; " + port["what"], "seconds": port["seconds"],
-                                      "omp": omp, "compute_encodings": cb["enc"]}
+                                      "omp": omp, "parity": cb["parity"], "compute_encodings": cb["enc"]}
+    if world > 1:
+        # the calibration exchange of this workload: what formed, and the two collectives' cost
+        result["config"]["dist_backend"] = dist.get_backend()
+        result["config"]["world_formed"] = dist.get_world_size()
+        result["config"]["allreduce_ms"] = time_exchange(dev, aq)
+        result["config"]["allreduce_timing"] = ("median of 20 synchronised calls per collective, max over ranks; "
+                                                "one MAX + one SUM per calibration batch")
+        # the encodings every rank computed must agree (they are reduced from the same global stats)
+        sig = torch.tensor([hash(tuple(e.to_tuple() for e in act_enc)) & 0x7FFFFFFFFFFF], dtype=torch.int64,
+                           device=dev if dist.get_backend() == "nccl" else "cpu")
+        lo, hi = sig.clone(), sig.clone()
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        result["config"]["encodings_identical_across_ranks"] = bool(lo.item() == hi.item())
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

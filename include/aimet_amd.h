@@ -232,6 +232,11 @@ int aimet_tq_batch_histogram_many(aimet_tensor_quantizer* const* qs, const float
                                   int64_t count, void* stream);
 int aimet_tq_fold_histogram_many(aimet_tensor_quantizer* const* qs, const int64_t* counts, int64_t count,
                                  void* stream);
+/* The same with the element counts read on the device from counts_dev[0..count) (int64 in HBM): the
+ * sharded calibration sums them over ranks in the same all_reduce as the bin counts, so the fold
+ * needs no host round trip. */
+int aimet_tq_fold_histogram_many_dev(aimet_tensor_quantizer* const* qs, const int64_t* counts_dev, int64_t count,
+                                     void* stream);
 /* updateStats of many quantizers of any channel count, each tensor viewed as [outers[i]][Cs[i]][Ks[i]]
  * (Cs[i] == num_channels of qs[i]), in two launches with one workgroup per channel: the weight
  * quantizers of a model (v1/tensor_quantizer.py:535-571 per weight, batched). Equivalent to
