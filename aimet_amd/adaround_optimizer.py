@@ -131,7 +131,7 @@ class _BoundSoftQuant:
         self.pd, self.po = P(self.d), P(self.o)
         self.pl = P(round_loss_out) if round_loss_out is not None else None
         self.reg = self.beta = 0.0
-        self.reg_beta = None   # graph mode: device tensor [reg, beta] read by the backward kernel
+        self.reg_beta = None   # graph mode: device tensor [reg, beta, beta - 1] read by the backward kernel
 
     def _stream(self):
         # the current stream at call time: a HIP-graph capture runs on torch's capture stream
@@ -154,7 +154,7 @@ class _BoundSoftQuant:
                               self.pl, self._stream())
         else:
             rc = self.bwd(self.pw, self.pa, ctypes.c_void_p(g.data_ptr()), ctypes.c_void_p(ga.data_ptr()),
-                          *self.shape, self.pd, self.po, self.bw, ctypes.c_float(self.reg), ctypes.c_float(self.beta),
+                          *self.shape, self.pd, self.po, self.bw, ctypes.c_double(self.reg), ctypes.c_double(self.beta),
                           self.pl if self.reg != 0.0 else None, self._stream())
         if rc:
             _native.check(rc)
@@ -274,10 +274,12 @@ class AdaroundOptimizer:
             staged.append(h)   # alive until the copies have run (synchronised below)
 
         draw(0, min(chunk, iters))
-        rb_all = torch.tensor([(0.0, 0.0) if it < warm else
-                               (opt_params.reg_param, compute_beta(iters, it, opt_params.beta_range,
-                                                                   opt_params.warm_start))
-                               for it in range(iters)], dtype=torch.float32, device=dev)
+        # {reg, beta, beta - 1} of every iteration, formed in double as the reference's python / ATen
+        # pow_backward do, then stored as float32 (the kernel's arithmetic type)
+        rb_all = torch.tensor([(0.0, 0.0, 0.0) if it < warm else
+                               (lambda b: (opt_params.reg_param, b, b - 1.0))(
+                                   compute_beta(iters, it, opt_params.beta_range, opt_params.warm_start))
+                               for it in range(iters)], dtype=torch.float64).to(torch.float32).to(dev)
         it_buf = torch.zeros(1, dtype=torch.long, device=dev)
         alpha.grad = torch.zeros_like(alpha)
 

@@ -7,7 +7,15 @@
 //
 // Here: one pass forward (reads W, alpha; writes Wq: 12 B/elem) and one pass backward (reads
 // grad_Wq, W, alpha; writes grad_alpha: 16 B/elem) that also produces the rounding-loss term
-// and its gradient. Floating-point results follow torch float32 op order (tolerance-checked).
+// and its gradient.
+//
+// Numerics: the reference's arithmetic is torch float32 ops on the CPU; every op here is the same
+// IEEE operation in the same order, and the sigmoid is torch's own vectorized CPU sigmoid
+// (1 / (1 + expf(-a)) with Sleef's expf_u10 polynomial, FMA form, then an IEEE divide), so Wq and
+// the reconstruction part of dL/dalpha are bit-identical to the reference
+// (tests/golden/golden_adaround.npz). The rounding-loss gradient uses a correctly rounded
+// pow(|2h-1|, beta-1) (double) where torch uses Sleef's powf_u10: identical except where that
+// pow is not correctly rounded (measured bound in DESIGN.md §2).
 #include "common.hpp"
 
 namespace aimet_amd
@@ -35,12 +43,60 @@ struct AdaChannel
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-// sigmoid with the hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32, ~1 ulp each): within a
-// few ulp of torch's 1/(1+expf(-a)); h enters Wq additively inside the clamp (no rounding after
-// it), so Wq stays within the tests' 1e-6 absolute tolerance, and dL/dalpha within 1e-5 relative.
+// expf as torch's CPU vector code computes it (ATen Vectorized<float>::exp = Sleef expf_u10):
+// q = rint(d * log2(e)); s = d - q*ln2 in two FMA steps (Cody-Waite); a degree-6 polynomial in
+// Horner FMA form; 2^q applied as two exact power-of-two multiplies (Sleef's vldexp2, so the
+// subnormal results round as there); d < -104 -> 0, d > 100 -> inf. Every step is an IEEE op, so
+// the result is Sleef's bit for bit. A correctly rounded expf would differ from it in ~1% of inputs
+// and the difference reaches Wq unattenuated where floor(W/delta) + h - offset nearly cancels.
+__device__ __forceinline__ float torch_cpu_expf(float d)
+{
+    const float qf = __builtin_rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
+    const int q    = (int) qf;
+    float s        = __builtin_fmaf(qf, -0.693145751953125f, d);
+    s              = __builtin_fmaf(qf, -1.428606765330187045e-06f, s);
+    float u        = 0.000198527617612853646278381f;
+    u              = __builtin_fmaf(u, s, 0.00139304355252534151077271f);
+    u              = __builtin_fmaf(u, s, 0.00833336077630519866943359f);
+    u              = __builtin_fmaf(u, s, 0.0416664853692054748535156f);
+    u              = __builtin_fmaf(u, s, 0.166666671633720397949219f);
+    u              = __builtin_fmaf(u, s, 0.5f);
+    u              = 1.0f + __builtin_fmaf(s * s, u, s);
+    const int q1   = q >> 1, q2 = q - q1;
+    u              = u * __int_as_float((q1 + 127) << 23);
+    u              = u * __int_as_float((q2 + 127) << 23);
+    u              = d < -104.0f ? 0.0f : u;
+    return d > 100.0f ? __builtin_inff() : u;
+}
+
+// torch.clamp(x, lo, hi) on the CPU (vectorized kernel: NaN propagates; maximum / minimum are
+// x86 MAXPS / MINPS, which return the second operand unless the first is strictly greater / less,
+// so clamp(-0.0, 0, 1) is +0.0)
+__device__ __forceinline__ float clamp_torch(float x, float lo, float hi)
+{
+    if (x != x)
+        return x;
+    const float m = x > lo ? x : lo;
+    return m < hi ? m : hi;
+}
+
+// torch.sigmoid on the CPU (vectorized kernel): a = 0 - a; a = exp(a); a = a + 1; 1 / a
 __device__ __forceinline__ float sigmoidf(float a)
 {
-    return __builtin_amdgcn_rcpf(1.0f + __expf(-a));
+    return 1.0f / (torch_cpu_expf(0.0f - a) + 1.0f);
+}
+
+// x^e for x in [0, 1], correctly rounded from double (torch: Sleef powf_u10, or x*x*x for e == 3,
+// ATen pow_tensor_scalar_optimized_kernel)
+__device__ __forceinline__ float pow01(float x, float e)
+{
+    if (e == 2.0f)
+        return x * x;
+    if (e == 3.0f)
+        return x * x * x;
+    if (x == 0.0f)
+        return e == 0.0f ? 1.0f : 0.0f;
+    return (float) exp((double) e * log((double) x));
 }
 
 // floor(w / d) exactly as the IEEE division gives it, from q = w * rcp (rcp = v_rcp_f32(d), within
@@ -56,16 +112,9 @@ __device__ __forceinline__ float floor_div(float w, float d, float rcp)
     return __builtin_floorf(w / d);
 }
 
-// |x|^beta for x in [0, 1] (the rounding-loss power): exp2(beta * log2 x) on the hardware
-// transcendental unit; the reference's (torch) powf differs by a few ulp
-__device__ __forceinline__ float pow01(float ax, float beta)
-{
-    return ax > 0.0f ? exp2f(beta * __log2f(ax)) : (beta == 0.0f ? 1.0f : 0.0f);
-}
-
 struct AdaParams
 {
-    float qmax, reg, beta;
+    float qmax, reg, beta, beta_m1;   // beta_m1 = (float)(beta - 1) in double, as torch's pow_backward
     int soft;
 };
 
@@ -76,11 +125,11 @@ __device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, con
     if (p.soft)
     {
         float pre = sigmoidf(a) * kZmG + kGamma;
-        h         = fminf(fmaxf(pre, 0.0f), 1.0f);
+        h         = clamp_torch(pre, 0.0f, 1.0f);
     }
     else
         h = a >= 0.0f ? 1.0f : 0.0f;
-    float q = fminf(fmaxf(t + h - o, 0.0f), p.qmax);
+    float q = clamp_torch(t + h - o, 0.0f, p.qmax);
     return (q + o) * d;
 }
 
@@ -91,23 +140,27 @@ __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, flo
     float t   = floor_div(w, d, rcp);
     float sg  = sigmoidf(a);
     float pre = sg * kZmG + kGamma;
-    float h   = fminf(fmaxf(pre, 0.0f), 1.0f);
+    float h   = clamp_torch(pre, 0.0f, 1.0f);
     float u   = t + h - o;
-    // d wq / d h = delta inside the clamp window (torch clamp_backward: min <= x <= max)
-    float gh = (u >= 0.0f && u <= p.qmax) ? g * d : 0.0f;
+    // autograd of apply_adaround, op by op: d wq / d tq = g * delta; clamp_backward passes it where
+    // min <= x <= max; the adds pass it on; h's clamp likewise; mul by (zeta - gamma) -> * 1.2f;
+    // sigmoid_backward: (grad * (1 - s)) * s
+    const bool in_h = pre >= 0.0f && pre <= 1.0f;
+    float gh        = (u >= 0.0f && u <= p.qmax) ? g * d : 0.0f;
+    float ga        = ((in_h ? gh : 0.0f) * kZmG * (1.0f - sg)) * sg;
     if (p.reg != 0.0f)
     {
-        float x  = 2.0f * h - 1.0f;
+        // compute_round_loss's own graph (adaround_loss.py:97-110), summed into alpha's gradient
+        // as autograd does: round_loss = reg * sum(1 - |2h - 1|^beta)
+        float x  = 2.0f * h + -1.0f;
         float ax = fabsf(x);
-        float pw = pow01(ax, p.beta);
-        loss += 1.0f - pw;
-        // d/dh [reg * (1 - |2h-1|^beta)] = -reg * beta * |x|^(beta-1) * sign(x) * 2
-        float dp = (ax > 0.0f) ? p.beta * (pw * __builtin_amdgcn_rcpf(ax)) * (x > 0.0f ? 1.0f : -1.0f) : 0.0f;
-        gh += -p.reg * dp * 2.0f;
+        loss += 1.0f - pow01(ax, p.beta);
+        // grad -reg at the pow; pow_backward: grad * (beta * x^(beta - 1)); abs: * sgn(x); 2*h: * 2
+        float dpw = (-p.reg) * (p.beta * pow01(ax, p.beta_m1));
+        float dh  = (dpw * (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f))) * 2.0f;
+        ga += ((in_h ? dh : 0.0f) * kZmG * (1.0f - sg)) * sg;
     }
-    // h = clamp(pre, 0, 1); pre = sigmoid(a) * (zeta - gamma) + gamma
-    float gpre = (pre >= 0.0f && pre <= 1.0f) ? gh : 0.0f;
-    return gpre * kZmG * (1.0f - sg) * sg;
+    return ga;
 }
 
 // 16-B streaming form: four consecutive elements share a channel (K % 4 == 0 or C == 1);
@@ -169,10 +222,11 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
                                                                   float* __restrict__ round_loss,
                                                                   const float* __restrict__ reg_beta)
 {
-    if (reg_beta)   // device-resident {reg, beta}: a HIP-graph replay per iteration
+    if (reg_beta)   // device-resident {reg, beta, beta - 1}: a HIP-graph replay per iteration
     {
-        p.reg  = reg_beta[0];
-        p.beta = reg_beta[1];
+        p.reg     = reg_beta[0];
+        p.beta    = reg_beta[1];
+        p.beta_m1 = reg_beta[2];
     }
     float loss = 0.0f;
     constexpr int U       = 4;   // quads in flight per lane (3 x 16-B loads each)
@@ -224,8 +278,9 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
 {
     if (reg_beta)
     {
-        p.reg  = reg_beta[0];
-        p.beta = reg_beta[1];
+        p.reg     = reg_beta[0];
+        p.beta    = reg_beta[1];
+        p.beta_m1 = reg_beta[2];
     }
     float loss = 0.0f;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
@@ -315,7 +370,7 @@ int aimet_adaround_forward(const float* w, const float* alpha, float* wq, int64_
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, soft};
+        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, soft};
         if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(wq))
         {
             uint32_t nq = (uint32_t) (n / 4);
@@ -336,7 +391,7 @@ namespace
 {
 
 int adaround_backward(const float* w, const float* alpha, const float* g, float* ga, int64_t outer, int64_t C,
-                      int64_t K, const float* delta, const float* offset, int32_t bw, float reg, float beta,
+                      int64_t K, const float* delta, const float* offset, int32_t bw, double reg, double beta,
                       const float* reg_beta, float* round_loss, void* stream)
 {
     return guarded([&] {
@@ -352,7 +407,7 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        AdaParams p {(float) ((1ull << bw) - 1), reg, beta, 1};
+        AdaParams p {(float) ((1ull << bw) - 1), (float) reg, (float) beta, (float) (beta - 1.0), 1};
         if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(g) &&
             aligned16(ga))
         {
@@ -375,7 +430,7 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
 extern "C" {
 
 int aimet_adaround_backward(const float* w, const float* alpha, const float* g, float* ga, int64_t outer, int64_t C,
-                            int64_t K, const float* delta, const float* offset, int32_t bw, float reg, float beta,
+                            int64_t K, const float* delta, const float* offset, int32_t bw, double reg, double beta,
                             float* round_loss, void* stream)
 {
     return adaround_backward(w, alpha, g, ga, outer, C, K, delta, offset, bw, reg, beta, nullptr, round_loss, stream);
@@ -428,7 +483,7 @@ int aimet_adaround_backward_dev(const float* w, const float* alpha, const float*
     });
     if (rc != AIMET_OK)
         return rc;
-    return adaround_backward(w, alpha, g, ga, outer, C, K, delta, offset, bw, 0.0f, 0.0f, reg_beta_dev, round_loss,
+    return adaround_backward(w, alpha, g, ga, outer, C, K, delta, offset, bw, 0.0, 0.0, reg_beta_dev, round_loss,
                              stream);
 }
 

@@ -281,22 +281,43 @@ class StaticGridPerChannelQuantizer(StaticGridTensorQuantizer):
 # ---------------------------------------------------------------------------------------------
 # autograd
 # ---------------------------------------------------------------------------------------------
+def _is_scalar_bound(v):
+    """A bound the reference's broadcast_to_tensor turns into a 0-dim tensor (a python number or a
+    0-dim tensor). A list or a 1-D tensor, even of one element, stays 1-D
+    (quantsim_straight_through_grad.py:66-88)."""
+    return isinstance(v, (int, float)) or (torch.is_tensor(v) and v.dim() == 0)
+
+
+def _scalar_bound(v, dtype):
+    """The value the reference compares x with for a scalar bound: broadcast_to_tensor makes a
+    python number a 0-dim tensor (torch.tensor(float) is float32), and a 0-dim tensor takes no part
+    in type promotion, so `encoding_min <= x` runs in x's dtype with the bound rounded to it
+    (float32 -> fp16/bf16 for a python float: two roundings)."""
+    t = v.detach().cpu() if torch.is_tensor(v) else torch.tensor(v)
+    return float(t.to(dtype))
+
+
 def compute_dloss_by_dx(x, grad, encoding_min, encoding_max, ch_axis=0):
     """quantsim_straight_through_grad.py:91-118 as one kernel: grad * (min <= x <= max).
 
-    encoding_min/max: python floats (per-tensor) or sequences / float32 tensors of C values."""
+    encoding_min/max: python floats / 0-dim tensors (per-tensor: compared in x's dtype, as the
+    reference's 0-dim bound is) or sequences / 1-D tensors of C values (compared in float32, the
+    promoted type of the reference's 1-D float32 bound tensor)."""
     _require_gpu(x, True, "x", allow_16bit=True)
     _require_gpu(grad, True, "grad", allow_16bit=True)
     x = x.contiguous()
     grad = grad.contiguous()
+    if _is_scalar_bound(encoding_min) and x.dtype in IO_DTYPES:
+        # rounded to x's dtype before any upcast: the mask is the reference's 16-bit compare
+        encoding_min, encoding_max = _scalar_bound(encoding_min, x.dtype), _scalar_bound(encoding_max, x.dtype)
     if x.dtype in IO_DTYPES and grad.dtype == x.dtype:
         return _ste_16(x, grad, encoding_min, encoding_max, ch_axis)
     if x.dtype != torch.float32 or grad.dtype != torch.float32:
         return compute_dloss_by_dx(x.float(), grad.float(), encoding_min, encoding_max, ch_axis).to(grad.dtype)
     out = torch.empty_like(grad)
-    if isinstance(encoding_min, (int, float)) or (torch.is_tensor(encoding_min) and encoding_min.numel() == 1):
-        mn = float(encoding_min)
-        mx = float(encoding_max)
+    if _is_scalar_bound(encoding_min):
+        mn = _scalar_bound(encoding_min, torch.float32)
+        mx = _scalar_bound(encoding_max, torch.float32)
         # torch.tensor(python float) is float32: the comparison bounds are rounded to float
         with torch.cuda.device(x.device):
             _native.call("aimet_ste_backward_per_tensor", x.data_ptr(), grad.data_ptr(), out.data_ptr(), x.numel(),
@@ -314,11 +335,13 @@ def compute_dloss_by_dx(x, grad, encoding_min, encoding_max, ch_axis=0):
 
 
 def _ste_16(x, grad, encoding_min, encoding_max, ch_axis):
-    """fp16 / bf16 STE in one pass (aimet_ste_backward_16): float(x) vs the float32 bounds."""
+    """fp16 / bf16 STE in one pass (aimet_ste_backward_16): float(x) vs float32 bounds. Scalar
+    bounds arrive already rounded to x's dtype (compute_dloss_by_dx), so the float32 compare is
+    the reference's 16-bit one; per-channel bounds are float32, as the reference's promoted ones."""
     out = torch.empty_like(grad)
     code = IO_DTYPES[x.dtype]
     with torch.cuda.device(x.device):
-        if isinstance(encoding_min, (int, float)) or (torch.is_tensor(encoding_min) and encoding_min.numel() == 1):
+        if _is_scalar_bound(encoding_min):
             _native.call("aimet_ste_backward_16", x.data_ptr(), grad.data_ptr(), out.data_ptr(), 1, 1, x.numel(), code,
                          None, None, float(encoding_min), float(encoding_max), _stream(x))
             return out
@@ -380,10 +403,10 @@ class QuantizeDequantize(torch.autograd.Function):
         if tq.enabled and tq.data_type == QuantizationDataType.int and tq.bitwidth != 32:
             (x,) = ctx.saved_tensors
             dtype = grad.dtype
-            if x.dtype == dtype and dtype in IO_DTYPES:
-                xf, gf = x, grad          # fused 16-bit STE
-            else:
-                xf, gf = x.to(torch.float32), grad.to(torch.float32)
+            # fp16 / bf16 x stays in its dtype: a scalar bound is compared in x's dtype, as in the
+            # reference (compute_dloss_by_dx rounds it, then fuses or upcasts)
+            xf = x if x.dtype in IO_DTYPES else x.to(torch.float32)
+            gf = grad if grad.dtype in IO_DTYPES else grad.to(torch.float32)
             if isinstance(tq, StaticGridPerChannelQuantizer):
                 mins, maxs = _ste_bounds(tq, x.device)
                 g = compute_dloss_by_dx(xf, gf, mins, maxs, tq.channel_axis)

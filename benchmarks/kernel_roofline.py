@@ -218,8 +218,8 @@ def main():
     t_ms = timed(lambda: T.adaround_forward(wv, av, d_b, o_b, 8), 2, stream)
     row("adaround_forward", "a15", 12, ms, None, t_ms)
     ms = timed(lambda: (rloss.zero_(), lib.aimet_adaround_backward(P(w), P(alpha), P(grad), P(gx), 1, C, K, P(delta),
-                                                                     P(offset), 8, ctypes.c_float(0.01),
-                                                                     ctypes.c_float(10.0), P(rloss), sp)),
+                                                                     P(offset), 8, ctypes.c_double(0.01),
+                                                                     ctypes.c_double(10.0), P(rloss), sp)),
                args.reps, stream)
 
     def torch_ada_bwd():

@@ -291,25 +291,29 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
 
 /* Wq = (clamp(floor(W/delta) + h(alpha) - offset, 0, 2^bw-1) + offset) * delta,
  * h = clamp(sigmoid(alpha)*(zeta-gamma)+gamma, 0, 1) (soft) or (alpha >= 0) (hard).
- * delta/offset broadcast along the channel axis of [outer][C][K] (per-tensor: C == 1). */
+ * delta/offset broadcast along the channel axis of [outer][C][K] (per-tensor: C == 1).
+ * Bit-identical to the reference's torch float32 ops on the CPU (torch's vectorized sigmoid). */
 int aimet_adaround_forward(const float* w, const float* alpha, float* wq, int64_t outer, int64_t C, int64_t K,
                            const float* delta_dev, const float* offset_dev, int32_t bw, int use_soft_rounding,
                            void* stream);
-/* dL/dalpha of the forward above (clamp pass-through masks as torch autograd) plus, when
- * reg_param != 0, the round-loss gradient reg*d/dalpha sum(1-|2h-1|^beta), and the round loss
- * itself accumulated into round_loss_dev[0] (fp32, atomically; caller zeroes it). */
+/* dL/dalpha of the forward above (torch autograd of apply_adaround, op by op) plus, when
+ * reg_param != 0, the round-loss gradient d/dalpha reg*sum(1-|2h-1|^beta) added as autograd adds
+ * the two branches, and the round loss itself accumulated into round_loss_dev[0] (fp32,
+ * atomically; caller zeroes it). reg_param / beta are the reference's python doubles (beta - 1 is
+ * formed in double, as torch's pow_backward does). */
 int aimet_adaround_backward(const float* w, const float* alpha, const float* grad_wq, float* grad_alpha,
                             int64_t outer, int64_t C, int64_t K, const float* delta_dev, const float* offset_dev,
-                            int32_t bw, float reg_param, float beta, float* round_loss_dev, void* stream);
-/* The same with {reg_param, beta} read from device memory (reg_beta_dev[2]) when the kernel runs:
- * the AdaRound iteration captured once in a HIP graph and replayed with the annealed beta of
- * each iteration (adaround_optimizer.py:115-222's loop; aimet_amd.adaround_optimizer). */
+                            int32_t bw, double reg_param, double beta, float* round_loss_dev, void* stream);
 /* adaround_loss.py:70-80 compute_recon_loss + its autograd backward in one pass: grad[i] =
  * d/dq of mean(||act(q) - act(t)||^2 over dim 1) = 2 (act(q) - act(t)) act'(q) / (n / reduced),
  * where `reduced` is the size of dim 1 (channels / features) and act is 0 none, 1 ReLU,
  * 2 ReLU6 (the layer's following activation, applied to both outputs as the reference does). */
 int aimet_adaround_recon_grad(const float* quant_out, const float* orig_out, float* grad, int64_t n, int64_t reduced,
                               int act, void* stream);
+/* aimet_adaround_backward with {reg_param, beta, beta - 1} read from device memory
+ * (reg_beta_dev[3], float32) when the kernel runs: the AdaRound iteration captured once in a HIP
+ * graph and replayed with the annealed beta of each iteration (adaround_optimizer.py:115-222's
+ * loop; aimet_amd.adaround_optimizer). */
 int aimet_adaround_backward_dev(const float* w, const float* alpha, const float* grad_wq, float* grad_alpha,
                                 int64_t outer, int64_t C, int64_t K, const float* delta_dev, const float* offset_dev,
                                 int32_t bw, const float* reg_beta_dev, float* round_loss_dev, void* stream);

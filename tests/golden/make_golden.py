@@ -14,6 +14,12 @@ Sources of truth, in order:
     for the STE mask and the AdaRound round-loss/beta.
   * torch CPU float32 ops in exactly the sequence of AimetTensorQuantizer.cpp:236-299 for the
     per-channel encoding tables (that is what the reference executes on that path).
+  * AdaroundWrapper.apply_adaround / _generate_alpha_parameter (adaround_wrapper.py:124-149,
+    211-224): the module cannot be imported here (its import chain needs bokeh, jsonschema,
+    torchvision, spconv and the aimet_torch.v1.nn package the reference snapshot lacks), so the
+    generator parses the reference file, takes those two function definitions as they stand and
+    executes them (torch CPU, one thread) with the attributes they read. Nothing of that source is
+    written anywhere; only inputs and outputs are stored (golden_adaround.npz).
 
 The fixtures are data (inputs + expected outputs); no reference source text is stored.
 """
@@ -258,7 +264,154 @@ def broadcast_golden():
     np.savez_compressed(os.path.join(HERE, "golden_broadcast.npz"), **g)
 
 
+def _reference_adaround_functions():
+    """apply_adaround and _generate_alpha_parameter exactly as the reference defines them
+    (adaround_wrapper.py), compiled from the reference file at generation time."""
+    import ast
+    for p in ("TrainingExtensions/torch/src/python", "TrainingExtensions/common/src/python"):
+        sys.path.insert(0, os.path.join(REF_ROOT, p))
+    from aimet_common.defs import AdaroundConstants
+    path = os.path.join(REF_ROOT, "TrainingExtensions/torch/src/python/aimet_torch/v1/adaround/adaround_wrapper.py")
+    tree = ast.parse(open(path).read(), path)
+    cls = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == "AdaroundWrapper")
+    fns = [n for n in cls.body if isinstance(n, ast.FunctionDef) and n.name in ("apply_adaround",
+                                                                                "_generate_alpha_parameter")]
+    for f in fns:
+        f.decorator_list = []
+    mod = ast.Module(body=fns, type_ignores=[])
+    ns = {"torch": torch, "AdaroundConstants": AdaroundConstants, "Tuple": tuple}
+    exec(compile(mod, path, "exec"), ns)
+    return ns["apply_adaround"], ns["_generate_alpha_parameter"]
+
+
+# MobileNet-v2 weight shapes (conv / depthwise / pointwise / classifier) + a ragged one
+ADAROUND_CASES = [   # (shape, bitwidth, alpha source)
+    ((32, 3, 3, 3), 8, "init"), ((32, 1, 3, 3), 8, "init"), ((96, 1, 3, 3), 4, "init"),
+    ((16, 32, 1, 1), 4, "wide"), ((64, 24, 1, 1), 8, "wide"), ((160, 320, 1, 1), 8, "init"),
+    ((100, 1280), 4, "wide"), ((24, 1, 3, 3), 8, "tails"), ((7, 5, 3, 3), 4, "wide"),
+]
+
+
+def adaround_golden():
+    """golden_adaround.npz: forward Wq of the reference's apply_adaround and d(loss)/d(alpha)
+    through torch autograd of the reference expressions, for (a) a reconstruction-like loss
+    sum(Wq * g) alone (warm start: no rounding loss) and (b) plus the reference's
+    AdaroundLoss.compute_round_loss after warm start. Per-channel symmetric delta / offset along
+    axis 0 (broadcast_to_tensor form), torch CPU float32 on ONE thread, so every element except a
+    tensor's last numel % 32 takes torch's vectorized sigmoid (Sleef expf_u10 + IEEE divide)."""
+    from types import SimpleNamespace
+    apply_adaround, gen_alpha = _reference_adaround_functions()
+    _, AdaroundLoss, AdaroundHyperParameters = reference_python()
+    torch.set_num_threads(1)
+    g = torch.Generator().manual_seed(20251107)
+    hp = AdaroundHyperParameters(num_iterations=10000, reg_param=0.01, beta_range=(20, 2), warm_start=0.2)
+    out = {}
+    for i, (shape, bw, src) in enumerate(ADAROUND_CASES):
+        C = shape[0]
+        w = torch.randn(shape, generator=g) * (0.05 + 0.3 * torch.rand(C, *[1] * (len(shape) - 1), generator=g))
+        steps = 2 ** bw - 1
+        absmax = w.reshape(C, -1).abs().amax(1)
+        # symmetric encodings (quantization_utils.cpp:83-93 form), float32 as makeDeltaOffsetTensor gives them
+        delta = (absmax / float(steps // 2)).float()
+        offset = torch.full((C,), -float((steps + 1) // 2))
+        bshape = (C,) + (1,) * (len(shape) - 1)
+        bd, bo = delta.view(bshape), offset.view(bshape)
+        if src == "init":
+            alpha = gen_alpha(w, bd).detach()
+        elif src == "wide":
+            alpha = torch.randn(shape, generator=g) * 4.0
+        else:   # sigmoid's saturated tails and |alpha| near the exp under/overflow range
+            alpha = (torch.rand(shape, generator=g) * 2 - 1) * 110.0
+        mod = SimpleNamespace(alpha=alpha.clone().requires_grad_(True), broadcasted_delta=bd, broadcasted_offset=bo,
+                              use_soft_rounding=True, clip_min=0, clip_max=steps)
+        wq = apply_adaround(mod, w)
+        grad = torch.randn(shape, generator=g) * 1e-3
+        (wq * grad).sum().backward()
+        ga_recon = mod.alpha.grad.detach().clone()
+        # + the rounding loss at iteration 6000 of 10000 (after the 20% warm start)
+        mod.alpha.grad = None
+        wq2 = apply_adaround(mod, w)
+        loss = (wq2 * grad).sum() + AdaroundLoss.compute_round_loss(mod.alpha, hp, 6000)
+        loss.backward()
+        ga_total = mod.alpha.grad.detach().clone()
+        round_loss = float(AdaroundLoss.compute_round_loss(mod.alpha.detach(), hp, 6000))
+        beta = float(AdaroundLoss._compute_beta(10000, 6000, (20, 2), 0.2))
+        # hard rounding (use_soft_rounding False)
+        mod.use_soft_rounding = False
+        wq_hard = apply_adaround(mod, w).detach()
+        k = "c%d_" % i
+        out[k + "w"], out[k + "alpha"], out[k + "delta"], out[k + "offset"] = (w.numpy(), alpha.numpy(),
+                                                                             delta.numpy(), offset.numpy())
+        out[k + "bw"] = np.array(bw)
+        out[k + "grad"], out[k + "wq"], out[k + "wq_hard"] = grad.numpy(), wq.detach().numpy(), wq_hard.numpy()
+        out[k + "ga_recon"], out[k + "ga_total"] = ga_recon.numpy(), ga_total.numpy()
+        out[k + "round_loss"], out[k + "beta"] = np.array(round_loss), np.array(beta)
+        if src == "init":
+            out[k + "alpha_init"] = alpha.numpy()   # _generate_alpha_parameter(w, delta)
+    out["count"] = np.array(len(ADAROUND_CASES))
+    out["reg_param"], out["cur_iter"] = np.array(0.01), np.array(6000)
+    np.savez_compressed(os.path.join(HERE, "golden_adaround.npz"), **out)
+
+
+def ste16_golden():
+    """golden_ste16.npz: the reference compute_dloss_by_dx with fp16 / bf16 x and grad, per-tensor
+    python-float bounds that are NOT representable in the 16-bit type (broadcast_to_tensor makes
+    them 0-dim float32 tensors: compared in x's dtype) and per-channel lists (1-D float32: compared
+    in float32), with x values placed exactly on and next to the rounded bounds; plus bf16 x with
+    an fp32 grad (mixed dtypes)."""
+    ste, _, _ = reference_python()
+    g = torch.Generator().manual_seed(77)
+    out = {}
+    cases = []
+    for dt in (torch.float16, torch.bfloat16):
+        for mn, mx in ((-0.1, 0.1), (-1.2345678, 2.7182818), (0.30000001, 0.7), (-3.1415926, -0.01)):
+            cases.append((dt, dt, mn, mx))
+    cases.append((torch.bfloat16, torch.float32, -0.1, 0.1))
+    cases.append((torch.float16, torch.float32, -1.2345678, 2.7182818))
+    for i, (xd, gd, mn, mx) in enumerate(cases):
+        x = (torch.randn(4096, generator=g) * max(abs(mn), abs(mx)) * 1.3).to(xd)
+        # the rounded bounds and their 16-bit neighbours
+        for j, b in enumerate((mn, mx)):
+            rb = torch.tensor(b).to(xd)
+            nb = torch.stack([rb, torch.nextafter(rb.float(), torch.tensor(1e9)).to(xd),
+                              torch.nextafter(rb.float(), torch.tensor(-1e9)).to(xd)])
+            x[100 * j:100 * j + 60] = nb.repeat(20)
+        grad = torch.randn(4096, generator=g).to(gd)
+        out["t%d_x" % i] = x.view(torch.int16).numpy()
+        out["t%d_grad" % i] = grad.view(torch.int16).numpy() if gd != torch.float32 else grad.numpy()
+        out["t%d_dtypes" % i] = np.array([str(xd), str(gd)])
+        out["t%d_bounds" % i] = np.array([mn, mx])
+        out["t%d_pt" % i] = _as_bits(ste.compute_dloss_by_dx(x, grad, mn, mx))
+    # per-channel lists (C = 1 included: a 1-D bound, compared in float32)
+    for C in (1, 8):
+        for dt in (torch.float16, torch.bfloat16):
+            x = (torch.randn(C, 256, generator=g) * 0.2).to(dt)
+            grad = torch.randn(C, 256, generator=g).to(dt)
+            mins = [-0.1 - 0.013 * c for c in range(C)]
+            maxs = [0.1 + 0.017 * c for c in range(C)]
+            for c in range(C):
+                x[c, :3] = torch.tensor(mins[c]).to(dt)
+                x[c, 3:6] = torch.tensor(maxs[c]).to(dt)
+            k = "p%d_%s_" % (C, str(dt).split(".")[1])
+            out[k + "x"] = x.view(torch.int16).numpy()
+            out[k + "grad"] = grad.view(torch.int16).numpy()
+            out[k + "mins"], out[k + "maxs"] = np.array(mins), np.array(maxs)
+            out[k + "out"] = _as_bits(ste.compute_dloss_by_dx(x, grad, mins, maxs, ch_axis=0))
+    out["count"] = np.array(len(cases))
+    np.savez_compressed(os.path.join(HERE, "golden_ste16.npz"), **out)
+
+
+def _as_bits(t):
+    return t.view(torch.int16).numpy() if t.dtype in (torch.float16, torch.bfloat16) else t.numpy()
+
+
 def main():
+    if "--adaround-only" in sys.argv:
+        adaround_golden()
+        return
+    if "--ste16-only" in sys.argv:
+        ste16_golden()
+        return
     if "--broadcast-only" in sys.argv:
         broadcast_golden()
         return
@@ -419,6 +572,8 @@ def main():
     }
     with open(os.path.join(HERE, "kat.json"), "w") as f:
         json.dump(kat, f, indent=1)
+    adaround_golden()
+    ste16_golden()
     print("golden fixtures written to", HERE)
 
 

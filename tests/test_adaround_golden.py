@@ -1,0 +1,168 @@
+"""AdaRound soft rounding against the reference's own arithmetic (tests/golden/golden_adaround.npz:
+AdaroundWrapper.apply_adaround / _generate_alpha_parameter and AdaroundLoss.compute_round_loss
+executed by make_golden.py on torch CPU float32, one thread) on MobileNet-v2 weight shapes
+(conv, depthwise [C,1,3,3], pointwise, classifier, a ragged [7,5,3,3]), 4 and 8 bits, alpha from
+the reference's initialisation, N(0, 4) and U(-110, 110) (the sigmoid's saturated tails and the
+exp underflow / overflow range).
+
+Bars (north_star "within 1 ULP on the dequantized float tensor"):
+* Wq (soft and hard rounding): bit-exact;
+* dL/dalpha of the reconstruction term (warm start, no rounding loss): bit-exact;
+* dL/dalpha with the rounding loss: the difference is confined to the rounding-loss branch, whose
+  pow(|2h-1|, beta-1) is correctly rounded here and Sleef powf_u10 in torch: |diff| <= 2^-21 x
+  |that branch's contribution| + 1 ulp of the result;
+* the rounding loss value: rtol 1e-5 (float32 sums in a different order)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")]
+
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module")
+def gad(golden_dir):
+    import os
+    return dict(np.load(os.path.join(golden_dir, "golden_adaround.npz")))
+
+
+def _case(z, i):
+    k = "c%d_" % i
+    return {n: z[k + n] for n in ("w", "alpha", "delta", "offset", "grad", "wq", "wq_hard", "ga_recon", "ga_total",
+                                  "round_loss", "beta")} | {"bw": int(z[k + "bw"])}
+
+
+def _ulps(a, b):
+    a = np.asarray(a, np.float32).ravel().view(np.int32).astype(np.int64)
+    b = np.asarray(b, np.float32).ravel().view(np.int32).astype(np.int64)
+    a = np.where(a < 0, -(a & 0x7FFFFFFF), a)
+    b = np.where(b < 0, -(b & 0x7FFFFFFF), b)
+    return np.abs(a - b)
+
+
+def test_adaround_forward_bit_exact_vs_reference(gad):
+    from aimet_amd.adaround import AdaroundFunction
+    worst = 0
+    for i in range(int(gad["count"])):
+        c = _case(gad, i)
+        w, a = torch.from_numpy(c["w"]).to(DEV), torch.from_numpy(c["alpha"]).to(DEV)
+        d, o = torch.from_numpy(c["delta"]).to(DEV), torch.from_numpy(c["offset"]).to(DEV)
+        with torch.no_grad():
+            wq = AdaroundFunction.apply(w, a, d, o, c["bw"], 0).cpu().numpy()
+            wh = AdaroundFunction.apply(w, a, d, o, c["bw"], 0, False).cpu().numpy()
+        u = _ulps(wq, c["wq"])
+        worst = max(worst, int(u.max()))
+        assert u.max() == 0, (i, c["w"].shape, int((u != 0).sum()), int(u.max()))
+        assert np.array_equal(wh.view(np.int32), c["wq_hard"].view(np.int32)), i
+    print("adaround Wq: max ulp vs reference = %d" % worst)
+
+
+def test_adaround_backward_vs_reference(gad):
+    from aimet_amd.adaround import AdaroundFunction
+    reg = float(gad["reg_param"])
+    for i in range(int(gad["count"])):
+        c = _case(gad, i)
+        w, alpha = torch.from_numpy(c["w"]).to(DEV), torch.from_numpy(c["alpha"]).to(DEV)
+        d, o = torch.from_numpy(c["delta"]).to(DEV), torch.from_numpy(c["offset"]).to(DEV)
+        g = torch.from_numpy(c["grad"]).to(DEV)
+        # warm start: reconstruction gradient only -> bit-exact
+        a = alpha.clone().requires_grad_(True)
+        (AdaroundFunction.apply(w, a, d, o, c["bw"], 0) * g).sum().backward()
+        got = a.grad.cpu().numpy()
+        assert np.array_equal(got.view(np.int32), c["ga_recon"].view(np.int32)), \
+            (i, int((_ulps(got, c["ga_recon"]) != 0).sum()))
+        # after warm start: + the rounding loss (fused in the same kernel)
+        a = alpha.clone().requires_grad_(True)
+        loss = torch.zeros(1, device=DEV)
+        (AdaroundFunction.apply(w, a, d, o, c["bw"], 0, True, reg, float(c["beta"]), loss) * g).sum().backward()
+        got = a.grad.cpu().numpy().astype(np.float64)
+        ref = c["ga_total"].astype(np.float64)
+        branch = np.abs(ref - c["ga_recon"].astype(np.float64))
+        ulp = np.spacing(np.abs(c["ga_total"])).astype(np.float64)
+        bad = np.abs(got - ref) > 2.0 ** -21 * branch + ulp
+        assert not bad.any(), (i, int(bad.sum()), got[bad][:3], ref[bad][:3])
+        want_loss = float(c["round_loss"])
+        assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss), (i, loss.item(), want_loss)
+
+
+def test_adaround_alpha_init_vs_reference(gad):
+    """aimet_amd.adaround.init_alpha (torch ops on the device) vs the reference's
+    _generate_alpha_parameter on the CPU: the device log differs from torch's CPU log by <= 2 ulp,
+    so alpha0 is within a few ulp (stated bound: 8 ulp, relative to |alpha0| >= 2^-20)."""
+    from aimet_amd.adaround import init_alpha
+    for i in range(int(gad["count"])):
+        k = "c%d_alpha_init" % i
+        if k not in gad:
+            continue
+        c = _case(gad, i)
+        w = torch.from_numpy(c["w"]).to(DEV)
+        shape = (-1,) + (1,) * (w.dim() - 1)
+        d = torch.from_numpy(c["delta"]).to(DEV).view(shape)
+        got = init_alpha(w, d).detach().cpu().numpy()
+        want = gad[k]
+        fin = np.isfinite(want)
+        assert np.array_equal(np.isfinite(got), fin)
+        u = _ulps(got[fin], want[fin])
+        big = np.abs(want[fin]).ravel() >= 2.0 ** -20
+        assert u[big].max() <= 8, (i, int(u.max()))
+
+
+# ------------------------------------------------------------------------------------------
+# fp16 / bf16 STE against the reference's compute_dloss_by_dx (golden_ste16.npz)
+# ------------------------------------------------------------------------------------------
+def _t16(a, dt):
+    return torch.from_numpy(np.ascontiguousarray(a)).view(dt)
+
+
+def test_ste_16bit_bounds_vs_reference(golden_dir):
+    """Per-tensor python-float bounds that fp16 / bf16 cannot represent: the reference compares in
+    x's dtype with the bound rounded (0-dim float32 tensor -> x's dtype); per-channel lists (C = 1
+    included) compare in float32. x sits exactly on and beside the rounded bounds."""
+    import os
+    from aimet_amd.quantizers import compute_dloss_by_dx
+    z = dict(np.load(os.path.join(golden_dir, "golden_ste16.npz")))
+    dts = {"torch.float16": torch.float16, "torch.bfloat16": torch.bfloat16, "torch.float32": torch.float32}
+    for i in range(int(z["count"])):
+        xd, gd = (dts[str(v)] for v in z["t%d_dtypes" % i])
+        x = _t16(z["t%d_x" % i], xd).to(DEV)
+        g = (_t16(z["t%d_grad" % i], gd) if gd != torch.float32 else torch.from_numpy(z["t%d_grad" % i])).to(DEV)
+        mn, mx = (float(v) for v in z["t%d_bounds" % i])
+        got = compute_dloss_by_dx(x, g, mn, mx).cpu()
+        want = z["t%d_pt" % i]
+        got = got.view(torch.int16).numpy() if got.dtype != torch.float32 else got.numpy().view(np.int32)
+        want = want if want.dtype == np.int16 else want.view(np.int32)
+        assert np.array_equal(got, want), (i, xd, gd, int((got != want).sum()))
+    for C in (1, 8):
+        for name, dt in (("float16", torch.float16), ("bfloat16", torch.bfloat16)):
+            k = "p%d_%s_" % (C, name)
+            x, g = _t16(z[k + "x"], dt).to(DEV), _t16(z[k + "grad"], dt).to(DEV)
+            got = compute_dloss_by_dx(x, g, z[k + "mins"].tolist(), z[k + "maxs"].tolist(), 0)
+            assert np.array_equal(got.cpu().view(torch.int16).numpy(), z[k + "out"]), (C, name)
+
+
+def test_ste_16bit_autograd_bounds_vs_reference():
+    """QuantizeDequantize.backward with a bf16 / fp16 input (v1/tensor_quantizer.py:1197-1213):
+    the mask uses the encoding bounds rounded to x's dtype, as the reference's torch expression."""
+    from aimet_amd.quantizers import QuantScheme, StaticGridPerTensorQuantizer
+    g = torch.Generator(device=DEV).manual_seed(12)
+    for dt in (torch.float16, torch.bfloat16):
+        tq = StaticGridPerTensorQuantizer(8, "nearest", QuantScheme.post_training_tf, False, True)
+        src = torch.randn(4096, device=DEV, generator=g) * 0.3
+        tq.update_encoding_stats(src)
+        tq.compute_encoding()
+        x = src.to(dt)
+        rmn, rmx = torch.tensor(tq.encoding.min).to(dt), torch.tensor(tq.encoding.max).to(dt)
+        x[:4] = rmn.to(DEV)
+        x[4:8] = rmx.to(DEV)
+        a = x.clone().requires_grad_(True)
+        y = tq.quantize_dequantize(a, "nearest")
+        up = torch.randn(4096, device=DEV, generator=g).to(dt)
+        y.backward(up)
+        # the reference's expression on the CPU (quantsim_straight_through_grad.py:66-118)
+        emin, emax = torch.tensor(tq.encoding.min), torch.tensor(tq.encoding.max)
+        xc = x.cpu()
+        want = up.cpu() * (emin <= xc).logical_and(xc <= emax)
+        assert torch.equal(a.grad.cpu().view(torch.int16), want.view(torch.int16)), dt

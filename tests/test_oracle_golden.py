@@ -169,3 +169,31 @@ def test_torch_ref_adaround_round_loss_kat(kat):
     alpha = torch.from_numpy(np.random.rand(*k["shape"]))
     loss = T.adaround_round_loss(alpha, k["reg_param"], kat["adaround_beta"]["expected"])
     assert abs(float(loss) - k["expected"]) < 10 ** -k["places"]
+
+
+def test_torch_ref_adaround_pinned_to_reference(golden_dir):
+    """oracle/torch_ref.adaround_forward / adaround_round_loss (the restatement the GPU tests and the
+    optimizer-loop test use) reproduce the reference's apply_adaround / compute_round_loss
+    (golden_adaround.npz) bit for bit on the CPU (one thread)."""
+    import os
+    import torch
+    from oracle import torch_ref as T
+    z = np.load(os.path.join(golden_dir, "golden_adaround.npz"))
+    nt = torch.get_num_threads()
+    torch.set_num_threads(1)
+    try:
+        for i in range(int(z["count"])):
+            k = "c%d_" % i
+            w = torch.from_numpy(z[k + "w"])
+            shape = (-1,) + (1,) * (w.dim() - 1)
+            d = torch.from_numpy(z[k + "delta"]).view(shape)
+            o = torch.from_numpy(z[k + "offset"]).view(shape)
+            a = torch.from_numpy(z[k + "alpha"]).requires_grad_(True)
+            wq = T.adaround_forward(w, a, d, o, int(z[k + "bw"]))
+            assert np.array_equal(wq.detach().numpy().view(np.int32), z[k + "wq"].view(np.int32)), i
+            (wq * torch.from_numpy(z[k + "grad"])).sum().backward()
+            assert np.array_equal(a.grad.numpy().view(np.int32), z[k + "ga_recon"].view(np.int32)), i
+            rl = T.adaround_round_loss(a.detach(), float(z["reg_param"]), float(z[k + "beta"]))
+            assert float(rl) == float(z[k + "round_loss"]), i
+    finally:
+        torch.set_num_threads(nt)
