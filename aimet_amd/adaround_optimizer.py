@@ -18,6 +18,14 @@ The loop is launch-bound for MobileNet-sized layers, so by default one iteration
 HIP graph and replayed (batch indices drawn up front in the eager loop's order, the annealed beta
 read from device memory, Adam capturable); depthwise convolutions run on PyTorch's native kernels
 (3-5x faster than MIOpen's here). MobileNet-v2, 53 layers: 0.47 ms -> 0.19 ms per iteration.
+
+Data parallel (adaround_optimizer.py:139-160,214-216), when torch.distributed is initialised (or a
+group is given): the cached samples are sharded rank::world, Adam's learning rate is multiplied by
+the world size, each rank runs num_iterations // world iterations on batches from its shard, and
+alpha.grad is all-reduced (SUM) and divided by the world size before every Adam step. As in the
+reference, the rounding-loss schedule keeps num_iterations as its horizon (so with world > 1 the
+iterations run are the first 1/world of it). In the HIP-graph form the iteration is two graphs with
+the collective between them: [forward + backward] -> all_reduce(alpha.grad) -> [/ world + Adam].
 """
 import contextlib
 import warnings
@@ -27,6 +35,7 @@ from typing import Callable, Optional, Tuple
 import ctypes
 
 import torch
+import torch.distributed as dist
 import torch.nn.functional as F
 
 from aimet_amd import _native
@@ -172,6 +181,25 @@ class _SoftQuantFn(torch.autograd.Function):
         return ctx.bound.backward(grad), None
 
 
+def _group_world(group):
+    if not (dist.is_available() and dist.is_initialized()):
+        return 0, 1
+    return dist.get_rank(group), dist.get_world_size(group)
+
+
+def _reduce_grad(grad, world, group, divide=True):
+    """adaround_optimizer.py:214-216: all_reduce(alpha.grad) (SUM), then / world_size."""
+    if world > 1:
+        if grad.is_cuda and dist.get_backend(group) == "gloo":
+            h = grad.cpu()
+            dist.all_reduce(h, group=group)
+            grad.copy_(h)
+        else:
+            dist.all_reduce(grad, group=group)
+    if divide:
+        grad.div_(world)
+
+
 class AdaroundOptimizer:
     """v1/adaround/adaround_optimizer.py."""
 
@@ -180,17 +208,25 @@ class AdaroundOptimizer:
                           delta: torch.Tensor, offset: torch.Tensor, bitwidth: int, ch_axis: int = 0,
                           opt_params: AdaroundHyperParameters = AdaroundHyperParameters(),
                           act_func: Optional[Callable] = None, generator: Optional[torch.Generator] = None,
-                          round_loss_out: Optional[torch.Tensor] = None, use_graph: bool = True
-                          ) -> torch.nn.Parameter:
+                          round_loss_out: Optional[torch.Tensor] = None, use_graph: bool = True,
+                          group=None) -> torch.nn.Parameter:
         """Optimises alpha for `module` on the cached activations (inp_data / out_data: [N, ...] on
         the device); returns alpha. delta / offset: the weight quantizer's (per-channel) encoding.
 
         use_graph: the iteration is captured once in a HIP graph and replayed num_iterations times
         (the batch indices of every iteration drawn up front from `generator` in the same order as
         the eager loop, the annealed beta read from device memory by the backward kernel, Adam in
-        its capturable form); the loop is launch-bound for MobileNet-sized layers."""
+        its capturable form); the loop is launch-bound for MobileNet-sized layers.
+
+        group: the process group to run data parallel over (default: the default group when
+        torch.distributed is initialised); see the module docstring."""
+        rank, world = _group_world(group)
+        if world > 1:
+            # adaround_optimizer.py:147-150: this rank's shard of the cached samples
+            shard = torch.arange(rank, inp_data.shape[0], world, device=inp_data.device)
+            inp_data, out_data = inp_data.index_select(0, shard), out_data.index_select(0, shard)
         args = (module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func, generator,
-                round_loss_out)
+                round_loss_out, world, group)
         with conv_backend(module):
             if use_graph:
                 rng = generator.get_state() if generator is not None else torch.get_rng_state()
@@ -211,7 +247,7 @@ class AdaroundOptimizer:
 
     @staticmethod
     def _optimize_eager(module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func,
-                        generator, round_loss_out):
+                        generator, round_loss_out, world=1, group=None):
         w = module.weight.detach()
         dev = w.device
         shape = [1] * w.dim()
@@ -219,15 +255,17 @@ class AdaroundOptimizer:
         d = torch.as_tensor(delta, dtype=torch.float32, device=dev).reshape(-1)
         o = torch.as_tensor(offset, dtype=torch.float32, device=dev).reshape(-1)
         alpha = init_alpha(w, d.view(shape) if d.numel() > 1 else d)
-        # one Adam kernel per step (the reference's default multi-tensor Adam: same update rule)
+        # one Adam kernel per step (the reference's default multi-tensor Adam: same update rule); the
+        # learning rate scaled by the world size (adaround_optimizer.py:155-158)
+        lr = 1e-3 * world
         try:
-            optimizer = torch.optim.Adam([alpha], fused=True)
+            optimizer = torch.optim.Adam([alpha], lr=lr, fused=True)
         except (RuntimeError, TypeError):
-            optimizer = torch.optim.Adam([alpha])
+            optimizer = torch.optim.Adam([alpha], lr=lr)
         sq = _BoundSoftQuant(w, alpha, d, o, bitwidth, ch_axis, round_loss_out)
         n = inp_data.shape[0]
         warm = opt_params.num_iterations * opt_params.warm_start
-        for it in range(opt_params.num_iterations):
+        for it in range(opt_params.num_iterations // world):
             idx = torch.randperm(n, generator=generator)[:BATCH_SIZE].to(dev, non_blocking=True)
             inp = inp_data.index_select(0, idx)
             target = out_data.index_select(0, idx)
@@ -241,12 +279,14 @@ class AdaroundOptimizer:
             q_out = layer_forward(module, inp, wq)
             # fused reconstruction-loss gradient; + the rounding-loss gradient, fused in the soft-quant kernel
             recon_loss_backward(q_out, target, act_func)
+            if world > 1:
+                _reduce_grad(alpha.grad, world, group)
             optimizer.step()
         return alpha
 
     @staticmethod
     def _optimize_graphed(module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func,
-                          generator, round_loss_out):
+                          generator, round_loss_out, world=1, group=None):
         w = module.weight.detach()
         dev = w.device
         shape = [1] * w.dim()
@@ -254,13 +294,14 @@ class AdaroundOptimizer:
         d = torch.as_tensor(delta, dtype=torch.float32, device=dev).reshape(-1)
         o = torch.as_tensor(offset, dtype=torch.float32, device=dev).reshape(-1)
         alpha = init_alpha(w, d.view(shape) if d.numel() > 1 else d)
+        lr = 1e-3 * world
         try:
-            optimizer = torch.optim.Adam([alpha], capturable=True, fused=True)
+            optimizer = torch.optim.Adam([alpha], lr=lr, capturable=True, fused=True)
         except (RuntimeError, TypeError):
-            optimizer = torch.optim.Adam([alpha], capturable=True)
+            optimizer = torch.optim.Adam([alpha], lr=lr, capturable=True)
         sq = _BoundSoftQuant(w, alpha, d, o, bitwidth, ch_axis, round_loss_out)
-        iters, n = opt_params.num_iterations, inp_data.shape[0]
-        warm = iters * opt_params.warm_start
+        iters, n = opt_params.num_iterations // world, inp_data.shape[0]
+        warm = opt_params.num_iterations * opt_params.warm_start
         # the eager loop's draws, in its order: drawn on the host chunk by chunk while the GPU replays
         # the previous chunk (stream-ordered pinned copies into idx_all)
         nb = min(n, BATCH_SIZE)
@@ -278,12 +319,13 @@ class AdaroundOptimizer:
         # pow_backward do, then stored as float32 (the kernel's arithmetic type)
         rb_all = torch.tensor([(0.0, 0.0, 0.0) if it < warm else
                                (lambda b: (opt_params.reg_param, b, b - 1.0))(
-                                   compute_beta(iters, it, opt_params.beta_range, opt_params.warm_start))
-                               for it in range(iters)], dtype=torch.float64).to(torch.float32).to(dev)
+                                   compute_beta(opt_params.num_iterations, it, opt_params.beta_range,
+                                                opt_params.warm_start))
+                               for it in range(max(iters, 1))], dtype=torch.float64).to(torch.float32).to(dev)
         it_buf = torch.zeros(1, dtype=torch.long, device=dev)
         alpha.grad = torch.zeros_like(alpha)
 
-        def step():
+        def grad_step():
             idx = idx_all.index_select(0, it_buf).view(-1)
             inp = inp_data.index_select(0, idx)
             target = out_data.index_select(0, idx)
@@ -292,8 +334,18 @@ class AdaroundOptimizer:
             wq = _SoftQuantFn.apply(alpha, sq)
             q_out = layer_forward(module, inp, wq)
             recon_loss_backward(q_out, target, act_func)
+
+        def update_step():
+            if world > 1:
+                alpha.grad.div_(world)
             optimizer.step()
             it_buf.add_(1)
+
+        def step():
+            grad_step()
+            if world > 1:
+                _reduce_grad(alpha.grad, world, group, divide=False)   # the SUM; / world in update_step
+            update_step()
 
         # warm-up on a side stream (library handles, allocator, autograd), then back to iteration 0
         alpha0 = alpha.detach().clone()
@@ -313,15 +365,29 @@ class AdaroundOptimizer:
                         v.zero_()
             if round_loss_out is not None:
                 round_loss_out.copy_(loss0)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step()
+        if world == 1:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                step()
+            replay = graph.replay
+        else:
+            # the collective between two graphs (any backend; gloo stages through the host)
+            g_grad, g_upd = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g_grad):
+                grad_step()
+            with torch.cuda.graph(g_upd):
+                update_step()
+
+            def replay():
+                g_grad.replay()
+                _reduce_grad(alpha.grad, world, group, divide=False)
+                g_upd.replay()
         for a in range(0, iters, chunk):
             b = min(a + chunk, iters)
             if b < iters:
                 draw(b, min(b + chunk, iters))
             for _ in range(a, b):
-                graph.replay()
+                replay()
         torch.cuda.current_stream(dev).synchronize()
         sq.reg_beta = None
         return alpha
