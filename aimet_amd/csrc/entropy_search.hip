@@ -148,7 +148,7 @@ void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, in
     const int grid = (int) (total < 65536 ? total : 65536);
     entropy_search_kernel<<<grid, kEntBlock, 0, s>>>(dj, n, total, sym ? 1 : 0, strict ? 1 : 0, unsign ? 1 : 0);
     AIMET_LAUNCH_CHECK();
-    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
+    scratch_free(dj, s);
 }
 
 }   // namespace aimet_amd

@@ -416,7 +416,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             const int U      = K4 % (kBlock * 4) == 0 ? 4 : K4 % (kBlock * 2) == 0 ? 2 : 1;
             const int64_t wg = n / 4 / (kBlock * U);
             float* partial   = nullptr;
-            AIMET_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&partial), sizeof(float) * 3 * wg, s));
+            partial = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * wg, s));
             auto xv = reinterpret_cast<const f4*>(x);
             auto gv = reinterpret_cast<const f4*>(grad);
             auto ov = reinterpret_cast<f4*>(grad_x);
@@ -434,7 +434,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
                 partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)));
             AIMET_LAUNCH_CHECK();
-            AIMET_HIP_CHECK(hipFreeAsync(partial, s));
+            scratch_free(partial, s);
             return;
         }
         else if (K % 4 == 0 && outer * (K / 4) < (int64_t(1) << 32) &&

@@ -267,7 +267,7 @@ void launch_mse_search_many(const TqDevice* const* ds, const int64_t* Cs, int n,
     mse_finish_many_kernel<<<(unsigned) ceil_div(chans, kBlock), kBlock, 0, s>>>(dj, n, chans, bw, sym ? 1 : 0,
                                                                                  strict ? 1 : 0, unsign ? 1 : 0);
     AIMET_LAUNCH_CHECK();
-    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
+    scratch_free(dj, s);
 }
 
 void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s)

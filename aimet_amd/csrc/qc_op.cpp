@@ -250,7 +250,7 @@ void per_channel(aimet_qc_quantize_info* info, int mode, const float* in, float*
     auto qdq = [&] {
         float* t = encoding_table(info->encodings, C, s);
         int rc   = aimet_qdq_per_channel(in, out, outer, C, K, t, info->rounding_mode, next_seed(), stream);
-        AIMET_HIP_CHECK(hipFreeAsync(t, s));
+        scratch_free(t, s);
         check(rc);
     };
     switch (mode)
@@ -296,20 +296,20 @@ void broadcast(aimet_qc_quantize_info* info, int mode, const float* in, float* o
         float* tmp       = nullptr;
         if (!si.contiguous_blocks && n > 0)
         {
-            AIMET_HIP_CHECK(hipMallocAsync(reinterpret_cast<void**>(&tmp), sizeof(float) * n, s));
+            tmp = static_cast<float*>(scratch_alloc(sizeof(float) * n, s));
             check(aimet_copy_to_contiguous_block_layout(in, tmp, &si, stream));
             buf = tmp;
         }
         int rc = aimet_tq_update_stats(info->quantizer, buf, 1, E, E ? n / E : 0, stream);
         if (tmp)
-            AIMET_HIP_CHECK(hipFreeAsync(tmp, s));
+            scratch_free(tmp, s);
         check(rc);
     };
     auto qdq = [&] {
         float* t = encoding_table(info->encodings, E, s);
         int rc   = aimet_qdq_broadcast(in, out, n, si.num_dims, si.tensor_strides, si.encoding_strides, t, t + E,
                                        t + 2 * E, t + 3 * E, stream);
-        AIMET_HIP_CHECK(hipFreeAsync(t, s));
+        scratch_free(t, s);
         check(rc);
     };
     switch (mode)

@@ -1009,7 +1009,7 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
         fold_histogram_many_kernel<<<n, kPdfSize, 0, s>>>(dj);
         AIMET_LAUNCH_CHECK();
     }
-    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
+    scratch_free(dj, s);
 }
 
 void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s)
@@ -1034,7 +1034,7 @@ void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s)
         channel_hist_fold_many_kernel<<<(unsigned) blocks, kBlock, 0, s>>>(dj, n);
         AIMET_LAUNCH_CHECK();
     }
-    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
+    scratch_free(dj, s);
 }
 
 void launch_reset_state_many(const std::vector<ResetJob>& jobs, hipStream_t s)
@@ -1044,7 +1044,7 @@ void launch_reset_state_many(const std::vector<ResetJob>& jobs, hipStream_t s)
     auto* dj = static_cast<ResetJob*>(upload_async(jobs.data(), sizeof(ResetJob) * jobs.size(), s));
     reset_acc_many_kernel<<<(unsigned) jobs.size(), kBlock, 0, s>>>(dj);
     AIMET_LAUNCH_CHECK();
-    AIMET_HIP_CHECK(hipFreeAsync(dj, s));
+    scratch_free(dj, s);
 }
 
 void launch_reset_state(const TqDevice& d, int64_t C, bool hist, hipStream_t s)

@@ -1,11 +1,24 @@
 // upload.cpp -- host -> device copies of small per-call tables (job / descriptor arrays) that
-// never block the host. hipMemcpyAsync from pageable memory stages the data synchronously
-// (the host waits for the stream); here the data goes through a ring of pinned staging buffers,
-// an event per slot guarding its reuse, into a stream-ordered allocation.
+// never block the host, and the per-call device scratch they and a few kernels (learned-grid
+// partial sums, blockwise re-layout) live in.
+//
+// Device scratch is a small caching allocator of its own rather than the stream-ordered pool
+// (hipMallocAsync / hipFreeAsync): a released block carries an event recorded on the releasing
+// stream after its consumers, and is handed out again only once that event has completed. The
+// stream-ordered pool was measured to let a job table be reused while the kernel reading it still
+// ran (tests/cpp/sanitize_host.cpp: an illegal access under ASan timing on a created stream, and
+// on the legacy null stream without it); this form needs no ordering guarantee beyond events.
+// Inside a HIP-graph capture the pool IS used (its allocations become graph memory nodes).
+//
+// Host staging goes through a ring of pinned buffers, an event per slot guarding its reuse. On
+// the legacy null stream everything is synchronous (hipMalloc, blocking copy, sync + hipFree).
 #include "common.hpp"
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <unordered_map>
+#include <vector>
 
 namespace aimet_amd
 {
@@ -17,9 +30,9 @@ constexpr int kDevices = 64;
 
 struct Slot
 {
-    void* host     = nullptr;
-    size_t cap     = 0;
-    hipEvent_t ev  = nullptr;
+    void* host    = nullptr;
+    size_t cap    = 0;
+    hipEvent_t ev = nullptr;
 };
 
 struct Ring
@@ -35,14 +48,174 @@ Ring& ring(int dev)
     return rings[dev];
 }
 
-}   // namespace
+// AIMET_SCRATCH_SYNC_ALLOC=1: the null-stream (synchronous) form on every stream (diagnostics)
+bool sync_alloc()
+{
+    static const bool v = [] {
+        const char* e = getenv("AIMET_SCRATCH_SYNC_ALLOC");
+        return e != nullptr && e[0] == '1';
+    }();
+    return v;
+}
 
-void* upload_async(const void* src, size_t bytes, hipStream_t s)
+bool capturing(hipStream_t s)
+{
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    AIMET_HIP_CHECK(hipStreamIsCapturing(s, &st));
+    return st != hipStreamCaptureStatusNone;
+}
+
+int current_device()
 {
     int dev = 0;
     AIMET_HIP_CHECK(hipGetDevice(&dev));
     AIMET_REQUIRE(dev >= 0 && dev < kDevices, "device id out of range");
-    Ring& r = ring(dev);
+    return dev;
+}
+
+// released blocks, reusable once their event has completed
+struct ScratchCache
+{
+    struct Block
+    {
+        int device;
+        void* p;
+        size_t bytes;
+        hipEvent_t ev;
+    };
+    struct Live
+    {
+        int device;
+        size_t bytes;
+        int mode;   // 0: cached block, 1: stream-ordered pool (capture), 2: synchronous (null stream)
+    };
+    std::mutex m;
+    std::vector<Block> free_blocks;
+    std::vector<hipEvent_t> spare_events;
+    std::unordered_map<void*, Live> live;
+};
+ScratchCache& cache()
+{
+    static ScratchCache* c = new ScratchCache();   // never destroyed: blocks live until process exit
+    return *c;
+}
+
+constexpr size_t kMaxCachedBlocks = 64;
+
+}   // namespace
+
+void* scratch_alloc(size_t bytes, hipStream_t s)
+{
+    if (bytes == 0)
+        bytes = 1;
+    ScratchCache& c = cache();
+    const int dev   = current_device();
+    void* d         = nullptr;
+    int mode        = 0;
+    size_t real     = bytes;   // a reused block keeps its own (possibly larger) size
+    if (s == nullptr || sync_alloc())
+    {
+        AIMET_HIP_CHECK(hipMalloc(&d, bytes));
+        mode = 2;
+    }
+    else if (capturing(s))
+    {
+        AIMET_HIP_CHECK(hipMallocAsync(&d, bytes, s));
+        mode = 1;
+    }
+    else
+    {
+        std::vector<void*> stale;
+        {
+            std::lock_guard<std::mutex> lock(c.m);
+            size_t best = c.free_blocks.size();
+            for (size_t i = 0; i < c.free_blocks.size(); ++i)
+            {
+                const ScratchCache::Block& b = c.free_blocks[i];
+                if (b.device != dev || b.bytes < bytes || b.bytes > 4 * bytes + 4096)
+                    continue;
+                if (hipEventQuery(b.ev) != hipSuccess)   // its consumers still run (or an error)
+                    continue;
+                if (best == c.free_blocks.size() || b.bytes < c.free_blocks[best].bytes)
+                    best = i;
+            }
+            if (best != c.free_blocks.size())
+            {
+                d    = c.free_blocks[best].p;
+                real = c.free_blocks[best].bytes;
+                c.spare_events.push_back(c.free_blocks[best].ev);
+                c.free_blocks.erase(c.free_blocks.begin() + (std::ptrdiff_t) best);
+            }
+            else if (c.free_blocks.size() >= kMaxCachedBlocks)
+                // trim: completed blocks of this device go back to the driver
+                for (size_t i = 0; i < c.free_blocks.size();)
+                    if (c.free_blocks[i].device == dev && hipEventQuery(c.free_blocks[i].ev) == hipSuccess)
+                    {
+                        stale.push_back(c.free_blocks[i].p);
+                        c.spare_events.push_back(c.free_blocks[i].ev);
+                        c.free_blocks.erase(c.free_blocks.begin() + (std::ptrdiff_t) i);
+                    }
+                    else
+                        ++i;
+        }
+        for (void* p: stale)
+            AIMET_HIP_CHECK(hipFree(p));
+        if (d == nullptr)
+            AIMET_HIP_CHECK(hipMalloc(&d, bytes));
+    }
+    std::lock_guard<std::mutex> lock(c.m);
+    c.live[d] = ScratchCache::Live {dev, real, mode};
+    return d;
+}
+
+void scratch_free(void* p, hipStream_t s)
+{
+    if (p == nullptr)
+        return;
+    ScratchCache& c = cache();
+    ScratchCache::Live l {};
+    hipEvent_t ev = nullptr;
+    {
+        std::lock_guard<std::mutex> lock(c.m);
+        auto it = c.live.find(p);
+        AIMET_REQUIRE(it != c.live.end(), "scratch_free of a pointer scratch_alloc did not return");
+        l = it->second;
+        c.live.erase(it);
+        if (l.mode == 0 && !c.spare_events.empty())
+        {
+            ev = c.spare_events.back();
+            c.spare_events.pop_back();
+        }
+    }
+    if (l.mode == 2)
+    {
+        AIMET_HIP_CHECK(hipStreamSynchronize(s));   // the consuming launches are done
+        AIMET_HIP_CHECK(hipFree(p));
+        return;
+    }
+    if (l.mode == 1)
+    {
+        AIMET_HIP_CHECK(hipFreeAsync(p, s));
+        return;
+    }
+    if (ev == nullptr)
+        AIMET_HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    AIMET_HIP_CHECK(hipEventRecord(ev, s));   // after every launch that reads the block
+    std::lock_guard<std::mutex> lock(c.m);
+    c.free_blocks.push_back(ScratchCache::Block {l.device, p, l.bytes, ev});
+}
+
+void* upload_async(const void* src, size_t bytes, hipStream_t s)
+{
+    // a captured copy would re-read the (reused) pinned slot at every replay
+    AIMET_REQUIRE(s == nullptr || !capturing(s), "host tables cannot be uploaded inside a HIP-graph capture");
+    void* d = scratch_alloc(bytes, s);
+    if (s == nullptr || sync_alloc())
+    {
+        AIMET_HIP_CHECK(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice));
+        return d;
+    }
+    Ring& r = ring(current_device());
     std::lock_guard<std::mutex> lock(r.m);
     Slot& slot = r.slots[r.next];
     r.next     = (r.next + 1) % kSlots;
@@ -61,8 +234,6 @@ void* upload_async(const void* src, size_t bytes, hipStream_t s)
     if (!slot.ev)
         AIMET_HIP_CHECK(hipEventCreateWithFlags(&slot.ev, hipEventDisableTiming));
     std::memcpy(slot.host, src, bytes);
-    void* d = nullptr;
-    AIMET_HIP_CHECK(hipMallocAsync(&d, bytes, s));
     AIMET_HIP_CHECK(hipMemcpyAsync(d, slot.host, bytes, hipMemcpyHostToDevice, s));
     AIMET_HIP_CHECK(hipEventRecord(slot.ev, s));
     return d;

@@ -3,7 +3,8 @@
 // A thin extern "C" face over the *reference* DlQuantization C++ (compiled from the
 // sources where they lie under /root/reference by oracle/build_ref.sh; nothing of the
 // reference is copied into this repository). Loaded only by tests/golden/make_golden.py
-// to produce golden vectors and by tests/test_oracle_vs_ref.py to pin oracle/dlq_oracle.c.
+// to produce golden vectors and by tests/test_oracle_golden.py, tests/test_entropy.py and
+// tests/test_blockwise.py to pin oracle/dlq_oracle.c against it.
 // The product (aimet_amd/) never loads it.
 #include <DlQuantization/IQuantizationEncodingAnalyzer.hpp>
 #include <DlQuantization/Quantization.hpp>
