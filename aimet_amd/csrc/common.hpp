@@ -152,11 +152,9 @@ __device__ __forceinline__ float glibc_fmaxf(float x, float y)
 // upload.cpp: stream-ordered device copy of a small host table without blocking the host
 // (pinned staging ring); release with scratch_free(ptr, s) after the consuming launches.
 void* upload_async(const void* src, size_t bytes, hipStream_t s);
-// Stream-ordered device scratch: hipMallocAsync / hipFreeAsync on a created stream. On the legacy
-// null stream (a C++ caller passing stream = nullptr) the stream-ordered pool and the pinned
-// staging events are not dependable (measured: a reused job table was overwritten while the
-// kernel reading it ran: tests/cpp/sanitize_host.cpp), so there the allocation is hipMalloc,
-// the upload a blocking copy and the free a null-stream synchronisation + hipFree.
+// Stream-ordered device scratch without the stream-ordered pool: released blocks are reused once
+// an event recorded after their consumers has completed (upload.cpp; the pool let a job table be
+// reused under a running kernel: tests/cpp/sanitize_host.cpp).
 void* scratch_alloc(size_t bytes, hipStream_t s);
 void scratch_free(void* p, hipStream_t s);
 

@@ -6,12 +6,12 @@
 // (hipMallocAsync / hipFreeAsync): a released block carries an event recorded on the releasing
 // stream after its consumers, and is handed out again only once that event has completed. The
 // stream-ordered pool was measured to let a job table be reused while the kernel reading it still
-// ran (tests/cpp/sanitize_host.cpp: an illegal access under ASan timing on a created stream, and
-// on the legacy null stream without it); this form needs no ordering guarantee beyond events.
-// Inside a HIP-graph capture the pool IS used (its allocations become graph memory nodes).
+// ran (tests/cpp/sanitize_host.cpp: an illegal access on the legacy null stream -- torch's default
+// stream -- and, under ASan timing, on a created stream); this form needs no ordering guarantee
+// beyond events. Inside a HIP-graph capture the pool IS used (its allocations become graph memory
+// nodes).
 //
-// Host staging goes through a ring of pinned buffers, an event per slot guarding its reuse. On
-// the legacy null stream everything is synchronous (hipMalloc, blocking copy, sync + hipFree).
+// Host staging goes through a ring of pinned buffers, an event per slot guarding its reuse.
 #include "common.hpp"
 
 #include <cstdlib>
@@ -87,7 +87,7 @@ struct ScratchCache
     {
         int device;
         size_t bytes;
-        int mode;   // 0: cached block, 1: stream-ordered pool (capture), 2: synchronous (null stream)
+        int mode;   // 0: cached block, 1: stream-ordered pool (capture), 2: synchronous (diagnostics)
     };
     std::mutex m;
     std::vector<Block> free_blocks;
@@ -113,12 +113,12 @@ void* scratch_alloc(size_t bytes, hipStream_t s)
     void* d         = nullptr;
     int mode        = 0;
     size_t real     = bytes;   // a reused block keeps its own (possibly larger) size
-    if (s == nullptr || sync_alloc())
+    if (sync_alloc())
     {
         AIMET_HIP_CHECK(hipMalloc(&d, bytes));
         mode = 2;
     }
-    else if (capturing(s))
+    else if (s != nullptr && capturing(s))
     {
         AIMET_HIP_CHECK(hipMallocAsync(&d, bytes, s));
         mode = 1;
@@ -210,7 +210,7 @@ void* upload_async(const void* src, size_t bytes, hipStream_t s)
     // a captured copy would re-read the (reused) pinned slot at every replay
     AIMET_REQUIRE(s == nullptr || !capturing(s), "host tables cannot be uploaded inside a HIP-graph capture");
     void* d = scratch_alloc(bytes, s);
-    if (s == nullptr || sync_alloc())
+    if (sync_alloc())
     {
         AIMET_HIP_CHECK(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice));
         return d;
