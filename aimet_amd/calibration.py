@@ -13,6 +13,7 @@ stack, bench.py), scheduled for the MI355X:
   encodings while the activation passes still stream;
 * activation encodings: one search launch + one synchronisation.
 """
+import os
 from typing import List, Optional, Sequence, Tuple
 
 import torch
@@ -21,6 +22,9 @@ from aimet_amd import distributed as D
 from aimet_amd.tensor_quantizer import AimetTensorQuantizer
 
 _SIDE = {}
+# tuning knobs (tools/enc_schedule_tune.py): launch order and the side stream's priority
+_SCHEDULE = os.environ.get("AIMET_CAL_SCHEDULE", "params_first")
+_SIDE_PRIORITY = int(os.environ.get("AIMET_CAL_SIDE_PRIORITY", "-1"))
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -31,7 +35,7 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     passes still stream."""
     key = dev.index if dev.index is not None else torch.cuda.current_device()
     if key not in _SIDE:
-        _SIDE[key] = torch.cuda.Stream(torch.device("cuda", key), priority=-1)
+        _SIDE[key] = torch.cuda.Stream(torch.device("cuda", key), priority=_SIDE_PRIORITY)
     return _SIDE[key]
 
 
@@ -54,11 +58,16 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
     AimetTensorQuantizer._ensure_many(list(act_quantizers) + list(param_quantizers), dev)
     side = _side_stream(dev)
     keep, p_res = None, []
+    acts_first = _SCHEDULE == "acts_first"
+    if act_quantizers and acts_first:
+        # the HBM-bound activation passes start first; the parameters' short statistics and their
+        # compute-bound searches run beside them on the side stream
+        D.sharded_update_stats(list(act_quantizers), list(activations), group=group)
     if param_quantizers:
         # enqueued first: the parameters' statistics take the CUs before the activation passes
         with torch.cuda.stream(side):
             keep = AimetTensorQuantizer.updateStatsPerChannelMany(param_quantizers, params, param_ch_axes)
-    if act_quantizers:
+    if act_quantizers and not acts_first:
         D.sharded_update_stats(list(act_quantizers), list(activations), group=group)
     if param_quantizers:
         with torch.cuda.stream(side):

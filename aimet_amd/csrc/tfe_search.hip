@@ -8,6 +8,9 @@
 // broadcast from LDS), then a first-minimum argmin across the workgroup. The arithmetic is the
 // shared header tfe_core.hpp, compiled for the host and the device from one source (bit-exact).
 #include "tfe_core.hpp"
+
+#include <cstring>
+#include <mutex>
 #include "tq_state.hpp"
 
 #include <mutex>
@@ -214,21 +217,20 @@ TfeJob job_of(const TqDevice& d, int64_t start)
     return TfeJob {d.pdf_init, d.hist_min, d.bucket_size, d.pdf, d.enc, start};
 }
 
-// Grow-only device scratch per device for batched searches (job table + results); held under
-// the lock until the call has synchronised, so concurrent callers never share it.
-struct Scratch
+// Grow-only pinned host buffer per device for the batched searches' results (a D2H copy into
+// pageable memory is staged through the driver's bounce buffer: 0.56 ms for ResNet-50's 27,560
+// encodings, against ~0.01 ms pinned); held under the lock until the call has synchronised.
+struct PinnedOut
 {
     std::mutex m;
-    char* p[64]   = {};
+    void* p[64]    = {};
     size_t cap[64] = {};
 };
-Scratch& scratch_state()
+PinnedOut& pinned_out()
 {
-    static Scratch s;
+    static PinnedOut s;
     return s;
 }
-
-
 }   // namespace
 
 void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s)
@@ -248,35 +250,31 @@ void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n,
         jobs[i] = job_of(*ds[i], total);
         total += Cs[i];
     }
-    // one stream-ordered scratch block: the job table, then every quantizer's encodings
-    // back to back so that a single copy brings them all to the host
-    const size_t jobs_bytes = (sizeof(TfeJob) * n + 255) & ~size_t(255);
-    const size_t need       = jobs_bytes + sizeof(aimet_tf_encoding) * total;
-    int dev                 = 0;
+    int dev = 0;
     AIMET_HIP_CHECK(hipGetDevice(&dev));
     AIMET_REQUIRE(dev >= 0 && dev < 64, "device id out of range");
-    Scratch& st = scratch_state();
-    std::lock_guard<std::mutex> lock(st.m);
-    if (st.cap[dev] < need)
-    {
-        AIMET_HIP_CHECK(hipStreamSynchronize(s));
-        if (st.p[dev])
-            AIMET_HIP_CHECK(hipFree(st.p[dev]));
-        st.p[dev]   = nullptr;
-        st.cap[dev] = 0;
-        AIMET_HIP_CHECK(hipMalloc((void**) &st.p[dev], need));
-        st.cap[dev] = need;
-    }
-    char* scratch = st.p[dev];
-    aimet_tf_encoding* dout = reinterpret_cast<aimet_tf_encoding*>(scratch + jobs_bytes);
+    auto* dout = static_cast<aimet_tf_encoding*>(scratch_alloc(sizeof(aimet_tf_encoding) * total, s));
     for (int i = 0; i < n; ++i)
         jobs[i].out = dout + jobs[i].start;
-    TfeJob* djobs = reinterpret_cast<TfeJob*>(scratch);
-    AIMET_HIP_CHECK(hipMemcpyAsync(djobs, jobs.data(), sizeof(TfeJob) * n, hipMemcpyHostToDevice, s));
+    auto* djobs = static_cast<TfeJob*>(upload_async(jobs.data(), sizeof(TfeJob) * n, s));
     launch_kernel(jobs[0], djobs, n, total, bw, sym, strict, unsign, s);
-    AIMET_HIP_CHECK(hipMemcpyAsync(host_out, dout, sizeof(aimet_tf_encoding) * total, hipMemcpyDeviceToHost, s));
-    // `jobs` (pageable source) and host_out must be complete before returning
+    const size_t out_bytes = sizeof(aimet_tf_encoding) * total;
+    PinnedOut& po = pinned_out();
+    std::lock_guard<std::mutex> lock(po.m);
+    if (po.cap[dev] < out_bytes)
+    {
+        if (po.p[dev])
+            AIMET_HIP_CHECK(hipHostFree(po.p[dev]));
+        po.p[dev]   = nullptr;
+        po.cap[dev] = 0;
+        AIMET_HIP_CHECK(hipHostMalloc(&po.p[dev], out_bytes, hipHostMallocDefault));
+        po.cap[dev] = out_bytes;
+    }
+    AIMET_HIP_CHECK(hipMemcpyAsync(po.p[dev], dout, out_bytes, hipMemcpyDeviceToHost, s));
+    scratch_free(djobs, s);
+    scratch_free(dout, s);
     AIMET_HIP_CHECK(hipStreamSynchronize(s));
+    std::memcpy(host_out, po.p[dev], out_bytes);
 }
 
 }   // namespace aimet_amd

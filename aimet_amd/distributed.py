@@ -80,8 +80,6 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
     if not quantizers:
         return exchange
     device = tensors[0].device
-    if exchange is None or exchange.quantizers != list(quantizers):
-        exchange = PackedExchange(quantizers, device)
     ch_axes = ch_axes or [0] * len(quantizers)
     world = _world(group)
 
@@ -94,9 +92,13 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
     mt = [tensors[i] for i in many]
 
     if world == 1 and not rest and fused:
-        # nothing to exchange: the fused single-pass update (4 launches for all quantizers)
+        # nothing to exchange (no packed buffers either): the fused single-pass update, 4 launches
+        # for all quantizers
         AimetTensorQuantizer.updateStatsMany(mq, mt)
         return exchange
+
+    if exchange is None or exchange.quantizers != list(quantizers):
+        exchange = PackedExchange(quantizers, device)
 
     if mq:
         AimetTensorQuantizer.batch_minmax_many(mq, mt)

@@ -87,7 +87,7 @@ def _worker(rank, port, q):
         conv, inp, out, d, o = _problem()
         alpha = AdaroundOptimizer.optimize_rounding(conv, inp, out, d, o, 4, 0, _params(), torch.nn.ReLU(),
                                                     torch.Generator().manual_seed(SEEDS[rank]), use_graph=False)
-        q.put((rank, alpha.detach().clone()))
+        q.put((rank, alpha.detach().numpy().copy()))   # by value: no shared-memory handle to outlive the child
     finally:
         dist.destroy_process_group()
 
@@ -139,7 +139,7 @@ def test_adaround_data_parallel_equals_union_of_shards():
     while len(res) < WORLD:
         try:
             r, a = q.get(timeout=2)
-            res[r] = a
+            res[r] = torch.from_numpy(a)
         except queue.Empty:
             assert all(p.exitcode in (None, 0) for p in procs), [p.exitcode for p in procs]
     for p in procs:
