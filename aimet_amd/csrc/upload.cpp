@@ -147,8 +147,10 @@ void* scratch_alloc(size_t bytes, hipStream_t s)
                 c.free_blocks.erase(c.free_blocks.begin() + (std::ptrdiff_t) best);
             }
             else if (c.free_blocks.size() >= kMaxCachedBlocks)
+            {
                 // trim: completed blocks of this device go back to the driver
                 for (size_t i = 0; i < c.free_blocks.size();)
+                {
                     if (c.free_blocks[i].device == dev && hipEventQuery(c.free_blocks[i].ev) == hipSuccess)
                     {
                         stale.push_back(c.free_blocks[i].p);
@@ -157,6 +159,8 @@ void* scratch_alloc(size_t bytes, hipStream_t s)
                     }
                     else
                         ++i;
+                }
+            }
         }
         for (void* p: stale)
             AIMET_HIP_CHECK(hipFree(p));
