@@ -15,7 +15,8 @@ import math
 import torch
 
 from aimet_amd import _native
-from aimet_amd.tensor_quantizer import _require_gpu, _stream, per_channel_view
+from aimet_amd.libpymo import TfEncoding
+from aimet_amd.tensor_quantizer import _stage, _stream, per_channel_view
 
 
 def get_computed_encodings(bitwidth, encoding_min, encoding_max, use_symmetric_encodings, use_strict_symmetric,
@@ -59,11 +60,12 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
                 is_unsigned_symmetric=False, ch_axis=0):
         if bitwidth >= 32:
             raise RuntimeError("Invalid bitwidth: %d" % bitwidth)
-        _require_gpu(tensor.float() if tensor.dtype != torch.float32 else tensor, True, "tensor")
         orig_dtype = tensor.dtype
-        x = tensor.to(torch.float32).contiguous()
-        emin = encoding_min.detach().to(torch.float32).reshape(-1).contiguous()
-        emax = encoding_max.detach().to(torch.float32).reshape(-1).contiguous()
+        # a CPU tensor (and its CPU range) is staged through HBM; results go back to the host
+        x, staged = _stage(tensor.to(torch.float32), "tensor")
+        x = x.contiguous()
+        emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
+        emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         delta, offset, steps = get_computed_encodings(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
                                                       is_unsigned_symmetric)
         delta, offset = delta.contiguous(), offset.contiguous()
@@ -76,14 +78,14 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
                          offset.data_ptr(), float(steps[0]), _stream(x))
         ctx.save_for_backward(x, delta, offset, emin, emax)
         ctx.cfg = (outer, C, K, float(steps[0]), use_symmetric, is_unsigned_symmetric, orig_dtype,
-                   encoding_min.shape, encoding_max.shape)
-        return y.to(orig_dtype)
+                   encoding_min.shape, encoding_max.shape, staged)
+        return y.to(orig_dtype).cpu() if staged else y.to(orig_dtype)
 
     @staticmethod
     def backward(ctx, grad):
         x, delta, offset, emin, emax = ctx.saved_tensors
-        outer, C, K, steps, sym, unsigned, dtype, min_shape, max_shape = ctx.cfg
-        g = grad.to(torch.float32).contiguous()
+        outer, C, K, steps, sym, unsigned, dtype, min_shape, max_shape, staged = ctx.cfg
+        g = grad.to(x.device, torch.float32).contiguous()
         gx = torch.empty_like(g) if ctx.needs_input_grad[0] else None
         sums = torch.empty((C, 3), dtype=torch.float32, device=x.device)
         with torch.cuda.device(x.device):
@@ -101,39 +103,226 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
             gmin = -term1 + emax * term2
             gmax = term1 - emin * term2
         gx_out = gx.to(dtype) if gx is not None else None
-        return gx_out, gmin.view(min_shape), gmax.view(max_shape), None, None, None, None, None
+        gmin, gmax = gmin.view(min_shape), gmax.view(max_shape)
+        if staged:
+            gx_out = gx_out.cpu() if gx_out is not None else None
+            gmin, gmax = gmin.cpu(), gmax.cpu()
+        return gx_out, gmin, gmax, None, None, None, None, None
+
+
+def set_encoding_min_max_gating_threshold(encoding_min, encoding_max):
+    """v1/tensor_quantizer.py:1347-1359: keep a trainable range ordered and around zero
+    (min <= 0 <= max, max >= min + 1e-5), in place."""
+    with torch.no_grad():
+        encoding_min.clamp_(max=0.0)
+        encoding_max.clamp_(min=0.0)
+        encoding_max.copy_(torch.maximum(encoding_max, encoding_min + torch.full_like(encoding_min, 1e-5)))
 
 
 class LearnedGridTensorQuantizer:
-    """Minimal mirror of v1 LearnedGridTensorQuantizer (v1/tensor_quantizer.py:573-893): learnable
-    encoding_min / encoding_max parameters and quantize_dequantize()."""
+    """v1/tensor_quantizer.py:573-893. The learnable range lives in the owning wrapper's
+    ``<name>_encoding_min`` / ``<name>_encoding_max`` parameters (one element per channel);
+    ``encoding`` is computed from them on every read, and setting it re-creates them."""
 
-    def __init__(self, bitwidth, use_symmetric_encodings, enabled_by_default=True, num_channels=1, ch_axis=0,
-                 device="cuda"):
-        self.bitwidth = bitwidth
+    def __init__(self, bitwidth, round_mode, quant_scheme, use_symmetric_encodings, enabled_by_default,
+                 data_type=None):
+        from aimet_amd.quantizers import QuantizationDataType, _round_mode
+        data_type = QuantizationDataType.int if data_type is None else data_type
+        if data_type != QuantizationDataType.int:
+            raise ValueError("Only QuantizationDataType.int is supported for LearnedGridTensorQuantizer")
+        self.round_mode = _round_mode(round_mode)
+        self.quant_scheme = quant_scheme
         self.use_symmetric_encodings = use_symmetric_encodings
         self.use_strict_symmetric = False
         self.use_unsigned_symmetric = False
         self.is_unsigned_symmetric = False
+        self.bitwidth = bitwidth
         self.enabled = enabled_by_default
-        self._ch_axis = ch_axis
-        shape = (num_channels,) if num_channels > 1 else (1,)
-        self.encoding_min = torch.nn.Parameter(torch.zeros(shape, device=device))
-        self.encoding_max = torch.nn.Parameter(torch.zeros(shape, device=device))
+        self.data_type = data_type
+        self.is_const = False
+        self._encoding_min_max_fixed_vals = None
+        self._is_encoding_frozen = False
+        self.wrapper_ref = None
+        self.name = None
+        self.device = None
+        self._ch_axis = 0
+
+    def __str__(self):
+        s = ["LearnedGrid TensorQuantizer:\n",
+             "    quant-scheme:{}, round_mode={}, bitwidth={}, enabled={}\n".format(
+                 self.quant_scheme, self.round_mode, self.bitwidth, self.enabled)]
+        enc = self.get_effective_encoding() if self.encoding else None
+        if enc is None:
+            s.append("    no encoding\n")
+        else:
+            for e in (enc if isinstance(enc, list) else [enc]):
+                s.append("    min:{}, max={}, delta={}, offset={}\n".format(e.min, e.max, e.delta, e.offset))
+        return "".join(s)
+
+    @property
+    def is_encoding_frozen(self):
+        return self._is_encoding_frozen
 
     @property
     def channel_axis(self):
         return self._ch_axis
 
-    def init_from(self, encodings):
-        """Initialise the learnable range from computed TfEncodings (QuantSim's tf/tf-e init)."""
-        with torch.no_grad():
-            self.encoding_min.copy_(torch.tensor([e.min for e in encodings], dtype=torch.float32))
-            self.encoding_max.copy_(torch.tensor([e.max for e in encodings], dtype=torch.float32))
+    @property
+    def encoding_min_max_fixed_vals(self):
+        return self._encoding_min_max_fixed_vals
 
-    def quantize_dequantize(self, tensor, round_mode=None):
+    @encoding_min_max_fixed_vals.setter
+    def encoding_min_max_fixed_vals(self, vals):
+        self._encoding_min_max_fixed_vals = vals
+
+    def _params(self):
+        if self.wrapper_ref is None or self.name is None:
+            return None, None
+        return getattr(self.wrapper_ref, self.name + "_encoding_min"), \
+            getattr(self.wrapper_ref, self.name + "_encoding_max")
+
+    def n(self, device=None):
+        return torch.tensor([0.0], device=device or self.device)
+
+    def p(self, device=None):
+        # the reference passes use_strict_symmetric for both flags (v1/tensor_quantizer.py:631-639)
+        p = 2 ** self.bitwidth - 1 - (1 if self.use_strict_symmetric else 0)
+        return torch.tensor([float(p)], device=device or self.device)
+
+    def compute_scaling_offset(self, encoding_min, encoding_max):
+        """v1/tensor_quantizer.py:744-758."""
+        if encoding_min is None or encoding_max is None:
+            return None, None
+        scaling, offset, _ = get_computed_encodings(self.bitwidth, encoding_min, encoding_max,
+                                                    self.use_symmetric_encodings, self.use_strict_symmetric,
+                                                    self.is_unsigned_symmetric)
+        return scaling, offset
+
+    @property
+    def encoding(self):
+        """v1/tensor_quantizer.py:687-702: the learned encoding(s), computed from the parameters."""
+        from aimet_amd.quantizers import QuantizationDataType
+        if not self.enabled or self.bitwidth == 32 or self.data_type == QuantizationDataType.float:
+            return None
+        return self._compute_updated_encoding()
+
+    @encoding.setter
+    def encoding(self, encoding):
+        """v1/tensor_quantizer.py:704-729."""
+        from aimet_amd.quantizers import QuantizationDataType
+        if not self.enabled or self.bitwidth == 32 or self.data_type == QuantizationDataType.float:
+            return
+        if encoding is None:
+            raise RuntimeError("Encodings cannot be None if Quantizer is enabled.")
+        bw = encoding[0].bw if isinstance(encoding, list) else encoding.bw
+        if bw != self.bitwidth:
+            raise RuntimeError("Bitwidth mismatched. The bitwidth for quantizer is %d, but the bitwidth in encodings "
+                               "is %d. If the intent is to change the bitwidth, please set quantizer bitwidth to %d "
+                               "first." % (self.bitwidth, bw, bw))
+        if self._is_encoding_frozen:
+            raise RuntimeError("Encoding can be set only when it is not frozen.")
+        self._set_encoding_min_max_parameters(encoding)
+
+    def _compute_updated_encoding(self):
+        """v1/tensor_quantizer.py:775-819: delta / offset from the parameters with the forward's
+        torch float32 arithmetic; asymmetric ranges are moved onto the grid (min = delta * offset)."""
+        emin, emax = self._params()
+        if emin is None or emax is None:
+            return None
+        emin, emax = emin.detach().float(), emax.detach().float()
+        scale, offset = self.compute_scaling_offset(emin, emax)
+        scale, offset = scale.expand_as(emin), offset.expand_as(emin)
+        if not self.use_symmetric_encodings or self.is_unsigned_symmetric:
+            adjusted_min = scale * offset
+            emax = emax - emin + adjusted_min
+            emin = adjusted_min
+        rows = torch.stack([emin, emax, scale, offset]).cpu().tolist()   # one device->host copy
+        encodings = []
+        for mn, mx, dl, off in zip(*rows):
+            e = TfEncoding()
+            e.min, e.max, e.delta, e.offset, e.bw = mn, mx, dl, off, self.bitwidth
+            encodings.append(e)
+        return encodings[0] if len(encodings) == 1 else encodings
+
+    def get_effective_encoding(self):
+        """v1/tensor_quantizer.py:642-685: non-strict symmetric quantizers learn a strictly
+        symmetric range; the effective (exported) min carries the extra bin."""
+        if not self.enabled:
+            return None
+        encodings = self.encoding
+        if not encodings:
+            return None
+        if isinstance(encodings, TfEncoding):
+            encodings = [encodings]
+        out = []
+        for e in encodings:
+            if self.use_symmetric_encodings and not self.use_strict_symmetric and not self.is_unsigned_symmetric:
+                f = TfEncoding()
+                f.min, f.max, f.offset, f.delta, f.bw = e.min - e.delta, e.max, e.offset, e.delta, e.bw
+                out.append(f)
+            else:
+                out.append(e)
+        return out[0] if len(out) == 1 else out
+
+    def _set_encoding_min_max_parameters(self, encodings):
+        """v1/tensor_quantizer.py:821-852 (float32 parameters on the wrapper's device)."""
+        encs = encodings if isinstance(encodings, list) else [encodings]
+        params = self.wrapper_ref._parameters
+        dev = self.wrapper_ref.device
+        params[self.name + "_encoding_min"] = torch.nn.Parameter(
+            torch.tensor([float(e.min) for e in encs], dtype=torch.float32).to(dev), requires_grad=True)
+        params[self.name + "_encoding_max"] = torch.nn.Parameter(
+            torch.tensor([float(e.max) for e in encs], dtype=torch.float32).to(dev), requires_grad=True)
+
+    def freeze_encoding(self):
+        """v1/tensor_quantizer.py:854-869."""
+        params = self.wrapper_ref._parameters
+        pmin, pmax = params.get(self.name + "_encoding_min"), params.get(self.name + "_encoding_max")
+        if pmin is None and pmax is None:
+            raise RuntimeError("Encoding can be frozen only when it is not None.")
+        self._is_encoding_frozen = True
+        pmin.requires_grad = False
+        pmax.requires_grad = False
+
+    def reset_encoding_stats(self):
+        """Range-learning quantizers hold no statistics."""
+
+    def quantize_dequantize(self, tensor, encoding_min, encoding_max):
+        """v1/tensor_quantizer.py:760-773 over the fused forward / backward kernels."""
         if not self.enabled or self.bitwidth == 32:
             return tensor
-        return LearnedGridQuantizeDequantize.apply(tensor, self.encoding_min, self.encoding_max, self.bitwidth,
+        if encoding_min is None or encoding_max is None:
+            raise RuntimeError("Forward pass used for compute_encodings differs from forward pass used during "
+                               "training")
+        return LearnedGridQuantizeDequantize.apply(tensor, encoding_min, encoding_max, self.bitwidth,
                                                    self.use_symmetric_encodings, self.use_strict_symmetric,
                                                    self.is_unsigned_symmetric, self._ch_axis)
+
+
+def initialize_learned_grid_quantizer_attributes(new_quantizer, old_quantizer):
+    """v1/tensor_quantizer.py:1285-1344: copy a static-grid quantizer's settings and encodings;
+    symmetric ranges become strictly symmetric (min = -max), unsigned-symmetric ones signed."""
+    from aimet_amd.quantizers import QuantizationDataType
+    new_quantizer.enabled = old_quantizer.enabled
+    new_quantizer.bitwidth = old_quantizer.bitwidth
+    new_quantizer.data_type = old_quantizer.data_type
+    new_quantizer.use_symmetric_encodings = old_quantizer.use_symmetric_encodings
+    new_quantizer.use_strict_symmetric = old_quantizer.use_strict_symmetric
+    new_quantizer.use_unsigned_symmetric = old_quantizer.use_unsigned_symmetric
+    new_quantizer.is_unsigned_symmetric = False
+    new_quantizer.encoding_min_max_fixed_vals = old_quantizer.encoding_min_max_fixed_vals
+    new_quantizer.is_const = old_quantizer.is_const
+    if new_quantizer.data_type == QuantizationDataType.float or new_quantizer.bitwidth == 32:
+        return
+    encoding = old_quantizer.encoding
+    encs = encoding if isinstance(encoding, list) else ([encoding] if encoding is not None else [])
+    if old_quantizer.enabled and old_quantizer.use_symmetric_encodings and not old_quantizer.is_unsigned_symmetric:
+        for e in encs:
+            e.min = -e.max
+    if old_quantizer.enabled and old_quantizer.is_unsigned_symmetric:
+        half = (2 ** old_quantizer.bitwidth - 1) / 2
+        for e in encs:
+            e.min = -e.max
+            e.delta = e.max / math.floor(half)
+            e.offset = -math.ceil(half)
+    new_quantizer.encoding = encoding

@@ -7,8 +7,10 @@ SteGatingFuncForParameters :1314-1366): same names, modes, quantizer layout
 behaviour and encoding import/export format. Every statistic and every QDQ runs on the gfx950
 kernels of aimet_amd (no CPU path; CPU tensors are refused by the core).
 """
+import contextlib
 import enum
 import os
+import threading
 from typing import Dict, Mapping, Optional
 
 import torch
@@ -16,6 +18,8 @@ from torch import nn
 
 from aimet_amd.encodings_io import (compute_partial_encoding, create_encoding_from_dict, export_quantizer_encoding,
                                     validate_is_symmetric_flag)
+from aimet_amd.learned_grid import (LearnedGridTensorQuantizer, initialize_learned_grid_quantizer_attributes,
+                                    set_encoding_min_max_gating_threshold)
 from aimet_amd.libpymo import RoundingMode
 from aimet_amd.quantizers import (MAP_ROUND_MODE_TO_PYMO, QuantizationDataType, QuantScheme,
                                   StaticGridPerChannelQuantizer, StaticGridPerTensorQuantizer, compute_dloss_by_dx)
@@ -36,6 +40,11 @@ TF_ENHANCED_USE_DOWNSAMPLING = bool(int(os.environ.get("AIMET_TFE_USE_DOWNSAMPLI
 TF_ENHANCED_OFFSET_FACTOR = 0
 TF_ENHANCED_STRIDE_FACTOR = 2
 
+# DataParallel replicas share their quantizer objects (replicate() copies module __dict__s) and run
+# in one thread per device; a parameter quantizer's reset -> statistics -> encoding -> QDQ sequence
+# runs under this lock so the replicas never interleave on one quantizer's device state
+_REPLICA_LOCK = threading.Lock()
+
 _IGNORED_DTYPES = (torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64, torch.bool)
 # wrapped modules that never modify their inputs in place
 _INPUT_PRESERVING_TYPES = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d, nn.ConvTranspose2d,
@@ -44,11 +53,15 @@ _INPUT_PRESERVING_TYPES = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d, 
 
 def tensor_quantizer_factory(bitwidth, round_mode, quant_scheme, use_symmetric_encodings, enabled_by_default,
                              data_type=QuantizationDataType.int):
-    """v1/qc_quantize_op.py:77-110 (static-grid schemes; learned grid lives in aimet_amd.learned_grid)."""
+    """v1/qc_quantize_op.py:77-110."""
     if quant_scheme in (QuantScheme.post_training_tf_enhanced, QuantScheme.post_training_tf,
                         QuantScheme.post_training_percentile):
         return StaticGridPerTensorQuantizer(bitwidth, round_mode, quant_scheme, use_symmetric_encodings,
                                             enabled_by_default, data_type=data_type)
+    if quant_scheme in (QuantScheme.training_range_learning_with_tf_init,
+                        QuantScheme.training_range_learning_with_tf_enhanced_init):
+        return LearnedGridTensorQuantizer(bitwidth, round_mode, quant_scheme, use_symmetric_encodings,
+                                          enabled_by_default, data_type)
     raise AssertionError("Unsupported quant_scheme: " + str(quant_scheme))
 
 
@@ -76,7 +89,12 @@ class QcQuantizeWrapper(nn.Module):
         self.supported_kernels = {}
 
     def get_named_parameters(self):
-        yield from self._module_to_wrap.named_parameters()
+        """v1/qc_quantize_op.py:257-269: a torch.nn.DataParallel replica holds its (broadcast)
+        parameters outside ``_parameters``; they are listed in ``_former_parameters``."""
+        if getattr(self, "_is_replica", False):
+            yield from self._module_to_wrap._former_parameters.items()
+        else:
+            yield from self._module_to_wrap.named_parameters()
 
     def __getattr__(self, name):
         try:
@@ -113,6 +131,15 @@ class QcQuantizeWrapper(nn.Module):
 
     def get_original_module(self) -> nn.Module:
         return self._module_to_wrap
+
+    @staticmethod
+    def should_perform_quant_dequant(tensor, tensor_quantizer) -> bool:
+        """v1/qc_quantize_op.py:451-473."""
+        if not isinstance(tensor, torch.Tensor) or tensor.dtype in _IGNORED_DTYPES or \
+                (tensor_quantizer.is_const and tensor.numel() == 1) or not tensor_quantizer.enabled:
+            tensor_quantizer.enabled = False
+            return False
+        return True
 
     # -- encodings export / import (v1/qc_quantize_op.py:363-676) -------------------------------
     def export_param_encodings(self):
@@ -167,7 +194,9 @@ class QcQuantizeWrapper(nn.Module):
                                        "configuration as the quantsim which was used to export the encodings")
                 continue
             per_channel = isinstance(q, StaticGridPerChannelQuantizer)
-            if per_channel and q._num_channels != len(encoding):
+            if isinstance(q, LearnedGridTensorQuantizer):
+                pass   # the range parameters take the encoding's channel count
+            elif per_channel and q._num_channels != len(encoding):
                 if len(encoding) != 1:
                     raise AssertionError("Number of Per Channel encodings provided (%d) is not same as number of "
                                          "channels (%d)" % (len(encoding), q._num_channels))
@@ -308,23 +337,27 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
     def _quantize_dequantize_params(self):
         """v1/qc_quantize_op.py:753-798. The reference saves a clone of every parameter and copies it
         back after the forward; here the fp32 original is kept by reference and the QDQ result
-        (a new tensor) is swapped in for the wrapped forward -- same values, no clone / copy."""
+        (a new tensor) is swapped in for the wrapped forward -- same values, no clone / copy. A
+        DataParallel replica (``_is_replica``, v1/qc_quantize_op.py:785-796) quantizes its
+        broadcast copy the same way, on its own device, under _REPLICA_LOCK."""
         shadow_params = {}
+        replica = getattr(self, "_is_replica", False)
         for name, param in self.get_named_parameters():
             q = self.param_quantizers[name]
             if not (q.enabled and q.bitwidth != 32):
                 continue
-            if self._module_to_wrap.training or q.encoding is None:
-                q.reset_encoding_stats()
-                q.update_encoding_stats(param.data)
-                if q.quant_scheme == QuantScheme.post_training_percentile:
-                    q.set_percentile_value(100)
-                q.compute_encoding()
-                if not q.enabled:
-                    continue
-            round_mode = q.round_mode if self.training else RoundingMode.ROUND_NEAREST
-            shadow_params[name] = param.data
-            param.data = q.quantize_dequantize(param.data, round_mode)
+            with _REPLICA_LOCK if replica else contextlib.nullcontext():
+                if self._module_to_wrap.training or q.encoding is None:
+                    q.reset_encoding_stats()
+                    q.update_encoding_stats(param.data)
+                    if q.quant_scheme == QuantScheme.post_training_percentile:
+                        q.set_percentile_value(100)
+                    q.compute_encoding()
+                    if not q.enabled:
+                        continue
+                round_mode = q.round_mode if self.training else RoundingMode.ROUND_NEAREST
+                shadow_params[name] = param.data
+                param.data = q.quantize_dequantize(param.data, round_mode)
         return shadow_params
 
     def compute_weight_encodings(self):
@@ -344,15 +377,6 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
     def set_percentile_value(self, percentile_value: float):
         for q in list(self.input_quantizers) + list(self.output_quantizers):
             q.set_percentile_value(percentile_value)
-
-    @staticmethod
-    def should_perform_quant_dequant(tensor, tensor_quantizer) -> bool:
-        """v1/qc_quantize_op.py:451-473."""
-        if not isinstance(tensor, torch.Tensor) or tensor.dtype in _IGNORED_DTYPES or \
-                (tensor_quantizer.is_const and tensor.numel() == 1) or not tensor_quantizer.enabled:
-            tensor_quantizer.enabled = False
-            return False
-        return True
 
     def _quantize_activation(self, tensor_quantizers, tensors_to_quantize):
         """v1/qc_quantize_op.py:837-897."""
@@ -417,3 +441,136 @@ class SteGatingFuncForParameters(torch.autograd.Function):
                 else:
                     param.grad = compute_dloss_by_dx(param, param.grad, q.encoding.min, q.encoding.max)
         return (None, *output_grad)
+
+
+@contextlib.contextmanager
+def _patched_params(module: nn.Module, patches: Dict[str, torch.Tensor]):
+    """v1/qc_quantize_op.py:1369-1410 (_patch_param): inside the block ``getattr(module, name)``
+    returns the quantized tensor (module.__dict__ is looked up before nn.Module.__getattr__), so
+    the wrapped forward differentiates through the QDQ into the parameter and its range."""
+    restore = {}
+    for name, value in patches.items():
+        original = getattr(module, name)
+        if original.shape != value.shape:
+            raise AssertionError("quantized %s has shape %s, parameter %s" % (name, value.shape, original.shape))
+        # DataParallel replicas keep their broadcast parameters in module.__dict__ itself
+        restore[name] = module.__dict__[name] if name in module.__dict__ else None
+    try:
+        module.__dict__.update(patches)
+        yield
+    finally:
+        for name, original in restore.items():
+            if original is None:
+                module.__dict__.pop(name, None)
+            else:
+                module.__dict__[name] = original
+
+
+class LearnedGridQuantWrapper(QcQuantizeWrapper):
+    """v1/qc_quantize_op.py:947-1198: range learning. Every enabled quantizer's range is a pair
+    of trainable parameters on the wrapper (``input0_encoding_min``, ``weight_encoding_max``, ...);
+    inputs, parameters and outputs are quantize-dequantized by the fused learned-grid kernels
+    (aimet_amd.learned_grid) in every mode, with gradients into the tensor and both range ends."""
+
+    def __init__(self, module_to_wrap: nn.Module, weight_bw: int, activation_bw: int, round_mode, quant_scheme,
+                 device, is_output_quantized=True, is_symmetric=False, num_inputs=1, num_outputs=1,
+                 data_type: QuantizationDataType = QuantizationDataType.int):
+        if data_type != QuantizationDataType.int:
+            raise ValueError("Only QuantizationDataType.int is supported for LearnedGridQuantWrapper")
+        round_mode = MAP_ROUND_MODE_TO_PYMO[round_mode] if isinstance(round_mode, str) else round_mode
+        super().__init__(module_to_wrap, weight_bw, activation_bw, round_mode, quant_scheme, is_output_quantized,
+                         is_symmetric, num_inputs, num_outputs, data_type)
+        self.device = device
+        self._initialize_trainable_parameters_and_tensor_quantizers(num_inputs, num_outputs)
+
+    def _initialize_trainable_parameters_and_tensor_quantizers(self, num_inputs, num_outputs):
+        """v1/qc_quantize_op.py:981-1017."""
+        for kind, quantizers in (("input", self.input_quantizers), ("output", self.output_quantizers)):
+            for index, q in enumerate(quantizers):
+                self.register_parameter("%s%d_encoding_min" % (kind, index), None)
+                self.register_parameter("%s%d_encoding_max" % (kind, index), None)
+                q.name, q.wrapper_ref, q.device = "%s%d" % (kind, index), self, self.device
+        for name, param in self.get_named_parameters():
+            self.register_parameter(name + "_encoding_min", None)
+            self.register_parameter(name + "_encoding_max", None)
+            q = self.param_quantizers[name]
+            q.name, q.wrapper_ref, q.device = name, self, self.device
+            q._ch_axis = _param_channel_axis(self._module_to_wrap, param)
+
+    def _ranges(self, q):
+        return getattr(self, q.name + "_encoding_min"), getattr(self, q.name + "_encoding_max")
+
+    def apply_gating_logic(self):
+        """v1/qc_quantize_op.py:1019-1055."""
+        quantizers = list(self.input_quantizers) + list(self.output_quantizers) + \
+            [self.param_quantizers[n] for n, _ in self._module_to_wrap.named_parameters()]
+        for q in quantizers:
+            if q.enabled and q.bitwidth != 32 and q.data_type != QuantizationDataType.float:
+                emin, emax = self._ranges(q)
+                if emin is not None and emax is not None:
+                    set_encoding_min_max_gating_threshold(emin, emax)
+
+    def forward(self, *inputs, **kwargs):
+        """v1/qc_quantize_op.py:1057-1098."""
+        self.apply_gating_logic()
+        quantized_inputs = self._quantize_activation(list(inputs), self.input_quantizers)
+        with self._quantize_params():
+            wrapped_output = self._module_to_wrap(*quantized_inputs, **kwargs)
+        if not isinstance(wrapped_output, (list, tuple)):
+            wrapped_output = [wrapped_output]
+        output = self._quantize_activation(list(wrapped_output), self.output_quantizers)
+        return output[0] if len(output) == 1 else output
+
+    def _quantize_params(self):
+        """v1/qc_quantize_op.py:1100-1127."""
+        patches = {}
+        for name, param in self.get_named_parameters():
+            q = self.param_quantizers[name]
+            if q.enabled:
+                emin, emax = self._ranges(q)
+                patches[name] = q.quantize_dequantize(param, emin, emax)
+        return _patched_params(self._module_to_wrap, patches)
+
+    def _quantize_activation(self, tensors_to_quantize, tensor_quantizers):
+        """v1/qc_quantize_op.py:1129-1170."""
+
+        def inner(t, index):
+            if isinstance(t, (list, tuple)):
+                return [inner(x, index) for x in t]
+            q = tensor_quantizers[index]
+            if not self.should_perform_quant_dequant(t, q):
+                return t
+            emin, emax = self._ranges(q)
+            return q.quantize_dequantize(t, emin, emax)
+
+        outputs = []
+        for index, t in enumerate(tensors_to_quantize):
+            if len(tensor_quantizers) <= index:
+                raise AssertionError("Not enough tensor quantizers (%d) allocated" % len(tensor_quantizers))
+            outputs.append(inner(t, index))
+        return outputs
+
+    def compute_encoding(self):
+        """Range-learning quantizers are initialised from a static-grid calibration (QuantSim
+        replaces the wrappers after compute_encodings); they have no statistics of their own."""
+
+    def set_percentile_value(self, percentile_value: float):
+        pass
+
+
+def construct_learned_grid_wrapper(post_training_module: StaticGridQuantWrapper, weight_bw: int,
+                                   activation_bw: int, round_mode, quant_scheme, device) -> LearnedGridQuantWrapper:
+    """v1/quantsim.py:786-831 (_construct_and_initialize_trainable_wrapper): a LearnedGridQuantWrapper
+    around the same module with every quantizer's settings and calibrated encodings copied."""
+    trainable = LearnedGridQuantWrapper(post_training_module._module_to_wrap, weight_bw, activation_bw, round_mode,
+                                        quant_scheme, device=device,
+                                        num_inputs=len(post_training_module.input_quantizers),
+                                        num_outputs=len(post_training_module.output_quantizers))
+    pairs = list(zip(trainable.output_quantizers, post_training_module.output_quantizers)) + \
+        list(zip(trainable.input_quantizers, post_training_module.input_quantizers)) + \
+        [(trainable.param_quantizers[n], q) for n, q in post_training_module.param_quantizers.items()]
+    for new, old in pairs:
+        initialize_learned_grid_quantizer_attributes(new, old)
+        if new.encoding_min_max_fixed_vals is not None:
+            new.freeze_encoding()
+    return trainable

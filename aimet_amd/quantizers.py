@@ -18,8 +18,8 @@ import torch
 
 from aimet_amd import _native
 from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding
-from aimet_amd.tensor_quantizer import (IO_DTYPES, AimetTensorQuantizer, _require_gpu, _stream, per_channel_view,
-                                        qdq_per_channel_table)
+from aimet_amd.tensor_quantizer import (IO_DTYPES, AimetTensorQuantizer, PerChannelTable, _require_gpu, _stage,
+                                        _stream, per_channel_view, qdq_per_channel_table)
 
 
 class QuantScheme(enum.Enum):
@@ -303,6 +303,10 @@ def compute_dloss_by_dx(x, grad, encoding_min, encoding_max, ch_axis=0):
     encoding_min/max: python floats / 0-dim tensors (per-tensor: compared in x's dtype, as the
     reference's 0-dim bound is) or sequences / 1-D tensors of C values (compared in float32, the
     promoted type of the reference's 1-D float32 bound tensor)."""
+    if not (x.is_cuda and grad.is_cuda):   # CPU tensors: staged through HBM, result back on grad's device
+        xd, _ = _stage(x, "x", allow_16bit=True)
+        gd, _ = _stage(grad, "grad", device=xd.device.index, allow_16bit=True)
+        return compute_dloss_by_dx(xd, gd, encoding_min, encoding_max, ch_axis).to(grad.device)
     _require_gpu(x, True, "x", allow_16bit=True)
     _require_gpu(grad, True, "grad", allow_16bit=True)
     x = x.contiguous()
@@ -359,13 +363,14 @@ def _ste_bounds(tq, device):
     """float32 per-channel STE bounds = the raw encoding min/max (the QDQ table holds the gated
     ones), cached until any encoding changes (the reference re-uploads them every backward,
     quantsim_straight_through_grad.py:75-76)."""
-    key = (id(tq._encoding), TfEncoding._version, device)
-    cache = getattr(tq, "_ste_cache", None)
-    if cache is None or cache[0] != key:
+    key = PerChannelTable.key(tq._encoding)
+    cache = tq.__dict__.setdefault("_ste_cache", {})   # device -> (key, mins, maxs)
+    hit = cache.get(device)
+    if hit is None or hit[0] != key:
         mins = torch.tensor([e.min for e in tq._encoding], dtype=torch.float32, device=device)
         maxs = torch.tensor([e.max for e in tq._encoding], dtype=torch.float32, device=device)
-        tq._ste_cache = (key, mins, maxs)
-    return tq._ste_cache[1], tq._ste_cache[2]
+        cache[device] = hit = (key, mins, maxs)
+    return hit[1], hit[2]
 
 
 class QuantizeDequantize(torch.autograd.Function):
@@ -384,9 +389,14 @@ class QuantizeDequantize(torch.autograd.Function):
                 return out
             raise NotImplementedError("fp8 quantization is outside the MI355X integer QDQ core")
         dtype = tensor.dtype
+        # a CPU tensor is staged through HBM (the same kernels; the result goes back to the host)
+        if tensor.is_cuda:
+            t, staged = tensor, False
+        else:
+            t, staged = _stage(tensor if dtype in IO_DTYPES else tensor.to(torch.float32), "tensor", allow_16bit=True)
         # fp16 / bf16 go through the fused 16-bit I/O kernels (identical to the reference's
         # upcast -> fp32 QDQ -> downcast, v1/tensor_quantizer.py:1116-1168); others upcast
-        t = tensor if dtype in IO_DTYPES else tensor.to(torch.float32)
+        t = t if dtype in IO_DTYPES else t.to(torch.float32)
         if isinstance(tq, StaticGridPerChannelQuantizer):
             t = t.contiguous()
             outer, C, K = per_channel_view(t.shape, tq.channel_axis)
@@ -395,7 +405,7 @@ class QuantizeDequantize(torch.autograd.Function):
         else:
             out = AimetTensorQuantizer.quantize_dequantize_tensor(t, tq.encoding, round_mode)
         ctx.save_for_backward(tensor)
-        return out.to(dtype)
+        return out.to(dtype).cpu() if staged else out.to(dtype)
 
     @staticmethod
     def backward(ctx, grad):

@@ -26,8 +26,9 @@ from typing import Any, Callable, Dict, Optional, Union
 import torch
 from torch import nn
 
-from aimet_amd.qc_quantize_op import (QUANTIZER_TYPE_INPUT, QUANTIZER_TYPE_OUTPUT, QcQuantizeOpMode,
-                                      QcQuantizeWrapper, StaticGridQuantWrapper)
+from aimet_amd.qc_quantize_op import (QUANTIZER_TYPE_INPUT, QUANTIZER_TYPE_OUTPUT, LearnedGridQuantWrapper,
+                                      QcQuantizeOpMode, QcQuantizeWrapper, StaticGridQuantWrapper,
+                                      construct_learned_grid_wrapper)
 from aimet_amd.quantizers import QuantizationDataType, QuantScheme, compute_encodings_batched
 
 ENCODING_VERSION = "0.6.1"
@@ -36,6 +37,24 @@ DEFAULT_QUANTIZABLE_TYPES = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d
 
 _SCHEME_NAMES = {"tf": QuantScheme.post_training_tf, "tf_enhanced": QuantScheme.post_training_tf_enhanced,
                  "percentile": QuantScheme.post_training_percentile}
+_RANGE_LEARNING = (QuantScheme.training_range_learning_with_tf_init,
+                   QuantScheme.training_range_learning_with_tf_enhanced_init)
+
+
+def get_v1_quant_scheme_for_initialization(quant_scheme: QuantScheme) -> QuantScheme:
+    """aimet_torch/utils.py:1199-1212: range learning is initialised by a TF / TF-E calibration."""
+    if quant_scheme == QuantScheme.training_range_learning_with_tf_init:
+        return QuantScheme.post_training_tf
+    if quant_scheme == QuantScheme.training_range_learning_with_tf_enhanced_init:
+        return QuantScheme.post_training_tf_enhanced
+    return quant_scheme
+
+
+def _model_device(model):
+    """aimet_torch/utils.py get_device: the device of the first parameter (CPU without any)."""
+    for p in model.parameters():
+        return p.device
+    return torch.device("cpu")
 
 
 def _truthy(v):
@@ -97,7 +116,8 @@ class QuantizationSimModel:
             for child_name, child in list(parent.named_children()):
                 if isinstance(child, quantizable_types) and not isinstance(child, QcQuantizeWrapper):
                     w = StaticGridQuantWrapper(child, default_param_bw, default_output_bw, rounding_mode,
-                                               quant_scheme, is_output_quantized=True,
+                                               get_v1_quant_scheme_for_initialization(quant_scheme),
+                                               is_output_quantized=True,
                                                is_symmetric=self._cfg["act_symmetric"])
                     for pname, pq in w.param_quantizers.items():
                         pq.use_symmetric_encodings = self._cfg["param_symmetric"]
@@ -144,7 +164,8 @@ class QuantizationSimModel:
     # -- calibration ------------------------------------------------------------------------------
     def compute_encodings(self, forward_pass_callback: Callable[[nn.Module, Any], Any],
                           forward_pass_callback_args: Any = None):
-        """v1/quantsim.py:381-449: reset, ANALYSIS forward(s), encodings, ACTIVE."""
+        """v1/quantsim.py:381-449: reset, ANALYSIS forward(s), encodings, ACTIVE; range-learning
+        schemes then swap in the trainable wrappers (v1/quantsim.py:423, 833-846)."""
         for _, w in self.quant_wrappers():
             w.reset_encodings()
             w.set_mode(QcQuantizeOpMode.ANALYSIS)
@@ -153,10 +174,26 @@ class QuantizationSimModel:
         with _eval_mode(self.model), torch.no_grad():
             forward_pass_callback(self.model, forward_pass_callback_args)
         # every activation / param quantizer of the model in one batched native call per setting
-        quantizers = [q for _, w in self.quant_wrappers() for q in self._quantizers_of(w)]
+        # range-learning wrappers keep their trained ranges (they have no statistics)
+        quantizers = [q for _, w in self.quant_wrappers() if not isinstance(w, LearnedGridQuantWrapper)
+                      for q in self._quantizers_of(w)]
         compute_encodings_batched(quantizers)
         for _, w in self.quant_wrappers():
             w.set_mode(QcQuantizeOpMode.ACTIVE)
+        self.replace_wrappers_for_quantize_dequantize()
+
+    def replace_wrappers_for_quantize_dequantize(self):
+        """v1/quantsim.py:833-846, 764-831: every StaticGridQuantWrapper becomes a
+        LearnedGridQuantWrapper initialised from its calibrated encodings (range-learning schemes)."""
+        if self._quant_scheme not in _RANGE_LEARNING:
+            return
+        device = _model_device(self.model)
+        for parent_name, parent in list(self.model.named_modules()):
+            for child_name, child in list(parent.named_children()):
+                if isinstance(child, StaticGridQuantWrapper):
+                    setattr(parent, child_name, construct_learned_grid_wrapper(
+                        child, self._default_param_bw, self._default_output_bw, self._rounding_mode,
+                        self._quant_scheme, device))
 
     def __call__(self, *args, **kwargs):
         return self.model(*args, **kwargs)

@@ -8,7 +8,9 @@ Same class name, method names and argument meaning. Differences, all MI355X-firs
   legacy default stream);
 * one object may hold the analyzers of C channels (``num_channels``), updated in one launch by
   ``updateStatsPerChannel`` -- the reference needed C objects and a Python loop;
-* there is no CPU path: CPU tensors / ``use_cuda=False`` raise ``RuntimeError``.
+* there is no CPU compute path: a CPU tensor (the reference's ``use_cuda=False``,
+  COMP_MODE_CPU) is staged through HBM -- copied to the device, computed by the same HIP
+  kernels, results copied back -- and a process without a HIP device raises ``RuntimeError``.
 """
 import ctypes
 import gc
@@ -40,6 +42,23 @@ def _require_gpu(t: torch.Tensor, use_cuda: bool = True, what: str = "input", al
                         "(v1/tensor_quantizer.py:1124)" % (what, t.dtype))
 
 
+def _stage(t: torch.Tensor, what: str = "input", device=None, allow_16bit: bool = False):
+    """(HIP tensor, staged) for a tensor given to a public entry point: a CPU tensor is copied to
+    `device` (default: the current HIP device) and `staged` is True, so the caller copies its
+    result back. Nothing is computed on the host."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError("%s must be a torch.Tensor" % what)
+    staged = False
+    if not t.is_cuda:
+        if not torch.cuda.is_available():
+            raise RuntimeError("aimet_amd: %s is a CPU tensor and no HIP device is visible; the MI355X core "
+                               "stages CPU tensors through HBM and has no CPU compute path" % what)
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        t, staged = t.to(dev), True
+    _require_gpu(t, True, what, allow_16bit)
+    return t, staged
+
+
 def per_channel_view(shape, ch_axis):
     """[outer][C][K] triple of a tensor quantized along ch_axis (v1/tensor_quantizer.py:1150-1153)."""
     sizes = list(shape)
@@ -59,18 +78,24 @@ class PerChannelTable:
     (AimetTensorQuantizer.cpp:262-299 rebuilt and re-uploaded it on every call)."""
 
     def __init__(self):
-        self._key = None
-        self.table = None
+        self._tables = {}   # device -> (key, table): DataParallel replicas read it on every device
+
+    @staticmethod
+    def key(encodings):
+        """Changes when any encoding field is assigned (TfEncoding._version) or any list element is
+        replaced, even by an older TfEncoding (the element identities)."""
+        return (TfEncoding._version, tuple(map(id, encodings)))
 
     def get(self, encodings, device):
-        key = (id(encodings), len(encodings), TfEncoding._version, device)
-        if self._key != key or self.table is None:
+        key = PerChannelTable.key(encodings)
+        hit = self._tables.get(device)
+        if hit is None or hit[0] != key:
             C = len(encodings)
             table = torch.empty((4, C), dtype=torch.float32, device=device)
             _native.call("aimet_per_channel_table", encodings_to_c(encodings), C, table.data_ptr(),
                          torch.cuda.current_stream(device).cuda_stream)
-            self.table, self._key = table, key
-        return self.table
+            self._tables[device] = hit = (key, table)
+        return hit[1]
 
 
 class AimetTensorQuantizer:
@@ -158,8 +183,8 @@ class AimetTensorQuantizer:
         """AimetTensorQuantizer.cpp:98-127 (per-tensor; the whole tensor feeds one analyzer)."""
         if self._num_channels != 1:
             raise ValueError("updateStats on a %d-channel quantizer: use updateStatsPerChannel" % self._num_channels)
-        _require_gpu(tensor, use_cuda)
-        t = tensor if tensor.is_contiguous() else tensor.contiguous()
+        t, _ = _stage(tensor, device=self._device)
+        t = t if t.is_contiguous() else t.contiguous()
         h = self._ensure(t.device)
         with torch.cuda.device(t.device):
             _native.call("aimet_tq_update_stats", h, t.data_ptr(), 1, 1, t.numel(), _stream(t))
@@ -168,8 +193,8 @@ class AimetTensorQuantizer:
     def updateStatsPerChannel(self, tensor: torch.Tensor, ch_axis: int = 0, use_cuda: bool = True):
         """All C channel analyzers in one pass: replaces the loop of
         v1/tensor_quantizer.py:567-570 (select(ch_axis, c).contiguous() + updateStats per channel)."""
-        _require_gpu(tensor, use_cuda)
-        t = tensor if tensor.is_contiguous() else tensor.contiguous()
+        t, _ = _stage(tensor, device=self._device)
+        t = t if t.is_contiguous() else t.contiguous()
         outer, C, K = per_channel_view(t.shape, ch_axis)
         if C != self._num_channels:
             raise ValueError("tensor has %d channels along axis %d, quantizer has %d" % (C, ch_axis,
@@ -450,20 +475,21 @@ class AimetTensorQuantizer:
 
     def quantizeDequantize(self, tensor, encoding, round_mode, use_cuda=True):
         """AimetTensorQuantizer.cpp:129-155: new output tensor, uses encoding.min/max/bw."""
-        _require_gpu(tensor, use_cuda)
-        t = tensor.contiguous(memory_format=_suggest_memory_format(tensor))
-        return AimetTensorQuantizer.quantize_dequantize_tensor(t, encoding, round_mode)
+        t, staged = _stage(tensor)
+        t = t.contiguous(memory_format=_suggest_memory_format(t))
+        out = AimetTensorQuantizer.quantize_dequantize_tensor(t, encoding, round_mode)
+        return out.cpu() if staged else out
 
     def quantize(self, tensor, encoding, round_mode, use_cuda=True, shift_to_signed=False):
         """AimetTensorQuantizer.cpp:157-178: float tensor of integer codes."""
-        _require_gpu(tensor, use_cuda)
-        t = tensor.contiguous(memory_format=_suggest_memory_format(tensor))
+        t, staged = _stage(tensor)
+        t = t.contiguous(memory_format=_suggest_memory_format(t))
         out = torch.empty_like(t)
         seed = next(_seed_counter) if int(round_mode) == RoundingMode.ROUND_STOCHASTIC else 0
         with torch.cuda.device(t.device):
             _native.call("aimet_quantize_per_tensor", t.data_ptr(), out.data_ptr(), t.numel(), encoding.to_c(),
                          int(round_mode), int(bool(shift_to_signed)), seed, _stream(t))
-        return out
+        return out.cpu() if staged else out
 
     def makeDeltaOffsetTensor(self, device, encodings):
         """AimetTensorQuantizer.cpp:209-231 -> (delta[C], offset[C]) float32 on `device`."""
@@ -484,8 +510,8 @@ class AimetTensorQuantizer:
     def quantizeDequantizePerChannel(self, tensor, encodings, num_channel, num_element, num_element_per_channel,
                                      round_mode, use_cuda=True):
         """AimetTensorQuantizer.cpp:233-307 (numChannel, numElement, numElementPerChannel)."""
-        _require_gpu(tensor, use_cuda)
-        t = tensor.contiguous()
+        t, staged = _stage(tensor)
+        t = t.contiguous()
         C, N, K = int(num_channel), int(num_element), int(num_element_per_channel)
         if len(encodings) != C:
             raise ValueError("expected %d encodings, got %d" % (C, len(encodings)))
@@ -493,7 +519,8 @@ class AimetTensorQuantizer:
             raise ValueError("inconsistent per-channel shape: numElement=%d numChannel=%d "
                              "numElementPerChannel=%d" % (N, C, K))
         table = self.channelTable(encodings, t.device)
-        return qdq_per_channel_table(t, table, N // (C * K), C, K, round_mode)
+        out = qdq_per_channel_table(t, table, N // (C * K), C, K, round_mode)
+        return out.cpu() if staged else out
 
 
 IO_DTYPES = {torch.float16: 1, torch.bfloat16: 2}   # aimet_*_16 io_dtype codes

@@ -1,16 +1,23 @@
 """Config 5 (BASELINE.json / SURVEY §8(d)): Llama-3-8B W4A16 QAT with learned-grid (range
 learning) per-channel 4-bit symmetric weight quantizers, seq 2048, micro-batch 1 per GPU.
 
-  python benchmarks/llama_qat.py [--layers 32] [--impl fused|reference]
+  python benchmarks/llama_qat.py [--layers 32] [--path quantsim|module] [--impl fused|reference]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 benchmarks/llama_qat.py
 
-Every linear layer (q/k/v/o, gate/up/down, lm_head) quantize-dequantizes its fp32 master weight
-with learnable per-output-channel encoding_min / encoding_max (initialised from the TF analyzer),
-then runs its matmul in bf16 (torch.autocast); Adam (fused) updates weights and encodings.
+--path quantsim (default): the reference's workflow. QuantizationSimModel(model,
+  quant_scheme=training_range_learning_with_tf_init, default_param_bw=4, default_output_bw=16,
+  per-channel symmetric params) wraps every linear layer (q/k/v/o, gate/up/down, lm_head);
+  compute_encodings calibrates them on one batch (TF, static grid), then QuantSim swaps in
+  LearnedGridQuantWrapper: each linear quantize-dequantizes its fp32 master weight (4-bit,
+  learnable per-output-channel range) and its output (16-bit, learnable per-tensor range) with
+  the fused learned-grid kernels; matmuls run in bf16 (torch.autocast); Adam (fused) updates
+  weights and ranges.
+--path module: the weight-only hand-built QAT linear of round 1 (no activation quantizers):
   --impl fused      aimet_amd's learned-grid kernels (one forward pass, one backward pass per weight)
   --impl reference  the reference's torch-op QuantizeDequantizeFunc (v1/tensor_quantizer.py:896-986 over
                     quantsim_straight_through_grad.py:121-347, restated in oracle/torch_ref.py)
-Unit of work = weight QDQ + STE elements per step (forward + backward over all linear weights).
+Unit of work = weight QDQ + STE elements per step (forward + backward over all linear weights);
+the activation elements quantized per step are reported beside it.
 Synthetic data: random token ids, random-init weights N(0, 0.02) (seed 0).
 """
 import argparse
@@ -77,6 +84,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--impl", choices=["fused", "reference"], default="fused")
+    ap.add_argument("--path", choices=["quantsim", "module"], default="quantsim")
+    ap.add_argument("--act-bw", type=int, default=16)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -93,27 +102,56 @@ def main():
 
     QatLinear.impl = args.impl
     torch.manual_seed(0)
+    linear_type = nn.Linear if args.path == "quantsim" else QatLinear
+    linear_cls = (lambda i, o: nn.Linear(i, o, bias=False)) if args.path == "quantsim" else QatLinear
     with torch.device(dev):
-        model = Llama(QatLinear, layers=args.layers)
-    qlin = [m for m in model.modules() if isinstance(m, QatLinear)]
+        model = Llama(linear_cls, layers=args.layers)
+    qlin = [m for m in model.modules() if isinstance(m, linear_type)]
+    vocab = model.lm_head.weight.shape[0]
     with torch.no_grad():
         g = torch.Generator(device=dev).manual_seed(0)
         model.embed_tokens.weight.normal_(0, 0.02, generator=g)
         for m in qlin:
             m.weight.normal_(0, 0.02, generator=g)
-            # TF per-channel symmetric init of the learnable range (QuantSim compute_encodings)
-            q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF, num_channels=m.weight.shape[0])
-            q.updateStatsPerChannel(m.weight, 0, True)
-            encs, _ = q.getEncoding(BITWIDTH, True, False, False)
-            m.encoding_min.copy_(torch.tensor([e.min for e in encs], dtype=torch.float32))
-            m.encoding_max.copy_(torch.tensor([e.max for e in encs], dtype=torch.float32))
+            if args.path == "module":
+                # TF per-channel symmetric init of the learnable range (QuantSim compute_encodings)
+                q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF, num_channels=m.weight.shape[0])
+                q.updateStatsPerChannel(m.weight, 0, True)
+                encs, _ = q.getEncoding(BITWIDTH, True, False, False)
+                m.encoding_min.copy_(torch.tensor([e.min for e in encs], dtype=torch.float32))
+                m.encoding_max.copy_(torch.tensor([e.max for e in encs], dtype=torch.float32))
     n_weights = sum(m.weight.numel() for m in qlin)
+    calib_s, n_act = None, 0
+    if args.path == "quantsim":
+        from aimet_amd.qc_quantize_op import LearnedGridQuantWrapper
+        from aimet_amd.quantizers import QuantScheme
+        from aimet_amd.quantsim import QuantizationSimModel
+        cfg = {"defaults": {"ops": {"is_output_quantized": "True"},
+                            "params": {"is_quantized": "True", "is_symmetric": "True"},
+                            "strict_symmetric": "False", "per_channel_quantization": "True"}}
+        sim = QuantizationSimModel(model, quant_scheme=QuantScheme.training_range_learning_with_tf_init,
+                                   default_param_bw=BITWIDTH, default_output_bw=args.act_bw, in_place=True,
+                                   config_file=cfg)
+        cal = torch.Generator(device=dev).manual_seed(99)
+        ids_cal = torch.randint(vocab, (1, args.seq), device=dev, generator=cal)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+
+        def calibrate(m, ids):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                m(ids)
+        sim.compute_encodings(calibrate, ids_cal)
+        torch.cuda.synchronize()
+        calib_s = time.perf_counter() - t0
+        wrappers = [w for w in sim.model.modules() if isinstance(w, LearnedGridQuantWrapper)]
+        assert len(wrappers) == len(qlin), (len(wrappers), len(qlin))
+        n_act = sum(w._module_to_wrap.weight.shape[0] for w in wrappers) * args.seq
+        model = sim.model
     ddp = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local]) if world > 1 else model
     try:
         opt = torch.optim.Adam(model.parameters(), lr=1e-5, fused=True)
     except (RuntimeError, TypeError):
         opt = torch.optim.Adam(model.parameters(), lr=1e-5)
-    vocab = model.lm_head.weight.shape[0]
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
 
     def step():
@@ -146,9 +184,14 @@ def main():
         ms = dt / args.steps * 1e3
         print(json.dumps({
             "metric": "Llama-3-8B W4A16 learned-grid QAT step (weight QDQ + STE elements / s)",
+            "scheme": "training_range_learning_with_tf_init" if args.path == "quantsim" else "hand-built QAT linear",
             "value": round(2 * n_weights * world / (ms * 1e-3) / 1e9, 3), "unit": "Gelem/s", "n_gpus": world,
-            "impl": args.impl, "ms_per_step": round(ms, 2), "layers": args.layers, "seq_len": args.seq,
-            "micro_batch": 1, "quantized_weight_elems": n_weights, "final_loss": round(loss.item(), 4),
+            "path": args.path, "impl": "fused" if args.path == "quantsim" else args.impl,
+            "ms_per_step": round(ms, 2), "layers": args.layers, "seq_len": args.seq,
+            "micro_batch": 1, "quantized_weight_elems": n_weights,
+            "quantized_act_elems_per_step": n_act, "act_bw": args.act_bw if args.path == "quantsim" else None,
+            "compute_encodings_s": None if calib_s is None else round(calib_s, 3),
+            "final_loss": round(loss.item(), 4),
             "peak_mem_GB": round(torch.cuda.max_memory_allocated(dev) / 1e9, 1),
             "data": "synthetic token ids, random-init weights N(0, 0.02) (seed 0)"}), flush=True)
     if world > 1:
