@@ -133,7 +133,8 @@ __device__ __forceinline__ Sums block_reduce(Sums s)
     return r;
 }
 
-// per-tensor (C == 1): grid-stride, block partial sums -> 3 float atomics per workgroup
+// per-tensor (C == 1): grid-stride, block partial sums -> partial[block][3] (folded in a fixed order
+// by lg_bwd_fold_one: the encoding gradients are reproducible run to run)
 __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ g, float* __restrict__ gx,
                                                                int64_t n, const float* __restrict__ delta,
@@ -179,9 +180,30 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
     Sums t = block_reduce(s);
     if (threadIdx.x == 0)
     {
-        atomicAdd(&sums[0], t.a);
-        atomicAdd(&sums[1], t.b);
-        atomicAdd(&sums[2], t.d);
+        sums[3 * blockIdx.x + 0] = t.a;
+        sums[3 * blockIdx.x + 1] = t.b;
+        sums[3 * blockIdx.x + 2] = t.d;
+    }
+}
+
+// sums[0..2] = the nparts partial triples, lane i taking parts i, i + kBlock, ... in order, then
+// the fixed shuffle tree of block_reduce: one result whatever the scheduling
+__global__ __launch_bounds__(kBlock) void lg_bwd_fold_one(const float* __restrict__ partial, int nparts,
+                                                          float* __restrict__ sums)
+{
+    Sums s {0, 0, 0};
+    for (int i = threadIdx.x; i < nparts; i += kBlock)
+    {
+        s.a += partial[3 * i + 0];
+        s.b += partial[3 * i + 1];
+        s.d += partial[3 * i + 2];
+    }
+    Sums t = block_reduce(s);
+    if (threadIdx.x == 0)
+    {
+        sums[0] = t.a;
+        sums[1] = t.b;
+        sums[2] = t.d;
     }
 }
 
@@ -219,8 +241,8 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
 }
 
 // per-channel, 16-B form (K % 4 == 0, aligned): a (channel, slice) grid; with one slice the sums
-// are stored (deterministic), with several (few channels: fill the chip) they are added atomically
-// into the zeroed sums.
+// are stored, with several (few channels: fill the chip) each slice stores its triple at
+// sums[(c * splits + slice) * 3] and lg_bwd_tile_fold adds them per channel in slice order.
 __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __restrict__ x, const f4* __restrict__ g,
                                                                     f4* __restrict__ gx, int64_t outer, int64_t C,
                                                                     int64_t K4, FastDiv divK4,
@@ -278,9 +300,10 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
             }
             else
             {
-                atomicAdd(&sums[3 * c + 0], t.a);
-                atomicAdd(&sums[3 * c + 1], t.b);
-                atomicAdd(&sums[3 * c + 2], t.d);
+                const int64_t p = c * splits + blockIdx.y;
+                sums[3 * p + 0] = t.a;
+                sums[3 * p + 1] = t.b;
+                sums[3 * p + 2] = t.d;
             }
         }
     }
@@ -392,9 +415,11 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
         int64_t n = outer * C * K;
         require_device_ptr(sums, "sums");
         hipStream_t s = as_stream(stream);
-        AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3 * C, s));
         if (n == 0)
+        {
+            AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3 * C, s));
             return;
+        }
         require_device_ptr(x, "x");
         require_device_ptr(grad, "grad");
         if (grad_x)
@@ -405,8 +430,15 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
         {
             bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                          reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
-            lg_bwd_tensor_kernel<<<stream_blocks(n, (int64_t) kBlock * 16), kBlock, 0, s>>>(
-                x, grad, grad_x, n, delta, offset, num_steps, sums, vec ? 1 : 0);
+            const unsigned nb = stream_blocks(n, (int64_t) kBlock * 16);
+            float* partial    = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * nb, s));
+            lg_bwd_tensor_kernel<<<nb, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset, num_steps, partial,
+                                                       vec ? 1 : 0);
+            AIMET_LAUNCH_CHECK();
+            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) nb, sums);
+            AIMET_LAUNCH_CHECK();
+            scratch_free(partial, s);
+            return;
         }
         else if (K % 1024 == 0 && n < (int64_t(1) << 31) && C < 65536 &&
                  ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
@@ -448,9 +480,20 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             if (splits > per)
                 splits = per > 0 ? per : 1;
             dim3 grid((unsigned) (C < 65536 ? C : 65536), (unsigned) splits);
+            float* partial = splits > 1 ? static_cast<float*>(scratch_alloc(sizeof(float) * 3 * C * splits, s))
+                                        : sums;
             lg_bwd_channel_vec_kernel<<<grid, kBlock, 0, s>>>(
                 reinterpret_cast<const f4*>(x), reinterpret_cast<const f4*>(grad), reinterpret_cast<f4*>(grad_x),
-                outer, C, K4, FastDiv((uint32_t) (K4 > 0 ? K4 : 1)), delta, offset, num_steps, sums);
+                outer, C, K4, FastDiv((uint32_t) (K4 > 0 ? K4 : 1)), delta, offset, num_steps, partial);
+            if (splits > 1)
+            {
+                AIMET_LAUNCH_CHECK();
+                lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(partial, sums, 1u, (uint32_t) C,
+                                                                                   (uint32_t) splits);
+                AIMET_LAUNCH_CHECK();
+                scratch_free(partial, s);
+                return;
+            }
         }
         else
         {

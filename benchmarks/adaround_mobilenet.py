@@ -35,7 +35,12 @@ def main():
                     help="launch every iteration from Python instead of replaying one captured HIP graph")
     ap.add_argument("--reference-iters", type=int, default=0,
                     help="also time N iterations per layer of the torch-op reference loop")
+    ap.add_argument("--miopen-find", action="store_true",
+                    help="torch.backends.cudnn.benchmark: MIOpen benchmarks its convolution solvers per shape "
+                         "(a fresh box has no find database; immediate mode may fall back to naive kernels)")
     args = ap.parse_args()
+    if args.miopen_find:
+        torch.backends.cudnn.benchmark = True
 
     from aimet_amd.adaround import AdaroundFunction, compute_beta, init_alpha
     from aimet_amd.adaround_optimizer import (AdaroundHyperParameters, AdaroundOptimizer, layer_forward,
@@ -161,6 +166,7 @@ def main():
         "layers": len(names), "iterations_per_layer": args.iterations, "images": args.images,
         "ms_per_iteration": round(t_opt / iters * 1e3, 4), "activation_caching_s": round(t_cache, 3),
         "loop": "eager" if args.eager else "hipgraph (one captured iteration replayed per iteration)",
+        "miopen_find": bool(args.miopen_find),
         "weights_elems": elems,
         "softquant_fwd_GBps": round(elems * 12 / (fwd_t * 1e-3) / 1e9, 1),
         "softquant_bwd_roundloss_GBps": round(elems * 16 / (bwd_t * 1e-3) / 1e9, 1),

@@ -6,8 +6,11 @@ the calibration batch sharded per sample across GPUs.
          benchmarks/vit_calibration.py                       # N GPUs (RCCL)
 
 256 images N(0,1) (seed 3), global batch 32 (8 calibration batches), each rank runs the forward
-on its 32/N images. Quantizers: one TF-Enhanced per-tensor activation quantizer per conv/linear
-output (+ the model input), as QuantizationSimModel places them for the default config. Per batch
+on its 32/N images. Quantizers: one TF-Enhanced per-tensor activation quantizer on the model input
+and on the output of every op QuantizationSimModel quantizes under the default config
+(workloads/vit.py activation_modules: patch conv, concat, pos add, and per block LayerNorm x2,
+qkv, q*scale, q@k^T, softmax, @v, proj, fc1, GELU, fc2, residual adds x2, final LN, head:
+317 ops + input, about 122.6 M elements per image). Per batch
 the ranks run the device statistics (min/max on the first batch, 512-bin histogram, PDF fold) and
 exchange them with ONE all_reduce(MAX) + ONE all_reduce(SUM) of the packed buffers
 (aimet_amd.distributed). Reported (rank 0, one JSON line):
@@ -16,7 +19,8 @@ exchange them with ONE all_reduce(MAX) + ONE all_reduce(SUM) of the packed buffe
     warmed by one untimed statistics pass on throwaway quantizers (--cold: without it),
   * time inside the two collectives, forward time,
   * encodings identical on every rank (all_gather of a digest) and, at N=1, bit-identical to the
-    CPU oracle fed the same tensors for the first --oracle-check quantizers.
+    CPU oracle fed the same tensors, for every quantizer (--oracle-check N: the first N only; the
+    oracle analyzers run in a thread pool on the host, outside the timed region).
 """
 import argparse
 import hashlib
@@ -37,7 +41,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--images", type=int, default=256)
     ap.add_argument("--batch", type=int, default=32, help="global calibration batch")
-    ap.add_argument("--oracle-check", type=int, default=3)
+    ap.add_argument("--oracle-check", type=int, default=-1, help="-1: every quantizer (N=1 only)")
+    ap.add_argument("--oracle-threads", type=int, default=16)
     ap.add_argument("--phased", action="store_true", help="single rank: run the sharded phases anyway")
     ap.add_argument("--cold", action="store_true", help="time the first batch in a cold process (no warm-up pass)")
     args = ap.parse_args()
@@ -53,17 +58,25 @@ def main():
     from aimet_amd import distributed as D
     from aimet_amd.libpymo import QuantizationMode
     from aimet_amd.tensor_quantizer import AimetTensorQuantizer
-    from workloads.vit import vit_l16
+    from workloads.vit import activation_modules, vit_l16
 
     model = vit_l16(seed=0, device=dev)
-    layers = [m for m in model.modules() if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear))]
+    layers = activation_modules(model)
     quantizers = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in range(len(layers) + 1)]
     acts = []
     hooks = [m.register_forward_hook(lambda mod, i, o: acts.append(o)) for m in layers]
     per_rank = args.batch // world
     g = torch.Generator().manual_seed(3)
     images = torch.randn(args.images, 3, 224, 224, generator=g)       # the same 256 images on every rank
-    check = [] if (world > 1 or args.oracle_check <= 0) else [[] for _ in range(args.oracle_check)]
+    n_check = 0 if world > 1 or args.oracle_check == 0 else \
+        len(quantizers) if args.oracle_check < 0 else min(args.oracle_check, len(quantizers))
+    oracle_pool = analyzers = None
+    if n_check:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from oracle import oracle as O
+        analyzers = [O.Analyzer(O.QUANTIZATION_TF_ENHANCED) for _ in range(n_check)]
+        oracle_pool = ThreadPoolExecutor(args.oracle_threads)
 
     stream = torch.cuda.current_stream(dev)
     t_fwd = t_stats = t_coll = 0.0
@@ -80,9 +93,8 @@ def main():
         torch.cuda.synchronize()
         t_fwd += time.perf_counter() - t0
         tensors = [x] + [a.contiguous() for a in acts]
+        assert len(tensors) == len(quantizers), (len(tensors), len(quantizers))
         elems += sum(t.numel() for t in tensors)
-        for i, lst in enumerate(check):
-            lst.append(tensors[i].cpu().numpy().ravel())
         if b0 == 0 and not args.cold:
             # warm the process once (code objects of the statistics kernels, allocator pools) on
             # throwaway quantizers: the timed calibration is what it costs in a warm process
@@ -98,6 +110,11 @@ def main():
         torch.cuda.synchronize()
         per_batch.append(time.perf_counter() - t0)
         t_stats += per_batch[-1]
+        if analyzers:
+            # the oracle sees the same tensors, one update per quantizer per batch (untimed)
+            host = [t.cpu().numpy().ravel() for t in tensors[:n_check]]
+            list(oracle_pool.map(lambda ia: analyzers[ia[0]].update(ia[1]), enumerate(host)))
+            del host
         # the collectives alone (same packed buffers, values already reduced: MAX / SUM of zeros
         # would change them, so time a copy of each buffer)
         if world > 1:
@@ -123,15 +140,11 @@ def main():
         digests = [None] * world
         dist.all_gather_object(digests, digest)
         same = all(d == digest for d in digests)
-    oracle_ok = None
-    if check:
-        from oracle import oracle as O
-        oracle_ok = True
-        for i, chunks in enumerate(check):
-            a = O.Analyzer(O.QUANTIZATION_TF_ENHANCED)
-            for c in chunks:
-                a.update(c)
-            oracle_ok &= encs[i][0].to_tuple() == a.compute(8).as_tuple()
+    oracle_ok, mismatches = None, None
+    if analyzers:
+        mismatches = [i for i, a in enumerate(analyzers) if encs[i][0].to_tuple() != a.compute(8).as_tuple()]
+        oracle_ok = not mismatches
+        oracle_pool.shutdown()
 
     if rank == 0:
         per_gpu = elems / t_stats / 1e9
@@ -144,7 +157,7 @@ def main():
             "quantizers": len(quantizers), "images": args.images, "global_batch": args.batch,
             "act_elems_per_image": round(elems * world / args.images),
             "encodings_identical_across_ranks": same, "encodings_equal_cpu_oracle": oracle_ok,
-            "oracle_checked_quantizers": len(check),
+            "oracle_checked_quantizers": n_check, "oracle_mismatches": mismatches,
             "data": "synthetic N(0,1) images (seed 3), random-init ViT-L/16 (seed 0)"}), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -7,12 +7,20 @@ exact tensors each quantizer saw.
 * the bench's own calibration path (bench.py -> aimet_amd.calibration.compute_encodings_resident:
   batched activation statistics, per-channel weight statistics and device searches on a second
   stream) on the config-1 network: one 32-image batch, TF-Enhanced and TF, every activation
-  encoding and every one of the 27,560 weight-channel encodings.
+  encoding and every one of the 27,560 weight-channel encodings;
+* config 4: ViT-L/16 TF-Enhanced calibration of every activation QuantSim quantizes (318
+  quantizers, ~122.6 M elements per image), one 8-image batch sharded over 2 ranks (gloo, both on
+  cuda:0) through aimet_amd.distributed.sharded_update_stats; both ranks' encodings == the oracle
+  fed the whole batch (tests/vit_dist_worker.py).
 
 The oracle work runs in a thread pool (ctypes releases the GIL); tensors stream to it one batch at
 a time so host memory stays at one batch of activations."""
 import concurrent.futures as cf
+import json
 import os
+import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -155,3 +163,28 @@ def test_bench_calibration_path_equals_oracle(mode):
         assert not bad, (weights[i][0], bad[:5], got[bad[0]], want[bad[0]])
         n_ch += len(got)
     assert n_ch == 27560
+
+
+def test_config4_vit_sharded_calibration(tmp_path):
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "vit_dist_worker.py")
+
+    def run(world, out):
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        procs = [subprocess.Popen([sys.executable, worker], env=dict(
+            os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+            OUT=out)) for r in range(world)]
+        for p in procs:
+            assert p.wait(timeout=300) == 0
+        return [json.load(open(out + ".%d" % r)) for r in range(world)]
+
+    oracle, = run(1, str(tmp_path / "oracle"))
+    ranks = run(2, str(tmp_path / "rank"))
+    assert len(oracle["encodings"]) == 318
+    assert oracle["elements"] > 8 * 120e6
+    for r, res in enumerate(ranks):
+        assert res["elements"] == oracle["elements"]
+        bad = [i for i, (a, b) in enumerate(zip(res["encodings"], oracle["encodings"])) if a != b]
+        assert not bad, "rank %d: %d of %d encodings differ from the oracle (first %s)" % (
+            r, len(bad), len(oracle["encodings"]), bad[:5])

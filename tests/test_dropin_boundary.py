@@ -97,7 +97,7 @@ def test_tensor_quantizer_use_cuda_false_stages_through_hbm():
         assert valid and enc.to_tuple() == o.compute(8).as_tuple()
         y = q.quantizeDequantize(xt, enc, RoundingMode.ROUND_NEAREST, False)
         assert y.device.type == "cpu"
-        np.testing.assert_array_equal(bits(y.numpy()), bits(O.qdq_per_tensor(x.ravel(), enc.min, enc.max, 8)))
+        np.testing.assert_array_equal(bits(y.numpy().ravel()), bits(O.qdq_per_tensor(x.ravel(), enc.min, enc.max, 8)))
     # per channel
     q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF, num_channels=8)
     q.updateStatsPerChannel(xt, 0, False)
@@ -110,7 +110,7 @@ def test_tensor_quantizer_use_cuda_false_stages_through_hbm():
     y = q.quantizeDequantizePerChannel(xt, encs, 8, x.size, K, RoundingMode.ROUND_NEAREST, False)
     assert y.device.type == "cpu"
     table = O.per_channel_table([e.to_tuple() for e in encs])
-    np.testing.assert_array_equal(bits(y.numpy()), bits(O.qdq_per_channel(x.ravel(), 8, K, table)))
+    np.testing.assert_array_equal(bits(y.numpy().ravel()), bits(O.qdq_per_channel(x.ravel(), 8, K, table)))
 
 
 @pytest.mark.gpu

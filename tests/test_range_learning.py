@@ -224,7 +224,10 @@ def _op_level_forward(m, x):
 @pytest.mark.gpu
 @gpu
 @pytest.mark.parametrize("scheme", [RL_TF, QuantScheme.training_range_learning_with_tf_enhanced_init])
-def test_qat_step_through_quantsim_equals_op_level(scheme):
+def test_qat_step_through_quantsim_equals_op_level(scheme, monkeypatch):
+    # MIOpen's weight-gradient convolutions may add partial sums atomically: pick deterministic ones
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
+    monkeypatch.setattr(torch.backends.cudnn, "benchmark", False)
     sim = QuantizationSimModel(make_net().cuda(), quant_scheme=scheme, config_file=PER_CHANNEL_CFG,
                                default_param_bw=4, default_output_bw=8)
     sim.compute_encodings(lambda m, d: [m(x) for x in d], _calib(1))
@@ -243,7 +246,7 @@ def test_qat_step_through_quantsim_equals_op_level(scheme):
                 w.apply_gating_logic()
         loss_ref = _op_level_forward(ref_model, x).square().mean()
         loss_ref.backward()
-        assert float(loss) == float(loss_ref), step
+        assert float(loss.detach()) == float(loss_ref.detach()), step
         got = dict(sim.model.named_parameters())
         for name, p in ref_model.named_parameters():
             assert got[name].grad is not None, name
@@ -262,14 +265,16 @@ def test_quantsim_forward_equals_reference_torch_ops():
     sim = QuantizationSimModel(make_net().cuda(), quant_scheme=RL_TF, config_file=PER_CHANNEL_CFG,
                                default_param_bw=4)
     sim.compute_encodings(lambda m, d: [m(x) for x in d], _calib(3))
-    rec = {}
-    hooks = [w._module_to_wrap.register_forward_hook(
-        lambda mod, i, o, n=n: rec.setdefault(n, (i[0].detach().clone(), o.detach().clone(),
-                                                 mod.weight.detach().clone())))
-        for n, w in sim.quant_wrappers()]
-    outs = {}
-    hooks += [w.register_forward_hook(lambda mod, i, o, n=n: outs.setdefault(n, o.detach().clone()))
-              for n, w in sim.quant_wrappers()]
+    rec, outs = {}, {}
+
+    def raw_hook(mod, i, o, n):   # a forward hook that returns a value replaces the output
+        rec[n] = (i[0].detach().clone(), o.detach().clone(), mod.weight.detach().clone())
+
+    def out_hook(mod, i, o, n):
+        outs[n] = o.detach().clone()
+    hooks = [w._module_to_wrap.register_forward_hook(lambda mod, i, o, n=n: raw_hook(mod, i, o, n))
+             for n, w in sim.quant_wrappers()]
+    hooks += [w.register_forward_hook(lambda mod, i, o, n=n: out_hook(mod, i, o, n)) for n, w in sim.quant_wrappers()]
     with torch.no_grad():
         sim(_calib(4, 1)[0])
     for h in hooks:
