@@ -56,15 +56,18 @@ class AdaroundHyperParameters:
 
 def layer_forward(module: torch.nn.Module, inp: torch.Tensor, weight: torch.Tensor) -> torch.Tensor:
     """The wrapped layer's forward with `weight` in place of its parameter
-    (adaround_optimizer.py:257-286 _compute_output_with_adarounded_weights)."""
+    (adaround_optimizer.py:257-286 _compute_output_with_adarounded_weights). The bias enters
+    detached: only alpha is optimised, so its gradient (a reduction over the whole layer output
+    per iteration) is never needed."""
+    bias = module.bias.detach() if module.bias is not None else None
     if isinstance(module, torch.nn.Conv2d):
-        return F.conv2d(inp, weight, module.bias, module.stride, module.padding, module.dilation, module.groups)
+        return F.conv2d(inp, weight, bias, module.stride, module.padding, module.dilation, module.groups)
     if isinstance(module, torch.nn.Conv1d):
-        return F.conv1d(inp, weight, module.bias, module.stride, module.padding, module.dilation, module.groups)
+        return F.conv1d(inp, weight, bias, module.stride, module.padding, module.dilation, module.groups)
     if isinstance(module, torch.nn.Linear):
-        return F.linear(inp, weight, module.bias)
+        return F.linear(inp, weight, bias)
     if isinstance(module, torch.nn.ConvTranspose2d):
-        return F.conv_transpose2d(inp, weight, module.bias, module.stride, module.padding, module.output_padding,
+        return F.conv_transpose2d(inp, weight, bias, module.stride, module.padding, module.output_padding,
                                   module.groups, module.dilation)
     raise NotImplementedError("AdaRound supports Conv1d / Conv2d / ConvTranspose2d / Linear (got %s)"
                               % type(module).__name__)
@@ -285,8 +288,124 @@ class AdaroundOptimizer:
         return alpha
 
     @staticmethod
+    def _drawer(generator, n, iters, dev):
+        """The eager loop's batch draws, in its order: idx_all [iters, nb] int64 on the device and
+        draw(a, b), which fills rows [a, b) from the host generator through a pinned buffer
+        (stream-ordered copy; the host buffers stay alive in `staged` until the caller
+        synchronises), so chunk k + 1 is drawn while the GPU replays chunk k."""
+        nb = min(n, BATCH_SIZE)
+        idx_all = torch.empty((max(iters, 1), nb), dtype=torch.long, device=dev)
+        staged = []
+
+        def draw(a, b):
+            h = torch.stack([torch.randperm(n, generator=generator)[:BATCH_SIZE] for _ in range(a, b)]).pin_memory()
+            idx_all[a:b].copy_(h, non_blocking=True)
+            staged.append(h)
+        return idx_all, draw, staged
+
+    @staticmethod
+    def _reg_beta_all(opt_params, iters, dev):
+        """{reg, beta, beta - 1} of every iteration, formed in double as the reference's python /
+        ATen pow_backward do, then stored as float32 (the kernel's arithmetic type)."""
+        warm = opt_params.num_iterations * opt_params.warm_start
+        return torch.tensor([(0.0, 0.0, 0.0) if it < warm else
+                             (lambda b: (opt_params.reg_param, b, b - 1.0))(
+                                 compute_beta(opt_params.num_iterations, it, opt_params.beta_range,
+                                              opt_params.warm_start))
+                             for it in range(max(iters, 1))], dtype=torch.float64).to(torch.float32).to(dev)
+
+    @staticmethod
+    def _optimize_fused_graph(module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func,
+                              generator, round_loss_out):
+        """Single-process HIP-graph loop with the iteration's bookkeeping fused into two kernels:
+        aimet_adaround_gather (the batch draw: index lookup + both row gathers, for the four
+        index_select kernels) and aimet_adaround_backward_adam (dL/dalpha + torch's fused-Adam
+        update of alpha in place, for the backward + gradient zero / accumulate + three Adam
+        kernels). The iteration counter and Adam moments live in device memory; the weight
+        gradient comes from torch.autograd.grad (no accumulation into a .grad)."""
+        w = module.weight.detach()
+        dev = w.device
+        shape = [1] * w.dim()
+        shape[ch_axis] = -1
+        d = torch.as_tensor(delta, dtype=torch.float32, device=dev).reshape(-1).contiguous()
+        o = torch.as_tensor(offset, dtype=torch.float32, device=dev).reshape(-1).contiguous()
+        alpha = init_alpha(w, d.view(shape) if d.numel() > 1 else d)
+        sq = _BoundSoftQuant(w, alpha, d, o, bitwidth, ch_axis, round_loss_out)
+        iters, n = opt_params.num_iterations, inp_data.shape[0]
+        nb = min(n, BATCH_SIZE)
+        idx_all, draw, staged = AdaroundOptimizer._drawer(generator, n, iters, dev)
+        chunk = 500
+        draw(0, min(chunk, iters))
+        rb_all = AdaroundOptimizer._reg_beta_all(opt_params, iters, dev)
+        inp_data = inp_data.contiguous()
+        out_data = out_data.contiguous()
+        inp = torch.empty((nb,) + tuple(inp_data.shape[1:]), dtype=inp_data.dtype, device=dev)
+        target = torch.empty((nb,) + tuple(out_data.shape[1:]), dtype=out_data.dtype, device=dev)
+        row_in, row_out = inp[0].numel(), target[0].numel()
+        exp_avg, exp_avg_sq = torch.zeros_like(alpha), torch.zeros_like(alpha)
+        counters = torch.zeros(2, dtype=torch.long, device=dev)   # [it_cur, it_next]
+        wq = torch.empty_like(sq.w).requires_grad_(True)
+        lib = _native.load()
+        P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
+        it_cur, it_next = ctypes.c_void_p(counters.data_ptr()), ctypes.c_void_p(counters.data_ptr() + 8)
+        adam = (ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999), ctypes.c_double(1e-8))
+        loss_ptr = P(round_loss_out) if round_loss_out is not None else None
+
+        def step():
+            s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp), P(target), P(idx_all), it_cur,
+                                                    it_next, nb, row_in, row_out, s))
+            _native.check(sq.fwd(sq.pw, sq.pa, P(wq), *sq.shape, sq.pd, sq.po, sq.bw, 1, s))
+            q_out = layer_forward(module, inp, wq)
+            code = _act_code(act_func)
+            if code is None or q_out.dim() < 2:
+                qa, ta = (act_func(q_out), act_func(target)) if act_func is not None else (q_out, target)
+                (gw,) = torch.autograd.grad(recon_loss(qa, ta), wq)
+            else:
+                g = torch.empty_like(q_out)
+                _native.check(lib.aimet_adaround_recon_grad(P(q_out), P(target), P(g), q_out.numel(), q_out.shape[1],
+                                                            code, s))
+                (gw,) = torch.autograd.grad(q_out, wq, grad_outputs=g)
+            gw = gw if gw.is_contiguous() else gw.contiguous()
+            _native.check(lib.aimet_adaround_backward_adam(sq.pw, sq.pa, P(gw), P(exp_avg), P(exp_avg_sq), *sq.shape,
+                                                           sq.pd, sq.po, sq.bw, P(rb_all), it_next, it_cur, *adam,
+                                                           loss_ptr, s))
+
+        # warm-up on a side stream (library handles, allocator, autograd), then back to iteration 0
+        alpha0 = alpha.detach().clone()
+        loss0 = round_loss_out.clone() if round_loss_out is not None else None
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side), torch.enable_grad():
+            for _ in range(min(2, iters)):
+                step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        with torch.no_grad():
+            alpha.copy_(alpha0)
+            exp_avg.zero_()
+            exp_avg_sq.zero_()
+            counters.zero_()
+            if round_loss_out is not None:
+                round_loss_out.copy_(loss0)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph), torch.enable_grad():
+            step()
+        for a in range(0, iters, chunk):
+            b = min(a + chunk, iters)
+            if b < iters:
+                draw(b, min(b + chunk, iters))
+            for _ in range(a, b):
+                graph.replay()
+        torch.cuda.current_stream(dev).synchronize()
+        del staged
+        return alpha
+
+    @staticmethod
     def _optimize_graphed(module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func,
-                          generator, round_loss_out, world=1, group=None):
+                          generator, round_loss_out, world=1, group=None, fused_step=True):
+        if world == 1 and fused_step:
+            return AdaroundOptimizer._optimize_fused_graph(module, inp_data, out_data, delta, offset, bitwidth,
+                                                           ch_axis, opt_params, act_func, generator, round_loss_out)
         w = module.weight.detach()
         dev = w.device
         shape = [1] * w.dim()

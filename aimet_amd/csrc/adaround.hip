@@ -301,6 +301,126 @@ bool aligned16(const void* p)
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0;
 }
 
+// ---- one optimizer step fused into the backward (single-process HIP-graph loop) -----------------
+// torch.optim.Adam(fused=True) per element, as ATen's adam_math (native/hip/fused_adam_utils.cuh)
+// computes it for a float parameter without weight decay / amsgrad / maximize: the moments in
+// double (double betas times float values), rounded to float; step size and denominator as there.
+struct AdamArgs
+{
+    double lr, beta1, beta2, eps;
+};
+
+__device__ __forceinline__ float adam_elem(float param, float grad, float& exp_avg, float& exp_avg_sq,
+                                           const AdamArgs& a, float bias_correction1, float bias_correction2_sqrt)
+{
+    exp_avg               = a.beta1 * exp_avg + (1 - a.beta1) * grad;
+    exp_avg_sq            = a.beta2 * exp_avg_sq + (1 - a.beta2) * grad * grad;
+    const float step_size = a.lr / bias_correction1;
+    const float denom     = (std::sqrt(exp_avg_sq) / bias_correction2_sqrt) + a.eps;
+    param -= step_size * exp_avg / denom;
+    return param;
+}
+
+// dL/dalpha (ada_bwd, with this iteration's {reg, beta, beta - 1} from reg_beta_all[it]) and the
+// Adam update of alpha in place; `step` = it_next[0] (= it + 1, written by the gather kernel of the
+// same iteration), workgroup 0 publishes it to it_cur for the next iteration's gather.
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* __restrict__ w,
+                                                                   float* __restrict__ alpha,
+                                                                   const float* __restrict__ g,
+                                                                   float* __restrict__ exp_avg,
+                                                                   float* __restrict__ exp_avg_sq, uint32_t n,
+                                                                   AdaChannel map, const float* __restrict__ delta,
+                                                                   const float* __restrict__ offset, AdaParams p,
+                                                                   const float* __restrict__ reg_beta_all,
+                                                                   const int64_t* __restrict__ it_next,
+                                                                   int64_t* __restrict__ it_cur, AdamArgs adam,
+                                                                   float* __restrict__ round_loss)
+{
+    const int64_t step = it_next[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        it_cur[0] = step;
+    const float* rb = reg_beta_all + 3 * (step - 1);
+    p.reg           = rb[0];
+    p.beta          = rb[1];
+    p.beta_m1       = rb[2];
+    // ATen: 1 - pow_(beta, float step) in double, handed to adam_math as float
+    const float step_f = (float) step;
+    const float bc1    = (float) (1 - pow(adam.beta1, (double) step_f));
+    const float bc2s   = (float) sqrt(1 - pow(adam.beta2, (double) step_f));
+    float loss         = 0.0f;
+    if (VEC)
+    {
+        const uint32_t nq = n / 4;
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nq; i += gridDim.x * kBlock)
+        {
+            const uint32_t c = map.channel(4 * i);
+            const float d = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(d);
+            f4 wv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(w) + i);
+            f4 gv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + i);
+            f4 av       = reinterpret_cast<const f4*>(alpha)[i];
+            f4 mv       = reinterpret_cast<const f4*>(exp_avg)[i];
+            f4 vv       = reinterpret_cast<const f4*>(exp_avg_sq)[i];
+            float m[4] = {mv.x, mv.y, mv.z, mv.w}, v[4] = {vv.x, vv.y, vv.z, vv.w};
+            float a[4] = {av.x, av.y, av.z, av.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                a[k] = adam_elem(a[k], ada_bwd(ww[k], a[k], gg[k], d, o, p, rcp, loss), m[k], v[k], adam, bc1, bc2s);
+            reinterpret_cast<f4*>(alpha)[i]      = f4 {a[0], a[1], a[2], a[3]};
+            reinterpret_cast<f4*>(exp_avg)[i]    = f4 {m[0], m[1], m[2], m[3]};
+            reinterpret_cast<f4*>(exp_avg_sq)[i] = f4 {v[0], v[1], v[2], v[3]};
+        }
+    }
+    else
+    {
+        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+        {
+            const uint32_t c = map.channel(i);
+            const float d = delta[c], o = offset[c];
+            const float ga = ada_bwd(w[i], alpha[i], g[i], d, o, p, __builtin_amdgcn_rcpf(d), loss);
+            alpha[i]       = adam_elem(alpha[i], ga, exp_avg[i], exp_avg_sq[i], adam, bc1, bc2s);
+        }
+    }
+    if (p.reg != 0.0f && round_loss)
+    {
+        float s = block_sum(loss);
+        if (threadIdx.x == 0)
+            atomicAdd(round_loss, p.reg * s);
+    }
+}
+
+// this iteration's batch: rows idx_all[it][b] of the cached inputs / outputs -> dst_in[b] /
+// dst_out[b] (blockIdx.y = 2 b + which); it = it_cur[0]; workgroup (0, 0) sets it_next = it + 1
+__global__ __launch_bounds__(kBlock) void adaround_gather_kernel(const float* __restrict__ src_in,
+                                                                 const float* __restrict__ src_out,
+                                                                 float* __restrict__ dst_in, float* __restrict__ dst_out,
+                                                                 const int64_t* __restrict__ idx_all,
+                                                                 const int64_t* __restrict__ it_cur,
+                                                                 int64_t* __restrict__ it_next, int nb, int64_t row_in,
+                                                                 int64_t row_out, int vec)
+{
+    const int64_t it = it_cur[0];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        it_next[0] = it + 1;
+    const int b          = blockIdx.y >> 1;
+    const bool out       = blockIdx.y & 1;
+    const int64_t row    = out ? row_out : row_in;
+    const int64_t r      = idx_all[it * nb + b];
+    const float* src     = (out ? src_out : src_in) + r * row;
+    float* dst           = (out ? dst_out : dst_in) + (int64_t) b * row;
+    const int64_t stride = (int64_t) gridDim.x * kBlock;
+    if (vec)
+    {
+        const f4* s4 = reinterpret_cast<const f4*>(src);
+        f4* d4       = reinterpret_cast<f4*>(dst);
+        for (int64_t q = (int64_t) blockIdx.x * kBlock + threadIdx.x; q < row / 4; q += stride)
+            d4[q] = __builtin_nontemporal_load(s4 + q);
+    }
+    else
+        for (int64_t q = (int64_t) blockIdx.x * kBlock + threadIdx.x; q < row; q += stride)
+            dst[q] = src[q];
+}
+
 // ---- reconstruction-loss gradient (adaround_loss.py:70-80) ------------------------------------
 // loss = mean over (N, spatial) of ||act(q) - act(t)||^2 over dim 1, so
 // dloss/dq = scale * (act(q) - act(t)) * act'(q) with scale = 2 / (N * spatial): one elementwise
@@ -485,6 +605,75 @@ int aimet_adaround_backward_dev(const float* w, const float* alpha, const float*
         return rc;
     return adaround_backward(w, alpha, g, ga, outer, C, K, delta, offset, bw, 0.0, 0.0, reg_beta_dev, round_loss,
                              stream);
+}
+
+}   // extern "C"
+
+extern "C" {
+
+int aimet_adaround_gather(const float* src_in, const float* src_out, float* dst_in, float* dst_out,
+                          const int64_t* idx_all, const int64_t* it_cur, int64_t* it_next, int64_t nb, int64_t row_in,
+                          int64_t row_out, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(nb > 0 && nb <= 32768 && row_in > 0 && row_out > 0, "invalid batch / row sizes");
+        require_device_ptr(src_in, "src_in");
+        require_device_ptr(src_out, "src_out");
+        require_device_ptr(dst_in, "dst_in");
+        require_device_ptr(dst_out, "dst_out");
+        require_device_ptr(idx_all, "idx_all");
+        require_device_ptr(it_cur, "it_cur");
+        require_device_ptr(it_next, "it_next");
+        const bool vec = row_in % 4 == 0 && row_out % 4 == 0 && aligned16(src_in) && aligned16(src_out) &&
+                         aligned16(dst_in) && aligned16(dst_out);
+        const int64_t work = (row_in > row_out ? row_in : row_out) / (vec ? 4 : 1);
+        int64_t bx         = ceil_div(work, kBlock * 4);   // >= 4 items per lane
+        bx                 = bx < 1 ? 1 : (bx > 256 ? 256 : bx);
+        dim3 grid((unsigned) bx, (unsigned) (2 * nb));
+        adaround_gather_kernel<<<grid, kBlock, 0, as_stream(stream)>>>(src_in, src_out, dst_in, dst_out, idx_all,
+                                                                        it_cur, it_next, (int) nb, row_in, row_out,
+                                                                        vec ? 1 : 0);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad_wq, float* exp_avg, float* exp_avg_sq,
+                                 int64_t outer, int64_t C, int64_t K, const float* delta, const float* offset,
+                                 int32_t bw, const float* reg_beta_all, const int64_t* it_next, int64_t* it_cur,
+                                 double lr, double beta1, double beta2, double eps, float* round_loss, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
+        const int64_t n = outer * C * K;
+        AIMET_REQUIRE(n > 0 && n < (int64_t(1) << 31), "AdaRound weight must have 1 .. 2^31-1 elements");
+        require_device_ptr(w, "weight");
+        require_device_ptr(alpha, "alpha");
+        require_device_ptr(grad_wq, "grad");
+        require_device_ptr(exp_avg, "exp_avg");
+        require_device_ptr(exp_avg_sq, "exp_avg_sq");
+        require_device_ptr(delta, "delta");
+        require_device_ptr(offset, "offset");
+        require_device_ptr(reg_beta_all, "reg_beta_all");
+        require_device_ptr(it_next, "it_next");
+        require_device_ptr(it_cur, "it_cur");
+        AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
+        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, 1};
+        AdamArgs a {lr, beta1, beta2, eps};
+        const bool vec = (C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) &&
+                         aligned16(grad_wq) && aligned16(exp_avg) && aligned16(exp_avg_sq);
+        const int64_t items = vec ? n / 4 : n;
+        int64_t blocks      = ceil_div(items, kBlock);
+        blocks              = blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid;
+        if (vec)
+            adaround_bwd_adam_kernel<true><<<(unsigned) blocks, kBlock, 0, as_stream(stream)>>>(
+                w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
+                it_cur, a, round_loss);
+        else
+            adaround_bwd_adam_kernel<false><<<(unsigned) blocks, kBlock, 0, as_stream(stream)>>>(
+                w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
+                it_cur, a, round_loss);
+        AIMET_LAUNCH_CHECK();
+    });
 }
 
 }   // extern "C"

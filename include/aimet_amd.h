@@ -317,6 +317,25 @@ int aimet_adaround_recon_grad(const float* quant_out, const float* orig_out, flo
 int aimet_adaround_backward_dev(const float* w, const float* alpha, const float* grad_wq, float* grad_alpha,
                                 int64_t outer, int64_t C, int64_t K, const float* delta_dev, const float* offset_dev,
                                 int32_t bw, const float* reg_beta_dev, float* round_loss_dev, void* stream);
+/* The single-process AdaRound loop's batch draw (adaround_optimizer.py:181-218: randperm'd
+ * indices, index_select of the cached inputs and fp outputs) as one kernel: it = it_cur_dev[0];
+ * rows idx_all_dev[it * nb + b] (int64, [iterations][nb]) of src_in / src_out ([N][row_in],
+ * [N][row_out]) are copied to dst_in[b] / dst_out[b]; it_next_dev[0] = it + 1. For a HIP-graph
+ * replayed iteration (the counters live in device memory). */
+int aimet_adaround_gather(const float* src_in, const float* src_out, float* dst_in, float* dst_out,
+                          const int64_t* idx_all_dev, const int64_t* it_cur_dev, int64_t* it_next_dev, int64_t nb,
+                          int64_t row_in, int64_t row_out, void* stream);
+/* aimet_adaround_backward + torch.optim.Adam(fused=True)'s update of alpha (no weight decay /
+ * amsgrad) in one pass, for the same replayed iteration: step = it_next_dev[0] (1-based),
+ * {reg, beta, beta - 1} = reg_beta_all_dev[3 * (step - 1) ..] (float32), alpha / exp_avg /
+ * exp_avg_sq (the Adam moments, zero-initialised by the caller) updated in place with ATen's
+ * per-element arithmetic (bias corrections 1 - beta^step in double); it_cur_dev[0] = step;
+ * the round loss accumulated into round_loss_dev[0] when non-null. */
+int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad_wq, float* exp_avg_dev,
+                                 float* exp_avg_sq_dev, int64_t outer, int64_t C, int64_t K, const float* delta_dev,
+                                 const float* offset_dev, int32_t bw, const float* reg_beta_all_dev,
+                                 const int64_t* it_next_dev, int64_t* it_cur_dev, double lr, double beta1,
+                                 double beta2, double eps, float* round_loss_dev, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Blockwise (broadcast) quantization and the ONNX QcQuantizeOp                                */

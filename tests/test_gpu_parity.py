@@ -863,6 +863,40 @@ def test_recon_loss_backward_fused_vs_torch(act, shape):
     torch.testing.assert_close(qa.grad, qb.grad, rtol=2e-6, atol=1e-12)
 
 
+@pytest.mark.parametrize("layer", ["conv", "depthwise", "linear"])
+def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
+    """The single-process loop with the batch draw and backward + Adam fused into two kernels
+    (aimet_adaround_gather, aimet_adaround_backward_adam) follows the graph of torch ops (index_select
+    x4, backward, grad accumulate, torch.optim.Adam(fused, capturable)): same batches, same
+    gradients; the Adam first moment can differ from torch's fused kernel by 1 ulp in ~0.1 % of
+    elements (profiles/r02/adam_probe.txt), so alpha agrees to fp32 tolerance after 80 steps."""
+    from aimet_amd.adaround_optimizer import AdaroundHyperParameters, AdaroundOptimizer, conv_backend
+    torch.manual_seed(4)
+    if layer == "conv":
+        mod, x = torch.nn.Conv2d(16, 24, 3, padding=1), torch.randn(96, 16, 10, 10)
+    elif layer == "depthwise":
+        mod, x = torch.nn.Conv2d(24, 24, 3, padding=1, groups=24), torch.randn(96, 24, 10, 10)
+    else:
+        mod, x = torch.nn.Linear(40, 30), torch.randn(96, 40)
+    mod, x = mod.to(DEV), x.to(DEV)
+    with torch.no_grad():
+        out = mod(x) + 0.01 * torch.randn_like(mod(x))
+    w = mod.weight.detach()
+    d = (w.abs().flatten(1).amax(dim=1) / 7).contiguous()
+    o = torch.full((w.shape[0],), -8.0, device=DEV)
+    params = AdaroundHyperParameters(num_iterations=80, warm_start=0.25)
+    res = {}
+    for fused in (True, False):
+        loss = torch.zeros(1, device=DEV)
+        with conv_backend(mod):
+            a = AdaroundOptimizer._optimize_graphed(mod, x, out, d, o, 4, 0, params, torch.nn.ReLU(),
+                                                    torch.Generator().manual_seed(9), loss, fused_step=fused)
+        res[fused] = (a.detach().clone(), loss.clone())
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-4, atol=1e-7)
+    assert float(res[True][1]) > 0
+
+
 def test_adaround_optimizer_matches_reference_loop():
     """AdaroundOptimizer (fused soft-quant + rounding-loss kernels) follows the reference's loop
     (torch-op soft quantization + AdaroundLoss, adaround_optimizer.py:181-218) iteration for
