@@ -88,6 +88,19 @@ def conv_backend(module: torch.nn.Module):
         torch.backends.cudnn.enabled = prev
 
 
+def depthwise_spec(module: torch.nn.Module):
+    """(K, stride, padding, dilation) when `module` is a depthwise Conv2d the native depthwise
+    kernels (aimet_dwconv2d_*) run: groups == in == out channels, square K in {3, 5}, square
+    stride / padding / dilation, zero padding; else None."""
+    if not isinstance(module, torch.nn.Conv2d) or not (module.groups == module.in_channels == module.out_channels) \
+            or module.groups == 1 or module.padding_mode != "zeros" or isinstance(module.padding, str):
+        return None
+    (kh, kw), (sh, sw), (ph, pw), (dh, dw) = module.kernel_size, module.stride, module.padding, module.dilation
+    if kh != kw or kh not in (3, 5) or sh != sw or ph != pw or dh != dw:
+        return None
+    return kh, sh, ph, dh
+
+
 def recon_loss(quant_out: torch.Tensor, orig_out: torch.Tensor) -> torch.Tensor:
     """adaround_loss.py:70-80."""
     return (torch.norm(quant_out - orig_out, p="fro", dim=1) ** 2).mean()
@@ -350,14 +363,36 @@ class AdaroundOptimizer:
         it_cur, it_next = ctypes.c_void_p(counters.data_ptr()), ctypes.c_void_p(counters.data_ptr() + 8)
         adam = (ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999), ctypes.c_double(1e-8))
         loss_ptr = P(round_loss_out) if round_loss_out is not None else None
+        code = _act_code(act_func)
+        dw = depthwise_spec(module) if inp.dim() == 4 and code is not None else None
+        if dw is not None:
+            # depthwise layers: native forward + weight gradient, no autograd (aimet_dwconv2d_*)
+            K, stride, pad, dil = dw
+            Nb, C, H, W = inp.shape
+            q_dw, g_dw = torch.empty_like(target), torch.empty_like(target)
+            gw_dw = torch.empty_like(sq.w)
+            ws_n = ctypes.c_int64()
+            _native.check(lib.aimet_dwconv2d_grad_weight_workspace(Nb, C, target.shape[2], target.shape[3], K,
+                                                                   ctypes.byref(ws_n)))
+            ws = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
+            bias = module.bias.detach().contiguous() if module.bias is not None else None
+            dims = (Nb, C, H, W, target.shape[2], target.shape[3], K, stride, pad, dil)
 
         def step():
             s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
             _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp), P(target), P(idx_all), it_cur,
                                                     it_next, nb, row_in, row_out, s))
             _native.check(sq.fwd(sq.pw, sq.pa, P(wq), *sq.shape, sq.pd, sq.po, sq.bw, 1, s))
+            if dw is not None:
+                _native.check(lib.aimet_dwconv2d_forward(P(inp), P(wq), P(bias) if bias is not None else None,
+                                                         P(q_dw), *dims, s))
+                _native.check(lib.aimet_adaround_recon_grad(P(q_dw), P(target), P(g_dw), q_dw.numel(), C, code, s))
+                _native.check(lib.aimet_dwconv2d_grad_weight(P(inp), P(g_dw), P(gw_dw), P(ws), *dims, s))
+                _native.check(lib.aimet_adaround_backward_adam(sq.pw, sq.pa, P(gw_dw), P(exp_avg), P(exp_avg_sq),
+                                                               *sq.shape, sq.pd, sq.po, sq.bw, P(rb_all), it_next,
+                                                               it_cur, *adam, loss_ptr, s))
+                return
             q_out = layer_forward(module, inp, wq)
-            code = _act_code(act_func)
             if code is None or q_out.dim() < 2:
                 qa, ta = (act_func(q_out), act_func(target)) if act_func is not None else (q_out, target)
                 (gw,) = torch.autograd.grad(recon_loss(qa, ta), wq)

@@ -1,0 +1,249 @@
+// dwconv.hip -- depthwise 2-D convolution forward and weight gradient for gfx950: the layer math
+// of the AdaRound loop on MobileNet-class depthwise layers (aimet_amd.adaround_optimizer).
+//
+// AdaRound's per-iteration work on a depthwise layer (adaround_optimizer.py:181-218) is
+// q_out = conv(x, Wq) and dL/dWq = conv_weight_grad(x, dL/dq_out) over a 32-sample batch; the
+// input gradient is never needed. PyTorch's native depthwise kernels take 36 us (forward) and
+// 100 us (weight gradient) per MobileNet-v2 depthwise layer-iteration (profiles/r02
+// adaround_loop_kernels_v1.csv); both are HBM-bound elementwise-plus-reduction work:
+//   forward:     reads x once (neighbours from L1/L2), writes y:   (|x| + |y|) * 4 B
+//   weight grad: reads x and dy once:                               (|x| + |dy|) * 4 B
+//
+// Layout NCHW fp32, square kernel K (3 or 5), square stride / padding / dilation, groups == C
+// (one filter per channel), weights [C][1][K][K].
+//
+// Forward: one lane per output in NCHW order (coalesced stores), y = bias + sum_kh sum_kw
+// w * x in that order with fused multiply-adds (PyTorch's conv_depthwise2d_forward_kernel order).
+// Weight grad: the (n, oh, ow) positions of a channel are split into S contiguous slices, one
+// workgroup each; every lane keeps K*K partial sums, reduced in the workgroup by a fixed shuffle
+// tree, stored per slice; a fold kernel adds the slices in order -- deterministic.
+#include "common.hpp"
+
+namespace aimet_amd
+{
+namespace
+{
+
+struct DwShape
+{
+    uint32_t N, C, H, W, OH, OW;
+    int stride, pad, dil;
+    FastDiv div_ow, div_ohow, div_c;
+};
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void dw_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                        const float* __restrict__ bias, float* __restrict__ y,
+                                                        DwShape s, uint32_t total)
+{
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= total)
+        return;
+    const uint32_t nc  = s.div_ohow.div(i);
+    const uint32_t rem = i - nc * (s.OH * s.OW);
+    const uint32_t oh  = s.div_ow.div(rem);
+    const uint32_t ow  = rem - oh * s.OW;
+    const uint32_t c   = nc - s.div_c.div(nc) * s.C;
+    const float* xp    = x + (size_t) nc * s.H * s.W;
+    const float* wp    = w + c * K * K;
+    float v            = bias ? bias[c] : 0.0f;
+    const int ih0 = (int) oh * s.stride - s.pad, iw0 = (int) ow * s.stride - s.pad;
+#pragma unroll
+    for (int kh = 0; kh < K; ++kh)
+    {
+        const int ih = ih0 + kh * s.dil;
+        if (ih < 0 || ih >= (int) s.H)
+            continue;
+#pragma unroll
+        for (int kw = 0; kw < K; ++kw)
+        {
+            const int iw = iw0 + kw * s.dil;
+            if (iw >= 0 && iw < (int) s.W)
+                v = __builtin_fmaf(wp[kh * K + kw], xp[ih * (int) s.W + iw], v);
+        }
+    }
+    y[i] = v;
+}
+
+// partial[(c * S + slice) * K*K + k]: channel c, positions [slice * per, (slice + 1) * per) of its
+// N*OH*OW outputs (position p = (n * OH + oh) * OW + ow)
+template <int K>
+__global__ __launch_bounds__(kBlock) void dw_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                                                          float* __restrict__ partial, DwShape s, uint32_t per)
+{
+    constexpr int KK  = K * K;
+    const uint32_t c  = blockIdx.y;
+    const uint32_t S  = gridDim.x;
+    const uint32_t np = s.N * s.OH * s.OW;
+    const uint32_t p0 = blockIdx.x * per;
+    const uint32_t p1 = p0 + per < np ? p0 + per : np;
+    float acc[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k)
+        acc[k] = 0.0f;
+    for (uint32_t p = p0 + threadIdx.x; p < p1; p += kBlock)
+    {
+        const uint32_t n   = s.div_ohow.div(p);
+        const uint32_t rem = p - n * (s.OH * s.OW);
+        const uint32_t oh  = s.div_ow.div(rem);
+        const uint32_t ow  = rem - oh * s.OW;
+        const size_t plane = (size_t) n * s.C + c;
+        const float g      = gy[plane * s.OH * s.OW + rem];
+        const float* xp    = x + plane * s.H * s.W;
+        const int ih0 = (int) oh * s.stride - s.pad, iw0 = (int) ow * s.stride - s.pad;
+#pragma unroll
+        for (int kh = 0; kh < K; ++kh)
+        {
+            const int ih     = ih0 + kh * s.dil;
+            const bool rowin = ih >= 0 && ih < (int) s.H;
+#pragma unroll
+            for (int kw = 0; kw < K; ++kw)
+            {
+                const int iw = iw0 + kw * s.dil;
+                if (rowin && iw >= 0 && iw < (int) s.W)
+                    acc[kh * K + kw] = __builtin_fmaf(g, xp[ih * (int) s.W + iw], acc[kh * K + kw]);
+            }
+        }
+    }
+    // workgroup reduction of the K*K sums: wave shuffles, then the waves in order
+    __shared__ float sh[KK][kBlock / 64];
+#pragma unroll
+    for (int k = 0; k < KK; ++k)
+    {
+        float v = acc[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0)
+            sh[k][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < KK)
+    {
+        float v = 0.0f;
+#pragma unroll
+        for (int i = 0; i < kBlock / 64; ++i)
+            v += sh[threadIdx.x][i];
+        partial[((size_t) c * S + blockIdx.x) * KK + threadIdx.x] = v;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void dw_wgrad_fold(const float* __restrict__ partial, float* __restrict__ gw,
+                                                        uint32_t C, uint32_t S, uint32_t KK)
+{
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;   // (c, k)
+    if (i >= C * KK)
+        return;
+    const uint32_t c = i / KK, k = i - c * KK;
+    float v          = 0.0f;
+    for (uint32_t sl = 0; sl < S; ++sl)
+        v += partial[((size_t) c * S + sl) * KK + k];
+    gw[i] = v;
+}
+
+// slices of >= 16 positions per lane, and enough workgroups (~2048) to fill the chip
+int64_t wgrad_slices(int64_t N, int64_t C, int64_t OH, int64_t OW, uint32_t* per_out)
+{
+    const int64_t np   = N * OH * OW;
+    int64_t S          = ceil_div(np, (int64_t) kBlock * 16);
+    const int64_t want = ceil_div(2048, C);
+    if (S < want)
+        S = want < ceil_div(np, kBlock) ? want : ceil_div(np, kBlock);
+    if (S < 1)
+        S = 1;
+    const uint32_t per = (uint32_t) ceil_div(np, S);
+    if (per_out)
+        *per_out = per;
+    return ceil_div(np, per);
+}
+
+DwShape make_shape(int64_t N, int64_t C, int64_t H, int64_t W, int64_t OH, int64_t OW, int K, int stride, int pad,
+                   int dil)
+{
+    AIMET_REQUIRE(K == 3 || K == 5, "depthwise kernel size must be 3 or 5");
+    AIMET_REQUIRE(N > 0 && C > 0 && H > 0 && W > 0 && OH > 0 && OW > 0, "invalid depthwise shape");
+    AIMET_REQUIRE(stride > 0 && pad >= 0 && dil > 0, "invalid stride / padding / dilation");
+    AIMET_REQUIRE((OH - 1) * stride - 2 * pad + dil * (K - 1) + 1 <= H && (OW - 1) * stride - 2 * pad + dil * (K - 1) + 1 <= W,
+                  "output size inconsistent with the input size");
+    AIMET_REQUIRE(N * C * H * W < (int64_t(1) << 31) && N * C * OH * OW < (int64_t(1) << 31),
+                  "depthwise tensors must have < 2^31 elements");
+    DwShape s;
+    s.N = (uint32_t) N, s.C = (uint32_t) C, s.H = (uint32_t) H, s.W = (uint32_t) W, s.OH = (uint32_t) OH;
+    s.OW = (uint32_t) OW, s.stride = stride, s.pad = pad, s.dil = dil;
+    s.div_ow   = FastDiv((uint32_t) OW);
+    s.div_ohow = FastDiv((uint32_t) (OH * OW));
+    s.div_c    = FastDiv((uint32_t) C);
+    return s;
+}
+
+}   // namespace
+}   // namespace aimet_amd
+
+using namespace aimet_amd;
+
+extern "C" {
+
+int aimet_dwconv2d_forward(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C,
+                           int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride, int32_t pad,
+                           int32_t dilation, void* stream)
+{
+    return guarded([&] {
+        DwShape s = make_shape(N, C, H, W, OH, OW, K, stride, pad, dilation);
+        require_device_ptr(x, "x");
+        require_device_ptr(w, "weight");
+        require_device_ptr(y, "y");
+        if (bias)
+            require_device_ptr(bias, "bias");
+        const uint32_t total = (uint32_t) (N * C * OH * OW);
+        const unsigned grid  = (unsigned) ceil_div(total, kBlock);
+        if (K == 3)
+            dw_fwd_kernel<3><<<grid, kBlock, 0, as_stream(stream)>>>(x, w, bias, y, s, total);
+        else
+            dw_fwd_kernel<5><<<grid, kBlock, 0, as_stream(stream)>>>(x, w, bias, y, s, total);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_dwconv2d_grad_weight_workspace(int64_t N, int64_t C, int64_t OH, int64_t OW, int32_t K, int64_t* elems)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(elems != nullptr, "elems is null");
+        AIMET_REQUIRE(N > 0 && C > 0 && OH > 0 && OW > 0 && (K == 3 || K == 5), "invalid depthwise shape");
+        *elems = C * wgrad_slices(N, C, OH, OW, nullptr) * K * K;
+    });
+}
+
+int aimet_dwconv2d_grad_weight(const float* x, const float* grad_y, float* grad_w, float* workspace, int64_t N,
+                               int64_t C, int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride,
+                               int32_t pad, int32_t dilation, void* stream)
+{
+    return guarded([&] {
+        DwShape s = make_shape(N, C, H, W, OH, OW, K, stride, pad, dilation);
+        require_device_ptr(x, "x");
+        require_device_ptr(grad_y, "grad_y");
+        require_device_ptr(grad_w, "grad_w");
+        AIMET_REQUIRE(C <= 65535, "depthwise weight gradient: at most 65535 channels");
+        hipStream_t st = as_stream(stream);
+        uint32_t per   = 0;
+        const int64_t S = wgrad_slices(N, C, OH, OW, &per);
+        // a caller-owned workspace (aimet_dwconv2d_grad_weight_workspace elements) keeps the call
+        // free of allocations, e.g. inside a HIP-graph capture
+        if (workspace)
+            require_device_ptr(workspace, "workspace");
+        float* partial = workspace ? workspace
+                                   : static_cast<float*>(scratch_alloc(sizeof(float) * (size_t) (C * S * K * K), st));
+        dim3 grid((unsigned) S, (unsigned) C);
+        if (K == 3)
+            dw_wgrad_kernel<3><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per);
+        else
+            dw_wgrad_kernel<5><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per);
+        AIMET_LAUNCH_CHECK();
+        dw_wgrad_fold<<<(unsigned) ceil_div(C * K * K, kBlock), kBlock, 0, st>>>(partial, grad_w, (uint32_t) C,
+                                                                                (uint32_t) S, (uint32_t) (K * K));
+        AIMET_LAUNCH_CHECK();
+        if (!workspace)
+            scratch_free(partial, st);
+    });
+}
+
+}   // extern "C"

@@ -337,6 +337,21 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
                                  const int64_t* it_next_dev, int64_t* it_cur_dev, double lr, double beta1,
                                  double beta2, double eps, float* round_loss_dev, void* stream);
 
+/* Depthwise 2-D convolution (groups == C, weights [C][1][K][K], K = 3 or 5, square stride /
+ * padding / dilation, NCHW fp32): the AdaRound loop's layer math on depthwise layers
+ * (adaround_optimizer.py:257-286 runs the wrapped layer's forward and autograd's weight gradient;
+ * no input gradient is needed). Forward: y = bias + sum w * x (bias may be null). Weight
+ * gradient: grad_w[C][K][K] = sum over n, oh, ow of grad_y * x, in a fixed order (deterministic);
+ * `workspace` (aimet_dwconv2d_grad_weight_workspace elements, device) may be null (internal
+ * scratch) -- pass one to keep the call allocation-free inside a HIP-graph capture. */
+int aimet_dwconv2d_forward(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C,
+                           int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride, int32_t pad,
+                           int32_t dilation, void* stream);
+int aimet_dwconv2d_grad_weight_workspace(int64_t N, int64_t C, int64_t OH, int64_t OW, int32_t K, int64_t* elems);
+int aimet_dwconv2d_grad_weight(const float* x, const float* grad_y, float* grad_w, float* workspace, int64_t N,
+                               int64_t C, int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride,
+                               int32_t pad, int32_t dilation, void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Blockwise (broadcast) quantization and the ONNX QcQuantizeOp                                */
 /* ------------------------------------------------------------------------------------------ */

@@ -863,6 +863,47 @@ def test_recon_loss_backward_fused_vs_torch(act, shape):
     torch.testing.assert_close(qa.grad, qb.grad, rtol=2e-6, atol=1e-12)
 
 
+@pytest.mark.parametrize("N,C,H,K,stride,pad,dil", [(32, 32, 112, 3, 1, 1, 1), (32, 96, 112, 3, 2, 1, 1),
+                                                    (5, 7, 13, 3, 2, 0, 1), (4, 16, 19, 5, 1, 2, 1),
+                                                    (3, 12, 17, 3, 1, 2, 2), (32, 960, 7, 3, 1, 1, 1)])
+def test_depthwise_conv_kernels_vs_torch(N, C, H, K, stride, pad, dil):
+    """aimet_dwconv2d_forward == torch's depthwise conv2d (native kernel, bias included) and
+    aimet_dwconv2d_grad_weight == autograd's weight gradient, to fp32 summation-order tolerance."""
+    import ctypes
+    from aimet_amd import _native
+    g = torch.Generator(device=DEV).manual_seed(N * C + K)
+    x = torch.randn(N, C, H, H, device=DEV, generator=g)
+    w = torch.randn(C, 1, K, K, device=DEV, generator=g) * 0.3
+    b = torch.randn(C, device=DEV, generator=g)
+    prev = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False
+    try:
+        wr = w.clone().requires_grad_(True)
+        ref = torch.nn.functional.conv2d(x, wr, b, stride, pad, dil, C)
+        gy = torch.randn(ref.shape, device=DEV, generator=g)
+        ref.backward(gy)
+    finally:
+        torch.backends.cudnn.enabled = prev
+    OH, OW = ref.shape[2], ref.shape[3]
+    y = torch.empty_like(ref)
+    s = torch.cuda.current_stream().cuda_stream
+    _native.call("aimet_dwconv2d_forward", x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(), N, C, H, H, OH, OW,
+                 K, stride, pad, dil, s)
+    torch.testing.assert_close(y, ref.detach(), rtol=1e-6, atol=1e-5)
+    gw = torch.empty_like(w)
+    _native.call("aimet_dwconv2d_grad_weight", x.data_ptr(), gy.data_ptr(), gw.data_ptr(), None, N, C, H, H, OH, OW,
+                 K, stride, pad, dil, s)
+    n_ws = ctypes.c_int64()
+    _native.call("aimet_dwconv2d_grad_weight_workspace", N, C, OH, OW, K, ctypes.byref(n_ws))
+    ws = torch.empty(n_ws.value, device=DEV)
+    gw2 = torch.empty_like(w)
+    _native.call("aimet_dwconv2d_grad_weight", x.data_ptr(), gy.data_ptr(), gw2.data_ptr(), ws.data_ptr(), N, C, H, H,
+                 OH, OW, K, stride, pad, dil, s)
+    torch.testing.assert_close(gw2, gw, rtol=0, atol=0)          # deterministic
+    scale = float((gy.abs().sum() * x.abs().max()) / (N * OH * OW) ** 0.5)
+    torch.testing.assert_close(gw, wr.grad, rtol=2e-5, atol=1e-6 * scale)
+
+
 @pytest.mark.parametrize("layer", ["conv", "depthwise", "linear"])
 def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
     """The single-process loop with the batch draw and backward + Adam fused into two kernels

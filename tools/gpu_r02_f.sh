@@ -1,0 +1,5 @@
+#!/usr/bin/env bash
+source "$(dirname "$0")/gpu_lib.sh"
+run t_ada 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py tests/test_adaround_golden.py tests/test_adaround_dist_gpu.py -k "adaround or recon or depthwise"
+run ada_bench 300 python benchmarks/adaround_mobilenet.py --iterations 500
+echo ALLDONE
