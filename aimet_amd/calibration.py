@@ -50,14 +50,21 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
     act_quantizers[i] (per-tensor) sees activations[i] (this rank's shard when `group` spans several
     ranks); param_quantizers[j] (per-tensor or per-channel along param_ch_axes[j]) sees params[j]
     (replicated). *_settings = (bitwidth, symmetric, strict symmetric, unsigned symmetric).
-    Returns ([(encoding, valid)] of the activations, [(encodings, valid)] of the parameters)."""
+    Returns ([(encoding, valid)] of the activations, [(encodings, valid)] of the parameters).
+
+    Everything is enqueued before the host waits for anything: both streams' statistics and both
+    streams' encoding searches (with the copies of their results) -- the activations' search
+    launch does not wait for the parameters' host work -- then the parameter encodings are built
+    (their stream finishes first) while the activation passes still stream."""
     if not activations and not params:
         return [], []
     dev = (activations[0] if activations else params[0]).device
-    torch.cuda.synchronize(dev)   # inputs produced on any stream are complete
     AimetTensorQuantizer._ensure_many(list(act_quantizers) + list(param_quantizers), dev)
     side = _side_stream(dev)
-    keep, p_res = None, []
+    # the inputs are ordered on the current stream (torch's stream semantics); the side stream
+    # starts after everything queued there so far (a device-side dependency, no host wait)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    keep, p_pending = None, None
     acts_first = _SCHEDULE == "acts_first"
     if act_quantizers and acts_first:
         # the HBM-bound activation passes start first; the parameters' short statistics and their
@@ -67,12 +74,12 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
         # enqueued first: the parameters' statistics take the CUs before the activation passes
         with torch.cuda.stream(side):
             keep = AimetTensorQuantizer.updateStatsPerChannelMany(param_quantizers, params, param_ch_axes)
+            p_pending = AimetTensorQuantizer.getEncodingsAsync(param_quantizers, *param_settings)
     if act_quantizers and not acts_first:
         D.sharded_update_stats(list(act_quantizers), list(activations), group=group)
-    if param_quantizers:
-        with torch.cuda.stream(side):
-            p_res = AimetTensorQuantizer.getEncodings(param_quantizers, *param_settings)   # syncs the side stream
-        del keep
-    a_res = AimetTensorQuantizer.getEncodings(act_quantizers, *act_settings) if act_quantizers else []
+    a_pending = AimetTensorQuantizer.getEncodingsAsync(act_quantizers, *act_settings) if act_quantizers else None
+    p_res = p_pending.result() if p_pending is not None else []
+    del keep
+    a_res = a_pending.result() if a_pending is not None else []
     torch.cuda.synchronize(dev)
     return a_res, p_res

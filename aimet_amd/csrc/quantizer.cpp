@@ -359,6 +359,38 @@ int aimet_tq_reset_encoding_stats(aimet_tensor_quantizer* q, void* stream)
     });
 }
 
+int aimet_tq_reset_encoding_stats_many(aimet_tensor_quantizer* const* qs, int64_t nq, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(nq >= 0 && (qs != nullptr || nq == 0), "null argument");
+        if (nq == 0)
+            return;
+        std::vector<ZeroJob> zero;
+        std::vector<ResetJob> resets;
+        for (int64_t i = 0; i < nq; ++i)
+        {
+            aimet_tensor_quantizer* q = qs[i];
+            AIMET_REQUIRE(q != nullptr, "null quantizer");
+            AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one batched reset share a device");
+            zero.push_back(ZeroJob {q->arena, (int64_t) q->arena_bytes});
+            if (q->d.minmax && !in_arena(q, q->d.minmax))
+                zero.push_back(ZeroJob {q->d.minmax, (int64_t) (sizeof(float) * 2 * q->C)});
+            if (q->d.counts && !in_arena(q, q->d.counts))
+                zero.push_back(ZeroJob {q->d.counts, (int64_t) (sizeof(unsigned long long) * kPdfSize * q->C)});
+            resets.push_back(ResetJob {q->d.acc, q->C});
+        }
+        DeviceGuard g(qs[0]->device);
+        hipStream_t st = as_stream(stream);
+        launch_zero_many(zero, st);
+        launch_reset_state_many(resets, st);
+        for (int64_t i = 0; i < nq; ++i)
+        {
+            qs[i]->stats_updated = false;
+            qs[i]->percentile    = 100.0f;
+        }
+    });
+}
+
 int aimet_tq_set_percentile_value(aimet_tensor_quantizer* q, float p)
 {
     return guarded([&] {
@@ -780,82 +812,218 @@ int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int sym, int s
     });
 }
 
-int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym, int strict,
-                           int unsign, aimet_tf_encoding* out, int* valid, void* stream)
+}   // extern "C"
+
+// A batched getEncoding in flight: every device search enqueued on `stream`, the TF-Enhanced
+// results on their way into a pinned block, `done` recorded after them.
+struct aimet_encoding_request
 {
-    return guarded([&] {
-        AIMET_REQUIRE(qs != nullptr && out != nullptr && nq >= 0, "null argument");
-        int64_t total = 0;
+    std::vector<aimet_tensor_quantizer*> qs;
+    int32_t b  = 0;
+    int sym    = 0, strict = 0, unsign = 0;
+    int device = 0;
+    hipEvent_t done = nullptr;
+    void* pinned    = nullptr;   // TF-Enhanced encodings, concatenated
+    size_t pinned_bytes = 0;
+    std::vector<int64_t> tfe_offs, tfe_Cs;   // per TF-E quantizer: offset in `out`, channels
+};
+
+namespace
+{
+
+// pinned result blocks and events, reused across requests (two may be in flight at once: the
+// parameters' on a side stream and the activations' on the main stream)
+struct RequestPool
+{
+    std::mutex m;
+    std::vector<std::pair<void*, size_t>> blocks;
+    std::vector<hipEvent_t> events;
+};
+RequestPool& request_pool()
+{
+    static RequestPool* p = new RequestPool;   // outlives static destruction (no HIP calls at exit)
+    return *p;
+}
+
+void* take_pinned(size_t bytes, size_t* real)
+{
+    RequestPool& p = request_pool();
+    {
+        std::lock_guard<std::mutex> lock(p.m);
+        size_t best = p.blocks.size();
+        for (size_t i = 0; i < p.blocks.size(); ++i)
+            if (p.blocks[i].second >= bytes && (best == p.blocks.size() || p.blocks[i].second < p.blocks[best].second))
+                best = i;
+        if (best != p.blocks.size())
+        {
+            auto blk = p.blocks[best];
+            p.blocks.erase(p.blocks.begin() + (std::ptrdiff_t) best);
+            *real = blk.second;
+            return blk.first;
+        }
+    }
+    void* ptr = nullptr;
+    AIMET_HIP_CHECK(hipHostMalloc(&ptr, bytes, hipHostMallocDefault));
+    *real = bytes;
+    return ptr;
+}
+
+hipEvent_t take_event()
+{
+    RequestPool& p = request_pool();
+    {
+        std::lock_guard<std::mutex> lock(p.m);
+        if (!p.events.empty())
+        {
+            hipEvent_t e = p.events.back();
+            p.events.pop_back();
+            return e;
+        }
+    }
+    hipEvent_t e = nullptr;
+    AIMET_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+}
+
+void release_request(aimet_encoding_request* r)
+{
+    if (r == nullptr)
+        return;
+    RequestPool& p = request_pool();
+    {
+        std::lock_guard<std::mutex> lock(p.m);
+        if (r->pinned)
+            p.blocks.emplace_back(r->pinned, r->pinned_bytes);
+        if (r->done)
+            p.events.push_back(r->done);
+    }
+    delete r;
+}
+
+}   // namespace
+
+extern "C" {
+
+int aimet_tq_get_encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym, int strict,
+                                  int unsign, void* stream, aimet_encoding_request** req_out)
+{
+    aimet_encoding_request* req = nullptr;
+    const int rc = guarded([&] {
+        AIMET_REQUIRE(req_out != nullptr && nq >= 0 && (qs != nullptr || nq == 0), "null argument");
+        *req_out = nullptr;
         for (int64_t i = 0; i < nq; ++i)
         {
             AIMET_REQUIRE(qs[i] != nullptr, "null quantizer");
             AIMET_REQUIRE(qs[i]->device == qs[0]->device, "quantizers of one batched getEncoding share a device");
-            total += qs[i]->C;
         }
-        std::memset(out, 0, sizeof(aimet_tf_encoding) * total);
+        req         = new aimet_encoding_request;
+        req->qs.assign(qs, qs + nq);
+        req->b      = (int32_t) (uint8_t) bw;   // computeEncoding(uint8_t bw, ...)
+        req->sym    = sym;
+        req->strict = strict;
+        req->unsign = unsign;
         if (nq == 0)
             return;
-        DeviceGuard g(qs[0]->device);
-        const int32_t b = (int32_t) (uint8_t) bw;
+        req->device = qs[0]->device;
+        DeviceGuard g(req->device);
+        hipStream_t st = as_stream(stream);
+        const int32_t b = req->b;
         // every TF-Enhanced search in ONE launch (one workgroup per channel of every quantizer),
-        // results back in one copy; the other schemes read back their statistics per quantizer
-        std::vector<const TqDevice*> ds;
-        std::vector<int64_t> Cs, offs;
+        // results back in one copy; the MSE / entropy searches enqueued beside it; the other
+        // schemes read back their statistics when the request is finished
+        std::vector<const TqDevice*> tfe, ent, mse;
+        std::vector<int64_t> entC, mseC;
         int64_t off = 0, tfe_total = 0;
         for (int64_t i = 0; i < nq; ++i)
         {
-            if (valid)
-                valid[i] = qs[i]->stats_updated ? 1 : 0;
-            if (qs[i]->stats_updated && qs[i]->hist && qs[i]->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
+            aimet_tensor_quantizer* q = qs[i];
+            if (q->stats_updated && q->hist && q->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
             {
-                ds.push_back(&qs[i]->d);
-                Cs.push_back(qs[i]->C);
-                offs.push_back(off);
-                tfe_total += qs[i]->C;
+                tfe.push_back(&q->d);
+                req->tfe_Cs.push_back(q->C);
+                req->tfe_offs.push_back(off);
+                tfe_total += q->C;
             }
-            off += qs[i]->C;
+            else if (q->stats_updated && entropy_device(q, b))
+            {
+                ent.push_back(&q->d);
+                entC.push_back(q->C);
+            }
+            else if (q->stats_updated && q->hist && q->scheme == AIMET_QUANTIZATION_MSE)
+            {
+                mse.push_back(&q->d);
+                mseC.push_back(q->C);
+            }
+            off += q->C;
         }
-        std::vector<const TqDevice*> ent, mse;
-        std::vector<int64_t> entC, mseC;
-        for (int64_t i = 0; i < nq; ++i)   // the other device searches (MSE, entropy), enqueued before the sync
+        launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0, st);
+        launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0, st);
+        if (tfe_total > 0)
         {
-            if (!qs[i]->stats_updated)
-                continue;
-            if (entropy_device(qs[i], b))
-            {
-                ent.push_back(&qs[i]->d);
-                entC.push_back(qs[i]->C);
-            }
-            else if (qs[i]->hist && qs[i]->scheme == AIMET_QUANTIZATION_MSE)
-            {
-                mse.push_back(&qs[i]->d);
-                mseC.push_back(qs[i]->C);
-            }
+            req->pinned = take_pinned(sizeof(aimet_tf_encoding) * (size_t) tfe_total, &req->pinned_bytes);
+            launch_tfe_search_many_to(tfe.data(), req->tfe_Cs.data(), (int) tfe.size(), b, sym, strict, unsign,
+                                      static_cast<aimet_tf_encoding*>(req->pinned), st);
         }
-        launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0,
-                               as_stream(stream));
-        launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0,
-                                   as_stream(stream));
-        std::vector<aimet_tf_encoding> tfe(tfe_total);
-        launch_tfe_search_many(ds.data(), Cs.data(), (int) ds.size(), b, sym, strict, unsign, tfe.data(),
-                               as_stream(stream));
-        for (size_t k = 0, src = 0; k < ds.size(); src += Cs[k], ++k)
-            std::memcpy(out + offs[k], tfe.data() + src, sizeof(aimet_tf_encoding) * Cs[k]);
-        AIMET_HIP_CHECK(hipStreamSynchronize(as_stream(stream)));
-        off = 0;
+        req->done = take_event();
+        AIMET_HIP_CHECK(hipEventRecord(req->done, st));
+    });
+    if (rc != AIMET_OK)
+    {
+        release_request(req);
+        return rc;
+    }
+    *req_out = req;
+    return rc;
+}
+
+int aimet_tq_get_encodings_finish(aimet_encoding_request* req, aimet_tf_encoding* out, int* valid)
+{
+    const int rc = guarded([&] {
+        AIMET_REQUIRE(req != nullptr, "request is null");
+        const int64_t nq = (int64_t) req->qs.size();
+        int64_t total    = 0;
+        for (aimet_tensor_quantizer* q: req->qs)
+            total += q->C;
+        AIMET_REQUIRE(out != nullptr || total == 0, "out is null");
+        if (total)
+            std::memset(out, 0, sizeof(aimet_tf_encoding) * total);
+        for (int64_t i = 0; i < nq; ++i)
+            if (valid)
+                valid[i] = req->qs[i]->stats_updated ? 1 : 0;
+        if (nq == 0)
+            return;
+        DeviceGuard g(req->device);
+        AIMET_HIP_CHECK(hipEventSynchronize(req->done));
+        auto* tfe = static_cast<const aimet_tf_encoding*>(req->pinned);
+        for (size_t k = 0, src = 0; k < req->tfe_Cs.size(); src += req->tfe_Cs[k], ++k)
+            std::memcpy(out + req->tfe_offs[k], tfe + src, sizeof(aimet_tf_encoding) * req->tfe_Cs[k]);
         std::vector<aimet_tensor_quantizer*> host_q;
         std::vector<aimet_tf_encoding*> host_out;
-        for (int64_t i = 0; i < nq; ++i)
+        int64_t off = 0;
+        for (aimet_tensor_quantizer* q: req->qs)
         {
-            if (qs[i]->stats_updated && !(qs[i]->hist && qs[i]->scheme == AIMET_QUANTIZATION_TF_ENHANCED))
+            if (q->stats_updated && !(q->hist && q->scheme == AIMET_QUANTIZATION_TF_ENHANCED))
             {
-                host_q.push_back(qs[i]);
+                host_q.push_back(q);
                 host_out.push_back(out + off);
             }
-            off += qs[i]->C;
+            off += q->C;
         }
-        collect_encodings(host_q.data(), host_out.data(), (int64_t) host_q.size(), b, sym, strict, unsign);
+        collect_encodings(host_q.data(), host_out.data(), (int64_t) host_q.size(), req->b, req->sym, req->strict,
+                          req->unsign);
     });
+    release_request(req);
+    return rc;
+}
+
+int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym, int strict,
+                           int unsign, aimet_tf_encoding* out, int* valid, void* stream)
+{
+    aimet_encoding_request* req = nullptr;
+    const int rc = aimet_tq_get_encodings_launch(qs, nq, bw, sym, strict, unsign, stream, &req);
+    if (rc != AIMET_OK)
+        return rc;
+    return aimet_tq_get_encodings_finish(req, out, valid);
 }
 
 int aimet_tq_get_stats_histogram(aimet_tensor_quantizer* q, int64_t channel, double* xleft, double* pdf, int* n,

@@ -238,6 +238,28 @@ void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool stri
     launch_kernel(job_of(d, 0), nullptr, 0, C, bw, sym, strict, unsign, s);
 }
 
+void launch_tfe_search_many_to(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
+                               bool unsign, aimet_tf_encoding* pinned_dst, hipStream_t s)
+{
+    if (n == 0)
+        return;
+    std::vector<TfeJob> jobs(n);
+    int64_t total = 0;
+    for (int i = 0; i < n; ++i)
+    {
+        jobs[i] = job_of(*ds[i], total);
+        total += Cs[i];
+    }
+    auto* dout = static_cast<aimet_tf_encoding*>(scratch_alloc(sizeof(aimet_tf_encoding) * total, s));
+    for (int i = 0; i < n; ++i)
+        jobs[i].out = dout + jobs[i].start;
+    auto* djobs = static_cast<TfeJob*>(upload_async(jobs.data(), sizeof(TfeJob) * n, s));
+    launch_kernel(jobs[0], djobs, n, total, bw, sym, strict, unsign, s);
+    AIMET_HIP_CHECK(hipMemcpyAsync(pinned_dst, dout, sizeof(aimet_tf_encoding) * total, hipMemcpyDeviceToHost, s));
+    scratch_free(djobs, s);
+    scratch_free(dout, s);
+}
+
 void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
                             bool unsign, aimet_tf_encoding* host_out, hipStream_t s)
 {

@@ -63,6 +63,13 @@ struct ResetJob
     int64_t C;
 };
 void launch_reset_state_many(const std::vector<ResetJob>& jobs, hipStream_t s);
+// zero many device ranges in one launch (16-B aligned starts; any length)
+struct ZeroJob
+{
+    void* p;
+    int64_t bytes;
+};
+void launch_zero_many(const std::vector<ZeroJob>& jobs, hipStream_t s);
 // Many per-tensor quantizers (C == 1) in one launch per phase (stats.hip: launch_stats_many)
 struct StatsJob
 {
@@ -104,6 +111,10 @@ void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool stri
 // (sum of Cs). Synchronises s.
 void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
                             bool unsign, aimet_tf_encoding* host_out, hipStream_t s);
+// the same, asynchronous: the encodings are copied into pinned_dst (host-pinned, sum of Cs entries)
+// on s; the caller synchronises before reading it
+void launch_tfe_search_many_to(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
+                               bool unsign, aimet_tf_encoding* pinned_dst, hipStream_t s);
 // mse_search.hip: d.enc[c] <- MSE encoding of channel c (statistics updated)
 size_t mse_part_bytes(int64_t C);
 void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);

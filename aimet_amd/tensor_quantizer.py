@@ -179,6 +179,24 @@ class AimetTensorQuantizer:
                 _native.call("aimet_tq_reset_encoding_stats", self._handle,
                              torch.cuda.current_stream(self._device).cuda_stream)
 
+    @staticmethod
+    def resetEncodingStatsMany(quantizers):
+        """resetEncodingStats of many quantizers: two launches on the current stream of their device
+        (aimet_tq_reset_encoding_stats_many), no host synchronisation."""
+        qs = list(quantizers)
+        for q in qs:
+            q._is_encoding_valid = False
+            q._pending_percentile = None
+        live = [q for q in qs if q._handle is not None]
+        by_dev = {}
+        for q in live:
+            by_dev.setdefault(q._device, []).append(q)
+        for dev, group in by_dev.items():
+            handles = (ctypes.c_void_p * len(group))(*[q._handle for q in group])
+            with torch.cuda.device(dev):
+                _native.call("aimet_tq_reset_encoding_stats_many", handles, len(group),
+                             torch.cuda.current_stream(dev).cuda_stream)
+
     def updateStats(self, tensor: torch.Tensor, use_cuda: bool = True):
         """AimetTensorQuantizer.cpp:98-127 (per-tensor; the whole tensor feeds one analyzer)."""
         if self._num_channels != 1:
@@ -372,41 +390,17 @@ class AimetTensorQuantizer:
         encoding search is enqueued first): the per-quantizer loop of
         QuantizationSimModel.compute_encodings (v1/quantsim.py:425-449), batched.
         Returns [(encoding or list of encodings, is_valid)] in input order."""
-        quantizers = list(quantizers)
-        live = [q for q in quantizers if q._handle is not None and q._is_encoding_valid]
-        results = {}
-        if live:
-            dev = live[0]._device
-            total = sum(q._num_channels for q in live)
-            out = TfEncoding.array(total)
-            valid = (ctypes.c_int * len(live))()
-            handles = (ctypes.c_void_p * len(live))(*[q._handle for q in live])
-            with torch.cuda.device(dev):
-                _native.call("aimet_tq_get_encodings", handles, len(live), int(bitwidth),
-                             int(bool(use_symmetric_encodings)), int(bool(use_strict_symmetric)),
-                             int(bool(use_unsigned_symmetric)), out, valid, torch.cuda.current_stream(dev).cuda_stream)
-            # tens of thousands of small objects: keep the cyclic GC from firing mid-list
-            gc_was_enabled = gc.isenabled()
-            gc.disable()
-            try:
-                # ctypes array slicing builds the element objects in one C-level pass (about 2x
-                # faster than list(out) + list slicing)
-                off = 0
-                for i, q in enumerate(live):
-                    C = q._num_channels
-                    results[id(q)] = (out[off] if C == 1 else out[off:off + C], bool(valid[i]))
-                    off += C
-            finally:
-                if gc_was_enabled:
-                    gc.enable()
-        res = []
-        for q in quantizers:
-            if id(q) in results:
-                res.append(results[id(q)])
-            else:
-                e = [TfEncoding() for _ in range(q._num_channels)]
-                res.append((e[0] if q._num_channels == 1 else e, False))
-        return res
+        return AimetTensorQuantizer.getEncodingsAsync(quantizers, bitwidth, use_symmetric_encodings,
+                                                      use_strict_symmetric, use_unsigned_symmetric).result()
+
+    @staticmethod
+    def getEncodingsAsync(quantizers, bitwidth, use_symmetric_encodings, use_strict_symmetric,
+                          use_unsigned_symmetric) -> "PendingEncodings":
+        """getEncodings in two halves: the device searches and the copies of their results are
+        enqueued on the current stream now (aimet_tq_get_encodings_launch); .result() waits for
+        them and builds the encodings. Between the two the host may enqueue other work."""
+        return PendingEncodings(list(quantizers), bitwidth, use_symmetric_encodings, use_strict_symmetric,
+                                use_unsigned_symmetric)
 
     def getStatsHistogram(self, channel: int = 0):
         """AimetTensorQuantizer.cpp:194-198 -> list of (xLeft, pdf)."""
@@ -521,6 +515,64 @@ class AimetTensorQuantizer:
         table = self.channelTable(encodings, t.device)
         out = qdq_per_channel_table(t, table, N // (C * K), C, K, round_mode)
         return out.cpu() if staged else out
+
+
+class PendingEncodings:
+    """A batched getEncoding in flight (AimetTensorQuantizer.getEncodingsAsync)."""
+
+    def __init__(self, quantizers, bitwidth, sym, strict, unsign):
+        self.quantizers = quantizers
+        self.live = [q for q in quantizers if q._handle is not None and q._is_encoding_valid]
+        self.req = None
+        if self.live:
+            dev = self.live[0]._device
+            handles = (ctypes.c_void_p * len(self.live))(*[q._handle for q in self.live])
+            req = ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                _native.call("aimet_tq_get_encodings_launch", handles, len(self.live), int(bitwidth), int(bool(sym)),
+                             int(bool(strict)), int(bool(unsign)), torch.cuda.current_stream(dev).cuda_stream,
+                             ctypes.byref(req))
+            self.req = req
+
+    def result(self):
+        results = {}
+        if self.live:
+            if self.req is None:
+                raise RuntimeError("PendingEncodings.result() called twice")
+            total = sum(q._num_channels for q in self.live)
+            out = TfEncoding.array(total)
+            valid = (ctypes.c_int * len(self.live))()
+            req, self.req = self.req, None
+            _native.call("aimet_tq_get_encodings_finish", req, out, valid)
+            # tens of thousands of small objects: keep the cyclic GC from firing mid-list
+            gc_was_enabled = gc.isenabled()
+            gc.disable()
+            try:
+                # ctypes array slicing builds the element objects in one C-level pass (about 2x
+                # faster than list(out) + list slicing)
+                off = 0
+                for i, q in enumerate(self.live):
+                    C = q._num_channels
+                    results[id(q)] = (out[off] if C == 1 else out[off:off + C], bool(valid[i]))
+                    off += C
+            finally:
+                if gc_was_enabled:
+                    gc.enable()
+        res = []
+        for q in self.quantizers:
+            if id(q) in results:
+                res.append(results[id(q)])
+            else:
+                e = [TfEncoding() for _ in range(q._num_channels)]
+                res.append((e[0] if q._num_channels == 1 else e, False))
+        return res
+
+    def __del__(self):
+        if getattr(self, "req", None) is not None:   # never finished: release it (waits for the searches)
+            try:
+                _native.call("aimet_tq_get_encodings_finish", self.req, None, None)
+            except Exception:
+                pass
 
 
 IO_DTYPES = {torch.float16: 1, torch.bfloat16: 2}   # aimet_*_16 io_dtype codes

@@ -184,6 +184,11 @@ int aimet_tq_create_many(const int* schemes, const int64_t* num_channels, int64_
                          aimet_tensor_quantizer** out);
 /* AimetTensorQuantizer.cpp:89-96 resetEncodingStats (synchronous w.r.t. `stream`). */
 int aimet_tq_reset_encoding_stats(aimet_tensor_quantizer* q, void* stream);
+/* resetEncodingStats of nq quantizers (one device) as two launches on `stream` (every state
+ * range zeroed by one kernel, the running min/max re-initialised by another); no host
+ * synchronisation (QuantizationSimModel.compute_encodings' reset of every quantizer,
+ * v1/quantsim.py:387-399). */
+int aimet_tq_reset_encoding_stats_many(aimet_tensor_quantizer* const* qs, int64_t nq, void* stream);
 /* AimetTensorQuantizer.cpp:200-207 setPercentileValue (percentile scheme only). */
 int aimet_tq_set_percentile_value(aimet_tensor_quantizer* q, float percentile);
 int aimet_tq_get_percentile_value(aimet_tensor_quantizer* q, float* percentile);
@@ -257,6 +262,17 @@ int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int use_symmet
 int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int use_symmetric,
                            int use_strict_symmetric, int use_unsigned_symmetric, aimet_tf_encoding* out, int* valid,
                            void* stream);
+
+/* aimet_tq_get_encodings in two halves, so the host can enqueue more work (another stream's
+ * searches, the next batch) before it waits: _launch enqueues every device search on `stream`
+ * and the copies of their results into pinned memory, and returns a request; _finish waits for
+ * it, finishes the host-side encodings (TF, percentile, entropy near-ties) and frees the request
+ * (always, also on error). */
+typedef struct aimet_encoding_request aimet_encoding_request;
+int aimet_tq_get_encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int use_symmetric,
+                                  int use_strict_symmetric, int use_unsigned_symmetric, void* stream,
+                                  aimet_encoding_request** request);
+int aimet_tq_get_encodings_finish(aimet_encoding_request* request, aimet_tf_encoding* out, int* valid);
 
 /* AimetTensorQuantizer.cpp:194-198 getStatsHistogram (histogram schemes): xleft/pdf[512] of
  * `channel`; *n = 0 when no histogram exists yet. Synchronises `stream`. */

@@ -845,6 +845,46 @@ def test_update_stats_channels_many_equals_individual():
                 assert qa.getStatsHistogram(c) == qb.getStatsHistogram(c)
 
 
+def test_reset_many_then_recompute_equals_fresh_quantizers():
+    """aimet_tq_reset_encoding_stats_many (one zeroing launch + one re-initialisation, no sync)
+    leaves quantizers that calibrate exactly like new ones (TF, TF-E, percentile, MSE, entropy;
+    per-tensor and per-channel)."""
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    g = torch.Generator(device=DEV).manual_seed(21)
+    modes = [QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
+             QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE,
+             QuantizationMode.QUANTIZATION_ENTROPY]
+
+    def make():
+        return [AimetTensorQuantizer(m) for m in modes] + [AimetTensorQuantizer(m, num_channels=6) for m in modes]
+
+    def feed(qs, seed):
+        gg = torch.Generator(device=DEV).manual_seed(seed)
+        x = torch.randn(4, 6, 9, 9, device=DEV, generator=gg) * 3 + 1
+        for q in qs:
+            if q.num_channels == 1:
+                q.updateStats(x, True)
+            else:
+                q.updateStatsPerChannel(x, 1, True)
+
+    def encs(qs):
+        out = []
+        for q in qs:
+            e, v = q.getEncoding(8, False, False, False)
+            out.append(([t.to_tuple() for t in e] if isinstance(e, list) else e.to_tuple(), v))
+        return out
+
+    used = make()
+    feed(used, 1)
+    feed(used, 2)
+    AimetTensorQuantizer.resetEncodingStatsMany(used)
+    assert all(not v for _, v in encs(used))
+    feed(used, 3)
+    fresh = make()
+    feed(fresh, 3)
+    assert encs(used) == encs(fresh)
+
+
 @pytest.mark.parametrize("act", [None, torch.nn.ReLU(), torch.nn.ReLU6()])
 @pytest.mark.parametrize("shape", [(32, 24, 12, 12), (32, 1000), (3, 5, 7)])
 def test_recon_loss_backward_fused_vs_torch(act, shape):

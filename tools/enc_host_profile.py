@@ -17,7 +17,8 @@ from aimet_amd.tensor_quantizer import AimetTensorQuantizer  # noqa: E402
 from workloads.resnet import resnet50  # noqa: E402
 
 
-def one(acts, weights, dev):
+def one(acts, weights, dev, qs=None):
+    """qs None: new quantizers (constructed + created in the call); else (aq, wq) reset."""
     TFE = QuantizationMode.QUANTIZATION_TF_ENHANCED
     t = []
     torch.cuda.synchronize()
@@ -25,24 +26,33 @@ def one(acts, weights, dev):
 
     def mark(k):
         t.append((k, time.perf_counter()))
-    aq = [AimetTensorQuantizer(TFE) for _ in acts]
-    wq = [AimetTensorQuantizer(TFE, num_channels=w.shape[0]) for w in weights]
-    mark("construct")
+    if qs is None:
+        aq = [AimetTensorQuantizer(TFE) for _ in acts]
+        wq = [AimetTensorQuantizer(TFE, num_channels=w.shape[0]) for w in weights]
+        mark("construct")
+    else:
+        aq, wq = qs
+        AimetTensorQuantizer.resetEncodingStatsMany(aq + wq)
+        mark("reset_many")
     torch.cuda.synchronize(dev)
     mark("sync_in")
     AimetTensorQuantizer._ensure_many(aq + wq, dev)
-    mark("create_many")
-    with torch.cuda.stream(CAL._side_stream(dev)):
+    mark("ensure_many")
+    side = CAL._side_stream(dev)
+    with torch.cuda.stream(side):
         keep = AimetTensorQuantizer.updateStatsPerChannelMany(wq, weights)
-    mark("w_update_launch")
+        mark("w_update_launch")
+        pw = AimetTensorQuantizer.getEncodingsAsync(wq, 8, True, False, False)
+        mark("w_getencs_launch")
     D.sharded_update_stats(aq, acts)
     mark("act_update_launch")
-    with torch.cuda.stream(CAL._side_stream(dev)):
-        p = AimetTensorQuantizer.getEncodings(wq, 8, True, False, False)
-        mark("w_getencs(sync side)")
-        del keep
-    a = AimetTensorQuantizer.getEncodings(aq, 8, False, False, False)
-    mark("act_getencs(sync)")
+    pa = AimetTensorQuantizer.getEncodingsAsync(aq, 8, False, False, False)
+    mark("act_getencs_launch")
+    pw.result()
+    mark("w_result(waits side)")
+    del keep
+    pa.result()
+    mark("act_result(waits main)")
     torch.cuda.synchronize(dev)
     mark("sync_out")
     prev, parts = t0, []
@@ -62,11 +72,14 @@ def main():
     acts = [a for _, a in acts]
     weights = [w for _, w in weights]
     keep = None
-    for rep in range(8):
+    for rep in range(4):
         del keep
         total, parts, aq, wq = one(acts, weights, dev)
         keep = (aq, wq)
-        print("rep %d total %.3f ms | %s" % (rep, total, " | ".join(parts)), flush=True)
+        print("fresh rep %d total %.3f ms | %s" % (rep, total, " | ".join(parts)), flush=True)
+    for rep in range(6):
+        total, parts, aq, wq = one(acts, weights, dev, keep)
+        print("reset rep %d total %.3f ms | %s" % (rep, total, " | ".join(parts)), flush=True)
     del keep
     for rep in range(4):
         *_, secs, aq, wq = bench.compute_encodings([("a", a) for a in acts], [("w", w) for w in weights])
