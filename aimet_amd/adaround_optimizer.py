@@ -28,6 +28,7 @@ iterations run are the first 1/world of it). In the HIP-graph form the iteration
 the collective between them: [forward + backward] -> all_reduce(alpha.grad) -> [/ world + Adam].
 """
 import contextlib
+import os
 import warnings
 from dataclasses import dataclass
 from typing import Callable, Optional, Tuple
@@ -86,6 +87,16 @@ def conv_backend(module: torch.nn.Module):
         yield
     finally:
         torch.backends.cudnn.enabled = prev
+
+
+# 1x1 convolutions and linear layers of the fused AdaRound loop as direct GEMMs (torch.matmul /
+# hipBLASLt) instead of MIOpen convolutions through autograd; AIMET_ADA_GEMM_LAYERS=0 turns it off
+_GEMM_LAYERS = os.environ.get("AIMET_ADA_GEMM_LAYERS", "1") != "0"
+
+
+def _is_pointwise(module: torch.nn.Module) -> bool:
+    return isinstance(module, torch.nn.Conv2d) and module.kernel_size == (1, 1) and module.stride == (1, 1) \
+        and module.padding in ((0, 0), "valid") and module.dilation == (1, 1) and module.groups == 1
 
 
 def depthwise_spec(module: torch.nn.Module):
@@ -364,47 +375,77 @@ class AdaroundOptimizer:
         adam = (ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999), ctypes.c_double(1e-8))
         loss_ptr = P(round_loss_out) if round_loss_out is not None else None
         code = _act_code(act_func)
-        dw = depthwise_spec(module) if inp.dim() == 4 and code is not None else None
-        if dw is not None:
+        out_shape = tuple(out_data.shape[1:])
+        # the fused reconstruction gradient reads the fp target in place (no gathered copy) when it
+        # has a fused form: [N, C, ...] outputs, ReLU / ReLU6 / no activation
+        indexed = code is not None and out_data.dim() >= 2 and out_data.dtype == torch.float32
+        C_out = out_shape[0] if out_data.dim() >= 2 else 1
+        hw = row_out // C_out if indexed else 1
+        bias = module.bias.detach().contiguous() if module.bias is not None else None
+        mode = "autograd"
+        if indexed and depthwise_spec(module) is not None and inp.dim() == 4:
+            mode = "dw"
+        elif indexed and _GEMM_LAYERS and _is_pointwise(module) and inp.dim() == 4:
+            mode = "pointwise"
+        elif indexed and _GEMM_LAYERS and isinstance(module, torch.nn.Linear) and inp.dim() == 2:
+            mode = "linear"
+        q_buf = torch.empty((nb,) + out_shape, dtype=torch.float32, device=dev)
+        g_buf = torch.empty_like(q_buf)
+        if mode == "dw":
             # depthwise layers: native forward + weight gradient, no autograd (aimet_dwconv2d_*)
-            K, stride, pad, dil = dw
+            K, stride, pad, dil = depthwise_spec(module)
             Nb, C, H, W = inp.shape
-            q_dw, g_dw = torch.empty_like(target), torch.empty_like(target)
             gw_dw = torch.empty_like(sq.w)
             ws_n = ctypes.c_int64()
-            _native.check(lib.aimet_dwconv2d_grad_weight_workspace(Nb, C, target.shape[2], target.shape[3], K,
+            _native.check(lib.aimet_dwconv2d_grad_weight_workspace(Nb, C, out_shape[1], out_shape[2], K,
                                                                    ctypes.byref(ws_n)))
             ws = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
-            bias = module.bias.detach().contiguous() if module.bias is not None else None
-            dims = (Nb, C, H, W, target.shape[2], target.shape[3], K, stride, pad, dil)
+            dims = (Nb, C, H, W, out_shape[1], out_shape[2], K, stride, pad, dil)
+        pbias = P(bias) if bias is not None else None
 
-        def step():
-            s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp), P(target), P(idx_all), it_cur,
-                                                    it_next, nb, row_in, row_out, s))
-            _native.check(sq.fwd(sq.pw, sq.pa, P(wq), *sq.shape, sq.pd, sq.po, sq.bw, 1, s))
-            if dw is not None:
-                _native.check(lib.aimet_dwconv2d_forward(P(inp), P(wq), P(bias) if bias is not None else None,
-                                                         P(q_dw), *dims, s))
-                _native.check(lib.aimet_adaround_recon_grad(P(q_dw), P(target), P(g_dw), q_dw.numel(), C, code, s))
-                _native.check(lib.aimet_dwconv2d_grad_weight(P(inp), P(g_dw), P(gw_dw), P(ws), *dims, s))
-                _native.check(lib.aimet_adaround_backward_adam(sq.pw, sq.pa, P(gw_dw), P(exp_avg), P(exp_avg_sq),
-                                                               *sq.shape, sq.pd, sq.po, sq.bw, P(rb_all), it_next,
-                                                               it_cur, *adam, loss_ptr, s))
-                return
-            q_out = layer_forward(module, inp, wq)
-            if code is None or q_out.dim() < 2:
-                qa, ta = (act_func(q_out), act_func(target)) if act_func is not None else (q_out, target)
-                (gw,) = torch.autograd.grad(recon_loss(qa, ta), wq)
-            else:
-                g = torch.empty_like(q_out)
-                _native.check(lib.aimet_adaround_recon_grad(P(q_out), P(target), P(g), q_out.numel(), q_out.shape[1],
-                                                            code, s))
-                (gw,) = torch.autograd.grad(q_out, wq, grad_outputs=g)
-            gw = gw if gw.is_contiguous() else gw.contiguous()
+        def recon(q, with_bias, s):
+            _native.check(lib.aimet_adaround_recon_grad_indexed(P(q), P(out_data), P(idx_all), it_cur, P(g_buf), nb,
+                                                                C_out, hw, pbias if with_bias else None, code, s))
+
+        def adam_step(gw, s):
             _native.check(lib.aimet_adaround_backward_adam(sq.pw, sq.pa, P(gw), P(exp_avg), P(exp_avg_sq), *sq.shape,
                                                            sq.pd, sq.po, sq.bw, P(rb_all), it_next, it_cur, *adam,
                                                            loss_ptr, s))
+
+        def step():
+            s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp), None if indexed else P(target),
+                                                    P(idx_all), it_cur, it_next, nb, row_in, row_out, s))
+            _native.check(sq.fwd(sq.pw, sq.pa, P(wq), *sq.shape, sq.pd, sq.po, sq.bw, 1, s))
+            if mode == "dw":
+                _native.check(lib.aimet_dwconv2d_forward(P(inp), P(wq), pbias, P(q_buf), *dims, s))
+                recon(q_buf, False, s)
+                _native.check(lib.aimet_dwconv2d_grad_weight(P(inp), P(g_buf), P(gw_dw), P(ws), *dims, s))
+                adam_step(gw_dw, s)
+                return
+            if mode == "pointwise":
+                # 1x1 convolution as one batched GEMM per direction (hipBLASLt, no NCHW<->NHWC
+                # transposes): q[n] = Wq @ x[n]; the bias is added inside the reconstruction kernel
+                x3 = inp.view(nb, inp.shape[1], -1)
+                w2 = wq.detach().view(wq.shape[0], wq.shape[1])
+                torch.matmul(w2, x3, out=q_buf.view(nb, w2.shape[0], -1))
+                recon(q_buf, True, s)
+                gw = torch.matmul(g_buf.view(nb, w2.shape[0], -1), x3.transpose(1, 2)).sum(0)
+                adam_step(gw.view_as(wq), s)
+                return
+            if mode == "linear":
+                torch.mm(inp, wq.detach().t(), out=q_buf)
+                recon(q_buf, True, s)
+                adam_step(torch.mm(g_buf.t(), inp), s)
+                return
+            q_out = layer_forward(module, inp, wq)
+            if indexed:
+                recon(q_out, False, s)
+                (gw,) = torch.autograd.grad(q_out, wq, grad_outputs=g_buf)
+            else:
+                qa, ta = (act_func(q_out), act_func(target)) if act_func is not None else (q_out, target)
+                (gw,) = torch.autograd.grad(recon_loss(qa, ta), wq)
+            adam_step(gw if gw.is_contiguous() else gw.contiguous(), s)
 
         # warm-up on a side stream (library handles, allocator, autograd), then back to iteration 0
         alpha0 = alpha.detach().clone()

@@ -404,6 +404,8 @@ __global__ __launch_bounds__(kBlock) void adaround_gather_kernel(const float* __
         it_next[0] = it + 1;
     const int b          = blockIdx.y >> 1;
     const bool out       = blockIdx.y & 1;
+    if (out && !dst_out)
+        return;   // the target is read in place (recon_grad_idx_kernel)
     const int64_t row    = out ? row_out : row_in;
     const int64_t r      = idx_all[it * nb + b];
     const float* src     = (out ? src_out : src_in) + r * row;
@@ -467,6 +469,58 @@ __global__ __launch_bounds__(kBlock) void recon_grad_kernel(const float* __restr
     for (int64_t i = begin + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
         g[i] = recon_g(q[i], t[i], scale, act);
 }
+
+// recon_grad with the fp target read in place from the cached outputs (row idx_all[it][b] for
+// sample b, it = it_cur[0]) and, optionally, the layer bias added to q first (q = the bias-free
+// GEMM output; channel = (i / hw) % C of the [nb][C][hw] batch): no gathered copy of the target,
+// no separate bias pass
+struct ReconIdx
+{
+    const float* out_data;
+    const int64_t* idx_all;
+    const int64_t* it_cur;
+    const float* bias;   // nullable
+    int64_t nb, row, hw, C;
+    FastDiv div_row, div_hw, div_c;
+};
+
+__device__ __forceinline__ float recon_bias(const ReconIdx& r, uint32_t e_in_row)
+{
+    if (!r.bias)
+        return 0.0f;
+    const uint32_t ch = r.div_hw.div(e_in_row);
+    return r.bias[ch - r.div_c.div(ch) * (uint32_t) r.C];
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kBlock) void recon_grad_idx_kernel(const float* __restrict__ q, float* __restrict__ g,
+                                                                ReconIdx r, float scale, int act)
+{
+    const int64_t it    = r.it_cur[0];
+    const uint32_t per  = VEC ? 4 : 1;
+    const uint32_t n    = (uint32_t) (r.nb * r.row);
+    const uint32_t i    = (blockIdx.x * kBlock + threadIdx.x) * per;
+    if (i >= n)
+        return;
+    const uint32_t b    = r.div_row.div(i);
+    const uint32_t e    = i - b * (uint32_t) r.row;
+    const float* t      = r.out_data + r.idx_all[it * r.nb + b] * r.row + e;
+    if (VEC)
+    {
+        const f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(q + i));
+        const f4 c = __builtin_nontemporal_load(reinterpret_cast<const f4*>(t));
+        const float bs = recon_bias(r, e);   // hw % 4 == 0: the quad shares its channel
+        f4 o;
+        o.x = recon_g(a.x + bs, c.x, scale, act);
+        o.y = recon_g(a.y + bs, c.y, scale, act);
+        o.z = recon_g(a.z + bs, c.z, scale, act);
+        o.w = recon_g(a.w + bs, c.w, scale, act);
+        __builtin_nontemporal_store(o, reinterpret_cast<f4*>(g + i));
+    }
+    else
+        g[i] = recon_g(q[i] + recon_bias(r, e), t[0], scale, act);
+}
+
 
 }   // namespace
 }   // namespace aimet_amd
@@ -620,12 +674,13 @@ int aimet_adaround_gather(const float* src_in, const float* src_out, float* dst_
         require_device_ptr(src_in, "src_in");
         require_device_ptr(src_out, "src_out");
         require_device_ptr(dst_in, "dst_in");
-        require_device_ptr(dst_out, "dst_out");
+        if (dst_out)   // null: only the inputs are gathered
+            require_device_ptr(dst_out, "dst_out");
         require_device_ptr(idx_all, "idx_all");
         require_device_ptr(it_cur, "it_cur");
         require_device_ptr(it_next, "it_next");
         const bool vec = row_in % 4 == 0 && row_out % 4 == 0 && aligned16(src_in) && aligned16(src_out) &&
-                         aligned16(dst_in) && aligned16(dst_out);
+                         aligned16(dst_in) && aligned16(dst_out);   // aligned16(nullptr) holds
         const int64_t work = (row_in > row_out ? row_in : row_out) / (vec ? 4 : 1);
         int64_t bx         = ceil_div(work, kBlock * 4);   // >= 4 items per lane
         bx                 = bx < 1 ? 1 : (bx > 256 ? 256 : bx);
@@ -633,6 +688,36 @@ int aimet_adaround_gather(const float* src_in, const float* src_out, float* dst_
         adaround_gather_kernel<<<grid, kBlock, 0, as_stream(stream)>>>(src_in, src_out, dst_in, dst_out, idx_all,
                                                                         it_cur, it_next, (int) nb, row_in, row_out,
                                                                         vec ? 1 : 0);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_adaround_recon_grad_indexed(const float* q, const float* out_data, const int64_t* idx_all,
+                                      const int64_t* it_cur, float* g, int64_t nb, int64_t C, int64_t hw,
+                                      const float* bias, int act, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(nb > 0 && C > 0 && hw > 0, "invalid shape");
+        AIMET_REQUIRE(act >= 0 && act <= 2, "act must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
+        const int64_t row = C * hw, n = nb * row;
+        AIMET_REQUIRE(n < (int64_t(1) << 31), "batch too large (>= 2^31 elements)");
+        require_device_ptr(q, "quant_out");
+        require_device_ptr(out_data, "out_data");
+        require_device_ptr(idx_all, "idx_all");
+        require_device_ptr(it_cur, "it_cur");
+        require_device_ptr(g, "grad");
+        if (bias)
+            require_device_ptr(bias, "bias");
+        // torch: mean over n / C values of the dim-1 squared norm; d/dq = 2 (a - b) / count
+        const float scale = (float) (2.0 / (double) (n / C));
+        ReconIdx r {out_data, idx_all, it_cur, bias, nb, row, hw, C,
+                    FastDiv((uint32_t) row), FastDiv((uint32_t) hw), FastDiv((uint32_t) C)};
+        const bool vec = row % 4 == 0 && hw % 4 == 0 && aligned16(q) && aligned16(out_data) && aligned16(g);
+        hipStream_t s  = as_stream(stream);
+        if (vec)
+            recon_grad_idx_kernel<true><<<(unsigned) ceil_div(n / 4, kBlock), kBlock, 0, s>>>(q, g, r, scale, act);
+        else
+            recon_grad_idx_kernel<false><<<(unsigned) ceil_div(n, kBlock), kBlock, 0, s>>>(q, g, r, scale, act);
         AIMET_LAUNCH_CHECK();
     });
 }

@@ -336,11 +336,19 @@ int aimet_adaround_backward_dev(const float* w, const float* alpha, const float*
 /* The single-process AdaRound loop's batch draw (adaround_optimizer.py:181-218: randperm'd
  * indices, index_select of the cached inputs and fp outputs) as one kernel: it = it_cur_dev[0];
  * rows idx_all_dev[it * nb + b] (int64, [iterations][nb]) of src_in / src_out ([N][row_in],
- * [N][row_out]) are copied to dst_in[b] / dst_out[b]; it_next_dev[0] = it + 1. For a HIP-graph
- * replayed iteration (the counters live in device memory). */
+ * [N][row_out]) are copied to dst_in[b] / dst_out[b] (dst_out may be null: inputs only);
+ * it_next_dev[0] = it + 1. For a HIP-graph replayed iteration (the counters live in device
+ * memory). */
 int aimet_adaround_gather(const float* src_in, const float* src_out, float* dst_in, float* dst_out,
                           const int64_t* idx_all_dev, const int64_t* it_cur_dev, int64_t* it_next_dev, int64_t nb,
                           int64_t row_in, int64_t row_out, void* stream);
+/* aimet_adaround_recon_grad for the same replayed iteration with the fp target read in place:
+ * sample b's target is row idx_all_dev[it * nb + b] of out_data ([N][C][hw]), it = it_cur_dev[0];
+ * bias_dev (nullable, [C]) is added to quant_out first (a bias-free GEMM output). grad and
+ * quant_out are the [nb][C][hw] batch. dst_out of aimet_adaround_gather may then be null. */
+int aimet_adaround_recon_grad_indexed(const float* quant_out, const float* out_data, const int64_t* idx_all_dev,
+                                      const int64_t* it_cur_dev, float* grad, int64_t nb, int64_t C, int64_t hw,
+                                      const float* bias_dev, int act, void* stream);
 /* aimet_adaround_backward + torch.optim.Adam(fused=True)'s update of alpha (no weight decay /
  * amsgrad) in one pass, for the same replayed iteration: step = it_next_dev[0] (1-based),
  * {reg, beta, beta - 1} = reg_beta_all_dev[3 * (step - 1) ..] (float32), alpha / exp_avg /

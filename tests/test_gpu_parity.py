@@ -944,7 +944,7 @@ def test_depthwise_conv_kernels_vs_torch(N, C, H, K, stride, pad, dil):
     torch.testing.assert_close(gw, wr.grad, rtol=2e-5, atol=1e-6 * scale)
 
 
-@pytest.mark.parametrize("layer", ["conv", "depthwise", "linear"])
+@pytest.mark.parametrize("layer", ["conv", "depthwise", "pointwise", "linear", "linear_noact"])
 def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
     """The single-process loop with the batch draw and backward + Adam fused into two kernels
     (aimet_adaround_gather, aimet_adaround_backward_adam) follows the graph of torch ops (index_select
@@ -957,8 +957,11 @@ def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
         mod, x = torch.nn.Conv2d(16, 24, 3, padding=1), torch.randn(96, 16, 10, 10)
     elif layer == "depthwise":
         mod, x = torch.nn.Conv2d(24, 24, 3, padding=1, groups=24), torch.randn(96, 24, 10, 10)
+    elif layer == "pointwise":
+        mod, x = torch.nn.Conv2d(24, 40, 1), torch.randn(96, 24, 10, 10)
     else:
         mod, x = torch.nn.Linear(40, 30), torch.randn(96, 40)
+    act = None if layer == "linear_noact" else torch.nn.ReLU()
     mod, x = mod.to(DEV), x.to(DEV)
     with torch.no_grad():
         out = mod(x) + 0.01 * torch.randn_like(mod(x))
@@ -970,7 +973,7 @@ def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
     for fused in (True, False):
         loss = torch.zeros(1, device=DEV)
         with conv_backend(mod):
-            a = AdaroundOptimizer._optimize_graphed(mod, x, out, d, o, 4, 0, params, torch.nn.ReLU(),
+            a = AdaroundOptimizer._optimize_graphed(mod, x, out, d, o, 4, 0, params, act,
                                                     torch.Generator().manual_seed(9), loss, fused_step=fused)
         res[fused] = (a.detach().clone(), loss.clone())
     torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-5, atol=1e-6)

@@ -53,6 +53,13 @@ def timed(fn, reps=10):
 
 ms_raw = timed(lambda: lib.read_many(ctypes.c_void_p(B.data_ptr()), ctypes.c_void_p(T.data_ptr()), ctypes.c_int64(tile),
                                      ctypes.c_void_p(out.data_ptr()), ctypes.c_void_p(s.cuda_stream)))
+gate = torch.zeros(len(ts), dtype=torch.int32, device=dev)
+part = torch.empty(tile * 4, 2, device=dev)
+ms_v = {}
+for v in (1, 2, 3):
+    ms_v[v] = timed(lambda v=v: lib.mm_many_v(v, ctypes.c_void_p(B.data_ptr()), ctypes.c_void_p(T.data_ptr()),
+                                              ctypes.c_int64(tile), ctypes.c_void_p(gate.data_ptr()),
+                                              ctypes.c_void_p(part.data_ptr()), ctypes.c_void_p(s.cuda_stream)))
 qs = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in ts]
 AimetTensorQuantizer._ensure_many(qs, dev)
 
@@ -72,5 +79,8 @@ ms_both = timed(both)
 gb = nbytes / 1e9
 print("activation bytes %.3f GB" % gb)
 print("raw read (16-KiB tiles, nt loads, no reduction): %.3f ms  %.2f TB/s" % (ms_raw, gb / ms_raw))
+for v, name in ((1, "+ block min/max, partial per tile"), (2, "+ a gate load (like pdf_init)"),
+                (3, "min/max, partial per wave (no LDS)")):
+    print("probe %d %-34s %.3f ms  %.2f TB/s" % (v, name, ms_v[v], gb / ms_v[v]))
 print("reset + min/max pass:                            %.3f ms  %.2f TB/s" % (ms_mm, gb / ms_mm))
 print("reset + min/max + histogram (updateStatsMany):   %.3f ms  %.2f TB/s (two passes)" % (ms_both, 2 * gb / ms_both))
