@@ -230,6 +230,8 @@ def _reduce_grad(grad, world, group, divide=True):
 class AdaroundOptimizer:
     """v1/adaround/adaround_optimizer.py."""
 
+    last_loop_form = None   # the layer form the last fused loop ran (dw / pointwise / linear / autograd)
+
     @staticmethod
     def optimize_rounding(module: torch.nn.Module, inp_data: torch.Tensor, out_data: torch.Tensor,
                           delta: torch.Tensor, offset: torch.Tensor, bitwidth: int, ch_axis: int = 0,
@@ -447,25 +449,65 @@ class AdaroundOptimizer:
                 (gw,) = torch.autograd.grad(recon_loss(qa, ta), wq)
             adam_step(gw if gw.is_contiguous() else gw.contiguous(), s)
 
-        # warm-up on a side stream (library handles, allocator, autograd), then back to iteration 0
         alpha0 = alpha.detach().clone()
         loss0 = round_loss_out.clone() if round_loss_out is not None else None
-        side = torch.cuda.Stream(dev)
-        side.wait_stream(torch.cuda.current_stream(dev))
-        with torch.cuda.stream(side), torch.enable_grad():
-            for _ in range(min(2, iters)):
+
+        def restart():   # back to iteration 0
+            with torch.no_grad():
+                alpha.copy_(alpha0)
+                exp_avg.zero_()
+                exp_avg_sq.zero_()
+                counters.zero_()
+                if round_loss_out is not None:
+                    round_loss_out.copy_(loss0)
+
+        def capture(m):
+            nonlocal mode
+            mode = m
+            # warm-up on a side stream (library handles, allocator, autograd), then capture
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side), torch.enable_grad():
+                for _ in range(min(2, iters)):
+                    step()
+            torch.cuda.current_stream(dev).wait_stream(side)
+            restart()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g), torch.enable_grad():
                 step()
-        torch.cuda.current_stream(dev).wait_stream(side)
-        with torch.no_grad():
-            alpha.copy_(alpha0)
-            exp_avg.zero_()
-            exp_avg_sq.zero_()
-            counters.zero_()
-            if round_loss_out is not None:
-                round_loss_out.copy_(loss0)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph), torch.enable_grad():
-            step()
+            return g
+
+        # layers with two forms (GEMM or MIOpen convolution through autograd): each is captured and
+        # timed over a few replays and the faster one runs the loop -- which wins depends on the
+        # shape (profiles/r02: the GEMMs win for small Cin at large spatial size, MIOpen for
+        # projections to few channels)
+        candidates = [mode] + (["autograd"] if mode in ("pointwise", "linear") and iters >= 50 else [])
+        best = None
+        for m in candidates:
+            try:
+                g = capture(m)
+            except RuntimeError:
+                if m == candidates[0] and len(candidates) > 1:
+                    continue
+                raise
+            if len(candidates) > 1:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                g.replay()
+                e0.record()
+                for _ in range(5):
+                    g.replay()
+                e1.record()
+                e1.synchronize()
+                t = e0.elapsed_time(e1)
+                restart()
+            else:
+                t = 0.0
+            if best is None or t < best[0]:
+                best = (t, m, g)
+            else:
+                del g
+        _, mode, graph = best
+        AdaroundOptimizer.last_loop_form = mode
         for a in range(0, iters, chunk):
             b = min(a + chunk, iters)
             if b < iters:

@@ -8,11 +8,12 @@ warm start 0.2, ReLU6 applied to both outputs when the layer feeds one); then wr
 hard-rounded weight. Weight encodings: 8-bit symmetric per-tensor TF-Enhanced (AIMET's AdaRound
 default) from the device analyzers.
 
-Reported (one JSON line): total AdaRound wall-clock, mean ms per iteration, and the soft-quant
-kernels' HBM rates: forward 12 B/elem (W, alpha -> Wq) and backward + rounding loss 16 B/elem
-(g, W, alpha -> g_alpha), measured with HIP events on every layer's weight; with --reference-iters
-the same loop using the reference's torch-op soft quantization + rounding loss
-(oracle/torch_ref.py) for comparison.
+Reported (one JSON line): total AdaRound wall-clock, mean ms per iteration, and per layer its ms
+per iteration and the loop form that ran it (dw: native depthwise kernels; pointwise / linear:
+direct GEMMs; autograd: MIOpen through autograd -- layers with two forms time both at capture and
+keep the faster); with --reference-iters the same loop using the reference's torch-op soft
+quantization + rounding loss (oracle/torch_ref.py) for comparison. The per-kernel split of the
+loop comes from rocprofv3 (tools/ada_trace_summary.py), not from host-timed launches.
 """
 import argparse
 import json
@@ -79,7 +80,6 @@ def main():
     gen = torch.Generator().manual_seed(0)
     loss_buf = torch.zeros(1, device=dev)
     t_opt = t_cache = t_ref = 0.0
-    kern = []   # (elements, fwd_ms, bwd_ms) per layer
     per_layer = []
     for name in names:
         torch.cuda.synchronize()
@@ -107,30 +107,10 @@ def main():
         torch.cuda.synchronize()
         dt_ours = time.perf_counter() - t0
         t_opt += dt_ours
-        per_layer.append([name, list(w.shape), round(dt_ours / args.iterations * 1e3, 4)])
+        per_layer.append([name, list(w.shape), round(dt_ours / args.iterations * 1e3, 4),
+                          AdaroundOptimizer.last_loop_form])
         with torch.no_grad():
             m.weight.copy_(AdaroundOptimizer.hard_rounded_weight(m, alpha, d, o, 8))
-        # soft-quant kernel rates on this weight (HIP events, 20 launches each)
-        g = torch.randn_like(w)
-        a = alpha.detach()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        from aimet_amd import _native
-        stream = torch.cuda.current_stream().cuda_stream
-        wq, ga = torch.empty_like(w), torch.empty_like(w)
-        e0.record()
-        for _ in range(20):
-            _native.call("aimet_adaround_forward", w.data_ptr(), a.data_ptr(), wq.data_ptr(), 1, 1, w.numel(),
-                         d.data_ptr(), o.data_ptr(), 8, 1, stream)
-        e1.record()
-        torch.cuda.synchronize()
-        fwd_ms = e0.elapsed_time(e1) / 20
-        e0.record()
-        for _ in range(20):
-            _native.call("aimet_adaround_backward", w.data_ptr(), a.data_ptr(), g.data_ptr(), ga.data_ptr(), 1, 1,
-                         w.numel(), d.data_ptr(), o.data_ptr(), 8, 0.01, 10.0, loss_buf.data_ptr(), stream)
-        e1.record()
-        torch.cuda.synchronize()
-        kern.append((w.numel(), fwd_ms, e0.elapsed_time(e1) / 20))
         if args.reference_iters:
             from oracle import torch_ref as T
             a_ref = init_alpha(w, d)
@@ -157,9 +137,6 @@ def main():
         del inp, out
 
     iters = args.iterations * len(names)
-    elems = sum(k[0] for k in kern)
-    fwd_t = sum(k[1] for k in kern)
-    bwd_t = sum(k[2] for k in kern)
     res = {
         "metric": "AdaRound wall-clock (MobileNet-v2, W8, all layers)",
         "value": round(t_opt, 3), "unit": "s", "higher_is_better": False, "n_gpus": 1,
@@ -167,17 +144,16 @@ def main():
         "ms_per_iteration": round(t_opt / iters * 1e3, 4), "activation_caching_s": round(t_cache, 3),
         "loop": "eager" if args.eager else "hipgraph (one captured iteration replayed per iteration)",
         "miopen_find": bool(args.miopen_find),
-        "weights_elems": elems,
-        "softquant_fwd_GBps": round(elems * 12 / (fwd_t * 1e-3) / 1e9, 1),
-        "softquant_bwd_roundloss_GBps": round(elems * 16 / (bwd_t * 1e-3) / 1e9, 1),
-        "softquant_fwd_bwd_us_per_iteration_all_layers": round((fwd_t + bwd_t) * 1e3, 2),
+        "weights_elems": sum(int(torch.Size(p[1]).numel()) for p in per_layer),
+        "kernel_split": "per-kernel time of the loop: rocprofv3 --kernel-trace + tools/ada_trace_summary.py "
+                        "(profiles/r02/adaround_loop_kernels_*.csv)",
         "data": "synthetic U(0,1) images (seed 7), random-init MobileNet-v2 with folded BN (seed 0)",
     }
     if args.reference_iters:
         res["reference_torch_ops_ms_per_iteration"] = round(t_ref / (args.reference_iters * len(names)) * 1e3, 4)
         res["speedup_vs_reference_loop"] = round(res["reference_torch_ops_ms_per_iteration"] /
                                                  res["ms_per_iteration"], 2)
-    res["per_layer_ms_per_iteration"] = per_layer   # [name, weight shape, ours(, reference)]
+    res["per_layer_ms_per_iteration"] = per_layer   # [name, weight shape, ours, loop form(, reference)]
     print(json.dumps(res), flush=True)
 
 
