@@ -944,7 +944,7 @@ def test_depthwise_conv_kernels_vs_torch(N, C, H, K, stride, pad, dil):
     torch.testing.assert_close(gw, wr.grad, rtol=2e-5, atol=1e-6 * scale)
 
 
-@pytest.mark.parametrize("layer", ["conv", "depthwise", "pointwise", "linear", "linear_noact"])
+@pytest.mark.parametrize("layer", ["conv", "depthwise", "pointwise", "linear", "linear_noact", "conv_gelu"])
 def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
     """The single-process loop with the batch draw and backward + Adam fused into two kernels
     (aimet_adaround_gather, aimet_adaround_backward_adam) follows the graph of torch ops (index_select
@@ -953,7 +953,7 @@ def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
     elements (profiles/r02/adam_probe.txt), so alpha agrees to fp32 tolerance after 80 steps."""
     from aimet_amd.adaround_optimizer import AdaroundHyperParameters, AdaroundOptimizer, conv_backend
     torch.manual_seed(4)
-    if layer == "conv":
+    if layer in ("conv", "conv_gelu"):
         mod, x = torch.nn.Conv2d(16, 24, 3, padding=1), torch.randn(96, 16, 10, 10)
     elif layer == "depthwise":
         mod, x = torch.nn.Conv2d(24, 24, 3, padding=1, groups=24), torch.randn(96, 24, 10, 10)
@@ -961,7 +961,8 @@ def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
         mod, x = torch.nn.Conv2d(24, 40, 1), torch.randn(96, 24, 10, 10)
     else:
         mod, x = torch.nn.Linear(40, 30), torch.randn(96, 40)
-    act = None if layer == "linear_noact" else torch.nn.ReLU()
+    # GELU has no fused reconstruction-gradient form: the target is gathered and autograd runs it
+    act = None if layer == "linear_noact" else torch.nn.GELU() if layer == "conv_gelu" else torch.nn.ReLU()
     mod, x = mod.to(DEV), x.to(DEV)
     with torch.no_grad():
         out = mod(x) + 0.01 * torch.randn_like(mod(x))
