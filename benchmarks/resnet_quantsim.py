@@ -10,6 +10,11 @@ Plus config 2's end-to-end step: the W8A8 per-channel QuantSim forward of a batc
 MIOpen, every activation / weight QDQ through the gfx950 kernels) against the fp32 forward.
 
   python benchmarks/resnet_quantsim.py [--batches 8] [--batch 32] [--e2e-batch 256] [--no-oracle]
+  python benchmarks/resnet_quantsim.py --cpu-model      # config 1 as stated: the aimet_torch CPU path
+
+--cpu-model: the model and the calibration images stay on the host (the reference's aimet_torch CPU
+path: forwards on the host cores); every quantizer's statistics and QDQ run on the MI355X, the
+tensors staged through HBM (aimet_amd.tensor_quantizer._stage). No config-2 step in this mode.
 """
 import argparse
 import json
@@ -68,13 +73,15 @@ def main():
     ap.add_argument("--e2e-batch", type=int, default=256)
     ap.add_argument("--e2e-steps", type=int, default=5)
     ap.add_argument("--no-oracle", action="store_true")
+    ap.add_argument("--cpu-model", action="store_true")
     args = ap.parse_args()
 
     from aimet_amd.quantizers import QuantScheme
     from aimet_amd.quantsim import QuantizationSimModel
     from workloads.resnet import resnet50
 
-    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    dev = torch.device("cpu") if args.cpu_model else torch.device("cuda", 0)
     model = resnet50(seed=0, device=dev).eval()
     g = torch.Generator().manual_seed(1234)
     images = torch.rand(args.batches * args.batch, 3, 224, 224, generator=g).to(dev)
@@ -87,7 +94,8 @@ def main():
 
     res = {"metric": "ResNet-50 W8A8 per-tensor compute_encodings wall-clock", "unit": "s",
            "higher_is_better": False, "n_gpus": 1, "calibration": "%d batches x %d images U(0,1) seed 1234"
-           % (args.batches, args.batch), "schemes": {}}
+           % (args.batches, args.batch), "model_device": str(dev),
+           "host_threads": torch.get_num_threads() if args.cpu_model else None, "schemes": {}}
     for scheme in (QuantScheme.post_training_tf_enhanced, QuantScheme.post_training_tf):
         sim = QuantizationSimModel(model, dummy, quant_scheme=scheme, default_output_bw=8, default_param_bw=8)
         # warm (kernels, MIOpen algorithm selection); timed run on a fresh calibration
@@ -134,6 +142,19 @@ def main():
         res["schemes"][scheme.name] = r
         del sim
         torch.cuda.empty_cache()
+
+    if args.cpu_model:
+        # the same 8 forwards of the plain model: what the calibration costs without QuantSim
+        with torch.no_grad():
+            t0 = time.perf_counter()
+            calibrate(model, None)
+            res["host_fp32_forwards_s"] = round(time.perf_counter() - t0, 4)
+        for r in res["schemes"].values():
+            r["quantsim_overhead_s"] = round(r["compute_encodings_s"] - res["host_fp32_forwards_s"], 4)
+            r.pop("speedup_vs_cpu_oracle", None)   # the timed call includes the host forwards here
+        res["data"] = "synthetic U(0,1) images (seed 1234), random-init ResNet-50 (seed 0) on the host"
+        print(json.dumps(res), flush=True)
+        return
 
     # config 2 end-to-end step: W8A8 per-channel QuantSim forward, batch 256
     cfg = {"defaults": {"params": {"is_symmetric": "True"}, "ops": {"is_symmetric": "False"},
