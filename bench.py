@@ -45,8 +45,8 @@ TRAFFIC_ELEMS = 2883971072
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)   # ~0.37 s timed region at N=1
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--batch", type=int, default=256)
     p.add_argument("--cpu-sample-images", type=int, default=32,
                    help="images of each activation tensor (plus all weights) timed on the CPU oracle")
