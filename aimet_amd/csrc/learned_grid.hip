@@ -13,6 +13,7 @@
 // symmetric:  grad_max = (A - B) / floor(steps/2), grad_min = -grad_max
 // (assembled from the C-vectors on the torch side). Float32; torch.round = round-half-even.
 #include "common.hpp"
+#include "io16.hpp"
 
 namespace aimet_amd
 {
@@ -377,6 +378,84 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restri
     sums[3 * c + 2] = d;
 }
 
+// ---- fp16 / bf16 I/O, per tensor (C == 1): the conversions in registers ------------------------
+// Identical results to x.to(float32) -> the fp32 kernels -> .to(dtype): the upcast is exact, the
+// arithmetic and the element -> lane -> workgroup order of the backward's sums are those of
+// lg_bwd_tensor_kernel (quads, then the tail), and the downcast is torch's (io16.hpp). 4 B/elem
+// forward and 6 B/elem backward instead of 20 and 24 for the three-pass chains.
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+template <int IO>
+__global__ __launch_bounds__(kBlock) void lg_fwd16_kernel(const unsigned short* __restrict__ x,
+                                                          unsigned short* __restrict__ y, uint32_t n,
+                                                          const float* __restrict__ delta,
+                                                          const float* __restrict__ offset, float steps, int vec)
+{
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    const float d = delta[0], o = offset[0];
+    if (vec)
+    {
+        if (t >= n / 4)
+            return;
+        const u16x4 v = __builtin_nontemporal_load(reinterpret_cast<const u16x4*>(x) + t);
+        u16x4 r;
+        r.x = from_f32<IO>(lg_qdq(to_f32<IO>(v.x), d, o, steps));
+        r.y = from_f32<IO>(lg_qdq(to_f32<IO>(v.y), d, o, steps));
+        r.z = from_f32<IO>(lg_qdq(to_f32<IO>(v.z), d, o, steps));
+        r.w = from_f32<IO>(lg_qdq(to_f32<IO>(v.w), d, o, steps));
+        __builtin_nontemporal_store(r, reinterpret_cast<u16x4*>(y) + t);
+    }
+    else if (t < n)
+        y[t] = from_f32<IO>(lg_qdq(to_f32<IO>(x[t]), d, o, steps));
+}
+
+template <int IO>
+__global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned short* __restrict__ x,
+                                                                 const unsigned short* __restrict__ g,
+                                                                 unsigned short* __restrict__ gx, int64_t n,
+                                                                 const float* __restrict__ delta,
+                                                                 const float* __restrict__ offset, float steps,
+                                                                 float* __restrict__ partial, int vec)
+{
+    const float dl = delta[0], o = offset[0], rcp = __builtin_amdgcn_rcpf(dl);
+    Sums s {0, 0, 0};
+    int64_t done = 0;
+    if (vec)
+    {
+        const int64_t nv = n / 4;
+        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t) gridDim.x * kBlock)
+        {
+            const u16x4 a = __builtin_nontemporal_load(reinterpret_cast<const u16x4*>(x) + i);
+            const u16x4 b = __builtin_nontemporal_load(reinterpret_cast<const u16x4*>(g) + i);
+            float r0, r1, r2, r3;
+            lg_bwd_elem(to_f32<IO>(a.x), to_f32<IO>(b.x), dl, o, steps, rcp, r0, s);
+            lg_bwd_elem(to_f32<IO>(a.y), to_f32<IO>(b.y), dl, o, steps, rcp, r1, s);
+            lg_bwd_elem(to_f32<IO>(a.z), to_f32<IO>(b.z), dl, o, steps, rcp, r2, s);
+            lg_bwd_elem(to_f32<IO>(a.w), to_f32<IO>(b.w), dl, o, steps, rcp, r3, s);
+            if (gx)
+            {
+                const u16x4 r = {from_f32<IO>(r0), from_f32<IO>(r1), from_f32<IO>(r2), from_f32<IO>(r3)};
+                __builtin_nontemporal_store(r, reinterpret_cast<u16x4*>(gx) + i);
+            }
+        }
+        done = nv * 4;
+    }
+    for (int64_t i = done + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
+    {
+        float r;
+        lg_bwd_elem(to_f32<IO>(x[i]), to_f32<IO>(g[i]), dl, o, steps, rcp, r, s);
+        if (gx)
+            gx[i] = from_f32<IO>(r);
+    }
+    Sums t = block_reduce(s);
+    if (threadIdx.x == 0)
+    {
+        partial[3 * blockIdx.x + 0] = t.a;
+        partial[3 * blockIdx.x + 1] = t.b;
+        partial[3 * blockIdx.x + 2] = t.d;
+    }
+}
+
 }   // namespace
 }   // namespace aimet_amd
 
@@ -502,6 +581,75 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
                                                           sums);
         }
         AIMET_LAUNCH_CHECK();
+    });
+}
+
+}   // extern "C"
+
+extern "C" {
+
+int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* delta, const float* offset,
+                        float num_steps, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(io_dtype == IO_F16 || io_dtype == IO_BF16, "io_dtype must be 1 (float16) or 2 (bfloat16)");
+        AIMET_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "learned-grid QDQ needs < 2^31 elements per call");
+        if (n == 0)
+            return;
+        require_device_ptr(x, "x");
+        require_device_ptr(y, "y");
+        require_device_ptr(delta, "delta");
+        require_device_ptr(offset, "offset");
+        const bool vec = n % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 7) == 0;
+        const int64_t work = vec ? n / 4 : n;
+        auto xs = static_cast<const unsigned short*>(x);
+        auto ys = static_cast<unsigned short*>(y);
+        if (io_dtype == IO_F16)
+            lg_fwd16_kernel<IO_F16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
+                xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0);
+        else
+            lg_fwd16_kernel<IO_BF16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
+                xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* sums, int64_t n, int io_dtype,
+                         const float* delta, const float* offset, float num_steps, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(io_dtype == IO_F16 || io_dtype == IO_BF16, "io_dtype must be 1 (float16) or 2 (bfloat16)");
+        AIMET_REQUIRE(n >= 0, "invalid size");
+        require_device_ptr(sums, "sums");
+        hipStream_t s = as_stream(stream);
+        if (n == 0)
+        {
+            AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3, s));
+            return;
+        }
+        require_device_ptr(x, "x");
+        require_device_ptr(grad, "grad");
+        if (grad_x)
+            require_device_ptr(grad_x, "grad_x");
+        require_device_ptr(delta, "delta");
+        require_device_ptr(offset, "offset");
+        const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
+                           reinterpret_cast<uintptr_t>(grad_x)) & 7) == 0;
+        const unsigned nb = stream_blocks(n, (int64_t) kBlock * 16);   // the fp32 kernel's grid
+        float* partial    = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * nb, s));
+        auto xs = static_cast<const unsigned short*>(x);
+        auto gs = static_cast<const unsigned short*>(grad);
+        auto os = static_cast<unsigned short*>(grad_x);
+        if (io_dtype == IO_F16)
+            lg_bwd16_tensor_kernel<IO_F16><<<nb, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps, partial,
+                                                                 vec ? 1 : 0);
+        else
+            lg_bwd16_tensor_kernel<IO_BF16><<<nb, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps, partial,
+                                                                  vec ? 1 : 0);
+        AIMET_LAUNCH_CHECK();
+        lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) nb, sums);
+        AIMET_LAUNCH_CHECK();
+        scratch_free(partial, s);
     });
 }
 

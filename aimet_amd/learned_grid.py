@@ -7,8 +7,10 @@ mask and runs ~10 torch kernels per tensor per step; here the forward is one ker
 nothing but x, and the backward one kernel that recomputes x_round and emits grad_x plus three
 per-channel sums, from which the encoding gradients are assembled on C-element vectors.
 
-Inputs are computed in float32 (fp16/bf16 tensors are upcast; the reference keeps bf16/fp16
-arithmetic for bitwidth <= 8 -- a documented difference, results are then at least as accurate).
+Inputs are computed in float32: fp16 / bf16 tensors with a per-tensor range run the 16-bit I/O
+kernels (aimet_lg_forward_16 / _backward_16: the casts in registers, results identical to the
+upcast -> fp32 -> downcast chain), other 16-bit cases are upcast. The reference keeps bf16/fp16
+arithmetic for bitwidth <= 8 -- a documented difference, results are then at least as accurate.
 """
 import math
 
@@ -16,7 +18,7 @@ import torch
 
 from aimet_amd import _native
 from aimet_amd.libpymo import TfEncoding
-from aimet_amd.tensor_quantizer import _stage, _stream, per_channel_view
+from aimet_amd.tensor_quantizer import IO_DTYPES, _stage, _stream, per_channel_view
 
 
 def get_computed_encodings(bitwidth, encoding_min, encoding_max, use_symmetric_encodings, use_strict_symmetric,
@@ -61,6 +63,10 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         if bitwidth >= 32:
             raise RuntimeError("Invalid bitwidth: %d" % bitwidth)
         orig_dtype = tensor.dtype
+        if tensor.is_cuda and orig_dtype in IO_DTYPES and encoding_min.numel() == 1:
+            return LearnedGridQuantizeDequantize._forward_16(ctx, tensor, encoding_min, encoding_max, bitwidth,
+                                                             use_symmetric, use_strict_symmetric,
+                                                             is_unsigned_symmetric)
         # a CPU tensor (and its CPU range) is staged through HBM; results go back to the host
         x, staged = _stage(tensor.to(torch.float32), "tensor")
         x = x.contiguous()
@@ -82,15 +88,44 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         return y.to(orig_dtype).cpu() if staged else y.to(orig_dtype)
 
     @staticmethod
+    def _forward_16(ctx, tensor, encoding_min, encoding_max, bitwidth, use_symmetric, use_strict_symmetric,
+                    is_unsigned_symmetric):
+        """fp16 / bf16 tensor, per-tensor range: aimet_lg_forward_16 (the casts in registers;
+        identical to the upcast -> fp32 kernel -> downcast chain). Saves the 16-bit input."""
+        x = tensor.contiguous()
+        emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
+        emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
+        delta, offset, steps = get_computed_encodings(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
+                                                      is_unsigned_symmetric)
+        delta, offset = delta.contiguous(), offset.contiguous()
+        y = torch.empty_like(x)
+        with torch.cuda.device(x.device):
+            _native.call("aimet_lg_forward_16", x.data_ptr(), y.data_ptr(), x.numel(), IO_DTYPES[x.dtype],
+                         delta.data_ptr(), offset.data_ptr(), float(steps[0]), _stream(x))
+        ctx.save_for_backward(x, delta, offset, emin, emax)
+        ctx.cfg = (1, 1, x.numel(), float(steps[0]), use_symmetric, is_unsigned_symmetric, x.dtype,
+                   encoding_min.shape, encoding_max.shape, False)
+        return y
+
+    @staticmethod
     def backward(ctx, grad):
         x, delta, offset, emin, emax = ctx.saved_tensors
         outer, C, K, steps, sym, unsigned, dtype, min_shape, max_shape, staged = ctx.cfg
-        g = grad.to(x.device, torch.float32).contiguous()
-        gx = torch.empty_like(g) if ctx.needs_input_grad[0] else None
         sums = torch.empty((C, 3), dtype=torch.float32, device=x.device)
-        with torch.cuda.device(x.device):
-            _native.call("aimet_lg_backward", x.data_ptr(), g.data_ptr(), gx.data_ptr() if gx is not None else None,
-                         sums.data_ptr(), outer, C, K, delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
+        if x.dtype in IO_DTYPES and grad.dtype == x.dtype and grad.is_cuda:
+            g = grad.contiguous()
+            gx = torch.empty_like(g) if ctx.needs_input_grad[0] else None
+            with torch.cuda.device(x.device):
+                _native.call("aimet_lg_backward_16", x.data_ptr(), g.data_ptr(),
+                             gx.data_ptr() if gx is not None else None, sums.data_ptr(), x.numel(), IO_DTYPES[x.dtype],
+                             delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
+        else:
+            x = x.to(torch.float32)   # a 16-bit input with a gradient of another dtype
+            g = grad.to(x.device, torch.float32).contiguous()
+            gx = torch.empty_like(g) if ctx.needs_input_grad[0] else None
+            with torch.cuda.device(x.device):
+                _native.call("aimet_lg_backward", x.data_ptr(), g.data_ptr(), gx.data_ptr() if gx is not None else None,
+                             sums.data_ptr(), outer, C, K, delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
         A, B, D = sums[:, 0], sums[:, 1], sums[:, 2]
         grad_scale_sum = A - B
         if sym:

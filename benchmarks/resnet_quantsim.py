@@ -10,11 +10,13 @@ Plus config 2's end-to-end step: the W8A8 per-channel QuantSim forward of a batc
 MIOpen, every activation / weight QDQ through the gfx950 kernels) against the fp32 forward.
 
   python benchmarks/resnet_quantsim.py [--batches 8] [--batch 32] [--e2e-batch 256] [--no-oracle]
-  python benchmarks/resnet_quantsim.py --cpu-model      # config 1 as stated: the aimet_torch CPU path
+  python benchmarks/resnet_quantsim.py --cpu-model --repeats 3   # config 1 as stated: the aimet_torch CPU path
 
 --cpu-model: the model and the calibration images stay on the host (the reference's aimet_torch CPU
 path: forwards on the host cores); every quantizer's statistics and QDQ run on the MI355X, the
-tensors staged through HBM (aimet_amd.tensor_quantizer._stage). No config-2 step in this mode.
+tensors staged through HBM (aimet_amd.tensor_quantizer._stage). No config-2 step in this mode. The
+host cores are shared on the GPU box, so host-forward times vary run to run: each figure is the
+minimum of --repeats runs (all runs listed).
 """
 import argparse
 import json
@@ -74,6 +76,8 @@ def main():
     ap.add_argument("--e2e-steps", type=int, default=5)
     ap.add_argument("--no-oracle", action="store_true")
     ap.add_argument("--cpu-model", action="store_true")
+    ap.add_argument("--repeats", type=int, default=1,
+                    help="timed compute_encodings (and, with --cpu-model, host forward) runs; the minimum is reported")
     args = ap.parse_args()
 
     from aimet_amd.quantizers import QuantScheme
@@ -100,14 +104,18 @@ def main():
         sim = QuantizationSimModel(model, dummy, quant_scheme=scheme, default_output_bw=8, default_param_bw=8)
         # warm (kernels, MIOpen algorithm selection); timed run on a fresh calibration
         sim.compute_encodings(calibrate, None)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        sim.compute_encodings(calibrate, None)
-        torch.cuda.synchronize()
-        secs = time.perf_counter() - t0
+        runs = []
+        for _ in range(args.repeats):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            sim.compute_encodings(calibrate, None)
+            torch.cuda.synchronize()
+            runs.append(time.perf_counter() - t0)
+        secs = min(runs)
         qmap = quantizer_map(sim)
         n_enc = sum(1 for q in qmap.values() if q.enabled and q.encoding is not None)
-        r = {"compute_encodings_s": round(secs, 4), "quantizers": n_enc}
+        r = {"compute_encodings_s": round(secs, 4), "compute_encodings_runs_s": [round(v, 4) for v in runs],
+             "quantizers": n_enc}
         if not args.no_oracle:
             from oracle import oracle as O
             seen = record_stats(sim)
@@ -145,10 +153,14 @@ def main():
 
     if args.cpu_model:
         # the same 8 forwards of the plain model: what the calibration costs without QuantSim
+        fw = []
         with torch.no_grad():
-            t0 = time.perf_counter()
-            calibrate(model, None)
-            res["host_fp32_forwards_s"] = round(time.perf_counter() - t0, 4)
+            for _ in range(args.repeats):
+                t0 = time.perf_counter()
+                calibrate(model, None)
+                fw.append(time.perf_counter() - t0)
+        res["host_fp32_forwards_s"] = round(min(fw), 4)
+        res["host_fp32_forwards_runs_s"] = [round(v, 4) for v in fw]
         for r in res["schemes"].values():
             r["quantsim_overhead_s"] = round(r["compute_encodings_s"] - res["host_fp32_forwards_s"], 4)
             r.pop("speedup_vs_cpu_oracle", None)   # the timed call includes the host forwards here

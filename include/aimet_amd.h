@@ -300,6 +300,15 @@ int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t
  * encoding-min/max gradients are assembled (asymmetric_gradients / symmetric_gradients). */
 int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* sums_dev, int64_t outer, int64_t C,
                       int64_t K, const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
+/* The learned-grid forward / backward for a per-tensor range on fp16 (io_dtype 1) or bf16 (2)
+ * tensors with the casts in registers: results identical to x.to(float32) -> aimet_lg_forward /
+ * aimet_lg_backward -> .to(dtype) (same arithmetic, same order of the backward's sums), 4 / 6 B
+ * per element instead of 20 / 24 (QAT under autocast: bf16 activations quantized by 16-bit
+ * output quantizers). sums_dev[3] as aimet_lg_backward's channel 0. */
+int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* delta_dev,
+                        const float* offset_dev, float num_steps, void* stream);
+int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* sums_dev, int64_t n, int io_dtype,
+                         const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* AdaRound soft rounding (v1/adaround/adaround_wrapper.py:124-149, adaround_loss.py:83-133)     */

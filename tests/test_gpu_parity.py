@@ -903,6 +903,31 @@ def test_recon_loss_backward_fused_vs_torch(act, shape):
     torch.testing.assert_close(qa.grad, qb.grad, rtol=2e-6, atol=1e-12)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("n", [4096 * 33 + 3, 1 << 22])
+@pytest.mark.parametrize("sym", [False, True])
+def test_learned_grid_16bit_io_equals_upcast_chain(dtype, n, sym):
+    """aimet_lg_forward_16 / aimet_lg_backward_16 == x.to(float32) -> the fp32 kernels -> .to(dtype),
+    bit for bit: y, grad_x and both encoding gradients (the sums run in the same order)."""
+    from aimet_amd.learned_grid import LearnedGridQuantizeDequantize as LG
+    g = torch.Generator(device=DEV).manual_seed(n % 1000 + int(sym))
+    x16 = (torch.randn(n, device=DEV, generator=g) * 3).to(dtype)
+    x16[:4] = torch.tensor([0.0, -0.0, float("inf"), float("nan")], device=DEV).to(dtype)
+    g16 = torch.randn(n, device=DEV, generator=g).to(dtype)
+    outs = []
+    for x_in, g_in in ((x16.clone(), g16), (x16.float(), g16.float())):
+        x_in.requires_grad_(True)
+        emin = torch.tensor([-2.5], device=DEV, requires_grad=True)
+        emax = torch.tensor([3.25], device=DEV, requires_grad=True)
+        y = LG.apply(x_in, emin, emax, 16 if dtype == torch.bfloat16 else 8, sym, False, False, 0)
+        y.backward(g_in)
+        outs.append((y.detach().to(dtype), x_in.grad.to(dtype), emin.grad, emax.grad))
+    (y_a, gx_a, gmin_a, gmax_a), (y_b, gx_b, gmin_b, gmax_b) = outs
+    assert torch.equal(y_a.view(torch.int16), y_b.view(torch.int16))
+    assert torch.equal(gx_a.view(torch.int16), gx_b.view(torch.int16))
+    assert torch.equal(gmin_a, gmin_b) and torch.equal(gmax_a, gmax_b)
+
+
 @pytest.mark.parametrize("N,C,H,K,stride,pad,dil", [(32, 32, 112, 3, 1, 1, 1), (32, 96, 112, 3, 2, 1, 1),
                                                     (5, 7, 13, 3, 2, 0, 1), (4, 16, 19, 5, 1, 2, 1),
                                                     (3, 12, 17, 3, 1, 2, 2), (32, 960, 7, 3, 1, 1, 1)])
