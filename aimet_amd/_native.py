@@ -132,10 +132,18 @@ _PROTOTYPES = {
                                             ctypes.POINTER(_i64), ctypes.POINTER(_i64), _i64, _vp],
     "aimet_tq_get_encodings": [ctypes.POINTER(_vp), _i64, ctypes.c_uint32, _int, _int, _int, _enc_p,
                                ctypes.POINTER(_int), _vp],
+    "aimet_stream_create_cu_masked": [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.POINTER(_vp)],
+    "aimet_stream_get_cu_mask": [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)],
+    "aimet_stream_destroy": [_vp],
     "aimet_tq_reset_encoding_stats_many": [ctypes.POINTER(_vp), _i64, _vp],
     "aimet_tq_get_encodings_launch": [ctypes.POINTER(_vp), _i64, ctypes.c_uint32, _int, _int, _int, _vp,
                                       ctypes.POINTER(_vp)],
     "aimet_tq_get_encodings_finish": [_vp, _enc_p, ctypes.POINTER(_int)],
+    "aimet_calibrate_launch": [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64), _i64,
+                               ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+                               ctypes.POINTER(_i64), _i64, ctypes.POINTER(ctypes.c_int32),
+                               ctypes.POINTER(ctypes.c_int32), _int, _vp, _vp, ctypes.POINTER(_vp),
+                               ctypes.POINTER(_vp)],
     "aimet_tq_get_stats_histogram": [_vp, _i64, _dp, _dp, ctypes.POINTER(_int), _vp],
     "aimet_tq_get_entropy_state": [_vp, _i64, _dp, _dp, ctypes.POINTER(_int), ctypes.POINTER(_int), _vp],
     "aimet_tq_num_channels": [_vp, ctypes.POINTER(_i64)],

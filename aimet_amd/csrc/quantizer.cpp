@@ -244,6 +244,37 @@ aimet_tensor_quantizer* new_quantizer(int scheme, int64_t num_channels, int devi
     return q;
 }
 
+// resetEncodingStats of many quantizers of one device in two launches (the zeroing of every state
+// range, the running min/max re-initialised), no host synchronisation
+void reset_many(aimet_tensor_quantizer* const* qs, int64_t nq, hipStream_t st)
+{
+    AIMET_REQUIRE(nq >= 0 && (qs != nullptr || nq == 0), "null argument");
+    if (nq == 0)
+        return;
+    std::vector<ZeroJob> zero;
+    std::vector<ResetJob> resets;
+    for (int64_t i = 0; i < nq; ++i)
+    {
+        aimet_tensor_quantizer* q = qs[i];
+        AIMET_REQUIRE(q != nullptr, "null quantizer");
+        AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one batched reset share a device");
+        zero.push_back(ZeroJob {q->arena, (int64_t) q->arena_bytes});
+        if (q->d.minmax && !in_arena(q, q->d.minmax))
+            zero.push_back(ZeroJob {q->d.minmax, (int64_t) (sizeof(float) * 2 * q->C)});
+        if (q->d.counts && !in_arena(q, q->d.counts))
+            zero.push_back(ZeroJob {q->d.counts, (int64_t) (sizeof(unsigned long long) * kPdfSize * q->C)});
+        resets.push_back(ResetJob {q->d.acc, q->C});
+    }
+    DeviceGuard g(qs[0]->device);
+    launch_zero_many(zero, st);
+    launch_reset_state_many(resets, st);
+    for (int64_t i = 0; i < nq; ++i)
+    {
+        qs[i]->stats_updated = false;
+        qs[i]->percentile    = 100.0f;
+    }
+}
+
 }   // namespace
 
 extern "C" {
@@ -361,34 +392,7 @@ int aimet_tq_reset_encoding_stats(aimet_tensor_quantizer* q, void* stream)
 
 int aimet_tq_reset_encoding_stats_many(aimet_tensor_quantizer* const* qs, int64_t nq, void* stream)
 {
-    return guarded([&] {
-        AIMET_REQUIRE(nq >= 0 && (qs != nullptr || nq == 0), "null argument");
-        if (nq == 0)
-            return;
-        std::vector<ZeroJob> zero;
-        std::vector<ResetJob> resets;
-        for (int64_t i = 0; i < nq; ++i)
-        {
-            aimet_tensor_quantizer* q = qs[i];
-            AIMET_REQUIRE(q != nullptr, "null quantizer");
-            AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one batched reset share a device");
-            zero.push_back(ZeroJob {q->arena, (int64_t) q->arena_bytes});
-            if (q->d.minmax && !in_arena(q, q->d.minmax))
-                zero.push_back(ZeroJob {q->d.minmax, (int64_t) (sizeof(float) * 2 * q->C)});
-            if (q->d.counts && !in_arena(q, q->d.counts))
-                zero.push_back(ZeroJob {q->d.counts, (int64_t) (sizeof(unsigned long long) * kPdfSize * q->C)});
-            resets.push_back(ResetJob {q->d.acc, q->C});
-        }
-        DeviceGuard g(qs[0]->device);
-        hipStream_t st = as_stream(stream);
-        launch_zero_many(zero, st);
-        launch_reset_state_many(resets, st);
-        for (int64_t i = 0; i < nq; ++i)
-        {
-            qs[i]->stats_updated = false;
-            qs[i]->percentile    = 100.0f;
-        }
-    });
+    return guarded([&] { reset_many(qs, nq, as_stream(stream)); });
 }
 
 int aimet_tq_set_percentile_value(aimet_tensor_quantizer* q, float p)
@@ -516,6 +520,39 @@ std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* 
     return jobs;
 }
 
+// per-channel statistics of many quantizers (two launches): the jobs of updateStatsPerChannelMany
+void channel_stats_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* outers,
+                        const int64_t* Cs, const int64_t* Ks, int64_t count, hipStream_t st)
+{
+    AIMET_REQUIRE(count >= 0, "negative quantizer count");
+    if (count == 0)
+        return;
+    AIMET_REQUIRE(qs && xs && outers && Cs && Ks, "null argument");
+    std::vector<ChannelJob> jobs;
+    jobs.reserve((size_t) count);
+    for (int64_t i = 0; i < count; ++i)
+    {
+        aimet_tensor_quantizer* q = qs[i];
+        check_shape(q, outers[i], Cs[i], Ks[i]);
+        AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one *_many call share a device");
+        if (outers[i] * Ks[i] > 0)
+            require_device_ptr(xs[i], "input");
+        ChannelJob j {};
+        j.x     = xs[i];
+        j.outer = outers[i];
+        j.C     = Cs[i];
+        j.K     = Ks[i];
+        j.d     = q->d;
+        j.kind  = (int32_t) q->kind;
+        j.vec   = ((reinterpret_cast<uintptr_t>(xs[i]) & 15) == 0 && Ks[i] % 4 == 0) ? 1 : 0;
+        jobs.push_back(j);
+    }
+    DeviceGuard g(qs[0]->device);
+    launch_channel_stats_many(jobs, st);
+    for (int64_t i = 0; i < count; ++i)
+        qs[i]->stats_updated = true;
+}
+
 int run_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns, const int64_t* counts,
              int64_t count, int phases, bool marks_updated, void* stream, const int64_t* counts_dev = nullptr)
 {
@@ -581,35 +618,7 @@ int aimet_tq_update_stats_channels_many(aimet_tensor_quantizer* const* qs, const
                                         const int64_t* outers, const int64_t* Cs, const int64_t* Ks, int64_t count,
                                         void* stream)
 {
-    return guarded([&] {
-        AIMET_REQUIRE(count >= 0, "negative quantizer count");
-        if (count == 0)
-            return;
-        AIMET_REQUIRE(qs && xs && outers && Cs && Ks, "null argument");
-        std::vector<ChannelJob> jobs;
-        jobs.reserve((size_t) count);
-        for (int64_t i = 0; i < count; ++i)
-        {
-            aimet_tensor_quantizer* q = qs[i];
-            check_shape(q, outers[i], Cs[i], Ks[i]);
-            AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one *_many call share a device");
-            if (outers[i] * Ks[i] > 0)
-                require_device_ptr(xs[i], "input");
-            ChannelJob j {};
-            j.x     = xs[i];
-            j.outer = outers[i];
-            j.C     = Cs[i];
-            j.K     = Ks[i];
-            j.d     = q->d;
-            j.kind  = (int32_t) q->kind;
-            j.vec   = ((reinterpret_cast<uintptr_t>(xs[i]) & 15) == 0 && Ks[i] % 4 == 0) ? 1 : 0;
-            jobs.push_back(j);
-        }
-        DeviceGuard g(qs[0]->device);
-        launch_channel_stats_many(jobs, as_stream(stream));
-        for (int64_t i = 0; i < count; ++i)
-            qs[i]->stats_updated = true;
-    });
+    return guarded([&] { channel_stats_many(qs, xs, outers, Cs, Ks, count, as_stream(stream)); });
 }
 
 int aimet_tq_minmax_buffer(aimet_tensor_quantizer* q, float** dev, int64_t* n)
@@ -902,6 +911,93 @@ void release_request(aimet_encoding_request* r)
 
 }   // namespace
 
+namespace
+{
+
+// The device half of a batched getEncoding (throws; the caller releases `req` on failure): every
+// TF-Enhanced search in ONE launch (one workgroup per channel of every quantizer), results back in
+// one copy; the MSE / entropy searches enqueued beside it; the other schemes read back their
+// statistics when the request is finished.
+aimet_encoding_request* encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym,
+                                         int strict, int unsign, hipStream_t st, aimet_encoding_request*& req)
+{
+    AIMET_REQUIRE(nq >= 0 && (qs != nullptr || nq == 0), "null argument");
+    for (int64_t i = 0; i < nq; ++i)
+    {
+        AIMET_REQUIRE(qs[i] != nullptr, "null quantizer");
+        AIMET_REQUIRE(qs[i]->device == qs[0]->device, "quantizers of one batched getEncoding share a device");
+    }
+    req         = new aimet_encoding_request;
+    req->qs.assign(qs, qs + nq);
+    req->b      = (int32_t) (uint8_t) bw;   // computeEncoding(uint8_t bw, ...)
+    req->sym    = sym;
+    req->strict = strict;
+    req->unsign = unsign;
+    if (nq == 0)
+        return req;
+    req->device = qs[0]->device;
+    DeviceGuard g(req->device);
+    const int32_t b = req->b;
+    std::vector<const TqDevice*> tfe, ent, mse;
+    std::vector<int64_t> entC, mseC;
+    int64_t off = 0, tfe_total = 0;
+    for (int64_t i = 0; i < nq; ++i)
+    {
+        aimet_tensor_quantizer* q = qs[i];
+        if (q->stats_updated && q->hist && q->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
+        {
+            tfe.push_back(&q->d);
+            req->tfe_Cs.push_back(q->C);
+            req->tfe_offs.push_back(off);
+            tfe_total += q->C;
+        }
+        else if (q->stats_updated && entropy_device(q, b))
+        {
+            ent.push_back(&q->d);
+            entC.push_back(q->C);
+        }
+        else if (q->stats_updated && q->hist && q->scheme == AIMET_QUANTIZATION_MSE)
+        {
+            mse.push_back(&q->d);
+            mseC.push_back(q->C);
+        }
+        off += q->C;
+    }
+    launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0, st);
+    launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0, st);
+    if (tfe_total > 0)
+    {
+        req->pinned = take_pinned(sizeof(aimet_tf_encoding) * (size_t) tfe_total, &req->pinned_bytes);
+        launch_tfe_search_many_to(tfe.data(), req->tfe_Cs.data(), (int) tfe.size(), b, sym, strict, unsign,
+                                  static_cast<aimet_tf_encoding*>(req->pinned), st);
+    }
+    req->done = take_event();
+    AIMET_HIP_CHECK(hipEventRecord(req->done, st));
+    return req;
+}
+
+// `waiter` continues after everything enqueued on `from` so far (a pooled event, no host wait)
+void stream_join(hipStream_t waiter, hipStream_t from)
+{
+    hipEvent_t e = take_event();
+    RequestPool& p = request_pool();
+    try
+    {
+        AIMET_HIP_CHECK(hipEventRecord(e, from));
+        AIMET_HIP_CHECK(hipStreamWaitEvent(waiter, e, 0));
+    }
+    catch (...)
+    {
+        std::lock_guard<std::mutex> lock(p.m);
+        p.events.push_back(e);
+        throw;
+    }
+    std::lock_guard<std::mutex> lock(p.m);
+    p.events.push_back(e);   // a later record does not affect the wait already enqueued
+}
+
+}   // namespace
+
 extern "C" {
 
 int aimet_tq_get_encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym, int strict,
@@ -909,63 +1005,9 @@ int aimet_tq_get_encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq,
 {
     aimet_encoding_request* req = nullptr;
     const int rc = guarded([&] {
-        AIMET_REQUIRE(req_out != nullptr && nq >= 0 && (qs != nullptr || nq == 0), "null argument");
+        AIMET_REQUIRE(req_out != nullptr, "null argument");
         *req_out = nullptr;
-        for (int64_t i = 0; i < nq; ++i)
-        {
-            AIMET_REQUIRE(qs[i] != nullptr, "null quantizer");
-            AIMET_REQUIRE(qs[i]->device == qs[0]->device, "quantizers of one batched getEncoding share a device");
-        }
-        req         = new aimet_encoding_request;
-        req->qs.assign(qs, qs + nq);
-        req->b      = (int32_t) (uint8_t) bw;   // computeEncoding(uint8_t bw, ...)
-        req->sym    = sym;
-        req->strict = strict;
-        req->unsign = unsign;
-        if (nq == 0)
-            return;
-        req->device = qs[0]->device;
-        DeviceGuard g(req->device);
-        hipStream_t st = as_stream(stream);
-        const int32_t b = req->b;
-        // every TF-Enhanced search in ONE launch (one workgroup per channel of every quantizer),
-        // results back in one copy; the MSE / entropy searches enqueued beside it; the other
-        // schemes read back their statistics when the request is finished
-        std::vector<const TqDevice*> tfe, ent, mse;
-        std::vector<int64_t> entC, mseC;
-        int64_t off = 0, tfe_total = 0;
-        for (int64_t i = 0; i < nq; ++i)
-        {
-            aimet_tensor_quantizer* q = qs[i];
-            if (q->stats_updated && q->hist && q->scheme == AIMET_QUANTIZATION_TF_ENHANCED)
-            {
-                tfe.push_back(&q->d);
-                req->tfe_Cs.push_back(q->C);
-                req->tfe_offs.push_back(off);
-                tfe_total += q->C;
-            }
-            else if (q->stats_updated && entropy_device(q, b))
-            {
-                ent.push_back(&q->d);
-                entC.push_back(q->C);
-            }
-            else if (q->stats_updated && q->hist && q->scheme == AIMET_QUANTIZATION_MSE)
-            {
-                mse.push_back(&q->d);
-                mseC.push_back(q->C);
-            }
-            off += q->C;
-        }
-        launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0, st);
-        launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0, st);
-        if (tfe_total > 0)
-        {
-            req->pinned = take_pinned(sizeof(aimet_tf_encoding) * (size_t) tfe_total, &req->pinned_bytes);
-            launch_tfe_search_many_to(tfe.data(), req->tfe_Cs.data(), (int) tfe.size(), b, sym, strict, unsign,
-                                      static_cast<aimet_tf_encoding*>(req->pinned), st);
-        }
-        req->done = take_event();
-        AIMET_HIP_CHECK(hipEventRecord(req->done, st));
+        encodings_launch(qs, nq, bw, sym, strict, unsign, as_stream(stream), req);
     });
     if (rc != AIMET_OK)
     {
@@ -973,6 +1015,63 @@ int aimet_tq_get_encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq,
         return rc;
     }
     *req_out = req;
+    return rc;
+}
+
+int aimet_calibrate_launch(aimet_tensor_quantizer* const* act_qs, const float* const* act_x, const int64_t* act_n,
+                           int64_t n_act, aimet_tensor_quantizer* const* par_qs, const float* const* par_x,
+                           const int64_t* par_outer, const int64_t* par_C, const int64_t* par_K, int64_t n_par,
+                           const int32_t* act_settings, const int32_t* par_settings, int reset, void* main_stream,
+                           void* side_stream, aimet_encoding_request** act_req, aimet_encoding_request** par_req)
+{
+    aimet_encoding_request *ra = nullptr, *rp = nullptr;
+    const int rc = guarded([&] {
+        AIMET_REQUIRE(act_req != nullptr && par_req != nullptr && act_settings != nullptr && par_settings != nullptr,
+                      "null argument");
+        AIMET_REQUIRE(n_act >= 0 && n_par >= 0, "negative quantizer count");
+        *act_req = *par_req = nullptr;
+        const int dev = n_act ? act_qs[0]->device : (n_par ? par_qs[0]->device : -1);
+        for (int64_t i = 0; i < n_par; ++i)
+            AIMET_REQUIRE(par_qs[i] != nullptr && par_qs[i]->device == dev, "quantizers of one calibration share a device");
+        hipStream_t ms = as_stream(main_stream), ss = as_stream(side_stream);
+        if (dev < 0)
+            return;
+        DeviceGuard g(dev);
+        // each side resets its own quantizers (the parameters' PDF arenas are most of the bytes)
+        if (reset)
+            reset_many(act_qs, n_act, ms);
+        if (n_par)
+        {
+            // the parameters first, on their own stream: their statistics take the CUs before the
+            // activation passes, their search runs beside them (aimet_amd/calibration.py)
+            if (ss != ms)
+                stream_join(ss, ms);
+            if (reset)
+                reset_many(par_qs, n_par, ss);
+            channel_stats_many(par_qs, par_x, par_outer, par_C, par_K, n_par, ss);
+            encodings_launch(par_qs, n_par, (uint32_t) par_settings[0], par_settings[1], par_settings[2],
+                             par_settings[3], ss, rp);
+        }
+        if (n_act)
+        {
+            auto jobs = make_jobs(act_qs, act_x, act_n, nullptr, n_act);
+            launch_stats_many(jobs, kPhaseMinmax | kPhaseFoldMinmax | kPhaseHistogram | kPhaseFoldHistogram, ms);
+            for (int64_t i = 0; i < n_act; ++i)
+                act_qs[i]->stats_updated = true;
+        }
+        encodings_launch(act_qs, n_act, (uint32_t) act_settings[0], act_settings[1], act_settings[2],
+                         act_settings[3], ms, ra);
+        if (n_par && ss != ms)
+            stream_join(ms, ss);   // later work on the main stream sees the parameters' state too
+    });
+    if (rc != AIMET_OK)
+    {
+        release_request(ra);
+        release_request(rp);
+        return rc;
+    }
+    *act_req = ra;
+    *par_req = rp;
     return rc;
 }
 

@@ -553,7 +553,9 @@ __device__ __forceinline__ void fold_hist_one(const TqDevice& d, int64_t c, int6
     int it        = d.iterations[c];
     int64_t idx   = c * kPdfSize + threadIdx.x;
     double prob   = (double) d.counts[idx] / (double) count;
-    d.pdf[idx]    = (d.pdf[idx] * it + prob) / (it + 1);
+    // first batch: (0 * 0 + prob) / 1 == prob exactly (the PDF is zero since the reset), so the
+    // old PDF is not read
+    d.pdf[idx]    = it == 0 ? prob : (d.pdf[idx] * it + prob) / (it + 1);
     d.counts[idx] = 0;
     __syncthreads();
     if (threadIdx.x == 0)
@@ -603,28 +605,82 @@ __global__ __launch_bounds__(kBlock) void reset_acc_many_kernel(const ResetJob* 
 // A calibration batch updates every activation quantizer of the model: per quantizer the single
 // launches are min/max + combine + fold + histogram + PDF fold (5 launches, ~5 us each); for
 // ViT-L's 99 quantizers that is ~500 launches per batch. Here each phase is ONE launch over all
-// quantizers: workgroup -> quantizer by a binary search over the quantizers' first workgroups.
+// quantizers: workgroup -> quantizer = the last quantizer whose first workgroup is <= blockIdx.x.
+// Every wave finds it with ONE round of loads (lane i reads quantizer i's first workgroup, a ballot
+// counts those <= b) instead of a binary search's chain of dependent loads: under a full HBM queue
+// each dependent load costs microseconds during which the new workgroup has no data load in flight.
+template <class Job, class First>
+__device__ __forceinline__ int find_job_ballot(const Job* __restrict__ jobs, int njobs, uint32_t b, First first)
+{
+    const int lane = threadIdx.x & 63;
+    int count      = 0;
+    for (int base = 0; base < njobs; base += 64)
+    {
+        const int i            = base + lane;
+        const bool le          = i < njobs && first(jobs[i]) <= b;
+        const unsigned long long m = __ballot(le);
+        count += __popcll(m);
+        if (m != ~0ull)
+            break;   // first workgroups ascend: no later quantizer starts at or before b
+    }
+    return count - 1;
+}
+
 __device__ __forceinline__ int find_job(const StatsJob* __restrict__ jobs, int njobs, uint32_t b, bool hist)
 {
-    int lo = 0, hi = njobs - 1;
-    while (lo < hi)
-    {
-        int mid        = (lo + hi + 1) >> 1;
-        uint32_t first = hist ? jobs[mid].h_block0 : jobs[mid].mm_block0;
-        if (first <= b)
-            lo = mid;
-        else
-            hi = mid - 1;
-    }
-    return lo;
+    return hist ? find_job_ballot(jobs, njobs, b, [](const StatsJob& j) { return j.h_block0; })
+                : find_job_ballot(jobs, njobs, b, [](const StatsJob& j) { return j.mm_block0; });
 }
+
+// One 16-KiB tile per workgroup (4 x 16-B nontemporal loads per lane), tiles of every quantizer
+// in address order, one {-min, max} partial per tile. Against grid-stride workgroups over each
+// tensor this streams at 6.7 vs 5.9 TB/s on ResNet-50's activations (tools/read_ceiling.py): the
+// workgroups resident at any moment read one contiguous window of HBM.
+constexpr int64_t kMmTile = (int64_t) kBlock * 16;   // elements per tile
+typedef const __attribute__((address_space(1))) f4* gf4p;
 
 __global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
 {
     const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, false)];
     if (J.hist && !J.ent && J.d.pdf_init[0])
         return;   // PDF schemes take min/max on the first (non-zero) batch only
-    minmax_part(J.x, J.n, J.vec, blockIdx.x - J.mm_block0, J.mm_blocks, reinterpret_cast<float2*>(J.d.partials));
+    const int64_t tile = blockIdx.x - J.mm_block0;
+    const int64_t n    = J.n;
+    float mn = INFINITY, mx = -INFINITY;
+    int64_t tail0 = 0;
+    if (J.vec)
+    {
+        gf4p x4            = (gf4p) J.x;
+        const int64_t nvec = n / 4;
+        const int64_t base = tile * (kMmTile / 4) + threadIdx.x;
+        f4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)   // NaN padding is ignored by fminf/fmaxf
+            v[u] = base + u * kBlock < nvec ? __builtin_nontemporal_load(x4 + base + u * kBlock)
+                                            : f4 {NAN, NAN, NAN, NAN};
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            accum4(make_float4(v[u].x, v[u].y, v[u].z, v[u].w), mn, mx);
+        tail0 = nvec * 4;   // the last tile also takes the < 4 trailing elements
+        if (tile == (int64_t) J.mm_blocks - 1)
+            for (int64_t i = tail0 + threadIdx.x; i < n; i += kBlock)
+            {
+                mn = fminf(mn, J.x[i]);
+                mx = fmaxf(mx, J.x[i]);
+            }
+    }
+    else
+    {
+        const int64_t end = (tile + 1) * kMmTile < n ? (tile + 1) * kMmTile : n;
+        for (int64_t i = tile * kMmTile + threadIdx.x; i < end; i += kBlock)
+        {
+            mn = fminf(mn, J.x[i]);
+            mx = fmaxf(mx, J.x[i]);
+        }
+    }
+    block_minmax(mn, mx);
+    if (threadIdx.x == 0)
+        reinterpret_cast<float2*>(J.mm_part)[tile] = make_float2(-mn, mx);
 }
 
 // one workgroup per quantizer: partials -> minmax[0] = {-min, max}; optionally the fold
@@ -633,12 +689,22 @@ __global__ __launch_bounds__(kBlock) void combine_many_kernel(const StatsJob* __
     const StatsJob& J = jobs[blockIdx.x];
     if (J.hist && !J.ent && J.d.pdf_init[0])
         return;
-    const float2* partials = reinterpret_cast<const float2*>(J.d.partials);
+    const float2* partials = reinterpret_cast<const float2*>(J.mm_part);
     float a = -INFINITY, b = -INFINITY;
-    for (uint32_t i = threadIdx.x; i < J.mm_blocks; i += kBlock)
+    // a 205-MB tensor leaves 12.5 K tile partials: 8 independent loads in flight per lane
+    const uint32_t nb = J.mm_blocks;
+    for (uint32_t i0 = threadIdx.x; i0 < nb; i0 += kBlock * 8)
     {
-        a = fmaxf(a, partials[i].x);
-        b = fmaxf(b, partials[i].y);
+        float2 p[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            p[u] = i0 + u * kBlock < nb ? partials[i0 + u * kBlock] : make_float2(-INFINITY, -INFINITY);
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+        {
+            a = fmaxf(a, p[u].x);
+            b = fmaxf(b, p[u].y);
+        }
     }
     float na = -a;
     block_minmax(na, b);
@@ -705,16 +771,7 @@ __global__ __launch_bounds__(kPdfSize) void fold_histogram_many_kernel(const Sta
 // the workgroup that reduces channel c also folds it.
 __device__ __forceinline__ int find_channel_job(const ChannelJob* __restrict__ jobs, int njobs, uint32_t b)
 {
-    int lo = 0, hi = njobs - 1;
-    while (lo < hi)
-    {
-        int mid = (lo + hi + 1) >> 1;
-        if (jobs[mid].block0 <= b)
-            lo = mid;
-        else
-            hi = mid - 1;
-    }
-    return lo;
+    return find_job_ballot(jobs, njobs, b, [](const ChannelJob& j) { return j.block0; });
 }
 
 __device__ __forceinline__ void channel_minmax(const ChannelJob& J, int64_t c, float& mn, float& mx)
@@ -829,6 +886,8 @@ __device__ __forceinline__ void channel_hist_fold(const ChannelJob& J, int64_t c
         const int64_t idx = c * kPdfSize + b;
         if (ENT)
             d.pdf[idx] = d.pdf[idx] + (double) s;                        // math_functions.cpp:554-559
+        else if (it == 0)   // (0 * 0 + p) / 1 == p exactly: the PDF is zero since the reset
+            d.pdf[idx] = (double) s / count;
         else
             d.pdf[idx] = (d.pdf[idx] * it + (double) s / count) / (it + 1);   // UpdatePdf:280-287
     }
@@ -969,8 +1028,7 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
     for (auto& j: jobs)
     {
         j.mm_block0 = (uint32_t) mm;
-        j.mm_blocks = (uint32_t) (j.n > 0 ? std::min<int64_t>(kMinmaxParts, ceil_div(j.n, (int64_t) kBlock * 16))
-                                          : 1);
+        j.mm_blocks = (uint32_t) std::max<int64_t>(1, ceil_div(j.n, kMmTile));
         j.h_block0  = (uint32_t) hb;
         j.h_blocks  = (uint32_t) (j.hist ? std::max<int64_t>(1, std::min<int64_t>(kHistGrid,
                                                                                ceil_div(j.n, hist_elems_per_block())))
@@ -980,6 +1038,13 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
     }
     AIMET_REQUIRE(mm < (uint64_t(1) << 31) && hb < (uint64_t(1) << 31), "too many workgroups");
     const int n = (int) jobs.size();
+    float* parts = nullptr;
+    if (phases & kPhaseMinmax)
+    {
+        parts = static_cast<float*>(scratch_alloc(sizeof(float) * 2 * mm, s));
+        for (auto& j: jobs)
+            j.mm_part = parts + 2 * (int64_t) j.mm_block0;
+    }
     auto* dj = static_cast<StatsJob*>(upload_async(jobs.data(), sizeof(StatsJob) * n, s));
     if (phases & kPhaseMinmax)
     {
@@ -1009,6 +1074,8 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
         fold_histogram_many_kernel<<<n, kPdfSize, 0, s>>>(dj);
         AIMET_LAUNCH_CHECK();
     }
+    if (parts)
+        scratch_free(parts, s);
     scratch_free(dj, s);
 }
 

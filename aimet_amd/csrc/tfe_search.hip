@@ -9,6 +9,7 @@
 // shared header tfe_core.hpp, compiled for the host and the device from one source (bit-exact).
 #include "tfe_core.hpp"
 
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include "tq_state.hpp"
@@ -201,10 +202,21 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 6 : 7) void tfe_search_kernel
 }
 
 // one candidate per lane: 101 symmetric candidates -> 2 waves, 358 asymmetric -> 6 waves
+int search_grid_cap()
+{
+    static int v = [] {
+        const char* e = getenv("AIMET_TUNE_TFE_GRID");   // tuning experiments only
+        int g         = e ? atoi(e) : 65536;
+        return g > 0 ? g : 65536;
+    }();
+    return v;
+}
+
 void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t total, int bw, bool sym, bool strict,
                    bool unsign, hipStream_t s)
 {
-    const int grid = (int) (total < 65536 ? total : 65536);
+    const int cap  = search_grid_cap();
+    const int grid = (int) (total < cap ? total : cap);
     if (sym)
         tfe_search_kernel<128><<<grid, 128, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign);
     else

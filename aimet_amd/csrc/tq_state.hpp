@@ -79,6 +79,7 @@ struct StatsJob
     const int64_t* count_dev;   // when set: the count is read on the device (summed over ranks in HBM)
     TqDevice d;
     uint32_t mm_block0, mm_blocks, h_block0, h_blocks;   // filled by launch_stats_many
+    float* mm_part;  // [mm_blocks][2] per-tile {-min, max} (launch_stats_many's scratch)
     int32_t hist, vec;
     int32_t ent;     // entropy analyzer (hist == 1 too): min/max every batch, TensorProfilingParams
 };

@@ -402,6 +402,66 @@ class AimetTensorQuantizer:
         return PendingEncodings(list(quantizers), bitwidth, use_symmetric_encodings, use_strict_symmetric,
                                 use_unsigned_symmetric)
 
+    @staticmethod
+    def calibrateResidentAsync(act_quantizers, activations, param_quantizers, params, param_ch_axes=None,
+                               act_settings=(8, False, False, False), param_settings=(8, True, False, False),
+                               reset=False, main_stream=None, side_stream=None):
+        """One calibration batch in ONE native call (aimet_calibrate_launch): optionally
+        resetEncodingStats of every quantizer, the activations' statistics (one launch per phase for
+        all per-tensor quantizers) + search on `main_stream`, the parameters' per-channel statistics
+        + search on `side_stream` (after everything queued on main so far). Returns
+        (PendingEncodings of the activations, PendingEncodings of the parameters) and the
+        contiguous inputs, to be kept alive until both are finished."""
+        aq, pq = list(act_quantizers), list(param_quantizers)
+        if any(q._num_channels != 1 for q in aq):
+            raise ValueError("calibrateResidentAsync: the activation quantizers are per-tensor")
+        dev = (activations[0] if aq else params[0]).device
+        ch_axes = list(param_ch_axes) if param_ch_axes is not None else [0] * len(pq)
+        keep, a_ptr, a_n = [], [], []
+        for t in activations:
+            _require_gpu(t)
+            t = t if t.is_contiguous() else t.contiguous()
+            if t.dtype != torch.float32:
+                raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
+            keep.append(t)
+            a_ptr.append(t.data_ptr())
+            a_n.append(t.numel())
+        p_ptr, outers, Cs, Ks = [], [], [], []
+        for q, t, ax in zip(pq, params, ch_axes):
+            _require_gpu(t)
+            t = t if t.is_contiguous() else t.contiguous()
+            if t.dtype != torch.float32:
+                raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
+            outer, C, K = per_channel_view(t.shape, ax) if q._num_channels != 1 else (1, 1, t.numel())
+            if C != q._num_channels:
+                raise ValueError("tensor has %d channels along axis %d, quantizer has %d" % (C, ax, q._num_channels))
+            keep.append(t)
+            p_ptr.append(t.data_ptr())
+            outers.append(outer)
+            Cs.append(C)
+            Ks.append(K)
+        handles = AimetTensorQuantizer._ensure_many(aq + pq, dev)
+        if reset:
+            for q in aq + pq:
+                q._pending_percentile = None
+        na, np_ = len(aq), len(pq)
+        ra, rp = ctypes.c_void_p(), ctypes.c_void_p()
+        main = main_stream if main_stream is not None else torch.cuda.current_stream(dev)
+        side = side_stream if side_stream is not None else main
+        with torch.cuda.device(dev):
+            _native.call("aimet_calibrate_launch", (ctypes.c_void_p * max(na, 1))(*handles[:na]),
+                         (ctypes.c_void_p * max(na, 1))(*a_ptr), (ctypes.c_int64 * max(na, 1))(*a_n), na,
+                         (ctypes.c_void_p * max(np_, 1))(*handles[na:]), (ctypes.c_void_p * max(np_, 1))(*p_ptr),
+                         (ctypes.c_int64 * max(np_, 1))(*outers), (ctypes.c_int64 * max(np_, 1))(*Cs),
+                         (ctypes.c_int64 * max(np_, 1))(*Ks), np_,
+                         (ctypes.c_int32 * 4)(*[int(v) for v in act_settings]),
+                         (ctypes.c_int32 * 4)(*[int(v) for v in param_settings]), int(bool(reset)),
+                         main.cuda_stream, side.cuda_stream, ctypes.byref(ra), ctypes.byref(rp))
+        for q in aq + pq:
+            q._is_encoding_valid = True
+        return (PendingEncodings(aq, *act_settings, request=ra), PendingEncodings(pq, *param_settings, request=rp),
+                keep)
+
     def getStatsHistogram(self, channel: int = 0):
         """AimetTensorQuantizer.cpp:194-198 -> list of (xLeft, pdf)."""
         import numpy as np
@@ -520,11 +580,16 @@ class AimetTensorQuantizer:
 class PendingEncodings:
     """A batched getEncoding in flight (AimetTensorQuantizer.getEncodingsAsync)."""
 
-    def __init__(self, quantizers, bitwidth, sym, strict, unsign):
+    def __init__(self, quantizers, bitwidth, sym, strict, unsign, request=None):
         self.quantizers = quantizers
         self.live = [q for q in quantizers if q._handle is not None and q._is_encoding_valid]
         self.req = None
-        if self.live:
+        if request is not None:
+            # a request launched for exactly these quantizers (aimet_calibrate_launch)
+            if len(self.live) != len(quantizers):
+                raise RuntimeError("a launched request covers every quantizer")
+            self.req = request if request.value else None
+        elif self.live:
             dev = self.live[0]._device
             handles = (ctypes.c_void_p * len(self.live))(*[q._handle for q in self.live])
             req = ctypes.c_void_p()

@@ -177,12 +177,12 @@ def compute_encodings(acts, weights, quantizers=None):
               for _, w in weights]
     else:
         aq, wq = quantizers
-        AimetTensorQuantizer.resetEncodingStatsMany(aq + wq)
     # activations (sharded across ranks, one packed collective per phase) and per-channel weights
-    # on a second stream: aimet_amd.calibration
+    # on a second stream, after the reset of the sim's quantizers: aimet_amd.calibration
     a_res, w_res = compute_encodings_resident(aq, [t for _, t in acts], wq, [w for _, w in weights],
                                               act_settings=(8, False, False, False),
-                                              param_settings=(8, True, False, False))
+                                              param_settings=(8, True, False, False),
+                                              reset=quantizers is not None)
     act_enc = [e for e, _ in a_res]
     w_enc = [e for e, _ in w_res]
     return act_enc, w_enc, time.perf_counter() - t0, aq, wq

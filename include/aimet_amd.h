@@ -63,6 +63,13 @@ const char* aimet_last_error(void);
 const char* aimet_version(void);
 /* Number of gfx950 devices visible; negative status on HIP failure. */
 int aimet_device_count(void);
+/* Streams restricted to a set of CUs (hipExtStreamCreateWithCUMask; bit i of the mask words =
+ * CU i, words of 32 bits). compute_encodings partitions the CUs between the HBM-bound activation
+ * passes and the compute-bound parameter searches with two such streams, so the two run side by
+ * side instead of competing for every CU (no reference counterpart: host scheduling only). */
+int aimet_stream_create_cu_masked(const uint32_t* cu_mask, uint32_t words, void** stream);
+int aimet_stream_get_cu_mask(void* stream, uint32_t words, uint32_t* cu_mask);
+int aimet_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Encoding math (host, exact reference arithmetic)                                            */
@@ -273,6 +280,20 @@ int aimet_tq_get_encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq,
                                   int use_strict_symmetric, int use_unsigned_symmetric, void* stream,
                                   aimet_encoding_request** request);
 int aimet_tq_get_encodings_finish(aimet_encoding_request* request, aimet_tf_encoding* out, int* valid);
+
+/* One calibration batch of tensors already resident in HBM, every quantizer in one call:
+ * QuantizationSimModel.compute_encodings' resetEncodingStats (reset != 0) + updateStats of every
+ * quantizer + getEncoding of every quantizer (v1/quantsim.py:381-449), enqueued with no host wait.
+ * Activations (per-tensor, act_x[i] of act_n[i] floats) on `main_stream`: one launch per phase for
+ * all of them + one search launch. Parameters (per channel of [outer][C][K]) first, on
+ * `side_stream` (which waits for `main_stream`; `main_stream` then waits for it) or, when the two
+ * are the same stream, ahead of the activations on it: two statistics launches + one search launch. act_settings / par_settings = {bw, symmetric, strict, unsigned}. The two
+ * requests are finished (and freed) with aimet_tq_get_encodings_finish; on error neither exists. */
+int aimet_calibrate_launch(aimet_tensor_quantizer* const* act_qs, const float* const* act_x, const int64_t* act_n,
+                           int64_t n_act, aimet_tensor_quantizer* const* par_qs, const float* const* par_x,
+                           const int64_t* par_outer, const int64_t* par_C, const int64_t* par_K, int64_t n_par,
+                           const int32_t* act_settings, const int32_t* par_settings, int reset, void* main_stream,
+                           void* side_stream, aimet_encoding_request** act_req, aimet_encoding_request** par_req);
 
 /* AimetTensorQuantizer.cpp:194-198 getStatsHistogram (histogram schemes): xleft/pdf[512] of
  * `channel`; *n = 0 when no histogram exists yet. Synchronises `stream`. */

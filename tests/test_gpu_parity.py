@@ -1087,6 +1087,50 @@ def test_create_many_shared_state_lifetime():
     torch.cuda.synchronize()
 
 
+@pytest.mark.parametrize("schemes", ["tfe", "mixed"])
+def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatch):
+    """compute_encodings_resident's one native call (aimet_calibrate_launch, reset folded in) ==
+    the phase-by-phase path from Python (resetEncodingStatsMany + per-phase *_many launches + the
+    two requests), on quantizers that already hold the previous batch's statistics; and a second
+    reset + recompute of the same data == the first (nothing of the earlier batch survives)."""
+    from aimet_amd import calibration
+    from aimet_amd.calibration import compute_encodings_resident
+    g = torch.Generator(device=DEV).manual_seed(21)
+    M = QuantizationMode
+    a_modes = [M.QUANTIZATION_TF_ENHANCED] * 4 if schemes == "tfe" else \
+        [M.QUANTIZATION_TF, M.QUANTIZATION_TF_ENHANCED, M.QUANTIZATION_PERCENTILE, M.QUANTIZATION_MSE]
+    p_modes = [M.QUANTIZATION_TF_ENHANCED] * 3 if schemes == "tfe" else \
+        [M.QUANTIZATION_TF, M.QUANTIZATION_TF_ENHANCED, M.QUANTIZATION_MSE]
+
+    def batch(scale):
+        acts = [torch.relu(torch.randn(n, device=DEV, generator=g) * scale * (1 + i)) for i, n in
+                enumerate((1 << 20, 3001, 77777, 1 << 18))]
+        params = [torch.randn(c, k, device=DEV, generator=g) * 0.05 * scale
+                  for c, k in ((64, 27), (128, 576), (10, 2048))]
+        return acts, params
+
+    old, new_ = batch(3.0), batch(1.0)
+    results = []
+    for native in (True, False):
+        monkeypatch.setattr(calibration, "_SCHEDULE", "params_first" if native else "params_first_phased")
+        aq = [AimetTensorQuantizer(m) for m in a_modes]
+        pq = [AimetTensorQuantizer(m, num_channels=p.shape[0]) for m, p in zip(p_modes, new_[1])]
+        compute_encodings_resident(aq, old[0], pq, old[1])                 # earlier statistics
+        r1 = compute_encodings_resident(aq, new_[0], pq, new_[1], reset=True)
+        r2 = compute_encodings_resident(aq, new_[0], pq, new_[1], reset=True)
+        flat = lambda r: ([e.to_tuple() for e, _ in r[0]],
+                          [[x.to_tuple() for x in (es if isinstance(es, list) else [es])] for es, _ in r[1]])
+        assert flat(r1) == flat(r2)
+        results.append(flat(r1))
+    assert results[0] == results[1]
+    # and == fresh quantizers fed only the new batch
+    fa = [AimetTensorQuantizer(m) for m in a_modes]
+    fp = [AimetTensorQuantizer(m, num_channels=p.shape[0]) for m, p in zip(p_modes, new_[1])]
+    monkeypatch.setattr(calibration, "_SCHEDULE", "params_first")
+    fresh = compute_encodings_resident(fa, new_[0], fp, new_[1])
+    assert ([e.to_tuple() for e, _ in fresh[0]]) == results[0][0]
+
+
 def test_compute_encodings_resident_equals_individual():
     """aimet_amd.calibration.compute_encodings_resident (batched activation statistics, parameter
     statistics + searches on a second stream) == updateStats / getEncoding quantizer by quantizer."""

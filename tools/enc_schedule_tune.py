@@ -33,8 +33,9 @@ print(json.dumps({"fresh_median_ms": round(w[len(w) // 2], 3), "reset_median_ms"
                   "reset_min_ms": round(r[0], 3), "reset_all": [round(t, 3) for t in tr]}))
 """ % REPO
 
-for sched, prio in itertools.product(("params_first", "acts_first"), ("-1", "0")):
-    env = dict(os.environ, AIMET_CAL_SCHEDULE=sched, AIMET_CAL_SIDE_PRIORITY=prio)
-    out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
-    line = [l for l in out.stdout.splitlines() if l.startswith("{")]
-    print(sched, prio, line[-1] if line else out.stderr[-2000:], flush=True)
+if __name__ == "__main__":
+    for sched, prio in itertools.product(("params_first", "acts_first"), ("-1", "0")):
+        env = dict(os.environ, AIMET_CAL_SCHEDULE=sched, AIMET_CAL_SIDE_PRIORITY=prio)
+        out = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+        line = [l for l in out.stdout.splitlines() if l.startswith("{")]
+        print(sched, prio, line[-1] if line else out.stderr[-2000:], flush=True)
