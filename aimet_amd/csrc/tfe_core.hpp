@@ -242,6 +242,64 @@ AIMET_HD inline int quant_code(float v, float delta, int offset, float rcp, floa
     return (int) roundf(v / delta - offset);
 }
 
+// The three sums of _quantAndSatCost over visited bins [k0, k1), ascending. Four bins' terms are
+// formed at once (independent LDS loads and products: a lane's loop is latency-bound otherwise)
+// and added in the serial order, so every sum is the reference's, bit for bit.
+AIMET_HD inline double sat_sum(const Bins& B, int k0, int k1, double mid)
+{
+    double s = 0;
+    int k    = k0;
+    for (; k + 4 <= k1; k += 4)
+    {
+        double t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            double d = B.cd_c[k + u] - mid;
+            t[u]     = B.pdf_c[k + u] * (d * d);
+        }
+        s += t[0];
+        s += t[1];
+        s += t[2];
+        s += t[3];
+    }
+    for (; k < k1; ++k)
+    {
+        double d = B.cd_c[k] - mid;
+        s += B.pdf_c[k] * (d * d);
+    }
+    return s;
+}
+
+AIMET_HD inline double quant_term(const Bins& B, int k, float delta, int offset, float rcp, float thr)
+{
+    float v   = B.cf_c[k];
+    int q     = quant_code(v, delta, offset, rcp, thr);
+    float deq = delta * (q + offset);
+    double d  = (double) (v - deq);
+    return B.pdf_c[k] * (d * d);
+}
+
+AIMET_HD inline double quant_sum(const Bins& B, int k0, int k1, float delta, int offset, float rcp, float thr)
+{
+    double s = 0;
+    int k    = k0;
+    for (; k + 4 <= k1; k += 4)
+    {
+        double t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            t[u] = quant_term(B, k + u, delta, offset, rcp, thr);
+        s += t[0];
+        s += t[1];
+        s += t[2];
+        s += t[3];
+    }
+    for (; k < k1; ++k)
+        s += quant_term(B, k, delta, offset, rcp, thr);
+    return s;
+}
+
 // _quantAndSatCost (:293-355) over the prepared bins. The reference's three loops are kept as
 // three loops, each over its own contiguous range of visited bins (i < iLo, i >= iHi,
 // iLo <= i < iHi) in ascending order, so every sum adds the same terms in the same order; a bin
@@ -295,24 +353,9 @@ AIMET_HD inline double cost(const Bins& B, int bw, float delta, int offset)
         double c = kGamma * (satLo + satHi) + quant;
         return smin(c, DBL_MAX);
     }
-    for (int k = 0; k < kLo; ++k)
-    {
-        double d = B.cd_c[k] - loMid;
-        satLo += B.pdf_c[k] * (d * d);
-    }
-    for (int k = kHi; k < B.nnz; ++k)
-    {
-        double d = B.cd_c[k] - hiMid;
-        satHi += B.pdf_c[k] * (d * d);
-    }
-    for (int k = kLo; k < kHi; ++k)   // empty unless iLo < iHi
-    {
-        float v   = B.cf_c[k];
-        int q     = quant_code(v, delta, offset, rcp, thr);
-        float deq = delta * (q + offset);
-        double d  = (double) (v - deq);
-        quant += B.pdf_c[k] * (d * d);
-    }
+    satLo = sat_sum(B, 0, kLo, loMid);
+    satHi = sat_sum(B, kHi, B.nnz, hiMid);
+    quant = quant_sum(B, kLo, kHi, delta, offset, rcp, thr);   // empty unless iLo < iHi
     double c = kGamma * (satLo + satHi) + quant;
     return smin(c, DBL_MAX);
 }

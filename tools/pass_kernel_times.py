@@ -1,6 +1,7 @@
-"""The activation passes of compute_encodings alone (bench.py's ResNet-50 bs256 activations, 55
-TF-Enhanced quantizers, reset + recompute, no weights), 12 calls: run under
-rocprofv3 --kernel-trace --stats for the per-kernel durations of the min/max and histogram passes."""
+"""The two halves of compute_encodings alone, 12 calls each (bench.py's ResNet-50 bs256 workload,
+reset + recompute): `acts` = the 55 TF-Enhanced activation quantizers (min/max and histogram
+passes), `weights` = the 54 per-channel symmetric weight quantizers (channel statistics + the
+27,560-channel TF-E search). Run under rocprofv3 --kernel-trace --stats for per-kernel durations."""
 import os
 import sys
 
@@ -18,12 +19,16 @@ dev = torch.device("cuda", 0)
 torch.cuda.set_device(dev)
 model = resnet50(seed=0, device=dev)
 x = torch.rand(256, 3, 224, 224, device=dev, generator=torch.Generator(device=dev).manual_seed(1234))
-acts, _ = bench.collect_tensors(model, x)
+acts, weights = bench.collect_tensors(model, x)
 del model, x
 torch.cuda.empty_cache()
-aq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in acts]
-A = [t for _, t in acts]
+TFE = QuantizationMode.QUANTIZATION_TF_ENHANCED
+which = sys.argv[1] if len(sys.argv) > 1 else "acts"
+aq = [AimetTensorQuantizer(TFE) for _ in acts] if which == "acts" else []
+A = [t for _, t in acts] if which == "acts" else []
+wq = [AimetTensorQuantizer(TFE, num_channels=w.shape[0]) for _, w in weights] if which == "weights" else []
+W = [w for _, w in weights] if which == "weights" else []
 for _ in range(12):
-    compute_encodings_resident(aq, A, [], [], reset=True)
+    compute_encodings_resident(aq, A, wq, W, param_settings=(8, True, False, False), reset=True)
 torch.cuda.synchronize()
 print("done", flush=True)
