@@ -53,7 +53,7 @@ struct TfeJob
 };
 
 template <int BLOCK>
-__global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 6 : 7) void tfe_search_kernel(TfeJob one, const TfeJob* __restrict__ jobs, int njobs,
+__global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : 7) void tfe_search_kernel(TfeJob one, const TfeJob* __restrict__ jobs, int njobs,
                                                            int64_t total, int bw, int sym, int strict, int unsign)
 {
     constexpr int kW = BLOCK / 64;
