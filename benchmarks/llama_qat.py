@@ -12,6 +12,8 @@ learning) per-channel 4-bit symmetric weight quantizers, seq 2048, micro-batch 1
   learnable per-output-channel range) and its output (16-bit, learnable per-tensor range) with
   the fused learned-grid kernels; matmuls run in bf16 (torch.autocast); Adam (fused) updates
   weights and ranges.
+  --impl reference: the same QuantSim with the reference's torch-op QuantizeDequantizeFunc for
+  every learned-grid quantizer (RefQuantizeDequantize), for a like-for-like step time.
 --path module: the weight-only hand-built QAT linear of round 1 (no activation quantizers):
   --impl fused      aimet_amd's learned-grid kernels (one forward pass, one backward pass per weight)
   --impl reference  the reference's torch-op QuantizeDequantizeFunc (v1/tensor_quantizer.py:896-986 over
@@ -56,6 +58,43 @@ class RefLearnedGrid(torch.autograd.Function):
         gmax = ((x_quant + offset) * grad).sum(dim=1) - (mask * (x / delta) * grad).sum(dim=1)
         gmax = gmax / torch.div(ctx.steps, 2, rounding_mode="floor")
         return grad_x, -gmax, gmax
+
+
+class RefQuantizeDequantize(torch.autograd.Function):
+    """--path quantsim --impl reference: the reference's QuantizeDequantizeFunc for every quantizer
+    QuantSim wraps (4-bit per-channel weights AND 16-bit per-tensor outputs), torch ops in float32
+    (v1/tensor_quantizer.py:896-986 over quantsim_straight_through_grad.py:191-328): the forward saves
+    mask and x_quant, the backward forms grad_x and the range gradients from them. Swapped in for
+    aimet_amd.learned_grid.LearnedGridQuantizeDequantize (same apply signature)."""
+
+    @staticmethod
+    def forward(ctx, x, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0):
+        from oracle import torch_ref as T
+        x32 = x.float()
+        y, mask, x_quant, delta, offset, steps = T.lg_forward(x32, emin.float(), emax.float(), bw, sym, strict,
+                                                              unsigned, ch_axis)
+        ctx.save_for_backward(x32, mask, x_quant, delta, offset, emin, emax)
+        ctx.meta = (sym, steps, ch_axis, x.dtype)
+        return y.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, grad):
+        x, mask, x_quant, delta, offset, emin, emax = ctx.saved_tensors
+        sym, steps, ch_axis, dtype = ctx.meta
+        g = grad.float()
+        grad_x = (mask * g).to(dtype)
+        dims = list(range(x.dim()))
+        if emin.numel() > 1:
+            dims.pop(ch_axis)
+        if sym:
+            gmax = ((x_quant + offset) * g).sum(dim=dims) - (mask * (x / delta) * g).sum(dim=dims)
+            gmax = gmax / torch.div(steps, 2, rounding_mode="floor")
+            return grad_x, (-gmax).view_as(emin), gmax.view_as(emax), None, None, None, None, None
+        grad_scale = (x_quant + offset - x * mask / delta) * g
+        grad_offset = (delta * g) * (~mask)
+        t1 = grad_scale.sum(dim=dims) / steps
+        t2 = steps / (emax - emin) ** 2 * grad_offset.sum(dim=dims)
+        return grad_x, (-t1 + emax * t2).view_as(emin), (t1 - emin * t2).view_as(emax), None, None, None, None, None
 
 
 class QatLinear(nn.Module):
@@ -126,6 +165,9 @@ def main():
         from aimet_amd.qc_quantize_op import LearnedGridQuantWrapper
         from aimet_amd.quantizers import QuantScheme
         from aimet_amd.quantsim import QuantizationSimModel
+        if args.impl == "reference":
+            import aimet_amd.learned_grid as LG
+            LG.LearnedGridQuantizeDequantize = RefQuantizeDequantize
         cfg = {"defaults": {"ops": {"is_output_quantized": "True"},
                             "params": {"is_quantized": "True", "is_symmetric": "True"},
                             "strict_symmetric": "False", "per_channel_quantization": "True"}}
@@ -186,7 +228,7 @@ def main():
             "metric": "Llama-3-8B W4A16 learned-grid QAT step (weight QDQ + STE elements / s)",
             "scheme": "training_range_learning_with_tf_init" if args.path == "quantsim" else "hand-built QAT linear",
             "value": round(2 * n_weights * world / (ms * 1e-3) / 1e9, 3), "unit": "Gelem/s", "n_gpus": world,
-            "path": args.path, "impl": "fused" if args.path == "quantsim" else args.impl,
+            "path": args.path, "impl": args.impl,
             "ms_per_step": round(ms, 2), "layers": args.layers, "seq_len": args.seq,
             "micro_batch": 1, "quantized_weight_elems": n_weights,
             "quantized_act_elems_per_step": n_act, "act_bw": args.act_bw if args.path == "quantsim" else None,
