@@ -21,27 +21,57 @@ from aimet_amd.libpymo import TfEncoding
 from aimet_amd.tensor_quantizer import IO_DTYPES, _stage, _stream, per_channel_view
 
 
-def get_computed_encodings(bitwidth, encoding_min, encoding_max, use_symmetric_encodings, use_strict_symmetric,
-                           is_unsigned_symmetric):
-    """quantsim_straight_through_grad.py:121-160 (torch ops on the C-element encoding vectors)."""
+_CONSTS = {}
+
+
+def _const(value: float, like: torch.Tensor) -> torch.Tensor:
+    """A cached 0-dim tensor holding `value` (no fill launch per call)."""
+    key = (value, like.dtype, like.device)
+    t = _CONSTS.get(key)
+    if t is None:
+        t = _CONSTS[key] = torch.full((), value, dtype=like.dtype, device=like.device)
+    return t
+
+
+def num_steps_of(bitwidth, use_symmetric_encodings, use_strict_symmetric) -> float:
+    """The quantisation grid's step count (host side: no device read-back per call)."""
     num_steps = 2 ** bitwidth - 1
     if use_symmetric_encodings and use_strict_symmetric:
         num_steps -= 1
+    return float(num_steps)
+
+
+def _delta_offset(bitwidth, encoding_min, encoding_max, use_symmetric_encodings, use_strict_symmetric,
+                  is_unsigned_symmetric):
+    """quantsim_straight_through_grad.py:121-160 with the reference's torch.full_like constant
+    tensors replaced by cached 0-dim device tensors of the same values: identical results (a
+    divisor stays a device tensor -- torch multiplies by the reciprocal of a host scalar divisor),
+    2-7 launches per call instead of 4-10 and no fill."""
+    num_steps = num_steps_of(bitwidth, use_symmetric_encodings, use_strict_symmetric)
     half_num_steps = num_steps / 2
-    num_steps_tensor = torch.full_like(encoding_min, num_steps)
     if use_symmetric_encodings and not is_unsigned_symmetric:
-        delta = encoding_max / torch.full_like(encoding_min, math.floor(half_num_steps))
-        offset = -torch.full_like(encoding_min, math.ceil(half_num_steps))
+        delta = encoding_max / _const(float(math.floor(half_num_steps)), encoding_max)
+        offset = torch.full_like(encoding_min, -float(math.ceil(half_num_steps)))
     else:
-        delta = (encoding_max - encoding_min) / num_steps_tensor
+        delta = (encoding_max - encoding_min) / _const(num_steps, encoding_min)
         if use_symmetric_encodings:
             offset = encoding_min / delta
         else:
-            zero = torch.full_like(encoding_min, 0.)
+            # torch.min(steps, torch.max(zero, b)) with cached 0-dim operands in the same argument
+            # order (the sign of a zero b_zero, hence of a zero offset, follows the reference)
             b_zero = torch.round(-encoding_min / delta)
-            b_zero = torch.min(num_steps_tensor, torch.max(zero, b_zero))
-            offset = -b_zero
-    return delta, offset, num_steps_tensor
+            b_zero = torch.minimum(_const(num_steps, b_zero), torch.maximum(_const(0.0, b_zero), b_zero))
+            offset = b_zero.neg_()
+    return delta, offset, num_steps
+
+
+def get_computed_encodings(bitwidth, encoding_min, encoding_max, use_symmetric_encodings, use_strict_symmetric,
+                           is_unsigned_symmetric):
+    """quantsim_straight_through_grad.py:121-160 (torch ops on the C-element encoding vectors):
+    (delta, offset, num_steps tensor)."""
+    delta, offset, num_steps = _delta_offset(bitwidth, encoding_min, encoding_max, use_symmetric_encodings,
+                                             use_strict_symmetric, is_unsigned_symmetric)
+    return delta, offset, torch.full_like(encoding_min, num_steps)
 
 
 def _channels(shape, ch_axis, per_channel):
@@ -72,8 +102,8 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x = x.contiguous()
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
-        delta, offset, steps = get_computed_encodings(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
-                                                      is_unsigned_symmetric)
+        delta, offset, steps = _delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
+                                             is_unsigned_symmetric)
         delta, offset = delta.contiguous(), offset.contiguous()
         outer, C, K = _channels(x.shape, ch_axis, emin.numel() > 1)
         if C != emin.numel():
@@ -81,9 +111,9 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         y = torch.empty_like(x)
         with torch.cuda.device(x.device):
             _native.call("aimet_lg_forward", x.data_ptr(), y.data_ptr(), outer, C, K, delta.data_ptr(),
-                         offset.data_ptr(), float(steps[0]), _stream(x))
+                         offset.data_ptr(), steps, _stream(x))
         ctx.save_for_backward(x, delta, offset, emin, emax)
-        ctx.cfg = (outer, C, K, float(steps[0]), use_symmetric, is_unsigned_symmetric, orig_dtype,
+        ctx.cfg = (outer, C, K, steps, use_symmetric, is_unsigned_symmetric, orig_dtype,
                    encoding_min.shape, encoding_max.shape, staged)
         return y.to(orig_dtype).cpu() if staged else y.to(orig_dtype)
 
@@ -95,15 +125,15 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x = tensor.contiguous()
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
-        delta, offset, steps = get_computed_encodings(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
-                                                      is_unsigned_symmetric)
+        delta, offset, steps = _delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
+                                             is_unsigned_symmetric)
         delta, offset = delta.contiguous(), offset.contiguous()
         y = torch.empty_like(x)
         with torch.cuda.device(x.device):
             _native.call("aimet_lg_forward_16", x.data_ptr(), y.data_ptr(), x.numel(), IO_DTYPES[x.dtype],
-                         delta.data_ptr(), offset.data_ptr(), float(steps[0]), _stream(x))
+                         delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
         ctx.save_for_backward(x, delta, offset, emin, emax)
-        ctx.cfg = (1, 1, x.numel(), float(steps[0]), use_symmetric, is_unsigned_symmetric, x.dtype,
+        ctx.cfg = (1, 1, x.numel(), steps, use_symmetric, is_unsigned_symmetric, x.dtype,
                    encoding_min.shape, encoding_max.shape, False)
         return y
 
@@ -128,13 +158,16 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
                              sums.data_ptr(), outer, C, K, delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
         A, B, D = sums[:, 0], sums[:, 1], sums[:, 2]
         grad_scale_sum = A - B
+        # divisors as device tensors, as the reference's num_steps tensor (a host scalar divisor
+        # would be applied as a multiplication by its reciprocal)
         if sym:
             # symmetric_gradients: (sum((xq+off)*g) - sum(mask*(x/delta)*g)) / floor(steps/2)
-            gmax = grad_scale_sum / math.floor(steps / 2)
+            gmax = grad_scale_sum / _const(float(math.floor(steps / 2)), grad_scale_sum)
             gmin = -gmax
         else:
-            term1 = grad_scale_sum / steps
-            term2 = steps / (emax - emin) ** 2 * (delta * D)
+            steps_t = _const(steps, grad_scale_sum)
+            term1 = grad_scale_sum / steps_t
+            term2 = steps_t / (emax - emin) ** 2 * (delta * D)
             gmin = -term1 + emax * term2
             gmax = term1 - emin * term2
         gx_out = gx.to(dtype) if gx is not None else None
@@ -151,7 +184,8 @@ def set_encoding_min_max_gating_threshold(encoding_min, encoding_max):
     with torch.no_grad():
         encoding_min.clamp_(max=0.0)
         encoding_max.clamp_(min=0.0)
-        encoding_max.copy_(torch.maximum(encoding_max, encoding_min + torch.full_like(encoding_min, 1e-5)))
+        # min + 1e-5 with the scalar rounded to float32, as the reference's full_like tensor
+        torch.maximum(encoding_max, encoding_min + 1e-5, out=encoding_max)
 
 
 class LearnedGridTensorQuantizer:

@@ -903,6 +903,27 @@ def test_recon_loss_backward_fused_vs_torch(act, shape):
     torch.testing.assert_close(qa.grad, qb.grad, rtol=2e-6, atol=1e-12)
 
 
+def test_learned_grid_encodings_equal_reference_torch_ops_on_device():
+    """learned_grid._delta_offset (cached 0-dim device constants, fewer launches) == the reference's
+    get_computed_encodings with its full_like tensors (oracle/torch_ref.lg_encodings), on the
+    device, bit for bit -- including NaN ranges and the sign of a zero offset."""
+    from aimet_amd.learned_grid import _delta_offset
+    from oracle import torch_ref as T
+    g = torch.Generator(device=DEV).manual_seed(31)
+    for bw in (2, 4, 8, 16):
+        for sym in (False, True):
+            for strict in (False, True):
+                for uns in (False, True):
+                    emin = torch.randn(4099, device=DEV, generator=g) * 3 - 1
+                    emax = emin.abs() + torch.rand(4099, device=DEV, generator=g) * 5
+                    emin[:4] = torch.tensor([float("nan"), 0.0, -0.0, float("inf")], device=DEV)
+                    emax[4:8] = torch.tensor([float("nan"), 0.0, 1e-30, -1.0], device=DEV)
+                    d_ref, o_ref, _ = T.lg_encodings(bw, emin, emax, sym, strict, uns)
+                    d, o, steps = _delta_offset(bw, emin, emax, sym, strict, uns)
+                    assert torch.equal(d.view(torch.int32), d_ref.view(torch.int32)), (bw, sym, strict, uns)
+                    assert torch.equal(o.view(torch.int32), o_ref.view(torch.int32)), (bw, sym, strict, uns)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("n", [4096 * 33 + 3, 1 << 22])
 @pytest.mark.parametrize("sym", [False, True])

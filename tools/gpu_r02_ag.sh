@@ -1,0 +1,5 @@
+#!/usr/bin/env bash
+source "$(dirname "$0")/gpu_lib.sh"
+run t_lg 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider -m gpu tests/test_gpu_parity.py tests/test_range_learning.py tests/test_configs_gpu.py -k "learned or range or lg or qat or config5"
+run llama 600 python -u benchmarks/llama_qat.py --path quantsim --layers 32 --steps 5 --warmup 2
+echo ALLDONE
