@@ -44,7 +44,12 @@ __device__ __forceinline__ float lg_qdq(float x, float d, float o, float steps)
     return (xq + o) * d;
 }
 
-__global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict__ x, float* __restrict__ y,
+typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
+
+// OUT = IO_F32: y float32. OUT = IO_F16 / IO_BF16: y written in 16 bits with torch's rounding --
+// the float32 result cast as autocast casts a weight for its matmul, fused into the store.
+template <int OUT>
+__global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict__ x, void* __restrict__ y,
                                                         uint32_t n, LgChannel map, const float* __restrict__ delta,
                                                         const float* __restrict__ offset, float steps, int vec)
 {
@@ -60,14 +65,37 @@ __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict_
         r.y = lg_qdq(v.y, d, o, steps);
         r.z = lg_qdq(v.z, d, o, steps);
         r.w = lg_qdq(v.w, d, o, steps);
-        __builtin_nontemporal_store(r, reinterpret_cast<f4*>(y) + t);
+        if constexpr (OUT == IO_F32)
+            __builtin_nontemporal_store(r, static_cast<f4*>(y) + t);
+        else
+        {
+            const u16x4 h = {from_f32<OUT>(r.x), from_f32<OUT>(r.y), from_f32<OUT>(r.z), from_f32<OUT>(r.w)};
+            __builtin_nontemporal_store(h, static_cast<u16x4*>(y) + t);
+        }
     }
     else
     {
         if (t >= n)
             return;
-        uint32_t c = map.channel(t);
-        y[t]       = lg_qdq(x[t], delta[c], offset[c], steps);
+        uint32_t c    = map.channel(t);
+        const float r = lg_qdq(x[t], delta[c], offset[c], steps);
+        if constexpr (OUT == IO_F32)
+            static_cast<float*>(y)[t] = r;
+        else
+            static_cast<unsigned short*>(y)[t] = from_f32<OUT>(r);
+    }
+}
+
+// four gradient elements of quad i: float32, or 16-bit upcast (exact)
+template <int GIO>
+__device__ __forceinline__ f4 load_grad4(const void* __restrict__ g, uint32_t i)
+{
+    if constexpr (GIO == IO_F32)
+        return __builtin_nontemporal_load(static_cast<const f4*>(g) + i);
+    else
+    {
+        const u16x4 h = __builtin_nontemporal_load(static_cast<const u16x4*>(g) + i);
+        return f4 {to_f32<GIO>(h.x), to_f32<GIO>(h.y), to_f32<GIO>(h.z), to_f32<GIO>(h.w)};
     }
 }
 
@@ -315,8 +343,8 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
 // like the streaming QDQ kernels (the (channel, slice) grid above streams from as many places as
 // there are channels in flight). Per-workgroup sums go to partial[b][3]; lg_bwd_tile_fold adds them
 // per channel in a fixed order (deterministic).
-template <int U>
-__global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restrict__ x, const f4* __restrict__ g,
+template <int U, int GIO>
+__global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restrict__ x, const void* __restrict__ g,
                                                              f4* __restrict__ gx, FastDiv divK4, FastDiv divC,
                                                              uint32_t C, const float* __restrict__ delta,
                                                              const float* __restrict__ offset, float steps,
@@ -331,7 +359,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restric
     for (int u = 0; u < U; ++u)
     {
         a[u] = __builtin_nontemporal_load(x + q0 + u * kBlock + threadIdx.x);
-        b[u] = __builtin_nontemporal_load(g + q0 + u * kBlock + threadIdx.x);
+        b[u] = load_grad4<GIO>(g, q0 + u * kBlock + threadIdx.x);
     }
     Sums s {0, 0, 0};
 #pragma unroll
@@ -383,7 +411,6 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restri
 // arithmetic and the element -> lane -> workgroup order of the backward's sums are those of
 // lg_bwd_tensor_kernel (quads, then the tail), and the downcast is torch's (io16.hpp). 4 B/elem
 // forward and 6 B/elem backward instead of 20 and 24 for the three-pass chains.
-typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 
 template <int IO>
 __global__ __launch_bounds__(kBlock) void lg_fwd16_kernel(const unsigned short* __restrict__ x,
@@ -456,6 +483,22 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
     }
 }
 
+template <int GIO>
+void launch_bwd_tile(int U, int64_t wg, const f4* x, const void* g, f4* gx, FastDiv dk, FastDiv dc, int64_t C,
+                     const float* delta, const float* offset, float steps, float* partial, hipStream_t s)
+{
+    if (U == 4)
+        lg_bwd_tile_kernel<4, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
+                                                                    steps, partial);
+    else if (U == 2)
+        lg_bwd_tile_kernel<2, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
+                                                                    steps, partial);
+    else
+        lg_bwd_tile_kernel<1, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
+                                                                    steps, partial);
+    AIMET_LAUNCH_CHECK();
+}
+
 }   // namespace
 }   // namespace aimet_amd
 
@@ -480,8 +523,37 @@ int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t
         bool vec     = (C == 1 || K % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0
                        && n % 4 == 0;
         int64_t work = vec ? n / 4 : n;
-        lg_fwd_kernel<<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
+        lg_fwd_kernel<IO_F32><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
             x, y, (uint32_t) n, map, delta, offset, num_steps, vec ? 1 : 0);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype,
+                          const float* delta, const float* offset, float num_steps, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(out_dtype == IO_F16 || out_dtype == IO_BF16, "out_dtype must be 1 (float16) or 2 (bfloat16)");
+        AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
+        int64_t n = outer * C * K;
+        if (n == 0)
+            return;
+        AIMET_REQUIRE(n < (int64_t(1) << 31), "learned-grid QDQ needs < 2^31 elements per call");
+        require_device_ptr(x, "x");
+        require_device_ptr(y, "y");
+        require_device_ptr(delta, "delta");
+        require_device_ptr(offset, "offset");
+        LgChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
+        bool vec = (C == 1 || K % 4 == 0) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(y) & 7) == 0 && n % 4 == 0;
+        int64_t work = vec ? n / 4 : n;
+        const unsigned grid = (unsigned) ceil_div(work, kBlock);
+        if (out_dtype == IO_F16)
+            lg_fwd_kernel<IO_F16><<<grid, kBlock, 0, as_stream(stream)>>>(x, y, (uint32_t) n, map, delta, offset,
+                                                                          num_steps, vec ? 1 : 0);
+        else
+            lg_fwd_kernel<IO_BF16><<<grid, kBlock, 0, as_stream(stream)>>>(x, y, (uint32_t) n, map, delta, offset,
+                                                                           num_steps, vec ? 1 : 0);
         AIMET_LAUNCH_CHECK();
     });
 }
@@ -532,16 +604,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             auto gv = reinterpret_cast<const f4*>(grad);
             auto ov = reinterpret_cast<f4*>(grad_x);
             FastDiv dk((uint32_t) K4), dc((uint32_t) C);
-            if (U == 4)
-                lg_bwd_tile_kernel<4><<<(unsigned) wg, kBlock, 0, s>>>(xv, gv, ov, dk, dc, (uint32_t) C, delta, offset,
-                                                                       num_steps, partial);
-            else if (U == 2)
-                lg_bwd_tile_kernel<2><<<(unsigned) wg, kBlock, 0, s>>>(xv, gv, ov, dk, dc, (uint32_t) C, delta, offset,
-                                                                       num_steps, partial);
-            else
-                lg_bwd_tile_kernel<1><<<(unsigned) wg, kBlock, 0, s>>>(xv, gv, ov, dk, dc, (uint32_t) C, delta, offset,
-                                                                       num_steps, partial);
-            AIMET_LAUNCH_CHECK();
+            launch_bwd_tile<IO_F32>(U, wg, xv, gv, ov, dk, dc, C, delta, offset, num_steps, partial, s);
             lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
                 partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)));
             AIMET_LAUNCH_CHECK();
@@ -612,6 +675,58 @@ int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const f
                 xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0);
         AIMET_LAUNCH_CHECK();
     });
+}
+
+int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, float* sums, int64_t outer, int64_t C,
+                             int64_t K, int grad_dtype, const float* delta, const float* offset, float num_steps,
+                             void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(grad_dtype == IO_F16 || grad_dtype == IO_BF16, "grad_dtype must be 1 (float16) or 2 (bfloat16)");
+        AIMET_REQUIRE(outer >= 0 && C > 1 && K >= 0, "invalid shape (per-channel tensors only)");
+        const int64_t n = outer * C * K;
+        require_device_ptr(sums, "sums");
+        hipStream_t s = as_stream(stream);
+        if (n == 0)
+        {
+            AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3 * C, s));
+            return;
+        }
+        AIMET_REQUIRE(aimet_lg_backward_grad16_supported(outer, C, K, x, grad, grad_x),
+                      "16-bit gradient backward: rows must be multiples of 1024 elements, 16-B / 8-B aligned");
+        require_device_ptr(x, "x");
+        require_device_ptr(grad, "grad");
+        if (grad_x)
+            require_device_ptr(grad_x, "grad_x");
+        require_device_ptr(delta, "delta");
+        require_device_ptr(offset, "offset");
+        // the tile path of aimet_lg_backward with the gradient upcast in registers (exact): the same
+        // arithmetic and summation order as aimet_lg_backward on grad.to(float32)
+        const int64_t K4 = K / 4;
+        const int U      = K4 % (kBlock * 4) == 0 ? 4 : K4 % (kBlock * 2) == 0 ? 2 : 1;
+        const int64_t wg = n / 4 / (kBlock * U);
+        float* partial   = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * wg, s));
+        FastDiv dk((uint32_t) K4), dc((uint32_t) C);
+        auto xv = reinterpret_cast<const f4*>(x);
+        auto ov = reinterpret_cast<f4*>(grad_x);
+        if (grad_dtype == IO_F16)
+            launch_bwd_tile<IO_F16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, partial, s);
+        else
+            launch_bwd_tile<IO_BF16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, partial, s);
+        lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
+            partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)));
+        AIMET_LAUNCH_CHECK();
+        scratch_free(partial, s);
+    });
+}
+
+int aimet_lg_backward_grad16_supported(int64_t outer, int64_t C, int64_t K, const void* x, const void* grad,
+                                       const void* grad_x)
+{
+    const int64_t n = outer * C * K;
+    return C > 1 && K % 1024 == 0 && n > 0 && n < (int64_t(1) << 31) && C < 65536 &&
+           ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0 &&
+           (reinterpret_cast<uintptr_t>(grad) & 7) == 0;
 }
 
 int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* sums, int64_t n, int io_dtype,

@@ -85,14 +85,24 @@ def _channels(shape, ch_axis, per_channel):
 
 class LearnedGridQuantizeDequantize(torch.autograd.Function):
     """apply(tensor, encoding_min, encoding_max, bitwidth, use_symmetric, use_strict_symmetric,
-    is_unsigned_symmetric, ch_axis)."""
+    is_unsigned_symmetric, ch_axis, out_dtype=None).
+
+    out_dtype (fp16 / bf16, float32 per-channel tensors only): return the result already cast to
+    it -- for a weight that autocast would cast anyway for its matmul (LearnedGridQuantWrapper
+    passes it for a Linear's weight under autocast); the cast happens in the kernel's store and
+    the 16-bit gradient is upcast in the backward kernel's loads. Results == the float32 op
+    followed by .to(out_dtype), gradients == the float32 op's on grad.to(float32)."""
 
     @staticmethod
     def forward(ctx, tensor, encoding_min, encoding_max, bitwidth, use_symmetric=False, use_strict_symmetric=False,
-                is_unsigned_symmetric=False, ch_axis=0):
+                is_unsigned_symmetric=False, ch_axis=0, out_dtype=None):
         if bitwidth >= 32:
             raise RuntimeError("Invalid bitwidth: %d" % bitwidth)
         orig_dtype = tensor.dtype
+        if out_dtype in IO_DTYPES and orig_dtype == torch.float32 and tensor.is_cuda and encoding_min.numel() > 1:
+            return LearnedGridQuantizeDequantize._forward_cast(ctx, tensor, encoding_min, encoding_max, bitwidth,
+                                                               use_symmetric, use_strict_symmetric,
+                                                               is_unsigned_symmetric, ch_axis, out_dtype)
         if tensor.is_cuda and orig_dtype in IO_DTYPES and encoding_min.numel() == 1:
             return LearnedGridQuantizeDequantize._forward_16(ctx, tensor, encoding_min, encoding_max, bitwidth,
                                                              use_symmetric, use_strict_symmetric,
@@ -116,6 +126,28 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         ctx.cfg = (outer, C, K, steps, use_symmetric, is_unsigned_symmetric, orig_dtype,
                    encoding_min.shape, encoding_max.shape, staged)
         return y.to(orig_dtype).cpu() if staged else y.to(orig_dtype)
+
+    @staticmethod
+    def _forward_cast(ctx, tensor, encoding_min, encoding_max, bitwidth, use_symmetric, use_strict_symmetric,
+                      is_unsigned_symmetric, ch_axis, out_dtype):
+        """float32 per-channel tensor, 16-bit result (aimet_lg_forward_cast). Saves the float32 input."""
+        x = tensor.contiguous()
+        emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
+        emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
+        delta, offset, steps = _delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
+                                             is_unsigned_symmetric)
+        delta, offset = delta.contiguous(), offset.contiguous()
+        outer, C, K = _channels(x.shape, ch_axis, True)
+        if C != emin.numel():
+            raise ValueError("encoding has %d channels, tensor has %d along axis %d" % (emin.numel(), C, ch_axis))
+        y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+        with torch.cuda.device(x.device):
+            _native.call("aimet_lg_forward_cast", x.data_ptr(), y.data_ptr(), outer, C, K, IO_DTYPES[out_dtype],
+                         delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
+        ctx.save_for_backward(x, delta, offset, emin, emax)
+        ctx.cfg = (outer, C, K, steps, use_symmetric, is_unsigned_symmetric, torch.float32,
+                   encoding_min.shape, encoding_max.shape, False)
+        return y
 
     @staticmethod
     def _forward_16(ctx, tensor, encoding_min, encoding_max, bitwidth, use_symmetric, use_strict_symmetric,
@@ -142,7 +174,17 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x, delta, offset, emin, emax = ctx.saved_tensors
         outer, C, K, steps, sym, unsigned, dtype, min_shape, max_shape, staged = ctx.cfg
         sums = torch.empty((C, 3), dtype=torch.float32, device=x.device)
-        if x.dtype in IO_DTYPES and grad.dtype == x.dtype and grad.is_cuda:
+        g16 = grad.contiguous() if (x.dtype == torch.float32 and grad.dtype in IO_DTYPES and grad.is_cuda
+                                    and C > 1) else None
+        gx = torch.empty_like(x) if (g16 is not None and ctx.needs_input_grad[0]) else None
+        if g16 is not None and _native.load().aimet_lg_backward_grad16_supported(
+                outer, C, K, x.data_ptr(), g16.data_ptr(), gx.data_ptr() if gx is not None else None):
+            # the 16-bit weight gradient of a cast-fused forward, upcast in the kernel's loads
+            with torch.cuda.device(x.device):
+                _native.call("aimet_lg_backward_grad16", x.data_ptr(), g16.data_ptr(),
+                             gx.data_ptr() if gx is not None else None, sums.data_ptr(), outer, C, K,
+                             IO_DTYPES[g16.dtype], delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
+        elif x.dtype in IO_DTYPES and grad.dtype == x.dtype and grad.is_cuda:
             g = grad.contiguous()
             gx = torch.empty_like(g) if ctx.needs_input_grad[0] else None
             with torch.cuda.device(x.device):
@@ -175,7 +217,7 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         if staged:
             gx_out = gx_out.cpu() if gx_out is not None else None
             gmin, gmax = gmin.cpu(), gmax.cpu()
-        return gx_out, gmin, gmax, None, None, None, None, None
+        return gx_out, gmin, gmax, None, None, None, None, None, None
 
 
 def set_encoding_min_max_gating_threshold(encoding_min, encoding_max):
@@ -356,8 +398,9 @@ class LearnedGridTensorQuantizer:
     def reset_encoding_stats(self):
         """Range-learning quantizers hold no statistics."""
 
-    def quantize_dequantize(self, tensor, encoding_min, encoding_max):
-        """v1/tensor_quantizer.py:760-773 over the fused forward / backward kernels."""
+    def quantize_dequantize(self, tensor, encoding_min, encoding_max, out_dtype=None):
+        """v1/tensor_quantizer.py:760-773 over the fused forward / backward kernels (out_dtype: see
+        LearnedGridQuantizeDequantize)."""
         if not self.enabled or self.bitwidth == 32:
             return tensor
         if encoding_min is None or encoding_max is None:
@@ -365,7 +408,7 @@ class LearnedGridTensorQuantizer:
                                "training")
         return LearnedGridQuantizeDequantize.apply(tensor, encoding_min, encoding_max, self.bitwidth,
                                                    self.use_symmetric_encodings, self.use_strict_symmetric,
-                                                   self.is_unsigned_symmetric, self._ch_axis)
+                                                   self.is_unsigned_symmetric, self._ch_axis, out_dtype)
 
 
 def initialize_learned_grid_quantizer_attributes(new_quantizer, old_quantizer):

@@ -466,6 +466,11 @@ def _patched_params(module: nn.Module, patches: Dict[str, torch.Tensor]):
                 module.__dict__[name] = original
 
 
+# fuse autocast's 16-bit cast of a quantized Linear weight into the learned-grid kernels (tests
+# switch it off to compare with the unfused chain)
+_FUSE_AUTOCAST_CAST = True
+
+
 class LearnedGridQuantWrapper(QcQuantizeWrapper):
     """v1/qc_quantize_op.py:947-1198: range learning. Every enabled quantizer's range is a pair
     of trainable parameters on the wrapper (``input0_encoding_min``, ``weight_encoding_max``, ...);
@@ -522,13 +527,21 @@ class LearnedGridQuantWrapper(QcQuantizeWrapper):
         return output[0] if len(output) == 1 else output
 
     def _quantize_params(self):
-        """v1/qc_quantize_op.py:1100-1127."""
+        """v1/qc_quantize_op.py:1100-1127. A Linear's weight under CUDA autocast at 16 bits is
+        returned already in that dtype (the cast autocast applies for the matmul, fused into the
+        quantizer's kernels: see LearnedGridQuantizeDequantize)."""
         patches = {}
+        cast = None
+        if isinstance(self._module_to_wrap, torch.nn.Linear) and torch.is_autocast_enabled("cuda"):
+            dt = torch.get_autocast_dtype("cuda")
+            cast = dt if dt in (torch.float16, torch.bfloat16) else None
         for name, param in self.get_named_parameters():
             q = self.param_quantizers[name]
             if q.enabled:
                 emin, emax = self._ranges(q)
-                patches[name] = q.quantize_dequantize(param, emin, emax)
+                out_dtype = cast if (name == "weight" and _FUSE_AUTOCAST_CAST and param.is_cuda) else None
+                patches[name] = q.quantize_dequantize(param, emin, emax, out_dtype) if out_dtype else \
+                    q.quantize_dequantize(param, emin, emax)
         return _patched_params(self._module_to_wrap, patches)
 
     def _quantize_activation(self, tensors_to_quantize, tensor_quantizers):

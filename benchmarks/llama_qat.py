@@ -123,7 +123,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--impl", choices=["fused", "reference"], default="fused")
-    ap.add_argument("--path", choices=["quantsim", "module"], default="quantsim")
+    ap.add_argument("--path", choices=["quantsim", "module", "plain"], default="quantsim",
+                    help="plain: the same model and step without any quantizer (the floor QAT adds to)")
     ap.add_argument("--act-bw", type=int, default=16)
     args = ap.parse_args()
 
@@ -141,8 +142,8 @@ def main():
 
     QatLinear.impl = args.impl
     torch.manual_seed(0)
-    linear_type = nn.Linear if args.path == "quantsim" else QatLinear
-    linear_cls = (lambda i, o: nn.Linear(i, o, bias=False)) if args.path == "quantsim" else QatLinear
+    linear_type = QatLinear if args.path == "module" else nn.Linear
+    linear_cls = QatLinear if args.path == "module" else (lambda i, o: nn.Linear(i, o, bias=False))
     with torch.device(dev):
         model = Llama(linear_cls, layers=args.layers)
     qlin = [m for m in model.modules() if isinstance(m, linear_type)]
@@ -226,7 +227,8 @@ def main():
         ms = dt / args.steps * 1e3
         print(json.dumps({
             "metric": "Llama-3-8B W4A16 learned-grid QAT step (weight QDQ + STE elements / s)",
-            "scheme": "training_range_learning_with_tf_init" if args.path == "quantsim" else "hand-built QAT linear",
+            "scheme": {"quantsim": "training_range_learning_with_tf_init", "module": "hand-built QAT linear",
+                       "plain": "no quantization (floor)"}[args.path],
             "value": round(2 * n_weights * world / (ms * 1e-3) / 1e9, 3), "unit": "Gelem/s", "n_gpus": world,
             "path": args.path, "impl": args.impl,
             "ms_per_step": round(ms, 2), "layers": args.layers, "seq_len": args.seq,

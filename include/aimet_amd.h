@@ -330,6 +330,19 @@ int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const f
                         const float* offset_dev, float num_steps, void* stream);
 int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* sums_dev, int64_t n, int io_dtype,
                          const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
+/* A float32 weight consumed in 16 bits (a Linear under autocast): the forward writes the
+ * quantize-dequantized weight cast to fp16 / bf16 in the same pass (== aimet_lg_forward then
+ * .to(dtype), as autocast casts it for the matmul); the backward takes the matmul's 16-bit weight
+ * gradient and upcasts it in registers (== aimet_lg_backward on grad.to(float32): same arithmetic,
+ * same summation order; per-channel rows of a multiple of 1024 elements, see _supported). 6 B and
+ * 10 B per element instead of 8 + 6 and 12 + 6 with the separate casts. */
+int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype,
+                          const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
+int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, float* sums_dev, int64_t outer,
+                             int64_t C, int64_t K, int grad_dtype, const float* delta_dev, const float* offset_dev,
+                             float num_steps, void* stream);
+int aimet_lg_backward_grad16_supported(int64_t outer, int64_t C, int64_t K, const void* x, const void* grad,
+                                       const void* grad_x);
 
 /* ------------------------------------------------------------------------------------------ */
 /* AdaRound soft rounding (v1/adaround/adaround_wrapper.py:124-149, adaround_loss.py:83-133)     */

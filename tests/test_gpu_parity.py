@@ -903,6 +903,77 @@ def test_recon_loss_backward_fused_vs_torch(act, shape):
     torch.testing.assert_close(qa.grad, qb.grad, rtol=2e-6, atol=1e-12)
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("sym", [True, False])
+def test_learned_grid_cast_fused_weight_equals_cast_after(dtype, sym):
+    """out_dtype: aimet_lg_forward_cast == the float32 op then .to(dtype); aimet_lg_backward_grad16
+    on the 16-bit gradient == the float32 backward on grad.to(float32) -- y, grad_x and both range
+    gradients bit for bit (per-channel [C, K] weights with K a multiple of 1024)."""
+    from aimet_amd.learned_grid import LearnedGridQuantizeDequantize as LG
+    g = torch.Generator(device=DEV).manual_seed(41 + int(sym))
+    C, K = 96, 4096
+    w = torch.randn(C, K, device=DEV, generator=g) * 0.02
+    amax = w.abs().amax(dim=1) * 0.8
+    gy = torch.randn(C, K, device=DEV, generator=g).to(dtype)
+    outs = []
+    for fused in (True, False):
+        x = w.clone().requires_grad_(True)
+        emin = (-amax if sym else w.amin(dim=1) * 0.9).clone().requires_grad_(True)
+        emax = amax.clone().requires_grad_(True)
+        if fused:
+            y = LG.apply(x, emin, emax, 4, sym, False, False, 0, dtype)
+            assert y.dtype == dtype
+            y.backward(gy)
+        else:
+            y = LG.apply(x, emin, emax, 4, sym, False, False, 0).to(dtype)
+            y.backward(gy)
+        outs.append((y.detach(), x.grad, emin.grad, emax.grad))
+    (y_a, gx_a, gn_a, gm_a), (y_b, gx_b, gn_b, gm_b) = outs
+    assert torch.equal(y_a.view(torch.int16), y_b.view(torch.int16))
+    assert torch.equal(gx_a.view(torch.int32), gx_b.view(torch.int32))
+    assert torch.equal(gn_a.view(torch.int32), gn_b.view(torch.int32))
+    assert torch.equal(gm_a.view(torch.int32), gm_b.view(torch.int32))
+
+
+def test_learned_grid_wrapper_autocast_cast_fusion_is_exact(monkeypatch):
+    """LearnedGridQuantWrapper around a Linear under bf16 autocast: with the weight's cast fused
+    into the quantizer kernels and without it, the forward output and every gradient (input,
+    weight, both ranges of the weight and output quantizers) are bit-identical."""
+    from aimet_amd import qc_quantize_op as Q
+    from aimet_amd.quantizers import QuantScheme
+    from aimet_amd.quantsim import QuantizationSimModel
+    torch.manual_seed(5)
+    cfg = {"defaults": {"ops": {"is_output_quantized": "True"},
+                        "params": {"is_quantized": "True", "is_symmetric": "True"},
+                        "strict_symmetric": "False", "per_channel_quantization": "True"}}
+    x = torch.randn(8, 64, 2048, device=DEV)
+    results = []
+    for fuse in (True, False):
+        monkeypatch.setattr(Q, "_FUSE_AUTOCAST_CAST", fuse)
+        torch.manual_seed(5)
+        model = torch.nn.Sequential(torch.nn.Linear(2048, 512, bias=False)).to(DEV)
+        sim = QuantizationSimModel(model, quant_scheme=QuantScheme.training_range_learning_with_tf_init,
+                                   default_param_bw=4, default_output_bw=16, config_file=cfg,
+                                   dummy_input=x[:1])
+
+        def cal(m, _):
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                m(x)
+        sim.compute_encodings(cal, None)
+        xin = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = sim.model(xin)
+        out.float().square().mean().backward()
+        grads = {n: p.grad.clone() for n, p in sim.model.named_parameters() if p.grad is not None}
+        results.append((out.detach(), xin.grad.clone(), grads))
+    (o_a, gx_a, g_a), (o_b, gx_b, g_b) = results
+    assert o_a.dtype == o_b.dtype and torch.equal(o_a, o_b)
+    assert torch.equal(gx_a, gx_b)
+    assert g_a.keys() == g_b.keys() and len(g_a) >= 3
+    for k in g_a:
+        assert torch.equal(g_a[k], g_b[k]), k
+
+
 def test_learned_grid_encodings_equal_reference_torch_ops_on_device():
     """learned_grid._delta_offset (cached 0-dim device constants, fewer launches) == the reference's
     get_computed_encodings with its full_like tensors (oracle/torch_ref.lg_encodings), on the
