@@ -13,6 +13,7 @@
 // symmetric:  grad_max = (A - B) / floor(steps/2), grad_min = -grad_max
 // (assembled from the C-vectors on the torch side). Float32; torch.round = round-half-even.
 #include "common.hpp"
+#include <cmath>
 #include "io16.hpp"
 
 namespace aimet_amd
@@ -483,6 +484,89 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
     }
 }
 
+// ---- the small per-channel vectors around the passes, one launch each -----------------------
+// Each expression is the reference's torch op sequence on float32 C-vectors, element by element,
+// with torch's NaN rules (clamp keeps a NaN input, maximum / minimum return the NaN operand) and
+// no contraction: results are those of the torch ops, bit for bit (tests/test_gpu_parity.py).
+__device__ __forceinline__ float t_maximum(float a, float b)
+{
+    return a != a ? a : (b != b ? b : fmaxf(a, b));
+}
+__device__ __forceinline__ float t_minimum(float a, float b)
+{
+    return a != a ? a : (b != b ? b : fminf(a, b));
+}
+
+// set_encoding_min_max_gating_threshold (v1/tensor_quantizer.py:1347-1359), in place
+__global__ __launch_bounds__(kBlock) void lg_gate_kernel(float* __restrict__ emin, float* __restrict__ emax,
+                                                         uint32_t C)
+{
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= C)
+        return;
+    float mn = emin[c], mx = emax[c];
+    mn = mn != mn ? mn : fminf(mn, 0.0f);   // clamp_(max=0)
+    mx = mx != mx ? mx : fmaxf(mx, 0.0f);   // clamp_(min=0)
+    emin[c] = mn;
+    emax[c] = t_maximum(mx, mn + 1e-5f);
+}
+
+// get_computed_encodings (quantsim_straight_through_grad.py:121-160)
+__global__ __launch_bounds__(kBlock) void lg_encodings_kernel(const float* __restrict__ emin,
+                                                              const float* __restrict__ emax, uint32_t C,
+                                                              float steps, int mode, float half_floor,
+                                                              float neg_half_ceil, float* __restrict__ delta,
+                                                              float* __restrict__ offset)
+{
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= C)
+        return;
+    const float mn = emin[c], mx = emax[c];
+    float d, o;
+    if (mode == 0)   // symmetric, signed
+    {
+        d = mx / half_floor;
+        o = neg_half_ceil;
+    }
+    else
+    {
+        d = (mx - mn) / steps;
+        if (mode == 1)   // symmetric, unsigned
+            o = mn / d;
+        else             // asymmetric: -min(steps, max(0, round(-min / delta)))
+            o = -t_minimum(steps, t_maximum(0.0f, __builtin_rintf(-mn / d)));
+    }
+    delta[c]  = d;
+    offset[c] = o;
+}
+
+// the encoding gradients from the backward's sums {A, B, D} (asymmetric / symmetric_gradients)
+__global__ __launch_bounds__(kBlock) void lg_range_grads_kernel(const float* __restrict__ sums,
+                                                                const float* __restrict__ emin,
+                                                                const float* __restrict__ emax,
+                                                                const float* __restrict__ delta, uint32_t C,
+                                                                float steps, int sym, float half_floor,
+                                                                float* __restrict__ gmin, float* __restrict__ gmax)
+{
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= C)
+        return;
+    const float gss = sums[3 * c] - sums[3 * c + 1];
+    if (sym)
+    {
+        const float g = gss / half_floor;
+        gmax[c]       = g;
+        gmin[c]       = -g;
+        return;
+    }
+    const float mn = emin[c], mx = emax[c];
+    const float term1 = gss / steps;
+    const float r     = mx - mn;
+    const float term2 = (steps / (r * r)) * (delta[c] * sums[3 * c + 2]);
+    gmin[c]           = -term1 + mx * term2;
+    gmax[c]           = term1 - mn * term2;
+}
+
 template <int GIO>
 void launch_bwd_tile(int U, int64_t wg, const f4* x, const void* g, f4* gx, FastDiv dk, FastDiv dc, int64_t C,
                      const float* delta, const float* offset, float steps, float* partial, hipStream_t s)
@@ -673,6 +757,51 @@ int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const f
         else
             lg_fwd16_kernel<IO_BF16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
                 xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_lg_gate_range(float* emin, float* emax, int64_t C, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(C >= 0 && C < (int64_t(1) << 31), "invalid channel count");
+        if (C == 0)
+            return;
+        lg_gate_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, as_stream(stream)>>>(emin, emax, (uint32_t) C);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_lg_encodings(const float* emin, const float* emax, int64_t C, int bw, int sym, int strict, int unsign,
+                       float* delta, float* offset, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(C >= 0 && C < (int64_t(1) << 31), "invalid channel count");
+        AIMET_REQUIRE(bw > 0 && bw < 32, "invalid bitwidth");
+        if (C == 0)
+            return;
+        double steps = std::ldexp(1.0, bw) - 1;
+        if (sym && strict)
+            steps -= 1;
+        const double half = steps / 2;
+        const int mode    = (sym && !unsign) ? 0 : (sym ? 1 : 2);
+        lg_encodings_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, as_stream(stream)>>>(
+            emin, emax, (uint32_t) C, (float) steps, mode, (float) std::floor(half), (float) -std::ceil(half), delta,
+            offset);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_lg_range_grads(const float* sums, const float* emin, const float* emax, const float* delta, int64_t C,
+                         float num_steps, int sym, float* grad_min, float* grad_max, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(C >= 0 && C < (int64_t(1) << 31), "invalid channel count");
+        if (C == 0)
+            return;
+        lg_range_grads_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, as_stream(stream)>>>(
+            sums, emin, emax, delta, (uint32_t) C, num_steps, sym, (float) std::floor(num_steps / 2.0), grad_min,
+            grad_max);
         AIMET_LAUNCH_CHECK();
     });
 }

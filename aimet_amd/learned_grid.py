@@ -74,6 +74,17 @@ def get_computed_encodings(bitwidth, encoding_min, encoding_max, use_symmetric_e
     return delta, offset, torch.full_like(encoding_min, num_steps)
 
 
+def _device_delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric, is_unsigned_symmetric):
+    """_delta_offset in ONE launch (aimet_lg_encodings, the same float32 expressions element by
+    element) for contiguous float32 device vectors."""
+    delta = torch.empty_like(emin)
+    offset = torch.empty_like(emin)
+    _native.call("aimet_lg_encodings", emin.data_ptr(), emax.data_ptr(), emin.numel(), int(bitwidth),
+                 int(bool(use_symmetric)), int(bool(use_strict_symmetric)), int(bool(is_unsigned_symmetric)),
+                 delta.data_ptr(), offset.data_ptr(), _stream(emin))
+    return delta, offset, num_steps_of(bitwidth, use_symmetric, use_strict_symmetric)
+
+
 def _channels(shape, ch_axis, per_channel):
     if not per_channel:
         n = 1
@@ -112,8 +123,9 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x = x.contiguous()
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
-        delta, offset, steps = _delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
-                                             is_unsigned_symmetric)
+        with torch.cuda.device(x.device):
+            delta, offset, steps = _device_delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
+                                                        is_unsigned_symmetric)
         delta, offset = delta.contiguous(), offset.contiguous()
         outer, C, K = _channels(x.shape, ch_axis, emin.numel() > 1)
         if C != emin.numel():
@@ -134,8 +146,9 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x = tensor.contiguous()
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
-        delta, offset, steps = _delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
-                                             is_unsigned_symmetric)
+        with torch.cuda.device(x.device):
+            delta, offset, steps = _device_delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
+                                                        is_unsigned_symmetric)
         delta, offset = delta.contiguous(), offset.contiguous()
         outer, C, K = _channels(x.shape, ch_axis, True)
         if C != emin.numel():
@@ -157,8 +170,9 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x = tensor.contiguous()
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
-        delta, offset, steps = _delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
-                                             is_unsigned_symmetric)
+        with torch.cuda.device(x.device):
+            delta, offset, steps = _device_delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
+                                                        is_unsigned_symmetric)
         delta, offset = delta.contiguous(), offset.contiguous()
         y = torch.empty_like(x)
         with torch.cuda.device(x.device):
@@ -198,20 +212,14 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
             with torch.cuda.device(x.device):
                 _native.call("aimet_lg_backward", x.data_ptr(), g.data_ptr(), gx.data_ptr() if gx is not None else None,
                              sums.data_ptr(), outer, C, K, delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
-        A, B, D = sums[:, 0], sums[:, 1], sums[:, 2]
-        grad_scale_sum = A - B
-        # divisors as device tensors, as the reference's num_steps tensor (a host scalar divisor
-        # would be applied as a multiplication by its reciprocal)
-        if sym:
-            # symmetric_gradients: (sum((xq+off)*g) - sum(mask*(x/delta)*g)) / floor(steps/2)
-            gmax = grad_scale_sum / _const(float(math.floor(steps / 2)), grad_scale_sum)
-            gmin = -gmax
-        else:
-            steps_t = _const(steps, grad_scale_sum)
-            term1 = grad_scale_sum / steps_t
-            term2 = steps_t / (emax - emin) ** 2 * (delta * D)
-            gmin = -term1 + emax * term2
-            gmax = term1 - emin * term2
+        # symmetric_gradients: gmax = (A - B) / floor(steps/2), gmin = -gmax; asymmetric_gradients:
+        # term1 = (A - B) / steps, term2 = steps / (max - min)^2 * (delta * D), gmin = -term1 + max *
+        # term2, gmax = term1 - min * term2 -- the torch expressions, one launch (aimet_lg_range_grads)
+        gmin = torch.empty_like(emin)
+        gmax = torch.empty_like(emax)
+        with torch.cuda.device(x.device):
+            _native.call("aimet_lg_range_grads", sums.data_ptr(), emin.data_ptr(), emax.data_ptr(), delta.data_ptr(),
+                         C, steps, int(bool(sym)), gmin.data_ptr(), gmax.data_ptr(), _stream(x))
         gx_out = gx.to(dtype) if gx is not None else None
         gmin, gmax = gmin.view(min_shape), gmax.view(max_shape)
         if staged:
@@ -223,6 +231,17 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
 def set_encoding_min_max_gating_threshold(encoding_min, encoding_max):
     """v1/tensor_quantizer.py:1347-1359: keep a trainable range ordered and around zero
     (min <= 0 <= max, max >= min + 1e-5), in place."""
+    if (encoding_min.is_cuda and encoding_max.is_cuda and encoding_min.dtype == torch.float32
+            and encoding_max.dtype == torch.float32 and encoding_min.is_contiguous() and encoding_max.is_contiguous()
+            and encoding_min.numel() == encoding_max.numel()):
+        # one launch, the same expressions element by element (aimet_lg_gate_range)
+        with torch.cuda.device(encoding_min.device):
+            _native.call("aimet_lg_gate_range", encoding_min.data_ptr(), encoding_max.data_ptr(),
+                         encoding_min.numel(), _stream(encoding_min))
+        # an in-place update, as the reference's clamp_ / copy_: bump the autograd version counters
+        torch.autograd.graph.increment_version(encoding_min)
+        torch.autograd.graph.increment_version(encoding_max)
+        return
     with torch.no_grad():
         encoding_min.clamp_(max=0.0)
         encoding_max.clamp_(min=0.0)

@@ -336,6 +336,18 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
  * gradient and upcasts it in registers (== aimet_lg_backward on grad.to(float32): same arithmetic,
  * same summation order; per-channel rows of a multiple of 1024 elements, see _supported). 6 B and
  * 10 B per element instead of 8 + 6 and 12 + 6 with the separate casts. */
+/* The per-channel vectors around the learned-grid passes, one launch each, results equal to the
+ * reference's torch ops bit for bit: _gate_range = set_encoding_min_max_gating_threshold
+ * (v1/tensor_quantizer.py:1347-1359) in place; _encodings = get_computed_encodings
+ * (quantsim_straight_through_grad.py:121-160) -> delta[C], offset[C]; _range_grads = the encoding
+ * gradients of asymmetric_gradients / symmetric_gradients (:252-328) from aimet_lg_backward's sums. */
+int aimet_lg_gate_range(float* emin_dev, float* emax_dev, int64_t C, void* stream);
+int aimet_lg_encodings(const float* emin_dev, const float* emax_dev, int64_t C, int bitwidth, int use_symmetric,
+                       int use_strict_symmetric, int is_unsigned_symmetric, float* delta_dev, float* offset_dev,
+                       void* stream);
+int aimet_lg_range_grads(const float* sums_dev, const float* emin_dev, const float* emax_dev, const float* delta_dev,
+                         int64_t C, float num_steps, int use_symmetric, float* grad_min_dev, float* grad_max_dev,
+                         void* stream);
 int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype,
                           const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
 int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, float* sums_dev, int64_t outer,

@@ -974,11 +974,62 @@ def test_learned_grid_wrapper_autocast_cast_fusion_is_exact(monkeypatch):
         assert torch.equal(g_a[k], g_b[k]), k
 
 
+def _same_bits_or_nan(a, b):
+    """Bit-equal float32 tensors, except that a NaN only has to be a NaN (its sign and payload
+    follow the instruction sequence that produced it, not the arithmetic)."""
+    na, nb = torch.isnan(a), torch.isnan(b)
+    return torch.equal(na, nb) and torch.equal(a.view(torch.int32)[~na], b.view(torch.int32)[~nb])
+
+
+def test_learned_grid_gate_and_range_grads_equal_torch_ops_on_device():
+    """aimet_lg_gate_range == the reference's clamp_ / clamp_ / maximum(max, min + 1e-5) and
+    aimet_lg_range_grads == asymmetric_gradients / symmetric_gradients' torch expressions on the
+    sums, on the device, bit for bit (NaN and signed-zero ranges included)."""
+    from aimet_amd import _native
+    from aimet_amd.learned_grid import set_encoding_min_max_gating_threshold
+    g = torch.Generator(device=DEV).manual_seed(43)
+    n = 5000
+    mn = torch.randn(n, device=DEV, generator=g)
+    mx = torch.randn(n, device=DEV, generator=g)
+    mn[:6] = torch.tensor([float("nan"), 0.0, -0.0, 1e-30, -1e-6, 3.0], device=DEV)
+    mx[6:12] = torch.tensor([float("nan"), 0.0, -0.0, -1e-30, 2e-6, -3.0], device=DEV)
+    a, b = mn.clone(), mx.clone()
+    with torch.no_grad():
+        a.clamp_(max=0.0)
+        b.clamp_(min=0.0)
+        b.copy_(torch.maximum(b, a + torch.full_like(a, 1e-5)))
+    c, d = mn.clone(), mx.clone()
+    set_encoding_min_max_gating_threshold(c, d)
+    assert _same_bits_or_nan(c, a)
+    assert _same_bits_or_nan(d, b)
+    # range gradients from random sums, both flavours
+    from aimet_amd.learned_grid import _delta_offset
+    emin, emax = -(torch.rand(n, device=DEV, generator=g) + 0.1), torch.rand(n, device=DEV, generator=g) + 0.1
+    sums = torch.randn(n, 3, device=DEV, generator=g) * 100
+    for bw, sym in ((4, True), (8, False), (16, False), (8, True)):
+        delta, _, steps = _delta_offset(bw, emin, emax, sym, False, False)
+        st = torch.full_like(emin, steps)
+        A, B, D = sums[:, 0], sums[:, 1], sums[:, 2]
+        gss = A - B
+        if sym:
+            want_max = gss / torch.div(st, 2, rounding_mode="floor")
+            want_min = -want_max
+        else:
+            term1 = gss / st
+            term2 = st / (emax - emin) ** 2 * (delta * D)
+            want_min, want_max = -term1 + emax * term2, term1 - emin * term2
+        gmin, gmax = torch.empty_like(emin), torch.empty_like(emax)
+        _native.call("aimet_lg_range_grads", sums.data_ptr(), emin.data_ptr(), emax.data_ptr(), delta.data_ptr(), n,
+                     steps, int(sym), gmin.data_ptr(), gmax.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        assert torch.equal(gmin.view(torch.int32), want_min.view(torch.int32)), (bw, sym)
+        assert torch.equal(gmax.view(torch.int32), want_max.view(torch.int32)), (bw, sym)
+
+
 def test_learned_grid_encodings_equal_reference_torch_ops_on_device():
     """learned_grid._delta_offset (cached 0-dim device constants, fewer launches) == the reference's
     get_computed_encodings with its full_like tensors (oracle/torch_ref.lg_encodings), on the
-    device, bit for bit -- including NaN ranges and the sign of a zero offset."""
-    from aimet_amd.learned_grid import _delta_offset
+    device, bit for bit -- including the sign of a zero offset; a NaN range gives NaN."""
+    from aimet_amd.learned_grid import _delta_offset, _device_delta_offset
     from oracle import torch_ref as T
     g = torch.Generator(device=DEV).manual_seed(31)
     for bw in (2, 4, 8, 16):
@@ -990,9 +1041,10 @@ def test_learned_grid_encodings_equal_reference_torch_ops_on_device():
                     emin[:4] = torch.tensor([float("nan"), 0.0, -0.0, float("inf")], device=DEV)
                     emax[4:8] = torch.tensor([float("nan"), 0.0, 1e-30, -1.0], device=DEV)
                     d_ref, o_ref, _ = T.lg_encodings(bw, emin, emax, sym, strict, uns)
-                    d, o, steps = _delta_offset(bw, emin, emax, sym, strict, uns)
-                    assert torch.equal(d.view(torch.int32), d_ref.view(torch.int32)), (bw, sym, strict, uns)
-                    assert torch.equal(o.view(torch.int32), o_ref.view(torch.int32)), (bw, sym, strict, uns)
+                    for fn in (_delta_offset, _device_delta_offset):
+                        d, o, steps = fn(bw, emin, emax, sym, strict, uns)
+                        assert _same_bits_or_nan(d, d_ref), (fn, bw, sym, strict, uns)
+                        assert _same_bits_or_nan(o, o_ref), (fn, bw, sym, strict, uns)
 
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
