@@ -516,6 +516,7 @@ std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* 
         j.hist  = q->hist ? 1 : 0;
         j.ent   = q->kind == kKindEntropy ? 1 : 0;
         j.vec   = (reinterpret_cast<uintptr_t>(j.x) & 15) == 0 ? 1 : 0;
+        j.seen  = q->stats_updated ? 1 : 0;
     }
     return jobs;
 }

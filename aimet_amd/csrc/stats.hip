@@ -632,25 +632,24 @@ __device__ __forceinline__ int find_job(const StatsJob* __restrict__ jobs, int n
                 : find_job_ballot(jobs, njobs, b, [](const StatsJob& j) { return j.mm_block0; });
 }
 
-// One 16-KiB tile per workgroup (4 x 16-B nontemporal loads per lane), tiles of every quantizer
-// in address order, one {-min, max} partial per tile. Against grid-stride workgroups over each
-// tensor this streams at 6.7 vs 5.9 TB/s on ResNet-50's activations (tools/read_ceiling.py): the
-// workgroups resident at any moment read one contiguous window of HBM.
+// One 16-KiB tile per step (4 x 16-B nontemporal loads per lane), the tiles of every quantizer in
+// address order, one {-min, max} partial per tile: the workgroups in flight read one contiguous
+// window of HBM (6.7 vs 5.9 TB/s for grid-stride workgroups inside each tensor,
+// tools/read_ceiling.py). A first batch runs one workgroup per tile (1.64 ms on ResNet-50's
+// activations); later batches of PDF schemes, where every quantizer's range is fixed, run
+// kMmGrid workgroups that walk the tiles and skip each quantizer at once (ViT-L/16 calibration:
+// 900 -> 1016 Gelem/s; profiles/r02/compute_encodings_study.txt).
 constexpr int64_t kMmTile = (int64_t) kBlock * 16;   // elements per tile
+constexpr int kMmGrid     = 2048;                    // 256 CUs x 8 workgroups of 256 lanes
 typedef const __attribute__((address_space(1))) f4* gf4p;
 
-__global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
+__device__ __forceinline__ float2 minmax_tile(const float* __restrict__ x, int64_t n, int vec, int64_t tile,
+                                              bool last_tile)
 {
-    const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, false)];
-    if (J.hist && !J.ent && J.d.pdf_init[0])
-        return;   // PDF schemes take min/max on the first (non-zero) batch only
-    const int64_t tile = blockIdx.x - J.mm_block0;
-    const int64_t n    = J.n;
     float mn = INFINITY, mx = -INFINITY;
-    int64_t tail0 = 0;
-    if (J.vec)
+    if (vec)
     {
-        gf4p x4            = (gf4p) J.x;
+        gf4p x4            = (gf4p) x;
         const int64_t nvec = n / 4;
         const int64_t base = tile * (kMmTile / 4) + threadIdx.x;
         f4 v[4];
@@ -661,12 +660,11 @@ __global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __r
 #pragma unroll
         for (int u = 0; u < 4; ++u)
             accum4(make_float4(v[u].x, v[u].y, v[u].z, v[u].w), mn, mx);
-        tail0 = nvec * 4;   // the last tile also takes the < 4 trailing elements
-        if (tile == (int64_t) J.mm_blocks - 1)
-            for (int64_t i = tail0 + threadIdx.x; i < n; i += kBlock)
+        if (last_tile)   // the last tile also takes the < 4 trailing elements
+            for (int64_t i = nvec * 4 + threadIdx.x; i < n; i += kBlock)
             {
-                mn = fminf(mn, J.x[i]);
-                mx = fmaxf(mx, J.x[i]);
+                mn = fminf(mn, x[i]);
+                mx = fmaxf(mx, x[i]);
             }
     }
     else
@@ -674,13 +672,71 @@ __global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __r
         const int64_t end = (tile + 1) * kMmTile < n ? (tile + 1) * kMmTile : n;
         for (int64_t i = tile * kMmTile + threadIdx.x; i < end; i += kBlock)
         {
-            mn = fminf(mn, J.x[i]);
-            mx = fmaxf(mx, J.x[i]);
+            mn = fminf(mn, x[i]);
+            mx = fmaxf(mx, x[i]);
         }
     }
-    block_minmax(mn, mx);
+    block_minmax(mn, mx);   // ends with the result in thread 0 (and an LDS barrier inside)
+    return make_float2(-mn, mx);
+}
+
+// one tile per workgroup (the first batch: every tile is read)
+__global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
+{
+    const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, false)];
+    if (J.hist && !J.ent && J.d.pdf_init[0])
+        return;   // PDF schemes take min/max on the first (non-zero) batch only
+    const int64_t tile = blockIdx.x - J.mm_block0;
+    const float2 r     = minmax_tile(J.x, J.n, J.vec, tile, tile + 1 == (int64_t) J.mm_blocks);
     if (threadIdx.x == 0)
-        reinterpret_cast<float2*>(J.mm_part)[tile] = make_float2(-mn, mx);
+        reinterpret_cast<float2*>(J.mm_part)[tile] = r;
+}
+
+// kMmGrid workgroups walking the tiles (later batches of PDF schemes, whose quantizers all skip
+// unless a range is still unset: a skip per quantizer instead of a workgroup per tile)
+__global__ __launch_bounds__(kBlock) void minmax_walk_kernel(const StatsJob* __restrict__ jobs, int njobs,
+                                                             uint32_t tiles)
+{
+    uint32_t t = blockIdx.x;
+    if (t >= tiles)
+        return;
+    int ji = find_job(jobs, njobs, t, false);
+    // the current quantizer's fields live in registers; tiles only grow, so the quantizer index
+    // only steps forward and a tile costs no table load
+    const float* x = nullptr;
+    int64_t n = 0;
+    float2* part = nullptr;
+    uint32_t b0 = 0, next_b0 = 0;
+    int vec = 0;
+    bool skip = false;
+    auto enter = [&](int j) {
+        const StatsJob& J = jobs[j];
+        x       = J.x;
+        n       = J.n;
+        vec     = J.vec;
+        part    = reinterpret_cast<float2*>(J.mm_part);
+        b0      = J.mm_block0;
+        next_b0 = j + 1 < njobs ? jobs[j + 1].mm_block0 : tiles;
+        // PDF schemes take min/max on the first (non-zero) batch only
+        skip = J.hist && !J.ent && J.d.pdf_init[0];
+    };
+    enter(ji);
+    while (t < tiles)
+    {
+        while (t >= next_b0)
+            enter(++ji);
+        if (skip)
+        {
+            t += (next_b0 - t + gridDim.x - 1) / gridDim.x * gridDim.x;
+            continue;
+        }
+        const int64_t tile = t - b0;
+        const float2 r     = minmax_tile(x, n, vec, tile, t + 1 == next_b0);
+        if (threadIdx.x == 0)
+            part[tile] = r;
+        __syncthreads();   // the block reduction's LDS is reused by the next tile
+        t += gridDim.x;
+    }
 }
 
 // one workgroup per quantizer: partials -> minmax[0] = {-min, max}; optionally the fold
@@ -1048,7 +1104,14 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
     auto* dj = static_cast<StatsJob*>(upload_async(jobs.data(), sizeof(StatsJob) * n, s));
     if (phases & kPhaseMinmax)
     {
-        minmax_many_kernel<<<(unsigned) mm, kBlock, 0, s>>>(dj, n);
+        // every quantizer a PDF scheme that has seen a batch: its range is (almost surely) fixed
+        bool walk = true;
+        for (const auto& j: jobs)
+            walk = walk && j.hist && !j.ent && j.seen;
+        if (walk)
+            minmax_walk_kernel<<<(unsigned) std::min<uint64_t>(mm, kMmGrid), kBlock, 0, s>>>(dj, n, (uint32_t) mm);
+        else
+            minmax_many_kernel<<<(unsigned) mm, kBlock, 0, s>>>(dj, n);
         AIMET_LAUNCH_CHECK();
         combine_many_kernel<<<n, kBlock, 0, s>>>(dj, (phases & kPhaseFoldMinmax) ? 1 : 0);
         AIMET_LAUNCH_CHECK();

@@ -82,6 +82,7 @@ struct StatsJob
     float* mm_part;  // [mm_blocks][2] per-tile {-min, max} (launch_stats_many's scratch)
     int32_t hist, vec;
     int32_t ent;     // entropy analyzer (hist == 1 too): min/max every batch, TensorProfilingParams
+    int32_t seen;    // the quantizer has seen a batch since its reset (host flag; a schedule hint only)
 };
 enum StatsPhase
 {
