@@ -175,21 +175,32 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
     Sums s {0, 0, 0};
     if (vec)
     {
-        const int64_t nv = n / 4;
-        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t) gridDim.x * kBlock)
+        // eight elements (two quads) per lane and step, then the < 8 trailing ones: the order of
+        // lg_bwd16_tensor_kernel, so the 16-bit path sums exactly what this one sums
+        const int64_t no = n / 8;
+        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < no; i += (int64_t) gridDim.x * kBlock)
         {
-            f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + i);
-            f4 b = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + i);
-            float r0, r1, r2, r3;
-            lg_bwd_elem(a.x, b.x, dl, o, steps, rcp, r0, s);
-            lg_bwd_elem(a.y, b.y, dl, o, steps, rcp, r1, s);
-            lg_bwd_elem(a.z, b.z, dl, o, steps, rcp, r2, s);
-            lg_bwd_elem(a.w, b.w, dl, o, steps, rcp, r3, s);
-            f4 r = {r0, r1, r2, r3};
+            const f4 a0 = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + 2 * i);
+            const f4 a1 = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + 2 * i + 1);
+            const f4 b0 = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + 2 * i);
+            const f4 b1 = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + 2 * i + 1);
+            float r[8];
+            lg_bwd_elem(a0.x, b0.x, dl, o, steps, rcp, r[0], s);
+            lg_bwd_elem(a0.y, b0.y, dl, o, steps, rcp, r[1], s);
+            lg_bwd_elem(a0.z, b0.z, dl, o, steps, rcp, r[2], s);
+            lg_bwd_elem(a0.w, b0.w, dl, o, steps, rcp, r[3], s);
+            lg_bwd_elem(a1.x, b1.x, dl, o, steps, rcp, r[4], s);
+            lg_bwd_elem(a1.y, b1.y, dl, o, steps, rcp, r[5], s);
+            lg_bwd_elem(a1.z, b1.z, dl, o, steps, rcp, r[6], s);
+            lg_bwd_elem(a1.w, b1.w, dl, o, steps, rcp, r[7], s);
             if (gx)
-                __builtin_nontemporal_store(r, reinterpret_cast<f4*>(gx) + i);
+            {
+                const f4 r0 = {r[0], r[1], r[2], r[3]}, r1 = {r[4], r[5], r[6], r[7]};
+                __builtin_nontemporal_store(r0, reinterpret_cast<f4*>(gx) + 2 * i);
+                __builtin_nontemporal_store(r1, reinterpret_cast<f4*>(gx) + 2 * i + 1);
+            }
         }
-        for (int64_t i = nv * 4 + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
+        for (int64_t i = no * 8 + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
         {
             float r;
             lg_bwd_elem(x[i], g[i], dl, o, steps, rcp, r, s);
@@ -413,6 +424,9 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restri
 // lg_bwd_tensor_kernel (quads, then the tail), and the downcast is torch's (io16.hpp). 4 B/elem
 // forward and 6 B/elem backward instead of 20 and 24 for the three-pass chains.
 
+typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
+
+// vec: eight elements (one 16-B load) per lane; otherwise one element per lane
 template <int IO>
 __global__ __launch_bounds__(kBlock) void lg_fwd16_kernel(const unsigned short* __restrict__ x,
                                                           unsigned short* __restrict__ y, uint32_t n,
@@ -423,20 +437,21 @@ __global__ __launch_bounds__(kBlock) void lg_fwd16_kernel(const unsigned short* 
     const float d = delta[0], o = offset[0];
     if (vec)
     {
-        if (t >= n / 4)
+        if (t >= n / 8)
             return;
-        const u16x4 v = __builtin_nontemporal_load(reinterpret_cast<const u16x4*>(x) + t);
-        u16x4 r;
-        r.x = from_f32<IO>(lg_qdq(to_f32<IO>(v.x), d, o, steps));
-        r.y = from_f32<IO>(lg_qdq(to_f32<IO>(v.y), d, o, steps));
-        r.z = from_f32<IO>(lg_qdq(to_f32<IO>(v.z), d, o, steps));
-        r.w = from_f32<IO>(lg_qdq(to_f32<IO>(v.w), d, o, steps));
-        __builtin_nontemporal_store(r, reinterpret_cast<u16x4*>(y) + t);
+        const u16x8 v = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + t);
+        u16x8 r;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            r[k] = from_f32<IO>(lg_qdq(to_f32<IO>(v[k]), d, o, steps));
+        __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(y) + t);
     }
     else if (t < n)
         y[t] = from_f32<IO>(lg_qdq(to_f32<IO>(x[t]), d, o, steps));
 }
 
+// the element -> lane -> workgroup order of lg_bwd_tensor_kernel (eight per lane and step, then
+// the tail), so the sums equal the float32 kernel's on the upcast tensors
 template <int IO>
 __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned short* __restrict__ x,
                                                                  const unsigned short* __restrict__ g,
@@ -450,23 +465,25 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
     int64_t done = 0;
     if (vec)
     {
-        const int64_t nv = n / 4;
-        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < nv; i += (int64_t) gridDim.x * kBlock)
+        const int64_t no = n / 8;
+        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < no; i += (int64_t) gridDim.x * kBlock)
         {
-            const u16x4 a = __builtin_nontemporal_load(reinterpret_cast<const u16x4*>(x) + i);
-            const u16x4 b = __builtin_nontemporal_load(reinterpret_cast<const u16x4*>(g) + i);
-            float r0, r1, r2, r3;
-            lg_bwd_elem(to_f32<IO>(a.x), to_f32<IO>(b.x), dl, o, steps, rcp, r0, s);
-            lg_bwd_elem(to_f32<IO>(a.y), to_f32<IO>(b.y), dl, o, steps, rcp, r1, s);
-            lg_bwd_elem(to_f32<IO>(a.z), to_f32<IO>(b.z), dl, o, steps, rcp, r2, s);
-            lg_bwd_elem(to_f32<IO>(a.w), to_f32<IO>(b.w), dl, o, steps, rcp, r3, s);
+            const u16x8 a = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + i);
+            const u16x8 b = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(g) + i);
+            float r[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                lg_bwd_elem(to_f32<IO>(a[k]), to_f32<IO>(b[k]), dl, o, steps, rcp, r[k], s);
             if (gx)
             {
-                const u16x4 r = {from_f32<IO>(r0), from_f32<IO>(r1), from_f32<IO>(r2), from_f32<IO>(r3)};
-                __builtin_nontemporal_store(r, reinterpret_cast<u16x4*>(gx) + i);
+                u16x8 h;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    h[k] = from_f32<IO>(r[k]);
+                __builtin_nontemporal_store(h, reinterpret_cast<u16x8*>(gx) + i);
             }
         }
-        done = nv * 4;
+        done = no * 8;
     }
     for (int64_t i = done + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
     {
@@ -747,8 +764,8 @@ int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const f
         require_device_ptr(y, "y");
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
-        const bool vec = n % 4 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 7) == 0;
-        const int64_t work = vec ? n / 4 : n;
+        const bool vec = n % 8 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
+        const int64_t work = vec ? n / 8 : n;
         auto xs = static_cast<const unsigned short*>(x);
         auto ys = static_cast<unsigned short*>(y);
         if (io_dtype == IO_F16)
@@ -878,7 +895,7 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
-                           reinterpret_cast<uintptr_t>(grad_x)) & 7) == 0;
+                           reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
         const unsigned nb = stream_blocks(n, (int64_t) kBlock * 16);   // the fp32 kernel's grid
         float* partial    = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * nb, s));
         auto xs = static_cast<const unsigned short*>(x);

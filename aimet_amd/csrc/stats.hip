@@ -635,10 +635,10 @@ __device__ __forceinline__ int find_job(const StatsJob* __restrict__ jobs, int n
 // One 16-KiB tile per step (4 x 16-B nontemporal loads per lane), the tiles of every quantizer in
 // address order, one {-min, max} partial per tile: the workgroups in flight read one contiguous
 // window of HBM (6.7 vs 5.9 TB/s for grid-stride workgroups inside each tensor,
-// tools/read_ceiling.py). A first batch runs one workgroup per tile (1.64 ms on ResNet-50's
-// activations); later batches of PDF schemes, where every quantizer's range is fixed, run
-// kMmGrid workgroups that walk the tiles and skip each quantizer at once (ViT-L/16 calibration:
-// 900 -> 1016 Gelem/s; profiles/r02/compute_encodings_study.txt).
+// tools/read_ceiling.py). A first batch of <= 64 quantizers runs one workgroup per tile (1.64 ms
+// on ResNet-50's activations); later batches of PDF schemes, where every quantizer's range is
+// fixed, and larger tables run kMmGrid workgroups that walk the tiles and skip a fixed quantizer
+// at once (ViT-L/16 calibration: 900 -> 1016 Gelem/s; profiles/r02/compute_encodings_study.txt).
 constexpr int64_t kMmTile = (int64_t) kBlock * 16;   // elements per tile
 constexpr int kMmGrid     = 2048;                    // 256 CUs x 8 workgroups of 256 lanes
 typedef const __attribute__((address_space(1))) f4* gf4p;
@@ -1104,10 +1104,15 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
     auto* dj = static_cast<StatsJob*>(upload_async(jobs.data(), sizeof(StatsJob) * n, s));
     if (phases & kPhaseMinmax)
     {
-        // every quantizer a PDF scheme that has seen a batch: its range is (almost surely) fixed
-        bool walk = true;
+        // walk the tiles when every quantizer is a PDF scheme that has seen a batch (its range is
+        // almost surely fixed) or when the job table needs more than one ballot round per
+        // workgroup (> 64 quantizers: ViT-L/16's 318 read their first batch in 5.8 ms walking vs
+        // 7.1 ms one tile per workgroup)
+        bool walk = n > 64;
+        bool fixed = true;
         for (const auto& j: jobs)
-            walk = walk && j.hist && !j.ent && j.seen;
+            fixed = fixed && j.hist && !j.ent && j.seen;
+        walk = walk || fixed;
         if (walk)
             minmax_walk_kernel<<<(unsigned) std::min<uint64_t>(mm, kMmGrid), kBlock, 0, s>>>(dj, n, (uint32_t) mm);
         else
