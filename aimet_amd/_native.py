@@ -170,7 +170,8 @@ _PROTOTYPES = {
     "aimet_adaround_gather": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
     "aimet_adaround_recon_grad_indexed": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp],
     "aimet_adaround_backward_adam": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp,
-                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _vp],
+                                     ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _vp,
+                                     _vp],
 }
 _RESTYPES = {"aimet_last_error": ctypes.c_char_p, "aimet_version": ctypes.c_char_p}
 

@@ -94,6 +94,11 @@ def conv_backend(module: torch.nn.Module):
 _GEMM_LAYERS = os.environ.get("AIMET_ADA_GEMM_LAYERS", "1") != "0"
 
 
+# the Adam step writes the next soft-quantized weight (AIMET_ADA_FUSE_WQ=0: a forward launch per
+# iteration instead; measurements only)
+_FUSE_SOFT_WEIGHT = os.environ.get("AIMET_ADA_FUSE_WQ", "1") == "1"
+
+
 def _is_pointwise(module: torch.nn.Module) -> bool:
     return isinstance(module, torch.nn.Conv2d) and module.kernel_size == (1, 1) and module.stride == (1, 1) \
         and module.padding in ((0, 0), "valid") and module.dilation == (1, 1) and module.groups == 1
@@ -409,16 +414,25 @@ class AdaroundOptimizer:
             _native.check(lib.aimet_adaround_recon_grad_indexed(P(q), P(out_data), P(idx_all), it_cur, P(g_buf), nb,
                                                                 C_out, hw, pbias if with_bias else None, code, s))
 
+        fuse_wq = _FUSE_SOFT_WEIGHT
+
         def adam_step(gw, s):
+            # the Adam step also writes the next iteration's soft-quantized weight into wq (it reads
+            # W and the new alpha anyway): no separate forward launch per iteration
             _native.check(lib.aimet_adaround_backward_adam(sq.pw, sq.pa, P(gw), P(exp_avg), P(exp_avg_sq), *sq.shape,
                                                            sq.pd, sq.po, sq.bw, P(rb_all), it_next, it_cur, *adam,
-                                                           loss_ptr, s))
+                                                           loss_ptr, P(wq) if fuse_wq else None, s))
+
+        def soft_weight():   # wq from the current alpha (before the first iteration)
+            s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            _native.check(sq.fwd(sq.pw, sq.pa, P(wq), *sq.shape, sq.pd, sq.po, sq.bw, 1, s))
 
         def step():
             s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
             _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp), None if indexed else P(target),
                                                     P(idx_all), it_cur, it_next, nb, row_in, row_out, s))
-            _native.check(sq.fwd(sq.pw, sq.pa, P(wq), *sq.shape, sq.pd, sq.po, sq.bw, 1, s))
+            if not fuse_wq:
+                soft_weight()
             if mode == "dw":
                 _native.check(lib.aimet_dwconv2d_forward(P(inp), P(wq), pbias, P(q_buf), *dims, s))
                 recon(q_buf, False, s)
@@ -460,6 +474,7 @@ class AdaroundOptimizer:
                 counters.zero_()
                 if round_loss_out is not None:
                     round_loss_out.copy_(loss0)
+            soft_weight()
 
         def capture(m):
             nonlocal mode
@@ -468,6 +483,7 @@ class AdaroundOptimizer:
             side = torch.cuda.Stream(dev)
             side.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(side), torch.enable_grad():
+                soft_weight()
                 for _ in range(min(2, iters)):
                     step()
             torch.cuda.current_stream(dev).wait_stream(side)

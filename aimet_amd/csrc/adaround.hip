@@ -335,7 +335,8 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                                                                    const float* __restrict__ reg_beta_all,
                                                                    const int64_t* __restrict__ it_next,
                                                                    int64_t* __restrict__ it_cur, AdamArgs adam,
-                                                                   float* __restrict__ round_loss)
+                                                                   float* __restrict__ round_loss,
+                                                                   float* __restrict__ wq_next)
 {
     const int64_t step = it_next[0];
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -369,6 +370,10 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             reinterpret_cast<f4*>(alpha)[i]      = f4 {a[0], a[1], a[2], a[3]};
             reinterpret_cast<f4*>(exp_avg)[i]    = f4 {m[0], m[1], m[2], m[3]};
             reinterpret_cast<f4*>(exp_avg_sq)[i] = f4 {v[0], v[1], v[2], v[3]};
+            if (wq_next)   // the next iteration's soft-quantized weight from the updated alpha
+                __builtin_nontemporal_store(f4 {ada_fwd(ww[0], a[0], d, o, p, rcp), ada_fwd(ww[1], a[1], d, o, p, rcp),
+                                                ada_fwd(ww[2], a[2], d, o, p, rcp), ada_fwd(ww[3], a[3], d, o, p, rcp)},
+                                            reinterpret_cast<f4*>(wq_next) + i);
         }
     }
     else
@@ -377,8 +382,12 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
         {
             const uint32_t c = map.channel(i);
             const float d = delta[c], o = offset[c];
-            const float ga = ada_bwd(w[i], alpha[i], g[i], d, o, p, __builtin_amdgcn_rcpf(d), loss);
-            alpha[i]       = adam_elem(alpha[i], ga, exp_avg[i], exp_avg_sq[i], adam, bc1, bc2s);
+            const float rcp = __builtin_amdgcn_rcpf(d);
+            const float ga  = ada_bwd(w[i], alpha[i], g[i], d, o, p, rcp, loss);
+            const float an  = adam_elem(alpha[i], ga, exp_avg[i], exp_avg_sq[i], adam, bc1, bc2s);
+            alpha[i]        = an;
+            if (wq_next)
+                wq_next[i] = ada_fwd(w[i], an, d, o, p, rcp);
         }
     }
     if (p.reg != 0.0f && round_loss)
@@ -725,10 +734,13 @@ int aimet_adaround_recon_grad_indexed(const float* q, const float* out_data, con
 int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad_wq, float* exp_avg, float* exp_avg_sq,
                                  int64_t outer, int64_t C, int64_t K, const float* delta, const float* offset,
                                  int32_t bw, const float* reg_beta_all, const int64_t* it_next, int64_t* it_cur,
-                                 double lr, double beta1, double beta2, double eps, float* round_loss, void* stream)
+                                 double lr, double beta1, double beta2, double eps, float* round_loss, float* wq_next,
+                                 void* stream)
 {
     return guarded([&] {
         AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
+        if (wq_next)
+            require_device_ptr(wq_next, "wq_next");
         const int64_t n = outer * C * K;
         AIMET_REQUIRE(n > 0 && n < (int64_t(1) << 31), "AdaRound weight must have 1 .. 2^31-1 elements");
         require_device_ptr(w, "weight");
@@ -745,18 +757,19 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
         AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, 1};
         AdamArgs a {lr, beta1, beta2, eps};
         const bool vec = (C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) &&
-                         aligned16(grad_wq) && aligned16(exp_avg) && aligned16(exp_avg_sq);
+                         aligned16(grad_wq) && aligned16(exp_avg) && aligned16(exp_avg_sq) &&
+                         (wq_next == nullptr || aligned16(wq_next));
         const int64_t items = vec ? n / 4 : n;
         int64_t blocks      = ceil_div(items, kBlock);
         blocks              = blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid;
         if (vec)
             adaround_bwd_adam_kernel<true><<<(unsigned) blocks, kBlock, 0, as_stream(stream)>>>(
                 w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss);
+                it_cur, a, round_loss, wq_next);
         else
             adaround_bwd_adam_kernel<false><<<(unsigned) blocks, kBlock, 0, as_stream(stream)>>>(
                 w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss);
+                it_cur, a, round_loss, wq_next);
         AIMET_LAUNCH_CHECK();
     });
 }

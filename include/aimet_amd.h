@@ -409,12 +409,14 @@ int aimet_adaround_recon_grad_indexed(const float* quant_out, const float* out_d
  * {reg, beta, beta - 1} = reg_beta_all_dev[3 * (step - 1) ..] (float32), alpha / exp_avg /
  * exp_avg_sq (the Adam moments, zero-initialised by the caller) updated in place with ATen's
  * per-element arithmetic (bias corrections 1 - beta^step in double); it_cur_dev[0] = step;
- * the round loss accumulated into round_loss_dev[0] when non-null. */
+ * the round loss accumulated into round_loss_dev[0] when non-null; when wq_next_dev is non-null,
+ * the next iteration's soft-quantized weight (aimet_adaround_forward of the updated alpha, same
+ * arithmetic) is written there in the same pass. */
 int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad_wq, float* exp_avg_dev,
                                  float* exp_avg_sq_dev, int64_t outer, int64_t C, int64_t K, const float* delta_dev,
                                  const float* offset_dev, int32_t bw, const float* reg_beta_all_dev,
                                  const int64_t* it_next_dev, int64_t* it_cur_dev, double lr, double beta1,
-                                 double beta2, double eps, float* round_loss_dev, void* stream);
+                                 double beta2, double eps, float* round_loss_dev, float* wq_next_dev, void* stream);
 
 /* Depthwise 2-D convolution (groups == C, weights [C][1][K][K], K = 3 or 5, square stride /
  * padding / dilation, NCHW fp32): the AdaRound loop's layer math on depthwise layers
