@@ -413,8 +413,8 @@ __global__ __launch_bounds__(kBlock) void adaround_gather_kernel(const float* __
         it_next[0] = it + 1;
     const int b          = blockIdx.y >> 1;
     const bool out       = blockIdx.y & 1;
-    if (out && !dst_out)
-        return;   // the target is read in place (recon_grad_idx_kernel)
+    if (out ? !dst_out : !dst_in)
+        return;   // read in place (recon_grad_idx_kernel, the depthwise kernels' row map)
     const int64_t row    = out ? row_out : row_in;
     const int64_t r      = idx_all[it * nb + b];
     const float* src     = (out ? src_out : src_in) + r * row;
@@ -682,15 +682,17 @@ int aimet_adaround_gather(const float* src_in, const float* src_out, float* dst_
         AIMET_REQUIRE(nb > 0 && nb <= 32768 && row_in > 0 && row_out > 0, "invalid batch / row sizes");
         require_device_ptr(src_in, "src_in");
         require_device_ptr(src_out, "src_out");
-        require_device_ptr(dst_in, "dst_in");
-        if (dst_out)   // null: only the inputs are gathered
+        if (dst_in)    // null: the inputs are read in place (only the iteration counter moves)
+            require_device_ptr(dst_in, "dst_in");
+        if (dst_out)   // null: the targets are read in place
             require_device_ptr(dst_out, "dst_out");
         require_device_ptr(idx_all, "idx_all");
         require_device_ptr(it_cur, "it_cur");
         require_device_ptr(it_next, "it_next");
         const bool vec = row_in % 4 == 0 && row_out % 4 == 0 && aligned16(src_in) && aligned16(src_out) &&
                          aligned16(dst_in) && aligned16(dst_out);   // aligned16(nullptr) holds
-        const int64_t work = (row_in > row_out ? row_in : row_out) / (vec ? 4 : 1);
+        const int64_t rin  = dst_in ? row_in : 0, rout = dst_out ? row_out : 0;
+        const int64_t work = (rin > rout ? rin : rout) / (vec ? 4 : 1);
         int64_t bx         = ceil_div(work, kBlock * 4);   // >= 4 items per lane
         bx                 = bx < 1 ? 1 : (bx > 256 ? 256 : bx);
         dim3 grid((unsigned) bx, (unsigned) (2 * nb));
