@@ -1183,19 +1183,25 @@ void launch_reset_state_many(const std::vector<ResetJob>& jobs, hipStream_t s)
 }
 
 // blockIdx.y = job; the workgroups along x stride over the job's 16-B words, then its tail bytes
+// any byte range: the 16-B aligned middle with vector stores, the unaligned head (e.g. a
+// quantizer's {-min, max} inside a packed exchange buffer) and tail byte by byte
 __global__ __launch_bounds__(kBlock) void zero_many_kernel(const ZeroJob* __restrict__ jobs)
 {
     const ZeroJob J   = jobs[blockIdx.y];
-    const int64_t nq  = J.bytes / 16;
-    f4* q             = static_cast<f4*>(J.p);
+    unsigned char* b  = static_cast<unsigned char*>(J.p);
+    const int64_t mis = (int64_t) (reinterpret_cast<uintptr_t>(b) & 15);
+    const int64_t head = mis ? (16 - mis < J.bytes ? 16 - mis : J.bytes) : 0;
+    const int64_t nq  = (J.bytes - head) / 16;
+    f4* q             = reinterpret_cast<f4*>(b + head);
     const f4 z        = {0.f, 0.f, 0.f, 0.f};
     const int64_t str = (int64_t) gridDim.x * kBlock;
     for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < nq; i += str)
         q[i] = z;
     if (blockIdx.x == 0)
     {
-        unsigned char* b = static_cast<unsigned char*>(J.p);
-        for (int64_t i = nq * 16 + threadIdx.x; i < J.bytes; i += kBlock)
+        for (int64_t i = threadIdx.x; i < head; i += kBlock)
+            b[i] = 0;
+        for (int64_t i = head + nq * 16 + threadIdx.x; i < J.bytes; i += kBlock)
             b[i] = 0;
     }
 }
@@ -1207,10 +1213,7 @@ void launch_zero_many(const std::vector<ZeroJob>& jobs, hipStream_t s)
     AIMET_REQUIRE(jobs.size() < 65536, "too many ranges to zero in one launch");
     int64_t most = 0;
     for (const ZeroJob& j: jobs)
-    {
-        AIMET_REQUIRE((reinterpret_cast<uintptr_t>(j.p) & 15) == 0, "zero_many: ranges must be 16-B aligned");
         most = std::max(most, j.bytes);
-    }
     const int64_t bx = std::max<int64_t>(1, std::min<int64_t>(64, ceil_div(most / 16, (int64_t) kBlock * 8)));
     auto* dj         = static_cast<ZeroJob*>(upload_async(jobs.data(), sizeof(ZeroJob) * jobs.size(), s));
     zero_many_kernel<<<dim3((unsigned) bx, (unsigned) jobs.size()), kBlock, 0, s>>>(dj);

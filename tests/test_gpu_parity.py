@@ -1249,6 +1249,27 @@ def test_create_many_shared_state_lifetime():
     torch.cuda.synchronize()
 
 
+def test_reset_of_quantizers_bound_to_exchange_buffers():
+    """Quantizers whose {-min, max} and counts live in the packed exchange buffers of the sharded
+    path (aimet_amd.distributed, 8-B slots at any offset) reset in the batched reset and then
+    recompute exactly what fresh quantizers compute."""
+    from aimet_amd import distributed as D
+    g = torch.Generator(device=DEV).manual_seed(23)
+    TFE = QuantizationMode.QUANTIZATION_TF_ENHANCED
+    tensors = [torch.relu(torch.randn(n, device=DEV, generator=g) * (i + 1)) for i, n in
+               enumerate((1 << 16, 1001, 3 << 14, 77))]
+    qs = [AimetTensorQuantizer(TFE) for _ in tensors]
+    D.sharded_update_stats(qs, [t * 3 for t in tensors], fused=False)       # bound to packed buffers
+    AimetTensorQuantizer.resetEncodingStatsMany(qs)
+    D.sharded_update_stats(qs, tensors, fused=False)
+    got = [e.to_tuple() for e, _ in AimetTensorQuantizer.getEncodings(qs, 8, False, False, False)]
+    fresh = [AimetTensorQuantizer(TFE) for _ in tensors]
+    for q, t in zip(fresh, tensors):
+        q.updateStats(t, True)
+    want = [e.to_tuple() for e, _ in AimetTensorQuantizer.getEncodings(fresh, 8, False, False, False)]
+    assert got == want
+
+
 @pytest.mark.parametrize("schemes", ["tfe", "mixed"])
 def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatch):
     """compute_encodings_resident's one native call (aimet_calibrate_launch, reset folded in) ==
