@@ -905,13 +905,14 @@ def test_recon_loss_backward_fused_vs_torch(act, shape):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("sym", [True, False])
-def test_learned_grid_cast_fused_weight_equals_cast_after(dtype, sym):
+@pytest.mark.parametrize("K", [4096, 1000])
+def test_learned_grid_cast_fused_weight_equals_cast_after(dtype, sym, K):
     """out_dtype: aimet_lg_forward_cast == the float32 op then .to(dtype); aimet_lg_backward_grad16
     on the 16-bit gradient == the float32 backward on grad.to(float32) -- y, grad_x and both range
     gradients bit for bit (per-channel [C, K] weights with K a multiple of 1024)."""
     from aimet_amd.learned_grid import LearnedGridQuantizeDequantize as LG
     g = torch.Generator(device=DEV).manual_seed(41 + int(sym))
-    C, K = 96, 4096
+    C = 96   # K = 1000: rows not a multiple of 1024 -> the backward upcasts the gradient first
     w = torch.randn(C, K, device=DEV, generator=g) * 0.02
     amax = w.abs().amax(dim=1) * 0.8
     gy = torch.randn(C, K, device=DEV, generator=g).to(dtype)
