@@ -149,15 +149,16 @@ _PROTOTYPES = {
     "aimet_tq_num_channels": [_vp, ctypes.POINTER(_i64)],
     "aimet_tq_quant_scheme": [_vp, ctypes.POINTER(_int)],
     "aimet_lg_forward": [_vp, _vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_float, _vp],
-    "aimet_lg_backward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_float, _vp],
+    "aimet_lg_backward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, ctypes.c_float, _vp, _vp],
     "aimet_lg_gate_range": [_vp, _vp, _i64, _vp],
     "aimet_lg_encodings": [_vp, _vp, _i64, _int, _int, _int, _int, _vp, _vp, _vp],
     "aimet_lg_range_grads": [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, _int, _vp, _vp, _vp],
     "aimet_lg_forward_cast": [_vp, _vp, _i64, _i64, _i64, _int, _vp, _vp, ctypes.c_float, _vp],
-    "aimet_lg_backward_grad16": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _int, _vp, _vp, ctypes.c_float, _vp],
+    "aimet_lg_backward_grad16": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _int, _vp, _vp, ctypes.c_float, _vp,
+                                 _vp],
     "aimet_lg_backward_grad16_supported": [_i64, _i64, _i64, _vp, _vp, _vp],
     "aimet_lg_forward_16": [_vp, _vp, _i64, _int, _vp, _vp, ctypes.c_float, _vp],
-    "aimet_lg_backward_16": [_vp, _vp, _vp, _vp, _i64, _int, _vp, _vp, ctypes.c_float, _vp],
+    "aimet_lg_backward_16": [_vp, _vp, _vp, _vp, _i64, _int, _vp, _vp, ctypes.c_float, _vp, _vp],
     "aimet_adaround_forward": [_vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _int, _vp],
     "aimet_adaround_backward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, ctypes.c_double,
                                 ctypes.c_double, _vp, _vp],

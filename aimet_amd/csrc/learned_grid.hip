@@ -227,10 +227,42 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
     }
 }
 
+// the encoding gradients of channel c from its sums {A, B, D} (asymmetric / symmetric_gradients,
+// the reference's torch expressions element by element); gmin == nullptr: not requested
+struct LgRange
+{
+    const float* emin;
+    const float* emax;
+    const float* delta;
+    float* gmin;
+    float* gmax;
+    float steps, half_floor;
+    int sym;
+};
+
+__device__ __forceinline__ void range_grads_one(float A, float B, float D, uint32_t c, const LgRange& r)
+{
+    const float gss = A - B;
+    if (r.sym)
+    {
+        const float g = gss / r.half_floor;
+        r.gmax[c]     = g;
+        r.gmin[c]     = -g;
+        return;
+    }
+    const float mn = r.emin[c], mx = r.emax[c];
+    const float term1 = gss / r.steps;
+    const float w     = mx - mn;
+    const float term2 = (r.steps / (w * w)) * (r.delta[c] * D);
+    r.gmin[c]         = -term1 + mx * term2;
+    r.gmax[c]         = term1 - mn * term2;
+}
+
 // sums[0..2] = the nparts partial triples, lane i taking parts i, i + kBlock, ... in order, then
-// the fixed shuffle tree of block_reduce: one result whatever the scheduling
+// the fixed shuffle tree of block_reduce: one result whatever the scheduling; the range
+// gradients follow in the same launch when requested
 __global__ __launch_bounds__(kBlock) void lg_bwd_fold_one(const float* __restrict__ partial, int nparts,
-                                                          float* __restrict__ sums)
+                                                          float* __restrict__ sums, LgRange range)
 {
     Sums s {0, 0, 0};
     for (int i = threadIdx.x; i < nparts; i += kBlock)
@@ -245,6 +277,8 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_fold_one(const float* __restric
         sums[0] = t.a;
         sums[1] = t.b;
         sums[2] = t.d;
+        if (range.gmin)
+            range_grads_one(t.a, t.b, t.d, 0, range);
     }
 }
 
@@ -399,7 +433,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restric
 
 // sums[c] = sum over the rows r of channel c and their workgroups w (in that order)
 __global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restrict__ partial, float* __restrict__ sums,
-                                                           uint32_t outer, uint32_t C, uint32_t per_row)
+                                                           uint32_t outer, uint32_t C, uint32_t per_row, LgRange range)
 {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= C)
@@ -416,6 +450,8 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restri
     sums[3 * c + 0] = a;
     sums[3 * c + 1] = b;
     sums[3 * c + 2] = d;
+    if (range.gmin)
+        range_grads_one(a, b, d, c, range);
 }
 
 // ---- fp16 / bf16 I/O, per tensor (C == 1): the conversions in registers ------------------------
@@ -558,30 +594,33 @@ __global__ __launch_bounds__(kBlock) void lg_encodings_kernel(const float* __res
 }
 
 // the encoding gradients from the backward's sums {A, B, D} (asymmetric / symmetric_gradients)
-__global__ __launch_bounds__(kBlock) void lg_range_grads_kernel(const float* __restrict__ sums,
-                                                                const float* __restrict__ emin,
-                                                                const float* __restrict__ emax,
-                                                                const float* __restrict__ delta, uint32_t C,
-                                                                float steps, int sym, float half_floor,
-                                                                float* __restrict__ gmin, float* __restrict__ gmax)
+__global__ __launch_bounds__(kBlock) void lg_range_grads_kernel(const float* __restrict__ sums, uint32_t C,
+                                                                LgRange range)
 {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
-    if (c >= C)
+    if (c < C)
+        range_grads_one(sums[3 * c], sums[3 * c + 1], sums[3 * c + 2], c, range);
+}
+
+LgRange range_of(const aimet_lg_range_spec* spec, float steps)
+{
+    LgRange r {};
+    if (spec == nullptr)
+        return r;
+    AIMET_REQUIRE(spec->grad_min && spec->grad_max && spec->encoding_min && spec->encoding_max && spec->delta,
+                  "aimet_lg_range_spec: every pointer must be set");
+    r = LgRange {spec->encoding_min, spec->encoding_max, spec->delta, spec->grad_min, spec->grad_max, steps,
+                 (float) std::floor(steps / 2.0), spec->use_symmetric};
+    return r;
+}
+
+// the range gradients as their own launch (backward paths whose sums come without a fold)
+void launch_range_grads(const float* sums, int64_t C, const LgRange& r, hipStream_t s)
+{
+    if (r.gmin == nullptr || C == 0)
         return;
-    const float gss = sums[3 * c] - sums[3 * c + 1];
-    if (sym)
-    {
-        const float g = gss / half_floor;
-        gmax[c]       = g;
-        gmin[c]       = -g;
-        return;
-    }
-    const float mn = emin[c], mx = emax[c];
-    const float term1 = gss / steps;
-    const float r     = mx - mn;
-    const float term2 = (steps / (r * r)) * (delta[c] * sums[3 * c + 2]);
-    gmin[c]           = -term1 + mx * term2;
-    gmax[c]           = term1 - mn * term2;
+    lg_range_grads_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(sums, (uint32_t) C, r);
+    AIMET_LAUNCH_CHECK();
 }
 
 template <int GIO>
@@ -660,16 +699,19 @@ int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int
 }
 
 int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* sums, int64_t outer, int64_t C,
-                      int64_t K, const float* delta, const float* offset, float num_steps, void* stream)
+                      int64_t K, const float* delta, const float* offset, float num_steps,
+                      const aimet_lg_range_spec* range_spec, void* stream)
 {
     return guarded([&] {
         AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
         int64_t n = outer * C * K;
         require_device_ptr(sums, "sums");
         hipStream_t s = as_stream(stream);
+        const LgRange range = range_of(range_spec, num_steps);
         if (n == 0)
         {
             AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3 * C, s));
+            launch_range_grads(sums, C, range, s);
             return;
         }
         require_device_ptr(x, "x");
@@ -687,7 +729,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             lg_bwd_tensor_kernel<<<nb, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset, num_steps, partial,
                                                        vec ? 1 : 0);
             AIMET_LAUNCH_CHECK();
-            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) nb, sums);
+            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) nb, sums, range);
             AIMET_LAUNCH_CHECK();
             scratch_free(partial, s);
             return;
@@ -707,7 +749,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             FastDiv dk((uint32_t) K4), dc((uint32_t) C);
             launch_bwd_tile<IO_F32>(U, wg, xv, gv, ov, dk, dc, C, delta, offset, num_steps, partial, s);
             lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
-                partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)));
+                partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)), range);
             AIMET_LAUNCH_CHECK();
             scratch_free(partial, s);
             return;
@@ -732,7 +774,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             {
                 AIMET_LAUNCH_CHECK();
                 lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(partial, sums, 1u, (uint32_t) C,
-                                                                                   (uint32_t) splits);
+                                                                                   (uint32_t) splits, range);
                 AIMET_LAUNCH_CHECK();
                 scratch_free(partial, s);
                 return;
@@ -745,6 +787,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
                                                           sums);
         }
         AIMET_LAUNCH_CHECK();
+        launch_range_grads(sums, C, range, s);
     });
 }
 
@@ -814,20 +857,17 @@ int aimet_lg_range_grads(const float* sums, const float* emin, const float* emax
 {
     return guarded([&] {
         AIMET_REQUIRE(C >= 0 && C < (int64_t(1) << 31), "invalid channel count");
-        if (C == 0)
-            return;
-        lg_range_grads_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, as_stream(stream)>>>(
-            sums, emin, emax, delta, (uint32_t) C, num_steps, sym, (float) std::floor(num_steps / 2.0), grad_min,
-            grad_max);
-        AIMET_LAUNCH_CHECK();
+        const aimet_lg_range_spec spec {emin, emax, delta, grad_min, grad_max, sym};
+        launch_range_grads(sums, C, range_of(&spec, num_steps), as_stream(stream));
     });
 }
 
 int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, float* sums, int64_t outer, int64_t C,
                              int64_t K, int grad_dtype, const float* delta, const float* offset, float num_steps,
-                             void* stream)
+                             const aimet_lg_range_spec* range_spec, void* stream)
 {
     return guarded([&] {
+        const LgRange range = range_of(range_spec, num_steps);
         AIMET_REQUIRE(grad_dtype == IO_F16 || grad_dtype == IO_BF16, "grad_dtype must be 1 (float16) or 2 (bfloat16)");
         AIMET_REQUIRE(outer >= 0 && C > 1 && K >= 0, "invalid shape (per-channel tensors only)");
         const int64_t n = outer * C * K;
@@ -836,6 +876,7 @@ int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, fl
         if (n == 0)
         {
             AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3 * C, s));
+            launch_range_grads(sums, C, range, s);
             return;
         }
         AIMET_REQUIRE(aimet_lg_backward_grad16_supported(outer, C, K, x, grad, grad_x),
@@ -860,7 +901,7 @@ int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, fl
         else
             launch_bwd_tile<IO_BF16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, partial, s);
         lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
-            partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)));
+            partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)), range);
         AIMET_LAUNCH_CHECK();
         scratch_free(partial, s);
     });
@@ -876,9 +917,11 @@ int aimet_lg_backward_grad16_supported(int64_t outer, int64_t C, int64_t K, cons
 }
 
 int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* sums, int64_t n, int io_dtype,
-                         const float* delta, const float* offset, float num_steps, void* stream)
+                         const float* delta, const float* offset, float num_steps,
+                         const aimet_lg_range_spec* range_spec, void* stream)
 {
     return guarded([&] {
+        const LgRange range = range_of(range_spec, num_steps);
         AIMET_REQUIRE(io_dtype == IO_F16 || io_dtype == IO_BF16, "io_dtype must be 1 (float16) or 2 (bfloat16)");
         AIMET_REQUIRE(n >= 0, "invalid size");
         require_device_ptr(sums, "sums");
@@ -886,6 +929,7 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         if (n == 0)
         {
             AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3, s));
+            launch_range_grads(sums, 1, range, s);
             return;
         }
         require_device_ptr(x, "x");
@@ -908,7 +952,7 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
             lg_bwd16_tensor_kernel<IO_BF16><<<nb, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps, partial,
                                                                   vec ? 1 : 0);
         AIMET_LAUNCH_CHECK();
-        lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) nb, sums);
+        lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) nb, sums, range);
         AIMET_LAUNCH_CHECK();
         scratch_free(partial, s);
     });

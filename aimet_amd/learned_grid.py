@@ -12,6 +12,7 @@ kernels (aimet_lg_forward_16 / _backward_16: the casts in registers, results ide
 upcast -> fp32 -> downcast chain), other 16-bit cases are upcast. The reference keeps bf16/fp16
 arithmetic for bitwidth <= 8 -- a documented difference, results are then at least as accurate.
 """
+import ctypes
 import math
 
 import torch
@@ -19,6 +20,12 @@ import torch
 from aimet_amd import _native
 from aimet_amd.libpymo import TfEncoding
 from aimet_amd.tensor_quantizer import IO_DTYPES, _stage, _stream, per_channel_view
+
+
+class _RangeSpec(ctypes.Structure):
+    """aimet_lg_range_spec (include/aimet_amd.h)."""
+    _fields_ = [("encoding_min", ctypes.c_void_p), ("encoding_max", ctypes.c_void_p), ("delta", ctypes.c_void_p),
+                ("grad_min", ctypes.c_void_p), ("grad_max", ctypes.c_void_p), ("use_symmetric", ctypes.c_int)]
 
 
 _CONSTS = {}
@@ -188,6 +195,14 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x, delta, offset, emin, emax = ctx.saved_tensors
         outer, C, K, steps, sym, unsigned, dtype, min_shape, max_shape, staged = ctx.cfg
         sums = torch.empty((C, 3), dtype=torch.float32, device=x.device)
+        # symmetric_gradients: gmax = (A - B) / floor(steps/2), gmin = -gmax; asymmetric_gradients:
+        # term1 = (A - B) / steps, term2 = steps / (max - min)^2 * (delta * D), gmin = -term1 + max *
+        # term2, gmax = term1 - min * term2 -- the torch expressions, evaluated by the kernel that
+        # folds the sums (aimet_lg_range_spec)
+        gmin = torch.empty_like(emin)
+        gmax = torch.empty_like(emax)
+        spec = ctypes.byref(_RangeSpec(emin.data_ptr(), emax.data_ptr(), delta.data_ptr(), gmin.data_ptr(),
+                                       gmax.data_ptr(), int(bool(sym))))
         g16 = grad.contiguous() if (x.dtype == torch.float32 and grad.dtype in IO_DTYPES and grad.is_cuda
                                     and C > 1) else None
         gx = torch.empty_like(x) if (g16 is not None and ctx.needs_input_grad[0]) else None
@@ -197,29 +212,22 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
             with torch.cuda.device(x.device):
                 _native.call("aimet_lg_backward_grad16", x.data_ptr(), g16.data_ptr(),
                              gx.data_ptr() if gx is not None else None, sums.data_ptr(), outer, C, K,
-                             IO_DTYPES[g16.dtype], delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
+                             IO_DTYPES[g16.dtype], delta.data_ptr(), offset.data_ptr(), steps, spec, _stream(x))
         elif x.dtype in IO_DTYPES and grad.dtype == x.dtype and grad.is_cuda:
             g = grad.contiguous()
             gx = torch.empty_like(g) if ctx.needs_input_grad[0] else None
             with torch.cuda.device(x.device):
                 _native.call("aimet_lg_backward_16", x.data_ptr(), g.data_ptr(),
                              gx.data_ptr() if gx is not None else None, sums.data_ptr(), x.numel(), IO_DTYPES[x.dtype],
-                             delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
+                             delta.data_ptr(), offset.data_ptr(), steps, spec, _stream(x))
         else:
             x = x.to(torch.float32)   # a 16-bit input with a gradient of another dtype
             g = grad.to(x.device, torch.float32).contiguous()
             gx = torch.empty_like(g) if ctx.needs_input_grad[0] else None
             with torch.cuda.device(x.device):
                 _native.call("aimet_lg_backward", x.data_ptr(), g.data_ptr(), gx.data_ptr() if gx is not None else None,
-                             sums.data_ptr(), outer, C, K, delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
-        # symmetric_gradients: gmax = (A - B) / floor(steps/2), gmin = -gmax; asymmetric_gradients:
-        # term1 = (A - B) / steps, term2 = steps / (max - min)^2 * (delta * D), gmin = -term1 + max *
-        # term2, gmax = term1 - min * term2 -- the torch expressions, one launch (aimet_lg_range_grads)
-        gmin = torch.empty_like(emin)
-        gmax = torch.empty_like(emax)
-        with torch.cuda.device(x.device):
-            _native.call("aimet_lg_range_grads", sums.data_ptr(), emin.data_ptr(), emax.data_ptr(), delta.data_ptr(),
-                         C, steps, int(bool(sym)), gmin.data_ptr(), gmax.data_ptr(), _stream(x))
+                             sums.data_ptr(), outer, C, K, delta.data_ptr(), offset.data_ptr(), steps, spec,
+                             _stream(x))
         gx_out = gx.to(dtype) if gx is not None else None
         gmin, gmax = gmin.view(min_shape), gmax.view(max_shape)
         if staged:

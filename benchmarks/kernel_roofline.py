@@ -206,7 +206,7 @@ def main():
     t_ms = timed(lambda: T.lg_forward(xv, emin, emax, 8), 2, stream)
     row("learned_grid_forward", "a14", 8, ms, None, t_ms)
     ms = timed(lambda: (sums.zero_(), lib.aimet_lg_backward(P(x), P(grad), P(gx), P(sums), 1, C, K, P(delta),
-                                                              P(offset), ctypes.c_float(steps), sp)),
+                                                              P(offset), ctypes.c_float(steps), None, sp)),
                args.reps, stream)
     t_ms = timed(lambda: T.lg_gradients(xv, gv, emin, emax, 8), 2, stream)
     row("learned_grid_backward (+ per-channel sums)", "a14", 12, ms, None, t_ms)

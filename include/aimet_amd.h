@@ -319,8 +319,21 @@ int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t
 /* grad_x = mask * grad (grad_x may be NULL) and per-channel sums_dev[C][3] =
  * { sum((x_quant+offset)*grad), sum(mask*(x/delta)*grad), sum(!mask*grad) } from which the
  * encoding-min/max gradients are assembled (asymmetric_gradients / symmetric_gradients). */
+/* Optional epilogue of the learned-grid backward entry points: the encoding-min/max gradients
+ * (aimet_lg_range_grads' arithmetic) written by the kernel that folds the sums, no extra launch.
+ * null: the sums only. */
+typedef struct
+{
+    const float* encoding_min;   /* [C] device */
+    const float* encoding_max;   /* [C] device */
+    const float* delta;          /* [C] device, as passed to the backward */
+    float* grad_min;             /* [C] device out */
+    float* grad_max;             /* [C] device out */
+    int use_symmetric;
+} aimet_lg_range_spec;
 int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* sums_dev, int64_t outer, int64_t C,
-                      int64_t K, const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
+                      int64_t K, const float* delta_dev, const float* offset_dev, float num_steps,
+                      const aimet_lg_range_spec* range_spec, void* stream);
 /* The learned-grid forward / backward for a per-tensor range on fp16 (io_dtype 1) or bf16 (2)
  * tensors with the casts in registers: results identical to x.to(float32) -> aimet_lg_forward /
  * aimet_lg_backward -> .to(dtype) (same arithmetic, same order of the backward's sums), 4 / 6 B
@@ -329,7 +342,8 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
 int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* delta_dev,
                         const float* offset_dev, float num_steps, void* stream);
 int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* sums_dev, int64_t n, int io_dtype,
-                         const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
+                         const float* delta_dev, const float* offset_dev, float num_steps,
+                         const aimet_lg_range_spec* range_spec, void* stream);
 /* A float32 weight consumed in 16 bits (a Linear under autocast): the forward writes the
  * quantize-dequantized weight cast to fp16 / bf16 in the same pass (== aimet_lg_forward then
  * .to(dtype), as autocast casts it for the matmul); the backward takes the matmul's 16-bit weight
@@ -352,7 +366,7 @@ int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int
                           const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
 int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, float* sums_dev, int64_t outer,
                              int64_t C, int64_t K, int grad_dtype, const float* delta_dev, const float* offset_dev,
-                             float num_steps, void* stream);
+                             float num_steps, const aimet_lg_range_spec* range_spec, void* stream);
 int aimet_lg_backward_grad16_supported(int64_t outer, int64_t C, int64_t K, const void* x, const void* grad,
                                        const void* grad_x);
 

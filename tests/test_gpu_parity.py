@@ -546,7 +546,8 @@ def test_learned_grid_backward_sums_channel_axis_inner(outer, C, K):
     gx = torch.empty_like(x)
     sums = torch.empty(3 * C, device=DEV)
     _native.call("aimet_lg_backward", x.data_ptr(), g.data_ptr(), gx.data_ptr(), sums.data_ptr(), outer, C, K,
-                 delta.data_ptr(), offset.data_ptr(), ctypes.c_float(steps), torch.cuda.current_stream().cuda_stream)
+                 delta.data_ptr(), offset.data_ptr(), ctypes.c_float(steps), None,
+                 torch.cuda.current_stream().cuda_stream)
     d3, o3 = delta.view(1, C, 1), offset.view(1, C, 1)
     xr = torch.round(x / d3) - o3
     mask = (xr >= 0) & (xr <= steps)
@@ -1024,6 +1025,34 @@ def test_learned_grid_gate_and_range_grads_equal_torch_ops_on_device():
                      steps, int(sym), gmin.data_ptr(), gmax.data_ptr(), torch.cuda.current_stream().cuda_stream)
         assert torch.equal(gmin.view(torch.int32), want_min.view(torch.int32)), (bw, sym)
         assert torch.equal(gmax.view(torch.int32), want_max.view(torch.int32)), (bw, sym)
+
+
+@pytest.mark.parametrize("shape", [(1, 1, 300001), (1, 64, 4096), (3, 16, 1000), (1, 8, 77)])
+@pytest.mark.parametrize("sym", [False, True])
+def test_learned_grid_range_epilogue_equals_separate_launch(shape, sym):
+    """The encoding gradients written by the backward's fold (aimet_lg_range_spec) == aimet_lg_range_grads
+    on the sums the same call returns, bit for bit, on every backward path (per tensor, tile,
+    channel x slice, channel)."""
+    from aimet_amd import _native
+    from aimet_amd.learned_grid import _RangeSpec, _device_delta_offset
+    outer, C, K = shape
+    g = torch.Generator(device=DEV).manual_seed(C * 7 + int(sym))
+    x = torch.randn(outer, C, K, device=DEV, generator=g)
+    gr = torch.randn(outer, C, K, device=DEV, generator=g)
+    emin = -(torch.rand(C, device=DEV, generator=g) + 0.5)
+    emax = torch.rand(C, device=DEV, generator=g) + 0.5
+    delta, offset, steps = _device_delta_offset(8, emin, emax, sym, False, False)
+    sums = torch.empty(C, 3, device=DEV)
+    gmin, gmax = torch.empty_like(emin), torch.empty_like(emax)
+    spec = ctypes.byref(_RangeSpec(emin.data_ptr(), emax.data_ptr(), delta.data_ptr(), gmin.data_ptr(),
+                                   gmax.data_ptr(), int(sym)))
+    s = torch.cuda.current_stream().cuda_stream
+    _native.call("aimet_lg_backward", x.data_ptr(), gr.data_ptr(), None, sums.data_ptr(), outer, C, K,
+                 delta.data_ptr(), offset.data_ptr(), ctypes.c_float(steps), spec, s)
+    want_min, want_max = torch.empty_like(emin), torch.empty_like(emax)
+    _native.call("aimet_lg_range_grads", sums.data_ptr(), emin.data_ptr(), emax.data_ptr(), delta.data_ptr(), C,
+                 ctypes.c_float(steps), int(sym), want_min.data_ptr(), want_max.data_ptr(), s)
+    assert torch.equal(gmin, want_min) and torch.equal(gmax, want_max)
 
 
 def test_learned_grid_encodings_equal_reference_torch_ops_on_device():
