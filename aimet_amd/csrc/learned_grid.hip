@@ -47,12 +47,72 @@ __device__ __forceinline__ float lg_qdq(float x, float d, float o, float steps)
 
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 
+// torch's maximum / minimum: a NaN operand is returned
+__device__ __forceinline__ float t_maximum(float a, float b)
+{
+    return a != a ? a : (b != b ? b : fmaxf(a, b));
+}
+__device__ __forceinline__ float t_minimum(float a, float b)
+{
+    return a != a ? a : (b != b ? b : fminf(a, b));
+}
+
+// get_computed_encodings (quantsim_straight_through_grad.py:121-160) of channel c, element by
+// element as the reference's torch ops on the C-vectors: computed in the forward kernel itself
+// when `emin` is set (the thread holding the first element of a channel's first row stores
+// them for the backward), else read from precomputed delta / offset
+struct LgEnc
+{
+    const float* emin;
+    const float* emax;
+    float* delta_out;
+    float* offset_out;
+    float steps, half_floor, neg_half_ceil;
+    int mode;        // 0 symmetric signed, 1 symmetric unsigned, 2 asymmetric
+    uint32_t K;      // elements per row (the store condition)
+    __device__ __forceinline__ void of(uint32_t c, float& d, float& o) const
+    {
+        const float mn = emin[c], mx = emax[c];
+        if (mode == 0)
+        {
+            d = mx / half_floor;
+            o = neg_half_ceil;
+        }
+        else
+        {
+            d = (mx - mn) / steps;
+            if (mode == 1)
+                o = mn / d;
+            else
+                o = -t_minimum(steps, t_maximum(0.0f, __builtin_rintf(-mn / d)));
+        }
+    }
+    // delta / offset of channel c for element e (flat index): from the range or the tables
+    __device__ __forceinline__ void get(uint32_t c, uint32_t e, const float* delta, const float* offset, float& d,
+                                        float& o) const
+    {
+        if (emin == nullptr)
+        {
+            d = delta[c];
+            o = offset[c];
+            return;
+        }
+        of(c, d, o);
+        if (e == c * K)
+        {
+            delta_out[c]  = d;
+            offset_out[c] = o;
+        }
+    }
+};
+
 // OUT = IO_F32: y float32. OUT = IO_F16 / IO_BF16: y written in 16 bits with torch's rounding --
 // the float32 result cast as autocast casts a weight for its matmul, fused into the store.
 template <int OUT>
 __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict__ x, void* __restrict__ y,
                                                         uint32_t n, LgChannel map, const float* __restrict__ delta,
-                                                        const float* __restrict__ offset, float steps, int vec)
+                                                        const float* __restrict__ offset, float steps, int vec,
+                                                        LgEnc enc)
 {
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
     if (vec)
@@ -60,7 +120,8 @@ __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict_
         if (t >= n / 4)
             return;
         uint32_t c = map.channel(t * 4);
-        float d = delta[c], o = offset[c];
+        float d, o;
+        enc.get(c, t * 4, delta, offset, d, o);
         f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + t), r;
         r.x = lg_qdq(v.x, d, o, steps);
         r.y = lg_qdq(v.y, d, o, steps);
@@ -78,8 +139,10 @@ __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict_
     {
         if (t >= n)
             return;
-        uint32_t c    = map.channel(t);
-        const float r = lg_qdq(x[t], delta[c], offset[c], steps);
+        uint32_t c = map.channel(t);
+        float d, o;
+        enc.get(c, t, delta, offset, d, o);
+        const float r = lg_qdq(x[t], d, o, steps);
         if constexpr (OUT == IO_F32)
             static_cast<float*>(y)[t] = r;
         else
@@ -467,10 +530,12 @@ template <int IO>
 __global__ __launch_bounds__(kBlock) void lg_fwd16_kernel(const unsigned short* __restrict__ x,
                                                           unsigned short* __restrict__ y, uint32_t n,
                                                           const float* __restrict__ delta,
-                                                          const float* __restrict__ offset, float steps, int vec)
+                                                          const float* __restrict__ offset, float steps, int vec,
+                                                          LgEnc enc)
 {
     const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    const float d = delta[0], o = offset[0];
+    float d, o;
+    enc.get(0, t, delta, offset, d, o);   // element 0's thread stores them
     if (vec)
     {
         if (t >= n / 8)
@@ -541,14 +606,6 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
 // Each expression is the reference's torch op sequence on float32 C-vectors, element by element,
 // with torch's NaN rules (clamp keeps a NaN input, maximum / minimum return the NaN operand) and
 // no contraction: results are those of the torch ops, bit for bit (tests/test_gpu_parity.py).
-__device__ __forceinline__ float t_maximum(float a, float b)
-{
-    return a != a ? a : (b != b ? b : fmaxf(a, b));
-}
-__device__ __forceinline__ float t_minimum(float a, float b)
-{
-    return a != a ? a : (b != b ? b : fminf(a, b));
-}
 
 // set_encoding_min_max_gating_threshold (v1/tensor_quantizer.py:1347-1359), in place
 __global__ __launch_bounds__(kBlock) void lg_gate_kernel(float* __restrict__ emin, float* __restrict__ emax,
@@ -664,8 +721,56 @@ int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t
                        && n % 4 == 0;
         int64_t work = vec ? n / 4 : n;
         lg_fwd_kernel<IO_F32><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
-            x, y, (uint32_t) n, map, delta, offset, num_steps, vec ? 1 : 0);
+            x, y, (uint32_t) n, map, delta, offset, num_steps, vec ? 1 : 0, LgEnc {});
         AIMET_LAUNCH_CHECK();
+    });
+}
+
+}   // extern "C"
+
+namespace
+{
+
+LgEnc enc_of(const float* emin, const float* emax, int64_t K, int bw, int sym, int strict, int unsign, float* delta,
+             float* offset)
+{
+    AIMET_REQUIRE(bw > 0 && bw < 32, "invalid bitwidth");
+    require_device_ptr(emin, "encoding_min");
+    require_device_ptr(emax, "encoding_max");
+    require_device_ptr(delta, "delta");
+    require_device_ptr(offset, "offset");
+    double steps = std::ldexp(1.0, bw) - 1;
+    if (sym && strict)
+        steps -= 1;
+    const double half = steps / 2;
+    return LgEnc {emin, emax, delta, offset, (float) steps, (float) std::floor(half), (float) -std::ceil(half),
+                  (sym && !unsign) ? 0 : (sym ? 1 : 2), (uint32_t) K};
+}
+
+void forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype, const float* delta,
+                  const float* offset, float num_steps, LgEnc enc, hipStream_t st);
+
+}   // namespace
+
+extern "C" {
+
+int aimet_lg_forward_range(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype,
+                           const float* emin, const float* emax, int bw, int sym, int strict, int unsign,
+                           float* delta_out, float* offset_out, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
+        const LgEnc enc = enc_of(emin, emax, K, bw, sym, strict, unsign, delta_out, offset_out);
+        if (outer * C * K == 0)
+        {
+            // no element to carry the encodings: compute them on their own
+            lg_encodings_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, as_stream(stream)>>>(
+                emin, emax, (uint32_t) C, enc.steps, enc.mode, enc.half_floor, enc.neg_half_ceil, delta_out,
+                offset_out);
+            AIMET_LAUNCH_CHECK();
+            return;
+        }
+        forward_cast(x, y, outer, C, K, out_dtype, nullptr, nullptr, enc.steps, enc, as_stream(stream));
     });
 }
 
@@ -674,6 +779,23 @@ int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int
 {
     return guarded([&] {
         AIMET_REQUIRE(out_dtype == IO_F16 || out_dtype == IO_BF16, "out_dtype must be 1 (float16) or 2 (bfloat16)");
+        require_device_ptr(delta, "delta");
+        require_device_ptr(offset, "offset");
+        forward_cast(x, y, outer, C, K, out_dtype, delta, offset, num_steps, LgEnc {}, as_stream(stream));
+    });
+}
+
+}   // extern "C"
+
+namespace
+{
+
+// out_dtype IO_F32: float32 result (aimet_lg_forward's arithmetic), else the 16-bit cast of it
+void forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype, const float* delta,
+                  const float* offset, float num_steps, LgEnc enc, hipStream_t st)
+{
+    {
+        AIMET_REQUIRE(out_dtype == IO_F32 || out_dtype == IO_F16 || out_dtype == IO_BF16, "invalid out_dtype");
         AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
         int64_t n = outer * C * K;
         if (n == 0)
@@ -681,22 +803,28 @@ int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int
         AIMET_REQUIRE(n < (int64_t(1) << 31), "learned-grid QDQ needs < 2^31 elements per call");
         require_device_ptr(x, "x");
         require_device_ptr(y, "y");
-        require_device_ptr(delta, "delta");
-        require_device_ptr(offset, "offset");
         LgChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
+        const int ya = out_dtype == IO_F32 ? 15 : 7;
         bool vec = (C == 1 || K % 4 == 0) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
-                   (reinterpret_cast<uintptr_t>(y) & 7) == 0 && n % 4 == 0;
+                   (reinterpret_cast<uintptr_t>(y) & ya) == 0 && n % 4 == 0;
         int64_t work = vec ? n / 4 : n;
         const unsigned grid = (unsigned) ceil_div(work, kBlock);
-        if (out_dtype == IO_F16)
-            lg_fwd_kernel<IO_F16><<<grid, kBlock, 0, as_stream(stream)>>>(x, y, (uint32_t) n, map, delta, offset,
-                                                                          num_steps, vec ? 1 : 0);
+        if (out_dtype == IO_F32)
+            lg_fwd_kernel<IO_F32><<<grid, kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta, offset, num_steps,
+                                                           vec ? 1 : 0, enc);
+        else if (out_dtype == IO_F16)
+            lg_fwd_kernel<IO_F16><<<grid, kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta, offset, num_steps,
+                                                           vec ? 1 : 0, enc);
         else
-            lg_fwd_kernel<IO_BF16><<<grid, kBlock, 0, as_stream(stream)>>>(x, y, (uint32_t) n, map, delta, offset,
-                                                                           num_steps, vec ? 1 : 0);
+            lg_fwd_kernel<IO_BF16><<<grid, kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta, offset, num_steps,
+                                                            vec ? 1 : 0, enc);
         AIMET_LAUNCH_CHECK();
-    });
+    }
 }
+
+}   // namespace
+
+extern "C" {
 
 int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* sums, int64_t outer, int64_t C,
                       int64_t K, const float* delta, const float* offset, float num_steps,
@@ -795,29 +923,62 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
 
 extern "C" {
 
+}   // extern "C"
+
+namespace
+{
+
+void forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* delta, const float* offset,
+                float num_steps, LgEnc enc, hipStream_t st)
+{
+    AIMET_REQUIRE(io_dtype == IO_F16 || io_dtype == IO_BF16, "io_dtype must be 1 (float16) or 2 (bfloat16)");
+    AIMET_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "learned-grid QDQ needs < 2^31 elements per call");
+    if (n == 0)
+        return;
+    require_device_ptr(x, "x");
+    require_device_ptr(y, "y");
+    const bool vec = n % 8 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
+    const int64_t work = vec ? n / 8 : n;
+    auto xs = static_cast<const unsigned short*>(x);
+    auto ys = static_cast<unsigned short*>(y);
+    if (io_dtype == IO_F16)
+        lg_fwd16_kernel<IO_F16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, st>>>(
+            xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0, enc);
+    else
+        lg_fwd16_kernel<IO_BF16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, st>>>(
+            xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0, enc);
+    AIMET_LAUNCH_CHECK();
+}
+
+}   // namespace
+
+extern "C" {
+
 int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* delta, const float* offset,
                         float num_steps, void* stream)
 {
     return guarded([&] {
-        AIMET_REQUIRE(io_dtype == IO_F16 || io_dtype == IO_BF16, "io_dtype must be 1 (float16) or 2 (bfloat16)");
-        AIMET_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "learned-grid QDQ needs < 2^31 elements per call");
-        if (n == 0)
-            return;
-        require_device_ptr(x, "x");
-        require_device_ptr(y, "y");
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
-        const bool vec = n % 8 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
-        const int64_t work = vec ? n / 8 : n;
-        auto xs = static_cast<const unsigned short*>(x);
-        auto ys = static_cast<unsigned short*>(y);
-        if (io_dtype == IO_F16)
-            lg_fwd16_kernel<IO_F16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
-                xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0);
-        else
-            lg_fwd16_kernel<IO_BF16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
-                xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0);
-        AIMET_LAUNCH_CHECK();
+        forward_16(x, y, n, io_dtype, delta, offset, num_steps, LgEnc {}, as_stream(stream));
+    });
+}
+
+int aimet_lg_forward_16_range(const void* x, void* y, int64_t n, int io_dtype, const float* emin, const float* emax,
+                              int bw, int sym, int strict, int unsign, float* delta_out, float* offset_out,
+                              void* stream)
+{
+    return guarded([&] {
+        const LgEnc enc = enc_of(emin, emax, n > 0 ? n : 1, bw, sym, strict, unsign, delta_out, offset_out);
+        if (n == 0)
+        {
+            lg_encodings_kernel<<<1, kBlock, 0, as_stream(stream)>>>(emin, emax, 1u, enc.steps, enc.mode,
+                                                                      enc.half_floor, enc.neg_half_ceil, delta_out,
+                                                                      offset_out);
+            AIMET_LAUNCH_CHECK();
+            return;
+        }
+        forward_16(x, y, n, io_dtype, nullptr, nullptr, enc.steps, enc, as_stream(stream));
     });
 }
 

@@ -130,17 +130,17 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x = x.contiguous()
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
-        with torch.cuda.device(x.device):
-            delta, offset, steps = _device_delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
-                                                        is_unsigned_symmetric)
-        delta, offset = delta.contiguous(), offset.contiguous()
         outer, C, K = _channels(x.shape, ch_axis, emin.numel() > 1)
         if C != emin.numel():
             raise ValueError("encoding has %d channels, tensor has %d along axis %d" % (emin.numel(), C, ch_axis))
         y = torch.empty_like(x)
+        # get_computed_encodings inside the forward kernel (delta / offset stored for the backward)
+        delta, offset = torch.empty_like(emin), torch.empty_like(emin)
+        steps = num_steps_of(bitwidth, use_symmetric, use_strict_symmetric)
         with torch.cuda.device(x.device):
-            _native.call("aimet_lg_forward", x.data_ptr(), y.data_ptr(), outer, C, K, delta.data_ptr(),
-                         offset.data_ptr(), steps, _stream(x))
+            _native.call("aimet_lg_forward_range", x.data_ptr(), y.data_ptr(), outer, C, K, 0, emin.data_ptr(),
+                         emax.data_ptr(), int(bitwidth), int(bool(use_symmetric)), int(bool(use_strict_symmetric)),
+                         int(bool(is_unsigned_symmetric)), delta.data_ptr(), offset.data_ptr(), _stream(x))
         ctx.save_for_backward(x, delta, offset, emin, emax)
         ctx.cfg = (outer, C, K, steps, use_symmetric, is_unsigned_symmetric, orig_dtype,
                    encoding_min.shape, encoding_max.shape, staged)
@@ -153,17 +153,17 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x = tensor.contiguous()
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
-        with torch.cuda.device(x.device):
-            delta, offset, steps = _device_delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
-                                                        is_unsigned_symmetric)
-        delta, offset = delta.contiguous(), offset.contiguous()
         outer, C, K = _channels(x.shape, ch_axis, True)
         if C != emin.numel():
             raise ValueError("encoding has %d channels, tensor has %d along axis %d" % (emin.numel(), C, ch_axis))
         y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
+        delta, offset = torch.empty_like(emin), torch.empty_like(emin)
+        steps = num_steps_of(bitwidth, use_symmetric, use_strict_symmetric)
         with torch.cuda.device(x.device):
-            _native.call("aimet_lg_forward_cast", x.data_ptr(), y.data_ptr(), outer, C, K, IO_DTYPES[out_dtype],
-                         delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
+            _native.call("aimet_lg_forward_range", x.data_ptr(), y.data_ptr(), outer, C, K, IO_DTYPES[out_dtype],
+                         emin.data_ptr(), emax.data_ptr(), int(bitwidth), int(bool(use_symmetric)),
+                         int(bool(use_strict_symmetric)), int(bool(is_unsigned_symmetric)), delta.data_ptr(),
+                         offset.data_ptr(), _stream(x))
         ctx.save_for_backward(x, delta, offset, emin, emax)
         ctx.cfg = (outer, C, K, steps, use_symmetric, is_unsigned_symmetric, torch.float32,
                    encoding_min.shape, encoding_max.shape, False)
@@ -177,14 +177,14 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         x = tensor.contiguous()
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
-        with torch.cuda.device(x.device):
-            delta, offset, steps = _device_delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetric,
-                                                        is_unsigned_symmetric)
-        delta, offset = delta.contiguous(), offset.contiguous()
         y = torch.empty_like(x)
+        delta, offset = torch.empty_like(emin), torch.empty_like(emin)
+        steps = num_steps_of(bitwidth, use_symmetric, use_strict_symmetric)
         with torch.cuda.device(x.device):
-            _native.call("aimet_lg_forward_16", x.data_ptr(), y.data_ptr(), x.numel(), IO_DTYPES[x.dtype],
-                         delta.data_ptr(), offset.data_ptr(), steps, _stream(x))
+            _native.call("aimet_lg_forward_16_range", x.data_ptr(), y.data_ptr(), x.numel(), IO_DTYPES[x.dtype],
+                         emin.data_ptr(), emax.data_ptr(), int(bitwidth), int(bool(use_symmetric)),
+                         int(bool(use_strict_symmetric)), int(bool(is_unsigned_symmetric)), delta.data_ptr(),
+                         offset.data_ptr(), _stream(x))
         ctx.save_for_backward(x, delta, offset, emin, emax)
         ctx.cfg = (1, 1, x.numel(), steps, use_symmetric, is_unsigned_symmetric, x.dtype,
                    encoding_min.shape, encoding_max.shape, False)

@@ -1055,6 +1055,40 @@ def test_learned_grid_range_epilogue_equals_separate_launch(shape, sym):
     assert torch.equal(gmin, want_min) and torch.equal(gmax, want_max)
 
 
+@pytest.mark.parametrize("shape", [(1, 1, 100003), (1, 48, 1024), (2, 16, 777), (1, 5, 3)])
+@pytest.mark.parametrize("flags", [(True, False, False), (False, False, False), (True, True, False), (True, False, True)])
+def test_learned_grid_forward_range_equals_tables(shape, flags):
+    """aimet_lg_forward_range (encodings computed in the forward kernel) == aimet_lg_encodings +
+    aimet_lg_forward: delta, offset and y bit for bit; the 16-bit per-tensor form likewise."""
+    from aimet_amd import _native
+    from aimet_amd.learned_grid import _device_delta_offset
+    outer, C, K = shape
+    sym, strict, uns = flags
+    g = torch.Generator(device=DEV).manual_seed(C + K)
+    x = torch.randn(outer, C, K, device=DEV, generator=g) * 2
+    emin = -(torch.rand(C, device=DEV, generator=g) + 0.3) if not uns else torch.zeros(C, device=DEV)
+    emax = torch.rand(C, device=DEV, generator=g) + 0.3
+    s = torch.cuda.current_stream().cuda_stream
+    d_ref, o_ref, steps = _device_delta_offset(8, emin, emax, sym, strict, uns)
+    y_ref = torch.empty_like(x)
+    _native.call("aimet_lg_forward", x.data_ptr(), y_ref.data_ptr(), outer, C, K, d_ref.data_ptr(), o_ref.data_ptr(),
+                 ctypes.c_float(steps), s)
+    y, d, o = torch.empty_like(x), torch.empty_like(emin), torch.empty_like(emin)
+    _native.call("aimet_lg_forward_range", x.data_ptr(), y.data_ptr(), outer, C, K, 0, emin.data_ptr(),
+                 emax.data_ptr(), 8, int(sym), int(strict), int(uns), d.data_ptr(), o.data_ptr(), s)
+    assert torch.equal(d, d_ref) and torch.equal(o, o_ref) and torch.equal(y, y_ref)
+    if C == 1:
+        xb = x.reshape(-1).to(torch.bfloat16)
+        yb_ref, yb = torch.empty_like(xb), torch.empty_like(xb)
+        _native.call("aimet_lg_forward_16", xb.data_ptr(), yb_ref.data_ptr(), xb.numel(), 2, d_ref.data_ptr(),
+                     o_ref.data_ptr(), ctypes.c_float(steps), s)
+        d2, o2 = torch.empty_like(emin), torch.empty_like(emin)
+        _native.call("aimet_lg_forward_16_range", xb.data_ptr(), yb.data_ptr(), xb.numel(), 2, emin.data_ptr(),
+                     emax.data_ptr(), 8, int(sym), int(strict), int(uns), d2.data_ptr(), o2.data_ptr(), s)
+        assert torch.equal(yb.view(torch.int16), yb_ref.view(torch.int16))
+        assert torch.equal(d2, d_ref) and torch.equal(o2, o_ref)
+
+
 def test_learned_grid_encodings_equal_reference_torch_ops_on_device():
     """learned_grid._delta_offset (cached 0-dim device constants, fewer launches) == the reference's
     get_computed_encodings with its full_like tensors (oracle/torch_ref.lg_encodings), on the
