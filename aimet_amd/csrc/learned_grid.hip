@@ -109,34 +109,62 @@ struct LgEnc
 // OUT = IO_F32: y float32. OUT = IO_F16 / IO_BF16: y written in 16 bits with torch's rounding --
 // the float32 result cast as autocast casts a weight for its matmul, fused into the store.
 template <int OUT>
+__device__ __forceinline__ void lg_store4(void* __restrict__ y, uint32_t q, f4 r)
+{
+    if constexpr (OUT == IO_F32)
+        __builtin_nontemporal_store(r, static_cast<f4*>(y) + q);
+    else
+    {
+        const u16x4 h = {from_f32<OUT>(r.x), from_f32<OUT>(r.y), from_f32<OUT>(r.z), from_f32<OUT>(r.w)};
+        __builtin_nontemporal_store(h, static_cast<u16x4*>(y) + q);
+    }
+}
+
+// OUT = IO_F32: y float32. OUT = IO_F16 / IO_BF16: y written in 16 bits with torch's rounding --
+// the float32 result cast as autocast casts a weight for its matmul, fused into the store.
+// Q quads per lane (vec form), kBlock apart: their loads are issued together and a channel's
+// encoding is computed once for consecutive quads of that channel (quad q with q * 4 == c * K
+// is never preceded by a quad of channel c, so the store of the first one still happens)
+template <int OUT, int Q>
 __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict__ x, void* __restrict__ y,
                                                         uint32_t n, LgChannel map, const float* __restrict__ delta,
                                                         const float* __restrict__ offset, float steps, int vec,
                                                         LgEnc enc)
 {
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
     if (vec)
     {
-        if (t >= n / 4)
-            return;
-        uint32_t c = map.channel(t * 4);
-        float d, o;
-        enc.get(c, t * 4, delta, offset, d, o);
-        f4 v = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + t), r;
-        r.x = lg_qdq(v.x, d, o, steps);
-        r.y = lg_qdq(v.y, d, o, steps);
-        r.z = lg_qdq(v.z, d, o, steps);
-        r.w = lg_qdq(v.w, d, o, steps);
-        if constexpr (OUT == IO_F32)
-            __builtin_nontemporal_store(r, static_cast<f4*>(y) + t);
-        else
+        const uint32_t nq = n / 4;
+        const uint32_t q0 = blockIdx.x * (kBlock * Q) + threadIdx.x;
+        f4 v[Q];
+#pragma unroll
+        for (int u = 0; u < Q; ++u)
+            if (q0 + u * kBlock < nq)
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q0 + u * kBlock);
+        uint32_t pc = 0xffffffffu;
+        float d = 0.0f, o = 0.0f;
+#pragma unroll
+        for (int u = 0; u < Q; ++u)
         {
-            const u16x4 h = {from_f32<OUT>(r.x), from_f32<OUT>(r.y), from_f32<OUT>(r.z), from_f32<OUT>(r.w)};
-            __builtin_nontemporal_store(h, static_cast<u16x4*>(y) + t);
+            const uint32_t q = q0 + u * kBlock;
+            if (q >= nq)
+                return;
+            const uint32_t c = map.channel(q * 4);
+            if (c != pc)
+            {
+                enc.get(c, q * 4, delta, offset, d, o);
+                pc = c;
+            }
+            f4 r;
+            r.x = lg_qdq(v[u].x, d, o, steps);
+            r.y = lg_qdq(v[u].y, d, o, steps);
+            r.z = lg_qdq(v[u].z, d, o, steps);
+            r.w = lg_qdq(v[u].w, d, o, steps);
+            lg_store4<OUT>(y, q, r);
         }
     }
     else
     {
+        const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
         if (t >= n)
             return;
         uint32_t c = map.channel(t);
@@ -148,6 +176,33 @@ __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict_
         else
             static_cast<unsigned short*>(y)[t] = from_f32<OUT>(r);
     }
+}
+
+// quads per lane of lg_fwd_kernel's vec form (1, 2 or 4; AIMET_TUNE_LG_FWD_QUADS for experiments)
+int lg_fwd_quads()
+{
+    static int v = [] {
+        const char* e = getenv("AIMET_TUNE_LG_FWD_QUADS");   // tuning experiments only
+        const int q   = e ? atoi(e) : 2;
+        return (q == 1 || q == 4) ? q : 2;
+    }();
+    return v;
+}
+
+template <int OUT>
+void launch_lg_fwd(const float* x, void* y, int64_t n, LgChannel map, const float* delta, const float* offset,
+                   float steps, bool vec, LgEnc enc, hipStream_t st)
+{
+    if (vec && lg_fwd_quads() == 4)
+        lg_fwd_kernel<OUT, 4><<<(unsigned) ceil_div(n / 4, kBlock * 4), kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta,
+                                                                                       offset, steps, 1, enc);
+    else if (vec && lg_fwd_quads() == 2)
+        lg_fwd_kernel<OUT, 2><<<(unsigned) ceil_div(n / 4, kBlock * 2), kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta,
+                                                                                       offset, steps, 1, enc);
+    else
+        lg_fwd_kernel<OUT, 1><<<(unsigned) ceil_div(vec ? n / 4 : n, kBlock), kBlock, 0, st>>>(
+            x, y, (uint32_t) n, map, delta, offset, steps, vec ? 1 : 0, enc);
+    AIMET_LAUNCH_CHECK();
 }
 
 // four gradient elements of quad i: float32, or 16-bit upcast (exact)
@@ -719,10 +774,7 @@ int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t
         LgChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
         bool vec     = (C == 1 || K % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0
                        && n % 4 == 0;
-        int64_t work = vec ? n / 4 : n;
-        lg_fwd_kernel<IO_F32><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, as_stream(stream)>>>(
-            x, y, (uint32_t) n, map, delta, offset, num_steps, vec ? 1 : 0, LgEnc {});
-        AIMET_LAUNCH_CHECK();
+        launch_lg_fwd<IO_F32>(x, y, n, map, delta, offset, num_steps, vec, LgEnc {}, as_stream(stream));
     });
 }
 
@@ -807,18 +859,12 @@ void forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, 
         const int ya = out_dtype == IO_F32 ? 15 : 7;
         bool vec = (C == 1 || K % 4 == 0) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(y) & ya) == 0 && n % 4 == 0;
-        int64_t work = vec ? n / 4 : n;
-        const unsigned grid = (unsigned) ceil_div(work, kBlock);
         if (out_dtype == IO_F32)
-            lg_fwd_kernel<IO_F32><<<grid, kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta, offset, num_steps,
-                                                           vec ? 1 : 0, enc);
+            launch_lg_fwd<IO_F32>(x, y, n, map, delta, offset, num_steps, vec, enc, st);
         else if (out_dtype == IO_F16)
-            lg_fwd_kernel<IO_F16><<<grid, kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta, offset, num_steps,
-                                                           vec ? 1 : 0, enc);
+            launch_lg_fwd<IO_F16>(x, y, n, map, delta, offset, num_steps, vec, enc, st);
         else
-            lg_fwd_kernel<IO_BF16><<<grid, kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta, offset, num_steps,
-                                                            vec ? 1 : 0, enc);
-        AIMET_LAUNCH_CHECK();
+            launch_lg_fwd<IO_BF16>(x, y, n, map, delta, offset, num_steps, vec, enc, st);
     }
 }
 
