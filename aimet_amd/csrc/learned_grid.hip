@@ -676,6 +676,35 @@ __global__ __launch_bounds__(kBlock) void lg_gate_kernel(float* __restrict__ emi
     emax[c] = t_maximum(mx, mn + 1e-5f);
 }
 
+// the gate over up to kGateRanges ranges in one launch (a wrapper's quantizers): range r owns the
+// threads [start[r], start[r + 1])
+constexpr int kGateRanges = 8;
+struct LgGateSet
+{
+    float* emin[kGateRanges];
+    float* emax[kGateRanges];
+    uint32_t start[kGateRanges + 1];
+    int n;
+};
+
+__global__ __launch_bounds__(kBlock) void lg_gate_many_kernel(LgGateSet set)
+{
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    if (t >= set.start[set.n])
+        return;
+    int r = 0;
+    while (r + 1 < set.n && t >= set.start[r + 1])
+        ++r;
+    const uint32_t c = t - set.start[r];
+    float* emin = set.emin[r];
+    float* emax = set.emax[r];
+    float mn = emin[c], mx = emax[c];
+    mn = mn != mn ? mn : fminf(mn, 0.0f);   // the expressions of lg_gate_kernel
+    mx = mx != mx ? mx : fmaxf(mx, 0.0f);
+    emin[c] = mn;
+    emax[c] = t_maximum(mx, mn + 1e-5f);
+}
+
 // get_computed_encodings (quantsim_straight_through_grad.py:121-160)
 __global__ __launch_bounds__(kBlock) void lg_encodings_kernel(const float* __restrict__ emin,
                                                               const float* __restrict__ emax, uint32_t C,
@@ -1035,6 +1064,33 @@ int aimet_lg_gate_range(float* emin, float* emax, int64_t C, void* stream)
         if (C == 0)
             return;
         lg_gate_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, as_stream(stream)>>>(emin, emax, (uint32_t) C);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_lg_gate_ranges(float* const* emin, float* const* emax, const int64_t* C, int n, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(n >= 0 && n <= kGateRanges, "aimet_lg_gate_ranges takes at most 8 ranges");
+        AIMET_REQUIRE(n == 0 || (emin && emax && C), "null range table");
+        LgGateSet set {};
+        int64_t total = 0;
+        for (int r = 0; r < n; ++r)
+        {
+            AIMET_REQUIRE(C[r] >= 0, "invalid channel count");
+            require_device_ptr(emin[r], "encoding_min");
+            require_device_ptr(emax[r], "encoding_max");
+            set.emin[r]  = emin[r];
+            set.emax[r]  = emax[r];
+            set.start[r] = (uint32_t) total;
+            total += C[r];
+            AIMET_REQUIRE(total < (int64_t(1) << 31), "too many channels");
+        }
+        set.start[n] = (uint32_t) total;
+        set.n        = n;
+        if (total == 0)
+            return;
+        lg_gate_many_kernel<<<(unsigned) ceil_div(total, kBlock), kBlock, 0, as_stream(stream)>>>(set);
         AIMET_LAUNCH_CHECK();
     });
 }

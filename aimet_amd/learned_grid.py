@@ -236,12 +236,39 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         return gx_out, gmin, gmax, None, None, None, None, None, None
 
 
+def _gate_fusable(encoding_min, encoding_max):
+    return (encoding_min.is_cuda and encoding_max.is_cuda and encoding_min.dtype == torch.float32
+            and encoding_max.dtype == torch.float32 and encoding_min.is_contiguous() and encoding_max.is_contiguous()
+            and encoding_min.numel() == encoding_max.numel() and encoding_min.device == encoding_max.device)
+
+
+def set_encoding_min_max_gating_threshold_many(ranges):
+    """set_encoding_min_max_gating_threshold over a wrapper's (encoding_min, encoding_max) pairs:
+    the device float32 ones of one device in launches of up to 8 ranges (aimet_lg_gate_ranges,
+    element by element the single-range gate), any other pair through the single-range call."""
+    fused = []
+    for emin, emax in ranges:
+        if _gate_fusable(emin, emax) and (not fused or fused[0][0].device == emin.device):
+            fused.append((emin, emax))
+        else:
+            set_encoding_min_max_gating_threshold(emin, emax)
+    for i in range(0, len(fused), 8):
+        chunk = fused[i:i + 8]
+        n = len(chunk)
+        mins = (ctypes.c_void_p * n)(*[a.data_ptr() for a, _ in chunk])
+        maxs = (ctypes.c_void_p * n)(*[b.data_ptr() for _, b in chunk])
+        counts = (ctypes.c_int64 * n)(*[a.numel() for a, _ in chunk])
+        with torch.cuda.device(chunk[0][0].device):
+            _native.call("aimet_lg_gate_ranges", mins, maxs, counts, n, _stream(chunk[0][0]))
+        for a, b in chunk:
+            torch.autograd.graph.increment_version(a)
+            torch.autograd.graph.increment_version(b)
+
+
 def set_encoding_min_max_gating_threshold(encoding_min, encoding_max):
     """v1/tensor_quantizer.py:1347-1359: keep a trainable range ordered and around zero
     (min <= 0 <= max, max >= min + 1e-5), in place."""
-    if (encoding_min.is_cuda and encoding_max.is_cuda and encoding_min.dtype == torch.float32
-            and encoding_max.dtype == torch.float32 and encoding_min.is_contiguous() and encoding_max.is_contiguous()
-            and encoding_min.numel() == encoding_max.numel()):
+    if _gate_fusable(encoding_min, encoding_max):
         # one launch, the same expressions element by element (aimet_lg_gate_range)
         with torch.cuda.device(encoding_min.device):
             _native.call("aimet_lg_gate_range", encoding_min.data_ptr(), encoding_max.data_ptr(),

@@ -19,7 +19,7 @@ from torch import nn
 from aimet_amd.encodings_io import (compute_partial_encoding, create_encoding_from_dict, export_quantizer_encoding,
                                     validate_is_symmetric_flag)
 from aimet_amd.learned_grid import (LearnedGridTensorQuantizer, initialize_learned_grid_quantizer_attributes,
-                                    set_encoding_min_max_gating_threshold)
+                                    set_encoding_min_max_gating_threshold_many)
 from aimet_amd.libpymo import RoundingMode
 from aimet_amd.quantizers import (MAP_ROUND_MODE_TO_PYMO, QuantizationDataType, QuantScheme,
                                   StaticGridPerChannelQuantizer, StaticGridPerTensorQuantizer, compute_dloss_by_dx)
@@ -509,11 +509,14 @@ class LearnedGridQuantWrapper(QcQuantizeWrapper):
         """v1/qc_quantize_op.py:1019-1055."""
         quantizers = list(self.input_quantizers) + list(self.output_quantizers) + \
             [self.param_quantizers[n] for n, _ in self._module_to_wrap.named_parameters()]
+        ranges = []
         for q in quantizers:
             if q.enabled and q.bitwidth != 32 and q.data_type != QuantizationDataType.float:
                 emin, emax = self._ranges(q)
                 if emin is not None and emax is not None:
-                    set_encoding_min_max_gating_threshold(emin, emax)
+                    ranges.append((emin, emax))
+        # one launch for the wrapper's device ranges (aimet_lg_gate_ranges), the same expressions
+        set_encoding_min_max_gating_threshold_many(ranges)
 
     def forward(self, *inputs, **kwargs):
         """v1/qc_quantize_op.py:1057-1098."""

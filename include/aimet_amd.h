@@ -356,6 +356,10 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
  * (quantsim_straight_through_grad.py:121-160) -> delta[C], offset[C]; _range_grads = the encoding
  * gradients of asymmetric_gradients / symmetric_gradients (:252-328) from aimet_lg_backward's sums. */
 int aimet_lg_gate_range(float* emin_dev, float* emax_dev, int64_t C, void* stream);
+/* The same gate over n <= 8 ranges (emin[r], emax[r] of C[r] floats each; host arrays of device
+ * pointers) in one launch: QcQuantizeWrapper.apply_gating_logic (v1/qc_quantize_op.py:1019-1055)
+ * over a wrapper's quantizers. */
+int aimet_lg_gate_ranges(float* const* emin_dev, float* const* emax_dev, const int64_t* C, int n, void* stream);
 int aimet_lg_encodings(const float* emin_dev, const float* emax_dev, int64_t C, int bitwidth, int use_symmetric,
                        int use_strict_symmetric, int is_unsigned_symmetric, float* delta_dev, float* offset_dev,
                        void* stream);
