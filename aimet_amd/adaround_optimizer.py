@@ -94,6 +94,14 @@ def conv_backend(module: torch.nn.Module):
 _GEMM_LAYERS = os.environ.get("AIMET_ADA_GEMM_LAYERS", "1") != "0"
 
 
+# 1x1 / linear layers have two loop forms that sum the weight gradient in different orders (GEMM or
+# MIOpen convolution through autograd), so the optimised alpha depends on the form. The form is a
+# fixed rule (the GEMM form), never a timing: two runs with the same seed give the same alpha.
+# AIMET_ADA_LOOP_FORM=autograd forces the convolution form; =timed picks the faster of the two by
+# timing graph replays (measurements only: results then depend on timing noise).
+_LOOP_FORM = os.environ.get("AIMET_ADA_LOOP_FORM", "gemm")
+
+
 # the Adam step writes the next soft-quantized weight (AIMET_ADA_FUSE_WQ=0: a forward launch per
 # iteration instead; measurements only)
 _FUSE_SOFT_WEIGHT = os.environ.get("AIMET_ADA_FUSE_WQ", "1") == "1"
@@ -265,6 +273,10 @@ class AdaroundOptimizer:
             inp_data, out_data = inp_data.index_select(0, shard), out_data.index_select(0, shard)
         args = (module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func, generator,
                 round_loss_out, world, group)
+        if opt_params.num_iterations // world == 0:
+            # fewer iterations than ranks (or none): the loop runs zero times and alpha keeps its
+            # initial value, as the reference's range() loop does -- no batch draw, no capture
+            use_graph = False
         with conv_backend(module):
             if use_graph:
                 rng = generator.get_state() if generator is not None else torch.get_rng_state()
@@ -508,20 +520,25 @@ class AdaroundOptimizer:
                 step()
             return g
 
-        # layers with two forms (GEMM or MIOpen convolution through autograd): each is captured and
-        # timed over a few replays and the faster one runs the loop -- which wins depends on the
-        # shape (profiles/r02: the GEMMs win for small Cin at large spatial size, MIOpen for
-        # projections to few channels)
-        candidates = [mode] + (["autograd"] if mode in ("pointwise", "linear") and iters >= 50 else [])
+        # layers with two forms (GEMM or MIOpen convolution through autograd): the form is fixed by
+        # _LOOP_FORM (deterministic results); only AIMET_ADA_LOOP_FORM=timed captures both and times
+        # a few replays of each
+        two_forms = mode in ("pointwise", "linear")
+        if two_forms and _LOOP_FORM == "autograd":
+            mode = "autograd"
+        timed = two_forms and _LOOP_FORM == "timed" and iters >= 50
+        candidates = [mode] + (["autograd"] if two_forms and mode != "autograd" else [])
         best = None
         for m in candidates:
+            if best is not None and not timed:
+                break   # the fixed form captured: the other is only a fallback
             try:
                 g = capture(m)
             except RuntimeError:
                 if m == candidates[0] and len(candidates) > 1:
-                    continue
+                    continue   # the GEMM form could not be captured: the convolution form
                 raise
-            if len(candidates) > 1:
+            if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 g.replay()
                 e0.record()

@@ -67,12 +67,13 @@ struct LgEnc
     const float* emax;
     float* delta_out;
     float* offset_out;
+    float* range_out;   // optional [2][C]: the range as the forward read it (saved for the backward)
     float steps, half_floor, neg_half_ceil;
     int mode;        // 0 symmetric signed, 1 symmetric unsigned, 2 asymmetric
     uint32_t K;      // elements per row (the store condition)
-    __device__ __forceinline__ void of(uint32_t c, float& d, float& o) const
+    uint32_t C;
+    __device__ __forceinline__ void of(float mn, float mx, float& d, float& o) const
     {
-        const float mn = emin[c], mx = emax[c];
         if (mode == 0)
         {
             d = mx / half_floor;
@@ -97,11 +98,17 @@ struct LgEnc
             o = offset[c];
             return;
         }
-        of(c, d, o);
+        const float mn = emin[c], mx = emax[c];
+        of(mn, mx, d, o);
         if (e == c * K)
         {
             delta_out[c]  = d;
             offset_out[c] = o;
+            if (range_out)
+            {
+                range_out[c]     = mn;
+                range_out[C + c] = mx;
+            }
         }
     }
 };
@@ -710,12 +717,17 @@ __global__ __launch_bounds__(kBlock) void lg_encodings_kernel(const float* __res
                                                               const float* __restrict__ emax, uint32_t C,
                                                               float steps, int mode, float half_floor,
                                                               float neg_half_ceil, float* __restrict__ delta,
-                                                              float* __restrict__ offset)
+                                                              float* __restrict__ offset, float* __restrict__ range_out)
 {
     const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
     if (c >= C)
         return;
     const float mn = emin[c], mx = emax[c];
+    if (range_out)
+    {
+        range_out[c]     = mn;
+        range_out[C + c] = mx;
+    }
     float d, o;
     if (mode == 0)   // symmetric, signed
     {
@@ -812,8 +824,8 @@ int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t
 namespace
 {
 
-LgEnc enc_of(const float* emin, const float* emax, int64_t K, int bw, int sym, int strict, int unsign, float* delta,
-             float* offset)
+LgEnc enc_of(const float* emin, const float* emax, int64_t C, int64_t K, int bw, int sym, int strict, int unsign,
+             float* delta, float* offset, float* range_out)
 {
     AIMET_REQUIRE(bw > 0 && bw < 32, "invalid bitwidth");
     require_device_ptr(emin, "encoding_min");
@@ -824,8 +836,10 @@ LgEnc enc_of(const float* emin, const float* emax, int64_t K, int bw, int sym, i
     if (sym && strict)
         steps -= 1;
     const double half = steps / 2;
-    return LgEnc {emin, emax, delta, offset, (float) steps, (float) std::floor(half), (float) -std::ceil(half),
-                  (sym && !unsign) ? 0 : (sym ? 1 : 2), (uint32_t) K};
+    if (range_out)
+        require_device_ptr(range_out, "range_out");
+    return LgEnc {emin, emax, delta, offset, range_out, (float) steps, (float) std::floor(half),
+                  (float) -std::ceil(half), (sym && !unsign) ? 0 : (sym ? 1 : 2), (uint32_t) K, (uint32_t) C};
 }
 
 void forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype, const float* delta,
@@ -837,17 +851,17 @@ extern "C" {
 
 int aimet_lg_forward_range(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype,
                            const float* emin, const float* emax, int bw, int sym, int strict, int unsign,
-                           float* delta_out, float* offset_out, void* stream)
+                           float* delta_out, float* offset_out, float* range_out, void* stream)
 {
     return guarded([&] {
         AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
-        const LgEnc enc = enc_of(emin, emax, K, bw, sym, strict, unsign, delta_out, offset_out);
+        const LgEnc enc = enc_of(emin, emax, C, K, bw, sym, strict, unsign, delta_out, offset_out, range_out);
         if (outer * C * K == 0)
         {
             // no element to carry the encodings: compute them on their own
             lg_encodings_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, as_stream(stream)>>>(
                 emin, emax, (uint32_t) C, enc.steps, enc.mode, enc.half_floor, enc.neg_half_ceil, delta_out,
-                offset_out);
+                offset_out, range_out);
             AIMET_LAUNCH_CHECK();
             return;
         }
@@ -1041,15 +1055,16 @@ int aimet_lg_forward_16(const void* x, void* y, int64_t n, int io_dtype, const f
 
 int aimet_lg_forward_16_range(const void* x, void* y, int64_t n, int io_dtype, const float* emin, const float* emax,
                               int bw, int sym, int strict, int unsign, float* delta_out, float* offset_out,
-                              void* stream)
+                              float* range_out, void* stream)
 {
     return guarded([&] {
-        const LgEnc enc = enc_of(emin, emax, n > 0 ? n : 1, bw, sym, strict, unsign, delta_out, offset_out);
+        const LgEnc enc = enc_of(emin, emax, 1, n > 0 ? n : 1, bw, sym, strict, unsign, delta_out, offset_out,
+                                 range_out);
         if (n == 0)
         {
             lg_encodings_kernel<<<1, kBlock, 0, as_stream(stream)>>>(emin, emax, 1u, enc.steps, enc.mode,
                                                                       enc.half_floor, enc.neg_half_ceil, delta_out,
-                                                                      offset_out);
+                                                                      offset_out, range_out);
             AIMET_LAUNCH_CHECK();
             return;
         }
@@ -1110,7 +1125,7 @@ int aimet_lg_encodings(const float* emin, const float* emax, int64_t C, int bw, 
         const int mode    = (sym && !unsign) ? 0 : (sym ? 1 : 2);
         lg_encodings_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, as_stream(stream)>>>(
             emin, emax, (uint32_t) C, (float) steps, mode, (float) std::floor(half), (float) -std::ceil(half), delta,
-            offset);
+            offset, nullptr);
         AIMET_LAUNCH_CHECK();
     });
 }

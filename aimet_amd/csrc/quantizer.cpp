@@ -832,6 +832,7 @@ struct aimet_encoding_request
     int32_t b  = 0;
     int sym    = 0, strict = 0, unsign = 0;
     int device = 0;
+    hipStream_t stream = nullptr;   // where the search and its result copy were enqueued
     hipEvent_t done = nullptr;
     void* pinned    = nullptr;   // TF-Enhanced encodings, concatenated
     size_t pinned_bytes = 0;
@@ -910,6 +911,26 @@ void release_request(aimet_encoding_request* r)
     delete r;
 }
 
+// release on an error path: the request's result copy may already be queued into its pinned block,
+// so the block goes back to the pool only after the stream has drained (else the next take_pinned
+// could hand it out while the copy still writes into it)
+void release_request_after_error(aimet_encoding_request* r)
+{
+    if (r == nullptr)
+        return;
+    if (r->pinned)
+    {
+        DeviceGuard g(r->device);
+        if (hipStreamSynchronize(r->stream) != hipSuccess)
+        {
+            // the stream is broken: leak the block rather than risk a live copy into a reused one
+            r->pinned = nullptr;
+            (void) hipGetLastError();
+        }
+    }
+    release_request(r);
+}
+
 }   // namespace
 
 namespace
@@ -937,6 +958,7 @@ aimet_encoding_request* encodings_launch(aimet_tensor_quantizer* const* qs, int6
     if (nq == 0)
         return req;
     req->device = qs[0]->device;
+    req->stream = st;
     DeviceGuard g(req->device);
     const int32_t b = req->b;
     std::vector<const TqDevice*> tfe, ent, mse;
@@ -1012,7 +1034,7 @@ int aimet_tq_get_encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq,
     });
     if (rc != AIMET_OK)
     {
-        release_request(req);
+        release_request_after_error(req);
         return rc;
     }
     *req_out = req;
@@ -1067,8 +1089,8 @@ int aimet_calibrate_launch(aimet_tensor_quantizer* const* act_qs, const float* c
     });
     if (rc != AIMET_OK)
     {
-        release_request(ra);
-        release_request(rp);
+        release_request_after_error(ra);
+        release_request_after_error(rp);
         return rc;
     }
     *act_req = ra;

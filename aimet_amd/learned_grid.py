@@ -92,6 +92,14 @@ def _device_delta_offset(bitwidth, emin, emax, use_symmetric, use_strict_symmetr
     return delta, offset, num_steps_of(bitwidth, use_symmetric, use_strict_symmetric)
 
 
+def _saved_encoding(emin):
+    """[4][C] float32: rows delta, offset, encoding_min, encoding_max, filled by the forward kernel.
+    The range rows are the reference's encoding_min/max.clone().detach() saved for the backward
+    (v1/tensor_quantizer.py:940-951): not aliases of the Parameters, which the wrapper's gate updates
+    in place on every call (a module run twice before backward keeps the range it saw)."""
+    return torch.empty((4, emin.numel()), dtype=torch.float32, device=emin.device)
+
+
 def _channels(shape, ch_axis, per_channel):
     if not per_channel:
         n = 1
@@ -134,14 +142,16 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         if C != emin.numel():
             raise ValueError("encoding has %d channels, tensor has %d along axis %d" % (emin.numel(), C, ch_axis))
         y = torch.empty_like(x)
-        # get_computed_encodings inside the forward kernel (delta / offset stored for the backward)
-        delta, offset = torch.empty_like(emin), torch.empty_like(emin)
+        # get_computed_encodings inside the forward kernel (delta / offset stored for the backward,
+        # with a copy of the range as the kernel read it)
+        enc = _saved_encoding(emin)
         steps = num_steps_of(bitwidth, use_symmetric, use_strict_symmetric)
         with torch.cuda.device(x.device):
             _native.call("aimet_lg_forward_range", x.data_ptr(), y.data_ptr(), outer, C, K, 0, emin.data_ptr(),
                          emax.data_ptr(), int(bitwidth), int(bool(use_symmetric)), int(bool(use_strict_symmetric)),
-                         int(bool(is_unsigned_symmetric)), delta.data_ptr(), offset.data_ptr(), _stream(x))
-        ctx.save_for_backward(x, delta, offset, emin, emax)
+                         int(bool(is_unsigned_symmetric)), enc[0].data_ptr(), enc[1].data_ptr(), enc[2].data_ptr(),
+                         _stream(x))
+        ctx.save_for_backward(x, enc)
         ctx.cfg = (outer, C, K, steps, use_symmetric, is_unsigned_symmetric, orig_dtype,
                    encoding_min.shape, encoding_max.shape, staged)
         return y.to(orig_dtype).cpu() if staged else y.to(orig_dtype)
@@ -157,14 +167,14 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         if C != emin.numel():
             raise ValueError("encoding has %d channels, tensor has %d along axis %d" % (emin.numel(), C, ch_axis))
         y = torch.empty(x.shape, dtype=out_dtype, device=x.device)
-        delta, offset = torch.empty_like(emin), torch.empty_like(emin)
+        enc = _saved_encoding(emin)
         steps = num_steps_of(bitwidth, use_symmetric, use_strict_symmetric)
         with torch.cuda.device(x.device):
             _native.call("aimet_lg_forward_range", x.data_ptr(), y.data_ptr(), outer, C, K, IO_DTYPES[out_dtype],
                          emin.data_ptr(), emax.data_ptr(), int(bitwidth), int(bool(use_symmetric)),
-                         int(bool(use_strict_symmetric)), int(bool(is_unsigned_symmetric)), delta.data_ptr(),
-                         offset.data_ptr(), _stream(x))
-        ctx.save_for_backward(x, delta, offset, emin, emax)
+                         int(bool(use_strict_symmetric)), int(bool(is_unsigned_symmetric)), enc[0].data_ptr(),
+                         enc[1].data_ptr(), enc[2].data_ptr(), _stream(x))
+        ctx.save_for_backward(x, enc)
         ctx.cfg = (outer, C, K, steps, use_symmetric, is_unsigned_symmetric, torch.float32,
                    encoding_min.shape, encoding_max.shape, False)
         return y
@@ -178,21 +188,22 @@ class LearnedGridQuantizeDequantize(torch.autograd.Function):
         emin = encoding_min.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         emax = encoding_max.detach().to(x.device, torch.float32).reshape(-1).contiguous()
         y = torch.empty_like(x)
-        delta, offset = torch.empty_like(emin), torch.empty_like(emin)
+        enc = _saved_encoding(emin)
         steps = num_steps_of(bitwidth, use_symmetric, use_strict_symmetric)
         with torch.cuda.device(x.device):
             _native.call("aimet_lg_forward_16_range", x.data_ptr(), y.data_ptr(), x.numel(), IO_DTYPES[x.dtype],
                          emin.data_ptr(), emax.data_ptr(), int(bitwidth), int(bool(use_symmetric)),
-                         int(bool(use_strict_symmetric)), int(bool(is_unsigned_symmetric)), delta.data_ptr(),
-                         offset.data_ptr(), _stream(x))
-        ctx.save_for_backward(x, delta, offset, emin, emax)
+                         int(bool(use_strict_symmetric)), int(bool(is_unsigned_symmetric)), enc[0].data_ptr(),
+                         enc[1].data_ptr(), enc[2].data_ptr(), _stream(x))
+        ctx.save_for_backward(x, enc)
         ctx.cfg = (1, 1, x.numel(), steps, use_symmetric, is_unsigned_symmetric, x.dtype,
                    encoding_min.shape, encoding_max.shape, False)
         return y
 
     @staticmethod
     def backward(ctx, grad):
-        x, delta, offset, emin, emax = ctx.saved_tensors
+        x, enc = ctx.saved_tensors
+        delta, offset, emin, emax = enc[0], enc[1], enc[2], enc[3]
         outer, C, K, steps, sym, unsigned, dtype, min_shape, max_shape, staged = ctx.cfg
         sums = torch.empty((C, 3), dtype=torch.float32, device=x.device)
         # symmetric_gradients: gmax = (A - B) / floor(steps/2), gmin = -gmax; asymmetric_gradients:

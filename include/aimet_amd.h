@@ -368,16 +368,19 @@ int aimet_lg_range_grads(const float* sums_dev, const float* emin_dev, const flo
                          void* stream);
 /* The learned-grid forward with get_computed_encodings done in the same kernel: delta / offset of
  * every channel computed from the range (equal to aimet_lg_encodings) and stored to
- * delta_out / offset_out for the backward. out_dtype 0: float32 result (aimet_lg_forward), 1 / 2:
+ * delta_out / offset_out for the backward. range_out (optional, [2][C]): the range as the kernel
+ * read it (min row, max row) -- the reference's encoding_min/max.clone() saved for the backward
+ * (v1/tensor_quantizer.py:940-951), so an in-place gate between forward and backward (a module
+ * called twice) leaves the saved range alone. out_dtype 0: float32 result (aimet_lg_forward), 1 / 2:
  * the fp16 / bf16 cast (aimet_lg_forward_cast); _16_range: aimet_lg_forward_16. */
 int aimet_lg_forward_range(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype,
                            const float* encoding_min_dev, const float* encoding_max_dev, int bitwidth,
                            int use_symmetric, int use_strict_symmetric, int is_unsigned_symmetric, float* delta_out,
-                           float* offset_out, void* stream);
+                           float* offset_out, float* range_out, void* stream);
 int aimet_lg_forward_16_range(const void* x, void* y, int64_t n, int io_dtype, const float* encoding_min_dev,
                               const float* encoding_max_dev, int bitwidth, int use_symmetric,
                               int use_strict_symmetric, int is_unsigned_symmetric, float* delta_out,
-                              float* offset_out, void* stream);
+                              float* offset_out, float* range_out, void* stream);
 int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype,
                           const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
 int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, float* sums_dev, int64_t outer,

@@ -163,3 +163,20 @@ def test_adaround_world_one_unchanged():
     # == the union reference with one "rank" holding everything
     want = union_reference(world=1, seeds=SEEDS[:1])
     torch.testing.assert_close(a.detach(), want, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("iters", [0, 1])
+def test_adaround_fewer_iterations_than_ranks(iters, monkeypatch):
+    """num_iterations // world == 0 (world 2, 0 or 1 iteration): the reference's loop runs zero
+    times and returns the initial alpha; no batch is drawn and no graph captured (use_graph=True
+    must not reach the capture path, which needs a GPU)."""
+    _patch()
+    import aimet_amd.adaround_optimizer as AO
+    from aimet_amd.adaround import init_alpha
+    monkeypatch.setattr(AO, "_group_world", lambda group: (0, 2))
+    conv, inp, out, d, o = _problem()
+    p = AO.AdaroundHyperParameters(num_iterations=iters)
+    a = AO.AdaroundOptimizer.optimize_rounding(conv, inp, out, d, o, 4, 0, p, torch.nn.ReLU(),
+                                               torch.Generator().manual_seed(1), use_graph=True)
+    want = init_alpha(conv.weight.detach(), d.view(-1, 1, 1, 1))
+    torch.testing.assert_close(a.detach(), want.detach(), rtol=0, atol=0)

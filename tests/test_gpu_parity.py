@@ -1074,9 +1074,11 @@ def test_learned_grid_forward_range_equals_tables(shape, flags):
     _native.call("aimet_lg_forward", x.data_ptr(), y_ref.data_ptr(), outer, C, K, d_ref.data_ptr(), o_ref.data_ptr(),
                  ctypes.c_float(steps), s)
     y, d, o = torch.empty_like(x), torch.empty_like(emin), torch.empty_like(emin)
+    rng = torch.full((2, C), float("nan"), device=DEV)
     _native.call("aimet_lg_forward_range", x.data_ptr(), y.data_ptr(), outer, C, K, 0, emin.data_ptr(),
-                 emax.data_ptr(), 8, int(sym), int(strict), int(uns), d.data_ptr(), o.data_ptr(), s)
+                 emax.data_ptr(), 8, int(sym), int(strict), int(uns), d.data_ptr(), o.data_ptr(), rng.data_ptr(), s)
     assert torch.equal(d, d_ref) and torch.equal(o, o_ref) and torch.equal(y, y_ref)
+    assert torch.equal(rng[0], emin) and torch.equal(rng[1], emax)   # the saved copy of the range
     if C == 1:
         xb = x.reshape(-1).to(torch.bfloat16)
         yb_ref, yb = torch.empty_like(xb), torch.empty_like(xb)
@@ -1084,7 +1086,7 @@ def test_learned_grid_forward_range_equals_tables(shape, flags):
                      o_ref.data_ptr(), ctypes.c_float(steps), s)
         d2, o2 = torch.empty_like(emin), torch.empty_like(emin)
         _native.call("aimet_lg_forward_16_range", xb.data_ptr(), yb.data_ptr(), xb.numel(), 2, emin.data_ptr(),
-                     emax.data_ptr(), 8, int(sym), int(strict), int(uns), d2.data_ptr(), o2.data_ptr(), s)
+                     emax.data_ptr(), 8, int(sym), int(strict), int(uns), d2.data_ptr(), o2.data_ptr(), None, s)
         assert torch.equal(yb.view(torch.int16), yb_ref.view(torch.int16))
         assert torch.equal(d2, d_ref) and torch.equal(o2, o_ref)
 

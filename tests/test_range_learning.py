@@ -287,3 +287,70 @@ def test_quantsim_forward_equals_reference_torch_ops():
         torch.testing.assert_close(wq, want_w, rtol=0, atol=0, msg=n)
         want_o = T.lg_forward(raw_out, w.output0_encoding_min.detach(), w.output0_encoding_max.detach(), 8)[0]
         torch.testing.assert_close(outs[n], want_o, rtol=0, atol=0, msg=n)
+
+
+class SharedNet(nn.Module):
+    """One Linear called twice per forward (a reused module, as torchvision ResNet's shared relu)."""
+    def __init__(self):
+        super().__init__()
+        self.fc = nn.Linear(32, 32)
+
+    def forward(self, x):
+        return self.fc(F.relu(self.fc(x)))
+
+
+@pytest.mark.gpu
+@gpu
+def test_learned_grid_wrapper_called_twice_before_backward():
+    """A LearnedGridQuantWrapper run twice before loss.backward(): its gate updates the range
+    Parameters in place on every call, so the forward must save a copy of the range (the reference
+    saves encoding_min/max.clone(), v1/tensor_quantizer.py:940-951) -- else backward fails with
+    'modified by an inplace operation'. Gradients == the op-level path on the same parameters, and
+    the output range's gradient == the sum of the reference's torch-op gradients of both calls
+    (oracle/torch_ref.lg_gradients; rtol 1e-4: fp32 summation order)."""
+    torch.manual_seed(5)
+    sim = QuantizationSimModel(SharedNet().cuda().eval(), quant_scheme=RL_TF, dummy_input=torch.rand(8, 32).cuda())
+    sim.compute_encodings(lambda m, d: [m(x) for x in d], [torch.randn(8, 32).cuda() for _ in range(2)])
+    assert isinstance(sim.model.fc, LearnedGridQuantWrapper)
+    ref = copy.deepcopy(sim.model)
+    x = torch.randn(8, 32).cuda()
+    sim.model.train()
+    loss = sim(x).square().mean()
+    loss.backward()                                    # raised before the saved range was a copy
+
+    rw = ref.fc
+    rw.apply_gating_logic()
+    m = rw._module_to_wrap
+    qi, qo, qw = rw.input_quantizers[0], rw.output_quantizers[0], rw.param_quantizers["weight"]
+    calls = []   # (pre-quantization output, its quantized tensor) per call
+
+    def lg(t, name, q):
+        return LearnedGridQuantizeDequantize.apply(t, getattr(rw, name + "_encoding_min"),
+                                                   getattr(rw, name + "_encoding_max"), q.bitwidth,
+                                                   q.use_symmetric_encodings, q.use_strict_symmetric,
+                                                   q.is_unsigned_symmetric, q.channel_axis)
+
+    def call(t):
+        if qi.enabled:
+            t = lg(t, "input0", qi)
+        out = F.linear(t, lg(m.weight, "weight", qw), m.bias)
+        y = lg(out, "output0", qo)
+        y.retain_grad()
+        calls.append((out.detach(), y))
+        return y
+    loss_ref = call(F.relu(call(x))).square().mean()
+    loss_ref.backward()
+    assert float(loss.detach()) == float(loss_ref.detach())
+    got = dict(sim.model.named_parameters())
+    for name, p in ref.named_parameters():
+        if p.grad is None:
+            assert got[name].grad is None, name
+        else:
+            torch.testing.assert_close(got[name].grad, p.grad, rtol=0, atol=0, msg=name)
+    emin, emax = rw.output0_encoding_min.detach(), rw.output0_encoding_max.detach()
+    want_min, want_max = torch.zeros_like(emin), torch.zeros_like(emax)
+    for out, y in calls:
+        _, gmin, gmax = T.lg_gradients(out, y.grad, emin, emax, qo.bitwidth, qo.use_symmetric_encodings)
+        want_min, want_max = want_min + gmin, want_max + gmax
+    torch.testing.assert_close(got["fc.output0_encoding_min"].grad, want_min, rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(got["fc.output0_encoding_max"].grad, want_max, rtol=1e-4, atol=1e-7)
