@@ -28,6 +28,7 @@ iterations run are the first 1/world of it). In the HIP-graph form the iteration
 the collective between them: [forward + backward] -> all_reduce(alpha.grad) -> [/ world + Adam].
 """
 import contextlib
+import logging
 import os
 import warnings
 from dataclasses import dataclass
@@ -44,6 +45,7 @@ from aimet_amd.adaround import AdaroundFunction, compute_beta, init_alpha
 from aimet_amd.tensor_quantizer import per_channel_view
 
 BATCH_SIZE = 32   # adaround_optimizer.py:58
+_log = logging.getLogger("aimet_amd.adaround")
 
 
 @dataclass
@@ -244,10 +246,116 @@ def _reduce_grad(grad, world, group, divide=True):
         grad.div_(world)
 
 
+def _starting_alpha(w, d, shape, alpha_init):
+    """The optimised alpha: a float32 copy of the caller's (an AdaroundWrapper's parameter) or
+    init_alpha of the weight (_generate_alpha_parameter, adaround_wrapper.py:211-224)."""
+    if alpha_init is not None:
+        if alpha_init.shape != w.shape:
+            raise ValueError("alpha has shape %s, the weight %s" % (tuple(alpha_init.shape), tuple(w.shape)))
+        return torch.nn.Parameter(alpha_init.detach().to(w.device, torch.float32).contiguous().clone(),
+                                  requires_grad=True)
+    return init_alpha(w, d.view(shape) if d.numel() > 1 else d)
+
+
+def _finish_alpha(alpha, alpha_init):
+    """The optimised values written back into the caller's alpha (returned), else alpha."""
+    if alpha_init is None:
+        return alpha
+    with torch.no_grad():
+        alpha_init.copy_(alpha.detach())
+    return alpha_init
+
+
 class AdaroundOptimizer:
     """v1/adaround/adaround_optimizer.py."""
 
     last_loop_form = None   # the layer form the last fused loop ran (dw / pointwise / linear / autograd)
+    is_activation_caching_enabled = True
+
+    # ---- the reference's caller surface (v1/adaround/adaround_optimizer.py:69-260) -------------
+    @classmethod
+    def adaround_module(cls, module: torch.nn.Module, quant_module, orig_model: torch.nn.Module,
+                        quant_model: torch.nn.Module, act_func, cached_dataset, forward_fn,
+                        opt_params: AdaroundHyperParameters, cached_quant_dataset=None):
+        """adaround_optimizer.py:69-113: the reconstruction metrics before / after (debug log),
+        the rounding optimisation of `quant_module` (an AdaroundWrapper), then hard rounding."""
+        from aimet_amd.activation_sampler import ActivationSampler
+        from aimet_amd.adaround_wrapper import AdaroundWrapper
+        assert isinstance(quant_module, AdaroundWrapper), "%s is not adaround wrapper module." % quant_module
+        sampler = ActivationSampler(module, quant_module, orig_model, quant_model, forward_fn)
+        if cached_quant_dataset:
+            inp_data, _ = sampler.sample_acts(cached_quant_dataset[0], collect_input=True, collect_output=False)
+            _, out_data = sampler.sample_acts(cached_dataset[0], collect_input=False, collect_output=True)
+        else:
+            inp_data, out_data = sampler.sample_acts(cached_dataset[0])
+        hard, soft = cls._compute_recons_metrics(quant_module, act_func, inp_data, out_data)
+        _log.debug("Before opt, Recons. error metrics using soft rounding=%f and hard rounding=%f", soft, hard)
+        cls._optimize_rounding(module, quant_module, orig_model, quant_model, act_func, cached_dataset, forward_fn,
+                               opt_params, cached_quant_dataset)
+        hard, soft = cls._compute_recons_metrics(quant_module, act_func, inp_data, out_data)
+        _log.debug("After opt, Recons. error metrics using soft rounding=%f and hard rounding=%f", soft, hard)
+        quant_module.use_soft_rounding = False
+
+    @classmethod
+    def _optimize_rounding(cls, module: torch.nn.Module, quant_module, orig_model: torch.nn.Module,
+                           quant_model: torch.nn.Module, act_func, cached_dataset, forward_fn,
+                           opt_params: AdaroundHyperParameters, cached_quant_dataset=None):
+        """adaround_optimizer.py:115-221 over the fused loop (optimize_rounding): the cached
+        dataset sharded by batch rank::world as the reference's Subset, every batch's layer input
+        (QuantSim model) and output (original model) sampled into HBM, then num_iterations // world
+        iterations of Adam (lr 1e-3 x world) on quant_module.alpha with batches of 32 drawn by
+        torch.randperm from the global generator, alpha.grad all-reduced / world."""
+        from aimet_amd.activation_sampler import ActivationSampler
+        from aimet_amd.adaround_wrapper import AdaroundWrapper
+        rank, world = _group_world(None)
+        indices = range(rank, len(cached_dataset), world)
+        shard = [cached_dataset[i] for i in indices]
+        shard_q = [cached_quant_dataset[i] for i in indices] if cached_quant_dataset is not None else None
+        assert isinstance(quant_module, AdaroundWrapper), "%s is not adaround wrapper module." % quant_module
+        assert quant_module.use_soft_rounding, "optimization should use soft rounding only."
+        assert quant_module.alpha is not None, "alpha parameter should be initialized."
+        original = quant_module.get_original_module()
+        device = original.weight.device
+        sampler = ActivationSampler(module, quant_module, orig_model, quant_model, forward_fn)
+        inp_data, out_data = sampler.sample_all_acts(shard, shard_q, device=device)
+        cls.optimize_rounding(original, inp_data, out_data, quant_module._delta_vec.to(device),
+                              quant_module._offset_vec.to(device), quant_module.bitwidth, quant_module._ch_axis,
+                              opt_params, act_func, generator=None, alpha=quant_module.alpha, presharded=True)
+
+    @classmethod
+    def _compute_recons_metrics(cls, quant_module, act_func, inp_data: torch.Tensor,
+                                out_data: torch.Tensor) -> Tuple[float, float]:
+        """adaround_optimizer.py:223-255: (MSE with hard rounding, MSE with soft rounding)."""
+        with torch.no_grad():
+            quant_module.use_soft_rounding = False
+            out_hard = cls._compute_output_with_adarounded_weights(quant_module, inp_data)
+            quant_module.use_soft_rounding = True
+            out_soft = cls._compute_output_with_adarounded_weights(quant_module, inp_data)
+            if act_func is not None:
+                out_data, out_soft, out_hard = act_func(out_data), act_func(out_soft), act_func(out_hard)
+            return float(F.mse_loss(out_hard, out_data)), float(F.mse_loss(out_soft, out_data))
+
+    @staticmethod
+    def _compute_output_with_adarounded_weights(quant_module, inp_data: torch.Tensor):
+        """adaround_optimizer.py:257-286."""
+        module = quant_module.get_original_module()
+        quant_module.to(inp_data.device)
+        if not isinstance(module, (torch.nn.Conv2d, torch.nn.ConvTranspose2d, torch.nn.Linear)):
+            raise ValueError("AdaRound is not supported for the module: ", module)
+        weight = quant_module.apply_adaround(quant_module.weight)
+        if isinstance(module, torch.nn.Conv2d):
+            return F.conv2d(inp_data, weight, bias=module.bias, stride=module.stride, dilation=module.dilation,
+                            padding=module.padding, groups=module.groups)
+        if isinstance(module, torch.nn.ConvTranspose2d):
+            return F.conv_transpose2d(inp_data, weight, bias=module.bias, stride=module.stride,
+                                      padding=module.padding, output_padding=module.output_padding,
+                                      groups=module.groups, dilation=module.dilation)
+        return F.linear(inp_data, weight, bias=module.bias)
+
+    @staticmethod
+    def enable_caching_acts_data() -> bool:
+        """adaround_optimizer.py:340-349: the samples are always cached here (in HBM)."""
+        return AdaroundOptimizer.is_activation_caching_enabled
 
     @staticmethod
     def optimize_rounding(module: torch.nn.Module, inp_data: torch.Tensor, out_data: torch.Tensor,
@@ -255,7 +363,8 @@ class AdaroundOptimizer:
                           opt_params: AdaroundHyperParameters = AdaroundHyperParameters(),
                           act_func: Optional[Callable] = None, generator: Optional[torch.Generator] = None,
                           round_loss_out: Optional[torch.Tensor] = None, use_graph: bool = True,
-                          group=None) -> torch.nn.Parameter:
+                          group=None, alpha: Optional[torch.Tensor] = None,
+                          presharded: bool = False) -> torch.nn.Parameter:
         """Optimises alpha for `module` on the cached activations (inp_data / out_data: [N, ...] on
         the device); returns alpha. delta / offset: the weight quantizer's (per-channel) encoding.
 
@@ -265,14 +374,19 @@ class AdaroundOptimizer:
         its capturable form); the loop is launch-bound for MobileNet-sized layers.
 
         group: the process group to run data parallel over (default: the default group when
-        torch.distributed is initialised); see the module docstring."""
+        torch.distributed is initialised); see the module docstring.
+
+        alpha: the starting alpha (an AdaroundWrapper's parameter, adaround_wrapper.py:211-224);
+        it is updated in place and returned. Default: init_alpha of the weight.
+        presharded: inp_data / out_data already hold only this rank's samples (adaround_module
+        shards the cached dataset by batch, as the reference does)"""
         rank, world = _group_world(group)
-        if world > 1:
+        if world > 1 and not presharded:
             # adaround_optimizer.py:147-150: this rank's shard of the cached samples
             shard = torch.arange(rank, inp_data.shape[0], world, device=inp_data.device)
             inp_data, out_data = inp_data.index_select(0, shard), out_data.index_select(0, shard)
         args = (module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func, generator,
-                round_loss_out, world, group)
+                round_loss_out, world, group, alpha)
         if opt_params.num_iterations // world == 0:
             # fewer iterations than ranks (or none): the loop runs zero times and alpha keeps its
             # initial value, as the reference's range() loop does -- no batch draw, no capture
@@ -297,14 +411,14 @@ class AdaroundOptimizer:
 
     @staticmethod
     def _optimize_eager(module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func,
-                        generator, round_loss_out, world=1, group=None):
+                        generator, round_loss_out, world=1, group=None, alpha_init=None):
         w = module.weight.detach()
         dev = w.device
         shape = [1] * w.dim()
         shape[ch_axis] = -1
         d = torch.as_tensor(delta, dtype=torch.float32, device=dev).reshape(-1)
         o = torch.as_tensor(offset, dtype=torch.float32, device=dev).reshape(-1)
-        alpha = init_alpha(w, d.view(shape) if d.numel() > 1 else d)
+        alpha = _starting_alpha(w, d, shape, alpha_init)
         # one Adam kernel per step (the reference's default multi-tensor Adam: same update rule); the
         # learning rate scaled by the world size (adaround_optimizer.py:155-158)
         lr = 1e-3 * world
@@ -332,7 +446,7 @@ class AdaroundOptimizer:
             if world > 1:
                 _reduce_grad(alpha.grad, world, group)
             optimizer.step()
-        return alpha
+        return _finish_alpha(alpha, alpha_init)
 
     @staticmethod
     def _drawer(generator, n, iters, dev):
@@ -363,7 +477,7 @@ class AdaroundOptimizer:
 
     @staticmethod
     def _optimize_fused_graph(module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func,
-                              generator, round_loss_out):
+                              generator, round_loss_out, alpha_init=None):
         """Single-process HIP-graph loop with the iteration's bookkeeping fused into two kernels:
         aimet_adaround_gather (the batch draw: index lookup + both row gathers, for the four
         index_select kernels) and aimet_adaround_backward_adam (dL/dalpha + torch's fused-Adam
@@ -376,7 +490,7 @@ class AdaroundOptimizer:
         shape[ch_axis] = -1
         d = torch.as_tensor(delta, dtype=torch.float32, device=dev).reshape(-1).contiguous()
         o = torch.as_tensor(offset, dtype=torch.float32, device=dev).reshape(-1).contiguous()
-        alpha = init_alpha(w, d.view(shape) if d.numel() > 1 else d)
+        alpha = _starting_alpha(w, d, shape, alpha_init)
         sq = _BoundSoftQuant(w, alpha, d, o, bitwidth, ch_axis, round_loss_out)
         iters, n = opt_params.num_iterations, inp_data.shape[0]
         nb = min(n, BATCH_SIZE)
@@ -564,21 +678,22 @@ class AdaroundOptimizer:
                 graph.replay()
         torch.cuda.current_stream(dev).synchronize()
         del staged
-        return alpha
+        return _finish_alpha(alpha, alpha_init)
 
     @staticmethod
     def _optimize_graphed(module, inp_data, out_data, delta, offset, bitwidth, ch_axis, opt_params, act_func,
-                          generator, round_loss_out, world=1, group=None, fused_step=True):
+                          generator, round_loss_out, world=1, group=None, alpha_init=None, fused_step=True):
         if world == 1 and fused_step:
             return AdaroundOptimizer._optimize_fused_graph(module, inp_data, out_data, delta, offset, bitwidth,
-                                                           ch_axis, opt_params, act_func, generator, round_loss_out)
+                                                           ch_axis, opt_params, act_func, generator, round_loss_out,
+                                                           alpha_init)
         w = module.weight.detach()
         dev = w.device
         shape = [1] * w.dim()
         shape[ch_axis] = -1
         d = torch.as_tensor(delta, dtype=torch.float32, device=dev).reshape(-1)
         o = torch.as_tensor(offset, dtype=torch.float32, device=dev).reshape(-1)
-        alpha = init_alpha(w, d.view(shape) if d.numel() > 1 else d)
+        alpha = _starting_alpha(w, d, shape, alpha_init)
         lr = 1e-3 * world
         try:
             optimizer = torch.optim.Adam([alpha], lr=lr, capturable=True, fused=True)
@@ -675,7 +790,7 @@ class AdaroundOptimizer:
                 replay()
         torch.cuda.current_stream(dev).synchronize()
         sq.reg_beta = None
-        return alpha
+        return _finish_alpha(alpha, alpha_init)
 
     @staticmethod
     def hard_rounded_weight(module: torch.nn.Module, alpha: torch.Tensor, delta, offset, bitwidth: int,

@@ -33,7 +33,6 @@ namespace
 constexpr int kWaves      = kBlock / 64;
 constexpr int kHistUnroll = 4;
 constexpr int kHistGrid   = 2048;   // 8 workgroups per CU: enough 16-B loads in flight for HBM
-constexpr int64_t kHistLargeN = int64_t(1) << 27;
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ float wave_min(float v)
@@ -399,16 +398,25 @@ struct BinnerOf<true>
 
 // per-tensor: many workgroups over one tensor, atomics into counts[0][:]. One workgroup's share
 // (block `blk` of `nblk`) of the pass over x[0, n).
-template <int BLOCK, bool ENT>
+//
+// The workgroup's LDS histogram is [bin][32]: lane l adds into column l & 31, so the 32 lanes that
+// a ds_add_u32 services together always address 32 different banks. With one [512] histogram per
+// wave, bins of ordinary activations (a few dozen bins around the bulk) put ~4 lanes on one bank
+// per group -- 73% of the kernel's LDS cycles were bank-conflict cycles on ViT-L/16's activations
+// (profiles/r03/vit_pmc_sq.txt) -- and lanes adding to one bin serialise. The columns of a bin are
+// folded once, when the workgroup ends.
+// COLS = 16 halves the LDS (32 KiB, more workgroups per CU): lanes l and l + 16 then share a
+// column, a conflict only when their bins have the same parity.
+template <int BLOCK, bool ENT, int COLS = 32>
 __device__ __forceinline__ void histogram_part(const float* __restrict__ x, int64_t n, int vec, int64_t blk,
                                                int64_t nblk, const TqDevice& d)
 {
-    constexpr int kWaves = BLOCK / 64;
-    __shared__ uint32_t lds[kWaves][kPdfSize];
+    constexpr int kHistCols = COLS;
+    __shared__ uint32_t lds[kPdfSize * kHistCols];   // 64 KiB (32 columns)
     typename BinnerOf<ENT>::type bn {d.bin_bucket[0], d.bin_offset[0]};
-    const int w = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < kWaves * kPdfSize; i += BLOCK)
-        (&lds[0][0])[i] = 0;
+    const uint32_t col = threadIdx.x & (kHistCols - 1);
+    for (int i = threadIdx.x; i < kPdfSize * kHistCols / 4; i += BLOCK)
+        reinterpret_cast<uint4*>(lds)[i] = make_uint4(0, 0, 0, 0);
     __syncthreads();
     const int zbin = bn.bin(0.0f);
     uint32_t zc    = 0;
@@ -420,7 +428,7 @@ __device__ __forceinline__ void histogram_part(const float* __restrict__ x, int6
         }
         int b = bn.bin(v);
         if (b >= 0)
-            atomicAdd(&lds[w][b], 1u);
+            atomicAdd(&lds[b * kHistCols + col], 1u);
     };
     int64_t done = 0;
     if (vec)
@@ -459,26 +467,32 @@ __device__ __forceinline__ void histogram_part(const float* __restrict__ x, int6
         add(x[i]);
     zc = wave_sum(zc);
     if ((threadIdx.x & 63) == 0 && zbin >= 0 && zc)
-        atomicAdd(&lds[w][zbin], zc);
+        atomicAdd(&lds[zbin * kHistCols + col], zc);
     __syncthreads();
     for (int b = threadIdx.x; b < kPdfSize; b += BLOCK)
     {
+        // the bin's 32 columns as 8 16-B reads, started at a lane-dependent quarter so that the
+        // 16 lanes of a ds_read_b128 group spread over the banks
+        const uint4* row = reinterpret_cast<const uint4*>(lds + b * kHistCols);
         uint32_t s = 0;
 #pragma unroll
-        for (int i = 0; i < kWaves; ++i)
-            s += lds[i][b];
+        for (int j = 0; j < kHistCols / 4; ++j)
+        {
+            const uint4 q = row[(j + b) & (kHistCols / 4 - 1)];
+            s += q.x + q.y + q.z + q.w;
+        }
         if (s)
             atomicAdd(&d.counts[b], (unsigned long long) s);
     }
 }
 
-template <int BLOCK, bool ENT>
+template <int BLOCK, bool ENT, int COLS>
 __global__ __launch_bounds__(BLOCK) void histogram_tensor_kernel(const float* __restrict__ x, int64_t n, int vec,
                                                                  TqDevice d)
 {
     if (!BinnerOf<ENT>::live(d, 0))
         return;
-    histogram_part<BLOCK, ENT>(x, n, vec, blockIdx.x, gridDim.x, d);
+    histogram_part<BLOCK, ENT, COLS>(x, n, vec, blockIdx.x, gridDim.x, d);
 }
 
 // per-channel: one workgroup per channel, counts written directly
@@ -720,6 +734,26 @@ __global__ __launch_bounds__(kBlock) void minmax_walk_kernel(const StatsJob* __r
         // PDF schemes take min/max on the first (non-zero) batch only
         skip = J.hist && !J.ent && J.d.pdf_init[0];
     };
+    // the first quantizer after `from` that is not skipped (njobs if none): 64 job entries per
+    // round of parallel loads, instead of one dependent load per skipped quantizer (a later ViT-L/16
+    // batch, all 318 quantizers fixed, spent 417 us stepping through the table one job at a time)
+    auto next_live = [&](int from) {
+        const int lane = threadIdx.x & 63;
+        for (int base = from; base < njobs; base += 64)
+        {
+            const int j = base + lane;
+            bool live   = false;
+            if (j < njobs)
+            {
+                const StatsJob& J = jobs[j];
+                live              = !(J.hist && !J.ent && J.d.pdf_init[0]);
+            }
+            const unsigned long long m = __ballot(live);
+            if (m)
+                return base + (int) __builtin_ctzll(m);
+        }
+        return njobs;
+    };
     enter(ji);
     while (t < tiles)
     {
@@ -727,7 +761,15 @@ __global__ __launch_bounds__(kBlock) void minmax_walk_kernel(const StatsJob* __r
             enter(++ji);
         if (skip)
         {
-            t += (next_b0 - t + gridDim.x - 1) / gridDim.x * gridDim.x;
+            const int nj = next_live(ji + 1);
+            if (nj >= njobs)
+                break;
+            const uint32_t b0n = jobs[nj].mm_block0;   // > t: every tile before it is skipped
+            t += (b0n - t + gridDim.x - 1) / gridDim.x * gridDim.x;
+            if (t >= tiles)
+                break;
+            ji = nj;
+            enter(ji);
             continue;
         }
         const int64_t tile = t - b0;
@@ -792,7 +834,7 @@ __global__ __launch_bounds__(kBlock) void fold_minmax_many_kernel(const StatsJob
         fold_one(J.d, 0, !J.hist);
 }
 
-template <int BLOCK>
+template <int BLOCK, int COLS>
 __global__ __launch_bounds__(BLOCK) void histogram_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
 {
     const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, true)];
@@ -801,10 +843,10 @@ __global__ __launch_bounds__(BLOCK) void histogram_many_kernel(const StatsJob* _
     if (J.ent)
     {
         if (J.d.active[0])
-            histogram_part<BLOCK, true>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
+            histogram_part<BLOCK, true, COLS>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
     }
     else if (J.d.pdf_init[0])
-        histogram_part<BLOCK, false>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
+        histogram_part<BLOCK, false, COLS>(J.x, J.n, J.vec, blockIdx.x - J.h_block0, J.h_blocks, J.d);
 }
 
 __global__ __launch_bounds__(kPdfSize) void fold_histogram_many_kernel(const StatsJob* __restrict__ jobs)
@@ -1006,27 +1048,57 @@ void launch_fold_minmax(const TqDevice& d, int64_t C, StatsKind kind, hipStream_
     AIMET_LAUNCH_CHECK();
 }
 
+// histogram launch shape: BLOCK lanes per workgroup x COLS LDS columns (tools/studies:
+// AIMET_TUNE_HIST_SHAPE=<block>x<cols> for the single-tensor kernel, AIMET_TUNE_HIST_BLOCK /
+// AIMET_TUNE_HIST_COLS for the batched one; experiments only)
+struct HistShape
+{
+    int block, cols;
+};
+static HistShape hist_shape_env(const char* name, HistShape dflt)
+{
+    const char* e = getenv(name);
+    if (!e)
+        return dflt;
+    HistShape h {0, 0};
+    if (sscanf(e, "%dx%d", &h.block, &h.cols) != 2 || (h.block != 256 && h.block != 512 && h.block != 1024) ||
+        (h.cols != 8 && h.cols != 16 && h.cols != 32))
+        return dflt;
+    return h;
+}
+
+template <bool ENT>
+static void launch_hist_tensor(HistShape h, unsigned grid, const float* x, int64_t n, int vec, const TqDevice& d,
+                               hipStream_t s)
+{
+#define AIMET_HIST_T(B, C)                                                                                          \
+    if (h.block == B && h.cols == C)                                                                                \
+    {                                                                                                               \
+        histogram_tensor_kernel<B, ENT, C><<<grid, B, 0, s>>>(x, n, vec, d);                                        \
+        return;                                                                                                     \
+    }
+    AIMET_HIST_T(256, 8) AIMET_HIST_T(256, 16) AIMET_HIST_T(512, 8) AIMET_HIST_T(512, 16) AIMET_HIST_T(1024, 8)
+    AIMET_HIST_T(1024, 16) AIMET_HIST_T(1024, 32)
+#undef AIMET_HIST_T
+    histogram_tensor_kernel<1024, ENT, 16><<<grid, 1024, 0, s>>>(x, n, vec, d);
+}
+
 template <bool ENT>
 static void batch_histogram(const TqDevice& d, const float* x, int64_t outer, int64_t C, int64_t K, hipStream_t s)
 {
     bool al = (reinterpret_cast<uintptr_t>(x) & 15) == 0;
     if (C == 1)
     {
-        int64_t n  = outer * K;
-        // tools/hist_variants.hip: large tensors stream best with 8 x 256-lane workgroups per CU;
-        // below that the fixed per-workgroup cost (LDS clear + 512-bin flush into the global
-        // counters) dominates, and one 1024-lane workgroup per CU (16 wave-private copies) wins
-        if (n >= kHistLargeN)
-        {
-            int blocks = stream_blocks(n, (int64_t) 256 * kHistUnroll * 4 * 4);
-            histogram_tensor_kernel<256, ENT><<<blocks < kHistGrid ? blocks : kHistGrid, 256, 0, s>>>(x, n, al ? 1 : 0,
-                                                                                                     d);
-        }
-        else
-        {
-            int blocks = stream_blocks(n, (int64_t) 1024 * kHistUnroll * 4 * 2);
-            histogram_tensor_kernel<1024, ENT><<<blocks < 256 ? blocks : 256, 1024, 0, s>>>(x, n, al ? 1 : 0, d);
-        }
+        int64_t n = outer * K;
+        // workgroups of 1024 lanes sharing one [512][16] LDS histogram (32 KiB: two per CU), each
+        // a contiguous share of ~128 K elements, the grid capped at 2 per CU
+        static const HistShape h = hist_shape_env("AIMET_TUNE_HIST_SHAPE", HistShape {1024, 16});
+        const int64_t per = (int64_t) h.block * kHistUnroll * 4 * 8;
+        int64_t blocks    = ceil_div(n, per);
+        const int64_t cap = 256 * 2048 / h.block;
+        blocks            = blocks < 1 ? 1 : (blocks > cap ? cap : blocks);
+        launch_hist_tensor<ENT>(h, (unsigned) blocks, x, n, al ? 1 : 0, d, s);
+        AIMET_LAUNCH_CHECK();
     }
     else
     {
@@ -1068,10 +1140,21 @@ static int64_t hist_elems_per_block()
 static int hist_many_block()
 {
     static int v = [] {
-        // tools/hist_many_tune.py (ResNet-50 bs256, 55 tensors): 512 lanes 5.48 TB/s, 256 lanes 5.33
+        // 1024 lanes sharing one [512][16] LDS histogram (profiles/r03: ViT-L/16 later batches
+        // 2.8-2.9 ms vs 3.1-3.2 with 512 lanes and 4.7 with 512 lanes x 32 columns)
         const char* e = getenv("AIMET_TUNE_HIST_BLOCK");   // tuning experiments only
-        int b         = e ? atoi(e) : 512;
-        return (b == 256 || b == 1024) ? b : 512;
+        int b         = e ? atoi(e) : 1024;
+        return (b == 256 || b == 512) ? b : 1024;
+    }();
+    return v;
+}
+
+static int hist_many_cols()
+{
+    static int v = [] {
+        const char* e = getenv("AIMET_TUNE_HIST_COLS");   // tuning experiments only
+        const int c   = e ? atoi(e) : 16;
+        return (c == 8 || c == 32) ? c : 16;
     }();
     return v;
 }
@@ -1128,13 +1211,15 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
     }
     if ((phases & kPhaseHistogram) && hb > 0)
     {
-        const int hbk = hist_many_block();
-        if (hbk == 1024)
-            histogram_many_kernel<1024><<<(unsigned) hb, 1024, 0, s>>>(dj, n);
-        else if (hbk == 256)
-            histogram_many_kernel<256><<<(unsigned) hb, 256, 0, s>>>(dj, n);
-        else
-            histogram_many_kernel<512><<<(unsigned) hb, 512, 0, s>>>(dj, n);
+        const int hbk = hist_many_block(), hc = hist_many_cols();
+#define AIMET_HIST_M(B, C)                                                                                          \
+    if (hbk == B && hc == C)                                                                                        \
+        histogram_many_kernel<B, C><<<(unsigned) hb, B, 0, s>>>(dj, n);                                           \
+    else
+        AIMET_HIST_M(256, 8) AIMET_HIST_M(256, 16) AIMET_HIST_M(512, 8) AIMET_HIST_M(512, 16) AIMET_HIST_M(1024, 8)
+        AIMET_HIST_M(1024, 32)
+        histogram_many_kernel<1024, 16><<<(unsigned) hb, 1024, 0, s>>>(dj, n);
+#undef AIMET_HIST_M
         AIMET_LAUNCH_CHECK();
     }
     if (phases & kPhaseFoldHistogram)

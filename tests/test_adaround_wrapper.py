@@ -1,0 +1,186 @@
+"""The reference's AdaRound caller surface on the fused kernels:
+AdaroundWrapper (v1/adaround/adaround_wrapper.py:93-224) and
+AdaroundOptimizer.adaround_module (v1/adaround/adaround_optimizer.py:69-221).
+
+GPU: the wrapper built around a StaticGridQuantWrapper whose per-channel weight quantizer holds
+the golden case's delta / offset reproduces golden_adaround.npz (the reference's own
+apply_adaround) bit for bit -- Wq soft and hard, and dL/dalpha of the reconstruction term;
+adaround_module on a MobileNet-v2-shaped layer gives the alpha that optimize_rounding gives on the
+same sampled activations, bit for bit.
+CPU: ModuleData / ActivationSampler collection (hooks, early stop, dataset sharding order)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+from conftest import gpu_available
+
+gpu = pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+DEV = "cuda"
+PER_CHANNEL_CFG = {"defaults": {"ops": {"is_output_quantized": "True"},
+                                "params": {"is_quantized": "True", "is_symmetric": "True"},
+                                "strict_symmetric": "False", "per_channel_quantization": "True"}}
+
+
+def _module_for(w):
+    if w.ndim == 2:
+        m = nn.Linear(w.shape[1], w.shape[0])
+    else:
+        cin_g = w.shape[1]
+        groups = w.shape[0] if cin_g == 1 and w.shape[0] > 1 else 1
+        m = nn.Conv2d(cin_g * groups, w.shape[0], w.shape[2], padding=w.shape[2] // 2, groups=groups)
+    with torch.no_grad():
+        m.weight.copy_(torch.from_numpy(w))
+    return m
+
+
+def _encodings(delta, offset, bw):
+    from aimet_amd.libpymo import TfEncoding
+    out = []
+    for d, o in zip(delta.tolist(), offset.tolist()):
+        e = TfEncoding()
+        e.delta, e.offset, e.bw = d, o, bw
+        e.min = o * d
+        e.max = e.min + d * (2 ** bw - 1)
+        out.append(e)
+    return out
+
+
+def _wrapped(w, delta, offset, bw):
+    from aimet_amd.qc_quantize_op import StaticGridQuantWrapper
+    from aimet_amd.quantizers import QuantScheme, StaticGridPerChannelQuantizer
+    m = _module_for(w).to(DEV)
+    qw = StaticGridQuantWrapper(m, bw, 8, "nearest", QuantScheme.post_training_tf_enhanced)
+    q = StaticGridPerChannelQuantizer(bw, "nearest", QuantScheme.post_training_tf_enhanced, True, w.shape[0], True)
+    q.encoding = _encodings(delta, offset, bw)
+    qw.param_quantizers["weight"] = q
+    qw.param_quantizers["bias"].enabled = False   # as QuantSim's default config: weights only
+    return qw
+
+
+@pytest.mark.gpu
+@gpu
+def test_adaround_wrapper_reproduces_reference_apply_adaround(golden_dir):
+    from aimet_amd.adaround_wrapper import AdaroundWrapper
+    z = dict(np.load(os.path.join(golden_dir, "golden_adaround.npz")))
+    for i in range(int(z["count"])):
+        k = "c%d_" % i
+        w, bw = z[k + "w"], int(z[k + "bw"])
+        ada = AdaroundWrapper(_wrapped(w, z[k + "delta"], z[k + "offset"], bw))
+        # makeDeltaOffsetTensor -> the fixture's float32 delta / offset, broadcast along axis 0
+        assert ada.broadcasted_delta.shape == (w.shape[0],) + (1,) * (w.ndim - 1)
+        assert np.array_equal(ada.broadcasted_delta.reshape(-1).cpu().numpy(), z[k + "delta"])
+        assert np.array_equal(ada.broadcasted_offset.reshape(-1).cpu().numpy(), z[k + "offset"])
+        assert (ada.bitwidth, ada.clip_min, ada.clip_max, ada.use_soft_rounding) == (bw, 0, 2 ** bw - 1, True)
+        with torch.no_grad():
+            ada.alpha.copy_(torch.from_numpy(z[k + "alpha"]))
+        weight = ada.weight
+        wq = ada.apply_adaround(weight)
+        assert np.array_equal(wq.detach().cpu().numpy().view(np.int32), z[k + "wq"].view(np.int32)), i
+        (wq * torch.from_numpy(z[k + "grad"]).to(DEV)).sum().backward()
+        assert np.array_equal(ada.alpha.grad.cpu().numpy().view(np.int32), z[k + "ga_recon"].view(np.int32)), i
+        ada.use_soft_rounding = False
+        with torch.no_grad():
+            wh = ada.apply_adaround(weight)
+        assert np.array_equal(wh.cpu().numpy().view(np.int32), z[k + "wq_hard"].view(np.int32)), i
+        # forward: the wrapped module with the adarounded weight, its weight quantizer off for the
+        # call only and the original Parameter back in place afterwards
+        x = torch.randn((2, w.shape[1]) if w.ndim == 2 else (2, ada.get_original_module().in_channels, 6, 6),
+                        device=DEV)
+        ada.module_to_wrap.output_quantizers[0].enabled = False
+        with torch.no_grad():
+            y = ada(x)
+            m = ada.get_original_module()
+            want = nn.functional.linear(x, wh, m.bias) if w.ndim == 2 else \
+                nn.functional.conv2d(x, wh, m.bias, m.stride, m.padding, m.dilation, m.groups)
+        assert torch.equal(y, want), i
+        assert ada.module_to_wrap.param_quantizers["weight"].enabled
+        assert isinstance(m.weight, nn.Parameter) and "weight" not in m.__dict__
+
+
+class Block(nn.Module):
+    """A MobileNet-v2 inverted-residual slice: pointwise expand -> depthwise -> pointwise project."""
+    def __init__(self):
+        super().__init__()
+        self.expand = nn.Conv2d(16, 96, 1, bias=False)
+        self.relu1 = nn.ReLU6()
+        self.dw = nn.Conv2d(96, 96, 3, padding=1, groups=96, bias=False)
+        self.relu2 = nn.ReLU6()
+        self.project = nn.Conv2d(96, 24, 1, bias=False)
+
+    def forward(self, x):
+        return self.project(self.relu2(self.dw(self.relu1(self.expand(x)))))
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("layer,act", [("expand", nn.ReLU6()), ("dw", nn.ReLU6()), ("project", None)])
+def test_adaround_module_equals_optimize_rounding(layer, act):
+    """adaround_module(module, quant_module, orig_model, quant_model, act_func, cached_dataset,
+    forward_fn, opt_params) == optimize_rounding on the activations it samples, bit for bit; the
+    wrapper ends in hard rounding."""
+    from aimet_amd.activation_sampler import ActivationSampler
+    from aimet_amd.adaround_optimizer import AdaroundHyperParameters, AdaroundOptimizer
+    from aimet_amd.adaround_wrapper import AdaroundWrapper
+    from aimet_amd.quantsim import QuantizationSimModel
+    torch.manual_seed(0)
+    orig = Block().to(DEV).eval()
+    g = torch.Generator().manual_seed(1)
+    data = [torch.rand(8, 16, 14, 14, generator=g).to(DEV) for _ in range(6)]
+    sim = QuantizationSimModel(Block().to(DEV).eval(), config_file=PER_CHANNEL_CFG, default_param_bw=4)
+    for (n, p), (_, q) in zip(orig.named_parameters(), sim.model.named_parameters()):
+        with torch.no_grad():
+            q.copy_(p)
+    sim.compute_encodings(lambda m, d: [m(x) for x in d], data[:2])
+    ada = AdaroundWrapper(getattr(sim.model, layer))
+    setattr(sim.model, layer, ada)
+    params = AdaroundHyperParameters(num_iterations=120, warm_start=0.25)
+    forward_fn = lambda m, x: m(x)   # noqa: E731
+    alpha0 = ada.alpha.detach().clone()
+    torch.manual_seed(7)
+    AdaroundOptimizer.adaround_module(getattr(orig, layer), ada, orig, sim.model, act, data, forward_fn, params)
+    assert not ada.use_soft_rounding
+    # the same loop called directly on the same samples and the same randperm stream
+    sampler = ActivationSampler(getattr(orig, layer), ada, orig, sim.model, forward_fn)
+    ada.use_soft_rounding = True
+    inp, out = sampler.sample_all_acts(data, device=torch.device(DEV))
+    torch.manual_seed(7)
+    want = AdaroundOptimizer.optimize_rounding(ada.get_original_module(), inp, out, ada._delta_vec.to(DEV),
+                                               ada._offset_vec.to(DEV), ada.bitwidth, ada._ch_axis, params, act,
+                                               alpha=alpha0.clone())
+    assert torch.equal(ada.alpha.detach(), want.detach())
+    assert not torch.equal(alpha0, want.detach())   # it did optimise
+
+
+# ------------------------------------------------------------------------------------------
+# CPU: activation collection
+# ------------------------------------------------------------------------------------------
+def test_module_data_collects_and_stops_early():
+    from aimet_amd.activation_sampler import ModuleData
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(4, 6), nn.ReLU(), nn.Linear(6, 3))
+    ran = []
+    net[2].register_forward_hook(lambda m, i, o: ran.append(1))
+    x = torch.randn(5, 4)
+    inp, out = ModuleData(net, net[0]).collect_inp_out_data(x, collect_input=True, collect_output=True)
+    assert torch.equal(inp, x) and torch.equal(out, net[0](x).detach())
+    assert not ran                                     # the forward stopped at the layer
+    inp, out = ModuleData(net, net[2], lambda m, d: m(d[0])).collect_inp_out_data([x], False, True)
+    assert inp is None and torch.equal(out, net(x).detach())
+    assert net.training                                # eval mode only for the collection
+
+
+def test_activation_sampler_concatenates_batches():
+    from aimet_amd.activation_sampler import ActivationSampler
+    torch.manual_seed(0)
+    orig = nn.Sequential(nn.Linear(4, 6), nn.ReLU(), nn.Linear(6, 3))
+    quant = nn.Sequential(nn.Linear(4, 6), nn.ReLU(), nn.Linear(6, 3))
+    data = [torch.randn(2, 4) for _ in range(3)]
+    s = ActivationSampler(orig[2], quant[2], orig, quant, None)
+    inp, out = s.sample_and_place_all_acts_on_cpu(data)
+    assert inp.shape == (6, 6) and out.shape == (6, 3)
+    with torch.no_grad():
+        assert torch.equal(inp, torch.cat([quant[1](quant[0](d)) for d in data]))
+        assert torch.equal(out, torch.cat([orig(d) for d in data]))
