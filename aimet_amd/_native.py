@@ -154,6 +154,7 @@ _PROTOTYPES = {
     "aimet_lg_gate_ranges": [_vp, _vp, _vp, ctypes.c_int, _vp],
     "aimet_lg_encodings": [_vp, _vp, _i64, _int, _int, _int, _int, _vp, _vp, _vp],
     "aimet_lg_range_grads": [_vp, _vp, _vp, _vp, _i64, ctypes.c_float, _int, _vp, _vp, _vp],
+    "aimet_lg_set_chunk_limit": [_i64],
     "aimet_lg_forward_range": [_vp, _vp, _i64, _i64, _i64, _int, _vp, _vp, _int, _int, _int, _int, _vp, _vp, _vp, _vp],
     "aimet_lg_forward_16_range": [_vp, _vp, _i64, _int, _vp, _vp, _int, _int, _int, _int, _vp, _vp, _vp, _vp],
     "aimet_lg_forward_cast": [_vp, _vp, _i64, _i64, _i64, _int, _vp, _vp, ctypes.c_float, _vp],

@@ -13,6 +13,7 @@
 // symmetric:  grad_max = (A - B) / floor(steps/2), grad_min = -grad_max
 // (assembled from the C-vectors on the torch side). Float32; torch.round = round-half-even.
 #include "common.hpp"
+#include <atomic>
 #include <cmath>
 #include "io16.hpp"
 
@@ -37,12 +38,79 @@ struct LgChannel
     }
 };
 
-// x_round = round(x / delta) - offset ; x_quant = clamp(x_round, 0, steps) ; y = (x_quant + offset) * delta
-__device__ __forceinline__ float lg_qdq(float x, float d, float o, float steps)
+// The quotient RN(x / d) without the IEEE division's ~10 instructions. y = lg_recip(d) = RN(1/d)
+// is computed once per encoding; then q0 = RN(x * y) is a faithful quotient, r = x - d * q0 is
+// exact (fma), and RN(q0 + r * y) is the correctly rounded quotient (Markstein's theorem) while
+// nothing under- or overflows: |d| in [2^-40, 2^40] (else y = NaN) and |q| in [2^-60, 2^60), so
+// |x| and r stay far from the subnormal range. A zero x takes q0 (= +-0 with the quotient's sign);
+// every other element -- and every non-finite one -- takes the IEEE division. Bit-identical to
+// x / d: tools/studies/markstein_div_check.c (754 M operand pairs, quotients at half-integers +-3
+// ulp and all-ones mantissas included; the same bounds fail only for |x| < 2^-100). 3 VALU plus a
+// range test per element instead of ~10 (the 16-bit kernels were VALU co-bound).
+__device__ __forceinline__ float lg_recip(float d)
 {
-    float xr = __builtin_rintf(x / d) - o;
+    const float a = __builtin_fabsf(d);
+    return (a >= 0x1p-40f && a <= 0x1p40f) ? 1.0f / d : __builtin_nanf("");
+}
+__device__ __forceinline__ float div_rn(float x, float d, float y)
+{
+    const float q0 = x * y;
+    const float r  = __builtin_fmaf(-q0, d, x);
+    const float q  = __builtin_fmaf(r, y, q0);
+    if ((__float_as_uint(q) & 0x7fffffffu) - 0x21800000u < 0x5d800000u - 0x21800000u)   // |q| in [2^-60, 2^60)
+        return q;
+    if (x == 0.0f && y == y)
+        return q0;
+    return x / d;
+}
+
+// div_rn over N independent elements with ONE branch to the division for the rare elements it does
+// not cover: the N quotient chains interleave (a branch per element serialised them)
+template <int N>
+__device__ __forceinline__ void div_rn_n(const float* x, float d, float y, float* q)
+{
+    uint32_t slow = 0;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+    {
+        const float q0  = x[k] * y;
+        const float r   = __builtin_fmaf(-q0, d, x[k]);
+        const float qm  = __builtin_fmaf(r, y, q0);
+        const bool zero = x[k] == 0.0f;
+        const bool ok   = ((__float_as_uint(qm) & 0x7fffffffu) - 0x21800000u < 0x5d800000u - 0x21800000u) ||
+                        (zero && y == y);
+        q[k] = zero ? q0 : qm;
+        slow |= ok ? 0u : (1u << k);
+    }
+    if (slow)
+    {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            if (slow & (1u << k))
+                q[k] = x[k] / d;
+    }
+}
+
+// x_round = round(x / delta) - offset ; x_quant = clamp(x_round, 0, steps) ; y = (x_quant + offset) * delta
+// (rd = lg_recip(d))
+__device__ __forceinline__ float lg_qdq(float x, float d, float o, float steps, float rd)
+{
+    float xr = __builtin_rintf(div_rn(x, d, rd)) - o;
     float xq = fminf(fmaxf(xr, 0.0f), steps);
     return (xq + o) * d;
+}
+template <int N>
+__device__ __forceinline__ void lg_qdq_n(const float* x, float d, float o, float steps, float rd, float* y)
+{
+    float q[N];
+    div_rn_n<N>(x, d, rd, q);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+    {
+        float xr = __builtin_rintf(q[k]) - o;
+        float xq = fminf(fmaxf(xr, 0.0f), steps);
+        y[k]     = (xq + o) * d;
+    }
 }
 
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
@@ -148,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict_
             if (q0 + u * kBlock < nq)
                 v[u] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q0 + u * kBlock);
         uint32_t pc = 0xffffffffu;
-        float d = 0.0f, o = 0.0f;
+        float d = 0.0f, o = 0.0f, rd = 0.0f;
 #pragma unroll
         for (int u = 0; u < Q; ++u)
         {
@@ -159,13 +227,13 @@ __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict_
             if (c != pc)
             {
                 enc.get(c, q * 4, delta, offset, d, o);
+                rd = lg_recip(d);
                 pc = c;
             }
-            f4 r;
-            r.x = lg_qdq(v[u].x, d, o, steps);
-            r.y = lg_qdq(v[u].y, d, o, steps);
-            r.z = lg_qdq(v[u].z, d, o, steps);
-            r.w = lg_qdq(v[u].w, d, o, steps);
+            const float xin[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+            float yo[4];
+            lg_qdq_n<4>(xin, d, o, steps, rd, yo);
+            const f4 r = {yo[0], yo[1], yo[2], yo[3]};
             lg_store4<OUT>(y, q, r);
         }
     }
@@ -177,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict_
         uint32_t c = map.channel(t);
         float d, o;
         enc.get(c, t, delta, offset, d, o);
-        const float r = lg_qdq(x[t], d, o, steps);
+        const float r = lg_qdq(x[t], d, o, steps, lg_recip(d));
         if constexpr (OUT == IO_F32)
             static_cast<float*>(y)[t] = r;
         else
@@ -230,18 +298,12 @@ struct Sums
     float a, b, d;
 };
 
-// q = x / dl from the reciprocal (rcp = v_rcp_f32(dl), within 1 ulp): |q - RN(x/dl)| <= 3.5 ulp(q).
-// rint(q) equals rint of the IEEE quotient unless a half-integer lies within 2^-21 (|q| + 1) of q
-// (ties-to-even only acts exactly on half-integers); then -- and for non-finite q -- the division
-// decides. The returned quotient feeds only the tolerance-checked sum B.
+// rint(RN(x / dl)) and q = RN(x / dl) itself (div_rn, rcp = lg_recip(dl)): the quotient is the
+// reference's x / delta bit for bit, so each term of sum B is the reference's
+// mask * (x / delta) * grad.
 __device__ __forceinline__ float rint_div(float x, float dl, float rcp, float& q)
 {
-    q               = x * rcp;
-    const float h   = q - __builtin_floorf(q);
-    const float thr = (__builtin_fabsf(q) + 1.0f) * 4.76837158203125e-7f;   // 2^-21
-    if (__builtin_fabsf(h - 0.5f) > thr)                                     // false for NaN / inf
-        return __builtin_rintf(q);
-    q = x / dl;
+    q = div_rn(x, dl, rcp);
     return __builtin_rintf(q);
 }
 
@@ -256,6 +318,26 @@ __device__ __forceinline__ void lg_bwd_elem(float x, float g, float dl, float o,
     s.a += (xq + o) * g;
     s.b += mask ? q * g : 0.0f;
     s.d += mask ? 0.0f : g;
+}
+
+// lg_bwd_elem over N elements in order (the same sums), the quotients by div_rn_n
+template <int N>
+__device__ __forceinline__ void lg_bwd_elems(const float* x, const float* g, float dl, float o, float steps,
+                                             float rcp, float* gx, Sums& s)
+{
+    float q[N];
+    div_rn_n<N>(x, dl, rcp, q);
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+    {
+        float xr  = __builtin_rintf(q[k]) - o;
+        bool mask = (xr >= 0.0f) && (xr <= steps);
+        float xq  = fminf(fmaxf(xr, 0.0f), steps);
+        gx[k]     = mask ? g[k] : 0.0f * g[k];
+        s.a += (xq + o) * g[k];
+        s.b += mask ? q[k] * g[k] : 0.0f;
+        s.d += mask ? 0.0f : g[k];
+    }
 }
 
 __device__ __forceinline__ Sums block_reduce(Sums s)
@@ -288,60 +370,74 @@ __device__ __forceinline__ Sums block_reduce(Sums s)
     return r;
 }
 
-// per-tensor (C == 1): grid-stride, block partial sums -> partial[block][3] (folded in a fixed order
-// by lg_bwd_fold_one: the encoding gradients are reproducible run to run)
+// per-tensor (C == 1), tile form: workgroup b owns the kLgTile consecutive elements
+// [b * kLgTile, (b + 1) * kLgTile); lane l of it takes the 8-element groups u * kBlock + l
+// (u < kLgTileSteps), every load of the tile issued before any arithmetic. The per-lane sums run
+// in (u, element) order, then the fixed shuffle tree of block_reduce, one partial triple per
+// workgroup, folded in workgroup order by lg_bwd_fold_one (deterministic). lg_bwd16_tensor_kernel
+// maps elements to lanes and workgroups identically, so the 16-bit path sums exactly what this one
+// sums. (A grid-stride form with one pair of loads per lane in flight ran at 0.47 of HBM peak on
+// the 16-bit Llama-3-8B activations.)
+constexpr int kLgTileSteps = 2;
+constexpr int64_t kLgTile  = (int64_t) kBlock * 8 * kLgTileSteps;
+
+// a tile's element e of lane `lane` in step u, k-th of its 8
+__device__ __forceinline__ int64_t lg_tile_elem(int64_t base, int u, int k)
+{
+    return base + ((int64_t) u * kBlock + threadIdx.x) * 8 + k;
+}
+
 __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ g, float* __restrict__ gx,
                                                                int64_t n, const float* __restrict__ delta,
                                                                const float* __restrict__ offset, float steps,
                                                                float* __restrict__ sums, int vec)
 {
-    const float dl = delta[0], o = offset[0], rcp = __builtin_amdgcn_rcpf(dl);
+    const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
+    const int64_t base = (int64_t) blockIdx.x * kLgTile;
     Sums s {0, 0, 0};
-    if (vec)
+    if (vec && base + kLgTile <= n)
     {
-        // eight elements (two quads) per lane and step, then the < 8 trailing ones: the order of
-        // lg_bwd16_tensor_kernel, so the 16-bit path sums exactly what this one sums
-        const int64_t no = n / 8;
-        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < no; i += (int64_t) gridDim.x * kBlock)
+        f4 a[kLgTileSteps][2], b[kLgTileSteps][2];
+#pragma unroll
+        for (int u = 0; u < kLgTileSteps; ++u)
         {
-            const f4 a0 = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + 2 * i);
-            const f4 a1 = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + 2 * i + 1);
-            const f4 b0 = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + 2 * i);
-            const f4 b1 = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + 2 * i + 1);
+            const int64_t q = lg_tile_elem(base, u, 0) / 4;
+            a[u][0] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q);
+            a[u][1] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q + 1);
+            b[u][0] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + q);
+            b[u][1] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + q + 1);
+        }
+#pragma unroll
+        for (int u = 0; u < kLgTileSteps; ++u)
+        {
             float r[8];
-            lg_bwd_elem(a0.x, b0.x, dl, o, steps, rcp, r[0], s);
-            lg_bwd_elem(a0.y, b0.y, dl, o, steps, rcp, r[1], s);
-            lg_bwd_elem(a0.z, b0.z, dl, o, steps, rcp, r[2], s);
-            lg_bwd_elem(a0.w, b0.w, dl, o, steps, rcp, r[3], s);
-            lg_bwd_elem(a1.x, b1.x, dl, o, steps, rcp, r[4], s);
-            lg_bwd_elem(a1.y, b1.y, dl, o, steps, rcp, r[5], s);
-            lg_bwd_elem(a1.z, b1.z, dl, o, steps, rcp, r[6], s);
-            lg_bwd_elem(a1.w, b1.w, dl, o, steps, rcp, r[7], s);
+            const float xv[8] = {a[u][0].x, a[u][0].y, a[u][0].z, a[u][0].w, a[u][1].x, a[u][1].y, a[u][1].z, a[u][1].w};
+            const float gv[8] = {b[u][0].x, b[u][0].y, b[u][0].z, b[u][0].w, b[u][1].x, b[u][1].y, b[u][1].z, b[u][1].w};
+            lg_bwd_elems<8>(xv, gv, dl, o, steps, rcp, r, s);
             if (gx)
             {
+                const int64_t q = lg_tile_elem(base, u, 0) / 4;
                 const f4 r0 = {r[0], r[1], r[2], r[3]}, r1 = {r[4], r[5], r[6], r[7]};
-                __builtin_nontemporal_store(r0, reinterpret_cast<f4*>(gx) + 2 * i);
-                __builtin_nontemporal_store(r1, reinterpret_cast<f4*>(gx) + 2 * i + 1);
+                __builtin_nontemporal_store(r0, reinterpret_cast<f4*>(gx) + q);
+                __builtin_nontemporal_store(r1, reinterpret_cast<f4*>(gx) + q + 1);
             }
-        }
-        for (int64_t i = no * 8 + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
-        {
-            float r;
-            lg_bwd_elem(x[i], g[i], dl, o, steps, rcp, r, s);
-            if (gx)
-                gx[i] = r;
         }
     }
     else
     {
-        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
-        {
-            float r;
-            lg_bwd_elem(x[i], g[i], dl, o, steps, rcp, r, s);
-            if (gx)
-                gx[i] = r;
-        }
+        // the last (partial) tile, or unaligned pointers: element by element, the same order
+        for (int u = 0; u < kLgTileSteps; ++u)
+            for (int k = 0; k < 8; ++k)
+            {
+                const int64_t e = lg_tile_elem(base, u, k);
+                if (e >= n)
+                    break;
+                float r;
+                lg_bwd_elem(x[e], g[e], dl, o, steps, rcp, r, s);
+                if (gx)
+                    gx[e] = r;
+            }
     }
     Sums t = block_reduce(s);
     if (threadIdx.x == 0)
@@ -417,7 +513,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
 {
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
     {
-        const float dl = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(dl);
+        const float dl = delta[c], o = offset[c], rcp = lg_recip(dl);
         Sums s {0, 0, 0};
         for (int64_t r = 0; r < outer; ++r)
         {
@@ -454,7 +550,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
     const int64_t Q  = outer * K4;
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
     {
-        const float dl = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(dl);
+        const float dl = delta[c], o = offset[c], rcp = lg_recip(dl);
         Sums s {0, 0, 0};
         // kLgUnroll quads (2 x 16-B loads each) in flight per lane
         const int64_t step = (int64_t) splits * kBlock;
@@ -477,14 +573,12 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
             {
                 if (j0 + u * step >= Q)
                     break;
-                float r0, r1, r2, r3;
-                lg_bwd_elem(a[u].x, b[u].x, dl, o, steps, rcp, r0, s);
-                lg_bwd_elem(a[u].y, b[u].y, dl, o, steps, rcp, r1, s);
-                lg_bwd_elem(a[u].z, b[u].z, dl, o, steps, rcp, r2, s);
-                lg_bwd_elem(a[u].w, b[u].w, dl, o, steps, rcp, r3, s);
+                float rr[4];
+                const float xv[4] = {a[u].x, a[u].y, a[u].z, a[u].w}, gv[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
+                lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s);
                 if (gx)
                 {
-                    f4 rv = {r0, r1, r2, r3};
+                    f4 rv = {rr[0], rr[1], rr[2], rr[3]};
                     __builtin_nontemporal_store(rv, gx + idx[u]);
                 }
             }
@@ -524,7 +618,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restric
     const uint32_t q0  = blockIdx.x * (uint32_t) (kBlock * U);
     const uint32_t row = divK4.div(q0);
     const uint32_t c   = row - divC.div(row) * C;
-    const float dl = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(dl);
+    const float dl = delta[c], o = offset[c], rcp = lg_recip(dl);
     f4 a[U], b[U];
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -536,14 +630,12 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restric
 #pragma unroll
     for (int u = 0; u < U; ++u)
     {
-        float r0, r1, r2, r3;
-        lg_bwd_elem(a[u].x, b[u].x, dl, o, steps, rcp, r0, s);
-        lg_bwd_elem(a[u].y, b[u].y, dl, o, steps, rcp, r1, s);
-        lg_bwd_elem(a[u].z, b[u].z, dl, o, steps, rcp, r2, s);
-        lg_bwd_elem(a[u].w, b[u].w, dl, o, steps, rcp, r3, s);
+        float rr[4];
+        const float xv[4] = {a[u].x, a[u].y, a[u].z, a[u].w}, gv[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
+        lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s);
         if (gx)
         {
-            f4 rv = {r0, r1, r2, r3};
+            f4 rv = {rr[0], rr[1], rr[2], rr[3]};
             __builtin_nontemporal_store(rv, gx + q0 + u * kBlock + threadIdx.x);
         }
     }
@@ -587,34 +679,58 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restri
 
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
-// vec: eight elements (one 16-B load) per lane; otherwise one element per lane
-template <int IO>
+// kLgFwd16Vecs 16-B vectors (8 elements each) per lane, all loaded before the encoding is formed
+// and the first element computed; workgroup b owns elements [b * kLgFwd16Tile, ...). vec == 0
+// (unaligned pointers): one element per lane and step over the same tile.
+// 2 vectors per lane: 11.3 us per 13.69 M-element bf16 call (4: 11.7-12.5, 1: 12.4; a plain copy
+// of the same bytes 9.9-10.2; profiles/r03/lg16_*.txt)
+constexpr int kLgFwd16Vecs     = 2;
+constexpr int64_t kLgFwd16Tile = (int64_t) kBlock * 8 * kLgFwd16Vecs;
+
+template <int IO, int kLgFwd16Vecs = kLgFwd16Vecs>
 __global__ __launch_bounds__(kBlock) void lg_fwd16_kernel(const unsigned short* __restrict__ x,
-                                                          unsigned short* __restrict__ y, uint32_t n,
+                                                          unsigned short* __restrict__ y, int64_t n,
                                                           const float* __restrict__ delta,
                                                           const float* __restrict__ offset, float steps, int vec,
                                                           LgEnc enc)
 {
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    float d, o;
-    enc.get(0, t, delta, offset, d, o);   // element 0's thread stores them
-    if (vec)
+    constexpr int64_t kLgFwd16Tile = (int64_t) kBlock * 8 * kLgFwd16Vecs;
+    const int64_t base = (int64_t) blockIdx.x * kLgFwd16Tile;
+    if (vec && base + kLgFwd16Tile <= n)
     {
-        if (t >= n / 8)
-            return;
-        const u16x8 v = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + t);
-        u16x8 r;
+        u16x8 v[kLgFwd16Vecs];
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-            r[k] = from_f32<IO>(lg_qdq(to_f32<IO>(v[k]), d, o, steps));
-        __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(y) + t);
+        for (int u = 0; u < kLgFwd16Vecs; ++u)
+            v[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + base / 8 + u * kBlock +
+                                              threadIdx.x);
+        float d, o;
+        enc.get(0, base + threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);   // element 0's thread stores them
+        const float rd = lg_recip(d);
+#pragma unroll
+        for (int u = 0; u < kLgFwd16Vecs; ++u)
+        {
+            float xin[8], yo[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                xin[k] = to_f32<IO>(v[u][k]);
+            lg_qdq_n<8>(xin, d, o, steps, rd, yo);
+            u16x8 r;
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                r[k] = from_f32<IO>(yo[k]);
+            __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(y) + base / 8 + u * kBlock + threadIdx.x);
+        }
+        return;
     }
-    else if (t < n)
-        y[t] = from_f32<IO>(lg_qdq(to_f32<IO>(x[t]), d, o, steps));
+    float d, o;
+    enc.get(0, base + threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);
+    const float rd = lg_recip(d);
+    for (int64_t e = base + threadIdx.x; e < base + kLgFwd16Tile && e < n; e += kBlock)
+        y[e] = from_f32<IO>(lg_qdq(to_f32<IO>(x[e]), d, o, steps, rd));
 }
 
-// the element -> lane -> workgroup order of lg_bwd_tensor_kernel (eight per lane and step, then
-// the tail), so the sums equal the float32 kernel's on the upcast tensors
+// the element -> lane -> workgroup order of lg_bwd_tensor_kernel (tiles of kLgTile, 8 elements per
+// lane and step), so the sums equal the float32 kernel's on the upcast tensors
 template <int IO>
 __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned short* __restrict__ x,
                                                                  const unsigned short* __restrict__ g,
@@ -623,37 +739,53 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
                                                                  const float* __restrict__ offset, float steps,
                                                                  float* __restrict__ partial, int vec)
 {
-    const float dl = delta[0], o = offset[0], rcp = __builtin_amdgcn_rcpf(dl);
+    const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
+    const int64_t base = (int64_t) blockIdx.x * kLgTile;
     Sums s {0, 0, 0};
-    int64_t done = 0;
-    if (vec)
+    if (vec && base + kLgTile <= n)
     {
-        const int64_t no = n / 8;
-        for (int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x; i < no; i += (int64_t) gridDim.x * kBlock)
+        u16x8 a[kLgTileSteps], b[kLgTileSteps];
+#pragma unroll
+        for (int u = 0; u < kLgTileSteps; ++u)
         {
-            const u16x8 a = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + i);
-            const u16x8 b = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(g) + i);
-            float r[8];
+            const int64_t q = lg_tile_elem(base, u, 0) / 8;
+            a[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + q);
+            b[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(g) + q);
+        }
+#pragma unroll
+        for (int u = 0; u < kLgTileSteps; ++u)
+        {
+            float r[8], xv[8], gv[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k)
-                lg_bwd_elem(to_f32<IO>(a[k]), to_f32<IO>(b[k]), dl, o, steps, rcp, r[k], s);
+            {
+                xv[k] = to_f32<IO>(a[u][k]);
+                gv[k] = to_f32<IO>(b[u][k]);
+            }
+            lg_bwd_elems<8>(xv, gv, dl, o, steps, rcp, r, s);
             if (gx)
             {
                 u16x8 h;
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
                     h[k] = from_f32<IO>(r[k]);
-                __builtin_nontemporal_store(h, reinterpret_cast<u16x8*>(gx) + i);
+                __builtin_nontemporal_store(h, reinterpret_cast<u16x8*>(gx) + lg_tile_elem(base, u, 0) / 8);
             }
         }
-        done = no * 8;
     }
-    for (int64_t i = done + (int64_t) blockIdx.x * kBlock + threadIdx.x; i < n; i += (int64_t) gridDim.x * kBlock)
+    else
     {
-        float r;
-        lg_bwd_elem(to_f32<IO>(x[i]), to_f32<IO>(g[i]), dl, o, steps, rcp, r, s);
-        if (gx)
-            gx[i] = from_f32<IO>(r);
+        for (int u = 0; u < kLgTileSteps; ++u)
+            for (int k = 0; k < 8; ++k)
+            {
+                const int64_t e = lg_tile_elem(base, u, k);
+                if (e >= n)
+                    break;
+                float r;
+                lg_bwd_elem(to_f32<IO>(x[e]), to_f32<IO>(g[e]), dl, o, steps, rcp, r, s);
+                if (gx)
+                    gx[e] = from_f32<IO>(r);
+            }
     }
     Sums t = block_reduce(s);
     if (threadIdx.x == 0)
@@ -797,32 +929,45 @@ void launch_bwd_tile(int U, int64_t wg, const f4* x, const void* g, f4* gx, Fast
 
 using namespace aimet_amd;
 
-extern "C" {
-
-int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t K, const float* delta,
-                     const float* offset, float num_steps, void* stream)
-{
-    return guarded([&] {
-        AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
-        int64_t n = outer * C * K;
-        if (n == 0)
-            return;
-        AIMET_REQUIRE(n < (int64_t(1) << 31), "learned-grid QDQ needs < 2^31 elements per call");
-        require_device_ptr(x, "x");
-        require_device_ptr(y, "y");
-        require_device_ptr(delta, "delta");
-        require_device_ptr(offset, "offset");
-        LgChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        bool vec     = (C == 1 || K % 4 == 0) && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0
-                       && n % 4 == 0;
-        launch_lg_fwd<IO_F32>(x, y, n, map, delta, offset, num_steps, vec, LgEnc {}, as_stream(stream));
-    });
-}
-
-}   // extern "C"
-
 namespace
 {
+
+// sub-problems of a [outer][C][K] learned-grid pass with <= lg_chunk_elems() elements each (the
+// fp32 forward's element -> channel map is 32-bit): whole rows when a row of C x K fits, else
+// channel ranges of one row, else pieces of one channel's K (a multiple of 16 elements, so every
+// piece keeps the 16-B alignment). fn(first element, outer', first channel, C', K').
+// aimet_lg_set_chunk_limit (tests only) lowers the bound to exercise the chunking on small tensors.
+std::atomic<int64_t> g_lg_chunk {int64_t(1) << 30};
+int64_t lg_chunk_elems()
+{
+    return g_lg_chunk.load(std::memory_order_relaxed);
+}
+
+template <class F>
+void for_each_lg_chunk(int64_t outer, int64_t C, int64_t K, F fn)
+{
+    const int64_t lim = lg_chunk_elems();
+    if (C * K <= lim)
+    {
+        const int64_t rows = lim / (C * K);
+        for (int64_t r = 0; r < outer; r += rows)
+            fn(r * C * K, std::min(rows, outer - r), 0, C, K);
+        return;
+    }
+    for (int64_t r = 0; r < outer; ++r)
+    {
+        if (K <= lim)
+        {
+            const int64_t cs = lim / K;
+            for (int64_t c = 0; c < C; c += cs)
+                fn((r * C + c) * K, 1, c, std::min(cs, C - c), K);
+        }
+        else
+            for (int64_t c = 0; c < C; ++c)
+                for (int64_t k = 0; k < K; k += lim)
+                    fn((r * C + c) * K + k, 1, c, 1, std::min(lim, K - k));
+    }
+}
 
 LgEnc enc_of(const float* emin, const float* emax, int64_t C, int64_t K, int bw, int sym, int strict, int unsign,
              float* delta, float* offset, float* range_out)
@@ -846,6 +991,22 @@ void forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, 
                   const float* offset, float num_steps, LgEnc enc, hipStream_t st);
 
 }   // namespace
+
+extern "C" {
+
+int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t K, const float* delta,
+                     const float* offset, float num_steps, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
+        require_device_ptr(delta, "delta");
+        require_device_ptr(offset, "offset");
+        forward_cast(x, y, outer, C, K, IO_F32, delta, offset, num_steps, LgEnc {}, as_stream(stream));
+    });
+}
+
+}   // extern "C"
+
 
 extern "C" {
 
@@ -895,9 +1056,29 @@ void forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, 
         int64_t n = outer * C * K;
         if (n == 0)
             return;
-        AIMET_REQUIRE(n < (int64_t(1) << 31), "learned-grid QDQ needs < 2^31 elements per call");
         require_device_ptr(x, "x");
         require_device_ptr(y, "y");
+        if (n > lg_chunk_elems())
+        {
+            // past 2^31 elements the kernels' 32-bit element -> channel arithmetic would wrap: the
+            // encodings first (when the kernel was to form them), then sub-problems of whole rows
+            // (or channel ranges, or row pieces) of <= lg_chunk_elems() elements each
+            if (enc.emin)
+            {
+                lg_encodings_kernel<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, st>>>(
+                    enc.emin, enc.emax, (uint32_t) C, enc.steps, enc.mode, enc.half_floor, enc.neg_half_ceil,
+                    enc.delta_out, enc.offset_out, enc.range_out);
+                AIMET_LAUNCH_CHECK();
+                delta  = enc.delta_out;
+                offset = enc.offset_out;
+            }
+            const size_t ysz = out_dtype == IO_F32 ? 4 : 2;
+            for_each_lg_chunk(outer, C, K, [&](int64_t first, int64_t o2, int64_t c0, int64_t C2, int64_t K2) {
+                forward_cast(x + first, static_cast<char*>(y) + first * ysz, o2, C2, K2, out_dtype, delta + c0,
+                             offset + c0, num_steps, LgEnc {}, st);
+            });
+            return;
+        }
         LgChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
         const int ya = out_dtype == IO_F32 ? 15 : 7;
         bool vec = (C == 1 || K % 4 == 0) && (reinterpret_cast<uintptr_t>(x) & 15) == 0 &&
@@ -941,7 +1122,8 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
         {
             bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                          reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
-            const unsigned nb = stream_blocks(n, (int64_t) kBlock * 16);
+            AIMET_REQUIRE(ceil_div(n, kLgTile) < (int64_t(1) << 31), "too many elements");
+            const unsigned nb = (unsigned) ceil_div(n, kLgTile);
             float* partial    = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * nb, s));
             lg_bwd_tensor_kernel<<<nb, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset, num_steps, partial,
                                                        vec ? 1 : 0);
@@ -1021,21 +1203,30 @@ void forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* de
                 float num_steps, LgEnc enc, hipStream_t st)
 {
     AIMET_REQUIRE(io_dtype == IO_F16 || io_dtype == IO_BF16, "io_dtype must be 1 (float16) or 2 (bfloat16)");
-    AIMET_REQUIRE(n >= 0 && n < (int64_t(1) << 31), "learned-grid QDQ needs < 2^31 elements per call");
+    AIMET_REQUIRE(n >= 0 && ceil_div(n, kLgFwd16Tile) < (int64_t(1) << 31), "too many elements");
     if (n == 0)
         return;
     require_device_ptr(x, "x");
     require_device_ptr(y, "y");
-    const bool vec = n % 8 == 0 && ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
-    const int64_t work = vec ? n / 8 : n;
+    const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
     auto xs = static_cast<const unsigned short*>(x);
     auto ys = static_cast<unsigned short*>(y);
-    if (io_dtype == IO_F16)
-        lg_fwd16_kernel<IO_F16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, st>>>(
-            xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0, enc);
-    else
-        lg_fwd16_kernel<IO_BF16><<<(unsigned) ceil_div(work, kBlock), kBlock, 0, st>>>(
-            xs, ys, (uint32_t) n, delta, offset, num_steps, vec ? 1 : 0, enc);
+    static const int vecs = [] {
+        const char* e = getenv("AIMET_TUNE_LG16_VECS");   // tuning experiments only
+        const int v   = e ? atoi(e) : kLgFwd16Vecs;
+        return (v == 1 || v == 2 || v == 8) ? v : kLgFwd16Vecs;
+    }();
+    const unsigned nb = (unsigned) ceil_div(n, (int64_t) kBlock * 8 * vecs);
+#define AIMET_LG16_FWD(V)                                                                                           \
+    if (vecs == V)                                                                                                  \
+    {                                                                                                               \
+        if (io_dtype == IO_F16)                                                                                     \
+            lg_fwd16_kernel<IO_F16, V><<<nb, kBlock, 0, st>>>(xs, ys, n, delta, offset, num_steps, vec ? 1 : 0, enc); \
+        else                                                                                                        \
+            lg_fwd16_kernel<IO_BF16, V><<<nb, kBlock, 0, st>>>(xs, ys, n, delta, offset, num_steps, vec ? 1 : 0, enc);\
+    }
+    AIMET_LG16_FWD(1) AIMET_LG16_FWD(2) AIMET_LG16_FWD(4) AIMET_LG16_FWD(8)
+#undef AIMET_LG16_FWD
     AIMET_LAUNCH_CHECK();
 }
 
@@ -1069,6 +1260,15 @@ int aimet_lg_forward_16_range(const void* x, void* y, int64_t n, int io_dtype, c
             return;
         }
         forward_16(x, y, n, io_dtype, nullptr, nullptr, enc.steps, enc, as_stream(stream));
+    });
+}
+
+int aimet_lg_set_chunk_limit(int64_t elems)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(elems == 0 || (elems >= 1024 && elems <= (int64_t(1) << 30)),
+                      "chunk limit: 0 (default) or 1024 .. 2^30 elements");
+        g_lg_chunk.store(elems == 0 ? (int64_t(1) << 30) : (elems / 16) * 16, std::memory_order_relaxed);
     });
 }
 
@@ -1218,7 +1418,8 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         require_device_ptr(offset, "offset");
         const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                            reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
-        const unsigned nb = stream_blocks(n, (int64_t) kBlock * 16);   // the fp32 kernel's grid
+        AIMET_REQUIRE(ceil_div(n, kLgTile) < (int64_t(1) << 31), "too many elements");
+        const unsigned nb = (unsigned) ceil_div(n, kLgTile);   // the fp32 kernel's grid
         float* partial    = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * nb, s));
         auto xs = static_cast<const unsigned short*>(x);
         auto gs = static_cast<const unsigned short*>(grad);

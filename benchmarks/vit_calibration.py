@@ -80,7 +80,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     t_fwd = t_stats = t_coll = 0.0
-    per_batch = []
+    per_batch, host_batch = [], []
     elems = 0
     ex = None
     for b0 in range(0, args.images, args.batch):
@@ -107,6 +107,7 @@ def main():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ex = D.sharded_update_stats(quantizers, tensors, exchange=ex, fused=not args.phased)
+        host_batch.append(time.perf_counter() - t0)   # until every launch is enqueued
         torch.cuda.synchronize()
         per_batch.append(time.perf_counter() - t0)
         t_stats += per_batch[-1]
@@ -153,6 +154,7 @@ def main():
             "value": round(per_gpu * world, 3), "unit": "Gelem/s", "n_gpus": world,
             "per_gpu_gelem_s": round(per_gpu, 3), "elements_per_rank": elems,
             "stats_s": round(t_stats, 4), "stats_ms_per_batch": [round(v * 1e3, 3) for v in per_batch],
+            "stats_enqueue_ms_per_batch": [round(v * 1e3, 3) for v in host_batch],
             "collectives_s": round(t_coll, 4), "forward_s": round(t_fwd, 3),
             "quantizers": len(quantizers), "images": args.images, "global_batch": args.batch,
             "act_elems_per_image": round(elems * world / args.images),

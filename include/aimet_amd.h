@@ -381,6 +381,11 @@ int aimet_lg_forward_16_range(const void* x, void* y, int64_t n, int io_dtype, c
                               const float* encoding_max_dev, int bitwidth, int use_symmetric,
                               int use_strict_symmetric, int is_unsigned_symmetric, float* delta_out,
                               float* offset_out, float* range_out, void* stream);
+/* The float32-input forward passes of more than 2^30 elements run as sub-problems of whole rows /
+ * channel ranges / row pieces (the reference's torch ops have no element limit,
+ * quantsim_straight_through_grad.py:191-249). Testing hook: lower that bound to `elems`
+ * (1024 .. 2^30; 0 restores the default) so the chunking is exercised on small tensors. */
+int aimet_lg_set_chunk_limit(int64_t elems);
 int aimet_lg_forward_cast(const float* x, void* y, int64_t outer, int64_t C, int64_t K, int out_dtype,
                           const float* delta_dev, const float* offset_dev, float num_steps, void* stream);
 int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, float* sums_dev, int64_t outer,

@@ -530,6 +530,45 @@ def test_learned_grid_large_vs_torch_ref(shape, sym):
     torch.testing.assert_close(emin.grad, gmin, rtol=2e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("bw,sym", [(16, False), (16, True), (8, False), (4, True)])
+def test_learned_grid_quotients_at_half_integers(bw, sym):
+    """The learned-grid kernels form x / delta from a per-encoding reciprocal with one Markstein
+    correction (learned_grid.hip: div_rn). Inputs built to land on and +-1..3 ulp around every
+    kind of rounding boundary of x / delta (half-integers, the clamp edges), zeros of both signs,
+    tiny / huge / non-finite values: y and grad_x == the reference's torch ops bit for bit, on the
+    float32 path, per tensor and per channel, and on the bf16 / fp16 per-tensor path (== the
+    upcast chain)."""
+    from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
+    from oracle import torch_ref as T
+    g = torch.Generator(device=DEV).manual_seed(bw * 10 + sym)
+    C = 4
+    emax = torch.tensor([3.1, 0.37, 1e-3, 5e4], device=DEV)
+    emin = -emax if sym else -emax * torch.tensor([0.3, 1.0, 0.01, 2.0], device=DEV)
+    delta, offset, steps = T.lg_encodings(bw, emin, emax, sym, False, False)
+    K = 1 << 14
+    n = torch.randint(-(1 << (bw - 1)) - 4, (1 << (bw - 1)) + 4, (C, K), device=DEV, generator=g).float()
+    x = ((n + 0.5) * delta.view(C, 1))
+    ulps = torch.randint(-3, 4, (C, K), device=DEV, generator=g, dtype=torch.int32)
+    x = (x.view(torch.int32) + ulps).view(torch.float32)
+    x[:, :64] = torch.tensor([0.0, -0.0, 1e-30, -1e-30, 3e38, -3e38, float("inf"), float("-inf")] * 8, device=DEV)
+    x[:, 64:128] = n[:, 64:128] * delta.view(C, 1)            # exact integers
+    grad = torch.randn(C, K, device=DEV, generator=g)
+    for per_channel in (True, False):
+        mn, mx = (emin, emax) if per_channel else (emin[:1], emax[:1])
+        xt = x.clone().requires_grad_(True)
+        y = LearnedGridQuantizeDequantize.apply(xt, mn, mx, bw, sym, False, False, 0)
+        yr = T.lg_forward(x, mn, mx, bw, sym)[0]
+        assert torch.equal(y.view(torch.int32), yr.view(torch.int32)), per_channel
+        y.backward(grad)
+        gx = T.lg_gradients(x, grad, mn, mx, bw, sym)[0]
+        assert torch.equal(xt.grad.view(torch.int32), gx.view(torch.int32)), per_channel
+    for dt in (torch.bfloat16, torch.float16):
+        xh = x[:1].reshape(-1).to(dt)
+        yh = LearnedGridQuantizeDequantize.apply(xh, emin[:1], emax[:1], bw, sym, False, False, 0)
+        want = T.lg_forward(xh.float(), emin[:1], emax[:1], bw, sym)[0].to(dt)
+        assert torch.equal(yh.view(torch.int16), want.view(torch.int16)), dt
+
+
 @pytest.mark.parametrize("outer,C,K", [(3, 5, 2048), (2, 7, 3072), (4, 3, 100)])
 def test_learned_grid_backward_sums_channel_axis_inner(outer, C, K):
     """aimet_lg_backward on [outer][C][K] with outer > 1 (channel axis not first): grad_x exact and
@@ -1426,3 +1465,68 @@ def test_learned_grid_gate_ranges_equals_single_range_gate():
     for (a, b), (ea, eb), v in zip(ranges, expect, v0):
         assert _same_bits_or_nan(a, ea) and _same_bits_or_nan(b, eb)
         assert a._version > v
+
+
+@pytest.mark.parametrize("outer,C,K", [(5, 3, 300), (2, 9, 1024), (3, 2, 5000), (1, 1, 20000)])
+@pytest.mark.parametrize("out_dtype", [0, 2])
+def test_learned_grid_forward_chunking_is_exact(outer, C, K, out_dtype):
+    """The fp32-input forward splits passes of more than 2^30 elements into sub-problems (whole
+    rows, channel ranges of a row, pieces of a channel). With the bound lowered to 4096 elements
+    (aimet_lg_set_chunk_limit) each split mode runs on a small tensor: y, delta, offset and the
+    saved range == the unsplit pass, bit for bit (float32 and the bf16-cast output)."""
+    from aimet_amd import _native
+    g = torch.Generator(device=DEV).manual_seed(outer * 7 + C)
+    x = torch.randn(outer, C, K, device=DEV, generator=g) * 0.7
+    emax = torch.rand(C, device=DEV, generator=g) + 0.5
+    emin = -emax * 0.6
+    s = torch.cuda.current_stream().cuda_stream
+    dt = torch.float32 if out_dtype == 0 else torch.bfloat16
+
+    def run():
+        y = torch.empty(x.shape, dtype=dt, device=DEV)
+        enc = torch.full((4, C), float("nan"), device=DEV)
+        _native.call("aimet_lg_forward_range", x.data_ptr(), y.data_ptr(), outer, C, K, out_dtype, emin.data_ptr(),
+                     emax.data_ptr(), 4, 0, 0, 0, enc[0].data_ptr(), enc[1].data_ptr(), enc[2].data_ptr(), s)
+        return y, enc
+    y_ref, enc_ref = run()
+    try:
+        _native.call("aimet_lg_set_chunk_limit", 4096)
+        y, enc = run()
+    finally:
+        _native.call("aimet_lg_set_chunk_limit", 0)
+    assert torch.equal(y.view(torch.int16 if out_dtype else torch.int32),
+                       y_ref.view(torch.int16 if out_dtype else torch.int32))
+    assert torch.equal(enc, enc_ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_learned_grid_past_2_31_elements(dtype):
+    """A per-tensor learned-grid forward + backward over 2^31 + 4100 elements (an activation the
+    size of Llama-3-8B's logits at micro-batch 2 x seq 8192; the reference's torch ops have no
+    element limit): y and grad_x bit-exact vs the reference's torch ops (oracle/torch_ref.py) on
+    slices at the start, across 2^31 and at the ragged end; the encoding gradients vs the torch
+    ops over the whole tensor (rtol 1e-4: fp32 summation order)."""
+    from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
+    from oracle import torch_ref as T
+    n = (1 << 31) + 4100
+    g = torch.Generator(device=DEV).manual_seed(31)
+    x = torch.randn(n, device=DEV, generator=g, dtype=torch.float32).to(dtype)
+    grad = torch.randn(n, device=DEV, generator=g, dtype=torch.float32).to(dtype)
+    emin = torch.tensor([-2.9], device=DEV, requires_grad=True)
+    emax = torch.tensor([3.3], device=DEV, requires_grad=True)
+    xt = x.requires_grad_(True)
+    y = LearnedGridQuantizeDequantize.apply(xt, emin, emax, 8)
+    y.backward(grad)
+    gx = xt.grad
+    for a, b in ((0, 1 << 20), ((1 << 31) - (1 << 20), (1 << 31) + (1 << 20)), (n - (1 << 20), n)):
+        xs = x[a:b].detach().float()
+        want = T.lg_forward(xs, emin.detach(), emax.detach(), 8)[0].to(dtype)
+        got = LearnedGridQuantizeDequantize.apply(x[a:b].detach(), emin.detach(), emax.detach(), 8)
+        assert torch.equal(got.view(torch.int16 if dtype != torch.float32 else torch.int32),
+                           want.view(torch.int16 if dtype != torch.float32 else torch.int32)), (a, b)
+        wgx = T.lg_gradients(xs, grad[a:b].float(), emin.detach(), emax.detach(), 8)[0].to(dtype)
+        assert torch.equal(gx[a:b], wgx), (a, b)
+    del gx
+    _, gmin, gmax = T.lg_gradients(x.detach().float(), grad.float(), emin.detach(), emax.detach(), 8)
+    torch.testing.assert_close(emin.grad, gmin, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(emax.grad, gmax, rtol=1e-4, atol=1e-3)
