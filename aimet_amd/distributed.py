@@ -85,7 +85,7 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
 
     # per-tensor AimetTensorQuantizers: one launch per phase for all of them (aimet_tq_*_many)
     from aimet_amd.tensor_quantizer import AimetTensorQuantizer
-    many = [i for i, q in enumerate(quantizers) if type(q) is AimetTensorQuantizer and q.num_channels == 1]
+    many = [i for i, q in enumerate(quantizers) if type(q) is AimetTensorQuantizer and q._num_channels == 1]
     many_set = set(many)
     rest = [i for i in range(len(quantizers)) if i not in many_set]
     mq = [quantizers[i] for i in many]
@@ -94,7 +94,8 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
     if world == 1 and not rest and fused:
         # nothing to exchange (no packed buffers either): the fused single-pass update, 4 launches
         # for all quantizers
-        AimetTensorQuantizer.updateStatsMany(mq, mt)
+        AimetTensorQuantizer.updateStatsMany(quantizers if len(mq) == len(quantizers) else mq,
+                                             tensors if len(mq) == len(quantizers) else mt)
         return exchange
 
     if exchange is None or exchange.quantizers != list(quantizers):

@@ -12,6 +12,7 @@ Same class name, method names and argument meaning. Differences, all MI355X-firs
   COMP_MODE_CPU) is staged through HBM -- copied to the device, computed by the same HIP
   kernels, results copied back -- and a process without a HIP device raises ``RuntimeError``.
 """
+import array
 import ctypes
 import gc
 import itertools
@@ -286,33 +287,52 @@ class AimetTensorQuantizer:
     # -- many per-tensor quantizers at once (aimet_tq_*_many: one launch per phase) ------------
     @staticmethod
     def _many(name, quantizers, tensors=None, counts=None):
-        qs = list(quantizers)
+        """One batched entry point over many per-tensor quantizers. The argument tables are built
+        from array.array buffers (no per-element ctypes conversion): for ViT-L/16's 318
+        quantizers the host side of a calibration batch is on the critical path (the GPU waits for
+        the first launch)."""
+        qs = quantizers if type(quantizers) is list else list(quantizers)
         if not qs:
             return
-        if any(q._num_channels != 1 for q in qs):
-            raise ValueError("the batched statistics entry points take per-tensor quantizers")
+        n = len(qs)
         ts = None
         if tensors is not None:
             ts = [t if t.is_contiguous() else t.contiguous() for t in tensors]
+            f32 = torch.float32
             for t in ts:
-                _require_gpu(t)
+                if not (t.is_cuda and t.dtype is f32):
+                    _require_gpu(t)
             dev = ts[0].device
-            handles = AimetTensorQuantizer._ensure_many(qs, dev)
+            idx = dev.index if dev.index is not None else torch.cuda.current_device()
         else:
-            dev = torch.device("cuda", qs[0]._device)
-            handles = [q._handle for q in qs]
-        n = len(qs)
-        args = [(ctypes.c_void_p * n)(*handles)]
+            idx = qs[0]._device
+            dev = torch.device("cuda", idx)
+        for q in qs:
+            if q._num_channels != 1:
+                raise ValueError("the batched statistics entry points take per-tensor quantizers")
+            if q._handle is None or q._device != idx:
+                if tensors is None:
+                    raise RuntimeError("aimet_amd: quantizer has no device state")
+                AimetTensorQuantizer._ensure_many(qs, dev)
+                break
+        handles = array.array("Q", [q._handle.value for q in qs])
+        args = [(ctypes.c_void_p * n).from_buffer(handles)]
+        keep = [handles]
         if ts is not None:
-            args += [(ctypes.c_void_p * n)(*[t.data_ptr() for t in ts]),
-                     (ctypes.c_int64 * n)(*[t.numel() for t in ts])]
+            ptrs = array.array("Q", [t.data_ptr() for t in ts])
+            sizes = array.array("q", [t.numel() for t in ts])
+            keep += [ptrs, sizes]
+            args += [(ctypes.c_void_p * n).from_buffer(ptrs), (ctypes.c_int64 * n).from_buffer(sizes)]
         if counts is not None:
-            args.append((ctypes.c_int64 * n)(*[int(c) for c in counts]))
+            cnt = array.array("q", [int(c) for c in counts])
+            keep.append(cnt)
+            args.append((ctypes.c_int64 * n).from_buffer(cnt))
         with torch.cuda.device(dev):
             _native.call(name, *args, n, torch.cuda.current_stream(dev).cuda_stream)
         if name in ("aimet_tq_update_stats_many", "aimet_tq_batch_minmax_many"):
             for q in qs:
                 q._is_encoding_valid = True
+        del keep
         return ts   # keep the contiguous copies alive until the caller synchronises
 
     @staticmethod

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--oracle-threads", type=int, default=16)
     ap.add_argument("--phased", action="store_true", help="single rank: run the sharded phases anyway")
     ap.add_argument("--cold", action="store_true", help="time the first batch in a cold process (no warm-up pass)")
+    ap.add_argument("--profile-host", action="store_true", help="cProfile the host side of the later batches")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,9 +106,17 @@ def main():
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
+        if args.profile_host and b0 > 0:
+            import cProfile
+            import pstats
+            prof = cProfile.Profile()
+            prof.enable()
         t0 = time.perf_counter()
         ex = D.sharded_update_stats(quantizers, tensors, exchange=ex, fused=not args.phased)
         host_batch.append(time.perf_counter() - t0)   # until every launch is enqueued
+        if args.profile_host and b0 > 0:
+            prof.disable()
+            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(12)
         torch.cuda.synchronize()
         per_batch.append(time.perf_counter() - t0)
         t_stats += per_batch[-1]

@@ -180,7 +180,7 @@ static void device_lifecycle()
             CHECK(aimet_tq_destroy(q));
     }
     CHECK(hipDeviceSynchronize() == hipSuccess ? AIMET_OK : 1);
-    hipFree(x);
+    (void) hipFree(x);
 }
 
 int main(int argc, char** argv)
