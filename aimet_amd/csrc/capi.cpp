@@ -1,4 +1,5 @@
 // capi.cpp -- error state, device checks and the host encoding-math entry points of the C-ABI.
+#include <map>
 #include <string>
 
 #include "encodings.hpp"
@@ -16,10 +17,47 @@ void set_last_error(const std::string& msg)
     g_last_error = msg;
 }
 
+// Device allocations already validated: [base, end) of the allocations (hipMemGetAddressRange)
+// that earlier device pointers lay in, keyed by base. A batched call over ViT-L/16's 318
+// activations (each its own torch segment) otherwise made 318 pointer queries per calibration
+// batch on the critical path. A hit only skips a validation: kernels run on the pointer either way.
+namespace
+{
+struct DeviceRanges
+{
+    std::map<uintptr_t, uintptr_t> r;   // base -> end
+    bool hit(uintptr_t a) const
+    {
+        auto it = r.upper_bound(a);
+        if (it == r.begin())
+            return false;
+        --it;
+        return a < it->second;
+    }
+    void add(const void* p)
+    {
+        hipDeviceptr_t b = nullptr;
+        size_t n         = 0;
+        if (hipMemGetAddressRange(&b, &n, const_cast<void*>(p)) != hipSuccess || b == nullptr || n == 0)
+        {
+            (void) hipGetLastError();
+            return;
+        }
+        if (r.size() >= 4096)
+            r.clear();
+        const uintptr_t base = reinterpret_cast<uintptr_t>(b);
+        r[base]              = base + n;
+    }
+};
+thread_local DeviceRanges t_ranges;
+}   // namespace
+
 void require_device_ptr(const void* p, const char* what)
 {
     if (p == nullptr)
         throw InvalidArgument(std::string(what) + " pointer is null");
+    if (t_ranges.hit(reinterpret_cast<uintptr_t>(p)))
+        return;
     hipPointerAttribute_t attr;
     hipError_t e = hipPointerGetAttributes(&attr, p);
     if (e != hipSuccess)
@@ -31,6 +69,8 @@ void require_device_ptr(const void* p, const char* what)
     if (attr.type != hipMemoryTypeDevice && attr.type != hipMemoryTypeManaged)
         throw InvalidArgument(std::string(what) +
                               " is not device memory: aimet_amd has no CPU path (move the tensor to an MI355X)");
+    if (attr.type == hipMemoryTypeDevice)
+        t_ranges.add(p);
 }
 
 }   // namespace aimet_amd

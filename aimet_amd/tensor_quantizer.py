@@ -297,30 +297,38 @@ class AimetTensorQuantizer:
         n = len(qs)
         ts = None
         if tensors is not None:
-            ts = [t if t.is_contiguous() else t.contiguous() for t in tensors]
+            ts = tensors if type(tensors) is list else list(tensors)
             f32 = torch.float32
-            for t in ts:
+            ptrs, sizes = array.array("Q"), array.array("q")
+            for i, t in enumerate(ts):   # one pass: layout, device, dtype, pointer, size
+                if not t.is_contiguous():
+                    if ts is tensors:
+                        ts = list(ts)
+                    t = ts[i] = t.contiguous()
                 if not (t.is_cuda and t.dtype is f32):
                     _require_gpu(t)
+                ptrs.append(t.data_ptr())
+                sizes.append(t.numel())
             dev = ts[0].device
             idx = dev.index if dev.index is not None else torch.cuda.current_device()
         else:
             idx = qs[0]._device
             dev = torch.device("cuda", idx)
+        hv = array.array("Q")
         for q in qs:
+            h = q._handle
             if q._num_channels != 1:
                 raise ValueError("the batched statistics entry points take per-tensor quantizers")
-            if q._handle is None or q._device != idx:
+            if h is None or q._device != idx:
                 if tensors is None:
                     raise RuntimeError("aimet_amd: quantizer has no device state")
                 AimetTensorQuantizer._ensure_many(qs, dev)
+                hv = array.array("Q", [q._handle.value for q in qs])
                 break
-        handles = array.array("Q", [q._handle.value for q in qs])
-        args = [(ctypes.c_void_p * n).from_buffer(handles)]
-        keep = [handles]
+            hv.append(h.value)
+        args = [(ctypes.c_void_p * n).from_buffer(hv)]
+        keep = [hv]
         if ts is not None:
-            ptrs = array.array("Q", [t.data_ptr() for t in ts])
-            sizes = array.array("q", [t.numel() for t in ts])
             keep += [ptrs, sizes]
             args += [(ctypes.c_void_p * n).from_buffer(ptrs), (ctypes.c_int64 * n).from_buffer(sizes)]
         if counts is not None:

@@ -81,7 +81,8 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     t_fwd = t_stats = t_coll = 0.0
-    per_batch, host_batch = [], []
+    per_batch, host_batch, gpu_batch = [], [], []
+    shadow = None
     elems = 0
     ex = None
     for b0 in range(0, args.images, args.batch):
@@ -102,23 +103,42 @@ def main():
             warm = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in quantizers]
             D.sharded_update_stats(warm, tensors, fused=not args.phased)
             AimetTensorQuantizer.getEncodings(warm, 8, False, False, False)
-            del warm
+            shadow = warm if world == 1 else None
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
-        if args.profile_host and b0 > 0:
-            import cProfile
-            import pstats
-            prof = cProfile.Profile()
-            prof.enable()
+        if args.profile_host:
+            from aimet_amd import _native
+            native_s = []
+            orig_call = _native.call
+
+            def timed_call(name, *a):
+                t = time.perf_counter()
+                r = orig_call(name, *a)
+                native_s.append((name, (time.perf_counter() - t) * 1e3))
+                return r
+            _native.call = timed_call
         t0 = time.perf_counter()
         ex = D.sharded_update_stats(quantizers, tensors, exchange=ex, fused=not args.phased)
         host_batch.append(time.perf_counter() - t0)   # until every launch is enqueued
-        if args.profile_host and b0 > 0:
-            prof.disable()
-            pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(12)
+        if args.profile_host:
+            _native.call = orig_call
+            print("host: batch %d enqueue %.3f ms, native calls %s" % (b0 // args.batch, host_batch[-1] * 1e3,
+                                                                      native_s), file=sys.stderr)
         torch.cuda.synchronize()
         per_batch.append(time.perf_counter() - t0)
+        if shadow is not None:
+            # the GPU time of the statistics alone, on the warm-up quantizers (the same state: they
+            # saw every earlier batch too): the stream is held by a sleep kernel while the host
+            # enqueues, so e_a .. e_b spans only the statistics kernels -- what a pipelined
+            # calibration loop, which enqueues the statistics while the forward still runs, pays
+            e_a, e_b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda._sleep(20_000_000)
+            e_a.record(stream)
+            D.sharded_update_stats(shadow, tensors, fused=not args.phased)
+            e_b.record(stream)
+            torch.cuda.synchronize()
+            gpu_batch.append(e_a.elapsed_time(e_b) / 1e3)
         t_stats += per_batch[-1]
         if analyzers:
             # the oracle sees the same tensors, one update per quantizer per batch (untimed)
@@ -164,6 +184,7 @@ def main():
             "per_gpu_gelem_s": round(per_gpu, 3), "elements_per_rank": elems,
             "stats_s": round(t_stats, 4), "stats_ms_per_batch": [round(v * 1e3, 3) for v in per_batch],
             "stats_enqueue_ms_per_batch": [round(v * 1e3, 3) for v in host_batch],
+            "stats_gpu_ms_per_batch": [round(v * 1e3, 3) for v in gpu_batch],
             "collectives_s": round(t_coll, 4), "forward_s": round(t_fwd, 3),
             "quantizers": len(quantizers), "images": args.images, "global_batch": args.batch,
             "act_elems_per_image": round(elems * world / args.images),
