@@ -21,7 +21,7 @@ import contextlib
 import copy
 import json
 import os
-from typing import Any, Callable, Dict, Optional, Union
+from typing import Any, Callable, Dict, List, Optional, Union
 
 import torch
 from torch import nn
@@ -62,16 +62,19 @@ def _truthy(v):
 
 
 def _load_config(config_file) -> Dict:
+    # no config file: the reference's default_config.json (params symmetric, per-tensor)
     cfg = {"param_symmetric": True, "act_symmetric": False, "strict_symmetric": False,
-           "unsigned_symmetric": False, "per_channel_quantization": False}
+           "unsigned_symmetric": False, "per_channel_quantization": False, "param_symmetric_given": True}
     if config_file is None:
         return cfg
+    cfg["param_symmetric_given"] = False
     if isinstance(config_file, (str, os.PathLike)):
         with open(config_file) as f:
             config_file = json.load(f)
     d = config_file.get("defaults", {})
     if "is_symmetric" in d.get("params", {}):
         cfg["param_symmetric"] = _truthy(d["params"]["is_symmetric"])
+        cfg["param_symmetric_given"] = True
     if "is_symmetric" in d.get("ops", {}):
         cfg["act_symmetric"] = _truthy(d["ops"]["is_symmetric"])
     for k in ("strict_symmetric", "unsigned_symmetric", "per_channel_quantization"):
@@ -217,12 +220,39 @@ class QuantizationSimModel:
 
     @property
     def quant_args(self) -> Dict:
-        """v1/quantsim.py quant_args: the settings the encodings were made with."""
-        return {"activation_bitwidth": self._default_output_bw, "param_bitwidth": self._default_param_bw,
-                "dtype": "int", "is_symmetric": self._cfg["param_symmetric"],
-                "per_channel_quantization": self._cfg["per_channel_quantization"],
-                "quant_scheme": self._quant_scheme.name, "strict_symmetric": self._cfg["strict_symmetric"],
-                "unsigned_symmetric": self._cfg["unsigned_symmetric"]}
+        """aimet_common/quantsim.py:280-310 extract_global_quantizer_args (v1/quantsim.py:295): the
+        scheme's name (range learning reports its init scheme), default bitwidths, dtype, the
+        params' is_symmetric (the per-channel setting when the config does not give it) and
+        per_channel_quantization."""
+        scheme = self._quant_scheme
+        if scheme == QuantScheme.training_range_learning_with_tf_init:
+            scheme = QuantScheme.post_training_tf
+        elif scheme == QuantScheme.training_range_learning_with_tf_enhanced_init:
+            scheme = QuantScheme.post_training_tf_enhanced
+        per_channel = self._cfg["per_channel_quantization"]
+        return {"quant_scheme": scheme.name, "param_bitwidth": self._default_param_bw,
+                "activation_bitwidth": self._default_output_bw, "dtype": "int",
+                "is_symmetric": self._cfg["param_symmetric"] if self._cfg["param_symmetric_given"] else per_channel,
+                "per_channel_quantization": per_channel}
+
+    def exclude_layers_from_quantization(self, layers_to_exclude: List[nn.Module]):
+        """v1/quantsim.py:731-751: every quantization wrapper inside the given layers is replaced by
+        its original module; the wrappers' names are recorded as the excluded layers."""
+        names = {m: n for n, m in self.model.named_modules()}
+        wrappers = []
+        for layer in layers_to_exclude:
+            for m in layer.modules():
+                if isinstance(m, QcQuantizeWrapper):
+                    wrappers.append(m)
+                    self._excluded_layer_names.append(names.get(m))
+
+        def strip(parent):
+            for child_name, child in list(parent.named_children()):
+                if any(child is w for w in wrappers):
+                    setattr(parent, child_name, child.get_original_module())
+                else:
+                    strip(child)
+        strip(self.model)
 
     def export(self, path: str, filename_prefix: str, dummy_input=None):
         """Writes `<path>/<prefix>_torch.encodings` (JSON) and the model state dict

@@ -401,6 +401,179 @@ def ste16_golden():
     np.savez_compressed(os.path.join(HERE, "golden_ste16.npz"), **out)
 
 
+# ---- encoding export (the `<prefix>_torch.encodings` file) -----------------------------------
+# One layer spec per wrapper of the stand-in sim model: (name, module kind, quantizer settings).
+# Encodings are exact binary fractions and small integers so the JSON carries them unrounded.
+ENCODING_LAYERS = [
+    # name, module, input quantizers, output quantizers, params {name: quantizer}
+    ("conv1", "conv", [{"enabled": True, "bw": 8, "sym": False, "enc": [-1.0, 2.984375, 0.015625, -64]}],
+     [{"enabled": True, "bw": 8, "sym": False, "enc": [-0.25, 3.734375, 0.015625, -16]}],
+     {"weight": {"enabled": True, "bw": 4, "sym": True,
+                 "enc": [[-0.5, 0.4375, 0.0625, -8], [-1.0, 0.875, 0.125, -8], [-0.25, 0.21875, 0.03125, -8]]},
+      "bias": {"enabled": False, "bw": 8, "sym": True, "enc": None}}),
+    ("conv2", "conv", [{"enabled": False, "bw": 8, "sym": False, "enc": None}],
+     [{"enabled": True, "bw": 16, "sym": True, "enc": [-4.0, 3.9998779296875, 0.0001220703125, -32768]}],
+     {"weight": {"enabled": True, "bw": 8, "sym": True, "enc": [-0.5, 0.49609375, 0.00390625, -128]},
+      "bias": {"enabled": False, "bw": 8, "sym": True, "enc": None}}),
+    ("head.fc", "linear", [{"enabled": False, "bw": 8, "sym": False, "enc": None}],
+     [{"enabled": True, "bw": 8, "sym": False, "enc": [-8.0, 7.9375, 0.0625, -128]}],
+     {"weight": {"enabled": True, "bw": 4, "sym": False, "enc": [-0.75, 1.125, 0.125, -6]},
+      "bias": {"enabled": True, "bw": 8, "sym": True, "enc": [-2.0, 1.984375, 0.015625, -128]}}),
+    ("head.quiet", "linear", [{"enabled": False, "bw": 8, "sym": False, "enc": None}],
+     [{"enabled": False, "bw": 8, "sym": False, "enc": None}],
+     {"weight": {"enabled": False, "bw": 8, "sym": True, "enc": None},
+      "bias": {"enabled": False, "bw": 8, "sym": True, "enc": None}}),
+]
+ENCODING_SETTINGS = {"quant_scheme": "post_training_tf_enhanced", "default_param_bw": 4, "default_output_bw": 8,
+                     "config": {"defaults": {"params": {"is_symmetric": True}, "per_channel_quantization": True}},
+                     "excluded_layers": ["head.dropout"]}
+
+
+def _ast_functions(rel, names, cls=None, keep_decorators=False):
+    import ast
+    path = os.path.join(REF_ROOT, rel)
+    tree = ast.parse(open(path).read(), path)
+    body = tree.body
+    if cls is not None:
+        body = next(n for n in tree.body if isinstance(n, ast.ClassDef) and n.name == cls).body
+    fns = [n for n in body if isinstance(n, ast.FunctionDef) and n.name in names]
+    assert {f.name for f in fns} == set(names), (rel, names)
+    if not keep_decorators:
+        for f in fns:
+            f.decorator_list = []
+    return ast.Module(body=fns, type_ignores=[]), path
+
+
+def encodings_golden():
+    """golden_encodings.json: the `<prefix>_torch.encodings` content that the reference's own export
+    code writes -- QuantizationSimModel._export_encodings_to_files (v1/quantsim.py:940-1043) with
+    _get_torch_encodings_for_missing_layers (:884-938), has_valid_encodings (:2302-2323),
+    QcQuantizeWrapper.export_*_encodings and export_quantizer_encoding / get_encoding_by_quantizer
+    (v1/qc_quantize_op.py:481-497, 1514-1545), create_encoding_dict (aimet_torch/utils.py:1156-1186),
+    extract_global_quantizer_args (aimet_common/quantsim.py:280-310) and save_json_yaml
+    (aimet_common/utils.py:347-360), compiled from the reference files at generation time -- run
+    over stand-in wrappers / quantizers holding ENCODING_LAYERS (the modules cannot be imported
+    here: their import chains need the compiled libpymo). With no ONNX graph every layer takes the
+    torch-only path, as the torch encodings file is built. Stored with the layer specs it came from."""
+    import logging
+    import types
+    for p in ("TrainingExtensions/torch/src/python", "TrainingExtensions/common/src/python"):
+        if os.path.join(REF_ROOT, p) not in sys.path:
+            sys.path.insert(0, os.path.join(REF_ROOT, p))
+    from typing import Dict, List, Optional, Union
+    from aimet_common.defs import QuantizationDataType, QuantScheme
+
+    class LearnedGridTensorQuantizer:   # none of the stand-in quantizers is one
+        pass
+
+    class QcQuantizeRecurrent:
+        pass
+
+    class TfEncoding:   # libpymo.TfEncoding's fields
+        def __init__(self, mn, mx, delta, offset, bw):
+            self.min, self.max, self.delta, self.offset, self.bw = mn, mx, delta, offset, bw
+
+    ns = {"QuantizationDataType": QuantizationDataType, "QuantScheme": QuantScheme, "Dict": Dict, "List": List,
+          "Optional": Optional, "Union": Union, "LearnedGridTensorQuantizer": LearnedGridTensorQuantizer,
+          "QcQuantizeRecurrent": QcQuantizeRecurrent, "logger": logging.getLogger("golden"), "os": os,
+          "json": json, "SAVE_TO_YAML": False, "QUANTIZER_TYPE_INPUT": "input", "QUANTIZER_TYPE_OUTPUT": "output",
+          "libpymo": types.SimpleNamespace(TfEncoding=TfEncoding), "StaticGridTensorQuantizer": object,
+          "QuantizedModuleProtocol": object, "QuantSimConfigurator": object, "TensorQuantizer": object,
+          "torch": torch, "Tuple": tuple, "Any": object}
+    for rel, names, cls in (
+            ("TrainingExtensions/torch/src/python/aimet_torch/utils.py", ["create_encoding_dict"], None),
+            ("TrainingExtensions/torch/src/python/aimet_torch/v1/qc_quantize_op.py",
+             ["get_encoding_by_quantizer", "export_quantizer_encoding"], None),
+            ("TrainingExtensions/common/src/python/aimet_common/quantsim.py", ["extract_global_quantizer_args"], None),
+            ("TrainingExtensions/common/src/python/aimet_common/utils.py", ["save_json_yaml"], None),
+            ("TrainingExtensions/torch/src/python/aimet_torch/v1/quantsim.py", ["has_valid_encodings"], None)):
+        mod, path = _ast_functions(rel, names, cls)
+        exec(compile(mod, path, "exec"), ns)
+    ns["utils"] = types.SimpleNamespace(create_encoding_dict=ns["create_encoding_dict"],
+                                        DROPOUT_TYPES=(torch.nn.Dropout, torch.nn.Dropout2d, torch.nn.Dropout3d))
+    wmod, wpath = _ast_functions("TrainingExtensions/torch/src/python/aimet_torch/v1/qc_quantize_op.py",
+                                 ["export_param_encodings", "export_output_encodings", "export_input_encodings",
+                                  "get_original_module"], cls="QcQuantizeWrapper")
+    wns = dict(ns)
+    exec(compile(wmod, wpath, "exec"), wns)
+
+    class Wrapper(torch.nn.Module):   # the reference wrapper's export surface over stand-in quantizers
+        export_param_encodings = wns["export_param_encodings"]
+        export_output_encodings = wns["export_output_encodings"]
+        export_input_encodings = wns["export_input_encodings"]
+        get_original_module = wns["get_original_module"]
+
+        def __init__(self, module, ins, outs, params):
+            super().__init__()
+            self._module_to_wrap = module
+            self.input_quantizers, self.output_quantizers, self.param_quantizers = ins, outs, params
+    ns["QuantizedModuleProtocol"] = Wrapper
+    # QuantizationSimModel's export methods with their static / class method decorators, on a class
+    # of their own; the ONNX map is synthetic (one op per layer, torch's pre-1.13 naming,
+    # EXPORT_TO_ONNX_DIRECT off) so every layer takes the path a real export takes
+    from packaging import version
+    ns["version"] = version
+    omod, opath = _ast_functions("TrainingExtensions/torch/src/python/aimet_torch/onnx_utils.py",
+                                 ["get_layers_in_io_tensor_map", "get_tensor_to_consumer_map"])
+    ons = dict(ns, EXPORT_TO_ONNX_DIRECT=False)
+    exec(compile(omod, opath, "exec"), ons)
+    ns["onnx_utils"] = types.SimpleNamespace(EXPORT_TO_ONNX_DIRECT=False,
+                                             get_layers_in_io_tensor_map=ons["get_layers_in_io_tensor_map"],
+                                             get_tensor_to_consumer_map=ons["get_tensor_to_consumer_map"])
+    ns["quantsim"] = types.SimpleNamespace(encoding_version="0.6.1")
+    qsm_methods = ["_get_torch_encodings_for_missing_layers", "_update_encoding_dicts_for_layer",
+                   "_export_encodings_to_files", "_update_param_encodings_dict_for_layer",
+                   "_update_encoding_dict_for_input_activations", "_update_encoding_dict_for_output_activations",
+                   "_get_layer_input_tensors", "_get_layer_activation_tensors", "find_op_names_for_layer",
+                   "_get_output_map_str"]
+    smod, spath = _ast_functions("TrainingExtensions/torch/src/python/aimet_torch/v1/quantsim.py", qsm_methods,
+                                 cls="QuantizationSimModel", keep_decorators=True)
+    exec(compile(smod, spath, "exec"), ns)
+
+    class QuantizationSimModel:
+        pass
+    for k in qsm_methods:
+        setattr(QuantizationSimModel, k, ns.pop(k))
+    ns["QuantizationSimModel"] = QuantizationSimModel
+
+    def quantizer(spec):
+        enc = spec["enc"]
+        if enc is not None:
+            enc = [TfEncoding(*e, spec["bw"]) for e in enc] if isinstance(enc[0], list) else \
+                TfEncoding(*enc, spec["bw"])
+        return types.SimpleNamespace(enabled=spec["enabled"], bitwidth=spec["bw"], use_symmetric_encodings=spec["sym"],
+                                     data_type=QuantizationDataType.int, encoding=enc)
+
+    model = torch.nn.Module()
+    model.head = torch.nn.Module()
+    valid = set()
+    for name, kind, ins, outs, params in ENCODING_LAYERS:
+        m = torch.nn.Conv2d(3, 3, 3) if kind == "conv" else torch.nn.Linear(4, 4)
+        w = Wrapper(m, [quantizer(q) for q in ins], [quantizer(q) for q in outs],
+                    {p: quantizer(q) for p, q in params.items()})
+        parent, leaf = (model.head, name.split(".")[1]) if "." in name else (model, name)
+        setattr(parent, leaf, w)
+        valid |= {name + "." + p for p in params}
+    cfg = ENCODING_SETTINGS
+    configurator = types.SimpleNamespace(quantsim_configs=cfg["config"], default_param_bw=cfg["default_param_bw"],
+                                         default_output_bw=cfg["default_output_bw"],
+                                         default_data_type=QuantizationDataType.int)
+    qargs = ns["extract_global_quantizer_args"](QuantScheme[cfg["quant_scheme"]], configurator)
+    io_map = {}
+    for name, kind, ins, outs, params in ENCODING_LAYERS:
+        io_map[name] = types.SimpleNamespace(inputs=[name + ".in"] + [name + "." + p for p in params],
+                                             outputs=[name + ".out"])
+    with tempfile.TemporaryDirectory() as d:
+        QuantizationSimModel._export_encodings_to_files(model, d, "golden", io_map, valid, cfg["excluded_layers"],
+                                                        False, qargs)
+        with open(os.path.join(d, "golden_torch.encodings")) as f:
+            torch_encodings = json.load(f)
+    out = {"source": "the reference's own export functions (tests/golden/make_golden.py: encodings_golden)",
+           "layers": ENCODING_LAYERS, "settings": ENCODING_SETTINGS, "torch_encodings": torch_encodings}
+    with open(os.path.join(HERE, "golden_encodings.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
 def _as_bits(t):
     return t.view(torch.int16).numpy() if t.dtype in (torch.float16, torch.bfloat16) else t.numpy()
 
@@ -574,8 +747,12 @@ def main():
         json.dump(kat, f, indent=1)
     adaround_golden()
     ste16_golden()
+    encodings_golden()
     print("golden fixtures written to", HERE)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 1 and sys.argv[1] == "encodings":
+        encodings_golden()
+    else:
+        main()
