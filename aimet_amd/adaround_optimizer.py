@@ -81,14 +81,18 @@ def conv_backend(module: torch.nn.Module):
     """Context for a layer's whole iteration (forward AND autograd backward, which picks its
     backend when it runs): depthwise convolutions on PyTorch's native depthwise kernels, 3-5x
     faster than MIOpen's for the forward + weight gradient at MobileNet-v2 shapes on MI355X
-    (tools/dw_conv_time.py); everything else unchanged."""
+    (tools/dw_conv_time.py); MIOpen restricted to deterministic solutions (its weight-gradient
+    kernels may add partial sums atomically: the optimised alpha of two runs with one seed then
+    differed, tools/studies/adaround_loop_divergence.py)."""
     depthwise = isinstance(module, torch.nn.Conv2d) and 1 < module.groups == module.in_channels
-    prev = torch.backends.cudnn.enabled
+    prev, prev_det = torch.backends.cudnn.enabled, torch.backends.cudnn.deterministic
     torch.backends.cudnn.enabled = prev and not depthwise
+    torch.backends.cudnn.deterministic = True
     try:
         yield
     finally:
         torch.backends.cudnn.enabled = prev
+        torch.backends.cudnn.deterministic = prev_det
 
 
 # 1x1 convolutions and linear layers of the fused AdaRound loop as direct GEMMs (torch.matmul /

@@ -10,12 +10,11 @@
 // and its gradient.
 //
 // Numerics: the reference's arithmetic is torch float32 ops on the CPU; every op here is the same
-// IEEE operation in the same order, and the sigmoid is torch's own vectorized CPU sigmoid
-// (1 / (1 + expf(-a)) with Sleef's expf_u10 polynomial, FMA form, then an IEEE divide), so Wq and
-// the reconstruction part of dL/dalpha are bit-identical to the reference
-// (tests/golden/golden_adaround.npz). The rounding-loss gradient uses a correctly rounded
-// pow(|2h-1|, beta-1) (double) where torch uses Sleef's powf_u10: identical except where that
-// pow is not correctly rounded (measured bound in DESIGN.md §2).
+// IEEE operation in the same order, the sigmoid is torch's own vectorized CPU sigmoid
+// (1 / (1 + expf(-a)) with Sleef's expf_u10 polynomial, FMA form, then an IEEE divide) and the
+// rounding loss's pow(|2h-1|, beta) / pow(|2h-1|, beta-1) is torch's CPU pow (Sleef powf_u10 in
+// the vectorized part, the scalar tail as std::pow), so Wq and dL/dalpha, the rounding-loss term
+// included, are bit-identical to the reference (tests/golden/golden_adaround.npz).
 #include "common.hpp"
 
 namespace aimet_amd
@@ -86,9 +85,138 @@ __device__ __forceinline__ float sigmoidf(float a)
     return 1.0f / (torch_cpu_expf(0.0f - a) + 1.0f);
 }
 
-// x^e for x in [0, 1], correctly rounded from double (torch: Sleef powf_u10, or x*x*x for e == 3,
-// ATen pow_tensor_scalar_optimized_kernel)
-__device__ __forceinline__ float pow01(float x, float e)
+// ---- torch's CPU pow(tensor, scalar) for float: Vectorized<float>::pow = Sleef_powf16_u10 (the
+// AVX512F build: logkf with getexp / getmant in [0.75, 1.5), double-float arithmetic in FMA form,
+// expkf), applied to all but the last (n mod 32) elements of the contiguous loop, which take the
+// scalar std::pow (within glibc powf's 0.82 ulp: the correctly rounded result from double here).
+// Every step below is an IEEE op, so the vector part is Sleef's bit for bit: 4.5 M elements x 40
+// exponents equal to torch.pow on the CPU (tools/studies/sleef_powf_check.py).
+struct F2
+{
+    float x, y;
+};
+__device__ __forceinline__ F2 f2(float x, float y)
+{
+    return F2 {x, y};
+}
+__device__ __forceinline__ float fmapn(float x, float y, float z)   // x * y - z
+{
+    return __builtin_fmaf(x, y, -z);
+}
+__device__ __forceinline__ float fmanp(float x, float y, float z)   // z - x * y
+{
+    return __builtin_fmaf(-x, y, z);
+}
+__device__ __forceinline__ F2 df_normalize(F2 t)
+{
+    const float s = t.x + t.y;
+    return f2(s, (t.x - s) + t.y);
+}
+__device__ __forceinline__ F2 df_scale(F2 d, float s)
+{
+    return f2(d.x * s, d.y * s);
+}
+__device__ __forceinline__ F2 df_add2_ff(float x, float y)
+{
+    const float s = x + y, v = s - x;
+    return f2(s, (x - (s - v)) + (y - v));
+}
+__device__ __forceinline__ F2 df_add2_f2f(F2 x, float y)
+{
+    const float s = x.x + y, v = s - x.x;
+    const float t = (x.x - (s - v)) + (y - v);
+    return f2(s, t + x.y);
+}
+__device__ __forceinline__ F2 df_add_f2f2(F2 x, F2 y)
+{
+    const float s = x.x + y.x;
+    return f2(s, (((x.x - s) + y.x) + x.y) + y.y);
+}
+__device__ __forceinline__ F2 df_add2_f2f2(F2 x, F2 y)
+{
+    const float s = x.x + y.x, v = s - x.x;
+    const float t = (x.x - (s - v)) + (y.x - v);
+    return f2(s, t + (x.y + y.y));
+}
+__device__ __forceinline__ F2 df_add_ff2(float x, F2 y)
+{
+    const float s = x + y.x;
+    return f2(s, ((x - s) + y.x) + y.y);
+}
+__device__ __forceinline__ F2 df_squ(F2 x)
+{
+    const float s = x.x * x.x;
+    return f2(s, __builtin_fmaf(x.x + x.x, x.y, fmapn(x.x, x.x, s)));
+}
+__device__ __forceinline__ F2 df_mul_f2f2(F2 x, F2 y)
+{
+    const float s = x.x * y.x;
+    return f2(s, __builtin_fmaf(x.x, y.y, __builtin_fmaf(x.y, y.x, fmapn(x.x, y.x, s))));
+}
+__device__ __forceinline__ F2 df_mul_f2f(F2 x, float y)
+{
+    const float s = x.x * y;
+    return f2(s, __builtin_fmaf(x.y, y, fmapn(x.x, y, s)));
+}
+__device__ __forceinline__ F2 df_div(F2 n, F2 d)
+{
+    const float t = 1.0f / d.x, s = n.x * t;
+    const float u = fmapn(t, n.x, s);
+    const float v = fmanp(d.y, t, fmanp(d.x, t, 1.0f));
+    return f2(s, __builtin_fmaf(s, v, __builtin_fmaf(n.y, t, u)));
+}
+// logkf (AVX512 form) for a positive finite d
+__device__ __forceinline__ F2 sleef_logkf(float d)
+{
+    int ee;
+    (void) __builtin_frexpf(d * (1.0f / 0.75f), &ee);   // getexp: floor(log2(d / 0.75))
+    const float e = (float) (ee - 1);
+    int em;
+    float m = __builtin_frexpf(d, &em) * 2.0f;          // getmant into [0.75, 1.5)
+    if (m >= 1.5f)
+        m *= 0.5f;
+    const F2 x  = df_div(df_add2_ff(-1.0f, m), df_add2_ff(1.0f, m));
+    const F2 x2 = df_squ(x);
+    float t     = 0.240320354700088500976562f;
+    t           = __builtin_fmaf(t, x2.x, 0.285112679004669189453125f);
+    t           = __builtin_fmaf(t, x2.x, 0.400007992982864379882812f);
+    const F2 c  = f2(0.66666662693023681640625f, 3.69183861259614332084311e-09f);
+    F2 s        = df_mul_f2f(f2(0.69314718246459960938f, -1.904654323148236017e-09f), e);
+    s           = df_add_f2f2(s, df_scale(x, 2.0f));
+    return df_add_f2f2(s, df_mul_f2f2(df_mul_f2f2(x2, x), df_add2_f2f2(df_mul_f2f(x2, t), c)));
+}
+__device__ __forceinline__ float sleef_ldexp(float x, int q)
+{
+    int m = q >> 31;
+    m     = (((m + q) >> 6) - m) << 4;
+    q     = q - (m << 2);
+    m     = 0x7f + m;
+    m     = m < 0 ? 0 : (m > 0xff ? 0xff : m);
+    float u = __int_as_float(m << 23);
+    x       = x * u * u * u * u;
+    return x * __int_as_float((q + 0x7f) << 23);
+}
+__device__ __forceinline__ float sleef_expkf(F2 d)
+{
+    float u     = (d.x + d.y) * 1.442695040888963407359924681001892137426645954152985934135449406931f;
+    const int q = (int) __builtin_rintf(u);
+    F2 s        = df_add2_f2f(d, (float) q * -0.693145751953125f);
+    s           = df_add2_f2f(s, (float) q * -1.428606765330187045e-06f);
+    s           = df_normalize(s);
+    u           = 0.00136324646882712841033936f;
+    u           = __builtin_fmaf(u, s.x, 0.00836596917361021041870117f);
+    u           = __builtin_fmaf(u, s.x, 0.0416710823774337768554688f);
+    u           = __builtin_fmaf(u, s.x, 0.166665524244308471679688f);
+    u           = __builtin_fmaf(u, s.x, 0.499999850988388061523438f);
+    F2 t        = df_add_f2f2(s, df_mul_f2f(df_squ(s), u));
+    t           = df_add_ff2(1.0f, t);
+    u           = sleef_ldexp(t.x + t.y, q);
+    return d.x < -104.0f ? 0.0f : u;
+}
+
+// x^e for x in [0, 1] as torch's CPU pow: e == 2 / 3 -> x*x / x*x*x (ATen's optimized kernel);
+// Sleef_powf_u10 in the vectorized part, the correctly rounded value in the scalar tail (`tail`)
+__device__ __forceinline__ float pow01(float x, float e, bool tail)
 {
     if (e == 2.0f)
         return x * x;
@@ -96,7 +224,12 @@ __device__ __forceinline__ float pow01(float x, float e)
         return x * x * x;
     if (x == 0.0f)
         return e == 0.0f ? 1.0f : 0.0f;
-    return (float) exp((double) e * log((double) x));
+    if (e == 0.0f || x == 1.0f)
+        return 1.0f;
+    if (tail)
+        return (float) exp((double) e * log((double) x));
+    const float r = sleef_expkf(df_mul_f2f(sleef_logkf(x), e));
+    return r != r ? __builtin_inff() : r;
 }
 
 // floor(w / d) exactly as the IEEE division gives it, from q = w * rcp (rcp = v_rcp_f32(d), within
@@ -116,6 +249,7 @@ struct AdaParams
 {
     float qmax, reg, beta, beta_m1;   // beta_m1 = (float)(beta - 1) in double, as torch's pow_backward
     int soft;
+    uint32_t vec_end;   // n - n % 32: the reference's pow runs elements >= vec_end in its scalar tail
 };
 
 __device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, const AdaParams& p, float rcp)
@@ -135,8 +269,9 @@ __device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, con
 
 // dL/dalpha of Wq (clamp pass-through masks as torch autograd) + the rounding-loss gradient
 __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, float o, const AdaParams& p, float rcp,
-                                         float& loss)
+                                         float& loss, uint32_t idx)
 {
+    const bool tail = idx >= p.vec_end;
     float t   = floor_div(w, d, rcp);
     float sg  = sigmoidf(a);
     float pre = sg * kZmG + kGamma;
@@ -154,9 +289,9 @@ __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, flo
         // as autograd does: round_loss = reg * sum(1 - |2h - 1|^beta)
         float x  = 2.0f * h + -1.0f;
         float ax = fabsf(x);
-        loss += 1.0f - pow01(ax, p.beta);
+        loss += 1.0f - pow01(ax, p.beta, tail);
         // grad -reg at the pow; pow_backward: grad * (beta * x^(beta - 1)); abs: * sgn(x); 2*h: * 2
-        float dpw = (-p.reg) * (p.beta * pow01(ax, p.beta_m1));
+        float dpw = (-p.reg) * (p.beta * pow01(ax, p.beta_m1, tail));
         float dh  = (dpw * (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f))) * 2.0f;
         ga += ((in_h ? dh : 0.0f) * kZmG * (1.0f - sg)) * sg;
     }
@@ -252,10 +387,10 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
             const uint32_t c = map.channel(4 * i);
             const float d = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(d);
             f4 r;
-            r.x = ada_bwd(wv[u].x, av[u].x, gv[u].x, d, o, p, rcp, loss);
-            r.y = ada_bwd(wv[u].y, av[u].y, gv[u].y, d, o, p, rcp, loss);
-            r.z = ada_bwd(wv[u].z, av[u].z, gv[u].z, d, o, p, rcp, loss);
-            r.w = ada_bwd(wv[u].w, av[u].w, gv[u].w, d, o, p, rcp, loss);
+            r.x = ada_bwd(wv[u].x, av[u].x, gv[u].x, d, o, p, rcp, loss, 4 * i);
+            r.y = ada_bwd(wv[u].y, av[u].y, gv[u].y, d, o, p, rcp, loss, 4 * i + 1);
+            r.z = ada_bwd(wv[u].z, av[u].z, gv[u].z, d, o, p, rcp, loss, 4 * i + 2);
+            r.w = ada_bwd(wv[u].w, av[u].w, gv[u].w, d, o, p, rcp, loss, 4 * i + 3);
             __builtin_nontemporal_store(r, ga + i);
         }
     }
@@ -286,7 +421,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
     {
         uint32_t c = map.channel(i);
-        ga[i]      = ada_bwd(w[i], alpha[i], g[i], delta[c], offset[c], p, __builtin_amdgcn_rcpf(delta[c]), loss);
+        ga[i]      = ada_bwd(w[i], alpha[i], g[i], delta[c], offset[c], p, __builtin_amdgcn_rcpf(delta[c]), loss, i);
     }
     if (p.reg != 0.0f && round_loss)
     {
@@ -366,7 +501,8 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             float a[4] = {av.x, av.y, av.z, av.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                a[k] = adam_elem(a[k], ada_bwd(ww[k], a[k], gg[k], d, o, p, rcp, loss), m[k], v[k], adam, bc1, bc2s);
+                a[k] = adam_elem(a[k], ada_bwd(ww[k], a[k], gg[k], d, o, p, rcp, loss, 4 * i + k), m[k], v[k], adam, bc1,
+                                 bc2s);
             reinterpret_cast<f4*>(alpha)[i]      = f4 {a[0], a[1], a[2], a[3]};
             reinterpret_cast<f4*>(exp_avg)[i]    = f4 {m[0], m[1], m[2], m[3]};
             reinterpret_cast<f4*>(exp_avg_sq)[i] = f4 {v[0], v[1], v[2], v[3]};
@@ -383,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             const uint32_t c = map.channel(i);
             const float d = delta[c], o = offset[c];
             const float rcp = __builtin_amdgcn_rcpf(d);
-            const float ga  = ada_bwd(w[i], alpha[i], g[i], d, o, p, rcp, loss);
+            const float ga  = ada_bwd(w[i], alpha[i], g[i], d, o, p, rcp, loss, i);
             const float an  = adam_elem(alpha[i], ga, exp_avg[i], exp_avg_sq[i], adam, bc1, bc2s);
             alpha[i]        = an;
             if (wq_next)
@@ -553,7 +689,7 @@ int aimet_adaround_forward(const float* w, const float* alpha, float* wq, int64_
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, soft};
+        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, soft, (uint32_t) (n - n % 32)};
         if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(wq))
         {
             uint32_t nq = (uint32_t) (n / 4);
@@ -590,7 +726,8 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        AdaParams p {(float) ((1ull << bw) - 1), (float) reg, (float) beta, (float) (beta - 1.0), 1};
+        AdaParams p {(float) ((1ull << bw) - 1), (float) reg, (float) beta, (float) (beta - 1.0), 1,
+                     (uint32_t) (n - n % 32)};
         if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(g) &&
             aligned16(ga))
         {
@@ -756,7 +893,7 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
         require_device_ptr(it_next, "it_next");
         require_device_ptr(it_cur, "it_cur");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, 1};
+        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, 1, (uint32_t) (n - n % 32)};
         AdamArgs a {lr, beta1, beta2, eps};
         const bool vec = (C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) &&
                          aligned16(grad_wq) && aligned16(exp_avg) && aligned16(exp_avg_sq) &&

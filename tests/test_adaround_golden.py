@@ -8,9 +8,9 @@ exp underflow / overflow range).
 Bars (north_star "within 1 ULP on the dequantized float tensor"):
 * Wq (soft and hard rounding): bit-exact;
 * dL/dalpha of the reconstruction term (warm start, no rounding loss): bit-exact;
-* dL/dalpha with the rounding loss: the difference is confined to the rounding-loss branch, whose
-  pow(|2h-1|, beta-1) is correctly rounded here and Sleef powf_u10 in torch: |diff| <= 2^-21 x
-  |that branch's contribution| + 1 ulp of the result;
+* dL/dalpha with the rounding loss: bit-exact (torch's CPU pow restated: Sleef powf_u10 in the
+  vectorized part, the correctly rounded value in the scalar tail of the last n mod 32 elements --
+  cases 7 and 8 have such tails; tools/studies/sleef_powf_check.py);
 * the rounding loss value: rtol 1e-5 (float32 sums in a different order)."""
 import numpy as np
 import pytest
@@ -78,12 +78,9 @@ def test_adaround_backward_vs_reference(gad):
         a = alpha.clone().requires_grad_(True)
         loss = torch.zeros(1, device=DEV)
         (AdaroundFunction.apply(w, a, d, o, c["bw"], 0, True, reg, float(c["beta"]), loss) * g).sum().backward()
-        got = a.grad.cpu().numpy().astype(np.float64)
-        ref = c["ga_total"].astype(np.float64)
-        branch = np.abs(ref - c["ga_recon"].astype(np.float64))
-        ulp = np.spacing(np.abs(c["ga_total"])).astype(np.float64)
-        bad = np.abs(got - ref) > 2.0 ** -21 * branch + ulp
-        assert not bad.any(), (i, int(bad.sum()), got[bad][:3], ref[bad][:3])
+        got = a.grad.cpu().numpy()
+        assert np.array_equal(got.view(np.int32), c["ga_total"].view(np.int32)), \
+            (i, int((_ulps(got, c["ga_total"]) != 0).sum()), int(_ulps(got, c["ga_total"]).max()))
         want_loss = float(c["round_loss"])
         assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss), (i, loss.item(), want_loss)
 

@@ -184,3 +184,32 @@ def test_activation_sampler_concatenates_batches():
     with torch.no_grad():
         assert torch.equal(inp, torch.cat([quant[1](quant[0](d)) for d in data]))
         assert torch.equal(out, torch.cat([orig(d) for d in data]))
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("kind", ["stem", "dw", "pointwise", "linear"])
+def test_adaround_loop_deterministic(kind):
+    """Two runs of the fused loop with one seed give bit-identical alpha, for every loop form
+    (MIOpen through autograd, native depthwise, GEMM pointwise / linear): the form is a fixed rule
+    and the convolutions deterministic."""
+    from aimet_amd.adaround_optimizer import AdaroundHyperParameters, AdaroundOptimizer
+    torch.manual_seed(3)
+    if kind == "stem":
+        m, shape_in = nn.Conv2d(3, 16, 3, stride=2, padding=1), (64, 3, 32, 32)
+    elif kind == "dw":
+        m, shape_in = nn.Conv2d(16, 16, 3, padding=1, groups=16), (64, 16, 14, 14)
+    elif kind == "pointwise":
+        m, shape_in = nn.Conv2d(16, 48, 1), (64, 16, 14, 14)
+    else:
+        m, shape_in = nn.Linear(96, 40), (64, 96)
+    m = m.to(DEV)
+    inp = torch.rand(shape_in, device=DEV)
+    with torch.no_grad():
+        out = m(inp) + 0.01 * torch.randn_like(m(inp))
+    d = (m.weight.detach().abs().max() / 127).reshape(1)
+    o = torch.full((1,), -128.0, device=DEV)
+    p = AdaroundHyperParameters(num_iterations=300, warm_start=0.2)
+    a = [AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, nn.ReLU6(),
+                                             torch.Generator().manual_seed(5)).detach().clone() for _ in range(2)]
+    assert torch.equal(a[0], a[1]), AdaroundOptimizer.last_loop_form
