@@ -132,9 +132,6 @@ _PROTOTYPES = {
                                             ctypes.POINTER(_i64), ctypes.POINTER(_i64), _i64, _vp],
     "aimet_tq_get_encodings": [ctypes.POINTER(_vp), _i64, ctypes.c_uint32, _int, _int, _int, _enc_p,
                                ctypes.POINTER(_int), _vp],
-    "aimet_stream_create_cu_masked": [ctypes.POINTER(ctypes.c_uint32), ctypes.c_uint32, ctypes.POINTER(_vp)],
-    "aimet_stream_get_cu_mask": [_vp, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32)],
-    "aimet_stream_destroy": [_vp],
     "aimet_tq_reset_encoding_stats_many": [ctypes.POINTER(_vp), _i64, _vp],
     "aimet_tq_get_encodings_launch": [ctypes.POINTER(_vp), _i64, ctypes.c_uint32, _int, _int, _int, _vp,
                                       ctypes.POINTER(_vp)],
@@ -169,10 +166,6 @@ _PROTOTYPES = {
     "aimet_adaround_backward_dev": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp],
     "aimet_adaround_recon_grad": [_vp, _vp, _vp, _i64, _i64, _int, _vp],
     "aimet_dwconv2d_forward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp],
-    "aimet_dwconv2d_forward_rows": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32,
-                                    _i32, _i32, _vp],
-    "aimet_dwconv2d_grad_weight_rows": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32,
-                                        _i32, _i32, _i32, _vp],
     "aimet_dwconv2d_grad_weight_workspace": [_i64, _i64, _i64, _i64, _i32, _vp],
     "aimet_dwconv2d_grad_weight": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                                    _vp],

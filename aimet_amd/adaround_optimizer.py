@@ -81,7 +81,7 @@ def conv_backend(module: torch.nn.Module):
     """Context for a layer's whole iteration (forward AND autograd backward, which picks its
     backend when it runs): depthwise convolutions on PyTorch's native depthwise kernels, 3-5x
     faster than MIOpen's for the forward + weight gradient at MobileNet-v2 shapes on MI355X
-    (tools/dw_conv_time.py); MIOpen restricted to deterministic solutions (its weight-gradient
+    (tools/studies/dw_conv_time.py); MIOpen restricted to deterministic solutions (its weight-gradient
     kernels may add partial sums atomically: the optimised alpha of two runs with one seed then
     differed, tools/studies/adaround_loop_divergence.py)."""
     depthwise = isinstance(module, torch.nn.Conv2d) and 1 < module.groups == module.in_channels
@@ -111,10 +111,6 @@ _LOOP_FORM = os.environ.get("AIMET_ADA_LOOP_FORM", "gemm")
 # the Adam step writes the next soft-quantized weight (AIMET_ADA_FUSE_WQ=0: a forward launch per
 # iteration instead; measurements only)
 _FUSE_SOFT_WEIGHT = os.environ.get("AIMET_ADA_FUSE_WQ", "1") == "1"
-# AIMET_ADA_DW_ROWS=1: depthwise layers read the drawn batch in place from the cache
-# (aimet_dwconv2d_*_rows) instead of a gathered copy -- measured 3% slower on MobileNet-v2 (the
-# row lookup per lane costs more than the gather saves), so off by default
-_DW_ROWS = os.environ.get("AIMET_ADA_DW_ROWS", "0") == "1"
 
 
 def _is_pointwise(module: torch.nn.Module) -> bool:
@@ -563,21 +559,11 @@ class AdaroundOptimizer:
 
         def step():
             s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            # the depthwise kernels read the drawn inputs in place: the gather only moves the counter
-            dw_rows = mode == "dw" and _DW_ROWS
-            _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), None if dw_rows else P(inp),
+            _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp),
                                                     None if indexed else P(target), P(idx_all), it_cur, it_next, nb,
                                                     row_in, row_out, s))
             if not fuse_wq:
                 soft_weight()
-            if dw_rows:
-                _native.check(lib.aimet_dwconv2d_forward_rows(P(inp_data), P(idx_all), it_cur, P(wq), pbias, P(q_buf),
-                                                              *dims, s))
-                recon(q_buf, False, s)
-                _native.check(lib.aimet_dwconv2d_grad_weight_rows(P(inp_data), P(idx_all), it_cur, P(g_buf), P(gw_dw),
-                                                                  P(ws), *dims, s))
-                adam_step(gw_dw, s)
-                return
             if mode == "dw":
                 _native.check(lib.aimet_dwconv2d_forward(P(inp), P(wq), pbias, P(q_buf), *dims, s))
                 recon(q_buf, False, s)

@@ -22,59 +22,11 @@ from aimet_amd import distributed as D
 from aimet_amd.tensor_quantizer import AimetTensorQuantizer
 
 _SIDE = {}
-# tuning knobs (tools/enc_schedule_tune.py): launch order and the side stream's priority
+# tuning knobs (tools/studies/enc_schedule_tune.py): launch order and the side stream's priority
 _SCHEDULE = os.environ.get("AIMET_CAL_SCHEDULE", "params_first")
 _SIDE_PRIORITY = int(os.environ.get("AIMET_CAL_SIDE_PRIORITY", "-1"))
-# CUs per XCD given to the parameters' stream when the CUs are partitioned (0: no partition, both
-# streams may use every CU)
-_SIDE_CUS_PER_XCD = int(os.environ.get("AIMET_CAL_SIDE_CUS_PER_XCD", "0"))
 # the parameters' statistics + search on the activations' stream, ahead of the passes (no overlap)
 _PARAMS_SERIAL = os.environ.get("AIMET_CAL_PARAMS_SERIAL", "0") == "1"
-_PARTITION = {}
-_XCDS = 8   # gfx950: 8 XCDs, 32 CUs each
-
-
-def side_cu_mask(n_cus: int, per_xcd: int, xcds: int = _XCDS) -> List[int]:
-    """CU-mask words (bit i = CU i) for the parameters' stream: `per_xcd` CUs on every XCD.
-
-    The driver distributes the mask bits of a multi-XCD device over the XCDs; whether it deals them
-    round-robin (bit i -> XCD i % 8) or in blocks of 32 (bit i -> XCD i // 32), this layout gives
-    every XCD exactly `per_xcd` of them: in block x it takes bits 32x + 8(j % 4) + (x + j) % 8,
-    j < per_xcd, whose residues mod 8 also cover every XCD equally. The activation stream gets the
-    complement, so each XCD keeps 32 - per_xcd CUs for the HBM passes."""
-    per_block = n_cus // xcds
-    if not 0 < per_xcd <= min(8, per_block // 4):
-        raise ValueError("per_xcd must be in [1, %d] for %d CUs" % (min(8, per_block // 4), n_cus))
-    bits = [per_block * x + 8 * (j % 4) + (x + j) % 8 for x in range(xcds) for j in range(per_xcd)]
-    words = [0] * ((n_cus + 31) // 32)
-    for b in bits:
-        words[b // 32] |= 1 << (b % 32)
-    return words
-
-
-def _partition_streams(dev: torch.device, per_xcd: int):
-    """(activation stream, parameter stream): two CU-masked streams created once per device
-    (aimet_stream_create_cu_masked), wrapped as torch ExternalStreams."""
-    import ctypes
-
-    from aimet_amd import _native as N
-    key = (dev.index if dev.index is not None else torch.cuda.current_device(), per_xcd)
-    if key not in _PARTITION:
-        n_cus = torch.cuda.get_device_properties(key[0]).multi_processor_count
-        side = side_cu_mask(n_cus, per_xcd)
-        full = [0xFFFFFFFF] * len(side)
-        if n_cus % 32:
-            full[-1] = (1 << (n_cus % 32)) - 1
-        main = [f & ~w for f, w in zip(full, side)]
-        out = []
-        with torch.cuda.device(key[0]):
-            for words in (main, side):
-                arr = (ctypes.c_uint32 * len(words))(*words)
-                h = ctypes.c_void_p()
-                N.call("aimet_stream_create_cu_masked", arr, len(words), ctypes.byref(h))
-                out.append(torch.cuda.ExternalStream(h.value, device=torch.device("cuda", key[0])))
-        _PARTITION[key] = tuple(out)
-    return _PARTITION[key]
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -124,29 +76,19 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
               and all(t.dtype == torch.float32 for t in list(activations) + list(params)))
     if native:
         cur = torch.cuda.current_stream(dev)
-        if _SIDE_CUS_PER_XCD:
-            main, side = _partition_streams(dev, _SIDE_CUS_PER_XCD)
-            main.wait_stream(cur)
-        else:
-            main, side = cur, (cur if _PARAMS_SERIAL else _side_stream(dev))
+        main, side = cur, (cur if _PARAMS_SERIAL else _side_stream(dev))
         a_pending, p_pending, keep = AimetTensorQuantizer.calibrateResidentAsync(
             act_quantizers, activations, param_quantizers, params, param_ch_axes, act_settings, param_settings,
             reset=reset, main_stream=main, side_stream=side)
         p_res = p_pending.result()
         a_res = a_pending.result()
-        if main is not cur:
-            cur.wait_stream(main)
         del keep
         return a_res, p_res
     if reset:
         AimetTensorQuantizer.resetEncodingStatsMany(list(act_quantizers) + list(param_quantizers))
     AimetTensorQuantizer._ensure_many(list(act_quantizers) + list(param_quantizers), dev)
     cur = torch.cuda.current_stream(dev)
-    if _SIDE_CUS_PER_XCD:
-        main, side = _partition_streams(dev, _SIDE_CUS_PER_XCD)
-        main.wait_stream(cur)
-    else:
-        main, side = cur, _side_stream(dev)
+    main, side = cur, _side_stream(dev)
     # the inputs are ordered on the current stream (torch's stream semantics); the side stream
     # starts after everything queued there so far (a device-side dependency, no host wait)
     side.wait_stream(cur)

@@ -96,36 +96,6 @@ int aimet_device_count(void)
     return rc == AIMET_OK ? n : rc;
 }
 
-int aimet_stream_create_cu_masked(const uint32_t* cu_mask, uint32_t words, void** stream)
-{
-    return guarded([&] {
-        if (cu_mask == nullptr || stream == nullptr || words == 0)
-            throw InvalidArgument("aimet_stream_create_cu_masked: null mask / stream or empty mask");
-        uint32_t any = 0;
-        for (uint32_t i = 0; i < words; ++i)
-            any |= cu_mask[i];
-        if (any == 0)
-            throw InvalidArgument("aimet_stream_create_cu_masked: the mask enables no CU");
-        hipStream_t s = nullptr;
-        AIMET_HIP_CHECK(hipExtStreamCreateWithCUMask(&s, words, cu_mask));
-        *stream = reinterpret_cast<void*>(s);
-    });
-}
-
-int aimet_stream_get_cu_mask(void* stream, uint32_t words, uint32_t* cu_mask)
-{
-    return guarded([&] {
-        if (cu_mask == nullptr || words == 0)
-            throw InvalidArgument("aimet_stream_get_cu_mask: null or empty mask buffer");
-        AIMET_HIP_CHECK(hipExtStreamGetCUMask(reinterpret_cast<hipStream_t>(stream), words, cu_mask));
-    });
-}
-
-int aimet_stream_destroy(void* stream)
-{
-    return guarded([&] { AIMET_HIP_CHECK(hipStreamDestroy(reinterpret_cast<hipStream_t>(stream))); });
-}
-
 int aimet_get_computed_encodings(int32_t bw, double mn, double mx, int sym, int strict, int unsign,
                                  aimet_tf_encoding* out)
 {

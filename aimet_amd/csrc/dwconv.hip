@@ -31,23 +31,10 @@ struct DwShape
     FastDiv div_ow, div_ohow, div_c;
 };
 
-// batch sample n of x: row rows[it * nb + n] of a cached [rows, C, H, W] tensor (the AdaRound
-// loop's drawn batch read in place, it = it_cur[0]), or sample n itself when rows is null
-struct DwRows
-{
-    const int64_t* rows;
-    const int64_t* it_cur;
-    int64_t nb;
-    __device__ __forceinline__ size_t sample(uint32_t n) const
-    {
-        return rows ? (size_t) rows[it_cur[0] * nb + n] : (size_t) n;
-    }
-};
-
 template <int K>
 __global__ __launch_bounds__(kBlock) void dw_fwd_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ bias, float* __restrict__ y,
-                                                        DwShape s, uint32_t total, DwRows rows)
+                                                        DwShape s, uint32_t total)
 {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= total)
@@ -58,7 +45,7 @@ __global__ __launch_bounds__(kBlock) void dw_fwd_kernel(const float* __restrict_
     const uint32_t ow  = rem - oh * s.OW;
     const uint32_t n   = s.div_c.div(nc);
     const uint32_t c   = nc - n * s.C;
-    const float* xp    = x + (rows.sample(n) * s.C + c) * s.H * s.W;
+    const float* xp    = x + ((size_t) n * s.C + c) * s.H * s.W;
     const float* wp    = w + c * K * K;
     float v            = bias ? bias[c] : 0.0f;
     const int ih0 = (int) oh * s.stride - s.pad, iw0 = (int) ow * s.stride - s.pad;
@@ -83,8 +70,7 @@ __global__ __launch_bounds__(kBlock) void dw_fwd_kernel(const float* __restrict_
 // N*OH*OW outputs (position p = (n * OH + oh) * OW + ow)
 template <int K>
 __global__ __launch_bounds__(kBlock) void dw_wgrad_kernel(const float* __restrict__ x, const float* __restrict__ gy,
-                                                          float* __restrict__ partial, DwShape s, uint32_t per,
-                                                          DwRows rows)
+                                                          float* __restrict__ partial, DwShape s, uint32_t per)
 {
     constexpr int KK  = K * K;
     const uint32_t c  = blockIdx.y;
@@ -104,7 +90,7 @@ __global__ __launch_bounds__(kBlock) void dw_wgrad_kernel(const float* __restric
         const uint32_t ow  = rem - oh * s.OW;
         const size_t plane = (size_t) n * s.C + c;
         const float g      = gy[plane * s.OH * s.OW + rem];
-        const float* xp    = x + (rows.sample(n) * s.C + c) * s.H * s.W;
+        const float* xp    = x + ((size_t) n * s.C + c) * s.H * s.W;
         const int ih0 = (int) oh * s.stride - s.pad, iw0 = (int) ow * s.stride - s.pad;
 #pragma unroll
         for (int kh = 0; kh < K; ++kh)
@@ -201,7 +187,7 @@ namespace
 
 void dw_forward(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,
                 int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride, int32_t pad, int32_t dilation,
-                DwRows rows, hipStream_t st)
+                hipStream_t st)
 {
     DwShape s = make_shape(N, C, H, W, OH, OW, K, stride, pad, dilation);
     require_device_ptr(x, "x");
@@ -212,15 +198,15 @@ void dw_forward(const float* x, const float* w, const float* bias, float* y, int
     const uint32_t total = (uint32_t) (N * C * OH * OW);
     const unsigned grid  = (unsigned) ceil_div(total, kBlock);
     if (K == 3)
-        dw_fwd_kernel<3><<<grid, kBlock, 0, st>>>(x, w, bias, y, s, total, rows);
+        dw_fwd_kernel<3><<<grid, kBlock, 0, st>>>(x, w, bias, y, s, total);
     else
-        dw_fwd_kernel<5><<<grid, kBlock, 0, st>>>(x, w, bias, y, s, total, rows);
+        dw_fwd_kernel<5><<<grid, kBlock, 0, st>>>(x, w, bias, y, s, total);
     AIMET_LAUNCH_CHECK();
 }
 
 void dw_grad_weight(const float* x, const float* grad_y, float* grad_w, float* workspace, int64_t N, int64_t C,
                     int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride, int32_t pad,
-                    int32_t dilation, DwRows rows, hipStream_t st)
+                    int32_t dilation, hipStream_t st)
 {
     DwShape s = make_shape(N, C, H, W, OH, OW, K, stride, pad, dilation);
     require_device_ptr(x, "x");
@@ -237,25 +223,15 @@ void dw_grad_weight(const float* x, const float* grad_y, float* grad_w, float* w
                                : static_cast<float*>(scratch_alloc(sizeof(float) * (size_t) (C * S * K * K), st));
     dim3 grid((unsigned) S, (unsigned) C);
     if (K == 3)
-        dw_wgrad_kernel<3><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per, rows);
+        dw_wgrad_kernel<3><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per);
     else
-        dw_wgrad_kernel<5><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per, rows);
+        dw_wgrad_kernel<5><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per);
     AIMET_LAUNCH_CHECK();
     dw_wgrad_fold<<<(unsigned) ceil_div(C * K * K, kBlock), kBlock, 0, st>>>(partial, grad_w, (uint32_t) C,
                                                                             (uint32_t) S, (uint32_t) (K * K));
     AIMET_LAUNCH_CHECK();
     if (!workspace)
         scratch_free(partial, st);
-}
-
-DwRows rows_of(const int64_t* idx_all, const int64_t* it_cur, int64_t nb)
-{
-    if (idx_all == nullptr)
-        return DwRows {nullptr, nullptr, 0};
-    require_device_ptr(idx_all, "idx_all");
-    require_device_ptr(it_cur, "it_cur");
-    AIMET_REQUIRE(nb > 0, "invalid batch size");
-    return DwRows {idx_all, it_cur, nb};
 }
 
 }   // namespace
@@ -267,18 +243,7 @@ int aimet_dwconv2d_forward(const float* x, const float* w, const float* bias, fl
                            int32_t dilation, void* stream)
 {
     return guarded([&] {
-        dw_forward(x, w, bias, y, N, C, H, W, OH, OW, K, stride, pad, dilation, DwRows {nullptr, nullptr, 0},
-                   as_stream(stream));
-    });
-}
-
-int aimet_dwconv2d_forward_rows(const float* x_cache, const int64_t* idx_all, const int64_t* it_cur, const float* w,
-                                const float* bias, float* y, int64_t N, int64_t C, int64_t H, int64_t W, int64_t OH,
-                                int64_t OW, int32_t K, int32_t stride, int32_t pad, int32_t dilation, void* stream)
-{
-    return guarded([&] {
-        dw_forward(x_cache, w, bias, y, N, C, H, W, OH, OW, K, stride, pad, dilation, rows_of(idx_all, it_cur, N),
-                   as_stream(stream));
+        dw_forward(x, w, bias, y, N, C, H, W, OH, OW, K, stride, pad, dilation, as_stream(stream));
     });
 }
 
@@ -297,18 +262,7 @@ int aimet_dwconv2d_grad_weight(const float* x, const float* grad_y, float* grad_
 {
     return guarded([&] {
         dw_grad_weight(x, grad_y, grad_w, workspace, N, C, H, W, OH, OW, K, stride, pad, dilation,
-                       DwRows {nullptr, nullptr, 0}, as_stream(stream));
-    });
-}
-
-int aimet_dwconv2d_grad_weight_rows(const float* x_cache, const int64_t* idx_all, const int64_t* it_cur,
-                                    const float* grad_y, float* grad_w, float* workspace, int64_t N, int64_t C,
-                                    int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride,
-                                    int32_t pad, int32_t dilation, void* stream)
-{
-    return guarded([&] {
-        dw_grad_weight(x_cache, grad_y, grad_w, workspace, N, C, H, W, OH, OW, K, stride, pad, dilation,
-                       rows_of(idx_all, it_cur, N), as_stream(stream));
+                       as_stream(stream));
     });
 }
 

@@ -2,7 +2,7 @@
 //
 // Reference: trim_functions.cu:46-92 (one element per thread, 512-thread blocks, fast-math
 // division, per-element global loads of the per-channel table, legacy default stream).
-// The per-element IEEE division stays (tools/qdq_variants.hip: the reciprocal fast path of
+// The per-element IEEE division stays (tools/studies/qdq_variants.hip: the reciprocal fast path of
 // common.hpp measures 4% slower here -- this kernel is HBM-bound, the fast path's extra VGPRs and
 // branch cost more than the division; it pays off in the 16-bit and histogram kernels).
 // MI355X design: HBM-bound streaming (8 B/elem fwd, 12 B/elem STE) -> one 16-B vector per lane,
@@ -41,7 +41,7 @@ __device__ __forceinline__ float apply(float x, const QdqParams& p, float shift,
 // Per-tensor: parameters are kernel arguments (SGPRs). One 16-B vector per lane, one tile per
 // workgroup, non-temporal (streaming) loads and stores: measured on MI355X at 6.6 TB/s for a
 // 2 GiB in+out stream vs 5.6 TB/s for a grid-strided 4-vector loop with default cache policy
-// (tools/qdq_variants.hip, profiles/r01/qdq_variants.txt).
+// (tools/studies/qdq_variants.hip, profiles/r01/qdq_variants.txt).
 // ---------------------------------------------------------------------------------------
 typedef float f4 __attribute__((ext_vector_type(4)));
 

@@ -98,7 +98,7 @@ __device__ __forceinline__ void minmax_part(const float* __restrict__ x, int64_t
     float mn = INFINITY, mx = -INFINITY;
     if (vec)
     {
-        // streaming 16-B loads, 4 in flight per lane (tools/hist_variants.hip: 6.8 TB/s)
+        // streaming 16-B loads, 4 in flight per lane (tools/studies/hist_variants.hip: 6.8 TB/s)
         const f4* x4         = reinterpret_cast<const f4*>(x);
         int64_t nvec         = n / 4;
         const int64_t stride = nblk * kBlock * 4;
@@ -433,7 +433,7 @@ __device__ __forceinline__ void histogram_part(const float* __restrict__ x, int6
     int64_t done = 0;
     if (vec)
     {
-        // 4 x 16-B streaming loads in flight per lane (tools/hist_variants.hip: 5.6-5.8 TB/s)
+        // 4 x 16-B streaming loads in flight per lane (tools/studies/hist_variants.hip: 5.6-5.8 TB/s)
         const f4* x4         = reinterpret_cast<const f4*>(x);
         const int64_t nv     = n / 4;
         const int64_t stride = nblk * BLOCK * kHistUnroll;
@@ -649,7 +649,7 @@ __device__ __forceinline__ int find_job(const StatsJob* __restrict__ jobs, int n
 // One 16-KiB tile per step (4 x 16-B nontemporal loads per lane), the tiles of every quantizer in
 // address order, one {-min, max} partial per tile: the workgroups in flight read one contiguous
 // window of HBM (6.7 vs 5.9 TB/s for grid-stride workgroups inside each tensor,
-// tools/read_ceiling.py). A first batch of <= 64 quantizers runs one workgroup per tile (1.64 ms
+// tools/studies/read_ceiling.py). A first batch of <= 64 quantizers runs one workgroup per tile (1.64 ms
 // on ResNet-50's activations); later batches of PDF schemes, where every quantizer's range is
 // fixed, and larger tables run kMmGrid workgroups that walk the tiles and skip a fixed quantizer
 // at once (ViT-L/16 calibration: 900 -> 1016 Gelem/s; profiles/r02/compute_encodings_study.txt).

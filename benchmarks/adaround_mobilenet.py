@@ -13,7 +13,7 @@ per iteration and the loop form that ran it (dw: native depthwise kernels; point
 direct GEMMs; autograd: MIOpen through autograd -- layers with two forms time both at capture and
 keep the faster); with --reference-iters the same loop using the reference's torch-op soft
 quantization + rounding loss (oracle/torch_ref.py) for comparison. The per-kernel split of the
-loop comes from rocprofv3 (tools/ada_trace_summary.py), not from host-timed launches.
+loop comes from rocprofv3 (tools/studies/ada_trace_summary.py), not from host-timed launches.
 """
 import argparse
 import json
@@ -145,7 +145,7 @@ def main():
         "loop": "eager" if args.eager else "hipgraph (one captured iteration replayed per iteration)",
         "miopen_find": bool(args.miopen_find),
         "weights_elems": sum(int(torch.Size(p[1]).numel()) for p in per_layer),
-        "kernel_split": "per-kernel time of the loop: rocprofv3 --kernel-trace + tools/ada_trace_summary.py "
+        "kernel_split": "per-kernel time of the loop: rocprofv3 --kernel-trace + tools/studies/ada_trace_summary.py "
                         "(profiles/r02/adaround_loop_kernels_*.csv)",
         "data": "synthetic U(0,1) images (seed 7), random-init MobileNet-v2 with folded BN (seed 0)",
     }

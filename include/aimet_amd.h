@@ -63,13 +63,6 @@ const char* aimet_last_error(void);
 const char* aimet_version(void);
 /* Number of gfx950 devices visible; negative status on HIP failure. */
 int aimet_device_count(void);
-/* Streams restricted to a set of CUs (hipExtStreamCreateWithCUMask; bit i of the mask words =
- * CU i, words of 32 bits). compute_encodings partitions the CUs between the HBM-bound activation
- * passes and the compute-bound parameter searches with two such streams, so the two run side by
- * side instead of competing for every CU (no reference counterpart: host scheduling only). */
-int aimet_stream_create_cu_masked(const uint32_t* cu_mask, uint32_t words, void** stream);
-int aimet_stream_get_cu_mask(void* stream, uint32_t words, uint32_t* cu_mask);
-int aimet_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Encoding math (host, exact reference arithmetic)                                            */
@@ -466,16 +459,6 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
 int aimet_dwconv2d_forward(const float* x, const float* w, const float* bias, float* y, int64_t N, int64_t C,
                            int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride, int32_t pad,
                            int32_t dilation, void* stream);
-/* The same with the batch read in place from a cached [rows][C][H][W] tensor: sample n of the
- * batch is row idx_all[it_cur[0] * N + n] (the AdaRound loop's drawn batch, no gathered copy). */
-int aimet_dwconv2d_forward_rows(const float* x_cache, const int64_t* idx_all_dev, const int64_t* it_cur_dev,
-                                const float* w, const float* bias, float* y, int64_t N, int64_t C, int64_t H,
-                                int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride, int32_t pad,
-                                int32_t dilation, void* stream);
-int aimet_dwconv2d_grad_weight_rows(const float* x_cache, const int64_t* idx_all_dev, const int64_t* it_cur_dev,
-                                    const float* grad_y, float* grad_w, float* workspace, int64_t N, int64_t C,
-                                    int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride,
-                                    int32_t pad, int32_t dilation, void* stream);
 int aimet_dwconv2d_grad_weight_workspace(int64_t N, int64_t C, int64_t OH, int64_t OW, int32_t K, int64_t* elems);
 int aimet_dwconv2d_grad_weight(const float* x, const float* grad_y, float* grad_w, float* workspace, int64_t N,
                                int64_t C, int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride,

@@ -1216,24 +1216,6 @@ def test_depthwise_conv_kernels_vs_torch(N, C, H, K, stride, pad, dil):
     torch.testing.assert_close(gw2, gw, rtol=0, atol=0)          # deterministic
     scale = float((gy.abs().sum() * x.abs().max()) / (N * OH * OW) ** 0.5)
     torch.testing.assert_close(gw, wr.grad, rtol=2e-5, atol=1e-6 * scale)
-    # the row-mapped forms read the batch in place from a larger cache: == the plain kernels on
-    # the gathered batch, bit for bit (iteration 1 of a 2-iteration index table)
-    cache = torch.randn(3 * N + 1, C, H, H, device=DEV, generator=g)
-    idx = torch.randint(0, cache.shape[0], (2, N), device=DEV, generator=g)
-    it = torch.tensor([1], dtype=torch.int64, device=DEV)
-    xb = cache.index_select(0, idx[1]).contiguous()
-    y_plain, y_rows = torch.empty_like(ref), torch.empty_like(ref)
-    _native.call("aimet_dwconv2d_forward", xb.data_ptr(), w.data_ptr(), b.data_ptr(), y_plain.data_ptr(), N, C, H, H,
-                 OH, OW, K, stride, pad, dil, s)
-    _native.call("aimet_dwconv2d_forward_rows", cache.data_ptr(), idx.data_ptr(), it.data_ptr(), w.data_ptr(),
-                 b.data_ptr(), y_rows.data_ptr(), N, C, H, H, OH, OW, K, stride, pad, dil, s)
-    assert torch.equal(y_rows, y_plain)
-    g_plain, g_rows = torch.empty_like(w), torch.empty_like(w)
-    _native.call("aimet_dwconv2d_grad_weight", xb.data_ptr(), gy.data_ptr(), g_plain.data_ptr(), ws.data_ptr(), N, C,
-                 H, H, OH, OW, K, stride, pad, dil, s)
-    _native.call("aimet_dwconv2d_grad_weight_rows", cache.data_ptr(), idx.data_ptr(), it.data_ptr(), gy.data_ptr(),
-                 g_rows.data_ptr(), ws.data_ptr(), N, C, H, H, OH, OW, K, stride, pad, dil, s)
-    assert torch.equal(g_rows, g_plain)
 
 
 @pytest.mark.parametrize("layer", ["conv", "depthwise", "pointwise", "linear", "linear_noact", "conv_gelu"])

@@ -1,0 +1,47 @@
+"""Isolated timing of the device encoding searches (TF-Enhanced tfe_search_kernel, MSE
+mse_search_kernel, entropy entropy_search_kernel) on ResNet-50's weights: 27,560 channels,
+per-channel symmetric and asymmetric 8-bit, statistics computed once, then getEncodings repeated.
+usage: tfe_search_time.py [TF_ENHANCED] [MSE] [ENTROPY]. Run under `rocprofv3 --kernel-trace --stats`
+for the kernel durations; the wall-clock per batched getEncodings (search + copy + host encodings) is printed. Tuning tool."""
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from aimet_amd.libpymo import QuantizationMode  # noqa: E402
+from aimet_amd.tensor_quantizer import AimetTensorQuantizer  # noqa: E402
+from workloads.resnet import resnet50  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    model = resnet50(seed=0, device=dev)
+    ws = [m.weight.detach().contiguous() for m in model.modules() if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear))]
+    schemes = sys.argv[1:] or ["TF_ENHANCED"]
+    for scheme in schemes:
+        qs = [AimetTensorQuantizer(getattr(QuantizationMode, "QUANTIZATION_" + scheme), num_channels=w.shape[0])
+              for w in ws]
+        AimetTensorQuantizer.updateStatsPerChannelMany(qs, ws)
+        torch.cuda.synchronize()
+        run(scheme, qs, ws)
+
+
+def run(scheme, qs, ws):
+    for sym in (True, False):
+        AimetTensorQuantizer.getEncodings(qs, 8, sym, False, False)   # warm
+        t = []
+        for _ in range(10):
+            t0 = time.perf_counter()
+            AimetTensorQuantizer.getEncodings(qs, 8, sym, False, False)
+            t.append(time.perf_counter() - t0)
+        t.sort()
+        print("%s %s: %d channels, getEncodings median %.3f ms" % (scheme, "sym" if sym else "asym",
+                                                                 sum(w.shape[0] for w in ws), t[len(t) // 2] * 1e3),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
