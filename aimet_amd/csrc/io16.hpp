@@ -35,7 +35,7 @@ __device__ __forceinline__ unsigned short from_f32(float f)
     // fptrunc(fmul(a, b)) into v_fma_mix{lo,hi}_f16(a, b, 0), which rounds the exact product
     // straight to fp16 (no fp32 rounding first: differs from torch's two-step cast near fp16
     // rounding boundaries) and adds +0 (turns a -0 result into +0).
-    asm volatile("" : "+v"(f));
+    asm("" : "+v"(f));
     if constexpr (IO == IO_F16)
         return __half_as_ushort(__float2half_rn(f));
     else

@@ -15,6 +15,9 @@
 #include "common.hpp"
 #include <atomic>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <utility>
 #include "io16.hpp"
 
 namespace aimet_amd
@@ -91,26 +94,62 @@ __device__ __forceinline__ void div_rn_n(const float* x, float d, float y, float
     }
 }
 
+// rint(RN(x / d)) where only the rounded quotient is consumed, from y = lg_recip(d) (not NaN:
+// |d| in [2^-40, 2^40]) and no branch: while |q0| < 2^60 the Markstein quotient q is RN(x / d)
+// (div_rn) -- except for |x| < 2^-100, where q may be off but |q| < 2^-59, so rint(q) is a zero
+// as rint(RN(x / d)) is; for |q0| >= 2^60 (and +-inf) rint(q0) is beyond every clamp bound of the
+// forward ( |offset| + steps < 2^33 ) on the same side as rint(RN(x / d)); a NaN x gives NaN. The
+// sign of a zero rint may differ from the division's, which the forward cannot observe: with
+// offset = +0, round - offset = +-0 is clamped and then + offset = +0 again, and with any other
+// offset round - offset does not depend on the zero's sign.
+__device__ __forceinline__ float lg_rint_quot(float x, float d, float y)
+{
+    const float q0 = x * y;
+    const float q  = __builtin_fmaf(__builtin_fmaf(-q0, d, x), y, q0);
+    return __builtin_rintf(__builtin_fabsf(q0) < 0x1p60f ? q : q0);
+}
+
+// torch's clamp(v, lo, hi) = minimum(maximum(v, lo), hi): a NaN passes through (gfx950's
+// v_maximum3 / v_minimum3, IEEE 754-2019). It differs from torch only in the sign of a zero
+// (maximum(-0, +0) = +0), which every use below adds an offset to, where -0 + o == +0 + o.
+__device__ __forceinline__ float t_clamp(float v, float lo, float hi)
+{
+    return __builtin_elementwise_minimum(__builtin_elementwise_maximum(v, lo), hi);
+}
+
+// the reference's forward with the division: encodings that lg_recip refuses (or a non-finite
+// offset)
+__device__ __forceinline__ float lg_qdq_div(float x, float d, float o, float steps)
+{
+    return (t_clamp(__builtin_rintf(x / d) - o, 0.0f, steps) + o) * d;
+}
+
+__device__ __forceinline__ bool lg_fast_enc(float o, float rd)
+{
+    return rd == rd && __builtin_fabsf(o) <= 0x1p32f;
+}
+
 // x_round = round(x / delta) - offset ; x_quant = clamp(x_round, 0, steps) ; y = (x_quant + offset) * delta
-// (rd = lg_recip(d))
+// (rd = lg_recip(d)); a NaN x gives NaN as torch's clamp does
 __device__ __forceinline__ float lg_qdq(float x, float d, float o, float steps, float rd)
 {
-    float xr = __builtin_rintf(div_rn(x, d, rd)) - o;
-    float xq = fminf(fmaxf(xr, 0.0f), steps);
-    return (xq + o) * d;
+    if (!lg_fast_enc(o, rd))
+        return lg_qdq_div(x, d, o, steps);
+    return (t_clamp(lg_rint_quot(x, d, rd) - o, 0.0f, steps) + o) * d;
 }
 template <int N>
 __device__ __forceinline__ void lg_qdq_n(const float* x, float d, float o, float steps, float rd, float* y)
 {
-    float q[N];
-    div_rn_n<N>(x, d, rd, q);
+    if (!lg_fast_enc(o, rd))
+    {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            y[k] = lg_qdq_div(x[k], d, o, steps);
+        return;
+    }
 #pragma unroll
     for (int k = 0; k < N; ++k)
-    {
-        float xr = __builtin_rintf(q[k]) - o;
-        float xq = fminf(fmaxf(xr, 0.0f), steps);
-        y[k]     = (xq + o) * d;
-    }
+        y[k] = (t_clamp(lg_rint_quot(x[k], d, rd) - o, 0.0f, steps) + o) * d;
 }
 
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
@@ -298,46 +337,42 @@ struct Sums
     float a, b, d;
 };
 
-// rint(RN(x / dl)) and q = RN(x / dl) itself (div_rn, rcp = lg_recip(dl)): the quotient is the
-// reference's x / delta bit for bit, so each term of sum B is the reference's
-// mask * (x / delta) * grad.
-__device__ __forceinline__ float rint_div(float x, float dl, float rcp, float& q)
+// One element of the backward (calculate_forward_pass + the gradient expressions of
+// QuantizeDequantizeFunc.backward / asymmetric_gradients / symmetric_gradients), with
+// q = RN(x / dl) itself (div_rn, rcp = lg_recip(dl)), the reference's x / delta bit for bit:
+//   grad_x += mask * grad ;  A += (x_quant + offset) * grad ;  D += grad where !mask ;
+//   B += mask * (x / delta) * grad   (asym: (x * mask / delta) * grad: where !mask the term is
+//        0 * x / delta -- NaN for a non-finite x -- rather than 0 * (x / delta), NaN also when
+//        the quotient overflows).
+// x_quant is torch's clamp, which passes a NaN round through (A turns NaN as the reference's sum).
+__device__ __forceinline__ void lg_bwd_term(float x, float q, float g, float o, float steps, bool asym, float& gx,
+                                            Sums& s)
 {
-    q = div_rn(x, dl, rcp);
-    return __builtin_rintf(q);
+    const float xr  = __builtin_rintf(q) - o;
+    const bool mask = (xr >= 0.0f) && (xr <= steps);
+    const float xq  = t_clamp(xr, 0.0f, steps);
+    gx = mask ? g : 0.0f * g;      // mask_tensor * grad (keeps -0 / NaN behaviour of a multiply)
+    s.a += (xq + o) * g;
+    s.b += (mask ? q : 0.0f * (asym ? x : q)) * g;
+    s.d += mask ? 0.0f : g;
 }
 
 __device__ __forceinline__ void lg_bwd_elem(float x, float g, float dl, float o, float steps, float rcp, float& gx,
-                                            Sums& s)
+                                            Sums& s, bool asym)
 {
-    float q;
-    float xr   = rint_div(x, dl, rcp, q) - o;
-    bool mask  = (xr >= 0.0f) && (xr <= steps);
-    float xq   = fminf(fmaxf(xr, 0.0f), steps);
-    gx         = mask ? g : 0.0f * g;      // mask_tensor * grad (keeps -0 / NaN behaviour of a multiply)
-    s.a += (xq + o) * g;
-    s.b += mask ? q * g : 0.0f;
-    s.d += mask ? 0.0f : g;
+    lg_bwd_term(x, div_rn(x, dl, rcp), g, o, steps, asym, gx, s);
 }
 
 // lg_bwd_elem over N elements in order (the same sums), the quotients by div_rn_n
 template <int N>
 __device__ __forceinline__ void lg_bwd_elems(const float* x, const float* g, float dl, float o, float steps,
-                                             float rcp, float* gx, Sums& s)
+                                             float rcp, float* gx, Sums& s, bool asym)
 {
     float q[N];
     div_rn_n<N>(x, dl, rcp, q);
 #pragma unroll
     for (int k = 0; k < N; ++k)
-    {
-        float xr  = __builtin_rintf(q[k]) - o;
-        bool mask = (xr >= 0.0f) && (xr <= steps);
-        float xq  = fminf(fmaxf(xr, 0.0f), steps);
-        gx[k]     = mask ? g[k] : 0.0f * g[k];
-        s.a += (xq + o) * g[k];
-        s.b += mask ? q[k] * g[k] : 0.0f;
-        s.d += mask ? 0.0f : g[k];
-    }
+        lg_bwd_term(x[k], q[k], g[k], o, steps, asym, gx[k], s);
 }
 
 __device__ __forceinline__ Sums block_reduce(Sums s)
@@ -379,7 +414,6 @@ __device__ __forceinline__ Sums block_reduce(Sums s)
 // sums. (A grid-stride form with one pair of loads per lane in flight ran at 0.47 of HBM peak on
 // the 16-bit Llama-3-8B activations.)
 constexpr int kLgTileSteps = 2;
-constexpr int64_t kLgTile  = (int64_t) kBlock * 8 * kLgTileSteps;
 
 // a tile's element e of lane `lane` in step u, k-th of its 8
 __device__ __forceinline__ int64_t lg_tile_elem(int64_t base, int u, int k)
@@ -387,65 +421,105 @@ __device__ __forceinline__ int64_t lg_tile_elem(int64_t base, int u, int k)
     return base + ((int64_t) u * kBlock + threadIdx.x) * 8 + k;
 }
 
+// Tiles per launch: tile b is processed by workgroup b % gridDim.x (grid = the tile count unless
+// a tuning cap is set); its partial triple goes to sums[3 * b], so the fold sees the same partials
+// in the same order whatever the grid.
+template <int STEPS>
 __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ g, float* __restrict__ gx,
                                                                int64_t n, const float* __restrict__ delta,
-                                                               const float* __restrict__ offset, float steps,
-                                                               float* __restrict__ sums, int vec)
+                                                               const float* __restrict__ offset, float steps, int asym,
+                                                               float* __restrict__ sums, int vec, int64_t ntiles)
 {
+    constexpr int64_t kTile = (int64_t) kBlock * 8 * STEPS;
     const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
-    const int64_t base = (int64_t) blockIdx.x * kLgTile;
-    Sums s {0, 0, 0};
-    if (vec && base + kLgTile <= n)
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
     {
-        f4 a[kLgTileSteps][2], b[kLgTileSteps][2];
-#pragma unroll
-        for (int u = 0; u < kLgTileSteps; ++u)
+        const int64_t base = tile * kTile;
+        Sums s {0, 0, 0};
+        if (vec && base + kTile <= n)
         {
-            const int64_t q = lg_tile_elem(base, u, 0) / 4;
-            a[u][0] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q);
-            a[u][1] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q + 1);
-            b[u][0] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + q);
-            b[u][1] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + q + 1);
-        }
+            f4 a[STEPS][2], b[STEPS][2];
 #pragma unroll
-        for (int u = 0; u < kLgTileSteps; ++u)
-        {
-            float r[8];
-            const float xv[8] = {a[u][0].x, a[u][0].y, a[u][0].z, a[u][0].w, a[u][1].x, a[u][1].y, a[u][1].z, a[u][1].w};
-            const float gv[8] = {b[u][0].x, b[u][0].y, b[u][0].z, b[u][0].w, b[u][1].x, b[u][1].y, b[u][1].z, b[u][1].w};
-            lg_bwd_elems<8>(xv, gv, dl, o, steps, rcp, r, s);
-            if (gx)
+            for (int u = 0; u < STEPS; ++u)
             {
                 const int64_t q = lg_tile_elem(base, u, 0) / 4;
-                const f4 r0 = {r[0], r[1], r[2], r[3]}, r1 = {r[4], r[5], r[6], r[7]};
-                __builtin_nontemporal_store(r0, reinterpret_cast<f4*>(gx) + q);
-                __builtin_nontemporal_store(r1, reinterpret_cast<f4*>(gx) + q + 1);
+                a[u][0] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q);
+                a[u][1] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q + 1);
+                b[u][0] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + q);
+                b[u][1] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + q + 1);
+            }
+#pragma unroll
+            for (int u = 0; u < STEPS; ++u)
+            {
+                float r[8];
+                const float xv[8] = {a[u][0].x, a[u][0].y, a[u][0].z, a[u][0].w,
+                                     a[u][1].x, a[u][1].y, a[u][1].z, a[u][1].w};
+                const float gv[8] = {b[u][0].x, b[u][0].y, b[u][0].z, b[u][0].w,
+                                     b[u][1].x, b[u][1].y, b[u][1].z, b[u][1].w};
+                lg_bwd_elems<8>(xv, gv, dl, o, steps, rcp, r, s, asym);
+                if (gx)
+                {
+                    const int64_t q = lg_tile_elem(base, u, 0) / 4;
+                    const f4 r0 = {r[0], r[1], r[2], r[3]}, r1 = {r[4], r[5], r[6], r[7]};
+                    __builtin_nontemporal_store(r0, reinterpret_cast<f4*>(gx) + q);
+                    __builtin_nontemporal_store(r1, reinterpret_cast<f4*>(gx) + q + 1);
+                }
             }
         }
+        else
+        {
+            // the last (partial) tile, or unaligned pointers: element by element, the same order
+            for (int u = 0; u < STEPS; ++u)
+                for (int k = 0; k < 8; ++k)
+                {
+                    const int64_t e = lg_tile_elem(base, u, k);
+                    if (e >= n)
+                        break;
+                    float r;
+                    lg_bwd_elem(x[e], g[e], dl, o, steps, rcp, r, s, asym);
+                    if (gx)
+                        gx[e] = r;
+                }
+        }
+        Sums t = block_reduce(s);
+        if (threadIdx.x == 0)
+        {
+            sums[3 * tile + 0] = t.a;
+            sums[3 * tile + 1] = t.b;
+            sums[3 * tile + 2] = t.d;
+        }
     }
-    else
-    {
-        // the last (partial) tile, or unaligned pointers: element by element, the same order
-        for (int u = 0; u < kLgTileSteps; ++u)
-            for (int k = 0; k < 8; ++k)
-            {
-                const int64_t e = lg_tile_elem(base, u, k);
-                if (e >= n)
-                    break;
-                float r;
-                lg_bwd_elem(x[e], g[e], dl, o, steps, rcp, r, s);
-                if (gx)
-                    gx[e] = r;
-            }
-    }
-    Sums t = block_reduce(s);
-    if (threadIdx.x == 0)
-    {
-        sums[3 * blockIdx.x + 0] = t.a;
-        sums[3 * blockIdx.x + 1] = t.b;
-        sums[3 * blockIdx.x + 2] = t.d;
-    }
+}
+
+// Launch shape of the per-tensor backward kernels (fp32 and 16-bit use the same, so their sums
+// stay identical): STEPS 8-element groups per lane and tile, grid = the tile count, or at most
+// `cap` workgroups looping over the tiles. AIMET_TUNE_LG_BWD="steps:cap" (tuning experiments).
+struct LgBwdLaunch
+{
+    int steps;
+    int64_t ntiles;
+    unsigned grid;
+};
+
+LgBwdLaunch lg_bwd_launch(int64_t n)
+{
+    static const std::pair<int, int64_t> shape = [] {
+        const char* e = getenv("AIMET_TUNE_LG_BWD");
+        int st = kLgTileSteps;
+        long long cap = 0;
+        if (e)
+            sscanf(e, "%d:%lld", &st, &cap);
+        if (st != 1 && st != 2 && st != 4)
+            st = kLgTileSteps;
+        return std::make_pair(st, (int64_t) (cap > 0 ? cap : 0));
+    }();
+    LgBwdLaunch L;
+    L.steps  = shape.first;
+    L.ntiles = ceil_div(n, (int64_t) kBlock * 8 * L.steps);
+    AIMET_REQUIRE(L.ntiles < (int64_t(1) << 31), "too many elements");
+    L.grid = (unsigned) (shape.second > 0 && L.ntiles > shape.second ? shape.second : L.ntiles);
+    return L;
 }
 
 // the encoding gradients of channel c from its sums {A, B, D} (asymmetric / symmetric_gradients,
@@ -508,7 +582,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
                                                                 const float* __restrict__ g, float* __restrict__ gx,
                                                                 int64_t outer, int64_t C, int64_t K,
                                                                 const float* __restrict__ delta,
-                                                                const float* __restrict__ offset, float steps,
+                                                                const float* __restrict__ offset, float steps, int asym,
                                                                 float* __restrict__ sums)
 {
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
@@ -521,7 +595,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
             for (int64_t k = threadIdx.x; k < K; k += kBlock)
             {
                 float v;
-                lg_bwd_elem(x[base + k], g[base + k], dl, o, steps, rcp, v, s);
+                lg_bwd_elem(x[base + k], g[base + k], dl, o, steps, rcp, v, s, asym);
                 if (gx)
                     gx[base + k] = v;
             }
@@ -543,7 +617,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
                                                                     f4* __restrict__ gx, int64_t outer, int64_t C,
                                                                     int64_t K4, FastDiv divK4,
                                                                     const float* __restrict__ delta,
-                                                                    const float* __restrict__ offset, float steps,
+                                                                    const float* __restrict__ offset, float steps, int asym,
                                                                     float* __restrict__ sums)
 {
     const int splits = gridDim.y;
@@ -575,7 +649,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
                     break;
                 float rr[4];
                 const float xv[4] = {a[u].x, a[u].y, a[u].z, a[u].w}, gv[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
-                lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s);
+                lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s, asym);
                 if (gx)
                 {
                     f4 rv = {rr[0], rr[1], rr[2], rr[3]};
@@ -612,7 +686,7 @@ template <int U, int GIO>
 __global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restrict__ x, const void* __restrict__ g,
                                                              f4* __restrict__ gx, FastDiv divK4, FastDiv divC,
                                                              uint32_t C, const float* __restrict__ delta,
-                                                             const float* __restrict__ offset, float steps,
+                                                             const float* __restrict__ offset, float steps, int asym,
                                                              float* __restrict__ partial)
 {
     const uint32_t q0  = blockIdx.x * (uint32_t) (kBlock * U);
@@ -632,7 +706,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restric
     {
         float rr[4];
         const float xv[4] = {a[u].x, a[u].y, a[u].z, a[u].w}, gv[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
-        lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s);
+        lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s, asym);
         if (gx)
         {
             f4 rv = {rr[0], rr[1], rr[2], rr[3]};
@@ -687,112 +761,129 @@ typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 constexpr int kLgFwd16Vecs     = 2;
 constexpr int64_t kLgFwd16Tile = (int64_t) kBlock * 8 * kLgFwd16Vecs;
 
-template <int IO, int kLgFwd16Vecs = kLgFwd16Vecs>
-__global__ __launch_bounds__(kBlock) void lg_fwd16_kernel(const unsigned short* __restrict__ x,
-                                                          unsigned short* __restrict__ y, int64_t n,
-                                                          const float* __restrict__ delta,
-                                                          const float* __restrict__ offset, float steps, int vec,
-                                                          LgEnc enc)
+template <int IO, int V, int BLOCK>
+__global__ __launch_bounds__(BLOCK) void lg_fwd16_kernel(const unsigned short* __restrict__ x,
+                                                         unsigned short* __restrict__ y, int64_t n,
+                                                         const float* __restrict__ delta,
+                                                         const float* __restrict__ offset, float steps, int vec,
+                                                         LgEnc enc, int64_t ntiles)
 {
-    constexpr int64_t kLgFwd16Tile = (int64_t) kBlock * 8 * kLgFwd16Vecs;
-    const int64_t base = (int64_t) blockIdx.x * kLgFwd16Tile;
-    if (vec && base + kLgFwd16Tile <= n)
+    constexpr int64_t kTile = (int64_t) BLOCK * 8 * V;
+    float d = 0.0f, o = 0.0f;
+    bool have = false;
+    float rd  = 0.0f;
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
     {
-        u16x8 v[kLgFwd16Vecs];
-#pragma unroll
-        for (int u = 0; u < kLgFwd16Vecs; ++u)
-            v[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + base / 8 + u * kBlock +
-                                              threadIdx.x);
-        float d, o;
-        enc.get(0, base + threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);   // element 0's thread stores them
-        const float rd = lg_recip(d);
-#pragma unroll
-        for (int u = 0; u < kLgFwd16Vecs; ++u)
+        const int64_t base = tile * kTile;
+        if (vec && base + kTile <= n)
         {
-            float xin[8], yo[8];
+            u16x8 v[V];
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                xin[k] = to_f32<IO>(v[u][k]);
-            lg_qdq_n<8>(xin, d, o, steps, rd, yo);
-            u16x8 r;
+            for (int u = 0; u < V; ++u)
+                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + base / 8 + u * BLOCK +
+                                                  threadIdx.x);
+            if (!have)
+            {
+                // element 0's thread stores the encoding
+                enc.get(0, base + threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);
+                rd   = lg_recip(d);
+                have = true;
+            }
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                r[k] = from_f32<IO>(yo[k]);
-            __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(y) + base / 8 + u * kBlock + threadIdx.x);
+            for (int u = 0; u < V; ++u)
+            {
+                float xin[8], yo[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    xin[k] = to_f32<IO>(v[u][k]);
+                lg_qdq_n<8>(xin, d, o, steps, rd, yo);
+                u16x8 r;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    r[k] = from_f32<IO>(yo[k]);
+                __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(y) + base / 8 + u * BLOCK + threadIdx.x);
+            }
+            continue;
         }
-        return;
+        if (!have)
+        {
+            enc.get(0, base + threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);
+            rd   = lg_recip(d);
+            have = true;
+        }
+        for (int64_t e = base + threadIdx.x; e < base + kTile && e < n; e += BLOCK)
+            y[e] = from_f32<IO>(lg_qdq(to_f32<IO>(x[e]), d, o, steps, rd));
     }
-    float d, o;
-    enc.get(0, base + threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);
-    const float rd = lg_recip(d);
-    for (int64_t e = base + threadIdx.x; e < base + kLgFwd16Tile && e < n; e += kBlock)
-        y[e] = from_f32<IO>(lg_qdq(to_f32<IO>(x[e]), d, o, steps, rd));
 }
 
 // the element -> lane -> workgroup order of lg_bwd_tensor_kernel (tiles of kLgTile, 8 elements per
 // lane and step), so the sums equal the float32 kernel's on the upcast tensors
-template <int IO>
+template <int IO, int STEPS>
 __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned short* __restrict__ x,
                                                                  const unsigned short* __restrict__ g,
                                                                  unsigned short* __restrict__ gx, int64_t n,
                                                                  const float* __restrict__ delta,
-                                                                 const float* __restrict__ offset, float steps,
-                                                                 float* __restrict__ partial, int vec)
+                                                                 const float* __restrict__ offset, float steps, int asym,
+                                                                 float* __restrict__ partial, int vec, int64_t ntiles)
 {
+    constexpr int64_t kTile = (int64_t) kBlock * 8 * STEPS;
     const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
-    const int64_t base = (int64_t) blockIdx.x * kLgTile;
-    Sums s {0, 0, 0};
-    if (vec && base + kLgTile <= n)
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
     {
-        u16x8 a[kLgTileSteps], b[kLgTileSteps];
-#pragma unroll
-        for (int u = 0; u < kLgTileSteps; ++u)
+        const int64_t base = tile * kTile;
+        Sums s {0, 0, 0};
+        if (vec && base + kTile <= n)
         {
-            const int64_t q = lg_tile_elem(base, u, 0) / 8;
-            a[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + q);
-            b[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(g) + q);
-        }
+            u16x8 a[STEPS], b[STEPS];
 #pragma unroll
-        for (int u = 0; u < kLgTileSteps; ++u)
-        {
-            float r[8], xv[8], gv[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
+            for (int u = 0; u < STEPS; ++u)
             {
-                xv[k] = to_f32<IO>(a[u][k]);
-                gv[k] = to_f32<IO>(b[u][k]);
+                const int64_t q = lg_tile_elem(base, u, 0) / 8;
+                a[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + q);
+                b[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(g) + q);
             }
-            lg_bwd_elems<8>(xv, gv, dl, o, steps, rcp, r, s);
-            if (gx)
+#pragma unroll
+            for (int u = 0; u < STEPS; ++u)
             {
-                u16x8 h;
+                float r[8], xv[8], gv[8];
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
-                    h[k] = from_f32<IO>(r[k]);
-                __builtin_nontemporal_store(h, reinterpret_cast<u16x8*>(gx) + lg_tile_elem(base, u, 0) / 8);
+                {
+                    xv[k] = to_f32<IO>(a[u][k]);
+                    gv[k] = to_f32<IO>(b[u][k]);
+                }
+                lg_bwd_elems<8>(xv, gv, dl, o, steps, rcp, r, s, asym);
+                if (gx)
+                {
+                    u16x8 h;
+#pragma unroll
+                    for (int k = 0; k < 8; ++k)
+                        h[k] = from_f32<IO>(r[k]);
+                    __builtin_nontemporal_store(h, reinterpret_cast<u16x8*>(gx) + lg_tile_elem(base, u, 0) / 8);
+                }
             }
         }
-    }
-    else
-    {
-        for (int u = 0; u < kLgTileSteps; ++u)
-            for (int k = 0; k < 8; ++k)
-            {
-                const int64_t e = lg_tile_elem(base, u, k);
-                if (e >= n)
-                    break;
-                float r;
-                lg_bwd_elem(to_f32<IO>(x[e]), to_f32<IO>(g[e]), dl, o, steps, rcp, r, s);
-                if (gx)
-                    gx[e] = from_f32<IO>(r);
-            }
-    }
-    Sums t = block_reduce(s);
-    if (threadIdx.x == 0)
-    {
-        partial[3 * blockIdx.x + 0] = t.a;
-        partial[3 * blockIdx.x + 1] = t.b;
-        partial[3 * blockIdx.x + 2] = t.d;
+        else
+        {
+            for (int u = 0; u < STEPS; ++u)
+                for (int k = 0; k < 8; ++k)
+                {
+                    const int64_t e = lg_tile_elem(base, u, k);
+                    if (e >= n)
+                        break;
+                    float r;
+                    lg_bwd_elem(to_f32<IO>(x[e]), to_f32<IO>(g[e]), dl, o, steps, rcp, r, s, asym);
+                    if (gx)
+                        gx[e] = from_f32<IO>(r);
+                }
+        }
+        Sums t = block_reduce(s);
+        if (threadIdx.x == 0)
+        {
+            partial[3 * tile + 0] = t.a;
+            partial[3 * tile + 1] = t.b;
+            partial[3 * tile + 2] = t.d;
+        }
     }
 }
 
@@ -910,17 +1001,17 @@ void launch_range_grads(const float* sums, int64_t C, const LgRange& r, hipStrea
 
 template <int GIO>
 void launch_bwd_tile(int U, int64_t wg, const f4* x, const void* g, f4* gx, FastDiv dk, FastDiv dc, int64_t C,
-                     const float* delta, const float* offset, float steps, float* partial, hipStream_t s)
+                     const float* delta, const float* offset, float steps, int asym, float* partial, hipStream_t s)
 {
     if (U == 4)
         lg_bwd_tile_kernel<4, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
-                                                                    steps, partial);
+                                                                    steps, asym, partial);
     else if (U == 2)
         lg_bwd_tile_kernel<2, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
-                                                                    steps, partial);
+                                                                    steps, asym, partial);
     else
         lg_bwd_tile_kernel<1, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
-                                                                    steps, partial);
+                                                                    steps, asym, partial);
     AIMET_LAUNCH_CHECK();
 }
 
@@ -1106,6 +1197,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
         require_device_ptr(sums, "sums");
         hipStream_t s = as_stream(stream);
         const LgRange range = range_of(range_spec, num_steps);
+        const int asym      = range.gmin != nullptr && !range.sym;   // lg_bwd_term's B
         if (n == 0)
         {
             AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3 * C, s));
@@ -1122,13 +1214,20 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
         {
             bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                          reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
-            AIMET_REQUIRE(ceil_div(n, kLgTile) < (int64_t(1) << 31), "too many elements");
-            const unsigned nb = (unsigned) ceil_div(n, kLgTile);
-            float* partial    = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * nb, s));
-            lg_bwd_tensor_kernel<<<nb, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset, num_steps, partial,
-                                                       vec ? 1 : 0);
+            const LgBwdLaunch L = lg_bwd_launch(n);
+            float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
+            const int v         = vec ? 1 : 0;
+            if (L.steps == 1)
+                lg_bwd_tensor_kernel<1><<<L.grid, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset, num_steps,
+                                                                  asym, partial, v, L.ntiles);
+            else if (L.steps == 4)
+                lg_bwd_tensor_kernel<4><<<L.grid, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset, num_steps,
+                                                                  asym, partial, v, L.ntiles);
+            else
+                lg_bwd_tensor_kernel<kLgTileSteps><<<L.grid, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset,
+                                                                             num_steps, asym, partial, v, L.ntiles);
             AIMET_LAUNCH_CHECK();
-            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) nb, sums, range);
+            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
             AIMET_LAUNCH_CHECK();
             scratch_free(partial, s);
             return;
@@ -1146,7 +1245,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             auto gv = reinterpret_cast<const f4*>(grad);
             auto ov = reinterpret_cast<f4*>(grad_x);
             FastDiv dk((uint32_t) K4), dc((uint32_t) C);
-            launch_bwd_tile<IO_F32>(U, wg, xv, gv, ov, dk, dc, C, delta, offset, num_steps, partial, s);
+            launch_bwd_tile<IO_F32>(U, wg, xv, gv, ov, dk, dc, C, delta, offset, num_steps, asym, partial, s);
             lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
                 partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)), range);
             AIMET_LAUNCH_CHECK();
@@ -1168,7 +1267,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
                                         : sums;
             lg_bwd_channel_vec_kernel<<<grid, kBlock, 0, s>>>(
                 reinterpret_cast<const f4*>(x), reinterpret_cast<const f4*>(grad), reinterpret_cast<f4*>(grad_x),
-                outer, C, K4, FastDiv((uint32_t) (K4 > 0 ? K4 : 1)), delta, offset, num_steps, partial);
+                outer, C, K4, FastDiv((uint32_t) (K4 > 0 ? K4 : 1)), delta, offset, num_steps, asym, partial);
             if (splits > 1)
             {
                 AIMET_LAUNCH_CHECK();
@@ -1183,16 +1282,12 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
         {
             int grid = (int) (C < 65536 ? C : 65536);
             lg_bwd_channel_kernel<<<grid, kBlock, 0, s>>>(x, grad, grad_x, outer, C, K, delta, offset, num_steps,
-                                                          sums);
+                                                          asym, sums);
         }
         AIMET_LAUNCH_CHECK();
         launch_range_grads(sums, C, range, s);
     });
 }
-
-}   // extern "C"
-
-extern "C" {
 
 }   // extern "C"
 
@@ -1211,21 +1306,51 @@ void forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* de
     const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
     auto xs = static_cast<const unsigned short*>(x);
     auto ys = static_cast<unsigned short*>(y);
-    static const int vecs = [] {
-        const char* e = getenv("AIMET_TUNE_LG16_VECS");   // tuning experiments only
-        const int v   = e ? atoi(e) : kLgFwd16Vecs;
-        return (v == 1 || v == 2 || v == 8) ? v : kLgFwd16Vecs;
+    // launch shape: V 16-B vectors per lane, BLOCK lanes per workgroup, grid = the tile count or
+    // at most `cap` workgroups looping over the tiles; AIMET_TUNE_LG16_FWD="V:BLOCK:cap" (tuning)
+    struct Shape
+    {
+        int v, block;
+        int64_t cap;
+    };
+    static const Shape sh = [] {
+        Shape r {kLgFwd16Vecs, kBlock, 0};
+        const char* e = getenv("AIMET_TUNE_LG16_FWD");
+        long long cap = 0;
+        if (e)
+            sscanf(e, "%d:%d:%lld", &r.v, &r.block, &cap);
+        if (r.v != 1 && r.v != 2 && r.v != 4 && r.v != 8)
+            r.v = kLgFwd16Vecs;
+        if (r.block != 256 && r.block != 512 && r.block != 1024)
+            r.block = kBlock;
+        r.cap = cap > 0 ? cap : 0;
+        return r;
     }();
-    const unsigned nb = (unsigned) ceil_div(n, (int64_t) kBlock * 8 * vecs);
-#define AIMET_LG16_FWD(V)                                                                                           \
-    if (vecs == V)                                                                                                  \
+    const int64_t ntiles = ceil_div(n, (int64_t) sh.block * 8 * sh.v);
+    const unsigned grid  = (unsigned) (sh.cap > 0 && ntiles > sh.cap ? sh.cap : ntiles);
+    const int v          = vec ? 1 : 0;
+#define AIMET_LG16_FWD(V, B)                                                                                        \
+    if (sh.v == V && sh.block == B)                                                                                 \
     {                                                                                                               \
         if (io_dtype == IO_F16)                                                                                     \
-            lg_fwd16_kernel<IO_F16, V><<<nb, kBlock, 0, st>>>(xs, ys, n, delta, offset, num_steps, vec ? 1 : 0, enc); \
+            lg_fwd16_kernel<IO_F16, V, B><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc, ntiles);  \
         else                                                                                                        \
-            lg_fwd16_kernel<IO_BF16, V><<<nb, kBlock, 0, st>>>(xs, ys, n, delta, offset, num_steps, vec ? 1 : 0, enc);\
+            lg_fwd16_kernel<IO_BF16, V, B><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc, ntiles); \
     }
-    AIMET_LG16_FWD(1) AIMET_LG16_FWD(2) AIMET_LG16_FWD(4) AIMET_LG16_FWD(8)
+    AIMET_LG16_FWD(1, 256) AIMET_LG16_FWD(2, 256) AIMET_LG16_FWD(4, 256) AIMET_LG16_FWD(8, 256)
+    AIMET_LG16_FWD(1, 512) AIMET_LG16_FWD(2, 512) AIMET_LG16_FWD(4, 512)
+    AIMET_LG16_FWD(1, 1024) AIMET_LG16_FWD(2, 1024)
+    else if (true)
+    {
+        // a combination not instantiated: the default shape
+        const int64_t nt = ceil_div(n, kLgFwd16Tile);
+        if (io_dtype == IO_F16)
+            lg_fwd16_kernel<IO_F16, kLgFwd16Vecs, kBlock><<<(unsigned) nt, kBlock, 0, st>>>(xs, ys, n, delta, offset,
+                                                                                       num_steps, v, enc, nt);
+        else
+            lg_fwd16_kernel<IO_BF16, kLgFwd16Vecs, kBlock><<<(unsigned) nt, kBlock, 0, st>>>(xs, ys, n, delta, offset,
+                                                                                        num_steps, v, enc, nt);
+    }
 #undef AIMET_LG16_FWD
     AIMET_LAUNCH_CHECK();
 }
@@ -1346,6 +1471,7 @@ int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, fl
 {
     return guarded([&] {
         const LgRange range = range_of(range_spec, num_steps);
+        const int asym      = range.gmin != nullptr && !range.sym;   // lg_bwd_term's B
         AIMET_REQUIRE(grad_dtype == IO_F16 || grad_dtype == IO_BF16, "grad_dtype must be 1 (float16) or 2 (bfloat16)");
         AIMET_REQUIRE(outer >= 0 && C > 1 && K >= 0, "invalid shape (per-channel tensors only)");
         const int64_t n = outer * C * K;
@@ -1375,9 +1501,9 @@ int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, fl
         auto xv = reinterpret_cast<const f4*>(x);
         auto ov = reinterpret_cast<f4*>(grad_x);
         if (grad_dtype == IO_F16)
-            launch_bwd_tile<IO_F16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, partial, s);
+            launch_bwd_tile<IO_F16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, asym, partial, s);
         else
-            launch_bwd_tile<IO_BF16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, partial, s);
+            launch_bwd_tile<IO_BF16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, asym, partial, s);
         lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
             partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)), range);
         AIMET_LAUNCH_CHECK();
@@ -1400,6 +1526,7 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
 {
     return guarded([&] {
         const LgRange range = range_of(range_spec, num_steps);
+        const int asym      = range.gmin != nullptr && !range.sym;   // lg_bwd_term's B
         AIMET_REQUIRE(io_dtype == IO_F16 || io_dtype == IO_BF16, "io_dtype must be 1 (float16) or 2 (bfloat16)");
         AIMET_REQUIRE(n >= 0, "invalid size");
         require_device_ptr(sums, "sums");
@@ -1418,20 +1545,36 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         require_device_ptr(offset, "offset");
         const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                            reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
-        AIMET_REQUIRE(ceil_div(n, kLgTile) < (int64_t(1) << 31), "too many elements");
-        const unsigned nb = (unsigned) ceil_div(n, kLgTile);   // the fp32 kernel's grid
-        float* partial    = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * nb, s));
+        const LgBwdLaunch L = lg_bwd_launch(n);   // the fp32 kernel's tiles
+        float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
         auto xs = static_cast<const unsigned short*>(x);
         auto gs = static_cast<const unsigned short*>(grad);
         auto os = static_cast<unsigned short*>(grad_x);
+        const int v = vec ? 1 : 0;
+#define AIMET_LG_BWD16(IO, ST)                                                                                    \
+    lg_bwd16_tensor_kernel<IO, ST><<<L.grid, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps, asym, partial, v, \
+                                                             L.ntiles)
         if (io_dtype == IO_F16)
-            lg_bwd16_tensor_kernel<IO_F16><<<nb, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps, partial,
-                                                                 vec ? 1 : 0);
+        {
+            if (L.steps == 1)
+                AIMET_LG_BWD16(IO_F16, 1);
+            else if (L.steps == 4)
+                AIMET_LG_BWD16(IO_F16, 4);
+            else
+                AIMET_LG_BWD16(IO_F16, kLgTileSteps);
+        }
         else
-            lg_bwd16_tensor_kernel<IO_BF16><<<nb, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps, partial,
-                                                                  vec ? 1 : 0);
+        {
+            if (L.steps == 1)
+                AIMET_LG_BWD16(IO_BF16, 1);
+            else if (L.steps == 4)
+                AIMET_LG_BWD16(IO_BF16, 4);
+            else
+                AIMET_LG_BWD16(IO_BF16, kLgTileSteps);
+        }
+#undef AIMET_LG_BWD16
         AIMET_LAUNCH_CHECK();
-        lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) nb, sums, range);
+        lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
         AIMET_LAUNCH_CHECK();
         scratch_free(partial, s);
     });

@@ -569,6 +569,49 @@ def test_learned_grid_quotients_at_half_integers(bw, sym):
         assert torch.equal(yh.view(torch.int16), want.view(torch.int16)), dt
 
 
+@pytest.mark.parametrize("sym", [False, True])
+def test_learned_grid_non_finite_inputs_follow_torch(sym):
+    """NaN / inf / overflowing inputs: the reference's torch ops pass a NaN through torch.clamp
+    (y = NaN), its mask * grad zeroes them, and its encoding-gradient sums turn NaN on a channel
+    holding a non-finite x (sym: mask * (x / delta) -- also where x / delta overflows; asym:
+    x * mask / delta -- only a non-finite x). y and grad_x bit for bit (NaN positions: the quieted
+    input), the encoding gradients NaN on exactly the reference's channels and close elsewhere;
+    per channel, per tensor, and the bf16 / fp16 per-tensor path (== the upcast chain)."""
+    from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
+    from oracle import torch_ref as T
+    g = torch.Generator(device=DEV).manual_seed(11 + sym)
+    C, K = 5, 4096
+    emax = torch.tensor([3.1, 0.37, 1e-3, 5e4, 2.0], device=DEV)
+    emin = -emax if sym else -emax * torch.tensor([0.3, 1.0, 0.01, 2.0, 0.5], device=DEV)
+    x = torch.randn(C, K, device=DEV, generator=g) * emax.view(C, 1)
+    x[0, 7] = float("nan")
+    x[0, 4000] = -float("nan")
+    x[1, 100] = float("inf")
+    x[2, 9] = 3e38                      # x / delta overflows on this channel (delta ~ 1e-5)
+    x[3, 17] = torch.tensor(0x7FC00123, dtype=torch.int32).view(torch.float32)   # a NaN payload
+    grad = torch.randn(C, K, device=DEV, generator=g)
+    for per_channel in (True, False):
+        mn, mx = (emin, emax) if per_channel else (emin[2:3], emax[2:3])
+        xt = x.clone().requires_grad_(True)
+        emn, emx = mn.clone().requires_grad_(True), mx.clone().requires_grad_(True)
+        y = LearnedGridQuantizeDequantize.apply(xt, emn, emx, 8, sym, False, False, 0)
+        # the reference on the host: x86 passes a NaN's payload through, as the kernels do
+        yr = T.lg_forward(x.cpu(), mn.cpu(), mx.cpu(), 8, sym)[0]
+        assert torch.equal(y.cpu().view(torch.int32), yr.view(torch.int32)), per_channel
+        y.backward(grad)
+        gx, gmin, gmax = T.lg_gradients(x.cpu(), grad.cpu(), mn.cpu(), mx.cpu(), 8, sym)
+        assert torch.equal(xt.grad.cpu().view(torch.int32), gx.view(torch.int32)), per_channel
+        for got, want in ((emn.grad.cpu(), gmin), (emx.grad.cpu(), gmax)):
+            assert torch.equal(torch.isnan(got), torch.isnan(want)), (per_channel, got, want)
+            fin = ~torch.isnan(want)
+            torch.testing.assert_close(got[fin], want[fin], rtol=2e-4, atol=1e-4)
+    for dt in (torch.bfloat16, torch.float16):
+        xh = x[:2].reshape(-1).to(dt)
+        yh = LearnedGridQuantizeDequantize.apply(xh, emin[:1], emax[:1], 8, sym, False, False, 0)
+        want = T.lg_forward(xh.float().cpu(), emin[:1].cpu(), emax[:1].cpu(), 8, sym)[0].to(dt)
+        assert torch.equal(yh.cpu().view(torch.int16), want.view(torch.int16)), dt
+
+
 @pytest.mark.parametrize("outer,C,K", [(3, 5, 2048), (2, 7, 3072), (4, 3, 100)])
 def test_learned_grid_backward_sums_channel_axis_inner(outer, C, K):
     """aimet_lg_backward on [outer][C][K] with outer > 1 (channel axis not first): grad_x exact and
