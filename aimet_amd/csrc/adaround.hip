@@ -158,9 +158,14 @@ __device__ __forceinline__ F2 df_mul_f2f(F2 x, float y)
     const float s = x.x * y;
     return f2(s, __builtin_fmaf(x.y, y, fmapn(x.x, y, s)));
 }
+// Sleef's vrec (1.0f / d.x, the IEEE division) as v_rcp_f32 + one Newton step: equal to the
+// division for every d.x in [1.5, 3] -- logkf's divisor 1 + m, m in [0.75, 1.5), lies in [1.75,
+// 2.5] -- exhaustively over those 8,388,609 bit patterns on the MI355X
+// (tools/studies/rcp_newton_check.hip; not for general d: it differs where 1/d is subnormal).
 __device__ __forceinline__ F2 df_div(F2 n, F2 d)
 {
-    const float t = 1.0f / d.x, s = n.x * t;
+    const float r0 = __builtin_amdgcn_rcpf(d.x);
+    const float t  = __builtin_fmaf(__builtin_fmaf(-d.x, r0, 1.0f), r0, r0), s = n.x * t;
     const float u = fmapn(t, n.x, s);
     const float v = fmanp(d.y, t, fmanp(d.x, t, 1.0f));
     return f2(s, __builtin_fmaf(s, v, __builtin_fmaf(n.y, t, u)));
@@ -215,8 +220,10 @@ __device__ __forceinline__ float sleef_expkf(F2 d)
 }
 
 // x^e for x in [0, 1] as torch's CPU pow: e == 2 / 3 -> x*x / x*x*x (ATen's optimized kernel);
-// Sleef_powf_u10 in the vectorized part, the correctly rounded value in the scalar tail (`tail`)
-__device__ __forceinline__ float pow01(float x, float e, bool tail)
+// Sleef_powf_u10 in the vectorized part, the correctly rounded value in the scalar tail (`tail`).
+// Sleef's powf is expkf(logkf(|x|) * e): `l` = sleef_logkf(x), shared by the two exponents of the
+// rounding loss and its gradient (one logkf per element instead of two; the same values).
+__device__ __forceinline__ float pow01_log(float x, float e, bool tail, F2 l)
 {
     if (e == 2.0f)
         return x * x;
@@ -228,7 +235,7 @@ __device__ __forceinline__ float pow01(float x, float e, bool tail)
         return 1.0f;
     if (tail)
         return (float) exp((double) e * log((double) x));
-    const float r = sleef_expkf(df_mul_f2f(sleef_logkf(x), e));
+    const float r = sleef_expkf(df_mul_f2f(l, e));
     return r != r ? __builtin_inff() : r;
 }
 
@@ -289,9 +296,10 @@ __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, flo
         // as autograd does: round_loss = reg * sum(1 - |2h - 1|^beta)
         float x  = 2.0f * h + -1.0f;
         float ax = fabsf(x);
-        loss += 1.0f - pow01(ax, p.beta, tail);
+        const F2 l = sleef_logkf(ax == 0.0f || ax == 1.0f || tail ? 0.5f : ax);
+        loss += 1.0f - pow01_log(ax, p.beta, tail, l);
         // grad -reg at the pow; pow_backward: grad * (beta * x^(beta - 1)); abs: * sgn(x); 2*h: * 2
-        float dpw = (-p.reg) * (p.beta * pow01(ax, p.beta_m1, tail));
+        float dpw = (-p.reg) * (p.beta * pow01_log(ax, p.beta_m1, tail, l));
         float dh  = (dpw * (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f))) * 2.0f;
         ga += ((in_h ? dh : 0.0f) * kZmG * (1.0f - sg)) * sg;
     }

@@ -17,6 +17,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 #include <utility>
 #include "io16.hpp"
 
@@ -41,72 +42,25 @@ struct LgChannel
     }
 };
 
-// The quotient RN(x / d) without the IEEE division's ~10 instructions. y = lg_recip(d) = RN(1/d)
-// is computed once per encoding; then q0 = RN(x * y) is a faithful quotient, r = x - d * q0 is
-// exact (fma), and RN(q0 + r * y) is the correctly rounded quotient (Markstein's theorem) while
-// nothing under- or overflows: |d| in [2^-40, 2^40] (else y = NaN) and |q| in [2^-60, 2^60), so
-// |x| and r stay far from the subnormal range. A zero x takes q0 (= +-0 with the quotient's sign);
-// every other element -- and every non-finite one -- takes the IEEE division. Bit-identical to
-// x / d: tools/studies/markstein_div_check.c (754 M operand pairs, quotients at half-integers +-3
-// ulp and all-ones mantissas included; the same bounds fail only for |x| < 2^-100). 3 VALU plus a
-// range test per element instead of ~10 (the 16-bit kernels were VALU co-bound).
+// The quotient x / d without the IEEE division's ~10 instructions. y = lg_recip(d) = RN(1/d) is
+// computed once per encoding; then q0 = RN(x * y) is a faithful quotient, r = x - d * q0 is exact
+// (fma), and RN(q0 + r * y) is the correctly rounded quotient (Markstein's theorem) while nothing
+// under- or overflows: |d| in [2^-40, 2^40] (else y = NaN and the kernels divide) and |q| in
+// [2^-60, 2^60), so |x| and r stay far from the subnormal range. Bit-identical to x / d there:
+// tools/studies/markstein_div_check.c (754 M operand pairs, quotients at half-integers +-3 ulp and
+// all-ones mantissas included; the same bounds fail only for |x| < 2^-100). Outside that range the
+// consumers below need less than the exact quotient (lg_rint_quot, lg_quot), so no element takes
+// a slow path: 3 VALU plus one compare per element (the 16-bit kernels are VALU co-bound).
 __device__ __forceinline__ float lg_recip(float d)
 {
     const float a = __builtin_fabsf(d);
     return (a >= 0x1p-40f && a <= 0x1p40f) ? 1.0f / d : __builtin_nanf("");
 }
-__device__ __forceinline__ float div_rn(float x, float d, float y)
-{
-    const float q0 = x * y;
-    const float r  = __builtin_fmaf(-q0, d, x);
-    const float q  = __builtin_fmaf(r, y, q0);
-    if ((__float_as_uint(q) & 0x7fffffffu) - 0x21800000u < 0x5d800000u - 0x21800000u)   // |q| in [2^-60, 2^60)
-        return q;
-    if (x == 0.0f && y == y)
-        return q0;
-    return x / d;
-}
 
-// div_rn over N independent elements with ONE branch to the division for the rare elements it does
-// not cover: the N quotient chains interleave (a branch per element serialised them)
-template <int N>
-__device__ __forceinline__ void div_rn_n(const float* x, float d, float y, float* q)
+// torch's NaN: the op chain passes a NaN input through (quieted)
+__device__ __forceinline__ float quiet_nan(float x)
 {
-    uint32_t slow = 0;
-#pragma unroll
-    for (int k = 0; k < N; ++k)
-    {
-        const float q0  = x[k] * y;
-        const float r   = __builtin_fmaf(-q0, d, x[k]);
-        const float qm  = __builtin_fmaf(r, y, q0);
-        const bool zero = x[k] == 0.0f;
-        const bool ok   = ((__float_as_uint(qm) & 0x7fffffffu) - 0x21800000u < 0x5d800000u - 0x21800000u) ||
-                        (zero && y == y);
-        q[k] = zero ? q0 : qm;
-        slow |= ok ? 0u : (1u << k);
-    }
-    if (slow)
-    {
-#pragma unroll
-        for (int k = 0; k < N; ++k)
-            if (slow & (1u << k))
-                q[k] = x[k] / d;
-    }
-}
-
-// rint(RN(x / d)) where only the rounded quotient is consumed, from y = lg_recip(d) (not NaN:
-// |d| in [2^-40, 2^40]) and no branch: while |q0| < 2^60 the Markstein quotient q is RN(x / d)
-// (div_rn) -- except for |x| < 2^-100, where q may be off but |q| < 2^-59, so rint(q) is a zero
-// as rint(RN(x / d)) is; for |q0| >= 2^60 (and +-inf) rint(q0) is beyond every clamp bound of the
-// forward ( |offset| + steps < 2^33 ) on the same side as rint(RN(x / d)); a NaN x gives NaN. The
-// sign of a zero rint may differ from the division's, which the forward cannot observe: with
-// offset = +0, round - offset = +-0 is clamped and then + offset = +0 again, and with any other
-// offset round - offset does not depend on the zero's sign.
-__device__ __forceinline__ float lg_rint_quot(float x, float d, float y)
-{
-    const float q0 = x * y;
-    const float q  = __builtin_fmaf(__builtin_fmaf(-q0, d, x), y, q0);
-    return __builtin_rintf(__builtin_fabsf(q0) < 0x1p60f ? q : q0);
+    return __uint_as_float(__float_as_uint(x) | 0x00400000u);
 }
 
 // torch's clamp(v, lo, hi) = minimum(maximum(v, lo), hi): a NaN passes through (gfx950's
@@ -129,13 +83,26 @@ __device__ __forceinline__ bool lg_fast_enc(float o, float rd)
     return rd == rd && __builtin_fabsf(o) <= 0x1p32f;
 }
 
+// The forward's element for an encoding lg_fast_enc accepts, never NaN: x is first clamped to
+// +-2^59 |d| (med3), inside which |x * y| < 2^60 and the Markstein quotient needs no range test;
+// a clamped x gives rint(q) ~ +-2^59, beyond every clamp bound on the same side as the division's
+// (+-inf included). A NaN x is the caller's to map (torch's clamp passes it through).
+__device__ __forceinline__ float lg_qdq_fast(float x, float d, float o, float steps, float rd, float xmax)
+{
+    const float xc = __builtin_amdgcn_fmed3f(x, -xmax, xmax);
+    const float q0 = xc * rd;
+    const float q  = __builtin_fmaf(__builtin_fmaf(-q0, d, xc), rd, q0);
+    return (__builtin_amdgcn_fmed3f(__builtin_rintf(q) - o, 0.0f, steps) + o) * d;
+}
+
 // x_round = round(x / delta) - offset ; x_quant = clamp(x_round, 0, steps) ; y = (x_quant + offset) * delta
 // (rd = lg_recip(d)); a NaN x gives NaN as torch's clamp does
 __device__ __forceinline__ float lg_qdq(float x, float d, float o, float steps, float rd)
 {
     if (!lg_fast_enc(o, rd))
         return lg_qdq_div(x, d, o, steps);
-    return (t_clamp(lg_rint_quot(x, d, rd) - o, 0.0f, steps) + o) * d;
+    const float y = lg_qdq_fast(x, d, o, steps, rd, 0x1p59f * __builtin_fabsf(d));
+    return x != x ? quiet_nan(x) : y;
 }
 template <int N>
 __device__ __forceinline__ void lg_qdq_n(const float* x, float d, float o, float steps, float rd, float* y)
@@ -147,9 +114,13 @@ __device__ __forceinline__ void lg_qdq_n(const float* x, float d, float o, float
             y[k] = lg_qdq_div(x[k], d, o, steps);
         return;
     }
+    const float xmax = 0x1p59f * __builtin_fabsf(d);
 #pragma unroll
     for (int k = 0; k < N; ++k)
-        y[k] = (t_clamp(lg_rint_quot(x[k], d, rd) - o, 0.0f, steps) + o) * d;
+    {
+        const float v = lg_qdq_fast(x[k], d, o, steps, rd, xmax);
+        y[k]          = x[k] != x[k] ? quiet_nan(x[k]) : v;
+    }
 }
 
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
@@ -339,40 +310,101 @@ struct Sums
 
 // One element of the backward (calculate_forward_pass + the gradient expressions of
 // QuantizeDequantizeFunc.backward / asymmetric_gradients / symmetric_gradients), with
-// q = RN(x / dl) itself (div_rn, rcp = lg_recip(dl)), the reference's x / delta bit for bit:
-//   grad_x += mask * grad ;  A += (x_quant + offset) * grad ;  D += grad where !mask ;
-//   B += mask * (x / delta) * grad   (asym: (x * mask / delta) * grad: where !mask the term is
-//        0 * x / delta -- NaN for a non-finite x -- rather than 0 * (x / delta), NaN also when
-//        the quotient overflows).
-// x_quant is torch's clamp, which passes a NaN round through (A turns NaN as the reference's sum).
-__device__ __forceinline__ void lg_bwd_term(float x, float q, float g, float o, float steps, bool asym, float& gx,
+// q = RN(x / dl) (lg_quot, rcp = lg_recip(dl)), the reference's x / delta:
+//   m = mask (0 / 1) ; grad_x = m * grad ;
+//   MODE 1 (symmetric_gradients): A += (x_quant + offset) * grad ; B += (m * (x / delta)) * grad
+//     (the reference's two sums, :311-314);
+//   MODE 2 (asymmetric_gradients): A += (x_quant + offset - (x * m) / delta) * grad, the
+//     reference's one grad_scale sum (:283-286, B stays 0), and D += grad where !m (grad_offset
+//     without its delta factor, applied to the sum);
+//   MODE 0 (no range gradients requested): A, B as MODE 1 and D as MODE 2.
+// Where !m, (x * m) / delta is 0 * x (NaN for a non-finite x) and m * (x / delta) is 0 * (x /
+// delta) (NaN also when the quotient overflows), as the reference evaluates them. mask is
+// x_quant == x_round with x_quant = med3(x_round, 0, steps) (one compare instead of two; false
+// for a NaN round); a NaN x makes the sums NaN through those 0 * NaN terms, as the reference's,
+// so x_quant need not pass the NaN through. Every kernel forms the same values.
+template <int MODE>
+__device__ __forceinline__ void lg_bwd_term_m(float x, float q, float g, float o, float steps, float& gx, Sums& s)
+{
+    const float xr = __builtin_rintf(q) - o;
+    const float xq = __builtin_amdgcn_fmed3f(xr, 0.0f, steps);
+    const bool in  = xq == xr;
+    const float m  = in ? 1.0f : 0.0f;
+    gx = m * g;
+    if constexpr (MODE == 2)
+    {
+        s.a += ((xq + o) - m * (in ? q : x)) * g;
+        s.d += in ? 0.0f : g;
+    }
+    else
+    {
+        s.a += (xq + o) * g;
+        s.b += (m * q) * g;
+        if constexpr (MODE == 0)
+            s.d += in ? 0.0f : g;
+    }
+}
+__device__ __forceinline__ void lg_bwd_term(float x, float q, float g, float o, float steps, int mode, float& gx,
                                             Sums& s)
 {
-    const float xr  = __builtin_rintf(q) - o;
-    const bool mask = (xr >= 0.0f) && (xr <= steps);
-    const float xq  = t_clamp(xr, 0.0f, steps);
-    gx = mask ? g : 0.0f * g;      // mask_tensor * grad (keeps -0 / NaN behaviour of a multiply)
-    s.a += (xq + o) * g;
-    s.b += (mask ? q : 0.0f * (asym ? x : q)) * g;
-    s.d += mask ? 0.0f : g;
+    if (mode == 2)
+        lg_bwd_term_m<2>(x, q, g, o, steps, gx, s);
+    else if (mode == 1)
+        lg_bwd_term_m<1>(x, q, g, o, steps, gx, s);
+    else
+        lg_bwd_term_m<0>(x, q, g, o, steps, gx, s);
+}
+
+// RN(x / d) for the backward from y = lg_recip(d) (not NaN), no branch: the Markstein quotient
+// while |q0| < 2^60 -- RN(x / d) itself except for |x| < 2^-100, where it is off by a few ulps of
+// a quotient below 2^-59 -- else q0 = RN(x * y) (infinite exactly when x is, or when x / d is
+// within an ulp of overflowing). rint(q) and the mask are therefore the division's (grad_x is
+// bit-exact); B's terms can differ only in those two corners, at the encoding gradients' tolerance.
+__device__ __forceinline__ float lg_quot(float x, float d, float y)
+{
+    const float q0 = x * y;
+    const float q  = __builtin_fmaf(__builtin_fmaf(-q0, d, x), y, q0);
+    return __builtin_fabsf(q0) < 0x1p60f ? q : q0;
 }
 
 __device__ __forceinline__ void lg_bwd_elem(float x, float g, float dl, float o, float steps, float rcp, float& gx,
-                                            Sums& s, bool asym)
+                                            Sums& s, int mode)
 {
-    lg_bwd_term(x, div_rn(x, dl, rcp), g, o, steps, asym, gx, s);
+    lg_bwd_term(x, lg_fast_enc(o, rcp) ? lg_quot(x, dl, rcp) : x / dl, g, o, steps, mode, gx, s);
 }
 
-// lg_bwd_elem over N elements in order (the same sums), the quotients by div_rn_n
+// lg_bwd_elem over N elements in order (the same sums)
 template <int N>
 __device__ __forceinline__ void lg_bwd_elems(const float* x, const float* g, float dl, float o, float steps,
-                                             float rcp, float* gx, Sums& s, bool asym)
+                                             float rcp, float* gx, Sums& s, int mode)
 {
     float q[N];
-    div_rn_n<N>(x, dl, rcp, q);
+    if (lg_fast_enc(o, rcp))
+    {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            q[k] = lg_quot(x[k], dl, rcp);
+    }
+    else
+    {
+#pragma unroll
+        for (int k = 0; k < N; ++k)
+            q[k] = x[k] / dl;
+    }
 #pragma unroll
     for (int k = 0; k < N; ++k)
-        lg_bwd_term(x[k], q[k], g[k], o, steps, asym, gx[k], s);
+        lg_bwd_term(x[k], q[k], g[k], o, steps, mode, gx[k], s);
+}
+
+// lg_bwd_elems for an encoding lg_fast_enc accepts: no division code in the caller's vector path
+// (its registers are then the streaming loads' and the sums', not the division's temporaries)
+template <int N, int MODE>
+__device__ __forceinline__ void lg_bwd_elems_fast(const float* x, const float* g, float dl, float o, float steps,
+                                                  float rcp, float* gx, Sums& s)
+{
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+        lg_bwd_term_m<MODE>(x[k], lg_quot(x[k], dl, rcp), g[k], o, steps, gx[k], s);
 }
 
 __device__ __forceinline__ Sums block_reduce(Sums s)
@@ -424,20 +456,21 @@ __device__ __forceinline__ int64_t lg_tile_elem(int64_t base, int u, int k)
 // Tiles per launch: tile b is processed by workgroup b % gridDim.x (grid = the tile count unless
 // a tuning cap is set); its partial triple goes to sums[3 * b], so the fold sees the same partials
 // in the same order whatever the grid.
-template <int STEPS>
+template <int STEPS, int MODE>
 __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __restrict__ x,
                                                                const float* __restrict__ g, float* __restrict__ gx,
                                                                int64_t n, const float* __restrict__ delta,
-                                                               const float* __restrict__ offset, float steps, int asym,
+                                                               const float* __restrict__ offset, float steps,
                                                                float* __restrict__ sums, int vec, int64_t ntiles)
 {
     constexpr int64_t kTile = (int64_t) kBlock * 8 * STEPS;
     const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
+    const bool fast = lg_fast_enc(o, rcp);   // else every tile takes the element path (the division)
     for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
     {
         const int64_t base = tile * kTile;
         Sums s {0, 0, 0};
-        if (vec && base + kTile <= n)
+        if (fast && vec && base + kTile <= n)
         {
             f4 a[STEPS][2], b[STEPS][2];
 #pragma unroll
@@ -457,7 +490,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
                                      a[u][1].x, a[u][1].y, a[u][1].z, a[u][1].w};
                 const float gv[8] = {b[u][0].x, b[u][0].y, b[u][0].z, b[u][0].w,
                                      b[u][1].x, b[u][1].y, b[u][1].z, b[u][1].w};
-                lg_bwd_elems<8>(xv, gv, dl, o, steps, rcp, r, s, asym);
+                lg_bwd_elems_fast<8, MODE>(xv, gv, dl, o, steps, rcp, r, s);
                 if (gx)
                 {
                     const int64_t q = lg_tile_elem(base, u, 0) / 4;
@@ -469,7 +502,8 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
         }
         else
         {
-            // the last (partial) tile, or unaligned pointers: element by element, the same order
+            // the last (partial) tile, unaligned pointers or an encoding for the division: element
+            // by element, the same order
             for (int u = 0; u < STEPS; ++u)
                 for (int k = 0; k < 8; ++k)
                 {
@@ -477,7 +511,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
                     if (e >= n)
                         break;
                     float r;
-                    lg_bwd_elem(x[e], g[e], dl, o, steps, rcp, r, s, asym);
+                    lg_bwd_elem(x[e], g[e], dl, o, steps, rcp, r, s, MODE);
                     if (gx)
                         gx[e] = r;
                 }
@@ -499,8 +533,9 @@ struct LgBwdLaunch
 {
     int steps;
     int64_t ntiles;
-    unsigned grid;
+    unsigned grid, grid16;
 };
+constexpr int64_t kLgBwd16Grid = 2048;
 
 LgBwdLaunch lg_bwd_launch(int64_t n)
 {
@@ -519,7 +554,32 @@ LgBwdLaunch lg_bwd_launch(int64_t n)
     L.ntiles = ceil_div(n, (int64_t) kBlock * 8 * L.steps);
     AIMET_REQUIRE(L.ntiles < (int64_t(1) << 31), "too many elements");
     L.grid = (unsigned) (shape.second > 0 && L.ntiles > shape.second ? shape.second : L.ntiles);
+    // the pipelined 16-bit kernel: one resident round of workgroups unless a cap is given
+    const int64_t cap16 = shape.second > 0 ? shape.second : kLgBwd16Grid;
+    L.grid16 = (unsigned) (L.ntiles > cap16 ? cap16 : L.ntiles);
     return L;
+}
+
+// f(integral_constant<STEPS>, integral_constant<MODE>) for the runtime tile steps and backward
+// mode: the per-tensor kernels are compiled per mode (lg_bwd_term_m), so their element loops carry
+// only the sums that mode needs
+template <class F>
+void lg_bwd_dispatch(int steps, int mode, F&& f)
+{
+    auto with_mode = [&](auto st) {
+        if (mode == 2)
+            f(st, std::integral_constant<int, 2> {});
+        else if (mode == 1)
+            f(st, std::integral_constant<int, 1> {});
+        else
+            f(st, std::integral_constant<int, 0> {});
+    };
+    if (steps == 1)
+        with_mode(std::integral_constant<int, 1> {});
+    else if (steps == 4)
+        with_mode(std::integral_constant<int, 4> {});
+    else
+        with_mode(std::integral_constant<int, kLgTileSteps> {});
 }
 
 // the encoding gradients of channel c from its sums {A, B, D} (asymmetric / symmetric_gradients,
@@ -582,7 +642,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
                                                                 const float* __restrict__ g, float* __restrict__ gx,
                                                                 int64_t outer, int64_t C, int64_t K,
                                                                 const float* __restrict__ delta,
-                                                                const float* __restrict__ offset, float steps, int asym,
+                                                                const float* __restrict__ offset, float steps, int mode,
                                                                 float* __restrict__ sums)
 {
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
@@ -595,7 +655,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_kernel(const float* __r
             for (int64_t k = threadIdx.x; k < K; k += kBlock)
             {
                 float v;
-                lg_bwd_elem(x[base + k], g[base + k], dl, o, steps, rcp, v, s, asym);
+                lg_bwd_elem(x[base + k], g[base + k], dl, o, steps, rcp, v, s, mode);
                 if (gx)
                     gx[base + k] = v;
             }
@@ -617,7 +677,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
                                                                     f4* __restrict__ gx, int64_t outer, int64_t C,
                                                                     int64_t K4, FastDiv divK4,
                                                                     const float* __restrict__ delta,
-                                                                    const float* __restrict__ offset, float steps, int asym,
+                                                                    const float* __restrict__ offset, float steps, int mode,
                                                                     float* __restrict__ sums)
 {
     const int splits = gridDim.y;
@@ -649,7 +709,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_channel_vec_kernel(const f4* __
                     break;
                 float rr[4];
                 const float xv[4] = {a[u].x, a[u].y, a[u].z, a[u].w}, gv[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
-                lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s, asym);
+                lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s, mode);
                 if (gx)
                 {
                     f4 rv = {rr[0], rr[1], rr[2], rr[3]};
@@ -686,7 +746,7 @@ template <int U, int GIO>
 __global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restrict__ x, const void* __restrict__ g,
                                                              f4* __restrict__ gx, FastDiv divK4, FastDiv divC,
                                                              uint32_t C, const float* __restrict__ delta,
-                                                             const float* __restrict__ offset, float steps, int asym,
+                                                             const float* __restrict__ offset, float steps, int mode,
                                                              float* __restrict__ partial)
 {
     const uint32_t q0  = blockIdx.x * (uint32_t) (kBlock * U);
@@ -706,7 +766,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_kernel(const f4* __restric
     {
         float rr[4];
         const float xv[4] = {a[u].x, a[u].y, a[u].z, a[u].w}, gv[4] = {b[u].x, b[u].y, b[u].z, b[u].w};
-        lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s, asym);
+        lg_bwd_elems<4>(xv, gv, dl, o, steps, rcp, rr, s, mode);
         if (gx)
         {
             f4 rv = {rr[0], rr[1], rr[2], rr[3]};
@@ -753,15 +813,55 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restri
 
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
-// kLgFwd16Vecs 16-B vectors (8 elements each) per lane, all loaded before the encoding is formed
-// and the first element computed; workgroup b owns elements [b * kLgFwd16Tile, ...). vec == 0
-// (unaligned pointers): one element per lane and step over the same tile.
-// 2 vectors per lane: 11.3 us per 13.69 M-element bf16 call (4: 11.7-12.5, 1: 12.4; a plain copy
-// of the same bytes 9.9-10.2; profiles/r03/lg16_*.txt)
-constexpr int kLgFwd16Vecs     = 2;
+// lg_fwd16_kernel's default shape: kLgFwd16Vecs 16-B vectors (8 elements) per lane and tile,
+// kLgFwd16Grid workgroups looping over the tiles (AIMET_TUNE_LG16_FWD for experiments)
+constexpr int kLgFwd16Vecs     = 1;
+constexpr int64_t kLgFwd16Grid  = 2048;   // workgroups: 8 per CU, one resident round
 constexpr int64_t kLgFwd16Tile = (int64_t) kBlock * 8 * kLgFwd16Vecs;
 
-template <int IO, int V, int BLOCK>
+// 16-B loads / stores of the 16-bit kernels: nontemporal (NT, the streaming default) or through
+// the caches (AIMET_TUNE_LG16_NT=0, for activations still resident in the MALL)
+template <bool NT>
+__device__ __forceinline__ u16x8 ld16(const u16x8* p)
+{
+    if constexpr (NT)
+        return __builtin_nontemporal_load(p);
+    else
+        return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st16(u16x8 v, u16x8* p)
+{
+    if constexpr (NT)
+        __builtin_nontemporal_store(v, p);
+    else
+        *p = v;
+}
+
+int lg16_nt()
+{
+    static const int v = [] {
+        const char* e = getenv("AIMET_TUNE_LG16_NT");
+        return e ? (atoi(e) != 0) : 1;
+    }();
+    return v;
+}
+
+template <int IO, int V, int BLOCK, bool NT>
+__device__ __forceinline__ void lg_fwd16_load(const unsigned short* __restrict__ x, int64_t tile, u16x8* v)
+{
+    constexpr int64_t kTile = (int64_t) BLOCK * 8 * V;
+#pragma unroll
+    for (int u = 0; u < V; ++u)
+        v[u] = ld16<NT>(reinterpret_cast<const u16x8*>(x) + tile * kTile / 8 + u * BLOCK + threadIdx.x);
+}
+
+// Workgroup b takes tiles b, b + grid, ... (grid capped near one resident wave of workgroups per
+// SIMD slot): the next tile's loads are issued before the current tile is computed, so each wave
+// keeps its 16-B loads in flight through its own arithmetic (a wave that loaded, waited and then
+// computed left the memory pipe idle during the ~20 VALU per element). Full tiles only; the
+// partial last tile, unaligned pointers and encodings for the division take the element loop.
+template <int IO, int V, int BLOCK, bool NT = true>
 __global__ __launch_bounds__(BLOCK) void lg_fwd16_kernel(const unsigned short* __restrict__ x,
                                                          unsigned short* __restrict__ y, int64_t n,
                                                          const float* __restrict__ delta,
@@ -769,79 +869,95 @@ __global__ __launch_bounds__(BLOCK) void lg_fwd16_kernel(const unsigned short* _
                                                          LgEnc enc, int64_t ntiles)
 {
     constexpr int64_t kTile = (int64_t) BLOCK * 8 * V;
-    float d = 0.0f, o = 0.0f;
-    bool have = false;
-    float rd  = 0.0f;
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
+    float d, o;
+    // element 0's thread (tile 0 is workgroup 0's first) stores the encoding
+    enc.get(0, blockIdx.x == 0 && threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);
+    const float rd   = lg_recip(d);
+    const float xmax = 0x1p59f * __builtin_fabsf(d);
+    const bool fast  = lg_fast_enc(o, rd);
+    const int64_t nfull = (vec && fast) ? n / kTile : 0;
+    int64_t tile = blockIdx.x;
+    if (tile < nfull)
     {
-        const int64_t base = tile * kTile;
-        if (vec && base + kTile <= n)
+        u16x8 cur[V];
+        lg_fwd16_load<IO, V, BLOCK, NT>(x, tile, cur);
+        for (; tile < nfull; tile += gridDim.x)
         {
-            u16x8 v[V];
-#pragma unroll
-            for (int u = 0; u < V; ++u)
-                v[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + base / 8 + u * BLOCK +
-                                                  threadIdx.x);
-            if (!have)
-            {
-                // element 0's thread stores the encoding
-                enc.get(0, base + threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);
-                rd   = lg_recip(d);
-                have = true;
-            }
+            u16x8 nxt[V];
+            const int64_t tn = tile + gridDim.x;
+            if (tn < nfull)
+                lg_fwd16_load<IO, V, BLOCK, NT>(x, tn, nxt);
 #pragma unroll
             for (int u = 0; u < V; ++u)
             {
-                float xin[8], yo[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                    xin[k] = to_f32<IO>(v[u][k]);
-                lg_qdq_n<8>(xin, d, o, steps, rd, yo);
                 u16x8 r;
 #pragma unroll
                 for (int k = 0; k < 8; ++k)
-                    r[k] = from_f32<IO>(yo[k]);
-                __builtin_nontemporal_store(r, reinterpret_cast<u16x8*>(y) + base / 8 + u * BLOCK + threadIdx.x);
+                {
+                    // never NaN for a fast encoding; a NaN input -> the 16-bit NaN torch's cast
+                    // of the passed-through NaN gives (one select, no NaN test of the result)
+                    const float xf = to_f32<IO>(cur[u][k]);
+                    const float yq = lg_qdq_fast(xf, d, o, steps, rd, xmax);
+                    r[k] = xf != xf ? from_f32<IO>(quiet_nan(xf)) : from_f32<IO, false>(yq);
+                }
+                st16<NT>(r, reinterpret_cast<u16x8*>(y) + tile * kTile / 8 + u * BLOCK + threadIdx.x);
             }
-            continue;
+#pragma unroll
+            for (int u = 0; u < V; ++u)
+                cur[u] = nxt[u];
         }
-        if (!have)
-        {
-            enc.get(0, base + threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);
-            rd   = lg_recip(d);
-            have = true;
-        }
-        for (int64_t e = base + threadIdx.x; e < base + kTile && e < n; e += BLOCK)
-            y[e] = from_f32<IO>(lg_qdq(to_f32<IO>(x[e]), d, o, steps, rd));
     }
+    // the rest element by element: tiles from nfull on (all of them when not vec / not fast)
+    for (; tile < ntiles; tile += gridDim.x)
+        for (int64_t e = tile * kTile + threadIdx.x; e < (tile + 1) * kTile && e < n; e += BLOCK)
+            y[e] = from_f32<IO>(lg_qdq(to_f32<IO>(x[e]), d, o, steps, rd));
 }
 
 // the element -> lane -> workgroup order of lg_bwd_tensor_kernel (tiles of kLgTile, 8 elements per
 // lane and step), so the sums equal the float32 kernel's on the upcast tensors
-template <int IO, int STEPS>
+template <int STEPS, bool NT>
+__device__ __forceinline__ void lg_bwd16_load(const unsigned short* __restrict__ x, const unsigned short* __restrict__ g,
+                                              int64_t base, u16x8* a, u16x8* b)
+{
+#pragma unroll
+    for (int u = 0; u < STEPS; ++u)
+    {
+        const int64_t q = lg_tile_elem(base, u, 0) / 8;
+        a[u] = ld16<NT>(reinterpret_cast<const u16x8*>(x) + q);
+        b[u] = ld16<NT>(reinterpret_cast<const u16x8*>(g) + q);
+    }
+}
+
+// Tiles b, b + grid, ... per workgroup with the next tile's loads issued before the current tile is
+// computed and reduced (see lg_fwd16_kernel); each tile's partial triple still goes to
+// partial[3 * tile], so the sums are those of any other grid.
+template <int IO, int STEPS, int MODE, bool NT = true>
 __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned short* __restrict__ x,
                                                                  const unsigned short* __restrict__ g,
                                                                  unsigned short* __restrict__ gx, int64_t n,
                                                                  const float* __restrict__ delta,
-                                                                 const float* __restrict__ offset, float steps, int asym,
+                                                                 const float* __restrict__ offset, float steps,
                                                                  float* __restrict__ partial, int vec, int64_t ntiles)
 {
     constexpr int64_t kTile = (int64_t) kBlock * 8 * STEPS;
     const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
-    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x)
+    // full tiles of an encoding lg_fast_enc accepts take the vector path; the rest (the partial
+    // last tile, unaligned pointers, an encoding for the division) the element path
+    const int64_t nfull = (lg_fast_enc(o, rcp) && vec) ? n / kTile : 0;
+    int64_t tile = blockIdx.x;
+    u16x8 a[STEPS], b[STEPS];
+    if (tile < nfull)
+        lg_bwd16_load<STEPS, NT>(x, g, tile * kTile, a, b);
+    for (; tile < ntiles; tile += gridDim.x)
     {
         const int64_t base = tile * kTile;
         Sums s {0, 0, 0};
-        if (vec && base + kTile <= n)
+        if (tile < nfull)
         {
-            u16x8 a[STEPS], b[STEPS];
-#pragma unroll
-            for (int u = 0; u < STEPS; ++u)
-            {
-                const int64_t q = lg_tile_elem(base, u, 0) / 8;
-                a[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(x) + q);
-                b[u] = __builtin_nontemporal_load(reinterpret_cast<const u16x8*>(g) + q);
-            }
+            u16x8 an[STEPS], bn[STEPS];
+            const int64_t tn = tile + gridDim.x;
+            if (tn < nfull)
+                lg_bwd16_load<STEPS, NT>(x, g, tn * kTile, an, bn);
 #pragma unroll
             for (int u = 0; u < STEPS; ++u)
             {
@@ -852,15 +968,21 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
                     xv[k] = to_f32<IO>(a[u][k]);
                     gv[k] = to_f32<IO>(b[u][k]);
                 }
-                lg_bwd_elems<8>(xv, gv, dl, o, steps, rcp, r, s, asym);
+                lg_bwd_elems_fast<8, MODE>(xv, gv, dl, o, steps, rcp, r, s);
                 if (gx)
                 {
                     u16x8 h;
 #pragma unroll
                     for (int k = 0; k < 8; ++k)
                         h[k] = from_f32<IO>(r[k]);
-                    __builtin_nontemporal_store(h, reinterpret_cast<u16x8*>(gx) + lg_tile_elem(base, u, 0) / 8);
+                    st16<NT>(h, reinterpret_cast<u16x8*>(gx) + lg_tile_elem(base, u, 0) / 8);
                 }
+            }
+#pragma unroll
+            for (int u = 0; u < STEPS; ++u)
+            {
+                a[u] = an[u];
+                b[u] = bn[u];
             }
         }
         else
@@ -872,7 +994,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
                     if (e >= n)
                         break;
                     float r;
-                    lg_bwd_elem(to_f32<IO>(x[e]), to_f32<IO>(g[e]), dl, o, steps, rcp, r, s, asym);
+                    lg_bwd_elem(to_f32<IO>(x[e]), to_f32<IO>(g[e]), dl, o, steps, rcp, r, s, MODE);
                     if (gx)
                         gx[e] = from_f32<IO>(r);
                 }
@@ -1001,17 +1123,17 @@ void launch_range_grads(const float* sums, int64_t C, const LgRange& r, hipStrea
 
 template <int GIO>
 void launch_bwd_tile(int U, int64_t wg, const f4* x, const void* g, f4* gx, FastDiv dk, FastDiv dc, int64_t C,
-                     const float* delta, const float* offset, float steps, int asym, float* partial, hipStream_t s)
+                     const float* delta, const float* offset, float steps, int mode, float* partial, hipStream_t s)
 {
     if (U == 4)
         lg_bwd_tile_kernel<4, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
-                                                                    steps, asym, partial);
+                                                                    steps, mode, partial);
     else if (U == 2)
         lg_bwd_tile_kernel<2, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
-                                                                    steps, asym, partial);
+                                                                    steps, mode, partial);
     else
         lg_bwd_tile_kernel<1, GIO><<<(unsigned) wg, kBlock, 0, s>>>(x, g, gx, dk, dc, (uint32_t) C, delta, offset,
-                                                                    steps, asym, partial);
+                                                                    steps, mode, partial);
     AIMET_LAUNCH_CHECK();
 }
 
@@ -1197,7 +1319,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
         require_device_ptr(sums, "sums");
         hipStream_t s = as_stream(stream);
         const LgRange range = range_of(range_spec, num_steps);
-        const int asym      = range.gmin != nullptr && !range.sym;   // lg_bwd_term's B
+        const int mode      = range.gmin == nullptr ? 0 : range.sym ? 1 : 2;   // lg_bwd_term_m
         if (n == 0)
         {
             AIMET_HIP_CHECK(hipMemsetAsync(sums, 0, sizeof(float) * 3 * C, s));
@@ -1217,15 +1339,10 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             const LgBwdLaunch L = lg_bwd_launch(n);
             float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
             const int v         = vec ? 1 : 0;
-            if (L.steps == 1)
-                lg_bwd_tensor_kernel<1><<<L.grid, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset, num_steps,
-                                                                  asym, partial, v, L.ntiles);
-            else if (L.steps == 4)
-                lg_bwd_tensor_kernel<4><<<L.grid, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset, num_steps,
-                                                                  asym, partial, v, L.ntiles);
-            else
-                lg_bwd_tensor_kernel<kLgTileSteps><<<L.grid, kBlock, 0, s>>>(x, grad, grad_x, n, delta, offset,
-                                                                             num_steps, asym, partial, v, L.ntiles);
+            lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
+                lg_bwd_tensor_kernel<decltype(st)::value, decltype(md)::value><<<L.grid, kBlock, 0, s>>>(
+                    x, grad, grad_x, n, delta, offset, num_steps, partial, v, L.ntiles);
+            });
             AIMET_LAUNCH_CHECK();
             lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
             AIMET_LAUNCH_CHECK();
@@ -1245,7 +1362,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             auto gv = reinterpret_cast<const f4*>(grad);
             auto ov = reinterpret_cast<f4*>(grad_x);
             FastDiv dk((uint32_t) K4), dc((uint32_t) C);
-            launch_bwd_tile<IO_F32>(U, wg, xv, gv, ov, dk, dc, C, delta, offset, num_steps, asym, partial, s);
+            launch_bwd_tile<IO_F32>(U, wg, xv, gv, ov, dk, dc, C, delta, offset, num_steps, mode, partial, s);
             lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
                 partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)), range);
             AIMET_LAUNCH_CHECK();
@@ -1267,7 +1384,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
                                         : sums;
             lg_bwd_channel_vec_kernel<<<grid, kBlock, 0, s>>>(
                 reinterpret_cast<const f4*>(x), reinterpret_cast<const f4*>(grad), reinterpret_cast<f4*>(grad_x),
-                outer, C, K4, FastDiv((uint32_t) (K4 > 0 ? K4 : 1)), delta, offset, num_steps, asym, partial);
+                outer, C, K4, FastDiv((uint32_t) (K4 > 0 ? K4 : 1)), delta, offset, num_steps, mode, partial);
             if (splits > 1)
             {
                 AIMET_LAUNCH_CHECK();
@@ -1282,7 +1399,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
         {
             int grid = (int) (C < 65536 ? C : 65536);
             lg_bwd_channel_kernel<<<grid, kBlock, 0, s>>>(x, grad, grad_x, outer, C, K, delta, offset, num_steps,
-                                                          asym, sums);
+                                                          mode, sums);
         }
         AIMET_LAUNCH_CHECK();
         launch_range_grads(sums, C, range, s);
@@ -1314,7 +1431,7 @@ void forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* de
         int64_t cap;
     };
     static const Shape sh = [] {
-        Shape r {kLgFwd16Vecs, kBlock, 0};
+        Shape r {kLgFwd16Vecs, kBlock, kLgFwd16Grid};
         const char* e = getenv("AIMET_TUNE_LG16_FWD");
         long long cap = 0;
         if (e)
@@ -1323,7 +1440,8 @@ void forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* de
             r.v = kLgFwd16Vecs;
         if (r.block != 256 && r.block != 512 && r.block != 1024)
             r.block = kBlock;
-        r.cap = cap > 0 ? cap : 0;
+        if (e)
+            r.cap = cap > 0 ? cap : 0;
         return r;
     }();
     const int64_t ntiles = ceil_div(n, (int64_t) sh.block * 8 * sh.v);
@@ -1332,10 +1450,16 @@ void forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* de
 #define AIMET_LG16_FWD(V, B)                                                                                        \
     if (sh.v == V && sh.block == B)                                                                                 \
     {                                                                                                               \
-        if (io_dtype == IO_F16)                                                                                     \
+        if (io_dtype == IO_F16 && lg16_nt())                                                                        \
             lg_fwd16_kernel<IO_F16, V, B><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc, ntiles);  \
-        else                                                                                                        \
+        else if (io_dtype == IO_F16)                                                                                \
+            lg_fwd16_kernel<IO_F16, V, B, false><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc,    \
+                                                                    ntiles);                                       \
+        else if (lg16_nt())                                                                                         \
             lg_fwd16_kernel<IO_BF16, V, B><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc, ntiles); \
+        else                                                                                                        \
+            lg_fwd16_kernel<IO_BF16, V, B, false><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc,   \
+                                                                     ntiles);                                      \
     }
     AIMET_LG16_FWD(1, 256) AIMET_LG16_FWD(2, 256) AIMET_LG16_FWD(4, 256) AIMET_LG16_FWD(8, 256)
     AIMET_LG16_FWD(1, 512) AIMET_LG16_FWD(2, 512) AIMET_LG16_FWD(4, 512)
@@ -1471,7 +1595,7 @@ int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, fl
 {
     return guarded([&] {
         const LgRange range = range_of(range_spec, num_steps);
-        const int asym      = range.gmin != nullptr && !range.sym;   // lg_bwd_term's B
+        const int mode      = range.gmin == nullptr ? 0 : range.sym ? 1 : 2;   // lg_bwd_term_m
         AIMET_REQUIRE(grad_dtype == IO_F16 || grad_dtype == IO_BF16, "grad_dtype must be 1 (float16) or 2 (bfloat16)");
         AIMET_REQUIRE(outer >= 0 && C > 1 && K >= 0, "invalid shape (per-channel tensors only)");
         const int64_t n = outer * C * K;
@@ -1501,9 +1625,9 @@ int aimet_lg_backward_grad16(const float* x, const void* grad, float* grad_x, fl
         auto xv = reinterpret_cast<const f4*>(x);
         auto ov = reinterpret_cast<f4*>(grad_x);
         if (grad_dtype == IO_F16)
-            launch_bwd_tile<IO_F16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, asym, partial, s);
+            launch_bwd_tile<IO_F16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, mode, partial, s);
         else
-            launch_bwd_tile<IO_BF16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, asym, partial, s);
+            launch_bwd_tile<IO_BF16>(U, wg, xv, grad, ov, dk, dc, C, delta, offset, num_steps, mode, partial, s);
         lg_bwd_tile_fold<<<(unsigned) ceil_div(C, kBlock), kBlock, 0, s>>>(
             partial, sums, (uint32_t) outer, (uint32_t) C, (uint32_t) (K4 / (kBlock * U)), range);
         AIMET_LAUNCH_CHECK();
@@ -1526,7 +1650,7 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
 {
     return guarded([&] {
         const LgRange range = range_of(range_spec, num_steps);
-        const int asym      = range.gmin != nullptr && !range.sym;   // lg_bwd_term's B
+        const int mode      = range.gmin == nullptr ? 0 : range.sym ? 1 : 2;   // lg_bwd_term_m
         AIMET_REQUIRE(io_dtype == IO_F16 || io_dtype == IO_BF16, "io_dtype must be 1 (float16) or 2 (bfloat16)");
         AIMET_REQUIRE(n >= 0, "invalid size");
         require_device_ptr(sums, "sums");
@@ -1551,28 +1675,21 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         auto gs = static_cast<const unsigned short*>(grad);
         auto os = static_cast<unsigned short*>(grad_x);
         const int v = vec ? 1 : 0;
-#define AIMET_LG_BWD16(IO, ST)                                                                                    \
-    lg_bwd16_tensor_kernel<IO, ST><<<L.grid, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps, asym, partial, v, \
-                                                             L.ntiles)
-        if (io_dtype == IO_F16)
-        {
-            if (L.steps == 1)
-                AIMET_LG_BWD16(IO_F16, 1);
-            else if (L.steps == 4)
-                AIMET_LG_BWD16(IO_F16, 4);
+        lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
+            constexpr int ST = decltype(st)::value, MD = decltype(md)::value;
+            if (io_dtype == IO_F16 && lg16_nt())
+                lg_bwd16_tensor_kernel<IO_F16, ST, MD><<<L.grid16, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps,
+                                                                                 partial, v, L.ntiles);
+            else if (io_dtype == IO_F16)
+                lg_bwd16_tensor_kernel<IO_F16, ST, MD, false><<<L.grid16, kBlock, 0, s>>>(
+                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles);
+            else if (lg16_nt())
+                lg_bwd16_tensor_kernel<IO_BF16, ST, MD><<<L.grid16, kBlock, 0, s>>>(xs, gs, os, n, delta, offset,
+                                                                                  num_steps, partial, v, L.ntiles);
             else
-                AIMET_LG_BWD16(IO_F16, kLgTileSteps);
-        }
-        else
-        {
-            if (L.steps == 1)
-                AIMET_LG_BWD16(IO_BF16, 1);
-            else if (L.steps == 4)
-                AIMET_LG_BWD16(IO_BF16, 4);
-            else
-                AIMET_LG_BWD16(IO_BF16, kLgTileSteps);
-        }
-#undef AIMET_LG_BWD16
+                lg_bwd16_tensor_kernel<IO_BF16, ST, MD, false><<<L.grid16, kBlock, 0, s>>>(
+                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles);
+        });
         AIMET_LAUNCH_CHECK();
         lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
         AIMET_LAUNCH_CHECK();

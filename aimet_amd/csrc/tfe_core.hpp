@@ -284,6 +284,50 @@ AIMET_HD inline double quant_sum(const Bins& B, int k0, int k1, float delta, int
 {
     double s = 0;
     int k    = k0;
+#if defined(__HIP_DEVICE_COMPILE__)
+    // Four bins at once with ONE exactness test for the four codes (a branch per bin serialised
+    // the wave). quantized + offset is formed in float, rint(x) + offset, where that sum is exact:
+    // thr = 2^-21 (vmax * rcp + |offset| + 1) < 4 bounds |rint(x) + offset| ~ |v * rcp| below
+    // 2^23 and both integer operands below 2^24, so it is the reference's int sum converted for
+    // the multiply, without the two conversions.
+    const float of   = (float) offset;
+    const bool fsum  = thr < 4.0f;   // false for a NaN thr
+    for (; k + 4 <= k1; k += 4)
+    {
+        float v[4], x[4], qf[4];
+        bool fast = fsum;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            v[u] = B.cf_c[k + u];
+            x[u] = v[u] * rcp - of;
+            fast &= __builtin_fabsf(__builtin_amdgcn_fractf(x[u]) - 0.5f) > thr;
+        }
+        if (fast)
+        {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                qf[u] = __builtin_rintf(x[u]) + of;
+        }
+        else
+        {
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                qf[u] = (float) (quant_code(v[u], delta, offset, rcp, thr) + offset);
+        }
+        double t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+        {
+            const double d = (double) (v[u] - delta * qf[u]);
+            t[u]           = B.pdf_c[k + u] * (d * d);
+        }
+        s += t[0];
+        s += t[1];
+        s += t[2];
+        s += t[3];
+    }
+#else
     for (; k + 4 <= k1; k += 4)
     {
         double t[4];
@@ -295,6 +339,7 @@ AIMET_HD inline double quant_sum(const Bins& B, int k0, int k1, float delta, int
         s += t[2];
         s += t[3];
     }
+#endif
     for (; k < k1; ++k)
         s += quant_term(B, k, delta, offset, rcp, thr);
     return s;
