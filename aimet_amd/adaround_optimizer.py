@@ -118,6 +118,29 @@ def _is_pointwise(module: torch.nn.Module) -> bool:
         and module.padding in ((0, 0), "valid") and module.dilation == (1, 1) and module.groups == 1
 
 
+# im2col form of small-Cin convolutions (the stem): C_in * k * k at most this, and the unfolded
+# input cache at most this many bytes
+_IM2COL_MAX_K = 64
+_IM2COL_MAX_BYTES = 8 << 30
+
+
+def _im2col_ok(module: torch.nn.Module, inp_data: torch.Tensor) -> bool:
+    """A groups-1 Conv2d (not 1x1 / stride 1, which _is_pointwise runs directly) whose
+    C_in * kh * kw <= _IM2COL_MAX_K and whose unfolded input cache fits _IM2COL_MAX_BYTES: its
+    loop runs as the pointwise form on the unfolded cache (deterministic GEMMs; MIOpen's
+    deterministic stem solutions were 4x slower than its default ones)."""
+    if not isinstance(module, torch.nn.Conv2d) or module.groups != 1 or _is_pointwise(module) \
+            or module.padding_mode != "zeros" or isinstance(module.padding, str) or inp_data.dim() != 4:
+        return False
+    kdim = module.in_channels * module.kernel_size[0] * module.kernel_size[1]
+    if kdim > _IM2COL_MAX_K:
+        return False
+    h, w = inp_data.shape[2], inp_data.shape[3]
+    oh = (h + 2 * module.padding[0] - module.dilation[0] * (module.kernel_size[0] - 1) - 1) // module.stride[0] + 1
+    ow = (w + 2 * module.padding[1] - module.dilation[1] * (module.kernel_size[1] - 1) - 1) // module.stride[1] + 1
+    return inp_data.shape[0] * kdim * oh * ow * inp_data.element_size() <= _IM2COL_MAX_BYTES
+
+
 def depthwise_spec(module: torch.nn.Module):
     """(K, stride, padding, dilation) when `module` is a depthwise Conv2d the native depthwise
     kernels (aimet_dwconv2d_*) run: groups == in == out channels, square K in {3, 5}, square
@@ -269,7 +292,7 @@ def _finish_alpha(alpha, alpha_init):
 class AdaroundOptimizer:
     """v1/adaround/adaround_optimizer.py."""
 
-    last_loop_form = None   # the layer form the last fused loop ran (dw / pointwise / linear / autograd)
+    last_loop_form = None   # the layer form the last fused loop ran (dw / pointwise / im2col / linear / autograd)
     is_activation_caching_enabled = True
 
     # ---- the reference's caller surface (v1/adaround/adaround_optimizer.py:69-260) -------------
@@ -498,6 +521,14 @@ class AdaroundOptimizer:
         chunk = 500
         draw(0, min(chunk, iters))
         rb_all = AdaroundOptimizer._reg_beta_all(opt_params, iters, dev)
+        im2col = (_GEMM_LAYERS and _LOOP_FORM != "autograd" and out_data.dim() == 4
+                  and out_data.dtype == torch.float32 and _act_code(act_func) is not None
+                  and _im2col_ok(module, inp_data))
+        if im2col:
+            # the cached inputs unfolded once ([N, C_in k k, OH OW]): each iteration's batch is then
+            # a pointwise GEMM problem, gathered by rows like any other cache
+            inp_data = torch.nn.functional.unfold(inp_data, module.kernel_size, module.dilation, module.padding,
+                                                  module.stride)
         inp_data = inp_data.contiguous()
         out_data = out_data.contiguous()
         inp = torch.empty((nb,) + tuple(inp_data.shape[1:]), dtype=inp_data.dtype, device=dev)
@@ -520,7 +551,9 @@ class AdaroundOptimizer:
         hw = row_out // C_out if indexed else 1
         bias = module.bias.detach().contiguous() if module.bias is not None else None
         mode = "autograd"
-        if indexed and depthwise_spec(module) is not None and inp.dim() == 4:
+        if im2col and indexed:
+            mode = "im2col"
+        elif indexed and depthwise_spec(module) is not None and inp.dim() == 4:
             mode = "dw"
         elif indexed and _GEMM_LAYERS and _is_pointwise(module) and inp.dim() == 4:
             mode = "pointwise"
@@ -570,11 +603,12 @@ class AdaroundOptimizer:
                 _native.check(lib.aimet_dwconv2d_grad_weight(P(inp), P(g_buf), P(gw_dw), P(ws), *dims, s))
                 adam_step(gw_dw, s)
                 return
-            if mode == "pointwise":
-                # 1x1 convolution as one batched GEMM per direction (hipBLASLt, no NCHW<->NHWC
-                # transposes): q[n] = Wq @ x[n]; the bias is added inside the reconstruction kernel
+            if mode in ("pointwise", "im2col"):
+                # 1x1 convolution (or the unfolded stem) as one batched GEMM per direction
+                # (hipBLASLt, no NCHW<->NHWC transposes): q[n] = Wq @ x[n]; the bias is added inside
+                # the reconstruction kernel
                 x3 = inp.view(nb, inp.shape[1], -1)
-                w2 = wq.detach().view(wq.shape[0], wq.shape[1])
+                w2 = wq.detach().view(wq.shape[0], -1)
                 torch.matmul(w2, x3, out=q_buf.view(nb, w2.shape[0], -1))
                 recon(q_buf, True, s)
                 gw = torch.matmul(g_buf.view(nb, w2.shape[0], -1), x3.transpose(1, 2)).sum(0)
