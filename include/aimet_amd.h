@@ -309,9 +309,13 @@ int aimet_tq_quant_scheme(aimet_tensor_quantizer* q, int* quant_scheme);
  * channel of [outer][C][K] (C == 1: per-tensor), float32 device vectors. */
 int aimet_lg_forward(const float* x, float* y, int64_t outer, int64_t C, int64_t K, const float* delta_dev,
                      const float* offset_dev, float num_steps, void* stream);
-/* grad_x = mask * grad (grad_x may be NULL) and per-channel sums_dev[C][3] =
- * { sum((x_quant+offset)*grad), sum(mask*(x/delta)*grad), sum(!mask*grad) } from which the
- * encoding-min/max gradients are assembled (asymmetric_gradients / symmetric_gradients). */
+/* grad_x = mask * grad (grad_x may be NULL) and per-channel sums_dev[C][3] = {A, B, D} from which
+ * the encoding-min/max gradients are assembled (asymmetric_gradients / symmetric_gradients, with
+ * (A - B) as grad_scale's sum): with no range spec, or a symmetric one,
+ * A = sum((x_quant+offset)*grad), B = sum((mask*(x/delta))*grad) (D = sum(!mask*grad) with no spec,
+ * 0 with a symmetric one); with an asymmetric spec A = sum((x_quant+offset - x*mask/delta)*grad),
+ * the reference's single grad_scale sum, B = 0 and D = sum(!mask*grad). NaN / inf inputs turn the
+ * sums NaN where the reference's do. */
 /* Optional epilogue of the learned-grid backward entry points: the encoding-min/max gradients
  * (aimet_lg_range_grads' arithmetic) written by the kernel that folds the sums, no extra launch.
  * null: the sums only. */
