@@ -180,7 +180,8 @@ __device__ __forceinline__ F2 sleef_logkf(float d)
     float m = __builtin_frexpf(d, &em) * 2.0f;          // getmant into [0.75, 1.5)
     if (m >= 1.5f)
         m *= 0.5f;
-    const F2 x  = df_div(df_add2_ff(-1.0f, m), df_add2_ff(1.0f, m));
+    // -1 + m is exact for m in [0.75, 1.5) (Sterbenz), so df_add2_ff(-1, m)'s error term is +0
+    const F2 x  = df_div(f2(-1.0f + m, 0.0f), df_add2_ff(1.0f, m));
     const F2 x2 = df_squ(x);
     float t     = 0.240320354700088500976562f;
     t           = __builtin_fmaf(t, x2.x, 0.285112679004669189453125f);
@@ -215,7 +216,9 @@ __device__ __forceinline__ float sleef_expkf(F2 d)
     u           = __builtin_fmaf(u, s.x, 0.499999850988388061523438f);
     F2 t        = df_add_f2f2(s, df_mul_f2f(df_squ(s), u));
     t           = df_add_ff2(1.0f, t);
-    u           = sleef_ldexp(t.x + t.y, q);
+    // t in [0.7, 1.42]: for q in [-125, 126] the result is normal, where every step of
+    // sleef_ldexp is an exact power-of-two scaling, i.e. the one-step ldexp
+    u           = (q >= -125 && q <= 126) ? __builtin_ldexpf(t.x + t.y, q) : sleef_ldexp(t.x + t.y, q);
     return d.x < -104.0f ? 0.0f : u;
 }
 
@@ -257,6 +260,7 @@ struct AdaParams
     float qmax, reg, beta, beta_m1;   // beta_m1 = (float)(beta - 1) in double, as torch's pow_backward
     int soft;
     uint32_t vec_end;   // n - n % 32: the reference's pow runs elements >= vec_end in its scalar tail
+    int want_loss;      // the rounding-loss value is requested (else only its gradient's pow runs)
 };
 
 __device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, const AdaParams& p, float rcp)
@@ -297,7 +301,8 @@ __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, flo
         float x  = 2.0f * h + -1.0f;
         float ax = fabsf(x);
         const F2 l = sleef_logkf(ax == 0.0f || ax == 1.0f || tail ? 0.5f : ax);
-        loss += 1.0f - pow01_log(ax, p.beta, tail, l);
+        if (p.want_loss)
+            loss += 1.0f - pow01_log(ax, p.beta, tail, l);
         // grad -reg at the pow; pow_backward: grad * (beta * x^(beta - 1)); abs: * sgn(x); 2*h: * 2
         float dpw = (-p.reg) * (p.beta * pow01_log(ax, p.beta_m1, tail, l));
         float dh  = (dpw * (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f))) * 2.0f;
@@ -697,7 +702,7 @@ int aimet_adaround_forward(const float* w, const float* alpha, float* wq, int64_
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, soft, (uint32_t) (n - n % 32)};
+        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, soft, (uint32_t) (n - n % 32), 0};
         if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(wq))
         {
             uint32_t nq = (uint32_t) (n / 4);
@@ -735,7 +740,7 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
         AdaParams p {(float) ((1ull << bw) - 1), (float) reg, (float) beta, (float) (beta - 1.0), 1,
-                     (uint32_t) (n - n % 32)};
+                     (uint32_t) (n - n % 32), round_loss != nullptr};
         if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(g) &&
             aligned16(ga))
         {
@@ -901,7 +906,7 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
         require_device_ptr(it_next, "it_next");
         require_device_ptr(it_cur, "it_cur");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
-        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, 1, (uint32_t) (n - n % 32)};
+        AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, 1, (uint32_t) (n - n % 32), round_loss != nullptr};
         AdamArgs a {lr, beta1, beta2, eps};
         const bool vec = (C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) &&
                          aligned16(grad_wq) && aligned16(exp_avg) && aligned16(exp_avg_sq) &&

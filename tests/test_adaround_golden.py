@@ -83,6 +83,11 @@ def test_adaround_backward_vs_reference(gad):
             (i, int((_ulps(got, c["ga_total"]) != 0).sum()), int(_ulps(got, c["ga_total"]).max()))
         want_loss = float(c["round_loss"])
         assert abs(loss.item() - want_loss) <= 1e-5 * abs(want_loss), (i, loss.item(), want_loss)
+        # the loss value not requested: the kernel skips pow(x, beta) (the loss term), the gradient's
+        # pow(x, beta - 1) is the same
+        a = alpha.clone().requires_grad_(True)
+        (AdaroundFunction.apply(w, a, d, o, c["bw"], 0, True, reg, float(c["beta"]), None) * g).sum().backward()
+        assert np.array_equal(a.grad.cpu().numpy().view(np.int32), c["ga_total"].view(np.int32)), i
 
 
 def test_adaround_alpha_init_vs_reference(gad):
