@@ -1460,11 +1460,12 @@ void forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* de
         else                                                                                                        \
             lg_fwd16_kernel<IO_BF16, V, B, false><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc,   \
                                                                      ntiles);                                      \
-    }
+    }                                                                                                               \
+    else
+    // one chain of else-ifs: exactly one launch per call
     AIMET_LG16_FWD(1, 256) AIMET_LG16_FWD(2, 256) AIMET_LG16_FWD(4, 256) AIMET_LG16_FWD(8, 256)
     AIMET_LG16_FWD(1, 512) AIMET_LG16_FWD(2, 512) AIMET_LG16_FWD(4, 512)
     AIMET_LG16_FWD(1, 1024) AIMET_LG16_FWD(2, 1024)
-    else if (true)
     {
         // a combination not instantiated: the default shape
         const int64_t nt = ceil_div(n, kLgFwd16Tile);
