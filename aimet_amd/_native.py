@@ -167,6 +167,10 @@ _PROTOTYPES = {
     "aimet_adaround_recon_grad": [_vp, _vp, _vp, _i64, _i64, _int, _vp],
     "aimet_dwconv2d_forward": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32, _vp],
     "aimet_dwconv2d_grad_weight_workspace": [_i64, _i64, _i64, _i64, _i32, _vp],
+    "aimet_adaround_dw_step": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
+                               _i32, _i32, _i32, _i32, _i32, _vp],
+    "aimet_adaround_pw_step_workspace": [_i64, _i64, _i64, _i64, _vp],
+    "aimet_adaround_pw_step": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp],
     "aimet_dwconv2d_grad_weight": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                                    _vp],
     "aimet_adaround_gather": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],

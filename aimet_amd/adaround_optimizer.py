@@ -116,6 +116,18 @@ _PW_GRAD = os.environ.get("AIMET_ADA_PW_GRAD", "auto")
 # the Adam step writes the next soft-quantized weight (AIMET_ADA_FUSE_WQ=0: a forward launch per
 # iteration instead; measurements only)
 _FUSE_SOFT_WEIGHT = os.environ.get("AIMET_ADA_FUSE_WQ", "1") == "1"
+# depthwise layers: the whole iteration up to dL/dWq as one pass over the cached rows
+# (aimet_adaround_dw_step, bit-identical to gather + forward + reconstruction gradient + weight
+# gradient); AIMET_ADA_DW_FUSED=0 runs those four launches instead (tests, measurements)
+_DW_FUSED = os.environ.get("AIMET_ADA_DW_FUSED", "1") == "1"
+# 1x1 layers / the unfolded stem with few channels (Cin, Cout <= 192, Cin * Cout <= 6144, HW % 4 == 0)
+# can run the iteration up to dL/dWq as one pass too (aimet_adaround_pw_step: q, g and the gradient
+# partials on chip; sums in a fixed order, not a library GEMM's). "auto" (default) takes it for the
+# expanding layers at >= 56 x 56 positions (C_out >= 4 C_in), where it measured faster than the GEMM
+# form (MobileNet-v2: 0.24 -> 0.19 and 0.127 -> 0.104 ms per iteration); the projecting layers and
+# the stem stay GEMMs (the one-pass kernel is slower there: profiles/r03/adaround_pw_fused_forms.txt).
+# "all": every eligible layer, "0": none. A fixed rule by shape, so results stay deterministic.
+_PW_FUSED = os.environ.get("AIMET_ADA_PW_FUSED", "auto")
 
 
 def _is_pointwise(module: torch.nn.Module) -> bool:
@@ -577,6 +589,17 @@ class AdaroundOptimizer:
             ws = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
             dims = (Nb, C, H, W, out_shape[1], out_shape[2], K, stride, pad, dil)
         pbias = P(bias) if bias is not None else None
+        pw_dims = None
+        if mode in ("pointwise", "im2col") and _PW_FUSED != "0" and _LOOP_FORM != "autograd":
+            cin, cout, hw_in = inp_data.shape[1], C_out, inp_data[0, 0].numel()
+            wanted = _PW_FUSED == "all" or (cout >= 4 * cin and hw >= 56 * 56)
+            if (wanted and cin <= 192 and cout <= 192 and cin * cout <= 6144 and hw_in == hw and hw % 4 == 0
+                    and inp_data.data_ptr() % 16 == 0 and out_data.data_ptr() % 16 == 0 and wq.is_contiguous()):
+                pw_dims = (nb, cin, cout, hw)
+                gw_pw = torch.empty_like(sq.w)
+                ws_n = ctypes.c_int64()
+                _native.check(lib.aimet_adaround_pw_step_workspace(*pw_dims, ctypes.byref(ws_n)))
+                ws_pw = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
 
         def recon(q, with_bias, s):
             _native.check(lib.aimet_adaround_recon_grad_indexed(P(q), P(out_data), P(idx_all), it_cur, P(g_buf), nb,
@@ -597,11 +620,23 @@ class AdaroundOptimizer:
 
         def step():
             s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+            if not fuse_wq:
+                soft_weight()
+            if mode == "dw" and _DW_FUSED:
+                # the batch read in place from the caches, q and g never stored; it_next moves here
+                _native.check(lib.aimet_adaround_dw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
+                                                         P(wq), pbias, P(gw_dw), P(ws), *dims, code, s))
+                adam_step(gw_dw, s)
+                return
+            if mode in ("pointwise", "im2col") and pw_dims is not None:
+                # 1x1 / unfolded stem with few channels: one pass, the batch read in place
+                _native.check(lib.aimet_adaround_pw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
+                                                         P(wq), pbias, P(gw_pw), P(ws_pw), *pw_dims, code, s))
+                adam_step(gw_pw, s)
+                return
             _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp),
                                                     None if indexed else P(target), P(idx_all), it_cur, it_next, nb,
                                                     row_in, row_out, s))
-            if not fuse_wq:
-                soft_weight()
             if mode == "dw":
                 _native.check(lib.aimet_dwconv2d_forward(P(inp), P(wq), pbias, P(q_buf), *dims, s))
                 recon(q_buf, False, s)
@@ -704,7 +739,7 @@ class AdaroundOptimizer:
             else:
                 del g
         _, mode, graph = best
-        AdaroundOptimizer.last_loop_form = mode
+        AdaroundOptimizer.last_loop_form = mode + ("_fused" if mode in ("pointwise", "im2col") and pw_dims else "")
         for a in range(0, iters, chunk):
             b = min(a + chunk, iters)
             if b < iters:

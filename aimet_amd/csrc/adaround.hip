@@ -16,6 +16,7 @@
 // the vectorized part, the scalar tail as std::pow), so Wq and dL/dalpha, the rounding-loss term
 // included, are bit-identical to the reference (tests/golden/golden_adaround.npz).
 #include "common.hpp"
+#include "recon.hpp"
 
 namespace aimet_amd
 {
@@ -581,30 +582,9 @@ __global__ __launch_bounds__(kBlock) void adaround_gather_kernel(const float* __
             dst[q] = src[q];
 }
 
-// ---- reconstruction-loss gradient (adaround_loss.py:70-80) ------------------------------------
-// loss = mean over (N, spatial) of ||act(q) - act(t)||^2 over dim 1, so
-// dloss/dq = scale * (act(q) - act(t)) * act'(q) with scale = 2 / (N * spatial): one elementwise
-// pass (12 B/elem) for the ~12 torch kernels of act / sub / norm / pow / mean and their backward.
-// act: 0 none, 1 ReLU (torch threshold_backward: x > 0), 2 ReLU6 (hardtanh(0, 6) backward:
-// 0 < x < 6).
-__device__ __forceinline__ float recon_g(float q, float t, float scale, int act)
-{
-    float a = q, b = t, m = 1.0f;
-    if (act == 1)
-    {
-        a = fmaxf(q, 0.0f);
-        b = fmaxf(t, 0.0f);
-        m = q > 0.0f ? 1.0f : 0.0f;
-    }
-    else if (act == 2)
-    {
-        a = fminf(fmaxf(q, 0.0f), 6.0f);
-        b = fminf(fmaxf(t, 0.0f), 6.0f);
-        m = (q > 0.0f && q < 6.0f) ? 1.0f : 0.0f;
-    }
-    return scale * (a - b) * m;
-}
-
+// ---- reconstruction-loss gradient (adaround_loss.py:70-80; recon_g in recon.hpp) --------------
+// one elementwise pass (12 B/elem) for the ~12 torch kernels of act / sub / norm / pow / mean and
+// their backward.
 __global__ __launch_bounds__(kBlock) void recon_grad_vec_kernel(const f4* __restrict__ q, const f4* __restrict__ t,
                                                                 f4* __restrict__ g, int64_t nq, float scale, int act)
 {

@@ -18,6 +18,7 @@
 // workgroup each; every lane keeps K*K partial sums, reduced in the workgroup by a fixed shuffle
 // tree, stored per slice; a fold kernel adds the slices in order -- deterministic.
 #include "common.hpp"
+#include "recon.hpp"
 
 namespace aimet_amd
 {
@@ -107,6 +108,157 @@ __global__ __launch_bounds__(kBlock) void dw_wgrad_kernel(const float* __restric
         }
     }
     // workgroup reduction of the K*K sums: wave shuffles, then the waves in order
+    __shared__ float sh[KK][kBlock / 64];
+#pragma unroll
+    for (int k = 0; k < KK; ++k)
+    {
+        float v = acc[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0)
+            sh[k][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < KK)
+    {
+        float v = 0.0f;
+#pragma unroll
+        for (int i = 0; i < kBlock / 64; ++i)
+            v += sh[threadIdx.x][i];
+        partial[((size_t) c * S + blockIdx.x) * KK + threadIdx.x] = v;
+    }
+}
+
+// The AdaRound iteration of a depthwise layer up to dL/dWq in ONE pass over the batch
+// (aimet_adaround_dw_step). For the positions of dw_wgrad_kernel's slices, sample n's input plane
+// and fp target are read in place from the caches (row idx_all[it][n]); q = dw_fwd_kernel's sum,
+// g = recon_grad_idx_kernel's gradient of q (recon_g), and the K*K products g * x accumulate in
+// dw_wgrad_kernel's order: the partials -- and grad_w after dw_wgrad_fold -- are bit-identical to
+// gather -> dw_fwd -> recon_grad_idx -> dw_wgrad, with no batch copy of the input and neither q nor
+// g in HBM (the caches are read once: |x| + |target| bytes per iteration instead of ~9 passes).
+struct DwStep
+{
+    const float* x_cache;     // [rows][C][H][W]
+    const float* t_cache;     // [rows][C][OH][OW]
+    const int64_t* idx_all;   // [iterations][N]
+    const int64_t* it_cur;
+    int64_t* it_next;         // workgroup (0, 0) writes it + 1 (as adaround_gather_kernel)
+    const float* w;           // [C][K][K]
+    const float* bias;        // nullable
+    float scale;              // 2 / (N * OH * OW)
+    int act;
+};
+
+// U positions per lane in flight (their taps, target and sample row loaded before any of them is
+// reduced; the accumulation order stays p, p + kBlock, ...), the batch's cache rows in LDS: the
+// loop is otherwise a chain of dependent loads per position
+template <int K>
+constexpr int kDwStepU = K == 3 ? 4 : 2;
+constexpr int kDwStepRows = 1024;   // batches up to this size keep their row table in LDS
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void dw_step_kernel(DwStep a, float* __restrict__ partial, DwShape s,
+                                                         uint32_t per)
+{
+    constexpr int KK  = K * K;
+    constexpr int U   = kDwStepU<K>;
+    const uint32_t c  = blockIdx.y;
+    const uint32_t S  = gridDim.x;
+    const uint32_t np = s.N * s.OH * s.OW;
+    const uint32_t p0 = blockIdx.x * per;
+    const uint32_t p1 = p0 + per < np ? p0 + per : np;
+    const int64_t it  = a.it_cur[0];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        a.it_next[0] = it + 1;
+    const int64_t* rows = a.idx_all + it * (int64_t) s.N;
+    __shared__ int64_t srows[kDwStepRows];
+    const bool lds_rows = s.N <= (uint32_t) kDwStepRows;
+    if (lds_rows)
+        for (uint32_t i = threadIdx.x; i < s.N; i += kBlock)
+            srows[i] = rows[i];
+    __syncthreads();
+    float wk[KK], acc[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k)
+    {
+        wk[k]  = a.w[c * KK + k];
+        acc[k] = 0.0f;
+    }
+    const float b0 = a.bias ? a.bias[c] : 0.0f;
+    for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += kBlock * U)
+    {
+        float xv[U][KK], tv[U];
+        int ih0[U], iw0[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t p = pb + u * kBlock;
+            ih0[u] = -(1 << 30);   // an out-of-range position: every tap skipped, nothing added
+            iw0[u] = 0;
+            tv[u]  = 0.0f;
+#pragma unroll
+            for (int k = 0; k < KK; ++k)
+                xv[u][k] = 0.0f;
+            if (p < p1)
+            {
+                const uint32_t n   = s.div_ohow.div(p);
+                const uint32_t rem = p - n * (s.OH * s.OW);
+                const uint32_t oh  = s.div_ow.div(rem);
+                const uint32_t ow  = rem - oh * s.OW;
+                const size_t plane = (size_t) (lds_rows ? srows[n] : rows[n]) * s.C + c;
+                const float* xp    = a.x_cache + plane * s.H * s.W;
+                tv[u]  = a.t_cache[plane * s.OH * s.OW + rem];
+                ih0[u] = (int) oh * s.stride - s.pad;
+                iw0[u] = (int) ow * s.stride - s.pad;
+#pragma unroll
+                for (int kh = 0; kh < K; ++kh)
+                {
+                    const int ih = ih0[u] + kh * s.dil;
+#pragma unroll
+                    for (int kw = 0; kw < K; ++kw)
+                    {
+                        const int iw = iw0[u] + kw * s.dil;
+                        if (ih >= 0 && ih < (int) s.H && iw >= 0 && iw < (int) s.W)
+                            xv[u][kh * K + kw] = xp[ih * (int) s.W + iw];
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            if (pb + u * kBlock >= p1)
+                break;
+            float v = b0;
+#pragma unroll
+            for (int kh = 0; kh < K; ++kh)
+            {
+                const int ih = ih0[u] + kh * s.dil;
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw)
+                {
+                    const int iw = iw0[u] + kw * s.dil;
+                    if (ih >= 0 && ih < (int) s.H && iw >= 0 && iw < (int) s.W)
+                        v = __builtin_fmaf(wk[kh * K + kw], xv[u][kh * K + kw], v);
+                }
+            }
+            // recon_grad_idx_kernel adds the (absent) bias as + 0.0f: the same here
+            const float g = recon_g(v + 0.0f, tv[u], a.scale, a.act);
+#pragma unroll
+            for (int kh = 0; kh < K; ++kh)
+            {
+                const int ih = ih0[u] + kh * s.dil;
+#pragma unroll
+                for (int kw = 0; kw < K; ++kw)
+                {
+                    const int iw = iw0[u] + kw * s.dil;
+                    if (ih >= 0 && ih < (int) s.H && iw >= 0 && iw < (int) s.W)
+                        acc[kh * K + kw] = __builtin_fmaf(g, xv[u][kh * K + kw], acc[kh * K + kw]);
+                }
+            }
+        }
+    }
     __shared__ float sh[KK][kBlock / 64];
 #pragma unroll
     for (int k = 0; k < KK; ++k)
@@ -234,6 +386,44 @@ void dw_grad_weight(const float* x, const float* grad_y, float* grad_w, float* w
         scratch_free(partial, st);
 }
 
+void dw_step(const float* x_cache, const float* t_cache, const int64_t* idx_all, const int64_t* it_cur,
+             int64_t* it_next, const float* w, const float* bias, float* grad_w, float* workspace, int64_t N,
+             int64_t C, int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride, int32_t pad,
+             int32_t dilation, int32_t act, hipStream_t st)
+{
+    DwShape s = make_shape(N, C, H, W, OH, OW, K, stride, pad, dilation);
+    AIMET_REQUIRE(act >= 0 && act <= 2, "act must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
+    AIMET_REQUIRE(C <= 65535, "depthwise weight gradient: at most 65535 channels");
+    require_device_ptr(x_cache, "x_cache");
+    require_device_ptr(t_cache, "target_cache");
+    require_device_ptr(idx_all, "idx_all");
+    require_device_ptr(it_cur, "it_cur");
+    require_device_ptr(it_next, "it_next");
+    require_device_ptr(w, "weight");
+    require_device_ptr(grad_w, "grad_w");
+    if (bias)
+        require_device_ptr(bias, "bias");
+    uint32_t per    = 0;
+    const int64_t S = wgrad_slices(N, C, OH, OW, &per);
+    if (workspace)
+        require_device_ptr(workspace, "workspace");
+    float* partial = workspace ? workspace
+                               : static_cast<float*>(scratch_alloc(sizeof(float) * (size_t) (C * S * K * K), st));
+    // aimet_adaround_recon_grad_indexed's scale: 2 / (number of dim-1 norms)
+    DwStep a {x_cache, t_cache, idx_all, it_cur, it_next, w, bias, (float) (2.0 / (double) (N * OH * OW)), act};
+    dim3 grid((unsigned) S, (unsigned) C);
+    if (K == 3)
+        dw_step_kernel<3><<<grid, kBlock, 0, st>>>(a, partial, s, per);
+    else
+        dw_step_kernel<5><<<grid, kBlock, 0, st>>>(a, partial, s, per);
+    AIMET_LAUNCH_CHECK();
+    dw_wgrad_fold<<<(unsigned) ceil_div(C * K * K, kBlock), kBlock, 0, st>>>(partial, grad_w, (uint32_t) C,
+                                                                            (uint32_t) S, (uint32_t) (K * K));
+    AIMET_LAUNCH_CHECK();
+    if (!workspace)
+        scratch_free(partial, st);
+}
+
 }   // namespace
 
 extern "C" {
@@ -263,6 +453,17 @@ int aimet_dwconv2d_grad_weight(const float* x, const float* grad_y, float* grad_
     return guarded([&] {
         dw_grad_weight(x, grad_y, grad_w, workspace, N, C, H, W, OH, OW, K, stride, pad, dilation,
                        as_stream(stream));
+    });
+}
+
+int aimet_adaround_dw_step(const float* x_cache, const float* target_cache, const int64_t* idx_all,
+                           const int64_t* it_cur, int64_t* it_next, const float* w, const float* bias, float* grad_w,
+                           float* workspace, int64_t N, int64_t C, int64_t H, int64_t W, int64_t OH, int64_t OW,
+                           int32_t K, int32_t stride, int32_t pad, int32_t dilation, int32_t act, void* stream)
+{
+    return guarded([&] {
+        dw_step(x_cache, target_cache, idx_all, it_cur, it_next, w, bias, grad_w, workspace, N, C, H, W, OH, OW, K,
+                stride, pad, dilation, act, as_stream(stream));
     });
 }
 

@@ -468,6 +468,33 @@ int aimet_dwconv2d_grad_weight(const float* x, const float* grad_y, float* grad_
                                int64_t C, int64_t H, int64_t W, int64_t OH, int64_t OW, int32_t K, int32_t stride,
                                int32_t pad, int32_t dilation, void* stream);
 
+/* The AdaRound iteration of a depthwise layer up to dL/dWq in one pass (no batch copy, no q / g
+ * tensors): for iteration it = it_cur_dev[0], sample n of the batch is row idx_all_dev[it * N + n]
+ * of x_cache ([rows][C][H][W]) and target_cache ([rows][C][OH][OW], the fp layer outputs); q =
+ * aimet_dwconv2d_forward(x, w, bias), g = aimet_adaround_recon_grad_indexed's gradient of q
+ * (act 0 none, 1 ReLU, 2 ReLU6) and grad_w = aimet_dwconv2d_grad_weight(x, g): bit-identical to
+ * aimet_adaround_gather + those three calls. it_next_dev[0] = it + 1 (as aimet_adaround_gather).
+ * `workspace` as aimet_dwconv2d_grad_weight. */
+int aimet_adaround_dw_step(const float* x_cache, const float* target_cache, const int64_t* idx_all_dev,
+                           const int64_t* it_cur_dev, int64_t* it_next_dev, const float* w, const float* bias,
+                           float* grad_w, float* workspace, int64_t N, int64_t C, int64_t H, int64_t W, int64_t OH,
+                           int64_t OW, int32_t K, int32_t stride, int32_t pad, int32_t dilation, int32_t act,
+                           void* stream);
+
+/* The AdaRound iteration of a 1x1 convolution (or the unfolded stem) with few channels up to
+ * dL/dWq in one pass: sample n of the batch is row idx_all_dev[it * N + n] (it = it_cur_dev[0])
+ * of x_cache ([rows][Cin][HW]) and target_cache ([rows][Cout][HW]); q = W @ x (W [Cout][Cin],
+ * sums over ci in order), g = aimet_adaround_recon_grad_indexed's gradient of q + bias (bias
+ * nullable; act 0 none, 1 ReLU, 2 ReLU6), grad_w = sum over the batch positions of g x^T in a
+ * fixed order (deterministic; fp32, not bit-identical to a library GEMM). it_next_dev[0] = it + 1.
+ * Cin, Cout <= 192, Cin * Cout <= 6144, HW % 4 == 0, x_cache 16-B aligned. `workspace`
+ * (aimet_adaround_pw_step_workspace elements, device) may be null (internal scratch). */
+int aimet_adaround_pw_step_workspace(int64_t N, int64_t Cin, int64_t Cout, int64_t HW, int64_t* elems);
+int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, const int64_t* idx_all_dev,
+                           const int64_t* it_cur_dev, int64_t* it_next_dev, const float* w, const float* bias,
+                           float* grad_w, float* workspace, int64_t N, int64_t Cin, int64_t Cout, int64_t HW,
+                           int32_t act, void* stream);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Blockwise (broadcast) quantization and the ONNX QcQuantizeOp                                */
 /* ------------------------------------------------------------------------------------------ */

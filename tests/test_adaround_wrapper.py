@@ -213,3 +213,55 @@ def test_adaround_loop_deterministic(kind):
     a = [AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, nn.ReLU6(),
                                              torch.Generator().manual_seed(5)).detach().clone() for _ in range(2)]
     assert torch.equal(a[0], a[1]), AdaroundOptimizer.last_loop_form
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("stride,act", [(1, nn.ReLU6()), (2, nn.ReLU()), (1, None)])
+def test_adaround_dw_fused_loop_equals_unfused(monkeypatch, stride, act):
+    """The depthwise loop with the fused step (aimet_adaround_dw_step: the batch read in place, q and g
+    never stored) gives the alpha of the four-launch loop (gather, forward, reconstruction gradient,
+    weight gradient), bit for bit."""
+    import aimet_amd.adaround_optimizer as ao
+    torch.manual_seed(4)
+    m = nn.Conv2d(24, 24, 3, stride=stride, padding=1, groups=24).to(DEV)
+    inp = torch.rand(48, 24, 28, 28, device=DEV)
+    with torch.no_grad():
+        out = m(inp) + 0.02 * torch.randn_like(m(inp))
+    d = (m.weight.detach().abs().amax(dim=(1, 2, 3)) / 127).contiguous()
+    o = torch.full((24,), -128.0, device=DEV)
+    p = ao.AdaroundHyperParameters(num_iterations=200, warm_start=0.2)
+    res = []
+    for fused in (True, False):
+        monkeypatch.setattr(ao, "_DW_FUSED", fused)
+        res.append(ao.AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, act,
+                                                          torch.Generator().manual_seed(6)).detach().clone())
+        assert ao.AdaroundOptimizer.last_loop_form == "dw"
+    assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.gpu
+@gpu
+def test_adaround_pw_fused_loop_deterministic_and_close_to_gemm_form(monkeypatch):
+    """The one-pass 1x1 loop (aimet_adaround_pw_step) gives one alpha per seed, and the alpha of the
+    GEMM form to fp32 summation-order tolerance (the two sum dL/dWq in different orders)."""
+    import aimet_amd.adaround_optimizer as ao
+    torch.manual_seed(5)
+    m = nn.Conv2d(16, 96, 1).to(DEV)
+    inp = torch.rand(48, 16, 16, 16, device=DEV)
+    with torch.no_grad():
+        out = m(inp) + 0.02 * torch.randn_like(m(inp))
+    d = (m.weight.detach().abs().amax(dim=(1, 2, 3)) / 127).contiguous()
+    o = torch.full((96,), -128.0, device=DEV)
+    p = ao.AdaroundHyperParameters(num_iterations=150, warm_start=0.2)
+
+    def run(form):
+        monkeypatch.setattr(ao, "_PW_FUSED", form)
+        a = ao.AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, nn.ReLU6(),
+                                                   torch.Generator().manual_seed(8)).detach().clone()
+        return a, ao.AdaroundOptimizer.last_loop_form
+
+    (a1, f1), (a2, _), (g, fg) = run("all"), run("all"), run("0")
+    assert (f1, fg) == ("pointwise_fused", "pointwise")
+    assert torch.equal(a1, a2)
+    torch.testing.assert_close(a1, g, rtol=1e-5, atol=1e-5)

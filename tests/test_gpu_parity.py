@@ -1267,6 +1267,103 @@ def test_depthwise_conv_kernels_vs_torch(N, C, H, K, stride, pad, dil):
     torch.testing.assert_close(gw, wr.grad, rtol=2e-5, atol=1e-6 * scale)
 
 
+@pytest.mark.parametrize("N,C,H,K,stride,pad,dil,act,with_bias", [(32, 32, 112, 3, 1, 1, 1, 2, False),
+                                                                   (8, 96, 56, 3, 2, 1, 1, 2, True),
+                                                                   (5, 7, 13, 3, 2, 0, 1, 0, True),
+                                                                   (4, 16, 19, 5, 1, 2, 1, 1, False),
+                                                                   (3, 12, 17, 3, 1, 2, 2, 1, True),
+                                                                   (32, 960, 7, 3, 1, 1, 1, 2, False)])
+def test_adaround_dw_step_equals_unfused_chain(N, C, H, K, stride, pad, dil, act, with_bias):
+    """aimet_adaround_dw_step (the depthwise AdaRound iteration in one pass over the cached rows)
+    == aimet_adaround_gather -> aimet_dwconv2d_forward -> aimet_adaround_recon_grad_indexed ->
+    aimet_dwconv2d_grad_weight, bit for bit, and moves the iteration counter the same way."""
+    import ctypes
+    from aimet_amd import _native
+    g = torch.Generator(device=DEV).manual_seed(N * C + K + act)
+    rows = N + 5
+    OH = (H + 2 * pad - dil * (K - 1) - 1) // stride + 1
+    x_cache = torch.randn(rows, C, H, H, device=DEV, generator=g)
+    t_cache = torch.randn(rows, C, OH, OH, device=DEV, generator=g) * 2 + 1
+    w = torch.randn(C, 1, K, K, device=DEV, generator=g) * 0.3
+    b = torch.randn(C, device=DEV, generator=g) if with_bias else None
+    iters = 3
+    idx = torch.stack([torch.randperm(rows, device=DEV, generator=g)[:N] for _ in range(iters)]).contiguous()
+    s = torch.cuda.current_stream().cuda_stream
+    P = lambda t: t.data_ptr() if t is not None else None   # noqa: E731
+    n_ws = ctypes.c_int64()
+    _native.call("aimet_dwconv2d_grad_weight_workspace", N, C, OH, OH, K, ctypes.byref(n_ws))
+    ws = torch.empty(n_ws.value, device=DEV)
+    for it in (0, 2):
+        # unfused chain
+        ctr = torch.tensor([it, -1], dtype=torch.long, device=DEV)
+        inp = torch.empty(N, C, H, H, device=DEV)
+        _native.call("aimet_adaround_gather", P(x_cache), P(t_cache), P(inp), None, P(idx), ctr.data_ptr(),
+                     ctr.data_ptr() + 8, N, C * H * H, C * OH * OH, s)
+        q = torch.empty(N, C, OH, OH, device=DEV)
+        _native.call("aimet_dwconv2d_forward", P(inp), P(w), P(b), P(q), N, C, H, H, OH, OH, K, stride, pad, dil, s)
+        gq = torch.empty_like(q)
+        _native.call("aimet_adaround_recon_grad_indexed", P(q), P(t_cache), P(idx), ctr.data_ptr(), P(gq), N, C,
+                     OH * OH, None, act, s)
+        gw_ref = torch.empty_like(w)
+        _native.call("aimet_dwconv2d_grad_weight", P(inp), P(gq), P(gw_ref), P(ws), N, C, H, H, OH, OH, K, stride,
+                     pad, dil, s)
+        # fused
+        ctr2 = torch.tensor([it, -1], dtype=torch.long, device=DEV)
+        gw = torch.empty_like(w)
+        _native.call("aimet_adaround_dw_step", P(x_cache), P(t_cache), P(idx), ctr2.data_ptr(), ctr2.data_ptr() + 8,
+                     P(w), P(b), P(gw), P(ws), N, C, H, H, OH, OH, K, stride, pad, dil, act, s)
+        assert torch.equal(gw.view(torch.int32), gw_ref.view(torch.int32)), it
+        assert ctr2.tolist() == ctr.tolist() == [it, it + 1]
+        assert bool(gw.abs().sum() > 0)
+
+
+@pytest.mark.parametrize("N,Cin,Cout,HW,act,with_bias", [(32, 16, 96, 112 * 112, 2, False),
+                                                          (32, 144, 24, 56 * 56, 0, True),
+                                                          (32, 32, 192, 28 * 28, 2, True),
+                                                          (7, 27, 32, 100, 1, False),
+                                                          (5, 3, 5, 12, 2, True),
+                                                          (4, 192, 32, 196, 0, False)])
+def test_adaround_pw_step_vs_torch(N, Cin, Cout, HW, act, with_bias):
+    """aimet_adaround_pw_step (a 1x1 layer's AdaRound iteration in one pass over the cached rows)
+    == the fp32 torch ops it replaces (index_select, W @ x, the reconstruction-loss gradient, the
+    weight gradient) to summation-order tolerance; deterministic; moves the iteration counter."""
+    import ctypes
+    from aimet_amd import _native
+    g = torch.Generator(device=DEV).manual_seed(Cin * Cout + HW)
+    rows = N + 3
+    x_cache = torch.rand(rows, Cin, HW, device=DEV, generator=g)
+    w = torch.randn(Cout, Cin, device=DEV, generator=g) / Cin ** 0.5
+    b = torch.randn(Cout, device=DEV, generator=g) * 0.1 if with_bias else None
+    t_cache = torch.randn(rows, Cout, HW, device=DEV, generator=g) * 0.5
+    idx = torch.stack([torch.randperm(rows, device=DEV, generator=g)[:N] for _ in range(2)]).contiguous()
+    it = 1
+    xb, tb = x_cache[idx[it]].double(), t_cache[idx[it]].double()
+    q = torch.einsum("oc,nch->noh", w.double(), xb) + (b.double()[None, :, None] if with_bias else 0)
+    actf = {0: lambda v: v, 1: torch.relu, 2: lambda v: v.clamp(0, 6)}[act]
+    mask = {0: lambda v: torch.ones_like(v), 1: lambda v: (v > 0).double(),
+            2: lambda v: ((v > 0) & (v < 6)).double()}[act]
+    gq = 2.0 / (N * HW) * (actf(q) - actf(tb)) * mask(q)
+    gw_ref = torch.einsum("noh,nch->oc", gq, xb)
+    n_ws = ctypes.c_int64()
+    _native.call("aimet_adaround_pw_step_workspace", N, Cin, Cout, HW, ctypes.byref(n_ws))
+    ws = torch.empty(n_ws.value, device=DEV)
+    s = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for use_ws in (True, False):
+        ctr = torch.tensor([it, -1], dtype=torch.long, device=DEV)
+        gw = torch.empty(Cout, Cin, device=DEV)
+        _native.call("aimet_adaround_pw_step", x_cache.data_ptr(), t_cache.data_ptr(), idx.data_ptr(),
+                     ctr.data_ptr(), ctr.data_ptr() + 8, w.data_ptr(), b.data_ptr() if with_bias else None,
+                     gw.data_ptr(), ws.data_ptr() if use_ws else None, N, Cin, Cout, HW, act, s)
+        assert ctr.tolist() == [it, it + 1]
+        outs.append(gw)
+    assert torch.equal(outs[0], outs[1])   # deterministic
+    # fp32 sums over N * HW positions: the error is bounded by a small multiple of eps * sum |g x|
+    bound = torch.einsum("noh,nch->oc", gq.abs(), xb.abs())
+    err = (outs[0].double() - gw_ref).abs()
+    assert bool((err <= 2e-5 * bound + 1e-12).all()), float((err / (bound + 1e-30)).max())
+
+
 @pytest.mark.parametrize("layer", ["conv", "depthwise", "pointwise", "linear", "linear_noact", "conv_gelu"])
 def test_adaround_fused_step_graph_equals_torch_adam_graph(layer):
     """The single-process loop with the batch draw and backward + Adam fused into two kernels
