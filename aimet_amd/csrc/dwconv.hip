@@ -20,6 +20,8 @@
 #include "common.hpp"
 #include "recon.hpp"
 
+#include <cstdlib>
+
 namespace aimet_amd
 {
 namespace
@@ -153,16 +155,16 @@ struct DwStep
 // U positions per lane in flight (their taps, target and sample row loaded before any of them is
 // reduced; the accumulation order stays p, p + kBlock, ...), the batch's cache rows in LDS: the
 // loop is otherwise a chain of dependent loads per position
-template <int K>
-constexpr int kDwStepU = K == 3 ? 4 : 2;
+template <int K, int UU>
+constexpr int kDwStepU = UU > 0 ? UU : (K == 3 ? 4 : 2);
 constexpr int kDwStepRows = 1024;   // batches up to this size keep their row table in LDS
 
-template <int K>
+template <int K, int UU = 0>
 __global__ __launch_bounds__(kBlock) void dw_step_kernel(DwStep a, float* __restrict__ partial, DwShape s,
                                                          uint32_t per)
 {
     constexpr int KK  = K * K;
-    constexpr int U   = kDwStepU<K>;
+    constexpr int U   = kDwStepU<K, UU>;
     const uint32_t c  = blockIdx.y;
     const uint32_t S  = gridDim.x;
     const uint32_t np = s.N * s.OH * s.OW;
@@ -298,7 +300,14 @@ __global__ __launch_bounds__(kBlock) void dw_wgrad_fold(const float* __restrict_
 int64_t wgrad_slices(int64_t N, int64_t C, int64_t OH, int64_t OW, uint32_t* per_out)
 {
     const int64_t np   = N * OH * OW;
-    int64_t S          = ceil_div(np, (int64_t) kBlock * 16);
+    // positions per lane per slice (16; AIMET_TUNE_DW_PER: tuning experiments only -- it changes the
+    // summation order of the weight gradient, for the fused and the unfused path alike)
+    static const int64_t ppl = [] {
+        const char* e = getenv("AIMET_TUNE_DW_PER");
+        const int64_t v = e ? atoll(e) : 16;
+        return v >= 1 && v <= 256 ? v : (int64_t) 16;
+    }();
+    int64_t S          = ceil_div(np, (int64_t) kBlock * ppl);
     const int64_t want = ceil_div(2048, C);
     if (S < want)
         S = want < ceil_div(np, kBlock) ? want : ceil_div(np, kBlock);
@@ -412,7 +421,17 @@ void dw_step(const float* x_cache, const float* t_cache, const int64_t* idx_all,
     // aimet_adaround_recon_grad_indexed's scale: 2 / (number of dim-1 norms)
     DwStep a {x_cache, t_cache, idx_all, it_cur, it_next, w, bias, (float) (2.0 / (double) (N * OH * OW)), act};
     dim3 grid((unsigned) S, (unsigned) C);
-    if (K == 3)
+    static const int u = [] {
+        const char* e = getenv("AIMET_TUNE_DW_U");   // tuning experiments only (same results)
+        return e ? atoi(e) : 0;
+    }();
+    if (K == 3 && u == 1)
+        dw_step_kernel<3, 1><<<grid, kBlock, 0, st>>>(a, partial, s, per);
+    else if (K == 3 && u == 2)
+        dw_step_kernel<3, 2><<<grid, kBlock, 0, st>>>(a, partial, s, per);
+    else if (K == 3 && u == 8)
+        dw_step_kernel<3, 8><<<grid, kBlock, 0, st>>>(a, partial, s, per);
+    else if (K == 3)
         dw_step_kernel<3><<<grid, kBlock, 0, st>>>(a, partial, s, per);
     else
         dw_step_kernel<5><<<grid, kBlock, 0, st>>>(a, partial, s, per);
