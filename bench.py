@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--cpu-sample-images", type=int, default=32,
                    help="images of each activation tensor (plus all weights) timed on the CPU oracle")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--enc-reps", type=int, default=5, help="timed compute_encodings calls after the cold one")
+    p.add_argument("--enc-reps", type=int, default=9, help="timed compute_encodings calls after the cold one")
     p.add_argument("--eager", action="store_true", help="launch every QDQ from Python instead of HIP graphs")
     p.add_argument("--per-weight-launches", action="store_true",
                    help="one per-channel QDQ launch per weight instead of the batched plan")
