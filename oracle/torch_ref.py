@@ -70,6 +70,43 @@ def lg_gradients(x, grad, emin, emax, bw, sym=False, strict=False, unsigned=Fals
     return grad_x, (-t1 + emax * t2).view_as(emin), (t1 - emin * t2).view_as(emax)
 
 
+def lg_encoding_grads_bound(x, grad, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0):
+    """The encoding gradients of lg_gradients in float64 from the same float32 forward quantities
+    (x_quant, delta, offset, mask), with the magnitude each one is summed from: returns
+    (gmin, gmax, bmin, bmax) where b = sum of |terms| carried through the same linear combination.
+    An fp32 result whose error is at most c * eps * b (c = a small multiple of the summation depth)
+    is as exact as an fp32 sum in any order can be; tests state c."""
+    _, mask, x_quant, delta, offset, steps = lg_forward(x, emin, emax, bw, sym, strict, unsigned, ch_axis)
+    dims = list(range(x.dim()))
+    if emin.numel() > 1:
+        dims.pop(ch_axis)
+    X, G, XQ, D, O, M = (t.double() for t in (x, grad, x_quant, delta, offset, mask))
+    st = float(steps)
+    if sym:
+        t1, t2 = (XQ + O) * G, M * (X / D) * G
+        half = math.floor(st / 2)
+        gmax = (t1.sum(dim=dims) - t2.sum(dim=dims)) / half
+        b = (t1.abs().sum(dim=dims) + t2.abs().sum(dim=dims)) / half
+        return (-gmax).view_as(emin), gmax.view_as(emax), b.view_as(emin), b.view_as(emax)
+    gs = (XQ + O - X * M / D) * G
+    go = D * G * (1 - M)
+    lo, hi = emin.double().reshape(-1), emax.double().reshape(-1)
+    k = st / (hi - lo) ** 2
+    t1, b1 = gs.sum(dim=dims).reshape(-1) / st, gs.abs().sum(dim=dims).reshape(-1) / st
+    s2, b2 = go.sum(dim=dims).reshape(-1), go.abs().sum(dim=dims).reshape(-1)
+    gmin, gmax = -t1 + hi * k * s2, t1 - lo * k * s2
+    bmin, bmax = b1 + hi.abs() * k * b2, b1 + lo.abs() * k * b2
+    return gmin.view_as(emin), gmax.view_as(emax), bmin.view_as(emin), bmax.view_as(emax)
+
+
+def assert_within_sum_bound(got, exact, bound, c, what=""):
+    """|got - exact| <= c * 2^-24 * bound elementwise (+ the smallest normal, for all-zero sums)."""
+    err = (got.double().reshape(-1).cpu() - exact.reshape(-1).cpu()).abs()
+    lim = c * 2.0 ** -24 * bound.reshape(-1).cpu() + 1.2e-38
+    worst = float((err / lim).max()) if err.numel() else 0.0
+    assert bool((err <= lim).all()), "%s: error %.3g x the bound (c = %d)" % (what, worst, c)
+
+
 ZETA, GAMMA = 1.1, -0.1   # aimet_common/defs.py:302-306
 
 

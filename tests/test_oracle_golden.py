@@ -197,3 +197,21 @@ def test_torch_ref_adaround_pinned_to_reference(golden_dir):
             assert float(rl) == float(z[k + "round_loss"]), i
     finally:
         torch.set_num_threads(nt)
+
+
+def test_lg_encoding_gradient_bound_holds_for_the_reference(golden_dir):
+    """The stated bound of the learned-grid encoding gradients (oracle/torch_ref.py:
+    lg_encoding_grads_bound): the reference module's own fp32 results (golden_lg.npz) lie within
+    16 eps x (sum of |terms|) of the float64 sums -- the bound the GPU kernels are held to."""
+    import os
+    import numpy as np
+    import torch
+    from oracle import torch_ref as T
+    g = dict(np.load(os.path.join(golden_dir, "golden_lg.npz")))
+    for i in range(5):
+        x, gr = torch.from_numpy(g["c%d_x" % i]), torch.from_numpy(g["c%d_grad" % i])
+        emin, emax = torch.from_numpy(g["c%d_emin" % i]), torch.from_numpy(g["c%d_emax" % i])
+        bw, sym = (int(v) for v in g["c%d_cfg" % i])
+        ex_min, ex_max, b_min, b_max = T.lg_encoding_grads_bound(x, gr, emin, emax, bw, bool(sym))
+        T.assert_within_sum_bound(torch.from_numpy(g["c%d_gmin" % i]), ex_min, b_min, 16, "grad_min %d" % i)
+        T.assert_within_sum_bound(torch.from_numpy(g["c%d_gmax" % i]), ex_max, b_max, 16, "grad_max %d" % i)
