@@ -517,6 +517,7 @@ std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* 
         j.ent   = q->kind == kKindEntropy ? 1 : 0;
         j.vec   = (reinterpret_cast<uintptr_t>(j.x) & 15) == 0 ? 1 : 0;
         j.seen  = q->stats_updated ? 1 : 0;
+        j.fresh = 0;
     }
     return jobs;
 }
@@ -1060,28 +1061,49 @@ int aimet_calibrate_launch(aimet_tensor_quantizer* const* act_qs, const float* c
         if (dev < 0)
             return;
         DeviceGuard g(dev);
-        // each side resets its own quantizers (the parameters' PDF arenas are most of the bytes)
-        if (reset)
-            reset_many(act_qs, n_act, ms);
-        if (n_par)
-        {
-            // the parameters first, on their own stream: their statistics take the CUs before the
-            // activation passes, their search runs beside them (aimet_amd/calibration.py)
-            if (ss != ms)
-                stream_join(ss, ms);
-            if (reset)
-                reset_many(par_qs, n_par, ss);
-            channel_stats_many(par_qs, par_x, par_outer, par_C, par_K, n_par, ss);
-            encodings_launch(par_qs, n_par, (uint32_t) par_settings[0], par_settings[1], par_settings[2],
-                             par_settings[3], ss, rp);
-        }
+        // the parameters' stream starts after everything already queued on the main stream (the
+        // inputs are ordered there), before the activation passes are added to it
+        if (n_par && ss != ms)
+            stream_join(ss, ms);
+        // enqueued right after the activations' min/max pass (launch_stats_many's `between`), so that
+        // pass starts at once: the resets (the activations' ones joined back into the main stream
+        // before the pass's combine / fold; the pass itself treats the quantizers as reset,
+        // StatsJob::fresh), then the parameters' statistics and search, run on the high-priority
+        // parameters' stream beside the activation passes (aimet_amd/calibration.py)
+        auto rest = [&] {
+            if (reset && n_act)
+            {
+                // on the parameters' stream, beside the min/max pass (it treats the quantizers as
+                // reset already): the main stream waits for it before the pass's combine / fold
+                reset_many(act_qs, n_act, ss);
+                if (ss != ms)
+                    stream_join(ms, ss);
+            }
+            if (n_par)
+            {
+                if (reset)
+                    reset_many(par_qs, n_par, ss);
+                channel_stats_many(par_qs, par_x, par_outer, par_C, par_K, n_par, ss);
+                encodings_launch(par_qs, n_par, (uint32_t) par_settings[0], par_settings[1], par_settings[2],
+                                 par_settings[3], ss, rp);
+            }
+        };
         if (n_act)
         {
             auto jobs = make_jobs(act_qs, act_x, act_n, nullptr, n_act);
-            launch_stats_many(jobs, kPhaseMinmax | kPhaseFoldMinmax | kPhaseHistogram | kPhaseFoldHistogram, ms);
+            if (reset)
+                for (auto& j: jobs)
+                {
+                    j.fresh = 1;
+                    j.seen  = 0;
+                }
+            launch_stats_many(jobs, kPhaseMinmax | kPhaseFoldMinmax | kPhaseHistogram | kPhaseFoldHistogram, ms,
+                              rest);
             for (int64_t i = 0; i < n_act; ++i)
                 act_qs[i]->stats_updated = true;
         }
+        else
+            rest();
         encodings_launch(act_qs, n_act, (uint32_t) act_settings[0], act_settings[1], act_settings[2],
                          act_settings[3], ms, ra);
         if (n_par && ss != ms)

@@ -698,7 +698,7 @@ __device__ __forceinline__ float2 minmax_tile(const float* __restrict__ x, int64
 __global__ __launch_bounds__(kBlock) void minmax_many_kernel(const StatsJob* __restrict__ jobs, int njobs)
 {
     const StatsJob& J = jobs[find_job(jobs, njobs, blockIdx.x, false)];
-    if (J.hist && !J.ent && J.d.pdf_init[0])
+    if (J.hist && !J.ent && !J.fresh && J.d.pdf_init[0])
         return;   // PDF schemes take min/max on the first (non-zero) batch only
     const int64_t tile = blockIdx.x - J.mm_block0;
     const float2 r     = minmax_tile(J.x, J.n, J.vec, tile, tile + 1 == (int64_t) J.mm_blocks);
@@ -732,7 +732,7 @@ __global__ __launch_bounds__(kBlock) void minmax_walk_kernel(const StatsJob* __r
         b0      = J.mm_block0;
         next_b0 = j + 1 < njobs ? jobs[j + 1].mm_block0 : tiles;
         // PDF schemes take min/max on the first (non-zero) batch only
-        skip = J.hist && !J.ent && J.d.pdf_init[0];
+        skip = J.hist && !J.ent && !J.fresh && J.d.pdf_init[0];
     };
     // the first quantizer after `from` that is not skipped (njobs if none): 64 job entries per
     // round of parallel loads, instead of one dependent load per skipped quantizer (a later ViT-L/16
@@ -746,7 +746,7 @@ __global__ __launch_bounds__(kBlock) void minmax_walk_kernel(const StatsJob* __r
             if (j < njobs)
             {
                 const StatsJob& J = jobs[j];
-                live              = !(J.hist && !J.ent && J.d.pdf_init[0]);
+                live              = !(J.hist && !J.ent && !J.fresh && J.d.pdf_init[0]);
             }
             const unsigned long long m = __ballot(live);
             if (m)
@@ -785,7 +785,7 @@ __global__ __launch_bounds__(kBlock) void minmax_walk_kernel(const StatsJob* __r
 __global__ __launch_bounds__(kBlock) void combine_many_kernel(const StatsJob* __restrict__ jobs, int fold)
 {
     const StatsJob& J = jobs[blockIdx.x];
-    if (J.hist && !J.ent && J.d.pdf_init[0])
+    if (J.hist && !J.ent && !J.fresh && J.d.pdf_init[0])
         return;
     const float2* partials = reinterpret_cast<const float2*>(J.mm_part);
     float a = -INFINITY, b = -INFINITY;
@@ -1159,7 +1159,7 @@ static int hist_many_cols()
     return v;
 }
 
-void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
+void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s, const std::function<void()>& between)
 {
     if (jobs.empty())
         return;
@@ -1201,6 +1201,23 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s)
         else
             minmax_many_kernel<<<(unsigned) mm, kBlock, 0, s>>>(dj, n);
         AIMET_LAUNCH_CHECK();
+    }
+    if (between)
+    {
+        try
+        {
+            between();
+        }
+        catch (...)
+        {
+            if (parts)
+                scratch_free(parts, s);
+            scratch_free(dj, s);
+            throw;
+        }
+    }
+    if (phases & kPhaseMinmax)
+    {
         combine_many_kernel<<<n, kBlock, 0, s>>>(dj, (phases & kPhaseFoldMinmax) ? 1 : 0);
         AIMET_LAUNCH_CHECK();
     }

@@ -6,6 +6,8 @@
 // of stream-ordered kernels with no host round trip; only getEncoding reads them back.
 #pragma once
 
+#include <functional>
+
 #include "common.hpp"
 
 #include <vector>
@@ -83,6 +85,8 @@ struct StatsJob
     int32_t hist, vec;
     int32_t ent;     // entropy analyzer (hist == 1 too): min/max every batch, TensorProfilingParams
     int32_t seen;    // the quantizer has seen a batch since its reset (host flag; a schedule hint only)
+    int32_t fresh;   // reset in this call after the min/max pass (launch_stats_many's `between`): its
+                     // PDF range counts as unset whatever the device state still says
 };
 enum StatsPhase
 {
@@ -91,7 +95,10 @@ enum StatsPhase
     kPhaseHistogram     = 4,
     kPhaseFoldHistogram = 8
 };
-void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s);
+// `between` (optional) runs on the host right after the min/max pass is enqueued and before its
+// combine / fold: the calibration enqueues the quantizers' reset and the parameters' work there
+void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s,
+                       const std::function<void()>& between = {});
 // Many per-channel quantizers ([outer][C][K] tensors) with the whole updateStats (min/max, fold,
 // histogram, fold) in TWO launches: every channel of every quantizer is one workgroup, and the
 // fold of a channel needs only that channel's statistics, so it runs in the workgroup that

@@ -143,7 +143,7 @@ class AimetTensorQuantizer:
                 q._handle, q._device = ctypes.c_void_p(h), idx
                 if q._pending_percentile is not None:
                     _native.call("aimet_tq_set_percentile_value", q._handle, float(q._pending_percentile))
-        return [q._ensure(device) for q in quantizers]
+        return [q._handle if q._handle is not None and q._device == idx else q._ensure(device) for q in quantizers]
 
     def _release(self):
         if self._handle is not None:
@@ -445,24 +445,36 @@ class AimetTensorQuantizer:
             raise ValueError("calibrateResidentAsync: the activation quantizers are per-tensor")
         dev = (activations[0] if aq else params[0]).device
         ch_axes = list(param_ch_axes) if param_ch_axes is not None else [0] * len(pq)
+        # host preparation is on the critical path of a ~4 ms call (the first launch waits for it):
+        # one pass over the tensors with the fewest torch attribute calls, the checks of
+        # _require_gpu folded in, the per-channel views cached by (shape, axis)
+        f32 = torch.float32
         keep, a_ptr, a_n = [], [], []
         for t in activations:
-            _require_gpu(t)
-            t = t if t.is_contiguous() else t.contiguous()
-            if t.dtype != torch.float32:
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == f32):
+                _require_gpu(t)
                 raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
+            if not t.is_contiguous():
+                t = t.contiguous()
             keep.append(t)
             a_ptr.append(t.data_ptr())
             a_n.append(t.numel())
         p_ptr, outers, Cs, Ks = [], [], [], []
+        views = _PER_CHANNEL_VIEWS
         for q, t, ax in zip(pq, params, ch_axes):
-            _require_gpu(t)
-            t = t if t.is_contiguous() else t.contiguous()
-            if t.dtype != torch.float32:
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == f32):
+                _require_gpu(t)
                 raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
-            outer, C, K = per_channel_view(t.shape, ax) if q._num_channels != 1 else (1, 1, t.numel())
-            if C != q._num_channels:
-                raise ValueError("tensor has %d channels along axis %d, quantizer has %d" % (C, ax, q._num_channels))
+            if not t.is_contiguous():
+                t = t.contiguous()
+            nc = q._num_channels
+            key = (t.shape, ax, nc)
+            v = views.get(key)
+            if v is None:
+                v = views[key] = per_channel_view(t.shape, ax) if nc != 1 else (1, 1, t.numel())
+            outer, C, K = v
+            if C != nc:
+                raise ValueError("tensor has %d channels along axis %d, quantizer has %d" % (C, ax, nc))
             keep.append(t)
             p_ptr.append(t.data_ptr())
             outers.append(outer)
@@ -603,6 +615,10 @@ class AimetTensorQuantizer:
         table = self.channelTable(encodings, t.device)
         out = qdq_per_channel_table(t, table, N // (C * K), C, K, round_mode)
         return out.cpu() if staged else out
+
+
+# (shape, channel axis, channels) -> per_channel_view (calibrateResidentAsync)
+_PER_CHANNEL_VIEWS = {}
 
 
 class PendingEncodings:
