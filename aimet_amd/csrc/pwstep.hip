@@ -19,6 +19,12 @@
 //
 // Sizes: Cin, Cout <= 192, Cin * Cout <= 6144 and at most 512 4 x 4 gradient blocks (two per
 // lane); fp32, NCHW caches with HW = H * W positions per channel plane, HW % 4 == 0.
+//
+// Measured (profiles/r03/adaround_pw_fused_forms.txt): faster than the GEMM form on expanding
+// layers (C_out >= 4 C_in) at >= 56^2 positions, slower on projecting layers, so the loop takes
+// it by that shape rule (adaround_optimizer.py: _PW_FUSED). The kernel is LDS-bound; the dL/dW
+// phase's 16-B reads of Xs rows 4 apart (stride 144 floats = 16 banks) conflict 4-way, and a
+// position-major copy of Xs / Gs for that phase is the next step.
 #include "common.hpp"
 #include "recon.hpp"
 
