@@ -9,22 +9,23 @@
 // (|x| + |q| bytes) and keeps q, g and the weight-gradient partials on chip:
 //
 //   per tile of T = 32 positions of one sample (rows idx_all[it][n] of the caches):
-//     Xs[ci][t]   <- x_cache[row][ci][hw0 + t]                         (LDS)
-//     q[co][t]     = sum_ci W[co][ci] * Xs[ci][t]  (ci ascending, fmaf) (registers)
-//     Gs[co][t]    = recon_g(q + bias[co], target[row][co][hw0 + t])    (LDS; recon.hpp, as
+//     XT[t][ci]   <- x_cache[row][ci][hw0 + t]                         (LDS)
+//     q[co][t]     = sum_ci W[co][ci] * XT[t][ci]  (ci ascending, fmaf) (registers)
+//     GT[t][co]    = recon_g(q + bias[co], target[row][co][hw0 + t])    (LDS; recon.hpp, as
 //                    aimet_adaround_recon_grad_indexed with the bias: the GEMM form's arithmetic)
-//     acc[co][ci] += sum_t Gs[co][t] * Xs[ci][t]   (t ascending, fmaf)  (registers, per lane)
+//     acc[co][ci] += sum_t GT[t][co] * XT[t][ci]   (t ascending, fmaf)  (registers, per lane)
 //   each workgroup walks tiles blockIdx.x, + gridDim.x, ... and stores its Cout x Cin partial;
 //   a fold adds the partials in workgroup order: deterministic.
 //
 // Sizes: Cin, Cout <= 192, Cin * Cout <= 6144 and at most 512 4 x 4 gradient blocks (two per
 // lane); fp32, NCHW caches with HW = H * W positions per channel plane, HW % 4 == 0.
 //
-// Measured (profiles/r03/adaround_pw_fused_forms.txt): faster than the GEMM form on expanding
-// layers (C_out >= 4 C_in) at >= 56^2 positions, slower on projecting layers, so the loop takes
-// it by that shape rule (adaround_optimizer.py: _PW_FUSED). The kernel is LDS-bound; the dL/dW
-// phase's 16-B reads of Xs rows 4 apart (stride 144 floats = 16 banks) conflict 4-way, and a
-// position-major copy of Xs / Gs for that phase is the next step.
+// Measured (profiles/r03/adaround_pw_fused_forms.txt): faster than the GEMM form on MobileNet-v2's
+// expanding layers and the stem (0.24 -> 0.16 ms per iteration at 16 -> 96 x 112^2), even at
+// 56^2 on projecting ones, slower on projecting layers below 56^2, which the loop's shape rule
+// leaves to the GEMM form (adaround_optimizer.py: _PW_FUSED). The kernel is LDS-bound; its LDS
+// images are position-major so the dL/dW phase's 16-B reads are contiguous across lanes (the
+// ci-major first version was 1.2-1.9x slower).
 #include "common.hpp"
 #include "recon.hpp"
 
@@ -34,7 +35,6 @@ namespace
 {
 
 constexpr int kPwT     = 32;                    // positions per tile
-constexpr int kPwPad   = kPwT + 4;              // LDS row stride (16-B aligned rows)
 constexpr int kPwMaxC  = 192;
 constexpr int kPwPairs = 6144;
 
@@ -72,32 +72,38 @@ __device__ __forceinline__ void pw_load_x(const PwStep& a, const int64_t* rows, 
     }
 }
 
-// Register blocking (LDS operand traffic, not HBM, bounded the first version: 2 LDS reads per FMA):
+// Register blocking, position-major LDS images (XT[t][ci], GT[t][co]; row stride kPwRow floats):
 //   q / g:  lane (tq, cr) = (lane % 8, lane / 8) computes t = 4 tq .. 4 tq + 3 of rows
-//           co = cr + 32 j: per ci one 16-B read of Xs and one read of W per row for 4 FMAs per row;
+//           co = cr + 32 j: per 4 input channels four 16-B reads of XT (its 4 positions) and one
+//           16-B read of W per row for 16 FMAs per row (ci ascending);
 //   dL/dW:  lane b owns blocks b and b + 256 of 4 x 4 (co, ci) pairs (blocks row-major over
-//           ceil(Cout / 4) x ceil(Cin / 4)): per 4 positions 8 16-B reads for 64 FMAs.
-// Rows of Xs / Gs past Cin / Cout up to the next multiple of 4 are zero, so partial blocks add 0.
-constexpr int kPwJ      = kPwMaxC / 32;   // 6 output rows per lane in the q / g phase
-constexpr int kPwBlocks = 2;              // 4 x 4 gradient blocks per lane
+//           ceil(Cout / 4) x ceil(Cin / 4)): per position one 16-B read of GT and one of XT for 16
+//           FMAs (t ascending); consecutive lanes read consecutive 16-B chunks of an XT row.
+// Columns of XT / GT / W past Cin / Cout up to the next multiple of 4 are zero.
+constexpr int kPwJ      = kPwMaxC / 32;     // 6 output rows per lane in the q / g phase
+constexpr int kPwBlocks = 2;                // 4 x 4 gradient blocks per lane
+constexpr int kPwRow    = kPwMaxC + 4;      // XT / GT row stride (16-B aligned)
 
 __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __restrict__ partial)
 {
-    __shared__ __attribute__((aligned(16))) float Xs[kPwMaxC * kPwPad];
-    __shared__ __attribute__((aligned(16))) float Gs[kPwMaxC * kPwPad];
-    __shared__ float Ws[kPwPairs];
+    __shared__ __attribute__((aligned(16))) float XT[kPwT * kPwRow];
+    __shared__ __attribute__((aligned(16))) float GT[kPwT * kPwRow];
+    __shared__ __attribute__((aligned(16))) float Ws[kPwPairs + 3 * kPwMaxC];
     const uint32_t Cin = a.Cin, Cout = a.Cout, pairs = Cin * Cout;
-    const uint32_t Cin4 = (Cin + 3) / 4, Cout4 = (Cout + 3) / 4;
+    const uint32_t Cin4 = (Cin + 3) / 4, Cout4 = (Cout + 3) / 4, wrow = 4 * Cin4;
     const int64_t it = a.it_cur[0];
     if (blockIdx.x == 0 && threadIdx.x == 0)
         a.it_next[0] = it + 1;
     const int64_t* rows = a.idx_all + it * (int64_t) a.N;
-    for (uint32_t e = threadIdx.x; e < pairs; e += kBlock)
-        Ws[e] = a.w[e];
-    for (uint32_t e = threadIdx.x; e < (4 * Cin4 - Cin) * kPwPad; e += kBlock)
-        Xs[Cin * kPwPad + e] = 0.0f;
-    for (uint32_t e = threadIdx.x; e < (4 * Cout4 - Cout) * kPwPad; e += kBlock)
-        Gs[Cout * kPwPad + e] = 0.0f;
+    for (uint32_t e = threadIdx.x; e < Cout * wrow; e += kBlock)
+    {
+        const uint32_t co = e / wrow, ci = e - co * wrow;
+        Ws[e] = ci < Cin ? a.w[co * Cin + ci] : 0.0f;
+    }
+    for (uint32_t e = threadIdx.x; e < kPwT * (wrow - Cin); e += kBlock)
+        XT[(e / (wrow - Cin)) * kPwRow + Cin + e % (wrow - Cin)] = 0.0f;
+    for (uint32_t e = threadIdx.x; e < kPwT * (4 * Cout4 - Cout); e += kBlock)
+        GT[(e / (4 * Cout4 - Cout)) * kPwRow + Cout + e % (4 * Cout4 - Cout)] = 0.0f;
     const uint32_t tq = threadIdx.x % 8, cr = threadIdx.x / 8;
     float acc[kPwBlocks][16];
 #pragma unroll
@@ -114,13 +120,19 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
         const uint32_t hw0 = (tile - n * a.tiles_per_sample) * kPwT;
         const bool t_in    = hw0 + 4 * tq < a.HW;   // HW % 4 == 0: the quad is in or out
         const float* tr    = a.t_cache + (size_t) rows[n] * Cout * a.HW;   // uniform base
-        __syncthreads();   // the previous tile's Xs / Gs are consumed (and Ws / the pads written)
+        __syncthreads();   // the previous tile's XT / GT are consumed (and W / the pads written)
 #pragma unroll
         for (int k = 0; k < kPwQuads; ++k)
         {
             const uint32_t q = threadIdx.x + kBlock * k;
             if (q < Cin * (kPwT / 4))
-                *reinterpret_cast<float4*>(Xs + (q / (kPwT / 4)) * kPwPad + 4 * (q % (kPwT / 4))) = nxt[k];
+            {
+                const uint32_t ci = q / (kPwT / 4), t = 4 * (q % (kPwT / 4));
+                XT[t * kPwRow + ci]       = nxt[k].x;
+                XT[(t + 1) * kPwRow + ci] = nxt[k].y;
+                XT[(t + 2) * kPwRow + ci] = nxt[k].z;
+                XT[(t + 3) * kPwRow + ci] = nxt[k].w;
+            }
         }
         __syncthreads();
         if (tile + gridDim.x < a.tiles)
@@ -134,24 +146,35 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
             tv[j] = co < Cout && t_in ? *reinterpret_cast<const float4*>(tr + co * a.HW + hw0 + 4 * tq)
                                       : make_float4(0.f, 0.f, 0.f, 0.f);
         }
-        float4 q[kPwJ];
+        float q[kPwJ][4];
 #pragma unroll
         for (int j = 0; j < kPwJ; ++j)
-            q[j] = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (uint32_t ci = 0; ci < Cin; ++ci)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                q[j][k] = 0.0f;
+        for (uint32_t c4 = 0; c4 < Cin4; ++c4)
         {
-            const float4 xv = *reinterpret_cast<const float4*>(Xs + ci * kPwPad + 4 * tq);
+            float4 xv[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                xv[k] = *reinterpret_cast<const float4*>(XT + (4 * tq + k) * kPwRow + 4 * c4);
 #pragma unroll
             for (int j = 0; j < kPwJ; ++j)
             {
                 const uint32_t co = cr + 32 * j;
                 if (co < Cout)
                 {
-                    const float wv = Ws[co * Cin + ci];
-                    q[j].x = __builtin_fmaf(wv, xv.x, q[j].x);
-                    q[j].y = __builtin_fmaf(wv, xv.y, q[j].y);
-                    q[j].z = __builtin_fmaf(wv, xv.z, q[j].z);
-                    q[j].w = __builtin_fmaf(wv, xv.w, q[j].w);
+                    const float4 wv = *reinterpret_cast<const float4*>(Ws + co * wrow + 4 * c4);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k)
+                    {
+                        float v = q[j][k];
+                        v = __builtin_fmaf(wv.x, xv[k].x, v);
+                        v = __builtin_fmaf(wv.y, xv[k].y, v);
+                        v = __builtin_fmaf(wv.z, xv[k].z, v);
+                        v = __builtin_fmaf(wv.w, xv[k].w, v);
+                        q[j][k] = v;
+                    }
                 }
             }
         }
@@ -162,15 +185,10 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
             if (co < Cout)
             {
                 const float bs = a.bias ? a.bias[co] : 0.0f;
-                float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (t_in)
-                {
-                    g.x = recon_g(q[j].x + bs, tv[j].x, a.scale, a.act);
-                    g.y = recon_g(q[j].y + bs, tv[j].y, a.scale, a.act);
-                    g.z = recon_g(q[j].z + bs, tv[j].z, a.scale, a.act);
-                    g.w = recon_g(q[j].w + bs, tv[j].w, a.scale, a.act);
-                }
-                *reinterpret_cast<float4*>(Gs + co * kPwPad + 4 * tq) = g;
+                const float tk[4] = {tv[j].x, tv[j].y, tv[j].z, tv[j].w};
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    GT[(4 * tq + k) * kPwRow + co] = t_in ? recon_g(q[j][k] + bs, tk[k], a.scale, a.act) : 0.0f;
             }
         }
         __syncthreads();
@@ -182,30 +200,17 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
             if (b < Cout4 * Cin4)
             {
                 const uint32_t cb = b / Cin4, ib = b - cb * Cin4;
-                const float* g0 = Gs + 4 * cb * kPwPad;
-                const float* x0 = Xs + 4 * ib * kPwPad;
-#pragma unroll 2
-                for (int t4 = 0; t4 < kPwT / 4; ++t4)
+#pragma unroll 4
+                for (int t = 0; t < kPwT; ++t)
                 {
-                    float4 gv[4], xv[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                    {
-                        gv[r] = *reinterpret_cast<const float4*>(g0 + r * kPwPad + 4 * t4);
-                        xv[r] = *reinterpret_cast<const float4*>(x0 + r * kPwPad + 4 * t4);
-                    }
+                    const float4 gv = *reinterpret_cast<const float4*>(GT + t * kPwRow + 4 * cb);
+                    const float4 xv = *reinterpret_cast<const float4*>(XT + t * kPwRow + 4 * ib);
+                    const float g4[4] = {gv.x, gv.y, gv.z, gv.w}, x4[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
 #pragma unroll
                         for (int c = 0; c < 4; ++c)
-                        {
-                            float v = acc[bl][r * 4 + c];
-                            v = __builtin_fmaf(gv[r].x, xv[c].x, v);
-                            v = __builtin_fmaf(gv[r].y, xv[c].y, v);
-                            v = __builtin_fmaf(gv[r].z, xv[c].z, v);
-                            v = __builtin_fmaf(gv[r].w, xv[c].w, v);
-                            acc[bl][r * 4 + c] = v;
-                        }
+                            acc[bl][r * 4 + c] = __builtin_fmaf(g4[r], x4[c], acc[bl][r * 4 + c]);
                 }
             }
         }
