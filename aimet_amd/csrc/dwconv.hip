@@ -192,13 +192,15 @@ __global__ __launch_bounds__(kBlock) void dw_step_kernel(DwStep a, float* __rest
     {
         float xv[U][KK], tv[U];
         int ih0[U], iw0[U];
+        uint32_t valid[U];   // bit k: tap k inside the plane
 #pragma unroll
         for (int u = 0; u < U; ++u)
         {
             const uint32_t p = pb + u * kBlock;
-            ih0[u] = -(1 << 30);   // an out-of-range position: every tap skipped, nothing added
-            iw0[u] = 0;
-            tv[u]  = 0.0f;
+            ih0[u]   = 0;
+            iw0[u]   = 0;
+            valid[u] = 0;   // an out-of-range position: every tap skipped, nothing added
+            tv[u]    = 0.0f;
 #pragma unroll
             for (int k = 0; k < KK; ++k)
                 xv[u][k] = 0.0f;
@@ -213,18 +215,29 @@ __global__ __launch_bounds__(kBlock) void dw_step_kernel(DwStep a, float* __rest
                 tv[u]  = a.t_cache[plane * s.OH * s.OW + rem];
                 ih0[u] = (int) oh * s.stride - s.pad;
                 iw0[u] = (int) ow * s.stride - s.pad;
+                // branch-free taps: every load reads an in-plane address (clamped) and a tap outside
+                // the plane is dropped by a select on a validity bit, never by control flow (per-tap
+                // branches cost ~300 scalar instructions per 4 positions); the FMAs and their order
+                // are the four-launch chain's
+                uint32_t m = 0;
 #pragma unroll
                 for (int kh = 0; kh < K; ++kh)
                 {
-                    const int ih = ih0[u] + kh * s.dil;
+                    const int ih   = ih0[u] + kh * s.dil;
+                    const bool rin = ih >= 0 && ih < (int) s.H;
+                    const int ihc  = ih < 0 ? 0 : (ih >= (int) s.H ? (int) s.H - 1 : ih);
 #pragma unroll
                     for (int kw = 0; kw < K; ++kw)
                     {
-                        const int iw = iw0[u] + kw * s.dil;
-                        if (ih >= 0 && ih < (int) s.H && iw >= 0 && iw < (int) s.W)
-                            xv[u][kh * K + kw] = xp[ih * (int) s.W + iw];
+                        const int iw  = iw0[u] + kw * s.dil;
+                        const bool ok = rin && iw >= 0 && iw < (int) s.W;
+                        const int iwc = iw < 0 ? 0 : (iw >= (int) s.W ? (int) s.W - 1 : iw);
+                        const float xval = xp[ihc * (int) s.W + iwc];
+                        xv[u][kh * K + kw] = ok ? xval : 0.0f;
+                        m |= (ok ? 1u : 0u) << (kh * K + kw);
                     }
                 }
+                valid[u] = m;
             }
         }
 #pragma unroll
@@ -232,32 +245,21 @@ __global__ __launch_bounds__(kBlock) void dw_step_kernel(DwStep a, float* __rest
         {
             if (pb + u * kBlock >= p1)
                 break;
+            const uint32_t m = valid[u];
             float v = b0;
 #pragma unroll
-            for (int kh = 0; kh < K; ++kh)
+            for (int k = 0; k < KK; ++k)
             {
-                const int ih = ih0[u] + kh * s.dil;
-#pragma unroll
-                for (int kw = 0; kw < K; ++kw)
-                {
-                    const int iw = iw0[u] + kw * s.dil;
-                    if (ih >= 0 && ih < (int) s.H && iw >= 0 && iw < (int) s.W)
-                        v = __builtin_fmaf(wk[kh * K + kw], xv[u][kh * K + kw], v);
-                }
+                const float f = __builtin_fmaf(wk[k], xv[u][k], v);
+                v = (m >> k) & 1u ? f : v;
             }
             // recon_grad_idx_kernel adds the (absent) bias as + 0.0f: the same here
             const float g = recon_g(v + 0.0f, tv[u], a.scale, a.act);
 #pragma unroll
-            for (int kh = 0; kh < K; ++kh)
+            for (int k = 0; k < KK; ++k)
             {
-                const int ih = ih0[u] + kh * s.dil;
-#pragma unroll
-                for (int kw = 0; kw < K; ++kw)
-                {
-                    const int iw = iw0[u] + kw * s.dil;
-                    if (ih >= 0 && ih < (int) s.H && iw >= 0 && iw < (int) s.W)
-                        acc[kh * K + kw] = __builtin_fmaf(g, xv[u][kh * K + kw], acc[kh * K + kw]);
-                }
+                const float f = __builtin_fmaf(g, xv[u][k], acc[k]);
+                acc[k] = (m >> k) & 1u ? f : acc[k];
             }
         }
     }
