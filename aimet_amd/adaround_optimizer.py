@@ -120,13 +120,13 @@ _FUSE_SOFT_WEIGHT = os.environ.get("AIMET_ADA_FUSE_WQ", "1") == "1"
 # (aimet_adaround_dw_step, bit-identical to gather + forward + reconstruction gradient + weight
 # gradient); AIMET_ADA_DW_FUSED=0 runs those four launches instead (tests, measurements)
 _DW_FUSED = os.environ.get("AIMET_ADA_DW_FUSED", "1") == "1"
-# 1x1 layers / the unfolded stem with few channels (Cin, Cout <= 192, Cin * Cout <= 6144, HW % 4 == 0)
+# 1x1 layers / the unfolded stem with few input channels (Cin <= 192, HW % 4 == 0)
 # can run the iteration up to dL/dWq as one pass too (aimet_adaround_pw_step: q, g and the gradient
 # partials on chip; sums in a fixed order, not a library GEMM's). "auto" (default) takes it for every
-# eligible layer except the projecting ones (C_in > C_out) below 56 x 56 positions, where the GEMM
-# form measured faster (MobileNet-v2 per iteration: 0.24 -> 0.16 ms at 16 -> 96 x 112^2, 0.127 ->
-# 0.088 at 24 -> 144 x 56^2, the stem 0.172 -> 0.133; 192 -> 32 x 28^2: 0.074 vs 0.092;
-# profiles/r03/adaround_pw_fused_forms.txt). "all": every eligible layer, "0": none. A fixed rule
+# eligible layer with >= 28 x 28 positions except the projecting ones (C_in > C_out) below 56 x 56,
+# where the GEMM form measured faster (MobileNet-v2 per iteration: 0.24 -> 0.16 ms at 16 -> 96 x
+# 112^2, 0.127 -> 0.088 at 24 -> 144 x 56^2, the stem 0.172 -> 0.133; 192 -> 32 x 28^2: 0.074 vs
+# 0.092; 64 -> 384 x 14^2: 0.064 vs 0.076; profiles/r03/adaround_pw_fused_forms.txt). "all": every eligible layer, "0": none. A fixed rule
 # by shape, so results stay deterministic.
 _PW_FUSED = os.environ.get("AIMET_ADA_PW_FUSED", "auto")
 
@@ -593,8 +593,8 @@ class AdaroundOptimizer:
         pw_dims = None
         if mode in ("pointwise", "im2col") and _PW_FUSED != "0" and _LOOP_FORM != "autograd":
             cin, cout, hw_in = inp_data.shape[1], C_out, inp_data[0, 0].numel()
-            wanted = _PW_FUSED == "all" or not (cin > cout and hw < 56 * 56)
-            if (wanted and cin <= 192 and cout <= 192 and cin * cout <= 6144 and hw_in == hw and hw % 4 == 0
+            wanted = _PW_FUSED == "all" or (hw >= 28 * 28 and not (cin > cout and hw < 56 * 56))
+            if (wanted and cin <= 192 and hw_in == hw and hw % 4 == 0
                     and inp_data.data_ptr() % 16 == 0 and out_data.data_ptr() % 16 == 0 and wq.is_contiguous()):
                 pw_dims = (nb, cin, cout, hw)
                 gw_pw = torch.empty_like(sq.w)

@@ -17,8 +17,10 @@
 //   each workgroup walks tiles blockIdx.x, + gridDim.x, ... and stores its Cout x Cin partial;
 //   a fold adds the partials in workgroup order: deterministic.
 //
-// Sizes: Cin, Cout <= 192, Cin * Cout <= 6144 and at most 512 4 x 4 gradient blocks (two per
-// lane); fp32, NCHW caches with HW = H * W positions per channel plane, HW % 4 == 0.
+// Sizes: Cin <= 192; a workgroup covers R output rows (blockIdx.y: row range) with R * Cin <= 6144
+// and at most 512 4 x 4 gradient blocks (two per lane) -- all of C_out when it fits, else several
+// row ranges, each reading the input tile again; fp32, NCHW caches with HW = H * W positions per
+// channel plane, HW % 4 == 0.
 //
 // Measured (profiles/r03/adaround_pw_fused_forms.txt): faster than the GEMM form on MobileNet-v2's
 // expanding layers and the stem (0.24 -> 0.16 ms per iteration at 16 -> 96 x 112^2), even at
@@ -50,6 +52,7 @@ struct PwStep
     float scale;              // 2 / (N * HW)
     int act;
     uint32_t N, Cin, Cout, HW, tiles_per_sample, tiles;
+    uint32_t R;               // output rows per workgroup row range (blockIdx.y): [y R, y R + R)
 };
 
 // one tile's input quads of this lane: q = threadIdx.x + kBlock k (ci = q / (T / 4), t = 4 (q % (T / 4)));
@@ -89,7 +92,9 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
     __shared__ __attribute__((aligned(16))) float XT[kPwT * kPwRow];
     __shared__ __attribute__((aligned(16))) float GT[kPwT * kPwRow];
     __shared__ __attribute__((aligned(16))) float Ws[kPwPairs + 3 * kPwMaxC];
-    const uint32_t Cin = a.Cin, Cout = a.Cout, pairs = Cin * Cout;
+    // this workgroup's output rows [r0, r0 + Cout) of the layer's a.Cout (blockIdx.y: row range)
+    const uint32_t r0 = blockIdx.y * a.R;
+    const uint32_t Cin = a.Cin, Cout = a.Cout - r0 < a.R ? a.Cout - r0 : a.R, pairs = Cin * a.Cout;
     const uint32_t Cin4 = (Cin + 3) / 4, Cout4 = (Cout + 3) / 4, wrow = 4 * Cin4;
     const int64_t it = a.it_cur[0];
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -98,7 +103,7 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
     for (uint32_t e = threadIdx.x; e < Cout * wrow; e += kBlock)
     {
         const uint32_t co = e / wrow, ci = e - co * wrow;
-        Ws[e] = ci < Cin ? a.w[co * Cin + ci] : 0.0f;
+        Ws[e] = ci < Cin ? a.w[(r0 + co) * Cin + ci] : 0.0f;
     }
     for (uint32_t e = threadIdx.x; e < kPwT * (wrow - Cin); e += kBlock)
         XT[(e / (wrow - Cin)) * kPwRow + Cin + e % (wrow - Cin)] = 0.0f;
@@ -119,7 +124,7 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
         const uint32_t n   = tile / a.tiles_per_sample;
         const uint32_t hw0 = (tile - n * a.tiles_per_sample) * kPwT;
         const bool t_in    = hw0 + 4 * tq < a.HW;   // HW % 4 == 0: the quad is in or out
-        const float* tr    = a.t_cache + (size_t) rows[n] * Cout * a.HW;   // uniform base
+        const float* tr    = a.t_cache + ((size_t) rows[n] * a.Cout + r0) * a.HW;   // uniform base
         __syncthreads();   // the previous tile's XT / GT are consumed (and W / the pads written)
 #pragma unroll
         for (int k = 0; k < kPwQuads; ++k)
@@ -184,7 +189,7 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
             const uint32_t co = cr + 32 * j;
             if (co < Cout)
             {
-                const float bs = a.bias ? a.bias[co] : 0.0f;
+                const float bs = a.bias ? a.bias[r0 + co] : 0.0f;
                 const float tk[4] = {tv[j].x, tv[j].y, tv[j].z, tv[j].w};
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
@@ -229,7 +234,7 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
                 {
                     const uint32_t co = 4 * cb + r, ci = 4 * ib + c;
                     if (co < Cout && ci < Cin)
-                        partial[(size_t) blockIdx.x * pairs + co * Cin + ci] = acc[bl][r * 4 + c];
+                        partial[(size_t) blockIdx.x * pairs + (r0 + co) * Cin + ci] = acc[bl][r * 4 + c];
                 }
         }
     }
@@ -283,6 +288,17 @@ using namespace aimet_amd;
 
 extern "C" {
 
+// output rows per workgroup row range: all of them when they fit (C_out <= 192, C_in C_out <= 6144),
+// else the most that do, a multiple of 4
+static int64_t pw_rows(int64_t Cin, int64_t Cout)
+{
+    int64_t r = kPwPairs / Cin;
+    r         = r > kPwMaxC ? kPwMaxC : r;
+    if (Cout <= r)
+        return Cout;
+    return r - r % 4;
+}
+
 int aimet_adaround_pw_step_workspace(int64_t N, int64_t Cin, int64_t Cout, int64_t HW, int64_t* elems)
 {
     return guarded([&] {
@@ -300,15 +316,13 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
 {
     return guarded([&] {
         AIMET_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && HW > 0, "invalid shape");
-        AIMET_REQUIRE(Cin <= kPwMaxC && Cout <= kPwMaxC && Cin * Cout <= kPwPairs,
-                      "pointwise step: Cin, Cout <= 192 and Cin * Cout <= 6144");
+        AIMET_REQUIRE(Cin <= kPwMaxC, "pointwise step: Cin <= 192");
+        AIMET_REQUIRE(Cout < (int64_t(1) << 24), "pointwise step: too many output channels");
         AIMET_REQUIRE(act >= 0 && act <= 2, "act must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
         AIMET_REQUIRE(N * HW < (int64_t(1) << 31) / kPwT, "batch too large");
         AIMET_REQUIRE(HW % 4 == 0 && (reinterpret_cast<uintptr_t>(x_cache) & 15) == 0 &&
                           (reinterpret_cast<uintptr_t>(target_cache) & 15) == 0,
                       "pointwise step: HW % 4 == 0 and 16-B aligned caches");
-        AIMET_REQUIRE(ceil_div(Cin, (int64_t) 4) * ceil_div(Cout, (int64_t) 4) <= (int64_t) kBlock * kPwBlocks,
-                      "pointwise step: at most 512 4x4 weight-gradient blocks");
         require_device_ptr(x_cache, "x_cache");
         require_device_ptr(target_cache, "target_cache");
         require_device_ptr(idx_all, "idx_all");
@@ -318,9 +332,15 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
         require_device_ptr(grad_w, "grad_w");
         if (bias)
             require_device_ptr(bias, "bias");
-        const int64_t tps   = ceil_div(HW, (int64_t) kPwT);
-        const int64_t tiles = N * tps;
-        const uint32_t grid = pw_grid(tiles);
+        const int64_t R = pw_rows(Cin, Cout);
+        AIMET_REQUIRE(R >= 4 && R * Cin <= kPwPairs && ceil_div(Cin, (int64_t) 4) * ceil_div(R, (int64_t) 4) <=
+                                                            (int64_t) kBlock * kPwBlocks,
+                      "pointwise step: at most 512 4x4 weight-gradient blocks per row range");
+        const int64_t tps    = ceil_div(HW, (int64_t) kPwT);
+        const int64_t tiles  = N * tps;
+        const uint32_t grid  = pw_grid(tiles);
+        const int64_t ranges = ceil_div(Cout, R);
+        AIMET_REQUIRE(ranges <= 65535, "pointwise step: too many row ranges");
         const int64_t pairs = Cin * Cout;
         hipStream_t st      = as_stream(stream);
         if (workspace)
@@ -330,8 +350,8 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
         float* part2 = part + (size_t) grid * pairs;
         PwStep a {x_cache, target_cache, idx_all, it_cur, it_next, w, bias,
                   (float) (2.0 / (double) (N * HW)), act, (uint32_t) N, (uint32_t) Cin, (uint32_t) Cout,
-                  (uint32_t) HW, (uint32_t) tps, (uint32_t) tiles};
-        pw_step_kernel<<<grid, kBlock, 0, st>>>(a, part);
+                  (uint32_t) HW, (uint32_t) tps, (uint32_t) tiles, (uint32_t) R};
+        pw_step_kernel<<<dim3(grid, (unsigned) ranges), kBlock, 0, st>>>(a, part);
         AIMET_LAUNCH_CHECK();
         const uint32_t chunk   = (uint32_t) ceil_div((int64_t) grid, (int64_t) kPwSlices);
         const uint32_t nslices = (uint32_t) ceil_div((int64_t) grid, (int64_t) chunk);

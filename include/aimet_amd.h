@@ -487,7 +487,8 @@ int aimet_adaround_dw_step(const float* x_cache, const float* target_cache, cons
  * sums over ci in order), g = aimet_adaround_recon_grad_indexed's gradient of q + bias (bias
  * nullable; act 0 none, 1 ReLU, 2 ReLU6), grad_w = sum over the batch positions of g x^T in a
  * fixed order (deterministic; fp32, not bit-identical to a library GEMM). it_next_dev[0] = it + 1.
- * Cin, Cout <= 192, Cin * Cout <= 6144, HW % 4 == 0, x_cache 16-B aligned. `workspace`
+ * Cin <= 192 (any Cout: row ranges of at most 6144 / Cin rows per workgroup), HW % 4 == 0, x_cache
+ * and target_cache 16-B aligned. `workspace`
  * (aimet_adaround_pw_step_workspace elements, device) may be null (internal scratch). */
 int aimet_adaround_pw_step_workspace(int64_t N, int64_t Cin, int64_t Cout, int64_t HW, int64_t* elems);
 int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, const int64_t* idx_all_dev,

@@ -1332,7 +1332,10 @@ def test_adaround_dw_step_equals_unfused_chain(N, C, H, K, stride, pad, dil, act
                                                           (32, 32, 192, 28 * 28, 2, True),
                                                           (7, 27, 32, 100, 1, False),
                                                           (5, 3, 5, 12, 2, True),
-                                                          (4, 192, 32, 196, 0, False)])
+                                                          (4, 192, 32, 196, 0, False),
+                                                          (32, 64, 384, 196, 2, True),
+                                                          (6, 96, 576, 196, 1, False),
+                                                          (3, 160, 200, 100, 0, True)])
 def test_adaround_pw_step_vs_torch(N, Cin, Cout, HW, act, with_bias):
     """aimet_adaround_pw_step (a 1x1 layer's AdaRound iteration in one pass over the cached rows)
     == the fp32 torch ops it replaces (index_select, W @ x, the reconstruction-loss gradient, the
