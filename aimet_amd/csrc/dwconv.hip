@@ -132,6 +132,121 @@ __global__ __launch_bounds__(kBlock) void dw_wgrad_kernel(const float* __restric
     }
 }
 
+// ---- quad forms (K = 3, dilation 1, stride 1 (2 instantiated, not taken), OW % 4 == 0) -----------
+// A lane takes 4 consecutive outputs of one row (a quad; OW % 4 == 0 keeps a quad inside its row):
+// their 3 x (3 ST + 3) input window is loaded once (18 or 27 loads for 36 taps), the index
+// divisions are done once per quad, and the weight-gradient partials accumulate quad by quad,
+// output j = 0..3 in order, taps (kh, kw) in order -- in the weight-gradient kernel and in the
+// one-pass step alike, so the two stay bit-identical. Taps outside the plane are dropped by selects.
+template <int ST>
+constexpr int kDwWin = 3 * ST + 3;
+
+template <int ST>
+__device__ __forceinline__ void dw_quad_window(const float* __restrict__ xp, int ih0, int iw0, const DwShape& s,
+                                               float (&xw)[3][kDwWin<ST>], uint32_t& rowv, uint32_t& colv)
+{
+    const int H = (int) s.H, W = (int) s.W;
+    int iwc[kDwWin<ST>];
+    colv = 0;
+#pragma unroll
+    for (int c = 0; c < kDwWin<ST>; ++c)
+    {
+        const int iw = iw0 + c;
+        colv |= (iw >= 0 && iw < W ? 1u : 0u) << c;
+        iwc[c] = iw < 0 ? 0 : (iw >= W ? W - 1 : iw);
+    }
+    rowv = 0;
+#pragma unroll
+    for (int kh = 0; kh < 3; ++kh)
+    {
+        const int ih   = ih0 + kh;
+        const bool rok = ih >= 0 && ih < H;
+        rowv |= (rok ? 1u : 0u) << kh;
+        const float* xr = xp + (ih < 0 ? 0 : (ih >= H ? H - 1 : ih)) * W;
+#pragma unroll
+        for (int c = 0; c < kDwWin<ST>; ++c)
+        {
+            const float v = xr[iwc[c]];
+            xw[kh][c]     = rok && ((colv >> c) & 1u) ? v : 0.0f;
+        }
+    }
+}
+
+// acc[k] += g[j] * tap(j, k) for the quad's outputs j = 0..3 in order (taps outside the plane skipped)
+template <int ST>
+__device__ __forceinline__ void dw_quad_accumulate(const float (&xw)[3][kDwWin<ST>], uint32_t rowv, uint32_t colv,
+                                                   const float (&g)[4], float (&acc)[9])
+{
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+            for (int kw = 0; kw < 3; ++kw)
+            {
+                const int c   = j * ST + kw;
+                const bool ok = ((rowv >> kh) & 1u) && ((colv >> c) & 1u);
+                const float f = __builtin_fmaf(g[j], xw[kh][c], acc[kh * 3 + kw]);
+                acc[kh * 3 + kw] = ok ? f : acc[kh * 3 + kw];
+            }
+}
+
+__device__ __forceinline__ void dw_block_partial(const float (&acc)[9], float* __restrict__ partial, uint32_t c,
+                                                 uint32_t S)
+{
+    __shared__ float sh[9][kBlock / 64];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+    {
+        float v = acc[k];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1)
+            v += __shfl_xor(v, o, 64);
+        if ((threadIdx.x & 63) == 0)
+            sh[k][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 9)
+    {
+        float v = 0.0f;
+#pragma unroll
+        for (int i = 0; i < kBlock / 64; ++i)
+            v += sh[threadIdx.x][i];
+        partial[((size_t) c * S + blockIdx.x) * 9 + threadIdx.x] = v;
+    }
+}
+
+// dw_wgrad_kernel in quads (positions [blockIdx.x * per, ...) of channel c, per % 4 == 0)
+template <int ST>
+__global__ __launch_bounds__(kBlock) void dw_wgrad_quad_kernel(const float* __restrict__ x, const float* __restrict__ gy,
+                                                               float* __restrict__ partial, DwShape s, uint32_t per)
+{
+    const uint32_t c  = blockIdx.y;
+    const uint32_t np = s.N * s.OH * s.OW;
+    const uint32_t p0 = blockIdx.x * per;
+    const uint32_t p1 = p0 + per < np ? p0 + per : np;
+    float acc[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+        acc[k] = 0.0f;
+    for (uint32_t qb = p0 / 4 + threadIdx.x; qb < p1 / 4; qb += kBlock)
+    {
+        const uint32_t p   = 4 * qb;
+        const uint32_t n   = s.div_ohow.div(p);
+        const uint32_t rem = p - n * (s.OH * s.OW);
+        const uint32_t oh  = s.div_ow.div(rem);
+        const uint32_t ow  = rem - oh * s.OW;
+        const size_t plane = (size_t) n * s.C + c;
+        const float4 g4    = *reinterpret_cast<const float4*>(gy + plane * s.OH * s.OW + rem);
+        const float g[4]   = {g4.x, g4.y, g4.z, g4.w};
+        float xw[3][kDwWin<ST>];
+        uint32_t rowv, colv;
+        dw_quad_window<ST>(x + plane * s.H * s.W, (int) oh * ST - s.pad, (int) ow * ST - s.pad, s, xw, rowv, colv);
+        dw_quad_accumulate<ST>(xw, rowv, colv, g, acc);
+    }
+    dw_block_partial(acc, partial, c, gridDim.x);
+}
+
 // The AdaRound iteration of a depthwise layer up to dL/dWq in ONE pass over the batch
 // (aimet_adaround_dw_step). For the positions of dw_wgrad_kernel's slices, sample n's input plane
 // and fp target are read in place from the caches (row idx_all[it][n]); q = dw_fwd_kernel's sum,
@@ -285,6 +400,92 @@ __global__ __launch_bounds__(kBlock) void dw_step_kernel(DwStep a, float* __rest
     }
 }
 
+// aimet_adaround_dw_step in quads: q of the quad's 4 outputs (dw_fwd_kernel's FMA order), their
+// gradients, and dw_wgrad_quad_kernel's accumulation -- bit-identical to gather + dw_fwd_kernel +
+// recon_grad_idx_kernel + dw_wgrad_quad_kernel; 2 quads per lane in flight
+template <int ST>
+__global__ __launch_bounds__(kBlock) void dw_step_quad_kernel(DwStep a, float* __restrict__ partial, DwShape s,
+                                                              uint32_t per)
+{
+    constexpr int U   = 2;
+    const uint32_t c  = blockIdx.y;
+    const uint32_t np = s.N * s.OH * s.OW;
+    const uint32_t p0 = blockIdx.x * per;
+    const uint32_t p1 = p0 + per < np ? p0 + per : np;
+    const int64_t it  = a.it_cur[0];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        a.it_next[0] = it + 1;
+    const int64_t* rows = a.idx_all + it * (int64_t) s.N;
+    __shared__ int64_t srows[kDwStepRows];
+    const bool lds_rows = s.N <= (uint32_t) kDwStepRows;
+    if (lds_rows)
+        for (uint32_t i = threadIdx.x; i < s.N; i += kBlock)
+            srows[i] = rows[i];
+    __syncthreads();
+    float wk[9], acc[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+    {
+        wk[k]  = a.w[c * 9 + k];
+        acc[k] = 0.0f;
+    }
+    const float b0 = a.bias ? a.bias[c] : 0.0f;
+    const uint32_t q1 = p1 / 4;
+    for (uint32_t qbb = p0 / 4 + threadIdx.x; qbb < q1; qbb += kBlock * U)
+    {
+        float xw[U][3][kDwWin<ST>], tq[U][4];
+        uint32_t rowv[U], colv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t qb = qbb + u * kBlock;
+            rowv[u] = colv[u] = 0;
+            if (qb < q1)
+            {
+                const uint32_t p   = 4 * qb;
+                const uint32_t n   = s.div_ohow.div(p);
+                const uint32_t rem = p - n * (s.OH * s.OW);
+                const uint32_t oh  = s.div_ow.div(rem);
+                const uint32_t ow  = rem - oh * s.OW;
+                const size_t plane = (size_t) (lds_rows ? srows[n] : rows[n]) * s.C + c;
+                const float4 t4    = *reinterpret_cast<const float4*>(a.t_cache + plane * s.OH * s.OW + rem);
+                tq[u][0] = t4.x;
+                tq[u][1] = t4.y;
+                tq[u][2] = t4.z;
+                tq[u][3] = t4.w;
+                dw_quad_window<ST>(a.x_cache + plane * s.H * s.W, (int) oh * ST - s.pad, (int) ow * ST - s.pad, s,
+                                   xw[u], rowv[u], colv[u]);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            if (qbb + u * kBlock >= q1)
+                break;
+            float g[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+            {
+                float v = b0;
+#pragma unroll
+                for (int kh = 0; kh < 3; ++kh)
+#pragma unroll
+                    for (int kw = 0; kw < 3; ++kw)
+                    {
+                        const int cc  = j * ST + kw;
+                        const bool ok = ((rowv[u] >> kh) & 1u) && ((colv[u] >> cc) & 1u);
+                        const float f = __builtin_fmaf(wk[kh * 3 + kw], xw[u][kh][cc], v);
+                        v = ok ? f : v;
+                    }
+                // recon_grad_idx_kernel adds the (absent) bias as + 0.0f: the same here
+                g[j] = recon_g(v + 0.0f, tq[u][j], a.scale, a.act);
+            }
+            dw_quad_accumulate<ST>(xw[u], rowv[u], colv[u], g, acc);
+        }
+    }
+    dw_block_partial(acc, partial, c, gridDim.x);
+}
+
 __global__ __launch_bounds__(kBlock) void dw_wgrad_fold(const float* __restrict__ partial, float* __restrict__ gw,
                                                         uint32_t C, uint32_t S, uint32_t KK)
 {
@@ -299,7 +500,20 @@ __global__ __launch_bounds__(kBlock) void dw_wgrad_fold(const float* __restrict_
 }
 
 // slices of >= 16 positions per lane, and enough workgroups (~2048) to fill the chip
-int64_t wgrad_slices(int64_t N, int64_t C, int64_t OH, int64_t OW, uint32_t* per_out)
+inline bool aligned16(const void* p)
+{
+    return (reinterpret_cast<uintptr_t>(p) & 15) == 0;
+}
+
+// the quad forms apply (dw_wgrad_quad_kernel, dw_step_quad_kernel)
+// (stride 2 measured slower in quads: 84 -> 125 us on 96 channels at 112^2, profiles/r03/dw_step_tune.jsonl;
+// the kernels keep the stride-2 instantiation for that comparison)
+bool dw_quads(int64_t K, int64_t stride, int64_t dil, int64_t OW)
+{
+    return K == 3 && dil == 1 && stride == 1 && OW % 4 == 0;
+}
+
+int64_t wgrad_slices(int64_t N, int64_t C, int64_t OH, int64_t OW, uint32_t* per_out, bool quads = false)
 {
     const int64_t np   = N * OH * OW;
     // positions per lane per slice (16; AIMET_TUNE_DW_PER: tuning experiments only -- it changes the
@@ -315,7 +529,9 @@ int64_t wgrad_slices(int64_t N, int64_t C, int64_t OH, int64_t OW, uint32_t* per
         S = want < ceil_div(np, kBlock) ? want : ceil_div(np, kBlock);
     if (S < 1)
         S = 1;
-    const uint32_t per = (uint32_t) ceil_div(np, S);
+    uint32_t per = (uint32_t) ceil_div(np, S);
+    if (quads)
+        per = (per + 3) / 4 * 4;   // slices of whole quads (np % 4 == 0 when OW % 4 == 0)
     if (per_out)
         *per_out = per;
     return ceil_div(np, per);
@@ -376,8 +592,9 @@ void dw_grad_weight(const float* x, const float* grad_y, float* grad_w, float* w
     require_device_ptr(grad_y, "grad_y");
     require_device_ptr(grad_w, "grad_w");
     AIMET_REQUIRE(C <= 65535, "depthwise weight gradient: at most 65535 channels");
-    uint32_t per    = 0;
-    const int64_t S = wgrad_slices(N, C, OH, OW, &per);
+    uint32_t per      = 0;
+    const bool quads  = dw_quads(K, stride, dilation, OW) && aligned16(grad_y);
+    const int64_t S   = wgrad_slices(N, C, OH, OW, &per, quads);
     // a caller-owned workspace (aimet_dwconv2d_grad_weight_workspace elements) keeps the call
     // free of allocations, e.g. inside a HIP-graph capture
     if (workspace)
@@ -385,7 +602,11 @@ void dw_grad_weight(const float* x, const float* grad_y, float* grad_w, float* w
     float* partial = workspace ? workspace
                                : static_cast<float*>(scratch_alloc(sizeof(float) * (size_t) (C * S * K * K), st));
     dim3 grid((unsigned) S, (unsigned) C);
-    if (K == 3)
+    if (quads && stride == 1)
+        dw_wgrad_quad_kernel<1><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per);
+    else if (quads)
+        dw_wgrad_quad_kernel<2><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per);
+    else if (K == 3)
         dw_wgrad_kernel<3><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per);
     else
         dw_wgrad_kernel<5><<<grid, kBlock, 0, st>>>(x, grad_y, partial, s, per);
@@ -414,8 +635,11 @@ void dw_step(const float* x_cache, const float* t_cache, const int64_t* idx_all,
     require_device_ptr(grad_w, "grad_w");
     if (bias)
         require_device_ptr(bias, "bias");
-    uint32_t per    = 0;
-    const int64_t S = wgrad_slices(N, C, OH, OW, &per);
+    uint32_t per     = 0;
+    // the quad form exactly when aimet_dwconv2d_grad_weight takes it (the gradient's buffer there
+    // is a 16-B aligned torch / scratch allocation; the target cache here is checked)
+    const bool quads = dw_quads(K, stride, dilation, OW) && aligned16(t_cache);
+    const int64_t S  = wgrad_slices(N, C, OH, OW, &per, quads);
     if (workspace)
         require_device_ptr(workspace, "workspace");
     float* partial = workspace ? workspace
@@ -427,7 +651,11 @@ void dw_step(const float* x_cache, const float* t_cache, const int64_t* idx_all,
         const char* e = getenv("AIMET_TUNE_DW_U");   // tuning experiments only (same results)
         return e ? atoi(e) : 0;
     }();
-    if (K == 3 && u == 1)
+    if (quads && stride == 1)
+        dw_step_quad_kernel<1><<<grid, kBlock, 0, st>>>(a, partial, s, per);
+    else if (quads)
+        dw_step_quad_kernel<2><<<grid, kBlock, 0, st>>>(a, partial, s, per);
+    else if (K == 3 && u == 1)
         dw_step_kernel<3, 1><<<grid, kBlock, 0, st>>>(a, partial, s, per);
     else if (K == 3 && u == 2)
         dw_step_kernel<3, 2><<<grid, kBlock, 0, st>>>(a, partial, s, per);
