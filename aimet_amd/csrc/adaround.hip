@@ -888,7 +888,10 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
         AdaParams p {(float) ((1ull << bw) - 1), 0.0f, 0.0f, 0.0f, 1, (uint32_t) (n - n % 32), round_loss != nullptr};
         AdamArgs a {lr, beta1, beta2, eps};
-        const bool vec = (C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) &&
+        // 4 elements per lane only for weights large enough to fill the chip that way: the per-element
+        // chain (sigmoid, Sleef pow, Adam) is long, and a small layer's step is latency-bound, so
+        // it takes one element per lane (4x the lanes; the same arithmetic per element)
+        const bool vec = n >= (int64_t(1) << 18) && (C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) &&
                          aligned16(grad_wq) && aligned16(exp_avg) && aligned16(exp_avg_sq) &&
                          (wq_next == nullptr || aligned16(wq_next));
         const int64_t items = vec ? n / 4 : n;
