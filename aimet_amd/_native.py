@@ -174,6 +174,8 @@ _PROTOTYPES = {
     "aimet_dwconv2d_grad_weight": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                                    _vp],
     "aimet_adaround_gather": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
+    "aimet_adaround_gather_cm": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp],
+    "aimet_adaround_recon_grad_indexed_cm": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp],
     "aimet_adaround_recon_grad_indexed": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _int, _vp],
     "aimet_adaround_backward_adam": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp, _vp,
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _vp,

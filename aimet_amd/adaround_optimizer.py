@@ -129,6 +129,12 @@ _DW_FUSED = os.environ.get("AIMET_ADA_DW_FUSED", "1") == "1"
 # 0.092; 64 -> 384 x 14^2: 0.064 vs 0.076; profiles/r03/adaround_pw_fused_forms.txt). "all": every eligible layer, "0": none. A fixed rule
 # by shape, so results stay deterministic.
 _PW_FUSED = os.environ.get("AIMET_ADA_PW_FUSED", "auto")
+# the GEMM form of 1x1 layers with channel-major batches (aimet_adaround_gather_cm: x as [C_in][nb hw],
+# so q = W x and dL/dW = g x^T are ONE GEMM each, no per-sample GEMMs, batch sum or transposes), for
+# layers of <= 14 x 14 positions (MobileNet-v2: 0.117 -> 0.063 ms per iteration at 576 -> 96 x 14^2;
+# slower at 28^2: 0.071 -> 0.09); AIMET_ADA_PW_CM=0: the [nb][C][hw] batches with per-sample GEMMs
+# (AIMET_ADA_PW_GRAD) everywhere
+_PW_CM = os.environ.get("AIMET_ADA_PW_CM", "1") == "1"
 
 
 def _is_pointwise(module: torch.nn.Module) -> bool:
@@ -590,7 +596,7 @@ class AdaroundOptimizer:
             ws = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
             dims = (Nb, C, H, W, out_shape[1], out_shape[2], K, stride, pad, dil)
         pbias = P(bias) if bias is not None else None
-        pw_dims = None
+        pw_dims, cm = None, None
         if mode in ("pointwise", "im2col") and _PW_FUSED != "0" and _LOOP_FORM != "autograd":
             cin, cout, hw_in = inp_data.shape[1], C_out, inp_data[0, 0].numel()
             wanted = _PW_FUSED == "all" or (hw >= 28 * 28 and not (cin > cout and hw < 56 * 56))
@@ -601,6 +607,12 @@ class AdaroundOptimizer:
                 ws_n = ctypes.c_int64()
                 _native.check(lib.aimet_adaround_pw_step_workspace(*pw_dims, ctypes.byref(ws_n)))
                 ws_pw = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
+        if (mode in ("pointwise", "im2col") and pw_dims is None and _PW_CM and hw <= 14 * 14
+                and inp_data[0].numel() % hw == 0):
+            cin_cm = inp_data[0].numel() // hw
+            x_cm = torch.empty((cin_cm, nb * hw), dtype=torch.float32, device=dev)
+            q_cm = torch.empty((C_out, nb * hw), dtype=torch.float32, device=dev)
+            cm = (cin_cm, x_cm, q_cm, torch.empty_like(q_cm))
 
         def recon(q, with_bias, s):
             _native.check(lib.aimet_adaround_recon_grad_indexed(P(q), P(out_data), P(idx_all), it_cur, P(g_buf), nb,
@@ -634,6 +646,17 @@ class AdaroundOptimizer:
                 _native.check(lib.aimet_adaround_pw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
                                                          P(wq), pbias, P(gw_pw), P(ws_pw), *pw_dims, code, s))
                 adam_step(gw_pw, s)
+                return
+            if mode in ("pointwise", "im2col") and cm is not None:
+                # channel-major batch: one GEMM per direction over all nb * hw positions
+                cin_cm, x_cm, q_cm, g_cm = cm
+                _native.check(lib.aimet_adaround_gather_cm(P(inp_data), P(x_cm), P(idx_all), it_cur, it_next, nb,
+                                                           cin_cm, hw, s))
+                w2 = wq.detach().view(wq.shape[0], -1)
+                torch.mm(w2, x_cm, out=q_cm)
+                _native.check(lib.aimet_adaround_recon_grad_indexed_cm(P(q_cm), P(out_data), P(idx_all), it_cur,
+                                                                       P(g_cm), nb, C_out, hw, pbias, code, s))
+                adam_step(torch.mm(g_cm, x_cm.t()).view_as(wq), s)
                 return
             _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp),
                                                     None if indexed else P(target), P(idx_all), it_cur, it_next, nb,
@@ -740,7 +763,8 @@ class AdaroundOptimizer:
             else:
                 del g
         _, mode, graph = best
-        AdaroundOptimizer.last_loop_form = mode + ("_fused" if mode in ("pointwise", "im2col") and pw_dims else "")
+        AdaroundOptimizer.last_loop_form = mode + ("_fused" if mode in ("pointwise", "im2col") and pw_dims else
+                                                   "_cm" if mode in ("pointwise", "im2col") and cm else "")
         for a in range(0, iters, chunk):
             b = min(a + chunk, iters)
             if b < iters:

@@ -630,6 +630,45 @@ __device__ __forceinline__ float recon_bias(const ReconIdx& r, uint32_t e_in_row
     return r.bias[ch - r.div_c.div(ch) * (uint32_t) r.C];
 }
 
+// Channel-major batches of a 1x1 layer's GEMM form: x_cm[ci][b][hw] = src_in[idx[it][b]][ci][hw]
+// (one GEMM over all positions then gives q_cm[co][b][hw] and the weight gradient
+// g_cm[co][(b, hw)] x_cm[ci][(b, hw)]^T, no per-sample GEMMs and no batch sum); blockIdx.y = ci * nb + b;
+// workgroup (0, 0) sets it_next = it + 1
+__global__ __launch_bounds__(kBlock) void adaround_gather_cm_kernel(const float* __restrict__ src_in,
+                                                                    float* __restrict__ dst,
+                                                                    const int64_t* __restrict__ idx_all,
+                                                                    const int64_t* __restrict__ it_cur,
+                                                                    int64_t* __restrict__ it_next, uint32_t nb,
+                                                                    uint32_t Cin, uint32_t hw)
+{
+    const int64_t it = it_cur[0];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        it_next[0] = it + 1;
+    const uint32_t ci = blockIdx.y / nb, b = blockIdx.y - ci * nb;
+    const float* src  = src_in + ((size_t) idx_all[it * nb + b] * Cin + ci) * hw;
+    float* d          = dst + (size_t) blockIdx.y * hw;
+    for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < hw; t += gridDim.x * kBlock)
+        d[t] = __builtin_nontemporal_load(src + t);
+}
+
+// recon_grad_idx_kernel for channel-major q / g ([C][nb][hw]): element i = (co nb + b) hw + t reads
+// the target out_data[idx[it][b]][co][t]; bias added first as there
+__global__ __launch_bounds__(kBlock) void recon_grad_idx_cm_kernel(const float* __restrict__ q, float* __restrict__ g,
+                                                                   ReconIdx r, float scale, int act)
+{
+    const int64_t it   = r.it_cur[0];
+    const uint32_t n   = (uint32_t) (r.C * r.nb * r.hw);
+    const uint32_t i   = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n)
+        return;
+    const uint32_t row = r.div_hw.div(i);   // co * nb + b
+    const uint32_t t   = i - row * (uint32_t) r.hw;
+    const uint32_t co  = r.div_c.div(row);   // div_c holds nb here
+    const uint32_t b   = row - co * (uint32_t) r.nb;
+    const float tv     = r.out_data[((size_t) r.idx_all[it * r.nb + b] * r.C + co) * r.hw + t];
+    g[i] = recon_g(q[i] + (r.bias ? r.bias[co] : 0.0f), tv, scale, act);
+}
+
 template <bool VEC>
 __global__ __launch_bounds__(kBlock) void recon_grad_idx_kernel(const float* __restrict__ q, float* __restrict__ g,
                                                                 ReconIdx r, float scale, int act)
@@ -859,6 +898,50 @@ int aimet_adaround_recon_grad_indexed(const float* q, const float* out_data, con
             recon_grad_idx_kernel<true><<<(unsigned) ceil_div(n / 4, kBlock), kBlock, 0, s>>>(q, g, r, scale, act);
         else
             recon_grad_idx_kernel<false><<<(unsigned) ceil_div(n, kBlock), kBlock, 0, s>>>(q, g, r, scale, act);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_adaround_gather_cm(const float* src_in, float* dst, const int64_t* idx_all, const int64_t* it_cur,
+                             int64_t* it_next, int64_t nb, int64_t Cin, int64_t hw, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(nb > 0 && Cin > 0 && hw > 0, "invalid shape");
+        AIMET_REQUIRE(Cin * nb <= 65535 && Cin * nb * hw < (int64_t(1) << 31), "batch too large for the channel-major gather");
+        require_device_ptr(src_in, "src_in");
+        require_device_ptr(dst, "dst");
+        require_device_ptr(idx_all, "idx_all");
+        require_device_ptr(it_cur, "it_cur");
+        require_device_ptr(it_next, "it_next");
+        int64_t bx = ceil_div(hw, (int64_t) kBlock);
+        bx         = bx > 64 ? 64 : bx;
+        adaround_gather_cm_kernel<<<dim3((unsigned) bx, (unsigned) (Cin * nb)), kBlock, 0, as_stream(stream)>>>(
+            src_in, dst, idx_all, it_cur, it_next, (uint32_t) nb, (uint32_t) Cin, (uint32_t) hw);
+        AIMET_LAUNCH_CHECK();
+    });
+}
+
+int aimet_adaround_recon_grad_indexed_cm(const float* q, const float* out_data, const int64_t* idx_all,
+                                         const int64_t* it_cur, float* g, int64_t nb, int64_t C, int64_t hw,
+                                         const float* bias, int act, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(nb > 0 && C > 0 && hw > 0, "invalid shape");
+        AIMET_REQUIRE(act >= 0 && act <= 2, "act must be 0 (none), 1 (ReLU) or 2 (ReLU6)");
+        const int64_t n = nb * C * hw;
+        AIMET_REQUIRE(n < (int64_t(1) << 31), "batch too large (>= 2^31 elements)");
+        require_device_ptr(q, "quant_out");
+        require_device_ptr(out_data, "out_data");
+        require_device_ptr(idx_all, "idx_all");
+        require_device_ptr(it_cur, "it_cur");
+        require_device_ptr(g, "grad");
+        if (bias)
+            require_device_ptr(bias, "bias");
+        const float scale = (float) (2.0 / (double) (nb * hw));   // as aimet_adaround_recon_grad_indexed
+        ReconIdx r {out_data, idx_all, it_cur, bias, nb, C * hw, hw, C,
+                    FastDiv((uint32_t) (C * hw)), FastDiv((uint32_t) hw), FastDiv((uint32_t) nb)};
+        recon_grad_idx_cm_kernel<<<(unsigned) ceil_div(n, (int64_t) kBlock), kBlock, 0, as_stream(stream)>>>(q, g, r,
+                                                                                                     scale, act);
         AIMET_LAUNCH_CHECK();
     });
 }

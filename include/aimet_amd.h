@@ -439,6 +439,16 @@ int aimet_adaround_gather(const float* src_in, const float* src_out, float* dst_
 int aimet_adaround_recon_grad_indexed(const float* quant_out, const float* out_data, const int64_t* idx_all_dev,
                                       const int64_t* it_cur_dev, float* grad, int64_t nb, int64_t C, int64_t hw,
                                       const float* bias_dev, int act, void* stream);
+/* Channel-major forms for a 1x1 layer's GEMM loop: aimet_adaround_gather_cm writes the batch's
+ * inputs as dst[ci][b][hw] (rows idx_all_dev[it * nb + b] of src_in [N][Cin][hw]; it_next_dev[0] =
+ * it + 1), so q = W x and dL/dW = g x^T are single GEMMs over all nb * hw positions;
+ * aimet_adaround_recon_grad_indexed_cm is aimet_adaround_recon_grad_indexed for q / grad in the
+ * [C][nb][hw] layout (targets read in place from out_data [N][C][hw]). */
+int aimet_adaround_gather_cm(const float* src_in, float* dst, const int64_t* idx_all_dev, const int64_t* it_cur_dev,
+                             int64_t* it_next_dev, int64_t nb, int64_t Cin, int64_t hw, void* stream);
+int aimet_adaround_recon_grad_indexed_cm(const float* quant_out, const float* out_data, const int64_t* idx_all_dev,
+                                         const int64_t* it_cur_dev, float* grad, int64_t nb, int64_t C, int64_t hw,
+                                         const float* bias_dev, int act, void* stream);
 /* aimet_adaround_backward + torch.optim.Adam(fused=True)'s update of alpha (no weight decay /
  * amsgrad) in one pass, for the same replayed iteration: step = it_next_dev[0] (1-based),
  * {reg, beta, beta - 1} = reg_beta_all_dev[3 * (step - 1) ..] (float32), alpha / exp_avg /

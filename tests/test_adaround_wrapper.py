@@ -188,7 +188,7 @@ def test_activation_sampler_concatenates_batches():
 
 @pytest.mark.gpu
 @gpu
-@pytest.mark.parametrize("kind", ["stem", "dw", "pointwise", "linear"])
+@pytest.mark.parametrize("kind", ["stem", "dw", "pointwise", "pointwise_wide", "linear"])
 def test_adaround_loop_deterministic(kind):
     """Two runs of the fused loop with one seed give bit-identical alpha, for every loop form
     (MIOpen through autograd, native depthwise, GEMM pointwise / linear): the form is a fixed rule
@@ -201,6 +201,8 @@ def test_adaround_loop_deterministic(kind):
         m, shape_in = nn.Conv2d(16, 16, 3, padding=1, groups=16), (64, 16, 14, 14)
     elif kind == "pointwise":
         m, shape_in = nn.Conv2d(16, 48, 1), (64, 16, 14, 14)
+    elif kind == "pointwise_wide":   # MobileNet-v2's 14x14 projection: the channel-major GEMM form
+        m, shape_in = nn.Conv2d(576, 96, 1), (64, 576, 14, 14)
     else:
         m, shape_in = nn.Linear(96, 40), (64, 96)
     m = m.to(DEV)
@@ -262,6 +264,6 @@ def test_adaround_pw_fused_loop_deterministic_and_close_to_gemm_form(monkeypatch
         return a, ao.AdaroundOptimizer.last_loop_form
 
     (a1, f1), (a2, _), (g, fg) = run("all"), run("all"), run("0")
-    assert (f1, fg) == ("pointwise_fused", "pointwise")
+    assert (f1, fg) == ("pointwise_fused", "pointwise")   # 16 x 16 positions: the per-sample GEMM form
     assert torch.equal(a1, a2)
     torch.testing.assert_close(a1, g, rtol=1e-5, atol=1e-5)
