@@ -16,6 +16,7 @@ import array
 import ctypes
 import gc
 import itertools
+import os
 
 import torch
 
@@ -24,6 +25,8 @@ from aimet_amd._native import TfEncodingC
 from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding, encodings_to_c
 
 _seed_counter = itertools.count(1)
+# calibrateResidentAsync: activations and parameters in two native calls (AIMET_CAL_SPLIT=0: one)
+_CAL_SPLIT = os.environ.get("AIMET_CAL_SPLIT", "1") != "0"
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -434,7 +437,9 @@ class AimetTensorQuantizer:
     def calibrateResidentAsync(act_quantizers, activations, param_quantizers, params, param_ch_axes=None,
                                act_settings=(8, False, False, False), param_settings=(8, True, False, False),
                                reset=False, main_stream=None, side_stream=None):
-        """One calibration batch in ONE native call (aimet_calibrate_launch): optionally
+        """One calibration batch in two native calls (aimet_calibrate_launch; one when `side_stream`
+        is `main_stream` or AIMET_CAL_SPLIT=0): the activations' call first, so their min/max pass
+        runs while the parameters' call is prepared. Optionally
         resetEncodingStats of every quantizer, the activations' statistics (one launch per phase for
         all per-tensor quantizers) + search on `main_stream`, the parameters' per-channel statistics
         + search on `side_stream` (after everything queued on main so far). Returns
@@ -459,6 +464,31 @@ class AimetTensorQuantizer:
             keep.append(t)
             a_ptr.append(t.data_ptr())
             a_n.append(t.numel())
+        main = main_stream if main_stream is not None else torch.cuda.current_stream(dev)
+        side = side_stream if side_stream is not None else main
+        if reset:
+            for q in aq + pq:
+                q._pending_percentile = None
+        na, np_ = len(aq), len(pq)
+        i32x4 = ctypes.c_int32 * 4
+        a_set, p_set = i32x4(*[int(v) for v in act_settings]), i32x4(*[int(v) for v in param_settings])
+        split = _CAL_SPLIT and na > 0 and np_ > 0 and side is not main
+        ra, rp = ctypes.c_void_p(), ctypes.c_void_p()
+        if split:
+            # two native calls: the activations' HBM passes are enqueued before the parameters'
+            # host preparation runs, which then overlaps the min/max pass instead of delaying it.
+            # The side stream starts after the inputs (everything on `main` so far); the first
+            # call resets the activation quantizers there, the second adds the parameters' work.
+            side.wait_stream(main)
+            ha = AimetTensorQuantizer._ensure_many(aq, dev)
+            nul = ctypes.c_void_p * 1
+            with torch.cuda.device(dev):
+                _native.call("aimet_calibrate_launch", (ctypes.c_void_p * na)(*ha), (ctypes.c_void_p * na)(*a_ptr),
+                             (ctypes.c_int64 * na)(*a_n), na, nul(), nul(), (ctypes.c_int64 * 1)(),
+                             (ctypes.c_int64 * 1)(), (ctypes.c_int64 * 1)(), 0, a_set, p_set, int(bool(reset)),
+                             main.cuda_stream, side.cuda_stream, ctypes.byref(ra), ctypes.byref(ctypes.c_void_p()))
+            for q in aq:
+                q._is_encoding_valid = True
         p_ptr, outers, Cs, Ks = [], [], [], []
         views = _PER_CHANNEL_VIEWS
         for q, t, ax in zip(pq, params, ch_axes):
@@ -480,25 +510,33 @@ class AimetTensorQuantizer:
             outers.append(outer)
             Cs.append(C)
             Ks.append(K)
-        handles = AimetTensorQuantizer._ensure_many(aq + pq, dev)
-        if reset:
+        if split:
+            hp = AimetTensorQuantizer._ensure_many(pq, dev)
+            nul, empty = ctypes.c_void_p * 1, ctypes.c_void_p()
+            with torch.cuda.device(dev):
+                # the parameters alone, every operation on the side stream; the main stream then
+                # waits for it (later work there sees the parameters' state, as in one call)
+                _native.call("aimet_calibrate_launch", nul(), nul(), (ctypes.c_int64 * 1)(), 0,
+                             (ctypes.c_void_p * np_)(*hp), (ctypes.c_void_p * np_)(*p_ptr),
+                             (ctypes.c_int64 * np_)(*outers), (ctypes.c_int64 * np_)(*Cs),
+                             (ctypes.c_int64 * np_)(*Ks), np_, a_set, p_set, int(bool(reset)),
+                             side.cuda_stream, side.cuda_stream, ctypes.byref(empty), ctypes.byref(rp))
+            main.wait_stream(side)
+            if empty.value:   # the second call's (empty) activation request
+                _native.call("aimet_tq_get_encodings_finish", empty, None, None)
+            for q in pq:
+                q._is_encoding_valid = True
+        else:
+            handles = AimetTensorQuantizer._ensure_many(aq + pq, dev)
+            with torch.cuda.device(dev):
+                _native.call("aimet_calibrate_launch", (ctypes.c_void_p * max(na, 1))(*handles[:na]),
+                             (ctypes.c_void_p * max(na, 1))(*a_ptr), (ctypes.c_int64 * max(na, 1))(*a_n), na,
+                             (ctypes.c_void_p * max(np_, 1))(*handles[na:]), (ctypes.c_void_p * max(np_, 1))(*p_ptr),
+                             (ctypes.c_int64 * max(np_, 1))(*outers), (ctypes.c_int64 * max(np_, 1))(*Cs),
+                             (ctypes.c_int64 * max(np_, 1))(*Ks), np_, a_set, p_set, int(bool(reset)),
+                             main.cuda_stream, side.cuda_stream, ctypes.byref(ra), ctypes.byref(rp))
             for q in aq + pq:
-                q._pending_percentile = None
-        na, np_ = len(aq), len(pq)
-        ra, rp = ctypes.c_void_p(), ctypes.c_void_p()
-        main = main_stream if main_stream is not None else torch.cuda.current_stream(dev)
-        side = side_stream if side_stream is not None else main
-        with torch.cuda.device(dev):
-            _native.call("aimet_calibrate_launch", (ctypes.c_void_p * max(na, 1))(*handles[:na]),
-                         (ctypes.c_void_p * max(na, 1))(*a_ptr), (ctypes.c_int64 * max(na, 1))(*a_n), na,
-                         (ctypes.c_void_p * max(np_, 1))(*handles[na:]), (ctypes.c_void_p * max(np_, 1))(*p_ptr),
-                         (ctypes.c_int64 * max(np_, 1))(*outers), (ctypes.c_int64 * max(np_, 1))(*Cs),
-                         (ctypes.c_int64 * max(np_, 1))(*Ks), np_,
-                         (ctypes.c_int32 * 4)(*[int(v) for v in act_settings]),
-                         (ctypes.c_int32 * 4)(*[int(v) for v in param_settings]), int(bool(reset)),
-                         main.cuda_stream, side.cuda_stream, ctypes.byref(ra), ctypes.byref(rp))
-        for q in aq + pq:
-            q._is_encoding_valid = True
+                q._is_encoding_valid = True
         return (PendingEncodings(aq, *act_settings, request=ra), PendingEncodings(pq, *param_settings, request=rp),
                 keep)
 

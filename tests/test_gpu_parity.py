@@ -1522,7 +1522,8 @@ def test_reset_of_quantizers_bound_to_exchange_buffers():
 
 @pytest.mark.parametrize("schemes", ["tfe", "mixed"])
 def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatch):
-    """compute_encodings_resident's one native call (aimet_calibrate_launch, reset folded in) ==
+    """compute_encodings_resident's native calls (aimet_calibrate_launch, reset folded in; the
+    activations' and the parameters' calls apart, and both in one call) ==
     the phase-by-phase path from Python (resetEncodingStatsMany + per-phase *_many launches + the
     two requests), on quantizers that already hold the previous batch's statistics; and a second
     reset + recompute of the same data == the first (nothing of the earlier batch survives)."""
@@ -1542,10 +1543,13 @@ def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatc
                   for c, k in ((64, 27), (128, 576), (10, 2048))]
         return acts, params
 
+    from aimet_amd import tensor_quantizer
     old, new_ = batch(3.0), batch(1.0)
     results = []
-    for native in (True, False):
+    # two native calls (activations, then parameters), one native call, the phased path
+    for native, split in ((True, True), (True, False), (False, False)):
         monkeypatch.setattr(calibration, "_SCHEDULE", "params_first" if native else "params_first_phased")
+        monkeypatch.setattr(tensor_quantizer, "_CAL_SPLIT", split)
         aq = [AimetTensorQuantizer(m) for m in a_modes]
         pq = [AimetTensorQuantizer(m, num_channels=p.shape[0]) for m, p in zip(p_modes, new_[1])]
         compute_encodings_resident(aq, old[0], pq, old[1])                 # earlier statistics
@@ -1555,7 +1559,7 @@ def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatc
                           [[x.to_tuple() for x in (es if isinstance(es, list) else [es])] for es, _ in r[1]])
         assert flat(r1) == flat(r2)
         results.append(flat(r1))
-    assert results[0] == results[1]
+    assert results[0] == results[1] == results[2]
     # and == fresh quantizers fed only the new batch
     fa = [AimetTensorQuantizer(m) for m in a_modes]
     fp = [AimetTensorQuantizer(m, num_channels=p.shape[0]) for m, p in zip(p_modes, new_[1])]
