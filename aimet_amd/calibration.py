@@ -62,8 +62,9 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
     reset=True: resetEncodingStats of every quantizer first (QuantizationSimModel.compute_encodings
     on quantizers that already hold statistics, v1/quantsim.py:387-399).
 
-    On one rank, with AimetTensorQuantizers and float32 tensors, all of it is ONE native call
-    (aimet_calibrate_launch: about a dozen HIP launches from C++, no Python per phase); otherwise
+    On one rank, with AimetTensorQuantizers and float32 tensors, all of it is two native calls
+    (aimet_calibrate_launch for the activations, then for the parameters while the activations'
+    min/max pass runs: about a dozen HIP launches from C++, no Python per phase); otherwise
     the phases are enqueued from here (sharded with collectives when `group` spans several ranks)."""
     if not activations and not params:
         if reset:
