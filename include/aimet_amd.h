@@ -281,7 +281,12 @@ int aimet_tq_get_encodings_finish(aimet_encoding_request* request, aimet_tf_enco
  * all of them + one search launch. Parameters (per channel of [outer][C][K]) first, on
  * `side_stream` (which waits for `main_stream`; `main_stream` then waits for it) or, when the two
  * are the same stream, ahead of the activations on it: two statistics launches + one search launch. act_settings / par_settings = {bw, symmetric, strict, unsigned}. The two
- * requests are finished (and freed) with aimet_tq_get_encodings_finish; on error neither exists. */
+ * requests are finished (and freed) with aimet_tq_get_encodings_finish; on error neither exists.
+ * Either count may be 0. aimet_amd's Python host issues two calls per batch: the activations
+ * (n_par = 0; *par_req is then null) with the side stream already waiting for the inputs, then the
+ * parameters (n_act = 0, both streams the side stream; *act_req is an empty request, finished like
+ * any other), after which the main stream waits for the side stream -- the parameters' host
+ * preparation then overlaps the activations' min/max pass. */
 int aimet_calibrate_launch(aimet_tensor_quantizer* const* act_qs, const float* const* act_x, const int64_t* act_n,
                            int64_t n_act, aimet_tensor_quantizer* const* par_qs, const float* const* par_x,
                            const int64_t* par_outer, const int64_t* par_C, const int64_t* par_K, int64_t n_par,
