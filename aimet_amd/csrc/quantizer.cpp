@@ -1125,7 +1125,18 @@ int aimet_tq_get_encodings_finish(aimet_encoding_request* req, aimet_tf_encoding
     const int rc = guarded([&] {
         AIMET_REQUIRE(req != nullptr, "request is null");
         const int64_t nq = (int64_t) req->qs.size();
-        int64_t total    = 0;
+        if (out == nullptr && valid == nullptr)
+        {
+            // discard: the request's result copy may still be writing into its pinned block, which
+            // goes back to the pool below -- wait for the request's device work first
+            if (nq && req->done)
+            {
+                DeviceGuard g(req->device);
+                AIMET_HIP_CHECK(hipEventSynchronize(req->done));
+            }
+            return;
+        }
+        int64_t total = 0;
         for (aimet_tensor_quantizer* q: req->qs)
             total += q->C;
         AIMET_REQUIRE(out != nullptr || total == 0, "out is null");
@@ -1156,13 +1167,18 @@ int aimet_tq_get_encodings_finish(aimet_encoding_request* req, aimet_tf_encoding
         collect_encodings(host_q.data(), host_out.data(), (int64_t) host_q.size(), req->b, req->sym, req->strict,
                           req->unsign);
     });
-    release_request(req);
+    if (rc != AIMET_OK)
+        release_request_after_error(req);   // the copy may not have been waited for
+    else
+        release_request(req);
     return rc;
 }
 
 int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym, int strict,
                            int unsign, aimet_tf_encoding* out, int* valid, void* stream)
 {
+    if (out == nullptr && valid == nullptr && nq > 0)
+        return guarded([] { AIMET_REQUIRE(false, "out is null"); });   // not a discard here
     aimet_encoding_request* req = nullptr;
     const int rc = aimet_tq_get_encodings_launch(qs, nq, bw, sym, strict, unsign, stream, &req);
     if (rc != AIMET_OK)

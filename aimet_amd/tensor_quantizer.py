@@ -489,44 +489,29 @@ class AimetTensorQuantizer:
                              main.cuda_stream, side.cuda_stream, ctypes.byref(ra), ctypes.byref(ctypes.c_void_p()))
             for q in aq:
                 q._is_encoding_valid = True
-        p_ptr, outers, Cs, Ks = [], [], [], []
-        views = _PER_CHANNEL_VIEWS
-        for q, t, ax in zip(pq, params, ch_axes):
-            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == f32):
-                _require_gpu(t)
-                raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
-            if not t.is_contiguous():
-                t = t.contiguous()
-            nc = q._num_channels
-            key = (t.shape, ax, nc)
-            v = views.get(key)
-            if v is None:
-                v = views[key] = per_channel_view(t.shape, ax) if nc != 1 else (1, 1, t.numel())
-            outer, C, K = v
-            if C != nc:
-                raise ValueError("tensor has %d channels along axis %d, quantizer has %d" % (C, ax, nc))
-            keep.append(t)
-            p_ptr.append(t.data_ptr())
-            outers.append(outer)
-            Cs.append(C)
-            Ks.append(K)
-        if split:
-            hp = AimetTensorQuantizer._ensure_many(pq, dev)
-            nul, empty = ctypes.c_void_p * 1, ctypes.c_void_p()
-            with torch.cuda.device(dev):
-                # the parameters alone, every operation on the side stream; the main stream then
-                # waits for it (later work there sees the parameters' state, as in one call)
-                _native.call("aimet_calibrate_launch", nul(), nul(), (ctypes.c_int64 * 1)(), 0,
-                             (ctypes.c_void_p * np_)(*hp), (ctypes.c_void_p * np_)(*p_ptr),
-                             (ctypes.c_int64 * np_)(*outers), (ctypes.c_int64 * np_)(*Cs),
-                             (ctypes.c_int64 * np_)(*Ks), np_, a_set, p_set, int(bool(reset)),
-                             side.cuda_stream, side.cuda_stream, ctypes.byref(empty), ctypes.byref(rp))
+            try:
+                p_ptr, outers, Cs, Ks = _param_views(pq, params, ch_axes, keep)
+                hp = AimetTensorQuantizer._ensure_many(pq, dev)
+                nul, empty = ctypes.c_void_p * 1, ctypes.c_void_p()
+                with torch.cuda.device(dev):
+                    # the parameters alone, every operation on the side stream; the main stream
+                    # then waits for it (later work there sees the parameters' state, as in one call)
+                    _native.call("aimet_calibrate_launch", nul(), nul(), (ctypes.c_int64 * 1)(), 0,
+                                 (ctypes.c_void_p * np_)(*hp), (ctypes.c_void_p * np_)(*p_ptr),
+                                 (ctypes.c_int64 * np_)(*outers), (ctypes.c_int64 * np_)(*Cs),
+                                 (ctypes.c_int64 * np_)(*Ks), np_, a_set, p_set, int(bool(reset)),
+                                 side.cuda_stream, side.cuda_stream, ctypes.byref(empty), ctypes.byref(rp))
+            except BaseException:
+                # the activations' call is in flight: discard its request (waits for its result copy)
+                _native.call("aimet_tq_get_encodings_finish", ra, None, None)
+                raise
             main.wait_stream(side)
             if empty.value:   # the second call's (empty) activation request
                 _native.call("aimet_tq_get_encodings_finish", empty, None, None)
             for q in pq:
                 q._is_encoding_valid = True
         else:
+            p_ptr, outers, Cs, Ks = _param_views(pq, params, ch_axes, keep)
             handles = AimetTensorQuantizer._ensure_many(aq + pq, dev)
             with torch.cuda.device(dev):
                 _native.call("aimet_calibrate_launch", (ctypes.c_void_p * max(na, 1))(*handles[:na]),
@@ -657,6 +642,34 @@ class AimetTensorQuantizer:
 
 # (shape, channel axis, channels) -> per_channel_view (calibrateResidentAsync)
 _PER_CHANNEL_VIEWS = {}
+
+
+def _param_views(pq, params, ch_axes, keep):
+    """calibrateResidentAsync's parameter half: (pointers, outers, Cs, Ks) of the float32 HIP
+    tensors, each kept alive in `keep`; the per-channel views cached by (shape, axis, channels)."""
+    f32 = torch.float32
+    p_ptr, outers, Cs, Ks = [], [], [], []
+    views = _PER_CHANNEL_VIEWS
+    for q, t, ax in zip(pq, params, ch_axes):
+        if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == f32):
+            _require_gpu(t)
+            raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
+        if not t.is_contiguous():
+            t = t.contiguous()
+        nc = q._num_channels
+        key = (t.shape, ax, nc)
+        v = views.get(key)
+        if v is None:
+            v = views[key] = per_channel_view(t.shape, ax) if nc != 1 else (1, 1, t.numel())
+        outer, C, K = v
+        if C != nc:
+            raise ValueError("tensor has %d channels along axis %d, quantizer has %d" % (C, ax, nc))
+        keep.append(t)
+        p_ptr.append(t.data_ptr())
+        outers.append(outer)
+        Cs.append(C)
+        Ks.append(K)
+    return p_ptr, outers, Cs, Ks
 
 
 class PendingEncodings:

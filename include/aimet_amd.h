@@ -267,7 +267,8 @@ int aimet_tq_get_encodings(aimet_tensor_quantizer* const* qs, int64_t nq, uint32
  * searches, the next batch) before it waits: _launch enqueues every device search on `stream`
  * and the copies of their results into pinned memory, and returns a request; _finish waits for
  * it, finishes the host-side encodings (TF, percentile, entropy near-ties) and frees the request
- * (always, also on error). */
+ * (always, also on error). out == valid == NULL discards the request: it waits for the request's
+ * device work (so its pinned result block is idle) and frees it. */
 typedef struct aimet_encoding_request aimet_encoding_request;
 int aimet_tq_get_encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int use_symmetric,
                                   int use_strict_symmetric, int use_unsigned_symmetric, void* stream,

@@ -1568,6 +1568,31 @@ def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatc
     assert ([e.to_tuple() for e, _ in fresh[0]]) == results[0][0]
 
 
+def test_calibrate_two_calls_bad_parameter_discards_the_activation_request():
+    """The two-call form launches the activations before it looks at the parameters: a parameter
+    it refuses (float16) raises TypeError after the activations' call, whose request is then
+    discarded (aimet_tq_get_encodings_finish with no outputs waits for its result copy and frees
+    it); the same quantizers calibrate normally afterwards, equal to fresh ones."""
+    from aimet_amd import calibration
+    from aimet_amd.calibration import compute_encodings_resident
+    g = torch.Generator(device=DEV).manual_seed(4)
+    TFE = QuantizationMode.QUANTIZATION_TF_ENHANCED
+    acts = [torch.randn(n, device=DEV, generator=g) for n in (1 << 20, 4099)]
+    params = [torch.randn(16, 75, device=DEV, generator=g) * 0.1]
+    aq = [AimetTensorQuantizer(TFE) for _ in acts]
+    pq = [AimetTensorQuantizer(TFE, num_channels=16)]
+    dev = torch.device(DEV, torch.cuda.current_device())
+    side = calibration._side_stream(dev)
+    with pytest.raises(TypeError):
+        AimetTensorQuantizer.calibrateResidentAsync(aq, acts, pq, [params[0].half()], reset=True,
+                                                    main_stream=torch.cuda.current_stream(dev), side_stream=side)
+    got = compute_encodings_resident(aq, acts, pq, params, reset=True)
+    fa, fp = [AimetTensorQuantizer(TFE) for _ in acts], [AimetTensorQuantizer(TFE, num_channels=16)]
+    want = compute_encodings_resident(fa, acts, fp, params)
+    assert [e.to_tuple() for e, _ in got[0]] == [e.to_tuple() for e, _ in want[0]]
+    assert [x.to_tuple() for x in got[1][0][0]] == [x.to_tuple() for x in want[1][0][0]]
+
+
 def test_compute_encodings_resident_equals_individual():
     """aimet_amd.calibration.compute_encodings_resident (batched activation statistics, parameter
     statistics + searches on a second stream) == updateStats / getEncoding quantizer by quantizer."""
