@@ -1,0 +1,6 @@
+#!/usr/bin/env bash
+# Round 3: cast-fused weight forward with the 16-bit fast store; Llama step.
+source "$(dirname "${BASH_SOURCE[0]}")/../../gpu_lib.sh"
+run lg_tests 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "learned or lg or range_learning or qat"
+run llama 600 python -u benchmarks/llama_qat.py --steps 5 --warmup 2
+run llama_trace 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/llama_trace2 -o run -- python3 benchmarks/llama_qat.py --steps 3 --warmup 1
