@@ -333,7 +333,7 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
         if (bias)
             require_device_ptr(bias, "bias");
         const int64_t R = pw_rows(Cin, Cout);
-        AIMET_REQUIRE(R >= 4 && R * Cin <= kPwPairs && ceil_div(Cin, (int64_t) 4) * ceil_div(R, (int64_t) 4) <=
+        AIMET_REQUIRE((R >= 4 || R == Cout) && R * Cin <= kPwPairs && ceil_div(Cin, (int64_t) 4) * ceil_div(R, (int64_t) 4) <=
                                                             (int64_t) kBlock * kPwBlocks,
                       "pointwise step: at most 512 4x4 weight-gradient blocks per row range");
         const int64_t tps    = ceil_div(HW, (int64_t) kPwT);

@@ -73,10 +73,13 @@ def _all_reduce(t, op, group):
         dist.all_reduce(t, op=op, group=group)
 
 
-def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange=None, fused=True):
+def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange=None, fused=True,
+                         force_exchange=False):
     """One calibration batch: every rank passes ITS shard of each quantizer's tensor.
 
-    Equivalent to ``q.updateStats(whole_batch_tensor)`` on one device for every quantizer."""
+    Equivalent to ``q.updateStats(whole_batch_tensor)`` on one device for every quantizer.
+    `force_exchange` runs both collectives even in a world of one rank (a world-size-1 RCCL group
+    then executes the device-buffer all_reduces of the N-rank path on a single GPU)."""
     if not quantizers:
         return exchange
     device = tensors[0].device
@@ -91,7 +94,8 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
     mq = [quantizers[i] for i in many]
     mt = [tensors[i] for i in many]
 
-    if world == 1 and not rest and fused:
+    exchanging = world > 1 or force_exchange
+    if not exchanging and not rest and fused:
         # nothing to exchange (no packed buffers either): the fused single-pass update, 4 launches
         # for all quantizers
         AimetTensorQuantizer.updateStatsMany(quantizers if len(mq) == len(quantizers) else mq,
@@ -105,7 +109,7 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
         AimetTensorQuantizer.batch_minmax_many(mq, mt)
     for i in rest:
         quantizers[i].batch_minmax(tensors[i], ch_axes[i])
-    if world > 1:
+    if exchanging:
         # {-min, max}: a single MAX reduces both ends exactly
         _all_reduce(exchange.minmax, dist.ReduceOp.MAX, group)
     if mq:
@@ -127,7 +131,7 @@ def sharded_update_stats(quantizers, tensors, ch_axes=None, group=None, exchange
         # kernel reads its slice of the reduced buffer), then the others
         order = hist_many + hist_rest
         by_pos = {i: k for k, i in enumerate(hist)}
-        if world > 1:
+        if exchanging:
             host = torch.tensor([local[by_pos[i]] for i in order], dtype=torch.int64)
             if exchange.elem_counts.is_cuda:
                 # a pinned staging buffer from torch's caching host allocator, which keeps it alive

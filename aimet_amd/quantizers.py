@@ -123,6 +123,33 @@ class StaticGridTensorQuantizer:
             self.quant_scheme = QuantScheme.post_training_tf
         self._encoding_min_max_fixed_vals = vals
 
+    def __getstate__(self):
+        """v1/tensor_quantizer.py:182-192 (PickableState :128-140): every attribute but the native
+        op travels; the encodings as (min, max, delta, offset, bw) tuples, and none when the
+        quantizer has no (or an empty) encoding list. The device caches (STE bounds) stay behind."""
+        state = self.__dict__.copy()
+        state.pop("_cppOp", None)
+        state.pop("_ste_cache", None)
+        encodings = state.pop("_encoding", None)
+        state["_pickled_encodings"] = [e.to_tuple() for e in encodings] if encodings else None
+        return state
+
+    def __setstate__(self, state):
+        """v1/tensor_quantizer.py:194-220: a fresh native op (empty statistics, created on the device
+        of first use) and new TfEncoding objects carrying the saved values."""
+        state = dict(state)
+        encodings = state.pop("_pickled_encodings", None)
+        self.__dict__.update(state)
+        self._make_op()
+        if encodings is None:
+            self._encoding = None
+        else:
+            self._encoding = []
+            for mn, mx, delta, offset, bw in encodings:
+                e = TfEncoding()
+                e.bw, e.max, e.min, e.delta, e.offset = bw, mx, mn, delta, offset
+                self._encoding.append(e)
+
     def _make_op(self):
         raise NotImplementedError
 

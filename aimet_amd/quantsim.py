@@ -21,6 +21,7 @@ import contextlib
 import copy
 import json
 import os
+import pickle
 from typing import Any, Callable, Dict, List, Optional, Union
 
 import torch
@@ -307,6 +308,64 @@ class QuantizationSimModel:
     def load_and_freeze_encodings(self, encoding_path: str, ignore_when_quantizer_disabled: bool = False):
         self.load_encodings(encoding_path, strict=not ignore_when_quantizer_disabled, partial=True,
                             requires_grad=False, allow_overwrite=False)
+
+    # -- the unwrapped model (v1/quantsim.py:1490-1575) -----------------------------------------
+    @classmethod
+    def _remove_quantization_wrappers(cls, starting_module: nn.Module, list_of_modules_to_exclude):
+        """v1/quantsim.py:1490-1517: every wrapper among `list_of_modules_to_exclude` below
+        `starting_module` is replaced by the module it wraps."""
+        for name, child in list(starting_module.named_children()):
+            if any(child is m for m in list_of_modules_to_exclude) and isinstance(child, QcQuantizeWrapper):
+                child = child.get_original_module()
+                setattr(starting_module, name, child)
+            cls._remove_quantization_wrappers(child, list_of_modules_to_exclude)
+
+    @classmethod
+    def get_original_model(cls, model: nn.Module, qdq_weights: bool = False) -> nn.Module:
+        """v1/quantsim.py:1519-1534: a deep copy of `model` with every quantization wrapper removed;
+        with `qdq_weights` the copy's parameters are first replaced by their quantize-dequantized
+        values. `model` itself is not changed."""
+        original = copy.deepcopy(model)
+        if qdq_weights:
+            cls._apply_qdq_to_model_parameters(original)
+        cls._remove_quantization_wrappers(original, list(original.modules()))
+        return original
+
+    @classmethod
+    @torch.no_grad()
+    def _apply_qdq_to_model_parameters(cls, model: nn.Module):
+        """v1/quantsim.py:1536-1552: every wrapper's parameters become their quantize-dequantized
+        values (eval mode: nearest rounding, no recalibration of calibrated weights)."""
+        for m in model.modules():
+            if isinstance(m, (StaticGridQuantWrapper, LearnedGridQuantWrapper)):
+                was = m.training
+                m.eval()
+                try:
+                    if isinstance(m, StaticGridQuantWrapper):
+                        m._quantize_dequantize_params()   # leaves the QDQ values in param.data
+                    else:
+                        with m._quantize_params():
+                            patched = {n: m._module_to_wrap.__dict__[n] for n, _ in m.get_named_parameters()
+                                       if n in m._module_to_wrap.__dict__}
+                        for n, p in m._module_to_wrap.named_parameters():
+                            if n in patched:
+                                p.data = patched[n].detach().to(p.dtype)
+                finally:
+                    m.train(was)
+
+
+def save_checkpoint(quant_sim_model: QuantizationSimModel, file_path: str):
+    """v1/quantsim.py:2216-2227: the whole sim pickled. Quantizers travel with their encodings and
+    settings; their device statistics do not (as the reference's C++ ops, they are rebuilt empty)."""
+    with open(file_path, "wb") as f:
+        pickle.dump(quant_sim_model, f)
+
+
+def load_checkpoint(file_path: str) -> QuantizationSimModel:
+    """v1/quantsim.py:2230-2240: a new QuantizationSimModel from a save_checkpoint file. Like the
+    reference this unpickles the file, so load only checkpoints you wrote yourself."""
+    with open(file_path, "rb") as f:
+        return pickle.load(f)
 
 
 def load_encodings_to_sim(quant_sim_model: QuantizationSimModel, pytorch_encoding_path: str):

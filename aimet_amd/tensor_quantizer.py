@@ -162,8 +162,14 @@ class AimetTensorQuantizer:
             pass
 
     def __getstate__(self):
-        raise TypeError("AimetTensorQuantizer holds device state and is not picklable "
-                        "(the reference drops it in StaticGridTensorQuantizer.__getstate__)")
+        """Pickle / deepcopy: the analyzer settings travel, the device statistics do not (the
+        reference never pickles its op: StaticGridTensorQuantizer.__getstate__ drops it and
+        __setstate__ builds a fresh one, v1/tensor_quantizer.py:182-220). The copy starts with
+        empty statistics and creates its native object on first use."""
+        return {"scheme": int(self._scheme), "num_channels": self._num_channels}
+
+    def __setstate__(self, state):
+        self.__init__(state["scheme"], state["num_channels"])
 
     @property
     def num_channels(self):
@@ -450,22 +456,28 @@ class AimetTensorQuantizer:
             raise ValueError("calibrateResidentAsync: the activation quantizers are per-tensor")
         dev = (activations[0] if aq else params[0]).device
         ch_axes = list(param_ch_axes) if param_ch_axes is not None else [0] * len(pq)
-        # host preparation is on the critical path of a ~4 ms call (the first launch waits for it):
-        # one pass over the tensors with the fewest torch attribute calls, the checks of
-        # _require_gpu folded in, the per-channel views cached by (shape, axis)
+        # every check runs before anything is launched or any quantizer changes: a refused call
+        # leaves all state as it was (only native failures reach the request-discard path below)
         f32 = torch.float32
-        keep, a_ptr, a_n = [], [], []
         for t in activations:
             if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == f32):
                 _require_gpu(t)
                 raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
-            if not t.is_contiguous():
-                t = t.contiguous()
-            keep.append(t)
-            a_ptr.append(t.data_ptr())
-            a_n.append(t.numel())
+        p_specs = _param_specs(pq, params, ch_axes)
         main = main_stream if main_stream is not None else torch.cuda.current_stream(dev)
         side = side_stream if side_stream is not None else main
+        # host preparation is on the critical path of a ~4 ms call (the first launch waits for it):
+        # one pass over the tensors with the fewest torch attribute calls. A non-contiguous input's
+        # copy is queued on `main`, the stream the activations' kernels run on (the caller's
+        # current stream may be another one).
+        keep, a_ptr, a_n = [], [], []
+        with torch.cuda.stream(main):
+            for t in activations:
+                if not t.is_contiguous():
+                    t = t.contiguous()
+                keep.append(t)
+                a_ptr.append(t.data_ptr())
+                a_n.append(t.numel())
         if reset:
             for q in aq + pq:
                 q._pending_percentile = None
@@ -490,9 +502,14 @@ class AimetTensorQuantizer:
             for q in aq:
                 q._is_encoding_valid = True
             try:
-                p_ptr, outers, Cs, Ks = _param_views(pq, params, ch_axes, keep)
+                # a non-contiguous parameter's copy goes on the side stream, after its wait for
+                # `main` above and before the parameters' kernels (the second call runs every
+                # operation on `side`, so no join would order a copy queued on `main`)
+                with torch.cuda.stream(side):
+                    p_ptr = _param_pointers(p_specs, keep)
                 hp = AimetTensorQuantizer._ensure_many(pq, dev)
                 nul, empty = ctypes.c_void_p * 1, ctypes.c_void_p()
+                outers, Cs, Ks = ([s[i] for s in p_specs] for i in (1, 2, 3))
                 with torch.cuda.device(dev):
                     # the parameters alone, every operation on the side stream; the main stream
                     # then waits for it (later work there sees the parameters' state, as in one call)
@@ -511,7 +528,10 @@ class AimetTensorQuantizer:
             for q in pq:
                 q._is_encoding_valid = True
         else:
-            p_ptr, outers, Cs, Ks = _param_views(pq, params, ch_axes, keep)
+            # the copies on `main`: the native call starts `side` after everything queued there
+            with torch.cuda.stream(main):
+                p_ptr = _param_pointers(p_specs, keep)
+            outers, Cs, Ks = ([s[i] for s in p_specs] for i in (1, 2, 3))
             handles = AimetTensorQuantizer._ensure_many(aq + pq, dev)
             with torch.cuda.device(dev):
                 _native.call("aimet_calibrate_launch", (ctypes.c_void_p * max(na, 1))(*handles[:na]),
@@ -644,18 +664,17 @@ class AimetTensorQuantizer:
 _PER_CHANNEL_VIEWS = {}
 
 
-def _param_views(pq, params, ch_axes, keep):
-    """calibrateResidentAsync's parameter half: (pointers, outers, Cs, Ks) of the float32 HIP
-    tensors, each kept alive in `keep`; the per-channel views cached by (shape, axis, channels)."""
+def _param_specs(pq, params, ch_axes):
+    """calibrateResidentAsync's parameter checks, before anything is launched: [(tensor, outer, C,
+    K)] of the float32 HIP tensors, the per-channel views (from the shape alone, no copy) cached by
+    (shape, axis, channels)."""
     f32 = torch.float32
-    p_ptr, outers, Cs, Ks = [], [], [], []
+    specs = []
     views = _PER_CHANNEL_VIEWS
     for q, t, ax in zip(pq, params, ch_axes):
         if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == f32):
             _require_gpu(t)
             raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
-        if not t.is_contiguous():
-            t = t.contiguous()
         nc = q._num_channels
         key = (t.shape, ax, nc)
         v = views.get(key)
@@ -664,12 +683,20 @@ def _param_views(pq, params, ch_axes, keep):
         outer, C, K = v
         if C != nc:
             raise ValueError("tensor has %d channels along axis %d, quantizer has %d" % (C, ax, nc))
+        specs.append((t, outer, C, K))
+    return specs
+
+
+def _param_pointers(specs, keep):
+    """The parameters' device pointers; a non-contiguous tensor is copied on the current stream
+    (the caller picks it) and every tensor is kept alive in `keep`."""
+    ptrs = []
+    for t, _, _, _ in specs:
+        if not t.is_contiguous():
+            t = t.contiguous()
         keep.append(t)
-        p_ptr.append(t.data_ptr())
-        outers.append(outer)
-        Cs.append(C)
-        Ks.append(K)
-    return p_ptr, outers, Cs, Ks
+        ptrs.append(t.data_ptr())
+    return ptrs
 
 
 class PendingEncodings:

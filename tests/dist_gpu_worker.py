@@ -1,6 +1,10 @@
 """Worker of tests/test_distributed_gpu.py (not collected by pytest): one rank of a sharded
 calibration on the GPU. Every rank uses cuda:0 (one-GPU box) and a gloo group (the exchange
-buffers are staged through host memory); the statistics are computed by the gfx950 kernels."""
+buffers are staged through host memory); the statistics are computed by the gfx950 kernels.
+
+BACKEND=nccl with WORLD_SIZE=1 and FORCE_EXCHANGE=1: a world-size-1 RCCL group formed before any
+other GPU call, and both packed collectives of every batch run on the device buffers (the branch
+of aimet_amd.distributed._all_reduce that the N-GPU bench takes)."""
 import json
 import os
 import sys
@@ -55,11 +59,17 @@ def encodings(qs):
 
 def main():
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
-    torch.cuda.set_device(0)
+    backend = os.environ.get("BACKEND", "gloo")
+    force = os.environ.get("FORCE_EXCHANGE") == "1"
     dev = torch.device("cuda", 0)
+    if backend == "nccl":
+        # the process group first, bound to the device, as bench.py forms it
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    torch.cuda.set_device(0)
     qs = make_quantizers()
-    if world > 1:
+    if world > 1 and backend == "gloo":
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    sharded = world > 1 or force
     ex = None
     for act, relu in batches():
         shard = slice(rank, None, world)      # per-sample sharding
@@ -68,8 +78,8 @@ def main():
             src = act if (i // 2) % 2 == 0 else relu
             tensors.append(torch.from_numpy(np.ascontiguousarray(src[shard])).to(dev))
             axes.append(1)
-        if world > 1:
-            ex = sharded_update_stats(qs, tensors, axes, exchange=ex)
+        if sharded:
+            ex = sharded_update_stats(qs, tensors, axes, exchange=ex, force_exchange=force)
         else:
             for q, t, ax in zip(qs, tensors, axes):
                 if q.num_channels == 1:
@@ -79,7 +89,9 @@ def main():
     res = encodings(qs)
     with open(os.environ["OUT"] + ".%d" % rank, "w") as f:
         json.dump(res, f)
-    if world > 1:
+    if dist.is_initialized():
+        with open(os.environ["OUT"] + ".backend", "w") as f:
+            f.write(dist.get_backend())
         dist.barrier()
         dist.destroy_process_group()
 

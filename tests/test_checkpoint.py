@@ -1,0 +1,228 @@
+"""Checkpoint / resume of quantizers, wrappers and QuantizationSimModel (SURVEY §5 "Checkpoint /
+resume"): pickle and deepcopy as the reference's (v1/tensor_quantizer.py:182-220 drops the native op
+and keeps the encodings; v1/quantsim.py:2216-2240 save_checkpoint / load_checkpoint pickle the sim;
+v1/quantsim.py:1519-1552 get_original_model deep-copies the wrapped model and strips the wrappers).
+
+CPU tests: the state that travels (settings, encodings as values, a fresh native op with empty
+statistics) with encodings set by hand. GPU tests: a calibrated ResNet-50 sim checkpointed and
+reloaded QDQs bit-identically, its deep copy too, and a reloaded range-learning sim steps
+bit-identically."""
+import copy
+import pickle
+
+import pytest
+import torch
+from torch import nn
+
+from conftest import gpu_available
+
+from aimet_amd.libpymo import TfEncoding
+from aimet_amd.qc_quantize_op import QcQuantizeWrapper, StaticGridQuantWrapper
+from aimet_amd.quantizers import QuantScheme, StaticGridPerChannelQuantizer, StaticGridPerTensorQuantizer
+from aimet_amd.quantsim import QuantizationSimModel, load_checkpoint, save_checkpoint
+from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+
+PER_CHANNEL_CFG = {"defaults": {"ops": {"is_output_quantized": "True"},
+                                "params": {"is_quantized": "True", "is_symmetric": "True"},
+                                "strict_symmetric": "False", "per_channel_quantization": "True"}}
+
+
+def _enc(mn, mx, bw=8):
+    e = TfEncoding()
+    e.min, e.max, e.bw = mn, mx, bw
+    e.delta = (mx - mn) / (2 ** bw - 1)
+    e.offset = round(mn / e.delta)
+    return e
+
+
+def _roundtrips(obj):
+    return [pickle.loads(pickle.dumps(obj)), copy.deepcopy(obj)]
+
+
+# ------------------------------------------------------------------------------------------
+# CPU
+# ------------------------------------------------------------------------------------------
+def test_per_tensor_quantizer_roundtrip():
+    q = StaticGridPerTensorQuantizer(8, "stochastic", QuantScheme.post_training_tf_enhanced, True, True)
+    q.use_strict_symmetric = True
+    q.is_const = True
+    q.encoding = _enc(-1.5, 2.25)
+    q.freeze_encoding()
+    for r in _roundtrips(q):
+        assert r.encoding.to_tuple() == q.encoding.to_tuple()
+        assert r.encoding is not q.encoding and isinstance(r.encoding, TfEncoding)
+        assert (r.bitwidth, r.round_mode, r.quant_scheme, r.use_symmetric_encodings, r.use_strict_symmetric,
+                r.enabled, r.is_const, r.is_encoding_frozen) == \
+            (8, q.round_mode, QuantScheme.post_training_tf_enhanced, True, True, True, True, True)
+        # a fresh native op: same analyzer, no device state until first use
+        op = r._op()
+        assert op is not q._op() and op._handle is None and op.num_channels == 1
+        assert int(op.quant_scheme) == int(q._op().quant_scheme)
+
+
+def test_per_channel_quantizer_roundtrip():
+    q = StaticGridPerChannelQuantizer(4, "nearest", QuantScheme.post_training_tf, True, 3, True, ch_axis=1)
+    q.encoding = [_enc(-1.0, 1.0, 4), _enc(-0.5, 0.25, 4), _enc(-3.0, 2.0, 4)]
+    q.encoding_min_max_fixed_vals = (-2.0, 2.0)
+    q._ste_cache = {"cuda:0": ("stale", None, None)}   # device caches stay behind
+    for r in _roundtrips(q):
+        assert [e.to_tuple() for e in r.encoding] == [e.to_tuple() for e in q.encoding]
+        assert r.channel_axis == 1 and r._num_channels == 3 and r._op().num_channels == 3
+        assert r.encoding_min_max_fixed_vals == (-2.0, 2.0)
+        assert "_ste_cache" not in r.__dict__
+        # the per-channel QDQ table is rebuilt for the new objects
+        assert r._op()._pc_table._tables == {}
+
+
+def test_quantizer_without_encoding_roundtrip():
+    """The reference keeps no encodings when the list is None or empty (PickableState :137)."""
+    q = StaticGridPerTensorQuantizer(8, "nearest", QuantScheme.post_training_tf, False, True)
+    assert all(r.encoding is None and r._encoding is None for r in _roundtrips(q))
+    q._encoding = []   # a failed compute_encoding
+    assert all(r._encoding is None for r in _roundtrips(q))
+
+
+def test_native_op_pickles_without_device_state():
+    op = AimetTensorQuantizer(3, num_channels=5)
+    op._is_encoding_valid = True
+    for r in _roundtrips(op):
+        assert r.num_channels == 5 and int(r.quant_scheme) == 3
+        assert r._handle is None and not r._is_encoding_valid
+
+
+class _Net(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.conv = nn.Conv2d(3, 8, 3, padding=1)
+        self.body = nn.Sequential(nn.ReLU(), nn.Conv2d(8, 4, 1))
+        self.fc = nn.Linear(4 * 8 * 8, 10)
+
+    def forward(self, x):
+        return self.fc(self.body(self.conv(x)).flatten(1))
+
+
+def _loaded_sim():
+    torch.manual_seed(0)
+    sim = QuantizationSimModel(_Net(), quant_scheme="tf_enhanced", config_file=PER_CHANNEL_CFG)
+    sim.load_encodings({"activation_encodings": {
+        "conv": {"input": {"0": {"bitwidth": 8, "dtype": "int", "is_symmetric": "False", "min": -1.0, "max": 1.0}},
+                 "output": {"0": {"bitwidth": 8, "dtype": "int", "is_symmetric": "False", "min": -2.0, "max": 3.0}}}},
+        "param_encodings": {"body.1.weight": [{"bitwidth": 8, "dtype": "int", "is_symmetric": "True",
+                                                "min": -0.25 * (c + 1), "max": 0.25 * (c + 1)} for c in range(4)]}},
+        strict=True, partial=True)
+    return sim
+
+
+def test_sim_checkpoint_roundtrip_cpu(tmp_path):
+    sim = _loaded_sim()
+    path = tmp_path / "sim.pkl"
+    save_checkpoint(sim, str(path))
+    loaded = load_checkpoint(str(path))
+    assert isinstance(loaded, QuantizationSimModel) and loaded.model is not sim.model
+    assert loaded.get_encodings_dict() == sim.get_encodings_dict()
+    assert [n for n, _ in loaded.quant_wrappers()] == [n for n, _ in sim.quant_wrappers()]
+    sd, lsd = sim.model.state_dict(), loaded.model.state_dict()
+    assert sd.keys() == lsd.keys() and all(torch.equal(sd[k], lsd[k]) for k in sd)
+    # deepcopy of the wrapped model (what get_original_model does)
+    m2 = copy.deepcopy(sim.model)
+    pq = m2.body[1].param_quantizers["weight"]
+    assert [e.to_tuple() for e in pq.encoding] == \
+        [e.to_tuple() for e in sim.model.body[1].param_quantizers["weight"].encoding]
+
+
+def test_get_original_model_cpu():
+    sim = _loaded_sim()
+    orig = QuantizationSimModel.get_original_model(sim.model)
+    assert not any(isinstance(m, QcQuantizeWrapper) for m in orig.modules())
+    assert isinstance(sim.model.conv, StaticGridQuantWrapper)   # the sim's model is untouched
+    assert isinstance(orig.conv, nn.Conv2d) and isinstance(orig.body[1], nn.Conv2d)
+    assert orig.conv.weight is not sim.model.conv._module_to_wrap.weight
+    assert torch.equal(orig.conv.weight, sim.model.conv._module_to_wrap.weight)
+    torch.manual_seed(0)
+    net = _Net()   # the model the sim was built from
+    x = torch.rand(2, 3, 8, 8)
+    assert torch.equal(orig(x), net(x))
+
+
+# ------------------------------------------------------------------------------------------
+# GPU
+# ------------------------------------------------------------------------------------------
+gpu = pytest.mark.skipif(not gpu_available(), reason="needs an MI355X")
+
+
+def _bits(t):
+    return t.detach().contiguous().view(torch.int32) if t.dtype == torch.float32 else t.detach().view(torch.int16)
+
+
+@pytest.mark.gpu
+@gpu
+def test_resnet50_sim_checkpoint_qdq_bit_identical(tmp_path):
+    """A calibrated per-channel ResNet-50 W8A8 sim, checkpointed and reloaded: the QDQ forward is
+    bit-identical, so is its deep copy's, and both recalibrate to the original's encodings."""
+    from workloads.resnet import resnet50
+    dev = torch.device("cuda", 0)
+    images = torch.rand(8, 3, 224, 224, generator=torch.Generator().manual_seed(1234)).to(dev)
+    sim = QuantizationSimModel(resnet50(seed=0, device=dev), images[:1], quant_scheme="tf_enhanced",
+                               config_file=PER_CHANNEL_CFG)
+    sim.compute_encodings(lambda m, _: m(images), None)
+    with torch.no_grad():
+        y0 = sim.model(images)
+    path = tmp_path / "resnet_sim.pkl"
+    save_checkpoint(sim, str(path))
+    loaded = load_checkpoint(str(path))
+    model_copy = copy.deepcopy(sim.model)
+    with torch.no_grad():
+        y1 = loaded.model(images)
+        y2 = model_copy(images)
+    assert torch.equal(_bits(y0), _bits(y1)) and torch.equal(_bits(y0), _bits(y2))
+    assert loaded.get_encodings_dict() == sim.get_encodings_dict()
+    # the reloaded quantizers have fresh native ops: recalibrating gives the same encodings
+    loaded.compute_encodings(lambda m, _: m(images), None)
+    assert loaded.get_encodings_dict() == sim.get_encodings_dict()
+    with torch.no_grad():
+        assert torch.equal(_bits(loaded.model(images)), _bits(y0))
+
+    # the unwrapped model, with and without the weights quantize-dequantized
+    plain = QuantizationSimModel.get_original_model(sim.model)
+    qdq = QuantizationSimModel.get_original_model(sim.model, qdq_weights=True)
+    assert not any(isinstance(m, QcQuantizeWrapper) for m in list(plain.modules()) + list(qdq.modules()))
+    n_checked = 0
+    for name, w in sim.quant_wrappers():
+        pq = w.param_quantizers["weight"]
+        w_orig = w._module_to_wrap.weight
+        w_plain = plain.get_submodule(name).weight
+        w_qdq = qdq.get_submodule(name).weight
+        assert torch.equal(_bits(w_plain), _bits(w_orig))
+        assert torch.equal(_bits(w_qdq), _bits(pq.quantize_dequantize(w_orig.detach(), 0)))
+        n_checked += 1
+    assert n_checked == 54
+
+
+@pytest.mark.gpu
+@gpu
+def test_range_learning_sim_checkpoint_step_bit_identical(tmp_path):
+    """A range-learning sim (LearnedGridQuantWrapper: trainable encoding_min / _max parameters)
+    reloaded from a checkpoint: forward and every gradient bit-identical."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    net = _Net().to(dev)
+    x = torch.randn(4, 3, 8, 8, device=dev)
+    sim = QuantizationSimModel(net, x[:1], quant_scheme=QuantScheme.training_range_learning_with_tf_init,
+                               config_file=PER_CHANNEL_CFG)
+    sim.compute_encodings(lambda m, _: m(x), None)
+    path = tmp_path / "lg_sim.pkl"
+    save_checkpoint(sim, str(path))
+    loaded = load_checkpoint(str(path))
+
+    def step(s):
+        s.model.zero_grad(set_to_none=True)
+        y = s.model(x)
+        y.square().sum().backward()
+        return y, {n: p.grad for n, p in s.model.named_parameters() if p.grad is not None}
+
+    y0, g0 = step(sim)
+    y1, g1 = step(loaded)
+    assert torch.equal(_bits(y0), _bits(y1))
+    assert g0.keys() == g1.keys() and any(n.endswith("_encoding_max") for n in g0)
+    for n in g0:
+        assert torch.equal(_bits(g0[n]), _bits(g1[n])), n

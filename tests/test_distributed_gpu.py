@@ -22,12 +22,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run(world, out):
+def _run(world, out, **extra):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), OUT=out)
+                   MASTER_PORT=str(port), OUT=out, **extra)
         procs.append(subprocess.Popen([sys.executable, WORKER], env=env))
     for p in procs:
         assert p.wait(timeout=240) == 0
@@ -39,3 +39,14 @@ def test_sharded_calibration_equals_whole_batch_on_gpu(tmp_path):
     shards = _run(2, str(tmp_path / "shard"))
     for r, res in enumerate(shards):
         assert res == whole, "rank %d" % r
+
+
+def test_rccl_world1_device_exchange_equals_unsharded(tmp_path):
+    """A world-size-1 RCCL ("nccl") group formed in a fresh process before any other GPU call;
+    every batch's two packed collectives run on the device buffers (distributed.py _all_reduce's
+    RCCL branch, stream-ordered between the statistics kernels): the encodings equal the unsharded
+    path bit for bit."""
+    whole, = _run(1, str(tmp_path / "whole"))
+    rccl, = _run(1, str(tmp_path / "rccl"), BACKEND="nccl", FORCE_EXCHANGE="1")
+    assert open(str(tmp_path / "rccl") + ".backend").read() == "nccl"
+    assert rccl == whole

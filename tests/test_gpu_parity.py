@@ -2,6 +2,7 @@
 C++ (bit-exact), the reference test-suites' KATs, the CPU oracle on seeded inputs, and at full
 size size-independent properties. Needs an MI355X."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -16,6 +17,8 @@ from aimet_amd import AimetTensorQuantizer  # noqa: E402
 from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding  # noqa: E402
 
 DEV = "cuda"
+# learned-grid range gradients: error bound in units of 2^-24 x (sum of |terms|) of the float64 sum
+LG_BOUND_C = float(os.environ.get("AIMET_LG_BOUND_C", "2"))
 NEAREST = RoundingMode.ROUND_NEAREST
 FLAGS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]
 
@@ -489,8 +492,8 @@ def test_channel_plan_equals_individual_launches():
 def test_learned_grid_vs_reference_golden(golden_dir, case):
     """Fused learned-grid fwd/bwd vs the reference module's outputs (golden_lg.npz): y and grad_x
     bit-exact; the encoding gradients are sums, so they are held to a stated bound instead: ours and
-    the reference's both within 16 eps x (the sum of |terms|) of the float64 value of the same sum
-    (the reference's own error is <= 1.3 of that unit on these cases)."""
+    the reference's both within LG_BOUND_C = 2 eps x (the sum of |terms|) of the float64 value of
+    the same sum (the reference's own error is <= 1.3 of that unit on these cases)."""
     import os
     from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
     from oracle import torch_ref as T
@@ -510,7 +513,7 @@ def test_learned_grid_vs_reference_golden(golden_dir, case):
     for got, ex, b, what in ((emin.grad, ex_min, b_min, "grad_min"), (emax.grad, ex_max, b_max, "grad_max"),
                              (torch.from_numpy(g["c%d_gmin" % i]), ex_min, b_min, "reference grad_min"),
                              (torch.from_numpy(g["c%d_gmax" % i]), ex_max, b_max, "reference grad_max")):
-        T.assert_within_sum_bound(got, ex, b, 16, what)
+        T.assert_within_sum_bound(got, ex, b, LG_BOUND_C, "golden c%d %s" % (i, what))
 
 
 @pytest.mark.parametrize("shape,sym", [((4096, 4096), True), ((8, 1 << 20), False), ((96, 3, 7), True),
@@ -518,8 +521,9 @@ def test_learned_grid_vs_reference_golden(golden_dir, case):
 def test_learned_grid_large_vs_torch_ref(shape, sym):
     """Llama-like weight (4096 x 4096, per-channel 4-bit symmetric; one workgroup per channel),
     few long channels (channel x slice grid, atomic sums) and K % 4 != 0 (scalar path): kernel vs
-    the torch restatement. grad_x bit-exact; encoding gradients within 64 eps x (sum of |terms|) of
-    the float64 sum (the restatement's fp32 sums within the same bound)."""
+    the torch restatement. grad_x bit-exact; encoding gradients within LG_BOUND_C = 2 eps x (sum of
+    |terms|) of the float64 sum; torch's own fp32 sums of the restatement are reported beside them
+    and held to 64 (they are the torch-op path's, not ours)."""
     from aimet_amd.learned_grid import LearnedGridQuantizeDequantize
     from oracle import torch_ref as T
     torch.manual_seed(2)
@@ -535,9 +539,12 @@ def test_learned_grid_large_vs_torch_ref(shape, sym):
     gx, gmin, gmax = T.lg_gradients(w.detach(), grad, emin.detach(), emax.detach(), 4, sym)
     assert torch.equal(w.grad, gx)
     ex_min, ex_max, b_min, b_max = T.lg_encoding_grads_bound(w.detach(), grad, emin.detach(), emax.detach(), 4, sym)
-    for got, ex, b, what in ((emin.grad, ex_min, b_min, "grad_min"), (emax.grad, ex_max, b_max, "grad_max"),
-                             (gmin, ex_min, b_min, "restatement grad_min"), (gmax, ex_max, b_max, "restatement grad_max")):
-        T.assert_within_sum_bound(got, ex, b, 64, what)
+    tag = "large %s sym=%d " % ("x".join(map(str, shape)), sym)
+    for got, ex, b, what, c in ((emin.grad, ex_min, b_min, "grad_min", LG_BOUND_C),
+                                (emax.grad, ex_max, b_max, "grad_max", LG_BOUND_C),
+                                (gmin, ex_min, b_min, "torch restatement grad_min", 64),
+                                (gmax, ex_max, b_max, "torch restatement grad_max", 64)):
+        T.assert_within_sum_bound(got, ex, b, c, tag + what)
 
 
 @pytest.mark.parametrize("bw,sym", [(16, False), (16, True), (8, False), (4, True)])
@@ -1335,7 +1342,10 @@ def test_adaround_dw_step_equals_unfused_chain(N, C, H, K, stride, pad, dil, act
                                                           (4, 192, 32, 196, 0, False),
                                                           (32, 64, 384, 196, 2, True),
                                                           (6, 96, 576, 196, 1, False),
-                                                          (3, 160, 200, 100, 0, True)])
+                                                          (3, 160, 200, 100, 0, True),
+                                                          (4, 32, 2, 64 * 64, 0, True),
+                                                          (4, 24, 1, 32 * 32, 1, False),
+                                                          (4, 192, 3, 64, 0, False)])
 def test_adaround_pw_step_vs_torch(N, Cin, Cout, HW, act, with_bias):
     """aimet_adaround_pw_step (a 1x1 layer's AdaRound iteration in one pass over the cached rows)
     == the fp32 torch ops it replaces (index_select, W @ x, the reconstruction-loss gradient, the
@@ -1568,29 +1578,67 @@ def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatc
     assert ([e.to_tuple() for e, _ in fresh[0]]) == results[0][0]
 
 
-def test_calibrate_two_calls_bad_parameter_discards_the_activation_request():
-    """The two-call form launches the activations before it looks at the parameters: a parameter
-    it refuses (float16) raises TypeError after the activations' call, whose request is then
-    discarded (aimet_tq_get_encodings_finish with no outputs waits for its result copy and frees
-    it); the same quantizers calibrate normally afterwards, equal to fresh ones."""
+def test_calibrate_two_calls_bad_parameter_is_refused_before_any_launch():
+    """A parameter the two-call form refuses (float16) raises TypeError before anything is
+    launched: the activation quantizers keep the statistics of their earlier batch (their encodings
+    equal those of quantizers that never saw the refused call), and the same quantizers then
+    calibrate normally, equal to fresh ones."""
     from aimet_amd import calibration
     from aimet_amd.calibration import compute_encodings_resident
     g = torch.Generator(device=DEV).manual_seed(4)
     TFE = QuantizationMode.QUANTIZATION_TF_ENHANCED
     acts = [torch.randn(n, device=DEV, generator=g) for n in (1 << 20, 4099)]
+    acts2 = [a * 3 + 1 for a in acts]
     params = [torch.randn(16, 75, device=DEV, generator=g) * 0.1]
     aq = [AimetTensorQuantizer(TFE) for _ in acts]
     pq = [AimetTensorQuantizer(TFE, num_channels=16)]
+    before = compute_encodings_resident(aq, acts, pq, params, reset=True)
     dev = torch.device(DEV, torch.cuda.current_device())
     side = calibration._side_stream(dev)
     with pytest.raises(TypeError):
-        AimetTensorQuantizer.calibrateResidentAsync(aq, acts, pq, [params[0].half()], reset=True,
+        AimetTensorQuantizer.calibrateResidentAsync(aq, acts2, pq, [params[0].half()], reset=True,
                                                     main_stream=torch.cuda.current_stream(dev), side_stream=side)
-    got = compute_encodings_resident(aq, acts, pq, params, reset=True)
+    untouched = AimetTensorQuantizer.getEncodings(aq, 8, False, False, False)
+    assert [e.to_tuple() for e, _ in untouched] == [e.to_tuple() for e, _ in before[0]]
+    got = compute_encodings_resident(aq, acts2, pq, params, reset=True)
     fa, fp = [AimetTensorQuantizer(TFE) for _ in acts], [AimetTensorQuantizer(TFE, num_channels=16)]
-    want = compute_encodings_resident(fa, acts, fp, params)
+    want = compute_encodings_resident(fa, acts2, fp, params)
     assert [e.to_tuple() for e, _ in got[0]] == [e.to_tuple() for e, _ in want[0]]
     assert [x.to_tuple() for x in got[1][0][0]] == [x.to_tuple() for x in want[1][0][0]]
+
+
+@pytest.mark.parametrize("split", [True, False])
+def test_calibrate_non_contiguous_parameters_and_activations(monkeypatch, split):
+    """Non-contiguous inputs (a transposed weight, a channels_last conv weight, a strided
+    activation) are copied on the stream that consumes them: the encodings equal those of the
+    contiguous tensors, in the two-call and the one-call form, with torch's current stream a
+    different one from the call's main stream."""
+    from aimet_amd import calibration, tensor_quantizer
+    monkeypatch.setattr(tensor_quantizer, "_CAL_SPLIT", split)
+    g = torch.Generator(device=DEV).manual_seed(9)
+    TFE = QuantizationMode.QUANTIZATION_TF_ENHANCED
+    w_t = (torch.randn(300, 64, device=DEV, generator=g) * 0.1).t()          # [64, 300], not contiguous
+    w_cl = (torch.randn(96, 48, 3, 3, device=DEV, generator=g) * 0.05).to(memory_format=torch.channels_last)
+    act = torch.randn(4096, 513, device=DEV, generator=g)[:, :512]           # strided rows
+    assert not (w_t.is_contiguous() or w_cl.is_contiguous() or act.is_contiguous())
+    dev = torch.device(DEV, torch.cuda.current_device())
+    main = torch.cuda.Stream(dev)
+    side = calibration._side_stream(dev)
+
+    def run(acts, params):
+        aq = [AimetTensorQuantizer(TFE) for _ in acts]
+        pq = [AimetTensorQuantizer(TFE, num_channels=p.shape[0]) for p in params]
+        main.wait_stream(torch.cuda.current_stream(dev))
+        a_p, p_p, keep = AimetTensorQuantizer.calibrateResidentAsync(aq, acts, pq, params, reset=True,
+                                                                      main_stream=main, side_stream=side)
+        res = a_p.result(), p_p.result()
+        torch.cuda.current_stream(dev).wait_stream(main)
+        return [e.to_tuple() for e, _ in res[0]], [[x.to_tuple() for x in es] for es, _ in res[1]]
+
+    # the tensors' values are written on the current stream right before the call
+    got = run([act], [w_t, w_cl])
+    want = run([act.contiguous()], [w_t.contiguous(), w_cl.contiguous()])
+    assert got == want
 
 
 def test_compute_encodings_resident_equals_individual():
