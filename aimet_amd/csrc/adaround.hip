@@ -45,11 +45,13 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 // expf as torch's CPU vector code computes it (ATen Vectorized<float>::exp = Sleef expf_u10):
 // q = rint(d * log2(e)); s = d - q*ln2 in two FMA steps (Cody-Waite); a degree-6 polynomial in
-// Horner FMA form; 2^q applied as two exact power-of-two multiplies (Sleef's vldexp2, so the
-// subnormal results round as there); d < -104 -> 0, d > 100 -> inf. Every step is an IEEE op, so
-// the result is Sleef's bit for bit. A correctly rounded expf would differ from it in ~1% of inputs
-// and the difference reaches Wq unattenuated where floor(W/delta) + h - offset nearly cancels.
-__device__ __forceinline__ float torch_cpu_expf(float d)
+// Horner FMA form; 2^q applied; d < -104 -> 0, d > 100 -> inf. Every step is an IEEE op, so the
+// result is Sleef's bit for bit wherever it is normal. A correctly rounded expf would differ from
+// it in ~1% of inputs and the difference reaches Wq unattenuated where floor(W/delta) + h - offset
+// nearly cancels. Sleef applies 2^q as two power-of-two multiplies (vldexp2); one v_ldexp_f32 is
+// the same exact scaling except where the result is subnormal (d < -87.3), which only feeds
+// sigmoidf's e + 1 == 1 (tools/studies/sigmoid_fast_check.hip: all 2^32 sigmoid inputs equal).
+__device__ __forceinline__ float sigmoid_expf(float d)
 {
     const float qf = __builtin_rintf(d * 1.442695040888963407359924681001892137426645954152985934135449406931f);
     const int q    = (int) qf;
@@ -61,10 +63,7 @@ __device__ __forceinline__ float torch_cpu_expf(float d)
     u              = __builtin_fmaf(u, s, 0.0416664853692054748535156f);
     u              = __builtin_fmaf(u, s, 0.166666671633720397949219f);
     u              = __builtin_fmaf(u, s, 0.5f);
-    u              = 1.0f + __builtin_fmaf(s * s, u, s);
-    const int q1   = q >> 1, q2 = q - q1;
-    u              = u * __int_as_float((q1 + 127) << 23);
-    u              = u * __int_as_float((q2 + 127) << 23);
+    u              = __builtin_ldexpf(1.0f + __builtin_fmaf(s * s, u, s), q);
     u              = d < -104.0f ? 0.0f : u;
     return d > 100.0f ? __builtin_inff() : u;
 }
@@ -80,10 +79,18 @@ __device__ __forceinline__ float clamp_torch(float x, float lo, float hi)
     return m < hi ? m : hi;
 }
 
-// torch.sigmoid on the CPU (vectorized kernel): a = 0 - a; a = exp(a); a = a + 1; 1 / a
+// torch.sigmoid on the CPU (vectorized kernel): a = 0 - a; a = exp(a); a = a + 1; 1 / a. The IEEE
+// division 1 / y as v_rcp_f32 + one Newton step: equal to it for every y in [1, 2^126), the range
+// of e + 1 here below 2^126 (tools/studies/sigmoid_fast_check.hip, exhaustive); beyond, the division.
 __device__ __forceinline__ float sigmoidf(float a)
 {
-    return 1.0f / (torch_cpu_expf(0.0f - a) + 1.0f);
+    const float y = sigmoid_expf(0.0f - a) + 1.0f;
+    if (y < 0x1p126f)
+    {
+        const float r = __builtin_amdgcn_rcpf(y);
+        return __builtin_fmaf(__builtin_fmaf(-y, r, 1.0f), r, r);
+    }
+    return 1.0f / y;
 }
 
 // ---- torch's CPU pow(tensor, scalar) for float: Vectorized<float>::pow = Sleef_powf16_u10 (the
@@ -279,37 +286,150 @@ __device__ __forceinline__ float ada_fwd(float w, float a, float d, float o, con
     return (q + o) * d;
 }
 
-// dL/dalpha of Wq (clamp pass-through masks as torch autograd) + the rounding-loss gradient
-__device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, float o, const AdaParams& p, float rcp,
-                                         float& loss, uint32_t idx)
+// dL/dalpha of Wq without the rounding loss (clamp pass-through masks as torch autograd); also
+// returns what the rounding-loss terms need: sigmoid(alpha), x = 2h - 1 and whether h lies inside
+// its clamp (in_h). Outside it h is exactly 0 or 1, so |x| = 1 (or NaN) and the loss's pow needs
+// no logarithm.
+__device__ __forceinline__ float ada_bwd_base(float w, float a, float g, float d, float o, const AdaParams& p,
+                                              float rcp, float& sg, float& x, bool& in_h)
 {
-    const bool tail = idx >= p.vec_end;
     float t   = floor_div(w, d, rcp);
-    float sg  = sigmoidf(a);
+    sg        = sigmoidf(a);
     float pre = sg * kZmG + kGamma;
     float h   = clamp_torch(pre, 0.0f, 1.0f);
     float u   = t + h - o;
     // autograd of apply_adaround, op by op: d wq / d tq = g * delta; clamp_backward passes it where
     // min <= x <= max; the adds pass it on; h's clamp likewise; mul by (zeta - gamma) -> * 1.2f;
     // sigmoid_backward: (grad * (1 - s)) * s
-    const bool in_h = pre >= 0.0f && pre <= 1.0f;
-    float gh        = (u >= 0.0f && u <= p.qmax) ? g * d : 0.0f;
-    float ga        = ((in_h ? gh : 0.0f) * kZmG * (1.0f - sg)) * sg;
+    in_h     = pre >= 0.0f && pre <= 1.0f;
+    float gh = (u >= 0.0f && u <= p.qmax) ? g * d : 0.0f;
+    x        = 2.0f * h + -1.0f;
+    return ((in_h ? gh : 0.0f) * kZmG * (1.0f - sg)) * sg;
+}
+
+// the rounding loss's pow terms need Sleef's logkf only for |x| in (0, 1) outside the scalar tail
+// (pow01_log's other cases are exact constants, products or the tail's double pow)
+__device__ __forceinline__ bool ada_needs_log(float ax, bool tail)
+{
+    return !(ax == 0.0f || ax == 1.0f || tail);
+}
+
+// compute_round_loss's own graph (adaround_loss.py:97-110), summed into alpha's gradient as
+// autograd does: round_loss = reg * sum(1 - |2h - 1|^beta); grad -reg at the pow; pow_backward:
+// grad * (beta * x^(beta - 1)) (= pbm1 here); abs: * sgn(x); 2*h: * 2. Lanes outside h's clamp add
+// the selected +0 term as the full expression does.
+__device__ __forceinline__ float ada_bwd_round(float ga, float sg, float x, bool in_h, float pbm1, const AdaParams& p)
+{
+    float dpw = (-p.reg) * (p.beta * pbm1);
+    float dh  = (dpw * (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f))) * 2.0f;
+    return ga + ((in_h ? dh : 0.0f) * kZmG * (1.0f - sg)) * sg;
+}
+
+// dL/dalpha of Wq + the rounding-loss gradient, one element (the loss term added to `loss`)
+__device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, float o, const AdaParams& p, float rcp,
+                                         float& loss, uint32_t idx)
+{
+    float sg, x;
+    bool in_h;
+    float ga = ada_bwd_base(w, a, g, d, o, p, rcp, sg, x, in_h);
     if (p.reg != 0.0f)
     {
-        // compute_round_loss's own graph (adaround_loss.py:97-110), summed into alpha's gradient
-        // as autograd does: round_loss = reg * sum(1 - |2h - 1|^beta)
-        float x  = 2.0f * h + -1.0f;
-        float ax = fabsf(x);
-        const F2 l = sleef_logkf(ax == 0.0f || ax == 1.0f || tail ? 0.5f : ax);
-        if (p.want_loss)
-            loss += 1.0f - pow01_log(ax, p.beta, tail, l);
-        // grad -reg at the pow; pow_backward: grad * (beta * x^(beta - 1)); abs: * sgn(x); 2*h: * 2
-        float dpw = (-p.reg) * (p.beta * pow01_log(ax, p.beta_m1, tail, l));
-        float dh  = (dpw * (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f))) * 2.0f;
-        ga += ((in_h ? dh : 0.0f) * kZmG * (1.0f - sg)) * sg;
+        const bool tail = idx >= p.vec_end;
+        const float ax  = fabsf(x);
+        float pbm1      = 0.0f;
+        // only lanes inside h's clamp use the gradient's pow, and the logarithm only where it is not
+        // an exact case: a real branch, so a wave whose alphas all saturate skips the ~250 VALU
+        // ops of logkf + expkf (the skipped values were dead: the selects below drop them)
+        if (in_h || p.want_loss)
+        {
+            F2 l {0.0f, 0.0f};
+            if (ada_needs_log(ax, tail))
+                l = sleef_logkf(ax);
+            if (p.want_loss)
+                loss += 1.0f - pow01_log(ax, p.beta, tail, l);
+            if (in_h)
+                pbm1 = pow01_log(ax, p.beta_m1, tail, l);
+        }
+        ga = ada_bwd_round(ga, sg, x, in_h, pbm1, p);
     }
     return ga;
+}
+
+// pow01_log for |x| in {0, 1} (its exact early returns, whatever the exponent)
+__device__ __forceinline__ float pow01_exact(float ax, float e)
+{
+    return ax == 0.0f ? (e == 0.0f ? 1.0f : 0.0f) : 1.0f;
+}
+
+// E elements per lane whose rounding-loss pow terms are evaluated wave-compacted: every used
+// element (inside h's clamp, or any element when the loss is requested) whose |x| is not 0 or 1
+// -- the ones that need Sleef's logkf, or the scalar tail's double pow -- is packed densely into
+// this wave's LDS slot (ballot + mbcnt prefix; the tail ones stored negated), evaluated
+// ceil(count / 64) per lane, and read back. A wave then pays for the logarithm in proportion to
+// the elements that need it, not to the elements any of its lanes hold (saturated alphas in a
+// converging AdaRound loop are mixed with unsaturated ones in every wave). Every value is the
+// same function of |x| as pow01_log's, so the results are bit-identical to ada_bwd. The slot is
+// the wave's own, so the lanes only order their LDS accesses among themselves (wave_sync); the
+// wave's lanes must all call it. `wl` = 2 * 64 * E floats per wave.
+// the LDS writes of this wave's lanes visible to its other lanes (a wave's LDS operations complete
+// in order; the fences keep the compiler from moving accesses across)
+__device__ __forceinline__ void wave_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <int E>
+__device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool (&tail)[E], const bool (&use)[E],
+                                               const AdaParams& p, float* __restrict__ wl, float (&pbm1)[E],
+                                               float (&pb)[E])
+{
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t cnt        = 0;
+    int pos[E];
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+    {
+        const bool need       = use[k] && !(ax[k] == 0.0f || ax[k] == 1.0f);
+        const uint64_t ballot = __ballot(need);
+        const uint32_t below  = __builtin_amdgcn_mbcnt_hi((uint32_t) (ballot >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t) ballot, 0u));
+        pos[k] = need ? (int) (cnt + below) : -1;
+        if (need)   // |x| >= 0 or NaN: the sign bit marks a tail element
+            wl[cnt + below] = tail[k] ? -ax[k] : ax[k];
+        cnt += (uint32_t) __popcll(ballot);
+    }
+    wave_sync();
+    float* wl1 = wl + 64 * E;
+    for (uint32_t j = lane; j < cnt; j += 64)
+    {
+        const float sv  = wl[j];
+        const bool tl   = __builtin_signbit(sv);   // a NaN keeps its sign through the negation
+        const float v   = __builtin_fabsf(sv);
+        F2 l {0.0f, 0.0f};
+        if (!tl)
+            l = sleef_logkf(v);
+        wl[j] = pow01_log(v, p.beta_m1, tl, l);
+        if (p.want_loss)
+            wl1[j] = pow01_log(v, p.beta, tl, l);
+    }
+    wave_sync();
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+    {
+        if (pos[k] >= 0)
+        {
+            pbm1[k] = wl[pos[k]];
+            pb[k]   = p.want_loss ? wl1[pos[k]] : 0.0f;
+        }
+        else
+        {
+            pbm1[k] = pow01_exact(ax[k], p.beta_m1);
+            pb[k]   = pow01_exact(ax[k], p.beta);
+        }
+    }
+    wave_sync();   // the slot is reused by the next call
 }
 
 // 16-B streaming form: four consecutive elements share a channel (K % 4 == 0 or C == 1);
@@ -362,26 +482,70 @@ __device__ __forceinline__ float block_sum(float v)
     return r;
 }
 
-// backward: grid-stride over quads (bounded grid: one round-loss atomic per workgroup)
+// The round loss of one launch: reg x (the per-workgroup sums folded in workgroup order by the
+// workgroup that finishes last), one add to *round_loss per launch, so the value does not depend
+// on the workgroups' timing (ticket_alloc; `part` holds gridDim.x floats, handed over write-through:
+// common.hpp publish_f32). Without a ticket, one atomic add per workgroup. Called by every thread
+// of every workgroup.
+__device__ __forceinline__ void round_loss_add(float loss, float reg, float* __restrict__ round_loss,
+                                               float* __restrict__ part, unsigned* __restrict__ ticket)
+{
+    const float s = block_sum(loss);
+    if (!ticket)
+    {
+        if (threadIdx.x == 0)
+            atomicAdd(round_loss, reg * s);
+        return;
+    }
+    __shared__ int last;
+    if (threadIdx.x == 0)
+    {
+        publish_f32(part + blockIdx.x, s);
+        last = arrive_is_last(ticket, gridDim.x);
+    }
+    __syncthreads();
+    if (!last)
+        return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the ticket
+    float t = 0.0f;
+    for (uint32_t i = threadIdx.x; i < gridDim.x; i += kBlock)
+        t += consume_f32(part + i);
+    t = block_sum(t);
+    if (threadIdx.x == 0)
+    {
+        atomicAdd(round_loss, reg * t);
+        ticket_reset(ticket);
+    }
+}
+
+// backward: grid-stride over tiles of kBlock x U quads (U quads in flight per lane, 3 x 16-B loads
+// each; bounded grid: one round-loss atomic per workgroup); the loop bounds are uniform over the
+// workgroup (ada_round_pows synchronises it)
+template <int U>
 __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
                                                                   const f4* __restrict__ g, f4* __restrict__ ga,
                                                                   uint32_t nq, AdaChannel map,
                                                                   const float* __restrict__ delta,
                                                                   const float* __restrict__ offset, AdaParams p,
                                                                   float* __restrict__ round_loss,
-                                                                  const float* __restrict__ reg_beta)
+                                                                  const float* __restrict__ reg_beta,
+                                                                  float* __restrict__ loss_part,
+                                                                  unsigned* __restrict__ ticket)
 {
+    constexpr int E = 4 * U;
+    __shared__ float lds[kBlock / 64][2 * 64 * E];
     if (reg_beta)   // device-resident {reg, beta, beta - 1}: a HIP-graph replay per iteration
     {
         p.reg     = reg_beta[0];
         p.beta    = reg_beta[1];
         p.beta_m1 = reg_beta[2];
     }
-    float loss = 0.0f;
-    constexpr int U       = 4;   // quads in flight per lane (3 x 16-B loads each)
+    float* wl             = lds[threadIdx.x >> 6];
+    float loss            = 0.0f;
     const uint32_t stride = gridDim.x * kBlock * U;
-    for (uint32_t base = blockIdx.x * kBlock * U + threadIdx.x; base < nq; base += stride)
+    for (uint32_t tile = blockIdx.x * kBlock * U; tile < nq; tile += stride)
     {
+        const uint32_t base = tile + threadIdx.x;
         f4 wv[U], av[U], gv[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
@@ -392,28 +556,49 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
             av[u] = __builtin_nontemporal_load(alpha + j);
             gv[u] = __builtin_nontemporal_load(g + j);
         }
+        float r[E], sg[E], x[E], ax[E];
+        bool in_h[E], tail[E], valid[E];
 #pragma unroll
         for (int u = 0; u < U; ++u)
         {
             const uint32_t i = base + u * kBlock;
-            if (i >= nq)
-                break;
-            const uint32_t c = map.channel(4 * i);
+            const uint32_t c = map.channel(4 * (i < nq ? i : nq - 1));
             const float d = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(d);
-            f4 r;
-            r.x = ada_bwd(wv[u].x, av[u].x, gv[u].x, d, o, p, rcp, loss, 4 * i);
-            r.y = ada_bwd(wv[u].y, av[u].y, gv[u].y, d, o, p, rcp, loss, 4 * i + 1);
-            r.z = ada_bwd(wv[u].z, av[u].z, gv[u].z, d, o, p, rcp, loss, 4 * i + 2);
-            r.w = ada_bwd(wv[u].w, av[u].w, gv[u].w, d, o, p, rcp, loss, 4 * i + 3);
-            __builtin_nontemporal_store(r, ga + i);
+            const float wu[4] = {wv[u].x, wv[u].y, wv[u].z, wv[u].w}, au[4] = {av[u].x, av[u].y, av[u].z, av[u].w},
+                        gu[4] = {gv[u].x, gv[u].y, gv[u].z, gv[u].w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+            {
+                const int k = 4 * u + e;
+                r[k]     = ada_bwd_base(wu[e], au[e], gu[e], d, o, p, rcp, sg[k], x[k], in_h[k]);
+                ax[k]    = fabsf(x[k]);
+                valid[k] = i < nq;
+                in_h[k]  = in_h[k] && valid[k];
+                tail[k]  = 4 * i + e >= p.vec_end;
+            }
+        }
+        if (p.reg != 0.0f)   // uniform: a kernel argument or the device-resident value
+        {
+            float pbm1[E], pb[E];
+            ada_round_pows<E>(ax, tail, p.want_loss ? valid : in_h, p, wl, pbm1, pb);
+#pragma unroll
+            for (int k = 0; k < E; ++k)
+            {
+                if (p.want_loss && valid[k])
+                    loss += 1.0f - pb[k];
+                r[k] = ada_bwd_round(r[k], sg[k], x[k], in_h[k], pbm1[k], p);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+        {
+            const uint32_t i = base + u * kBlock;
+            if (i < nq)
+                __builtin_nontemporal_store(f4 {r[4 * u], r[4 * u + 1], r[4 * u + 2], r[4 * u + 3]}, ga + i);
         }
     }
     if (p.reg != 0.0f && round_loss)
-    {
-        float s = block_sum(loss);
-        if (threadIdx.x == 0)
-            atomicAdd(round_loss, p.reg * s);
-    }
+        round_loss_add(loss, p.reg, round_loss, loss_part, ticket);
 }
 
 __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __restrict__ w,
@@ -423,7 +608,8 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
                                                               const float* __restrict__ delta,
                                                               const float* __restrict__ offset, AdaParams p,
                                                               float* __restrict__ round_loss,
-                                                              const float* __restrict__ reg_beta)
+                                                              const float* __restrict__ reg_beta,
+                                                              float* __restrict__ loss_part, unsigned* __restrict__ ticket)
 {
     if (reg_beta)
     {
@@ -438,12 +624,39 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
         ga[i]      = ada_bwd(w[i], alpha[i], g[i], delta[c], offset[c], p, __builtin_amdgcn_rcpf(delta[c]), loss, i);
     }
     if (p.reg != 0.0f && round_loss)
-    {
-        float s = block_sum(loss);
-        if (threadIdx.x == 0)
-            atomicAdd(round_loss, p.reg * s);
-    }
+        round_loss_add(loss, p.reg, round_loss, loss_part, ticket);
 }
+
+// the round loss's per-workgroup partials and completion ticket for one launch (round_loss_add);
+// none when no loss is requested. The partials are released after the launch that uses them.
+struct LossFold
+{
+    float* part      = nullptr;
+    unsigned* ticket = nullptr;
+    hipStream_t s;
+    LossFold(const float* round_loss, unsigned grid, hipStream_t st) : s(st)
+    {
+        if (!round_loss)
+            return;
+        ticket = ticket_alloc(st);
+        if (ticket)
+            part = static_cast<float*>(scratch_alloc(sizeof(float) * grid, st));
+    }
+    ~LossFold()
+    {
+        if (!part)
+            return;
+        try
+        {
+            scratch_free(part, s);
+        }
+        catch (...)   // a failing event record: the block is leaked, never handed out again
+        {
+        }
+    }
+    LossFold(const LossFold&)            = delete;
+    LossFold& operator=(const LossFold&) = delete;
+};
 
 bool aligned16(const void* p)
 {
@@ -485,7 +698,9 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                                                                    const int64_t* __restrict__ it_next,
                                                                    int64_t* __restrict__ it_cur, AdamArgs adam,
                                                                    float* __restrict__ round_loss,
-                                                                   float* __restrict__ wq_next)
+                                                                   float* __restrict__ wq_next,
+                                                                   float* __restrict__ loss_part,
+                                                                   unsigned* __restrict__ ticket)
 {
     const int64_t step = it_next[0];
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -501,22 +716,53 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
     float loss         = 0.0f;
     if (VEC)
     {
+        // one quad per lane; the rounding-loss pows wave-compacted (ada_round_pows), so the loop
+        // bounds are uniform over the workgroup
+        __shared__ float lds[kBlock / 64][2 * 64 * 4];
+        float* wl         = lds[threadIdx.x >> 6];
         const uint32_t nq = n / 4;
-        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < nq; i += gridDim.x * kBlock)
+        for (uint32_t i0 = blockIdx.x * kBlock; i0 < nq; i0 += gridDim.x * kBlock)
         {
-            const uint32_t c = map.channel(4 * i);
+            const uint32_t i  = i0 + threadIdx.x;
+            const bool valid  = i < nq;
+            const uint32_t ic = valid ? i : nq - 1;   // clamped (never stored)
+            const uint32_t c  = map.channel(4 * ic);
             const float d = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(d);
-            f4 wv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(w) + i);
-            f4 gv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + i);
-            f4 av       = reinterpret_cast<const f4*>(alpha)[i];
-            f4 mv       = reinterpret_cast<const f4*>(exp_avg)[i];
-            f4 vv       = reinterpret_cast<const f4*>(exp_avg_sq)[i];
-            float m[4] = {mv.x, mv.y, mv.z, mv.w}, v[4] = {vv.x, vv.y, vv.z, vv.w};
+            f4 wv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(w) + ic);
+            f4 gv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + ic);
+            f4 av       = reinterpret_cast<const f4*>(alpha)[ic];
             float a[4] = {av.x, av.y, av.z, av.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
+            float r[4], sg[4], x[4], ax[4];
+            bool in_h[4], tail[4], use[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                a[k] = adam_elem(a[k], ada_bwd(ww[k], a[k], gg[k], d, o, p, rcp, loss, 4 * i + k), m[k], v[k], adam, bc1,
-                                 bc2s);
+            {
+                r[k]    = ada_bwd_base(ww[k], a[k], gg[k], d, o, p, rcp, sg[k], x[k], in_h[k]);
+                ax[k]   = fabsf(x[k]);
+                in_h[k] = in_h[k] && valid;
+                tail[k] = 4 * ic + k >= p.vec_end;
+                use[k]  = p.want_loss ? valid : in_h[k];
+            }
+            if (p.reg != 0.0f)   // uniform: this iteration's device-resident value
+            {
+                float pbm1[4], pb[4];
+                ada_round_pows<4>(ax, tail, use, p, wl, pbm1, pb);
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                {
+                    if (p.want_loss && valid)
+                        loss += 1.0f - pb[k];
+                    r[k] = ada_bwd_round(r[k], sg[k], x[k], in_h[k], pbm1[k], p);
+                }
+            }
+            if (!valid)
+                continue;
+            f4 mv      = reinterpret_cast<const f4*>(exp_avg)[i];
+            f4 vv      = reinterpret_cast<const f4*>(exp_avg_sq)[i];
+            float m[4] = {mv.x, mv.y, mv.z, mv.w}, v[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                a[k] = adam_elem(a[k], r[k], m[k], v[k], adam, bc1, bc2s);
             reinterpret_cast<f4*>(alpha)[i]      = f4 {a[0], a[1], a[2], a[3]};
             reinterpret_cast<f4*>(exp_avg)[i]    = f4 {m[0], m[1], m[2], m[3]};
             reinterpret_cast<f4*>(exp_avg_sq)[i] = f4 {v[0], v[1], v[2], v[3]};
@@ -541,11 +787,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
         }
     }
     if (p.reg != 0.0f && round_loss)
-    {
-        float s = block_sum(loss);
-        if (threadIdx.x == 0)
-            atomicAdd(round_loss, p.reg * s);
-    }
+        round_loss_add(loss, p.reg, round_loss, loss_part, ticket);
 }
 
 // this iteration's batch: rows idx_all[it][b] of the cached inputs / outputs -> dst_in[b] /
@@ -760,20 +1002,41 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
         AdaParams p {(float) ((1ull << bw) - 1), (float) reg, (float) beta, (float) (beta - 1.0), 1,
                      (uint32_t) (n - n % 32), round_loss != nullptr};
+        hipStream_t st = as_stream(stream);
         if ((C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) && aligned16(g) &&
             aligned16(ga))
         {
             uint32_t nq = (uint32_t) (n / 4);
-            int64_t blocks = ceil_div(nq, kBlock * 4);
-            adaround_bwd_vec_kernel<<<(unsigned) (blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid), kBlock, 0,
-                                      as_stream(stream)>>>(
-                reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),
-                reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss, reg_beta);
+            // quads in flight per lane (AIMET_ADA_BWD_U = 1 / 2 / 4 for tuning; 2 measured best)
+            static const int U = [] {
+                const char* e = getenv("AIMET_ADA_BWD_U");
+                const int u   = e ? atoi(e) : 2;
+                return u == 1 || u == 4 ? u : 2;
+            }();
+            int64_t blocks    = ceil_div(nq, kBlock * U);
+            const unsigned gx = (unsigned) (blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid);
+            LossFold lf(round_loss, gx, st);
+            auto launch = [&](auto kernel) {
+                kernel<<<gx, kBlock, 0, st>>>(
+                    reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),
+                    reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss, reg_beta, lf.part, lf.ticket);
+            };
+            if (U == 1)
+                launch(adaround_bwd_vec_kernel<1>);
+            else if (U == 4)
+                launch(adaround_bwd_vec_kernel<4>);
+            else
+                launch(adaround_bwd_vec_kernel<2>);
+            AIMET_LAUNCH_CHECK();
         }
         else
-            adaround_bwd_kernel<<<stream_blocks(n, kBlock), kBlock, 0, as_stream(stream)>>>(
-                w, alpha, g, ga, (uint32_t) n, map, delta, offset, p, round_loss, reg_beta);
-        AIMET_LAUNCH_CHECK();
+        {
+            const unsigned gx = stream_blocks(n, kBlock);
+            LossFold lf(round_loss, gx, st);
+            adaround_bwd_kernel<<<gx, kBlock, 0, st>>>(w, alpha, g, ga, (uint32_t) n, map, delta, offset, p, round_loss,
+                                                      reg_beta, lf.part, lf.ticket);
+            AIMET_LAUNCH_CHECK();
+        }
     });
 }
 
@@ -980,14 +1243,16 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
         const int64_t items = vec ? n / 4 : n;
         int64_t blocks      = ceil_div(items, kBlock);
         blocks              = blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid;
+        hipStream_t st = as_stream(stream);
+        LossFold lf(round_loss, (unsigned) blocks, st);
         if (vec)
-            adaround_bwd_adam_kernel<true><<<(unsigned) blocks, kBlock, 0, as_stream(stream)>>>(
+            adaround_bwd_adam_kernel<true><<<(unsigned) blocks, kBlock, 0, st>>>(
                 w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss, wq_next);
+                it_cur, a, round_loss, wq_next, lf.part, lf.ticket);
         else
-            adaround_bwd_adam_kernel<false><<<(unsigned) blocks, kBlock, 0, as_stream(stream)>>>(
+            adaround_bwd_adam_kernel<false><<<(unsigned) blocks, kBlock, 0, st>>>(
                 w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss, wq_next);
+                it_cur, a, round_loss, wq_next, lf.part, lf.ticket);
         AIMET_LAUNCH_CHECK();
     });
 }

@@ -140,6 +140,42 @@ struct FastDiv
 
 // glibc fminf/fmaxf (x86-64): a NaN operand yields the other operand; otherwise
 // minss/maxss, i.e. the SECOND operand on ties (matters for +-0).
+// ---- hand-off of per-workgroup partials to the last-arriving workgroup (one launch) ------------
+// The per-XCD L2s are not coherent and a CU's L1 is never refreshed by another CU's stores. The
+// partials are stored write-through (agent-scope relaxed atomic store: a `global_store ... sc1`),
+// the storing wave drains them (s_waitcnt vmcnt(0)) before its ticket add, and the last arriver
+// reads them with agent-scope loads (`sc1`, past L1 and L2): no release fence (an agent release is
+// a whole-L2 write-back, buffer_wbl2, per workgroup) and no acquire. MI355X_MICROARCH.md
+// § visibility, cdna_hip_programming.md Guideline 16 (R1).
+__device__ __forceinline__ void publish_f32(float* p, float v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float consume_f32(const float* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void publish_u64(uint64_t* p, uint64_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t consume_u64(const uint64_t* p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// the calling lane's published partials drained, then its ticket: true for the last of
+// `arrivals` (one call per workgroup, from the lane that published)
+__device__ __forceinline__ bool arrive_is_last(unsigned* ticket, unsigned arrivals)
+{
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == arrivals - 1;
+}
+// the last arriver leaves the ticket at zero for its next user (ticket_alloc)
+__device__ __forceinline__ void ticket_reset(unsigned* ticket)
+{
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ float glibc_fminf(float x, float y)
 {
     return (x < y || __builtin_isnan(y)) ? x : y;
@@ -156,6 +192,8 @@ void* upload_async(const void* src, size_t bytes, hipStream_t s);
 // an event recorded after their consumers has completed (upload.cpp; the pool let a job table be
 // reused under a running kernel: tests/cpp/sanitize_host.cpp).
 void* scratch_alloc(size_t bytes, hipStream_t s);
+// `count` consecutive zeroed completion counters for last-workgroup folds, or nullptr: upload.cpp
+unsigned* ticket_alloc(hipStream_t s, unsigned count = 1);
 void scratch_free(void* p, hipStream_t s);
 
 struct QdqParams

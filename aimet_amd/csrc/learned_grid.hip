@@ -437,6 +437,90 @@ __device__ __forceinline__ Sums block_reduce(Sums s)
     return r;
 }
 
+// the encoding gradients of channel c from its sums {A, B, D} (asymmetric / symmetric_gradients,
+// the reference's torch expressions element by element); gmin == nullptr: not requested
+struct LgRange
+{
+    const float* emin;
+    const float* emax;
+    const float* delta;
+    float* gmin;
+    float* gmax;
+    float steps, half_floor;
+    int sym;
+};
+
+__device__ __forceinline__ void range_grads_one(float A, float B, float D, uint32_t c, const LgRange& r)
+{
+    const float gss = A - B;
+    if (r.sym)
+    {
+        const float g = gss / r.half_floor;
+        r.gmax[c]     = g;
+        r.gmin[c]     = -g;
+        return;
+    }
+    const float mn = r.emin[c], mx = r.emax[c];
+    const float term1 = gss / r.steps;
+    const float w     = mx - mn;
+    const float term2 = (r.steps / (w * w)) * (r.delta[c] * D);
+    r.gmin[c]         = -term1 + mx * term2;
+    r.gmax[c]         = term1 - mn * term2;
+}
+
+// the nparts partial triples folded as one triple: lane i sums parts i, i + kBlock, ... in order,
+// then the fixed shuffle tree of block_reduce -- one result whatever the scheduling; the range
+// gradients follow when requested. Called by every thread of one workgroup. The partials are
+// read with agent-scope loads (written write-through by other workgroups of the same launch).
+__device__ __forceinline__ void fold_partials(const float* __restrict__ partial, int64_t nparts,
+                                              float* __restrict__ sums, const LgRange& range)
+{
+    Sums s {0, 0, 0};
+    for (int64_t i = threadIdx.x; i < nparts; i += kBlock)
+    {
+        s.a += consume_f32(partial + 3 * i + 0);
+        s.b += consume_f32(partial + 3 * i + 1);
+        s.d += consume_f32(partial + 3 * i + 2);
+    }
+    Sums t = block_reduce(s);
+    if (threadIdx.x == 0)
+    {
+        sums[0] = t.a;
+        sums[1] = t.b;
+        sums[2] = t.d;
+        if (range.gmin)
+            range_grads_one(t.a, t.b, t.d, 0, range);
+    }
+}
+
+// a tile's partial triple, stored write-through for the fold (fold_partials)
+__device__ __forceinline__ void publish_sums(float* p, const Sums& t)
+{
+    publish_f32(p + 0, t.a);
+    publish_f32(p + 1, t.b);
+    publish_f32(p + 2, t.d);
+}
+
+// The per-tensor backward's fold in the workgroup that finishes last (no second launch): thread
+// 0 of each workgroup (the one that published its tiles' partials) drains them and takes a
+// ticket; the workgroup drawing the last one runs fold_partials -- the same arithmetic as
+// lg_bwd_fold_one, so the same bits -- and leaves the ticket at zero (ticket_alloc). Called by every
+// thread of every workgroup; none waits for another, so they need not be co-resident.
+__device__ __forceinline__ void fold_in_last_workgroup(const float* partial, int64_t nparts, float* sums,
+                                                       const LgRange& range, unsigned* ticket)
+{
+    __shared__ int last;
+    if (threadIdx.x == 0)
+        last = arrive_is_last(ticket, gridDim.x);
+    __syncthreads();
+    if (!last)
+        return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the ticket
+    fold_partials(partial, nparts, sums, range);
+    if (threadIdx.x == 0)
+        ticket_reset(ticket);
+}
+
 // per-tensor (C == 1), tile form: workgroup b owns the kLgTile consecutive elements
 // [b * kLgTile, (b + 1) * kLgTile); lane l of it takes the 8-element groups u * kBlock + l
 // (u < kLgTileSteps), every load of the tile issued before any arithmetic. The per-lane sums run
@@ -461,7 +545,9 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
                                                                const float* __restrict__ g, float* __restrict__ gx,
                                                                int64_t n, const float* __restrict__ delta,
                                                                const float* __restrict__ offset, float steps,
-                                                               float* __restrict__ sums, int vec, int64_t ntiles)
+                                                               float* __restrict__ sums, int vec, int64_t ntiles,
+                                                               float* __restrict__ folded, LgRange range,
+                                                               unsigned* __restrict__ ticket)
 {
     constexpr int64_t kTile = (int64_t) kBlock * 8 * STEPS;
     const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
@@ -518,12 +604,10 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
         }
         Sums t = block_reduce(s);
         if (threadIdx.x == 0)
-        {
-            sums[3 * tile + 0] = t.a;
-            sums[3 * tile + 1] = t.b;
-            sums[3 * tile + 2] = t.d;
-        }
+            publish_sums(sums + 3 * tile, t);
     }
+    if (ticket)   // uniform: the fold in the last workgroup (else lg_bwd_fold_one follows)
+        fold_in_last_workgroup(sums, ntiles, folded, range, ticket);
 }
 
 // Launch shape of the per-tensor backward kernels (fp32 and 16-bit use the same, so their sums
@@ -582,59 +666,11 @@ void lg_bwd_dispatch(int steps, int mode, F&& f)
         with_mode(std::integral_constant<int, kLgTileSteps> {});
 }
 
-// the encoding gradients of channel c from its sums {A, B, D} (asymmetric / symmetric_gradients,
-// the reference's torch expressions element by element); gmin == nullptr: not requested
-struct LgRange
-{
-    const float* emin;
-    const float* emax;
-    const float* delta;
-    float* gmin;
-    float* gmax;
-    float steps, half_floor;
-    int sym;
-};
-
-__device__ __forceinline__ void range_grads_one(float A, float B, float D, uint32_t c, const LgRange& r)
-{
-    const float gss = A - B;
-    if (r.sym)
-    {
-        const float g = gss / r.half_floor;
-        r.gmax[c]     = g;
-        r.gmin[c]     = -g;
-        return;
-    }
-    const float mn = r.emin[c], mx = r.emax[c];
-    const float term1 = gss / r.steps;
-    const float w     = mx - mn;
-    const float term2 = (r.steps / (w * w)) * (r.delta[c] * D);
-    r.gmin[c]         = -term1 + mx * term2;
-    r.gmax[c]         = term1 - mn * term2;
-}
-
-// sums[0..2] = the nparts partial triples, lane i taking parts i, i + kBlock, ... in order, then
-// the fixed shuffle tree of block_reduce: one result whatever the scheduling; the range
-// gradients follow in the same launch when requested
+// the per-tensor backward's fold as its own launch (graph capture: no ticket)
 __global__ __launch_bounds__(kBlock) void lg_bwd_fold_one(const float* __restrict__ partial, int nparts,
                                                           float* __restrict__ sums, LgRange range)
 {
-    Sums s {0, 0, 0};
-    for (int i = threadIdx.x; i < nparts; i += kBlock)
-    {
-        s.a += partial[3 * i + 0];
-        s.b += partial[3 * i + 1];
-        s.d += partial[3 * i + 2];
-    }
-    Sums t = block_reduce(s);
-    if (threadIdx.x == 0)
-    {
-        sums[0] = t.a;
-        sums[1] = t.b;
-        sums[2] = t.d;
-        if (range.gmin)
-            range_grads_one(t.a, t.b, t.d, 0, range);
-    }
+    fold_partials(partial, nparts, sums, range);
 }
 
 // per-channel: one workgroup per channel of [outer][C][K], sums written directly
@@ -869,18 +905,22 @@ __global__ __launch_bounds__(BLOCK) void lg_fwd16_kernel(const unsigned short* _
                                                          LgEnc enc, int64_t ntiles)
 {
     constexpr int64_t kTile = (int64_t) BLOCK * 8 * V;
+    // the first tile's loads go out before the encoding is read (they do not depend on it; on a
+    // small call the two latencies in a row were most of the kernel)
+    const int64_t nvec = vec ? n / kTile : 0;
+    int64_t tile       = blockIdx.x;
+    u16x8 cur[V];
+    if (tile < nvec)
+        lg_fwd16_load<IO, V, BLOCK, NT>(x, tile, cur);
     float d, o;
     // element 0's thread (tile 0 is workgroup 0's first) stores the encoding
     enc.get(0, blockIdx.x == 0 && threadIdx.x == 0 ? 0u : 1u, delta, offset, d, o);
     const float rd   = lg_recip(d);
     const float xmax = 0x1p59f * __builtin_fabsf(d);
     const bool fast  = lg_fast_enc(o, rd);
-    const int64_t nfull = (vec && fast) ? n / kTile : 0;
-    int64_t tile = blockIdx.x;
+    const int64_t nfull = fast ? nvec : 0;
     if (tile < nfull)
     {
-        u16x8 cur[V];
-        lg_fwd16_load<IO, V, BLOCK, NT>(x, tile, cur);
         for (; tile < nfull; tile += gridDim.x)
         {
             u16x8 nxt[V];
@@ -937,17 +977,22 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
                                                                  unsigned short* __restrict__ gx, int64_t n,
                                                                  const float* __restrict__ delta,
                                                                  const float* __restrict__ offset, float steps,
-                                                                 float* __restrict__ partial, int vec, int64_t ntiles)
+                                                                 float* __restrict__ partial, int vec, int64_t ntiles,
+                                                                 float* __restrict__ folded, LgRange range,
+                                                                 unsigned* __restrict__ ticket)
 {
     constexpr int64_t kTile = (int64_t) kBlock * 8 * STEPS;
+    // the first tile's loads go out before the encoding is read: they do not depend on it, and on
+    // a small call (a few tiles per CU) the two latencies in a row were most of the kernel
+    const int64_t nvec = vec ? n / kTile : 0;
+    int64_t tile = blockIdx.x;
+    u16x8 a[STEPS], b[STEPS];
+    if (tile < nvec)
+        lg_bwd16_load<STEPS, NT>(x, g, tile * kTile, a, b);
     const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
     // full tiles of an encoding lg_fast_enc accepts take the vector path; the rest (the partial
     // last tile, unaligned pointers, an encoding for the division) the element path
-    const int64_t nfull = (lg_fast_enc(o, rcp) && vec) ? n / kTile : 0;
-    int64_t tile = blockIdx.x;
-    u16x8 a[STEPS], b[STEPS];
-    if (tile < nfull)
-        lg_bwd16_load<STEPS, NT>(x, g, tile * kTile, a, b);
+    const int64_t nfull = lg_fast_enc(o, rcp) ? nvec : 0;
     for (; tile < ntiles; tile += gridDim.x)
     {
         const int64_t base = tile * kTile;
@@ -1001,12 +1046,10 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
         }
         Sums t = block_reduce(s);
         if (threadIdx.x == 0)
-        {
-            partial[3 * tile + 0] = t.a;
-            partial[3 * tile + 1] = t.b;
-            partial[3 * tile + 2] = t.d;
-        }
+            publish_sums(partial + 3 * tile, t);
     }
+    if (ticket)   // uniform: the fold in the last workgroup (else lg_bwd_fold_one follows)
+        fold_in_last_workgroup(partial, ntiles, folded, range, ticket);
 }
 
 // ---- the small per-channel vectors around the passes, one launch each -----------------------
@@ -1339,13 +1382,18 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             const LgBwdLaunch L = lg_bwd_launch(n);
             float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
             const int v         = vec ? 1 : 0;
+            // the fold in the kernel's last workgroup; its own launch when there is no ticket
+            unsigned* ticket = ticket_alloc(s);
             lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
                 lg_bwd_tensor_kernel<decltype(st)::value, decltype(md)::value><<<L.grid, kBlock, 0, s>>>(
-                    x, grad, grad_x, n, delta, offset, num_steps, partial, v, L.ntiles);
+                    x, grad, grad_x, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
             });
             AIMET_LAUNCH_CHECK();
-            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
-            AIMET_LAUNCH_CHECK();
+            if (!ticket)
+            {
+                lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
+                AIMET_LAUNCH_CHECK();
+            }
             scratch_free(partial, s);
             return;
         }
@@ -1676,24 +1724,29 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         auto gs = static_cast<const unsigned short*>(grad);
         auto os = static_cast<unsigned short*>(grad_x);
         const int v = vec ? 1 : 0;
+        // the fold in the kernel's last workgroup; its own launch when there is no ticket
+        unsigned* ticket = ticket_alloc(s);
         lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
             constexpr int ST = decltype(st)::value, MD = decltype(md)::value;
             if (io_dtype == IO_F16 && lg16_nt())
-                lg_bwd16_tensor_kernel<IO_F16, ST, MD><<<L.grid16, kBlock, 0, s>>>(xs, gs, os, n, delta, offset, num_steps,
-                                                                                 partial, v, L.ntiles);
+                lg_bwd16_tensor_kernel<IO_F16, ST, MD><<<L.grid16, kBlock, 0, s>>>(
+                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
             else if (io_dtype == IO_F16)
                 lg_bwd16_tensor_kernel<IO_F16, ST, MD, false><<<L.grid16, kBlock, 0, s>>>(
-                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles);
+                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
             else if (lg16_nt())
-                lg_bwd16_tensor_kernel<IO_BF16, ST, MD><<<L.grid16, kBlock, 0, s>>>(xs, gs, os, n, delta, offset,
-                                                                                  num_steps, partial, v, L.ntiles);
+                lg_bwd16_tensor_kernel<IO_BF16, ST, MD><<<L.grid16, kBlock, 0, s>>>(
+                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
             else
                 lg_bwd16_tensor_kernel<IO_BF16, ST, MD, false><<<L.grid16, kBlock, 0, s>>>(
-                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles);
+                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
         });
         AIMET_LAUNCH_CHECK();
-        lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
-        AIMET_LAUNCH_CHECK();
+        if (!ticket)
+        {
+            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
+            AIMET_LAUNCH_CHECK();
+        }
         scratch_free(partial, s);
     });
 }

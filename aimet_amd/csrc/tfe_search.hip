@@ -9,6 +9,7 @@
 // shared header tfe_core.hpp, compiled for the host and the device from one source (bit-exact).
 #include "tfe_core.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -52,9 +53,16 @@ struct TfeJob
     int64_t start;   // first global channel of this job
 };
 
-template <int BLOCK>
-__global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : 7) void tfe_search_kernel(TfeJob one, const TfeJob* __restrict__ jobs, int njobs,
-                                                           int64_t total, int bw, int sym, int strict, int unsign)
+// Channel g's candidates over `splits` workgroups (few channels: the activations' quantizers of a
+// batch): workgroup (g, s) takes candidates s * BLOCK + lane, s * BLOCK + lane + BLOCK * splits, ...,
+// publishes its first minimum (cost, index) write-through, and the last of the g's workgroups to
+// arrive (tickets[g]) takes the first minimum of those -- `better` orders by (cost, index), so the
+// choice is the one-workgroup argmin's -- and finishes the encoding. splits == 1: one workgroup
+// per channel, no hand-off. SYMFORM: tfe::cost's branch-free symmetric loops (same sums).
+template <int BLOCK, bool SYMFORM>
+__global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : (BLOCK == 64 ? 8 : 7)) void tfe_search_kernel(
+    TfeJob one, const TfeJob* __restrict__ jobs, int njobs, int64_t total, int bw, int sym, int strict, int unsign,
+    int splits, uint64_t* __restrict__ part, unsigned* __restrict__ tickets)
 {
     constexpr int kW = BLOCK / 64;
     __shared__ double pdf_c[tfe::kBins];
@@ -73,8 +81,10 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : 7) void tfe_search_kernel
             tfe::fseq_asym(fseq);
     }
     const int lane = threadIdx.x & 63;
-    for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
+    for (int64_t gs = blockIdx.x; gs < total * splits; gs += gridDim.x)
     {
+        const int64_t g = gs / splits;
+        const int sp    = (int) (gs - g * splits);
         TfeJob j = one;
         if (jobs)
         {
@@ -92,7 +102,7 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : 7) void tfe_search_kernel
         const int64_t c = g - j.start;
         if (!j.pdf_init[c])
         {
-            if (threadIdx.x == 0)
+            if (threadIdx.x == 0 && sp == 0)
             {
                 // statistics updated but all data zero (TfEnhancedEncodingAnalyzer.cpp:86-99)
                 int isteps = (int) (float) (ldexp(1.0, bw) - 1);
@@ -160,13 +170,13 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : 7) void tfe_search_kernel
         const tfe::Bins B {start, step, cf, pdf_c, cd_c, cf_c, pos, nnz};
 
         Best b {0.0, -1, -1.0f, -1};
-        for (int t = threadIdx.x; t < st.ncand; t += BLOCK)
+        for (int t = threadIdx.x + sp * BLOCK; t < st.ncand; t += BLOCK * splits)
         {
             float dl;
             int o;
             if (!tfe::candidate(st, fseq, t, dl, o))
                 continue;
-            double cst = tfe::cost<BLOCK == 128>(B, bw, dl, o);
+            double cst = tfe::cost<SYMFORM>(B, bw, dl, o);
             if (!(cst < DBL_MAX))
                 continue;
             Best me {cst, t, dl, o};
@@ -192,10 +202,36 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : 7) void tfe_search_kernel
             for (int w = 1; w < kW; ++w)
                 if (better(wbest[w], b))
                     b = wbest[w];
-            float bd = b.idx >= 0 ? b.delta : -1.0f;
-            int bo   = b.idx >= 0 ? b.offset : -1;
-            tfe::Result r = tfe::finish(st, bd, bo);
-            j.out[c]      = aimet_tf_encoding {r.min, r.max, r.delta, r.offset, bw};
+            bool finish = splits == 1;
+            if (!finish)
+            {
+                uint64_t* my = part + 2 * gs;
+                publish_u64(my, (uint64_t) __double_as_longlong(b.cost));
+                publish_u64(my + 1, (uint64_t) (uint32_t) b.idx);
+                if (arrive_is_last(tickets + g, (unsigned) splits))
+                {
+                    finish = true;
+                    b      = Best {0.0, -1, -1.0f, -1};
+                    for (int q = 0; q < splits; ++q)
+                    {
+                        const uint64_t* pq = part + 2 * (g * splits + q);
+                        Best o {__longlong_as_double((long long) consume_u64(pq)), (int) (uint32_t) consume_u64(pq + 1),
+                                -1.0f, -1};
+                        if (better(o, b))
+                            b = o;
+                    }
+                    if (b.idx >= 0)   // the winner's delta / offset, as its lane formed them
+                        tfe::candidate(st, fseq, b.idx, b.delta, b.offset);
+                    ticket_reset(tickets + g);
+                }
+            }
+            if (finish)
+            {
+                float bd = b.idx >= 0 ? b.delta : -1.0f;
+                int bo   = b.idx >= 0 ? b.offset : -1;
+                tfe::Result r = tfe::finish(st, bd, bo);
+                j.out[c]      = aimet_tf_encoding {r.min, r.max, r.delta, r.offset, bw};
+            }
         }
         __syncthreads();
     }
@@ -212,15 +248,40 @@ int search_grid_cap()
     return v;
 }
 
+// channels below which each one's candidates are split over one-wave workgroups (the activations'
+// quantizers of a batch: ResNet-50's 55 asymmetric searches took 58 us as 55 workgroups)
+constexpr int64_t kTfeSplitBelow = 512;
+
 void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t total, int bw, bool sym, bool strict,
                    bool unsign, hipStream_t s)
 {
-    const int cap  = search_grid_cap();
+    const int cap = search_grid_cap();
+    if (total < kTfeSplitBelow && getenv("AIMET_TFE_NO_SPLIT") == nullptr)
+    {
+        const int splits  = (int) ceil_div(sym ? tfe::kSymF : tfe::kMaxCand, 64);
+        unsigned* tickets = ticket_alloc(s, (unsigned) total);
+        if (tickets)
+        {
+            auto* part     = static_cast<uint64_t*>(scratch_alloc(sizeof(uint64_t) * 2 * total * splits, s));
+            const int grid = (int) std::min<int64_t>(total * splits, cap);
+            if (sym)
+                tfe_search_kernel<64, true><<<grid, 64, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign, splits,
+                                                              part, tickets);
+            else
+                tfe_search_kernel<64, false><<<grid, 64, 0, s>>>(one, jobs, njobs, total, bw, 0, strict, unsign,
+                                                               splits, part, tickets);
+            AIMET_LAUNCH_CHECK();
+            scratch_free(part, s);
+            return;
+        }
+    }
     const int grid = (int) (total < cap ? total : cap);
     if (sym)
-        tfe_search_kernel<128><<<grid, 128, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign);
+        tfe_search_kernel<128, true><<<grid, 128, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign, 1, nullptr,
+                                                        nullptr);
     else
-        tfe_search_kernel<384><<<grid, 384, 0, s>>>(one, jobs, njobs, total, bw, 0, strict, unsign);
+        tfe_search_kernel<384, false><<<grid, 384, 0, s>>>(one, jobs, njobs, total, bw, 0, strict, unsign, 1, nullptr,
+                                                         nullptr);
     AIMET_LAUNCH_CHECK();
 }
 

@@ -209,6 +209,59 @@ void scratch_free(void* p, hipStream_t s)
     c.free_blocks.push_back(ScratchCache::Block {l.device, p, l.bytes, ev});
 }
 
+// Completion tickets of the kernels that fold their per-workgroup partials in the last-arriving
+// workgroup: `count` consecutive zeroed counters (one per group of workgroups that fold together),
+// each left at zero again by the workgroup that folds.
+// * Outside a HIP-graph capture, a ring per device: a counter is reused only after kTicketRing
+//   later calls, so calls in flight on different streams never share one.
+// * Inside a capture, a counter of its own that is never handed out again (the captured launch
+//   keeps it for every replay; replays of one graph run one after the other).
+// nullptr (the caller then launches its fold, or adds per workgroup): the synchronous diagnostics
+// mode, a capture before any eager call made the pool (it cannot be allocated and zeroed inside a
+// capture), or the capture counters used up.
+unsigned* ticket_alloc(hipStream_t s, unsigned count)
+{
+    if (sync_alloc())
+        return nullptr;
+    constexpr unsigned kTicketRing = 1u << 16, kTicketCapture = 1u << 16;
+    struct TicketPool
+    {
+        std::mutex m;
+        unsigned* dev = nullptr;
+        unsigned next = 0, captured = 0;
+    };
+    static TicketPool pools[kDevices];
+    TicketPool& p = pools[current_device()];
+    const bool cap = s != nullptr && capturing(s);
+    std::lock_guard<std::mutex> lock(p.m);
+    if (p.dev == nullptr)
+    {
+        if (cap)
+            return nullptr;
+        const size_t bytes = sizeof(unsigned) * (kTicketRing + kTicketCapture);
+        unsigned* d        = nullptr;
+        AIMET_HIP_CHECK(hipMalloc(&d, bytes));
+        AIMET_HIP_CHECK(hipMemsetAsync(d, 0, bytes, s));
+        AIMET_HIP_CHECK(hipStreamSynchronize(s));   // once per device: zero before any stream uses it
+        p.dev = d;
+    }
+    if (count == 0 || count > kTicketRing / 16)
+        return nullptr;
+    if (!cap)
+    {
+        if (p.next % kTicketRing + count > kTicketRing)   // consecutive counters: skip the ring's end
+            p.next += kTicketRing - p.next % kTicketRing;
+        unsigned* t = p.dev + p.next % kTicketRing;
+        p.next += count;
+        return t;
+    }
+    if (p.captured + count > kTicketCapture)
+        return nullptr;
+    unsigned* t = p.dev + kTicketRing + p.captured;
+    p.captured += count;
+    return t;
+}
+
 void* upload_async(const void* src, size_t bytes, hipStream_t s)
 {
     // a captured copy would re-read the (reused) pinned slot at every replay

@@ -101,12 +101,43 @@ def lg_encoding_grads_bound(x, grad, emin, emax, bw, sym=False, strict=False, un
     return gmin.view_as(emin), gmax.view_as(emax), bmin.view_as(emin), bmax.view_as(emax)
 
 
+def lg_range_grads_rounded_sums(x, grad, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0):
+    """The reference's float32 range-gradient expressions (lg_gradients) applied to the float64
+    values of its sums rounded once to float32: the closest any float32 evaluation of the
+    reference's formula can come, i.e. the part of the error that is the formula's, not the sums'."""
+    _, mask, x_quant, delta, offset, steps = lg_forward(x, emin, emax, bw, sym, strict, unsigned, ch_axis)
+    dims = list(range(x.dim()))
+    if emin.numel() > 1:
+        dims.pop(ch_axis)
+    X, G, XQ, D, O, M = (t.double() for t in (x, grad, x_quant, delta, offset, mask))
+    if sym:
+        s1 = ((XQ + O) * G).sum(dim=dims).float()
+        s2 = (M * (X / D) * G).sum(dim=dims).float()
+        gmax = (s1 - s2) / torch.div(steps, 2, rounding_mode="floor")
+        return (-gmax).view_as(emin), gmax.view_as(emax)
+    gs = ((XQ + O - X * M / D) * G).sum(dim=dims).float()
+    go = (D * G * (1 - M)).sum(dim=dims).float()
+    t1 = gs / steps
+    t2 = steps / (emax - emin) ** 2 * go.view_as(emax)
+    return (-t1.view_as(emin) + emax * t2).view_as(emin), (t1.view_as(emax) - emin * t2).view_as(emax)
+
+
 def sum_bound_units(got, exact, bound):
     """The worst |got - exact| / (2^-24 * bound) over the elements: the error in the unit the
     learned-grid tests bound (an fp32 sum of n terms in any order is within ~log2(n) of it)."""
     err = (got.double().reshape(-1).cpu() - exact.reshape(-1).cpu()).abs()
     unit = 2.0 ** -24 * bound.reshape(-1).cpu() + 1.2e-38
     return float((err / unit).max()) if err.numel() else 0.0
+
+
+def report_sum_bound_units(got, exact, bound, what):
+    """sum_bound_units, appended to AIMET_BOUND_REPORT when set (figures reported beside a bound)."""
+    units = sum_bound_units(got, exact, bound)
+    report = os.environ.get("AIMET_BOUND_REPORT")
+    if report:
+        with open(report, "a") as f:
+            f.write(json.dumps({"what": what, "units": round(units, 4), "c": None}) + "\n")
+    return units
 
 
 def assert_within_sum_bound(got, exact, bound, c, what=""):

@@ -156,10 +156,14 @@ def _bits(t):
 
 @pytest.mark.gpu
 @gpu
-def test_resnet50_sim_checkpoint_qdq_bit_identical(tmp_path):
+def test_resnet50_sim_checkpoint_qdq_bit_identical(tmp_path, monkeypatch):
     """A calibrated per-channel ResNet-50 W8A8 sim, checkpointed and reloaded: the QDQ forward is
-    bit-identical, so is its deep copy's, and both recalibrate to the original's encodings."""
+    bit-identical, so is its deep copy's, and both recalibrate to the original's encodings.
+    MIOpen is held to deterministic solutions: its default ones for some strided convolutions
+    differ in the last bit between two copies of the same layer (seen at layer2.0.conv2,
+    tools/studies/ckpt_debug.py), which is the convolution's, not the quantizers'."""
     from workloads.resnet import resnet50
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
     dev = torch.device("cuda", 0)
     images = torch.rand(8, 3, 224, 224, generator=torch.Generator().manual_seed(1234)).to(dev)
     sim = QuantizationSimModel(resnet50(seed=0, device=dev), images[:1], quant_scheme="tf_enhanced",
@@ -200,9 +204,11 @@ def test_resnet50_sim_checkpoint_qdq_bit_identical(tmp_path):
 
 @pytest.mark.gpu
 @gpu
-def test_range_learning_sim_checkpoint_step_bit_identical(tmp_path):
+def test_range_learning_sim_checkpoint_step_bit_identical(tmp_path, monkeypatch):
     """A range-learning sim (LearnedGridQuantWrapper: trainable encoding_min / _max parameters)
-    reloaded from a checkpoint: forward and every gradient bit-identical."""
+    reloaded from a checkpoint: forward and every gradient bit-identical (MIOpen held to
+    deterministic solutions: its default 1x1 weight gradient differs run to run on the same sim)."""
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
     net = _Net().to(dev)

@@ -220,11 +220,13 @@ def test_per_channel_stats_vs_per_channel_oracle(scheme, shape, axis):
 
 
 @pytest.mark.parametrize("scheme,C,bws", [(QuantizationMode.QUANTIZATION_TF_ENHANCED, 600, (4, 8, 16)),
+                                          (QuantizationMode.QUANTIZATION_TF_ENHANCED, 200, (4, 8, 16)),
                                           (QuantizationMode.QUANTIZATION_MSE, 160, (8, 4))])
 def test_device_search_many_channels(scheme, C, bws):
-    """Device encoding searches (tfe_search.hip: one workgroup per channel; mse_search.hip:
-    channel x candidate-slice grid) == the oracle's host searches, for channels of varied shape,
-    every flag set and several bit-widths."""
+    """Device encoding searches (tfe_search.hip: one workgroup per channel, or below 512 channels
+    each channel's candidates split over one-wave workgroups merged by the last to finish;
+    mse_search.hip: channel x candidate-slice grid) == the oracle's host searches, for channels of
+    varied shape, every flag set and several bit-widths."""
     rng = np.random.default_rng(21)
     K = 96
     scale = rng.uniform(1e-3, 30, (C, 1))
@@ -250,6 +252,28 @@ def test_device_search_many_channels(scheme, C, bws):
             assert valid
             for c in range(C):
                 assert encs[c].to_tuple() == orcs[c].compute(bw, *fl).as_tuple(), (c, bw, fl)
+
+
+def test_tfe_split_search_equals_one_workgroup_per_channel(monkeypatch):
+    """The split TF-E search (few channels: candidates over one-wave workgroups, first minimum by
+    (cost, index) across them) == one workgroup per channel (AIMET_TFE_NO_SPLIT), for a batch of
+    per-tensor quantizers (the activations' getEncodings) and every flag set."""
+    rng = np.random.default_rng(33)
+    qs = []
+    for i in range(40):
+        q = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED)
+        x = rng.standard_t(2 + i % 5, 4096 + 97 * i) * rng.uniform(1e-3, 10) + rng.uniform(-2, 2)
+        if i % 7 == 3:
+            x = np.abs(x)
+        q.updateStats(gpu(x.astype(np.float32)), True)
+        qs.append(q)
+    for bw in (8, 16):
+        for fl in FLAGS:
+            split = AimetTensorQuantizer.getEncodings(qs, bw, *fl)
+            monkeypatch.setenv("AIMET_TFE_NO_SPLIT", "1")
+            whole = AimetTensorQuantizer.getEncodings(qs, bw, *fl)
+            monkeypatch.delenv("AIMET_TFE_NO_SPLIT")
+            assert [(e.to_tuple(), v) for e, v in split] == [(e.to_tuple(), v) for e, v in whole], (bw, fl)
 
 
 def test_mse_device_search_per_tensor_large():

@@ -161,6 +161,7 @@ def test_llama_two_layers_quantsim_backward_equals_reference_ops():
         torch.testing.assert_close(W.grad, gx, rtol=0, atol=0, msg=n)
         ex_min, ex_max, bmin, bmax = T.lg_encoding_grads_bound(W.detach(), gw[n].float(), emin, emax, 4, True,
                                                                ch_axis=pq.channel_axis)
+        T.report_sum_bound_units(gmin, ex_min, bmin, "llama %s weight grad_min, reference torch ops" % n)
         T.assert_within_sum_bound(w.weight_encoding_min.grad, ex_min, bmin, LG_BOUND_C, "llama %s weight grad_min" % n)
         T.assert_within_sum_bound(w.weight_encoding_max.grad, ex_max, bmax, LG_BOUND_C, "llama %s weight grad_max" % n)
 
@@ -169,5 +170,10 @@ def test_llama_two_layers_quantsim_backward_equals_reference_ops():
         gx, gmin, gmax = T.lg_gradients(x, up, omin, omax, 16)
         torch.testing.assert_close(raw_in_grads[n], gx.to(raw_in_grads[n].dtype), rtol=0, atol=0, msg=n)
         ex_min, ex_max, bmin, bmax = T.lg_encoding_grads_bound(x, up, omin, omax, 16)
+        T.report_sum_bound_units(gmin, ex_min, bmin, "llama %s output grad_min, reference torch ops" % n)
+        T.report_sum_bound_units(gmax, ex_max, bmax, "llama %s output grad_max, reference torch ops" % n)
+        r_min, r_max = T.lg_range_grads_rounded_sums(x, up, omin, omax, 16)
+        T.report_sum_bound_units(r_min, ex_min, bmin, "llama %s output grad_min, formula on rounded exact sums" % n)
+        T.report_sum_bound_units(r_max, ex_max, bmax, "llama %s output grad_max, formula on rounded exact sums" % n)
         T.assert_within_sum_bound(w.output0_encoding_min.grad, ex_min, bmin, LG_BOUND_C, "llama %s output grad_min" % n)
         T.assert_within_sum_bound(w.output0_encoding_max.grad, ex_max, bmax, LG_BOUND_C, "llama %s output grad_max" % n)
