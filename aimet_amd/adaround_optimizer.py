@@ -135,6 +135,12 @@ _PW_FUSED = os.environ.get("AIMET_ADA_PW_FUSED", "auto")
 # slower at 28^2: 0.071 -> 0.09); AIMET_ADA_PW_CM=0: the [nb][C][hw] batches with per-sample GEMMs
 # (AIMET_ADA_PW_GRAD) everywhere
 _PW_CM = os.environ.get("AIMET_ADA_PW_CM", "1") == "1"
+# the channel-major form as two kernels on the f32 matrix cores (aimet_adaround_pw_cm_forward: the
+# gather, q = W x and the reconstruction gradient; aimet_adaround_pw_cm_wgrad: dL/dW in position
+# slices that the Adam step adds, aimet_adaround_backward_adam_parts) instead of gather + GEMM +
+# reconstruction gradient + GEMM; AIMET_ADA_PW_CM_FUSED=0: the library-GEMM chain (fp32 sums in
+# another order, so alpha differs at summation-order tolerance)
+_PW_CM_FUSED = os.environ.get("AIMET_ADA_PW_CM_FUSED", "1") == "1"
 
 
 def _is_pointwise(module: torch.nn.Module) -> bool:
@@ -610,9 +616,16 @@ class AdaroundOptimizer:
         if (mode in ("pointwise", "im2col") and pw_dims is None and _PW_CM and hw <= 14 * 14
                 and inp_data[0].numel() % hw == 0):
             cin_cm = inp_data[0].numel() // hw
-            x_cm = torch.empty((cin_cm, nb * hw), dtype=torch.float32, device=dev)
-            q_cm = torch.empty((C_out, nb * hw), dtype=torch.float32, device=dev)
-            cm = (cin_cm, x_cm, q_cm, torch.empty_like(q_cm))
+            if _PW_CM_FUSED and wq.is_contiguous():
+                slices = ctypes.c_int64()
+                _native.check(lib.aimet_adaround_pw_cm_wgrad_slices(nb, cin_cm, C_out, hw, ctypes.byref(slices)))
+                g_cm = torch.empty((C_out, nb * hw), dtype=torch.float32, device=dev)
+                parts = torch.empty((slices.value,) + tuple(wq.shape), dtype=torch.float32, device=dev)
+                cm = (cin_cm, None, g_cm, parts)
+            else:
+                x_cm = torch.empty((cin_cm, nb * hw), dtype=torch.float32, device=dev)
+                q_cm = torch.empty((C_out, nb * hw), dtype=torch.float32, device=dev)
+                cm = (cin_cm, x_cm, q_cm, torch.empty_like(q_cm))
 
         def recon(q, with_bias, s):
             _native.check(lib.aimet_adaround_recon_grad_indexed(P(q), P(out_data), P(idx_all), it_cur, P(g_buf), nb,
@@ -646,6 +659,18 @@ class AdaroundOptimizer:
                 _native.check(lib.aimet_adaround_pw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
                                                          P(wq), pbias, P(gw_pw), P(ws_pw), *pw_dims, code, s))
                 adam_step(gw_pw, s)
+                return
+            if mode in ("pointwise", "im2col") and cm is not None and cm[1] is None:
+                # channel-major batch on the matrix cores: the gathered GEMM with the reconstruction
+                # gradient, the sliced weight gradient, the Adam step adding the slices
+                cin_cm, _, g_cm, parts = cm
+                _native.check(lib.aimet_adaround_pw_cm_forward(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
+                                                               P(wq), pbias, P(g_cm), nb, cin_cm, C_out, hw, code, s))
+                _native.check(lib.aimet_adaround_pw_cm_wgrad(P(inp_data), P(idx_all), it_cur, P(g_cm), P(parts),
+                                                             parts.shape[0], nb, cin_cm, C_out, hw, s))
+                _native.check(lib.aimet_adaround_backward_adam_parts(
+                    sq.pw, sq.pa, P(parts), parts.shape[0], P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po,
+                    sq.bw, P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, s))
                 return
             if mode in ("pointwise", "im2col") and cm is not None:
                 # channel-major batch: one GEMM per direction over all nb * hw positions
@@ -764,7 +789,8 @@ class AdaroundOptimizer:
                 del g
         _, mode, graph = best
         AdaroundOptimizer.last_loop_form = mode + ("_fused" if mode in ("pointwise", "im2col") and pw_dims else
-                                                   "_cm" if mode in ("pointwise", "im2col") and cm else "")
+                                                   ("_cm_mfma" if cm[1] is None else "_cm")
+                                                   if mode in ("pointwise", "im2col") and cm else "")
         for a in range(0, iters, chunk):
             b = min(a + chunk, iters)
             if b < iters:

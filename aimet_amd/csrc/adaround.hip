@@ -501,7 +501,7 @@ __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __r
     if (threadIdx.x == 0)
     {
         publish_f32(part + blockIdx.x, s);
-        last = arrive_is_last(ticket, gridDim.x);
+        last = arrive_is_last_grid(ticket);
     }
     __syncthreads();
     if (!last)
@@ -514,7 +514,7 @@ __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __r
     if (threadIdx.x == 0)
     {
         atomicAdd(round_loss, reg * t);
-        ticket_reset(ticket);
+        ticket_reset(ticket + kTicketGroups);
     }
 }
 
@@ -638,7 +638,7 @@ struct LossFold
     {
         if (!round_loss)
             return;
-        ticket = ticket_alloc(st);
+        ticket = ticket_alloc(st, kTicketGroups + 1);
         if (ticket)
             part = static_cast<float*>(scratch_alloc(sizeof(float) * grid, st));
     }
@@ -700,7 +700,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                                                                    float* __restrict__ round_loss,
                                                                    float* __restrict__ wq_next,
                                                                    float* __restrict__ loss_part,
-                                                                   unsigned* __restrict__ ticket)
+                                                                   unsigned* __restrict__ ticket, uint32_t nparts)
 {
     const int64_t step = it_next[0];
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -730,6 +730,8 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             const float d = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(d);
             f4 wv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(w) + ic);
             f4 gv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + ic);
+            for (uint32_t s = 1; s < nparts; ++s)   // the gradient's slices, added in slice order
+                gv += __builtin_nontemporal_load(reinterpret_cast<const f4*>(g + (size_t) s * n) + ic);
             f4 av       = reinterpret_cast<const f4*>(alpha)[ic];
             float a[4] = {av.x, av.y, av.z, av.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
             float r[4], sg[4], x[4], ax[4];
@@ -779,7 +781,10 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             const uint32_t c = map.channel(i);
             const float d = delta[c], o = offset[c];
             const float rcp = __builtin_amdgcn_rcpf(d);
-            const float ga  = ada_bwd(w[i], alpha[i], g[i], d, o, p, rcp, loss, i);
+            float gi        = g[i];
+            for (uint32_t s = 1; s < nparts; ++s)
+                gi += g[(size_t) s * n + i];
+            const float ga  = ada_bwd(w[i], alpha[i], gi, d, o, p, rcp, loss, i);
             const float an  = adam_elem(alpha[i], ga, exp_avg[i], exp_avg_sq[i], adam, bc1, bc2s);
             alpha[i]        = an;
             if (wq_next)
@@ -1007,11 +1012,12 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
             aligned16(ga))
         {
             uint32_t nq = (uint32_t) (n / 4);
-            // quads in flight per lane (AIMET_ADA_BWD_U = 1 / 2 / 4 for tuning; 2 measured best)
+            // quads in flight per lane (AIMET_ADA_BWD_U = 1 / 2 / 4 for tuning; 1 measured best:
+            // profiles/r04/ada_bwd_tune.jsonl)
             static const int U = [] {
                 const char* e = getenv("AIMET_ADA_BWD_U");
-                const int u   = e ? atoi(e) : 2;
-                return u == 1 || u == 4 ? u : 2;
+                const int u   = e ? atoi(e) : 1;
+                return u == 2 || u == 4 ? u : 1;
             }();
             int64_t blocks    = ceil_div(nq, kBlock * U);
             const unsigned gx = (unsigned) (blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid);
@@ -1209,11 +1215,11 @@ int aimet_adaround_recon_grad_indexed_cm(const float* q, const float* out_data, 
     });
 }
 
-int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad_wq, float* exp_avg, float* exp_avg_sq,
-                                 int64_t outer, int64_t C, int64_t K, const float* delta, const float* offset,
-                                 int32_t bw, const float* reg_beta_all, const int64_t* it_next, int64_t* it_cur,
-                                 double lr, double beta1, double beta2, double eps, float* round_loss, float* wq_next,
-                                 void* stream)
+int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float* grad_parts, int64_t nparts,
+                                       float* exp_avg, float* exp_avg_sq, int64_t outer, int64_t C, int64_t K,
+                                       const float* delta, const float* offset, int32_t bw, const float* reg_beta_all,
+                                       const int64_t* it_next, int64_t* it_cur, double lr, double beta1, double beta2,
+                                       double eps, float* round_loss, float* wq_next, void* stream)
 {
     return guarded([&] {
         AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
@@ -1223,7 +1229,9 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
         AIMET_REQUIRE(n > 0 && n < (int64_t(1) << 31), "AdaRound weight must have 1 .. 2^31-1 elements");
         require_device_ptr(w, "weight");
         require_device_ptr(alpha, "alpha");
-        require_device_ptr(grad_wq, "grad");
+        require_device_ptr(grad_parts, "grad");
+        AIMET_REQUIRE(nparts >= 1 && nparts <= 65535, "nparts out of range");
+        const float* grad_wq = grad_parts;
         require_device_ptr(exp_avg, "exp_avg");
         require_device_ptr(exp_avg_sq, "exp_avg_sq");
         require_device_ptr(delta, "delta");
@@ -1248,13 +1256,24 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
         if (vec)
             adaround_bwd_adam_kernel<true><<<(unsigned) blocks, kBlock, 0, st>>>(
                 w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss, wq_next, lf.part, lf.ticket);
+                it_cur, a, round_loss, wq_next, lf.part, lf.ticket, (uint32_t) nparts);
         else
             adaround_bwd_adam_kernel<false><<<(unsigned) blocks, kBlock, 0, st>>>(
                 w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss, wq_next, lf.part, lf.ticket);
+                it_cur, a, round_loss, wq_next, lf.part, lf.ticket, (uint32_t) nparts);
         AIMET_LAUNCH_CHECK();
     });
+}
+
+int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad_wq, float* exp_avg, float* exp_avg_sq,
+                                 int64_t outer, int64_t C, int64_t K, const float* delta, const float* offset,
+                                 int32_t bw, const float* reg_beta_all, const int64_t* it_next, int64_t* it_cur,
+                                 double lr, double beta1, double beta2, double eps, float* round_loss, float* wq_next,
+                                 void* stream)
+{
+    return aimet_adaround_backward_adam_parts(w, alpha, grad_wq, 1, exp_avg, exp_avg_sq, outer, C, K, delta, offset, bw,
+                                              reg_beta_all, it_next, it_cur, lr, beta1, beta2, eps, round_loss, wq_next,
+                                              stream);
 }
 
 }   // extern "C"

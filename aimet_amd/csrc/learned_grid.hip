@@ -502,8 +502,8 @@ __device__ __forceinline__ void publish_sums(float* p, const Sums& t)
 }
 
 // The per-tensor backward's fold in the workgroup that finishes last (no second launch): thread
-// 0 of each workgroup (the one that published its tiles' partials) drains them and takes a
-// ticket; the workgroup drawing the last one runs fold_partials -- the same arithmetic as
+// 0 of each workgroup (the one that published its tiles' partials) drains them and arrives
+// (arrive_is_last_grid); the workgroup arriving last runs fold_partials -- the same arithmetic as
 // lg_bwd_fold_one, so the same bits -- and leaves the ticket at zero (ticket_alloc). Called by every
 // thread of every workgroup; none waits for another, so they need not be co-resident.
 __device__ __forceinline__ void fold_in_last_workgroup(const float* partial, int64_t nparts, float* sums,
@@ -511,14 +511,14 @@ __device__ __forceinline__ void fold_in_last_workgroup(const float* partial, int
 {
     __shared__ int last;
     if (threadIdx.x == 0)
-        last = arrive_is_last(ticket, gridDim.x);
+        last = arrive_is_last_grid(ticket);
     __syncthreads();
     if (!last)
         return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the ticket
     fold_partials(partial, nparts, sums, range);
     if (threadIdx.x == 0)
-        ticket_reset(ticket);
+        ticket_reset(ticket + kTicketGroups);
 }
 
 // per-tensor (C == 1), tile form: workgroup b owns the kLgTile consecutive elements
@@ -1383,7 +1383,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
             const int v         = vec ? 1 : 0;
             // the fold in the kernel's last workgroup; its own launch when there is no ticket
-            unsigned* ticket = ticket_alloc(s);
+            unsigned* ticket = ticket_alloc(s, kTicketGroups + 1);
             lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
                 lg_bwd_tensor_kernel<decltype(st)::value, decltype(md)::value><<<L.grid, kBlock, 0, s>>>(
                     x, grad, grad_x, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
@@ -1725,7 +1725,7 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         auto os = static_cast<unsigned short*>(grad_x);
         const int v = vec ? 1 : 0;
         // the fold in the kernel's last workgroup; its own launch when there is no ticket
-        unsigned* ticket = ticket_alloc(s);
+        unsigned* ticket = ticket_alloc(s, kTicketGroups + 1);
         lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
             constexpr int ST = decltype(st)::value, MD = decltype(md)::value;
             if (io_dtype == IO_F16 && lg16_nt())

@@ -60,7 +60,7 @@ struct TfeJob
 // choice is the one-workgroup argmin's -- and finishes the encoding. splits == 1: one workgroup
 // per channel, no hand-off. SYMFORM: tfe::cost's branch-free symmetric loops (same sums).
 template <int BLOCK, bool SYMFORM>
-__global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : (BLOCK == 64 ? 8 : 7)) void tfe_search_kernel(
+__global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : (BLOCK == 64 ? 2 : 7)) void tfe_search_kernel(
     TfeJob one, const TfeJob* __restrict__ jobs, int njobs, int64_t total, int bw, int sym, int strict, int unsign,
     int splits, uint64_t* __restrict__ part, unsigned* __restrict__ tickets)
 {

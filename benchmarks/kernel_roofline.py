@@ -12,6 +12,7 @@ usage: python benchmarks/kernel_roofline.py [--elems N] [--reps R] [--cpu-elems 
 import argparse
 import ctypes
 import json
+import math
 import os
 import sys
 import time
@@ -229,7 +230,18 @@ def main():
         loss.backward()
     t_ms = timed(torch_ada_bwd, 2, stream)
     row("adaround_backward (+ round loss)", "a15", 16, ms, None, t_ms,
-        note="reference: torch forward + autograd backward + round loss")
+        note="reference: torch forward + autograd backward + round loss; alpha ~ N(0, 1): %.1f %% of the "
+             "rectified sigmoids saturate" % (100 * float((alpha.abs() > math.log(11.0)).float().mean())))
+    # a converging loop's alphas: N(0, 16) saturates ~55 % of them (the wave-compacted rounding-loss
+    # pows then run for the rest only); with and without the loss value (the optimisation loop's form)
+    alpha_sat = alpha * 4.0
+    sat = 100 * float((alpha_sat.abs() > math.log(11.0)).float().mean())
+    for want_loss in (True, False):
+        ms = timed(lambda: (rloss.zero_(), lib.aimet_adaround_backward(
+            P(w), P(alpha_sat), P(grad), P(gx), 1, C, K, P(delta), P(offset), 8, ctypes.c_double(0.01),
+            ctypes.c_double(10.0), P(rloss) if want_loss else None, sp)), args.reps, stream)
+        row("adaround_backward (%s), %.0f %% saturated" % ("+ round loss" if want_loss else "gradient only", sat),
+            "a15", 16, ms, note="alpha ~ N(0, 16)")
 
     if args.out:
         with open(args.out, "w") as f:

@@ -469,6 +469,36 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
                                  const int64_t* it_next_dev, int64_t* it_cur_dev, double lr, double beta1,
                                  double beta2, double eps, float* round_loss_dev, float* wq_next_dev, void* stream);
 
+/* aimet_adaround_backward_adam with the weight gradient given as `nparts` slices grad_parts[s][n]
+ * (n = outer * C * K) that are added in slice order (s = 0, 1, ...) element by element: the sliced
+ * weight gradient of aimet_adaround_pw_cm_wgrad. nparts == 1 is aimet_adaround_backward_adam. */
+int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float* grad_parts, int64_t nparts,
+                                       float* exp_avg_dev, float* exp_avg_sq_dev, int64_t outer, int64_t C, int64_t K,
+                                       const float* delta_dev, const float* offset_dev, int32_t bw,
+                                       const float* reg_beta_all_dev, const int64_t* it_next_dev, int64_t* it_cur_dev,
+                                       double lr, double beta1, double beta2, double eps, float* round_loss_dev,
+                                       float* wq_next_dev, void* stream);
+
+/* The channel-major GEMM form of a 1x1 layer's AdaRound iteration (adaround_optimizer.py:181-218)
+ * in two kernels on the f32 matrix cores, for many channels at small spatial sizes. Batch position
+ * p = b * hw + t of iteration it = it_cur_dev[0] is element t of row idx_all_dev[it * nb + b] of
+ * x_cache ([rows][Cin][hw]) and target_cache ([rows][Cout][hw]), read in place.
+ * aimet_adaround_pw_cm_forward: grad_q[co][p] = the reconstruction-loss gradient
+ * (aimet_adaround_recon_grad_indexed_cm's, act 0 none / 1 ReLU / 2 ReLU6) of
+ * q = sum over ci of w[co][ci] x[ci][p] (ci ascending) + bias[co] (nullable); it_next_dev[0] =
+ * it + 1. aimet_adaround_pw_cm_wgrad: parts[s][co][ci] = sum over the positions of slice s of
+ * grad_q[co][p] x[ci][p] (positions ascending), `slices` from aimet_adaround_pw_cm_wgrad_slices;
+ * aimet_adaround_backward_adam_parts adds them. Fixed summation orders (deterministic, fp32; not
+ * bit-identical to a library GEMM). */
+int aimet_adaround_pw_cm_forward(const float* x_cache, const float* target_cache, const int64_t* idx_all_dev,
+                                 const int64_t* it_cur_dev, int64_t* it_next_dev, const float* w, const float* bias,
+                                 float* grad_q, int64_t nb, int64_t Cin, int64_t Cout, int64_t hw, int32_t act,
+                                 void* stream);
+int aimet_adaround_pw_cm_wgrad_slices(int64_t nb, int64_t Cin, int64_t Cout, int64_t hw, int64_t* slices);
+int aimet_adaround_pw_cm_wgrad(const float* x_cache, const int64_t* idx_all_dev, const int64_t* it_cur_dev,
+                               const float* grad_q, float* parts, int64_t slices, int64_t nb, int64_t Cin, int64_t Cout,
+                               int64_t hw, void* stream);
+
 /* Depthwise 2-D convolution (groups == C, weights [C][1][K][K], K = 3 or 5, square stride /
  * padding / dilation, NCHW fp32): the AdaRound loop's layer math on depthwise layers
  * (adaround_optimizer.py:257-286 runs the wrapped layer's forward and autograd's weight gradient;

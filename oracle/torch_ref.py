@@ -73,25 +73,26 @@ def lg_gradients(x, grad, emin, emax, bw, sym=False, strict=False, unsigned=Fals
 
 
 def lg_encoding_grads_bound(x, grad, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0):
-    """The encoding gradients of lg_gradients in float64 from the same float32 forward quantities
-    (x_quant, delta, offset, mask), with the magnitude each one is summed from: returns
-    (gmin, gmax, bmin, bmax) where b = sum of |terms| carried through the same linear combination.
-    An fp32 result whose error is at most c * eps * b (c = a small multiple of the summation depth)
-    is as exact as an fp32 sum in any order can be; tests state c."""
+    """The encoding gradients of lg_gradients with its float32 terms summed exactly (float64) and
+    combined in float64, and the magnitude each one is summed from: returns (gmin, gmax, bmin,
+    bmax) where b = sum of |terms| carried through the same linear combination. The terms are the
+    reference's float32 expressions element by element (which the kernels reproduce bit for bit),
+    so an fp32 result whose error is at most c * eps * b differs from the exact sum of those very
+    terms by summation order (and the combination's few roundings) only; tests state c."""
     _, mask, x_quant, delta, offset, steps = lg_forward(x, emin, emax, bw, sym, strict, unsigned, ch_axis)
     dims = list(range(x.dim()))
     if emin.numel() > 1:
         dims.pop(ch_axis)
-    X, G, XQ, D, O, M = (t.double() for t in (x, grad, x_quant, delta, offset, mask))
     st = float(steps)
     if sym:
-        t1, t2 = (XQ + O) * G, M * (X / D) * G
+        t1 = ((x_quant + offset) * grad).double()
+        t2 = (mask * (x / delta) * grad).double()
         half = math.floor(st / 2)
         gmax = (t1.sum(dim=dims) - t2.sum(dim=dims)) / half
         b = (t1.abs().sum(dim=dims) + t2.abs().sum(dim=dims)) / half
         return (-gmax).view_as(emin), gmax.view_as(emax), b.view_as(emin), b.view_as(emax)
-    gs = (XQ + O - X * M / D) * G
-    go = D * G * (1 - M)
+    gs = ((x_quant + offset - x * mask / delta) * grad).double()
+    go = ((delta * grad) * (~mask)).double()
     lo, hi = emin.double().reshape(-1), emax.double().reshape(-1)
     k = st / (hi - lo) ** 2
     t1, b1 = gs.sum(dim=dims).reshape(-1) / st, gs.abs().sum(dim=dims).reshape(-1) / st
@@ -102,21 +103,21 @@ def lg_encoding_grads_bound(x, grad, emin, emax, bw, sym=False, strict=False, un
 
 
 def lg_range_grads_rounded_sums(x, grad, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0):
-    """The reference's float32 range-gradient expressions (lg_gradients) applied to the float64
-    values of its sums rounded once to float32: the closest any float32 evaluation of the
-    reference's formula can come, i.e. the part of the error that is the formula's, not the sums'."""
+    """The reference's float32 range-gradient expressions (lg_gradients) applied to the exact
+    (float64) sums of its float32 terms, each rounded once to float32: the closest any float32
+    evaluation of the reference's formula can come, i.e. the part of the error that is the
+    formula's, not the sums'."""
     _, mask, x_quant, delta, offset, steps = lg_forward(x, emin, emax, bw, sym, strict, unsigned, ch_axis)
     dims = list(range(x.dim()))
     if emin.numel() > 1:
         dims.pop(ch_axis)
-    X, G, XQ, D, O, M = (t.double() for t in (x, grad, x_quant, delta, offset, mask))
     if sym:
-        s1 = ((XQ + O) * G).sum(dim=dims).float()
-        s2 = (M * (X / D) * G).sum(dim=dims).float()
+        s1 = ((x_quant + offset) * grad).double().sum(dim=dims).float()
+        s2 = (mask * (x / delta) * grad).double().sum(dim=dims).float()
         gmax = (s1 - s2) / torch.div(steps, 2, rounding_mode="floor")
         return (-gmax).view_as(emin), gmax.view_as(emax)
-    gs = ((XQ + O - X * M / D) * G).sum(dim=dims).float()
-    go = (D * G * (1 - M)).sum(dim=dims).float()
+    gs = ((x_quant + offset - x * mask / delta) * grad).double().sum(dim=dims).float()
+    go = ((delta * grad) * (~mask)).double().sum(dim=dims).float()
     t1 = gs / steps
     t2 = steps / (emax - emin) ** 2 * go.view_as(emax)
     return (-t1.view_as(emin) + emax * t2).view_as(emin), (t1.view_as(emax) - emin * t2).view_as(emax)
