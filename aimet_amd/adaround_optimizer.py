@@ -140,7 +140,13 @@ _PW_CM = os.environ.get("AIMET_ADA_PW_CM", "1") == "1"
 # slices that the Adam step adds, aimet_adaround_backward_adam_parts) instead of gather + GEMM +
 # reconstruction gradient + GEMM; AIMET_ADA_PW_CM_FUSED=0: the library-GEMM chain (fp32 sums in
 # another order, so alpha differs at summation-order tolerance)
-_PW_CM_FUSED = os.environ.get("AIMET_ADA_PW_CM_FUSED", "1") == "1"
+_PW_CM_FUSED = os.environ.get("AIMET_ADA_PW_CM_FUSED", "0") == "1"
+# iterations per captured HIP graph in the single-process loop: one hipGraphLaunch per iteration
+# left the GPU waiting on the host between replays for small layers (a depthwise layer's ~10 us of
+# kernels per iteration in a ~100 us window, profiles/r04/adaround_loop_summary.txt); the counters and
+# the batch table live on the device, so k consecutive iterations are one graph. Results are those
+# of one iteration per graph, bit for bit.
+_GRAPH_ITERS = max(1, int(os.environ.get("AIMET_ADA_GRAPH_ITERS", "10")))
 
 
 def _is_pointwise(module: torch.nn.Module) -> bool:
@@ -736,7 +742,7 @@ class AdaroundOptimizer:
                     round_loss_out.copy_(loss0)
             soft_weight()
 
-        def capture(m):
+        def capture(m, k=1):
             nonlocal mode
             mode = m
             # warm-up on a side stream (library handles, allocator, autograd), then capture
@@ -750,7 +756,8 @@ class AdaroundOptimizer:
             restart()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g), torch.enable_grad():
-                step()
+                for _ in range(k):   # k consecutive iterations (the counters advance on the device)
+                    step()
             return g
 
         # layers with two forms (GEMM or MIOpen convolution through autograd): the form is fixed by
@@ -791,11 +798,17 @@ class AdaroundOptimizer:
         AdaroundOptimizer.last_loop_form = mode + ("_fused" if mode in ("pointwise", "im2col") and pw_dims else
                                                    ("_cm_mfma" if cm[1] is None else "_cm")
                                                    if mode in ("pointwise", "im2col") and cm else "")
+        k = min(_GRAPH_ITERS, chunk)
+        graph_k = capture(mode, k) if k > 1 and iters >= k else None
         for a in range(0, iters, chunk):
             b = min(a + chunk, iters)
             if b < iters:
                 draw(b, min(b + chunk, iters))
-            for _ in range(a, b):
+            i = a
+            while graph_k is not None and i + k <= b:
+                graph_k.replay()
+                i += k
+            for _ in range(i, b):
                 graph.replay()
         torch.cuda.current_stream(dev).synchronize()
         del staged

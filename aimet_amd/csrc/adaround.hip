@@ -386,17 +386,47 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
                                                float (&pb)[E])
 {
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t cnt        = 0;
+    bool need[E];
+    uint32_t total = 0;
+#pragma unroll
+    for (int k = 0; k < E; ++k)
+    {
+        need[k] = use[k] && !(ax[k] == 0.0f || ax[k] == 1.0f);
+        total += (uint32_t) __popcll(__ballot(need[k]));
+    }
+    if (4 * total >= 3 * 64 * E)
+    {
+        // a dense wave (few saturated alphas): each lane evaluates its own elements in place, the
+        // compaction's LDS round trip would not pay (the same values)
+#pragma unroll
+        for (int k = 0; k < E; ++k)
+        {
+            if (need[k])
+            {
+                F2 l {0.0f, 0.0f};
+                if (!tail[k])
+                    l = sleef_logkf(ax[k]);
+                pbm1[k] = pow01_log(ax[k], p.beta_m1, tail[k], l);
+                pb[k]   = p.want_loss ? pow01_log(ax[k], p.beta, tail[k], l) : 0.0f;
+            }
+            else
+            {
+                pbm1[k] = pow01_exact(ax[k], p.beta_m1);
+                pb[k]   = pow01_exact(ax[k], p.beta);
+            }
+        }
+        return;
+    }
+    uint32_t cnt = 0;
     int pos[E];
 #pragma unroll
     for (int k = 0; k < E; ++k)
     {
-        const bool need       = use[k] && !(ax[k] == 0.0f || ax[k] == 1.0f);
-        const uint64_t ballot = __ballot(need);
+        const uint64_t ballot = __ballot(need[k]);
         const uint32_t below  = __builtin_amdgcn_mbcnt_hi((uint32_t) (ballot >> 32),
                                                           __builtin_amdgcn_mbcnt_lo((uint32_t) ballot, 0u));
-        pos[k] = need ? (int) (cnt + below) : -1;
-        if (need)   // |x| >= 0 or NaN: the sign bit marks a tail element
+        pos[k] = need[k] ? (int) (cnt + below) : -1;
+        if (need[k])   // |x| >= 0 or NaN: the sign bit marks a tail element
             wl[cnt + below] = tail[k] ? -ax[k] : ax[k];
         cnt += (uint32_t) __popcll(ballot);
     }
@@ -507,9 +537,19 @@ __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __r
     if (!last)
         return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the ticket
+    constexpr int kFoldBatch = 8;   // loads in flight per lane; each lane adds its parts in order
     float t = 0.0f;
-    for (uint32_t i = threadIdx.x; i < gridDim.x; i += kBlock)
-        t += consume_f32(part + i);
+    for (uint32_t i0 = threadIdx.x; i0 < gridDim.x; i0 += kBlock * kFoldBatch)
+    {
+        float v[kFoldBatch];
+#pragma unroll
+        for (int u = 0; u < kFoldBatch; ++u)
+            v[u] = i0 + u * kBlock < gridDim.x ? consume_f32(part + i0 + u * kBlock) : 0.0f;
+#pragma unroll
+        for (int u = 0; u < kFoldBatch; ++u)
+            if (i0 + u * kBlock < gridDim.x)
+                t += v[u];
+    }
     t = block_sum(t);
     if (threadIdx.x == 0)
     {
@@ -633,22 +673,21 @@ struct LossFold
 {
     float* part      = nullptr;
     unsigned* ticket = nullptr;
+    FoldBuffers fb;
     hipStream_t s;
     LossFold(const float* round_loss, unsigned grid, hipStream_t st) : s(st)
     {
         if (!round_loss)
             return;
-        ticket = ticket_alloc(st, kTicketGroups + 1);
-        if (ticket)
-            part = static_cast<float*>(scratch_alloc(sizeof(float) * grid, st));
+        fb     = fold_buffers(st, kTicketGroups + 1, grid);
+        ticket = fb.ticket;
+        part   = fb.part;
     }
     ~LossFold()
     {
-        if (!part)
-            return;
         try
         {
-            scratch_free(part, s);
+            fold_buffers_release(fb, s);
         }
         catch (...)   // a failing event record: the block is leaked, never handed out again
         {

@@ -212,6 +212,17 @@ void* upload_async(const void* src, size_t bytes, hipStream_t s);
 void* scratch_alloc(size_t bytes, hipStream_t s);
 // `count` consecutive zeroed completion counters for last-workgroup folds, or nullptr: upload.cpp
 unsigned* ticket_alloc(hipStream_t s, unsigned count = 1);
+// tickets + a partial-sum buffer of `part_floats` for one launch's last-workgroup fold; both null
+// when there is no ticket (the caller then falls back). Inside a HIP-graph capture the buffer is a
+// permanent slot of its own (no graph memory node); release with fold_buffers_release.
+struct FoldBuffers
+{
+    unsigned* ticket = nullptr;
+    float* part      = nullptr;
+    bool scratch     = false;
+};
+FoldBuffers fold_buffers(hipStream_t s, unsigned tickets, size_t part_floats);
+void fold_buffers_release(const FoldBuffers& f, hipStream_t s);
 void scratch_free(void* p, hipStream_t s);
 
 struct QdqParams

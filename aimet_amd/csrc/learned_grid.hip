@@ -475,12 +475,30 @@ __device__ __forceinline__ void range_grads_one(float A, float B, float D, uint3
 __device__ __forceinline__ void fold_partials(const float* __restrict__ partial, int64_t nparts,
                                               float* __restrict__ sums, const LgRange& range)
 {
+    // each lane's parts in ascending order, kFoldBatch triples of loads in flight at a time (one
+    // dependent round trip per part made a 3,342-part fold 5 us long)
+    constexpr int kFoldBatch = 8;
     Sums s {0, 0, 0};
-    for (int64_t i = threadIdx.x; i < nparts; i += kBlock)
+    for (int64_t i0 = threadIdx.x; i0 < nparts; i0 += (int64_t) kBlock * kFoldBatch)
     {
-        s.a += consume_f32(partial + 3 * i + 0);
-        s.b += consume_f32(partial + 3 * i + 1);
-        s.d += consume_f32(partial + 3 * i + 2);
+        float a[kFoldBatch], b[kFoldBatch], d[kFoldBatch];
+#pragma unroll
+        for (int u = 0; u < kFoldBatch; ++u)
+        {
+            const int64_t i = i0 + (int64_t) u * kBlock;
+            const bool in   = i < nparts;
+            a[u]            = in ? consume_f32(partial + 3 * i + 0) : 0.0f;
+            b[u]            = in ? consume_f32(partial + 3 * i + 1) : 0.0f;
+            d[u]            = in ? consume_f32(partial + 3 * i + 2) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kFoldBatch; ++u)
+            if (i0 + (int64_t) u * kBlock < nparts)
+            {
+                s.a += a[u];
+                s.b += b[u];
+                s.d += d[u];
+            }
     }
     Sums t = block_reduce(s);
     if (threadIdx.x == 0)
@@ -1380,10 +1398,12 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                          reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
             const LgBwdLaunch L = lg_bwd_launch(n);
-            float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
+            // the partials and the ticket of the fold in the last workgroup (its own launch without one)
+            const FoldBuffers fb = fold_buffers(s, kTicketGroups + 1, 3 * (size_t) L.ntiles);
+            float* partial      = fb.part ? fb.part : static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
             const int v         = vec ? 1 : 0;
-            // the fold in the kernel's last workgroup; its own launch when there is no ticket
-            unsigned* ticket = ticket_alloc(s, kTicketGroups + 1);
+
+            unsigned* ticket = fb.ticket;
             lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
                 lg_bwd_tensor_kernel<decltype(st)::value, decltype(md)::value><<<L.grid, kBlock, 0, s>>>(
                     x, grad, grad_x, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
@@ -1394,7 +1414,10 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
                 lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
                 AIMET_LAUNCH_CHECK();
             }
-            scratch_free(partial, s);
+            if (fb.part)
+                fold_buffers_release(fb, s);
+            else
+                scratch_free(partial, s);
             return;
         }
         else if (K % 1024 == 0 && n < (int64_t(1) << 31) && C < 65536 &&
@@ -1719,13 +1742,15 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                            reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
         const LgBwdLaunch L = lg_bwd_launch(n);   // the fp32 kernel's tiles
-        float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
+        // the partials and the ticket of the fold in the last workgroup (its own launch without one)
+        const FoldBuffers fb = fold_buffers(s, kTicketGroups + 1, 3 * (size_t) L.ntiles);
+        float* partial      = fb.part ? fb.part : static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
         auto xs = static_cast<const unsigned short*>(x);
         auto gs = static_cast<const unsigned short*>(grad);
         auto os = static_cast<unsigned short*>(grad_x);
         const int v = vec ? 1 : 0;
-        // the fold in the kernel's last workgroup; its own launch when there is no ticket
-        unsigned* ticket = ticket_alloc(s, kTicketGroups + 1);
+
+        unsigned* ticket = fb.ticket;
         lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
             constexpr int ST = decltype(st)::value, MD = decltype(md)::value;
             if (io_dtype == IO_F16 && lg16_nt())
@@ -1747,7 +1772,10 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
             lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, (int) L.ntiles, sums, range);
             AIMET_LAUNCH_CHECK();
         }
-        scratch_free(partial, s);
+        if (fb.part)
+            fold_buffers_release(fb, s);
+        else
+            scratch_free(partial, s);
     });
 }
 

@@ -198,40 +198,57 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : (BLOCK == 64 ? 2 : 7)) vo
             wbest[threadIdx.x >> 6] = b;
         __syncthreads();
         if (threadIdx.x == 0)
-        {
             for (int w = 1; w < kW; ++w)
                 if (better(wbest[w], b))
                     b = wbest[w];
-            bool finish = splits == 1;
-            if (!finish)
+        bool finish = splits == 1;
+        if (!finish)
+        {
+            // publish (cost, index) write-through; the last of channel g's workgroups takes the
+            // first minimum over them: lane q loads split q's pair, lane 0 scans them in order
+            __shared__ int lastw;
+            if (threadIdx.x == 0)
             {
                 uint64_t* my = part + 2 * gs;
                 publish_u64(my, (uint64_t) __double_as_longlong(b.cost));
                 publish_u64(my + 1, (uint64_t) (uint32_t) b.idx);
-                if (arrive_is_last(tickets + g, (unsigned) splits))
+                lastw = arrive_is_last(tickets + g, (unsigned) splits);
+            }
+            __syncthreads();
+            if (lastw)
+            {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                double qc = 0.0;
+                int qi    = -1;
+                if (threadIdx.x < (unsigned) splits)
+                {
+                    const uint64_t* pq = part + 2 * (g * splits + threadIdx.x);
+                    qc                 = __longlong_as_double((long long) consume_u64(pq));
+                    qi                 = (int) (uint32_t) consume_u64(pq + 1);
+                }
+                Best m {0.0, -1, -1.0f, -1};
+                for (int q = 0; q < splits; ++q)   // uniform over the wave (splits <= 64)
+                {
+                    Best o {__shfl(qc, q, 64), __shfl(qi, q, 64), -1.0f, -1};
+                    if (better(o, m))
+                        m = o;
+                }
+                if (threadIdx.x == 0)
                 {
                     finish = true;
-                    b      = Best {0.0, -1, -1.0f, -1};
-                    for (int q = 0; q < splits; ++q)
-                    {
-                        const uint64_t* pq = part + 2 * (g * splits + q);
-                        Best o {__longlong_as_double((long long) consume_u64(pq)), (int) (uint32_t) consume_u64(pq + 1),
-                                -1.0f, -1};
-                        if (better(o, b))
-                            b = o;
-                    }
+                    b      = m;
                     if (b.idx >= 0)   // the winner's delta / offset, as its lane formed them
                         tfe::candidate(st, fseq, b.idx, b.delta, b.offset);
                     ticket_reset(tickets + g);
                 }
             }
-            if (finish)
-            {
-                float bd = b.idx >= 0 ? b.delta : -1.0f;
-                int bo   = b.idx >= 0 ? b.offset : -1;
-                tfe::Result r = tfe::finish(st, bd, bo);
-                j.out[c]      = aimet_tf_encoding {r.min, r.max, r.delta, r.offset, bw};
-            }
+        }
+        if (threadIdx.x == 0 && finish)
+        {
+            float bd = b.idx >= 0 ? b.delta : -1.0f;
+            int bo   = b.idx >= 0 ? b.offset : -1;
+            tfe::Result r = tfe::finish(st, bd, bo);
+            j.out[c]      = aimet_tf_encoding {r.min, r.max, r.delta, r.offset, bw};
         }
         __syncthreads();
     }

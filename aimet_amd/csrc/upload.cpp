@@ -219,32 +219,45 @@ void scratch_free(void* p, hipStream_t s)
 // nullptr (the caller then launches its fold, or adds per workgroup): the synchronous diagnostics
 // mode, a capture before any eager call made the pool (it cannot be allocated and zeroed inside a
 // capture), or the capture counters used up.
-unsigned* ticket_alloc(hipStream_t s, unsigned count)
+namespace
 {
-    if (sync_alloc())
-        return nullptr;
-    constexpr unsigned kTicketRing = 1u << 16, kTicketCapture = 1u << 16;
-    struct TicketPool
-    {
-        std::mutex m;
-        unsigned* dev = nullptr;
-        unsigned next = 0, captured = 0;
-    };
+constexpr unsigned kTicketRing = 1u << 16, kTicketCapture = 1u << 20;
+constexpr size_t kCaptureArenaFloats = size_t(16) << 20;   // 64 MB of captured launches' partials
+struct TicketPool
+{
+    std::mutex m;
+    unsigned* dev = nullptr;
+    unsigned next = 0, captured = 0;
+    float* arena      = nullptr;   // partial-sum slots of captured launches, handed out once
+    size_t arena_used = 0;
+};
+TicketPool& ticket_pool(int dev)
+{
     static TicketPool pools[kDevices];
-    TicketPool& p = pools[current_device()];
-    const bool cap = s != nullptr && capturing(s);
-    std::lock_guard<std::mutex> lock(p.m);
+    return pools[dev];
+}
+// the pool of the current device, created (and zeroed) on first use outside a capture
+TicketPool* ready_pool(hipStream_t s, bool cap)
+{
+    TicketPool& p = ticket_pool(current_device());
     if (p.dev == nullptr)
     {
         if (cap)
             return nullptr;
         const size_t bytes = sizeof(unsigned) * (kTicketRing + kTicketCapture);
         unsigned* d        = nullptr;
+        float* a           = nullptr;
         AIMET_HIP_CHECK(hipMalloc(&d, bytes));
+        AIMET_HIP_CHECK(hipMalloc(&a, sizeof(float) * kCaptureArenaFloats));
         AIMET_HIP_CHECK(hipMemsetAsync(d, 0, bytes, s));
         AIMET_HIP_CHECK(hipStreamSynchronize(s));   // once per device: zero before any stream uses it
-        p.dev = d;
+        p.dev   = d;
+        p.arena = a;
     }
+    return &p;
+}
+unsigned* take_tickets(TicketPool& p, bool cap, unsigned count)
+{
     if (count == 0 || count > kTicketRing / 16)
         return nullptr;
     if (!cap)
@@ -260,6 +273,58 @@ unsigned* ticket_alloc(hipStream_t s, unsigned count)
     unsigned* t = p.dev + kTicketRing + p.captured;
     p.captured += count;
     return t;
+}
+}   // namespace
+
+unsigned* ticket_alloc(hipStream_t s, unsigned count)
+{
+    if (sync_alloc())
+        return nullptr;
+    const bool cap = s != nullptr && capturing(s);
+    std::lock_guard<std::mutex> lock(ticket_pool(current_device()).m);
+    TicketPool* p = ready_pool(s, cap);
+    return p ? take_tickets(*p, cap, count) : nullptr;
+}
+
+FoldBuffers fold_buffers(hipStream_t s, unsigned tickets, size_t part_floats)
+{
+    FoldBuffers f;
+    if (sync_alloc())
+        return f;
+    const bool cap = s != nullptr && capturing(s);
+    {
+        std::lock_guard<std::mutex> lock(ticket_pool(current_device()).m);
+        TicketPool* p = ready_pool(s, cap);
+        if (p == nullptr)
+            return f;
+        if (cap)
+        {
+            // a captured launch keeps its partials slot for every replay: from the arena, never
+            // handed out again (a graph memory node per replay cost ~10 us of every AdaRound iteration)
+            const size_t n = (part_floats + 63) & ~size_t(63);
+            if (p->arena_used + n > kCaptureArenaFloats)
+                return f;
+            unsigned* t = take_tickets(*p, cap, tickets);
+            if (t == nullptr)
+                return f;
+            f.ticket = t;
+            f.part   = p->arena + p->arena_used;
+            p->arena_used += n;
+            return f;
+        }
+        f.ticket = take_tickets(*p, cap, tickets);
+        if (f.ticket == nullptr)
+            return f;
+    }
+    f.part    = static_cast<float*>(scratch_alloc(sizeof(float) * part_floats, s));
+    f.scratch = true;
+    return f;
+}
+
+void fold_buffers_release(const FoldBuffers& f, hipStream_t s)
+{
+    if (f.scratch && f.part)
+        scratch_free(f.part, s);
 }
 
 void* upload_async(const void* src, size_t bytes, hipStream_t s)

@@ -217,6 +217,69 @@ def test_adaround_loop_deterministic(kind):
     assert torch.equal(a[0], a[1]), AdaroundOptimizer.last_loop_form
 
 
+def _loop_problem(kind, seed=3):
+    torch.manual_seed(seed)
+    if kind == "stem":
+        m, shape_in = nn.Conv2d(3, 16, 3, stride=2, padding=1), (64, 3, 32, 32)
+    elif kind == "dw":
+        m, shape_in = nn.Conv2d(16, 16, 3, padding=1, groups=16), (64, 16, 14, 14)
+    elif kind == "pointwise_wide":
+        m, shape_in = nn.Conv2d(576, 96, 1), (64, 576, 14, 14)
+    else:
+        m, shape_in = nn.Linear(96, 40), (64, 96)
+    m = m.to(DEV)
+    inp = torch.rand(shape_in, device=DEV)
+    with torch.no_grad():
+        out = m(inp) + 0.01 * torch.randn_like(m(inp))
+    d = (m.weight.detach().abs().max() / 127).reshape(1)
+    o = torch.full((1,), -128.0, device=DEV)
+    return m, inp, out, d, o
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("kind", ["stem", "dw", "pointwise_wide", "linear"])
+def test_adaround_multi_iteration_graph_equals_one_per_graph(monkeypatch, kind):
+    """k iterations captured in one HIP graph (AIMET_ADA_GRAPH_ITERS; the counters and the batch
+    table live on the device) give the alpha of one iteration per graph, bit for bit, also when k
+    does not divide the iteration count (the rest replays the one-iteration graph)."""
+    import aimet_amd.adaround_optimizer as ao
+    from aimet_amd.adaround_optimizer import AdaroundHyperParameters, AdaroundOptimizer
+    m, inp, out, d, o = _loop_problem(kind)
+    p = AdaroundHyperParameters(num_iterations=303, warm_start=0.2)
+    res = []
+    for k in (1, 10, 7):
+        monkeypatch.setattr(ao, "_GRAPH_ITERS", k)
+        loss = torch.zeros(1, device=DEV)
+        a = AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, nn.ReLU6(), torch.Generator().manual_seed(5),
+                                                loss)
+        res.append((a.detach().clone(), loss.clone()))
+    for a, loss in res[1:]:
+        assert torch.equal(a, res[0][0]), (kind, AdaroundOptimizer.last_loop_form)
+        assert torch.equal(loss, res[0][1])
+
+
+@pytest.mark.gpu
+@gpu
+def test_adaround_pw_cm_mfma_loop_close_to_library_form(monkeypatch):
+    """The channel-major 1x1 loop on the f32 matrix cores (AIMET_ADA_PW_CM_FUSED=1) is
+    deterministic and gives the library-GEMM form's alpha to fp32 summation-order tolerance."""
+    import aimet_amd.adaround_optimizer as ao
+    from aimet_amd.adaround_optimizer import AdaroundHyperParameters, AdaroundOptimizer
+    m, inp, out, d, o = _loop_problem("pointwise_wide")
+    p = AdaroundHyperParameters(num_iterations=200, warm_start=0.2)
+    res = {}
+    for fused in (True, True, False):
+        monkeypatch.setattr(ao, "_PW_CM_FUSED", fused)
+        a = AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, nn.ReLU6(),
+                                                torch.Generator().manual_seed(5)).detach().clone()
+        assert AdaroundOptimizer.last_loop_form == ("pointwise_cm_mfma" if fused else "pointwise_cm")
+        if fused in res:
+            assert torch.equal(a, res[fused])
+        res[fused] = a
+    torch.testing.assert_close(res[True], res[False], rtol=1e-4, atol=1e-4)
+
+
 @pytest.mark.gpu
 @gpu
 @pytest.mark.parametrize("stride,act", [(1, nn.ReLU6()), (2, nn.ReLU()), (1, None)])
