@@ -10,9 +10,11 @@
 //
 //  * aimet_adaround_pw_cm_forward: g[co][p] = recon_g(sum_ci W[co][ci] x[ci][p] + bias[co],
 //    target) for p = b * hw + t over the batch, x[ci][p] gathered in place from row
-//    idx_all[it][b] of the input cache (no channel-major copy), the target read in place; 64 x 64
-//    output tiles, 32-deep K chunks staged in LDS, one 32 x 32 v_mfma_f32_32x32x2_f32 accumulator
-//    per wave (the f32 matrix instruction: exact fmaf chains in ci order, deterministic);
+//    idx_all[it][b] of the input cache (no channel-major copy), the target read in place; each wave
+//    owns a 32 x 64 sub-tile (two v_mfma_f32_32x32x2_f32 accumulators: the f32 matrix instruction,
+//    exact fmaf chains), stages 16-deep K chunks in its own LDS slot with the next chunk's loads in
+//    flight, and deep sums are split over up to 4 waves whose accumulators are added in a fixed
+//    order (deterministic);
 //  * aimet_adaround_pw_cm_wgrad: part[s][co][ci] = sum over the positions of slice s of
 //    g[co][p] x[ci][p] (x gathered again), slices over the positions so that the small
 //    [Cout][Cin] output still fills the chip; aimet_adaround_backward_adam_parts adds the slices
@@ -30,10 +32,10 @@ namespace
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-constexpr int kT  = 64;   // output tile (rows x columns), 2 x 2 waves of 32 x 32
-constexpr int kKc = 32;   // K chunk staged in LDS per step
-constexpr int kLdA = kKc + 1;    // [64][33]: lanes reading one k column hit distinct banks
-constexpr int kLdB = kT + 4;     // [32][68]
+constexpr int kKc  = 16;          // K chunk per wave step
+constexpr int kLdA = kKc + 1;     // [32][17]: the lanes reading one k column hit distinct banks
+constexpr int kLdB = 64 + 4;      // [16][68]
+constexpr int kStage = 32 * kLdA + kKc * kLdB;   // one wave's staging floats
 
 struct CmBatch
 {
@@ -44,117 +46,219 @@ struct CmBatch
     FastDiv div_hw;
 };
 
-// x[ci][p] of this iteration's batch (0 outside the problem)
-__device__ __forceinline__ float load_x(const CmBatch& B, const int64_t* rows, uint32_t ci, uint32_t p)
+// the LDS writes of this wave visible to its own lanes (wave-local staging, in-order LDS)
+__device__ __forceinline__ void wave_sync()
 {
-    if (ci >= B.Cin || p >= B.P)
-        return 0.0f;
-    const uint32_t b = B.div_hw.div(p), t = p - b * B.hw;
-    return B.x[((size_t) rows[b] * B.Cin + ci) * B.hw + t];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// acc += A[64 x kKc] . B[kKc x 64] for this wave's 32 x 32 quarter (wr, wc): 16 MFMA steps of k = 2
-__device__ __forceinline__ void mfma_chunk(const float (*As)[kLdA], const float (*Bs)[kLdB], int wr, int wc, f32x16& acc)
+// acc0 / acc1 += A[32 x kKc] . B[kKc x 64] (columns 0-31 / 32-63): kKc / 2 steps of the 32 x 32 x 2
+// f32 MFMA, the two accumulators' chains interleaved
+__device__ __forceinline__ void mfma_chunk(const float* As, const float* Bs, f32x16& acc0, f32x16& acc1)
 {
     const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
 #pragma unroll
-    for (int s = 0; s < kKc / 2; ++s)
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(As[wr * 32 + i][2 * s + h], Bs[2 * s + h][wc * 32 + i], acc, 0, 0, 0);
+    for (int st = 0; st < kKc / 2; ++st)
+    {
+        const float a = As[i * kLdA + 2 * st + h];
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[(2 * st + h) * kLdB + i], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[(2 * st + h) * kLdB + 32 + i], acc1, 0, 0, 0);
+    }
 }
 
-// forward + reconstruction gradient: tile (blockIdx.y: 64 output channels, blockIdx.x: 64 positions)
+// SK > 1 waves computed the same 32 x 64 sub-tile over interleaved K chunks: wave `part` 0 adds the
+// others' accumulators in part order (deterministic). Every thread of the workgroup calls it.
+template <int SK>
+__device__ __forceinline__ void reduce_parts(f32x16& acc0, f32x16& acc1, float* red)
+{
+    if constexpr (SK > 1)
+    {
+        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, part = wave % SK;
+        if (part != 0)
+        {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+            {
+                red[(wave * 32 + r) * 64 + lane]      = acc0[r];
+                red[(wave * 32 + 16 + r) * 64 + lane] = acc1[r];
+            }
+        }
+        __syncthreads();
+        if (part == 0)
+            for (int q = 1; q < SK; ++q)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                {
+                    acc0[r] += red[((wave + q) * 32 + r) * 64 + lane];
+                    acc1[r] += red[((wave + q) * 32 + 16 + r) * 64 + lane];
+                }
+    }
+}
+
+// forward + reconstruction gradient. A workgroup's 4 waves cover 4 / SK sub-tiles of 32 output
+// channels x 64 positions (blockIdx.y: channel block, blockIdx.x: 64 positions); the SK waves of a
+// sub-tile take the Cin chunks part, part + SK, ... (each with the next chunk's loads in flight
+// while its MFMAs run), and their accumulators are added in part order.
+template <int SK>
 __global__ __launch_bounds__(256) void pw_cm_forward_kernel(CmBatch B, const float* __restrict__ target,
                                                             const float* __restrict__ w, const float* __restrict__ bias,
                                                             float* __restrict__ g, int64_t* __restrict__ it_next,
                                                             float scale, int act)
 {
-    __shared__ float As[kT][kLdA];   // W[co][ci]
-    __shared__ float Bs[kKc][kLdB];  // x[ci][p]
+    constexpr int SUB = 4 / SK;
+    __shared__ float stage[4][kStage];
+    __shared__ float red[SK > 1 ? 4 * 32 * 64 : 1];
     const int64_t it = B.it_cur[0];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         it_next[0] = it + 1;
     const int64_t* rows = B.idx_all + it * B.nb;
-    const uint32_t p0 = blockIdx.x * kT, co0 = blockIdx.y * kT;
-    const int tid = threadIdx.x, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
-    f32x16 acc = {};
-    for (uint32_t k0 = 0; k0 < B.Cin; k0 += kKc)
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, part = wave % SK;
+    const uint32_t co0 = blockIdx.y * (32 * SUB) + (wave / SK) * 32, p0 = blockIdx.x * 64;
+    // B loads: lane = position p0 + lane, k = 0 .. kKc - 1 (consecutive positions across lanes)
+    const uint32_t pl = p0 + lane;
+    const bool pv     = pl < B.P;
+    size_t xbase      = 0;
+    if (pv)
     {
-#pragma unroll
-        for (int j = 0; j < kT * kKc / 256; ++j)   // A: 64 x 32, consecutive ci across lanes
-        {
-            const int e = tid + 256 * j, r = e / kKc, k = e % kKc;
-            const uint32_t co = co0 + r, ci = k0 + k;
-            As[r][k] = (co < B.Cout && ci < B.Cin) ? w[(size_t) co * B.Cin + ci] : 0.0f;
-        }
-#pragma unroll
-        for (int j = 0; j < kT * kKc / 256; ++j)   // B: 32 x 64, consecutive positions across lanes
-        {
-            const int e = tid + 256 * j, k = e / kT, c = e % kT;
-            Bs[k][c] = load_x(B, rows, k0 + k, p0 + c);
-        }
-        __syncthreads();
-        mfma_chunk(As, Bs, wr, wc, acc);
-        __syncthreads();
+        const uint32_t b = B.div_hw.div(pl);
+        xbase            = (size_t) rows[b] * B.Cin * B.hw + (pl - b * B.hw);
     }
-    // C/D map of the 32 x 32 f32 MFMA: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-    const int lane = tid & 63;
-    const uint32_t p = p0 + wc * 32 + (lane & 31);
-    if (p >= B.P)
-        return;
-    const uint32_t b = B.div_hw.div(p), t = p - b * B.hw;
-    const float* trow = target + (size_t) rows[b] * B.Cout * B.hw + t;
+    // A loads: k = lane & 15, rows (lane >> 4) + 4 j
+    const int ak = lane & 15, ar = lane >> 4;
+    float* As = stage[wave];
+    float* Bs = As + 32 * kLdA;
+    const uint32_t nch = (B.Cin + kKc - 1) / kKc;
+    float ra[8], rb[kKc];
+    auto load = [&](uint32_t c) {
+        const uint32_t k0 = c * kKc;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
+        for (int j = 0; j < 8; ++j)
+        {
+            const uint32_t co = co0 + ar + 4 * j, ci = k0 + ak;
+            ra[j] = (co < B.Cout && ci < B.Cin) ? w[(size_t) co * B.Cin + ci] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < kKc; ++k)
+            rb[k] = (pv && k0 + k < B.Cin) ? B.x[xbase + (size_t) (k0 + k) * B.hw] : 0.0f;
+    };
+    f32x16 acc0 = {}, acc1 = {};
+    uint32_t c = part;
+    if (c < nch)
+        load(c);
+    for (; c < nch; c += SK)
     {
-        const uint32_t co = co0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (co < B.Cout)
-            g[(size_t) co * B.P + p] = recon_g(acc[r] + (bias ? bias[co] : 0.0f), trow[(size_t) co * B.hw], scale, act);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            As[(ar + 4 * j) * kLdA + ak] = ra[j];
+#pragma unroll
+        for (int k = 0; k < kKc; ++k)
+            Bs[k * kLdB + lane] = rb[k];
+        wave_sync();
+        if (c + SK < nch)
+            load(c + SK);
+        mfma_chunk(As, Bs, acc0, acc1);
+        wave_sync();
+    }
+    reduce_parts<SK>(acc0, acc1, red);
+    if (part != 0)
+        return;
+    // C/D map of the 32 x 32 f32 MFMA: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+    {
+        const uint32_t p = p0 + 32 * h + (lane & 31);
+        if (p >= B.P)
+            continue;
+        const uint32_t b = B.div_hw.div(p), t = p - b * B.hw;
+        const float* trow = target + (size_t) rows[b] * B.Cout * B.hw + t;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+        {
+            const uint32_t co = co0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            const float q     = h ? acc1[r] : acc0[r];
+            if (co < B.Cout)
+                g[(size_t) co * B.P + p] = recon_g(q + (bias ? bias[co] : 0.0f), trow[(size_t) co * B.hw], scale, act);
+        }
     }
 }
 
-// weight-gradient slice s (blockIdx.z) for the tile (blockIdx.y: 64 output channels, blockIdx.x:
-// 64 input channels): sum over the slice's positions in order, K chunks of 32 positions
+// weight-gradient slice s (blockIdx.z): sub-tile 32 output channels (blockIdx.y) x 64 input channels
+// (blockIdx.x); the 4 waves take the slice's 16-position chunks part, part + 4, ... and are added in
+// part order
 __global__ __launch_bounds__(256) void pw_cm_wgrad_kernel(CmBatch B, const float* __restrict__ g,
-                                                          float* __restrict__ part, uint32_t per_slice)
+                                                          float* __restrict__ part_out, uint32_t per_slice)
 {
-    __shared__ float As[kT][kLdA];   // g[co][p]
-    __shared__ float Bs[kKc][kLdB];  // x[ci][p], stored [p][ci]
+    constexpr int SK = 4;
+    __shared__ float stage[4][kStage];
+    __shared__ float red[4 * 32 * 64];
     const int64_t it    = B.it_cur[0];
     const int64_t* rows = B.idx_all + it * B.nb;
-    const uint32_t ci0 = blockIdx.x * kT, co0 = blockIdx.y * kT;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, part = wave;
+    const uint32_t ci0 = blockIdx.x * 64, co0 = blockIdx.y * 32;
     const uint32_t ps = blockIdx.z * per_slice, pe = ps + per_slice < B.P ? ps + per_slice : B.P;
-    const int tid = threadIdx.x, wave = tid >> 6, wr = wave >> 1, wc = wave & 1;
-    f32x16 acc = {};
-    for (uint32_t k0 = ps; k0 < pe; k0 += kKc)
+    const int kk = lane & 15, sub = lane >> 4;   // position in the chunk, row / column group
+    float* As = stage[wave];
+    float* Bs = As + 32 * kLdA;
+    float ra[8], rb[16];
+    auto load = [&](uint32_t k0) {
+        const uint32_t p = k0 + kk;
+        const bool in    = p < pe;
+        size_t xb        = 0;
+        if (in)
+        {
+            const uint32_t b = B.div_hw.div(p);
+            xb               = (size_t) rows[b] * B.Cin * B.hw + (p - b * B.hw);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j)   // A: g[co][p], 4 rows x 16 consecutive positions per load
+        {
+            const uint32_t co = co0 + sub + 4 * j;
+            ra[j] = (in && co < B.Cout) ? g[(size_t) co * B.P + p] : 0.0f;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j)   // B: x[ci][p], 4 input channels x 16 consecutive positions per load
+        {
+            const uint32_t ci = ci0 + sub + 4 * j;
+            rb[j] = (in && ci < B.Cin) ? B.x[xb + (size_t) ci * B.hw] : 0.0f;
+        }
+    };
+    f32x16 acc0 = {}, acc1 = {};
+    uint32_t k0 = ps + part * kKc;
+    if (k0 < pe)
+        load(k0);
+    for (; k0 < pe; k0 += SK * kKc)
     {
 #pragma unroll
-        for (int j = 0; j < kT * kKc / 256; ++j)   // A: g rows, consecutive positions across lanes
-        {
-            const int e = tid + 256 * j, r = e / kKc, k = e % kKc;
-            const uint32_t co = co0 + r, p = k0 + k;
-            As[r][k] = (co < B.Cout && p < pe) ? g[(size_t) co * B.P + p] : 0.0f;
-        }
+        for (int j = 0; j < 8; ++j)
+            As[(sub + 4 * j) * kLdA + kk] = ra[j];
 #pragma unroll
-        for (int j = 0; j < kT * kKc / 256; ++j)   // B: x^T, consecutive positions across lanes
-        {
-            const int e = tid + 256 * j, c = e / kKc, k = e % kKc;
-            Bs[k][c] = k0 + k < pe ? load_x(B, rows, ci0 + c, k0 + k) : 0.0f;
-        }
-        __syncthreads();
-        mfma_chunk(As, Bs, wr, wc, acc);
-        __syncthreads();
+        for (int j = 0; j < 16; ++j)
+            Bs[kk * kLdB + sub + 4 * j] = rb[j];
+        wave_sync();
+        if (k0 + SK * kKc < pe)
+            load(k0 + SK * kKc);
+        mfma_chunk(As, Bs, acc0, acc1);
+        wave_sync();
     }
-    const int lane = tid & 63;
-    const uint32_t ci = ci0 + wc * 32 + (lane & 31);
-    if (ci >= B.Cin)
+    reduce_parts<SK>(acc0, acc1, red);
+    if (part != 0)
         return;
-    float* out = part + (size_t) blockIdx.z * B.Cout * B.Cin;
+    float* out = part_out + (size_t) blockIdx.z * B.Cout * B.Cin;
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
+    for (int h = 0; h < 2; ++h)
     {
-        const uint32_t co = co0 + wr * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (co < B.Cout)
-            out[(size_t) co * B.Cin + ci] = acc[r];
+        const uint32_t ci = ci0 + 32 * h + (lane & 31);
+        if (ci >= B.Cin)
+            continue;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+        {
+            const uint32_t co = co0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+            if (co < B.Cout)
+                out[(size_t) co * B.Cin + ci] = h ? acc1[r] : acc0[r];
+        }
     }
 }
 
@@ -194,9 +298,18 @@ int aimet_adaround_pw_cm_forward(const float* x_cache, const float* target_cache
         if (bias)
             require_device_ptr(bias, "bias");
         const float scale = (float) (2.0 / (double) (nb * hw));   // as aimet_adaround_recon_grad_indexed_cm
-        const dim3 grid((unsigned) ceil_div(B.P, kT), (unsigned) ceil_div(Cout, kT));
+        // waves per sub-tile by the depth of the sum: deep Cin splits over the workgroup's waves
+        const int sk      = Cin >= 256 ? 4 : (Cin >= 96 ? 2 : 1);
+        const int64_t sub = 32 * (4 / sk);
+        const dim3 grid((unsigned) ceil_div((int64_t) B.P, (int64_t) 64), (unsigned) ceil_div(Cout, sub));
         AIMET_REQUIRE(grid.y <= 65535, "too many output channels");
-        pw_cm_forward_kernel<<<grid, 256, 0, as_stream(stream)>>>(B, target_cache, w, bias, grad_q, it_next, scale, act);
+        hipStream_t st = as_stream(stream);
+        if (sk == 4)
+            pw_cm_forward_kernel<4><<<grid, 256, 0, st>>>(B, target_cache, w, bias, grad_q, it_next, scale, act);
+        else if (sk == 2)
+            pw_cm_forward_kernel<2><<<grid, 256, 0, st>>>(B, target_cache, w, bias, grad_q, it_next, scale, act);
+        else
+            pw_cm_forward_kernel<1><<<grid, 256, 0, st>>>(B, target_cache, w, bias, grad_q, it_next, scale, act);
         AIMET_LAUNCH_CHECK();
     });
 }
@@ -206,11 +319,11 @@ int aimet_adaround_pw_cm_wgrad_slices(int64_t nb, int64_t Cin, int64_t Cout, int
     return guarded([&] {
         AIMET_REQUIRE(slices != nullptr, "slices is null");
         AIMET_REQUIRE(nb > 0 && Cin > 0 && Cout > 0 && hw > 0, "invalid shape");
-        // enough slices for ~2 workgroups per CU, each at least 8 K chunks of positions deep
-        const int64_t tiles = ceil_div(Cin, kT) * ceil_div(Cout, kT), P = nb * hw;
-        int64_t s = ceil_div(512, tiles);
-        const int64_t smax = std::max<int64_t>(1, P / (8 * kKc));
-        *slices = std::min<int64_t>(std::min<int64_t>(s, smax), 64);
+        // enough slices for ~2 workgroups per CU, each at least 2 chunks deep per wave
+        const int64_t tiles = ceil_div(Cin, (int64_t) 64) * ceil_div(Cout, (int64_t) 32), P = nb * hw;
+        const int64_t s     = ceil_div((int64_t) 512, tiles);
+        const int64_t smax  = std::max<int64_t>(1, P / (8 * kKc));
+        *slices             = std::min<int64_t>(std::min<int64_t>(s, smax), 64);
     });
 }
 
@@ -225,8 +338,8 @@ int aimet_adaround_pw_cm_wgrad(const float* x_cache, const int64_t* idx_all, con
         AIMET_REQUIRE(slices >= 1 && slices <= 65535, "slices out of range");
         // slice boundaries on K-chunk multiples: every slice but the last holds whole chunks
         const int64_t per = ceil_div(ceil_div((int64_t) B.P, slices), (int64_t) kKc) * kKc;
-        AIMET_REQUIRE(ceil_div((int64_t) B.P, per) <= slices, "slices");
-        const dim3 grid((unsigned) ceil_div(Cin, kT), (unsigned) ceil_div(Cout, kT), (unsigned) slices);
+        const dim3 grid((unsigned) ceil_div(Cin, (int64_t) 64), (unsigned) ceil_div(Cout, (int64_t) 32),
+                        (unsigned) slices);
         AIMET_REQUIRE(grid.y <= 65535, "too many output channels");
         pw_cm_wgrad_kernel<<<grid, 256, 0, as_stream(stream)>>>(B, grad_q, parts, (uint32_t) per);
         AIMET_LAUNCH_CHECK();
