@@ -182,7 +182,8 @@ _PROTOTYPES = {
                                      _vp],
     "aimet_adaround_backward_adam_parts": [_vp, _vp, _vp, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp,
                                            _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
-                                           _vp, _vp, _vp],
+                                           _vp, _vp, _vp, _vp],
+    "aimet_adaround_adam_bias_corrections": [ctypes.c_double, ctypes.c_double, _i64, _vp, _vp],
     "aimet_adaround_pw_cm_forward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp],
     "aimet_adaround_pw_cm_wgrad_slices": [_i64, _i64, _i64, _i64, _vp],
     "aimet_adaround_pw_cm_wgrad": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp],

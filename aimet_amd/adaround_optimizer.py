@@ -577,6 +577,11 @@ class AdaroundOptimizer:
         P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
         it_cur, it_next = ctypes.c_void_p(counters.data_ptr()), ctypes.c_void_p(counters.data_ptr() + 8)
         adam = (ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999), ctypes.c_double(1e-8))
+        # Adam's bias corrections for every step of the loop, computed once (the same device
+        # arithmetic the step would run per wave: same bits)
+        bias_corr = torch.empty(iters, 2, dtype=torch.float32, device=dev)
+        _native.check(lib.aimet_adaround_adam_bias_corrections(adam[1], adam[2], iters, P(bias_corr),
+                                                               ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)))
         loss_ptr = P(round_loss_out) if round_loss_out is not None else None
         code = _act_code(act_func)
         out_shape = tuple(out_data.shape[1:])
@@ -642,9 +647,10 @@ class AdaroundOptimizer:
         def adam_step(gw, s):
             # the Adam step also writes the next iteration's soft-quantized weight into wq (it reads
             # W and the new alpha anyway): no separate forward launch per iteration
-            _native.check(lib.aimet_adaround_backward_adam(sq.pw, sq.pa, P(gw), P(exp_avg), P(exp_avg_sq), *sq.shape,
-                                                           sq.pd, sq.po, sq.bw, P(rb_all), it_next, it_cur, *adam,
-                                                           loss_ptr, P(wq) if fuse_wq else None, s))
+            _native.check(lib.aimet_adaround_backward_adam_parts(sq.pw, sq.pa, P(gw), 1, P(exp_avg), P(exp_avg_sq),
+                                                                 *sq.shape, sq.pd, sq.po, sq.bw, P(rb_all), it_next,
+                                                                 it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None,
+                                                                 P(bias_corr), s))
 
         def soft_weight():   # wq from the current alpha (before the first iteration)
             s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -676,7 +682,7 @@ class AdaroundOptimizer:
                                                              parts.shape[0], nb, cin_cm, C_out, hw, s))
                 _native.check(lib.aimet_adaround_backward_adam_parts(
                     sq.pw, sq.pa, P(parts), parts.shape[0], P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po,
-                    sq.bw, P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, s))
+                    sq.bw, P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, P(bias_corr), s))
                 return
             if mode in ("pointwise", "im2col") and cm is not None:
                 # channel-major batch: one GEMM per direction over all nb * hw positions

@@ -722,6 +722,26 @@ __device__ __forceinline__ float adam_elem(float param, float grad, float& exp_a
     return param;
 }
 
+// ATen: 1 - pow_(beta, float step) in double, handed to adam_math as float (bias_correction2 as
+// its square root); one definition for the in-kernel path and the per-step table, so both give
+// the same bits
+__device__ __forceinline__ void adam_bias_corrections(double beta1, double beta2, int64_t step, float& bc1,
+                                                      float& bc2s)
+{
+    const float step_f = (float) step;
+    bc1                = (float) (1 - pow(beta1, (double) step_f));
+    bc2s               = (float) sqrt(1 - pow(beta2, (double) step_f));
+}
+
+// bias_corr[2 (step - 1) ..] = {bc1, bc2s} for step = 1 .. steps
+__global__ __launch_bounds__(kBlock) void adam_bias_corr_kernel(double beta1, double beta2, int64_t steps,
+                                                                float* __restrict__ bias_corr)
+{
+    const int64_t i = (int64_t) blockIdx.x * kBlock + threadIdx.x;
+    if (i < steps)
+        adam_bias_corrections(beta1, beta2, i + 1, bias_corr[2 * i], bias_corr[2 * i + 1]);
+}
+
 // dL/dalpha (ada_bwd, with this iteration's {reg, beta, beta - 1} from reg_beta_all[it]) and the
 // Adam update of alpha in place; `step` = it_next[0] (= it + 1, written by the gather kernel of the
 // same iteration), workgroup 0 publishes it to it_cur for the next iteration's gather.
@@ -739,7 +759,8 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                                                                    float* __restrict__ round_loss,
                                                                    float* __restrict__ wq_next,
                                                                    float* __restrict__ loss_part,
-                                                                   unsigned* __restrict__ ticket, uint32_t nparts)
+                                                                   unsigned* __restrict__ ticket, uint32_t nparts,
+                                                                   const float* __restrict__ bias_corr)
 {
     const int64_t step = it_next[0];
     if (blockIdx.x == 0 && threadIdx.x == 0)
@@ -748,10 +769,16 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
     p.reg           = rb[0];
     p.beta          = rb[1];
     p.beta_m1       = rb[2];
-    // ATen: 1 - pow_(beta, float step) in double, handed to adam_math as float
-    const float step_f = (float) step;
-    const float bc1    = (float) (1 - pow(adam.beta1, (double) step_f));
-    const float bc2s   = (float) sqrt(1 - pow(adam.beta2, (double) step_f));
+    // ATen's bias corrections: from the per-step table when given (two loads instead of ~540
+    // dependent f64 instructions ahead of every wave's first element), else computed here
+    float bc1, bc2s;
+    if (bias_corr)
+    {
+        bc1  = bias_corr[2 * (step - 1)];
+        bc2s = bias_corr[2 * (step - 1) + 1];
+    }
+    else
+        adam_bias_corrections(adam.beta1, adam.beta2, step, bc1, bc2s);
     float loss         = 0.0f;
     if (VEC)
     {
@@ -918,41 +945,60 @@ __device__ __forceinline__ float recon_bias(const ReconIdx& r, uint32_t e_in_row
 
 // Channel-major batches of a 1x1 layer's GEMM form: x_cm[ci][b][hw] = src_in[idx[it][b]][ci][hw]
 // (one GEMM over all positions then gives q_cm[co][b][hw] and the weight gradient
-// g_cm[co][(b, hw)] x_cm[ci][(b, hw)]^T, no per-sample GEMMs and no batch sum); blockIdx.y = ci * nb + b;
-// workgroup (0, 0) sets it_next = it + 1
+// g_cm[co][(b, hw)] x_cm[ci][(b, hw)]^T, no per-sample GEMMs and no batch sum). Flat over the
+// destination, PER consecutive elements per lane (4 when hw % 4 == 0: one 16-B load and store,
+// the quad inside one plane); a workgroup per (ci, b) plane of 49..196 floats ran at 11 us for
+// 1.6 MB. Workgroup 0 sets it_next = it + 1.
+template <int PER>
 __global__ __launch_bounds__(kBlock) void adaround_gather_cm_kernel(const float* __restrict__ src_in,
                                                                     float* __restrict__ dst,
                                                                     const int64_t* __restrict__ idx_all,
                                                                     const int64_t* __restrict__ it_cur,
                                                                     int64_t* __restrict__ it_next, uint32_t nb,
-                                                                    uint32_t Cin, uint32_t hw)
+                                                                    uint32_t Cin, uint32_t hw, uint32_t n,
+                                                                    FastDiv div_hw, FastDiv div_nb)
 {
     const int64_t it = it_cur[0];
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
         it_next[0] = it + 1;
-    const uint32_t ci = blockIdx.y / nb, b = blockIdx.y - ci * nb;
-    const float* src  = src_in + ((size_t) idx_all[it * nb + b] * Cin + ci) * hw;
-    float* d          = dst + (size_t) blockIdx.y * hw;
-    for (uint32_t t = blockIdx.x * kBlock + threadIdx.x; t < hw; t += gridDim.x * kBlock)
-        d[t] = __builtin_nontemporal_load(src + t);
+    const uint32_t i = (blockIdx.x * kBlock + threadIdx.x) * PER;
+    if (i >= n)
+        return;
+    const uint32_t row = div_hw.div(i), t = i - row * hw;   // row = ci * nb + b
+    const uint32_t ci = div_nb.div(row), b = row - ci * nb;
+    const float* src  = src_in + ((size_t) idx_all[it * nb + b] * Cin + ci) * hw + t;
+    if constexpr (PER == 4)
+        *reinterpret_cast<f4*>(dst + i) = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src));
+    else
+        dst[i] = __builtin_nontemporal_load(src);
 }
 
 // recon_grad_idx_kernel for channel-major q / g ([C][nb][hw]): element i = (co nb + b) hw + t reads
-// the target out_data[idx[it][b]][co][t]; bias added first as there
+// the target out_data[idx[it][b]][co][t]; bias added first as there. PER = 4 when hw % 4 == 0.
+template <int PER>
 __global__ __launch_bounds__(kBlock) void recon_grad_idx_cm_kernel(const float* __restrict__ q, float* __restrict__ g,
                                                                    ReconIdx r, float scale, int act)
 {
     const int64_t it   = r.it_cur[0];
     const uint32_t n   = (uint32_t) (r.C * r.nb * r.hw);
-    const uint32_t i   = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t i   = (blockIdx.x * kBlock + threadIdx.x) * PER;
     if (i >= n)
         return;
     const uint32_t row = r.div_hw.div(i);   // co * nb + b
     const uint32_t t   = i - row * (uint32_t) r.hw;
     const uint32_t co  = r.div_c.div(row);   // div_c holds nb here
     const uint32_t b   = row - co * (uint32_t) r.nb;
-    const float tv     = r.out_data[((size_t) r.idx_all[it * r.nb + b] * r.C + co) * r.hw + t];
-    g[i] = recon_g(q[i] + (r.bias ? r.bias[co] : 0.0f), tv, scale, act);
+    const float* tp    = r.out_data + ((size_t) r.idx_all[it * r.nb + b] * r.C + co) * r.hw + t;
+    const float bs     = r.bias ? r.bias[co] : 0.0f;
+    if constexpr (PER == 4)
+    {
+        const f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(q + i));
+        const f4 c = __builtin_nontemporal_load(reinterpret_cast<const f4*>(tp));
+        *reinterpret_cast<f4*>(g + i) = f4 {recon_g(a.x + bs, c.x, scale, act), recon_g(a.y + bs, c.y, scale, act),
+                                            recon_g(a.z + bs, c.z, scale, act), recon_g(a.w + bs, c.w, scale, act)};
+    }
+    else
+        g[i] = recon_g(q[i] + bs, *tp, scale, act);
 }
 
 template <bool VEC>
@@ -1215,16 +1261,23 @@ int aimet_adaround_gather_cm(const float* src_in, float* dst, const int64_t* idx
 {
     return guarded([&] {
         AIMET_REQUIRE(nb > 0 && Cin > 0 && hw > 0, "invalid shape");
-        AIMET_REQUIRE(Cin * nb <= 65535 && Cin * nb * hw < (int64_t(1) << 31), "batch too large for the channel-major gather");
+        AIMET_REQUIRE(Cin * nb * hw < (int64_t(1) << 31), "batch too large for the channel-major gather");
         require_device_ptr(src_in, "src_in");
         require_device_ptr(dst, "dst");
         require_device_ptr(idx_all, "idx_all");
         require_device_ptr(it_cur, "it_cur");
         require_device_ptr(it_next, "it_next");
-        int64_t bx = ceil_div(hw, (int64_t) kBlock);
-        bx         = bx > 64 ? 64 : bx;
-        adaround_gather_cm_kernel<<<dim3((unsigned) bx, (unsigned) (Cin * nb)), kBlock, 0, as_stream(stream)>>>(
-            src_in, dst, idx_all, it_cur, it_next, (uint32_t) nb, (uint32_t) Cin, (uint32_t) hw);
+        const int64_t n = Cin * nb * hw;
+        const bool vec  = hw % 4 == 0 && aligned16(src_in) && aligned16(dst);
+        const int per   = vec ? 4 : 1;
+        const unsigned blocks = (unsigned) ceil_div(n, (int64_t) kBlock * per);
+        const FastDiv dhw((uint32_t) hw), dnb((uint32_t) nb);
+        if (vec)
+            adaround_gather_cm_kernel<4><<<blocks, kBlock, 0, as_stream(stream)>>>(
+                src_in, dst, idx_all, it_cur, it_next, (uint32_t) nb, (uint32_t) Cin, (uint32_t) hw, (uint32_t) n, dhw, dnb);
+        else
+            adaround_gather_cm_kernel<1><<<blocks, kBlock, 0, as_stream(stream)>>>(
+                src_in, dst, idx_all, it_cur, it_next, (uint32_t) nb, (uint32_t) Cin, (uint32_t) hw, (uint32_t) n, dhw, dnb);
         AIMET_LAUNCH_CHECK();
     });
 }
@@ -1248,8 +1301,12 @@ int aimet_adaround_recon_grad_indexed_cm(const float* q, const float* out_data, 
         const float scale = (float) (2.0 / (double) (nb * hw));   // as aimet_adaround_recon_grad_indexed
         ReconIdx r {out_data, idx_all, it_cur, bias, nb, C * hw, hw, C,
                     FastDiv((uint32_t) (C * hw)), FastDiv((uint32_t) hw), FastDiv((uint32_t) nb)};
-        recon_grad_idx_cm_kernel<<<(unsigned) ceil_div(n, (int64_t) kBlock), kBlock, 0, as_stream(stream)>>>(q, g, r,
-                                                                                                     scale, act);
+        if (hw % 4 == 0 && aligned16(q) && aligned16(out_data) && aligned16(g))
+            recon_grad_idx_cm_kernel<4><<<(unsigned) ceil_div(n, (int64_t) kBlock * 4), kBlock, 0, as_stream(stream)>>>(
+                q, g, r, scale, act);
+        else
+            recon_grad_idx_cm_kernel<1><<<(unsigned) ceil_div(n, (int64_t) kBlock), kBlock, 0, as_stream(stream)>>>(
+                q, g, r, scale, act);
         AIMET_LAUNCH_CHECK();
     });
 }
@@ -1258,10 +1315,13 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
                                        float* exp_avg, float* exp_avg_sq, int64_t outer, int64_t C, int64_t K,
                                        const float* delta, const float* offset, int32_t bw, const float* reg_beta_all,
                                        const int64_t* it_next, int64_t* it_cur, double lr, double beta1, double beta2,
-                                       double eps, float* round_loss, float* wq_next, void* stream)
+                                       double eps, float* round_loss, float* wq_next, const float* bias_corr,
+                                       void* stream)
 {
     return guarded([&] {
         AIMET_REQUIRE(outer >= 0 && C > 0 && K >= 0, "invalid shape");
+        if (bias_corr)
+            require_device_ptr(bias_corr, "bias_corr");
         if (wq_next)
             require_device_ptr(wq_next, "wq_next");
         const int64_t n = outer * C * K;
@@ -1295,11 +1355,11 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
         if (vec)
             adaround_bwd_adam_kernel<true><<<(unsigned) blocks, kBlock, 0, st>>>(
                 w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss, wq_next, lf.part, lf.ticket, (uint32_t) nparts);
+                it_cur, a, round_loss, wq_next, lf.part, lf.ticket, (uint32_t) nparts, bias_corr);
         else
             adaround_bwd_adam_kernel<false><<<(unsigned) blocks, kBlock, 0, st>>>(
                 w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss, wq_next, lf.part, lf.ticket, (uint32_t) nparts);
+                it_cur, a, round_loss, wq_next, lf.part, lf.ticket, (uint32_t) nparts, bias_corr);
         AIMET_LAUNCH_CHECK();
     });
 }
@@ -1312,7 +1372,18 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
 {
     return aimet_adaround_backward_adam_parts(w, alpha, grad_wq, 1, exp_avg, exp_avg_sq, outer, C, K, delta, offset, bw,
                                               reg_beta_all, it_next, it_cur, lr, beta1, beta2, eps, round_loss, wq_next,
-                                              stream);
+                                              nullptr, stream);
+}
+
+int aimet_adaround_adam_bias_corrections(double beta1, double beta2, int64_t steps, float* bias_corr, void* stream)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(steps > 0 && steps < (int64_t(1) << 31), "steps out of range");
+        require_device_ptr(bias_corr, "bias_corr");
+        adam_bias_corr_kernel<<<(unsigned) ceil_div(steps, (int64_t) kBlock), kBlock, 0, as_stream(stream)>>>(
+            beta1, beta2, steps, bias_corr);
+        AIMET_LAUNCH_CHECK();
+    });
 }
 
 }   // extern "C"

@@ -471,13 +471,21 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
 
 /* aimet_adaround_backward_adam with the weight gradient given as `nparts` slices grad_parts[s][n]
  * (n = outer * C * K) that are added in slice order (s = 0, 1, ...) element by element: the sliced
- * weight gradient of aimet_adaround_pw_cm_wgrad. nparts == 1 is aimet_adaround_backward_adam. */
+ * weight gradient of aimet_adaround_pw_cm_wgrad. bias_corr_dev (nullable): the table of
+ * aimet_adaround_adam_bias_corrections for beta1 / beta2, read at step instead of computing the
+ * bias corrections in the kernel (same bits). nparts == 1 and bias_corr_dev == NULL is
+ * aimet_adaround_backward_adam. */
 int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float* grad_parts, int64_t nparts,
                                        float* exp_avg_dev, float* exp_avg_sq_dev, int64_t outer, int64_t C, int64_t K,
                                        const float* delta_dev, const float* offset_dev, int32_t bw,
                                        const float* reg_beta_all_dev, const int64_t* it_next_dev, int64_t* it_cur_dev,
                                        double lr, double beta1, double beta2, double eps, float* round_loss_dev,
-                                       float* wq_next_dev, void* stream);
+                                       float* wq_next_dev, const float* bias_corr_dev, void* stream);
+/* Adam's bias corrections for step = 1 .. steps, as ATen's fused Adam computes them (1 - beta^step
+ * in double, rounded to float; the second as its square root): bias_corr_dev[2 (step - 1)] =
+ * bc1, [2 (step - 1) + 1] = sqrt(bc2) (float32, 2 * steps entries). */
+int aimet_adaround_adam_bias_corrections(double beta1, double beta2, int64_t steps, float* bias_corr_dev,
+                                         void* stream);
 
 /* The channel-major GEMM form of a 1x1 layer's AdaRound iteration (adaround_optimizer.py:181-218)
  * in two kernels on the f32 matrix cores, for many channels at small spatial sizes. Batch position

@@ -1483,7 +1483,12 @@ def test_adaround_pw_cm_mfma_vs_torch(N, Cin, Cout, HW, act, with_bias):
     for k in range(1, S):
         gsum += parts[k]
     res = []
-    for fn, grad, extra in (("aimet_adaround_backward_adam_parts", parts, (S,)), ("aimet_adaround_backward_adam", gsum, ())):
+    bc = torch.empty(2, device=DEV)
+    _native.call("aimet_adaround_adam_bias_corrections", ctypes.c_double(0.9), ctypes.c_double(0.999), 1,
+                 bc.data_ptr(), s)
+    for fn, grad, extra, tab in (("aimet_adaround_backward_adam_parts", parts, (S,), (None,)),
+                                 ("aimet_adaround_backward_adam_parts", parts, (S,), (bc.data_ptr(),)),
+                                 ("aimet_adaround_backward_adam", gsum, (), ())):
         alpha = torch.randn(C, K, device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
         m, v = torch.zeros_like(alpha), torch.zeros_like(alpha)
         rb = torch.tensor([[0.01, 10.0, 9.0]], device=DEV)
@@ -1492,11 +1497,53 @@ def test_adaround_pw_cm_mfma_vs_torch(N, Cin, Cout, HW, act, with_bias):
         args = [w_ada.data_ptr(), alpha.data_ptr(), grad.data_ptr(), *extra, m.data_ptr(), v.data_ptr(), 1, C, K,
                 d.data_ptr(), o.data_ptr(), 4, rb.data_ptr(), ctr.data_ptr() + 8, ctr.data_ptr(),
                 ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999), ctypes.c_double(1e-8), None,
-                wq.data_ptr(), s]
+                wq.data_ptr(), *tab, s]
         _native.call(fn, *args)
         res.append((alpha, m, v, wq))
-    for a_, b_ in zip(res[0], res[1]):
-        assert torch.equal(a_, b_)
+    for r in res[1:]:
+        for a_, b_ in zip(res[0], r):
+            assert torch.equal(a_, b_)
+
+
+def test_adam_bias_correction_table_equals_in_kernel():
+    """aimet_adaround_adam_bias_corrections' per-step table read by the Adam step gives the same
+    alpha / moments / soft weight bit for bit as the bias corrections computed in the kernel, at
+    steps across a 10k-iteration loop; the table equals ATen's 1 - beta^step (double, rounded to
+    float; the second as its square root) to one float ulp."""
+    import ctypes
+    from aimet_amd import _native
+    s = torch.cuda.current_stream().cuda_stream
+    steps = 10000
+    b1, b2 = 0.9, 0.999
+    bc = torch.empty(steps, 2, device=DEV)
+    _native.call("aimet_adaround_adam_bias_corrections", ctypes.c_double(b1), ctypes.c_double(b2), steps,
+                 bc.data_ptr(), s)
+    st = torch.arange(1, steps + 1, dtype=torch.float64)
+    ref = torch.stack([(1 - b1 ** st).float(), (1 - b2 ** st).sqrt().float()], 1)
+    ulp = torch.finfo(torch.float32).eps * ref.abs()
+    assert bool(((bc.cpu() - ref).abs() <= ulp).all())
+    g = torch.Generator(device=DEV).manual_seed(11)
+    C, K = 24, 40
+    w = torch.randn(C, K, device=DEV, generator=g) * 0.05
+    d = (w.abs().amax(1) / 7).contiguous()
+    o = torch.full((C,), -8.0, device=DEV)
+    grad = torch.randn(C, K, device=DEV, generator=g) * 1e-3
+    rb = torch.tensor([[0.01, 10.0, 9.0]] * steps, device=DEV)
+    for step in (1, 2, 7, 100, 999, 5000, 10000):
+        res = []
+        for tab in (None, bc.data_ptr()):
+            alpha = torch.randn(C, K, device=DEV, generator=torch.Generator(device=DEV).manual_seed(step))
+            m = torch.full_like(alpha, 1e-4)
+            v = torch.full_like(alpha, 1e-7)
+            wq = torch.empty_like(alpha)
+            ctr = torch.tensor([step - 1, step], dtype=torch.long, device=DEV)
+            _native.call("aimet_adaround_backward_adam_parts", w.data_ptr(), alpha.data_ptr(), grad.data_ptr(), 1,
+                         m.data_ptr(), v.data_ptr(), 1, C, K, d.data_ptr(), o.data_ptr(), 4, rb.data_ptr(),
+                         ctr.data_ptr() + 8, ctr.data_ptr(), ctypes.c_double(1e-3), ctypes.c_double(b1),
+                         ctypes.c_double(b2), ctypes.c_double(1e-8), None, wq.data_ptr(), tab, s)
+            res.append((alpha, m, v, wq))
+        for a_, b_ in zip(*res):
+            assert torch.equal(a_, b_), step
 
 
 @pytest.mark.parametrize("layer", ["conv", "depthwise", "pointwise", "linear", "linear_noact", "conv_gelu"])

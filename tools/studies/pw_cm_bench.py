@@ -24,24 +24,31 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=200)
     ap.add_argument("--nb", type=int, default=32)
+    ap.add_argument("--forms", default="mfma,library")
+    ap.add_argument("--shapes", default="", help="indices into SHAPES, comma-separated (default: all)")
+    ap.add_argument("--seq", action="store_true", help="batch rows 0 .. nb-1 every iteration (no random gather)")
     args = ap.parse_args()
+    shapes = [SHAPES[int(i)] for i in args.shapes.split(",")] if args.shapes else SHAPES
     lib = _native.load()
     dev = torch.device("cuda", 0)
     P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
     nb, rows, iters = args.nb, 256, args.reps + 8
-    for cin, cout, hw in SHAPES:
+    for cin, cout, hw in shapes:
         g = torch.Generator(device=dev).manual_seed(cin + cout)
         x = torch.rand(rows, cin, hw, device=dev, generator=g)
         t = torch.randn(rows, cout, hw, device=dev, generator=g)
         w = torch.randn(cout, cin, device=dev, generator=g) * 0.05
         bias = torch.randn(cout, device=dev, generator=g) * 0.1
-        idx = torch.stack([torch.randperm(rows, device=dev, generator=g)[:nb] for _ in range(iters)]).contiguous()
+        if args.seq:
+            idx = torch.arange(nb, device=dev).repeat(iters, 1).contiguous()
+        else:
+            idx = torch.stack([torch.randperm(rows, device=dev, generator=g)[:nb] for _ in range(iters)]).contiguous()
         d = (w.abs().amax(1) / 127).contiguous()
         o = torch.full((cout,), -128.0, device=dev)
         rb = torch.tensor([[0.01, 10.0, 9.0]] * iters, device=dev)
         adam = (ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999), ctypes.c_double(1e-8))
-        res = {"cin": cin, "cout": cout, "hw": hw, "nb": nb}
-        for form in ("mfma", "library"):
+        res = {"cin": cin, "cout": cout, "hw": hw, "nb": nb, "seq": args.seq}
+        for form in args.forms.split(","):
             alpha = torch.randn(cout, cin, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
             m, v = torch.zeros_like(alpha), torch.zeros_like(alpha)
             wq = w.clone()
@@ -61,7 +68,7 @@ def main():
                                                                  cin, cout, hw, s))
                     _native.check(lib.aimet_adaround_backward_adam_parts(P(w), P(alpha), P(parts), sl.value, P(m), P(v),
                                                                          1, cout, cin, P(d), P(o), 8, P(rb), it_next,
-                                                                         it_cur, *adam, None, P(wq), s))
+                                                                         it_cur, *adam, None, P(wq), None, s))
             else:
                 x_cm = torch.empty(cin, nb * hw, device=dev)
                 q_cm = torch.empty(cout, nb * hw, device=dev)
