@@ -147,6 +147,10 @@ _PW_CM_FUSED = os.environ.get("AIMET_ADA_PW_CM_FUSED", "0") == "1"
 # the batch table live on the device, so k consecutive iterations are one graph. Results are those
 # of one iteration per graph, bit for bit.
 _GRAPH_ITERS = max(1, int(os.environ.get("AIMET_ADA_GRAPH_ITERS", "10")))
+# the channel-major weight gradient as S GEMMs over consecutive position slices (one batched GEMM;
+# the Adam step adds the S slices in order): the single [C_out, nb hw] x [nb hw, C_in] GEMM has a
+# small output and a long sum, which the library tiles onto few workgroups
+_CM_SPLITK = max(1, int(os.environ.get("AIMET_ADA_CM_SPLITK", "1")))
 
 
 def _is_pointwise(module: torch.nn.Module) -> bool:
@@ -613,7 +617,7 @@ class AdaroundOptimizer:
             ws = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
             dims = (Nb, C, H, W, out_shape[1], out_shape[2], K, stride, pad, dil)
         pbias = P(bias) if bias is not None else None
-        pw_dims, cm = None, None
+        pw_dims, cm, gw_parts = None, None, None
         if mode in ("pointwise", "im2col") and _PW_FUSED != "0" and _LOOP_FORM != "autograd":
             cin, cout, hw_in = inp_data.shape[1], C_out, inp_data[0, 0].numel()
             wanted = _PW_FUSED == "all" or (hw >= 28 * 28 and not (cin > cout and hw < 56 * 56))
@@ -637,6 +641,9 @@ class AdaroundOptimizer:
                 x_cm = torch.empty((cin_cm, nb * hw), dtype=torch.float32, device=dev)
                 q_cm = torch.empty((C_out, nb * hw), dtype=torch.float32, device=dev)
                 cm = (cin_cm, x_cm, q_cm, torch.empty_like(q_cm))
+                splitk = _CM_SPLITK if (nb * hw) % _CM_SPLITK == 0 else 1
+                gw_parts = torch.empty((splitk,) + tuple(wq.shape), dtype=torch.float32, device=dev) if splitk > 1 \
+                    else None
 
         def recon(q, with_bias, s):
             _native.check(lib.aimet_adaround_recon_grad_indexed(P(q), P(out_data), P(idx_all), it_cur, P(g_buf), nb,
@@ -693,7 +700,15 @@ class AdaroundOptimizer:
                 torch.mm(w2, x_cm, out=q_cm)
                 _native.check(lib.aimet_adaround_recon_grad_indexed_cm(P(q_cm), P(out_data), P(idx_all), it_cur,
                                                                        P(g_cm), nb, C_out, hw, pbias, code, s))
-                adam_step(torch.mm(g_cm, x_cm.t()).view_as(wq), s)
+                if gw_parts is None:
+                    adam_step(torch.mm(g_cm, x_cm.t()).view_as(wq), s)
+                    return
+                S, L = gw_parts.shape[0], (nb * hw) // gw_parts.shape[0]
+                torch.bmm(g_cm.view(C_out, S, L).transpose(0, 1), x_cm.view(cin_cm, S, L).permute(1, 2, 0),
+                          out=gw_parts.view(S, C_out, cin_cm))
+                _native.check(lib.aimet_adaround_backward_adam_parts(
+                    sq.pw, sq.pa, P(gw_parts), S, P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po, sq.bw,
+                    P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, P(bias_corr), s))
                 return
             _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp),
                                                     None if indexed else P(target), P(idx_all), it_cur, it_next, nb,

@@ -796,8 +796,19 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             const float d = delta[c], o = offset[c], rcp = __builtin_amdgcn_rcpf(d);
             f4 wv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(w) + ic);
             f4 gv       = __builtin_nontemporal_load(reinterpret_cast<const f4*>(g) + ic);
-            for (uint32_t s = 1; s < nparts; ++s)   // the gradient's slices, added in slice order
-                gv += __builtin_nontemporal_load(reinterpret_cast<const f4*>(g + (size_t) s * n) + ic);
+            // the gradient's slices, added in slice order; up to 8 loads in flight at a time
+            for (uint32_t s = 1; s < nparts; s += 8)
+            {
+                f4 t[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    t[u] = __builtin_nontemporal_load(
+                        reinterpret_cast<const f4*>(g + (size_t) (s + u < nparts ? s + u : s) * n) + ic);
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (s + u < nparts)
+                        gv += t[u];
+            }
             f4 av       = reinterpret_cast<const f4*>(alpha)[ic];
             float a[4] = {av.x, av.y, av.z, av.w}, ww[4] = {wv.x, wv.y, wv.z, wv.w}, gg[4] = {gv.x, gv.y, gv.z, gv.w};
             float r[4], sg[4], x[4], ax[4];
@@ -848,8 +859,17 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             const float d = delta[c], o = offset[c];
             const float rcp = __builtin_amdgcn_rcpf(d);
             float gi        = g[i];
-            for (uint32_t s = 1; s < nparts; ++s)
-                gi += g[(size_t) s * n + i];
+            for (uint32_t s = 1; s < nparts; s += 16)   // slice order; up to 16 loads in flight
+            {
+                float t[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    t[u] = g[(size_t) (s + u < nparts ? s + u : s) * n + i];
+#pragma unroll
+                for (int u = 0; u < 16; ++u)
+                    if (s + u < nparts)
+                        gi += t[u];
+            }
             const float ga  = ada_bwd(w[i], alpha[i], gi, d, o, p, rcp, loss, i);
             const float an  = adam_elem(alpha[i], ga, exp_avg[i], exp_avg_sq[i], adam, bc1, bc2s);
             alpha[i]        = an;

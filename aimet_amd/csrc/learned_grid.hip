@@ -639,6 +639,17 @@ struct LgBwdLaunch
 };
 constexpr int64_t kLgBwd16Grid = 2048;
 
+// the per-tensor backward's fold in the kernel's last workgroup (default) or as its own launch
+// (AIMET_LG_FOLD_LAUNCH=1, for A/B measurements; the same arithmetic, the same bits)
+bool lg_fold_in_kernel()
+{
+    static const bool v = [] {
+        const char* e = getenv("AIMET_LG_FOLD_LAUNCH");
+        return !(e && e[0] == '1');
+    }();
+    return v;
+}
+
 LgBwdLaunch lg_bwd_launch(int64_t n)
 {
     static const std::pair<int, int64_t> shape = [] {
@@ -943,12 +954,7 @@ __global__ __launch_bounds__(BLOCK) void lg_fwd16_kernel(const unsigned short* _
     const int64_t nfull = fast ? nvec : 0;
     if (tile < nfull)
     {
-        for (; tile < nfull; tile += gridDim.x)
-        {
-            u16x8 nxt[V];
-            const int64_t tn = tile + gridDim.x;
-            if (tn < nfull)
-                lg_fwd16_load<IO, V, BLOCK, NT>(x, tn, nxt);
+        auto compute = [&](const u16x8 (&v)[V], int64_t t) {
 #pragma unroll
             for (int u = 0; u < V; ++u)
             {
@@ -958,15 +964,32 @@ __global__ __launch_bounds__(BLOCK) void lg_fwd16_kernel(const unsigned short* _
                 {
                     // never NaN for a fast encoding; a NaN input -> the 16-bit NaN torch's cast
                     // of the passed-through NaN gives (one select, no NaN test of the result)
-                    const float xf = to_f32<IO>(cur[u][k]);
+                    const float xf = to_f32<IO>(v[u][k]);
                     const float yq = lg_qdq_fast(xf, d, o, steps, rd, xmax);
                     r[k] = xf != xf ? from_f32<IO>(quiet_nan(xf)) : from_f32<IO, false>(yq);
                 }
-                st16<NT>(r, reinterpret_cast<u16x8*>(y) + tile * kTile / 8 + u * BLOCK + threadIdx.x);
+                st16<NT>(r, reinterpret_cast<u16x8*>(y) + t * kTile / 8 + u * BLOCK + threadIdx.x);
             }
-#pragma unroll
-            for (int u = 0; u < V; ++u)
-                cur[u] = nxt[u];
+        };
+        // two register buffers in turn (no copy of the next tile's registers, which made the
+        // compiler wait for its loads at the end of every tile); the next tile's loads are
+        // unconditional -- the last tile reloads itself, unused -- so the same number of loads is
+        // outstanding on every path and the wait at each tile's first use leaves them in flight
+        u16x8 nxt[V];
+        for (;;)
+        {
+            int64_t tn = tile + gridDim.x < nfull ? tile + gridDim.x : tile;
+            lg_fwd16_load<IO, V, BLOCK, NT>(x, tn, nxt);
+            compute(cur, tile);
+            tile += gridDim.x;
+            if (tile >= nfull)
+                break;
+            tn = tile + gridDim.x < nfull ? tile + gridDim.x : tile;
+            lg_fwd16_load<IO, V, BLOCK, NT>(x, tn, cur);
+            compute(nxt, tile);
+            tile += gridDim.x;
+            if (tile >= nfull)
+                break;
         }
     }
     // the rest element by element: tiles from nfull on (all of them when not vec / not fast)
@@ -1015,60 +1038,74 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
     // full tiles of an encoding lg_fast_enc accepts take the vector path; the rest (the partial
     // last tile, unaligned pointers, an encoding for the division) the element path
     const int64_t nfull = lg_fast_enc(o, rcp) ? nvec : 0;
+    // full tiles: two register buffers in turn, the next tile's loads unconditional (see
+    // lg_fwd16_kernel), each tile's partial triple published as before
+    auto full_tile = [&](const u16x8 (&a_)[STEPS], const u16x8 (&b_)[STEPS], int64_t t) {
+        const int64_t base = t * kTile;
+        Sums s {0, 0, 0};
+#pragma unroll
+        for (int u = 0; u < STEPS; ++u)
+        {
+            float r[8], xv[8], gv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+            {
+                xv[k] = to_f32<IO>(a_[u][k]);
+                gv[k] = to_f32<IO>(b_[u][k]);
+            }
+            lg_bwd_elems_fast<8, MODE>(xv, gv, dl, o, steps, rcp, r, s);
+            if (gx)
+            {
+                u16x8 h;
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    h[k] = from_f32<IO>(r[k]);
+                st16<NT>(h, reinterpret_cast<u16x8*>(gx) + lg_tile_elem(base, u, 0) / 8);
+            }
+        }
+        Sums t3 = block_reduce(s);
+        if (threadIdx.x == 0)
+            publish_sums(partial + 3 * t, t3);
+    };
+    if (tile < nfull)
+    {
+        u16x8 an[STEPS], bn[STEPS];
+        for (;;)
+        {
+            int64_t tn = tile + gridDim.x < nfull ? tile + gridDim.x : tile;
+            lg_bwd16_load<STEPS, NT>(x, g, tn * kTile, an, bn);
+            full_tile(a, b, tile);
+            tile += gridDim.x;
+            if (tile >= nfull)
+                break;
+            tn = tile + gridDim.x < nfull ? tile + gridDim.x : tile;
+            lg_bwd16_load<STEPS, NT>(x, g, tn * kTile, a, b);
+            full_tile(an, bn, tile);
+            tile += gridDim.x;
+            if (tile >= nfull)
+                break;
+        }
+    }
+    // the rest element by element (the partial last tile, unaligned pointers, an encoding for the
+    // division), the same order
     for (; tile < ntiles; tile += gridDim.x)
     {
         const int64_t base = tile * kTile;
         Sums s {0, 0, 0};
-        if (tile < nfull)
-        {
-            u16x8 an[STEPS], bn[STEPS];
-            const int64_t tn = tile + gridDim.x;
-            if (tn < nfull)
-                lg_bwd16_load<STEPS, NT>(x, g, tn * kTile, an, bn);
-#pragma unroll
-            for (int u = 0; u < STEPS; ++u)
+        for (int u = 0; u < STEPS; ++u)
+            for (int k = 0; k < 8; ++k)
             {
-                float r[8], xv[8], gv[8];
-#pragma unroll
-                for (int k = 0; k < 8; ++k)
-                {
-                    xv[k] = to_f32<IO>(a[u][k]);
-                    gv[k] = to_f32<IO>(b[u][k]);
-                }
-                lg_bwd_elems_fast<8, MODE>(xv, gv, dl, o, steps, rcp, r, s);
+                const int64_t e = lg_tile_elem(base, u, k);
+                if (e >= n)
+                    break;
+                float r;
+                lg_bwd_elem(to_f32<IO>(x[e]), to_f32<IO>(g[e]), dl, o, steps, rcp, r, s, MODE);
                 if (gx)
-                {
-                    u16x8 h;
-#pragma unroll
-                    for (int k = 0; k < 8; ++k)
-                        h[k] = from_f32<IO>(r[k]);
-                    st16<NT>(h, reinterpret_cast<u16x8*>(gx) + lg_tile_elem(base, u, 0) / 8);
-                }
+                    gx[e] = from_f32<IO>(r);
             }
-#pragma unroll
-            for (int u = 0; u < STEPS; ++u)
-            {
-                a[u] = an[u];
-                b[u] = bn[u];
-            }
-        }
-        else
-        {
-            for (int u = 0; u < STEPS; ++u)
-                for (int k = 0; k < 8; ++k)
-                {
-                    const int64_t e = lg_tile_elem(base, u, k);
-                    if (e >= n)
-                        break;
-                    float r;
-                    lg_bwd_elem(to_f32<IO>(x[e]), to_f32<IO>(g[e]), dl, o, steps, rcp, r, s, MODE);
-                    if (gx)
-                        gx[e] = from_f32<IO>(r);
-                }
-        }
-        Sums t = block_reduce(s);
+        Sums t3 = block_reduce(s);
         if (threadIdx.x == 0)
-            publish_sums(partial + 3 * tile, t);
+            publish_sums(partial + 3 * tile, t3);
     }
     if (ticket)   // uniform: the fold in the last workgroup (else lg_bwd_fold_one follows)
         fold_in_last_workgroup(partial, ntiles, folded, range, ticket);
@@ -1407,7 +1444,7 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             float* partial      = fb.part ? fb.part : static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
             const int v         = vec ? 1 : 0;
 
-            unsigned* ticket = fb.ticket;
+            unsigned* ticket = lg_fold_in_kernel() ? fb.ticket : nullptr;
             lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
                 lg_bwd_tensor_kernel<decltype(st)::value, decltype(md)::value><<<L.grid, kBlock, 0, s>>>(
                     x, grad, grad_x, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
@@ -1754,7 +1791,7 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         auto os = static_cast<unsigned short*>(grad_x);
         const int v = vec ? 1 : 0;
 
-        unsigned* ticket = fb.ticket;
+        unsigned* ticket = lg_fold_in_kernel() ? fb.ticket : nullptr;
         lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
             constexpr int ST = decltype(st)::value, MD = decltype(md)::value;
             if (io_dtype == IO_F16 && lg16_nt())

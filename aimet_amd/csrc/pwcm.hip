@@ -31,11 +31,9 @@ namespace
 {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int kKc  = 16;          // K chunk per wave step
-constexpr int kLdA = kKc + 1;     // [32][17]: the lanes reading one k column hit distinct banks
-constexpr int kLdB = 64 + 4;      // [16][68]
-constexpr int kStage = 32 * kLdA + kKc * kLdB;   // one wave's staging floats
+constexpr int kKc = 32;   // K per chunk: 16 steps of the 32 x 32 x 2 f32 MFMA
 
 struct CmBatch
 {
@@ -46,219 +44,258 @@ struct CmBatch
     FastDiv div_hw;
 };
 
-// the LDS writes of this wave visible to its own lanes (wave-local staging, in-order LDS)
-__device__ __forceinline__ void wave_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
+// The operands go from memory straight into the MFMA's register layout (no LDS staging): lane
+// (i, h) = (lane & 31, lane >> 5) supplies A[i][k] and B[k][i] of step st at
+// k = kk(st, h), so every lane loads only its own values. Both operands use the same k map, so
+// each step still adds the products of one k pair; the order over a chunk is fixed
+// (deterministic).
+//   forward (K = input channels):  kk = 4 (st / 2) + 2 h + st % 2 -- W[co][k0 + kk] as float2 pairs
+//   wgrad   (K = positions):       kk = 8 (st / 4) + 4 h + st % 4 -- 4 consecutive positions per load
 
-// acc0 / acc1 += A[32 x kKc] . B[kKc x 64] (columns 0-31 / 32-63): kKc / 2 steps of the 32 x 32 x 2
-// f32 MFMA, the two accumulators' chains interleaved
-__device__ __forceinline__ void mfma_chunk(const float* As, const float* Bs, f32x16& acc0, f32x16& acc1)
+// forward + reconstruction gradient. One 32 x 64 sub-tile (32 output channels x 64 positions) per
+// workgroup of SK waves; wave `part` takes the K chunks part, part + SK, ... with the next chunk's
+// loads in flight while its MFMAs run; the waves' accumulators are added in part order through
+// LDS (deterministic). EVEN: Cin % 32 == 0 (no ragged chunk: W read as float2 pairs, no zeroing).
+// Wave 0 issues the 32 target values of its outputs before the sums, so the epilogue waits for
+// nothing.
+template <int SK, bool EVEN>
+__global__ __launch_bounds__(64 * SK) void pw_cm_forward_kernel(CmBatch B, const float* __restrict__ target,
+                                                                const float* __restrict__ w,
+                                                                const float* __restrict__ bias, float* __restrict__ g,
+                                                                int64_t* __restrict__ it_next, float scale, int act)
 {
-    const int lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
-#pragma unroll
-    for (int st = 0; st < kKc / 2; ++st)
-    {
-        const float a = As[i * kLdA + 2 * st + h];
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[(2 * st + h) * kLdB + i], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bs[(2 * st + h) * kLdB + 32 + i], acc1, 0, 0, 0);
-    }
-}
-
-// SK > 1 waves computed the same 32 x 64 sub-tile over interleaved K chunks: wave `part` 0 adds the
-// others' accumulators in part order (deterministic). Every thread of the workgroup calls it.
-template <int SK>
-__device__ __forceinline__ void reduce_parts(f32x16& acc0, f32x16& acc1, float* red)
-{
-    if constexpr (SK > 1)
-    {
-        const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, part = wave % SK;
-        if (part != 0)
-        {
-#pragma unroll
-            for (int r = 0; r < 16; ++r)
-            {
-                red[(wave * 32 + r) * 64 + lane]      = acc0[r];
-                red[(wave * 32 + 16 + r) * 64 + lane] = acc1[r];
-            }
-        }
-        __syncthreads();
-        if (part == 0)
-            for (int q = 1; q < SK; ++q)
-#pragma unroll
-                for (int r = 0; r < 16; ++r)
-                {
-                    acc0[r] += red[((wave + q) * 32 + r) * 64 + lane];
-                    acc1[r] += red[((wave + q) * 32 + 16 + r) * 64 + lane];
-                }
-    }
-}
-
-// forward + reconstruction gradient. A workgroup's 4 waves cover 4 / SK sub-tiles of 32 output
-// channels x 64 positions (blockIdx.y: channel block, blockIdx.x: 64 positions); the SK waves of a
-// sub-tile take the Cin chunks part, part + SK, ... (each with the next chunk's loads in flight
-// while its MFMAs run), and their accumulators are added in part order.
-template <int SK>
-__global__ __launch_bounds__(256) void pw_cm_forward_kernel(CmBatch B, const float* __restrict__ target,
-                                                            const float* __restrict__ w, const float* __restrict__ bias,
-                                                            float* __restrict__ g, int64_t* __restrict__ it_next,
-                                                            float scale, int act)
-{
-    constexpr int SUB = 4 / SK;
-    __shared__ float stage[4][kStage];
-    __shared__ float red[SK > 1 ? 4 * 32 * 64 : 1];
+    __shared__ float red[SK > 1 ? (SK - 1) * 32 * 64 : 1];
     const int64_t it = B.it_cur[0];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         it_next[0] = it + 1;
     const int64_t* rows = B.idx_all + it * B.nb;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, part = wave % SK;
-    const uint32_t co0 = blockIdx.y * (32 * SUB) + (wave / SK) * 32, p0 = blockIdx.x * 64;
-    // B loads: lane = position p0 + lane, k = 0 .. kKc - 1 (consecutive positions across lanes)
-    const uint32_t pl = p0 + lane;
-    const bool pv     = pl < B.P;
-    size_t xbase      = 0;
-    if (pv)
-    {
-        const uint32_t b = B.div_hw.div(pl);
-        xbase            = (size_t) rows[b] * B.Cin * B.hw + (pl - b * B.hw);
-    }
-    // A loads: k = lane & 15, rows (lane >> 4) + 4 j
-    const int ak = lane & 15, ar = lane >> 4;
-    float* As = stage[wave];
-    float* Bs = As + 32 * kLdA;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    const uint32_t co0 = blockIdx.y * 32, p0 = blockIdx.x * 64;
+    // this lane's two B columns (positions p0 + i, p0 + 32 + i, clamped into the batch: a column past
+    // P is computed from real data and never stored)
+    const uint32_t pa = min(p0 + i, B.P - 1), pb = min(p0 + 32 + i, B.P - 1);
+    const uint32_t ba = B.div_hw.div(pa), bb = B.div_hw.div(pb);
+    const size_t ra = (size_t) rows[ba], rb = (size_t) rows[bb];
+    const float* xa = B.x + ra * B.Cin * B.hw + (pa - ba * B.hw);
+    const float* xb = B.x + rb * B.Cin * B.hw + (pb - bb * B.hw);
+    const float* wr = w + (size_t) min(co0 + i, B.Cout - 1) * B.Cin;
     const uint32_t nch = (B.Cin + kKc - 1) / kKc;
-    float ra[8], rb[kKc];
-    auto load = [&](uint32_t c) {
+    float a0[16], x0[16], y0[16], a1[16], x1[16], y1[16];
+    auto load = [&](uint32_t c, float (&a)[16], float (&xv)[16], float (&yv)[16]) {
         const uint32_t k0 = c * kKc;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int s2 = 0; s2 < 8; ++s2)
         {
-            const uint32_t co = co0 + ar + 4 * j, ci = k0 + ak;
-            ra[j] = (co < B.Cout && ci < B.Cin) ? w[(size_t) co * B.Cin + ci] : 0.0f;
-        }
+            const uint32_t k = k0 + 4 * s2 + 2 * h;   // steps 2 s2 (k) and 2 s2 + 1 (k + 1)
+            if constexpr (EVEN)
+            {
+                const float2 v = *reinterpret_cast<const float2*>(wr + k);
+                a[2 * s2]      = v.x;
+                a[2 * s2 + 1]  = v.y;
 #pragma unroll
-        for (int k = 0; k < kKc; ++k)
-            rb[k] = (pv && k0 + k < B.Cin) ? B.x[xbase + (size_t) (k0 + k) * B.hw] : 0.0f;
+                for (int e = 0; e < 2; ++e)
+                {
+                    xv[2 * s2 + e] = xa[(size_t) (k + e) * B.hw];
+                    yv[2 * s2 + e] = xb[(size_t) (k + e) * B.hw];
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < 2; ++e)
+                {
+                    const uint32_t ke = k + e, kc = min(ke, B.Cin - 1);
+                    const bool in     = ke < B.Cin;
+                    const float av = wr[kc], xv_ = xa[(size_t) kc * B.hw], yv_ = xb[(size_t) kc * B.hw];
+                    a[2 * s2 + e]  = in ? av : 0.0f;
+                    xv[2 * s2 + e] = in ? xv_ : 0.0f;
+                    yv[2 * s2 + e] = in ? yv_ : 0.0f;
+                }
+            }
+        }
     };
     f32x16 acc0 = {}, acc1 = {};
-    uint32_t c = part;
+    auto mfma = [&](const float (&a)[16], const float (&xv)[16], const float (&yv)[16]) {
+#pragma unroll
+        for (int st = 0; st < 16; ++st)
+        {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], xv[st], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], yv[st], acc1, 0, 0, 0);
+        }
+    };
+    uint32_t c = wave;
     if (c < nch)
-        load(c);
-    for (; c < nch; c += SK)
+        load(c, a0, x0, y0);
+    // the targets of wave 0's outputs: C/D map of the 32 x 32 f32 MFMA, element r of lane (i, h) is
+    // row (r & 3) + 8 (r >> 2) + 4 h, column i
+    float t0[16], t1[16];
+    if (wave == 0)
     {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            As[(ar + 4 * j) * kLdA + ak] = ra[j];
-#pragma unroll
-        for (int k = 0; k < kKc; ++k)
-            Bs[k * kLdB + lane] = rb[k];
-        wave_sync();
-        if (c + SK < nch)
-            load(c + SK);
-        mfma_chunk(As, Bs, acc0, acc1);
-        wave_sync();
-    }
-    reduce_parts<SK>(acc0, acc1, red);
-    if (part != 0)
-        return;
-    // C/D map of the 32 x 32 f32 MFMA: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-    {
-        const uint32_t p = p0 + 32 * h + (lane & 31);
-        if (p >= B.P)
-            continue;
-        const uint32_t b = B.div_hw.div(p), t = p - b * B.hw;
-        const float* trow = target + (size_t) rows[b] * B.Cout * B.hw + t;
+        const float* ta = target + ra * B.Cout * B.hw + (pa - ba * B.hw);
+        const float* tb = target + rb * B.Cout * B.hw + (pb - bb * B.hw);
 #pragma unroll
         for (int r = 0; r < 16; ++r)
         {
-            const uint32_t co = co0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            const float q     = h ? acc1[r] : acc0[r];
-            if (co < B.Cout)
-                g[(size_t) co * B.P + p] = recon_g(q + (bias ? bias[co] : 0.0f), trow[(size_t) co * B.hw], scale, act);
+            const uint32_t co = min(co0 + (r & 3) + 8 * (r >> 2) + 4 * h, B.Cout - 1);
+            t0[r]             = ta[(size_t) co * B.hw];
+            t1[r]             = tb[(size_t) co * B.hw];
         }
+    }
+    for (; c < nch; c += 2 * SK)
+    {
+        if (c + SK < nch)
+            load(c + SK, a1, x1, y1);
+        mfma(a0, x0, y0);
+        if (c + SK >= nch)
+            break;
+        if (c + 2 * SK < nch)
+            load(c + 2 * SK, a0, x0, y0);
+        mfma(a1, x1, y1);
+    }
+    if constexpr (SK > 1)
+    {
+        if (wave != 0)
+        {
+            float* rd = red + (wave - 1) * 32 * 64;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+            {
+                rd[r * 64 + lane]        = acc0[r];
+                rd[(16 + r) * 64 + lane] = acc1[r];
+            }
+        }
+        __syncthreads();
+        if (wave != 0)
+            return;
+        for (int q = 0; q < SK - 1; ++q)
+        {
+            const float* rd = red + q * 32 * 64;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+            {
+                acc0[r] += rd[r * 64 + lane];
+                acc1[r] += rd[(16 + r) * 64 + lane];
+            }
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+    {
+        const uint32_t co = co0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co >= B.Cout)
+            continue;
+        const float bs = bias ? bias[co] : 0.0f;
+        if (p0 + i < B.P)
+            g[(size_t) co * B.P + p0 + i] = recon_g(acc0[r] + bs, t0[r], scale, act);
+        if (p0 + 32 + i < B.P)
+            g[(size_t) co * B.P + p0 + 32 + i] = recon_g(acc1[r] + bs, t1[r], scale, act);
     }
 }
 
-// weight-gradient slice s (blockIdx.z): sub-tile 32 output channels (blockIdx.y) x 64 input channels
-// (blockIdx.x); the 4 waves take the slice's 16-position chunks part, part + 4, ... and are added in
-// part order
-__global__ __launch_bounds__(256) void pw_cm_wgrad_kernel(CmBatch B, const float* __restrict__ g,
-                                                          float* __restrict__ part_out, uint32_t per_slice)
+constexpr int kMaxRowsLds = 256;   // the batch's row table in LDS (wgrad) up to this nb
+
+// weight-gradient slice s (blockIdx.z): one wave per 32 output channels (blockIdx.y) x 64 input
+// channels (blockIdx.x) over positions [s per_slice, (s + 1) per_slice), 32-position chunks with
+// the next chunk's loads in flight. V4: hw % 4 == 0 (4 consecutive positions are one sample's, so
+// x comes as float4; per_slice and the chunks are multiples of 8, so the groups stay aligned).
+template <bool V4>
+__global__ __launch_bounds__(64) void pw_cm_wgrad_kernel(CmBatch B, const float* __restrict__ g,
+                                                         float* __restrict__ part_out, uint32_t per_slice)
 {
-    constexpr int SK = 4;
-    __shared__ float stage[4][kStage];
-    __shared__ float red[4 * 32 * 64];
+    __shared__ int64_t srows[kMaxRowsLds];
     const int64_t it    = B.it_cur[0];
     const int64_t* rows = B.idx_all + it * B.nb;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, part = wave;
+    const bool lds_rows = B.nb <= kMaxRowsLds;
+    if (lds_rows)
+        for (uint32_t b = threadIdx.x; b < B.nb; b += 64)
+            srows[b] = rows[b];
+    __syncthreads();
+    const int lane = threadIdx.x, i = lane & 31, h = lane >> 5;
     const uint32_t ci0 = blockIdx.x * 64, co0 = blockIdx.y * 32;
-    const uint32_t ps = blockIdx.z * per_slice, pe = ps + per_slice < B.P ? ps + per_slice : B.P;
-    const int kk = lane & 15, sub = lane >> 4;   // position in the chunk, row / column group
-    float* As = stage[wave];
-    float* Bs = As + 32 * kLdA;
-    float ra[8], rb[16];
-    auto load = [&](uint32_t k0) {
-        const uint32_t p = k0 + kk;
-        const bool in    = p < pe;
-        size_t xb        = 0;
-        if (in)
-        {
-            const uint32_t b = B.div_hw.div(p);
-            xb               = (size_t) rows[b] * B.Cin * B.hw + (p - b * B.hw);
-        }
+    const uint32_t ps = blockIdx.z * per_slice, pe = min(ps + per_slice, B.P);
+    const float* gr   = g + (size_t) min(co0 + i, B.Cout - 1) * B.P;
+    const uint32_t cia = min(ci0 + i, B.Cin - 1), cib = min(ci0 + 32 + i, B.Cin - 1);
+    const size_t plane = (size_t) B.Cin * B.hw;
+    // x[ci][q] for a position q of the batch
+    auto xrow = [&](uint32_t b) -> size_t { return (size_t) (lds_rows ? srows[b] : rows[b]) * plane; };
+    float a0[16], x0[16], y0[16], a1[16], x1[16], y1[16];
+    auto load = [&](uint32_t q0, float (&a)[16], float (&xv)[16], float (&yv)[16]) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j)   // A: g[co][p], 4 rows x 16 consecutive positions per load
+        for (int s4 = 0; s4 < 4; ++s4)
         {
-            const uint32_t co = co0 + sub + 4 * j;
-            ra[j] = (in && co < B.Cout) ? g[(size_t) co * B.P + p] : 0.0f;
-        }
+            const uint32_t q = q0 + 8 * s4 + 4 * h;   // steps 4 s4 .. 4 s4 + 3: positions q .. q + 3
+            if constexpr (V4)
+            {
+                const uint32_t qc = min(q, pe - 4);   // pe - ps is a multiple of 4 (P = nb hw, hw % 4 == 0)
+                const uint32_t b = B.div_hw.div(qc), t = qc - b * B.hw;
+                const size_t base = xrow(b) + t;
+                const f4 gv = *reinterpret_cast<const f4*>(gr + qc);
+                const f4 xv4 = *reinterpret_cast<const f4*>(B.x + base + (size_t) cia * B.hw);
+                const f4 yv4 = *reinterpret_cast<const f4*>(B.x + base + (size_t) cib * B.hw);
+                const bool in = q < pe;
+                const float ga[4] = {gv.x, gv.y, gv.z, gv.w}, xa[4] = {xv4.x, xv4.y, xv4.z, xv4.w},
+                            ya[4] = {yv4.x, yv4.y, yv4.z, yv4.w};
 #pragma unroll
-        for (int j = 0; j < 16; ++j)   // B: x[ci][p], 4 input channels x 16 consecutive positions per load
-        {
-            const uint32_t ci = ci0 + sub + 4 * j;
-            rb[j] = (in && ci < B.Cin) ? B.x[xb + (size_t) ci * B.hw] : 0.0f;
+                for (int e = 0; e < 4; ++e)
+                {
+                    a[4 * s4 + e]  = in ? ga[e] : 0.0f;
+                    xv[4 * s4 + e] = in ? xa[e] : 0.0f;
+                    yv[4 * s4 + e] = in ? ya[e] : 0.0f;
+                }
+            }
+            else
+            {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                {
+                    const uint32_t qe = q + e, qc = min(qe, pe - 1);
+                    const uint32_t b = B.div_hw.div(qc), t = qc - b * B.hw;
+                    const size_t base = xrow(b) + t;
+                    const bool in     = qe < pe;
+                    const float gv = gr[qc], xv_ = B.x[base + (size_t) cia * B.hw], yv_ = B.x[base + (size_t) cib * B.hw];
+                    a[4 * s4 + e]  = in ? gv : 0.0f;
+                    xv[4 * s4 + e] = in ? xv_ : 0.0f;
+                    yv[4 * s4 + e] = in ? yv_ : 0.0f;
+                }
+            }
         }
     };
     f32x16 acc0 = {}, acc1 = {};
-    uint32_t k0 = ps + part * kKc;
-    if (k0 < pe)
-        load(k0);
-    for (; k0 < pe; k0 += SK * kKc)
+    auto mfma = [&](const float (&a)[16], const float (&xv)[16], const float (&yv)[16]) {
+#pragma unroll
+        for (int st = 0; st < 16; ++st)
+        {
+            acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], xv[st], acc0, 0, 0, 0);
+            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], yv[st], acc1, 0, 0, 0);
+        }
+    };
+    uint32_t q0 = ps;
+    if (q0 < pe)
+        load(q0, a0, x0, y0);
+    for (; q0 < pe; q0 += 2 * kKc)
     {
-#pragma unroll
-        for (int j = 0; j < 8; ++j)
-            As[(sub + 4 * j) * kLdA + kk] = ra[j];
-#pragma unroll
-        for (int j = 0; j < 16; ++j)
-            Bs[kk * kLdB + sub + 4 * j] = rb[j];
-        wave_sync();
-        if (k0 + SK * kKc < pe)
-            load(k0 + SK * kKc);
-        mfma_chunk(As, Bs, acc0, acc1);
-        wave_sync();
+        if (q0 + kKc < pe)
+            load(q0 + kKc, a1, x1, y1);
+        mfma(a0, x0, y0);
+        if (q0 + kKc >= pe)
+            break;
+        if (q0 + 2 * kKc < pe)
+            load(q0 + 2 * kKc, a0, x0, y0);
+        mfma(a1, x1, y1);
     }
-    reduce_parts<SK>(acc0, acc1, red);
-    if (part != 0)
-        return;
+    // part[s][co][ci]: element r of lane (i, h) is output channel co0 + (r & 3) + 8 (r >> 2) + 4 h,
+    // input channel ci0 + i (acc0) / ci0 + 32 + i (acc1)
     float* out = part_out + (size_t) blockIdx.z * B.Cout * B.Cin;
 #pragma unroll
-    for (int h = 0; h < 2; ++h)
+    for (int r = 0; r < 16; ++r)
     {
-        const uint32_t ci = ci0 + 32 * h + (lane & 31);
-        if (ci >= B.Cin)
+        const uint32_t co = co0 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (co >= B.Cout)
             continue;
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-        {
-            const uint32_t co = co0 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-            if (co < B.Cout)
-                out[(size_t) co * B.Cin + ci] = h ? acc1[r] : acc0[r];
-        }
+        if (ci0 + i < B.Cin)
+            out[(size_t) co * B.Cin + ci0 + i] = acc0[r];
+        if (ci0 + 32 + i < B.Cin)
+            out[(size_t) co * B.Cin + ci0 + 32 + i] = acc1[r];
     }
 }
 
@@ -298,18 +335,35 @@ int aimet_adaround_pw_cm_forward(const float* x_cache, const float* target_cache
         if (bias)
             require_device_ptr(bias, "bias");
         const float scale = (float) (2.0 / (double) (nb * hw));   // as aimet_adaround_recon_grad_indexed_cm
-        // waves per sub-tile by the depth of the sum: deep Cin splits over the workgroup's waves
-        const int sk      = Cin >= 256 ? 4 : (Cin >= 96 ? 2 : 1);
-        const int64_t sub = 32 * (4 / sk);
-        const dim3 grid((unsigned) ceil_div((int64_t) B.P, (int64_t) 64), (unsigned) ceil_div(Cout, sub));
+        const bool even   = Cin % kKc == 0 && (reinterpret_cast<uintptr_t>(w) & 7) == 0;
+        // waves per sub-tile: enough to give every SIMD a wave (the sums are latency-bound at one wave
+        // per SIMD), at most one per K chunk
+        const int64_t tiles = ceil_div((int64_t) B.P, (int64_t) 64) * ceil_div(Cout, (int64_t) 32);
+        const int64_t nch   = ceil_div(Cin, (int64_t) kKc);
+        int sk              = 1;
+        while (sk < 4 && tiles * sk < 1024 && 2 * sk <= nch)   // 8 waves of ~200 VGPRs would spill
+            sk *= 2;
+        const dim3 grid((unsigned) ceil_div((int64_t) B.P, (int64_t) 64), (unsigned) ceil_div(Cout, (int64_t) 32));
         AIMET_REQUIRE(grid.y <= 65535, "too many output channels");
         hipStream_t st = as_stream(stream);
+        auto go = [&](auto skc, auto evc) {
+            constexpr int SK    = decltype(skc)::value;
+            constexpr bool EVEN = decltype(evc)::value;
+            pw_cm_forward_kernel<SK, EVEN><<<grid, 64 * SK, 0, st>>>(B, target_cache, w, bias, grad_q, it_next, scale,
+                                                                      act);
+        };
+        auto with_even = [&](auto skc) {
+            if (even)
+                go(skc, std::true_type {});
+            else
+                go(skc, std::false_type {});
+        };
         if (sk == 4)
-            pw_cm_forward_kernel<4><<<grid, 256, 0, st>>>(B, target_cache, w, bias, grad_q, it_next, scale, act);
+            with_even(std::integral_constant<int, 4> {});
         else if (sk == 2)
-            pw_cm_forward_kernel<2><<<grid, 256, 0, st>>>(B, target_cache, w, bias, grad_q, it_next, scale, act);
+            with_even(std::integral_constant<int, 2> {});
         else
-            pw_cm_forward_kernel<1><<<grid, 256, 0, st>>>(B, target_cache, w, bias, grad_q, it_next, scale, act);
+            with_even(std::integral_constant<int, 1> {});
         AIMET_LAUNCH_CHECK();
     });
 }
@@ -319,10 +373,11 @@ int aimet_adaround_pw_cm_wgrad_slices(int64_t nb, int64_t Cin, int64_t Cout, int
     return guarded([&] {
         AIMET_REQUIRE(slices != nullptr, "slices is null");
         AIMET_REQUIRE(nb > 0 && Cin > 0 && Cout > 0 && hw > 0, "invalid shape");
-        // enough slices for ~2 workgroups per CU, each at least 2 chunks deep per wave
+        // one wave per (32 x 64 tile, slice): about one wave per SIMD (1024), each slice at least
+        // two 32-position chunks deep; at most 64 slices (the Adam step adds them per element)
         const int64_t tiles = ceil_div(Cin, (int64_t) 64) * ceil_div(Cout, (int64_t) 32), P = nb * hw;
-        const int64_t s     = ceil_div((int64_t) 512, tiles);
-        const int64_t smax  = std::max<int64_t>(1, P / (8 * kKc));
+        const int64_t s     = ceil_div((int64_t) 1024, tiles);
+        const int64_t smax  = std::max<int64_t>(1, P / (2 * kKc));
         *slices             = std::min<int64_t>(std::min<int64_t>(s, smax), 64);
     });
 }
@@ -336,12 +391,18 @@ int aimet_adaround_pw_cm_wgrad(const float* x_cache, const int64_t* idx_all, con
         require_device_ptr(grad_q, "grad_q");
         require_device_ptr(parts, "parts");
         AIMET_REQUIRE(slices >= 1 && slices <= 65535, "slices out of range");
-        // slice boundaries on K-chunk multiples: every slice but the last holds whole chunks
-        const int64_t per = ceil_div(ceil_div((int64_t) B.P, slices), (int64_t) kKc) * kKc;
+        // slice boundaries on multiples of 8 positions (the float4 groups stay inside one sample
+        // and aligned when hw % 4 == 0)
+        const int64_t per = ceil_div(ceil_div((int64_t) B.P, slices), (int64_t) 8) * 8;
         const dim3 grid((unsigned) ceil_div(Cin, (int64_t) 64), (unsigned) ceil_div(Cout, (int64_t) 32),
                         (unsigned) slices);
         AIMET_REQUIRE(grid.y <= 65535, "too many output channels");
-        pw_cm_wgrad_kernel<<<grid, 256, 0, as_stream(stream)>>>(B, grad_q, parts, (uint32_t) per);
+        const bool v4 = hw % 4 == 0 && (reinterpret_cast<uintptr_t>(x_cache) & 15) == 0 &&
+                        (reinterpret_cast<uintptr_t>(grad_q) & 15) == 0;
+        if (v4)
+            pw_cm_wgrad_kernel<true><<<grid, 64, 0, as_stream(stream)>>>(B, grad_q, parts, (uint32_t) per);
+        else
+            pw_cm_wgrad_kernel<false><<<grid, 64, 0, as_stream(stream)>>>(B, grad_q, parts, (uint32_t) per);
         AIMET_LAUNCH_CHECK();
     });
 }

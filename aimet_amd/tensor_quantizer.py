@@ -134,6 +134,9 @@ class AimetTensorQuantizer:
         """_ensure for many quantizers: the ones without device state on `device` get it from one
         aimet_tq_create_many call (one allocation + one initialisation launch for all)."""
         idx = device.index if device.index is not None else torch.cuda.current_device()
+        handles = [q._handle if q._device == idx else None for q in quantizers]
+        if None not in handles:   # every quantizer already has its state on this device
+            return handles
         fresh = [q for q in quantizers if q._handle is None or q._device != idx]
         if len(fresh) > 1:
             for q in fresh:
@@ -458,29 +461,31 @@ class AimetTensorQuantizer:
         ch_axes = list(param_ch_axes) if param_ch_axes is not None else [0] * len(pq)
         # every check runs before anything is launched or any quantizer changes: a refused call
         # leaves all state as it was (only native failures reach the request-discard path below)
+        # host preparation is on the critical path of a ~4 ms call (the first launch waits for it):
+        # one pass over the activations (checks, pointers, sizes) with the fewest torch attribute
+        # calls, then the parameters' checks; a non-contiguous input's copy is queued only after
+        # every check passed, on `main`, the stream the activations' kernels run on (the caller's
+        # current stream may be another one)
         f32 = torch.float32
-        for t in activations:
+        keep, a_ptr, a_n, copies = list(activations), [], [], []
+        for i, t in enumerate(keep):
             if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == f32):
                 _require_gpu(t)
                 raise TypeError("calibrateResidentAsync takes float32 tensors (got %s)" % t.dtype)
+            if t.is_contiguous():
+                a_ptr.append(t.data_ptr())
+            else:
+                copies.append(i)
+                a_ptr.append(0)
+            a_n.append(t.numel())
         p_specs = _param_specs(pq, params, ch_axes)
         main = main_stream if main_stream is not None else torch.cuda.current_stream(dev)
         side = side_stream if side_stream is not None else main
-        # host preparation is on the critical path of a ~4 ms call (the first launch waits for it):
-        # one pass over the tensors with the fewest torch attribute calls. A non-contiguous input's
-        # copy is queued on `main`, the stream the activations' kernels run on (the caller's
-        # current stream may be another one).
-        keep, a_ptr, a_n = [], [], []
-        with torch.cuda.stream(main):
-            for t in activations:
-                if not t.is_contiguous():
-                    t = t.contiguous()
-                keep.append(t)
-                a_ptr.append(t.data_ptr())
-                a_n.append(t.numel())
-        if reset:
-            for q in aq + pq:
-                q._pending_percentile = None
+        if copies:
+            with torch.cuda.stream(main):
+                for i in copies:
+                    keep[i] = keep[i].contiguous()
+                    a_ptr[i] = keep[i].data_ptr()
         na, np_ = len(aq), len(pq)
         i32x4 = ctypes.c_int32 * 4
         a_set, p_set = i32x4(*[int(v) for v in act_settings]), i32x4(*[int(v) for v in param_settings])
@@ -501,6 +506,9 @@ class AimetTensorQuantizer:
                              main.cuda_stream, side.cuda_stream, ctypes.byref(ra), ctypes.byref(ctypes.c_void_p()))
             for q in aq:
                 q._is_encoding_valid = True
+            if reset:
+                for q in aq + pq:
+                    q._pending_percentile = None
             try:
                 # a non-contiguous parameter's copy goes on the side stream, after its wait for
                 # `main` above and before the parameters' kernels (the second call runs every
@@ -528,6 +536,9 @@ class AimetTensorQuantizer:
             for q in pq:
                 q._is_encoding_valid = True
         else:
+            if reset:
+                for q in aq + pq:
+                    q._pending_percentile = None
             # the copies on `main`: the native call starts `side` after everything queued there
             with torch.cuda.stream(main):
                 p_ptr = _param_pointers(p_specs, keep)
