@@ -561,7 +561,7 @@ __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __r
 // backward: grid-stride over tiles of kBlock x U quads (U quads in flight per lane, 3 x 16-B loads
 // each; bounded grid: one round-loss atomic per workgroup); the loop bounds are uniform over the
 // workgroup (ada_round_pows synchronises it)
-template <int U>
+template <int U, bool WL>
 __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
                                                                   const f4* __restrict__ g, f4* __restrict__ ga,
                                                                   uint32_t nq, AdaChannel map,
@@ -574,6 +574,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
 {
     constexpr int E = 4 * U;
     __shared__ float lds[kBlock / 64][2 * 64 * E];
+    p.want_loss = WL;   // a constant from here on: the form without the loss value carries none of its work
     if (reg_beta)   // device-resident {reg, beta, beta - 1}: a HIP-graph replay per iteration
     {
         p.reg     = reg_beta[0];
@@ -745,7 +746,7 @@ __global__ __launch_bounds__(kBlock) void adam_bias_corr_kernel(double beta1, do
 // dL/dalpha (ada_bwd, with this iteration's {reg, beta, beta - 1} from reg_beta_all[it]) and the
 // Adam update of alpha in place; `step` = it_next[0] (= it + 1, written by the gather kernel of the
 // same iteration), workgroup 0 publishes it to it_cur for the next iteration's gather.
-template <bool VEC>
+template <bool VEC, bool WL>
 __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* __restrict__ w,
                                                                    float* __restrict__ alpha,
                                                                    const float* __restrict__ g,
@@ -762,6 +763,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                                                                    unsigned* __restrict__ ticket, uint32_t nparts,
                                                                    const float* __restrict__ bias_corr)
 {
+    p.want_loss        = WL;   // constant: see adaround_bwd_vec_kernel
     const int64_t step = it_next[0];
     if (blockIdx.x == 0 && threadIdx.x == 0)
         it_cur[0] = step;
@@ -1132,12 +1134,13 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
                     reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),
                     reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss, reg_beta, lf.part, lf.ticket);
             };
+            const bool wl = p.want_loss != 0;
             if (U == 1)
-                launch(adaround_bwd_vec_kernel<1>);
+                wl ? launch(adaround_bwd_vec_kernel<1, true>) : launch(adaround_bwd_vec_kernel<1, false>);
             else if (U == 4)
-                launch(adaround_bwd_vec_kernel<4>);
+                wl ? launch(adaround_bwd_vec_kernel<4, true>) : launch(adaround_bwd_vec_kernel<4, false>);
             else
-                launch(adaround_bwd_vec_kernel<2>);
+                wl ? launch(adaround_bwd_vec_kernel<2, true>) : launch(adaround_bwd_vec_kernel<2, false>);
             AIMET_LAUNCH_CHECK();
         }
         else
@@ -1372,14 +1375,16 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
         blocks              = blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid;
         hipStream_t st = as_stream(stream);
         LossFold lf(round_loss, (unsigned) blocks, st);
+        auto launch = [&](auto kernel) {
+            kernel<<<(unsigned) blocks, kBlock, 0, st>>>(w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta,
+                                                         offset, p, reg_beta_all, it_next, it_cur, a, round_loss,
+                                                         wq_next, lf.part, lf.ticket, (uint32_t) nparts, bias_corr);
+        };
+        const bool wl = round_loss != nullptr;
         if (vec)
-            adaround_bwd_adam_kernel<true><<<(unsigned) blocks, kBlock, 0, st>>>(
-                w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss, wq_next, lf.part, lf.ticket, (uint32_t) nparts, bias_corr);
+            wl ? launch(adaround_bwd_adam_kernel<true, true>) : launch(adaround_bwd_adam_kernel<true, false>);
         else
-            adaround_bwd_adam_kernel<false><<<(unsigned) blocks, kBlock, 0, st>>>(
-                w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta, offset, p, reg_beta_all, it_next,
-                it_cur, a, round_loss, wq_next, lf.part, lf.ticket, (uint32_t) nparts, bias_corr);
+            wl ? launch(adaround_bwd_adam_kernel<false, true>) : launch(adaround_bwd_adam_kernel<false, false>);
         AIMET_LAUNCH_CHECK();
     });
 }

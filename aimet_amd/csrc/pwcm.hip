@@ -51,37 +51,58 @@ struct CmBatch
 // (deterministic).
 //   forward (K = input channels):  kk = 4 (st / 2) + 2 h + st % 2 -- W[co][k0 + kk] as float2 pairs
 //   wgrad   (K = positions):       kk = 8 (st / 4) + 4 h + st % 4 -- 4 consecutive positions per load
+//                                  (hw % 4 == 0), else kk = 16 h + st (the sample followed incrementally)
 
-// forward + reconstruction gradient. One 32 x 64 sub-tile (32 output channels x 64 positions) per
-// workgroup of SK waves; wave `part` takes the K chunks part, part + SK, ... with the next chunk's
-// loads in flight while its MFMAs run; the waves' accumulators are added in part order through
-// LDS (deterministic). EVEN: Cin % 32 == 0 (no ragged chunk: W read as float2 pairs, no zeroing).
-// Wave 0 issues the 32 target values of its outputs before the sums, so the epilogue waits for
-// nothing.
-template <int SK, bool EVEN>
+// forward + reconstruction gradient. One 32 x NP sub-tile (32 output channels x NP = 32 or 64
+// positions) per workgroup of SK waves; wave `part` takes the K chunks part, part + SK, ... with
+// the next chunk's loads in flight while its MFMAs run; the waves' accumulators are added in part
+// order through LDS (deterministic). EVEN: Cin % 32 == 0 (no ragged chunk: W read as float2
+// pairs, no zeroing). Wave 0 issues its outputs' targets and biases before the first chunk's loads
+// (tools/studies/pw_cm_probe.hip: loading them in the epilogue doubled the kernel); NP = 32 gives
+// twice the waves of NP = 64 for layers with few output tiles (one wave per SIMD left the loads'
+// latency exposed).
+template <int SK, bool EVEN, int NP>
 __global__ __launch_bounds__(64 * SK) void pw_cm_forward_kernel(CmBatch B, const float* __restrict__ target,
                                                                 const float* __restrict__ w,
                                                                 const float* __restrict__ bias, float* __restrict__ g,
                                                                 int64_t* __restrict__ it_next, float scale, int act)
 {
-    __shared__ float red[SK > 1 ? (SK - 1) * 32 * 64 : 1];
+    constexpr bool TWO = NP == 64;   // two accumulators (positions i and 32 + i)
+    __shared__ float red[SK > 1 ? (SK - 1) * 32 * NP : 1];
     const int64_t it = B.it_cur[0];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         it_next[0] = it + 1;
     const int64_t* rows = B.idx_all + it * B.nb;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
-    const uint32_t co0 = blockIdx.y * 32, p0 = blockIdx.x * 64;
-    // this lane's two B columns (positions p0 + i, p0 + 32 + i, clamped into the batch: a column past
-    // P is computed from real data and never stored)
-    const uint32_t pa = min(p0 + i, B.P - 1), pb = min(p0 + 32 + i, B.P - 1);
+    const uint32_t co0 = blockIdx.y * 32, p0 = blockIdx.x * NP;
+    // this lane's B columns (positions p0 + i and, NP = 64, p0 + 32 + i; clamped into the batch: a
+    // column past P is computed from real data and never stored)
+    const uint32_t pa = min(p0 + i, B.P - 1), pb = min(p0 + (TWO ? 32 : 0) + i, B.P - 1);
     const uint32_t ba = B.div_hw.div(pa), bb = B.div_hw.div(pb);
     const size_t ra = (size_t) rows[ba], rb = (size_t) rows[bb];
     const float* xa = B.x + ra * B.Cin * B.hw + (pa - ba * B.hw);
     const float* xb = B.x + rb * B.Cin * B.hw + (pb - bb * B.hw);
     const float* wr = w + (size_t) min(co0 + i, B.Cout - 1) * B.Cin;
     const uint32_t nch = (B.Cin + kKc - 1) / kKc;
-    float a0[16], x0[16], y0[16], a1[16], x1[16], y1[16];
-    auto load = [&](uint32_t c, float (&a)[16], float (&xv)[16], float (&yv)[16]) {
+    // wave 0's epilogue operands first: C/D map of the 32 x 32 f32 MFMA, element r of lane (i, h)
+    // is row (r & 3) + 8 (r >> 2) + 4 h, column i
+    float t0[16], t1[TWO ? 16 : 1], bs[16];
+    if (wave == 0)
+    {
+        const float* ta = target + ra * B.Cout * B.hw + (pa - ba * B.hw);
+        const float* tb = target + rb * B.Cout * B.hw + (pb - bb * B.hw);
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+        {
+            const uint32_t co = min(co0 + (r & 3) + 8 * (r >> 2) + 4 * h, B.Cout - 1);
+            t0[r]             = ta[(size_t) co * B.hw];
+            if constexpr (TWO)
+                t1[r] = tb[(size_t) co * B.hw];
+            bs[r] = bias ? bias[co] : 0.0f;
+        }
+    }
+    float a0[16], x0[16], y0[TWO ? 16 : 1], a1[16], x1[16], y1[TWO ? 16 : 1];
+    auto load = [&](uint32_t c, float (&a)[16], float (&xv)[16], auto& yv) {
         const uint32_t k0 = c * kKc;
 #pragma unroll
         for (int s2 = 0; s2 < 8; ++s2)
@@ -96,7 +117,8 @@ __global__ __launch_bounds__(64 * SK) void pw_cm_forward_kernel(CmBatch B, const
                 for (int e = 0; e < 2; ++e)
                 {
                     xv[2 * s2 + e] = xa[(size_t) (k + e) * B.hw];
-                    yv[2 * s2 + e] = xb[(size_t) (k + e) * B.hw];
+                    if constexpr (TWO)
+                        yv[2 * s2 + e] = xb[(size_t) (k + e) * B.hw];
                 }
             }
             else
@@ -106,41 +128,31 @@ __global__ __launch_bounds__(64 * SK) void pw_cm_forward_kernel(CmBatch B, const
                 {
                     const uint32_t ke = k + e, kc = min(ke, B.Cin - 1);
                     const bool in     = ke < B.Cin;
-                    const float av = wr[kc], xv_ = xa[(size_t) kc * B.hw], yv_ = xb[(size_t) kc * B.hw];
+                    const float av = wr[kc], xv_ = xa[(size_t) kc * B.hw];
                     a[2 * s2 + e]  = in ? av : 0.0f;
                     xv[2 * s2 + e] = in ? xv_ : 0.0f;
-                    yv[2 * s2 + e] = in ? yv_ : 0.0f;
+                    if constexpr (TWO)
+                    {
+                        const float yv_ = xb[(size_t) kc * B.hw];
+                        yv[2 * s2 + e]  = in ? yv_ : 0.0f;
+                    }
                 }
             }
         }
     };
     f32x16 acc0 = {}, acc1 = {};
-    auto mfma = [&](const float (&a)[16], const float (&xv)[16], const float (&yv)[16]) {
+    auto mfma = [&](const float (&a)[16], const float (&xv)[16], const auto& yv) {
 #pragma unroll
         for (int st = 0; st < 16; ++st)
         {
             acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], xv[st], acc0, 0, 0, 0);
-            acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], yv[st], acc1, 0, 0, 0);
+            if constexpr (TWO)
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], yv[st], acc1, 0, 0, 0);
         }
     };
     uint32_t c = wave;
     if (c < nch)
         load(c, a0, x0, y0);
-    // the targets of wave 0's outputs: C/D map of the 32 x 32 f32 MFMA, element r of lane (i, h) is
-    // row (r & 3) + 8 (r >> 2) + 4 h, column i
-    float t0[16], t1[16];
-    if (wave == 0)
-    {
-        const float* ta = target + ra * B.Cout * B.hw + (pa - ba * B.hw);
-        const float* tb = target + rb * B.Cout * B.hw + (pb - bb * B.hw);
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-        {
-            const uint32_t co = min(co0 + (r & 3) + 8 * (r >> 2) + 4 * h, B.Cout - 1);
-            t0[r]             = ta[(size_t) co * B.hw];
-            t1[r]             = tb[(size_t) co * B.hw];
-        }
-    }
     for (; c < nch; c += 2 * SK)
     {
         if (c + SK < nch)
@@ -156,12 +168,13 @@ __global__ __launch_bounds__(64 * SK) void pw_cm_forward_kernel(CmBatch B, const
     {
         if (wave != 0)
         {
-            float* rd = red + (wave - 1) * 32 * 64;
+            float* rd = red + (wave - 1) * 32 * NP;
 #pragma unroll
             for (int r = 0; r < 16; ++r)
             {
-                rd[r * 64 + lane]        = acc0[r];
-                rd[(16 + r) * 64 + lane] = acc1[r];
+                rd[r * 64 + lane] = acc0[r];
+                if constexpr (TWO)
+                    rd[(16 + r) * 64 + lane] = acc1[r];
             }
         }
         __syncthreads();
@@ -169,12 +182,13 @@ __global__ __launch_bounds__(64 * SK) void pw_cm_forward_kernel(CmBatch B, const
             return;
         for (int q = 0; q < SK - 1; ++q)
         {
-            const float* rd = red + q * 32 * 64;
+            const float* rd = red + q * 32 * NP;
 #pragma unroll
             for (int r = 0; r < 16; ++r)
             {
                 acc0[r] += rd[r * 64 + lane];
-                acc1[r] += rd[(16 + r) * 64 + lane];
+                if constexpr (TWO)
+                    acc1[r] += rd[(16 + r) * 64 + lane];
             }
         }
     }
@@ -184,11 +198,11 @@ __global__ __launch_bounds__(64 * SK) void pw_cm_forward_kernel(CmBatch B, const
         const uint32_t co = co0 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (co >= B.Cout)
             continue;
-        const float bs = bias ? bias[co] : 0.0f;
         if (p0 + i < B.P)
-            g[(size_t) co * B.P + p0 + i] = recon_g(acc0[r] + bs, t0[r], scale, act);
-        if (p0 + 32 + i < B.P)
-            g[(size_t) co * B.P + p0 + 32 + i] = recon_g(acc1[r] + bs, t1[r], scale, act);
+            g[(size_t) co * B.P + p0 + i] = recon_g(acc0[r] + bs[r], t0[r], scale, act);
+        if constexpr (TWO)
+            if (p0 + 32 + i < B.P)
+                g[(size_t) co * B.P + p0 + 32 + i] = recon_g(acc1[r] + bs[r], t1[r], scale, act);
     }
 }
 
@@ -243,20 +257,29 @@ __global__ __launch_bounds__(64) void pw_cm_wgrad_kernel(CmBatch B, const float*
                     yv[4 * s4 + e] = in ? ya[e] : 0.0f;
                 }
             }
-            else
-            {
+        }
+    };
+    // hw % 4 != 0 (7 x 7 layers): lane h takes positions q0 + 16 h .. + 15 (step st: q0 + 16 h + st),
+    // following the sample boundary incrementally instead of a division per position
+    auto load_s = [&](uint32_t q0, float (&a)[16], float (&xv)[16], float (&yv)[16]) {
+        const uint32_t qs = q0 + 16 * h, qc0 = min(qs, pe - 1);
+        uint32_t b = B.div_hw.div(qc0), t = qc0 - b * B.hw;
+        size_t base = xrow(b);
 #pragma unroll
-                for (int e = 0; e < 4; ++e)
-                {
-                    const uint32_t qe = q + e, qc = min(qe, pe - 1);
-                    const uint32_t b = B.div_hw.div(qc), t = qc - b * B.hw;
-                    const size_t base = xrow(b) + t;
-                    const bool in     = qe < pe;
-                    const float gv = gr[qc], xv_ = B.x[base + (size_t) cia * B.hw], yv_ = B.x[base + (size_t) cib * B.hw];
-                    a[4 * s4 + e]  = in ? gv : 0.0f;
-                    xv[4 * s4 + e] = in ? xv_ : 0.0f;
-                    yv[4 * s4 + e] = in ? yv_ : 0.0f;
-                }
+        for (int e = 0; e < 16; ++e)
+        {
+            const uint32_t q = qs + e;
+            const bool in    = q < pe;
+            const float gv = gr[min(q, pe - 1)], xv_ = B.x[base + (size_t) cia * B.hw + t],
+                        yv_ = B.x[base + (size_t) cib * B.hw + t];
+            a[e]  = in ? gv : 0.0f;
+            xv[e] = in ? xv_ : 0.0f;
+            yv[e] = in ? yv_ : 0.0f;
+            if (++t == B.hw)
+            {
+                t    = 0;
+                b    = min(b + 1, B.nb - 1);
+                base = xrow(b);
             }
         }
     };
@@ -269,18 +292,24 @@ __global__ __launch_bounds__(64) void pw_cm_wgrad_kernel(CmBatch B, const float*
             acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[st], yv[st], acc1, 0, 0, 0);
         }
     };
+    auto ld = [&](uint32_t q, float (&a)[16], float (&xv)[16], float (&yv)[16]) {
+        if constexpr (V4)
+            load(q, a, xv, yv);
+        else
+            load_s(q, a, xv, yv);
+    };
     uint32_t q0 = ps;
     if (q0 < pe)
-        load(q0, a0, x0, y0);
+        ld(q0, a0, x0, y0);
     for (; q0 < pe; q0 += 2 * kKc)
     {
         if (q0 + kKc < pe)
-            load(q0 + kKc, a1, x1, y1);
+            ld(q0 + kKc, a1, x1, y1);
         mfma(a0, x0, y0);
         if (q0 + kKc >= pe)
             break;
         if (q0 + 2 * kKc < pe)
-            load(q0 + 2 * kKc, a0, x0, y0);
+            ld(q0 + 2 * kKc, a0, x0, y0);
         mfma(a1, x1, y1);
     }
     // part[s][co][ci]: element r of lane (i, h) is output channel co0 + (r & 3) + 8 (r >> 2) + 4 h,
@@ -336,27 +365,37 @@ int aimet_adaround_pw_cm_forward(const float* x_cache, const float* target_cache
             require_device_ptr(bias, "bias");
         const float scale = (float) (2.0 / (double) (nb * hw));   // as aimet_adaround_recon_grad_indexed_cm
         const bool even   = Cin % kKc == 0 && (reinterpret_cast<uintptr_t>(w) & 7) == 0;
-        // waves per sub-tile: enough to give every SIMD a wave (the sums are latency-bound at one wave
-        // per SIMD), at most one per K chunk
-        const int64_t tiles = ceil_div((int64_t) B.P, (int64_t) 64) * ceil_div(Cout, (int64_t) 32);
-        const int64_t nch   = ceil_div(Cin, (int64_t) kKc);
-        int sk              = 1;
+        // positions per wave and waves per sub-tile: enough waves to give every SIMD one (the sums
+        // are latency-bound at one wave per SIMD) -- 32-position tiles first, then the K chunks split
+        // over up to 4 waves
+        const int64_t ctiles = ceil_div(Cout, (int64_t) 32);
+        const int np         = ceil_div((int64_t) B.P, (int64_t) 64) * ctiles >= 1024 ? 64 : 32;
+        const int64_t tiles  = ceil_div((int64_t) B.P, (int64_t) np) * ctiles;
+        const int64_t nch    = ceil_div(Cin, (int64_t) kKc);
+        int sk               = 1;
         while (sk < 4 && tiles * sk < 1024 && 2 * sk <= nch)   // 8 waves of ~200 VGPRs would spill
             sk *= 2;
-        const dim3 grid((unsigned) ceil_div((int64_t) B.P, (int64_t) 64), (unsigned) ceil_div(Cout, (int64_t) 32));
+        const dim3 grid((unsigned) ceil_div((int64_t) B.P, (int64_t) np), (unsigned) ctiles);
         AIMET_REQUIRE(grid.y <= 65535, "too many output channels");
         hipStream_t st = as_stream(stream);
-        auto go = [&](auto skc, auto evc) {
+        auto go = [&](auto skc, auto evc, auto npc) {
             constexpr int SK    = decltype(skc)::value;
             constexpr bool EVEN = decltype(evc)::value;
-            pw_cm_forward_kernel<SK, EVEN><<<grid, 64 * SK, 0, st>>>(B, target_cache, w, bias, grad_q, it_next, scale,
-                                                                      act);
+            constexpr int NP    = decltype(npc)::value;
+            pw_cm_forward_kernel<SK, EVEN, NP><<<grid, 64 * SK, 0, st>>>(B, target_cache, w, bias, grad_q, it_next,
+                                                                          scale, act);
+        };
+        auto with_np = [&](auto skc, auto evc) {
+            if (np == 64)
+                go(skc, evc, std::integral_constant<int, 64> {});
+            else
+                go(skc, evc, std::integral_constant<int, 32> {});
         };
         auto with_even = [&](auto skc) {
             if (even)
-                go(skc, std::true_type {});
+                with_np(skc, std::true_type {});
             else
-                go(skc, std::false_type {});
+                with_np(skc, std::false_type {});
         };
         if (sk == 4)
             with_even(std::integral_constant<int, 4> {});

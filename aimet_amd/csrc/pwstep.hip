@@ -31,6 +31,9 @@
 #include "common.hpp"
 #include "recon.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+
 namespace aimet_amd
 {
 namespace
@@ -240,6 +243,156 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
     }
 }
 
+// ---- the same step on the f32 matrix cores ------------------------------------------------
+// pw_step_kernel spends its time on LDS operand reads for VALU FMAs (16 FMAs per two 16-B reads).
+// Here both contractions are v_mfma_f32_32x32x2_f32 (A[i][k] from lane (i, h) = (lane & 31,
+// lane >> 5) at k = 2 st + h, B[k][j] at j = i; C row (r & 3) + 8 (r >> 2) + 4 h, column i):
+//   per tile of 32 positions of one sample, X[ci][p] staged in LDS (rows padded to 33 floats: the
+//   column reads of the second product hit distinct banks), W[co][ci] staged once;
+//   Q (Cp x 32, Cp = rows rounded up to 32) = W X, one 32 x 32 block per wave (blocks w, w + 4);
+//   G = recon_g(Q + bias, target) into LDS (zero past the sample's end); the next tile's X and
+//   targets are loaded while this tile's weight gradient runs;
+//   dW (Cp x Kp, Kp = Cin rounded up to 32) += G X^T over the 32 positions, the 32 x 32 output
+//   blocks spread over the waves (<= 3 each) and kept in accumulators across the workgroup's
+//   tiles; the partial per workgroup is folded as pw_step_kernel's (pw_fold_slices / _final).
+// Sums in a fixed order (deterministic); not bit-identical to pw_step_kernel's FMA chains.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kPmT   = 32;   // positions per tile
+constexpr int kPmLd  = 33;   // X / G row stride (floats)
+constexpr int kPmMaxT = 3;   // weight-gradient blocks per wave
+
+struct PmShape
+{
+    uint32_t Cp, Kw, Kx, nblk1, nblk3n, nblk3;   // rows padded, W row stride, X rows, block counts
+};
+
+template <int XB, int TB>
+__global__ __launch_bounds__(kBlock, 2) void pw_mfma_step_kernel(PwStep a, PmShape m, float* __restrict__ partial)
+{
+    extern __shared__ float lds[];
+    float* Ws = lds;                         // [Cp][Kw]
+    float* Xs = Ws + m.Cp * m.Kw;            // [Kx][33]
+    float* Gs = Xs + m.Kx * kPmLd;           // [Cp][33]
+    const uint32_t r0 = blockIdx.y * a.R;
+    const uint32_t Cin = a.Cin, Cout = a.Cout - r0 < a.R ? a.Cout - r0 : a.R, pairs = Cin * a.Cout;
+    const int64_t it = a.it_cur[0];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        a.it_next[0] = it + 1;
+    const int64_t* rows = a.idx_all + it * (int64_t) a.N;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
+    // W (zero past Cin / the range's rows) and the X rows past Cin (zero, never rewritten)
+    for (uint32_t e = threadIdx.x; e < m.Cp * m.Kw; e += kBlock)
+    {
+        const uint32_t co = e / m.Kw, ci = e - co * m.Kw;
+        Ws[e] = (co < Cout && ci < Cin) ? a.w[(size_t) (r0 + co) * Cin + ci] : 0.0f;
+    }
+    for (uint32_t e = Cin * kPmLd + threadIdx.x; e < m.Kx * kPmLd; e += kBlock)
+        Xs[e] = 0.0f;
+    // this tile's X (XB per lane: element q = threadIdx.x + kBlock j -> ci = q / 32, p = q % 32)
+    // and this wave's targets (its GEMM1 blocks w, w + 4, ...: 16 per block)
+    float xr[XB], tr[TB][16];
+    auto load = [&](uint32_t tile) {
+        const uint32_t n   = tile / a.tiles_per_sample;
+        const uint32_t hw0 = (tile - n * a.tiles_per_sample) * kPmT;
+        const size_t row   = (size_t) rows[n];
+        const float* xb    = a.x_cache + row * Cin * a.HW + hw0;
+#pragma unroll
+        for (int j = 0; j < XB; ++j)
+        {
+            const uint32_t q = threadIdx.x + kBlock * j, ci = q / kPmT, p = q % kPmT;
+            const bool in    = ci < Cin && hw0 + p < a.HW;
+            xr[j]            = in ? xb[(size_t) ci * a.HW + p] : 0.0f;
+        }
+        const float* tb = a.t_cache + (row * a.Cout + r0) * a.HW + hw0 + i;
+        const bool pin  = hw0 + i < a.HW;
+#pragma unroll
+        for (int b = 0; b < TB; ++b)
+        {
+            const uint32_t mb = wave + 4 * b;
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+            {
+                const uint32_t co = mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                tr[b][r]          = (mb < m.nblk1 && co < Cout && pin) ? tb[(size_t) co * a.HW] : 0.0f;
+            }
+        }
+    };
+    f32x16 acc3[kPmMaxT];
+#pragma unroll
+    for (int t = 0; t < kPmMaxT; ++t)
+        acc3[t] = f32x16 {};
+    if (blockIdx.x < a.tiles)
+        load(blockIdx.x);
+    for (uint32_t tile = blockIdx.x; tile < a.tiles; tile += gridDim.x)
+    {
+        const uint32_t n   = tile / a.tiles_per_sample;
+        const uint32_t hw0 = (tile - n * a.tiles_per_sample) * kPmT;
+        __syncthreads();   // the previous tile's products are done with Xs / Gs (and Ws is written)
+#pragma unroll
+        for (int j = 0; j < XB; ++j)
+        {
+            const uint32_t q = threadIdx.x + kBlock * j, ci = q / kPmT, p = q % kPmT;
+            if (ci < Cin)
+                Xs[ci * kPmLd + p] = xr[j];
+        }
+        __syncthreads();
+        // Q = W X for this wave's blocks, then G into LDS
+        const bool pin = hw0 + i < a.HW;
+#pragma unroll
+        for (int b = 0; b < TB; ++b)
+        {
+            const uint32_t mb = wave + 4 * b;
+            if (mb >= m.nblk1)
+                continue;
+            f32x16 q = {};
+            const float* wrow = Ws + (mb * 32 + i) * m.Kw;
+            for (uint32_t st = 0; 2 * st < Cin; ++st)   // k = 2 st + h < Cin rounded up to even (zero pad)
+                q = __builtin_amdgcn_mfma_f32_32x32x2f32(wrow[2 * st + h], Xs[(2 * st + h) * kPmLd + i], q, 0, 0, 0);
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+            {
+                const uint32_t co = mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+                float gv          = 0.0f;
+                if (co < Cout && pin)
+                    gv = recon_g(q[r] + (a.bias ? a.bias[r0 + co] : 0.0f), tr[b][r], a.scale, a.act);
+                Gs[co * kPmLd + i] = gv;
+            }
+        }
+        if (tile + gridDim.x < a.tiles)
+            load(tile + gridDim.x);   // in flight through the weight gradient below
+        __syncthreads();
+        // dW += G X^T over the tile's 32 positions
+#pragma unroll
+        for (int t = 0; t < kPmMaxT; ++t)
+        {
+            const uint32_t blk = wave + 4 * t;
+            if (blk >= m.nblk3)
+                continue;
+            const uint32_t mb = blk / m.nblk3n, nbk = blk - mb * m.nblk3n;
+            const float* grow = Gs + (mb * 32 + i) * kPmLd;
+            const float* xrow = Xs + (nbk * 32 + i) * kPmLd;
+#pragma unroll 4
+            for (int st = 0; st < kPmT / 2; ++st)
+                acc3[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(grow[2 * st + h], xrow[2 * st + h], acc3[t], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < kPmMaxT; ++t)
+    {
+        const uint32_t blk = wave + 4 * t;
+        if (blk >= m.nblk3)
+            continue;
+        const uint32_t mb = blk / m.nblk3n, nbk = blk - mb * m.nblk3n, ci = nbk * 32 + i;
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+        {
+            const uint32_t co = mb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (co < Cout && ci < Cin)
+                partial[(size_t) blockIdx.x * pairs + (size_t) (r0 + co) * Cin + ci] = acc3[t][r];
+        }
+    }
+}
+
 // The fold of the workgroups' partials, in two levels so that ~512 partials of up to 6144 pairs
 // are read by enough lanes: level 1 sums workgroups [s * chunk, (s + 1) * chunk) of pair e in
 // order into part2[s][e]; level 2 sums the kPwSlices slices in order (deterministic).
@@ -288,6 +441,39 @@ using namespace aimet_amd;
 
 extern "C" {
 
+// the matrix-core form's padded shape for a row range of R rows (pw_mfma_step_kernel)
+static PmShape pm_shape(int64_t Cin, int64_t R)
+{
+    PmShape m;
+    m.Cp     = (uint32_t) (ceil_div(R, (int64_t) 32) * 32);
+    const uint32_t cin2 = (uint32_t) (ceil_div(Cin, (int64_t) 2) * 2);
+    m.Kw     = cin2 + 1;
+    m.nblk1  = m.Cp / 32;
+    m.nblk3n = (uint32_t) ceil_div(Cin, (int64_t) 32);
+    m.Kx     = std::max<uint32_t>(cin2, m.nblk3n * 32);
+    m.nblk3  = m.nblk1 * m.nblk3n;
+    return m;
+}
+
+// the matrix-core form's row ranges: at most 128 rows (one 32-row output block per wave), as few
+// ranges as that allows, each a multiple of 32 rows but the last
+static int64_t pm_rows(int64_t Cin, int64_t Cout)
+{
+    const int64_t nr = ceil_div(Cout, (int64_t) 128);
+    (void) Cin;
+    return ceil_div(ceil_div(Cout, nr), (int64_t) 32) * 32;
+}
+
+// AIMET_ADA_PW_MFMA=0: the VALU form (pw_step_kernel) for comparisons
+static bool pw_mfma_enabled()
+{
+    static const bool v = [] {
+        const char* e = getenv("AIMET_ADA_PW_MFMA");
+        return !(e && e[0] == '0');
+    }();
+    return v;
+}
+
 // output rows per workgroup row range: all of them when they fit (C_out <= 192, C_in C_out <= 6144),
 // else the most that do, a multiple of 4
 static int64_t pw_rows(int64_t Cin, int64_t Cout)
@@ -332,9 +518,14 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
         require_device_ptr(grad_w, "grad_w");
         if (bias)
             require_device_ptr(bias, "bias");
-        const int64_t R = pw_rows(Cin, Cout);
-        AIMET_REQUIRE((R >= 4 || R == Cout) && R * Cin <= kPwPairs && ceil_div(Cin, (int64_t) 4) * ceil_div(R, (int64_t) 4) <=
-                                                            (int64_t) kBlock * kPwBlocks,
+        // the matrix-core form where its staging fits (W, X and G in <= 64 KiB of LDS, <= 3 weight-
+        // gradient blocks per wave), else the VALU form
+        const PmShape pm  = pm_shape(Cin, pm_rows(Cin, Cout));
+        const size_t lds  = sizeof(float) * ((size_t) pm.Cp * pm.Kw + (size_t) pm.Kx * kPmLd + (size_t) pm.Cp * kPmLd);
+        const bool mfma   = pw_mfma_enabled() && lds <= 65536 && pm.nblk1 <= 4 && pm.nblk3 <= 4 * kPmMaxT;
+        const int64_t R   = mfma ? pm_rows(Cin, Cout) : pw_rows(Cin, Cout);
+        AIMET_REQUIRE(mfma || ((R >= 4 || R == Cout) && R * Cin <= kPwPairs &&
+                               ceil_div(Cin, (int64_t) 4) * ceil_div(R, (int64_t) 4) <= (int64_t) kBlock * kPwBlocks),
                       "pointwise step: at most 512 4x4 weight-gradient blocks per row range");
         const int64_t tps    = ceil_div(HW, (int64_t) kPwT);
         const int64_t tiles  = N * tps;
@@ -351,7 +542,27 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
         PwStep a {x_cache, target_cache, idx_all, it_cur, it_next, w, bias,
                   (float) (2.0 / (double) (N * HW)), act, (uint32_t) N, (uint32_t) Cin, (uint32_t) Cout,
                   (uint32_t) HW, (uint32_t) tps, (uint32_t) tiles, (uint32_t) R};
-        pw_step_kernel<<<dim3(grid, (unsigned) ranges), kBlock, 0, st>>>(a, part);
+        if (mfma)
+        {
+            // X loads per lane (Cin x 32 / 256, bucketed) sized per layer, so a small layer holds no
+            // idle registers; one target block per wave (row ranges of <= 128 rows, pm_rows)
+            const dim3 g2(grid, (unsigned) ranges);
+            auto go = [&](auto xb) {
+                pw_mfma_step_kernel<decltype(xb)::value, 1><<<g2, kBlock, lds, st>>>(a, pm, part);
+            };
+            if (Cin <= 32)
+                go(std::integral_constant<int, 4> {});
+            else if (Cin <= 64)
+                go(std::integral_constant<int, 8> {});
+            else if (Cin <= 96)
+                go(std::integral_constant<int, 12> {});
+            else if (Cin <= 144)
+                go(std::integral_constant<int, 18> {});
+            else
+                go(std::integral_constant<int, 24> {});
+        }
+        else
+            pw_step_kernel<<<dim3(grid, (unsigned) ranges), kBlock, 0, st>>>(a, part);
         AIMET_LAUNCH_CHECK();
         const uint32_t chunk   = (uint32_t) ceil_div((int64_t) grid, (int64_t) kPwSlices);
         const uint32_t nslices = (uint32_t) ceil_div((int64_t) grid, (int64_t) chunk);
