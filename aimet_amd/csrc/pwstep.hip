@@ -518,11 +518,15 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
         require_device_ptr(grad_w, "grad_w");
         if (bias)
             require_device_ptr(bias, "bias");
-        // the matrix-core form where its staging fits (W, X and G in <= 64 KiB of LDS, <= 3 weight-
-        // gradient blocks per wave), else the VALU form
+        // the matrix-core form for C_in >= 32 where its staging fits (W, X and G in <= 64 KiB of LDS,
+        // <= 3 weight-gradient blocks per wave), else the VALU form. Below 32 input channels the
+        // weight gradient's 32-wide blocks are mostly padding and the forward's sums 8-16 steps deep:
+        // MobileNet-v2's stem and its 16 / 24-channel expanding layers ran 16-40 % slower there, the
+        // C_in >= 32 layers 9-20 % faster (profiles/r04/README.md)
         const PmShape pm  = pm_shape(Cin, pm_rows(Cin, Cout));
         const size_t lds  = sizeof(float) * ((size_t) pm.Cp * pm.Kw + (size_t) pm.Kx * kPmLd + (size_t) pm.Cp * kPmLd);
-        const bool mfma   = pw_mfma_enabled() && lds <= 65536 && pm.nblk1 <= 4 && pm.nblk3 <= 4 * kPmMaxT;
+        const bool mfma   = pw_mfma_enabled() && Cin >= 32 && lds <= 65536 && pm.nblk1 <= 4 &&
+                          pm.nblk3 <= 4 * kPmMaxT;
         const int64_t R   = mfma ? pm_rows(Cin, Cout) : pw_rows(Cin, Cout);
         AIMET_REQUIRE(mfma || ((R >= 4 || R == Cout) && R * Cin <= kPwPairs &&
                                ceil_div(Cin, (int64_t) 4) * ceil_div(R, (int64_t) 4) <= (int64_t) kBlock * kPwBlocks),
