@@ -765,7 +765,23 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                                                                    unsigned* __restrict__ ticket, uint32_t nparts,
                                                                    const float* __restrict__ bias_corr)
 {
-    p.want_loss        = WL;   // constant: see adaround_bwd_vec_kernel
+    p.want_loss = WL;   // constant: see adaround_bwd_vec_kernel
+    // the one-element-per-lane form's first element: its operands are loaded before the step's
+    // table entries, which they do not depend on, so the two round trips overlap (a small layer's
+    // step is a chain of latencies: the counter, the table entries, the operands, the arithmetic)
+    const uint32_t i0 = blockIdx.x * kBlock + threadIdx.x;
+    float f_w = 0.0f, f_a = 0.0f, f_g = 0.0f, f_m = 0.0f, f_v = 0.0f, f_d = 1.0f, f_o = 0.0f;
+    if (!VEC && i0 < n)
+    {
+        const uint32_t c = map.channel(i0);
+        f_d              = delta[c];
+        f_o              = offset[c];
+        f_w              = w[i0];
+        f_a              = alpha[i0];
+        f_g              = g[i0];
+        f_m              = exp_avg[i0];
+        f_v              = exp_avg_sq[i0];
+    }
     const int64_t step = it_next[0];
     if (blockIdx.x == 0 && threadIdx.x == 0)
         it_cur[0] = step;
@@ -857,12 +873,21 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
     }
     else
     {
-        for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+        for (uint32_t i = i0; i < n; i += gridDim.x * kBlock)
         {
-            const uint32_t c = map.channel(i);
-            const float d = delta[c], o = offset[c];
+            float d = f_d, o = f_o, wi = f_w, ai = f_a, gi = f_g, mi = f_m, vi = f_v;
+            if (i != i0)
+            {
+                const uint32_t c = map.channel(i);
+                d                = delta[c];
+                o                = offset[c];
+                wi               = w[i];
+                ai               = alpha[i];
+                gi               = g[i];
+                mi               = exp_avg[i];
+                vi               = exp_avg_sq[i];
+            }
             const float rcp = __builtin_amdgcn_rcpf(d);
-            float gi        = g[i];
             for (uint32_t s = 1; s < nparts; s += 16)   // slice order; up to 16 loads in flight
             {
                 float t[16];
@@ -874,11 +899,13 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                     if (s + u < nparts)
                         gi += t[u];
             }
-            const float ga  = ada_bwd(w[i], alpha[i], gi, d, o, p, rcp, loss, i);
-            const float an  = adam_elem(alpha[i], ga, exp_avg[i], exp_avg_sq[i], adam, bc1, bc2s);
+            const float ga  = ada_bwd(wi, ai, gi, d, o, p, rcp, loss, i);
+            const float an  = adam_elem(ai, ga, mi, vi, adam, bc1, bc2s);
             alpha[i]        = an;
+            exp_avg[i]      = mi;
+            exp_avg_sq[i]   = vi;
             if (wq_next)
-                wq_next[i] = ada_fwd(w[i], an, d, o, p, rcp);
+                wq_next[i] = ada_fwd(wi, an, d, o, p, rcp);
         }
     }
     if (p.reg != 0.0f && round_loss)
