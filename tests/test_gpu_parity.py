@@ -1267,6 +1267,43 @@ def test_learned_grid_16bit_io_equals_upcast_chain(dtype, n, sym, specials):
     assert bool(torch.isfinite(gmin_a).all()) == all(abs(v) < float("inf") for v in specials)
 
 
+_LG_FOLD_CHILD = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[1])
+from aimet_amd.learned_grid import LearnedGridQuantizeDequantize as LG
+dev = torch.device("cuda", 0)
+out = []
+for n, dtype in ((13_690_000, torch.bfloat16), (2_100_000, torch.float16), (1_000_003, torch.float32)):
+    g = torch.Generator(device=dev).manual_seed(n)
+    x = (torch.randn(n, device=dev, generator=g) * 3).to(dtype).requires_grad_(True)
+    gy = torch.randn(n, device=dev, generator=g).to(dtype)
+    emin = torch.tensor([-2.5], device=dev, requires_grad=True)
+    emax = torch.tensor([3.25], device=dev, requires_grad=True)
+    LG.apply(x, emin, emax, 16 if dtype != torch.float32 else 8, False, False, False, 0).backward(gy)
+    out += [emin.grad.view(torch.int32).item(), emax.grad.view(torch.int32).item()]
+print(" ".join(str(v) for v in out))
+"""
+
+
+def test_learned_grid_fold_in_kernel_equals_fold_launch():
+    """The per-tensor backward's fold in the kernel's last workgroup (AIMET_LG_FOLD_IN_KERNEL=1)
+    and as its own launch (the default) give the same encoding gradients bit for bit (one fold
+    order, fold_partials), fp32 and 16-bit, on Llama-3-8B call sizes. Each form in a child process
+    (the switch is read once per process)."""
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    res = []
+    for flag in ("0", "1"):
+        env = dict(os.environ, AIMET_LG_FOLD_IN_KERNEL=flag)
+        r = subprocess.run([sys.executable, "-c", _LG_FOLD_CHILD, repo], env=env, capture_output=True, text=True,
+                           timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        res.append(r.stdout.strip().splitlines()[-1])
+    assert res[0] == res[1], res
+
+
 @pytest.mark.parametrize("N,C,H,K,stride,pad,dil", [(32, 32, 112, 3, 1, 1, 1), (32, 96, 112, 3, 2, 1, 1),
                                                     (5, 7, 13, 3, 2, 0, 1), (4, 16, 19, 5, 1, 2, 1),
                                                     (3, 12, 17, 3, 1, 2, 2), (32, 960, 7, 3, 1, 1, 1)])
