@@ -563,8 +563,8 @@ __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __r
 // backward: grid-stride over tiles of kBlock x U quads (U quads in flight per lane, 3 x 16-B loads
 // each; bounded grid: one round-loss atomic per workgroup); the loop bounds are uniform over the
 // workgroup (ada_round_pows synchronises it)
-template <int U, bool WL>
-__global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
+template <int U, bool WL, int MINW = 1>
+__global__ __launch_bounds__(kBlock, MINW) void adaround_bwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
                                                                   const f4* __restrict__ g, f4* __restrict__ ga,
                                                                   uint32_t nq, AdaChannel map,
                                                                   const float* __restrict__ delta,
@@ -1164,7 +1164,14 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
                     reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss, reg_beta, lf.part, lf.ticket);
             };
             const bool wl = p.want_loss != 0;
-            if (U == 1)
+            // AIMET_ADA_BWD_OCC=8: the one-quad form compiled for 8 waves per SIMD (64 VGPRs; tuning)
+            static const bool occ8 = [] {
+                const char* e = getenv("AIMET_ADA_BWD_OCC");
+                return e && atoi(e) == 8;
+            }();
+            if (U == 1 && occ8)
+                wl ? launch(adaround_bwd_vec_kernel<1, true, 8>) : launch(adaround_bwd_vec_kernel<1, false, 8>);
+            else if (U == 1)
                 wl ? launch(adaround_bwd_vec_kernel<1, true>) : launch(adaround_bwd_vec_kernel<1, false>);
             else if (U == 4)
                 wl ? launch(adaround_bwd_vec_kernel<4, true>) : launch(adaround_bwd_vec_kernel<4, false>);
