@@ -285,6 +285,16 @@ __global__ __launch_bounds__(kBlock) void dw_step_kernel(DwStep a, float* __rest
     const uint32_t np = s.N * s.OH * s.OW;
     const uint32_t p0 = blockIdx.x * per;
     const uint32_t p1 = p0 + per < np ? p0 + per : np;
+    // the channel's taps and bias first: they do not depend on the iteration counter, so their
+    // loads overlap its round trip and the batch-row table's
+    float wk[KK], acc[KK];
+#pragma unroll
+    for (int k = 0; k < KK; ++k)
+    {
+        wk[k]  = a.w[c * KK + k];
+        acc[k] = 0.0f;
+    }
+    const float b0    = a.bias ? a.bias[c] : 0.0f;
     const int64_t it  = a.it_cur[0];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         a.it_next[0] = it + 1;
@@ -295,14 +305,6 @@ __global__ __launch_bounds__(kBlock) void dw_step_kernel(DwStep a, float* __rest
         for (uint32_t i = threadIdx.x; i < s.N; i += kBlock)
             srows[i] = rows[i];
     __syncthreads();
-    float wk[KK], acc[KK];
-#pragma unroll
-    for (int k = 0; k < KK; ++k)
-    {
-        wk[k]  = a.w[c * KK + k];
-        acc[k] = 0.0f;
-    }
-    const float b0 = a.bias ? a.bias[c] : 0.0f;
     for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += kBlock * U)
     {
         float xv[U][KK], tv[U];
@@ -412,6 +414,15 @@ __global__ __launch_bounds__(kBlock) void dw_step_quad_kernel(DwStep a, float* _
     const uint32_t np = s.N * s.OH * s.OW;
     const uint32_t p0 = blockIdx.x * per;
     const uint32_t p1 = p0 + per < np ? p0 + per : np;
+    // the taps and bias ahead of the iteration counter (see dw_step_kernel)
+    float wk[9], acc[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+    {
+        wk[k]  = a.w[c * 9 + k];
+        acc[k] = 0.0f;
+    }
+    const float b0    = a.bias ? a.bias[c] : 0.0f;
     const int64_t it  = a.it_cur[0];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
         a.it_next[0] = it + 1;
@@ -422,14 +433,6 @@ __global__ __launch_bounds__(kBlock) void dw_step_quad_kernel(DwStep a, float* _
         for (uint32_t i = threadIdx.x; i < s.N; i += kBlock)
             srows[i] = rows[i];
     __syncthreads();
-    float wk[9], acc[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k)
-    {
-        wk[k]  = a.w[c * 9 + k];
-        acc[k] = 0.0f;
-    }
-    const float b0 = a.bias ? a.bias[c] : 0.0f;
     const uint32_t q1 = p1 / 4;
     for (uint32_t qbb = p0 / 4 + threadIdx.x; qbb < q1; qbb += kBlock * U)
     {

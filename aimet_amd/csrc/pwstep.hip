@@ -99,15 +99,16 @@ __global__ __launch_bounds__(kBlock, 2) void pw_step_kernel(PwStep a, float* __r
     const uint32_t r0 = blockIdx.y * a.R;
     const uint32_t Cin = a.Cin, Cout = a.Cout - r0 < a.R ? a.Cout - r0 : a.R, pairs = Cin * a.Cout;
     const uint32_t Cin4 = (Cin + 3) / 4, Cout4 = (Cout + 3) / 4, wrow = 4 * Cin4;
-    const int64_t it = a.it_cur[0];
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        a.it_next[0] = it + 1;
-    const int64_t* rows = a.idx_all + it * (int64_t) a.N;
+    // W first: it does not depend on the iteration counter, so its loads overlap that round trip
     for (uint32_t e = threadIdx.x; e < Cout * wrow; e += kBlock)
     {
         const uint32_t co = e / wrow, ci = e - co * wrow;
         Ws[e] = ci < Cin ? a.w[(r0 + co) * Cin + ci] : 0.0f;
     }
+    const int64_t it = a.it_cur[0];
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        a.it_next[0] = it + 1;
+    const int64_t* rows = a.idx_all + it * (int64_t) a.N;
     for (uint32_t e = threadIdx.x; e < kPwT * (wrow - Cin); e += kBlock)
         XT[(e / (wrow - Cin)) * kPwRow + Cin + e % (wrow - Cin)] = 0.0f;
     for (uint32_t e = threadIdx.x; e < kPwT * (4 * Cout4 - Cout); e += kBlock)
@@ -275,12 +276,9 @@ __global__ __launch_bounds__(kBlock, 2) void pw_mfma_step_kernel(PwStep a, PmSha
     float* Gs = Xs + m.Kx * kPmLd;           // [Cp][33]
     const uint32_t r0 = blockIdx.y * a.R;
     const uint32_t Cin = a.Cin, Cout = a.Cout - r0 < a.R ? a.Cout - r0 : a.R, pairs = Cin * a.Cout;
-    const int64_t it = a.it_cur[0];
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
-        a.it_next[0] = it + 1;
-    const int64_t* rows = a.idx_all + it * (int64_t) a.N;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, i = lane & 31, h = lane >> 5;
-    // W (zero past Cin / the range's rows) and the X rows past Cin (zero, never rewritten)
+    // W (zero past Cin / the range's rows) and the X rows past Cin (zero, never rewritten), ahead
+    // of the iteration counter (independent of it)
     for (uint32_t e = threadIdx.x; e < m.Cp * m.Kw; e += kBlock)
     {
         const uint32_t co = e / m.Kw, ci = e - co * m.Kw;
@@ -288,6 +286,10 @@ __global__ __launch_bounds__(kBlock, 2) void pw_mfma_step_kernel(PwStep a, PmSha
     }
     for (uint32_t e = Cin * kPmLd + threadIdx.x; e < m.Kx * kPmLd; e += kBlock)
         Xs[e] = 0.0f;
+    const int64_t it = a.it_cur[0];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+        a.it_next[0] = it + 1;
+    const int64_t* rows = a.idx_all + it * (int64_t) a.N;
     // this tile's X (XB per lane: element q = threadIdx.x + kBlock j -> ci = q / 32, p = q % 32)
     // and this wave's targets (its GEMM1 blocks w, w + 4, ...: 16 per block)
     float xr[XB], tr[TB][16];
