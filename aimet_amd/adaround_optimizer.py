@@ -120,6 +120,9 @@ _FUSE_SOFT_WEIGHT = os.environ.get("AIMET_ADA_FUSE_WQ", "1") == "1"
 # (aimet_adaround_dw_step, bit-identical to gather + forward + reconstruction gradient + weight
 # gradient); AIMET_ADA_DW_FUSED=0 runs those four launches instead (tests, measurements)
 _DW_FUSED = os.environ.get("AIMET_ADA_DW_FUSED", "1") == "1"
+# the depthwise step's per-channel weight-gradient slices folded by the Adam step
+# (aimet_adaround_backward_adam_parts with part_kk = K K: dw_wgrad_fold's sum, one launch fewer)
+_DW_FOLD_ADAM = os.environ.get("AIMET_ADA_DW_FOLD_ADAM", "1") == "1"
 # 1x1 layers / the unfolded stem with few input channels (Cin <= 192, HW % 4 == 0)
 # can run the iteration up to dL/dWq as one pass too (aimet_adaround_pw_step: q, g and the gradient
 # partials on chip; sums in a fixed order, not a library GEMM's). "auto" (default) takes it for every
@@ -606,6 +609,7 @@ class AdaroundOptimizer:
             mode = "linear"
         q_buf = torch.empty((nb,) + out_shape, dtype=torch.float32, device=dev)
         g_buf = torch.empty_like(q_buf)
+        dw_slices = 0
         if mode == "dw":
             # depthwise layers: native forward + weight gradient, no autograd (aimet_dwconv2d_*)
             K, stride, pad, dil = depthwise_spec(module)
@@ -616,6 +620,11 @@ class AdaroundOptimizer:
                                                                    ctypes.byref(ws_n)))
             ws = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
             dims = (Nb, C, H, W, out_shape[1], out_shape[2], K, stride, pad, dil)
+            if _DW_FOLD_ADAM and _DW_FUSED and sq.shape[0] * sq.shape[1] * sq.shape[2] == C * K * K:
+                sl = ctypes.c_int64()
+                _native.check(lib.aimet_adaround_dw_step_slices(P(out_data), Nb, C, out_shape[1], out_shape[2], K,
+                                                                stride, dil, ctypes.byref(sl)))
+                dw_slices = sl.value
         pbias = P(bias) if bias is not None else None
         pw_dims, cm, gw_parts = None, None, None
         if mode in ("pointwise", "im2col") and _PW_FUSED != "0" and _LOOP_FORM != "autograd":
@@ -654,7 +663,7 @@ class AdaroundOptimizer:
         def adam_step(gw, s):
             # the Adam step also writes the next iteration's soft-quantized weight into wq (it reads
             # W and the new alpha anyway): no separate forward launch per iteration
-            _native.check(lib.aimet_adaround_backward_adam_parts(sq.pw, sq.pa, P(gw), 1, P(exp_avg), P(exp_avg_sq),
+            _native.check(lib.aimet_adaround_backward_adam_parts(sq.pw, sq.pa, P(gw), 1, 0, P(exp_avg), P(exp_avg_sq),
                                                                  *sq.shape, sq.pd, sq.po, sq.bw, P(rb_all), it_next,
                                                                  it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None,
                                                                  P(bias_corr), s))
@@ -669,6 +678,15 @@ class AdaroundOptimizer:
                 soft_weight()
             if mode == "dw" and _DW_FUSED:
                 # the batch read in place from the caches, q and g never stored; it_next moves here
+                if dw_slices:
+                    # the per-channel slices folded by the Adam step (one launch fewer; the same sum)
+                    _native.check(lib.aimet_adaround_dw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
+                                                             P(wq), pbias, None, P(ws), *dims, code, s))
+                    _native.check(lib.aimet_adaround_backward_adam_parts(
+                        sq.pw, sq.pa, P(ws), dw_slices, dims[6] * dims[6], P(exp_avg), P(exp_avg_sq), *sq.shape,
+                        sq.pd, sq.po, sq.bw, P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None,
+                        P(bias_corr), s))
+                    return
                 _native.check(lib.aimet_adaround_dw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
                                                          P(wq), pbias, P(gw_dw), P(ws), *dims, code, s))
                 adam_step(gw_dw, s)
@@ -688,7 +706,7 @@ class AdaroundOptimizer:
                 _native.check(lib.aimet_adaround_pw_cm_wgrad(P(inp_data), P(idx_all), it_cur, P(g_cm), P(parts),
                                                              parts.shape[0], nb, cin_cm, C_out, hw, s))
                 _native.check(lib.aimet_adaround_backward_adam_parts(
-                    sq.pw, sq.pa, P(parts), parts.shape[0], P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po,
+                    sq.pw, sq.pa, P(parts), parts.shape[0], 0, P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po,
                     sq.bw, P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, P(bias_corr), s))
                 return
             if mode in ("pointwise", "im2col") and cm is not None:
@@ -707,7 +725,7 @@ class AdaroundOptimizer:
                 torch.bmm(g_cm.view(C_out, S, L).transpose(0, 1), x_cm.view(cin_cm, S, L).permute(1, 2, 0),
                           out=gw_parts.view(S, C_out, cin_cm))
                 _native.check(lib.aimet_adaround_backward_adam_parts(
-                    sq.pw, sq.pa, P(gw_parts), S, P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po, sq.bw,
+                    sq.pw, sq.pa, P(gw_parts), S, 0, P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po, sq.bw,
                     P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, P(bias_corr), s))
                 return
             _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp),

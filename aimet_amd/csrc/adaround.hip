@@ -763,13 +763,26 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                                                                    float* __restrict__ wq_next,
                                                                    float* __restrict__ loss_part,
                                                                    unsigned* __restrict__ ticket, uint32_t nparts,
-                                                                   const float* __restrict__ bias_corr)
+                                                                   const float* __restrict__ bias_corr,
+                                                                   uint32_t part_kk)
 {
     p.want_loss = WL;   // constant: see adaround_bwd_vec_kernel
     // the one-element-per-lane form's first element: its operands are loaded before the step's
     // table entries, which they do not depend on, so the two round trips overlap (a small layer's
     // step is a chain of latencies: the counter, the table entries, the operands, the arithmetic)
     const uint32_t i0 = blockIdx.x * kBlock + threadIdx.x;
+    // slice s of element i's gradient: [nparts][n] (slice-major), or [n / part_kk][nparts][part_kk]
+    // (the depthwise step's per-channel slices; the first slice added to +0 as dw_wgrad_fold does,
+    // so the sum is that fold's bit for bit)
+    auto gpart = [&](uint32_t i, uint32_t sl) -> float {
+        if (part_kk)
+        {
+            const uint32_t ch = i / part_kk, k = i - ch * part_kk;
+            const float v     = g[((size_t) ch * nparts + sl) * part_kk + k];
+            return sl == 0 ? 0.0f + v : v;
+        }
+        return g[(size_t) sl * n + i];
+    };
     float f_w = 0.0f, f_a = 0.0f, f_g = 0.0f, f_m = 0.0f, f_v = 0.0f, f_d = 1.0f, f_o = 0.0f;
     if (!VEC && i0 < n)
     {
@@ -778,7 +791,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
         f_o              = offset[c];
         f_w              = w[i0];
         f_a              = alpha[i0];
-        f_g              = g[i0];
+        f_g              = gpart(i0, 0);
         f_m              = exp_avg[i0];
         f_v              = exp_avg_sq[i0];
     }
@@ -883,7 +896,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                 o                = offset[c];
                 wi               = w[i];
                 ai               = alpha[i];
-                gi               = g[i];
+                gi               = gpart(i, 0);
                 mi               = exp_avg[i];
                 vi               = exp_avg_sq[i];
             }
@@ -893,7 +906,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                 float t[16];
 #pragma unroll
                 for (int u = 0; u < 16; ++u)
-                    t[u] = g[(size_t) (s + u < nparts ? s + u : s) * n + i];
+                    t[u] = gpart(i, s + u < nparts ? s + u : s);
 #pragma unroll
                 for (int u = 0; u < 16; ++u)
                     if (s + u < nparts)
@@ -1371,7 +1384,7 @@ int aimet_adaround_recon_grad_indexed_cm(const float* q, const float* out_data, 
 }
 
 int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float* grad_parts, int64_t nparts,
-                                       float* exp_avg, float* exp_avg_sq, int64_t outer, int64_t C, int64_t K,
+                                       int64_t part_kk, float* exp_avg, float* exp_avg_sq, int64_t outer, int64_t C, int64_t K,
                                        const float* delta, const float* offset, int32_t bw, const float* reg_beta_all,
                                        const int64_t* it_next, int64_t* it_cur, double lr, double beta1, double beta2,
                                        double eps, float* round_loss, float* wq_next, const float* bias_corr,
@@ -1389,6 +1402,8 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
         require_device_ptr(alpha, "alpha");
         require_device_ptr(grad_parts, "grad");
         AIMET_REQUIRE(nparts >= 1 && nparts <= 65535, "nparts out of range");
+        AIMET_REQUIRE(part_kk >= 0 && part_kk <= 4096 && (part_kk == 0 || (outer * C * K) % part_kk == 0),
+                      "part_kk must be 0 or divide the weight's element count");
         const float* grad_wq = grad_parts;
         require_device_ptr(exp_avg, "exp_avg");
         require_device_ptr(exp_avg_sq, "exp_avg_sq");
@@ -1403,7 +1418,7 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
         // 4 elements per lane only for weights large enough to fill the chip that way: the per-element
         // chain (sigmoid, Sleef pow, Adam) is long, and a small layer's step is latency-bound, so
         // it takes one element per lane (4x the lanes; the same arithmetic per element)
-        const bool vec = n >= (int64_t(1) << 18) && (C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) &&
+        const bool vec = part_kk == 0 && n >= (int64_t(1) << 18) && (C == 1 || K % 4 == 0) && n % 4 == 0 && aligned16(w) && aligned16(alpha) &&
                          aligned16(grad_wq) && aligned16(exp_avg) && aligned16(exp_avg_sq) &&
                          (wq_next == nullptr || aligned16(wq_next));
         const int64_t items = vec ? n / 4 : n;
@@ -1414,7 +1429,8 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
         auto launch = [&](auto kernel) {
             kernel<<<(unsigned) blocks, kBlock, 0, st>>>(w, alpha, grad_wq, exp_avg, exp_avg_sq, (uint32_t) n, map, delta,
                                                          offset, p, reg_beta_all, it_next, it_cur, a, round_loss,
-                                                         wq_next, lf.part, lf.ticket, (uint32_t) nparts, bias_corr);
+                                                         wq_next, lf.part, lf.ticket, (uint32_t) nparts, bias_corr,
+                                                         (uint32_t) part_kk);
         };
         const bool wl = round_loss != nullptr;
         if (vec)
@@ -1431,7 +1447,7 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
                                  double lr, double beta1, double beta2, double eps, float* round_loss, float* wq_next,
                                  void* stream)
 {
-    return aimet_adaround_backward_adam_parts(w, alpha, grad_wq, 1, exp_avg, exp_avg_sq, outer, C, K, delta, offset, bw,
+    return aimet_adaround_backward_adam_parts(w, alpha, grad_wq, 1, 0, exp_avg, exp_avg_sq, outer, C, K, delta, offset, bw,
                                               reg_beta_all, it_next, it_cur, lr, beta1, beta2, eps, round_loss, wq_next,
                                               nullptr, stream);
 }

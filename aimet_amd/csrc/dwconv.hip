@@ -635,7 +635,9 @@ void dw_step(const float* x_cache, const float* t_cache, const int64_t* idx_all,
     require_device_ptr(it_cur, "it_cur");
     require_device_ptr(it_next, "it_next");
     require_device_ptr(w, "weight");
-    require_device_ptr(grad_w, "grad_w");
+    AIMET_REQUIRE(grad_w || workspace, "grad_w may be null only with a workspace (the slices stay there)");
+    if (grad_w)
+        require_device_ptr(grad_w, "grad_w");
     if (bias)
         require_device_ptr(bias, "bias");
     uint32_t per     = 0;
@@ -669,9 +671,12 @@ void dw_step(const float* x_cache, const float* t_cache, const int64_t* idx_all,
     else
         dw_step_kernel<5><<<grid, kBlock, 0, st>>>(a, partial, s, per);
     AIMET_LAUNCH_CHECK();
-    dw_wgrad_fold<<<(unsigned) ceil_div(C * K * K, kBlock), kBlock, 0, st>>>(partial, grad_w, (uint32_t) C,
-                                                                            (uint32_t) S, (uint32_t) (K * K));
-    AIMET_LAUNCH_CHECK();
+    if (grad_w)   // else the Adam step folds the [C][S][K K] slices (aimet_adaround_backward_adam_parts)
+    {
+        dw_wgrad_fold<<<(unsigned) ceil_div(C * K * K, kBlock), kBlock, 0, st>>>(partial, grad_w, (uint32_t) C,
+                                                                                (uint32_t) S, (uint32_t) (K * K));
+        AIMET_LAUNCH_CHECK();
+    }
     if (!workspace)
         scratch_free(partial, st);
 }
@@ -716,6 +721,18 @@ int aimet_adaround_dw_step(const float* x_cache, const float* target_cache, cons
     return guarded([&] {
         dw_step(x_cache, target_cache, idx_all, it_cur, it_next, w, bias, grad_w, workspace, N, C, H, W, OH, OW, K,
                 stride, pad, dilation, act, as_stream(stream));
+    });
+}
+
+int aimet_adaround_dw_step_slices(const float* target_cache, int64_t N, int64_t C, int64_t OH, int64_t OW, int32_t K,
+                                  int32_t stride, int32_t dilation, int64_t* slices)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(slices != nullptr, "slices is null");
+        AIMET_REQUIRE(N > 0 && C > 0 && OH > 0 && OW > 0 && (K == 3 || K == 5), "invalid depthwise shape");
+        const bool quads = dw_quads(K, stride, dilation, OW) && aligned16(target_cache);
+        uint32_t per     = 0;
+        *slices          = wgrad_slices(N, C, OH, OW, &per, quads);
     });
 }
 

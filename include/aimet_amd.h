@@ -469,14 +469,16 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
                                  const int64_t* it_next_dev, int64_t* it_cur_dev, double lr, double beta1,
                                  double beta2, double eps, float* round_loss_dev, float* wq_next_dev, void* stream);
 
-/* aimet_adaround_backward_adam with the weight gradient given as `nparts` slices grad_parts[s][n]
- * (n = outer * C * K) that are added in slice order (s = 0, 1, ...) element by element: the sliced
- * weight gradient of aimet_adaround_pw_cm_wgrad. bias_corr_dev (nullable): the table of
+/* aimet_adaround_backward_adam with the weight gradient given as `nparts` slices added in slice
+ * order (s = 0, 1, ...) element by element: part_kk == 0: grad_parts[s][n] (n = outer * C * K; the
+ * sliced weight gradient of aimet_adaround_pw_cm_wgrad); part_kk > 0: grad_parts[n / part_kk][s]
+ * [part_kk] from +0 (the depthwise step's per-channel slices, aimet_adaround_dw_step with grad_w
+ * NULL: the sum is its fold's, bit for bit). bias_corr_dev (nullable): the table of
  * aimet_adaround_adam_bias_corrections for beta1 / beta2, read at step instead of computing the
  * bias corrections in the kernel (same bits). nparts == 1 and bias_corr_dev == NULL is
  * aimet_adaround_backward_adam. */
 int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float* grad_parts, int64_t nparts,
-                                       float* exp_avg_dev, float* exp_avg_sq_dev, int64_t outer, int64_t C, int64_t K,
+                                       int64_t part_kk, float* exp_avg_dev, float* exp_avg_sq_dev, int64_t outer, int64_t C, int64_t K,
                                        const float* delta_dev, const float* offset_dev, int32_t bw,
                                        const float* reg_beta_all_dev, const int64_t* it_next_dev, int64_t* it_cur_dev,
                                        double lr, double beta1, double beta2, double eps, float* round_loss_dev,
@@ -534,6 +536,10 @@ int aimet_adaround_dw_step(const float* x_cache, const float* target_cache, cons
                            float* grad_w, float* workspace, int64_t N, int64_t C, int64_t H, int64_t W, int64_t OH,
                            int64_t OW, int32_t K, int32_t stride, int32_t pad, int32_t dilation, int32_t act,
                            void* stream);
+/* the slice count S of aimet_adaround_dw_step's [C][S][K K] weight-gradient partials (its
+ * workspace, left unfolded when grad_w is NULL) for the same shape and target cache */
+int aimet_adaround_dw_step_slices(const float* target_cache, int64_t N, int64_t C, int64_t OH, int64_t OW, int32_t K,
+                                  int32_t stride, int32_t dilation, int64_t* slices);
 
 /* The AdaRound iteration of a 1x1 convolution (or the unfolded stem) with few channels up to
  * dL/dWq in one pass: sample n of the batch is row idx_all_dev[it * N + n] (it = it_cur_dev[0])

@@ -1523,8 +1523,8 @@ def test_adaround_pw_cm_mfma_vs_torch(N, Cin, Cout, HW, act, with_bias):
     bc = torch.empty(2, device=DEV)
     _native.call("aimet_adaround_adam_bias_corrections", ctypes.c_double(0.9), ctypes.c_double(0.999), 1,
                  bc.data_ptr(), s)
-    for fn, grad, extra, tab in (("aimet_adaround_backward_adam_parts", parts, (S,), (None,)),
-                                 ("aimet_adaround_backward_adam_parts", parts, (S,), (bc.data_ptr(),)),
+    for fn, grad, extra, tab in (("aimet_adaround_backward_adam_parts", parts, (S, 0), (None,)),
+                                 ("aimet_adaround_backward_adam_parts", parts, (S, 0), (bc.data_ptr(),)),
                                  ("aimet_adaround_backward_adam", gsum, (), ())):
         alpha = torch.randn(C, K, device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
         m, v = torch.zeros_like(alpha), torch.zeros_like(alpha)
@@ -1574,7 +1574,7 @@ def test_adam_bias_correction_table_equals_in_kernel():
             v = torch.full_like(alpha, 1e-7)
             wq = torch.empty_like(alpha)
             ctr = torch.tensor([step - 1, step], dtype=torch.long, device=DEV)
-            _native.call("aimet_adaround_backward_adam_parts", w.data_ptr(), alpha.data_ptr(), grad.data_ptr(), 1,
+            _native.call("aimet_adaround_backward_adam_parts", w.data_ptr(), alpha.data_ptr(), grad.data_ptr(), 1, 0,
                          m.data_ptr(), v.data_ptr(), 1, C, K, d.data_ptr(), o.data_ptr(), 4, rb.data_ptr(),
                          ctr.data_ptr() + 8, ctr.data_ptr(), ctypes.c_double(1e-3), ctypes.c_double(b1),
                          ctypes.c_double(b2), ctypes.c_double(1e-8), None, wq.data_ptr(), tab, s)

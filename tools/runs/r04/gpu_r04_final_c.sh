@@ -8,3 +8,4 @@ python tools/studies/ada_trace_summary.py $OUT/ada_trace $((53*200)) > $OUT/ada_
 rm -rf $OUT/ada_trace
 run llama 600 python -u benchmarks/llama_qat.py --steps 5 --warmup 2
 run vit 600 python -u benchmarks/vit_calibration.py --images 160
+AIMET_ADA_BWD_OCC=8 run ada_tune_occ8 300 python -u tools/studies/ada_bwd_tune.py

@@ -66,7 +66,7 @@ def main():
                                                                    P(g_cm), nb, cin, cout, hw, 2, s))
                     _native.check(lib.aimet_adaround_pw_cm_wgrad(P(x), P(idx), it_cur, P(g_cm), P(parts), sl.value, nb,
                                                                  cin, cout, hw, s))
-                    _native.check(lib.aimet_adaround_backward_adam_parts(P(w), P(alpha), P(parts), sl.value, P(m), P(v),
+                    _native.check(lib.aimet_adaround_backward_adam_parts(P(w), P(alpha), P(parts), sl.value, 0, P(m), P(v),
                                                                          1, cout, cin, P(d), P(o), 8, P(rb), it_next,
                                                                          it_cur, *adam, None, P(wq), None, s))
             else:
