@@ -181,6 +181,7 @@ _PROTOTYPES = {
                                      ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double, _vp, _vp,
                                      _vp],
     "aimet_adaround_dw_step_slices": [_vp, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _vp],
+    "aimet_adaround_pw_step_slices": [_i64, _i64, _i64, _i64, _vp, _vp],
     "aimet_adaround_backward_adam_parts": [_vp, _vp, _vp, _i64, _i64, _vp, _vp, _i64, _i64, _i64, _vp, _vp, _i32, _vp, _vp,
                                            _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                            _vp, _vp, _vp, _vp],

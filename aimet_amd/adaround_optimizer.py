@@ -120,8 +120,8 @@ _FUSE_SOFT_WEIGHT = os.environ.get("AIMET_ADA_FUSE_WQ", "1") == "1"
 # (aimet_adaround_dw_step, bit-identical to gather + forward + reconstruction gradient + weight
 # gradient); AIMET_ADA_DW_FUSED=0 runs those four launches instead (tests, measurements)
 _DW_FUSED = os.environ.get("AIMET_ADA_DW_FUSED", "1") == "1"
-# the depthwise step's per-channel weight-gradient slices folded by the Adam step
-# (aimet_adaround_backward_adam_parts with part_kk = K K: dw_wgrad_fold's sum, one launch fewer)
+# the depthwise / 1x1 one-pass steps' weight-gradient slices folded by the Adam step
+# (aimet_adaround_backward_adam_parts with part_kk: the folds' sums, one launch fewer per iteration)
 _DW_FOLD_ADAM = os.environ.get("AIMET_ADA_DW_FOLD_ADAM", "1") == "1"
 # 1x1 layers / the unfolded stem with few input channels (Cin <= 192, HW % 4 == 0)
 # can run the iteration up to dL/dWq as one pass too (aimet_adaround_pw_step: q, g and the gradient
@@ -626,7 +626,7 @@ class AdaroundOptimizer:
                                                                 stride, dil, ctypes.byref(sl)))
                 dw_slices = sl.value
         pbias = P(bias) if bias is not None else None
-        pw_dims, cm, gw_parts = None, None, None
+        pw_dims, cm, gw_parts, pw_slices = None, None, None, None
         if mode in ("pointwise", "im2col") and _PW_FUSED != "0" and _LOOP_FORM != "autograd":
             cin, cout, hw_in = inp_data.shape[1], C_out, inp_data[0, 0].numel()
             wanted = _PW_FUSED == "all" or (hw >= 28 * 28 and not (cin > cout and hw < 56 * 56))
@@ -637,6 +637,11 @@ class AdaroundOptimizer:
                 ws_n = ctypes.c_int64()
                 _native.check(lib.aimet_adaround_pw_step_workspace(*pw_dims, ctypes.byref(ws_n)))
                 ws_pw = torch.empty(ws_n.value, dtype=torch.float32, device=dev)
+                if _DW_FOLD_ADAM and sq.w.numel() == cin * cout:
+                    # the step's slices added by the Adam step (pw_fold_final's sum, one launch fewer)
+                    off, nsl = ctypes.c_int64(), ctypes.c_int64()
+                    _native.check(lib.aimet_adaround_pw_step_slices(*pw_dims, ctypes.byref(off), ctypes.byref(nsl)))
+                    pw_slices = (off.value, nsl.value)
         if (mode in ("pointwise", "im2col") and pw_dims is None and _PW_CM and hw <= 14 * 14
                 and inp_data[0].numel() % hw == 0):
             cin_cm = inp_data[0].numel() // hw
@@ -693,6 +698,14 @@ class AdaroundOptimizer:
                 return
             if mode in ("pointwise", "im2col") and pw_dims is not None:
                 # 1x1 / unfolded stem with few channels: one pass, the batch read in place
+                if pw_slices:
+                    _native.check(lib.aimet_adaround_pw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
+                                                             P(wq), pbias, None, P(ws_pw), *pw_dims, code, s))
+                    _native.check(lib.aimet_adaround_backward_adam_parts(
+                        sq.pw, sq.pa, ctypes.c_void_p(ws_pw.data_ptr() + 4 * pw_slices[0]), pw_slices[1],
+                        sq.w.numel(), P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po, sq.bw, P(rb_all), it_next,
+                        it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, P(bias_corr), s))
+                    return
                 _native.check(lib.aimet_adaround_pw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
                                                          P(wq), pbias, P(gw_pw), P(ws_pw), *pw_dims, code, s))
                 adam_step(gw_pw, s)

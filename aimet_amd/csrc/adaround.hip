@@ -1402,7 +1402,7 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
         require_device_ptr(alpha, "alpha");
         require_device_ptr(grad_parts, "grad");
         AIMET_REQUIRE(nparts >= 1 && nparts <= 65535, "nparts out of range");
-        AIMET_REQUIRE(part_kk >= 0 && part_kk <= 4096 && (part_kk == 0 || (outer * C * K) % part_kk == 0),
+        AIMET_REQUIRE(part_kk >= 0 && part_kk <= outer * C * K && (part_kk == 0 || (outer * C * K) % part_kk == 0),
                       "part_kk must be 0 or divide the weight's element count");
         const float* grad_wq = grad_parts;
         require_device_ptr(exp_avg, "exp_avg");

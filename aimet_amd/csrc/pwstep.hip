@@ -497,6 +497,23 @@ int aimet_adaround_pw_step_workspace(int64_t N, int64_t Cin, int64_t Cout, int64
     });
 }
 
+// where aimet_adaround_pw_step leaves its second-level slices when grad_w is NULL: workspace
+// elements [offset, offset + slices * C_in * C_out), [slices][C_out][C_in], added in slice order
+// from +0 by pw_fold_final (aimet_adaround_backward_adam_parts with part_kk = C_in * C_out: the same
+// sum)
+int aimet_adaround_pw_step_slices(int64_t N, int64_t Cin, int64_t Cout, int64_t HW, int64_t* offset, int64_t* slices)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(offset != nullptr && slices != nullptr, "null output");
+        AIMET_REQUIRE(N > 0 && Cin > 0 && Cout > 0 && HW > 0, "invalid shape");
+        const int64_t tiles  = N * ceil_div(HW, (int64_t) kPwT);
+        const uint32_t grid  = pw_grid(tiles);
+        const uint32_t chunk = (uint32_t) ceil_div((int64_t) grid, (int64_t) kPwSlices);
+        *offset              = (int64_t) grid * Cin * Cout;
+        *slices              = ceil_div((int64_t) grid, (int64_t) chunk);
+    });
+}
+
 int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, const int64_t* idx_all,
                            const int64_t* it_cur, int64_t* it_next, const float* w, const float* bias, float* grad_w,
                            float* workspace, int64_t N, int64_t Cin, int64_t Cout, int64_t HW, int32_t act,
@@ -517,7 +534,9 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
         require_device_ptr(it_cur, "it_cur");
         require_device_ptr(it_next, "it_next");
         require_device_ptr(w, "weight");
-        require_device_ptr(grad_w, "grad_w");
+        AIMET_REQUIRE(grad_w || workspace, "grad_w may be null only with a workspace (the slices stay there)");
+        if (grad_w)
+            require_device_ptr(grad_w, "grad_w");
         if (bias)
             require_device_ptr(bias, "bias");
         // the matrix-core form for C_in >= 32 where its staging fits (W, X and G in <= 64 KiB of LDS,
@@ -575,8 +594,11 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
         const unsigned gx      = (unsigned) ceil_div(pairs, (int64_t) kBlock);
         pw_fold_slices<<<dim3(gx, nslices), kBlock, 0, st>>>(part, part2, (uint32_t) pairs, grid, chunk);
         AIMET_LAUNCH_CHECK();
-        pw_fold_final<<<gx, kBlock, 0, st>>>(part2, grad_w, (uint32_t) pairs, nslices);
-        AIMET_LAUNCH_CHECK();
+        if (grad_w)   // else the Adam step adds the slices (aimet_adaround_pw_step_slices)
+        {
+            pw_fold_final<<<gx, kBlock, 0, st>>>(part2, grad_w, (uint32_t) pairs, nslices);
+            AIMET_LAUNCH_CHECK();
+        }
         if (!workspace)
             scratch_free(part, st);
     });

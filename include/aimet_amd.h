@@ -555,6 +555,10 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
                            const int64_t* it_cur_dev, int64_t* it_next_dev, const float* w, const float* bias,
                            float* grad_w, float* workspace, int64_t N, int64_t Cin, int64_t Cout, int64_t HW,
                            int32_t act, void* stream);
+/* aimet_adaround_pw_step with grad_w NULL leaves the weight gradient as ordered slices in its
+ * workspace: elements [offset, offset + slices * C_in * C_out) hold [slices][C_out][C_in], which
+ * aimet_adaround_backward_adam_parts adds with part_kk = C_in * C_out (from +0, the fold's sum) */
+int aimet_adaround_pw_step_slices(int64_t N, int64_t Cin, int64_t Cout, int64_t HW, int64_t* offset, int64_t* slices);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Blockwise (broadcast) quantization and the ONNX QcQuantizeOp                                */

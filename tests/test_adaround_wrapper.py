@@ -261,6 +261,34 @@ def test_adaround_multi_iteration_graph_equals_one_per_graph(monkeypatch, kind):
 
 @pytest.mark.gpu
 @gpu
+@pytest.mark.parametrize("cin,cout,k,hw", [(3, 32, 3, 64), (16, 96, 1, 28), (64, 192, 1, 28), (144, 24, 1, 56)])
+def test_adaround_one_pass_step_slices_folded_by_adam(monkeypatch, cin, cout, k, hw):
+    """The one-pass 1x1 / stem step leaving its weight-gradient slices for the Adam step to add
+    (aimet_adaround_pw_step_slices, part_kk = C_in C_out) gives the alpha of the separate fold
+    launch (pw_fold_final), bit for bit: VALU (C_in < 32) and matrix-core (C_in >= 32) forms."""
+    import aimet_amd.adaround_optimizer as ao
+    torch.manual_seed(8)
+    m = nn.Conv2d(cin, cout, k, stride=2 if k == 3 else 1, padding=k // 2).to(DEV)
+    inp = torch.rand(32, cin, hw, hw, device=DEV)
+    with torch.no_grad():
+        out = m(inp) + 0.02 * torch.randn_like(m(inp))
+    d = (m.weight.detach().abs().amax(dim=(1, 2, 3)) / 127).contiguous()
+    o = torch.full((cout,), -128.0, device=DEV)
+    p = ao.AdaroundHyperParameters(num_iterations=200, warm_start=0.2)
+    res = []
+    for fold in (True, False):
+        monkeypatch.setattr(ao, "_DW_FOLD_ADAM", fold)
+        loss = torch.zeros(1, device=DEV)
+        res.append((ao.AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, nn.ReLU6(),
+                                                           torch.Generator().manual_seed(6), loss).detach().clone(),
+                    loss.clone()))
+        assert ao.AdaroundOptimizer.last_loop_form in ("pointwise_fused", "im2col_fused")
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+
+
+@pytest.mark.gpu
+@gpu
 def test_adaround_pw_cm_mfma_loop_close_to_library_form(monkeypatch):
     """The channel-major 1x1 loop on the f32 matrix cores (AIMET_ADA_PW_CM_FUSED=1) is
     deterministic and gives the library-GEMM form's alpha to fp32 summation-order tolerance."""
