@@ -257,7 +257,8 @@ __device__ __forceinline__ float floor_div(float w, float d, float rcp)
 {
     const float q   = w * rcp;
     const float f   = __builtin_floorf(q);
-    const float thr = (__builtin_fabsf(q) + 1.0f) * 4.76837158203125e-7f;   // 2^-21
+    // (|q| + 1) 2^-21 in one instruction: scaling by a power of two commutes with the rounding
+    const float thr = __builtin_fmaf(__builtin_fabsf(q), 4.76837158203125e-7f, 4.76837158203125e-7f);
     if (q - f > thr && (f + 1.0f) - q > thr)
         return f;
     return __builtin_floorf(w / d);
@@ -370,7 +371,9 @@ __device__ __forceinline__ float pow01_exact(float ax, float e)
 // converging AdaRound loop are mixed with unsaturated ones in every wave). Every value is the
 // same function of |x| as pow01_log's, so the results are bit-identical to ada_bwd. The slot is
 // the wave's own, so the lanes only order their LDS accesses among themselves (wave_sync); the
-// wave's lanes must all call it. `wl` = 2 * 64 * E floats per wave.
+// wave's lanes must all call it. `wl` = 2 * 64 * E floats per wave. TAIL = false
+// when no element of the wave's tile lies in the scalar tail (every tile but the last): the tail
+// flags are then compile-time false and cost nothing per element.
 // the LDS writes of this wave's lanes visible to its other lanes (a wave's LDS operations complete
 // in order; the fences keep the compiler from moving accesses across)
 __device__ __forceinline__ void wave_sync()
@@ -380,19 +383,22 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int E>
-__device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool (&tail)[E], const bool (&use)[E],
+template <int E, bool TAIL>
+__device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool (&tail_in)[E], const bool (&use)[E],
                                                const AdaParams& p, float* __restrict__ wl, float (&pbm1)[E],
                                                float (&pb)[E])
 {
     const uint32_t lane = threadIdx.x & 63;
-    bool need[E];
+    bool need[E], tail[E];
+    uint64_t ballot[E];   // the lane masks themselves (__ballot would round-trip each flag through a VGPR)
     uint32_t total = 0;
 #pragma unroll
     for (int k = 0; k < E; ++k)
     {
-        need[k] = use[k] && !(ax[k] == 0.0f || ax[k] == 1.0f);
-        total += (uint32_t) __popcll(__ballot(need[k]));
+        tail[k]   = TAIL && tail_in[k];
+        need[k]   = use[k] && !(ax[k] == 0.0f || ax[k] == 1.0f);
+        ballot[k] = __builtin_amdgcn_ballot_w64(need[k]);
+        total += (uint32_t) __popcll(ballot[k]);
     }
     if (4 * total >= 3 * 64 * E)
     {
@@ -422,13 +428,12 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
 #pragma unroll
     for (int k = 0; k < E; ++k)
     {
-        const uint64_t ballot = __ballot(need[k]);
-        const uint32_t below  = __builtin_amdgcn_mbcnt_hi((uint32_t) (ballot >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t) ballot, 0u));
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t) (ballot[k] >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t) ballot[k], 0u));
         pos[k] = need[k] ? (int) (cnt + below) : -1;
         if (need[k])   // |x| >= 0 or NaN: the sign bit marks a tail element
             wl[cnt + below] = tail[k] ? -ax[k] : ax[k];
-        cnt += (uint32_t) __popcll(ballot);
+        cnt += (uint32_t) __popcll(ballot[k]);
     }
     wave_sync();
     float* wl1 = wl + 64 * E;
@@ -437,7 +442,7 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
     for (uint32_t j = lane; j < cnt; j += 64)
     {
         const float sv  = wl[j];
-        const bool tl   = __builtin_signbit(sv);   // a NaN keeps its sign through the negation
+        const bool tl   = TAIL && __builtin_signbit(sv);   // a NaN keeps its sign through the negation
         const float v   = __builtin_fabsf(sv);
         F2 l {0.0f, 0.0f};
         if (!tl)
@@ -563,8 +568,9 @@ __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __r
 // backward: grid-stride over tiles of kBlock x U quads (U quads in flight per lane, 3 x 16-B loads
 // each; bounded grid: one round-loss atomic per workgroup); the loop bounds are uniform over the
 // workgroup (ada_round_pows synchronises it)
-template <int U, bool WL, int MINW = 1>
-__global__ __launch_bounds__(kBlock, MINW) void adaround_bwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
+// TAIL = false: n % 32 == 0, no element lies in the reference's scalar pow tail (compile-time)
+template <int U, bool WL, bool TAIL>
+__global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
                                                                   const f4* __restrict__ g, f4* __restrict__ ga,
                                                                   uint32_t nq, AdaChannel map,
                                                                   const float* __restrict__ delta,
@@ -623,7 +629,7 @@ __global__ __launch_bounds__(kBlock, MINW) void adaround_bwd_vec_kernel(const f4
         if (p.reg != 0.0f)   // uniform: a kernel argument or the device-resident value
         {
             float pbm1[E], pb[E];
-            ada_round_pows<E>(ax, tail, p.want_loss ? valid : in_h, p, wl, pbm1, pb);
+            ada_round_pows<E, TAIL>(ax, tail, p.want_loss ? valid : in_h, p, wl, pbm1, pb);
 #pragma unroll
             for (int k = 0; k < E; ++k)
             {
@@ -748,7 +754,7 @@ __global__ __launch_bounds__(kBlock) void adam_bias_corr_kernel(double beta1, do
 // dL/dalpha (ada_bwd, with this iteration's {reg, beta, beta - 1} from reg_beta_all[it]) and the
 // Adam update of alpha in place; `step` = it_next[0] (= it + 1, written by the gather kernel of the
 // same iteration), workgroup 0 publishes it to it_cur for the next iteration's gather.
-template <bool VEC, bool WL>
+template <bool VEC, bool WL, bool TAIL = true>
 __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* __restrict__ w,
                                                                    float* __restrict__ alpha,
                                                                    const float* __restrict__ g,
@@ -858,7 +864,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             if (p.reg != 0.0f)   // uniform: this iteration's device-resident value
             {
                 float pbm1[4], pb[4];
-                ada_round_pows<4>(ax, tail, use, p, wl, pbm1, pb);
+                ada_round_pows<4, TAIL>(ax, tail, use, p, wl, pbm1, pb);
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                 {
@@ -1176,20 +1182,22 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
                     reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),
                     reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss, reg_beta, lf.part, lf.ticket);
             };
-            const bool wl = p.want_loss != 0;
-            // AIMET_ADA_BWD_OCC=8: the one-quad form compiled for 8 waves per SIMD (64 VGPRs; tuning)
-            static const bool occ8 = [] {
-                const char* e = getenv("AIMET_ADA_BWD_OCC");
-                return e && atoi(e) == 8;
-            }();
-            if (U == 1 && occ8)
-                wl ? launch(adaround_bwd_vec_kernel<1, true, 8>) : launch(adaround_bwd_vec_kernel<1, false, 8>);
-            else if (U == 1)
-                wl ? launch(adaround_bwd_vec_kernel<1, true>) : launch(adaround_bwd_vec_kernel<1, false>);
+            const bool wl = p.want_loss != 0, tl = n % 32 != 0;
+            // (a form compiled for 8 waves per SIMD spilled and measured slower:
+            // profiles/r04/ada_bwd_tune_occ8.jsonl)
+            auto go = [&](auto u) {
+                constexpr int UU = decltype(u)::value;
+                if (tl)
+                    wl ? launch(adaround_bwd_vec_kernel<UU, true, true>) : launch(adaround_bwd_vec_kernel<UU, false, true>);
+                else
+                    wl ? launch(adaround_bwd_vec_kernel<UU, true, false>) : launch(adaround_bwd_vec_kernel<UU, false, false>);
+            };
+            if (U == 1)
+                go(std::integral_constant<int, 1> {});
             else if (U == 4)
-                wl ? launch(adaround_bwd_vec_kernel<4, true>) : launch(adaround_bwd_vec_kernel<4, false>);
+                go(std::integral_constant<int, 4> {});
             else
-                wl ? launch(adaround_bwd_vec_kernel<2, true>) : launch(adaround_bwd_vec_kernel<2, false>);
+                go(std::integral_constant<int, 2> {});
             AIMET_LAUNCH_CHECK();
         }
         else
@@ -1433,7 +1441,9 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
                                                          (uint32_t) part_kk);
         };
         const bool wl = round_loss != nullptr;
-        if (vec)
+        if (vec && n % 32 == 0)   // no element in the scalar pow tail
+            wl ? launch(adaround_bwd_adam_kernel<true, true, false>) : launch(adaround_bwd_adam_kernel<true, false, false>);
+        else if (vec)
             wl ? launch(adaround_bwd_adam_kernel<true, true>) : launch(adaround_bwd_adam_kernel<true, false>);
         else
             wl ? launch(adaround_bwd_adam_kernel<false, true>) : launch(adaround_bwd_adam_kernel<false, false>);

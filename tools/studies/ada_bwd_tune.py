@@ -4,7 +4,7 @@ with the round-loss value requested (want_loss) or not (the optimisation loop's 
 JSON line per case; `checksum` (sum of the gradient's bit patterns) lets runs with different
 AIMET_ADA_BWD_U be compared bit for bit.
 
-    AIMET_ADA_BWD_U=2 python tools/studies/ada_bwd_tune.py [--elems N] [--reps R]
+    [AIMET_ADA_BWD_U=2] python tools/studies/ada_bwd_tune.py [--elems N] [--reps R]
 """
 import argparse
 import ctypes
@@ -39,7 +39,7 @@ def main():
     rloss = torch.zeros(1, device=dev)
     P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
     s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    u = os.environ.get("AIMET_ADA_BWD_U", "2")
+    u = os.environ.get("AIMET_ADA_BWD_U", "1")   # the library's default
     for scale in [float(v) for v in args.scales.split(",")]:
         alpha = torch.randn(N, device=dev, generator=torch.Generator(device=dev).manual_seed(1)) * scale
         sat = float((alpha.abs() > math.log(11.0)).float().mean())
