@@ -942,7 +942,8 @@ namespace
 // one copy; the MSE / entropy searches enqueued beside it; the other schemes read back their
 // statistics when the request is finished.
 aimet_encoding_request* encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym,
-                                         int strict, int unsign, hipStream_t st, aimet_encoding_request*& req)
+                                         int strict, int unsign, hipStream_t st, aimet_encoding_request*& req,
+                                         hipStream_t prep = nullptr)
 {
     AIMET_REQUIRE(nq >= 0 && (qs != nullptr || nq == 0), "null argument");
     for (int64_t i = 0; i < nq; ++i)
@@ -993,15 +994,17 @@ aimet_encoding_request* encodings_launch(aimet_tensor_quantizer* const* qs, int6
     {
         req->pinned = take_pinned(sizeof(aimet_tf_encoding) * (size_t) tfe_total, &req->pinned_bytes);
         launch_tfe_search_many_to(tfe.data(), req->tfe_Cs.data(), (int) tfe.size(), b, sym, strict, unsign,
-                                  static_cast<aimet_tf_encoding*>(req->pinned), st);
+                                  static_cast<aimet_tf_encoding*>(req->pinned), st, prep);
     }
     req->done = take_event();
     AIMET_HIP_CHECK(hipEventRecord(req->done, st));
     return req;
 }
 
+}   // namespace
+
 // `waiter` continues after everything enqueued on `from` so far (a pooled event, no host wait)
-void stream_join(hipStream_t waiter, hipStream_t from)
+void aimet_amd::stream_join(hipStream_t waiter, hipStream_t from)
 {
     hipEvent_t e = take_event();
     RequestPool& p = request_pool();
@@ -1019,8 +1022,6 @@ void stream_join(hipStream_t waiter, hipStream_t from)
     std::lock_guard<std::mutex> lock(p.m);
     p.events.push_back(e);   // a later record does not affect the wait already enqueued
 }
-
-}   // namespace
 
 extern "C" {
 
@@ -1104,8 +1105,11 @@ int aimet_calibrate_launch(aimet_tensor_quantizer* const* act_qs, const float* c
         }
         else
             rest();
+        // the search's job table goes up on the parameters' stream, long before the main stream
+        // reaches the search (the activation passes take ~3.5 ms): no copy between the last fold
+        // and the search on the critical path
         encodings_launch(act_qs, n_act, (uint32_t) act_settings[0], act_settings[1], act_settings[2],
-                         act_settings[3], ms, ra);
+                         act_settings[3], ms, ra, ss);
         if (n_par && ss != ms)
             stream_join(ms, ss);   // later work on the main stream sees the parameters' state too
     });

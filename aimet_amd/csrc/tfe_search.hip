@@ -329,7 +329,7 @@ void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool stri
 }
 
 void launch_tfe_search_many_to(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
-                               bool unsign, aimet_tf_encoding* pinned_dst, hipStream_t s)
+                               bool unsign, aimet_tf_encoding* pinned_dst, hipStream_t s, hipStream_t prep)
 {
     if (n == 0)
         return;
@@ -343,7 +343,10 @@ void launch_tfe_search_many_to(const TqDevice* const* ds, const int64_t* Cs, int
     auto* dout = static_cast<aimet_tf_encoding*>(scratch_alloc(sizeof(aimet_tf_encoding) * total, s));
     for (int i = 0; i < n; ++i)
         jobs[i].out = dout + jobs[i].start;
-    auto* djobs = static_cast<TfeJob*>(upload_async(jobs.data(), sizeof(TfeJob) * n, s));
+    const hipStream_t us = (prep != nullptr && prep != s) ? prep : s;
+    auto* djobs = static_cast<TfeJob*>(upload_async(jobs.data(), sizeof(TfeJob) * n, us));
+    if (us != s)
+        stream_join(s, us);   // the copy ran long before s gets here (the statistics passes)
     launch_kernel(jobs[0], djobs, n, total, bw, sym, strict, unsign, s);
     AIMET_HIP_CHECK(hipMemcpyAsync(pinned_dst, dout, sizeof(aimet_tf_encoding) * total, hipMemcpyDeviceToHost, s));
     scratch_free(djobs, s);

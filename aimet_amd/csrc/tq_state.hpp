@@ -121,9 +121,13 @@ void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool stri
 void launch_tfe_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
                             bool unsign, aimet_tf_encoding* host_out, hipStream_t s);
 // the same, asynchronous: the encodings are copied into pinned_dst (host-pinned, sum of Cs entries)
-// on s; the caller synchronises before reading it
+// on s; the caller synchronises before reading it. `prep` (optional, another stream): the job
+// table's upload runs there, so it is done before s reaches the search (s waits for prep's work
+// enqueued so far) instead of adding a copy's latency between the statistics and the search
 void launch_tfe_search_many_to(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
-                               bool unsign, aimet_tf_encoding* pinned_dst, hipStream_t s);
+                               bool unsign, aimet_tf_encoding* pinned_dst, hipStream_t s, hipStream_t prep = nullptr);
+// quantizer.cpp: `waiter` continues after everything enqueued on `from` so far (no host wait)
+void stream_join(hipStream_t waiter, hipStream_t from);
 // mse_search.hip: d.enc[c] <- MSE encoding of channel c (statistics updated)
 size_t mse_part_bytes(int64_t C);
 void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
