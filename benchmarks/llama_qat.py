@@ -65,17 +65,18 @@ class RefQuantizeDequantize(torch.autograd.Function):
     QuantSim wraps (4-bit per-channel weights AND 16-bit per-tensor outputs), torch ops in float32
     (v1/tensor_quantizer.py:896-986 over quantsim_straight_through_grad.py:191-328): the forward saves
     mask and x_quant, the backward forms grad_x and the range gradients from them. Swapped in for
-    aimet_amd.learned_grid.LearnedGridQuantizeDequantize (same apply signature)."""
+    aimet_amd.learned_grid.LearnedGridQuantizeDequantize (same apply signature; `out_dtype`, the
+    dtype autocast would cast the result to, is applied as that cast after the float32 result)."""
 
     @staticmethod
-    def forward(ctx, x, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0):
+    def forward(ctx, x, emin, emax, bw, sym=False, strict=False, unsigned=False, ch_axis=0, out_dtype=None):
         from oracle import torch_ref as T
         x32 = x.float()
         y, mask, x_quant, delta, offset, steps = T.lg_forward(x32, emin.float(), emax.float(), bw, sym, strict,
                                                               unsigned, ch_axis)
         ctx.save_for_backward(x32, mask, x_quant, delta, offset, emin, emax)
         ctx.meta = (sym, steps, ch_axis, x.dtype)
-        return y.to(x.dtype)
+        return y.to(x.dtype).to(out_dtype if out_dtype is not None else x.dtype)
 
     @staticmethod
     def backward(ctx, grad):
@@ -89,12 +90,12 @@ class RefQuantizeDequantize(torch.autograd.Function):
         if sym:
             gmax = ((x_quant + offset) * g).sum(dim=dims) - (mask * (x / delta) * g).sum(dim=dims)
             gmax = gmax / torch.div(steps, 2, rounding_mode="floor")
-            return grad_x, (-gmax).view_as(emin), gmax.view_as(emax), None, None, None, None, None
+            return grad_x, (-gmax).view_as(emin), gmax.view_as(emax), None, None, None, None, None, None
         grad_scale = (x_quant + offset - x * mask / delta) * g
         grad_offset = (delta * g) * (~mask)
         t1 = grad_scale.sum(dim=dims) / steps
         t2 = steps / (emax - emin) ** 2 * grad_offset.sum(dim=dims)
-        return grad_x, (-t1 + emax * t2).view_as(emin), (t1 - emin * t2).view_as(emax), None, None, None, None, None
+        return grad_x, (-t1 + emax * t2).view_as(emin), (t1 - emin * t2).view_as(emax), None, None, None, None, None, None
 
 
 class QatLinear(nn.Module):
@@ -126,6 +127,10 @@ def main():
     ap.add_argument("--path", choices=["quantsim", "module", "plain"], default="quantsim",
                     help="plain: the same model and step without any quantizer (the floor QAT adds to)")
     ap.add_argument("--act-bw", type=int, default=16)
+    ap.add_argument("--dump-first", default=None,
+                    help="save the first step's loss, per-parameter weight-gradient sums and the encoding "
+                         "range gradients to this path (full-size parity of --impl fused vs reference: "
+                         "tools/studies/llama_first_step_compare.py)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -196,6 +201,7 @@ def main():
     except (RuntimeError, TypeError):
         opt = torch.optim.Adam(model.parameters(), lr=1e-5)
     gen = torch.Generator(device=dev).manual_seed(1234 + rank)
+    first = [args.dump_first]
 
     def step():
         ids = torch.randint(vocab, (1, args.seq + 1), device=dev, generator=gen)
@@ -203,6 +209,16 @@ def main():
             logits = ddp(ids[:, :-1])
         loss = F.cross_entropy(logits.float().view(-1, vocab), ids[:, 1:].reshape(-1))
         loss.backward()
+        if first[0] and rank == 0:
+            # the first step's results before any update: the loss, every weight gradient's float64
+            # sum (in parameter order) and the encoding range gradients, for a run of each impl
+            named = list(model.named_parameters())
+            torch.save({"impl": args.impl, "loss": loss.detach().float().cpu(),
+                        "weight_grad_sums": torch.stack([p.grad.double().sum() for n, p in named
+                                                         if p.grad is not None and "encoding" not in n]).cpu(),
+                        "range_grads": {n: p.grad.detach().float().cpu() for n, p in named
+                                        if p.grad is not None and "encoding" in n}}, first[0])
+            first[0] = None
         opt.step()
         opt.zero_grad(set_to_none=True)
         return loss
