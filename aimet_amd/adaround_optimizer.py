@@ -129,8 +129,11 @@ _DW_FOLD_ADAM = os.environ.get("AIMET_ADA_DW_FOLD_ADAM", "1") == "1"
 # eligible layer with >= 28 x 28 positions except the projecting ones (C_in > C_out) below 56 x 56,
 # where the GEMM form measured faster (MobileNet-v2 per iteration: 0.24 -> 0.16 ms at 16 -> 96 x
 # 112^2, 0.127 -> 0.088 at 24 -> 144 x 56^2, the stem 0.172 -> 0.133; 192 -> 32 x 28^2: 0.074 vs
-# 0.092; 64 -> 384 x 14^2: 0.064 vs 0.076; profiles/r03/adaround_pw_fused_forms.txt). "all": every eligible layer, "0": none. A fixed rule
-# by shape, so results stay deterministic.
+# 0.092; 64 -> 384 x 14^2: 0.064 vs 0.076; profiles/r03/adaround_pw_fused_forms.txt). Since the step
+# runs on the matrix cores for C_in >= 32 (round 4), the projecting layers at 28 x 28 with C_in >= 32
+# take it too (144 -> 32: 0.073 -> 0.056 ms, 192 -> 32: 0.070 -> 0.067; profiles/r04/
+# adaround_pw_fused_all.txt); below 28 x 28 the channel-major GEMMs stay faster. "all": every
+# eligible layer, "0": none. A fixed rule by shape, so results stay deterministic.
 _PW_FUSED = os.environ.get("AIMET_ADA_PW_FUSED", "auto")
 # the GEMM form of 1x1 layers with channel-major batches (aimet_adaround_gather_cm: x as [C_in][nb hw],
 # so q = W x and dL/dW = g x^T are ONE GEMM each, no per-sample GEMMs, batch sum or transposes), for
@@ -629,7 +632,7 @@ class AdaroundOptimizer:
         pw_dims, cm, gw_parts, pw_slices = None, None, None, None
         if mode in ("pointwise", "im2col") and _PW_FUSED != "0" and _LOOP_FORM != "autograd":
             cin, cout, hw_in = inp_data.shape[1], C_out, inp_data[0, 0].numel()
-            wanted = _PW_FUSED == "all" or (hw >= 28 * 28 and not (cin > cout and hw < 56 * 56))
+            wanted = _PW_FUSED == "all" or (hw >= 28 * 28 and (not (cin > cout and hw < 56 * 56) or cin >= 32))
             if (wanted and cin <= 192 and hw_in == hw and hw % 4 == 0
                     and inp_data.data_ptr() % 16 == 0 and out_data.data_ptr() % 16 == 0 and wq.is_contiguous()):
                 pw_dims = (nb, cin, cout, hw)
