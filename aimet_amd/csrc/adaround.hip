@@ -1167,8 +1167,8 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
             aligned16(ga))
         {
             uint32_t nq = (uint32_t) (n / 4);
-            // quads in flight per lane (AIMET_ADA_BWD_U = 1 / 2 / 4 for tuning; 1 measured best:
-            // profiles/r04/ada_bwd_tune.jsonl)
+            // quads in flight per lane (AIMET_ADA_BWD_U = 1 / 2 / 4 for tuning; 1 measured best,
+            // 2 equal within noise: profiles/r04/ada_bwd_tune_tail_flag.jsonl)
             static const int U = [] {
                 const char* e = getenv("AIMET_ADA_BWD_U");
                 const int u   = e ? atoi(e) : 1;

@@ -403,7 +403,7 @@ struct BinnerOf<true>
 // a ds_add_u32 services together always address 32 different banks. With one [512] histogram per
 // wave, bins of ordinary activations (a few dozen bins around the bulk) put ~4 lanes on one bank
 // per group -- 73% of the kernel's LDS cycles were bank-conflict cycles on ViT-L/16's activations
-// (profiles/r03/vit_pmc_sq.txt) -- and lanes adding to one bin serialise. The columns of a bin are
+// (round 3's SQ_LDS_BANK_CONFLICT pass) -- and lanes adding to one bin serialise. The columns of a bin are
 // folded once, when the workgroup ends.
 // COLS = 16 halves the LDS (32 KiB, more workgroups per CU): lanes l and l + 16 then share a
 // column, a conflict only when their bins have the same parity.
