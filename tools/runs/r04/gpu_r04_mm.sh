@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # Round 4, session mm: the parameters' statistics and search beside the histogram pass instead of the
-# min/max pass (AIMET_CAL_PARAMS_AFTER_MINMAX=1) -- compute_encodings medians and bench lines.
+# min/max pass (AIMET_CAL_PARAMS_AFTER_MINMAX=1: a study switch in quantizer.cpp, removed after this
+# run measured it slower) -- compute_encodings medians and bench lines.
 source "$(dirname "${BASH_SOURCE[0]}")/../../gpu_lib.sh"
 run enc_default 300 python -u tools/studies/enc_split_cost.py --reps 11
 AIMET_CAL_PARAMS_AFTER_MINMAX=1 run enc_after 300 python -u tools/studies/enc_split_cost.py --reps 11
