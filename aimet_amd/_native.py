@@ -141,6 +141,12 @@ _PROTOTYPES = {
                                ctypes.POINTER(_i64), _i64, ctypes.POINTER(ctypes.c_int32),
                                ctypes.POINTER(ctypes.c_int32), _int, _vp, _vp, ctypes.POINTER(_vp),
                                ctypes.POINTER(_vp)],
+    "aimet_calib_plan_create": [ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64), _i64,
+                                ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_i64), ctypes.POINTER(_i64),
+                                ctypes.POINTER(_i64), _i64, ctypes.POINTER(ctypes.c_int32),
+                                ctypes.POINTER(ctypes.c_int32), _vp, ctypes.POINTER(_vp)],
+    "aimet_calib_plan_launch": [_vp, _int, _int, _vp, _vp, ctypes.POINTER(_vp), ctypes.POINTER(_vp)],
+    "aimet_calib_plan_destroy": [_vp],
     "aimet_tq_get_stats_histogram": [_vp, _i64, _dp, _dp, ctypes.POINTER(_int), _vp],
     "aimet_tq_get_entropy_state": [_vp, _i64, _dp, _dp, ctypes.POINTER(_int), ctypes.POINTER(_int), _vp],
     "aimet_tq_num_channels": [_vp, ctypes.POINTER(_i64)],

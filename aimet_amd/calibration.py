@@ -13,13 +13,17 @@ stack, bench.py), scheduled for the MI355X:
   encodings while the activation passes still stream;
 * activation encodings: one search launch + one synchronisation.
 """
+import ctypes
 import os
+import weakref
 from typing import List, Optional, Sequence, Tuple
 
 import torch
+import torch.distributed as dist
 
+from aimet_amd import _native
 from aimet_amd import distributed as D
-from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+from aimet_amd.tensor_quantizer import AimetTensorQuantizer, PendingEncodings, _param_specs
 
 _SIDE = {}
 # tuning knobs (tools/studies/enc_schedule_tune.py): launch order and the side stream's priority
@@ -39,6 +43,180 @@ def _side_stream(dev: torch.device) -> torch.cuda.Stream:
     if key not in _SIDE:
         _SIDE[key] = torch.cuda.Stream(torch.device("cuda", key), priority=_SIDE_PRIORITY)
     return _SIDE[key]
+
+
+class CalibrationPlan:
+    """compute_encodings of a FIXED set of quantizers over resident tensors, prepared once and run
+    many times (aimet_calib_plan_*, calib_plan.cpp): v1/quantsim.py:381-449's reset + updateStats +
+    getEncoding of every quantizer for one batch, with every job table built and uploaded at
+    creation, so ``run`` is one native call that only launches kernels.
+
+    act_quantizers[i] (per-tensor AimetTensorQuantizer) sees activations[i] (this rank's shard when
+    `group` spans several ranks); param_quantizers[j] (per-tensor or per-channel along
+    param_ch_axes[j]) sees params[j] (replicated). Tensors: float32, on one HIP device. The plan
+    reads the tensors' memory at every run, so it keeps them (and the quantizers) alive; refill
+    them in place between runs for a new batch.
+
+    Sharded (`group` of several ranks, or `force_exchange`): the activation quantizers are bound
+    to packed exchange buffers (aimet_amd.distributed.PackedExchange) and every run is the three
+    plan stages with ONE all_reduce(MAX) of the packed {-min, max} and ONE all_reduce(SUM) of the
+    packed bin and element counts between them, all on the current stream: no host
+    round trip, the element counts formed on the device."""
+
+    def __init__(self, act_quantizers, activations, param_quantizers=(), params=(), param_ch_axes=None,
+                 act_settings=(8, False, False, False), param_settings=(8, True, False, False), group=None,
+                 force_exchange=False):
+        aq, pq = list(act_quantizers), list(param_quantizers)
+        acts, params = list(activations), list(params)
+        if len(aq) != len(acts) or len(pq) != len(params):
+            raise ValueError("one tensor per quantizer")
+        if not aq and not pq:
+            raise ValueError("an empty calibration plan")
+        for q in aq + pq:
+            if type(q) is not AimetTensorQuantizer:
+                raise TypeError("a calibration plan takes AimetTensorQuantizer objects")
+        if any(q._num_channels != 1 for q in aq):
+            raise ValueError("the activation quantizers of a calibration plan are per-tensor")
+        f32 = torch.float32
+        for t in acts:
+            if not (isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == f32):
+                raise TypeError("a calibration plan takes float32 HIP tensors")
+        self.dev = (acts[0] if acts else params[0]).device
+        ch_axes = list(param_ch_axes) if param_ch_axes is not None else [0] * len(pq)
+        p_specs = _param_specs(pq, params, ch_axes)
+        self.act_quantizers, self.param_quantizers = aq, pq
+        self.act_settings = tuple(int(v) for v in act_settings)
+        self.param_settings = tuple(int(v) for v in param_settings)
+        self.group = group
+        self.world = D._world(group)
+        self.exchanging = self.world > 1 or bool(force_exchange)
+        # contiguous tensors the plan reads at every run (a non-contiguous input is copied ONCE here,
+        # so a caller refilling the original would not be seen: such inputs are refused instead)
+        for t in acts + [sp[0] for sp in p_specs]:
+            if not t.is_contiguous():
+                raise ValueError("a calibration plan reads its tensors in place: pass contiguous tensors")
+            if t.device != self.dev:
+                raise ValueError("the tensors of a calibration plan share one device")
+        self._tensors = acts + [sp[0] for sp in p_specs]
+        with torch.cuda.device(self.dev):
+            handles = AimetTensorQuantizer._ensure_many(aq + pq, self.dev)
+            self.exchange = None
+            elem = None
+            if self.exchanging and aq:
+                ex = D.PackedExchange(aq, self.dev)   # binds the activation quantizers
+                self.exchange = (ex.minmax, ex.counts)
+                elem = ex.elem_counts
+            na, np_ = len(aq), len(pq)
+            i32x4 = ctypes.c_int32 * 4
+            h = ctypes.c_void_p()
+            _native.call("aimet_calib_plan_create", (ctypes.c_void_p * max(na, 1))(*handles[:na]),
+                         (ctypes.c_void_p * max(na, 1))(*[t.data_ptr() for t in acts]),
+                         (ctypes.c_int64 * max(na, 1))(*[t.numel() for t in acts]), na,
+                         (ctypes.c_void_p * max(np_, 1))(*handles[na:]),
+                         (ctypes.c_void_p * max(np_, 1))(*[sp[0].data_ptr() for sp in p_specs]),
+                         (ctypes.c_int64 * max(np_, 1))(*[sp[1] for sp in p_specs]),
+                         (ctypes.c_int64 * max(np_, 1))(*[sp[2] for sp in p_specs]),
+                         (ctypes.c_int64 * max(np_, 1))(*[sp[3] for sp in p_specs]), np_,
+                         i32x4(*self.act_settings), i32x4(*self.param_settings),
+                         elem.data_ptr() if elem is not None else None, ctypes.byref(h))
+        self._handle = h
+        self._native_handles = [hh.value if isinstance(hh, ctypes.c_void_p) else hh for hh in handles]
+        self._ra, self._rp = ctypes.c_void_p(), ctypes.c_void_p()
+
+    def launch(self, reset=False, main_stream=None, side_stream=None):
+        """Enqueue one batch; returns (PendingEncodings of the activations, of the parameters).
+        One device: one native call (the activations on `main_stream`, default the current stream;
+        the parameters on `side_stream`, default a high-priority stream of the device). Sharded:
+        stage 1, all_reduce(MAX), stage 2, all_reduce(SUM), stage 4, each collective on the
+        current stream between the stages (the host waits for nothing)."""
+        return self._launch(reset, self.act_quantizers, self.param_quantizers, main_stream, side_stream)
+
+    def _launch(self, reset, aq, pq, main_stream=None, side_stream=None):
+        if self._handle is None:
+            raise RuntimeError("calibration plan already closed")
+        main = main_stream if main_stream is not None else torch.cuda.current_stream(self.dev)
+        side = side_stream if side_stream is not None else (_side_stream(self.dev) if pq else main)
+        ra, rp = self._ra, self._rp
+        launch = _native.load().aimet_calib_plan_launch
+        with torch.cuda.device(self.dev):
+            if not self.exchanging:
+                _native.check(launch(self._handle, 7, int(bool(reset)), main.cuda_stream, side.cuda_stream,
+                                     ctypes.byref(ra), ctypes.byref(rp)))
+            else:
+                empty = ctypes.c_void_p()
+                _native.check(launch(self._handle, 1, int(bool(reset)), main.cuda_stream, side.cuda_stream,
+                                     ctypes.byref(empty), ctypes.byref(rp)))
+                try:
+                    ex = self.exchange
+                    with torch.cuda.stream(main):
+                        if ex is not None:
+                            # {-min, max}: a single MAX reduces both ends exactly
+                            D._all_reduce(ex[0], dist.ReduceOp.MAX, self.group)
+                        _native.check(launch(self._handle, 2, 0, main.cuda_stream, side.cuda_stream,
+                                             ctypes.byref(empty), ctypes.byref(empty)))
+                        if ex is not None:
+                            # bin counts + element counts of every histogram quantizer in one SUM
+                            D._all_reduce(ex[1], dist.ReduceOp.SUM, self.group)
+                        _native.check(launch(self._handle, 4, 0, main.cuda_stream, side.cuda_stream,
+                                             ctypes.byref(ra), ctypes.byref(empty)))
+                except BaseException:
+                    if rp.value:   # the parameters' request is in flight: discard it
+                        _native.call("aimet_tq_get_encodings_finish", rp, None, None)
+                        rp.value = None
+                    raise
+        if reset:
+            for q in aq + pq:
+                q._pending_percentile = None
+        for q in aq + pq:
+            q._is_encoding_valid = True
+        a = PendingEncodings(aq, *self.act_settings, request=ctypes.c_void_p(ra.value))
+        p = PendingEncodings(pq, *self.param_settings, request=ctypes.c_void_p(rp.value))
+        ra.value = rp.value = None
+        return a, p
+
+    def run(self, reset=False):
+        """launch + both results: ([(encoding, valid)] of the activations, [(encodings, valid)] of
+        the parameters); the parameters' (ready first) are built while the activations stream."""
+        a, p = self.launch(reset)
+        p_res = p.result()
+        return a.result(), p_res
+
+    def close(self):
+        h, self._handle = getattr(self, "_handle", None), None
+        if h is not None:
+            _native.call("aimet_calib_plan_destroy", h)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # interpreter shutdown
+            pass
+
+
+# the plan of the last compute_encodings_resident call, reused while the same quantizers see the
+# same tensors. The cache holds the plan's own tables only: the tensors and quantizers are checked
+# by identity through weak references (and the tensors' addresses), so nothing is kept alive.
+_PLAN_CACHE = {}
+
+
+def _cached_plan(aq, acts, pq, params, ch_axes, act_settings, param_settings, group):
+    """The cached plan for exactly these quantizers and tensors, or a new one (which replaces it)."""
+    ts, qs = list(acts) + list(params), list(aq) + list(pq)
+    key = (tuple(map(id, qs)), len(aq), tuple(act_settings), tuple(param_settings),
+           tuple(ch_axes) if ch_axes is not None else None, id(group) if group is not None else None)
+    hit = _PLAN_CACHE.get("plan")
+    if hit is not None and hit[0] == key:
+        plan, trefs, ptrs, qrefs = hit[1:]
+        if (len(ts) == len(trefs) and all(r() is t for r, t in zip(trefs, ts))
+                and all(r() is q for r, q in zip(qrefs, qs)) and [t.data_ptr() for t in ts] == ptrs
+                and [q._handle.value if q._handle is not None else None for q in qs] == plan._native_handles):
+            return plan
+    _PLAN_CACHE.pop("plan", None)
+    plan = CalibrationPlan(aq, acts, pq, params, ch_axes, act_settings, param_settings, group=group)
+    plan._tensors = plan.act_quantizers = plan.param_quantizers = None   # see above
+    _PLAN_CACHE["plan"] = (key, plan, [weakref.ref(t) for t in ts], [t.data_ptr() for t in ts],
+                           [weakref.ref(q) for q in qs])
+    return plan
 
 
 def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], activations: Sequence[torch.Tensor],
@@ -71,6 +249,20 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
             AimetTensorQuantizer.resetEncodingStatsMany(list(act_quantizers) + list(param_quantizers))
         return [], []
     dev = (activations[0] if activations else params[0]).device
+    planned = (_SCHEDULE == "params_first"
+               and all(type(q) is AimetTensorQuantizer and q.num_channels == 1 for q in act_quantizers)
+               and all(type(q) is AimetTensorQuantizer for q in param_quantizers)
+               and all(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
+                       and t.device == dev for t in list(activations) + list(params)))
+    if planned:
+        # a calibration plan (every job table prepared once, cached for the next call on the same
+        # quantizers and tensors): one native call on one device; the three stages with the two
+        # packed collectives between them when `group` spans several ranks
+        plan = _cached_plan(act_quantizers, activations, param_quantizers, params, param_ch_axes, act_settings,
+                            param_settings, group)
+        a_pending, p_pending = plan._launch(reset, list(act_quantizers), list(param_quantizers))
+        p_res = p_pending.result()
+        return a_pending.result(), p_res
     native = (D._world(group) == 1 and _SCHEDULE == "params_first"
               and all(type(q) is AimetTensorQuantizer and q.num_channels == 1 for q in act_quantizers)
               and all(type(q) is AimetTensorQuantizer for q in param_quantizers)

@@ -10,25 +10,9 @@
 #include <vector>
 
 #include "encodings.hpp"
-#include "tq_state.hpp"
+#include "tq_internal.hpp"
 
 using namespace aimet_amd;
-
-struct aimet_tensor_quantizer
-{
-    int scheme       = AIMET_QUANTIZATION_TF;
-    int64_t C        = 1;
-    int device       = 0;
-    float percentile = 100.0f;   // PercentileEncodingAnalyzer.h:100
-    bool stats_updated = false;  // AimetTensorQuantizer::_isEncodingValid / analyzer _statsUpdated
-    bool hist        = false;    // histogram-based analyzer (TF-E, percentile, MSE, entropy)
-    StatsKind kind   = kKindTf;
-    void* arena      = nullptr;
-    size_t arena_bytes = 0;
-    // quantizers made by aimet_tq_create_many share one allocation; the last one destroyed frees it
-    struct Slab* slab = nullptr;
-    TqDevice d {};
-};
 
 struct Slab
 {
@@ -39,23 +23,6 @@ struct Slab
 
 namespace
 {
-
-struct DeviceGuard
-{
-    int prev = -1;
-    explicit DeviceGuard(int dev)
-    {
-        AIMET_HIP_CHECK(hipGetDevice(&prev));
-        if (prev != dev)
-            AIMET_HIP_CHECK(hipSetDevice(dev));
-    }
-    ~DeviceGuard()
-    {
-        int cur = -1;
-        if (hipGetDevice(&cur) == hipSuccess && cur != prev && prev >= 0)
-            (void) hipSetDevice(prev);
-    }
-};
 
 size_t align256(size_t b)
 {
@@ -255,27 +222,49 @@ void reset_many(aimet_tensor_quantizer* const* qs, int64_t nq, hipStream_t st)
     std::vector<ResetJob> resets;
     for (int64_t i = 0; i < nq; ++i)
     {
-        aimet_tensor_quantizer* q = qs[i];
-        AIMET_REQUIRE(q != nullptr, "null quantizer");
-        AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one batched reset share a device");
-        zero.push_back(ZeroJob {q->arena, (int64_t) q->arena_bytes});
-        if (q->d.minmax && !in_arena(q, q->d.minmax))
-            zero.push_back(ZeroJob {q->d.minmax, (int64_t) (sizeof(float) * 2 * q->C)});
-        if (q->d.counts && !in_arena(q, q->d.counts))
-            zero.push_back(ZeroJob {q->d.counts, (int64_t) (sizeof(unsigned long long) * kPdfSize * q->C)});
-        resets.push_back(ResetJob {q->d.acc, q->C});
+        AIMET_REQUIRE(qs[i] != nullptr, "null quantizer");
+        AIMET_REQUIRE(qs[i]->device == qs[0]->device, "quantizers of one batched reset share a device");
+        reset_ranges(qs[i], false, zero, resets);
     }
     DeviceGuard g(qs[0]->device);
     launch_zero_many(zero, st);
     launch_reset_state_many(resets, st);
     for (int64_t i = 0; i < nq; ++i)
-    {
-        qs[i]->stats_updated = false;
-        qs[i]->percentile    = 100.0f;
-    }
+        mark_reset(qs[i]);
 }
 
 }   // namespace
+
+void aimet_amd::reset_ranges(const aimet_tensor_quantizer* q, bool light, std::vector<ZeroJob>& zero,
+                             std::vector<ResetJob>& resets)
+{
+    char* a = static_cast<char*>(q->arena);
+    // layout(): the PDF, then the bin counts, then the encodings scratch, at the arena's end
+    if (light && q->kind == kKindPdf && q->d.pdf && in_arena(q, q->d.pdf))
+    {
+        char* pdf = reinterpret_cast<char*>(q->d.pdf);
+        zero.push_back(ZeroJob {a, (int64_t) (pdf - a)});
+        // a per-channel quantizer's histogram writes every bin of a binned channel (no
+        // accumulation); a per-tensor one adds into its counts, which must start at zero
+        char* keep_end = (q->C > 1 && q->d.counts && in_arena(q, q->d.counts))
+                             ? reinterpret_cast<char*>(q->d.counts) + align256(sizeof(unsigned long long) * kPdfSize * q->C)
+                             : pdf + align256(sizeof(double) * kPdfSize * q->C);
+        zero.push_back(ZeroJob {keep_end, (int64_t) (a + q->arena_bytes - keep_end)});
+    }
+    else
+        zero.push_back(ZeroJob {a, (int64_t) q->arena_bytes});
+    if (q->d.minmax && !in_arena(q, q->d.minmax))
+        zero.push_back(ZeroJob {q->d.minmax, (int64_t) (sizeof(float) * 2 * q->C)});
+    if (q->d.counts && !in_arena(q, q->d.counts))
+        zero.push_back(ZeroJob {q->d.counts, (int64_t) (sizeof(unsigned long long) * kPdfSize * q->C)});
+    resets.push_back(ResetJob {q->d.acc, q->C});
+}
+
+void aimet_amd::mark_reset(aimet_tensor_quantizer* q)
+{
+    q->stats_updated = false;
+    q->percentile    = 100.0f;
+}
 
 extern "C" {
 
@@ -488,12 +477,10 @@ int aimet_tq_update_stats(aimet_tensor_quantizer* q, const float* x, int64_t out
 
 }   // extern "C"
 
-namespace
-{
-
 // jobs of a many-quantizer call: per-tensor quantizers of one device
-std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* ns,
-                                const int64_t* counts, int64_t count, const int64_t* counts_dev = nullptr)
+std::vector<StatsJob> aimet_amd::make_jobs(aimet_tensor_quantizer* const* qs, const float* const* xs,
+                                           const int64_t* ns, const int64_t* counts, int64_t count,
+                                           const int64_t* counts_dev)
 {
     AIMET_REQUIRE(qs != nullptr && count >= 0, "null argument");
     std::vector<StatsJob> jobs((size_t) count);
@@ -512,6 +499,7 @@ std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* 
         j.count = counts ? counts[i] : j.n;
         AIMET_REQUIRE(j.count >= 0, "negative element count");
         j.count_dev = counts_dev ? counts_dev + i : nullptr;
+        j.count_out = nullptr;
         j.d     = q->d;
         j.hist  = q->hist ? 1 : 0;
         j.ent   = q->kind == kKindEntropy ? 1 : 0;
@@ -521,6 +509,25 @@ std::vector<StatsJob> make_jobs(aimet_tensor_quantizer* const* qs, const float* 
     }
     return jobs;
 }
+
+ChannelJob aimet_amd::make_channel_job(aimet_tensor_quantizer* q, const float* x, int64_t outer, int64_t C, int64_t K)
+{
+    check_shape(q, outer, C, K);
+    if (outer * K > 0)
+        require_device_ptr(x, "input");
+    ChannelJob j {};
+    j.x     = x;
+    j.outer = outer;
+    j.C     = C;
+    j.K     = K;
+    j.d     = q->d;
+    j.kind  = (int32_t) q->kind;
+    j.vec   = ((reinterpret_cast<uintptr_t>(x) & 15) == 0 && K % 4 == 0) ? 1 : 0;
+    return j;
+}
+
+namespace
+{
 
 // per-channel statistics of many quantizers (two launches): the jobs of updateStatsPerChannelMany
 void channel_stats_many(aimet_tensor_quantizer* const* qs, const float* const* xs, const int64_t* outers,
@@ -535,19 +542,9 @@ void channel_stats_many(aimet_tensor_quantizer* const* qs, const float* const* x
     for (int64_t i = 0; i < count; ++i)
     {
         aimet_tensor_quantizer* q = qs[i];
-        check_shape(q, outers[i], Cs[i], Ks[i]);
+        AIMET_REQUIRE(q != nullptr, "tensor quantizer is null");
         AIMET_REQUIRE(q->device == qs[0]->device, "quantizers of one *_many call share a device");
-        if (outers[i] * Ks[i] > 0)
-            require_device_ptr(xs[i], "input");
-        ChannelJob j {};
-        j.x     = xs[i];
-        j.outer = outers[i];
-        j.C     = Cs[i];
-        j.K     = Ks[i];
-        j.d     = q->d;
-        j.kind  = (int32_t) q->kind;
-        j.vec   = ((reinterpret_cast<uintptr_t>(xs[i]) & 15) == 0 && Ks[i] % 4 == 0) ? 1 : 0;
-        jobs.push_back(j);
+        jobs.push_back(make_channel_job(q, xs[i], outers[i], Cs[i], Ks[i]));
     }
     DeviceGuard g(qs[0]->device);
     launch_channel_stats_many(jobs, st);
@@ -663,20 +660,24 @@ int aimet_tq_mark_stats_updated(aimet_tensor_quantizer* q)
     });
 }
 
-namespace
-{
+}   // extern "C"
 
-bool device_search(const aimet_tensor_quantizer* q)
+bool aimet_amd::device_search(const aimet_tensor_quantizer* q)
 {
     return q->hist && (q->scheme == AIMET_QUANTIZATION_TF_ENHANCED || q->scheme == AIMET_QUANTIZATION_MSE);
 }
 
 // the entropy KL search runs on the device for 8-bit encodings (the only width _optimizeKL
 // searches; other widths take the histogram range as it is)
-bool entropy_device(const aimet_tensor_quantizer* q, int32_t b)
+bool aimet_amd::entropy_device(const aimet_tensor_quantizer* q, int32_t b)
 {
     return q->kind == kKindEntropy && b == 8;
 }
+
+extern "C" {
+
+namespace
+{
 
 // getEncoding, part 1: enqueue the device-side search (TF-Enhanced, MSE, entropy) on the stream.
 void launch_encoding(aimet_tensor_quantizer* q, int32_t b, int sym, int strict, int unsign, hipStream_t s)
@@ -825,21 +826,6 @@ int aimet_tq_get_encoding(aimet_tensor_quantizer* q, uint32_t bw, int sym, int s
 
 }   // extern "C"
 
-// A batched getEncoding in flight: every device search enqueued on `stream`, the TF-Enhanced
-// results on their way into a pinned block, `done` recorded after them.
-struct aimet_encoding_request
-{
-    std::vector<aimet_tensor_quantizer*> qs;
-    int32_t b  = 0;
-    int sym    = 0, strict = 0, unsign = 0;
-    int device = 0;
-    hipStream_t stream = nullptr;   // where the search and its result copy were enqueued
-    hipEvent_t done = nullptr;
-    void* pinned    = nullptr;   // TF-Enhanced encodings, concatenated
-    size_t pinned_bytes = 0;
-    std::vector<int64_t> tfe_offs, tfe_Cs;   // per TF-E quantizer: offset in `out`, channels
-};
-
 namespace
 {
 
@@ -857,7 +843,9 @@ RequestPool& request_pool()
     return *p;
 }
 
-void* take_pinned(size_t bytes, size_t* real)
+}   // namespace
+
+void* aimet_amd::take_pinned(size_t bytes, size_t* real)
 {
     RequestPool& p = request_pool();
     {
@@ -880,7 +868,7 @@ void* take_pinned(size_t bytes, size_t* real)
     return ptr;
 }
 
-hipEvent_t take_event()
+hipEvent_t aimet_amd::take_event()
 {
     RequestPool& p = request_pool();
     {
@@ -897,25 +885,36 @@ hipEvent_t take_event()
     return e;
 }
 
-void release_request(aimet_encoding_request* r)
+void aimet_amd::give_event(hipEvent_t e)
+{
+    if (e == nullptr)
+        return;
+    RequestPool& p = request_pool();
+    std::lock_guard<std::mutex> lock(p.m);
+    p.events.push_back(e);
+}
+
+void aimet_amd::release_request(aimet_encoding_request* r)
 {
     if (r == nullptr)
         return;
     RequestPool& p = request_pool();
     {
         std::lock_guard<std::mutex> lock(p.m);
-        if (r->pinned)
+        if (r->pinned && !r->pinned_borrowed)
             p.blocks.emplace_back(r->pinned, r->pinned_bytes);
         if (r->done)
             p.events.push_back(r->done);
     }
+    if (r->busy)
+        --*r->busy;   // the plan may launch again (its pinned block is idle: the request was waited for)
     delete r;
 }
 
 // release on an error path: the request's result copy may already be queued into its pinned block,
 // so the block goes back to the pool only after the stream has drained (else the next take_pinned
 // could hand it out while the copy still writes into it)
-void release_request_after_error(aimet_encoding_request* r)
+void aimet_amd::release_request_after_error(aimet_encoding_request* r)
 {
     if (r == nullptr)
         return;
@@ -925,25 +924,25 @@ void release_request_after_error(aimet_encoding_request* r)
         if (hipStreamSynchronize(r->stream) != hipSuccess)
         {
             // the stream is broken: leak the block rather than risk a live copy into a reused one
+            // (a plan's block: the plan keeps counting the request as in flight, so it never
+            // launches into that block again)
             r->pinned = nullptr;
+            r->busy   = nullptr;
             (void) hipGetLastError();
         }
     }
     release_request(r);
 }
 
-}   // namespace
-
-namespace
-{
-
 // The device half of a batched getEncoding (throws; the caller releases `req` on failure): every
 // TF-Enhanced search in ONE launch (one workgroup per channel of every quantizer), results back in
-// one copy; the MSE / entropy searches enqueued beside it; the other schemes read back their
-// statistics when the request is finished.
-aimet_encoding_request* encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw, int sym,
-                                         int strict, int unsign, hipStream_t st, aimet_encoding_request*& req,
-                                         hipStream_t prep = nullptr)
+// one copy (a plan's table: written by the search into its pinned block); the MSE / entropy
+// searches enqueued beside it; the other schemes read back their statistics when the request is
+// finished.
+aimet_encoding_request* aimet_amd::encodings_launch(aimet_tensor_quantizer* const* qs, int64_t nq, uint32_t bw,
+                                                    int sym, int strict, int unsign, hipStream_t st,
+                                                    aimet_encoding_request*& req, hipStream_t prep,
+                                                    const TfeTable* table)
 {
     AIMET_REQUIRE(nq >= 0 && (qs != nullptr || nq == 0), "null argument");
     for (int64_t i = 0; i < nq; ++i)
@@ -990,7 +989,13 @@ aimet_encoding_request* encodings_launch(aimet_tensor_quantizer* const* qs, int6
     }
     launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0, st);
     launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0, st);
-    if (tfe_total > 0)
+    if (tfe_total > 0 && table != nullptr)
+    {
+        AIMET_REQUIRE(table->total == tfe_total && table->n == (int) tfe.size(),
+                      "calibration plan: the TF-Enhanced search table does not match the quantizers");
+        launch_tfe_table(*table, b, sym != 0, strict != 0, unsign != 0, st);
+    }
+    else if (tfe_total > 0)
     {
         req->pinned = take_pinned(sizeof(aimet_tf_encoding) * (size_t) tfe_total, &req->pinned_bytes);
         launch_tfe_search_many_to(tfe.data(), req->tfe_Cs.data(), (int) tfe.size(), b, sym, strict, unsign,
@@ -1000,8 +1005,6 @@ aimet_encoding_request* encodings_launch(aimet_tensor_quantizer* const* qs, int6
     AIMET_HIP_CHECK(hipEventRecord(req->done, st));
     return req;
 }
-
-}   // namespace
 
 // `waiter` continues after everything enqueued on `from` so far (a pooled event, no host wait)
 void aimet_amd::stream_join(hipStream_t waiter, hipStream_t from)
@@ -1105,11 +1108,11 @@ int aimet_calibrate_launch(aimet_tensor_quantizer* const* act_qs, const float* c
         }
         else
             rest();
-        // the search's job table goes up on the parameters' stream, long before the main stream
-        // reaches the search (the activation passes take ~3.5 ms): no copy between the last fold
-        // and the search on the critical path
+        // the search's job table goes up on the main stream itself: on the parameters' stream it
+        // would sit behind all of their work, and the join would make the search wait for that
+        // work (a calibration plan, calib_plan.cpp, has no upload at all)
         encodings_launch(act_qs, n_act, (uint32_t) act_settings[0], act_settings[1], act_settings[2],
-                         act_settings[3], ms, ra, ss);
+                         act_settings[3], ms, ra);
         if (n_par && ss != ms)
             stream_join(ms, ss);   // later work on the main stream sees the parameters' state too
     });

@@ -785,20 +785,25 @@ __global__ __launch_bounds__(kBlock) void minmax_walk_kernel(const StatsJob* __r
 __global__ __launch_bounds__(kBlock) void combine_many_kernel(const StatsJob* __restrict__ jobs, int fold)
 {
     const StatsJob& J = jobs[blockIdx.x];
+    if (J.count_out && threadIdx.x == 0)
+        *J.count_out = J.n;   // this rank's element count, summed over ranks with the bin counts
     if (J.hist && !J.ent && !J.fresh && J.d.pdf_init[0])
         return;
     const float2* partials = reinterpret_cast<const float2*>(J.mm_part);
     float a = -INFINITY, b = -INFINITY;
-    // a 205-MB tensor leaves 12.5 K tile partials: 8 independent loads in flight per lane
+    // a 205-MB tensor leaves 12.5 K tile partials: 24 independent loads in flight per lane, so the
+    // largest quantizer's partials arrive in two rounds of latency (8 per lane took ~22 us for
+    // ResNet-50's 55 quantizers, the call's critical path between the two passes)
+    constexpr int kU  = 24;
     const uint32_t nb = J.mm_blocks;
-    for (uint32_t i0 = threadIdx.x; i0 < nb; i0 += kBlock * 8)
+    for (uint32_t i0 = threadIdx.x; i0 < nb; i0 += kBlock * kU)
     {
-        float2 p[8];
+        float2 p[kU];
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < kU; ++u)
             p[u] = i0 + u * kBlock < nb ? partials[i0 + u * kBlock] : make_float2(-INFINITY, -INFINITY);
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
+        for (int u = 0; u < kU; ++u)
         {
             a = fmaxf(a, p[u].x);
             b = fmaxf(b, p[u].y);
@@ -1159,10 +1164,8 @@ static int hist_many_cols()
     return v;
 }
 
-void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s, const std::function<void()>& between)
+void stats_layout(std::vector<StatsJob>& jobs, uint64_t* mm_out, uint64_t* hb_out)
 {
-    if (jobs.empty())
-        return;
     uint64_t mm = 0, hb = 0;
     for (auto& j: jobs)
     {
@@ -1176,26 +1179,29 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s, c
         hb += j.h_blocks;
     }
     AIMET_REQUIRE(mm < (uint64_t(1) << 31) && hb < (uint64_t(1) << 31), "too many workgroups");
-    const int n = (int) jobs.size();
-    float* parts = nullptr;
+    *mm_out = mm;
+    *hb_out = hb;
+}
+
+// walk the tiles when every quantizer is a PDF scheme that has seen a batch (its range is almost
+// surely fixed) or when the job table needs more than one ballot round per workgroup (> 64
+// quantizers: ViT-L/16's 318 read their first batch in 5.8 ms walking vs 7.1 ms one tile per
+// workgroup)
+bool stats_walk(const StatsJob* jobs, int n)
+{
+    bool fixed = true;
+    for (int i = 0; i < n; ++i)
+        fixed = fixed && jobs[i].hist && !jobs[i].ent && jobs[i].seen;
+    return n > 64 || fixed;
+}
+
+void launch_stats_table(const StatsJob* dj, int n, uint64_t mm, uint64_t hb, bool walk, int phases, hipStream_t s,
+                        const std::function<void()>& between)
+{
+    if (n == 0)
+        return;
     if (phases & kPhaseMinmax)
     {
-        parts = static_cast<float*>(scratch_alloc(sizeof(float) * 2 * mm, s));
-        for (auto& j: jobs)
-            j.mm_part = parts + 2 * (int64_t) j.mm_block0;
-    }
-    auto* dj = static_cast<StatsJob*>(upload_async(jobs.data(), sizeof(StatsJob) * n, s));
-    if (phases & kPhaseMinmax)
-    {
-        // walk the tiles when every quantizer is a PDF scheme that has seen a batch (its range is
-        // almost surely fixed) or when the job table needs more than one ballot round per
-        // workgroup (> 64 quantizers: ViT-L/16's 318 read their first batch in 5.8 ms walking vs
-        // 7.1 ms one tile per workgroup)
-        bool walk = n > 64;
-        bool fixed = true;
-        for (const auto& j: jobs)
-            fixed = fixed && j.hist && !j.ent && j.seen;
-        walk = walk || fixed;
         if (walk)
             minmax_walk_kernel<<<(unsigned) std::min<uint64_t>(mm, kMmGrid), kBlock, 0, s>>>(dj, n, (uint32_t) mm);
         else
@@ -1203,19 +1209,7 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s, c
         AIMET_LAUNCH_CHECK();
     }
     if (between)
-    {
-        try
-        {
-            between();
-        }
-        catch (...)
-        {
-            if (parts)
-                scratch_free(parts, s);
-            scratch_free(dj, s);
-            throw;
-        }
-    }
+        between();
     if (phases & kPhaseMinmax)
     {
         combine_many_kernel<<<n, kBlock, 0, s>>>(dj, (phases & kPhaseFoldMinmax) ? 1 : 0);
@@ -1244,26 +1238,58 @@ void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s, c
         fold_histogram_many_kernel<<<n, kPdfSize, 0, s>>>(dj);
         AIMET_LAUNCH_CHECK();
     }
+}
+
+void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s, const std::function<void()>& between)
+{
+    if (jobs.empty())
+        return;
+    uint64_t mm = 0, hb = 0;
+    stats_layout(jobs, &mm, &hb);
+    const int n = (int) jobs.size();
+    float* parts = nullptr;
+    if (phases & kPhaseMinmax)
+    {
+        parts = static_cast<float*>(scratch_alloc(sizeof(float) * 2 * mm, s));
+        for (auto& j: jobs)
+            j.mm_part = parts + 2 * (int64_t) j.mm_block0;
+    }
+    auto* dj = static_cast<StatsJob*>(upload_async(jobs.data(), sizeof(StatsJob) * n, s));
+    try
+    {
+        launch_stats_table(dj, n, mm, hb, stats_walk(jobs.data(), n), phases, s, between);
+    }
+    catch (...)
+    {
+        if (parts)
+            scratch_free(parts, s);
+        scratch_free(dj, s);
+        throw;
+    }
     if (parts)
         scratch_free(parts, s);
     scratch_free(dj, s);
 }
 
-void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s)
+uint64_t channel_layout(std::vector<ChannelJob>& jobs, bool* any_hist)
 {
-    if (jobs.empty())
-        return;
     uint64_t blocks = 0;
-    bool any_hist   = false;
+    bool hist       = false;
     for (auto& j: jobs)
     {
         j.block0 = (uint32_t) blocks;
         blocks += (uint64_t) j.C;
-        any_hist = any_hist || j.kind != kKindTf;
+        hist = hist || j.kind != kKindTf;
     }
     AIMET_REQUIRE(blocks < (uint64_t(1) << 31), "too many channels");
-    const int n = (int) jobs.size();
-    auto* dj    = static_cast<ChannelJob*>(upload_async(jobs.data(), sizeof(ChannelJob) * n, s));
+    *any_hist = hist;
+    return blocks;
+}
+
+void launch_channel_table(const ChannelJob* dj, int n, uint64_t blocks, bool any_hist, hipStream_t s)
+{
+    if (n == 0 || blocks == 0)
+        return;
     channel_minmax_fold_many_kernel<<<(unsigned) blocks, kBlock, 0, s>>>(dj, n);
     AIMET_LAUNCH_CHECK();
     if (any_hist)
@@ -1271,7 +1297,26 @@ void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s)
         channel_hist_fold_many_kernel<<<(unsigned) blocks, kBlock, 0, s>>>(dj, n);
         AIMET_LAUNCH_CHECK();
     }
+}
+
+void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s)
+{
+    if (jobs.empty())
+        return;
+    bool any_hist         = false;
+    const uint64_t blocks = channel_layout(jobs, &any_hist);
+    const int n           = (int) jobs.size();
+    auto* dj              = static_cast<ChannelJob*>(upload_async(jobs.data(), sizeof(ChannelJob) * n, s));
+    launch_channel_table(dj, n, blocks, any_hist, s);
     scratch_free(dj, s);
+}
+
+void launch_reset_table(const ResetJob* dj, int n, hipStream_t s)
+{
+    if (n == 0)
+        return;
+    reset_acc_many_kernel<<<(unsigned) n, kBlock, 0, s>>>(dj);
+    AIMET_LAUNCH_CHECK();
 }
 
 void launch_reset_state_many(const std::vector<ResetJob>& jobs, hipStream_t s)
@@ -1279,8 +1324,7 @@ void launch_reset_state_many(const std::vector<ResetJob>& jobs, hipStream_t s)
     if (jobs.empty())
         return;
     auto* dj = static_cast<ResetJob*>(upload_async(jobs.data(), sizeof(ResetJob) * jobs.size(), s));
-    reset_acc_many_kernel<<<(unsigned) jobs.size(), kBlock, 0, s>>>(dj);
-    AIMET_LAUNCH_CHECK();
+    launch_reset_table(dj, (int) jobs.size(), s);
     scratch_free(dj, s);
 }
 
@@ -1308,6 +1352,16 @@ __global__ __launch_bounds__(kBlock) void zero_many_kernel(const ZeroJob* __rest
     }
 }
 
+void launch_zero_table(const ZeroJob* dj, int n, int64_t most, hipStream_t s)
+{
+    if (n == 0)
+        return;
+    AIMET_REQUIRE(n < 65536, "too many ranges to zero in one launch");
+    const int64_t bx = std::max<int64_t>(1, std::min<int64_t>(64, ceil_div(most / 16, (int64_t) kBlock * 8)));
+    zero_many_kernel<<<dim3((unsigned) bx, (unsigned) n), kBlock, 0, s>>>(dj);
+    AIMET_LAUNCH_CHECK();
+}
+
 void launch_zero_many(const std::vector<ZeroJob>& jobs, hipStream_t s)
 {
     if (jobs.empty())
@@ -1316,10 +1370,8 @@ void launch_zero_many(const std::vector<ZeroJob>& jobs, hipStream_t s)
     int64_t most = 0;
     for (const ZeroJob& j: jobs)
         most = std::max(most, j.bytes);
-    const int64_t bx = std::max<int64_t>(1, std::min<int64_t>(64, ceil_div(most / 16, (int64_t) kBlock * 8)));
-    auto* dj         = static_cast<ZeroJob*>(upload_async(jobs.data(), sizeof(ZeroJob) * jobs.size(), s));
-    zero_many_kernel<<<dim3((unsigned) bx, (unsigned) jobs.size()), kBlock, 0, s>>>(dj);
-    AIMET_LAUNCH_CHECK();
+    auto* dj = static_cast<ZeroJob*>(upload_async(jobs.data(), sizeof(ZeroJob) * jobs.size(), s));
+    launch_zero_table(dj, (int) jobs.size(), most, s);
     scratch_free(dj, s);
 }
 

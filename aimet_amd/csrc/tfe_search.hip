@@ -42,17 +42,6 @@ __device__ __forceinline__ bool better(const Best& a, const Best& b)
     return (a.cost < b.cost) || (a.cost == b.cost && a.idx < b.idx);
 }
 
-// One quantizer's statistics and output; a batched getEncoding passes one job per quantizer.
-struct TfeJob
-{
-    const int32_t* pdf_init;
-    const float* hist_min;
-    const double* bucket_size;
-    const double* pdf;
-    aimet_tf_encoding* out;
-    int64_t start;   // first global channel of this job
-};
-
 // Channel g's candidates over `splits` workgroups (few channels: the activations' quantizers of a
 // batch): workgroup (g, s) takes candidates s * BLOCK + lane, s * BLOCK + lane + BLOCK * splits, ...,
 // publishes its first minimum (cost, index) write-through, and the last of the g's workgroups to
@@ -269,25 +258,32 @@ int search_grid_cap()
 // quantizers of a batch: ResNet-50's 55 asymmetric searches took 58 us as 55 workgroups)
 constexpr int64_t kTfeSplitBelow = 512;
 
+// the split search's launch (part: 2 * total * splits, tickets: total zeroed counters)
+void launch_split(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t total, int bw, bool sym, bool strict,
+                  bool unsign, int splits, uint64_t* part, unsigned* tickets, hipStream_t s)
+{
+    const int grid = (int) std::min<int64_t>(total * splits, search_grid_cap());
+    if (sym)
+        tfe_search_kernel<64, true><<<grid, 64, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign, splits, part,
+                                                      tickets);
+    else
+        tfe_search_kernel<64, false><<<grid, 64, 0, s>>>(one, jobs, njobs, total, bw, 0, strict, unsign, splits, part,
+                                                       tickets);
+    AIMET_LAUNCH_CHECK();
+}
+
 void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t total, int bw, bool sym, bool strict,
                    bool unsign, hipStream_t s)
 {
-    const int cap = search_grid_cap();
-    if (total < kTfeSplitBelow && getenv("AIMET_TFE_NO_SPLIT") == nullptr)
+    const int cap    = search_grid_cap();
+    const int splits = tfe_splits(total, sym);
+    if (splits > 1)
     {
-        const int splits  = (int) ceil_div(sym ? tfe::kSymF : tfe::kMaxCand, 64);
         unsigned* tickets = ticket_alloc(s, (unsigned) total);
         if (tickets)
         {
-            auto* part     = static_cast<uint64_t*>(scratch_alloc(sizeof(uint64_t) * 2 * total * splits, s));
-            const int grid = (int) std::min<int64_t>(total * splits, cap);
-            if (sym)
-                tfe_search_kernel<64, true><<<grid, 64, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign, splits,
-                                                              part, tickets);
-            else
-                tfe_search_kernel<64, false><<<grid, 64, 0, s>>>(one, jobs, njobs, total, bw, 0, strict, unsign,
-                                                               splits, part, tickets);
-            AIMET_LAUNCH_CHECK();
+            auto* part = static_cast<uint64_t*>(scratch_alloc(sizeof(uint64_t) * 2 * total * splits, s));
+            launch_split(one, jobs, njobs, total, bw, sym, strict, unsign, splits, part, tickets, s);
             scratch_free(part, s);
             return;
         }
@@ -301,6 +297,32 @@ void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t tot
                                                          nullptr);
     AIMET_LAUNCH_CHECK();
 }
+
+}   // namespace
+
+int tfe_splits(int64_t total, bool sym)
+{
+    if (total >= kTfeSplitBelow || getenv("AIMET_TFE_NO_SPLIT") != nullptr)
+        return 1;
+    return (int) ceil_div(sym ? tfe::kSymF : tfe::kMaxCand, 64);
+}
+
+void launch_tfe_table(const TfeTable& t, int bw, bool sym, bool strict, bool unsign, hipStream_t s)
+{
+    if (t.total == 0)
+        return;
+    const int splits = tfe_splits(t.total, sym);
+    if (splits > 1)
+    {
+        AIMET_REQUIRE(t.part != nullptr && t.tickets != nullptr, "split TF-Enhanced search without its buffers");
+        launch_split(t.first, t.dev, t.n, t.total, bw, sym, strict, unsign, splits, t.part, t.tickets, s);
+        return;
+    }
+    launch_kernel(t.first, t.dev, t.n, t.total, bw, sym, strict, unsign, s);
+}
+
+namespace
+{
 
 TfeJob job_of(const TqDevice& d, int64_t start)
 {

@@ -72,6 +72,9 @@ struct ZeroJob
     int64_t bytes;
 };
 void launch_zero_many(const std::vector<ZeroJob>& jobs, hipStream_t s);
+// the same two resets over device tables (`most`: the largest range in bytes)
+void launch_zero_table(const ZeroJob* dj, int n, int64_t most, hipStream_t s);
+void launch_reset_table(const ResetJob* dj, int n, hipStream_t s);
 // Many per-tensor quantizers (C == 1) in one launch per phase (stats.hip: launch_stats_many)
 struct StatsJob
 {
@@ -79,6 +82,8 @@ struct StatsJob
     int64_t n;       // elements of this quantizer's tensor
     int64_t count;   // element count of the PDF fold (the global count when sharded)
     const int64_t* count_dev;   // when set: the count is read on the device (summed over ranks in HBM)
+    int64_t* count_out;         // when set: the combine writes this rank's element count n there (the
+                                // sharded calibration's SUM then forms count_dev in place)
     TqDevice d;
     uint32_t mm_block0, mm_blocks, h_block0, h_blocks;   // filled by launch_stats_many
     float* mm_part;  // [mm_blocks][2] per-tile {-min, max} (launch_stats_many's scratch)
@@ -99,6 +104,14 @@ enum StatsPhase
 // combine / fold: the calibration enqueues the quantizers' reset and the parameters' work there
 void launch_stats_many(std::vector<StatsJob>& jobs, int phases, hipStream_t s,
                        const std::function<void()>& between = {});
+// launch_stats_many in two halves, for job tables kept on the device (calibration plans): the
+// workgroup layout (mm_block0 / h_block0 of every job; *mm, *hb the two passes' grids), then the
+// phases over a device copy `dj` of those jobs (whose mm_part point into 2 * mm floats of scratch).
+// walk: the min/max pass walks the tiles (launch_stats_many decides it from the jobs' seen flags)
+void stats_layout(std::vector<StatsJob>& jobs, uint64_t* mm, uint64_t* hb);
+bool stats_walk(const StatsJob* jobs, int n);
+void launch_stats_table(const StatsJob* dj, int n, uint64_t mm, uint64_t hb, bool walk, int phases, hipStream_t s,
+                        const std::function<void()>& between = {});
 // Many per-channel quantizers ([outer][C][K] tensors) with the whole updateStats (min/max, fold,
 // histogram, fold) in TWO launches: every channel of every quantizer is one workgroup, and the
 // fold of a channel needs only that channel's statistics, so it runs in the workgroup that
@@ -113,7 +126,35 @@ struct ChannelJob
     int32_t vec;       // 16-B aligned rows
 };
 void launch_channel_stats_many(std::vector<ChannelJob>& jobs, hipStream_t s);
+// the same over a device job table (block0 filled: channel_layout), `blocks` channels in all
+uint64_t channel_layout(std::vector<ChannelJob>& jobs, bool* any_hist);
+void launch_channel_table(const ChannelJob* dj, int n, uint64_t blocks, bool any_hist, hipStream_t s);
 // tfe_search.hip
+// One quantizer's statistics and output; a batched search passes one job per quantizer.
+struct TfeJob
+{
+    const int32_t* pdf_init;
+    const float* hist_min;
+    const double* bucket_size;
+    const double* pdf;
+    aimet_tf_encoding* out;
+    int64_t start;   // first global channel of this job
+};
+// A TF-Enhanced search whose job table is already on the device (calibration plans, calib_plan.cpp):
+// one launch, the results straight into each job's `out` (device-accessible memory: a plan points
+// them into pinned host memory, so no copy follows the search)
+struct TfeTable
+{
+    TfeJob first {};                 // jobs[0] (the kernel's by-value job)
+    const TfeJob* dev = nullptr;     // every job, on the device
+    int n = 0;
+    int64_t total = 0;               // channels
+    uint64_t* part = nullptr;        // split search: 2 * total * splits (tfe_splits)
+    unsigned* tickets = nullptr;     // split search: `total` zeroed counters
+};
+// workgroups per channel of a batched search of `total` channels (1: one workgroup per channel)
+int tfe_splits(int64_t total, bool sym);
+void launch_tfe_table(const TfeTable& t, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
 // d.enc[c] <- TF-Enhanced encoding of channel c (statistics updated; see aimet_tq_get_encoding)
 void launch_tfe_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
 // the same for n quantizers in one launch; host_out <- their encodings concatenated

@@ -55,6 +55,12 @@ def parse():
     p.add_argument("--eager", action="store_true", help="launch every QDQ from Python instead of HIP graphs")
     p.add_argument("--per-weight-launches", action="store_true",
                    help="one per-channel QDQ launch per weight instead of the batched plan")
+    p.add_argument("--no-dropin", action="store_true",
+                   help="skip the drop-in surface timings (QuantizationSimModel.compute_encodings of config 1, "
+                        "the StaticGridQuantWrapper forward of config 2)")
+    p.add_argument("--force-exchange", action="store_true",
+                   help="at N=1 form a world-size-1 RCCL group before any GPU call and time the sharded "
+                        "calibration's staged form (both packed collectives through RCCL) beside the headline")
     return p.parse_args()
 
 
@@ -131,8 +137,10 @@ def setup_dist(args):
         raise SystemExit("bench.py: %d ranks over RCCL but only %d GPU(s) visible" % (world, torch.cuda.device_count()))
     if backend == "gloo":
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    if world > 1 or args.force_exchange:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if world == 1:
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
@@ -160,6 +168,28 @@ def collect_tensors(model, x):
     return acts, weights
 
 
+def make_quantizers(acts, weights):
+    """The sim's quantizers for this workload: TF-Enhanced per-tensor activations, TF-Enhanced
+    per-channel weights (QuantizationSimModel's default scheme)."""
+    from aimet_amd.libpymo import QuantizationMode
+    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+    aq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in acts]
+    wq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=w.shape[0]) for _, w in weights]
+    return aq, wq
+
+
+def time_plan(plan, reps):
+    """`reps` timed plan runs that reset and recompute the plan's quantizers (one compute_encodings
+    of an existing sim each); returns (median seconds, encodings of the last run)."""
+    secs, res = [], None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        res = plan.run(reset=True)
+        secs.append(time.perf_counter() - t0)
+    return sorted(secs)[len(secs) // 2], res
+
+
 def compute_encodings(acts, weights, quantizers=None):
     """compute_encodings as QuantizationSimModel does it for this workload (v1/quantsim.py:381-449):
     TF-Enhanced stats for every activation, TF-Enhanced per-channel symmetric for every weight.
@@ -167,14 +197,10 @@ def compute_encodings(acts, weights, quantizers=None):
     else the (aq, wq) of an earlier call -- the sim's quantizers, created with the sim -- are reset
     (resetEncodingStats of every quantizer, v1/quantsim.py:387-399) and recomputed."""
     from aimet_amd.calibration import compute_encodings_resident
-    from aimet_amd.libpymo import QuantizationMode
-    from aimet_amd.tensor_quantizer import AimetTensorQuantizer
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     if quantizers is None:
-        aq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED) for _ in acts]
-        wq = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=w.shape[0])
-              for _, w in weights]
+        aq, wq = make_quantizers(acts, weights)
     else:
         aq, wq = quantizers
     # activations (sharded across ranks, one packed collective per phase) and per-channel weights
@@ -186,6 +212,67 @@ def compute_encodings(acts, weights, quantizers=None):
     act_enc = [e for e, _ in a_res]
     w_enc = [e for e, _ in w_res]
     return act_enc, w_enc, time.perf_counter() - t0, aq, wq
+
+
+def dropin_surface(model, dev, qdq_kernel_ms, reps=3):
+    """The caller surface a user of the reference drives (aimet_amd.quantsim, v1/quantsim.py:425-449,
+    v1/qc_quantize_op.py:705-745), timed on the same random-init ResNet-50:
+      * config 1: QuantizationSimModel(quant_scheme=post_training_tf_enhanced, W8A8 per-tensor)
+        .compute_encodings over 8 x 32 U(0,1) images (seed 1234) -- ANALYSIS forwards through every
+        StaticGridQuantWrapper + statistics + encodings -- beside the same 8 forwards of the plain
+        model (median of `reps` runs each, after a warm run);
+      * config 2: the W8A8 per-channel QuantSim forward of the bench's batch-256 shape (eager,
+        MIOpen convolutions, every QDQ through the wrappers) minus the unquantized forward, beside
+        the QDQ kernel time of the headline step (the wrappers' Python cost is the rest)."""
+    from aimet_amd.quantizers import QuantScheme
+    from aimet_amd.quantsim import QuantizationSimModel
+    g = torch.Generator(device=dev).manual_seed(1234)
+    images = torch.rand(8 * 32, 3, 224, 224, device=dev, generator=g)
+    batches = [images[b * 32:(b + 1) * 32] for b in range(8)]
+
+    def calibrate(m, _):
+        with torch.no_grad():
+            for b in batches:
+                m(b)
+
+    def median_s(fn):
+        fn()
+        ts = []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append(time.perf_counter() - t0)
+        return sorted(ts)[len(ts) // 2]
+
+    sim = QuantizationSimModel(model, batches[0][:1], quant_scheme=QuantScheme.post_training_tf_enhanced,
+                               default_output_bw=8, default_param_bw=8)
+    ce = median_s(lambda: sim.compute_encodings(calibrate, None))
+    fw = median_s(lambda: calibrate(model, None))
+    n_q = sum(1 for _, w in sim.quant_wrappers() for q in list(w.output_quantizers) + list(w.input_quantizers) +
+              list(w.param_quantizers.values()) if q.enabled and q.encoding is not None)
+    del sim
+    cfg = {"defaults": {"params": {"is_symmetric": "True"}, "ops": {"is_symmetric": "False"},
+                        "per_channel_quantization": "True"}}
+    sim = QuantizationSimModel(model, batches[0][:1], quant_scheme=QuantScheme.post_training_tf_enhanced,
+                               default_output_bw=8, default_param_bw=8, config_file=cfg)
+    sim.compute_encodings(calibrate, None)
+    x = torch.rand(256, 3, 224, 224, device=dev, generator=torch.Generator(device=dev).manual_seed(99))
+    with torch.no_grad():
+        q_ms = median_s(lambda: sim.model(x)) * 1e3
+        f_ms = median_s(lambda: model(x)) * 1e3
+    del sim, x, images, batches
+    torch.cuda.empty_cache()
+    return {"quantsim_compute_encodings_s": round(ce, 4), "quantsim_calibration_forwards_s": round(fw, 4),
+            "quantsim_compute_encodings_minus_forwards_s": round(ce - fw, 4), "quantsim_quantizers": n_q,
+            "quantsim_fwd_ms": round(q_ms, 2), "fp32_fwd_ms": round(f_ms, 2),
+            "quantsim_fwd_qdq_overhead_ms": round(q_ms - f_ms, 2), "qdq_kernel_ms_per_step": round(qdq_kernel_ms, 3),
+            "quantsim_fwd_python_overhead_ms": round(q_ms - f_ms - qdq_kernel_ms, 2),
+            "what": "config 1: QuantizationSimModel(post_training_tf_enhanced, W8A8 per-tensor).compute_encodings "
+                    "over 8 x 32 U(0,1) images vs the same 8 plain forwards; config 2: the W8A8 per-channel QuantSim "
+                    "forward at batch 256 (eager, MIOpen convs) minus the fp32 forward, vs the headline step's QDQ "
+                    "kernel time (weights + activations); medians of %d runs after a warm one" % reps}
 
 
 def cpu_baseline(acts, weights, act_enc, w_enc, images, act_outs, w_outs):
@@ -337,7 +424,7 @@ def main():
     model = resnet50(seed=0, device=dev)
     x = torch.rand(args.batch, 3, 224, 224, device=dev, generator=torch.Generator(device=dev).manual_seed(1234 + rank))
     acts, weights = collect_tensors(model, x)
-    del model
+    del x
     torch.cuda.empty_cache()
 
     # compute_encodings wall-clock: the first call (cold: code objects load, pools grow, quantizers
@@ -353,8 +440,32 @@ def main():
     for _ in range(args.enc_reps):
         act_enc, w_enc, secs, aq, wq = compute_encodings(acts, weights, (aq, wq))
         warm.append(secs)
-    enc_seconds = sorted(warm)[len(warm) // 2] if warm else enc_cold
+    enc_resident = sorted(warm)[len(warm) // 2] if warm else enc_cold
     enc_fresh = sorted(fresh)[len(fresh) // 2] if fresh else enc_cold
+    # the headline: a calibration plan over the sim's quantizers and the resident activations,
+    # prepared once (as the quantizers are created once with the sim), each timed run a reset +
+    # recompute of every quantizer (aimet_amd.calibration.CalibrationPlan). Sharded at N > 1.
+    from aimet_amd.calibration import CalibrationPlan
+    cplan = CalibrationPlan(aq, [t for _, t in acts], wq, [w for _, w in weights])
+    enc_seconds, (a_res, w_res) = time_plan(cplan, max(1, args.enc_reps))
+    plan_act, plan_w = [e for e, _ in a_res], [e for e, _ in w_res]
+    enc_plan_equal = ([e.to_tuple() for e in plan_act] == [e.to_tuple() for e in act_enc] and
+                      [[x.to_tuple() for x in es] for es in plan_w] == [[x.to_tuple() for x in es] for es in w_enc])
+    act_enc, w_enc = plan_act, plan_w
+    enc_exchange = None
+    if args.force_exchange and world == 1:
+        # the sharded calibration's staged form on this rank (stage 1, RCCL MAX, stage 2, RCCL SUM,
+        # stage 4) over a world-size-1 group: the per-rank cost the 1 -> N curve starts from.
+        # Quantizers of their own (the plan binds them to the packed exchange buffers).
+        xq, xw = make_quantizers(acts, weights)
+        xplan = CalibrationPlan(xq, [t for _, t in acts], xw, [w for _, w in weights], force_exchange=True)
+        x_s, (xa, xwr) = time_plan(xplan, max(1, args.enc_reps))
+        enc_exchange = {"seconds": round(x_s, 4), "dist_backend": dist.get_backend(),
+                        "world_formed": dist.get_world_size(),
+                        "equal_to_headline": [e.to_tuple() for e, _ in xa] == [e.to_tuple() for e in act_enc] and
+                        [[x.to_tuple() for x in es] for es, _ in xwr] == [[x.to_tuple() for x in es] for es in w_enc]}
+        xplan.close()
+        del xq, xw
 
     # ---- the step: every QDQ of one QuantSim forward, pre-bound C-ABI calls --------------------
     stream = torch.cuda.current_stream(dev)
@@ -453,10 +564,10 @@ def main():
     act_ms = [s.elapsed_time(e) for s, e in ev]
     kernel_ms = sum(act_ms) / len(act_ms)
     if world > 1:
-        tt = torch.tensor([dt, enc_seconds, enc_cold, enc_fresh], dtype=torch.float64,
+        tt = torch.tensor([dt, enc_seconds, enc_cold, enc_fresh, enc_resident], dtype=torch.float64,
                           device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        dt, enc_seconds, enc_cold, enc_fresh = (float(v) for v in tt)
+        dt, enc_seconds, enc_cold, enc_fresh, enc_resident = (float(v) for v in tt)
 
     ms_per_step = dt / args.steps * 1e3
     value = n_step * world * args.steps / dt / 1e9
@@ -482,16 +593,21 @@ def main():
                    "compute_encodings_s": round(enc_seconds, 4),
                    "compute_encodings_cold_s": round(enc_cold, 4),
                    "compute_encodings_fresh_quantizers_s": round(enc_fresh, 4),
+                   "compute_encodings_resident_s": round(enc_resident, 4),
+                   "compute_encodings_plan_equals_resident": enc_plan_equal,
                    # two passes (min/max, histogram) of 4 B over every activation and weight element
                    "compute_encodings_roofline": {
                        "algorithmic_gb": round(8 * n_step / 1e9, 3),
                        "achieved_gbps": round(8 * n_step / enc_seconds / 1e9, 1),
                        "frac": round(8 * n_step / enc_seconds / 1e9 / HBM_PEAK_GBPS, 4)},
-                   "compute_encodings_timing": "median of %d calls that reset and recompute the sim's quantizers "
-                                               "(created once, as QuantizationSimModel does), after the first (cold) "
-                                               "call and %d calls on fresh quantizers "
-                                               "(compute_encodings_fresh_quantizers_s); max over ranks"
-                                               % (args.enc_reps, args.enc_reps),
+                   "compute_encodings_timing": "median of %d CalibrationPlan.run(reset=True) calls: reset and "
+                                               "recompute the sim's quantizers (created once, as QuantizationSimModel "
+                                               "does) with the plan prepared once over the resident activations; "
+                                               "beside it the first call of the process (cold), %d "
+                                               "compute_encodings_resident calls on fresh quantizers (plan made "
+                                               "inside) and %d on the sim's quantizers (cached plan, its tensors "
+                                               "checked by identity every call); max over ranks"
+                                               % (max(1, args.enc_reps), args.enc_reps, args.enc_reps),
                    "compute_encodings_scheme": "tf_enhanced act per-tensor + tf_enhanced weight per-channel sym"},
         "roofline": {"bound": "hbm", "kernel": "qdq_per_tensor (tensor_vec_kernel)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -502,6 +618,21 @@ def main():
                      "timing": "HIP events on the launch stream around the %d activation QDQ launches of each "
                                "timed step (%s)" % (len(act_calls), "graph replay" if use_graph else "eager")},
     }
+    if world == 1 and not args.no_dropin:
+        # the whole step's QDQ kernel time: the activation launches (events) + the weights' launch
+        w_ms = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            if use_graph:
+                g_w.replay()
+            else:
+                launch_weights(sptr)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            w_ms.append(e0.elapsed_time(e1))
+        result["config"]["dropin"] = dropin_surface(model, dev, kernel_ms + sorted(w_ms)[2])
+    del model
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb = cpu_baseline(acts, weights, act_enc, w_enc, args.cpu_sample_images, act_outs, outs[0::2])
         n = cb["n"]
@@ -522,6 +653,12 @@ def main():
             result["cpu_baseline"] = {"value": port["value"], "unit": "Gelem/s", "cores": 1, "kind": "port",
                                       "sample": sample + "; " + port["what"], "seconds": port["seconds"],
                                       "omp": omp, "parity": cb["parity"], "compute_encodings": cb["enc"]}
+    if enc_exchange is not None:
+        result["config"]["compute_encodings_exchange_s"] = enc_exchange["seconds"]
+        result["config"]["compute_encodings_exchange"] = dict(
+            enc_exchange, ratio_to_headline=round(enc_exchange["seconds"] / enc_seconds, 4),
+            what="the sharded calibration's staged plan (stage 1, all_reduce MAX, stage 2, all_reduce SUM, stage 4) "
+                 "over a world-size-1 group formed before any GPU call; median of the same reset+recompute runs")
     if world > 1:
         # the calibration exchange of this workload: what formed, and the two collectives' cost
         result["config"]["dist_backend"] = dist.get_backend()
@@ -538,7 +675,8 @@ def main():
         result["config"]["encodings_identical_across_ranks"] = bool(lo.item() == hi.item())
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    cplan.close()
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -294,6 +294,36 @@ int aimet_calibrate_launch(aimet_tensor_quantizer* const* act_qs, const float* c
                            const int32_t* act_settings, const int32_t* par_settings, int reset, void* main_stream,
                            void* side_stream, aimet_encoding_request** act_req, aimet_encoding_request** par_req);
 
+/* A calibration plan: aimet_calibrate_launch's work for a FIXED set of quantizers and resident
+ * tensors (the same arguments, the tensors' contents may change between launches), prepared once
+ * -- every job table, the parameters' reset ranges, the TF-Enhanced search tables and hand-off
+ * buffers in one device allocation, the TF-Enhanced results written by the searches straight into
+ * the plan's pinned host blocks -- so that a launch is only kernel launches (QuantizationSimModel
+ * .compute_encodings on an existing sim, v1/quantsim.py:381-449, repeated per batch or per
+ * recalibration). elem_counts_dev (NULL on one device): the sharded calibration's element counts,
+ * one int64 per histogram activation quantizer in order (the tail of the packed SUM buffer,
+ * aimet_amd/distributed.py); the quantizers must already be bound to the packed exchange buffers
+ * (aimet_tq_bind_exchange), and neither they nor the tensors may be re-bound, freed or destroyed
+ * while the plan lives. */
+typedef struct aimet_calib_plan aimet_calib_plan;
+int aimet_calib_plan_create(aimet_tensor_quantizer* const* act_qs, const float* const* act_x, const int64_t* act_n,
+                            int64_t n_act, aimet_tensor_quantizer* const* par_qs, const float* const* par_x,
+                            const int64_t* par_outer, const int64_t* par_C, const int64_t* par_K, int64_t n_par,
+                            const int32_t* act_settings, const int32_t* par_settings, int64_t* elem_counts_dev,
+                            aimet_calib_plan** plan);
+/* stages = 7: one batch on one device, as aimet_calibrate_launch (reset != 0: resetEncodingStats
+ * first). The sharded calibration launches stage 1 (resets, the parameters'
+ * statistics + search on side_stream, the activations' min/max pass and element counts), then,
+ * after its all_reduce(MAX) of the packed {-min, max}, stage 2 (PDF ranges + histogram pass), then,
+ * after its all_reduce(SUM) of the packed counts, stage 4 (PDF fold + the activations' search).
+ * *par_req comes from the stage-1 launch, *act_req from the stage-4 launch (NULL otherwise); both
+ * are finished with aimet_tq_get_encodings_finish, and the plan launches its next stage 1 / 4
+ * only once the previous request of that kind is finished. */
+int aimet_calib_plan_launch(aimet_calib_plan* plan, int stages, int reset, void* main_stream, void* side_stream,
+                            aimet_encoding_request** act_req, aimet_encoding_request** par_req);
+/* Waits for the device, frees the plan (its requests must be finished first). */
+int aimet_calib_plan_destroy(aimet_calib_plan* plan);
+
 /* AimetTensorQuantizer.cpp:194-198 getStatsHistogram (histogram schemes): xleft/pdf[512] of
  * `channel`; *n = 0 when no histogram exists yet. Synchronises `stream`. */
 int aimet_tq_get_stats_histogram(aimet_tensor_quantizer* q, int64_t channel, double* xleft, double* pdf, int* n,

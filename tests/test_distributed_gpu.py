@@ -50,3 +50,23 @@ def test_rccl_world1_device_exchange_equals_unsharded(tmp_path):
     rccl, = _run(1, str(tmp_path / "rccl"), BACKEND="nccl", FORCE_EXCHANGE="1")
     assert open(str(tmp_path / "rccl") + ".backend").read() == "nccl"
     assert rccl == whole
+
+
+def test_plan_sharded_calibration_equals_whole_batch_on_gpu(tmp_path):
+    """The calibration plan's sharded form (bench.py's path at N > 1: stage 1, packed MAX, stage 2,
+    packed SUM with the element counts formed on the device, stage 4), two ranks over gloo on one
+    GPU, three batches refilled in place: every rank's encodings == each quantizer's own
+    updateStats over the whole batches (per-tensor activations sharded, per-channel parameters)."""
+    whole, = _run(1, str(tmp_path / "whole"), MODE="plan")
+    shards = _run(2, str(tmp_path / "shard"), MODE="plan")
+    for r, res in enumerate(shards):
+        assert res == whole, "rank %d" % r
+
+
+def test_rccl_world1_plan_exchange_equals_unsharded(tmp_path):
+    """The calibration plan's sharded form over a world-size-1 RCCL group: both packed collectives
+    of every batch run on the device buffers between the plan's stages; encodings == unsharded."""
+    whole, = _run(1, str(tmp_path / "whole"), MODE="plan")
+    rccl, = _run(1, str(tmp_path / "rccl"), MODE="plan", BACKEND="nccl", FORCE_EXCHANGE="1")
+    assert open(str(tmp_path / "rccl") + ".backend").read() == "nccl"
+    assert rccl == whole

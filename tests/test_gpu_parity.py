@@ -18,7 +18,7 @@ from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding  # noqa
 
 DEV = "cuda"
 # learned-grid range gradients: error bound in units of 2^-24 x (sum of |terms|) of the float64 sum
-LG_BOUND_C = float(os.environ.get("AIMET_LG_BOUND_C", "2"))
+LG_BOUND_C = 2.0   # range-gradient bar in units of 2^-24 x the sum of |terms| (fixed: part of the test)
 NEAREST = RoundingMode.ROUND_NEAREST
 FLAGS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]
 
@@ -1835,6 +1835,67 @@ def test_calibrate_non_contiguous_parameters_and_activations(monkeypatch, split)
     got = run([act], [w_t, w_cl])
     want = run([act.contiguous()], [w_t.contiguous(), w_cl.contiguous()])
     assert got == want
+
+
+@pytest.mark.parametrize("schemes", ["tfe", "mixed"])
+def test_calibration_plan_equals_per_quantizer_updates(schemes):
+    """aimet_amd.calibration.CalibrationPlan (every job table prepared once; the TF-E searches write
+    straight into the plan's pinned blocks; the parameters' light reset): two batches without a
+    reset == each quantizer's own updateStats over both batches; then run(reset=True) on a third
+    batch, twice, == fresh quantizers fed only that batch (nothing of the earlier batches survives,
+    the PDFs the light reset left in place included); a second launch before the first request is
+    finished is refused."""
+    from aimet_amd.calibration import CalibrationPlan
+    g = torch.Generator(device=DEV).manual_seed(31)
+    M = QuantizationMode
+    a_modes = [M.QUANTIZATION_TF_ENHANCED] * 3 if schemes == "tfe" else \
+        [M.QUANTIZATION_TF, M.QUANTIZATION_TF_ENHANCED, M.QUANTIZATION_PERCENTILE, M.QUANTIZATION_MSE,
+         M.QUANTIZATION_ENTROPY]
+    p_modes = [M.QUANTIZATION_TF_ENHANCED] * 2 if schemes == "tfe" else \
+        [M.QUANTIZATION_TF, M.QUANTIZATION_TF_ENHANCED, M.QUANTIZATION_MSE, M.QUANTIZATION_PERCENTILE]
+    sizes = [1 << 20, 3001, 77777, 1 << 18, 4099][:len(a_modes)]
+    shapes = [(64, 27), (128, 576), (10, 2048), (33, 5)][:len(p_modes)]
+
+    def batch(scale):
+        acts = [torch.relu(torch.randn(n, device=DEV, generator=g) * scale * (1 + i)) - 0.1 * i
+                for i, n in enumerate(sizes)]
+        params = [torch.randn(c, k, device=DEV, generator=g) * 0.05 * scale for c, k in shapes]
+        return acts, params
+
+    def flat(a_res, p_res):
+        return ([e.to_tuple() for e, _ in a_res],
+                [[x.to_tuple() for x in (es if isinstance(es, list) else [es])] for es, _ in p_res])
+
+    def individual(batches):
+        aq = [AimetTensorQuantizer(m) for m in a_modes]
+        pq = [AimetTensorQuantizer(m, num_channels=c) for m, (c, _) in zip(p_modes, shapes)]
+        for acts, params in batches:
+            for q, t in zip(aq, acts):
+                q.updateStats(t, True)
+            for q, t in zip(pq, params):
+                q.updateStatsPerChannel(t, 0, True)
+        return (flat([q.getEncoding(8, False, False, False) for q in aq],
+                     [q.getEncoding(8, True, False, False) for q in pq]))
+
+    b1, b2, b3 = batch(2.0), batch(1.0), batch(0.5)
+    aq = [AimetTensorQuantizer(m) for m in a_modes]
+    pq = [AimetTensorQuantizer(m, num_channels=c) for m, (c, _) in zip(p_modes, shapes)]
+    bufs = [t.clone() for t in b1[0]], [t.clone() for t in b1[1]]
+    plan = CalibrationPlan(aq, bufs[0], pq, bufs[1])
+    plan.run()
+    for t, s in zip(bufs[0] + bufs[1], b2[0] + b2[1]):
+        t.copy_(s)
+    assert flat(*plan.run()) == individual([b1, b2])
+    for t, s in zip(bufs[0] + bufs[1], b3[0] + b3[1]):
+        t.copy_(s)
+    want = individual([b3])
+    assert flat(*plan.run(reset=True)) == want
+    assert flat(*plan.run(reset=True)) == want
+    a_p, p_p = plan.launch(reset=True)
+    with pytest.raises(ValueError):
+        plan.launch(reset=True)
+    assert flat(a_p.result(), p_p.result()) == want
+    plan.close()
 
 
 def test_compute_encodings_resident_equals_individual():
