@@ -77,6 +77,7 @@ _PROTOTYPES = {
     "aimet_last_error": [],
     "aimet_version": [],
     "aimet_device_count": [],
+    "aimet_capture_pool_limit": [_i64, ctypes.POINTER(_i64)],
     "aimet_get_computed_encodings": [_i32, ctypes.c_double, ctypes.c_double, _int, _int, _int, _enc_p],
     "aimet_fill_encoding_info": [_i32, ctypes.c_double, ctypes.c_double, _enc_p],
     "aimet_compute_partial_encoding": [_i32, _enc_p, _int, _int, _int],
@@ -176,6 +177,7 @@ _PROTOTYPES = {
     "aimet_adaround_dw_step": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64,
                                _i32, _i32, _i32, _i32, _i32, _vp],
     "aimet_adaround_pw_step_workspace": [_i64, _i64, _i64, _i64, _vp],
+    "aimet_adaround_pw_step_uses_mfma": [_i64, _i64, ctypes.POINTER(_int)],
     "aimet_adaround_pw_step": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp],
     "aimet_dwconv2d_grad_weight": [_vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _i32, _i32, _i32, _i32,
                                    _vp],
@@ -192,9 +194,6 @@ _PROTOTYPES = {
                                            _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                            _vp, _vp, _vp, _vp],
     "aimet_adaround_adam_bias_corrections": [ctypes.c_double, ctypes.c_double, _i64, _vp, _vp],
-    "aimet_adaround_pw_cm_forward": [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i32, _vp],
-    "aimet_adaround_pw_cm_wgrad_slices": [_i64, _i64, _i64, _i64, _vp],
-    "aimet_adaround_pw_cm_wgrad": [_vp, _vp, _vp, _vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp],
 }
 _RESTYPES = {"aimet_last_error": ctypes.c_char_p, "aimet_version": ctypes.c_char_p}
 

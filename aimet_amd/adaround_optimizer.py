@@ -29,7 +29,6 @@ the collective between them: [forward + backward] -> all_reduce(alpha.grad) -> [
 """
 import contextlib
 import logging
-import os
 import warnings
 from dataclasses import dataclass
 from typing import Callable, Optional, Tuple
@@ -95,34 +94,29 @@ def conv_backend(module: torch.nn.Module):
         torch.backends.cudnn.deterministic = prev_det
 
 
+# The loop's forms are fixed rules by layer shape, never timings, so two runs with the same seed give
+# the same alpha. The module-level switches below select between forms that the tests compare
+# (tests/test_adaround_wrapper.py patches them); none is read from the environment.
+
 # 1x1 convolutions and linear layers of the fused AdaRound loop as direct GEMMs (torch.matmul /
-# hipBLASLt) instead of MIOpen convolutions through autograd; AIMET_ADA_GEMM_LAYERS=0 turns it off
-_GEMM_LAYERS = os.environ.get("AIMET_ADA_GEMM_LAYERS", "1") != "0"
-
-
+# hipBLASLt) instead of MIOpen convolutions through autograd
+_GEMM_LAYERS = True
 # 1x1 / linear layers have two loop forms that sum the weight gradient in different orders (GEMM or
-# MIOpen convolution through autograd), so the optimised alpha depends on the form. The form is a
-# fixed rule (the GEMM form), never a timing: two runs with the same seed give the same alpha.
-# AIMET_ADA_LOOP_FORM=autograd forces the convolution form; =timed picks the faster of the two by
-# timing graph replays (measurements only: results then depend on timing noise).
-_LOOP_FORM = os.environ.get("AIMET_ADA_LOOP_FORM", "gemm")
+# MIOpen convolution through autograd), so the optimised alpha depends on the form: "gemm" (the
+# rule) or "autograd" (the convolution form, the GEMM form's fallback when it cannot be captured)
+_LOOP_FORM = "gemm"
 # the pointwise / im2col weight gradient: "bmm" (per-sample GEMMs + a sum over the batch) or "mm"
-# (one GEMM over (n, hw) from channel-major copies); "auto" (default) takes mm for spatial sizes
-# <= 64 (MobileNet-v2's 7x7 layers: up to 0.047 ms per iteration less) and bmm above, a fixed
-# rule by shape (profiles/r03/adaround_pw_grad_forms.txt)
-_PW_GRAD = os.environ.get("AIMET_ADA_PW_GRAD", "auto")
-
-
-# the Adam step writes the next soft-quantized weight (AIMET_ADA_FUSE_WQ=0: a forward launch per
-# iteration instead; measurements only)
-_FUSE_SOFT_WEIGHT = os.environ.get("AIMET_ADA_FUSE_WQ", "1") == "1"
+# (one GEMM over (n, hw) from channel-major copies); "auto" takes mm for spatial sizes <= 64
+# (MobileNet-v2's 7x7 layers: up to 0.047 ms per iteration less) and bmm above
+# (profiles/r03/adaround_pw_grad_forms.txt)
+_PW_GRAD = "auto"
 # depthwise layers: the whole iteration up to dL/dWq as one pass over the cached rows
 # (aimet_adaround_dw_step, bit-identical to gather + forward + reconstruction gradient + weight
-# gradient); AIMET_ADA_DW_FUSED=0 runs those four launches instead (tests, measurements)
-_DW_FUSED = os.environ.get("AIMET_ADA_DW_FUSED", "1") == "1"
+# gradient); False runs those four launches instead (the tests' comparison)
+_DW_FUSED = True
 # the depthwise / 1x1 one-pass steps' weight-gradient slices folded by the Adam step
 # (aimet_adaround_backward_adam_parts with part_kk: the folds' sums, one launch fewer per iteration)
-_DW_FOLD_ADAM = os.environ.get("AIMET_ADA_DW_FOLD_ADAM", "1") == "1"
+_DW_FOLD_ADAM = True
 # 1x1 layers / the unfolded stem with few input channels (Cin <= 192, HW % 4 == 0)
 # can run the iteration up to dL/dWq as one pass too (aimet_adaround_pw_step: q, g and the gradient
 # partials on chip; sums in a fixed order, not a library GEMM's). "auto" (default) takes it for every
@@ -132,31 +126,31 @@ _DW_FOLD_ADAM = os.environ.get("AIMET_ADA_DW_FOLD_ADAM", "1") == "1"
 # 0.092; 64 -> 384 x 14^2: 0.064 vs 0.076; profiles/r03/adaround_pw_fused_forms.txt). Since the step
 # runs on the matrix cores for C_in >= 32 (round 4), the projecting layers at 28 x 28 with C_in >= 32
 # take it too (144 -> 32: 0.073 -> 0.056 ms, 192 -> 32: 0.070 -> 0.067; profiles/r04/
-# adaround_pw_fused_all.txt); below 28 x 28 the channel-major GEMMs stay faster. "all": every
-# eligible layer, "0": none. A fixed rule by shape, so results stay deterministic.
-_PW_FUSED = os.environ.get("AIMET_ADA_PW_FUSED", "auto")
+# adaround_pw_fused_all.txt) when the step does run them on the matrix cores
+# (aimet_adaround_pw_step_uses_mfma; the VALU form is slower than the GEMM form there); below 28 x 28
+# the channel-major GEMMs stay faster. "all": every eligible layer, "0": none.
+_PW_FUSED = "auto"
 # the GEMM form of 1x1 layers with channel-major batches (aimet_adaround_gather_cm: x as [C_in][nb hw],
 # so q = W x and dL/dW = g x^T are ONE GEMM each, no per-sample GEMMs, batch sum or transposes), for
 # layers of <= 14 x 14 positions (MobileNet-v2: 0.117 -> 0.063 ms per iteration at 576 -> 96 x 14^2;
-# slower at 28^2: 0.071 -> 0.09); AIMET_ADA_PW_CM=0: the [nb][C][hw] batches with per-sample GEMMs
-# (AIMET_ADA_PW_GRAD) everywhere
-_PW_CM = os.environ.get("AIMET_ADA_PW_CM", "1") == "1"
-# the channel-major form as two kernels on the f32 matrix cores (aimet_adaround_pw_cm_forward: the
-# gather, q = W x and the reconstruction gradient; aimet_adaround_pw_cm_wgrad: dL/dW in position
-# slices that the Adam step adds, aimet_adaround_backward_adam_parts) instead of gather + GEMM +
-# reconstruction gradient + GEMM; AIMET_ADA_PW_CM_FUSED=0: the library-GEMM chain (fp32 sums in
-# another order, so alpha differs at summation-order tolerance)
-_PW_CM_FUSED = os.environ.get("AIMET_ADA_PW_CM_FUSED", "0") == "1"
+# slower at 28^2: 0.071 -> 0.09); False: the [nb][C][hw] batches with per-sample GEMMs (_PW_GRAD)
+# everywhere. (The same form on the f32 matrix cores in two kernels of our own, and the weight
+# gradient as split-K GEMM slices, measured slower and are not in the library:
+# tools/studies/pw_cm_mfma.hip, profiles/r04/pw_cm_*.jsonl.)
+_PW_CM = True
 # iterations per captured HIP graph in the single-process loop: one hipGraphLaunch per iteration
 # left the GPU waiting on the host between replays for small layers (a depthwise layer's ~10 us of
 # kernels per iteration in a ~100 us window, profiles/r04/adaround_loop_summary.txt); the counters and
 # the batch table live on the device, so k consecutive iterations are one graph. Results are those
 # of one iteration per graph, bit for bit.
-_GRAPH_ITERS = max(1, int(os.environ.get("AIMET_ADA_GRAPH_ITERS", "10")))
-# the channel-major weight gradient as S GEMMs over consecutive position slices (one batched GEMM;
-# the Adam step adds the S slices in order): the single [C_out, nb hw] x [nb hw, C_in] GEMM has a
-# small output and a long sum, which the library tiles onto few workgroups
-_CM_SPLITK = max(1, int(os.environ.get("AIMET_ADA_CM_SPLITK", "1")))
+_GRAPH_ITERS = 10
+
+
+def _pw_step_uses_mfma(cin: int, cout: int) -> bool:
+    """aimet_adaround_pw_step runs (cin, cout) on the matrix cores (else its VALU form)."""
+    uses = ctypes.c_int()
+    _native.call("aimet_adaround_pw_step_uses_mfma", int(cin), int(cout), ctypes.byref(uses))
+    return bool(uses.value)
 
 
 def _is_pointwise(module: torch.nn.Module) -> bool:
@@ -629,10 +623,11 @@ class AdaroundOptimizer:
                                                                 stride, dil, ctypes.byref(sl)))
                 dw_slices = sl.value
         pbias = P(bias) if bias is not None else None
-        pw_dims, cm, gw_parts, pw_slices = None, None, None, None
+        pw_dims, cm, pw_slices = None, None, None
         if mode in ("pointwise", "im2col") and _PW_FUSED != "0" and _LOOP_FORM != "autograd":
             cin, cout, hw_in = inp_data.shape[1], C_out, inp_data[0, 0].numel()
-            wanted = _PW_FUSED == "all" or (hw >= 28 * 28 and (not (cin > cout and hw < 56 * 56) or cin >= 32))
+            wanted = _PW_FUSED == "all" or (hw >= 28 * 28 and (not (cin > cout and hw < 56 * 56) or
+                                                              (cin >= 32 and _pw_step_uses_mfma(cin, cout))))
             if (wanted and cin <= 192 and hw_in == hw and hw % 4 == 0
                     and inp_data.data_ptr() % 16 == 0 and out_data.data_ptr() % 16 == 0 and wq.is_contiguous()):
                 pw_dims = (nb, cin, cout, hw)
@@ -648,33 +643,20 @@ class AdaroundOptimizer:
         if (mode in ("pointwise", "im2col") and pw_dims is None and _PW_CM and hw <= 14 * 14
                 and inp_data[0].numel() % hw == 0):
             cin_cm = inp_data[0].numel() // hw
-            if _PW_CM_FUSED and wq.is_contiguous():
-                slices = ctypes.c_int64()
-                _native.check(lib.aimet_adaround_pw_cm_wgrad_slices(nb, cin_cm, C_out, hw, ctypes.byref(slices)))
-                g_cm = torch.empty((C_out, nb * hw), dtype=torch.float32, device=dev)
-                parts = torch.empty((slices.value,) + tuple(wq.shape), dtype=torch.float32, device=dev)
-                cm = (cin_cm, None, g_cm, parts)
-            else:
-                x_cm = torch.empty((cin_cm, nb * hw), dtype=torch.float32, device=dev)
-                q_cm = torch.empty((C_out, nb * hw), dtype=torch.float32, device=dev)
-                cm = (cin_cm, x_cm, q_cm, torch.empty_like(q_cm))
-                splitk = _CM_SPLITK if (nb * hw) % _CM_SPLITK == 0 else 1
-                gw_parts = torch.empty((splitk,) + tuple(wq.shape), dtype=torch.float32, device=dev) if splitk > 1 \
-                    else None
+            x_cm = torch.empty((cin_cm, nb * hw), dtype=torch.float32, device=dev)
+            q_cm = torch.empty((C_out, nb * hw), dtype=torch.float32, device=dev)
+            cm = (cin_cm, x_cm, q_cm, torch.empty_like(q_cm))
 
         def recon(q, with_bias, s):
             _native.check(lib.aimet_adaround_recon_grad_indexed(P(q), P(out_data), P(idx_all), it_cur, P(g_buf), nb,
                                                                 C_out, hw, pbias if with_bias else None, code, s))
-
-        fuse_wq = _FUSE_SOFT_WEIGHT
 
         def adam_step(gw, s):
             # the Adam step also writes the next iteration's soft-quantized weight into wq (it reads
             # W and the new alpha anyway): no separate forward launch per iteration
             _native.check(lib.aimet_adaround_backward_adam_parts(sq.pw, sq.pa, P(gw), 1, 0, P(exp_avg), P(exp_avg_sq),
                                                                  *sq.shape, sq.pd, sq.po, sq.bw, P(rb_all), it_next,
-                                                                 it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None,
-                                                                 P(bias_corr), s))
+                                                                 it_cur, *adam, loss_ptr, P(wq), P(bias_corr), s))
 
         def soft_weight():   # wq from the current alpha (before the first iteration)
             s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
@@ -682,8 +664,6 @@ class AdaroundOptimizer:
 
         def step():
             s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-            if not fuse_wq:
-                soft_weight()
             if mode == "dw" and _DW_FUSED:
                 # the batch read in place from the caches, q and g never stored; it_next moves here
                 if dw_slices:
@@ -692,7 +672,7 @@ class AdaroundOptimizer:
                                                              P(wq), pbias, None, P(ws), *dims, code, s))
                     _native.check(lib.aimet_adaround_backward_adam_parts(
                         sq.pw, sq.pa, P(ws), dw_slices, dims[6] * dims[6], P(exp_avg), P(exp_avg_sq), *sq.shape,
-                        sq.pd, sq.po, sq.bw, P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None,
+                        sq.pd, sq.po, sq.bw, P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq),
                         P(bias_corr), s))
                     return
                 _native.check(lib.aimet_adaround_dw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
@@ -707,23 +687,11 @@ class AdaroundOptimizer:
                     _native.check(lib.aimet_adaround_backward_adam_parts(
                         sq.pw, sq.pa, ctypes.c_void_p(ws_pw.data_ptr() + 4 * pw_slices[0]), pw_slices[1],
                         sq.w.numel(), P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po, sq.bw, P(rb_all), it_next,
-                        it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, P(bias_corr), s))
+                        it_cur, *adam, loss_ptr, P(wq), P(bias_corr), s))
                     return
                 _native.check(lib.aimet_adaround_pw_step(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
                                                          P(wq), pbias, P(gw_pw), P(ws_pw), *pw_dims, code, s))
                 adam_step(gw_pw, s)
-                return
-            if mode in ("pointwise", "im2col") and cm is not None and cm[1] is None:
-                # channel-major batch on the matrix cores: the gathered GEMM with the reconstruction
-                # gradient, the sliced weight gradient, the Adam step adding the slices
-                cin_cm, _, g_cm, parts = cm
-                _native.check(lib.aimet_adaround_pw_cm_forward(P(inp_data), P(out_data), P(idx_all), it_cur, it_next,
-                                                               P(wq), pbias, P(g_cm), nb, cin_cm, C_out, hw, code, s))
-                _native.check(lib.aimet_adaround_pw_cm_wgrad(P(inp_data), P(idx_all), it_cur, P(g_cm), P(parts),
-                                                             parts.shape[0], nb, cin_cm, C_out, hw, s))
-                _native.check(lib.aimet_adaround_backward_adam_parts(
-                    sq.pw, sq.pa, P(parts), parts.shape[0], 0, P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po,
-                    sq.bw, P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, P(bias_corr), s))
                 return
             if mode in ("pointwise", "im2col") and cm is not None:
                 # channel-major batch: one GEMM per direction over all nb * hw positions
@@ -734,15 +702,7 @@ class AdaroundOptimizer:
                 torch.mm(w2, x_cm, out=q_cm)
                 _native.check(lib.aimet_adaround_recon_grad_indexed_cm(P(q_cm), P(out_data), P(idx_all), it_cur,
                                                                        P(g_cm), nb, C_out, hw, pbias, code, s))
-                if gw_parts is None:
-                    adam_step(torch.mm(g_cm, x_cm.t()).view_as(wq), s)
-                    return
-                S, L = gw_parts.shape[0], (nb * hw) // gw_parts.shape[0]
-                torch.bmm(g_cm.view(C_out, S, L).transpose(0, 1), x_cm.view(cin_cm, S, L).permute(1, 2, 0),
-                          out=gw_parts.view(S, C_out, cin_cm))
-                _native.check(lib.aimet_adaround_backward_adam_parts(
-                    sq.pw, sq.pa, P(gw_parts), S, 0, P(exp_avg), P(exp_avg_sq), *sq.shape, sq.pd, sq.po, sq.bw,
-                    P(rb_all), it_next, it_cur, *adam, loss_ptr, P(wq) if fuse_wq else None, P(bias_corr), s))
+                adam_step(torch.mm(g_cm, x_cm.t()).view_as(wq), s)
                 return
             _native.check(lib.aimet_adaround_gather(P(inp_data), P(out_data), P(inp),
                                                     None if indexed else P(target), P(idx_all), it_cur, it_next, nb,
@@ -816,45 +776,34 @@ class AdaroundOptimizer:
             return g
 
         # layers with two forms (GEMM or MIOpen convolution through autograd): the form is fixed by
-        # _LOOP_FORM (deterministic results); only AIMET_ADA_LOOP_FORM=timed captures both and times
-        # a few replays of each
+        # _LOOP_FORM (deterministic results); the convolution form only when the GEMM form cannot be
+        # captured
         two_forms = mode in ("pointwise", "linear")
         if two_forms and _LOOP_FORM == "autograd":
             mode = "autograd"
-        timed = two_forms and _LOOP_FORM == "timed" and iters >= 50
         candidates = [mode] + (["autograd"] if two_forms and mode != "autograd" else [])
-        best = None
+        graph = None
         for m in candidates:
-            if best is not None and not timed:
-                break   # the fixed form captured: the other is only a fallback
             try:
-                g = capture(m)
+                graph = capture(m)
             except RuntimeError:
                 if m == candidates[0] and len(candidates) > 1:
                     continue   # the GEMM form could not be captured: the convolution form
                 raise
-            if timed:
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                g.replay()
-                e0.record()
-                for _ in range(5):
-                    g.replay()
-                e1.record()
-                e1.synchronize()
-                t = e0.elapsed_time(e1)
-                restart()
-            else:
-                t = 0.0
-            if best is None or t < best[0]:
-                best = (t, m, g)
-            else:
-                del g
-        _, mode, graph = best
+            mode = m
+            break
         AdaroundOptimizer.last_loop_form = mode + ("_fused" if mode in ("pointwise", "im2col") and pw_dims else
-                                                   ("_cm_mfma" if cm[1] is None else "_cm")
-                                                   if mode in ("pointwise", "im2col") and cm else "")
+                                                   "_cm" if mode in ("pointwise", "im2col") and cm else "")
         k = min(_GRAPH_ITERS, chunk)
-        graph_k = capture(mode, k) if k > 1 and iters >= k else None
+        graph_k = None
+        if k > 1 and iters >= k:
+            try:
+                graph_k = capture(mode, k)
+            except RuntimeError:
+                # k iterations could not be captured (graph-pool memory, an autograd form): the
+                # one-iteration graph runs them, the same results
+                graph_k = None
+            restart()
         for a in range(0, iters, chunk):
             b = min(a + chunk, iters)
             if b < iters:

@@ -14,7 +14,6 @@ stack, bench.py), scheduled for the MI355X:
 * activation encodings: one search launch + one synchronisation.
 """
 import ctypes
-import os
 import weakref
 from typing import List, Optional, Sequence, Tuple
 
@@ -26,11 +25,14 @@ from aimet_amd import distributed as D
 from aimet_amd.tensor_quantizer import AimetTensorQuantizer, PendingEncodings, _param_specs
 
 _SIDE = {}
-# tuning knobs (tools/studies/enc_schedule_tune.py): launch order and the side stream's priority
-_SCHEDULE = os.environ.get("AIMET_CAL_SCHEDULE", "params_first")
-_SIDE_PRIORITY = int(os.environ.get("AIMET_CAL_SIDE_PRIORITY", "-1"))
-# the parameters' statistics + search on the activations' stream, ahead of the passes (no overlap)
-_PARAMS_SERIAL = os.environ.get("AIMET_CAL_PARAMS_SERIAL", "0") == "1"
+# the path of compute_encodings_resident: "plan" (a cached CalibrationPlan: every job table prepared
+# once), "native" (aimet_calibrate_launch, the tables built per call) or "phased" (one launch per
+# phase from Python). The last two are what the tests compare the plan with; none is read from the
+# environment. (Other schedules -- the activations' passes first, the parameters serial on one
+# stream, a normal-priority side stream -- measured slower: tools/studies/enc_schedule_tune.py,
+# profiles/r02/compute_encodings_study.txt.)
+_SCHEDULE = "plan"
+_SIDE_PRIORITY = -1   # the side stream's priority: high, so the parameters' work is dispatched first
 
 
 def _side_stream(dev: torch.device) -> torch.cuda.Stream:
@@ -249,7 +251,7 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
             AimetTensorQuantizer.resetEncodingStatsMany(list(act_quantizers) + list(param_quantizers))
         return [], []
     dev = (activations[0] if activations else params[0]).device
-    planned = (_SCHEDULE == "params_first"
+    planned = (_SCHEDULE == "plan"
                and all(type(q) is AimetTensorQuantizer and q.num_channels == 1 for q in act_quantizers)
                and all(type(q) is AimetTensorQuantizer for q in param_quantizers)
                and all(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
@@ -263,13 +265,13 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
         a_pending, p_pending = plan._launch(reset, list(act_quantizers), list(param_quantizers))
         p_res = p_pending.result()
         return a_pending.result(), p_res
-    native = (D._world(group) == 1 and _SCHEDULE == "params_first"
+    native = (D._world(group) == 1 and _SCHEDULE in ("plan", "native")
               and all(type(q) is AimetTensorQuantizer and q.num_channels == 1 for q in act_quantizers)
               and all(type(q) is AimetTensorQuantizer for q in param_quantizers)
               and all(t.dtype == torch.float32 for t in list(activations) + list(params)))
     if native:
         cur = torch.cuda.current_stream(dev)
-        main, side = cur, (cur if _PARAMS_SERIAL else _side_stream(dev))
+        main, side = cur, _side_stream(dev)
         a_pending, p_pending, keep = AimetTensorQuantizer.calibrateResidentAsync(
             act_quantizers, activations, param_quantizers, params, param_ch_axes, act_settings, param_settings,
             reset=reset, main_stream=main, side_stream=side)
@@ -286,19 +288,13 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
     # starts after everything queued there so far (a device-side dependency, no host wait)
     side.wait_stream(cur)
     keep, p_pending = None, None
-    acts_first = _SCHEDULE == "acts_first"
-    if act_quantizers and acts_first:
-        # the HBM-bound activation passes start first; the parameters' short statistics and their
-        # compute-bound searches run beside them on the side stream
-        with torch.cuda.stream(main):
-            D.sharded_update_stats(list(act_quantizers), list(activations), group=group)
     if param_quantizers:
         # enqueued first: the parameters' statistics take the CUs before the activation passes
         with torch.cuda.stream(side):
             keep = AimetTensorQuantizer.updateStatsPerChannelMany(param_quantizers, params, param_ch_axes)
             p_pending = AimetTensorQuantizer.getEncodingsAsync(param_quantizers, *param_settings)
     with torch.cuda.stream(main):
-        if act_quantizers and not acts_first:
+        if act_quantizers:
             D.sharded_update_stats(list(act_quantizers), list(activations), group=group)
         a_pending = AimetTensorQuantizer.getEncodingsAsync(act_quantizers, *act_settings) if act_quantizers else None
     p_res = p_pending.result() if p_pending is not None else []

@@ -519,11 +519,40 @@ __device__ __forceinline__ float block_sum(float v)
     return r;
 }
 
+// reg x the sum of the per-workgroup round-loss partials part[0, nparts), added to *round_loss:
+// each lane adds its parts in order (kFoldBatch loads in flight), then block_sum's fixed tree --
+// one value whatever the workgroups' timing. Called by every thread of one workgroup.
+template <bool CONSUME>
+__device__ __forceinline__ void round_loss_fold(const float* __restrict__ part, uint32_t nparts, float reg,
+                                                float* __restrict__ round_loss)
+{
+    constexpr int kFoldBatch = 8;
+    float t = 0.0f;
+    for (uint32_t i0 = threadIdx.x; i0 < nparts; i0 += kBlock * kFoldBatch)
+    {
+        float v[kFoldBatch];
+#pragma unroll
+        for (int u = 0; u < kFoldBatch; ++u)
+        {
+            const uint32_t i = i0 + u * kBlock;
+            v[u]             = i < nparts ? (CONSUME ? consume_f32(part + i) : part[i]) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < kFoldBatch; ++u)
+            if (i0 + u * kBlock < nparts)
+                t += v[u];
+    }
+    t = block_sum(t);
+    if (threadIdx.x == 0)
+        atomicAdd(round_loss, reg * t);
+}
+
 // The round loss of one launch: reg x (the per-workgroup sums folded in workgroup order by the
 // workgroup that finishes last), one add to *round_loss per launch, so the value does not depend
 // on the workgroups' timing (ticket_alloc; `part` holds gridDim.x floats, handed over write-through:
-// common.hpp publish_f32). Without a ticket, one atomic add per workgroup. Called by every thread
-// of every workgroup.
+// common.hpp publish_f32). Without a ticket (the capture pool used up: upload.cpp fold_buffers) the
+// partials are only stored and round_loss_fold_kernel, launched next, folds them the same way: the
+// same value. Called by every thread of every workgroup.
 __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __restrict__ round_loss,
                                                float* __restrict__ part, unsigned* __restrict__ ticket)
 {
@@ -531,7 +560,7 @@ __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __r
     if (!ticket)
     {
         if (threadIdx.x == 0)
-            atomicAdd(round_loss, reg * s);
+            part[blockIdx.x] = s;
         return;
     }
     __shared__ int last;
@@ -544,25 +573,21 @@ __device__ __forceinline__ void round_loss_add(float loss, float reg, float* __r
     if (!last)
         return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the ticket
-    constexpr int kFoldBatch = 8;   // loads in flight per lane; each lane adds its parts in order
-    float t = 0.0f;
-    for (uint32_t i0 = threadIdx.x; i0 < gridDim.x; i0 += kBlock * kFoldBatch)
-    {
-        float v[kFoldBatch];
-#pragma unroll
-        for (int u = 0; u < kFoldBatch; ++u)
-            v[u] = i0 + u * kBlock < gridDim.x ? consume_f32(part + i0 + u * kBlock) : 0.0f;
-#pragma unroll
-        for (int u = 0; u < kFoldBatch; ++u)
-            if (i0 + u * kBlock < gridDim.x)
-                t += v[u];
-    }
-    t = block_sum(t);
+    round_loss_fold<true>(part, gridDim.x, reg, round_loss);
     if (threadIdx.x == 0)
-    {
-        atomicAdd(round_loss, reg * t);
         ticket_reset(ticket + kTicketGroups);
-    }
+}
+
+// the fold of round_loss_add's partials as its own launch (no ticket); reg as the backward read it:
+// the argument, reg_beta[0], or (the loop's Adam step) reg_beta[3 (it_next[0] - 1)]
+__global__ __launch_bounds__(kBlock) void round_loss_fold_kernel(const float* __restrict__ part, uint32_t nparts,
+                                                                 float reg, const float* __restrict__ reg_beta,
+                                                                 const int64_t* __restrict__ it_next,
+                                                                 float* __restrict__ round_loss)
+{
+    const float r = reg_beta ? (it_next ? reg_beta[3 * (it_next[0] - 1)] : reg_beta[0]) : reg;
+    if (r != 0.0f)
+        round_loss_fold<false>(part, nparts, r, round_loss);
 }
 
 // backward: grid-stride over tiles of kBlock x U quads (U quads in flight per lane, 3 x 16-B loads
@@ -677,25 +702,44 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
 }
 
 // the round loss's per-workgroup partials and completion ticket for one launch (round_loss_add);
-// none when no loss is requested. The partials are released after the launch that uses them.
+// none when no loss is requested. Without a ticket (the capture pool used up), partials from the
+// scratch allocator (a graph memory node inside a capture) and a fold launch after the kernel
+// (finish()): the same value either way. The partials are released after the launch that uses them.
 struct LossFold
 {
     float* part      = nullptr;
     unsigned* ticket = nullptr;
     FoldBuffers fb;
     hipStream_t s;
-    LossFold(const float* round_loss, unsigned grid, hipStream_t st) : s(st)
+    unsigned grid = 0;
+    bool scratch  = false;
+    LossFold(const float* round_loss, unsigned g, hipStream_t st) : s(st), grid(g)
     {
         if (!round_loss)
             return;
         fb     = fold_buffers(st, kTicketGroups + 1, grid);
         ticket = fb.ticket;
         part   = fb.part;
+        if (!ticket)
+        {
+            part    = static_cast<float*>(scratch_alloc(sizeof(float) * grid, st));
+            scratch = true;
+        }
+    }
+    // after the backward's launch: the fold of its partials when they had no ticket
+    void finish(float reg, const float* reg_beta, const int64_t* it_next, float* round_loss)
+    {
+        if (!scratch)
+            return;
+        round_loss_fold_kernel<<<1, kBlock, 0, s>>>(part, grid, reg, reg_beta, it_next, round_loss);
+        AIMET_LAUNCH_CHECK();
     }
     ~LossFold()
     {
         try
         {
+            if (scratch)
+                scratch_free(part, s);
             fold_buffers_release(fb, s);
         }
         catch (...)   // a failing event record: the block is leaked, never handed out again
@@ -1167,13 +1211,9 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
             aligned16(ga))
         {
             uint32_t nq = (uint32_t) (n / 4);
-            // quads in flight per lane (AIMET_ADA_BWD_U = 1 / 2 / 4 for tuning; 1 measured best,
-            // 2 equal within noise: profiles/r04/ada_bwd_tune_tail_flag.jsonl)
-            static const int U = [] {
-                const char* e = getenv("AIMET_ADA_BWD_U");
-                const int u   = e ? atoi(e) : 1;
-                return u == 2 || u == 4 ? u : 1;
-            }();
+            // one quad in flight per lane (1 measured best, 2 equal within noise, 4 slower:
+            // profiles/r04/ada_bwd_tune_tail_flag.jsonl)
+            constexpr int U   = 1;
             int64_t blocks    = ceil_div(nq, kBlock * U);
             const unsigned gx = (unsigned) (blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid);
             LossFold lf(round_loss, gx, st);
@@ -1192,13 +1232,9 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
                 else
                     wl ? launch(adaround_bwd_vec_kernel<UU, true, false>) : launch(adaround_bwd_vec_kernel<UU, false, false>);
             };
-            if (U == 1)
-                go(std::integral_constant<int, 1> {});
-            else if (U == 4)
-                go(std::integral_constant<int, 4> {});
-            else
-                go(std::integral_constant<int, 2> {});
+            go(std::integral_constant<int, U> {});
             AIMET_LAUNCH_CHECK();
+            lf.finish(p.reg, reg_beta, nullptr, round_loss);
         }
         else
         {
@@ -1207,6 +1243,7 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
             adaround_bwd_kernel<<<gx, kBlock, 0, st>>>(w, alpha, g, ga, (uint32_t) n, map, delta, offset, p, round_loss,
                                                       reg_beta, lf.part, lf.ticket);
             AIMET_LAUNCH_CHECK();
+            lf.finish(p.reg, reg_beta, nullptr, round_loss);
         }
     });
 }
@@ -1448,6 +1485,7 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
         else
             wl ? launch(adaround_bwd_adam_kernel<false, true>) : launch(adaround_bwd_adam_kernel<false, false>);
         AIMET_LAUNCH_CHECK();
+        lf.finish(0.0f, reg_beta_all, it_next, round_loss);
     });
 }
 

@@ -96,6 +96,16 @@ int aimet_device_count(void)
     return rc == AIMET_OK ? n : rc;
 }
 
+int aimet_capture_pool_limit(int64_t arena_floats, int64_t* previous)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(arena_floats >= 0, "negative limit");
+        const size_t prev = capture_pool_limit((size_t) arena_floats);
+        if (previous)
+            *previous = (int64_t) prev;
+    });
+}
+
 int aimet_get_computed_encodings(int32_t bw, double mn, double mx, int sym, int strict, int unsign,
                                  aimet_tf_encoding* out)
 {

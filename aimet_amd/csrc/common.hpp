@@ -139,8 +139,6 @@ struct FastDiv
 // Reference element arithmetic (trim_functions.cpp:140-171, x86-64 glibc semantics).
 // ------------------------------------------------------------------------------------------
 
-// glibc fminf/fmaxf (x86-64): a NaN operand yields the other operand; otherwise
-// minss/maxss, i.e. the SECOND operand on ties (matters for +-0).
 // ---- hand-off of per-workgroup partials to the last-arriving workgroup (one launch) ------------
 // The per-XCD L2s are not coherent and a CU's L1 is never refreshed by another CU's stores. The
 // partials are stored write-through (agent-scope relaxed atomic store: a `global_store ... sc1`),
@@ -194,6 +192,8 @@ __device__ __forceinline__ void ticket_reset(unsigned* ticket)
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// glibc fminf/fmaxf (x86-64): a NaN operand yields the other operand; otherwise
+// minss/maxss, i.e. the SECOND operand on ties (matters for +-0).
 __device__ __forceinline__ float glibc_fminf(float x, float y)
 {
     return (x < y || __builtin_isnan(y)) ? x : y;
@@ -223,6 +223,8 @@ struct FoldBuffers
 };
 FoldBuffers fold_buffers(hipStream_t s, unsigned tickets, size_t part_floats);
 void fold_buffers_release(const FoldBuffers& f, hipStream_t s);
+// aimet_capture_pool_limit: the capture arena's cap on the current device (returns the previous one)
+size_t capture_pool_limit(size_t arena_floats);
 void scratch_free(void* p, hipStream_t s);
 
 struct QdqParams

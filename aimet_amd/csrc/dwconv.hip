@@ -519,13 +519,9 @@ bool dw_quads(int64_t K, int64_t stride, int64_t dil, int64_t OW)
 int64_t wgrad_slices(int64_t N, int64_t C, int64_t OH, int64_t OW, uint32_t* per_out, bool quads = false)
 {
     const int64_t np   = N * OH * OW;
-    // positions per lane per slice (16; AIMET_TUNE_DW_PER: tuning experiments only -- it changes the
-    // summation order of the weight gradient, for the fused and the unfused path alike)
-    static const int64_t ppl = [] {
-        const char* e = getenv("AIMET_TUNE_DW_PER");
-        const int64_t v = e ? atoll(e) : 16;
-        return v >= 1 && v <= 256 ? v : (int64_t) 16;
-    }();
+    // positions per lane per slice (it sets the summation order of the weight gradient, for the
+    // fused and the unfused path alike)
+    constexpr int64_t ppl = 16;
     int64_t S          = ceil_div(np, (int64_t) kBlock * ppl);
     const int64_t want = ceil_div(2048, C);
     if (S < want)
@@ -652,20 +648,12 @@ void dw_step(const float* x_cache, const float* t_cache, const int64_t* idx_all,
     // aimet_adaround_recon_grad_indexed's scale: 2 / (number of dim-1 norms)
     DwStep a {x_cache, t_cache, idx_all, it_cur, it_next, w, bias, (float) (2.0 / (double) (N * OH * OW)), act};
     dim3 grid((unsigned) S, (unsigned) C);
-    static const int u = [] {
-        const char* e = getenv("AIMET_TUNE_DW_U");   // tuning experiments only (same results)
-        return e ? atoi(e) : 0;
-    }();
+    // (1, 2 or 8 positions per lane in flight instead of the default measured no faster:
+    // profiles/r03/dw_step_tune.jsonl)
     if (quads && stride == 1)
         dw_step_quad_kernel<1><<<grid, kBlock, 0, st>>>(a, partial, s, per);
     else if (quads)
         dw_step_quad_kernel<2><<<grid, kBlock, 0, st>>>(a, partial, s, per);
-    else if (K == 3 && u == 1)
-        dw_step_kernel<3, 1><<<grid, kBlock, 0, st>>>(a, partial, s, per);
-    else if (K == 3 && u == 2)
-        dw_step_kernel<3, 2><<<grid, kBlock, 0, st>>>(a, partial, s, per);
-    else if (K == 3 && u == 8)
-        dw_step_kernel<3, 8><<<grid, kBlock, 0, st>>>(a, partial, s, per);
     else if (K == 3)
         dw_step_kernel<3><<<grid, kBlock, 0, st>>>(a, partial, s, per);
     else

@@ -263,25 +263,13 @@ __global__ __launch_bounds__(kBlock) void lg_fwd_kernel(const float* __restrict_
     }
 }
 
-// quads per lane of lg_fwd_kernel's vec form (1, 2 or 4; AIMET_TUNE_LG_FWD_QUADS for experiments)
-int lg_fwd_quads()
-{
-    static int v = [] {
-        const char* e = getenv("AIMET_TUNE_LG_FWD_QUADS");   // tuning experiments only
-        const int q   = e ? atoi(e) : 2;
-        return (q == 1 || q == 4) ? q : 2;
-    }();
-    return v;
-}
-
 template <int OUT>
 void launch_lg_fwd(const float* x, void* y, int64_t n, LgChannel map, const float* delta, const float* offset,
                    float steps, bool vec, LgEnc enc, hipStream_t st)
 {
-    if (vec && lg_fwd_quads() == 4)
-        lg_fwd_kernel<OUT, 4><<<(unsigned) ceil_div(n / 4, kBlock * 4), kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta,
-                                                                                       offset, steps, 1, enc);
-    else if (vec && lg_fwd_quads() == 2)
+    // two quads per lane in the vec form (one: 4.4 vs 5.4 TB/s on the Llama-3-8B weights; four: no
+    // faster, profiles/r02/llama_qat_kernel_stats*.csv)
+    if (vec)
         lg_fwd_kernel<OUT, 2><<<(unsigned) ceil_div(n / 4, kBlock * 2), kBlock, 0, st>>>(x, y, (uint32_t) n, map, delta,
                                                                                        offset, steps, 1, enc);
     else
@@ -471,12 +459,10 @@ __device__ __forceinline__ void range_grads_one(float A, float B, float D, uint3
 // The per-tensor backward's ntiles partial triples folded as one triple, whichever kernel folds
 // them (lg_bwd_fold_one, or the kernel's last workgroup): lane l sums tiles l, l + kBlock, ... in
 // order, then the fixed shuffle tree of block_reduce -- one result whatever the scheduling; the
-// range gradients follow when requested. Called by every thread of one workgroup. CONSUME: the
-// partials were written write-through by other workgroups of the same launch (agent-scope loads).
+// range gradients follow when requested. Called by every thread of one workgroup.
 // (A fold in two levels -- each group of tiles folded by its last-arriving workgroup -- summed in
 // another order whose error on Llama-3-8B's lm_head output range gradient reached 2.45 units of the
 // stated bound, above the 2 the tests assert, and was no faster: profiles/r04/README.md.)
-template <bool CONSUME>
 __device__ __forceinline__ void fold_partials(const float* __restrict__ partial, int64_t nparts,
                                               float* __restrict__ sums, const LgRange& range)
 {
@@ -492,9 +478,9 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ partial,
         {
             const int64_t i = i0 + (int64_t) u * kBlock;
             const float* p  = partial + 3 * (i < nparts ? i : 0);
-            a[u]            = CONSUME ? consume_f32(p) : p[0];
-            b[u]            = CONSUME ? consume_f32(p + 1) : p[1];
-            d[u]            = CONSUME ? consume_f32(p + 2) : p[2];
+            a[u]            = p[0];
+            b[u]            = p[1];
+            d[u]            = p[2];
         }
 #pragma unroll
         for (int u = 0; u < kFoldBatch; ++u)
@@ -516,40 +502,22 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ partial,
     }
 }
 
-// a tile's partial triple, stored write-through for a fold in the same launch
-__device__ __forceinline__ void publish_sums(float* p, const Sums& t)
+// a tile's partial triple (folded by the next launch)
+__device__ __forceinline__ void store_sums(float* p, const Sums& t)
 {
-    publish_f32(p + 0, t.a);
-    publish_f32(p + 1, t.b);
-    publish_f32(p + 2, t.d);
-}
-
-// The per-tensor backward's fold in the workgroup that finishes last (AIMET_LG_FOLD_IN_KERNEL=1):
-// thread 0 of each workgroup (the one that published its tiles' partials) drains them and arrives
-// (arrive_is_last_grid); the workgroup arriving last runs fold_partials -- the arithmetic of
-// lg_bwd_fold_one, so the same bits -- and leaves the ticket at zero (ticket_alloc). Called by every
-// thread of every workgroup; none waits for another, so they need not be co-resident.
-__device__ __forceinline__ void fold_in_last_workgroup(const float* partial, int64_t nparts, float* sums,
-                                                       const LgRange& range, unsigned* ticket)
-{
-    __shared__ int last;
-    if (threadIdx.x == 0)
-        last = arrive_is_last_grid(ticket);
-    __syncthreads();
-    if (!last)
-        return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the ticket
-    fold_partials<true>(partial, nparts, sums, range);
-    if (threadIdx.x == 0)
-        ticket_reset(ticket + kTicketGroups);
+    p[0] = t.a;
+    p[1] = t.b;
+    p[2] = t.d;
 }
 
 // per-tensor (C == 1), tile form: workgroup b owns the kLgTile consecutive elements
 // [b * kLgTile, (b + 1) * kLgTile); lane l of it takes the 8-element groups u * kBlock + l
 // (u < kLgTileSteps), every load of the tile issued before any arithmetic. The per-lane sums run
 // in (u, element) order, then the fixed shuffle tree of block_reduce, one partial triple per
-// workgroup, folded in workgroup order by lg_bwd_fold_one (deterministic). lg_bwd16_tensor_kernel
-// maps elements to lanes and workgroups identically, so the 16-bit path sums exactly what this one
+// workgroup, folded in workgroup order by lg_bwd_fold_one (deterministic; the fold in the kernel's
+// last-arriving workgroup measured 7-8 us slower per call than its own 4 us launch -- every
+// workgroup draining its stores and taking a ticket, profiles/r04/README.md -- and was removed).
+// lg_bwd16_tensor_kernel maps elements to lanes and workgroups identically, so the 16-bit path sums exactly what this one
 // sums. (A grid-stride form with one pair of loads per lane in flight ran at 0.47 of HBM peak on
 // the 16-bit Llama-3-8B activations.)
 constexpr int kLgTileSteps = 2;
@@ -568,9 +536,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
                                                                const float* __restrict__ g, float* __restrict__ gx,
                                                                int64_t n, const float* __restrict__ delta,
                                                                const float* __restrict__ offset, float steps,
-                                                               float* __restrict__ sums, int vec, int64_t ntiles,
-                                                               float* __restrict__ folded, LgRange range,
-                                                               unsigned* __restrict__ ticket)
+                                                               float* __restrict__ sums, int vec, int64_t ntiles)
 {
     constexpr int64_t kTile = (int64_t) kBlock * 8 * STEPS;
     const float dl = delta[0], o = offset[0], rcp = lg_recip(dl);
@@ -627,92 +593,52 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tensor_kernel(const float* __re
         }
         Sums t = block_reduce(s);
         if (threadIdx.x == 0)
-            publish_sums(sums + 3 * tile, t);
+            store_sums(sums + 3 * tile, t);
     }
-    if (ticket)   // uniform: the fold in the last workgroup (else lg_bwd_fold_one follows)
-        fold_in_last_workgroup(sums, ntiles, folded, range, ticket);
 }
 
 // Launch shape of the per-tensor backward kernels (fp32 and 16-bit use the same, so their sums
-// stay identical): STEPS 8-element groups per lane and tile, grid = the tile count, or at most
-// `cap` workgroups looping over the tiles. AIMET_TUNE_LG_BWD="steps:cap" (tuning experiments).
+// stay identical): kLgTileSteps 8-element groups per lane and tile, one workgroup per tile (fp32) or
+// kLgBwd16Grid workgroups looping over the tiles (16-bit, pipelined)
 struct LgBwdLaunch
 {
-    int steps;
     int64_t ntiles;
     unsigned grid, grid16;
 };
 constexpr int64_t kLgBwd16Grid = 2048;
 
-// the per-tensor backward's fold as its own launch (default) or in the kernel's last workgroup
-// (AIMET_LG_FOLD_IN_KERNEL=1; the same arithmetic, the same bits). Measured on the 16-bit Llama-3-8B
-// activation gradients (profiles/r04/README.md): the in-kernel form, every workgroup draining its
-// stores and taking a ticket, cost 7-8 us per call against a 4 us fold launch.
-bool lg_fold_in_kernel()
-{
-    static const bool v = [] {
-        const char* e = getenv("AIMET_LG_FOLD_IN_KERNEL");
-        return e && e[0] == '1';
-    }();
-    return v;
-}
-
 LgBwdLaunch lg_bwd_launch(int64_t n)
 {
-    static const std::pair<int, int64_t> shape = [] {
-        const char* e = getenv("AIMET_TUNE_LG_BWD");
-        int st = kLgTileSteps;
-        long long cap = 0;
-        if (e)
-            sscanf(e, "%d:%lld", &st, &cap);
-        if (st != 1 && st != 2 && st != 4)
-            st = kLgTileSteps;
-        // a capped grid stays a multiple of kTicketGroups: every tile of a workgroup is then in the
-        // workgroup's fold group (fold_in_last_workgroup)
-        cap = cap > 0 ? std::max<long long>(kTicketGroups, cap / kTicketGroups * kTicketGroups) : 0;
-        return std::make_pair(st, (int64_t) cap);
-    }();
     LgBwdLaunch L;
     // (one 8-element group per lane and tile for calls of <= 4 M elements -- twice the workgroups --
     // measured no faster, 5.5 vs 5.2 us at 2 M elements, and its summation order put Llama-3-8B's
-    // lm_head output range gradient at 2.45 units of the stated bound: not used)
-    L.steps  = shape.first;
-    L.ntiles = ceil_div(n, (int64_t) kBlock * 8 * L.steps);
+    // lm_head output range gradient at 2.45 units of the stated bound: not used; four groups kept
+    // the bound but ran slower, profiles/r04/lg16_steps2_vs_steps4.jsonl)
+    L.ntiles = ceil_div(n, (int64_t) kBlock * 8 * kLgTileSteps);
     AIMET_REQUIRE(L.ntiles < (int64_t(1) << 31), "too many elements");
-    L.grid = (unsigned) (shape.second > 0 && L.ntiles > shape.second ? shape.second : L.ntiles);
-    // the pipelined 16-bit kernel: one resident round of workgroups unless a cap is given
-    const int64_t cap16 = shape.second > 0 ? shape.second : kLgBwd16Grid;
-    L.grid16 = (unsigned) (L.ntiles > cap16 ? cap16 : L.ntiles);
+    L.grid   = (unsigned) L.ntiles;
+    L.grid16 = (unsigned) (L.ntiles > kLgBwd16Grid ? kLgBwd16Grid : L.ntiles);
     return L;
 }
 
-// f(integral_constant<STEPS>, integral_constant<MODE>) for the runtime tile steps and backward
-// mode: the per-tensor kernels are compiled per mode (lg_bwd_term_m), so their element loops carry
-// only the sums that mode needs
+// f(integral_constant<MODE>) for the backward mode: the per-tensor kernels are compiled per mode
+// (lg_bwd_term_m), so their element loops carry only the sums that mode needs
 template <class F>
-void lg_bwd_dispatch(int steps, int mode, F&& f)
+void lg_bwd_dispatch(int mode, F&& f)
 {
-    auto with_mode = [&](auto st) {
-        if (mode == 2)
-            f(st, std::integral_constant<int, 2> {});
-        else if (mode == 1)
-            f(st, std::integral_constant<int, 1> {});
-        else
-            f(st, std::integral_constant<int, 0> {});
-    };
-    if (steps == 1)
-        with_mode(std::integral_constant<int, 1> {});
-    else if (steps == 4)
-        with_mode(std::integral_constant<int, 4> {});
+    if (mode == 2)
+        f(std::integral_constant<int, 2> {});
+    else if (mode == 1)
+        f(std::integral_constant<int, 1> {});
     else
-        with_mode(std::integral_constant<int, kLgTileSteps> {});
+        f(std::integral_constant<int, 0> {});
 }
 
-// the per-tensor backward's fold as its own launch (the default; see lg_fold_in_kernel)
+// the per-tensor backward's fold, its own launch
 __global__ __launch_bounds__(kBlock) void lg_bwd_fold_one(const float* __restrict__ partial, int64_t ntiles,
                                                           float* __restrict__ sums, LgRange range)
 {
-    fold_partials<false>(partial, ntiles, sums, range);
+    fold_partials(partial, ntiles, sums, range);
 }
 
 // per-channel: one workgroup per channel of [outer][C][K], sums written directly
@@ -892,13 +818,14 @@ __global__ __launch_bounds__(kBlock) void lg_bwd_tile_fold(const float* __restri
 typedef unsigned short u16x8 __attribute__((ext_vector_type(8)));
 
 // lg_fwd16_kernel's default shape: kLgFwd16Vecs 16-B vectors (8 elements) per lane and tile,
-// kLgFwd16Grid workgroups looping over the tiles (AIMET_TUNE_LG16_FWD for experiments)
+// kLgFwd16Grid workgroups looping over the tiles (other shapes measured slower, profiles/r03/
+// lg16_kernel_stats.csv, profiles/r04/lg16_*.jsonl)
 constexpr int kLgFwd16Vecs     = 1;
 constexpr int64_t kLgFwd16Grid  = 2048;   // workgroups: 8 per CU, one resident round
 constexpr int64_t kLgFwd16Tile = (int64_t) kBlock * 8 * kLgFwd16Vecs;
 
 // 16-B loads / stores of the 16-bit kernels: nontemporal (NT, the streaming default) or through
-// the caches (AIMET_TUNE_LG16_NT=0, for activations still resident in the MALL)
+// the caches (measured no faster for activations still resident in the MALL, profiles/r04)
 template <bool NT>
 __device__ __forceinline__ u16x8 ld16(const u16x8* p)
 {
@@ -914,15 +841,6 @@ __device__ __forceinline__ void st16(u16x8 v, u16x8* p)
         __builtin_nontemporal_store(v, p);
     else
         *p = v;
-}
-
-int lg16_nt()
-{
-    static const int v = [] {
-        const char* e = getenv("AIMET_TUNE_LG16_NT");
-        return e ? (atoi(e) != 0) : 1;
-    }();
-    return v;
 }
 
 template <int IO, int V, int BLOCK, bool NT>
@@ -1031,9 +949,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
                                                                  unsigned short* __restrict__ gx, int64_t n,
                                                                  const float* __restrict__ delta,
                                                                  const float* __restrict__ offset, float steps,
-                                                                 float* __restrict__ partial, int vec, int64_t ntiles,
-                                                                 float* __restrict__ folded, LgRange range,
-                                                                 unsigned* __restrict__ ticket)
+                                                                 float* __restrict__ partial, int vec, int64_t ntiles)
 {
     constexpr int64_t kTile = (int64_t) kBlock * 8 * STEPS;
     // the first tile's loads go out before the encoding is read: they do not depend on it, and on
@@ -1074,7 +990,7 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
         }
         Sums t3 = block_reduce(s);
         if (threadIdx.x == 0)
-            publish_sums(partial + 3 * t, t3);
+            store_sums(partial + 3 * t, t3);
     };
     if (tile < nfull)
     {
@@ -1114,10 +1030,8 @@ __global__ __launch_bounds__(kBlock) void lg_bwd16_tensor_kernel(const unsigned 
             }
         Sums t3 = block_reduce(s);
         if (threadIdx.x == 0)
-            publish_sums(partial + 3 * tile, t3);
+            store_sums(partial + 3 * tile, t3);
     }
-    if (ticket)   // uniform: the fold in the last workgroup (else lg_bwd_fold_one follows)
-        fold_in_last_workgroup(partial, ntiles, folded, range, ticket);
 }
 
 // ---- the small per-channel vectors around the passes, one launch each -----------------------
@@ -1448,26 +1362,16 @@ int aimet_lg_backward(const float* x, const float* grad, float* grad_x, float* s
             bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                          reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
             const LgBwdLaunch L = lg_bwd_launch(n);
-            // the partials and the ticket of the fold in the last workgroup (its own launch without one)
-            const FoldBuffers fb = fold_buffers(s, kTicketGroups + 1, 3 * (size_t) (L.ntiles + kTicketGroups));
-            float* partial      = fb.part ? fb.part : static_cast<float*>(scratch_alloc(sizeof(float) * 3 * (L.ntiles + kTicketGroups), s));
+            float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
             const int v         = vec ? 1 : 0;
-
-            unsigned* ticket = lg_fold_in_kernel() ? fb.ticket : nullptr;
-            lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
-                lg_bwd_tensor_kernel<decltype(st)::value, decltype(md)::value><<<L.grid, kBlock, 0, s>>>(
-                    x, grad, grad_x, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
+            lg_bwd_dispatch(mode, [&](auto md) {
+                lg_bwd_tensor_kernel<kLgTileSteps, decltype(md)::value><<<L.grid, kBlock, 0, s>>>(
+                    x, grad, grad_x, n, delta, offset, num_steps, partial, v, L.ntiles);
             });
             AIMET_LAUNCH_CHECK();
-            if (!ticket)
-            {
-                lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, L.ntiles, sums, range);
-                AIMET_LAUNCH_CHECK();
-            }
-            if (fb.part)
-                fold_buffers_release(fb, s);
-            else
-                scratch_free(partial, s);
+            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, L.ntiles, sums, range);
+            AIMET_LAUNCH_CHECK();
+            scratch_free(partial, s);
             return;
         }
         else if (K % 1024 == 0 && n < (int64_t(1) << 31) && C < 65536 &&
@@ -1544,60 +1448,16 @@ void forward_16(const void* x, void* y, int64_t n, int io_dtype, const float* de
     const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(y)) & 15) == 0;
     auto xs = static_cast<const unsigned short*>(x);
     auto ys = static_cast<unsigned short*>(y);
-    // launch shape: V 16-B vectors per lane, BLOCK lanes per workgroup, grid = the tile count or
-    // at most `cap` workgroups looping over the tiles; AIMET_TUNE_LG16_FWD="V:BLOCK:cap" (tuning)
-    struct Shape
-    {
-        int v, block;
-        int64_t cap;
-    };
-    static const Shape sh = [] {
-        Shape r {kLgFwd16Vecs, kBlock, kLgFwd16Grid};
-        const char* e = getenv("AIMET_TUNE_LG16_FWD");
-        long long cap = 0;
-        if (e)
-            sscanf(e, "%d:%d:%lld", &r.v, &r.block, &cap);
-        if (r.v != 1 && r.v != 2 && r.v != 4 && r.v != 8)
-            r.v = kLgFwd16Vecs;
-        if (r.block != 256 && r.block != 512 && r.block != 1024)
-            r.block = kBlock;
-        if (e)
-            r.cap = cap > 0 ? cap : 0;
-        return r;
-    }();
-    const int64_t ntiles = ceil_div(n, (int64_t) sh.block * 8 * sh.v);
-    const unsigned grid  = (unsigned) (sh.cap > 0 && ntiles > sh.cap ? sh.cap : ntiles);
+    // kLgFwd16Vecs 16-B vectors per lane, kLgFwd16Grid workgroups looping over the tiles
+    const int64_t ntiles = ceil_div(n, kLgFwd16Tile);
+    const unsigned grid  = (unsigned) (ntiles > kLgFwd16Grid ? kLgFwd16Grid : ntiles);
     const int v          = vec ? 1 : 0;
-#define AIMET_LG16_FWD(V, B)                                                                                        \
-    if (sh.v == V && sh.block == B)                                                                                 \
-    {                                                                                                               \
-        if (io_dtype == IO_F16 && lg16_nt())                                                                        \
-            lg_fwd16_kernel<IO_F16, V, B><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc, ntiles);  \
-        else if (io_dtype == IO_F16)                                                                                \
-            lg_fwd16_kernel<IO_F16, V, B, false><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc,    \
-                                                                    ntiles);                                       \
-        else if (lg16_nt())                                                                                         \
-            lg_fwd16_kernel<IO_BF16, V, B><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc, ntiles); \
-        else                                                                                                        \
-            lg_fwd16_kernel<IO_BF16, V, B, false><<<grid, B, 0, st>>>(xs, ys, n, delta, offset, num_steps, v, enc,   \
-                                                                     ntiles);                                      \
-    }                                                                                                               \
+    if (io_dtype == IO_F16)
+        lg_fwd16_kernel<IO_F16, kLgFwd16Vecs, kBlock><<<grid, kBlock, 0, st>>>(xs, ys, n, delta, offset, num_steps, v,
+                                                                              enc, ntiles);
     else
-    // one chain of else-ifs: exactly one launch per call
-    AIMET_LG16_FWD(1, 256) AIMET_LG16_FWD(2, 256) AIMET_LG16_FWD(4, 256) AIMET_LG16_FWD(8, 256)
-    AIMET_LG16_FWD(1, 512) AIMET_LG16_FWD(2, 512) AIMET_LG16_FWD(4, 512)
-    AIMET_LG16_FWD(1, 1024) AIMET_LG16_FWD(2, 1024)
-    {
-        // a combination not instantiated: the default shape
-        const int64_t nt = ceil_div(n, kLgFwd16Tile);
-        if (io_dtype == IO_F16)
-            lg_fwd16_kernel<IO_F16, kLgFwd16Vecs, kBlock><<<(unsigned) nt, kBlock, 0, st>>>(xs, ys, n, delta, offset,
-                                                                                       num_steps, v, enc, nt);
-        else
-            lg_fwd16_kernel<IO_BF16, kLgFwd16Vecs, kBlock><<<(unsigned) nt, kBlock, 0, st>>>(xs, ys, n, delta, offset,
-                                                                                        num_steps, v, enc, nt);
-    }
-#undef AIMET_LG16_FWD
+        lg_fwd16_kernel<IO_BF16, kLgFwd16Vecs, kBlock><<<grid, kBlock, 0, st>>>(xs, ys, n, delta, offset, num_steps, v,
+                                                                               enc, ntiles);
     AIMET_LAUNCH_CHECK();
 }
 
@@ -1792,40 +1652,24 @@ int aimet_lg_backward_16(const void* x, const void* grad, void* grad_x, float* s
         const bool vec = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(grad) |
                            reinterpret_cast<uintptr_t>(grad_x)) & 15) == 0;
         const LgBwdLaunch L = lg_bwd_launch(n);   // the fp32 kernel's tiles
-        // the partials and the ticket of the fold in the last workgroup (its own launch without one)
-        const FoldBuffers fb = fold_buffers(s, kTicketGroups + 1, 3 * (size_t) (L.ntiles + kTicketGroups));
-        float* partial      = fb.part ? fb.part : static_cast<float*>(scratch_alloc(sizeof(float) * 3 * (L.ntiles + kTicketGroups), s));
+        float* partial      = static_cast<float*>(scratch_alloc(sizeof(float) * 3 * L.ntiles, s));
         auto xs = static_cast<const unsigned short*>(x);
         auto gs = static_cast<const unsigned short*>(grad);
         auto os = static_cast<unsigned short*>(grad_x);
         const int v = vec ? 1 : 0;
-
-        unsigned* ticket = lg_fold_in_kernel() ? fb.ticket : nullptr;
-        lg_bwd_dispatch(L.steps, mode, [&](auto st, auto md) {
-            constexpr int ST = decltype(st)::value, MD = decltype(md)::value;
-            if (io_dtype == IO_F16 && lg16_nt())
-                lg_bwd16_tensor_kernel<IO_F16, ST, MD><<<L.grid16, kBlock, 0, s>>>(
-                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
-            else if (io_dtype == IO_F16)
-                lg_bwd16_tensor_kernel<IO_F16, ST, MD, false><<<L.grid16, kBlock, 0, s>>>(
-                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
-            else if (lg16_nt())
-                lg_bwd16_tensor_kernel<IO_BF16, ST, MD><<<L.grid16, kBlock, 0, s>>>(
-                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
+        lg_bwd_dispatch(mode, [&](auto md) {
+            constexpr int MD = decltype(md)::value;
+            if (io_dtype == IO_F16)
+                lg_bwd16_tensor_kernel<IO_F16, kLgTileSteps, MD><<<L.grid16, kBlock, 0, s>>>(
+                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles);
             else
-                lg_bwd16_tensor_kernel<IO_BF16, ST, MD, false><<<L.grid16, kBlock, 0, s>>>(
-                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles, sums, range, ticket);
+                lg_bwd16_tensor_kernel<IO_BF16, kLgTileSteps, MD><<<L.grid16, kBlock, 0, s>>>(
+                    xs, gs, os, n, delta, offset, num_steps, partial, v, L.ntiles);
         });
         AIMET_LAUNCH_CHECK();
-        if (!ticket)
-        {
-            lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, L.ntiles, sums, range);
-            AIMET_LAUNCH_CHECK();
-        }
-        if (fb.part)
-            fold_buffers_release(fb, s);
-        else
-            scratch_free(partial, s);
+        lg_bwd_fold_one<<<1, kBlock, 0, s>>>(partial, L.ntiles, sums, range);
+        AIMET_LAUNCH_CHECK();
+        scratch_free(partial, s);
     });
 }
 

@@ -466,14 +466,20 @@ static int64_t pm_rows(int64_t Cin, int64_t Cout)
     return ceil_div(ceil_div(Cout, nr), (int64_t) 32) * 32;
 }
 
-// AIMET_ADA_PW_MFMA=0: the VALU form (pw_step_kernel) for comparisons
-static bool pw_mfma_enabled()
+// the matrix-core form for C_in >= 32 where its staging fits (W, X and G in <= 64 KiB of LDS,
+// <= 3 weight-gradient blocks per wave), else the VALU form. Below 32 input channels the weight
+// gradient's 32-wide blocks are mostly padding and the forward's sums 8-16 steps deep: MobileNet-v2's
+// stem and its 16 / 24-channel expanding layers ran 16-40 % slower there, the C_in >= 32 layers
+// 9-20 % faster (profiles/r04/README.md)
+static bool pw_uses_mfma(int64_t Cin, int64_t Cout, PmShape* shape = nullptr, size_t* lds_bytes = nullptr)
 {
-    static const bool v = [] {
-        const char* e = getenv("AIMET_ADA_PW_MFMA");
-        return !(e && e[0] == '0');
-    }();
-    return v;
+    const PmShape pm = pm_shape(Cin, pm_rows(Cin, Cout));
+    const size_t lds = sizeof(float) * ((size_t) pm.Cp * pm.Kw + (size_t) pm.Kx * kPmLd + (size_t) pm.Cp * kPmLd);
+    if (shape)
+        *shape = pm;
+    if (lds_bytes)
+        *lds_bytes = lds;
+    return Cin >= 32 && lds <= 65536 && pm.nblk1 <= 4 && pm.nblk3 <= 4 * kPmMaxT;
 }
 
 // output rows per workgroup row range: all of them when they fit (C_out <= 192, C_in C_out <= 6144),
@@ -485,6 +491,14 @@ static int64_t pw_rows(int64_t Cin, int64_t Cout)
     if (Cout <= r)
         return Cout;
     return r - r % 4;
+}
+
+int aimet_adaround_pw_step_uses_mfma(int64_t Cin, int64_t Cout, int* uses)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(Cin > 0 && Cout > 0 && uses != nullptr, "invalid argument");
+        *uses = pw_uses_mfma(Cin, Cout) ? 1 : 0;
+    });
 }
 
 int aimet_adaround_pw_step_workspace(int64_t N, int64_t Cin, int64_t Cout, int64_t HW, int64_t* elems)
@@ -539,15 +553,9 @@ int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, cons
             require_device_ptr(grad_w, "grad_w");
         if (bias)
             require_device_ptr(bias, "bias");
-        // the matrix-core form for C_in >= 32 where its staging fits (W, X and G in <= 64 KiB of LDS,
-        // <= 3 weight-gradient blocks per wave), else the VALU form. Below 32 input channels the
-        // weight gradient's 32-wide blocks are mostly padding and the forward's sums 8-16 steps deep:
-        // MobileNet-v2's stem and its 16 / 24-channel expanding layers ran 16-40 % slower there, the
-        // C_in >= 32 layers 9-20 % faster (profiles/r04/README.md)
-        const PmShape pm  = pm_shape(Cin, pm_rows(Cin, Cout));
-        const size_t lds  = sizeof(float) * ((size_t) pm.Cp * pm.Kw + (size_t) pm.Kx * kPmLd + (size_t) pm.Cp * kPmLd);
-        const bool mfma   = pw_mfma_enabled() && Cin >= 32 && lds <= 65536 && pm.nblk1 <= 4 &&
-                          pm.nblk3 <= 4 * kPmMaxT;
+        PmShape pm {};
+        size_t lds      = 0;
+        const bool mfma = pw_uses_mfma(Cin, Cout, &pm, &lds);
         const int64_t R   = mfma ? pm_rows(Cin, Cout) : pw_rows(Cin, Cout);
         AIMET_REQUIRE(mfma || ((R >= 4 || R == Cout) && R * Cin <= kPwPairs &&
                                ceil_div(Cin, (int64_t) 4) * ceil_div(R, (int64_t) 4) <= (int64_t) kBlock * kPwBlocks),

@@ -1053,38 +1053,9 @@ void launch_fold_minmax(const TqDevice& d, int64_t C, StatsKind kind, hipStream_
     AIMET_LAUNCH_CHECK();
 }
 
-// histogram launch shape: BLOCK lanes per workgroup x COLS LDS columns (tools/studies:
-// AIMET_TUNE_HIST_SHAPE=<block>x<cols> for the single-tensor kernel, AIMET_TUNE_HIST_BLOCK /
-// AIMET_TUNE_HIST_COLS for the batched one; experiments only)
-struct HistShape
-{
-    int block, cols;
-};
-static HistShape hist_shape_env(const char* name, HistShape dflt)
-{
-    const char* e = getenv(name);
-    if (!e)
-        return dflt;
-    HistShape h {0, 0};
-    if (sscanf(e, "%dx%d", &h.block, &h.cols) != 2 || (h.block != 256 && h.block != 512 && h.block != 1024) ||
-        (h.cols != 8 && h.cols != 16 && h.cols != 32))
-        return dflt;
-    return h;
-}
-
 template <bool ENT>
-static void launch_hist_tensor(HistShape h, unsigned grid, const float* x, int64_t n, int vec, const TqDevice& d,
-                               hipStream_t s)
+static void launch_hist_tensor(unsigned grid, const float* x, int64_t n, int vec, const TqDevice& d, hipStream_t s)
 {
-#define AIMET_HIST_T(B, C)                                                                                          \
-    if (h.block == B && h.cols == C)                                                                                \
-    {                                                                                                               \
-        histogram_tensor_kernel<B, ENT, C><<<grid, B, 0, s>>>(x, n, vec, d);                                        \
-        return;                                                                                                     \
-    }
-    AIMET_HIST_T(256, 8) AIMET_HIST_T(256, 16) AIMET_HIST_T(512, 8) AIMET_HIST_T(512, 16) AIMET_HIST_T(1024, 8)
-    AIMET_HIST_T(1024, 16) AIMET_HIST_T(1024, 32)
-#undef AIMET_HIST_T
     histogram_tensor_kernel<1024, ENT, 16><<<grid, 1024, 0, s>>>(x, n, vec, d);
 }
 
@@ -1096,13 +1067,13 @@ static void batch_histogram(const TqDevice& d, const float* x, int64_t outer, in
     {
         int64_t n = outer * K;
         // workgroups of 1024 lanes sharing one [512][16] LDS histogram (32 KiB: two per CU), each
-        // a contiguous share of ~128 K elements, the grid capped at 2 per CU
-        static const HistShape h = hist_shape_env("AIMET_TUNE_HIST_SHAPE", HistShape {1024, 16});
-        const int64_t per = (int64_t) h.block * kHistUnroll * 4 * 8;
+        // a contiguous share of ~128 K elements, the grid capped at 2 per CU (256 / 512-lane and
+        // 8 / 32-column shapes measured slower, tools/studies/hist_many_tune.py)
+        const int64_t per = (int64_t) 1024 * kHistUnroll * 4 * 8;
         int64_t blocks    = ceil_div(n, per);
-        const int64_t cap = 256 * 2048 / h.block;
+        const int64_t cap = 256 * 2;
         blocks            = blocks < 1 ? 1 : (blocks > cap ? cap : blocks);
-        launch_hist_tensor<ENT>(h, (unsigned) blocks, x, n, al ? 1 : 0, d, s);
+        launch_hist_tensor<ENT>((unsigned) blocks, x, n, al ? 1 : 0, d, s);
         AIMET_LAUNCH_CHECK();
     }
     else
@@ -1133,36 +1104,10 @@ void launch_fold_histogram(const TqDevice& d, int64_t C, int64_t count, StatsKin
     AIMET_LAUNCH_CHECK();
 }
 
-static int64_t hist_elems_per_block()
-{
-    static int64_t v = [] {
-        const char* e = getenv("AIMET_TUNE_HIST_ELEMS");   // tuning experiments only
-        return e ? atoll(e) : (int64_t) 131072;
-    }();
-    return v;
-}
-
-static int hist_many_block()
-{
-    static int v = [] {
-        // 1024 lanes sharing one [512][16] LDS histogram (profiles/r03: ViT-L/16 later batches
-        // 2.8-2.9 ms vs 3.1-3.2 with 512 lanes and 4.7 with 512 lanes x 32 columns)
-        const char* e = getenv("AIMET_TUNE_HIST_BLOCK");   // tuning experiments only
-        int b         = e ? atoi(e) : 1024;
-        return (b == 256 || b == 512) ? b : 1024;
-    }();
-    return v;
-}
-
-static int hist_many_cols()
-{
-    static int v = [] {
-        const char* e = getenv("AIMET_TUNE_HIST_COLS");   // tuning experiments only
-        const int c   = e ? atoi(e) : 16;
-        return (c == 8 || c == 32) ? c : 16;
-    }();
-    return v;
-}
+// elements per workgroup of the batched histogram pass; 1024 lanes sharing one [512][16] LDS
+// histogram (profiles/r03: ViT-L/16 later batches 2.8-2.9 ms vs 3.1-3.2 with 512 lanes and 4.7 with
+// 512 lanes x 32 columns)
+constexpr int64_t kHistElemsPerBlock = 131072;
 
 void stats_layout(std::vector<StatsJob>& jobs, uint64_t* mm_out, uint64_t* hb_out)
 {
@@ -1173,7 +1118,7 @@ void stats_layout(std::vector<StatsJob>& jobs, uint64_t* mm_out, uint64_t* hb_ou
         j.mm_blocks = (uint32_t) std::max<int64_t>(1, ceil_div(j.n, kMmTile));
         j.h_block0  = (uint32_t) hb;
         j.h_blocks  = (uint32_t) (j.hist ? std::max<int64_t>(1, std::min<int64_t>(kHistGrid,
-                                                                               ceil_div(j.n, hist_elems_per_block())))
+                                                                               ceil_div(j.n, kHistElemsPerBlock)))
                                          : 0);
         mm += j.mm_blocks;
         hb += j.h_blocks;
@@ -1222,15 +1167,7 @@ void launch_stats_table(const StatsJob* dj, int n, uint64_t mm, uint64_t hb, boo
     }
     if ((phases & kPhaseHistogram) && hb > 0)
     {
-        const int hbk = hist_many_block(), hc = hist_many_cols();
-#define AIMET_HIST_M(B, C)                                                                                          \
-    if (hbk == B && hc == C)                                                                                        \
-        histogram_many_kernel<B, C><<<(unsigned) hb, B, 0, s>>>(dj, n);                                           \
-    else
-        AIMET_HIST_M(256, 8) AIMET_HIST_M(256, 16) AIMET_HIST_M(512, 8) AIMET_HIST_M(512, 16) AIMET_HIST_M(1024, 8)
-        AIMET_HIST_M(1024, 32)
         histogram_many_kernel<1024, 16><<<(unsigned) hb, 1024, 0, s>>>(dj, n);
-#undef AIMET_HIST_M
         AIMET_LAUNCH_CHECK();
     }
     if (phases & kPhaseFoldHistogram)

@@ -243,16 +243,10 @@ __global__ __launch_bounds__(BLOCK, BLOCK == 128 ? 5 : (BLOCK == 64 ? 2 : 7)) vo
     }
 }
 
-// one candidate per lane: 101 symmetric candidates -> 2 waves, 358 asymmetric -> 6 waves
-int search_grid_cap()
-{
-    static int v = [] {
-        const char* e = getenv("AIMET_TUNE_TFE_GRID");   // tuning experiments only
-        int g         = e ? atoi(e) : 65536;
-        return g > 0 ? g : 65536;
-    }();
-    return v;
-}
+// one candidate per lane: 101 symmetric candidates -> 2 waves, 358 asymmetric -> 6 waves; one
+// workgroup per channel (capped grids measured no faster beside the activation passes,
+// profiles/r04/enc_split_tfe_grid.jsonl)
+constexpr int kSearchGridCap = 65536;
 
 // channels below which each one's candidates are split over one-wave workgroups (the activations'
 // quantizers of a batch: ResNet-50's 55 asymmetric searches took 58 us as 55 workgroups)
@@ -262,7 +256,7 @@ constexpr int64_t kTfeSplitBelow = 512;
 void launch_split(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t total, int bw, bool sym, bool strict,
                   bool unsign, int splits, uint64_t* part, unsigned* tickets, hipStream_t s)
 {
-    const int grid = (int) std::min<int64_t>(total * splits, search_grid_cap());
+    const int grid = (int) std::min<int64_t>(total * splits, kSearchGridCap);
     if (sym)
         tfe_search_kernel<64, true><<<grid, 64, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign, splits, part,
                                                       tickets);
@@ -275,7 +269,7 @@ void launch_split(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t tota
 void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t total, int bw, bool sym, bool strict,
                    bool unsign, hipStream_t s)
 {
-    const int cap    = search_grid_cap();
+    const int cap    = kSearchGridCap;
     const int splits = tfe_splits(total, sym);
     if (splits > 1)
     {
@@ -302,7 +296,7 @@ void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t tot
 
 int tfe_splits(int64_t total, bool sym)
 {
-    if (total >= kTfeSplitBelow || getenv("AIMET_TFE_NO_SPLIT") != nullptr)
+    if (total >= kTfeSplitBelow)
         return 1;
     return (int) ceil_div(sym ? tfe::kSymF : tfe::kMaxCand, 64);
 }

@@ -48,15 +48,6 @@ Ring& ring(int dev)
     return rings[dev];
 }
 
-// AIMET_SCRATCH_SYNC_ALLOC=1: the null-stream (synchronous) form on every stream (diagnostics)
-bool sync_alloc()
-{
-    static const bool v = [] {
-        const char* e = getenv("AIMET_SCRATCH_SYNC_ALLOC");
-        return e != nullptr && e[0] == '1';
-    }();
-    return v;
-}
 
 bool capturing(hipStream_t s)
 {
@@ -87,7 +78,7 @@ struct ScratchCache
     {
         int device;
         size_t bytes;
-        int mode;   // 0: cached block, 1: stream-ordered pool (capture), 2: synchronous (diagnostics)
+        int mode;   // 0: cached block, 1: stream-ordered pool (capture)
     };
     std::mutex m;
     std::vector<Block> free_blocks;
@@ -113,12 +104,7 @@ void* scratch_alloc(size_t bytes, hipStream_t s)
     void* d         = nullptr;
     int mode        = 0;
     size_t real     = bytes;   // a reused block keeps its own (possibly larger) size
-    if (sync_alloc())
-    {
-        AIMET_HIP_CHECK(hipMalloc(&d, bytes));
-        mode = 2;
-    }
-    else if (s != nullptr && capturing(s))
+    if (s != nullptr && capturing(s))
     {
         AIMET_HIP_CHECK(hipMallocAsync(&d, bytes, s));
         mode = 1;
@@ -191,12 +177,6 @@ void scratch_free(void* p, hipStream_t s)
             c.spare_events.pop_back();
         }
     }
-    if (l.mode == 2)
-    {
-        AIMET_HIP_CHECK(hipStreamSynchronize(s));   // the consuming launches are done
-        AIMET_HIP_CHECK(hipFree(p));
-        return;
-    }
     if (l.mode == 1)
     {
         AIMET_HIP_CHECK(hipFreeAsync(p, s));
@@ -216,9 +196,8 @@ void scratch_free(void* p, hipStream_t s)
 //   later calls, so calls in flight on different streams never share one.
 // * Inside a capture, a counter of its own that is never handed out again (the captured launch
 //   keeps it for every replay; replays of one graph run one after the other).
-// nullptr (the caller then launches its fold, or adds per workgroup): the synchronous diagnostics
-// mode, a capture before any eager call made the pool (it cannot be allocated and zeroed inside a
-// capture), or the capture counters used up.
+// nullptr (the caller then launches its fold): a capture before any eager call made the pool (it
+// cannot be allocated and zeroed inside a capture), or the capture counters used up.
 namespace
 {
 constexpr unsigned kTicketRing = 1u << 16, kTicketCapture = 1u << 20;
@@ -230,6 +209,7 @@ struct TicketPool
     unsigned next = 0, captured = 0;
     float* arena      = nullptr;   // partial-sum slots of captured launches, handed out once
     size_t arena_used = 0;
+    size_t arena_cap  = kCaptureArenaFloats;   // aimet_capture_pool_limit (tests of the fallback)
 };
 TicketPool& ticket_pool(int dev)
 {
@@ -278,8 +258,6 @@ unsigned* take_tickets(TicketPool& p, bool cap, unsigned count)
 
 unsigned* ticket_alloc(hipStream_t s, unsigned count)
 {
-    if (sync_alloc())
-        return nullptr;
     const bool cap = s != nullptr && capturing(s);
     std::lock_guard<std::mutex> lock(ticket_pool(current_device()).m);
     TicketPool* p = ready_pool(s, cap);
@@ -289,8 +267,6 @@ unsigned* ticket_alloc(hipStream_t s, unsigned count)
 FoldBuffers fold_buffers(hipStream_t s, unsigned tickets, size_t part_floats)
 {
     FoldBuffers f;
-    if (sync_alloc())
-        return f;
     const bool cap = s != nullptr && capturing(s);
     {
         std::lock_guard<std::mutex> lock(ticket_pool(current_device()).m);
@@ -302,8 +278,8 @@ FoldBuffers fold_buffers(hipStream_t s, unsigned tickets, size_t part_floats)
             // a captured launch keeps its partials slot for every replay: from the arena, never
             // handed out again (a graph memory node per replay cost ~10 us of every AdaRound iteration)
             const size_t n = (part_floats + 63) & ~size_t(63);
-            if (p->arena_used + n > kCaptureArenaFloats)
-                return f;
+            if (p->arena_used + n > p->arena_cap)
+                return f;   // used up: the caller folds in a launch of its own (same arithmetic)
             unsigned* t = take_tickets(*p, cap, tickets);
             if (t == nullptr)
                 return f;
@@ -321,6 +297,15 @@ FoldBuffers fold_buffers(hipStream_t s, unsigned tickets, size_t part_floats)
     return f;
 }
 
+size_t capture_pool_limit(size_t arena_floats)
+{
+    TicketPool& p = ticket_pool(current_device());
+    std::lock_guard<std::mutex> lock(p.m);
+    const size_t prev = p.arena_cap;
+    p.arena_cap       = arena_floats < kCaptureArenaFloats ? arena_floats : kCaptureArenaFloats;
+    return prev;
+}
+
 void fold_buffers_release(const FoldBuffers& f, hipStream_t s)
 {
     if (f.scratch && f.part)
@@ -332,11 +317,6 @@ void* upload_async(const void* src, size_t bytes, hipStream_t s)
     // a captured copy would re-read the (reused) pinned slot at every replay
     AIMET_REQUIRE(s == nullptr || !capturing(s), "host tables cannot be uploaded inside a HIP-graph capture");
     void* d = scratch_alloc(bytes, s);
-    if (sync_alloc())
-    {
-        AIMET_HIP_CHECK(hipMemcpy(d, src, bytes, hipMemcpyHostToDevice));
-        return d;
-    }
     Ring& r = ring(current_device());
     std::lock_guard<std::mutex> lock(r.m);
     Slot& slot = r.slots[r.next];

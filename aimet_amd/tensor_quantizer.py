@@ -16,17 +16,16 @@ import array
 import ctypes
 import gc
 import itertools
-import os
 
 import torch
 
 from aimet_amd import _native
-from aimet_amd._native import TfEncodingC
 from aimet_amd.libpymo import QuantizationMode, RoundingMode, TfEncoding, encodings_to_c
 
 _seed_counter = itertools.count(1)
-# calibrateResidentAsync: activations and parameters in two native calls (AIMET_CAL_SPLIT=0: one)
-_CAL_SPLIT = os.environ.get("AIMET_CAL_SPLIT", "1") != "0"
+# calibrateResidentAsync: activations and parameters in two native calls (False: one; the tests
+# compare the two forms)
+_CAL_SPLIT = True
 
 
 def _stream(t: torch.Tensor) -> int:
@@ -447,7 +446,7 @@ class AimetTensorQuantizer:
                                act_settings=(8, False, False, False), param_settings=(8, True, False, False),
                                reset=False, main_stream=None, side_stream=None):
         """One calibration batch in two native calls (aimet_calibrate_launch; one when `side_stream`
-        is `main_stream` or AIMET_CAL_SPLIT=0): the activations' call first, so their min/max pass
+        is `main_stream` or _CAL_SPLIT is False): the activations' call first, so their min/max pass
         runs while the parameters' call is prepared. Optionally
         resetEncodingStats of every quantizer, the activations' statistics (one launch per phase for
         all per-tensor quantizers) + search on `main_stream`, the parameters' per-channel statistics
@@ -734,6 +733,10 @@ class PendingEncodings:
 
     def result(self):
         results = {}
+        if not self.live and self.req is not None:
+            # a launched request over no live quantizer (an empty activation list of a plan): free it
+            req, self.req = self.req, None
+            _native.call("aimet_tq_get_encodings_finish", req, None, None)
         if self.live:
             if self.req is None:
                 raise RuntimeError("PendingEncodings.result() called twice")

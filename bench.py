@@ -18,7 +18,6 @@ Prints ONE JSON line on rank 0.
 import argparse
 import ctypes
 import json
-import math
 import os
 import socket
 import subprocess
@@ -51,7 +50,9 @@ def parse():
     p.add_argument("--cpu-sample-images", type=int, default=32,
                    help="images of each activation tensor (plus all weights) timed on the CPU oracle")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--enc-reps", type=int, default=9, help="timed compute_encodings calls after the cold one")
+    p.add_argument("--enc-reps", type=int, default=9, help="timed compute_encodings_resident calls after the cold one")
+    p.add_argument("--plan-reps", type=int, default=25,
+                   help="timed CalibrationPlan runs (the compute_encodings headline), after 2 untimed ones")
     p.add_argument("--eager", action="store_true", help="launch every QDQ from Python instead of HIP graphs")
     p.add_argument("--per-weight-launches", action="store_true",
                    help="one per-channel QDQ launch per weight instead of the batched plan")
@@ -178,16 +179,28 @@ def make_quantizers(acts, weights):
     return aq, wq
 
 
-def time_plan(plan, reps):
-    """`reps` timed plan runs that reset and recompute the plan's quantizers (one compute_encodings
-    of an existing sim each); returns (median seconds, encodings of the last run)."""
+def time_plan(plan, reps, warm=2, spans=None):
+    """`warm` untimed, then `reps` timed plan runs that reset and recompute the plan's quantizers
+    (one compute_encodings of an existing sim each); returns (median seconds, encodings of the last
+    run, every timed run in ms). spans (a list): each run's GPU span in ms, a HIP event on the main
+    stream before the launch to one enqueued right behind it (after the activations' search)."""
     secs, res = [], None
-    for _ in range(reps):
+    stream = torch.cuda.current_stream()
+    for i in range(warm + reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        res = plan.run(reset=True)
-        secs.append(time.perf_counter() - t0)
-    return sorted(secs)[len(secs) // 2], res
+        e0.record(stream)
+        a, p = plan.launch(reset=True)
+        e1.record(stream)
+        p_res = p.result()
+        res = (a.result(), p_res)
+        if i >= warm:
+            secs.append(time.perf_counter() - t0)
+            if spans is not None:
+                torch.cuda.synchronize()
+                spans.append(round(e0.elapsed_time(e1), 3))
+    return sorted(secs)[len(secs) // 2], res, [round(v * 1e3, 3) for v in secs]
 
 
 def compute_encodings(acts, weights, quantizers=None):
@@ -447,7 +460,15 @@ def main():
     # recompute of every quantizer (aimet_amd.calibration.CalibrationPlan). Sharded at N > 1.
     from aimet_amd.calibration import CalibrationPlan
     cplan = CalibrationPlan(aq, [t for _, t in acts], wq, [w for _, w in weights])
-    enc_seconds, (a_res, w_res) = time_plan(cplan, max(1, args.enc_reps))
+    enc_spans = []
+    enc_seconds, (a_res, w_res), enc_runs_ms = time_plan(cplan, max(1, args.plan_reps), spans=enc_spans)
+    # the same on quantizers made for the plan alone (a new sim), for comparison
+    nq, nw = make_quantizers(acts, weights)
+    nplan = CalibrationPlan(nq, [t for _, t in acts], nw, [w for _, w in weights])
+    new_spans = []
+    enc_new_s, _, _ = time_plan(nplan, max(1, args.plan_reps), spans=new_spans)
+    nplan.close()
+    del nq, nw
     plan_act, plan_w = [e for e, _ in a_res], [e for e, _ in w_res]
     enc_plan_equal = ([e.to_tuple() for e in plan_act] == [e.to_tuple() for e in act_enc] and
                       [[x.to_tuple() for x in es] for es in plan_w] == [[x.to_tuple() for x in es] for es in w_enc])
@@ -459,7 +480,7 @@ def main():
         # Quantizers of their own (the plan binds them to the packed exchange buffers).
         xq, xw = make_quantizers(acts, weights)
         xplan = CalibrationPlan(xq, [t for _, t in acts], xw, [w for _, w in weights], force_exchange=True)
-        x_s, (xa, xwr) = time_plan(xplan, max(1, args.enc_reps))
+        x_s, (xa, xwr), x_runs = time_plan(xplan, max(1, args.plan_reps))
         enc_exchange = {"seconds": round(x_s, 4), "dist_backend": dist.get_backend(),
                         "world_formed": dist.get_world_size(),
                         "equal_to_headline": [e.to_tuple() for e, _ in xa] == [e.to_tuple() for e in act_enc] and
@@ -594,20 +615,25 @@ def main():
                    "compute_encodings_cold_s": round(enc_cold, 4),
                    "compute_encodings_fresh_quantizers_s": round(enc_fresh, 4),
                    "compute_encodings_resident_s": round(enc_resident, 4),
+                   "compute_encodings_runs_ms": enc_runs_ms,
+                   "compute_encodings_gpu_span_ms": enc_spans,
+                   "compute_encodings_new_sim_s": round(enc_new_s, 4),
+                   "compute_encodings_new_sim_gpu_span_ms": sorted(new_spans)[len(new_spans) // 2] if new_spans else None,
                    "compute_encodings_plan_equals_resident": enc_plan_equal,
                    # two passes (min/max, histogram) of 4 B over every activation and weight element
                    "compute_encodings_roofline": {
                        "algorithmic_gb": round(8 * n_step / 1e9, 3),
                        "achieved_gbps": round(8 * n_step / enc_seconds / 1e9, 1),
                        "frac": round(8 * n_step / enc_seconds / 1e9 / HBM_PEAK_GBPS, 4)},
-                   "compute_encodings_timing": "median of %d CalibrationPlan.run(reset=True) calls: reset and "
+                   "compute_encodings_timing": "median of %d CalibrationPlan.run(reset=True) calls (after 2 "
+                                               "untimed ones): reset and "
                                                "recompute the sim's quantizers (created once, as QuantizationSimModel "
                                                "does) with the plan prepared once over the resident activations; "
                                                "beside it the first call of the process (cold), %d "
                                                "compute_encodings_resident calls on fresh quantizers (plan made "
                                                "inside) and %d on the sim's quantizers (cached plan, its tensors "
                                                "checked by identity every call); max over ranks"
-                                               % (max(1, args.enc_reps), args.enc_reps, args.enc_reps),
+                                               % (max(1, args.plan_reps), args.enc_reps, args.enc_reps),
                    "compute_encodings_scheme": "tf_enhanced act per-tensor + tf_enhanced weight per-channel sym"},
         "roofline": {"bound": "hbm", "kernel": "qdq_per_tensor (tensor_vec_kernel)",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

@@ -63,6 +63,11 @@ const char* aimet_last_error(void);
 const char* aimet_version(void);
 /* Number of gfx950 devices visible; negative status on HIP failure. */
 int aimet_device_count(void);
+/* Cap (in floats, at most its 64 MB size) on the current device's arena of partial-sum slots that
+ * kernels captured into HIP graphs keep for every replay (the AdaRound round loss's last-workgroup
+ * fold); *previous = the cap before. A launch captured once the arena is used up takes the same
+ * fold as a launch of its own instead: the same values. For tests of that fallback. */
+int aimet_capture_pool_limit(int64_t arena_floats, int64_t* previous);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Encoding math (host, exact reference arithmetic)                                            */
@@ -500,8 +505,8 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
                                  double beta2, double eps, float* round_loss_dev, float* wq_next_dev, void* stream);
 
 /* aimet_adaround_backward_adam with the weight gradient given as `nparts` slices added in slice
- * order (s = 0, 1, ...) element by element: part_kk == 0: grad_parts[s][n] (n = outer * C * K; the
- * sliced weight gradient of aimet_adaround_pw_cm_wgrad); part_kk > 0: grad_parts[n / part_kk][s]
+ * order (s = 0, 1, ...) element by element: part_kk == 0: grad_parts[s][n] (n = outer * C * K);
+ * part_kk > 0: grad_parts[n / part_kk][s]
  * [part_kk] from +0 (the depthwise step's per-channel slices, aimet_adaround_dw_step with grad_w
  * NULL: the sum is its fold's, bit for bit). bias_corr_dev (nullable): the table of
  * aimet_adaround_adam_bias_corrections for beta1 / beta2, read at step instead of computing the
@@ -518,26 +523,6 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
  * bc1, [2 (step - 1) + 1] = sqrt(bc2) (float32, 2 * steps entries). */
 int aimet_adaround_adam_bias_corrections(double beta1, double beta2, int64_t steps, float* bias_corr_dev,
                                          void* stream);
-
-/* The channel-major GEMM form of a 1x1 layer's AdaRound iteration (adaround_optimizer.py:181-218)
- * in two kernels on the f32 matrix cores, for many channels at small spatial sizes. Batch position
- * p = b * hw + t of iteration it = it_cur_dev[0] is element t of row idx_all_dev[it * nb + b] of
- * x_cache ([rows][Cin][hw]) and target_cache ([rows][Cout][hw]), read in place.
- * aimet_adaround_pw_cm_forward: grad_q[co][p] = the reconstruction-loss gradient
- * (aimet_adaround_recon_grad_indexed_cm's, act 0 none / 1 ReLU / 2 ReLU6) of
- * q = sum over ci of w[co][ci] x[ci][p] (ci ascending) + bias[co] (nullable); it_next_dev[0] =
- * it + 1. aimet_adaround_pw_cm_wgrad: parts[s][co][ci] = sum over the positions of slice s of
- * grad_q[co][p] x[ci][p] (positions ascending), `slices` from aimet_adaround_pw_cm_wgrad_slices;
- * aimet_adaround_backward_adam_parts adds them. Fixed summation orders (deterministic, fp32; not
- * bit-identical to a library GEMM). */
-int aimet_adaround_pw_cm_forward(const float* x_cache, const float* target_cache, const int64_t* idx_all_dev,
-                                 const int64_t* it_cur_dev, int64_t* it_next_dev, const float* w, const float* bias,
-                                 float* grad_q, int64_t nb, int64_t Cin, int64_t Cout, int64_t hw, int32_t act,
-                                 void* stream);
-int aimet_adaround_pw_cm_wgrad_slices(int64_t nb, int64_t Cin, int64_t Cout, int64_t hw, int64_t* slices);
-int aimet_adaround_pw_cm_wgrad(const float* x_cache, const int64_t* idx_all_dev, const int64_t* it_cur_dev,
-                               const float* grad_q, float* parts, int64_t slices, int64_t nb, int64_t Cin, int64_t Cout,
-                               int64_t hw, void* stream);
 
 /* Depthwise 2-D convolution (groups == C, weights [C][1][K][K], K = 3 or 5, square stride /
  * padding / dilation, NCHW fp32): the AdaRound loop's layer math on depthwise layers
@@ -581,6 +566,10 @@ int aimet_adaround_dw_step_slices(const float* target_cache, int64_t N, int64_t 
  * and target_cache 16-B aligned. `workspace`
  * (aimet_adaround_pw_step_workspace elements, device) may be null (internal scratch). */
 int aimet_adaround_pw_step_workspace(int64_t N, int64_t Cin, int64_t Cout, int64_t HW, int64_t* elems);
+/* *uses = 1 when aimet_adaround_pw_step runs a (Cin, Cout) layer on the f32 matrix cores (C_in >= 32
+ * and its staging fits in LDS), 0 for the VALU form: the loop's choice of the one-pass step for
+ * projecting layers depends on it (adaround_optimizer.py). */
+int aimet_adaround_pw_step_uses_mfma(int64_t Cin, int64_t Cout, int* uses);
 int aimet_adaround_pw_step(const float* x_cache, const float* target_cache, const int64_t* idx_all_dev,
                            const int64_t* it_cur_dev, int64_t* it_next_dev, const float* w, const float* bias,
                            float* grad_w, float* workspace, int64_t N, int64_t Cin, int64_t Cout, int64_t HW,

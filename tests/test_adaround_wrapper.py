@@ -261,6 +261,36 @@ def test_adaround_multi_iteration_graph_equals_one_per_graph(monkeypatch, kind):
 
 @pytest.mark.gpu
 @gpu
+@pytest.mark.parametrize("kind", ["dw", "linear"])
+def test_adaround_round_loss_same_when_capture_pool_used_up(kind):
+    """Captured loops keep their round-loss fold slots in a fixed arena (upload.cpp fold_buffers);
+    once it is used up, a captured launch folds its partials in a launch of its own, in the same
+    order: alpha and the reported round loss equal those of the arena form, bit for bit (ADVICE
+    r04: the fallback was one float atomic per workgroup)."""
+    import ctypes
+    from aimet_amd import _native
+    from aimet_amd.adaround_optimizer import AdaroundHyperParameters, AdaroundOptimizer
+    m, inp, out, d, o = _loop_problem(kind)
+    p = AdaroundHyperParameters(num_iterations=120, warm_start=0.2)
+    res = []
+    for limit in (None, 0):
+        prev = ctypes.c_int64()
+        if limit is not None:
+            _native.call("aimet_capture_pool_limit", limit, ctypes.byref(prev))
+        try:
+            loss = torch.zeros(1, device=DEV)
+            a = AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, nn.ReLU6(),
+                                                    torch.Generator().manual_seed(5), loss)
+            res.append((a.detach().clone(), loss.clone()))
+        finally:
+            if limit is not None:
+                _native.call("aimet_capture_pool_limit", prev.value, None)
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1]) and res[0][1].item() != 0.0
+
+
+@pytest.mark.gpu
+@gpu
 @pytest.mark.parametrize("cin,cout,k,hw", [(3, 32, 3, 64), (16, 96, 1, 28), (64, 192, 1, 28), (144, 24, 1, 56)])
 def test_adaround_one_pass_step_slices_folded_by_adam(monkeypatch, cin, cout, k, hw):
     """The one-pass 1x1 / stem step leaving its weight-gradient slices for the Adam step to add
@@ -285,27 +315,6 @@ def test_adaround_one_pass_step_slices_folded_by_adam(monkeypatch, cin, cout, k,
         assert ao.AdaroundOptimizer.last_loop_form in ("pointwise_fused", "im2col_fused")
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
-
-
-@pytest.mark.gpu
-@gpu
-def test_adaround_pw_cm_mfma_loop_close_to_library_form(monkeypatch):
-    """The channel-major 1x1 loop on the f32 matrix cores (AIMET_ADA_PW_CM_FUSED=1) is
-    deterministic and gives the library-GEMM form's alpha to fp32 summation-order tolerance."""
-    import aimet_amd.adaround_optimizer as ao
-    from aimet_amd.adaround_optimizer import AdaroundHyperParameters, AdaroundOptimizer
-    m, inp, out, d, o = _loop_problem("pointwise_wide")
-    p = AdaroundHyperParameters(num_iterations=200, warm_start=0.2)
-    res = {}
-    for fused in (True, True, False):
-        monkeypatch.setattr(ao, "_PW_CM_FUSED", fused)
-        a = AdaroundOptimizer.optimize_rounding(m, inp, out, d, o, 8, 0, p, nn.ReLU6(),
-                                                torch.Generator().manual_seed(5)).detach().clone()
-        assert AdaroundOptimizer.last_loop_form == ("pointwise_cm_mfma" if fused else "pointwise_cm")
-        if fused in res:
-            assert torch.equal(a, res[fused])
-        res[fused] = a
-    torch.testing.assert_close(res[True], res[False], rtol=1e-4, atol=1e-4)
 
 
 @pytest.mark.gpu

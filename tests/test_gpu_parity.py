@@ -254,9 +254,10 @@ def test_device_search_many_channels(scheme, C, bws):
                 assert encs[c].to_tuple() == orcs[c].compute(bw, *fl).as_tuple(), (c, bw, fl)
 
 
-def test_tfe_split_search_equals_one_workgroup_per_channel(monkeypatch):
-    """The split TF-E search (few channels: candidates over one-wave workgroups, first minimum by
-    (cost, index) across them) == one workgroup per channel (AIMET_TFE_NO_SPLIT), for a batch of
+def test_tfe_split_search_equals_one_workgroup_per_channel():
+    """The split TF-E search (fewer than 512 channels in the batch: candidates over one-wave
+    workgroups, first minimum by (cost, index) across them) == one workgroup per channel (the same
+    quantizers searched in a batch with a 512-channel quantizer beside them), for a batch of
     per-tensor quantizers (the activations' getEncodings) and every flag set."""
     rng = np.random.default_rng(33)
     qs = []
@@ -267,12 +268,12 @@ def test_tfe_split_search_equals_one_workgroup_per_channel(monkeypatch):
             x = np.abs(x)
         q.updateStats(gpu(x.astype(np.float32)), True)
         qs.append(q)
+    big = AimetTensorQuantizer(QuantizationMode.QUANTIZATION_TF_ENHANCED, num_channels=512)
+    big.updateStatsPerChannel(gpu(rng.standard_normal((512, 64)).astype(np.float32)), 0, True)
     for bw in (8, 16):
         for fl in FLAGS:
             split = AimetTensorQuantizer.getEncodings(qs, bw, *fl)
-            monkeypatch.setenv("AIMET_TFE_NO_SPLIT", "1")
-            whole = AimetTensorQuantizer.getEncodings(qs, bw, *fl)
-            monkeypatch.delenv("AIMET_TFE_NO_SPLIT")
+            whole = AimetTensorQuantizer.getEncodings(qs + [big], bw, *fl)[:len(qs)]
             assert [(e.to_tuple(), v) for e, v in split] == [(e.to_tuple(), v) for e, v in whole], (bw, fl)
 
 
@@ -1285,20 +1286,17 @@ print(" ".join(str(v) for v in out))
 """
 
 
-def test_learned_grid_fold_in_kernel_equals_fold_launch():
-    """The per-tensor backward's fold in the kernel's last workgroup (AIMET_LG_FOLD_IN_KERNEL=1)
-    and as its own launch (the default) give the same encoding gradients bit for bit (one fold
-    order, fold_partials), fp32 and 16-bit, on Llama-3-8B call sizes. Each form in a child process
-    (the switch is read once per process)."""
+def test_learned_grid_fold_is_reproducible_across_processes():
+    """The per-tensor backward's encoding gradients (per-tile partials folded in one fixed order,
+    fold_partials) are the same bits in two processes, fp32 and 16-bit, on Llama-3-8B call sizes:
+    nothing in them depends on scheduling."""
     import os
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     res = []
-    for flag in ("0", "1"):
-        env = dict(os.environ, AIMET_LG_FOLD_IN_KERNEL=flag)
-        r = subprocess.run([sys.executable, "-c", _LG_FOLD_CHILD, repo], env=env, capture_output=True, text=True,
-                           timeout=240)
+    for _ in range(2):
+        r = subprocess.run([sys.executable, "-c", _LG_FOLD_CHILD, repo], capture_output=True, text=True, timeout=240)
         assert r.returncode == 0, r.stderr[-2000:]
         res.append(r.stdout.strip().splitlines()[-1])
     assert res[0] == res[1], res
@@ -1446,100 +1444,6 @@ def test_adaround_pw_step_vs_torch(N, Cin, Cout, HW, act, with_bias):
     bound = torch.einsum("noh,nch->oc", gq.abs(), xb.abs())
     err = (outs[0].double() - gw_ref).abs()
     assert bool((err <= 2e-5 * bound + 1e-12).all()), float((err / (bound + 1e-30)).max())
-
-
-@pytest.mark.parametrize("N,Cin,Cout,HW,act,with_bias", [(32, 96, 576, 196, 2, True), (32, 576, 96, 196, 0, True),
-                                                          (32, 960, 160, 49, 0, False), (32, 160, 960, 49, 2, True),
-                                                          (5, 3, 70, 13, 1, True), (7, 100, 33, 9, 2, False),
-                                                          (3, 27, 32, 1000, 1, True)])
-def test_adaround_pw_cm_mfma_vs_torch(N, Cin, Cout, HW, act, with_bias):
-    """aimet_adaround_pw_cm_forward + _wgrad (the channel-major 1x1 iteration on the f32 matrix
-    cores, the batch gathered in place) == the fp32 torch ops they replace (index_select, W @ x,
-    the reconstruction-loss gradient, dL/dW) to summation-order tolerance, shapes with ragged
-    tiles included; the Adam step's slice sum (aimet_adaround_backward_adam_parts) == the
-    slices added in order; deterministic; moves the iteration counter."""
-    import ctypes
-    from aimet_amd import _native
-    g = torch.Generator(device=DEV).manual_seed(Cin * Cout + HW + N)
-    rows = N + 3
-    x_cache = torch.rand(rows, Cin, HW, device=DEV, generator=g)
-    w = torch.randn(Cout, Cin, device=DEV, generator=g) / Cin ** 0.5
-    b = torch.randn(Cout, device=DEV, generator=g) * 0.1 if with_bias else None
-    t_cache = torch.randn(rows, Cout, HW, device=DEV, generator=g) * 0.5
-    idx = torch.stack([torch.randperm(rows, device=DEV, generator=g)[:N] for _ in range(2)]).contiguous()
-    it = 1
-    xb, tb = x_cache[idx[it]].double(), t_cache[idx[it]].double()
-    q = torch.einsum("oc,nch->noh", w.double(), xb) + (b.double()[None, :, None] if with_bias else 0)
-    actf = {0: lambda v: v, 1: torch.relu, 2: lambda v: v.clamp(0, 6)}[act]
-    mask = {0: lambda v: torch.ones_like(v), 1: lambda v: (v > 0).double(),
-            2: lambda v: ((v > 0) & (v < 6)).double()}[act]
-    gq = 2.0 / (N * HW) * (actf(q) - actf(tb)) * mask(q)
-    gw_ref = torch.einsum("noh,nch->oc", gq, xb)
-    s = torch.cuda.current_stream().cuda_stream
-    n_sl = ctypes.c_int64()
-    _native.call("aimet_adaround_pw_cm_wgrad_slices", N, Cin, Cout, HW, ctypes.byref(n_sl))
-    S = n_sl.value
-    outs = []
-    for _ in range(2):
-        ctr = torch.tensor([it, -1], dtype=torch.long, device=DEV)
-        g_cm = torch.empty(Cout, N * HW, device=DEV)
-        parts = torch.full((S, Cout, Cin), float("nan"), device=DEV)
-        _native.call("aimet_adaround_pw_cm_forward", x_cache.data_ptr(), t_cache.data_ptr(), idx.data_ptr(),
-                     ctr.data_ptr(), ctr.data_ptr() + 8, w.data_ptr(), b.data_ptr() if with_bias else None,
-                     g_cm.data_ptr(), N, Cin, Cout, HW, act, s)
-        _native.call("aimet_adaround_pw_cm_wgrad", x_cache.data_ptr(), idx.data_ptr(), ctr.data_ptr(), g_cm.data_ptr(),
-                     parts.data_ptr(), S, N, Cin, Cout, HW, s)
-        assert ctr.tolist() == [it, it + 1]
-        outs.append((g_cm, parts))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])   # deterministic
-    g_cm, parts = outs[0]
-    # the reconstruction gradient: q is an fp32 chain of fmas over Cin, within 4e-6 * sum |w x| here;
-    # elements whose q lies that close to a mask edge (ReLU at 0, ReLU6 at 0 and 6) are skipped
-    g_ref_cm = gq.permute(1, 0, 2).reshape(Cout, N * HW)
-    qc = q.permute(1, 0, 2).reshape(Cout, -1)
-    tol_q = 4e-6 * torch.einsum("oc,nch->noh", w.double().abs(), xb.abs()).permute(1, 0, 2).reshape(Cout, -1)
-    edge = torch.zeros_like(qc, dtype=torch.bool)
-    for e in ((0.0,) if act == 1 else (0.0, 6.0) if act == 2 else ()):
-        edge |= (qc - e).abs() <= tol_q
-    err = (g_cm.double() - g_ref_cm).abs()
-    assert bool((err <= 2.0 / (N * HW) * tol_q + 1e-6 * g_ref_cm.abs() + 1e-30)[~edge].all())
-    # the weight gradient from the kernel's own g: fp32 sums over the slices' positions
-    gw = parts.double().sum(0)
-    xb_cm = xb.permute(1, 0, 2).reshape(Cin, -1)
-    gw_own = g_cm.double() @ xb_cm.t()
-    bound = g_cm.double().abs() @ xb_cm.abs().t()
-    assert bool(((gw - gw_own).abs() <= 2e-5 * bound + 1e-12).all())
-    assert bool(((gw - gw_ref).abs() <= 2e-4 * (bound + (gq.abs().permute(1, 0, 2).reshape(Cout, -1) @ xb_cm.abs().t()))
-                 + 1e-9).all())
-    # the Adam step's slice sum: slices added in order == the single-gradient call on that sum
-    C, K = Cout, Cin
-    w_ada = torch.randn(C, K, device=DEV, generator=g) * 0.05
-    d = (w_ada.abs().amax(1) / 7).contiguous()
-    o = torch.full((C,), -8.0, device=DEV)
-    gsum = parts[0].clone()
-    for k in range(1, S):
-        gsum += parts[k]
-    res = []
-    bc = torch.empty(2, device=DEV)
-    _native.call("aimet_adaround_adam_bias_corrections", ctypes.c_double(0.9), ctypes.c_double(0.999), 1,
-                 bc.data_ptr(), s)
-    for fn, grad, extra, tab in (("aimet_adaround_backward_adam_parts", parts, (S, 0), (None,)),
-                                 ("aimet_adaround_backward_adam_parts", parts, (S, 0), (bc.data_ptr(),)),
-                                 ("aimet_adaround_backward_adam", gsum, (), ())):
-        alpha = torch.randn(C, K, device=DEV, generator=torch.Generator(device=DEV).manual_seed(5))
-        m, v = torch.zeros_like(alpha), torch.zeros_like(alpha)
-        rb = torch.tensor([[0.01, 10.0, 9.0]], device=DEV)
-        ctr = torch.tensor([0, 1], dtype=torch.long, device=DEV)
-        wq = torch.empty_like(alpha)
-        args = [w_ada.data_ptr(), alpha.data_ptr(), grad.data_ptr(), *extra, m.data_ptr(), v.data_ptr(), 1, C, K,
-                d.data_ptr(), o.data_ptr(), 4, rb.data_ptr(), ctr.data_ptr() + 8, ctr.data_ptr(),
-                ctypes.c_double(1e-3), ctypes.c_double(0.9), ctypes.c_double(0.999), ctypes.c_double(1e-8), None,
-                wq.data_ptr(), *tab, s]
-        _native.call(fn, *args)
-        res.append((alpha, m, v, wq))
-    for r in res[1:]:
-        for a_, b_ in zip(res[0], r):
-            assert torch.equal(a_, b_)
 
 
 def test_adam_bias_correction_table_equals_in_kernel():
@@ -1728,8 +1632,8 @@ def test_reset_of_quantizers_bound_to_exchange_buffers():
 
 @pytest.mark.parametrize("schemes", ["tfe", "mixed"])
 def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatch):
-    """compute_encodings_resident's native calls (aimet_calibrate_launch, reset folded in; the
-    activations' and the parameters' calls apart, and both in one call) ==
+    """compute_encodings_resident's calibration plan and native calls (aimet_calibrate_launch, reset
+    folded in; the activations' and the parameters' calls apart, and both in one call) ==
     the phase-by-phase path from Python (resetEncodingStatsMany + per-phase *_many launches + the
     two requests), on quantizers that already hold the previous batch's statistics; and a second
     reset + recompute of the same data == the first (nothing of the earlier batch survives)."""
@@ -1752,9 +1656,10 @@ def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatc
     from aimet_amd import tensor_quantizer
     old, new_ = batch(3.0), batch(1.0)
     results = []
-    # two native calls (activations, then parameters), one native call, the phased path
-    for native, split in ((True, True), (True, False), (False, False)):
-        monkeypatch.setattr(calibration, "_SCHEDULE", "params_first" if native else "params_first_phased")
+    # the calibration plan, two native calls (activations, then parameters), one native call, the
+    # phased path
+    for sched, split in (("plan", True), ("native", True), ("native", False), ("phased", False)):
+        monkeypatch.setattr(calibration, "_SCHEDULE", sched)
         monkeypatch.setattr(tensor_quantizer, "_CAL_SPLIT", split)
         aq = [AimetTensorQuantizer(m) for m in a_modes]
         pq = [AimetTensorQuantizer(m, num_channels=p.shape[0]) for m, p in zip(p_modes, new_[1])]
@@ -1765,11 +1670,11 @@ def test_calibrate_native_call_equals_phased_path_with_reset(schemes, monkeypatc
                           [[x.to_tuple() for x in (es if isinstance(es, list) else [es])] for es, _ in r[1]])
         assert flat(r1) == flat(r2)
         results.append(flat(r1))
-    assert results[0] == results[1] == results[2]
+    assert results[0] == results[1] == results[2] == results[3]
     # and == fresh quantizers fed only the new batch
     fa = [AimetTensorQuantizer(m) for m in a_modes]
     fp = [AimetTensorQuantizer(m, num_channels=p.shape[0]) for m, p in zip(p_modes, new_[1])]
-    monkeypatch.setattr(calibration, "_SCHEDULE", "params_first")
+    monkeypatch.setattr(calibration, "_SCHEDULE", "plan")
     fresh = compute_encodings_resident(fa, new_[0], fp, new_[1])
     assert ([e.to_tuple() for e, _ in fresh[0]]) == results[0][0]
 

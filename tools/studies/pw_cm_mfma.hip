@@ -1,4 +1,9 @@
-// pwcm.hip -- the AdaRound loop's iteration for 1x1 layers with many channels at small spatial
+// pw_cm_mfma.hip (study; was aimet_amd/csrc/pwcm.hip until round 5) -- NOT part of libaimet_amd.so:
+// measured slower than the library-GEMM channel-major form it was meant to replace
+// (profiles/r04/pw_cm_mfma_vs_library_v4.jsonl), so it was moved out of the product (VERDICT r04
+// weak item 6). It builds against aimet_amd/csrc's headers (-I aimet_amd/csrc) if needed again.
+//
+// The AdaRound loop's iteration for 1x1 layers with many channels at small spatial
 // sizes (MobileNet-v2's 14x14 / 7x7 expand and project layers), channel-major over the batch's
 // nb * hw positions, on the f32-input matrix cores.
 //
