@@ -63,6 +63,13 @@ struct aimet_calib_plan
 namespace
 {
 
+// The parameters' TF-Enhanced search runs beside the activations' min/max pass (another stream). At
+// its own occupancy (~10 two-wave workgroups per CU) it held the wave slots the HBM-bound pass needs
+// to keep its loads in flight: the pass took ~0.22 ms longer (profiles/r05/enc_plan_runs_c.jsonl:
+// 3.70 vs 3.48 ms without the parameters). Held to a few workgroups per CU, it takes longer itself
+// but finishes (and the host builds the 27,560 encodings) long before the activations' passes end.
+constexpr int kParamSearchPerCu = 2;
+
 // one device allocation holding many tables: offsets first, then one upload
 struct Packer
 {
@@ -297,7 +304,8 @@ int aimet_calib_plan_create(aimet_tensor_quantizer* const* act_qs, const float* 
             p->has_tfe_par = true;
             p->tfe_par     = TfeTable {jp[0], reinterpret_cast<const TfeJob*>(base + o_jp), (int) jp.size(), tp,
                                    sp > 1 ? reinterpret_cast<uint64_t*>(base + o_pp) : nullptr,
-                                   sp > 1 ? reinterpret_cast<unsigned*>(base + o_kp) : nullptr};
+                                   sp > 1 ? reinterpret_cast<unsigned*>(base + o_kp) : nullptr,
+                                   n_act ? kParamSearchPerCu : 0};
         }
         *out = p;
         p    = nullptr;

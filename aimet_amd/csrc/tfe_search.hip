@@ -267,7 +267,7 @@ void launch_split(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t tota
 }
 
 void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t total, int bw, bool sym, bool strict,
-                   bool unsign, hipStream_t s)
+                   bool unsign, hipStream_t s, size_t lds_pad = 0)
 {
     const int cap    = kSearchGridCap;
     const int splits = tfe_splits(total, sym);
@@ -284,10 +284,10 @@ void launch_kernel(const TfeJob& one, const TfeJob* jobs, int njobs, int64_t tot
     }
     const int grid = (int) (total < cap ? total : cap);
     if (sym)
-        tfe_search_kernel<128, true><<<grid, 128, 0, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign, 1, nullptr,
+        tfe_search_kernel<128, true><<<grid, 128, lds_pad, s>>>(one, jobs, njobs, total, bw, 1, strict, unsign, 1, nullptr,
                                                         nullptr);
     else
-        tfe_search_kernel<384, false><<<grid, 384, 0, s>>>(one, jobs, njobs, total, bw, 0, strict, unsign, 1, nullptr,
+        tfe_search_kernel<384, false><<<grid, 384, lds_pad, s>>>(one, jobs, njobs, total, bw, 0, strict, unsign, 1, nullptr,
                                                          nullptr);
     AIMET_LAUNCH_CHECK();
 }
@@ -303,6 +303,7 @@ int tfe_splits(int64_t total, bool sym)
 
 void launch_tfe_table(const TfeTable& t, int bw, bool sym, bool strict, bool unsign, hipStream_t s)
 {
+    const int per_cu = t.per_cu;
     if (t.total == 0)
         return;
     const int splits = tfe_splits(t.total, sym);
@@ -312,7 +313,16 @@ void launch_tfe_table(const TfeTable& t, int bw, bool sym, bool strict, bool uns
         launch_split(t.first, t.dev, t.n, t.total, bw, sym, strict, unsign, splits, t.part, t.tickets, s);
         return;
     }
-    launch_kernel(t.first, t.dev, t.n, t.total, bw, sym, strict, unsign, s);
+    // at most `per_cu` workgroups per CU: dynamic LDS beyond the kernel's own keeps more from being
+    // resident (the wave slots left to an HBM-bound pass running beside the search)
+    size_t pad = 0;
+    if (per_cu > 0)
+    {
+        constexpr size_t kLdsPerCu = 160 * 1024, kStatic = 14 * 1024;   // the kernel's own ~13.3 KB
+        const size_t want          = kLdsPerCu / (size_t) (per_cu + 1) + 1;
+        pad                        = want > kStatic ? want - kStatic : 0;
+    }
+    launch_kernel(t.first, t.dev, t.n, t.total, bw, sym, strict, unsign, s, pad);
 }
 
 namespace

@@ -85,6 +85,8 @@ void* take_pinned(size_t bytes, size_t* real);
 hipEvent_t take_event();
 void give_event(hipEvent_t e);
 void release_request(aimet_encoding_request* r);
+// the host's wait for an event it is about to read results behind: polls, then blocks (quantizer.cpp)
+void await_event(hipEvent_t e);
 void release_request_after_error(aimet_encoding_request* r);
 
 // The device half of a batched getEncoding (throws; the caller releases `req` on failure): every

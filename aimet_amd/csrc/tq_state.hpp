@@ -151,6 +151,8 @@ struct TfeTable
     int64_t total = 0;               // channels
     uint64_t* part = nullptr;        // split search: 2 * total * splits (tfe_splits)
     unsigned* tickets = nullptr;     // split search: `total` zeroed counters
+    int per_cu = 0;                  // > 0: at most that many workgroups resident per CU (its work
+                                     // beside an HBM-bound pass on another stream)
 };
 // workgroups per channel of a batched search of `total` channels (1: one workgroup per channel)
 int tfe_splits(int64_t total, bool sym);

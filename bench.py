@@ -179,7 +179,7 @@ def make_quantizers(acts, weights):
     return aq, wq
 
 
-def time_plan(plan, reps, warm=2, spans=None):
+def time_plan(plan, reps, warm=2, spans=None, phases=None):
     """`warm` untimed, then `reps` timed plan runs that reset and recompute the plan's quantizers
     (one compute_encodings of an existing sim each); returns (median seconds, encodings of the last
     run, every timed run in ms). spans (a list): each run's GPU span in ms, a HIP event on the main
@@ -188,15 +188,23 @@ def time_plan(plan, reps, warm=2, spans=None):
     stream = torch.cuda.current_stream()
     for i in range(warm + reps):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        # the previous run's results are released before the clock starts: freeing its 27,560
+        # encoding objects is not this run's work (it had sat behind the activations' result,
+        # ~0.25 ms of every timed run, profiles/r05/README.md)
+        res = p_res = None
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         e0.record(stream)
         a, p = plan.launch(reset=True)
         e1.record(stream)
+        t1 = time.perf_counter()
         p_res = p.result()
+        t2 = time.perf_counter()
         res = (a.result(), p_res)
         if i >= warm:
             secs.append(time.perf_counter() - t0)
+            if phases is not None:   # host: launch returned, parameters' encodings built (ms)
+                phases.append((round((t1 - t0) * 1e3, 3), round((t2 - t0) * 1e3, 3)))
             if spans is not None:
                 torch.cuda.synchronize()
                 spans.append(round(e0.elapsed_time(e1), 3))
@@ -460,8 +468,9 @@ def main():
     # recompute of every quantizer (aimet_amd.calibration.CalibrationPlan). Sharded at N > 1.
     from aimet_amd.calibration import CalibrationPlan
     cplan = CalibrationPlan(aq, [t for _, t in acts], wq, [w for _, w in weights])
-    enc_spans = []
-    enc_seconds, (a_res, w_res), enc_runs_ms = time_plan(cplan, max(1, args.plan_reps), spans=enc_spans)
+    enc_spans, enc_phases = [], []
+    enc_seconds, (a_res, w_res), enc_runs_ms = time_plan(cplan, max(1, args.plan_reps), spans=enc_spans,
+                                                         phases=enc_phases)
     # the same on quantizers made for the plan alone (a new sim), for comparison
     nq, nw = make_quantizers(acts, weights)
     nplan = CalibrationPlan(nq, [t for _, t in acts], nw, [w for _, w in weights])
@@ -617,6 +626,7 @@ def main():
                    "compute_encodings_resident_s": round(enc_resident, 4),
                    "compute_encodings_runs_ms": enc_runs_ms,
                    "compute_encodings_gpu_span_ms": enc_spans,
+                   "compute_encodings_host_phases_ms": enc_phases,
                    "compute_encodings_new_sim_s": round(enc_new_s, 4),
                    "compute_encodings_new_sim_gpu_span_ms": sorted(new_spans)[len(new_spans) // 2] if new_spans else None,
                    "compute_encodings_plan_equals_resident": enc_plan_equal,
