@@ -250,6 +250,167 @@ __device__ __forceinline__ float pow01_log(float x, float e, bool tail, F2 l)
     return r != r ? __builtin_inff() : r;
 }
 
+// ---- the same pow for two elements at once (packed f32: v_pk_fma / v_pk_mul / v_pk_add) ------
+// Every operation below is the scalar path's, component by component (packed f32 instructions are
+// the IEEE ops per component), so each component is bit-identical to pow01_log / sleef_logkf /
+// sleef_expkf; the few non-arithmetic steps (frexp, rint, ldexp, rcp) run per component. ~110 of the
+// ~142 VALU instructions of one scalar pow are packable adds, multiplies and FMAs, so a pair costs
+// ~87 per element instead of 142: the dense waves of the backward (alpha mostly unsaturated, early
+// in an AdaRound loop) evaluate their elements two at a time.
+typedef float fl2 __attribute__((ext_vector_type(2)));
+struct V2
+{
+    fl2 x, y;
+};
+__device__ __forceinline__ fl2 vfma(fl2 a, fl2 b, fl2 c)
+{
+    return __builtin_elementwise_fma(a, b, c);
+}
+__device__ __forceinline__ fl2 vsplat(float v)
+{
+    return fl2 {v, v};
+}
+__device__ __forceinline__ V2 v2(fl2 x, fl2 y)
+{
+    return V2 {x, y};
+}
+__device__ __forceinline__ V2 vdf_normalize(V2 t)
+{
+    const fl2 s = t.x + t.y;
+    return v2(s, (t.x - s) + t.y);
+}
+__device__ __forceinline__ V2 vdf_add2_ff(fl2 x, fl2 y)
+{
+    const fl2 s = x + y, v = s - x;
+    return v2(s, (x - (s - v)) + (y - v));
+}
+__device__ __forceinline__ V2 vdf_add2_f2f(V2 x, fl2 y)
+{
+    const fl2 s = x.x + y, v = s - x.x;
+    const fl2 t = (x.x - (s - v)) + (y - v);
+    return v2(s, t + x.y);
+}
+__device__ __forceinline__ V2 vdf_add_f2f2(V2 x, V2 y)
+{
+    const fl2 s = x.x + y.x;
+    return v2(s, (((x.x - s) + y.x) + x.y) + y.y);
+}
+__device__ __forceinline__ V2 vdf_add2_f2f2(V2 x, V2 y)
+{
+    const fl2 s = x.x + y.x, v = s - x.x;
+    const fl2 t = (x.x - (s - v)) + (y.x - v);
+    return v2(s, t + (x.y + y.y));
+}
+__device__ __forceinline__ V2 vdf_add_ff2(fl2 x, V2 y)
+{
+    const fl2 s = x + y.x;
+    return v2(s, ((x - s) + y.x) + y.y);
+}
+__device__ __forceinline__ V2 vdf_squ(V2 x)
+{
+    const fl2 s = x.x * x.x;
+    return v2(s, vfma(x.x + x.x, x.y, vfma(x.x, x.x, -s)));
+}
+__device__ __forceinline__ V2 vdf_mul_f2f2(V2 x, V2 y)
+{
+    const fl2 s = x.x * y.x;
+    return v2(s, vfma(x.x, y.y, vfma(x.y, y.x, vfma(x.x, y.x, -s))));
+}
+__device__ __forceinline__ V2 vdf_mul_f2f(V2 x, fl2 y)
+{
+    const fl2 s = x.x * y;
+    return v2(s, vfma(x.y, y, vfma(x.x, y, -s)));
+}
+__device__ __forceinline__ V2 vdf_div(V2 n, V2 d)
+{
+    const fl2 r0 = fl2 {__builtin_amdgcn_rcpf(d.x.x), __builtin_amdgcn_rcpf(d.x.y)};
+    const fl2 t  = vfma(vfma(-d.x, r0, vsplat(1.0f)), r0, r0), s = n.x * t;
+    const fl2 u  = vfma(t, n.x, -s);
+    const fl2 v  = vfma(-d.y, t, vfma(-d.x, t, vsplat(1.0f)));
+    return v2(s, vfma(s, v, vfma(n.y, t, u)));
+}
+__device__ __forceinline__ V2 vsleef_logkf(fl2 d)
+{
+    fl2 e, m;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+    {
+        int ee, em;
+        (void) __builtin_frexpf(d[c] * (1.0f / 0.75f), &ee);
+        e[c]     = (float) (ee - 1);
+        float mc = __builtin_frexpf(d[c], &em) * 2.0f;
+        m[c]     = mc >= 1.5f ? mc * 0.5f : mc;
+    }
+    const V2 x  = vdf_div(v2(vsplat(-1.0f) + m, vsplat(0.0f)), vdf_add2_ff(vsplat(1.0f), m));
+    const V2 x2 = vdf_squ(x);
+    fl2 t       = vsplat(0.240320354700088500976562f);
+    t           = vfma(t, x2.x, vsplat(0.285112679004669189453125f));
+    t           = vfma(t, x2.x, vsplat(0.400007992982864379882812f));
+    const V2 c  = v2(vsplat(0.66666662693023681640625f), vsplat(3.69183861259614332084311e-09f));
+    V2 s        = vdf_mul_f2f(v2(vsplat(0.69314718246459960938f), vsplat(-1.904654323148236017e-09f)), e);
+    s           = vdf_add_f2f2(s, v2(x.x * 2.0f, x.y * 2.0f));
+    return vdf_add_f2f2(s, vdf_mul_f2f2(vdf_mul_f2f2(x2, x), vdf_add2_f2f2(vdf_mul_f2f(x2, t), c)));
+}
+__device__ __forceinline__ fl2 vsleef_expkf(V2 d)
+{
+    const fl2 u0 = (d.x + d.y) * 1.442695040888963407359924681001892137426645954152985934135449406931f;
+    fl2 qf;
+    int q[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+    {
+        q[c]  = (int) __builtin_rintf(u0[c]);
+        qf[c] = (float) q[c];
+    }
+    V2 s = vdf_add2_f2f(d, qf * -0.693145751953125f);
+    s    = vdf_add2_f2f(s, qf * -1.428606765330187045e-06f);
+    s    = vdf_normalize(s);
+    fl2 u = vsplat(0.00136324646882712841033936f);
+    u     = vfma(u, s.x, vsplat(0.00836596917361021041870117f));
+    u     = vfma(u, s.x, vsplat(0.0416710823774337768554688f));
+    u     = vfma(u, s.x, vsplat(0.166665524244308471679688f));
+    u     = vfma(u, s.x, vsplat(0.499999850988388061523438f));
+    V2 t  = vdf_add_f2f2(s, vdf_mul_f2f(vdf_squ(s), u));
+    t     = vdf_add_ff2(vsplat(1.0f), t);
+    const fl2 tv = t.x + t.y;
+    fl2 r;
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+    {
+        const float rc = (q[c] >= -125 && q[c] <= 126) ? __builtin_ldexpf(tv[c], q[c]) : sleef_ldexp(tv[c], q[c]);
+        r[c]           = d.x[c] < -104.0f ? 0.0f : rc;
+    }
+    return r;
+}
+// pow01_log for two elements known to need the logarithm or the tail's double pow (|x| not 0 or
+// 1): `l` = vsleef_logkf(x); components marked `tail` take the double pow
+__device__ __forceinline__ fl2 vpow01_log(fl2 x, float e, bool tail0, bool tail1, V2 l)
+{
+    fl2 r;
+    if (e == 2.0f)
+        r = x * x;
+    else if (e == 3.0f)
+        r = x * x * x;
+    else
+    {
+        r = vsleef_expkf(vdf_mul_f2f(l, vsplat(e)));
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+        {
+            const float xc = x[c];
+            float rc       = r[c] != r[c] ? __builtin_inff() : r[c];
+            if (xc == 0.0f)
+                rc = e == 0.0f ? 1.0f : 0.0f;
+            else if (e == 0.0f || xc == 1.0f)
+                rc = 1.0f;
+            else if (c == 0 ? tail0 : tail1)
+                rc = (float) exp((double) e * log((double) xc));
+            r[c] = rc;
+        }
+    }
+    return r;
+}
+
 // floor(w / d) exactly as the IEEE division gives it, from q = w * rcp (rcp = v_rcp_f32(d), within
 // 1 ulp): |q - RN(w/d)| <= 3.5 ulp(q) < 2^-21 (|q| + 1), so when q lies farther than that from
 // every integer both floors agree; otherwise (and for non-finite q) the division decides.
@@ -403,10 +564,37 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
     if (4 * total >= 3 * 64 * E)
     {
         // a dense wave (few saturated alphas): each lane evaluates its own elements in place, the
-        // compaction's LDS round trip would not pay (the same values)
+        // compaction's LDS round trip would not pay (the same values), two at a time in packed f32
+        // (vsleef_logkf / vpow01_log: component by component the scalar arithmetic). A pair with no
+        // element needing the logarithm skips it; an element that does not need it takes its exact
+        // value (its packed component is computed on a harmless stand-in, 0.5, and dropped).
 #pragma unroll
-        for (int k = 0; k < E; ++k)
+        for (int k = 0; k + 1 < E; k += 2)
         {
+            if (need[k] || need[k + 1])
+            {
+                const fl2 xv {need[k] ? ax[k] : 0.5f, need[k + 1] ? ax[k + 1] : 0.5f};
+                V2 l {vsplat(0.0f), vsplat(0.0f)};
+                if (!(tail[k] && tail[k + 1]))
+                    l = vsleef_logkf(xv);
+                const fl2 r1 = vpow01_log(xv, p.beta_m1, tail[k], tail[k + 1], l);
+                const fl2 r0 = p.want_loss ? vpow01_log(xv, p.beta, tail[k], tail[k + 1], l) : vsplat(0.0f);
+                pbm1[k]     = need[k] ? r1[0] : pow01_exact(ax[k], p.beta_m1);
+                pbm1[k + 1] = need[k + 1] ? r1[1] : pow01_exact(ax[k + 1], p.beta_m1);
+                pb[k]       = need[k] ? r0[0] : pow01_exact(ax[k], p.beta);
+                pb[k + 1]   = need[k + 1] ? r0[1] : pow01_exact(ax[k + 1], p.beta);
+            }
+            else
+            {
+                pbm1[k]     = pow01_exact(ax[k], p.beta_m1);
+                pb[k]       = pow01_exact(ax[k], p.beta);
+                pbm1[k + 1] = pow01_exact(ax[k + 1], p.beta_m1);
+                pb[k + 1]   = pow01_exact(ax[k + 1], p.beta);
+            }
+        }
+        if constexpr (E % 2 == 1)
+        {
+            constexpr int k = E - 1;
             if (need[k])
             {
                 F2 l {0.0f, 0.0f};

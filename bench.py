@@ -33,11 +33,12 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBPS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 BYTES_QDQ = 8            # fp32 read + fp32 write per element
-# HBM bytes per step of the activation QDQ launches from the rocprofv3 PMC passes
-# (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM), profiles/r01/bench_summary_*.txt
+# HBM bytes per step of the activation QDQ launches from the rocprofv3 PMC passes of this bench
+# (FETCH_SIZE x 2 + WRITE_SIZE, MI355X_MICROARCH.md §HBM; separate --pmc FETCH_SIZE / WRITE_SIZE runs,
+# tools/runs/r05/gpu_r05_g.sh): profiles/r05/bench_pmc_summary.txt, 11.5375 + 11.5359 = 23.0734 GB
 # (measured at the default workload: 2,883,971,072 activation elements per step; other batch sizes
-# report null)
-TRAFFIC_GB = 23.075
+# report null). The same figure as rounds 1-4 (the QDQ kernels are unchanged).
+TRAFFIC_GB = 23.0734
 TRAFFIC_ELEMS = 2883971072
 
 

@@ -1,10 +1,10 @@
 """AdaRound backward kernel (aimet_adaround_backward, adaround_bwd_vec_kernel) at 2^28 elements:
 HBM rate for alpha drawn N(0, s^2) -- s = 1: ~2 % of the rectified sigmoids saturate, s = 4: ~55 % --
 with the round-loss value requested (want_loss) or not (the optimisation loop's form). Prints one
-JSON line per case; `checksum` (sum of the gradient's bit patterns) lets runs with different
-AIMET_ADA_BWD_U be compared bit for bit.
+JSON line per case; `checksum` (sum of the gradient's bit patterns) lets runs of different kernel
+forms be compared bit for bit (--tag names the form in the output).
 
-    [AIMET_ADA_BWD_U=2] python tools/studies/ada_bwd_tune.py [--elems N] [--reps R]
+    python tools/studies/ada_bwd_tune.py [--elems N] [--reps R] [--tag NAME]
 """
 import argparse
 import ctypes
@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--channels", type=int, default=4096)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--scales", default="1,4")
+    ap.add_argument("--tag", default="")
     args = ap.parse_args()
     lib = aimet_amd.native_library()
     dev = torch.device("cuda", 0)
@@ -39,7 +40,6 @@ def main():
     rloss = torch.zeros(1, device=dev)
     P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
     s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
-    u = os.environ.get("AIMET_ADA_BWD_U", "1")   # the library's default
     for scale in [float(v) for v in args.scales.split(",")]:
         alpha = torch.randn(N, device=dev, generator=torch.Generator(device=dev).manual_seed(1)) * scale
         sat = float((alpha.abs() > math.log(11.0)).float().mean())
@@ -61,7 +61,7 @@ def main():
             torch.cuda.synchronize()
             ms = ev[0].elapsed_time(ev[1]) / args.reps
             gbps = 16 * N / ms / 1e6
-            print(json.dumps({"kernel": "adaround_bwd_vec_kernel", "U": int(u), "elems": N, "alpha_scale": scale,
+            print(json.dumps({"kernel": "adaround_bwd_vec_kernel", "tag": args.tag, "elems": N, "alpha_scale": scale,
                               "saturated_frac": round(sat, 4), "want_loss": want_loss, "avg_ms": round(ms, 4),
                               "achieved_GBps": round(gbps, 1), "frac_of_peak": round(gbps / 8000, 4),
                               "checksum": int(out.view(torch.int32).to(torch.int64).sum().item()),
