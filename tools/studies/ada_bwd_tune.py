@@ -4,7 +4,7 @@ with the round-loss value requested (want_loss) or not (the optimisation loop's 
 JSON line per case; `checksum` (sum of the gradient's bit patterns) lets runs of different kernel
 forms be compared bit for bit (--tag names the form in the output).
 
-    python tools/studies/ada_bwd_tune.py [--elems N] [--reps R] [--tag NAME]
+    python tools/studies/ada_bwd_tune.py [--elems N] [--reps R] [--tag NAME] [--lib PATH]
 """
 import argparse
 import ctypes
@@ -26,7 +26,10 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--scales", default="1,4")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--lib", default=None, help="another build of libaimet_amd.so")
     args = ap.parse_args()
+    if args.lib:
+        aimet_amd._native.LIB_PATH = os.path.abspath(args.lib)
     lib = aimet_amd.native_library()
     dev = torch.device("cuda", 0)
     N, C = args.elems, args.channels
