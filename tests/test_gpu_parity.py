@@ -438,8 +438,9 @@ def test_adaround_forward_backward_vs_torch(kat):
 def test_adaround_backward_with_round_loss_vs_torch(beta, shape):
     """Fused backward with the rounding loss (reg != 0): dL/dalpha and the loss itself vs torch
     autograd of the reference formulas (adaround_wrapper.py:124-149 + adaround_loss.py:97-110).
-    Wq bit-exact; loss rtol 1e-5 (fp32 sum order); gradient rtol 1e-5 (the rounding-loss branch's
-    pow: correctly rounded here, Sleef powf_u10 in torch; golden bound in test_adaround_golden.py)."""
+    Wq bit-exact; loss rtol 1e-5 (fp32 sum order); gradient rtol 1e-5: the kernel restates the
+    AVX512F build of Sleef's powf_u10 that produced the reference's golden vectors (bit-equal there,
+    test_adaround_golden.py), while torch on this host may dispatch another Sleef build."""
     from aimet_amd.adaround import AdaroundFunction
     from oracle import torch_ref as T
     torch.manual_seed(1)
@@ -463,9 +464,46 @@ def test_adaround_backward_with_round_loss_vs_torch(beta, shape):
     wq = AdaroundFunction.apply(w, a, delta.view(-1), offset.view(-1), 8, 0, True, reg, beta, loss)
     (wq * g).sum().backward()
     assert torch.equal(wq.cpu(), wq_ref)
-    # only the rounding-loss branch's pow differs (correctly rounded here, Sleef powf in torch)
+    # only the rounding-loss branch's pow may differ (the host's Sleef build)
     torch.testing.assert_close(a.grad.cpu(), ga_ref, rtol=1e-5, atol=1e-9)
     assert abs(loss.item() - loss_ref) <= 1e-5 * abs(loss_ref)
+
+
+@pytest.mark.parametrize("beta", [3.0, 4.0, 7.25, 20.0])   # beta - 1 = 2 / 3: x*x / x*x*x (no logarithm)
+@pytest.mark.parametrize("want_loss", [False, True])
+@pytest.mark.parametrize("n, C", [(1 << 19, 64), ((1 << 19) + 16, 1)])   # n % 32 == 16: the scalar pow tail
+def test_adaround_backward_dense_waves_equal_compacted(beta, want_loss, n, C):
+    """The fused backward evaluates the rounding-loss pows of a dense wave (>= 3/4 of its elements
+    need the logarithm) in place, two at a time in packed f32, and those of a sparse wave compacted
+    through LDS with the scalar arithmetic (adaround.hip / sleef_pow.hpp: ada_round_pows). The same
+    element must give the same bits either way: run A has every alpha unsaturated (dense waves),
+    run B saturates 3 of every 4 quads (sparse waves), and the unsaturated quads' gradients of the
+    two runs are compared bit for bit."""
+    from aimet_amd import _native
+    g = torch.Generator(device=DEV).manual_seed(5)
+    K = n // C
+    w = torch.randn(n, device=DEV, generator=g) * 0.05
+    grad = torch.randn(n, device=DEV, generator=g)
+    delta = (w.view(C, K).abs().amax(1) / 127).contiguous()
+    offset = torch.full((C,), -128.0, device=DEV)
+    alpha_a = torch.randn(n, device=DEV, generator=g) * 0.7
+    quad = torch.arange(n, device=DEV) // 4
+    keep = quad % 4 == 0
+    alpha_b = torch.where(keep, alpha_a, torch.full_like(alpha_a, 60.0))
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for alpha in (alpha_a, alpha_b):
+        out = torch.empty_like(w)
+        loss = torch.zeros(1, device=DEV)
+        _native.call("aimet_adaround_backward", w.data_ptr(), alpha.data_ptr(), grad.data_ptr(), out.data_ptr(), 1,
+                     C, K, delta.data_ptr(), offset.data_ptr(), 8, ctypes.c_double(0.01), ctypes.c_double(beta),
+                     loss.data_ptr() if want_loss else None, stream)
+        outs.append(out)
+    torch.cuda.synchronize()
+    a, b = outs[0][keep].view(torch.int32), outs[1][keep].view(torch.int32)
+    assert torch.equal(a, b), int((a != b).sum())
+    # and the saturated quads took the exact |x| == 1 value: the Wq gradient alone (h's clamp passes none)
+    assert torch.isfinite(outs[1]).all()
 
 
 def test_adaround_hard_rounding_floor_exact_at_multiples():
