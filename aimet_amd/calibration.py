@@ -242,10 +242,12 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
     reset=True: resetEncodingStats of every quantizer first (QuantizationSimModel.compute_encodings
     on quantizers that already hold statistics, v1/quantsim.py:387-399).
 
-    On one rank, with AimetTensorQuantizers and float32 tensors, all of it is two native calls
-    (aimet_calibrate_launch for the activations, then for the parameters while the activations'
-    min/max pass runs: about a dozen HIP launches from C++, no Python per phase); otherwise
-    the phases are enqueued from here (sharded with collectives when `group` spans several ranks)."""
+    With AimetTensorQuantizers (per-tensor activations) and contiguous float32 device tensors, all
+    of it is a calibration plan (CalibrationPlan, aimet_calib_plan_*: every job table prepared once
+    and cached for the next call on the same quantizers and tensors): one native launch of about
+    fifteen HIP calls on one rank; on several ranks its three stages with the packed all_reduce(MAX)
+    and all_reduce(SUM) between them. Otherwise the phases are enqueued from here (sharded with the
+    same collectives when `group` spans several ranks)."""
     if not activations and not params:
         if reset:
             AimetTensorQuantizer.resetEncodingStatsMany(list(act_quantizers) + list(param_quantizers))

@@ -168,23 +168,23 @@ def test_bench_calibration_path_equals_oracle(mode):
 def test_config4_vit_sharded_calibration(tmp_path):
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "vit_dist_worker.py")
 
-    def run(world, out):
+    def run(world, out, mode="phased"):
         with socket.socket() as sk:
             sk.bind(("127.0.0.1", 0))
             port = sk.getsockname()[1]
         procs = [subprocess.Popen([sys.executable, worker], env=dict(
             os.environ, RANK=str(r), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-            OUT=out)) for r in range(world)]
+            OUT=out, MODE=mode)) for r in range(world)]
         for p in procs:
             assert p.wait(timeout=300) == 0
         return [json.load(open(out + ".%d" % r)) for r in range(world)]
 
     oracle, = run(1, str(tmp_path / "oracle"))
-    ranks = run(2, str(tmp_path / "rank"))
     assert len(oracle["encodings"]) == 318
     assert oracle["elements"] > 8 * 120e6
-    for r, res in enumerate(ranks):
-        assert res["elements"] == oracle["elements"]
-        bad = [i for i, (a, b) in enumerate(zip(res["encodings"], oracle["encodings"])) if a != b]
-        assert not bad, "rank %d: %d of %d encodings differ from the oracle (first %s)" % (
-            r, len(bad), len(oracle["encodings"]), bad[:5])
+    for mode in ("phased", "plan"):   # sharded_update_stats / the calibration plan's staged launch
+        for r, res in enumerate(run(2, str(tmp_path / mode), mode)):
+            assert res["elements"] == oracle["elements"]
+            bad = [i for i, (a, b) in enumerate(zip(res["encodings"], oracle["encodings"])) if a != b]
+            assert not bad, "%s, rank %d: %d of %d encodings differ from the oracle (first %s)" % (
+                mode, r, len(bad), len(oracle["encodings"]), bad[:5])
