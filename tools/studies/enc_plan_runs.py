@@ -28,7 +28,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--forms", default="both,both_after_resident")
+    ap.add_argument("--lib", default=None, help="another build of libaimet_amd.so")
+    ap.add_argument("--tag", default="")
     args = ap.parse_args()
+    if args.lib:
+        import aimet_amd
+        aimet_amd._native.LIB_PATH = os.path.abspath(args.lib)
     from aimet_amd.calibration import CalibrationPlan
     from workloads.resnet import resnet50
     dev = torch.device("cuda", 0)
@@ -80,7 +85,7 @@ def main():
                 wall.append((t1 - t0) * 1e3)
                 span.append(e0.elapsed_time(e1))
         med = lambda v: sorted(v)[len(v) // 2]
-        print(json.dumps({"form": form, "wall_ms_median": round(med(wall), 4), "wall_ms_min": round(min(wall), 4),
+        print(json.dumps({"form": form, "tag": args.tag, "wall_ms_median": round(med(wall), 4), "wall_ms_min": round(min(wall), 4),
                           "gpu_span_ms_median": round(med(span), 4), "gpu_span_ms_min": round(min(span), 4),
                           "frac_of_8TBps_wall_median": round(8 * n_elem / (med(wall) / 1e3) / 8e12, 4),
                           "wall_ms": [round(v, 3) for v in wall], "host_launch_params_ms": host[:8]}), flush=True)
