@@ -1,14 +1,14 @@
 """Worker of tests/test_configs_gpu.py::test_config4_vit_sharded_calibration (not collected by
-pytest). Config 4 at its stated workload, scaled to one 8-image calibration batch: every activation
+pytest). Config 4 at its stated workload and batch: every activation
 QuantizationSimModel quantizes on ViT-L/16 (workloads/vit.py activation_modules + the model
-input), TF-Enhanced, per-tensor.
+input), TF-Enhanced, per-tensor, over one 32-image calibration batch (config 4's batch size).
 
-  WORLD_SIZE=2: rank r forwards images [4r, 4r+4) on cuda:0 and the ranks calibrate over a gloo
+  WORLD_SIZE=2: rank r forwards images [16r, 16r+16) on cuda:0 and the ranks calibrate over a gloo
                 group (one MAX + one SUM): MODE=phased through
                 aimet_amd.distributed.sharded_update_stats, MODE=plan through
                 compute_encodings_resident -- the native calibration plan's staged launch (318
                 quantizers: the min/max walk form) with the two collectives between its stages;
-  WORLD_SIZE=1 (oracle): forwards the same two 4-image shards, feeds the CPU oracle analyzers
+  WORLD_SIZE=1 (oracle): forwards the same two 16-image shards, feeds the CPU oracle analyzers
                 each quantizer's two shards concatenated as ONE batch (min/max and bin counts do
                 not depend on element order), in a host thread pool.
 Writes every quantizer's 8-bit asymmetric encoding (and the element count) to OUT.<rank>."""
@@ -30,7 +30,7 @@ from aimet_amd.libpymo import QuantizationMode  # noqa: E402
 from aimet_amd.tensor_quantizer import AimetTensorQuantizer  # noqa: E402
 from workloads.vit import activation_modules, vit_l16  # noqa: E402
 
-IMAGES, SHARDS = 8, 2
+IMAGES, SHARDS = 32, 2
 
 
 def shard_activations(model, images, s):
