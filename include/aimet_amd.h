@@ -323,7 +323,8 @@ int aimet_calib_plan_create(aimet_tensor_quantizer* const* act_qs, const float* 
  * after its all_reduce(SUM) of the packed counts, stage 4 (PDF fold + the activations' search).
  * *par_req comes from the stage-1 launch, *act_req from the stage-4 launch (NULL otherwise); both
  * are finished with aimet_tq_get_encodings_finish, and the plan launches its next stage 1 / 4
- * only once the previous request of that kind is finished. */
+ * only once the previous request of that kind is finished. A plan (like its quantizers) is used by
+ * one host thread at a time. */
 int aimet_calib_plan_launch(aimet_calib_plan* plan, int stages, int reset, void* main_stream, void* side_stream,
                             aimet_encoding_request** act_req, aimet_encoding_request** par_req);
 /* Waits for the device, frees the plan (its requests must be finished first). */
