@@ -28,6 +28,9 @@ from aimet_amd.tensor_quantizer import AimetTensorQuantizer  # noqa: E402
 SCHEMES = [QuantizationMode.QUANTIZATION_TF, QuantizationMode.QUANTIZATION_TF_ENHANCED,
            QuantizationMode.QUANTIZATION_PERCENTILE, QuantizationMode.QUANTIZATION_MSE]
 FLAGS = [(0, 0, 0), (1, 0, 0), (1, 1, 0), (1, 0, 1)]
+# the plan's forms also carry the entropy analyzer (its per-batch range widening from the global
+# min/max)
+PLAN_SCHEMES = SCHEMES + [QuantizationMode.QUANTIZATION_ENTROPY]
 
 
 def batches(n_batches=3, batch=8, seed=0):
@@ -65,8 +68,8 @@ def encodings(qs):
 def plan_main(rank, world, force, dev):
     """MODE=plan (see the module docstring)."""
     from aimet_amd.calibration import CalibrationPlan
-    aq = [AimetTensorQuantizer(s) for s in SCHEMES]
-    pq = [AimetTensorQuantizer(s, num_channels=6) for s in SCHEMES]
+    aq = [AimetTensorQuantizer(s) for s in PLAN_SCHEMES]
+    pq = [AimetTensorQuantizer(s, num_channels=6) for s in PLAN_SCHEMES]
     for q in aq + pq:
         if q.quant_scheme == QuantizationMode.QUANTIZATION_PERCENTILE:
             q.setPercentileValue(99.0)

@@ -1795,9 +1795,10 @@ def test_calibration_plan_equals_per_quantizer_updates(schemes):
         [M.QUANTIZATION_TF, M.QUANTIZATION_TF_ENHANCED, M.QUANTIZATION_PERCENTILE, M.QUANTIZATION_MSE,
          M.QUANTIZATION_ENTROPY]
     p_modes = [M.QUANTIZATION_TF_ENHANCED] * 2 if schemes == "tfe" else \
-        [M.QUANTIZATION_TF, M.QUANTIZATION_TF_ENHANCED, M.QUANTIZATION_MSE, M.QUANTIZATION_PERCENTILE]
+        [M.QUANTIZATION_TF, M.QUANTIZATION_TF_ENHANCED, M.QUANTIZATION_MSE, M.QUANTIZATION_PERCENTILE,
+         M.QUANTIZATION_ENTROPY]
     sizes = [1 << 20, 3001, 77777, 1 << 18, 4099][:len(a_modes)]
-    shapes = [(64, 27), (128, 576), (10, 2048), (33, 5)][:len(p_modes)]
+    shapes = [(64, 27), (128, 576), (10, 2048), (33, 5), (17, 300)][:len(p_modes)]
 
     def batch(scale):
         acts = [torch.relu(torch.randn(n, device=DEV, generator=g) * scale * (1 + i)) - 0.1 * i
