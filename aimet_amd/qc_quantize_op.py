@@ -312,6 +312,9 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
 
     def forward(self, *inputs, **kwargs):
         """v1/qc_quantize_op.py:705-745."""
+        ran = self.__dict__.get("_analysis_ran")   # QuantizationSimModel.compute_encodings is watching
+        if ran is not None:
+            ran[0] = True
         quantized_inputs = self._quantize_activation(self.input_quantizers, list(inputs))
         shadow_params = self._quantize_dequantize_params()
         if torch.is_grad_enabled() or not isinstance(self._module_to_wrap, _INPUT_PRESERVING_TYPES):

@@ -56,10 +56,14 @@ def test_config1_quantsim_compute_encodings_equals_oracle(scheme_name):
     sim = QuantizationSimModel(model, batches[0][:1], quant_scheme=scheme, default_output_bw=8, default_param_bw=8)
 
     # every per-tensor quantizer feeds a CPU oracle analyzer with exactly what it was given
+    # (the parameter quantizers' statistics are computed for every wrapper at once before the
+    # forwards, quantsim._precompute_param_encodings, not through update_encoding_stats: their
+    # analyzers are fed the parameter itself, what the first forward would have given them)
     analyzers, pending = {}, []
     pool = cf.ThreadPoolExecutor(THREADS)
-    qmap = {}
+    qmap, params = {}, {}
     for name, w in sim.quant_wrappers():
+        pnames = list(w.param_quantizers.keys())
         for kind, qs in (("in", list(w.input_quantizers)), ("out", list(w.output_quantizers)),
                          ("param", list(w.param_quantizers.values()))):
             for i, q in enumerate(qs):
@@ -67,6 +71,8 @@ def test_config1_quantsim_compute_encodings_equals_oracle(scheme_name):
                     continue
                 key = (name, kind, i)
                 qmap[key] = q
+                if kind == "param":
+                    params[key] = getattr(w._module_to_wrap, pnames[i])
                 upd = q.update_encoding_stats
 
                 def u(t, upd=upd, key=key, q=q):
@@ -97,6 +103,10 @@ def test_config1_quantsim_compute_encodings_equals_oracle(scheme_name):
     sim.compute_encodings(calibrate, None)
     torch.cuda.synchronize()
     pool.shutdown()
+    for key, t in params.items():
+        if key not in analyzers:
+            analyzers[key] = O.Analyzer(mode)
+            analyzers[key].update(t.detach().float().reshape(-1).cpu().numpy())
     checked, bad = 0, []
     for key, q in qmap.items():
         if not q.enabled or q.encoding is None or key not in analyzers:

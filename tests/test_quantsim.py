@@ -252,3 +252,64 @@ def test_qat_step_gates_parameter_gradients():
         maxs = torch.tensor([e.max for e in pq.encoding], dtype=torch.float32, device="cuda").view(shape)
         outside = (wt.detach() < mins) | (wt.detach() > maxs)
         assert (g[outside] == 0).all(), name
+
+
+class BranchNet(nn.Module):
+    """Two layers the forward runs and one it never calls."""
+
+    def __init__(self):
+        super().__init__()
+        self.fc1 = nn.Linear(64, 32)
+        self.fc2 = nn.Linear(32, 10)
+        self.unused = nn.Linear(64, 10)
+
+    def forward(self, x):
+        return self.fc2(torch.relu(self.fc1(x)))
+
+
+def _quantizer_state(sim):
+    out = {}
+    for name, w in sim.quant_wrappers():
+        for kind, qs in (("in", list(w.input_quantizers)), ("out", list(w.output_quantizers)),
+                         ("param", [w.param_quantizers[k] for k in sorted(w.param_quantizers)])):
+            for i, q in enumerate(qs):
+                enc = q.encoding
+                encs = enc if isinstance(enc, list) else ([] if enc is None else [enc])
+                out[(name, kind, i)] = (bool(q.enabled), [(e.min, e.max, e.delta, e.offset, e.bw) for e in encs])
+    return out
+
+
+@pytest.mark.gpu
+@gpu
+@pytest.mark.parametrize("scheme", ["tf_enhanced", "tf", "percentile"])
+@pytest.mark.parametrize("per_channel", [False, True])
+def test_compute_encodings_precomputed_parameter_encodings_equal_per_wrapper(monkeypatch, scheme, per_channel):
+    """compute_encodings computes the executed wrappers' parameter encodings up front in batched
+    calls (quantsim._precompute_param_encodings) instead of one at a time inside the first ANALYSIS
+    forward: every quantizer of the sim -- parameters, inputs, outputs, enabled flags -- ends as with
+    the per-wrapper computation, a wrapper no forward runs included (no encoding, as the reference
+    leaves it), over two calibrations of the same sim."""
+    import aimet_amd.quantsim as QS
+    data = [torch.randn(16, 64, device="cuda", generator=torch.Generator(device="cuda").manual_seed(i))
+            for i in range(2)]
+
+    def run(precompute):
+        torch.manual_seed(3)
+        net = BranchNet().cuda().eval()
+        sim = QuantizationSimModel(net, torch.randn(1, 64, device="cuda"), quant_scheme=scheme,
+                                   config_file=PER_CHANNEL_CFG if per_channel else None)
+        if scheme == "percentile":
+            sim.set_percentile_value(99.9)
+        if not precompute:
+            monkeypatch.setattr(QS, "_precompute_param_encodings", lambda wrappers: [])
+        states = []
+        for _ in range(2):
+            sim.compute_encodings(lambda m, d: [m(x) for x in d], data)
+            states.append(_quantizer_state(sim))
+        monkeypatch.undo()
+        return states
+
+    per_wrapper = run(False)
+    batched = run(True)
+    assert batched == per_wrapper
+    assert per_wrapper[0][("unused", "param", sorted(["weight", "bias"]).index("weight"))][1] == []
