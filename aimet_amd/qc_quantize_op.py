@@ -45,6 +45,55 @@ TF_ENHANCED_STRIDE_FACTOR = 2
 # runs under this lock so the replicas never interleave on one quantizer's device state
 _REPLICA_LOCK = threading.Lock()
 
+
+class StatsBatch:
+    """The activation statistics of QuantizationSimModel.compute_encodings' ANALYSIS forwards,
+    batched: a wrapper hands (quantizer, tensor) here instead of launching the quantizer's update
+    (aimet_tq_update_stats: ~4 launches and ~25 us of host time each), and flush() updates every
+    pending quantizer with one AimetTensorQuantizer.updateStatsMany call per device (one launch per
+    phase). Each quantizer still sees its tensors in the order the forward produced them: a second
+    tensor for a pending quantizer flushes first. The tensors stay alive until flushed, so at most
+    `limit` elements are held (then flushed); compute_encodings flushes after every forward of the
+    model and at the end. Shared by DataParallel replicas (their wrappers' __dict__ is a shallow copy)."""
+
+    def __init__(self, limit: int = 1 << 30):
+        self.limit = limit
+        self.lock = threading.Lock()
+        self.items = []
+        self.pending = set()
+        self.elems = 0
+
+    @staticmethod
+    def eligible(q, t) -> bool:
+        from aimet_amd.quantizers import StaticGridPerTensorQuantizer
+        from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+        return (type(q) is StaticGridPerTensorQuantizer and q.enabled and not q._is_encoding_frozen and
+                q.bitwidth != 32 and q.data_type == QuantizationDataType.int and
+                q.encoding_min_max_fixed_vals is None and isinstance(t, torch.Tensor) and t.is_cuda and
+                t.dtype == torch.float32 and type(q._op()) is AimetTensorQuantizer)
+
+    def add(self, q, t):
+        with self.lock:
+            if id(q) in self.pending or self.elems + t.numel() > self.limit:
+                self._flush_locked()
+            self.items.append((q, t if t.is_contiguous() else t.contiguous()))
+            self.pending.add(id(q))
+            self.elems += t.numel()
+
+    def flush(self):
+        with self.lock:
+            self._flush_locked()
+
+    def _flush_locked(self):
+        from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+        items, self.items, self.pending, self.elems = self.items, [], set(), 0
+        by_dev = {}
+        for q, t in items:
+            by_dev.setdefault(t.device, []).append((q, t))
+        for dev, group in by_dev.items():
+            with torch.cuda.device(dev):
+                AimetTensorQuantizer.updateStatsMany([q._op() for q, _ in group], [t for _, t in group])
+
 _IGNORED_DTYPES = (torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64, torch.bool)
 # wrapped modules that never modify their inputs in place
 _INPUT_PRESERVING_TYPES = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d, nn.ConvTranspose2d,
@@ -392,10 +441,14 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
                 return t
             if self._mode is QcQuantizeOpMode.ANALYSIS and not q.is_encoding_frozen:
                 if TF_ENHANCED_USE_DOWNSAMPLING and q.quant_scheme == QuantScheme.post_training_tf_enhanced:
-                    q.update_encoding_stats(t.reshape(-1)[TF_ENHANCED_OFFSET_FACTOR::TF_ENHANCED_STRIDE_FACTOR]
-                                            .contiguous())
+                    x = t.reshape(-1)[TF_ENHANCED_OFFSET_FACTOR::TF_ENHANCED_STRIDE_FACTOR].contiguous()
                 else:
-                    q.update_encoding_stats(t)
+                    x = t
+                batch = self.__dict__.get("_stats_batch")   # QuantizationSimModel.compute_encodings
+                if batch is not None and StatsBatch.eligible(q, x):
+                    batch.add(q, x)
+                else:
+                    q.update_encoding_stats(x)
                 return t
             if self._mode is QcQuantizeOpMode.ACTIVE or \
                     (self._mode is QcQuantizeOpMode.ANALYSIS and q.is_encoding_frozen):

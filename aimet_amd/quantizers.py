@@ -182,6 +182,9 @@ class StaticGridTensorQuantizer:
                                       all(e.min >= 0 and e.max >= 0 for e in self._encoding))
 
     def quantize_dequantize(self, tensor, round_mode):
+        if not (torch.is_grad_enabled() and isinstance(tensor, torch.Tensor) and tensor.requires_grad):
+            # no graph would be recorded: the forward's values without the autograd call
+            return _qdq_values(tensor, self, _round_mode(round_mode))
         return QuantizeDequantize.apply(tensor, self, _round_mode(round_mode))
 
     def quantize(self, tensor, round_mode):
@@ -400,6 +403,33 @@ def _ste_bounds(tq, device):
     return hit[1], hit[2]
 
 
+def _qdq_values(tensor, tq, round_mode):
+    """QuantizeDequantize's forward values (v1/tensor_quantizer.py:1098-1168)."""
+    if not tq.enabled or tq.bitwidth == 32:
+        return tensor
+    if tq.data_type == QuantizationDataType.float:
+        if tq.bitwidth == 16:
+            return tensor.half().float()
+        raise NotImplementedError("fp8 quantization is outside the MI355X integer QDQ core")
+    dtype = tensor.dtype
+    # a CPU tensor is staged through HBM (the same kernels; the result goes back to the host)
+    if tensor.is_cuda:
+        t, staged = tensor, False
+    else:
+        t, staged = _stage(tensor if dtype in IO_DTYPES else tensor.to(torch.float32), "tensor", allow_16bit=True)
+    # fp16 / bf16 go through the fused 16-bit I/O kernels (identical to the reference's
+    # upcast -> fp32 QDQ -> downcast, v1/tensor_quantizer.py:1116-1168); others upcast
+    t = t if dtype in IO_DTYPES else t.to(torch.float32)
+    if isinstance(tq, StaticGridPerChannelQuantizer):
+        t = t.contiguous()
+        outer, C, K = per_channel_view(t.shape, tq.channel_axis)
+        table = tq.channel_table(t.device)
+        out = qdq_per_channel_table(t, table, outer, C, K, round_mode)
+    else:
+        out = AimetTensorQuantizer.quantize_dequantize_tensor(t, tq.encoding, round_mode)
+    return out.to(dtype).cpu() if staged else out.to(dtype)
+
+
 class QuantizeDequantize(torch.autograd.Function):
     """v1/tensor_quantizer.py:1098-1213."""
 
@@ -407,32 +437,10 @@ class QuantizeDequantize(torch.autograd.Function):
     def forward(ctx, tensor, tensor_quantizer, round_mode):
         tq = tensor_quantizer
         ctx.tensor_quantizer = tq
-        if not tq.enabled or tq.bitwidth == 32:
-            return tensor
-        if tq.data_type == QuantizationDataType.float:
-            if tq.bitwidth == 16:
-                out = tensor.half().float()
-                ctx.save_for_backward(tensor)
-                return out
-            raise NotImplementedError("fp8 quantization is outside the MI355X integer QDQ core")
-        dtype = tensor.dtype
-        # a CPU tensor is staged through HBM (the same kernels; the result goes back to the host)
-        if tensor.is_cuda:
-            t, staged = tensor, False
-        else:
-            t, staged = _stage(tensor if dtype in IO_DTYPES else tensor.to(torch.float32), "tensor", allow_16bit=True)
-        # fp16 / bf16 go through the fused 16-bit I/O kernels (identical to the reference's
-        # upcast -> fp32 QDQ -> downcast, v1/tensor_quantizer.py:1116-1168); others upcast
-        t = t if dtype in IO_DTYPES else t.to(torch.float32)
-        if isinstance(tq, StaticGridPerChannelQuantizer):
-            t = t.contiguous()
-            outer, C, K = per_channel_view(t.shape, tq.channel_axis)
-            table = tq.channel_table(t.device)
-            out = qdq_per_channel_table(t, table, outer, C, K, round_mode)
-        else:
-            out = AimetTensorQuantizer.quantize_dequantize_tensor(t, tq.encoding, round_mode)
-        ctx.save_for_backward(tensor)
-        return out.to(dtype).cpu() if staged else out.to(dtype)
+        out = _qdq_values(tensor, tq, round_mode)
+        if out is not tensor:
+            ctx.save_for_backward(tensor)
+        return out
 
     @staticmethod
     def backward(ctx, grad):

@@ -28,7 +28,7 @@ import torch
 from torch import nn
 
 from aimet_amd.qc_quantize_op import (QUANTIZER_TYPE_INPUT, QUANTIZER_TYPE_OUTPUT, LearnedGridQuantWrapper,
-                                      QcQuantizeOpMode, QcQuantizeWrapper, StaticGridQuantWrapper,
+                                      QcQuantizeOpMode, QcQuantizeWrapper, StaticGridQuantWrapper, StatsBatch,
                                       construct_learned_grid_wrapper)
 from aimet_amd.quantizers import QuantizationDataType, QuantScheme, compute_encodings_batched
 
@@ -171,11 +171,13 @@ class QuantizationSimModel:
         """v1/quantsim.py:381-449: reset, ANALYSIS forward(s), encodings, ACTIVE; range-learning
         schemes then swap in the trainable wrappers (v1/quantsim.py:423, 833-846).
 
-        The resets of every static-grid quantizer are one batched call, and the parameter
-        encodings the first ANALYSIS forward would compute wrapper by wrapper (a statistics
-        launch, a device search and a synchronisation per parameter, v1/qc_quantize_op.py:753-798)
-        are computed for every wrapper at once beforehand (_precompute_param_encodings): the same
-        encodings, since the parameters do not change during the forwards."""
+        The resets of every static-grid quantizer are one batched call, the parameter encodings the
+        first ANALYSIS forward would compute wrapper by wrapper (a statistics launch, a device search
+        and a synchronisation per parameter, v1/qc_quantize_op.py:753-798) are computed for every
+        wrapper at once beforehand (_precompute_param_encodings: the same encodings, since the
+        parameters do not change during the forwards), and the activation statistics of each
+        forward are launched together when the model's forward returns (StatsBatch: the same
+        statistics, every quantizer updated in its own order)."""
         wrappers = [w for _, w in self.quant_wrappers()]
         _reset_many(wrappers)
         for w in wrappers:
@@ -184,9 +186,18 @@ class QuantizationSimModel:
                 w.set_percentile_value(self._percentile_value)
         with _eval_mode(self.model), torch.no_grad():
             pre = _precompute_param_encodings(wrappers)
+            batch = StatsBatch()
+            static = [w for w in wrappers if isinstance(w, StaticGridQuantWrapper)]
+            for w in static:
+                w.__dict__["_stats_batch"] = batch
+            hook = self.model.register_forward_hook(lambda *_: batch.flush())
             try:
                 forward_pass_callback(self.model, forward_pass_callback_args)
+                batch.flush()
             finally:
+                hook.remove()
+                for w in static:
+                    w.__dict__.pop("_stats_batch", None)
                 _forget_unused_param_encodings(pre)
         # every activation / param quantizer of the model in one batched native call per setting
         # range-learning wrappers keep their trained ranges (they have no statistics)

@@ -45,7 +45,7 @@ def _resnet():
 
 
 @pytest.mark.parametrize("scheme_name", ["post_training_tf_enhanced", "post_training_tf"])
-def test_config1_quantsim_compute_encodings_equals_oracle(scheme_name):
+def test_config1_quantsim_compute_encodings_equals_oracle(scheme_name, monkeypatch):
     from aimet_amd.quantizers import QuantScheme, StaticGridPerTensorQuantizer
     from aimet_amd.quantsim import QuantizationSimModel
     scheme = getattr(QuantScheme, scheme_name)
@@ -80,6 +80,18 @@ def test_config1_quantsim_compute_encodings_equals_oracle(scheme_name):
                         pending.append((key, t.detach().float().reshape(-1).cpu().numpy()))
                     return upd(t)
                 q.update_encoding_stats = u
+
+    # the ANALYSIS forwards hand the activation quantizers' tensors to a StatsBatch (one batched
+    # update per forward) instead of update_encoding_stats: record them there too
+    from aimet_amd import qc_quantize_op as QO
+    keys = {id(q): key for key, q in qmap.items()}
+    orig_add = QO.StatsBatch.add
+
+    def add(self, q, t):
+        if id(q) in keys:
+            pending.append((keys[id(q)], t.detach().float().reshape(-1).cpu().numpy()))
+        return orig_add(self, q, t)
+    monkeypatch.setattr(QO.StatsBatch, "add", add)
 
     def flush():
         # one batch: the analyzers of different quantizers update in parallel, each in batch order

@@ -255,7 +255,8 @@ def test_qat_step_gates_parameter_gradients():
 
 
 class BranchNet(nn.Module):
-    """Two layers the forward runs and one it never calls."""
+    """Two layers the forward runs -- the first twice per forward, so its quantizers see two tensors
+    per batch -- and one it never calls."""
 
     def __init__(self):
         super().__init__()
@@ -264,7 +265,7 @@ class BranchNet(nn.Module):
         self.unused = nn.Linear(64, 10)
 
     def forward(self, x):
-        return self.fc2(torch.relu(self.fc1(x)))
+        return self.fc2(torch.relu(self.fc1(x)) + self.fc1(x * 0.5))
 
 
 def _quantizer_state(sim):
@@ -286,9 +287,12 @@ def _quantizer_state(sim):
 def test_compute_encodings_precomputed_parameter_encodings_equal_per_wrapper(monkeypatch, scheme, per_channel):
     """compute_encodings computes the executed wrappers' parameter encodings up front in batched
     calls (quantsim._precompute_param_encodings) instead of one at a time inside the first ANALYSIS
-    forward: every quantizer of the sim -- parameters, inputs, outputs, enabled flags -- ends as with
-    the per-wrapper computation, a wrapper no forward runs included (no encoding, as the reference
-    leaves it), over two calibrations of the same sim."""
+    forward, and launches each forward's activation statistics together (qc_quantize_op.StatsBatch)
+    instead of one update per quantizer: every quantizer of the sim -- parameters, inputs, outputs,
+    enabled flags -- ends as with the per-wrapper, per-call computation, a layer run twice per
+    forward and a wrapper no forward runs included (no encoding, as the reference leaves it), over
+    two calibrations of the same sim."""
+    import aimet_amd.qc_quantize_op as QO
     import aimet_amd.quantsim as QS
     data = [torch.randn(16, 64, device="cuda", generator=torch.Generator(device="cuda").manual_seed(i))
             for i in range(2)]
@@ -302,6 +306,7 @@ def test_compute_encodings_precomputed_parameter_encodings_equal_per_wrapper(mon
             sim.set_percentile_value(99.9)
         if not precompute:
             monkeypatch.setattr(QS, "_precompute_param_encodings", lambda wrappers: [])
+            monkeypatch.setattr(QO.StatsBatch, "eligible", staticmethod(lambda q, t: False))
         states = []
         for _ in range(2):
             sim.compute_encodings(lambda m, d: [m(x) for x in d], data)
