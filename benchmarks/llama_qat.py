@@ -127,6 +127,8 @@ def main():
     ap.add_argument("--path", choices=["quantsim", "module", "plain"], default="quantsim",
                     help="plain: the same model and step without any quantizer (the floor QAT adds to)")
     ap.add_argument("--act-bw", type=int, default=16)
+    ap.add_argument("--profile-calib", action="store_true",
+                    help="print a cProfile of QuantizationSimModel.compute_encodings (top functions by own time)")
     ap.add_argument("--dump-first", default=None,
                     help="save the first step's loss, per-parameter weight-gradient sums and the encoding "
                          "range gradients to this path (full-size parity of --impl fused vs reference: "
@@ -188,9 +190,23 @@ def main():
         def calibrate(m, ids):
             with torch.autocast("cuda", dtype=torch.bfloat16):
                 m(ids)
+        if args.profile_calib:
+            import cProfile
+            import io
+            import pstats
+            pr = cProfile.Profile()
+            pr.enable()
         sim.compute_encodings(calibrate, ids_cal)
         torch.cuda.synchronize()
         calib_s = time.perf_counter() - t0
+        if args.profile_calib:
+            pr.disable()
+            buf = io.StringIO()
+            pstats.Stats(pr, stream=buf).sort_stats("tottime").print_stats(25)
+            print(buf.getvalue(), file=sys.stderr)
+            buf = io.StringIO()
+            pstats.Stats(pr, stream=buf).sort_stats("cumtime").print_stats(25)
+            print(buf.getvalue(), file=sys.stderr)
         wrappers = [w for w in sim.model.modules() if isinstance(w, LearnedGridQuantWrapper)]
         assert len(wrappers) == len(qlin), (len(wrappers), len(qlin))
         n_act = sum(w._module_to_wrap.weight.shape[0] for w in wrappers) * args.seq
