@@ -48,10 +48,10 @@ _REPLICA_LOCK = threading.Lock()
 
 class StatsBatch:
     """The activation statistics of QuantizationSimModel.compute_encodings' ANALYSIS forwards,
-    batched: a wrapper hands (quantizer, tensor) here instead of launching the quantizer's update
-    (aimet_tq_update_stats: ~4 launches and ~25 us of host time each), and flush() updates every
-    pending quantizer with one AimetTensorQuantizer.updateStatsMany call per device (one launch per
-    phase). Each quantizer still sees its tensors in the order the forward produced them: a second
+    batched: a wrapper hands (quantizer, a copy of the tensor) here instead of launching the
+    quantizer's update (aimet_tq_update_stats: ~4 launches and ~25 us of host time each; the copy
+    is one), and flush() updates every pending quantizer with one AimetTensorQuantizer.updateStatsMany
+    call per device (one launch per phase). Each quantizer still sees its tensors in the order the forward produced them: a second
     tensor for a pending quantizer flushes first. The tensors stay alive until flushed, so at most
     `limit` elements are held (then flushed); compute_encodings flushes after every forward of the
     model and at the end. Shared by DataParallel replicas (their wrappers' __dict__ is a shallow copy)."""
@@ -72,11 +72,17 @@ class StatsBatch:
                 q.encoding_min_max_fixed_vals is None and isinstance(t, torch.Tensor) and t.is_cuda and
                 t.dtype == torch.float32 and type(q._op()) is AimetTensorQuantizer)
 
-    def add(self, q, t):
+    def add(self, q, t, owned: bool = False):
+        """Queue q's update with t. Unless the caller owns t (a copy nobody else sees), t is copied
+        first: the network may overwrite it in place before the flush (nn.ReLU(inplace=True),
+        `out += identity`), and the statistics must see the values the quantizer was given -- what
+        the per-call update, launched at once on the stream, reads."""
+        if not owned or not t.is_contiguous():
+            t = t.clone(memory_format=torch.contiguous_format)
         with self.lock:
             if id(q) in self.pending or self.elems + t.numel() > self.limit:
                 self._flush_locked()
-            self.items.append((q, t if t.is_contiguous() else t.contiguous()))
+            self.items.append((q, t))
             self.pending.add(id(q))
             self.elems += t.numel()
 
@@ -446,7 +452,7 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
                     x = t
                 batch = self.__dict__.get("_stats_batch")   # QuantizationSimModel.compute_encodings
                 if batch is not None and StatsBatch.eligible(q, x):
-                    batch.add(q, x)
+                    batch.add(q, x, owned=x is not t and x._base is None)
                 else:
                     q.update_encoding_stats(x)
                 return t

@@ -87,10 +87,10 @@ def test_config1_quantsim_compute_encodings_equals_oracle(scheme_name, monkeypat
     keys = {id(q): key for key, q in qmap.items()}
     orig_add = QO.StatsBatch.add
 
-    def add(self, q, t):
+    def add(self, q, t, owned=False):
         if id(q) in keys:
             pending.append((keys[id(q)], t.detach().float().reshape(-1).cpu().numpy()))
-        return orig_add(self, q, t)
+        return orig_add(self, q, t, owned)
     monkeypatch.setattr(QO.StatsBatch, "add", add)
 
     def flush():

@@ -256,7 +256,8 @@ def test_qat_step_gates_parameter_gradients():
 
 class BranchNet(nn.Module):
     """Two layers the forward runs -- the first twice per forward, so its quantizers see two tensors
-    per batch -- and one it never calls."""
+    per batch, and its first output is then overwritten in place (as nn.ReLU(inplace=True) and
+    `out += identity` do in torchvision's ResNet) -- and one it never calls."""
 
     def __init__(self):
         super().__init__()
@@ -265,7 +266,11 @@ class BranchNet(nn.Module):
         self.unused = nn.Linear(64, 10)
 
     def forward(self, x):
-        return self.fc2(torch.relu(self.fc1(x)) + self.fc1(x * 0.5))
+        a = self.fc1(x)
+        a.relu_()
+        b = self.fc1(x * 0.5)
+        b += a
+        return self.fc2(b)
 
 
 def _quantizer_state(sim):
