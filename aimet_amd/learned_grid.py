@@ -15,10 +15,12 @@ arithmetic for bitwidth <= 8 -- a documented difference, results are then at lea
 import ctypes
 import math
 
+import numpy as np
+
 import torch
 
 from aimet_amd import _native
-from aimet_amd.libpymo import TfEncoding
+from aimet_amd.libpymo import TfEncoding, encodings_to_c
 from aimet_amd.tensor_quantizer import IO_DTYPES, _stage, _stream, per_channel_view
 
 
@@ -443,12 +445,23 @@ class LearnedGridTensorQuantizer:
     def _set_encoding_min_max_parameters(self, encodings):
         """v1/tensor_quantizer.py:821-852 (float32 parameters on the wrapper's device)."""
         encs = encodings if isinstance(encodings, list) else [encodings]
+        if len(encs) > 1:
+            arr = _encoding_array(encs)
+            self._set_min_max_arrays(arr["min"], arr["max"])
+            return
+        self._set_min_max_arrays(np.array([float(e.min) for e in encs]), np.array([float(e.max) for e in encs]))
+
+    def _set_min_max_arrays(self, mins, maxs):
+        """The encoding-min / -max Parameters from float64 arrays (rounded to float32 as
+        torch.tensor([python floats], dtype=float32) rounds them)."""
         params = self.wrapper_ref._parameters
         dev = self.wrapper_ref.device
         params[self.name + "_encoding_min"] = torch.nn.Parameter(
-            torch.tensor([float(e.min) for e in encs], dtype=torch.float32).to(dev), requires_grad=True)
+            torch.from_numpy(np.ascontiguousarray(mins, dtype=np.float64)).to(torch.float32).to(dev),
+            requires_grad=True)
         params[self.name + "_encoding_max"] = torch.nn.Parameter(
-            torch.tensor([float(e.max) for e in encs], dtype=torch.float32).to(dev), requires_grad=True)
+            torch.from_numpy(np.ascontiguousarray(maxs, dtype=np.float64)).to(torch.float32).to(dev),
+            requires_grad=True)
 
     def freeze_encoding(self):
         """v1/tensor_quantizer.py:854-869."""
@@ -476,6 +489,20 @@ class LearnedGridTensorQuantizer:
                                                    self.is_unsigned_symmetric, self._ch_axis, out_dtype)
 
 
+_TF_ENCODING_DTYPE = np.dtype({"names": ["min", "max", "delta", "offset", "bw"],
+                               "formats": ["<f8", "<f8", "<f8", "<f8", "<i4"],
+                               "offsets": [_native.TfEncodingC.min.offset, _native.TfEncodingC.max.offset,
+                                           _native.TfEncodingC.delta.offset, _native.TfEncodingC.offset.offset,
+                                           _native.TfEncodingC.bw.offset],
+                               "itemsize": ctypes.sizeof(_native.TfEncodingC)})
+
+
+def _encoding_array(encodings):
+    """A numpy structured array (min, max, delta, offset, bw) of a sequence of TfEncoding: one
+    C-level copy."""
+    return np.frombuffer(encodings_to_c(encodings), dtype=_TF_ENCODING_DTYPE)
+
+
 def initialize_learned_grid_quantizer_attributes(new_quantizer, old_quantizer):
     """v1/tensor_quantizer.py:1285-1344: copy a static-grid quantizer's settings and encodings;
     symmetric ranges become strictly symmetric (min = -max), unsigned-symmetric ones signed."""
@@ -493,6 +520,18 @@ def initialize_learned_grid_quantizer_attributes(new_quantizer, old_quantizer):
         return
     encoding = old_quantizer.encoding
     encs = encoding if isinstance(encoding, list) else ([encoding] if encoding is not None else [])
+    if len(encs) > 1 and new_quantizer.enabled and not new_quantizer._is_encoding_frozen:
+        # per-channel (Llama-3-8B: 1.5 M channels): the same values from arrays, without a Python
+        # assignment per channel; the static-grid quantizer being replaced keeps its encodings
+        arr = _encoding_array(encs)
+        if int(arr["bw"][0]) != new_quantizer.bitwidth:
+            new_quantizer.encoding = encoding   # the setter's bitwidth error
+        maxs = arr["max"]
+        mins = -maxs if old_quantizer.enabled and (
+            (old_quantizer.use_symmetric_encodings and not old_quantizer.is_unsigned_symmetric) or
+            old_quantizer.is_unsigned_symmetric) else arr["min"]
+        new_quantizer._set_min_max_arrays(mins, maxs)
+        return
     if old_quantizer.enabled and old_quantizer.use_symmetric_encodings and not old_quantizer.is_unsigned_symmetric:
         for e in encs:
             e.min = -e.max
