@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--scales", default="1,4")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--reg", type=float, default=0.01, help="reg_param (0: no rounding loss, no pow)")
     ap.add_argument("--lib", default=None, help="another build of libaimet_amd.so")
     args = ap.parse_args()
     if args.lib:
@@ -51,7 +52,7 @@ def main():
                 if want_loss:
                     rloss.zero_()
                 rc = lib.aimet_adaround_backward(P(w), P(alpha), P(grad), P(out), 1, C, K, P(delta), P(offset), 8,
-                                                 ctypes.c_double(0.01), ctypes.c_double(10.0),
+                                                 ctypes.c_double(args.reg), ctypes.c_double(10.0),
                                                  P(rloss) if want_loss else None, s)
                 assert rc == 0, rc
             call()
@@ -64,7 +65,7 @@ def main():
             torch.cuda.synchronize()
             ms = ev[0].elapsed_time(ev[1]) / args.reps
             gbps = 16 * N / ms / 1e6
-            print(json.dumps({"kernel": "adaround_bwd_vec_kernel", "tag": args.tag, "elems": N, "alpha_scale": scale,
+            print(json.dumps({"kernel": "adaround_bwd_vec_kernel", "tag": args.tag, "reg": args.reg, "elems": N, "alpha_scale": scale,
                               "saturated_frac": round(sat, 4), "want_loss": want_loss, "avg_ms": round(ms, 4),
                               "achieved_GBps": round(gbps, 1), "frac_of_peak": round(gbps / 8000, 4),
                               "checksum": int(out.view(torch.int32).to(torch.int64).sum().item()),
