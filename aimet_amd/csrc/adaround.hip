@@ -27,7 +27,7 @@ namespace
 constexpr float kGamma = -0.1f;
 // python: (ZETA - GAMMA) = 1.2000000000000002 -> float32 scalar 1.2f in the torch op
 constexpr float kZmG = (float) (1.1 - (-0.1));
-constexpr int kAdaBwdGrid = 8192;   // 32 workgroups per CU; bounds the round-loss atomics
+constexpr int kAdaBwdGrid = 8192;   // 32 workgroups per CU; bounds the round-loss partials
 
 struct AdaChannel
 {
@@ -1075,6 +1075,8 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
         require_device_ptr(delta, "delta");
         require_device_ptr(offset, "offset");
         AdaChannel map {FastDiv((uint32_t) (K > 0 ? K : 1)), FastDiv((uint32_t) C), (uint32_t) C};
+        if ((float) reg == 0.0f && !reg_beta)   // the kernels add no loss term at reg 0: no partials to fold
+            round_loss = nullptr;
         AdaParams p {(float) ((1ull << bw) - 1), (float) reg, (float) beta, (float) (beta - 1.0), 1,
                      (uint32_t) (n - n % 32), round_loss != nullptr};
         hipStream_t st = as_stream(stream);
@@ -1086,7 +1088,12 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
             // profiles/r04/ada_bwd_tune_tail_flag.jsonl)
             constexpr int U   = 1;
             int64_t blocks    = ceil_div(nq, kBlock * U);
-            const unsigned gx = (unsigned) (blocks < kAdaBwdGrid ? blocks : kAdaBwdGrid);
+            // one tile per workgroup unless round-loss partials are folded (one per workgroup): a
+            // grid-stride loop over 8192 workgroups holds the 3-read + 1-write stream to 0.60 of
+            // 8 TB/s, a full grid reaches 0.78-0.82 (tools/studies/stream_mix.hip); without the
+            // pow (reg 0) the kernel follows, 0.58 -> 0.79-0.82 (profiles/r05/ada_bwd_grid.jsonl)
+            const int64_t cap = round_loss ? kAdaBwdGrid : blocks;
+            const unsigned gx = (unsigned) (blocks < cap ? blocks : cap);
             LossFold lf(round_loss, gx, st);
             auto launch = [&](auto kernel) {
                 kernel<<<gx, kBlock, 0, st>>>(

@@ -506,6 +506,34 @@ def test_adaround_backward_dense_waves_equal_compacted(beta, want_loss, n, C):
     assert torch.isfinite(outs[1]).all()
 
 
+@pytest.mark.parametrize("reg", [0.0, 0.01])
+def test_adaround_backward_grid_forms_equal(reg):
+    """Above 8192 workgroups' worth of quads the backward without the loss value runs one tile per
+    workgroup, with it a grid-stride loop over 8192 workgroups (adaround.hip: adaround_backward).
+    Both forms must give the same gradient bits; 12.6 M elements (1.5 x the bounded grid's tile)."""
+    from aimet_amd import _native
+    g = torch.Generator(device=DEV).manual_seed(9)
+    n, C = 3 << 22, 96
+    K = n // C
+    w = torch.randn(n, device=DEV, generator=g) * 0.05
+    grad = torch.randn(n, device=DEV, generator=g)
+    alpha = torch.randn(n, device=DEV, generator=g) * 2
+    delta = (w.view(C, K).abs().amax(1) / 127).contiguous()
+    offset = torch.full((C,), -128.0, device=DEV)
+    stream = torch.cuda.current_stream().cuda_stream
+    outs = []
+    for want_loss in (False, True):
+        out = torch.full_like(w, float("nan"))
+        loss = torch.zeros(1, device=DEV)
+        _native.call("aimet_adaround_backward", w.data_ptr(), alpha.data_ptr(), grad.data_ptr(), out.data_ptr(), 1,
+                     C, K, delta.data_ptr(), offset.data_ptr(), 8, ctypes.c_double(reg), ctypes.c_double(8.0),
+                     loss.data_ptr() if want_loss else None, stream)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    assert torch.isfinite(outs[0]).all()
+
+
 def test_adaround_hard_rounding_floor_exact_at_multiples():
     """floor(W / delta) in the AdaRound kernels (reciprocal fast path, adaround.hip: floor_div) equals
     torch's IEEE floor(W / delta) bit for bit, on weights at exact multiples of delta and 1-2 ulp

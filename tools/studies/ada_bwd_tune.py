@@ -4,7 +4,7 @@ with the round-loss value requested (want_loss) or not (the optimisation loop's 
 JSON line per case; `checksum` (sum of the gradient's bit patterns) lets runs of different kernel
 forms be compared bit for bit (--tag names the form in the output).
 
-    python tools/studies/ada_bwd_tune.py [--elems N] [--reps R] [--tag NAME] [--lib PATH]
+    python tools/studies/ada_bwd_tune.py [--elems N] [--reps R] [--tag NAME] [--lib PATH] [--reg R] [--skew BYTES]
 """
 import argparse
 import ctypes
@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--tag", default="")
     ap.add_argument("--reg", type=float, default=0.01, help="reg_param (0: no rounding loss, no pow)")
     ap.add_argument("--lib", default=None, help="another build of libaimet_amd.so")
+    ap.add_argument("--skew", type=int, default=0, help="start buffer k (w, grad, out, alpha) k x SKEW bytes into its allocation")
     args = ap.parse_args()
     if args.lib:
         aimet_amd._native.LIB_PATH = os.path.abspath(args.lib)
@@ -36,16 +37,22 @@ def main():
     N, C = args.elems, args.channels
     K = N // C
     g = torch.Generator(device=dev).manual_seed(0)
-    w = torch.randn(N, device=dev, generator=g) * 0.05
-    grad = torch.randn(N, device=dev, generator=g)
-    out = torch.empty_like(w)
+    assert args.skew % 16 == 0
+
+    def buf(k):   # N floats starting k x skew bytes into a fresh allocation
+        off = k * args.skew // 4
+        return torch.empty(N + off, device=dev)[off:]
+
+    w = buf(0).copy_(torch.randn(N, device=dev, generator=g) * 0.05)
+    grad = buf(1).copy_(torch.randn(N, device=dev, generator=g))
+    out = buf(2)
     delta = (w.view(C, K).abs().amax(1) / 127).contiguous()
     offset = torch.full((C,), -128.0, device=dev)
     rloss = torch.zeros(1, device=dev)
     P = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
     s = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
     for scale in [float(v) for v in args.scales.split(",")]:
-        alpha = torch.randn(N, device=dev, generator=torch.Generator(device=dev).manual_seed(1)) * scale
+        alpha = buf(3).copy_(torch.randn(N, device=dev, generator=torch.Generator(device=dev).manual_seed(1)) * scale)
         sat = float((alpha.abs() > math.log(11.0)).float().mean())
         for want_loss in (True, False):
             def call():
@@ -65,7 +72,7 @@ def main():
             torch.cuda.synchronize()
             ms = ev[0].elapsed_time(ev[1]) / args.reps
             gbps = 16 * N / ms / 1e6
-            print(json.dumps({"kernel": "adaround_bwd_vec_kernel", "tag": args.tag, "reg": args.reg, "elems": N, "alpha_scale": scale,
+            print(json.dumps({"kernel": "adaround_bwd_vec_kernel", "tag": args.tag, "reg": args.reg, "skew": args.skew, "elems": N, "alpha_scale": scale,
                               "saturated_frac": round(sat, 4), "want_loss": want_loss, "avg_ms": round(ms, 4),
                               "achieved_GBps": round(gbps, 1), "frac_of_peak": round(gbps / 8000, 4),
                               "checksum": int(out.view(torch.int32).to(torch.int64).sum().item()),
