@@ -532,6 +532,10 @@ def test_adaround_backward_grid_forms_equal(reg):
     torch.cuda.synchronize()
     assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
     assert torch.isfinite(outs[0]).all()
+    if reg == 0.0:   # no loss term at reg 0 (the launch takes the no-loss form): the value is untouched
+        assert loss.item() == 0.0
+    else:
+        assert loss.item() > 0.0
 
 
 def test_adaround_hard_rounding_floor_exact_at_multiples():
