@@ -507,13 +507,13 @@ def test_adaround_backward_dense_waves_equal_compacted(beta, want_loss, n, C):
 
 
 @pytest.mark.parametrize("reg", [0.0, 0.01])
-def test_adaround_backward_grid_forms_equal(reg):
+@pytest.mark.parametrize("n, C", [(3 << 22, 96), ((3 << 22) + 16, 1)])   # n % 32 == 16: the scalar pow tail
+def test_adaround_backward_grid_forms_equal(reg, n, C):
     """Above 8192 workgroups' worth of quads the backward without the loss value runs one tile per
     workgroup, with it a grid-stride loop over 8192 workgroups (adaround.hip: adaround_backward).
     Both forms must give the same gradient bits; 12.6 M elements (1.5 x the bounded grid's tile)."""
     from aimet_amd import _native
     g = torch.Generator(device=DEV).manual_seed(9)
-    n, C = 3 << 22, 96
     K = n // C
     w = torch.randn(n, device=DEV, generator=g) * 0.05
     grad = torch.randn(n, device=DEV, generator=g)
