@@ -20,7 +20,7 @@ from aimet_amd.encodings_io import (compute_partial_encoding, create_encoding_fr
                                     validate_is_symmetric_flag)
 from aimet_amd.learned_grid import (LearnedGridTensorQuantizer, initialize_learned_grid_quantizer_attributes,
                                     set_encoding_min_max_gating_threshold_many)
-from aimet_amd.libpymo import RoundingMode
+from aimet_amd.libpymo import RoundingMode, TfEncoding
 from aimet_amd.quantizers import (MAP_ROUND_MODE_TO_PYMO, QuantizationDataType, QuantScheme,
                                   StaticGridPerChannelQuantizer, StaticGridPerTensorQuantizer, compute_dloss_by_dx)
 
@@ -46,22 +46,67 @@ TF_ENHANCED_STRIDE_FACTOR = 2
 _REPLICA_LOCK = threading.Lock()
 
 
+def _tensor_version(t):
+    """t's autograd version counter (bumped by every in-place op on t or on any view of its
+    storage), or None for an inference-mode tensor, which keeps none."""
+    try:
+        return t._version
+    except RuntimeError:
+        return None
+
+
+def _default_stats_limit():
+    """Elements a StatsBatch may hold: a quarter of the free device memory in float32, between
+    2^24 and 2^30 (peak memory of the calibration stays bounded on a large model)."""
+    try:
+        free, _ = torch.cuda.mem_get_info()
+    except Exception:   # noqa: BLE001 -- no device (CPU tests)
+        return 1 << 30
+    return max(1 << 24, min(1 << 30, free // 16))
+
+
 class StatsBatch:
     """The activation statistics of QuantizationSimModel.compute_encodings' ANALYSIS forwards,
-    batched: a wrapper hands (quantizer, a copy of the tensor) here instead of launching the
-    quantizer's update (aimet_tq_update_stats: ~4 launches and ~25 us of host time each; the copy
-    is one), and flush() updates every pending quantizer with one AimetTensorQuantizer.updateStatsMany
-    call per device (one launch per phase). Each quantizer still sees its tensors in the order the forward produced them: a second
-    tensor for a pending quantizer flushes first. The tensors stay alive until flushed, so at most
-    `limit` elements are held (then flushed); compute_encodings flushes after every forward of the
-    model and at the end. Shared by DataParallel replicas (their wrappers' __dict__ is a shallow copy)."""
+    batched: a wrapper hands (quantizer, tensor) here instead of launching the quantizer's update
+    (aimet_tq_update_stats: ~4 launches and ~25 us of host time each), and flush() updates every
+    pending quantizer with one AimetTensorQuantizer.updateStatsMany call per device (one launch per
+    phase). Each quantizer still sees its tensors in the order the forward produced them: a second
+    tensor for a pending quantizer flushes first. compute_encodings flushes when every forward of
+    the model returns (end_forward) and at the end. Shared by DataParallel replicas (their wrappers'
+    __dict__ is a shallow copy).
 
-    def __init__(self, limit: int = 1 << 30):
-        self.limit = limit
+    In-place writes. The statistics must see the values the quantizer was given -- what the
+    per-call update, launched at once on the stream, reads -- but the network may overwrite a
+    queued tensor before the flush (nn.ReLU(inplace=True) after a folded conv, `out += identity`).
+    The first forward (`learning`) therefore queues copies, and watches the originals' version
+    counters: a quantizer whose tensor some op wrote in place before the flush is copied in every
+    later forward; the others are queued as they are (no copy: one read of each tensor instead of
+    three), and their version counters are checked at the flush. A tensor overwritten in a later
+    forward but not in the first (control flow that changes between batches) raises instead of
+    giving statistics of the overwritten values.
+
+    Sharded (`group` spans several ranks): every rank passes its shard of the
+    calibration batch; each flush runs the per-batch exchange of aimet_amd.distributed over the
+    flushed quantizers (one all_reduce(MAX) of the packed {-min, max}, one all_reduce(SUM) of the
+    packed bin and element counts), so every rank ends with the statistics of one device fed the
+    whole batch. Flush points are then rank-invariant: the end of every model forward and a
+    quantizer's second tensor within one forward, never an element budget (ranks holding unequal
+    shards would reach it at different points); per-channel and 16-bit activations are batched too,
+    so no data-dependent statistics bypass the exchange. Held memory is then one forward's queued
+    activations (plus their copies in the first)."""
+
+    def __init__(self, limit: Optional[int] = None, group=None, sharded: bool = False):
+        self.limit = _default_stats_limit() if limit is None else int(limit)
+        self.group = group
+        self.sharded = bool(sharded)
         self.lock = threading.Lock()
-        self.items = []
+        self.items = []          # (quantizer, tensor queued, channel axis, watch)
         self.pending = set()
         self.elems = 0
+        self.learning = True     # the first forward: copy everything, learn who is written in place
+        self.copy_ids = set()    # quantizers whose tensor the network overwrote before a flush
+        self.exchange = None     # the packed exchange buffers of the last sharded flush
+        self.copied = 0          # elements copied (reported by the tests)
 
     @staticmethod
     def eligible(q, t) -> bool:
@@ -72,35 +117,107 @@ class StatsBatch:
                 q.encoding_min_max_fixed_vals is None and isinstance(t, torch.Tensor) and t.is_cuda and
                 t.dtype == torch.float32 and type(q._op()) is AimetTensorQuantizer)
 
+    @staticmethod
+    def eligible_sharded(q, t) -> bool:
+        """Every quantizer whose statistics depend on this rank's data: per-tensor or per-channel,
+        any floating dtype (upcast to float32, as update_encoding_stats does). The operator is
+        duck-typed (the phased statistics interface of aimet_amd.distributed)."""
+        from aimet_amd.quantizers import StaticGridPerChannelQuantizer, StaticGridPerTensorQuantizer
+        if not (type(q) in (StaticGridPerTensorQuantizer, StaticGridPerChannelQuantizer) and q.enabled and
+                not q._is_encoding_frozen and q.bitwidth != 32 and q.data_type == QuantizationDataType.int and
+                q.encoding_min_max_fixed_vals is None and isinstance(t, torch.Tensor) and t.is_floating_point()):
+            return False
+        op = q._op()
+        if not hasattr(op, "bind_exchange"):
+            return False
+        from aimet_amd.tensor_quantizer import AimetTensorQuantizer
+        if isinstance(op, AimetTensorQuantizer) and not t.is_cuda:
+            raise NotImplementedError("sharded calibration exchanges device statistics: the activations of a "
+                                      "QuantizationSimModel calibrated over several ranks must be on the GPU")
+        return True
+
+    def accepts(self, q, t) -> bool:
+        return self.eligible_sharded(q, t) if self.sharded else self.eligible(q, t)
+
     def add(self, q, t, owned: bool = False):
-        """Queue q's update with t. Unless the caller owns t (a copy nobody else sees), t is copied
-        first: the network may overwrite it in place before the flush (nn.ReLU(inplace=True),
-        `out += identity`), and the statistics must see the values the quantizer was given -- what
-        the per-call update, launched at once on the stream, reads."""
-        if not owned or not t.is_contiguous():
-            t = t.clone(memory_format=torch.contiguous_format)
+        """Queue q's update with t (`owned`: a copy nobody else sees, e.g. the downsampled one)."""
+        from aimet_amd.quantizers import StaticGridPerChannelQuantizer
+        ch_axis = q.channel_axis if isinstance(q, StaticGridPerChannelQuantizer) else None
+        if t.dtype != torch.float32:
+            t, owned = t.to(torch.float32), True
+        watch = None
+        if not owned:
+            ver = _tensor_version(t)
+            if ver is None or self.learning or id(q) in self.copy_ids:
+                if ver is not None and self.learning:
+                    watch = (t, ver, True)
+                t = t.clone(memory_format=torch.contiguous_format)
+                self.copied += t.numel()
+            else:
+                watch = (t, ver, False)
+        if not t.is_contiguous():
+            t = t.contiguous()   # a copy of the values as they are now: nothing to watch
+            watch = None
         with self.lock:
-            if id(q) in self.pending or self.elems + t.numel() > self.limit:
+            held = t.numel() * (2 if watch is not None and watch[2] else 1)
+            if id(q) in self.pending or (not self.sharded and self.elems + held > self.limit):
                 self._flush_locked()
-            self.items.append((q, t))
+            self.items.append((q, t, ch_axis, watch))
             self.pending.add(id(q))
-            self.elems += t.numel()
+            self.elems += held
 
     def flush(self):
         with self.lock:
             self._flush_locked()
 
+    def end_forward(self):
+        """The model's forward returned: flush, and stop copying what the first forward showed
+        is not written in place."""
+        with self.lock:
+            self._flush_locked()
+            self.learning = False
+
     def _flush_locked(self):
         from aimet_amd.tensor_quantizer import AimetTensorQuantizer
         items, self.items, self.pending, self.elems = self.items, [], set(), 0
+        overwritten = []
+        for q, _, _, watch in items:
+            if watch is None:
+                continue
+            src, ver, learning = watch
+            if _tensor_version(src) != ver:
+                if learning:
+                    self.copy_ids.add(id(q))   # the copy was right; copy it from now on
+                else:
+                    overwritten.append(q)
+        if overwritten:
+            raise RuntimeError("compute_encodings: %d activation tensor(s) were written in place before their "
+                               "statistics were taken, in a calibration forward after the first (whose in-place "
+                               "writes decide which tensors are copied); the model's in-place behaviour must be "
+                               "the same in every calibration forward" % len(overwritten))
+        if not items:
+            return
+        if self.sharded:
+            from aimet_amd import distributed as D
+            self.exchange = D.sharded_update_stats([q._op() for q, _, _, _ in items], [t for _, t, _, _ in items],
+                                                   [ax or 0 for _, _, ax, _ in items], group=self.group,
+                                                   exchange=self.exchange)
+            return
         by_dev = {}
-        for q, t in items:
+        for q, t, _, _ in items:
             by_dev.setdefault(t.device, []).append((q, t))
         for dev, group in by_dev.items():
             with torch.cuda.device(dev):
                 AimetTensorQuantizer.updateStatsMany([q._op() for q, _ in group], [t for _, t in group])
 
-_IGNORED_DTYPES = (torch.int8, torch.uint8, torch.int16, torch.int32, torch.int64, torch.bool)
+def _data_dependent(q) -> bool:
+    """update_encoding_stats(t) of q reads t (not a fixed range, not a disabled / frozen / 32-bit
+    quantizer, which ignore it)."""
+    return (q.enabled and not q._is_encoding_frozen and q.bitwidth != 32 and
+            getattr(q, "encoding_min_max_fixed_vals", None) is None)
+
+
+_IGNORED_DTYPES = (torch.int8,torch.uint8, torch.int16, torch.int32, torch.int64, torch.bool)
 # wrapped modules that never modify their inputs in place
 _INPUT_PRESERVING_TYPES = (nn.Conv1d, nn.Conv2d, nn.Conv3d, nn.ConvTranspose1d, nn.ConvTranspose2d,
                            nn.ConvTranspose3d, nn.Linear)
@@ -400,6 +517,10 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
         broadcast copy the same way, on its own device, under _REPLICA_LOCK."""
         shadow_params = {}
         replica = getattr(self, "_is_replica", False)
+        # QuantizationSimModel.compute_encodings: the QDQ'd parameters of one ANALYSIS forward are
+        # reused by the next while the parameter, its encoding and the rounding are unchanged (the
+        # same values: the reference recomputes them in every forward)
+        cache = None if replica else self.__dict__.get("_param_qdq_cache")
         for name, param in self.get_named_parameters():
             q = self.param_quantizers[name]
             if not (q.enabled and q.bitwidth != 32):
@@ -411,11 +532,22 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
                     if q.quant_scheme == QuantScheme.post_training_percentile:
                         q.set_percentile_value(100)
                     q.compute_encoding()
+                    if cache is not None:
+                        cache.pop(name, None)
                     if not q.enabled:
                         continue
                 round_mode = q.round_mode if self.training else RoundingMode.ROUND_NEAREST
                 shadow_params[name] = param.data
-                param.data = q.quantize_dequantize(param.data, round_mode)
+                if cache is None:
+                    param.data = q.quantize_dequantize(param.data, round_mode)
+                    continue
+                # TfEncoding._version moves whenever any encoding is created or assigned
+                key = (param.data_ptr(), param._version, tuple(param.shape), param.dtype, id(q._encoding),
+                       TfEncoding._version, int(round_mode))
+                hit = cache.get(name)
+                if hit is None or hit[0] != key:
+                    hit = cache[name] = (key, q.quantize_dequantize(param.data, round_mode))
+                param.data = hit[1]
         return shadow_params
 
     def compute_weight_encodings(self):
@@ -451,8 +583,11 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
                 else:
                     x = t
                 batch = self.__dict__.get("_stats_batch")   # QuantizationSimModel.compute_encodings
-                if batch is not None and StatsBatch.eligible(q, x):
+                if batch is not None and batch.accepts(q, x):
                     batch.add(q, x, owned=x is not t and x._base is None)
+                elif batch is not None and batch.sharded and _data_dependent(q):
+                    raise NotImplementedError("sharded calibration cannot exchange the statistics of %r (tensor "
+                                              "%s)" % (type(q).__name__, getattr(x, "dtype", type(x))))
                 else:
                     q.update_encoding_stats(x)
                 return t

@@ -84,6 +84,28 @@ def _load_config(config_file) -> Dict:
     return cfg
 
 
+def _count_inputs(model, dummy_input, types):
+    """The positional input count of every module of `types` in a forward on `dummy_input`: the
+    wrapper's input quantizer count, from one forward with hooks as the reference does
+    (v1/quantsim.py:282-283, 2202-2215; aimet_torch/utils.py:768 get_inout_tensor_shape_per_module).
+    Modules the forward does not reach keep one (v1/quantsim.py:1409-1410)."""
+    counts = {}
+
+    def pre(m, args):
+        counts[id(m)] = max(counts.get(id(m), 1), len(args))
+    hooks = [m.register_forward_pre_hook(pre) for m in model.modules() if isinstance(m, types)]
+    try:
+        with _eval_mode(model), torch.no_grad():
+            if isinstance(dummy_input, (list, tuple)):
+                model(*dummy_input)
+            else:
+                model(dummy_input)
+    finally:
+        for h in hooks:
+            h.remove()
+    return counts
+
+
 @contextlib.contextmanager
 def _eval_mode(model):
     was = model.training
@@ -115,6 +137,8 @@ class QuantizationSimModel:
         self._percentile_value = 100
         self._cfg = _load_config(config_file)
         self._excluded_layer_names = []
+        self._last_calibration = None
+        n_inputs = _count_inputs(self.model, dummy_input, quantizable_types) if dummy_input is not None else {}
         first = True
         for parent_name, parent in list(self.model.named_modules()):
             for child_name, child in list(parent.named_children()):
@@ -122,7 +146,8 @@ class QuantizationSimModel:
                     w = StaticGridQuantWrapper(child, default_param_bw, default_output_bw, rounding_mode,
                                                get_v1_quant_scheme_for_initialization(quant_scheme),
                                                is_output_quantized=True,
-                                               is_symmetric=self._cfg["act_symmetric"])
+                                               is_symmetric=self._cfg["act_symmetric"],
+                                               num_inputs=n_inputs.get(id(child), 1))
                     for pname, pq in w.param_quantizers.items():
                         pq.use_symmetric_encodings = self._cfg["param_symmetric"]
                         if pname == "bias":
@@ -167,7 +192,8 @@ class QuantizationSimModel:
 
     # -- calibration ------------------------------------------------------------------------------
     def compute_encodings(self, forward_pass_callback: Callable[[nn.Module, Any], Any],
-                          forward_pass_callback_args: Any = None):
+                          forward_pass_callback_args: Any = None, *, process_group=None,
+                          sharded: Optional[bool] = None):
         """v1/quantsim.py:381-449: reset, ANALYSIS forward(s), encodings, ACTIVE; range-learning
         schemes then swap in the trainable wrappers (v1/quantsim.py:423, 833-846).
 
@@ -175,9 +201,27 @@ class QuantizationSimModel:
         first ANALYSIS forward would compute wrapper by wrapper (a statistics launch, a device search
         and a synchronisation per parameter, v1/qc_quantize_op.py:753-798) are computed for every
         wrapper at once beforehand (_precompute_param_encodings: the same encodings, since the
-        parameters do not change during the forwards), and the activation statistics of each
-        forward are launched together when the model's forward returns (StatsBatch: the same
-        statistics, every quantizer updated in its own order)."""
+        parameters do not change during the forwards), the QDQ'd parameters of one forward are
+        reused by the next, and the activation statistics of each forward are launched together
+        when the model's forward returns (StatsBatch: the same statistics, every quantizer updated
+        in its own order).
+
+        Sharded calibration (the reference calibrates on one device only,
+        Docs/api_docs/torch_multi_gpu.rst): when torch.distributed is initialised with more than
+        one rank in `process_group` (default: the world), every rank runs the callback on ITS
+        shard of the calibration data, and each forward's activation statistics are exchanged --
+        one all_reduce(MAX) of the packed batch min/max and one all_reduce(SUM) of the packed
+        histogram and element counts per forward, over RCCL -- so that every rank ends with the
+        encodings of one device fed every rank's samples. Every rank must then call
+        compute_encodings and run the same number of model forwards. `sharded=False` keeps the
+        reference's behaviour (each rank calibrates on its own data alone), e.g. to calibrate on
+        one rank only; `sharded=True` insists on a process group."""
+        from aimet_amd import distributed as D
+        world = D._world(process_group)
+        if sharded is None:
+            sharded = world > 1
+        elif sharded and not (torch.distributed.is_available() and torch.distributed.is_initialized()):
+            raise RuntimeError("sharded calibration needs an initialised torch.distributed process group")
         wrappers = [w for _, w in self.quant_wrappers()]
         _reset_many(wrappers)
         for w in wrappers:
@@ -186,11 +230,12 @@ class QuantizationSimModel:
                 w.set_percentile_value(self._percentile_value)
         with _eval_mode(self.model), torch.no_grad():
             pre = _precompute_param_encodings(wrappers)
-            batch = StatsBatch()
+            batch = StatsBatch(group=process_group, sharded=bool(sharded))
             static = [w for w in wrappers if isinstance(w, StaticGridQuantWrapper)]
             for w in static:
                 w.__dict__["_stats_batch"] = batch
-            hook = self.model.register_forward_hook(lambda *_: batch.flush())
+                w.__dict__["_param_qdq_cache"] = {}
+            hook = self.model.register_forward_hook(lambda *_: batch.end_forward())
             try:
                 forward_pass_callback(self.model, forward_pass_callback_args)
                 batch.flush()
@@ -198,7 +243,11 @@ class QuantizationSimModel:
                 hook.remove()
                 for w in static:
                     w.__dict__.pop("_stats_batch", None)
+                    w.__dict__.pop("_param_qdq_cache", None)
                 _forget_unused_param_encodings(pre)
+                # what the calibration copied / exchanged (reported by the tests and bench.py)
+                self._last_calibration = {"sharded": batch.sharded, "world": world, "copied_elements": batch.copied,
+                                          "copied_quantizers": len(batch.copy_ids)}
         # every activation / param quantizer of the model in one batched native call per setting
         # range-learning wrappers keep their trained ranges (they have no statistics)
         quantizers = [q for _, w in self.quant_wrappers() if not isinstance(w, LearnedGridQuantWrapper)

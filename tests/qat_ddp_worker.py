@@ -2,10 +2,15 @@
 Llama (workloads/llama.py, vocab 1024) through QuantizationSimModel, under DistributedDataParallel
 when WORLD_SIZE > 1 (gloo; every rank on cuda:0), else one process on the union batch.
 
-Every rank calibrates on the same batch (identical encodings), then runs ONE step on its share
-of the union batch (rank r: sequence r of UNION sequences), loss = mean token cross-entropy,
-backward (DDP all-reduces and averages the gradients). One process runs the union batch as UNION
-micro-batches with gradient accumulation (the ranks' GEMM shapes). Saves, per parameter: the full gradient of
+Every rank calibrates on ITS shard of the calibration batch (rank r: sequence r of UNION
+sequences): QuantizationSimModel.compute_encodings shards by itself (the ranks form a process
+group), exchanging each forward's activation statistics. The one process calibrates on the union
+batch as ONE statistics batch whose tensors come from one forward per sequence (the ranks' GEMM
+shapes, so every activation is the ranks' bit for bit): each quantizer's two tensors are
+concatenated and updated once, as one device fed the whole batch. Then every rank runs ONE step on
+its share (rank r: sequence r), loss = mean token cross-entropy, backward (DDP all-reduces and
+averages the gradients). One process runs the union batch as UNION micro-batches with gradient
+accumulation (the ranks' GEMM shapes). Saves, per parameter: the full gradient of
 every *_encoding_min / *_encoding_max, and a fixed sample of 4096 elements + the norm of every
 other gradient."""
 import json
@@ -58,7 +63,29 @@ def main():
                 return m(ids)
         return m(ids)
 
-    sim.compute_encodings(lambda m, ids: fwd(m, ids), ids_all[:, :-1])
+    if world > 1:
+        sim.compute_encodings(lambda m, ids: fwd(m, ids), ids_all[rank:rank + 1, :-1])
+        assert sim._last_calibration["sharded"], sim._last_calibration
+    else:
+        import aimet_amd.qc_quantize_op as QO
+        stash = {}
+        orig_add, orig_flush, orig_accepts = QO.StatsBatch.add, QO.StatsBatch.flush, QO.StatsBatch.accepts
+        orig_end = QO.StatsBatch.end_forward
+
+        def add(self, q, t, owned=False):   # every forward's tensors held until the end
+            stash.setdefault(id(q), (q, []))[1].append(t.detach().float().clone())
+
+        def flush(self):                    # then one update per quantizer of the concatenation
+            for q, ts in stash.values():
+                orig_add(self, q, torch.cat([t.reshape(-1) for t in ts]), True)
+            stash.clear()
+            orig_flush(self)
+        QO.StatsBatch.add, QO.StatsBatch.flush, QO.StatsBatch.end_forward = add, flush, lambda self: None
+        # the 16-bit (autocast) activations too, as the sharded batch takes them
+        QO.StatsBatch.accepts = lambda self, q, t: self.eligible_sharded(q, t)
+        sim.compute_encodings(lambda m, ids: [fwd(m, ids[i:i + 1]) for i in range(UNION)], ids_all[:, :-1])
+        QO.StatsBatch.add, QO.StatsBatch.flush, QO.StatsBatch.accepts = orig_add, orig_flush, orig_accepts
+        QO.StatsBatch.end_forward = orig_end
     assert sum(isinstance(w, LearnedGridQuantWrapper) for w in sim.model.modules()) >= 2 * 7 + 1
     net = sim.model
     net.train()

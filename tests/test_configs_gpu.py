@@ -9,9 +9,10 @@ exact tensors each quantizer saw.
   stream) on the config-1 network: one 32-image batch, TF-Enhanced and TF, every activation
   encoding and every one of the 27,560 weight-channel encodings;
 * config 4: ViT-L/16 TF-Enhanced calibration of every activation QuantSim quantizes (318
-  quantizers, ~122.6 M elements per image), one 8-image batch sharded over 2 ranks (gloo, both on
-  cuda:0) through aimet_amd.distributed.sharded_update_stats; both ranks' encodings == the oracle
-  fed the whole batch (tests/vit_dist_worker.py).
+  quantizers, ~122.6 M elements per image), one 32-image batch sharded over 2 ranks (gloo, both on
+  cuda:0) through aimet_amd.distributed.sharded_update_stats, the calibration plan, and the
+  drop-in QuantizationSimModel.compute_encodings; both ranks' encodings == the oracle fed the whole
+  batch (tests/vit_dist_worker.py).
 
 The oracle work runs in a thread pool (ctypes releases the GIL); tensors stream to it one batch at
 a time so host memory stays at one batch of activations."""
@@ -201,10 +202,14 @@ def test_config4_vit_sharded_calibration(tmp_path):
             assert p.wait(timeout=300) == 0
         return [json.load(open(out + ".%d" % r)) for r in range(world)]
 
-    oracle, = run(1, str(tmp_path / "oracle"))
-    assert len(oracle["encodings"]) == 318
-    assert oracle["elements"] > 32 * 120e6
-    for mode in ("phased", "plan"):   # sharded_update_stats / the calibration plan's staged launch
+    oracles = {"hooks": run(1, str(tmp_path / "oracle"))[0], "sim": run(1, str(tmp_path / "oracle_sim"), "sim")[0]}
+    for oracle in oracles.values():
+        assert len(oracle["encodings"]) == 318
+        assert oracle["elements"] > 32 * 120e6
+    # sharded_update_stats / the calibration plan's staged launch (on the model's own activations)
+    # / the drop-in QuantizationSimModel sharding by itself (its ANALYSIS forwards: weights QDQ'd)
+    for mode in ("phased", "plan", "sim"):
+        oracle = oracles["sim" if mode == "sim" else "hooks"]
         for r, res in enumerate(run(2, str(tmp_path / mode), mode)):
             assert res["elements"] == oracle["elements"]
             bad = [i for i, (a, b) in enumerate(zip(res["encodings"], oracle["encodings"])) if a != b]
