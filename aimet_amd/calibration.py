@@ -197,27 +197,43 @@ class CalibrationPlan:
 
 # the plan of the last compute_encodings_resident call, reused while the same quantizers see the
 # same tensors. The cache holds the plan's own tables only: the tensors and quantizers are checked
-# by identity through weak references (and the tensors' addresses), so nothing is kept alive.
+# by identity through weak references (and the tensors' addresses, shapes and strides, which the
+# plan's tables hold), so nothing is kept alive. A plan is built only when a call sees the tensors
+# of the previous call again: a calibration loop passing new activation tensors every batch takes
+# the per-call native path instead of building (and dropping) a plan per call.
 _PLAN_CACHE = {}
 
 
-def _cached_plan(aq, acts, pq, params, ch_axes, act_settings, param_settings, group):
-    """The cached plan for exactly these quantizers and tensors, or a new one (which replaces it)."""
+def _identity(aq, acts, pq, params, ch_axes, act_settings, param_settings, group):
     ts, qs = list(acts) + list(params), list(aq) + list(pq)
     key = (tuple(map(id, qs)), len(aq), tuple(act_settings), tuple(param_settings),
-           tuple(ch_axes) if ch_axes is not None else None, id(group) if group is not None else None)
+           tuple(ch_axes) if ch_axes is not None else None, id(group) if group is not None else None,
+           tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride())) for t in ts))
+    return key, ts, qs
+
+
+def _same(entry, key, ts, qs):
+    return (entry is not None and entry[0] == key and len(ts) == len(entry[1])
+            and all(r() is t for r, t in zip(entry[1], ts)) and all(r() is q for r, q in zip(entry[2], qs)))
+
+
+def _cached_plan(aq, acts, pq, params, ch_axes, act_settings, param_settings, group):
+    """The cached plan for exactly these quantizers and tensors; a new one (which replaces it) when
+    the previous call passed the same ones; else None (the caller takes the per-call path)."""
+    key, ts, qs = _identity(aq, acts, pq, params, ch_axes, act_settings, param_settings, group)
     hit = _PLAN_CACHE.get("plan")
-    if hit is not None and hit[0] == key:
-        plan, trefs, ptrs, qrefs = hit[1:]
-        if (len(ts) == len(trefs) and all(r() is t for r, t in zip(trefs, ts))
-                and all(r() is q for r, q in zip(qrefs, qs)) and [t.data_ptr() for t in ts] == ptrs
-                and [q._handle.value if q._handle is not None else None for q in qs] == plan._native_handles):
+    if _same(hit, key, ts, qs):
+        plan = hit[3]
+        if [q._handle.value if q._handle is not None else None for q in qs] == plan._native_handles:
             return plan
+    seen = _PLAN_CACHE.get("seen")
+    _PLAN_CACHE["seen"] = (key, [weakref.ref(t) for t in ts], [weakref.ref(q) for q in qs])
+    if not _same(seen, key, ts, qs):
+        return None
     _PLAN_CACHE.pop("plan", None)
     plan = CalibrationPlan(aq, acts, pq, params, ch_axes, act_settings, param_settings, group=group)
     plan._tensors = plan.act_quantizers = plan.param_quantizers = None   # see above
-    _PLAN_CACHE["plan"] = (key, plan, [weakref.ref(t) for t in ts], [t.data_ptr() for t in ts],
-                           [weakref.ref(q) for q in qs])
+    _PLAN_CACHE["plan"] = (key, [weakref.ref(t) for t in ts], [weakref.ref(q) for q in qs], plan)
     return plan
 
 
@@ -242,12 +258,13 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
     reset=True: resetEncodingStats of every quantizer first (QuantizationSimModel.compute_encodings
     on quantizers that already hold statistics, v1/quantsim.py:387-399).
 
-    With AimetTensorQuantizers (per-tensor activations) and contiguous float32 device tensors, all
-    of it is a calibration plan (CalibrationPlan, aimet_calib_plan_*: every job table prepared once
-    and cached for the next call on the same quantizers and tensors): one native launch of about
-    fifteen HIP calls on one rank; on several ranks its three stages with the packed all_reduce(MAX)
-    and all_reduce(SUM) between them. Otherwise the phases are enqueued from here (sharded with the
-    same collectives when `group` spans several ranks)."""
+    With AimetTensorQuantizers (per-tensor activations) and contiguous float32 device tensors, a
+    call that sees the quantizers and tensors of the previous call again runs a calibration plan
+    (CalibrationPlan, aimet_calib_plan_*: every job table prepared once and cached for the next call
+    on the same quantizers and tensors): one native launch of about fifteen HIP calls on one rank;
+    on several ranks its three stages with the packed all_reduce(MAX) and all_reduce(SUM) between
+    them. Other calls take the per-call native path (one rank: aimet_calibrate_launch) or enqueue
+    the phases from here (sharded with the same collectives when `group` spans several ranks)."""
     if not activations and not params:
         if reset:
             AimetTensorQuantizer.resetEncodingStatsMany(list(act_quantizers) + list(param_quantizers))
@@ -258,12 +275,14 @@ def compute_encodings_resident(act_quantizers: Sequence[AimetTensorQuantizer], a
                and all(type(q) is AimetTensorQuantizer for q in param_quantizers)
                and all(isinstance(t, torch.Tensor) and t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()
                        and t.device == dev for t in list(activations) + list(params)))
+    plan = None
     if planned:
         # a calibration plan (every job table prepared once, cached for the next call on the same
         # quantizers and tensors): one native call on one device; the three stages with the two
         # packed collectives between them when `group` spans several ranks
         plan = _cached_plan(act_quantizers, activations, param_quantizers, params, param_ch_axes, act_settings,
                             param_settings, group)
+    if plan is not None:
         a_pending, p_pending = plan._launch(reset, list(act_quantizers), list(param_quantizers))
         p_res = p_pending.result()
         return a_pending.result(), p_res

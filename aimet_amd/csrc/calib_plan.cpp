@@ -20,6 +20,7 @@
 // stages = 7 is the single-device form (the fold fused into the min/max combine).
 #include <algorithm>
 #include <cstring>
+#include <mutex>
 #include <vector>
 
 #include "tq_internal.hpp"
@@ -58,6 +59,7 @@ struct aimet_calib_plan
     size_t pinned_act_bytes = 0, pinned_par_bytes = 0;
     int busy_act = 0, busy_par = 0;   // requests in flight (their pinned block is being written)
     void* dev_block = nullptr;        // every device table above
+    hipEvent_t done = nullptr;        // recorded on the main stream after every launch
 };
 
 namespace
@@ -104,24 +106,84 @@ std::vector<TfeJob> tfe_jobs(const std::vector<aimet_tensor_quantizer*>& qs, int
     return jobs;
 }
 
+// Memory of destroyed plans, freed once the event recorded after their last launch has completed:
+// destroying a plan (possibly from a garbage collection while another stream is being captured
+// into a HIP graph) neither synchronises the device nor frees memory kernels may still read. The
+// blocks are reaped when a plan is created (outside any capture).
+struct DeadPlan
+{
+    int device;
+    void* dev_block;
+    void* pinned_act;
+    void* pinned_par;
+    hipEvent_t done;
+};
+struct Graveyard
+{
+    std::mutex m;
+    std::vector<DeadPlan> items;
+};
+Graveyard& graveyard()
+{
+    static Graveyard* g = new Graveyard();   // never destroyed: reaped while the process runs
+    return *g;
+}
+
+void reap_dead_plans()
+{
+    std::vector<DeadPlan> ready;
+    {
+        Graveyard& g = graveyard();
+        std::lock_guard<std::mutex> lock(g.m);
+        for (size_t i = 0; i < g.items.size();)
+            if (g.items[i].done == nullptr || hipEventQuery(g.items[i].done) == hipSuccess)
+            {
+                ready.push_back(g.items[i]);
+                g.items.erase(g.items.begin() + (std::ptrdiff_t) i);
+            }
+            else
+                ++i;
+    }
+    for (const DeadPlan& d: ready)
+    {
+        DeviceGuard guard(d.device);
+        if (d.dev_block)
+            (void) hipFree(d.dev_block);
+        if (d.pinned_act)
+            (void) hipHostFree(d.pinned_act);
+        if (d.pinned_par)
+            (void) hipHostFree(d.pinned_par);
+        if (d.done)
+            (void) hipEventDestroy(d.done);
+    }
+}
+
 void destroy_plan(aimet_calib_plan* p)
 {
     if (p == nullptr)
         return;
     // a plan is destroyed only with no request in flight (aimet_calib_plan_destroy checks); its
-    // device tables may still be read by launched kernels, so wait for the device
-    if (p->dev_block || p->pinned_act || p->pinned_par)
+    // device tables may still be read by launched kernels: freed once `done` has completed
+    if (p->dev_block || p->pinned_act || p->pinned_par || p->done)
     {
-        DeviceGuard g(p->device);
-        (void) hipDeviceSynchronize();
-        if (p->dev_block)
-            (void) hipFree(p->dev_block);
-        if (p->pinned_act)
-            (void) hipHostFree(p->pinned_act);
-        if (p->pinned_par)
-            (void) hipHostFree(p->pinned_par);
+        Graveyard& g = graveyard();
+        std::lock_guard<std::mutex> lock(g.m);
+        g.items.push_back(DeadPlan {p->device, p->dev_block, p->pinned_act, p->pinned_par, p->done});
     }
     delete p;
+}
+
+// the device's stream for the plan's one table upload: non-blocking, so the upload waits for no
+// work queued on the legacy default stream (torch's current stream)
+hipStream_t upload_stream(int device)
+{
+    static std::mutex m;
+    static std::vector<hipStream_t> streams(64, nullptr);
+    AIMET_REQUIRE(device >= 0 && device < 64, "device id out of range");
+    std::lock_guard<std::mutex> lock(m);
+    if (streams[(size_t) device] == nullptr)
+        AIMET_HIP_CHECK(hipStreamCreateWithFlags(&streams[(size_t) device], hipStreamNonBlocking));
+    return streams[(size_t) device];
 }
 
 // the requests of a launch: the plan's pinned block borrowed, the plan's in-flight count raised
@@ -157,6 +219,7 @@ int aimet_calib_plan_create(aimet_tensor_quantizer* const* act_qs, const float* 
                           (n_par == 0 || (par_qs && par_x && par_outer && par_C && par_K)),
                       "null argument");
         *out = nullptr;
+        reap_dead_plans();
         p    = new aimet_calib_plan;
         std::copy(act_settings, act_settings + 4, p->aset);
         std::copy(par_settings, par_settings + 4, p->pset);
@@ -291,7 +354,10 @@ int aimet_calib_plan_create(aimet_tensor_quantizer* const* act_qs, const float* 
             p->dr_par = reinterpret_cast<ResetJob*>(base + o_rpar);
         }
         // hand-off buffers: partials need no initial value, the tickets start (and end) at zero
-        AIMET_HIP_CHECK(hipMemcpy(p->dev_block, pk.host.data(), pk.host.size(), hipMemcpyHostToDevice));
+        hipStream_t up = upload_stream(p->device);
+        AIMET_HIP_CHECK(hipMemcpyAsync(p->dev_block, pk.host.data(), pk.host.size(), hipMemcpyHostToDevice, up));
+        AIMET_HIP_CHECK(hipStreamSynchronize(up));
+        AIMET_HIP_CHECK(hipEventCreateWithFlags(&p->done, hipEventDisableTiming));
         if (ta)
         {
             p->has_tfe_act = true;
@@ -402,6 +468,8 @@ int aimet_calib_plan_launch(aimet_calib_plan* p, int stages, int reset, void* ma
         }
         if (first && n_par && ss != ms)
             stream_join(ms, ss);   // later work on the main stream sees the parameters' state too
+        if (p->done)
+            AIMET_HIP_CHECK(hipEventRecord(p->done, ms));   // the plan's memory is in use until here
     });
     if (rc != AIMET_OK)
     {

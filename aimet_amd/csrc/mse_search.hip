@@ -23,6 +23,97 @@ struct MsePart
     float obs_lo, obs_hi;   // the search range: result when no candidate is ever selected
 };
 
+// round(c / delta - offset) of the reference (mse::cost) for a clamped value c, exactly
+__device__ __forceinline__ int code_exact(float c, const aimet_tf_encoding& e)
+{
+    return (int) round(c / e.delta - e.offset);
+}
+
+// mse::cost (_computeMSECost, MseEncodingAnalyzer.cpp:202-264) over the bins (zv[i], zw[i]),
+// i < n, in the same order and float / double arithmetic, for a channel whose observed range is
+// finite (every bin centre, candidate end and term finite; compact_bins), with two exact shortcuts:
+//  * the double division c / delta is a multiply by RN(1 / delta): y' = fma(c, RN(1/delta), -offset)
+//    lies within 2^-50 (|c / delta| + |offset| + 1) of the reference's RN(RN(c / delta) - offset),
+//    so round() picks the same integer wherever y' is farther than `thr` >= that from a
+//    half-integer (no tie: rint == round); otherwise, and for any non-finite y', the division
+//    decides. |c / delta| <= steps + 1 and |offset| <= steps for every MSE candidate (0 lies in
+//    [cLo, cHi]), so thr = 2^(bw + 2 - 48) bounds it;
+//  * monotone early exit: every term cw * d^2 is >= 0, so the float sum never decreases; once it
+//    exceeds `prune` (an error some candidate of this slice reached) the candidate cannot be the
+//    first minimum, and it is dropped (`pruned`).
+// The bin values come as double (zvd, zwd: exact copies of the float centres and masses) and as
+// float (zv, for the float subtraction v - deq).
+__device__ __forceinline__ float cost_fast(int bw, const float* zv, const double* zvd, const double* zwd, int n,
+                                           float cLo, float cHi, bool sym, bool strict, bool unsign, float prune,
+                                           bool& pruned)
+{
+    const aimet_tf_encoding e = mse::computed_encoding(bw, cLo, cHi, sym, strict, unsign);
+    const double rcp          = 1.0 / e.delta;
+    const double lo = cLo, hi = cHi, off = e.offset;
+    const double thr = __builtin_ldexp(1.0, bw - 46);
+    float err        = 0;
+    pruned           = false;
+    for (int i = 0; i < n; ++i)
+    {
+        // std::max(cLo, std::min(v, cHi)) for finite values (the sign of a zero does not matter:
+        // it only meets 0 / delta)
+        const double c = __builtin_fmax(lo, __builtin_fmin(zvd[i], hi));
+        const double y = __builtin_fma(c, rcp, -off);
+        double k;
+        if (__builtin_fabs((y - __builtin_floor(y)) - 0.5) > thr)   // false for NaN
+            k = __builtin_rint(y) + off;
+        else
+            k = (double) code_exact((float) c, e) + off;
+        const float deq = (float) (e.delta * k);
+        const double d  = (double) (zv[i] - deq);
+        err += zwd[i] * (d * d);
+        if ((i & 7) == 7 && err > prune)
+        {
+            pruned = true;
+            break;
+        }
+    }
+    return err;
+}
+
+// The bins of non-zero mass (cv, cw) -> (zv, zw) in order (and as double in zvd, zwd), by wave 0;
+// returns how many; `finite`: the observed range is finite (cost_fast applies). Skipping a
+// zero-mass bin is exact when its term cw * d^2 is +0, i.e. d finite: |d| <= |v| + |deq| with v a
+// bin centre and deq inside the candidate range, both within the observed range, so every term
+// is finite when the range stays below 2^100 in magnitude. Otherwise (and with a NaN mass, which
+// is kept) the full list is used.
+__device__ int compact_bins(const mse::Setup& st, const float* cv, const float* cw, float* zv, float* zw, double* zvd,
+                             double* zwd, bool& finite)
+{
+    __shared__ int count;
+    const bool finite_range = __builtin_fabsf(st.lo) < 1.2676506e30f && __builtin_fabsf(st.hi) < 1.2676506e30f;
+    if (threadIdx.x < 64)
+    {
+        const int lane = threadIdx.x;
+        int base       = 0;
+        for (int i0 = 0; i0 < st.nc; i0 += 64)
+        {
+            const int i     = i0 + lane;
+            const bool keep = i < st.nc && (!finite_range || !(cw[i] == 0.0f));
+            const unsigned long long m = __ballot(keep);
+            if (keep)
+            {
+                const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+                zv[pos]       = cv[i];
+                zw[pos]       = cw[i];
+                zvd[pos]      = (double) cv[i];
+                zwd[pos]      = (double) cw[i];
+            }
+            base += __popcll(m);
+        }
+        if (lane == 0)
+            count = base;
+    }
+    __syncthreads();
+    finite = finite_range;
+    return count;
+}
+
 __device__ __forceinline__ bool better(float e, long long t, float be, long long bt)
 {
     if (t < 0)
@@ -38,6 +129,9 @@ __device__ void search_slice(const TqDevice& d, int64_t c, int y, int splits, in
 {
     __shared__ double pdf[tfe::kBins];
     __shared__ float mins[mse::kMaxEdges + 1], maxs[mse::kMaxEdges + 1], cv[mse::kMaxEdges], cw[mse::kMaxEdges];
+    __shared__ float zv[mse::kMaxEdges], zw[mse::kMaxEdges];
+    __shared__ double zvd[mse::kMaxEdges], zwd[mse::kMaxEdges];
+    __shared__ float wg_best, wmin[kBlock / 64];
     __shared__ mse::Setup st;
     __shared__ int first, last;
     __shared__ float werr[kBlock / 64];
@@ -77,25 +171,61 @@ __device__ void search_slice(const TqDevice& d, int64_t c, int y, int splits, in
             st = mse::setup(h, first, last, mins, maxs, cv, cw);
         }
         __syncthreads();
-        const long long chunk = (st.total + splits - 1) / splits;
-        const long long t0 = (long long) y * chunk;
-        const long long t1 = t0 + chunk < st.total ? t0 + chunk : st.total;
+        bool finite;
+        const int nz = compact_bins(st, cv, cw, zv, zw, zvd, zwd, finite);
+        // candidates in the order j: iMin ascending (widest low end first), iMax from the widest
+        // positive end down (maxs[nx - 2] ... maxs[0], then the 0 end): the first round holds the
+        // near-full ranges, whose errors are small, and later rounds are pruned against the best
+        // error the workgroup has reached (cost_fast). The selection still compares the reference's
+        // candidate index t = iMin * nx + iMax (the first minimum in its order).
+        const int nx          = st.nmaxs;
+        const long long full  = (long long) st.nmins * nx;   // t = full - 1 is not a candidate
+        const long long chunk = (full + splits - 1) / splits;
+        const long long j0    = (long long) y * chunk;
+        const long long j1    = j0 + chunk < full ? j0 + chunk : full;
+        if (threadIdx.x == 0)
+            wg_best = FLT_MAX;
+        __syncthreads();
         float be = 0, blo = 0, bhi = 0;
         long long bt = -1;
-        for (long long t = t0 + threadIdx.x; t < t1; t += kBlock)
+        for (long long jb = j0; jb < j1; jb += kBlock)
         {
-            float cLo, cHi;
-            mse::candidate(st, mins, maxs, t, cLo, cHi);
-            float err = mse::cost(bw, cv, cw, st.nc, cLo, cHi, sym != 0, strict != 0, unsign != 0);
-            if (!(err < FLT_MAX))
-                continue;   // `err < bestErr` with bestErr = FLT_MAX never selects it
-            if (better(err, t, be, bt))
+            const long long j = jb + threadIdx.x;
+            const float prune = bt >= 0 && be < wg_best ? be : wg_best;
+            if (j < j1)
             {
-                be  = err;
-                bt  = t;
-                blo = cLo;
-                bhi = cHi;
+                const int iMin = (int) (j / nx);
+                const int jm   = (int) (j - (long long) iMin * nx);
+                const int iMax = jm < nx - 1 ? nx - 2 - jm : nx - 1;
+                const long long t = (long long) iMin * nx + iMax;
+                if (t != full - 1)
+                {
+                    const float cLo = mins[iMin], cHi = maxs[iMax];
+                    bool pruned     = false;
+                    const float err = finite ? cost_fast(bw, zv, zvd, zwd, nz, cLo, cHi, sym != 0, strict != 0,
+                                                         unsign != 0, prune, pruned)
+                                             : mse::cost(bw, zv, zw, nz, cLo, cHi, sym != 0, strict != 0, unsign != 0);
+                    // `err < bestErr` with bestErr = FLT_MAX never selects err >= FLT_MAX
+                    if (!pruned && err < FLT_MAX && better(err, t, be, bt))
+                    {
+                        be  = err;
+                        bt  = t;
+                        blo = cLo;
+                        bhi = cHi;
+                    }
+                }
             }
+            // the workgroup's best error so far (every lane's selected error is a complete one)
+            float m = bt >= 0 ? be : FLT_MAX;
+            for (int k = 32; k > 0; k >>= 1)
+                m = fminf(m, __shfl_xor(m, k, 64));
+            if (lane == 0)
+                wmin[threadIdx.x >> 6] = m;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                for (int w = 0; w < kBlock / 64; ++w)
+                    wg_best = fminf(wg_best, wmin[w]);
+            __syncthreads();
         }
         for (int k = 32; k > 0; k >>= 1)
         {

@@ -1011,6 +1011,8 @@ aimet_encoding_request* aimet_amd::encodings_launch(aimet_tensor_quantizer* cons
 // results (a calibration's last step), and hipEventSynchronize's wake-up after the kernel has ended
 // was measured at up to ~0.25 ms in some processes (profiles/r05/README.md), 6 % of a ResNet-50
 // compute_encodings. After 20 ms of polling the blocking wait takes over (a long device queue).
+// The first 200 us poll back to back; after that each poll is followed by a 20 us sleep, so a wait
+// that several ranks (or loader threads) share a host with does not hold a core at 100 %.
 void aimet_amd::await_event(hipEvent_t e)
 {
     const auto t0 = std::chrono::steady_clock::now();
@@ -1021,8 +1023,11 @@ void aimet_amd::await_event(hipEvent_t e)
             return;
         if (q != hipErrorNotReady)
             AIMET_HIP_CHECK(q);
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(20))
+        const auto waited = std::chrono::steady_clock::now() - t0;
+        if (waited > std::chrono::milliseconds(20))
             break;
+        if (waited > std::chrono::microseconds(200))
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     AIMET_HIP_CHECK(hipEventSynchronize(e));
 }
