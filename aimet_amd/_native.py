@@ -194,6 +194,8 @@ _PROTOTYPES = {
                                            _vp, ctypes.c_double, ctypes.c_double, ctypes.c_double, ctypes.c_double,
                                            _vp, _vp, _vp, _vp],
     "aimet_adaround_adam_bias_corrections": [ctypes.c_double, ctypes.c_double, _i64, _vp, _vp],
+    "aimet_adaround_set_exact_pow": [_int],
+    "aimet_adaround_get_exact_pow": [ctypes.POINTER(_int)],
 }
 _RESTYPES = {"aimet_last_error": ctypes.c_char_p, "aimet_version": ctypes.c_char_p}
 

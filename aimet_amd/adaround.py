@@ -16,6 +16,24 @@ ZETA = 1.1     # aimet_common/defs.py:305
 GAMMA = -0.1   # aimet_common/defs.py:304
 
 
+def set_exact_pow(exact: bool):
+    """The rounding loss's pow for every AdaRound backward launched afterwards (process-wide,
+    aimet_adaround_set_exact_pow): False (default) the f64 pow, within 1 ulp of torch's CPU pow
+    (Sleef powf_u10) over every f32 input in (0, 1) and the AdaRound beta schedules
+    (profiles/r06/pow_fast_check.txt); True the bit-exact emulation of torch's pow, about 3x the
+    arithmetic. Returns the previous setting."""
+    prev = get_exact_pow()
+    _native.call("aimet_adaround_set_exact_pow", int(bool(exact)))
+    return prev
+
+
+def get_exact_pow() -> bool:
+    import ctypes
+    v = ctypes.c_int(0)
+    _native.call("aimet_adaround_get_exact_pow", ctypes.byref(v))
+    return bool(v.value)
+
+
 def _channel_vec(v, C, device):
     v = torch.as_tensor(v, dtype=torch.float32, device=device).reshape(-1)
     if v.numel() == 1 and C != 1:

@@ -10,14 +10,21 @@
 // and its gradient.
 //
 // Numerics: the reference's arithmetic is torch float32 ops on the CPU; every op here is the same
-// IEEE operation in the same order, the sigmoid is torch's own vectorized CPU sigmoid
-// (1 / (1 + expf(-a)) with Sleef's expf_u10 polynomial, FMA form, then an IEEE divide) and the
-// rounding loss's pow(|2h-1|, beta) / pow(|2h-1|, beta-1) is torch's CPU pow (Sleef powf_u10 in
-// the vectorized part, the scalar tail as std::pow), so Wq and dL/dalpha, the rounding-loss term
-// included, are bit-identical to the reference (tests/golden/golden_adaround.npz).
+// IEEE operation in the same order, and the sigmoid is torch's own vectorized CPU sigmoid
+// (1 / (1 + expf(-a)) with Sleef's expf_u10 polynomial, FMA form, then an IEEE divide), so Wq is
+// bit-identical to the reference (tests/golden/golden_adaround.npz). The rounding loss's
+// pow(|2h-1|, beta) / pow(|2h-1|, beta-1) is, by default, the f64 pow of fast_pow.hpp: within
+// 1 ulp of torch's CPU pow (Sleef powf_u10) for every f32 |2h-1| in (0, 1) and every exponent of
+// the AdaRound schedules (profiles/r06/pow_fast_check.txt), at ~30 f64 instructions instead of
+// Sleef's ~142 f32 ones. aimet_adaround_set_exact_pow(1) selects the bit-exact emulation of
+// torch's pow instead (sleef_pow.hpp: Sleef powf_u10 in the vectorized part, the scalar tail as
+// std::pow), with which dL/dalpha, the rounding-loss term included, is bit-identical too.
 #include "common.hpp"
+#include "fast_pow.hpp"
 #include "recon.hpp"
 #include "sleef_pow.hpp"
+
+#include <atomic>
 
 namespace aimet_amd
 {
@@ -170,7 +177,10 @@ __device__ __forceinline__ float ada_bwd_round(float ga, float sg, float x, bool
     return ga + ((in_h ? dh : 0.0f) * kZmG * (1.0f - sg)) * sg;
 }
 
-// dL/dalpha of Wq + the rounding-loss gradient, one element (the loss term added to `loss`)
+// dL/dalpha of Wq + the rounding-loss gradient, one element (the loss term added to `loss`).
+// EXACT: the rounding loss's pow is the bit-exact emulation of torch's (sleef_pow.hpp), else the
+// f64 pow (fast_pow.hpp, within 1 ulp of it)
+template <bool EXACT>
 __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, float o, const AdaParams& p, float rcp,
                                          float& loss, uint32_t idx)
 {
@@ -183,17 +193,30 @@ __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, flo
         const float ax  = fabsf(x);
         float pbm1      = 0.0f;
         // only lanes inside h's clamp use the gradient's pow, and the logarithm only where it is not
-        // an exact case: a real branch, so a wave whose alphas all saturate skips the ~250 VALU
-        // ops of logkf + expkf (the skipped values were dead: the selects below drop them)
+        // an exact case: a real branch, so a wave whose alphas all saturate skips the logarithm and
+        // the exponentials (the skipped values were dead: the selects below drop them)
         if (in_h || p.want_loss)
         {
-            F2 l {0.0f, 0.0f};
-            if (ada_needs_log(ax, tail))
-                l = sleef_logkf(ax);
-            if (p.want_loss)
-                loss += 1.0f - pow01_log(ax, p.beta, tail, l);
-            if (in_h)
-                pbm1 = pow01_log(ax, p.beta_m1, tail, l);
+            if constexpr (EXACT)
+            {
+                F2 l {0.0f, 0.0f};
+                if (ada_needs_log(ax, tail))
+                    l = sleef_logkf(ax);
+                if (p.want_loss)
+                    loss += 1.0f - pow01_log(ax, p.beta, tail, l);
+                if (in_h)
+                    pbm1 = pow01_log(ax, p.beta_m1, tail, l);
+            }
+            else
+            {
+                double l = 0.0;
+                if (!(ax == 0.0f || ax == 1.0f))
+                    l = ln01(ax);
+                if (p.want_loss)
+                    loss += 1.0f - pow01_fast_l(ax, p.beta, l);
+                if (in_h)
+                    pbm1 = pow01_fast_l(ax, p.beta_m1, l);
+            }
         }
         ga = ada_bwd_round(ga, sg, x, in_h, pbm1, p);
     }
@@ -227,7 +250,7 @@ __device__ __forceinline__ void wave_sync()
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int E, bool TAIL>
+template <int E, bool TAIL, bool EXACT>
 __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool (&tail_in)[E], const bool (&use)[E],
                                                const AdaParams& p, float* __restrict__ wl, float (&pbm1)[E],
                                                float (&pb)[E])
@@ -244,7 +267,28 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
         ballot[k] = __builtin_amdgcn_ballot_w64(need[k]);
         total += (uint32_t) __popcll(ballot[k]);
     }
-    if (4 * total >= 3 * 64 * E)
+    if (!EXACT && 4 * total >= 3 * 64 * E)
+    {
+        // a dense wave: each lane evaluates its own elements in place with the f64 pow (its
+        // logarithm shared by the two exponents; the scalar tail takes it too: fast_pow.hpp)
+#pragma unroll
+        for (int k = 0; k < E; ++k)
+        {
+            if (need[k])
+            {
+                const double l = ln01(ax[k]);
+                pbm1[k]        = pow01_fast_l(ax[k], p.beta_m1, l);
+                pb[k]          = p.want_loss ? pow01_fast_l(ax[k], p.beta, l) : 0.0f;
+            }
+            else
+            {
+                pbm1[k] = pow01_exact(ax[k], p.beta_m1);
+                pb[k]   = pow01_exact(ax[k], p.beta);
+            }
+        }
+        return;
+    }
+    if (EXACT && 4 * total >= 3 * 64 * E)
     {
         // a dense wave (few saturated alphas): each lane evaluates its own elements in place, the
         // compaction's LDS round trip would not pay (the same values), two at a time in packed f32
@@ -315,12 +359,22 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
         const float sv  = wl[j];
         const bool tl   = TAIL && __builtin_signbit(sv);   // a NaN keeps its sign through the negation
         const float v   = __builtin_fabsf(sv);
-        F2 l {0.0f, 0.0f};
-        if (!tl)
-            l = sleef_logkf(v);
-        wl[j] = pow01_log(v, p.beta_m1, tl, l);
-        if (p.want_loss)
-            wl1[j] = pow01_log(v, p.beta, tl, l);
+        if constexpr (EXACT)
+        {
+            F2 l {0.0f, 0.0f};
+            if (!tl)
+                l = sleef_logkf(v);
+            wl[j] = pow01_log(v, p.beta_m1, tl, l);
+            if (p.want_loss)
+                wl1[j] = pow01_log(v, p.beta, tl, l);
+        }
+        else
+        {
+            const double l = ln01(v);
+            wl[j]          = pow01_fast_l(v, p.beta_m1, l);
+            if (p.want_loss)
+                wl1[j] = pow01_fast_l(v, p.beta, l);
+        }
     }
     wave_sync();
 #pragma unroll
@@ -465,7 +519,7 @@ __global__ __launch_bounds__(kBlock) void round_loss_fold_kernel(const float* __
 // each; bounded grid: one round-loss atomic per workgroup); the loop bounds are uniform over the
 // workgroup (ada_round_pows synchronises it)
 // TAIL = false: n % 32 == 0, no element lies in the reference's scalar pow tail (compile-time)
-template <int U, bool WL, bool TAIL>
+template <int U, bool WL, bool TAIL, bool EXACT>
 __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __restrict__ w, const f4* __restrict__ alpha,
                                                                   const f4* __restrict__ g, f4* __restrict__ ga,
                                                                   uint32_t nq, AdaChannel map,
@@ -525,7 +579,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
         if (p.reg != 0.0f)   // uniform: a kernel argument or the device-resident value
         {
             float pbm1[E], pb[E];
-            ada_round_pows<E, TAIL>(ax, tail, p.want_loss ? valid : in_h, p, wl, pbm1, pb);
+            ada_round_pows<E, TAIL, EXACT>(ax, tail, p.want_loss ? valid : in_h, p, wl, pbm1, pb);
 #pragma unroll
             for (int k = 0; k < E; ++k)
             {
@@ -546,6 +600,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
         round_loss_add(loss, p.reg, round_loss, loss_part, ticket);
 }
 
+template <bool EXACT>
 __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __restrict__ w,
                                                               const float* __restrict__ alpha,
                                                               const float* __restrict__ g, float* __restrict__ ga,
@@ -566,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
     {
         uint32_t c = map.channel(i);
-        ga[i]      = ada_bwd(w[i], alpha[i], g[i], delta[c], offset[c], p, __builtin_amdgcn_rcpf(delta[c]), loss, i);
+        ga[i]      = ada_bwd<EXACT>(w[i], alpha[i], g[i], delta[c], offset[c], p, __builtin_amdgcn_rcpf(delta[c]), loss, i);
     }
     if (p.reg != 0.0f && round_loss)
         round_loss_add(loss, p.reg, round_loss, loss_part, ticket);
@@ -626,6 +681,18 @@ bool aligned16(const void* p)
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0;
 }
 
+// the rounding loss's pow for launches from now on: the f64 pow (0, default) or the bit-exact
+// emulation of torch's (1); aimet_adaround_set_exact_pow
+std::atomic<int>& exact_pow_flag()
+{
+    static std::atomic<int> f {0};
+    return f;
+}
+bool exact_pow()
+{
+    return exact_pow_flag().load(std::memory_order_relaxed) != 0;
+}
+
 // ---- one optimizer step fused into the backward (single-process HIP-graph loop) -----------------
 // torch.optim.Adam(fused=True) per element, as ATen's adam_math (native/hip/fused_adam_utils.cuh)
 // computes it for a float parameter without weight decay / amsgrad / maximize: the moments in
@@ -669,7 +736,7 @@ __global__ __launch_bounds__(kBlock) void adam_bias_corr_kernel(double beta1, do
 // dL/dalpha (ada_bwd, with this iteration's {reg, beta, beta - 1} from reg_beta_all[it]) and the
 // Adam update of alpha in place; `step` = it_next[0] (= it + 1, written by the gather kernel of the
 // same iteration), workgroup 0 publishes it to it_cur for the next iteration's gather.
-template <bool VEC, bool WL, bool TAIL = true>
+template <bool VEC, bool WL, bool TAIL, bool EXACT>
 __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* __restrict__ w,
                                                                    float* __restrict__ alpha,
                                                                    const float* __restrict__ g,
@@ -779,7 +846,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
             if (p.reg != 0.0f)   // uniform: this iteration's device-resident value
             {
                 float pbm1[4], pb[4];
-                ada_round_pows<4, TAIL>(ax, tail, use, p, wl, pbm1, pb);
+                ada_round_pows<4, TAIL, EXACT>(ax, tail, use, p, wl, pbm1, pb);
 #pragma unroll
                 for (int k = 0; k < 4; ++k)
                 {
@@ -833,7 +900,7 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                     if (s + u < nparts)
                         gi += t[u];
             }
-            const float ga  = ada_bwd(wi, ai, gi, d, o, p, rcp, loss, i);
+            const float ga  = ada_bwd<EXACT>(wi, ai, gi, d, o, p, rcp, loss, i);
             const float an  = adam_elem(ai, ga, mi, vi, adam, bc1, bc2s);
             alpha[i]        = an;
             exp_avg[i]      = mi;
@@ -1100,15 +1167,21 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
                     reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),
                     reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss, reg_beta, lf.part, lf.ticket);
             };
-            const bool wl = p.want_loss != 0, tl = n % 32 != 0;
+            // the scalar pow tail exists only for the exact pow (the f64 pow takes every element alike)
+            const bool wl = p.want_loss != 0, ex = exact_pow(), tl = ex && n % 32 != 0;
             // (a form compiled for 8 waves per SIMD spilled and measured slower:
             // profiles/r04/ada_bwd_tune_occ8.jsonl)
             auto go = [&](auto u) {
                 constexpr int UU = decltype(u)::value;
-                if (tl)
-                    wl ? launch(adaround_bwd_vec_kernel<UU, true, true>) : launch(adaround_bwd_vec_kernel<UU, false, true>);
+                if (!ex)
+                    wl ? launch(adaround_bwd_vec_kernel<UU, true, false, false>)
+                       : launch(adaround_bwd_vec_kernel<UU, false, false, false>);
+                else if (tl)
+                    wl ? launch(adaround_bwd_vec_kernel<UU, true, true, true>)
+                       : launch(adaround_bwd_vec_kernel<UU, false, true, true>);
                 else
-                    wl ? launch(adaround_bwd_vec_kernel<UU, true, false>) : launch(adaround_bwd_vec_kernel<UU, false, false>);
+                    wl ? launch(adaround_bwd_vec_kernel<UU, true, false, true>)
+                       : launch(adaround_bwd_vec_kernel<UU, false, false, true>);
             };
             go(std::integral_constant<int, U> {});
             AIMET_LAUNCH_CHECK();
@@ -1118,8 +1191,11 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
         {
             const unsigned gx = stream_blocks(n, kBlock);
             LossFold lf(round_loss, gx, st);
-            adaround_bwd_kernel<<<gx, kBlock, 0, st>>>(w, alpha, g, ga, (uint32_t) n, map, delta, offset, p, round_loss,
-                                                      reg_beta, lf.part, lf.ticket);
+            auto launch = [&](auto kernel) {
+                kernel<<<gx, kBlock, 0, st>>>(w, alpha, g, ga, (uint32_t) n, map, delta, offset, p, round_loss, reg_beta,
+                                              lf.part, lf.ticket);
+            };
+            exact_pow() ? launch(adaround_bwd_kernel<true>) : launch(adaround_bwd_kernel<false>);
             AIMET_LAUNCH_CHECK();
             lf.finish(p.reg, reg_beta, nullptr, round_loss);
         }
@@ -1356,12 +1432,24 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
                                                          (uint32_t) part_kk);
         };
         const bool wl = round_loss != nullptr;
-        if (vec && n % 32 == 0)   // no element in the scalar pow tail
-            wl ? launch(adaround_bwd_adam_kernel<true, true, false>) : launch(adaround_bwd_adam_kernel<true, false, false>);
+        if (!exact_pow())   // the f64 pow: no scalar pow tail
+        {
+            if (vec)
+                wl ? launch(adaround_bwd_adam_kernel<true, true, false, false>)
+                   : launch(adaround_bwd_adam_kernel<true, false, false, false>);
+            else
+                wl ? launch(adaround_bwd_adam_kernel<false, true, true, false>)
+                   : launch(adaround_bwd_adam_kernel<false, false, true, false>);
+        }
+        else if (vec && n % 32 == 0)   // no element in the scalar pow tail
+            wl ? launch(adaround_bwd_adam_kernel<true, true, false, true>)
+               : launch(adaround_bwd_adam_kernel<true, false, false, true>);
         else if (vec)
-            wl ? launch(adaround_bwd_adam_kernel<true, true>) : launch(adaround_bwd_adam_kernel<true, false>);
+            wl ? launch(adaround_bwd_adam_kernel<true, true, true, true>)
+               : launch(adaround_bwd_adam_kernel<true, false, true, true>);
         else
-            wl ? launch(adaround_bwd_adam_kernel<false, true>) : launch(adaround_bwd_adam_kernel<false, false>);
+            wl ? launch(adaround_bwd_adam_kernel<false, true, true, true>)
+               : launch(adaround_bwd_adam_kernel<false, false, true, true>);
         AIMET_LAUNCH_CHECK();
         lf.finish(0.0f, reg_beta_all, it_next, round_loss);
     });
@@ -1376,6 +1464,19 @@ int aimet_adaround_backward_adam(const float* w, float* alpha, const float* grad
     return aimet_adaround_backward_adam_parts(w, alpha, grad_wq, 1, 0, exp_avg, exp_avg_sq, outer, C, K, delta, offset, bw,
                                               reg_beta_all, it_next, it_cur, lr, beta1, beta2, eps, round_loss, wq_next,
                                               nullptr, stream);
+}
+
+int aimet_adaround_set_exact_pow(int exact)
+{
+    return guarded([&] { exact_pow_flag().store(exact ? 1 : 0); });
+}
+
+int aimet_adaround_get_exact_pow(int* exact)
+{
+    return guarded([&] {
+        AIMET_REQUIRE(exact != nullptr, "null argument");
+        *exact = exact_pow() ? 1 : 0;
+    });
 }
 
 int aimet_adaround_adam_bias_corrections(double beta1, double beta2, int64_t steps, float* bias_corr, void* stream)

@@ -3,18 +3,25 @@
 //
 // Reference: EntropyEncodingAnalyzer::computeEncoding -> _optimizeKL (EntropyEncodingAnalyzer.cpp:
 // 226-435) runs on the host, one channel at a time: 129 windows x ~5 passes over up to 512 bins,
-// with a log per bin (~3 ms per channel). Here: one workgroup per channel; lane 0 prepares the
-// histogram (symmetric rescale) and enumerates the windows (entropy_kl.hpp: the window sequence
-// never depends on a KL value), then one window per lane computes its KL divergence with the
-// reference's float/double arithmetic streamed in bin order, and lane 0 picks the first strict
-// minimum.
+// with a log per bin (~3 ms per channel). Here: one workgroup per channel:
+//  1. the histogram the windows run over (the symmetric rescale) and its prefix tables: in
+//     parallel over the bins when every bin count is an integer below 2^43 (bin counts always
+//     are: sums of integers are then exact in any order), else by lane 0 as the reference loops;
+//     lane 0 enumerates the windows (entropy_kl.hpp: the window sequence never depends on a KL
+//     value);
+//  2. one window per lane: the reference's float normalisers of P and Q, streamed in bin order
+//     with its float / double operations (exact);
+//  3. the divergence sum_i p_i log(p_i / q_i) of every window, split into kSegs segments of its 255
+//     levels over all lanes, the segments' sums added per window;
+//  4. lane 0 picks the first strict minimum.
 //
-// Bit parity: every operation equals the host's except the natural logarithm (device library vs
-// glibc, each within a couple of ulp of the true value). With t_i = p_i log(p_i/q_i), the two
-// sums differ by at most ~2^-43 * sum |t_i| for <= 512 terms; a window is accepted as the winner
-// only when every other window's divergence exceeds it by more than 1e-11 * (sum |t| of both),
-// otherwise (and for non-finite ranges) the channel is flagged and the host re-runs the glibc
-// search for it (quantizer.cpp). The accepted winner is then the host's winner too.
+// Bit parity: every operation of 1, 2 and the window choice equals the host's. The divergence
+// differs from the host's (the device's log, p and q as multiplies by 1 / normaliser instead of
+// divisions, the segments' sums re-associated): per term by at most ~2 ulp of |t| plus 2^-51 p, so
+// the two sums differ by < 2^-43 sum|t| + 1e-15. A window is accepted as the winner only when every
+// other window's divergence exceeds it by more than 1e-11 * (sum |t| of both) + 1e-14; otherwise
+// (and for non-finite ranges) the channel is flagged and the host re-runs the glibc search for it
+// (quantizer.cpp). The accepted winner is then the host's winner too.
 #include "entropy_kl.hpp"
 #include "tq_state.hpp"
 
@@ -23,8 +30,11 @@ namespace aimet_amd
 namespace
 {
 
-constexpr int kEntBlock = 192;   // >= kWindows (129): one window per lane
+constexpr int kEntBlock = 192;   // >= kWindows (129): one window per lane in step 2
 static_assert(kEntBlock >= entropy::kWindows, "one window per lane");
+constexpr int kSegs   = 4;                              // step 3: segments of 64 levels per window
+constexpr int kItems  = entropy::kWindows * kSegs;      // 516 (window, segment) items
+constexpr int kSegLev = (entropy::kLevels + kSegs - 1) / kSegs;
 
 struct EntJob
 {
@@ -33,21 +43,140 @@ struct EntJob
     const double* hist;         // [C][512] bin counts
     EntropyRange* out;          // [C]
     int64_t start;              // first global channel of this job
+    EntropyRange* flat;         // optional: every job's ranges concatenated (+ start)
 };
+
+// a window's step-2 results, read by step 3
+struct WinState
+{
+    double left, right;       // the saturated end bins of P
+    double rdP, rdQ;          // 1 / the normalisers of the conditioned P and Q
+    double rqz;               // 1 / (the conditioned Q of an empty bin / dQ)
+    entropy::Cond cP, cQ;
+    int brk;                  // the reference loop stops at this window (P or Q sums to 0)
+};
+
+// step 2 for window [a, b] with the prefix tables (q_zero_rule holds: integral histograms) or
+// without them (two streamed passes, as entropy::window_kl)
+__device__ void window_norms(const double* hist, int a, int b, const entropy::Prefix* pre, WinState& st)
+{
+    using namespace entropy;
+    const int win = b - a + 1;
+    double left = 0, right = 0;
+    if (pre)
+        left = pre->left[a];
+    else
+        for (int i = 0; i <= a; ++i)
+            left += hist[i];
+    for (int i = b; i < kBins; ++i)
+        right += hist[i];
+    float aP = 0.f, aQ = 0.f, sP = 0.f, sQ = 0.f;
+    Cond cP, cQ;
+    if (pre && pre->q_zero_rule)
+    {
+        const uint64_t zP = (uint64_t) (pre->zeros[b] - pre->zeros[a + 1]) + (left == 0.f) + (right == 0.f);
+        const uint64_t zQ = (uint64_t) (pre->zeros[b + 1] - pre->zeros[a]);
+        cP = cond_of(zP, (uint64_t) win);
+        cQ = cond_of(zQ, (uint64_t) win);
+        stream_pq(hist, a, b, left, right, [&](int, double p, double q) {
+            aP = (float) ((double) aP + p);
+            aQ = (float) ((double) aQ + q);
+            sP = (float) ((double) sP + cond_apply(cP, p));
+            sQ = (float) ((double) sQ + cond_apply(cQ, q));
+        });
+    }
+    else
+    {
+        uint64_t zP = 0, zQ = 0;
+        stream_pq(hist, a, b, left, right, [&](int, double p, double q) {
+            aP = (float) ((double) aP + p);
+            aQ = (float) ((double) aQ + q);
+            zP += (p == 0.f);
+            zQ += (q == 0.f);
+        });
+        cP = cond_of(zP, (uint64_t) win);
+        cQ = cond_of(zQ, (uint64_t) win);
+        if (!(aP == 0 || aQ == 0))
+            stream_pq(hist, a, b, left, right, [&](int, double p, double q) {
+                sP = (float) ((double) sP + cond_apply(cP, p));
+                sQ = (float) ((double) sQ + cond_apply(cQ, q));
+            });
+    }
+    st.left  = left;
+    st.right = right;
+    st.cP    = cP;
+    st.cQ    = cQ;
+    st.brk   = (aP == 0 || aQ == 0) ? 1 : 0;
+    const double dP = sP, dQ = sQ;
+    st.rdP = 1.0 / dP;
+    st.rdQ = 1.0 / dQ;
+    st.rqz = 1.0 / (cond_apply(cQ, 0.0) * st.rdQ);
+}
+
+// step 3: the divergence terms of levels [q0, q1) of window [a, b] (entropy::stream_pq's levels),
+// p = cond(P) / dP, q = cond(Q) / dQ, sum of p log(p / q) over p, q > 0, and of its magnitudes
+__device__ void window_segment(const double* hist, int a, int b, int q0, int q1, const WinState& st, double& dv,
+                               double& mag)
+{
+    using namespace entropy;
+    const int win       = b - a + 1;
+    const double* hw    = hist + a;
+    const double merged = (double) win / (double) kLevels;
+    const double qz     = cond_apply(st.cQ, 0.0) * st.rdQ;
+    dv = 0;
+    mag = 0;
+    for (int q = q0; q < q1; ++q)
+    {
+        const int i0 = (int) (uint64_t) ceil((double) q * merged);
+        const int i1 = q < kLevels - 1 ? (int) (uint64_t) ceil((double) (q + 1) * merged) : win;
+        double sum = 0, norm = 0;
+        for (int i = i0; i < i1; ++i)
+        {
+            sum += hw[i];
+            norm += (hw[i] != 0);
+        }
+        // the level's Q where its bin is non-empty (the reference's sum / norm, per bin)
+        double qnz = 0.0, rqnz = 0.0;
+        if (norm != 0)
+        {
+            qnz  = cond_apply(st.cQ, sum / norm) * st.rdQ;
+            rqnz = 1.0 / qnz;
+        }
+        for (int i = i0; i < i1; ++i)
+        {
+            const bool nz   = norm != 0 && hw[i] != 0;
+            const double Pi = i == 0 ? 0.0 + st.left : (i == win - 1 ? 0.0 + st.right : hw[i]);
+            const double pn = cond_apply(st.cP, Pi) * st.rdP;
+            const double qn = nz ? qnz : qz;
+            if (pn > 0 && qn > 0)
+            {
+                const double t = pn * log(pn * (nz ? rqnz : st.rqz));
+                dv += t;
+                mag += fabs(t);
+            }
+        }
+    }
+}
 
 __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob* __restrict__ jobs, int njobs,
                                                                    int64_t total, int sym, int strict, int unsign)
 {
-    __shared__ double tpp[entropy::kBins];
+    // step 1's source histogram and integer accumulators share their LDS with step 3's sums
+    __shared__ double scratch[2 * kItems];
+    double* tpp                 = scratch;
+    unsigned long long* acc_u   = reinterpret_cast<unsigned long long*>(scratch + entropy::kBins);
+    double* part_dv             = scratch;
+    double* part_mag            = scratch + kItems;
+    static_assert(2 * kItems >= 2 * entropy::kBins, "step 1 fits the scratch");
     __shared__ double hist[entropy::kBins];
     __shared__ short wa[entropy::kWindows], wb[entropy::kWindows];
-    __shared__ double dv[entropy::kWindows], mag[entropy::kWindows];
-    __shared__ int brk[entropy::kWindows];
+    __shared__ WinState ws[entropy::kWindows];
     __shared__ double left[entropy::kBins];
     __shared__ int zeros[entropy::kBins + 1];
     __shared__ double s_lo, s_hi;
-    __shared__ int s_n, s_rule;
+    __shared__ int s_n, s_rule, s_integral;
     const int t = threadIdx.x;
+    const int lane = t & 63;
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
     {
         int lo_j = 0, hi_j = njobs - 1;   // last job with start <= g
@@ -67,13 +196,123 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
             // no histogram (the host returns the unseen / all-zero encoding), or a non-finite
             // range: the host search decides
             if (t == 0)
-                j.out[c] = EntropyRange {0.f, 0.f, j.pdf_init[c] ? kEntHost : kEntNoHist, 0};
+            {
+                const EntropyRange r {0.f, 0.f, j.pdf_init[c] ? kEntHost : kEntNoHist, 0};
+                j.out[c] = r;
+                if (j.flat)
+                    j.flat[j.start + c] = r;
+            }
             continue;
         }
-        for (int i = t; i < entropy::kBins; i += kEntBlock)
-            tpp[i] = j.hist[c * entropy::kBins + i];
-        __syncthreads();
+        // ---- 1. the histogram, its prefix tables, the windows ----------------------------------
         if (t == 0)
+            s_integral = 1;
+        __syncthreads();
+        for (int i = t; i < entropy::kBins; i += kEntBlock)
+        {
+            const double v = j.hist[c * entropy::kBins + i];
+            tpp[i]         = v;
+            acc_u[i]       = 0;
+            // an integer in [0, 2^43): every sum of the 512 bins below is exact in any order
+            if (!(v >= 0.0 && v < 8796093022208.0 && __builtin_floor(v) == v))
+                s_integral = 0;
+        }
+        __syncthreads();
+        const bool integral = s_integral != 0;
+        // the symmetric rescale (kl_histogram) and whether it applies
+        const bool rescale = sym && (tmin < 0.0 || !unsign);
+        const float amax   = (float) entropy::kmax(fabs(tmax), fabs(tmin));
+        const double dlo = rescale ? (double) -amax : tmin, dhi = rescale ? (double) amax : tmax;
+        const bool same = !rescale || (tmin == dlo && tmax == dhi);
+        if (integral)
+        {
+            if (same)
+            {
+                for (int i = t; i < entropy::kBins; i += kEntBlock)
+                    hist[i] = tpp[i];
+            }
+            else
+            {
+                // rescale_histogram with every source bin's parts added as integers (any order)
+                const uint64_t n  = entropy::kBins;
+                const double srcW = (tmax - tmin) / (double) n;
+                const double dstW = (dhi - dlo) / (double) n;
+                for (int bb = t; bb < entropy::kBins; bb += kEntBlock)
+                {
+                    const double v = tpp[bb];
+                    if (v == 0)
+                        continue;
+                    const double s0 = tmin + (double) bb * srcW;
+                    const double s1 = tmin + (double) (bb + 1) * srcW;
+                    uint64_t d0     = entropy::x86_d2u64(entropy::kmax(floor((s0 - dlo) / dstW), 0.0));
+                    uint64_t d1     = entropy::x86_d2u64(entropy::kmax(ceil((s1 - dlo) / dstW), 0.0));
+                    d0              = entropy::kmin(d0, n - 1);
+                    d1              = entropy::kmin(d1, n - 1);
+                    double rem      = v;
+                    for (uint64_t k = d0; k <= d1; ++k)
+                    {
+                        const double o0 = entropy::kmax(s0, dlo + (double) k * dstW);
+                        const double o1 = entropy::kmin(s1, dlo + (double) (k + 1) * dstW);
+                        double ratio    = (o1 - o0) / srcW;
+                        ratio           = ratio >= 0.0f ? ratio : 0.0f;
+                        ratio           = ratio <= 1.0f ? ratio : 1.0f;
+                        double part     = round(ratio * v);
+                        part            = part <= rem ? part : rem;
+                        atomicAdd(&acc_u[k], (unsigned long long) part);
+                        rem -= part;
+                    }
+                }
+                __syncthreads();
+                for (int i = t; i < entropy::kBins; i += kEntBlock)
+                    hist[i] = (double) acc_u[i];
+            }
+            __syncthreads();
+            // prefix tables: wave 0, 8 bins per lane, then the lanes' running totals
+            if (t < 64)
+            {
+                double l = 0;
+                int z    = 0;
+                for (int k = 0; k < 8; ++k)
+                {
+                    const double h = hist[8 * lane + k];
+                    l += h;
+                    z += h == 0;
+                }
+                double lx = l;
+                int zx    = z;
+                for (int o = 1; o < 64; o <<= 1)   // inclusive scan
+                {
+                    const double lo = __shfl_up(lx, o, 64);
+                    const int zo    = __shfl_up(zx, o, 64);
+                    if (lane >= o)
+                    {
+                        lx += lo;
+                        zx += zo;
+                    }
+                }
+                double run = lx - l;
+                int zr     = zx - z;
+                for (int k = 0; k < 8; ++k)
+                {
+                    const double h = hist[8 * lane + k];
+                    run += h;
+                    zr += h == 0;
+                    left[8 * lane + k]      = run;
+                    zeros[8 * lane + k + 1] = zr;
+                }
+                if (lane == 0)
+                    zeros[0] = 0;
+            }
+            __syncthreads();
+            if (t == 0)
+            {
+                s_lo   = dlo;
+                s_hi   = dhi;
+                s_n    = entropy::windows(hist, dlo, (dhi - dlo) / (double) entropy::kBins, sym || strict, wa, wb);
+                s_rule = 1;   // integral bins: 0 or >= 1
+            }
+        }
+        else if (t == 0)
         {
             double lo, hi;
             entropy::kl_histogram(tmin, tmax, tpp, sym != 0, unsign != 0, hist, lo, hi);
@@ -85,36 +324,69 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
             s_rule = rule ? 1 : 0;
         }
         __syncthreads();
+        // ---- 2. the normalisers of every window (exact) -----------------------------------------
+        const entropy::Prefix pre {left, zeros, s_rule != 0};
         if (t < s_n)
+            window_norms(hist, wa[t], wb[t], &pre, ws[t]);
+        __syncthreads();
+        // ---- 3. the divergences, (window, segment) items over every lane --------------------------
+        for (int it = t; it < s_n * kSegs; it += kEntBlock)
         {
-            const entropy::Prefix pre {left, zeros, s_rule != 0};
-            const entropy::WindowKl r =
-                entropy::window_kl(hist, wa[t], wb[t], [](double v) { return log(v); }, &pre);
-            dv[t]  = r.dv;
-            mag[t] = r.mag;
-            brk[t] = r.brk ? 1 : 0;
+            const int w = it / kSegs, sgm = it - w * kSegs;
+            double dv = 0, mag = 0;
+            if (!ws[w].brk)
+            {
+                const int q0 = sgm * kSegLev, q1 = q0 + kSegLev < entropy::kLevels ? q0 + kSegLev : entropy::kLevels;
+                window_segment(hist, wa[w], wb[w], q0, q1, ws[w], dv, mag);
+            }
+            part_dv[it]  = dv;
+            part_mag[it] = mag;
         }
         __syncthreads();
+        // ---- 4. the first strict minimum ----------------------------------------------------------
         if (t == 0)
         {
             // the reference loop: stop at the first breaking window, keep the first strict minimum
             int nv = 0;
-            while (nv < s_n && !brk[nv])
+            while (nv < s_n && !ws[nv].brk)
                 ++nv;
-            int best = -1;
+            auto dv_of = [&](int k) {
+                double v = 0;
+                for (int sgm = 0; sgm < kSegs; ++sgm)
+                    v += part_dv[k * kSegs + sgm];
+                return v;
+            };
+            auto mag_of = [&](int k) {
+                double v = 0;
+                for (int sgm = 0; sgm < kSegs; ++sgm)
+                    v += part_mag[k * kSegs + sgm];
+                return v;
+            };
+            int best      = -1;
+            double best_v = __builtin_inf();
             for (int k = 0; k < nv; ++k)
-                if (best < 0 ? dv[k] < __builtin_inf() : dv[k] < dv[best])
-                    best = k;
-            int status = kEntFinal;
-            for (int k = 0; k < nv && best >= 0; ++k)
             {
-                if (k == best)
-                    continue;
-                const double tol = 1e-11 * (mag[k] + mag[best]) + 1e-300;
-                if (!(dv[k] - dv[best] > tol))   // a near-tie (or NaN): glibc decides
+                const double v = dv_of(k);
+                if (best < 0 ? v < __builtin_inf() : v < best_v)
                 {
-                    status = kEntHost;
-                    break;
+                    best   = k;
+                    best_v = v;
+                }
+            }
+            int status = kEntFinal;
+            if (best >= 0)
+            {
+                const double best_m = mag_of(best);
+                for (int k = 0; k < nv; ++k)
+                {
+                    if (k == best)
+                        continue;
+                    const double tol = 1e-11 * (mag_of(k) + best_m) + 1e-14;
+                    if (!(dv_of(k) - best_v > tol))   // a near-tie (or NaN): glibc decides
+                    {
+                        status = kEntHost;
+                        break;
+                    }
                 }
             }
             const double w = (s_hi - s_lo) / (double) entropy::kBins;
@@ -125,6 +397,8 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
                 hi = (float) (s_lo + (double) (wb[best] + 1) * w);
             }
             j.out[c] = EntropyRange {lo, hi, status, 0};
+            if (j.flat)
+                j.flat[j.start + c] = EntropyRange {lo, hi, status, 0};
         }
         __syncthreads();
     }
@@ -133,15 +407,20 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
 }   // namespace
 
 void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, bool sym, bool strict, bool unsign,
-                                hipStream_t s)
+                                hipStream_t s, EntropyRange* pinned_dst)
 {
     if (n == 0)
         return;
     std::vector<EntJob> jobs((size_t) n);
     int64_t total = 0;
     for (int i = 0; i < n; ++i)
+        total += Cs[i];
+    // every quantizer's ranges side by side, for one copy into the caller's pinned block
+    auto* flat = pinned_dst ? static_cast<EntropyRange*>(scratch_alloc(sizeof(EntropyRange) * total, s)) : nullptr;
+    total = 0;
+    for (int i = 0; i < n; ++i)
     {
-        jobs[(size_t) i] = EntJob {ds[i]->acc, ds[i]->pdf_init, ds[i]->pdf, entropy_ranges(*ds[i]), total};
+        jobs[(size_t) i] = EntJob {ds[i]->acc, ds[i]->pdf_init, ds[i]->pdf, entropy_ranges(*ds[i]), total, flat};
         total += Cs[i];
     }
     auto* dj       = static_cast<EntJob*>(upload_async(jobs.data(), sizeof(EntJob) * (size_t) n, s));
@@ -149,6 +428,11 @@ void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, in
     entropy_search_kernel<<<grid, kEntBlock, 0, s>>>(dj, n, total, sym ? 1 : 0, strict ? 1 : 0, unsign ? 1 : 0);
     AIMET_LAUNCH_CHECK();
     scratch_free(dj, s);
+    if (flat)
+    {
+        AIMET_HIP_CHECK(hipMemcpyAsync(pinned_dst, flat, sizeof(EntropyRange) * total, hipMemcpyDeviceToHost, s));
+        scratch_free(flat, s);
+    }
 }
 
 }   // namespace aimet_amd

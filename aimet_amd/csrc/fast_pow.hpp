@@ -22,8 +22,8 @@ namespace aimet_amd
 namespace
 {
 
-// x^e for x in (0, 1) (normal or subnormal), e in (0, 64]: x^e rounded from f64
-__device__ __forceinline__ float powf01_f64(float x, float e)
+// ln x for x in (0, 1) (normal or subnormal), |error| <= 1.5e-12 + 2^-52 |ln x|
+__device__ __forceinline__ double ln01(float x)
 {
     int k;
     float mf = __builtin_frexpf(x, &k);   // x = mf 2^k, mf in [0.5, 1)
@@ -32,7 +32,7 @@ __device__ __forceinline__ float powf01_f64(float x, float e)
         mf *= 2.0f;
         k -= 1;
     }
-    const double m = (double) mf;   // [sqrt(1/2), sqrt(2))
+    const double m = (double) mf;            // [sqrt(1/2), sqrt(2))
     const double a = m + 1.0, b = m - 1.0;   // exact
     double r       = __builtin_amdgcn_rcp(a);
     r              = __builtin_fma(__builtin_fma(-a, r, 1.0), r, r);   // one Newton step: 2^-50
@@ -43,30 +43,42 @@ __device__ __forceinline__ float powf01_f64(float x, float e)
     p              = __builtin_fma(p, s, 0.4000038467237519);
     p              = __builtin_fma(p, s, 0.6666666524748752);
     p              = __builtin_fma(p, s, 2.0000000000083595);
-    const double l = __builtin_fma((double) k, 0.6931471805599453, t * p);   // ln x
-    const double y = l * (double) e;                                        // <= 0
+    return __builtin_fma((double) k, 0.6931471805599453, t * p);
+}
+
+// exp(l e) rounded to f32, for l = ln01(x) and e in (0, 64] (l e <= 0)
+__device__ __forceinline__ float exp_ln(double l, float e)
+{
+    const double y = l * (double) e;
     // exp(y) = 2^n exp(rr): n = rint(y / ln 2), rr = y - n ln2 (ln 2 split: n ln2_hi exact for |n| < 2^11)
-    const double n  = __builtin_rint(y * 1.4426950408889634);
-    double rr       = __builtin_fma(n, -6.93147180369123816490e-01, y);
-    rr              = __builtin_fma(n, -1.90821492927058770002e-10, rr);
-    double q        = 0.00019907569310848288;
-    q               = __builtin_fma(q, rr, 0.0013948578326459795);
-    q               = __builtin_fma(q, rr, 0.008333283538708528);
-    q               = __builtin_fma(q, rr, 0.041666218319291945);
-    q               = __builtin_fma(q, rr, 0.16666666786308587);
-    q               = __builtin_fma(q, rr, 0.5000000107729166);
-    q               = __builtin_fma(q, rr, 0.999999999995509);
-    q               = __builtin_fma(q, rr, 0.9999999999595618);
+    const double n = __builtin_rint(y * 1.4426950408889634);
+    double rr      = __builtin_fma(n, -6.93147180369123816490e-01, y);
+    rr             = __builtin_fma(n, -1.90821492927058770002e-10, rr);
+    double q       = 0.00019907569310848288;
+    q              = __builtin_fma(q, rr, 0.0013948578326459795);
+    q              = __builtin_fma(q, rr, 0.008333283538708528);
+    q              = __builtin_fma(q, rr, 0.041666218319291945);
+    q              = __builtin_fma(q, rr, 0.16666666786308587);
+    q              = __builtin_fma(q, rr, 0.5000000107729166);
+    q              = __builtin_fma(q, rr, 0.999999999995509);
+    q              = __builtin_fma(q, rr, 0.9999999999595618);
     // 2^n: y >= 64 ln(2^-149) > -6700, so n > -9700 and the scaled value underflows to +0 in
     // double (and then in float) below 2^-1074, as x^e does below f32's 2^-150
     return (float) __builtin_ldexp(q, n < -2000.0 ? -2000 : (int) n);
 }
 
-// x^e with x = |2h - 1| in [0, 1] (or NaN) for the rounding loss: the exact cases of torch's pow
-// as sleef_pow.hpp's pow01_log returns them (e == 2 / 3: ATen's x*x / x*x*x; x == 0; e == 0 or
-// x == 1: 1; a NaN result: inf), the rest powf01_f64 (the reference's scalar tail too: within
-// glibc powf's 0.82 ulp of the correctly rounded value as the vector part is within Sleef's)
-__device__ __forceinline__ float pow01_fast(float x, float e)
+// x^e for x in (0, 1), e in (0, 64]: x^e rounded from f64
+__device__ __forceinline__ float powf01_f64(float x, float e)
+{
+    return exp_ln(ln01(x), e);
+}
+
+// x^e with x = |2h - 1| in [0, 1] (or NaN) for the rounding loss, `l` = ln01(x) (any value where
+// x is 0 or 1): the exact cases of torch's pow as sleef_pow.hpp's pow01_log returns them (e == 2 /
+// 3: ATen's x*x / x*x*x; x == 0; e == 0 or x == 1: 1; a NaN result: inf), the rest exp_ln (the
+// reference's scalar tail too: within glibc powf's 0.82 ulp of the correctly rounded value as the
+// vector part is within Sleef's)
+__device__ __forceinline__ float pow01_fast_l(float x, float e, double l)
 {
     if (e == 2.0f)
         return x * x;
@@ -76,8 +88,13 @@ __device__ __forceinline__ float pow01_fast(float x, float e)
         return e == 0.0f ? 1.0f : 0.0f;
     if (e == 0.0f || x == 1.0f)
         return 1.0f;
-    const float r = powf01_f64(x, e);
+    const float r = exp_ln(l, e);
     return r != r ? __builtin_inff() : r;
+}
+
+__device__ __forceinline__ float pow01_fast(float x, float e)
+{
+    return pow01_fast_l(x, e, ln01(x));
 }
 
 }   // namespace

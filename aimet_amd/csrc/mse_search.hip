@@ -278,8 +278,9 @@ struct MseJob
     TqDevice d;
     int64_t C;
     int splits;
-    int64_t wstart;   // first work item (channel x slice) of this job
-    int64_t cstart;   // first channel of this job
+    int64_t wstart;            // first work item (channel x slice) of this job
+    int64_t cstart;            // first channel of this job
+    aimet_tf_encoding* flat;   // optional: the encodings of every job concatenated (+ cstart)
 };
 
 __device__ __forceinline__ int job_of(const MseJob* jobs, int njobs, int64_t g, bool by_channel)
@@ -308,7 +309,8 @@ __global__ __launch_bounds__(kBlock) void mse_search_many_kernel(const MseJob* _
 }
 
 // fold the slices of every channel (in candidate order) and write the encodings
-__device__ void finish_channel(const TqDevice& d, int64_t c, int splits, int bw, int sym, int strict, int unsign)
+__device__ void finish_channel(const TqDevice& d, int64_t c, int splits, int bw, int sym, int strict, int unsign,
+                               aimet_tf_encoding* flat = nullptr)
 {
     if (!d.pdf_init[c])
     {
@@ -325,6 +327,8 @@ __device__ void finish_channel(const TqDevice& d, int64_t c, int splits, int bw,
         e.max    = e.min + isteps * e.delta;
         e.bw     = bw;
         d.enc[c] = e;
+        if (flat)
+            flat[c] = e;
         return;
     }
     const MsePart* parts = reinterpret_cast<const MsePart*>(d.search_part) + c * splits;
@@ -338,7 +342,10 @@ __device__ void finish_channel(const TqDevice& d, int64_t c, int splits, int bw,
             blo = parts[y].lo;
             bhi = parts[y].hi;
         }
-    d.enc[c] = mse::finish(bw, blo, bhi, sym != 0, strict != 0, unsign != 0);
+    const aimet_tf_encoding e = mse::finish(bw, blo, bhi, sym != 0, strict != 0, unsign != 0);
+    d.enc[c] = e;
+    if (flat)
+        flat[c] = e;
 }
 
 __global__ __launch_bounds__(kBlock) void mse_finish_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
@@ -356,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void mse_finish_many_kernel(const MseJob* _
     if (g >= total)
         return;
     const MseJob& j = jobs[job_of(jobs, njobs, g, true)];
-    finish_channel(j.d, g - j.cstart, j.splits, bw, sym, strict, unsign);
+    finish_channel(j.d, g - j.cstart, j.splits, bw, sym, strict, unsign, j.flat ? j.flat + j.cstart : nullptr);
 }
 
 }   // namespace
@@ -377,16 +384,22 @@ int mse_splits(int64_t C)
 }   // namespace
 
 void launch_mse_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
-                            bool unsign, hipStream_t s)
+                            bool unsign, hipStream_t s, aimet_tf_encoding* pinned_dst)
 {
     if (n == 0)
         return;
     std::vector<MseJob> jobs((size_t) n);
     int64_t work = 0, chans = 0;
     for (int i = 0; i < n; ++i)
+        chans += Cs[i];
+    // the encodings of every quantizer side by side, for one copy into the caller's pinned block
+    auto* flat = pinned_dst ? static_cast<aimet_tf_encoding*>(scratch_alloc(sizeof(aimet_tf_encoding) * chans, s))
+                            : nullptr;
+    chans = 0;
+    for (int i = 0; i < n; ++i)
     {
         const int splits = mse_splits(Cs[i]);
-        jobs[(size_t) i] = MseJob {*ds[i], Cs[i], splits, work, chans};
+        jobs[(size_t) i] = MseJob {*ds[i], Cs[i], splits, work, chans, flat};
         work += Cs[i] * splits;
         chans += Cs[i];
     }
@@ -398,6 +411,11 @@ void launch_mse_search_many(const TqDevice* const* ds, const int64_t* Cs, int n,
                                                                                  strict ? 1 : 0, unsign ? 1 : 0);
     AIMET_LAUNCH_CHECK();
     scratch_free(dj, s);
+    if (flat)
+    {
+        AIMET_HIP_CHECK(hipMemcpyAsync(pinned_dst, flat, sizeof(aimet_tf_encoding) * chans, hipMemcpyDeviceToHost, s));
+        scratch_free(flat, s);
+    }
 }
 
 void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s)

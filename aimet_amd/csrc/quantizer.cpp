@@ -711,14 +711,16 @@ struct HostStats
     bool host_search = false;        // some channel still needs the host KL search
 };
 
-bool fetch_stats(aimet_tensor_quantizer* q, int32_t b, aimet_tf_encoding* out, HostStats& h)
+bool fetch_stats(aimet_tensor_quantizer* q, int32_t b, aimet_tf_encoding* out, HostStats& h,
+                 const EntropyRange* ranges = nullptr)
 {
     const int64_t C = q->C;
     h.q   = q;
     h.out = out;
     if (entropy_device(q, b))
     {
-        h.ent = d2h(entropy_ranges(q->d), C);
+        // the ranges of a batched request arrive in its pinned block; else read them back here
+        h.ent = ranges ? std::vector<EntropyRange>(ranges, ranges + C) : d2h(entropy_ranges(q->d), C);
         for (const EntropyRange& r: h.ent)
             h.host_search = h.host_search || r.status == kEntHost;
         if (h.host_search)
@@ -774,14 +776,14 @@ void host_encoding(const HostStats& h, int64_t c, int32_t b, int sym, int strict
 // the host-finished encodings of every (quantizer, channel) in one thread pool: the entropy KL
 // search is ~3 ms per channel, so a model's per-tensor entropy quantizers run in parallel too
 void collect_encodings(aimet_tensor_quantizer* const* qs, aimet_tf_encoding* const* outs, int64_t n, int32_t b,
-                       int sym, int strict, int unsign)
+                       int sym, int strict, int unsign, const EntropyRange* const* ranges = nullptr)
 {
     std::vector<HostStats> hs;
     hs.reserve((size_t) n);
     for (int64_t i = 0; i < n; ++i)
     {
         HostStats h;
-        if (fetch_stats(qs[i], b, outs[i], h))
+        if (fetch_stats(qs[i], b, outs[i], h, ranges ? ranges[i] : nullptr))
             hs.push_back(std::move(h));
     }
     std::vector<std::pair<int32_t, int64_t>> tasks;
@@ -904,6 +906,8 @@ void aimet_amd::release_request(aimet_encoding_request* r)
         std::lock_guard<std::mutex> lock(p.m);
         if (r->pinned && !r->pinned_borrowed)
             p.blocks.emplace_back(r->pinned, r->pinned_bytes);
+        if (r->pinned_dev)
+            p.blocks.emplace_back(r->pinned_dev, r->pinned_dev_bytes);
         if (r->done)
             p.events.push_back(r->done);
     }
@@ -919,7 +923,7 @@ void aimet_amd::release_request_after_error(aimet_encoding_request* r)
 {
     if (r == nullptr)
         return;
-    if (r->pinned)
+    if (r->pinned || r->pinned_dev)
     {
         DeviceGuard g(r->device);
         if (hipStreamSynchronize(r->stream) != hipSuccess)
@@ -927,8 +931,9 @@ void aimet_amd::release_request_after_error(aimet_encoding_request* r)
             // the stream is broken: leak the block rather than risk a live copy into a reused one
             // (a plan's block: the plan keeps counting the request as in flight, so it never
             // launches into that block again)
-            r->pinned = nullptr;
-            r->busy   = nullptr;
+            r->pinned     = nullptr;
+            r->pinned_dev = nullptr;
+            r->busy       = nullptr;
             (void) hipGetLastError();
         }
     }
@@ -980,16 +985,35 @@ aimet_encoding_request* aimet_amd::encodings_launch(aimet_tensor_quantizer* cons
         {
             ent.push_back(&q->d);
             entC.push_back(q->C);
+            req->ent_q.push_back(i);
         }
         else if (q->stats_updated && q->hist && q->scheme == AIMET_QUANTIZATION_MSE)
         {
             mse.push_back(&q->d);
             mseC.push_back(q->C);
+            req->mse_q.push_back(i);
+            req->mse_total += q->C;
         }
         off += q->C;
     }
-    launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0, st);
-    launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0, st);
+    // the MSE encodings and the entropy ranges come back in one pinned block (two copies enqueued
+    // behind the searches), not in a synchronous copy per quantizer when the request is finished
+    int64_t ent_total = 0;
+    for (int64_t c: entC)
+        ent_total += c;
+    aimet_tf_encoding* mse_dst = nullptr;
+    EntropyRange* ent_dst      = nullptr;
+    if (req->mse_total + ent_total > 0)
+    {
+        const size_t mse_bytes = sizeof(aimet_tf_encoding) * (size_t) req->mse_total;
+        req->pinned_dev = take_pinned(mse_bytes + sizeof(EntropyRange) * (size_t) ent_total, &req->pinned_dev_bytes);
+        mse_dst         = req->mse_total ? static_cast<aimet_tf_encoding*>(req->pinned_dev) : nullptr;
+        ent_dst = ent_total ? reinterpret_cast<EntropyRange*>(static_cast<char*>(req->pinned_dev) + mse_bytes) : nullptr;
+    }
+    launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0, st,
+                           mse_dst);
+    launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0, st,
+                               ent_dst);
     if (tfe_total > 0 && table != nullptr)
     {
         AIMET_REQUIRE(table->total == tfe_total && table->n == (int) tfe.size(),
@@ -1185,20 +1209,44 @@ int aimet_tq_get_encodings_finish(aimet_encoding_request* req, aimet_tf_encoding
         auto* tfe = static_cast<const aimet_tf_encoding*>(req->pinned);
         for (size_t k = 0, src = 0; k < req->tfe_Cs.size(); src += req->tfe_Cs[k], ++k)
             std::memcpy(out + req->tfe_offs[k], tfe + src, sizeof(aimet_tf_encoding) * req->tfe_Cs[k]);
+        // the device-searched MSE encodings and entropy ranges, from the request's pinned block
+        std::vector<int64_t> offs((size_t) nq);
+        for (int64_t i = 0, o = 0; i < nq; o += req->qs[(size_t) i]->C, ++i)
+            offs[(size_t) i] = o;
+        std::vector<char> from_pinned((size_t) nq, 0);
+        std::vector<const EntropyRange*> ranges((size_t) nq, nullptr);
+        {
+            auto* m = static_cast<const aimet_tf_encoding*>(req->pinned_dev);
+            for (int64_t i: req->mse_q)
+            {
+                const int64_t C = req->qs[(size_t) i]->C;
+                std::memcpy(out + offs[(size_t) i], m, sizeof(aimet_tf_encoding) * C);
+                m += C;
+                from_pinned[(size_t) i] = 1;
+            }
+            auto* r = reinterpret_cast<const EntropyRange*>(static_cast<const char*>(req->pinned_dev) +
+                                                            sizeof(aimet_tf_encoding) * (size_t) req->mse_total);
+            for (int64_t i: req->ent_q)
+            {
+                ranges[(size_t) i] = r;
+                r += req->qs[(size_t) i]->C;
+            }
+        }
         std::vector<aimet_tensor_quantizer*> host_q;
         std::vector<aimet_tf_encoding*> host_out;
-        int64_t off = 0;
-        for (aimet_tensor_quantizer* q: req->qs)
+        std::vector<const EntropyRange*> host_ranges;
+        for (int64_t i = 0; i < nq; ++i)
         {
-            if (q->stats_updated && !(q->hist && q->scheme == AIMET_QUANTIZATION_TF_ENHANCED))
+            aimet_tensor_quantizer* q = req->qs[(size_t) i];
+            if (q->stats_updated && !(q->hist && q->scheme == AIMET_QUANTIZATION_TF_ENHANCED) && !from_pinned[(size_t) i])
             {
                 host_q.push_back(q);
-                host_out.push_back(out + off);
+                host_out.push_back(out + offs[(size_t) i]);
+                host_ranges.push_back(ranges[(size_t) i]);
             }
-            off += q->C;
         }
         collect_encodings(host_q.data(), host_out.data(), (int64_t) host_q.size(), req->b, req->sym, req->strict,
-                          req->unsign);
+                          req->unsign, host_ranges.data());
     });
     if (rc != AIMET_OK)
         release_request_after_error(req);   // the copy may not have been waited for

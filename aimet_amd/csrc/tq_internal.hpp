@@ -40,6 +40,12 @@ struct aimet_encoding_request
     bool pinned_borrowed = false;   // a calibration plan's block: not returned to the pool
     int* busy = nullptr;            // a calibration plan's in-flight count, decremented on release
     std::vector<int64_t> tfe_offs, tfe_Cs;   // per TF-E quantizer: offset in `out`, channels
+    // the MSE encodings and the entropy KL ranges of the device searches, copied into one pinned
+    // block of their own (MSE encodings first, then the ranges); per quantizer its index in qs
+    void* pinned_dev        = nullptr;
+    size_t pinned_dev_bytes = 0;
+    std::vector<int64_t> mse_q, ent_q;
+    int64_t mse_total = 0;
 };
 
 namespace aimet_amd

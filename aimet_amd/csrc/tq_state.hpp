@@ -174,9 +174,10 @@ void stream_join(hipStream_t waiter, hipStream_t from);
 // mse_search.hip: d.enc[c] <- MSE encoding of channel c (statistics updated)
 size_t mse_part_bytes(int64_t C);
 void launch_mse_search(const TqDevice& d, int64_t C, int bw, bool sym, bool strict, bool unsign, hipStream_t s);
-// the same for n quantizers in one launch (+ one fold launch)
+// the same for n quantizers in one launch (+ one fold launch); pinned_dst (optional, host-pinned,
+// sum of Cs entries): the encodings concatenated, copied there on s (the caller synchronises)
 void launch_mse_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, int bw, bool sym, bool strict,
-                            bool unsign, hipStream_t s);
+                            bool unsign, hipStream_t s, aimet_tf_encoding* pinned_dst = nullptr);
 
 // entropy_search.hip: the KL range of every channel of an 8-bit entropy getEncoding, written over
 // the first 16 B per channel of d.enc (the quantizer's encoding scratch, 40 B per channel)
@@ -197,7 +198,8 @@ inline EntropyRange* entropy_ranges(const TqDevice& d)
 {
     return reinterpret_cast<EntropyRange*>(d.enc);
 }
+// pinned_dst (optional, host-pinned, sum of Cs entries): the ranges concatenated, copied there on s
 void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, bool sym, bool strict, bool unsign,
-                                hipStream_t s);
+                                hipStream_t s, EntropyRange* pinned_dst = nullptr);
 
 }   // namespace aimet_amd

@@ -13,6 +13,13 @@ Multi-GPU: one process per GPU (torch.distributed, RCCL). Each rank runs its own
 scaling, no data-path collective); calibration is sharded per sample across ranks with one RCCL
 exchange of the packed statistics per batch (aimet_amd.distributed).
 
+At N=1 the line also carries BASELINE configs 3 and 5 (`secondary`), each run by its own benchmark
+in a child process after the headline (benchmarks/adaround_mobilenet.py: MobileNet-v2 AdaRound, all
+53 layers x 10k iterations; benchmarks/llama_qat.py: Llama-3-8B W4A16 QAT at seq 2048, mb 1, full
+model, beside the same step without quantizers), within a time budget that keeps the whole run
+inside the driver's limit; a config that fails or does not fit is recorded as such in the line.
+The process that launches them never touches the GPU (the headline runs in a child too).
+
 Prints ONE JSON line on rank 0.
 """
 import argparse
@@ -60,6 +67,10 @@ def parse():
     p.add_argument("--no-dropin", action="store_true",
                    help="skip the drop-in surface timings (QuantizationSimModel.compute_encodings of config 1, "
                         "the StaticGridQuantWrapper forward of config 2)")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="skip BASELINE configs 3 and 5 (run at N=1 after the headline, in child processes)")
+    p.add_argument("--secondary-budget", type=float, default=480.0,
+                   help="seconds from the start of bench.py by which the secondary configs must end")
     p.add_argument("--force-exchange", action="store_true",
                    help="at N=1 form a world-size-1 RCCL group before any GPU call and time the sharded "
                         "calibration's staged form (both packed collectives through RCCL) beside the headline")
@@ -428,11 +439,80 @@ def _max_over_ranks(v, dev):
     return float(t.item())
 
 
+def _run_child(cmd, timeout, env=None):
+    """One child benchmark: (its last JSON line or None, a note on failure)."""
+    try:
+        r = subprocess.run(cmd, stdout=subprocess.PIPE, timeout=timeout, env=env, cwd=REPO)
+    except subprocess.TimeoutExpired:
+        return None, "timed out after %.0f s" % timeout
+    lines = [ln for ln in r.stdout.decode(errors="replace").splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return None, "exit status %d" % r.returncode
+    try:
+        return json.loads(lines[-1]), None
+    except ValueError as e:
+        return None, "unparsable line: %s" % e
+
+
+def secondary_configs(t_start, budget):
+    """BASELINE configs 3 and 5, each in a child process (its own GPU memory), in the time left of
+    `budget` seconds since t_start; what ran, what failed and what did not fit."""
+    out = {"budget_s": budget}
+    runs = [
+        # the AdaRound backward kernel alone at 2^28 elements, N(0, 1) alpha (its roofline line)
+        ("adaround_backward_kernel_2p28", [sys.executable, "tools/studies/ada_bwd_tune.py", "--scales", "1",
+                                           "--tag", "bench"], 20.0),
+        ("config3_adaround_mobilenet_v2", [sys.executable, "benchmarks/adaround_mobilenet.py"], 150.0),
+        ("config5_llama3_8b_w4a16_qat", [sys.executable, "benchmarks/llama_qat.py"], 150.0),
+        ("config5_llama3_8b_no_quantizer", [sys.executable, "benchmarks/llama_qat.py", "--path", "plain"], 120.0),
+    ]
+    for key, cmd, need in runs:
+        left = budget - (time.perf_counter() - t_start)
+        if left < need:
+            out[key] = {"skipped": "%.0f s of the budget left, %.0f s needed" % (left, need)}
+            continue
+        t0 = time.perf_counter()
+        res, err = _run_child(cmd, timeout=left)
+        wall = round(time.perf_counter() - t0, 1)
+        out[key] = dict(res, child_wall_s=wall) if res is not None else {"error": err, "child_wall_s": wall}
+    c3, c5, c5p = (out.get(k, {}) for k in ("config3_adaround_mobilenet_v2", "config5_llama3_8b_w4a16_qat",
+                                             "config5_llama3_8b_no_quantizer"))
+    if "value" in c3:
+        out["config3_adaround_s"] = c3["value"]
+    kb = out.get("adaround_backward_kernel_2p28", {})
+    if "achieved_GBps" in kb:   # the last line: the loop's form, without the loss value
+        out["adaround_bwd_GBps"] = kb["achieved_GBps"]
+        out["adaround_bwd_frac_of_8TBps"] = kb["frac_of_peak"]
+    if "ms_per_step" in c5:
+        out["config5_qat_ms_per_step"] = c5["ms_per_step"]
+        if "ms_per_step" in c5p:
+            out["config5_no_quantizer_ms_per_step"] = c5p["ms_per_step"]
+            out["config5_quantizer_ms_per_step"] = round(c5["ms_per_step"] - c5p["ms_per_step"], 2)
+    return out
+
+
+def orchestrate(args):
+    """N=1 with the secondary configs: the headline bench in a child (this process never touches
+    the GPU), then configs 3 and 5; one merged JSON line."""
+    t_start = time.perf_counter()
+    env = dict(os.environ, AIMET_BENCH_CHILD="1")
+    res, err = _run_child([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], timeout=None, env=env)
+    if res is None:
+        print("bench.py: the headline run failed (%s)" % err, file=sys.stderr)
+        return 1
+    res["secondary"] = secondary_configs(t_start, args.secondary_budget)
+    print(json.dumps(res), flush=True)
+    return 0
+
+
 def main():
     args = parse()
     world_env = os.environ.get("WORLD_SIZE")
     if world_env is None and args.gpus > 1:
         sys.exit(spawn_ranks(args.gpus))
+    if (world_env is None and args.gpus == 1 and not args.no_secondary and not os.environ.get("AIMET_BENCH_CHILD")
+            and not os.environ.get("AIMET_BENCH_LAUNCH_CHECK")):
+        sys.exit(orchestrate(args))
     if os.environ.get("AIMET_BENCH_LAUNCH_CHECK"):
         return launch_check(int(world_env or 1), int(os.environ.get("RANK", "0")))
     rank, world, dev = setup_dist(args)

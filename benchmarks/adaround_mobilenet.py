@@ -36,6 +36,8 @@ def main():
                     help="launch every iteration from Python instead of replaying one captured HIP graph")
     ap.add_argument("--reference-iters", type=int, default=0,
                     help="also time N iterations per layer of the torch-op reference loop")
+    ap.add_argument("--exact-pow", action="store_true",
+                    help="the rounding loss's bit-exact emulation of torch's pow (default: the f64 pow, within 1 ulp)")
     ap.add_argument("--miopen-find", action="store_true",
                     help="torch.backends.cudnn.benchmark: MIOpen benchmarks its convolution solvers per shape "
                          "(a fresh box has no find database; immediate mode may fall back to naive kernels)")
@@ -43,7 +45,7 @@ def main():
     if args.miopen_find:
         torch.backends.cudnn.benchmark = True
 
-    from aimet_amd.adaround import AdaroundFunction, compute_beta, init_alpha
+    from aimet_amd.adaround import AdaroundFunction, compute_beta, init_alpha, set_exact_pow
     from aimet_amd.adaround_optimizer import (AdaroundHyperParameters, AdaroundOptimizer, layer_forward,
                                               recon_loss)
     from aimet_amd.libpymo import QuantizationMode
@@ -51,6 +53,7 @@ def main():
     from workloads.mobilenet_v2 import mobilenet_v2
 
     dev = torch.device("cuda", 0)
+    set_exact_pow(args.exact_pow)
     fp = mobilenet_v2(seed=0, device=dev)
     qm = mobilenet_v2(seed=0, device=dev)     # receives the adarounded weights layer by layer
     images = torch.rand(args.images, 3, 224, 224, generator=torch.Generator().manual_seed(7)).to(dev)
@@ -144,6 +147,7 @@ def main():
         "ms_per_iteration": round(t_opt / iters * 1e3, 4), "activation_caching_s": round(t_cache, 3),
         "loop": "eager" if args.eager else "hipgraph (one captured iteration replayed per iteration)",
         "miopen_find": bool(args.miopen_find),
+        "rounding_loss_pow": "exact (torch's CPU pow, bit for bit)" if args.exact_pow else "f64 (within 1 ulp of torch's)",
         "weights_elems": sum(int(torch.Size(p[1]).numel()) for p in per_layer),
         "kernel_split": "per-kernel time of the loop: rocprofv3 --kernel-trace + tools/studies/ada_trace_summary.py "
                         "(profiles/r02/adaround_loop_kernels_*.csv)",

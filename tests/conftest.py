@@ -22,6 +22,16 @@ def gpu_available():
         return False
 
 
+@pytest.fixture(params=[True, False], ids=["exact_pow", "f64_pow"])
+def exact_pow(request):
+    """Both forms of the AdaRound rounding loss's pow (aimet_amd.adaround.set_exact_pow): the
+    bit-exact emulation of torch's CPU pow and the default f64 pow."""
+    from aimet_amd.adaround import set_exact_pow
+    prev = set_exact_pow(request.param)
+    yield request.param
+    set_exact_pow(prev)
+
+
 @pytest.fixture(scope="session")
 def golden_dir():
     return os.path.join(REPO, "tests", "golden")

@@ -472,10 +472,10 @@ def test_adaround_backward_with_round_loss_vs_torch(beta, shape):
 @pytest.mark.parametrize("beta", [3.0, 4.0, 7.25, 20.0])   # beta - 1 = 2 / 3: x*x / x*x*x (no logarithm)
 @pytest.mark.parametrize("want_loss", [False, True])
 @pytest.mark.parametrize("n, C", [(1 << 19, 64), ((1 << 19) + 16, 1)])   # n % 32 == 16: the scalar pow tail
-def test_adaround_backward_dense_waves_equal_compacted(beta, want_loss, n, C):
+def test_adaround_backward_dense_waves_equal_compacted(beta, want_loss, n, C, exact_pow):
     """The fused backward evaluates the rounding-loss pows of a dense wave (>= 3/4 of its elements
-    need the logarithm) in place, two at a time in packed f32, and those of a sparse wave compacted
-    through LDS with the scalar arithmetic (adaround.hip / sleef_pow.hpp: ada_round_pows). The same
+    need the logarithm) in place (the exact pow two at a time in packed f32) and those of a sparse
+    wave compacted through LDS (adaround.hip: ada_round_pows), in either pow form. The same
     element must give the same bits either way: run A has every alpha unsaturated (dense waves),
     run B saturates 3 of every 4 quads (sparse waves), and the unsaturated quads' gradients of the
     two runs are compared bit for bit."""
@@ -508,7 +508,7 @@ def test_adaround_backward_dense_waves_equal_compacted(beta, want_loss, n, C):
 
 @pytest.mark.parametrize("reg", [0.0, 0.01])
 @pytest.mark.parametrize("n, C", [(3 << 22, 96), ((3 << 22) + 16, 1)])   # n % 32 == 16: the scalar pow tail
-def test_adaround_backward_grid_forms_equal(reg, n, C):
+def test_adaround_backward_grid_forms_equal(reg, n, C, exact_pow):
     """Above 8192 workgroups' worth of quads the backward without the loss value runs one tile per
     workgroup, with it a grid-stride loop over 8192 workgroups (adaround.hip: adaround_backward).
     Both forms must give the same gradient bits; 12.6 M elements (1.5 x the bounded grid's tile)."""

@@ -55,6 +55,9 @@ def main():
             return r
         return w
     QS.compute_encodings_batched = timed("encodings_batched", orig_batched)
+    others = {n: getattr(QS, n) for n in ("_reset_many", "_precompute_param_encodings", "_forget_unused_param_encodings")}
+    for n, fn in others.items():
+        setattr(QS, n, timed(n.strip("_"), fn))
     cal_timed = timed("analysis_forwards", calibrate)
     for _ in range(args.reps + 1):
         torch.cuda.synchronize()
@@ -66,6 +69,8 @@ def main():
     for _ in range(args.reps + 1):
         plain(model, None)
     QS.compute_encodings_batched = orig_batched
+    for n, fn in others.items():
+        setattr(QS, n, fn)
     for k, v in phases.items():
         v = v[1:]
         print("%-20s median %.2f ms  runs %s" % (k, sorted(v)[len(v) // 2], [round(x, 2) for x in v]))
