@@ -13,10 +13,10 @@
 // IEEE operation in the same order, and the sigmoid is torch's own vectorized CPU sigmoid
 // (1 / (1 + expf(-a)) with Sleef's expf_u10 polynomial, FMA form, then an IEEE divide), so Wq is
 // bit-identical to the reference (tests/golden/golden_adaround.npz). The rounding loss's
-// pow(|2h-1|, beta) / pow(|2h-1|, beta-1) is, by default, the f64 pow of fast_pow.hpp: within
-// 1 ulp of torch's CPU pow (Sleef powf_u10) for every f32 |2h-1| in (0, 1) and every exponent of
-// the AdaRound schedules (profiles/r06/pow_fast_check.txt), at ~30 f64 instructions instead of
-// Sleef's ~142 f32 ones. aimet_adaround_set_exact_pow(1) selects the bit-exact emulation of
+// pow(|2h-1|, beta) / pow(|2h-1|, beta-1) is, by default, the table-driven f32 pow of
+// fast_pow.hpp: within 1 ulp of torch's CPU pow (Sleef powf_u10) for every f32 |2h-1| in (0, 1)
+// and every exponent of the AdaRound schedules (profiles/r06/pow_fast_check.txt), at ~33 f32
+// instructions and 5 LDS reads instead of Sleef's ~142 f32 instructions. aimet_adaround_set_exact_pow(1) selects the bit-exact emulation of
 // torch's pow instead (sleef_pow.hpp: Sleef powf_u10 in the vectorized part, the scalar tail as
 // std::pow), with which dL/dalpha, the rounding-loss term included, is bit-identical too.
 #include "common.hpp"
@@ -179,7 +179,7 @@ __device__ __forceinline__ float ada_bwd_round(float ga, float sg, float x, bool
 
 // dL/dalpha of Wq + the rounding-loss gradient, one element (the loss term added to `loss`).
 // EXACT: the rounding loss's pow is the bit-exact emulation of torch's (sleef_pow.hpp), else the
-// f64 pow (fast_pow.hpp, within 1 ulp of it)
+// fast pow (fast_pow.hpp, within 1 ulp of it; its tables filled into LDS by the kernel)
 template <bool EXACT>
 __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, float o, const AdaParams& p, float rcp,
                                          float& loss, uint32_t idx)
@@ -209,7 +209,7 @@ __device__ __forceinline__ float ada_bwd(float w, float a, float g, float d, flo
             }
             else
             {
-                double l = 0.0;
+                LnSplit l {0.0f, 0.0f};
                 if (!(ax == 0.0f || ax == 1.0f))
                     l = ln01(ax);
                 if (p.want_loss)
@@ -269,14 +269,14 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
     }
     if (!EXACT && 4 * total >= 3 * 64 * E)
     {
-        // a dense wave: each lane evaluates its own elements in place with the f64 pow (its
+        // a dense wave: each lane evaluates its own elements in place with the fast pow (its
         // logarithm shared by the two exponents; the scalar tail takes it too: fast_pow.hpp)
 #pragma unroll
         for (int k = 0; k < E; ++k)
         {
             if (need[k])
             {
-                const double l = ln01(ax[k]);
+                const LnSplit l = ln01(ax[k]);
                 pbm1[k]        = pow01_fast_l(ax[k], p.beta_m1, l);
                 pb[k]          = p.want_loss ? pow01_fast_l(ax[k], p.beta, l) : 0.0f;
             }
@@ -370,7 +370,7 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
         }
         else
         {
-            const double l = ln01(v);
+            const LnSplit l = ln01(v);
             wl[j]          = pow01_fast_l(v, p.beta_m1, l);
             if (p.want_loss)
                 wl1[j] = pow01_fast_l(v, p.beta, l);
@@ -542,6 +542,11 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
     float* wl             = lds[threadIdx.x >> 6];
     float loss            = 0.0f;
     const uint32_t stride = gridDim.x * kBlock * U;
+    // the fast pow's tables: their loads first, the LDS copy after the first tile's loads are issued
+    PowTabPart<kBlock> tab;
+    if constexpr (!EXACT)
+        tab = pow_tab_load<kBlock>();
+    bool first = true;
     for (uint32_t tile = blockIdx.x * kBlock * U; tile < nq; tile += stride)
     {
         const uint32_t base = tile + threadIdx.x;
@@ -554,6 +559,12 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
             wv[u] = __builtin_nontemporal_load(w + j);
             av[u] = __builtin_nontemporal_load(alpha + j);
             gv[u] = __builtin_nontemporal_load(g + j);
+        }
+        if (!EXACT && first)   // uniform over the workgroup
+        {
+            pow_tab_store<kBlock>(tab);
+            __syncthreads();
+            first = false;
         }
         float r[E], sg[E], x[E], ax[E];
         bool in_h[E], tail[E], valid[E];
@@ -616,6 +627,11 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_kernel(const float* __res
         p.reg     = reg_beta[0];
         p.beta    = reg_beta[1];
         p.beta_m1 = reg_beta[2];
+    }
+    if constexpr (!EXACT)
+    {
+        pow_tab_fill<kBlock>();
+        __syncthreads();
     }
     float loss = 0.0f;
     for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
@@ -681,7 +697,7 @@ bool aligned16(const void* p)
     return (reinterpret_cast<uintptr_t>(p) & 15) == 0;
 }
 
-// the rounding loss's pow for launches from now on: the f64 pow (0, default) or the bit-exact
+// the rounding loss's pow for launches from now on: the fast pow (0, default) or the bit-exact
 // emulation of torch's (1); aimet_adaround_set_exact_pow
 std::atomic<int>& exact_pow_flag()
 {
@@ -755,6 +771,10 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
                                                                    uint32_t part_kk)
 {
     p.want_loss = WL;   // constant: see adaround_bwd_vec_kernel
+    // the fast pow's tables: loaded first, copied into LDS once the step's operands are in flight
+    PowTabPart<kBlock> tab;
+    if constexpr (!EXACT)
+        tab = pow_tab_load<kBlock>();
     // the one-element-per-lane form's first element: its operands are loaded before the step's
     // table entries, which they do not depend on, so the two round trips overlap (a small layer's
     // step is a chain of latencies: the counter, the table entries, the operands, the arithmetic)
@@ -800,6 +820,11 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_adam_kernel(const float* 
     }
     else
         adam_bias_corrections(adam.beta1, adam.beta2, step, bc1, bc2s);
+    if constexpr (!EXACT)
+    {
+        pow_tab_store<kBlock>(tab);
+        __syncthreads();
+    }
     float loss         = 0.0f;
     if (VEC)
     {
@@ -1167,7 +1192,7 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
                     reinterpret_cast<const f4*>(w), reinterpret_cast<const f4*>(alpha), reinterpret_cast<const f4*>(g),
                     reinterpret_cast<f4*>(ga), nq, map, delta, offset, p, round_loss, reg_beta, lf.part, lf.ticket);
             };
-            // the scalar pow tail exists only for the exact pow (the f64 pow takes every element alike)
+            // the scalar pow tail exists only for the exact pow (the fast pow takes every element alike)
             const bool wl = p.want_loss != 0, ex = exact_pow(), tl = ex && n % 32 != 0;
             // (a form compiled for 8 waves per SIMD spilled and measured slower:
             // profiles/r04/ada_bwd_tune_occ8.jsonl)
@@ -1432,7 +1457,7 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
                                                          (uint32_t) part_kk);
         };
         const bool wl = round_loss != nullptr;
-        if (!exact_pow())   // the f64 pow: no scalar pow tail
+        if (!exact_pow())   // the fast pow: no scalar pow tail
         {
             if (vec)
                 wl ? launch(adaround_bwd_adam_kernel<true, true, false, false>)

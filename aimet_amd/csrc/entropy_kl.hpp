@@ -109,9 +109,9 @@ AIMET_ENT_HD void kl_histogram(double tmin, double tmax, const double* tpp_hist,
 // Returns the count (kWindows); wa/wb[k] = the inclusive bounds of window k.
 AIMET_ENT_HD int windows(const double* hist, double lo, double w, bool both_ends, short* wa, short* wb)
 {
-    uint64_t a = 0, b = kBins - 1;
-    int n      = 0;
-    while (b - a + 1 >= (uint64_t) kLevels)
+    int a = 0, b = kBins - 1;   // the reference's size_t indices: the same values, converted to double exactly
+    int n = 0;
+    while (b - a + 1 >= kLevels)
     {
         wa[n] = (short) a;
         wb[n] = (short) b;

@@ -56,8 +56,73 @@ struct WinState
     int brk;                  // the reference loop stops at this window (P or Q sums to 0)
 };
 
-// step 2 for window [a, b] with the prefix tables (q_zero_rule holds: integral histograms) or
-// without them (two streamed passes, as entropy::window_kl)
+// a level's Q where its bins are non-empty: the reference's sum / norm, exactly (norm 1 and 2 --
+// nearly every level of a window of 256-512 bins over 255 levels -- without the division)
+__device__ __forceinline__ double level_q(double sum, double norm)
+{
+    return norm == 1.0 ? sum : (norm == 2.0 ? sum * 0.5 : sum / norm);
+}
+
+// [i0, i1) of level q of a window of `win` bins (stream_pq's bounds: ceil of the double products)
+__device__ __forceinline__ int level_end(int q, double merged, int win)
+{
+    return q < entropy::kLevels - 1 ? (int) __builtin_ceil((double) (q + 1) * merged) : win;
+}
+
+// step 2 for window [a, b] of an integral histogram (every bin an integer below 2^43, so every
+// sum of bins is exact in any order): the float normalisers of the conditioned P and Q in the
+// reference's bin order (exact: the same float / double operations), with the level sums, the
+// zero counts and the right-hand saturation from the prefix tables, and whether the reference
+// loop stops here (the float sums of P or Q are 0 exactly when every bin of P or Q is 0)
+__device__ void window_norms_integral(const double* hist, int a, int b, const entropy::Prefix& pre, WinState& st)
+{
+    using namespace entropy;
+    const int win       = b - a + 1;
+    const double total  = pre.left[kBins - 1];
+    const double left   = pre.left[a];
+    const double right  = total - (b > 0 ? pre.left[b - 1] : 0.0);
+    const uint64_t zP   = (uint64_t) (pre.zeros[b] - pre.zeros[a + 1]) + (left == 0.0) + (right == 0.0);
+    const uint64_t zQ   = (uint64_t) (pre.zeros[b + 1] - pre.zeros[a]);
+    const Cond cP = cond_of(zP, (uint64_t) win), cQ = cond_of(zQ, (uint64_t) win);
+    const double merged = (double) win / (double) kLevels;
+    auto lsum = [&](int i) { return a + i > 0 ? pre.left[a + i - 1] : 0.0; };   // hist[0, a + i)
+    float sP = 0.f, sQ = 0.f;
+    int q = 0, i0 = 0, i1 = level_end(0, merged, win);
+    double qv = 0.0;
+    bool qnz  = false;
+    for (int i = 0; i < win; ++i)
+    {
+        if (i == 0 || i == i1)
+        {
+            if (i != 0)
+            {
+                ++q;
+                i0 = i1;
+                i1 = level_end(q, merged, win);
+            }
+            const double norm = (double) ((i1 - i0) - (pre.zeros[a + i1] - pre.zeros[a + i0]));
+            qnz               = norm != 0;
+            qv                = qnz ? level_q(lsum(i1) - lsum(i0), norm) : 0.0;
+        }
+        const double h  = hist[a + i];
+        const double Qi = (qnz && h != 0) ? qv : 0.0;
+        const double Pi = i == 0 ? 0.0 + left : (i == win - 1 ? 0.0 + right : h);
+        sP              = (float) ((double) sP + cond_apply(cP, Pi));
+        sQ              = (float) ((double) sQ + cond_apply(cQ, Qi));
+    }
+    st.left  = left;
+    st.right = right;
+    st.cP    = cP;
+    st.cQ    = cQ;
+    st.brk   = (zP == (uint64_t) win || zQ == (uint64_t) win) ? 1 : 0;
+    const double dP = sP, dQ = sQ;
+    st.rdP = 1.0 / dP;
+    st.rdQ = 1.0 / dQ;
+    st.rqz = 1.0 / (cond_apply(cQ, 0.0) * st.rdQ);
+}
+
+// step 2 for window [a, b] without the integral tables' shortcuts (lane per window, two streamed
+// passes, as entropy::window_kl)
 __device__ void window_norms(const double* hist, int a, int b, const entropy::Prefix* pre, WinState& st)
 {
     using namespace entropy;
@@ -115,8 +180,8 @@ __device__ void window_norms(const double* hist, int a, int b, const entropy::Pr
 
 // step 3: the divergence terms of levels [q0, q1) of window [a, b] (entropy::stream_pq's levels),
 // p = cond(P) / dP, q = cond(Q) / dQ, sum of p log(p / q) over p, q > 0, and of its magnitudes
-__device__ void window_segment(const double* hist, int a, int b, int q0, int q1, const WinState& st, double& dv,
-                               double& mag)
+__device__ void window_segment(const double* hist, int a, int b, int q0, int q1, const WinState& st,
+                               const entropy::Prefix& pre, bool integral, double& dv, double& mag)
 {
     using namespace entropy;
     const int win       = b - a + 1;
@@ -125,22 +190,32 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
     const double qz     = cond_apply(st.cQ, 0.0) * st.rdQ;
     dv = 0;
     mag = 0;
+    int i1 = (int) (uint64_t) ceil((double) q0 * merged);
     for (int q = q0; q < q1; ++q)
     {
-        const int i0 = (int) (uint64_t) ceil((double) q * merged);
-        const int i1 = q < kLevels - 1 ? (int) (uint64_t) ceil((double) (q + 1) * merged) : win;
+        const int i0 = i1;
+        i1           = level_end(q, merged, win);
         double sum = 0, norm = 0;
-        for (int i = i0; i < i1; ++i)
+        if (integral)   // integral bins: the level's sum and non-empty count from the tables (exact)
         {
-            sum += hw[i];
-            norm += (hw[i] != 0);
+            sum  = (pre.left[a + i1 - 1] - (a + i0 > 0 ? pre.left[a + i0 - 1] : 0.0));
+            norm = (double) ((i1 - i0) - (pre.zeros[a + i1] - pre.zeros[a + i0]));
         }
-        // the level's Q where its bin is non-empty (the reference's sum / norm, per bin)
+        else
+            for (int i = i0; i < i1; ++i)
+            {
+                sum += hw[i];
+                norm += (hw[i] != 0);
+            }
+        // the level's Q where its bin is non-empty (the reference's sum / norm, per bin), and its
+        // reciprocal (v_rcp_f64 + two Newton steps: within an ulp, inside the terms' error bound)
         double qnz = 0.0, rqnz = 0.0;
         if (norm != 0)
         {
-            qnz  = cond_apply(st.cQ, sum / norm) * st.rdQ;
-            rqnz = 1.0 / qnz;
+            qnz  = cond_apply(st.cQ, level_q(sum, norm)) * st.rdQ;
+            rqnz = __builtin_amdgcn_rcp(qnz);
+            rqnz = __builtin_fma(__builtin_fma(-qnz, rqnz, 1.0), rqnz, rqnz);
+            rqnz = __builtin_fma(__builtin_fma(-qnz, rqnz, 1.0), rqnz, rqnz);
         }
         for (int i = i0; i < i1; ++i)
         {
@@ -175,6 +250,8 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
     __shared__ int zeros[entropy::kBins + 1];
     __shared__ double s_lo, s_hi;
     __shared__ int s_n, s_rule, s_integral;
+    __shared__ int s_first_brk[kEntBlock / 64], s_best_k[kEntBlock / 64], s_tie;
+    __shared__ double s_best_v[kEntBlock / 64], s_best_m;
     const int t = threadIdx.x;
     const int lane = t & 63;
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
@@ -304,11 +381,20 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
                     zeros[0] = 0;
             }
             __syncthreads();
+            if (sym || strict)   // both ends shrink by one bin per window: window n is [n, 511 - n]
+            {
+                for (int n = t; n < entropy::kWindows; n += kEntBlock)
+                {
+                    wa[n] = (short) n;
+                    wb[n] = (short) (entropy::kBins - 1 - n);
+                }
+            }
             if (t == 0)
             {
                 s_lo   = dlo;
                 s_hi   = dhi;
-                s_n    = entropy::windows(hist, dlo, (dhi - dlo) / (double) entropy::kBins, sym || strict, wa, wb);
+                s_n    = (sym || strict) ? entropy::kWindows
+                                         : entropy::windows(hist, dlo, (dhi - dlo) / (double) entropy::kBins, false, wa, wb);
                 s_rule = 1;   // integral bins: 0 or >= 1
             }
         }
@@ -327,7 +413,12 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
         // ---- 2. the normalisers of every window (exact) -----------------------------------------
         const entropy::Prefix pre {left, zeros, s_rule != 0};
         if (t < s_n)
-            window_norms(hist, wa[t], wb[t], &pre, ws[t]);
+        {
+            if (integral)
+                window_norms_integral(hist, wa[t], wb[t], pre, ws[t]);
+            else
+                window_norms(hist, wa[t], wb[t], &pre, ws[t]);
+        }
         __syncthreads();
         // ---- 3. the divergences, (window, segment) items over every lane --------------------------
         for (int it = t; it < s_n * kSegs; it += kEntBlock)
@@ -337,61 +428,82 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
             if (!ws[w].brk)
             {
                 const int q0 = sgm * kSegLev, q1 = q0 + kSegLev < entropy::kLevels ? q0 + kSegLev : entropy::kLevels;
-                window_segment(hist, wa[w], wb[w], q0, q1, ws[w], dv, mag);
+                window_segment(hist, wa[w], wb[w], q0, q1, ws[w], pre, integral, dv, mag);
             }
             part_dv[it]  = dv;
             part_mag[it] = mag;
         }
         __syncthreads();
-        // ---- 4. the first strict minimum ----------------------------------------------------------
+        // ---- 4. the first strict minimum: every window's sums on its own lane, wave reductions --
+        // the reference loop stops at the first breaking window (nv) and keeps the first strict
+        // minimum below +inf; the window is accepted only if every other one before nv exceeds it
+        // by more than the tolerance (a near-tie or a NaN: the host's glibc search decides)
+        const int wave = t >> 6;
+        double v = __builtin_inf(), m = 0.0;
+        bool brk = true;
+        if (t < s_n)
+        {
+            v = 0.0;
+            for (int sgm = 0; sgm < kSegs; ++sgm)   // the segments' sums in segment order
+            {
+                v += part_dv[t * kSegs + sgm];
+                m += part_mag[t * kSegs + sgm];
+            }
+            brk = ws[t].brk != 0;
+        }
+        const uint64_t brk_mask = __ballot(brk);
+        if (lane == 0)
+            s_first_brk[wave] = brk_mask ? wave * 64 + __ffsll((long long) brk_mask) - 1 : kEntBlock;
+        __syncthreads();
+        int nv = kEntBlock;
+        for (int k = 0; k < kEntBlock / 64; ++k)
+            nv = s_first_brk[k] < nv ? s_first_brk[k] : nv;
+        nv = nv < s_n ? nv : s_n;
+        // (value, index) argmin: the smallest value below +inf, the first index among equals
+        double bv = (t < nv && v < __builtin_inf()) ? v : __builtin_inf();
+        int bk    = bv < __builtin_inf() ? t : kEntBlock;
+        for (int o = 32; o > 0; o >>= 1)
+        {
+            const double ov = __shfl_xor(bv, o, 64);
+            const int ok    = __shfl_xor(bk, o, 64);
+            if (ov < bv || (ov == bv && ok < bk))
+            {
+                bv = ov;
+                bk = ok;
+            }
+        }
+        if (lane == 0)
+        {
+            s_best_v[wave] = bv;
+            s_best_k[wave] = bk;
+        }
+        if (t == 0)
+            s_tie = 0;
+        __syncthreads();
+        int best      = kEntBlock;
+        double best_v = __builtin_inf();
+        for (int k = 0; k < kEntBlock / 64; ++k)
+            if (s_best_v[k] < best_v || (s_best_v[k] == best_v && s_best_k[k] < best))
+            {
+                best_v = s_best_v[k];
+                best   = s_best_k[k];
+            }
+        if (best < kEntBlock && t == best)
+            s_best_m = m;
+        __syncthreads();
+        if (best < kEntBlock && t < nv && t != best)
+        {
+            const double tol = 1e-11 * (m + s_best_m) + 1e-14;
+            if (!(v - best_v > tol))
+                s_tie = 1;
+        }
+        __syncthreads();
         if (t == 0)
         {
-            // the reference loop: stop at the first breaking window, keep the first strict minimum
-            int nv = 0;
-            while (nv < s_n && !ws[nv].brk)
-                ++nv;
-            auto dv_of = [&](int k) {
-                double v = 0;
-                for (int sgm = 0; sgm < kSegs; ++sgm)
-                    v += part_dv[k * kSegs + sgm];
-                return v;
-            };
-            auto mag_of = [&](int k) {
-                double v = 0;
-                for (int sgm = 0; sgm < kSegs; ++sgm)
-                    v += part_mag[k * kSegs + sgm];
-                return v;
-            };
-            int best      = -1;
-            double best_v = __builtin_inf();
-            for (int k = 0; k < nv; ++k)
-            {
-                const double v = dv_of(k);
-                if (best < 0 ? v < __builtin_inf() : v < best_v)
-                {
-                    best   = k;
-                    best_v = v;
-                }
-            }
-            int status = kEntFinal;
-            if (best >= 0)
-            {
-                const double best_m = mag_of(best);
-                for (int k = 0; k < nv; ++k)
-                {
-                    if (k == best)
-                        continue;
-                    const double tol = 1e-11 * (mag_of(k) + best_m) + 1e-14;
-                    if (!(dv_of(k) - best_v > tol))   // a near-tie (or NaN): glibc decides
-                    {
-                        status = kEntHost;
-                        break;
-                    }
-                }
-            }
-            const double w = (s_hi - s_lo) / (double) entropy::kBins;
-            float lo       = (float) s_lo, hi = (float) s_hi;
-            if (best >= 0)
+            const int status = s_tie ? kEntHost : kEntFinal;
+            const double w   = (s_hi - s_lo) / (double) entropy::kBins;
+            float lo         = (float) s_lo, hi = (float) s_hi;
+            if (best < kEntBlock)
             {
                 lo = (float) (s_lo + (double) wa[best] * w);
                 hi = (float) (s_lo + (double) (wb[best] + 1) * w);

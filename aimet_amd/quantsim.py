@@ -517,8 +517,10 @@ def _precompute_param_encodings(wrappers):
                                                                        [t for _, t in group],
                                                                        [q.channel_axis for q, _ in group]))
     enabled = [q.enabled for _, q, _ in items]
-    for _, q, _ in items:
+    percentile = [None] * len(items)
+    for i, (_, q, _) in enumerate(items):
         if q.quant_scheme == QuantScheme.post_training_percentile:
+            percentile[i] = q._op().getPercentileValue()
             q.set_percentile_value(100)
         q._encoding = None
     compute_encodings_batched([q for _, q, _ in items])
@@ -527,18 +529,21 @@ def _precompute_param_encodings(wrappers):
     # forward marks the same list
     for w in {id(w): w for w, _, _ in items}.values():
         w.__dict__["_analysis_ran"] = [False]
-    return [(w, q, e) for (w, q, _), e in zip(items, enabled)]
+    return [(w, q, (e, p)) for (w, q, _), e, p in zip(items, enabled, percentile)]
 
 
 def _forget_unused_param_encodings(pre):
     """The parameter encodings precomputed for wrappers that no ANALYSIS forward ran: back to the
-    reset state the reference leaves them in (no statistics, no encoding, enabled as before)."""
+    reset state the reference leaves them in (no statistics, no encoding, enabled and percentile
+    as before)."""
     from aimet_amd.tensor_quantizer import AimetTensorQuantizer
     unused = [(w, q, e) for w, q, e in pre if not w.__dict__.get("_analysis_ran", [True])[0]]
     if unused:
         AimetTensorQuantizer.resetEncodingStatsMany([q._op() for _, q, _ in unused])
-        for _, q, e in unused:
+        for _, q, (e, p) in unused:
             q._encoding = None
             q.enabled = e
+            if p is not None:
+                q.set_percentile_value(p)
     for w, _, _ in pre:
         w.__dict__.pop("_analysis_ran", None)

@@ -281,7 +281,8 @@ def _quantizer_state(sim):
             for i, q in enumerate(qs):
                 enc = q.encoding
                 encs = enc if isinstance(enc, list) else ([] if enc is None else [enc])
-                out[(name, kind, i)] = (bool(q.enabled), [(e.min, e.max, e.delta, e.offset, e.bw) for e in encs])
+                pct = q._op().getPercentileValue() if q.quant_scheme == QuantScheme.post_training_percentile else None
+                out[(name, kind, i)] = (bool(q.enabled), [(e.min, e.max, e.delta, e.offset, e.bw) for e in encs], pct)
     return out
 
 
@@ -295,8 +296,8 @@ def test_compute_encodings_precomputed_parameter_encodings_equal_per_wrapper(mon
     forward, and launches each forward's activation statistics together (qc_quantize_op.StatsBatch)
     instead of one update per quantizer: every quantizer of the sim -- parameters, inputs, outputs,
     enabled flags -- ends as with the per-wrapper, per-call computation, a layer run twice per
-    forward and a wrapper no forward runs included (no encoding, as the reference leaves it), over
-    two calibrations of the same sim."""
+    forward and a wrapper no forward runs included (no encoding and its percentile as before, as
+    the reference leaves it), over two calibrations of the same sim."""
     import aimet_amd.qc_quantize_op as QO
     import aimet_amd.quantsim as QS
     data = [torch.randn(16, 64, device="cuda", generator=torch.Generator(device="cuda").manual_seed(i))

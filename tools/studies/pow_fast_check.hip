@@ -1,4 +1,5 @@
-// Exhaustive check of the library's f64 pow (aimet_amd/csrc/fast_pow.hpp: pow01_fast / powf01_f64)
+// Exhaustive check of the library's fast pow (aimet_amd/csrc/fast_pow.hpp: pow01_fast, the
+// table-driven f32 form; round 6's first form evaluated ln / exp in f64: pow_fast_check_f64.txt)
 // against the bit-exact emulation of torch's CPU pow (aimet_amd/csrc/sleef_pow.hpp: pow01_log over
 // sleef_logkf, equal to torch.pow on the CPU: tests/test_adaround_golden.py,
 // tools/studies/sleef_powf_check.py).
@@ -70,6 +71,8 @@ __device__ __forceinline__ unsigned wave_maxu(unsigned v)
 __global__ __launch_bounds__(kThreads) void check_kernel(const float* __restrict__ exps, int ne, int ncr, uint32_t x0,
                                                          Stats* st)
 {
+    pow_tab_fill<kThreads>();
+    __syncthreads();
     const uint32_t xb = x0 + blockIdx.x * kThreads + threadIdx.x;
     unsigned long long pairs = 0, eq = 0, one = 0, more = 0, crp = 0, fcr = 0, scr = 0;
     unsigned mx = 0, mf = 0, ms = 0;
@@ -152,6 +155,8 @@ __global__ __launch_bounds__(kThreads) void time_sleef(const float* __restrict__
 }
 __global__ __launch_bounds__(kThreads) void time_fast(const float* __restrict__ x, float* __restrict__ y, int n, float e)
 {
+    pow_tab_fill<kThreads>();
+    __syncthreads();
     const int i = blockIdx.x * kThreads + threadIdx.x;
     if (i < n)
         y[i] = pow01_fast(x[i], e);
@@ -277,7 +282,7 @@ int main(int argc, char** argv)
                 CK(hipEventElapsedTime(&ms, t0, t1));
                 best[form] = std::min(best[form], ms);
             }
-        std::printf("e = %g: Sleef emulation %.3f ms, f64 pow %.3f ms for 2^26 pows\n", e, best[0], best[1]);
+        std::printf("e = %g: Sleef emulation %.3f ms, fast pow %.3f ms for 2^26 pows\n", e, best[0], best[1]);
     }
     return h.more ? 2 : 0;
 }
