@@ -35,6 +35,9 @@ constexpr float kGamma = -0.1f;
 // python: (ZETA - GAMMA) = 1.2000000000000002 -> float32 scalar 1.2f in the torch op
 constexpr float kZmG = (float) (1.1 - (-0.1));
 constexpr int kAdaBwdGrid = 8192;   // 32 workgroups per CU; bounds the round-loss partials
+#ifndef AIMET_ADA_BWD_U
+#define AIMET_ADA_BWD_U 1   // quads per lane per tile of adaround_bwd_vec_kernel
+#endif
 
 struct AdaChannel
 {
@@ -270,7 +273,31 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
     if (!EXACT && 4 * total >= 3 * 64 * E)
     {
         // a dense wave: each lane evaluates its own elements in place with the fast pow (its
-        // logarithm shared by the two exponents; the scalar tail takes it too: fast_pow.hpp)
+        // logarithm shared by the two exponents; the scalar tail takes it too: fast_pow.hpp).
+        // Exponents other than 0, 2, 3 (uniform): branch-free -- every element is evaluated (on a
+        // stand-in 0.5 where |x| is 0 or 1) and the exact cases selected after, so the wave keeps
+        // no per-element exec masks (the pow runs for most lanes of a dense wave anyway)
+        const bool generic_m1 = !(p.beta_m1 == 0.0f || p.beta_m1 == 2.0f || p.beta_m1 == 3.0f);
+        const bool generic_b  = !(p.beta == 0.0f || p.beta == 2.0f || p.beta == 3.0f);
+        if (generic_m1 && (!p.want_loss || generic_b))
+        {
+#pragma unroll
+            for (int k = 0; k < E; ++k)
+            {
+                const bool edge = ax[k] == 0.0f || ax[k] == 1.0f;
+                const LnSplit l = ln01(edge ? 0.5f : ax[k]);
+                const float r1  = exp_ln(l, p.beta_m1);
+                pbm1[k]         = edge ? pow01_exact(ax[k], p.beta_m1) : (r1 != r1 ? __builtin_inff() : r1);
+                if (p.want_loss)
+                {
+                    const float r0 = exp_ln(l, p.beta);
+                    pb[k]          = edge ? pow01_exact(ax[k], p.beta) : (r0 != r0 ? __builtin_inff() : r0);
+                }
+                else
+                    pb[k] = 0.0f;
+            }
+            return;
+        }
 #pragma unroll
         for (int k = 0; k < E; ++k)
         {
@@ -1176,9 +1203,9 @@ int adaround_backward(const float* w, const float* alpha, const float* g, float*
             aligned16(ga))
         {
             uint32_t nq = (uint32_t) (n / 4);
-            // one quad in flight per lane (1 measured best, 2 equal within noise, 4 slower:
-            // profiles/r04/ada_bwd_tune_tail_flag.jsonl)
-            constexpr int U   = 1;
+            // quads in flight per lane (round 4 with the exact pow: 1 measured best, 2 equal within
+            // noise, 4 slower: profiles/r04/ada_bwd_tune_tail_flag.jsonl); a study build may set it
+            constexpr int U   = AIMET_ADA_BWD_U;
             int64_t blocks    = ceil_div(nq, kBlock * U);
             // one tile per workgroup unless round-loss partials are folded (one per workgroup): a
             // grid-stride loop over 8192 workgroups holds the 3-read + 1-write stream to 0.60 of

@@ -7,21 +7,25 @@
 //  1. the histogram the windows run over (the symmetric rescale) and its prefix tables: in
 //     parallel over the bins when every bin count is an integer below 2^43 (bin counts always
 //     are: sums of integers are then exact in any order), else by lane 0 as the reference loops;
-//     lane 0 enumerates the windows (entropy_kl.hpp: the window sequence never depends on a KL
-//     value);
+//     the windows (entropy_kl.hpp: the window sequence never depends on a KL value): listed in
+//     parallel when both ends shrink together (symmetric / strict), else by lane 0;
 //  2. one window per lane: the reference's float normalisers of P and Q, streamed in bin order
-//     with its float / double operations (exact);
+//     with its float / double operations (exact); with integral bins the level sums, the zero
+//     counts and the saturated ends come from the prefix tables;
 //  3. the divergence sum_i p_i log(p_i / q_i) of every window, split into kSegs segments of its 255
-//     levels over all lanes, the segments' sums added per window;
-//  4. lane 0 picks the first strict minimum.
+//     levels over all lanes (segment-major), the segments' sums added per window; the window's
+//     empty bins all have the same term, evaluated once and counted;
+//  4. the first strict minimum and the near-tie test by wave reductions over one window per lane.
 //
 // Bit parity: every operation of 1, 2 and the window choice equals the host's. The divergence
-// differs from the host's (the device's log, p and q as multiplies by 1 / normaliser instead of
-// divisions, the segments' sums re-associated): per term by at most ~2 ulp of |t| plus 2^-51 p, so
-// the two sums differ by < 2^-43 sum|t| + 1e-15. A window is accepted as the winner only when every
-// other window's divergence exceeds it by more than 1e-11 * (sum |t| of both) + 1e-14; otherwise
-// (and for non-finite ranges) the channel is flagged and the host re-runs the glibc search for it
-// (quantizer.cpp). The accepted winner is then the host's winner too.
+// differs from the host's (the device's log, p and q as multiplies by reciprocals -- the levels'
+// by v_rcp_f64 and two Newton steps -- instead of divisions, the empty bins' equal terms counted,
+// the segments' sums re-associated): per term by at most ~3 ulp of |t| plus 2^-51 p, and the sums'
+// order by 2^-44 sum|t|, so the two sums differ by < 2^-42 sum|t| + 1e-15. A window is accepted as
+// the winner only when every other window's divergence exceeds it by more than
+// 1e-11 * (sum |t| of both) + 1e-14; otherwise (and for non-finite ranges) the channel is flagged
+// and the host re-runs the glibc search for it (quantizer.cpp). The accepted winner is then the
+// host's winner too.
 #include "entropy_kl.hpp"
 #include "tq_state.hpp"
 
@@ -190,6 +194,7 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
     const double qz     = cond_apply(st.cQ, 0.0) * st.rdQ;
     dv = 0;
     mag = 0;
+    int zeros_inside = 0;
     int i1 = (int) (uint64_t) ceil((double) q0 * merged);
     for (int q = q0; q < q1; ++q)
     {
@@ -219,8 +224,14 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
         }
         for (int i = i0; i < i1; ++i)
         {
-            const bool nz   = norm != 0 && hw[i] != 0;
-            const double Pi = i == 0 ? 0.0 + st.left : (i == win - 1 ? 0.0 + st.right : hw[i]);
+            const double h = hw[i];
+            if (h == 0 && i != 0 && i != win - 1)
+            {
+                ++zeros_inside;   // the window's constant empty-bin term, added once below
+                continue;
+            }
+            const bool nz   = norm != 0 && h != 0;
+            const double Pi = i == 0 ? 0.0 + st.left : (i == win - 1 ? 0.0 + st.right : h);
             const double pn = cond_apply(st.cP, Pi) * st.rdP;
             const double qn = nz ? qnz : qz;
             if (pn > 0 && qn > 0)
@@ -230,6 +241,15 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
                 mag += fabs(t);
             }
         }
+    }
+    // every empty bin inside the window has P = cond(0) / dP and Q = cond(0) / dQ: one term,
+    // counted (the sum re-associated: within the terms' error bound)
+    const double pz = cond_apply(st.cP, 0.0) * st.rdP;
+    if (zeros_inside && pz > 0 && qz > 0)
+    {
+        const double t = pz * log(pz * st.rqz);
+        dv += (double) zeros_inside * t;
+        mag += (double) zeros_inside * fabs(t);
     }
 }
 
@@ -421,17 +441,19 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
         }
         __syncthreads();
         // ---- 3. the divergences, (window, segment) items over every lane --------------------------
+        // segment-major: neighbouring lanes take the same segment of neighbouring windows, whose
+        // bins -- and empty bins, which skip the logarithm -- lie at nearly the same positions
         for (int it = t; it < s_n * kSegs; it += kEntBlock)
         {
-            const int w = it / kSegs, sgm = it - w * kSegs;
+            const int sgm = it / s_n, w = it - sgm * s_n;
             double dv = 0, mag = 0;
             if (!ws[w].brk)
             {
                 const int q0 = sgm * kSegLev, q1 = q0 + kSegLev < entropy::kLevels ? q0 + kSegLev : entropy::kLevels;
                 window_segment(hist, wa[w], wb[w], q0, q1, ws[w], pre, integral, dv, mag);
             }
-            part_dv[it]  = dv;
-            part_mag[it] = mag;
+            part_dv[w * kSegs + sgm]  = dv;
+            part_mag[w * kSegs + sgm] = mag;
         }
         __syncthreads();
         // ---- 4. the first strict minimum: every window's sums on its own lane, wave reductions --

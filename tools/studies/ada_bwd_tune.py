@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--reg", type=float, default=0.01, help="reg_param (0: no rounding loss, no pow)")
     ap.add_argument("--lib", default=None, help="another build of libaimet_amd.so")
     ap.add_argument("--skew", type=int, default=0, help="start buffer k (w, grad, out, alpha) k x SKEW bytes into its allocation")
-    ap.add_argument("--exact-pow", action="store_true", help="the bit-exact Sleef pow instead of the f64 pow")
+    ap.add_argument("--exact-pow", action="store_true", help="the bit-exact Sleef pow instead of the fast (table-driven f32) pow")
     args = ap.parse_args()
     if args.lib:
         aimet_amd._native.LIB_PATH = os.path.abspath(args.lib)
@@ -75,7 +75,7 @@ def main():
             ms = ev[0].elapsed_time(ev[1]) / args.reps
             gbps = 16 * N / ms / 1e6
             print(json.dumps({"kernel": "adaround_bwd_vec_kernel", "tag": args.tag, "reg": args.reg, "skew": args.skew,
-                              "pow": "exact" if args.exact_pow else "f64", "elems": N, "alpha_scale": scale,
+                              "pow": "exact" if args.exact_pow else "fast", "elems": N, "alpha_scale": scale,
                               "saturated_frac": round(sat, 4), "want_loss": want_loss, "avg_ms": round(ms, 4),
                               "achieved_GBps": round(gbps, 1), "frac_of_peak": round(gbps / 8000, 4),
                               "checksum": int(out.view(torch.int32).to(torch.int64).sum().item()),

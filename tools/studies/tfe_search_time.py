@@ -1,7 +1,8 @@
 """Isolated timing of the device encoding searches (TF-Enhanced tfe_search_kernel, MSE
 mse_search_kernel, entropy entropy_search_kernel) on ResNet-50's weights: 27,560 channels,
 per-channel symmetric and asymmetric 8-bit, statistics computed once, then getEncodings repeated.
-usage: tfe_search_time.py [TF_ENHANCED] [MSE] [ENTROPY]. Run under `rocprofv3 --kernel-trace --stats`
+usage: tfe_search_time.py [--lib PATH] [TF_ENHANCED] [MSE] [ENTROPY] (--lib: another build of
+libaimet_amd.so, e.g. tools/studies/ent_variants.sh's). Run under `rocprofv3 --kernel-trace --stats`
 for the kernel durations; the wall-clock per batched getEncodings (search + copy + host encodings) is printed. Tuning tool."""
 import os
 import sys
@@ -16,11 +17,16 @@ from workloads.resnet import resnet50  # noqa: E402
 
 
 def main():
+    args = sys.argv[1:]
+    if args[:1] == ["--lib"]:
+        import aimet_amd._native
+        aimet_amd._native.LIB_PATH = os.path.abspath(args[1])
+        args = args[2:]
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     model = resnet50(seed=0, device=dev)
     ws = [m.weight.detach().contiguous() for m in model.modules() if isinstance(m, (torch.nn.Conv2d, torch.nn.Linear))]
-    schemes = sys.argv[1:] or ["TF_ENHANCED"]
+    schemes = args or ["TF_ENHANCED"]
     for scheme in schemes:
         qs = [AimetTensorQuantizer(getattr(QuantizationMode, "QUANTIZATION_" + scheme), num_channels=w.shape[0])
               for w in ws]
