@@ -18,10 +18,11 @@
 //  4. the first strict minimum and the near-tie test by wave reductions over one window per lane.
 //
 // Bit parity: every operation of 1, 2 and the window choice equals the host's. The divergence
-// differs from the host's (the device's log, p and q as multiplies by reciprocals -- the levels'
-// by v_rcp_f64 and two Newton steps -- instead of divisions, the empty bins' equal terms counted,
-// the segments' sums re-associated): per term by at most ~3 ulp of |t| plus 2^-51 p, and the sums'
-// order by 2^-44 sum|t|, so the two sums differ by < 2^-42 sum|t| + 1e-15. A window is accepted as
+// differs from the host's (log_kl, relative error < 2^-49, for glibc's log; p and q as multiplies
+// by reciprocals -- the levels' by v_rcp_f64 and two Newton steps -- instead of divisions; the
+// empty bins' equal terms counted; the segments' sums re-associated): per term by at most 2^-48
+// |t| plus 2^-51 p, and the sums' order by 2^-44 sum|t|, so the two sums differ by
+// < 2^-42 sum|t| + 1e-15. A window is accepted as
 // the winner only when every other window's divergence exceeds it by more than
 // 1e-11 * (sum |t| of both) + 1e-14; otherwise (and for non-finite ranges) the channel is flagged
 // and the host re-runs the glibc search for it (quantizer.cpp). The accepted winner is then the
@@ -89,30 +90,37 @@ __device__ void window_norms_integral(const double* hist, int a, int b, const en
     const uint64_t zQ   = (uint64_t) (pre.zeros[b + 1] - pre.zeros[a]);
     const Cond cP = cond_of(zP, (uint64_t) win), cQ = cond_of(zQ, (uint64_t) win);
     const double merged = (double) win / (double) kLevels;
-    auto lsum = [&](int i) { return a + i > 0 ? pre.left[a + i - 1] : 0.0; };   // hist[0, a + i)
+    // cond_apply in select form (the same value: h + 0.0001 * 1 - eps * 0 = 0.0001 for an empty
+    // bin, h + 0.0001 * 0 - eps * 1 = h - eps otherwise)
+    auto cfast = [](const Cond& c, double h) { return c.skip ? h : (h == 0 ? 0.0001 : h - c.eps); };
+    const double cQz = cfast(cQ, 0.0);
     float sP = 0.f, sQ = 0.f;
-    int q = 0, i0 = 0, i1 = level_end(0, merged, win);
-    double qv = 0.0;
-    bool qnz  = false;
-    for (int i = 0; i < win; ++i)
+    // level by level (255 iterations for every lane), each level's 1-3 bins in order; the level's
+    // sum and non-empty count from the prefix tables at its two bounds, the lower one carried over
+    double Lprev = a > 0 ? pre.left[a - 1] : 0.0;   // hist[0, a + i0)
+    int Zprev    = pre.zeros[a];
+    int i0       = 0;
+    for (int q = 0; q < kLevels; ++q)
     {
-        if (i == 0 || i == i1)
+        const int i1      = level_end(q, merged, win);
+        const double Lcur = pre.left[a + i1 - 1];
+        const int Zcur    = pre.zeros[a + i1];
+        const int norm    = (i1 - i0) - (Zcur - Zprev);
+        const double sum  = Lcur - Lprev;
+        double qv         = norm == 2 ? sum * 0.5 : sum;
+        if (norm > 2)   // three bins per level: only the widest windows, rarely
+            qv = sum / (double) norm;
+        const double cQn = norm != 0 ? cfast(cQ, qv) : cQz;   // the level's non-empty bins
+        for (int i = i0; i < i1; ++i)
         {
-            if (i != 0)
-            {
-                ++q;
-                i0 = i1;
-                i1 = level_end(q, merged, win);
-            }
-            const double norm = (double) ((i1 - i0) - (pre.zeros[a + i1] - pre.zeros[a + i0]));
-            qnz               = norm != 0;
-            qv                = qnz ? level_q(lsum(i1) - lsum(i0), norm) : 0.0;
+            const double h  = hist[a + i];
+            const double Pi = i == 0 ? 0.0 + left : (i == win - 1 ? 0.0 + right : h);
+            sP              = (float) ((double) sP + cfast(cP, Pi));
+            sQ              = (float) ((double) sQ + (h != 0 ? cQn : cQz));
         }
-        const double h  = hist[a + i];
-        const double Qi = (qnz && h != 0) ? qv : 0.0;
-        const double Pi = i == 0 ? 0.0 + left : (i == win - 1 ? 0.0 + right : h);
-        sP              = (float) ((double) sP + cond_apply(cP, Pi));
-        sQ              = (float) ((double) sQ + cond_apply(cQ, Qi));
+        i0    = i1;
+        Lprev = Lcur;
+        Zprev = Zcur;
     }
     st.left  = left;
     st.right = right;
@@ -182,6 +190,41 @@ __device__ void window_norms(const double* hist, int a, int b, const entropy::Pr
     st.rqz = 1.0 / (cond_apply(cQ, 0.0) * st.rdQ);
 }
 
+// ln x for a positive finite double (the divergence terms' logarithm): x = 2^k m, m in [sqrt(1/2),
+// sqrt(2)), ln m = 2 atanh(s) = 2 s (1 + s^2/3 + ... + s^16/17), s = (m - 1) / (m + 1) (|s| <=
+// 0.1716; m - 1 exact; the quotient from v_rcp_f64 and two Newton steps). Relative error of ln m
+// below 2^-49 (series truncation 2^-50, roundings a few ulp; ln m is small only where s is, so
+// the error stays relative near x = 1), k ln2 in two parts: ~30 instructions where the device
+// library's correctly rounded log takes ~95 (double-double arithmetic) -- the divergence only
+// needs the accuracy its near-tie tolerance assumes (file header)
+__device__ __forceinline__ double log_kl(double x)
+{
+    int k    = __builtin_amdgcn_frexp_exp(x);
+    double m = __builtin_amdgcn_frexp_mant(x);   // [0.5, 1)
+    if (m < 0.70710678118654752440)
+    {
+        m += m;
+        --k;
+    }
+    const double f = m - 1.0;
+    const double d = m + 1.0;
+    double r       = __builtin_amdgcn_rcp(d);
+    r              = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    r              = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    const double s = f * r, z = s * s;
+    double p = 1.0 / 17.0;
+    p        = __builtin_fma(p, z, 1.0 / 15.0);
+    p        = __builtin_fma(p, z, 1.0 / 13.0);
+    p        = __builtin_fma(p, z, 1.0 / 11.0);
+    p        = __builtin_fma(p, z, 1.0 / 9.0);
+    p        = __builtin_fma(p, z, 1.0 / 7.0);
+    p        = __builtin_fma(p, z, 1.0 / 5.0);
+    p        = __builtin_fma(p, z, 1.0 / 3.0);
+    const double lm = 2.0 * __builtin_fma(s * z, p, s);
+    const double kd = (double) k;
+    return __builtin_fma(kd, 6.93147180369123816490e-01, __builtin_fma(kd, 1.90821492927058770002e-10, lm));
+}
+
 // step 3: the divergence terms of levels [q0, q1) of window [a, b] (entropy::stream_pq's levels),
 // p = cond(P) / dP, q = cond(Q) / dQ, sum of p log(p / q) over p, q > 0, and of its magnitudes
 __device__ void window_segment(const double* hist, int a, int b, int q0, int q1, const WinState& st,
@@ -196,15 +239,28 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
     mag = 0;
     int zeros_inside = 0;
     int i1 = (int) (uint64_t) ceil((double) q0 * merged);
+    // integral bins: the levels' sums and non-empty counts from the prefix tables (exact), the
+    // lower bound's entries carried over from the previous level
+    double Lprev = 0.0;
+    int Zprev    = 0;
+    if (integral)
+    {
+        Lprev = a + i1 > 0 ? pre.left[a + i1 - 1] : 0.0;
+        Zprev = pre.zeros[a + i1];
+    }
     for (int q = q0; q < q1; ++q)
     {
         const int i0 = i1;
         i1           = level_end(q, merged, win);
         double sum = 0, norm = 0;
-        if (integral)   // integral bins: the level's sum and non-empty count from the tables (exact)
+        if (integral)
         {
-            sum  = (pre.left[a + i1 - 1] - (a + i0 > 0 ? pre.left[a + i0 - 1] : 0.0));
-            norm = (double) ((i1 - i0) - (pre.zeros[a + i1] - pre.zeros[a + i0]));
+            const double Lcur = pre.left[a + i1 - 1];
+            const int Zcur    = pre.zeros[a + i1];
+            sum               = Lcur - Lprev;
+            norm              = (double) ((i1 - i0) - (Zcur - Zprev));
+            Lprev             = Lcur;
+            Zprev             = Zcur;
         }
         else
             for (int i = i0; i < i1; ++i)
@@ -217,7 +273,10 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
         double qnz = 0.0, rqnz = 0.0;
         if (norm != 0)
         {
-            qnz  = cond_apply(st.cQ, level_q(sum, norm)) * st.rdQ;
+            double qv = norm == 2 ? sum * 0.5 : sum;
+            if (norm > 2)   // three bins per level: only the widest windows, rarely
+                qv = sum / norm;
+            qnz  = cond_apply(st.cQ, qv) * st.rdQ;
             rqnz = __builtin_amdgcn_rcp(qnz);
             rqnz = __builtin_fma(__builtin_fma(-qnz, rqnz, 1.0), rqnz, rqnz);
             rqnz = __builtin_fma(__builtin_fma(-qnz, rqnz, 1.0), rqnz, rqnz);
@@ -236,7 +295,7 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
             const double qn = nz ? qnz : qz;
             if (pn > 0 && qn > 0)
             {
-                const double t = pn * log(pn * (nz ? rqnz : st.rqz));
+                const double t = pn * log_kl(pn * (nz ? rqnz : st.rqz));
                 dv += t;
                 mag += fabs(t);
             }
@@ -247,7 +306,7 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
     const double pz = cond_apply(st.cP, 0.0) * st.rdP;
     if (zeros_inside && pz > 0 && qz > 0)
     {
-        const double t = pz * log(pz * st.rqz);
+        const double t = pz * log_kl(pz * st.rqz);
         dv += (double) zeros_inside * t;
         mag += (double) zeros_inside * fabs(t);
     }

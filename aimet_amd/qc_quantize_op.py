@@ -210,6 +210,37 @@ class StatsBatch:
             with torch.cuda.device(dev):
                 AimetTensorQuantizer.updateStatsMany([q._op() for q, _ in group], [t for _, t in group])
 
+class ParamQdqCache:
+    """The QDQ'd parameters of QuantizationSimModel.compute_encodings' ANALYSIS forwards, kept for
+    the next forward while the parameter, its encoding and the rounding are unchanged (the same
+    values: the reference recomputes them in every forward). Shared by the sim's wrappers and
+    bounded (`limit` elements, 2^27 by default): on a model whose quantized weights exceed it --
+    Llama-3-8B's 7.5 G -- the cache would hold a second copy of every weight through the whole
+    calibration, and the caching allocator would keep those segments reserved afterwards (measured:
+    the QAT step after such a calibration took 11 ms more); parameters past the limit are
+    recomputed per forward, as the reference does."""
+
+    def __init__(self, limit: int = 1 << 27):
+        self.limit = int(limit)
+        self.entries = {}
+        self.elems = 0
+
+    def get(self, owner, name, key):
+        hit = self.entries.get((id(owner), name))
+        return hit[1] if hit is not None and hit[0] == key else None
+
+    def put(self, owner, name, key, value):
+        self.drop(owner, name)
+        if self.elems + value.numel() <= self.limit:
+            self.entries[(id(owner), name)] = (key, value)
+            self.elems += value.numel()
+
+    def drop(self, owner, name):
+        hit = self.entries.pop((id(owner), name), None)
+        if hit is not None:
+            self.elems -= hit[1].numel()
+
+
 def _data_dependent(q) -> bool:
     """update_encoding_stats(t) of q reads t (not a fixed range, not a disabled / frozen / 32-bit
     quantizer, which ignore it)."""
@@ -533,7 +564,7 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
                         q.set_percentile_value(100)
                     q.compute_encoding()
                     if cache is not None:
-                        cache.pop(name, None)
+                        cache.drop(self, name)
                     if not q.enabled:
                         continue
                 round_mode = q.round_mode if self.training else RoundingMode.ROUND_NEAREST
@@ -544,10 +575,11 @@ class StaticGridQuantWrapper(QcQuantizeWrapper):
                 # TfEncoding._version moves whenever any encoding is created or assigned
                 key = (param.data_ptr(), param._version, tuple(param.shape), param.dtype, id(q._encoding),
                        TfEncoding._version, int(round_mode))
-                hit = cache.get(name)
-                if hit is None or hit[0] != key:
-                    hit = cache[name] = (key, q.quantize_dequantize(param.data, round_mode))
-                param.data = hit[1]
+                out = cache.get(self, name, key)
+                if out is None:
+                    out = q.quantize_dequantize(param.data, round_mode)
+                    cache.put(self, name, key, out)
+                param.data = out
         return shadow_params
 
     def compute_weight_encodings(self):

@@ -28,7 +28,8 @@ import torch
 from torch import nn
 
 from aimet_amd.qc_quantize_op import (QUANTIZER_TYPE_INPUT, QUANTIZER_TYPE_OUTPUT, LearnedGridQuantWrapper,
-                                      QcQuantizeOpMode, QcQuantizeWrapper, StaticGridQuantWrapper, StatsBatch,
+                                      ParamQdqCache, QcQuantizeOpMode, QcQuantizeWrapper, StaticGridQuantWrapper,
+                                      StatsBatch,
                                       construct_learned_grid_wrapper)
 from aimet_amd.quantizers import QuantizationDataType, QuantScheme, compute_encodings_batched
 
@@ -232,9 +233,10 @@ class QuantizationSimModel:
             pre = _precompute_param_encodings(wrappers)
             batch = StatsBatch(group=process_group, sharded=bool(sharded))
             static = [w for w in wrappers if isinstance(w, StaticGridQuantWrapper)]
+            qdq_cache = ParamQdqCache()
             for w in static:
                 w.__dict__["_stats_batch"] = batch
-                w.__dict__["_param_qdq_cache"] = {}
+                w.__dict__["_param_qdq_cache"] = qdq_cache
             hook = self.model.register_forward_hook(lambda *_: batch.end_forward())
             try:
                 forward_pass_callback(self.model, forward_pass_callback_args)
