@@ -284,17 +284,12 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
 #pragma unroll
             for (int k = 0; k < E; ++k)
             {
-                const bool edge = ax[k] == 0.0f || ax[k] == 1.0f;
-                const LnSplit l = ln01(edge ? 0.5f : ax[k]);
-                const float r1  = exp_ln(l, p.beta_m1);
-                pbm1[k]         = edge ? pow01_exact(ax[k], p.beta_m1) : (r1 != r1 ? __builtin_inff() : r1);
-                if (p.want_loss)
-                {
-                    const float r0 = exp_ln(l, p.beta);
-                    pb[k]          = edge ? pow01_exact(ax[k], p.beta) : (r0 != r0 ? __builtin_inff() : r0);
-                }
-                else
-                    pb[k] = 0.0f;
+                // |x| outside (0, 1): 0, 1 or NaN (pow01_fast_l's exact cases and its NaN -> inf)
+                const bool inside = ax[k] > 0.0f && ax[k] < 1.0f;
+                const LnSplit l   = ln01(inside ? ax[k] : 0.5f);
+                const float fixed = ax[k] == 0.0f ? 0.0f : (ax[k] == 1.0f ? 1.0f : __builtin_inff());
+                pbm1[k]           = inside ? exp_ln(l, p.beta_m1) : fixed;
+                pb[k]             = p.want_loss ? (inside ? exp_ln(l, p.beta) : fixed) : 0.0f;
             }
             return;
         }

@@ -6,7 +6,7 @@
 // within 1 ulp of Sleef's, and Sleef's error is below 1 ulp, so any pow whose own error stays below
 // 1 ulp qualifies (two results on the f32 grid closer than 2 ulps to the same value differ by at
 // most 1 ulp); this one keeps its error below ~0.3 ulp before the final rounding, in ~33 f32
-// instructions and 5 LDS reads:
+// instructions and 2 LDS reads:
 //   ln x = k ln2 + ln m (x = m 2^k, m in [0.5, 1)); m's top 7 fraction bits pick c = 1 / m_j and
 //   tau = -ln c from a 128-entry table, so ln m = tau + ln(1 + r), r = m c - 1 (one FMA, rounded:
 //   |r| <= 2^-8, error <= 2^-33), ln(1 + r) = r + r^2 (-1/2 + r/3 - r^2/4) (truncation 2^-42);
@@ -33,9 +33,12 @@ namespace aimet_amd
 namespace
 {
 
+typedef float f4t __attribute__((ext_vector_type(4)));
+typedef float f2t __attribute__((ext_vector_type(2)));
+
 // the tables in LDS: every kernel that evaluates the fast pow fills them first (pow_tab_fill or
 // pow_tab_load + pow_tab_store, then a workgroup barrier)
-__shared__ PowTab g_pow_tab;
+__shared__ __attribute__((aligned(16))) PowTab g_pow_tab;
 
 // the workgroup's BLOCK threads copy the tables into LDS in two halves, so that a kernel can issue
 // its own first loads between them: pow_tab_load (global -> registers), then pow_tab_store
@@ -91,13 +94,14 @@ __device__ __forceinline__ LnSplit ln01(float x)
     const int k     = __builtin_amdgcn_frexp_expf(x);
     const float m   = __builtin_amdgcn_frexp_mantf(x);   // [0.5, 1)
     const uint32_t j = (__float_as_uint(m) >> 16) & 127u;
-    const float r   = __builtin_fmaf(m, g_pow_tab.c[j], -1.0f);
+    const f4t e     = *reinterpret_cast<const f4t*>(g_pow_tab.ln[j]);   // one 16-B LDS read
+    const float r   = __builtin_fmaf(m, e.x, -1.0f);
     float t         = __builtin_fmaf(r, -0.25f, 0.333333343f);
     t               = __builtin_fmaf(r, t, -0.5f);
     const float p   = (r * r) * t;
     const float kf  = (float) k;
-    const float a   = __builtin_fmaf(kf, kLn2Hi, g_pow_tab.th[j]);   // exact
-    const float b   = __builtin_fmaf(kf, kLn2Lo, g_pow_tab.tl[j]);
+    const float a   = __builtin_fmaf(kf, kLn2Hi, e.y);   // exact
+    const float b   = __builtin_fmaf(kf, kLn2Lo, e.z);
     return LnSplit {a, (r + p) + b};
 }
 
@@ -115,9 +119,8 @@ __device__ __forceinline__ float exp_ln(LnSplit l, float e)
     rr             = __builtin_fmaf(nf, -kCl, rr);
     const float t  = __builtin_fmaf(rr, 0.166666672f, 0.5f);
     const float em = __builtin_fmaf(rr * rr, t, rr);   // exp(rr) - 1
-    const uint32_t i = (uint32_t) n & 31u;
-    const float eh = g_pow_tab.eh[i];
-    const float v  = eh + __builtin_fmaf(eh, em, g_pow_tab.el[i]);
+    const f2t x    = *reinterpret_cast<const f2t*>(g_pow_tab.ex[(uint32_t) n & 31u]);   // {eh, el}: one 8-B read
+    const float v  = x.x + __builtin_fmaf(x.x, em, x.y);
     // y >= 64 ln(2^-149), so n > -10000: below 2^-149 the scaled value is +0, as x^e is
     return __builtin_ldexpf(v, n >> 5);
 }

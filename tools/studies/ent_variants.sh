@@ -18,7 +18,7 @@ for v in no3 no23; do
   out=build/ent_variants/entropy_search_$v.hip
   sed 's/window_segment(hist, wa\[w\], wb\[w\], q0, q1, ws\[w\], pre, integral, dv, mag);/(void) q0; (void) q1;/' $SRC > $out
   if [ $v = no23 ]; then
-    sed -i 's/window_norms_integral(hist, wa\[t\], wb\[t\], pre, ws\[t\]);/ws[t].brk = 0;/' $out
+    sed -i 's/window_norms_integral(hist, wa\[t\], wb\[t\], pre, ws\[t\], est);/ws[t].brk = 0;/' $out
   fi
   grep -q "window_segment(hist, wa" $out && { echo "step 3 call not replaced"; exit 1; }
   /opt/rocm/bin/hipcc $FLAGS -x hip -c $out -o build/ent_variants/entropy_search_$v.o
