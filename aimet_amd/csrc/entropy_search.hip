@@ -9,13 +9,18 @@
 //     are: sums of integers are then exact in any order), else by lane 0 as the reference loops;
 //     the windows (entropy_kl.hpp: the window sequence never depends on a KL value): listed in
 //     parallel when both ends shrink together (symmetric / strict), else by lane 0;
-//  2. one window per lane: the reference's float normalisers of P and Q, streamed in bin order
-//     with its float / double operations (exact); with integral bins the level sums, the zero
-//     counts and the saturated ends come from the prefix tables;
-//  3. the divergence sum_i p_i log(p_i / q_i) of every window, split into kSegs segments of its 255
-//     levels over all lanes (segment-major), the segments' sums added per window; the window's
-//     empty bins all have the same term, evaluated once and counted;
-//  4. the first strict minimum and the near-tie test by wave reductions over one window per lane.
+//  2. one window per lane: the reference's float normalisers of P and Q, streamed level by level
+//     in bin order with its float / double operations (exact); with integral bins the level sums,
+//     the zero counts and the saturated ends come from the prefix tables, and the same pass
+//     accumulates an f32 estimate of the window's divergence with a rigorous error bound
+//     (window_norms_integral: the filter);
+//  3. the windows the estimates cannot rule out (candidates: possibly the minimum or within the
+//     near-tie tolerance of it; usually a handful of the 129) get the divergence
+//     sum_i p_i log(p_i / q_i) in double, split into kSegs segments of their 255 levels over all
+//     lanes, the segments' sums added per window; a window's empty bins all have the same term,
+//     evaluated once and counted; without the filter (non-integral bins) every window is one;
+//  4. the first strict minimum among the candidates and the near-tie test by wave reductions
+//     (a window ruled out by the filter exceeds the minimum by more than the tolerance).
 //
 // Bit parity: every operation of 1, 2 and the window choice equals the host's. The divergence
 // differs from the host's (log_kl, relative error < 2^-49, for glibc's log; p and q as multiplies
@@ -61,6 +66,41 @@ struct WinState
     int brk;                  // the reference loop stops at this window (P or Q sums to 0)
 };
 
+// ln x for a positive finite double (the divergence terms' logarithm): x = 2^k m, m in [sqrt(1/2),
+// sqrt(2)), ln m = 2 atanh(s) = 2 s (1 + s^2/3 + ... + s^16/17), s = (m - 1) / (m + 1) (|s| <=
+// 0.1716; m - 1 exact; the quotient from v_rcp_f64 and two Newton steps). Relative error of ln m
+// below 2^-49 (series truncation 2^-50, roundings a few ulp; ln m is small only where s is, so
+// the error stays relative near x = 1), k ln2 in two parts: ~30 instructions where the device
+// library's correctly rounded log takes ~95 (double-double arithmetic) -- the divergence only
+// needs the accuracy its near-tie tolerance assumes (file header)
+__device__ __forceinline__ double log_kl(double x)
+{
+    int k    = __builtin_amdgcn_frexp_exp(x);
+    double m = __builtin_amdgcn_frexp_mant(x);   // [0.5, 1)
+    if (m < 0.70710678118654752440)
+    {
+        m += m;
+        --k;
+    }
+    const double f = m - 1.0;
+    const double d = m + 1.0;
+    double r       = __builtin_amdgcn_rcp(d);
+    r              = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    r              = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
+    const double s = f * r, z = s * s;
+    double p = 1.0 / 17.0;
+    p        = __builtin_fma(p, z, 1.0 / 15.0);
+    p        = __builtin_fma(p, z, 1.0 / 13.0);
+    p        = __builtin_fma(p, z, 1.0 / 11.0);
+    p        = __builtin_fma(p, z, 1.0 / 9.0);
+    p        = __builtin_fma(p, z, 1.0 / 7.0);
+    p        = __builtin_fma(p, z, 1.0 / 5.0);
+    p        = __builtin_fma(p, z, 1.0 / 3.0);
+    const double lm = 2.0 * __builtin_fma(s * z, p, s);
+    const double kd = (double) k;
+    return __builtin_fma(kd, 6.93147180369123816490e-01, __builtin_fma(kd, 1.90821492927058770002e-10, lm));
+}
+
 // a level's Q where its bins are non-empty: the reference's sum / norm, exactly (norm 1 and 2 --
 // nearly every level of a window of 256-512 bins over 255 levels -- without the division)
 __device__ __forceinline__ double level_q(double sum, double norm)
@@ -79,7 +119,22 @@ __device__ __forceinline__ int level_end(int q, double merged, int win)
 // reference's bin order (exact: the same float / double operations), with the level sums, the
 // zero counts and the right-hand saturation from the prefix tables, and whether the reference
 // loop stops here (the float sums of P or Q are 0 exactly when every bin of P or Q is 0)
-__device__ void window_norms_integral(const double* hist, int a, int b, const entropy::Prefix& pre, WinState& st)
+// The filter (round 6): while the exact normalisers are streamed, the same pass accumulates an
+// estimate of the window's divergence in f32 arithmetic, KL = (S1 + ln(dQ / dP) S0) / dP with
+// S1 = sum cP ln(cP / cQ) and S0 = sum cP over the terms the reference adds (cP, cQ the
+// conditioned P and Q; p = cP / dP, q = cQ / dQ), and a bound on its error: per term the f32
+// ratio (reciprocal of the level's cQ, one product) is within 2^-22 relative, v_log_f32 * ln2
+// within kLogAbs + kLogRel |ln| (tools/studies/log_f32_check.hip, profiles/r06/log_f32_check.txt),
+// the f32 product within 2^-23; summed in double. Only windows whose estimate could be the
+// minimum or a near-tie of it are then evaluated exactly (step 3).
+constexpr double kLogAbs = 0x1p-20, kLogRel = 0x1p-20;   // >= 4x the measured bounds plus the ratio's
+struct WinEstimate
+{
+    double kl, err, mag;   // estimate, bound on |estimate - divergence|, bound on sum |p ln(p / q)|
+};
+
+__device__ void window_norms_integral(const double* hist, int a, int b, const entropy::Prefix& pre, WinState& st,
+                                      WinEstimate& est)
 {
     using namespace entropy;
     const int win       = b - a + 1;
@@ -94,7 +149,9 @@ __device__ void window_norms_integral(const double* hist, int a, int b, const en
     // bin, h + 0.0001 * 0 - eps * 1 = h - eps otherwise)
     auto cfast = [](const Cond& c, double h) { return c.skip ? h : (h == 0 ? 0.0001 : h - c.eps); };
     const double cQz = cfast(cQ, 0.0);
+    const float rqz32 = __builtin_amdgcn_rcpf((float) cQz);
     float sP = 0.f, sQ = 0.f;
+    double S1 = 0.0, M1 = 0.0, S0 = 0.0;   // the filter's sums
     // level by level (255 iterations for every lane), each level's 1-3 bins in order; the level's
     // sum and non-empty count from the prefix tables at its two bounds, the lower one carried over
     double Lprev = a > 0 ? pre.left[a - 1] : 0.0;   // hist[0, a + i0)
@@ -111,12 +168,22 @@ __device__ void window_norms_integral(const double* hist, int a, int b, const en
         if (norm > 2)   // three bins per level: only the widest windows, rarely
             qv = sum / (double) norm;
         const double cQn = norm != 0 ? cfast(cQ, qv) : cQz;   // the level's non-empty bins
+        const float rqn32 = __builtin_amdgcn_rcpf((float) cQn);
         for (int i = i0; i < i1; ++i)
         {
             const double h  = hist[a + i];
             const double Pi = i == 0 ? 0.0 + left : (i == win - 1 ? 0.0 + right : h);
-            sP              = (float) ((double) sP + cfast(cP, Pi));
-            sQ              = (float) ((double) sQ + (h != 0 ? cQn : cQz));
+            const double cp = cfast(cP, Pi), cq = h != 0 ? cQn : cQz;
+            sP              = (float) ((double) sP + cp);
+            sQ              = (float) ((double) sQ + cq);
+            // the filter's term (p > 0 and q > 0 exactly when cP > 0 and cQ > 0)
+            const bool inc  = cp > 0 && cq > 0;
+            const float c32 = (float) cp;
+            const float l   = __builtin_amdgcn_logf(c32 * (h != 0 ? rqn32 : rqz32)) * 0.693147182f;
+            const float tt  = inc ? c32 * l : 0.0f;
+            S1 += (double) tt;
+            M1 += (double) __builtin_fabsf(tt);
+            S0 += inc ? cp : 0.0;
         }
         i0    = i1;
         Lprev = Lcur;
@@ -131,6 +198,12 @@ __device__ void window_norms_integral(const double* hist, int a, int b, const en
     st.rdP = 1.0 / dP;
     st.rdQ = 1.0 / dQ;
     st.rqz = 1.0 / (cond_apply(cQ, 0.0) * st.rdQ);
+    // KL = sum p ln(p / q) = (S1 + ln(dQ / dP) S0) / dP; |sum p ln(p / q)| terms <= (M1 + |L| S0) / dP
+    const double L   = log_kl(dQ * st.rdP);
+    const double mag = (M1 + __builtin_fabs(L) * S0) * st.rdP;
+    est.kl  = (S1 + L * S0) * st.rdP;
+    est.err = ((kLogAbs * S0 + kLogRel * M1) * st.rdP + 0x1p-40 * mag) * 1.0009765625 + 1e-300;
+    est.mag = mag * (1.0 + 0x1p-20) + est.err;
 }
 
 // step 2 for window [a, b] without the integral tables' shortcuts (lane per window, two streamed
@@ -188,41 +261,6 @@ __device__ void window_norms(const double* hist, int a, int b, const entropy::Pr
     st.rdP = 1.0 / dP;
     st.rdQ = 1.0 / dQ;
     st.rqz = 1.0 / (cond_apply(cQ, 0.0) * st.rdQ);
-}
-
-// ln x for a positive finite double (the divergence terms' logarithm): x = 2^k m, m in [sqrt(1/2),
-// sqrt(2)), ln m = 2 atanh(s) = 2 s (1 + s^2/3 + ... + s^16/17), s = (m - 1) / (m + 1) (|s| <=
-// 0.1716; m - 1 exact; the quotient from v_rcp_f64 and two Newton steps). Relative error of ln m
-// below 2^-49 (series truncation 2^-50, roundings a few ulp; ln m is small only where s is, so
-// the error stays relative near x = 1), k ln2 in two parts: ~30 instructions where the device
-// library's correctly rounded log takes ~95 (double-double arithmetic) -- the divergence only
-// needs the accuracy its near-tie tolerance assumes (file header)
-__device__ __forceinline__ double log_kl(double x)
-{
-    int k    = __builtin_amdgcn_frexp_exp(x);
-    double m = __builtin_amdgcn_frexp_mant(x);   // [0.5, 1)
-    if (m < 0.70710678118654752440)
-    {
-        m += m;
-        --k;
-    }
-    const double f = m - 1.0;
-    const double d = m + 1.0;
-    double r       = __builtin_amdgcn_rcp(d);
-    r              = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
-    r              = __builtin_fma(__builtin_fma(-d, r, 1.0), r, r);
-    const double s = f * r, z = s * s;
-    double p = 1.0 / 17.0;
-    p        = __builtin_fma(p, z, 1.0 / 15.0);
-    p        = __builtin_fma(p, z, 1.0 / 13.0);
-    p        = __builtin_fma(p, z, 1.0 / 11.0);
-    p        = __builtin_fma(p, z, 1.0 / 9.0);
-    p        = __builtin_fma(p, z, 1.0 / 7.0);
-    p        = __builtin_fma(p, z, 1.0 / 5.0);
-    p        = __builtin_fma(p, z, 1.0 / 3.0);
-    const double lm = 2.0 * __builtin_fma(s * z, p, s);
-    const double kd = (double) k;
-    return __builtin_fma(kd, 6.93147180369123816490e-01, __builtin_fma(kd, 1.90821492927058770002e-10, lm));
 }
 
 // step 3: the divergence terms of levels [q0, q1) of window [a, b] (entropy::stream_pq's levels),
@@ -329,8 +367,9 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
     __shared__ int zeros[entropy::kBins + 1];
     __shared__ double s_lo, s_hi;
     __shared__ int s_n, s_rule, s_integral;
-    __shared__ int s_first_brk[kEntBlock / 64], s_best_k[kEntBlock / 64], s_tie;
-    __shared__ double s_best_v[kEntBlock / 64], s_best_m;
+    __shared__ int s_first_brk[kEntBlock / 64], s_best_k[kEntBlock / 64], s_tie, s_ncand[kEntBlock / 64];
+    __shared__ double s_best_v[kEntBlock / 64], s_best_m, s_mag[kEntBlock / 64];
+    __shared__ short s_cand[entropy::kWindows];
     const int t = threadIdx.x;
     const int lane = t & 63;
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
@@ -489,40 +528,83 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
             s_rule = rule ? 1 : 0;
         }
         __syncthreads();
-        // ---- 2. the normalisers of every window (exact) -----------------------------------------
+        // ---- 2. the normalisers of every window (exact) and the filter's estimate ---------------
         const entropy::Prefix pre {left, zeros, s_rule != 0};
+        WinEstimate est {0.0, __builtin_inf(), __builtin_inf()};   // (no filter: every window exact)
         if (t < s_n)
         {
             if (integral)
-                window_norms_integral(hist, wa[t], wb[t], pre, ws[t]);
+                window_norms_integral(hist, wa[t], wb[t], pre, ws[t], est);
             else
                 window_norms(hist, wa[t], wb[t], &pre, ws[t]);
         }
+        const int wave = t >> 6;
+        const bool brk = t >= s_n || ws[t].brk != 0;
+        const uint64_t brk_mask = __ballot(brk);
+        if (lane == 0)
+            s_first_brk[wave] = brk_mask ? wave * 64 + __ffsll((long long) brk_mask) - 1 : kEntBlock;
         __syncthreads();
-        // ---- 3. the divergences, (window, segment) items over every lane --------------------------
-        // segment-major: neighbouring lanes take the same segment of neighbouring windows, whose
-        // bins -- and empty bins, which skip the logarithm -- lie at nearly the same positions
-        for (int it = t; it < s_n * kSegs; it += kEntBlock)
+        // the reference loop stops at the first breaking window (nv)
+        int nv = kEntBlock;
+        for (int k = 0; k < kEntBlock / 64; ++k)
+            nv = s_first_brk[k] < nv ? s_first_brk[k] : nv;
+        nv = nv < s_n ? nv : s_n;
+        // ---- 3a. the windows the estimate cannot rule out --------------------------------------
+        // U = min (kl + err) >= the smallest divergence; a window with kl - err > U + T, T above
+        // the near-tie tolerance 1e-11 (mag_k + mag_best) + 1e-14, is larger than the minimum by
+        // more than that tolerance: it is neither the winner nor a near-tie, and is not evaluated
+        double up = t < nv ? est.kl + est.err : __builtin_inf();
+        double mg = t < nv ? est.mag : 0.0;
+        for (int o = 32; o > 0; o >>= 1)
         {
-            const int sgm = it / s_n, w = it - sgm * s_n;
+            up = __builtin_fmin(up, __shfl_xor(up, o, 64));
+            mg = __builtin_fmax(mg, __shfl_xor(mg, o, 64));
+        }
+        if (lane == 0)
+        {
+            s_best_v[wave] = up;
+            s_mag[wave]    = mg;
+        }
+        __syncthreads();
+        double U = __builtin_inf(), maxmag = 0.0;
+        for (int k = 0; k < kEntBlock / 64; ++k)
+        {
+            U      = __builtin_fmin(U, s_best_v[k]);
+            maxmag = __builtin_fmax(maxmag, s_mag[k]);
+        }
+        // (a NaN estimate, an infinite bound or no filter: a candidate)
+        const double T  = 1e-11 * (est.mag + maxmag) * 1.0009765625 + 1e-14;
+        const bool cand = t < nv && !(est.kl - est.err > U + T);
+        const uint64_t cand_mask = __ballot(cand);
+        if (lane == 0)
+            s_ncand[wave] = __popcll(cand_mask);
+        __syncthreads();
+        int cbase = 0, ncand = 0;
+        for (int k = 0; k < kEntBlock / 64; ++k)
+        {
+            cbase += k < wave ? s_ncand[k] : 0;
+            ncand += s_ncand[k];
+        }
+        if (cand)
+            s_cand[cbase + (int) __builtin_amdgcn_mbcnt_hi((uint32_t) (cand_mask >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((uint32_t) cand_mask, 0u))] = (short) t;
+        __syncthreads();
+        // ---- 3b. the candidates' divergences, (window, segment) items over every lane ------------
+        for (int it = t; it < ncand * kSegs; it += kEntBlock)
+        {
+            const int w = s_cand[it / kSegs], sgm = it % kSegs;
+            const int q0 = sgm * kSegLev, q1 = q0 + kSegLev < entropy::kLevels ? q0 + kSegLev : entropy::kLevels;
             double dv = 0, mag = 0;
-            if (!ws[w].brk)
-            {
-                const int q0 = sgm * kSegLev, q1 = q0 + kSegLev < entropy::kLevels ? q0 + kSegLev : entropy::kLevels;
-                window_segment(hist, wa[w], wb[w], q0, q1, ws[w], pre, integral, dv, mag);
-            }
+            window_segment(hist, wa[w], wb[w], q0, q1, ws[w], pre, integral, dv, mag);
             part_dv[w * kSegs + sgm]  = dv;
             part_mag[w * kSegs + sgm] = mag;
         }
         __syncthreads();
-        // ---- 4. the first strict minimum: every window's sums on its own lane, wave reductions --
-        // the reference loop stops at the first breaking window (nv) and keeps the first strict
-        // minimum below +inf; the window is accepted only if every other one before nv exceeds it
-        // by more than the tolerance (a near-tie or a NaN: the host's glibc search decides)
-        const int wave = t >> 6;
+        // ---- 4. the first strict minimum among the candidates (wave reductions), near-tie test ---
+        // the window is accepted only if every other one before nv exceeds it by more than the
+        // tolerance (a near-tie or a NaN: the host's glibc search decides)
         double v = __builtin_inf(), m = 0.0;
-        bool brk = true;
-        if (t < s_n)
+        if (cand)
         {
             v = 0.0;
             for (int sgm = 0; sgm < kSegs; ++sgm)   // the segments' sums in segment order
@@ -530,16 +612,7 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
                 v += part_dv[t * kSegs + sgm];
                 m += part_mag[t * kSegs + sgm];
             }
-            brk = ws[t].brk != 0;
         }
-        const uint64_t brk_mask = __ballot(brk);
-        if (lane == 0)
-            s_first_brk[wave] = brk_mask ? wave * 64 + __ffsll((long long) brk_mask) - 1 : kEntBlock;
-        __syncthreads();
-        int nv = kEntBlock;
-        for (int k = 0; k < kEntBlock / 64; ++k)
-            nv = s_first_brk[k] < nv ? s_first_brk[k] : nv;
-        nv = nv < s_n ? nv : s_n;
         // (value, index) argmin: the smallest value below +inf, the first index among equals
         double bv = (t < nv && v < __builtin_inf()) ? v : __builtin_inf();
         int bk    = bv < __builtin_inf() ? t : kEntBlock;

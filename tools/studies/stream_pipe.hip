@@ -8,10 +8,12 @@
 //   chunkN -- the same without the prefetch (loads, arithmetic, store per tile).
 // Prints one JSON line per case.
 //   hipcc -O3 --offload-arch=gfx950 tools/studies/stream_pipe.hip -o tools/studies/stream_pipe
+//   tools/studies/stream_pipe [knee]
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <cstdio>
+#include <vector>
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -87,8 +89,10 @@ __global__ __launch_bounds__(256) void chunk_kernel(const f4* __restrict__ a, co
     }
 }
 
-int main()
+int main(int argc, char** argv)
 {
+    // "knee": the tile form only, at heavier arithmetic (where the stream stops hiding it)
+    const bool knee = argc > 1;
     const uint64_t n = 1ull << 28, nq = n / 4, bytes = n * 4;
     f4* buf[4];
     for (int k = 0; k < 4; ++k)
@@ -101,9 +105,11 @@ int main()
     CHECK(hipEventCreate(&e1));
     const int reps = 10;
     const uint32_t ntile = (uint32_t) (nq / 256);
-    for (int work : {0, 30, 60, 90})
+    const int works_all[]  = {0, 30, 60, 90};
+    const int works_knee[] = {90, 120, 150, 180, 240, 300};
+    for (int work : knee ? std::vector<int>(works_knee, works_knee + 6) : std::vector<int>(works_all, works_all + 4))
     {
-        for (int form = 0; form < 7; ++form)
+        for (int form = 0; form < (knee ? 1 : 7); ++form)
         {
             // form 0: tile; 1-3: chunk with prefetch at 2 / 4 / 8 workgroups per CU-resident slot;
             // 4-6: the same without prefetch
