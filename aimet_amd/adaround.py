@@ -18,7 +18,7 @@ GAMMA = -0.1   # aimet_common/defs.py:304
 
 def set_exact_pow(exact: bool):
     """The rounding loss's pow for every AdaRound backward launched afterwards (process-wide,
-    aimet_adaround_set_exact_pow): False (default) the f64 pow, within 1 ulp of torch's CPU pow
+    aimet_adaround_set_exact_pow): False (default) the table-driven f32 pow, within 1 ulp of torch's CPU pow
     (Sleef powf_u10) over every f32 input in (0, 1) and the AdaRound beta schedules
     (profiles/r06/pow_fast_check.txt); True the bit-exact emulation of torch's pow, about 3x the
     arithmetic. Returns the previous setting."""

@@ -16,7 +16,7 @@
 // pow(|2h-1|, beta) / pow(|2h-1|, beta-1) is, by default, the table-driven f32 pow of
 // fast_pow.hpp: within 1 ulp of torch's CPU pow (Sleef powf_u10) for every f32 |2h-1| in (0, 1)
 // and every exponent of the AdaRound schedules (profiles/r06/pow_fast_check.txt), at ~33 f32
-// instructions and 5 LDS reads instead of Sleef's ~142 f32 instructions. aimet_adaround_set_exact_pow(1) selects the bit-exact emulation of
+// instructions and 2 LDS reads instead of Sleef's ~142 f32 instructions. aimet_adaround_set_exact_pow(1) selects the bit-exact emulation of
 // torch's pow instead (sleef_pow.hpp: Sleef powf_u10 in the vectorized part, the scalar tail as
 // std::pow), with which dL/dalpha, the rounding-loss term included, is bit-identical too.
 #include "common.hpp"

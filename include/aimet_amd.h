@@ -525,9 +525,9 @@ int aimet_adaround_backward_adam_parts(const float* w, float* alpha, const float
 int aimet_adaround_adam_bias_corrections(double beta1, double beta2, int64_t steps, float* bias_corr_dev,
                                          void* stream);
 /* The rounding loss's pow(|2h - 1|, beta) / pow(|2h - 1|, beta - 1) (adaround_loss.py:83-110) of
- * every AdaRound backward launched afterwards, process-wide: 0 (default) an f64 evaluation within
- * 1 ulp of torch's CPU pow (Sleef powf_u10) over every f32 input in (0, 1) and the AdaRound beta
- * schedules; 1 the bit-exact emulation of torch's pow (about 3x the arithmetic). Wq and the
+ * every AdaRound backward launched afterwards, process-wide: 0 (default) a table-driven f32
+ * evaluation within 1 ulp of torch's CPU pow (Sleef powf_u10) over every f32 input in (0, 1) and
+ * the AdaRound beta schedules; 1 the bit-exact emulation of torch's pow (about 3x the arithmetic). Wq and the
  * reconstruction term of dL/dalpha do not depend on it. */
 int aimet_adaround_set_exact_pow(int exact);
 int aimet_adaround_get_exact_pow(int* exact);

@@ -36,6 +36,7 @@ def main():
 
 
 def run(scheme, qs, ws):
+    phases(scheme, qs)
     for sym in (True, False):
         AimetTensorQuantizer.getEncodings(qs, 8, sym, False, False)   # warm
         t = []
@@ -47,6 +48,27 @@ def run(scheme, qs, ws):
         print("%s %s: %d channels, getEncodings median %.3f ms" % (scheme, "sym" if sym else "asym",
                                                                  sum(w.shape[0] for w in ws), t[len(t) // 2] * 1e3),
               flush=True)
+
+
+def phases(scheme, qs):
+    """launch (host enqueue), device (until the stream is done), finish (read-back, host fallbacks,
+    the per-channel Python objects), medians of 10, symmetric"""
+    from aimet_amd.tensor_quantizer import PendingEncodings
+    AimetTensorQuantizer.getEncodings(qs, 8, True, False, False)
+    t = {"launch": [], "device": [], "finish": []}
+    for _ in range(10):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pend = PendingEncodings(qs, 8, True, False, False)
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        pend.result()
+        t3 = time.perf_counter()
+        t["launch"].append(t1 - t0)
+        t["device"].append(t2 - t1)
+        t["finish"].append(t3 - t2)
+    print("%s sym phases (median ms): %s" % (scheme, {k: round(sorted(v)[5] * 1e3, 3) for k, v in t.items()}), flush=True)
 
 
 if __name__ == "__main__":
