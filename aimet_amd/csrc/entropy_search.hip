@@ -33,6 +33,7 @@
 // and the host re-runs the glibc search for it (quantizer.cpp). The accepted winner is then the
 // host's winner too.
 #include "entropy_kl.hpp"
+#include "mse_core.hpp"
 #include "tq_state.hpp"
 
 namespace aimet_amd
@@ -53,7 +54,7 @@ struct EntJob
     const double* hist;         // [C][512] bin counts
     EntropyRange* out;          // [C]
     int64_t start;              // first global channel of this job
-    EntropyRange* flat;         // optional: every job's ranges concatenated (+ start)
+    EntropyOut* flat;           // optional: every job's finished encodings concatenated (+ start)
 };
 
 // a window's step-2 results, read by step 3
@@ -350,8 +351,39 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
     }
 }
 
-__global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob* __restrict__ jobs, int njobs,
-                                                                   int64_t total, int sym, int strict, int unsign)
+// A channel's finished encoding: entropy_encoding_from_range of the KL range (kEntFinal) or
+// unseen_or_zero's all-zero encoding (kEntNoHist; encodings.cpp), the same double operations
+// (mse::computed_encoding is the host's own getComputedEncodings); kEntHost: left to the host
+__device__ __noinline__ EntropyOut entropy_out(float kl_lo, float kl_hi, int status, int bw, bool sym, bool strict, bool unsign)
+{
+    EntropyOut o {0, 0, 0, 0, 0, status};
+    if (status == kEntFinal)
+    {
+        const float lo          = 0.0f < kl_lo ? 0.0f : kl_lo;   // std::min(kl_lo, 0.0f)
+        const float hi          = kl_hi < 0.0f ? 0.0f : kl_hi;   // std::max(kl_hi, 0.0f)
+        const aimet_tf_encoding e = mse::computed_encoding(bw, (double) lo, (double) hi, sym, strict, unsign);
+        o = EntropyOut {e.min, e.max, e.delta, e.offset, e.bw, status};
+    }
+    else if (status == kEntNoHist)
+    {
+        float steps = (float) (ldexp(1.0, bw) - 1);   // (float) (std::pow(2.0, bw) - 1)
+        if (sym && strict)
+            steps -= 1;
+        const int isteps   = (int) steps;
+        const double delta = (1.0 - (-1.0)) / isteps;
+        const double off   = floor(-1.0 / delta);
+        const double lo    = off * delta;
+        o = EntropyOut {lo, lo + isteps * delta, delta, off, bw, status};
+    }
+    return o;
+}
+
+// 4 waves per SIMD (<= 128 VGPRs): with the kernel's 29.8 KB of LDS, 5 workgroups per CU; at 137
+// VGPRs (entropy_out inlined) 4 fit, and the kernel took 6.0 ms instead of 5.15 on ResNet-50's
+// weights (profiles/r06/entropy_waves_ab.txt): entropy_out stays a call (one lane per channel)
+__global__ __launch_bounds__(kEntBlock) __attribute__((amdgpu_waves_per_eu(4))) void entropy_search_kernel(const EntJob* __restrict__ jobs, int njobs,
+                                                                   int64_t total, int sym, int strict, int unsign,
+                                                                   int bw)
 {
     // step 1's source histogram and integer accumulators share their LDS with step 3's sums
     __shared__ double scratch[2 * kItems];
@@ -395,7 +427,7 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
                 const EntropyRange r {0.f, 0.f, j.pdf_init[c] ? kEntHost : kEntNoHist, 0};
                 j.out[c] = r;
                 if (j.flat)
-                    j.flat[j.start + c] = r;
+                    j.flat[j.start + c] = entropy_out(r.lo, r.hi, r.status, bw, sym, strict, unsign);
             }
             continue;
         }
@@ -664,7 +696,7 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
             }
             j.out[c] = EntropyRange {lo, hi, status, 0};
             if (j.flat)
-                j.flat[j.start + c] = EntropyRange {lo, hi, status, 0};
+                j.flat[j.start + c] = entropy_out(lo, hi, status, bw, sym, strict, unsign);
         }
         __syncthreads();
     }
@@ -673,7 +705,7 @@ __global__ __launch_bounds__(kEntBlock) void entropy_search_kernel(const EntJob*
 }   // namespace
 
 void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, bool sym, bool strict, bool unsign,
-                                hipStream_t s, EntropyRange* pinned_dst)
+                                hipStream_t s, EntropyOut* pinned_dst, int bw)
 {
     if (n == 0)
         return;
@@ -681,8 +713,8 @@ void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, in
     int64_t total = 0;
     for (int i = 0; i < n; ++i)
         total += Cs[i];
-    // every quantizer's ranges side by side, for one copy into the caller's pinned block
-    auto* flat = pinned_dst ? static_cast<EntropyRange*>(scratch_alloc(sizeof(EntropyRange) * total, s)) : nullptr;
+    // every quantizer's encodings side by side, for one copy into the caller's pinned block
+    auto* flat = pinned_dst ? static_cast<EntropyOut*>(scratch_alloc(sizeof(EntropyOut) * total, s)) : nullptr;
     total = 0;
     for (int i = 0; i < n; ++i)
     {
@@ -691,12 +723,13 @@ void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, in
     }
     auto* dj       = static_cast<EntJob*>(upload_async(jobs.data(), sizeof(EntJob) * (size_t) n, s));
     const int grid = (int) (total < 65536 ? total : 65536);
-    entropy_search_kernel<<<grid, kEntBlock, 0, s>>>(dj, n, total, sym ? 1 : 0, strict ? 1 : 0, unsign ? 1 : 0);
+    entropy_search_kernel<<<grid, kEntBlock, 0, s>>>(dj, n, total, sym ? 1 : 0, strict ? 1 : 0, unsign ? 1 : 0,
+                                                               bw);
     AIMET_LAUNCH_CHECK();
     scratch_free(dj, s);
     if (flat)
     {
-        AIMET_HIP_CHECK(hipMemcpyAsync(pinned_dst, flat, sizeof(EntropyRange) * total, hipMemcpyDeviceToHost, s));
+        AIMET_HIP_CHECK(hipMemcpyAsync(pinned_dst, flat, sizeof(EntropyOut) * total, hipMemcpyDeviceToHost, s));
         scratch_free(flat, s);
     }
 }

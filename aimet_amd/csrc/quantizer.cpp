@@ -708,29 +708,58 @@ struct HostStats
     std::vector<int32_t> init;
     std::vector<float> hmin;
     std::vector<EntropyRange> ent;   // device KL ranges (entropy, 8 bit)
+    const EntropyOut* dev = nullptr; // or a batched request's finished encodings (already in out)
     bool host_search = false;        // some channel still needs the host KL search
+    std::vector<int32_t> pdf_row;    // when only some rows were read back: channel -> row of pdf
+    bool only_host(int64_t c) const  // the channels of `dev` the host finishes
+    {
+        return dev == nullptr || dev[c].status == kEntHost;
+    }
+    const double* pdf_of(int64_t c) const
+    {
+        return pdf.data() + kPdfSize * (pdf_row.empty() ? c : (int64_t) pdf_row[(size_t) c]);
+    }
 };
 
 bool fetch_stats(aimet_tensor_quantizer* q, int32_t b, aimet_tf_encoding* out, HostStats& h,
-                 const EntropyRange* ranges = nullptr)
+                 const EntropyOut* dev = nullptr)
 {
     const int64_t C = q->C;
     h.q   = q;
     h.out = out;
     if (entropy_device(q, b))
     {
-        // the ranges of a batched request arrive in its pinned block; else read them back here
-        h.ent = ranges ? std::vector<EntropyRange>(ranges, ranges + C) : d2h(entropy_ranges(q->d), C);
-        for (const EntropyRange& r: h.ent)
-            h.host_search = h.host_search || r.status == kEntHost;
+        // a batched request's encodings arrive finished in its pinned block (only its kEntHost
+        // channels are left); else the ranges are read back here
+        h.dev = dev;
+        if (dev == nullptr)
+            h.ent = d2h(entropy_ranges(q->d), C);
+        std::vector<int64_t> flagged;
+        for (int64_t c = 0; c < C; ++c)
+            if (dev ? dev[c].status == kEntHost : h.ent[(size_t) c].status == kEntHost)
+                flagged.push_back(c);
+        h.host_search = !flagged.empty();
         if (h.host_search)
         {
             // near-ties (or non-finite ranges) on some channel: its statistics for the glibc search
+            // (a few flagged channels: their histogram rows only)
             h.init = d2h(q->d.pdf_init, C);
-            h.pdf  = d2h(q->d.pdf, (size_t) kPdfSize * C);
             h.acc  = d2h(q->d.acc, 2 * C);
+            if ((int64_t) flagged.size() * 8 >= C)
+                h.pdf = d2h(q->d.pdf, (size_t) kPdfSize * C);
+            else
+            {
+                h.pdf.resize((size_t) kPdfSize * flagged.size());
+                h.pdf_row.assign((size_t) C, 0);
+                for (size_t k = 0; k < flagged.size(); ++k)
+                {
+                    h.pdf_row[(size_t) flagged[k]] = (int32_t) k;
+                    AIMET_HIP_CHECK(hipMemcpy(h.pdf.data() + kPdfSize * k, q->d.pdf + kPdfSize * flagged[k],
+                                              sizeof(double) * kPdfSize, hipMemcpyDeviceToHost));
+                }
+            }
         }
-        return true;
+        return dev == nullptr || h.host_search;
     }
     if (!q->hist)
     {
@@ -759,6 +788,8 @@ bool fetch_stats(aimet_tensor_quantizer* q, int32_t b, aimet_tf_encoding* out, H
 void host_encoding(const HostStats& h, int64_t c, int32_t b, int sym, int strict, int unsign)
 {
     const aimet_tensor_quantizer* q = h.q;
+    if (!h.only_host(c))
+        return;   // finished on the device, already in out
     if (!q->hist)
         h.out[c] = tf_encoding(h.acc[2 * c], h.acc[2 * c + 1], b, sym, strict, unsign);
     else if (!h.ent.empty() && h.ent[(size_t) c].status != kEntHost)
@@ -766,8 +797,8 @@ void host_encoding(const HostStats& h, int64_t c, int32_t b, int sym, int strict
                        ? entropy_encoding_from_range(h.ent[(size_t) c].lo, h.ent[(size_t) c].hi, b, sym, strict, unsign)
                        : entropy_encoding(false, true, 0.0, 0.0, nullptr, b, sym, strict, unsign);
     else if (q->kind == kKindEntropy)
-        h.out[c] = entropy_encoding(h.init[c] != 0, true, h.acc[2 * c], h.acc[2 * c + 1], h.pdf.data() + kPdfSize * c,
-                                    b, sym, strict, unsign);
+        h.out[c] = entropy_encoding(h.init[c] != 0, true, h.acc[2 * c], h.acc[2 * c + 1], h.pdf_of(c), b, sym, strict,
+                                    unsign);
     else
         h.out[c] = histogram_encoding(q->scheme, h.init[c] != 0, true, h.hmin[c], h.bsz[c], h.pdf.data() + kPdfSize * c,
                                       q->percentile, b, sym, strict, unsign);
@@ -776,14 +807,14 @@ void host_encoding(const HostStats& h, int64_t c, int32_t b, int sym, int strict
 // the host-finished encodings of every (quantizer, channel) in one thread pool: the entropy KL
 // search is ~3 ms per channel, so a model's per-tensor entropy quantizers run in parallel too
 void collect_encodings(aimet_tensor_quantizer* const* qs, aimet_tf_encoding* const* outs, int64_t n, int32_t b,
-                       int sym, int strict, int unsign, const EntropyRange* const* ranges = nullptr)
+                       int sym, int strict, int unsign, const EntropyOut* const* dev = nullptr)
 {
     std::vector<HostStats> hs;
     hs.reserve((size_t) n);
     for (int64_t i = 0; i < n; ++i)
     {
         HostStats h;
-        if (fetch_stats(qs[i], b, outs[i], h, ranges ? ranges[i] : nullptr))
+        if (fetch_stats(qs[i], b, outs[i], h, dev ? dev[i] : nullptr))
             hs.push_back(std::move(h));
     }
     std::vector<std::pair<int32_t, int64_t>> tasks;
@@ -792,7 +823,8 @@ void collect_encodings(aimet_tensor_quantizer* const* qs, aimet_tf_encoding* con
     {
         costly = costly || (hs[k].q->kind == kKindEntropy && (hs[k].ent.empty() || hs[k].host_search));
         for (int64_t c = 0; c < hs[k].q->C; ++c)
-            tasks.emplace_back((int32_t) k, c);
+            if (hs[k].only_host(c))
+                tasks.emplace_back((int32_t) k, c);
     }
     parallel_channels(
         (int64_t) tasks.size(),
@@ -1002,18 +1034,18 @@ aimet_encoding_request* aimet_amd::encodings_launch(aimet_tensor_quantizer* cons
     for (int64_t c: entC)
         ent_total += c;
     aimet_tf_encoding* mse_dst = nullptr;
-    EntropyRange* ent_dst      = nullptr;
+    EntropyOut* ent_dst        = nullptr;
     if (req->mse_total + ent_total > 0)
     {
         const size_t mse_bytes = sizeof(aimet_tf_encoding) * (size_t) req->mse_total;
-        req->pinned_dev = take_pinned(mse_bytes + sizeof(EntropyRange) * (size_t) ent_total, &req->pinned_dev_bytes);
+        req->pinned_dev = take_pinned(mse_bytes + sizeof(EntropyOut) * (size_t) ent_total, &req->pinned_dev_bytes);
         mse_dst         = req->mse_total ? static_cast<aimet_tf_encoding*>(req->pinned_dev) : nullptr;
-        ent_dst = ent_total ? reinterpret_cast<EntropyRange*>(static_cast<char*>(req->pinned_dev) + mse_bytes) : nullptr;
+        ent_dst = ent_total ? reinterpret_cast<EntropyOut*>(static_cast<char*>(req->pinned_dev) + mse_bytes) : nullptr;
     }
     launch_mse_search_many(mse.data(), mseC.data(), (int) mse.size(), b, sym != 0, strict != 0, unsign != 0, st,
                            mse_dst);
     launch_entropy_search_many(ent.data(), entC.data(), (int) ent.size(), sym != 0, strict != 0, unsign != 0, st,
-                               ent_dst);
+                               ent_dst, b);
     if (tfe_total > 0 && table != nullptr)
     {
         AIMET_REQUIRE(table->total == tfe_total && table->n == (int) tfe.size(),
@@ -1209,12 +1241,12 @@ int aimet_tq_get_encodings_finish(aimet_encoding_request* req, aimet_tf_encoding
         auto* tfe = static_cast<const aimet_tf_encoding*>(req->pinned);
         for (size_t k = 0, src = 0; k < req->tfe_Cs.size(); src += req->tfe_Cs[k], ++k)
             std::memcpy(out + req->tfe_offs[k], tfe + src, sizeof(aimet_tf_encoding) * req->tfe_Cs[k]);
-        // the device-searched MSE encodings and entropy ranges, from the request's pinned block
+        // the device-searched MSE and entropy encodings, from the request's pinned block
         std::vector<int64_t> offs((size_t) nq);
         for (int64_t i = 0, o = 0; i < nq; o += req->qs[(size_t) i]->C, ++i)
             offs[(size_t) i] = o;
         std::vector<char> from_pinned((size_t) nq, 0);
-        std::vector<const EntropyRange*> ranges((size_t) nq, nullptr);
+        std::vector<const EntropyOut*> dev((size_t) nq, nullptr);
         {
             auto* m = static_cast<const aimet_tf_encoding*>(req->pinned_dev);
             for (int64_t i: req->mse_q)
@@ -1224,17 +1256,28 @@ int aimet_tq_get_encodings_finish(aimet_encoding_request* req, aimet_tf_encoding
                 m += C;
                 from_pinned[(size_t) i] = 1;
             }
-            auto* r = reinterpret_cast<const EntropyRange*>(static_cast<const char*>(req->pinned_dev) +
-                                                            sizeof(aimet_tf_encoding) * (size_t) req->mse_total);
+            auto* r = reinterpret_cast<const EntropyOut*>(static_cast<const char*>(req->pinned_dev) +
+                                                          sizeof(aimet_tf_encoding) * (size_t) req->mse_total);
             for (int64_t i: req->ent_q)
             {
-                ranges[(size_t) i] = r;
-                r += req->qs[(size_t) i]->C;
+                // every channel's encoding as the device finished it; the host search then
+                // overwrites the flagged (kEntHost) ones
+                const int64_t C = req->qs[(size_t) i]->C;
+                aimet_tf_encoding* o = out + offs[(size_t) i];
+                bool flagged = false;
+                for (int64_t c = 0; c < C; ++c)
+                {
+                    o[c]    = aimet_tf_encoding {r[c].min, r[c].max, r[c].delta, r[c].offset, r[c].bw};
+                    flagged = flagged || r[c].status == kEntHost;
+                }
+                dev[(size_t) i]         = r;
+                from_pinned[(size_t) i] = flagged ? 0 : 1;
+                r += C;
             }
         }
         std::vector<aimet_tensor_quantizer*> host_q;
         std::vector<aimet_tf_encoding*> host_out;
-        std::vector<const EntropyRange*> host_ranges;
+        std::vector<const EntropyOut*> host_dev;
         for (int64_t i = 0; i < nq; ++i)
         {
             aimet_tensor_quantizer* q = req->qs[(size_t) i];
@@ -1242,11 +1285,11 @@ int aimet_tq_get_encodings_finish(aimet_encoding_request* req, aimet_tf_encoding
             {
                 host_q.push_back(q);
                 host_out.push_back(out + offs[(size_t) i]);
-                host_ranges.push_back(ranges[(size_t) i]);
+                host_dev.push_back(dev[(size_t) i]);
             }
         }
         collect_encodings(host_q.data(), host_out.data(), (int64_t) host_q.size(), req->b, req->sym, req->strict,
-                          req->unsign, host_ranges.data());
+                          req->unsign, host_dev.data());
     });
     if (rc != AIMET_OK)
         release_request_after_error(req);   // the copy may not have been waited for

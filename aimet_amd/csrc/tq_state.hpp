@@ -6,6 +6,7 @@
 // of stream-ordered kernels with no host round trip; only getEncoding reads them back.
 #pragma once
 
+#include <cstddef>
 #include <functional>
 
 #include "common.hpp"
@@ -198,8 +199,21 @@ inline EntropyRange* entropy_ranges(const TqDevice& d)
 {
     return reinterpret_cast<EntropyRange*>(d.enc);
 }
-// pinned_dst (optional, host-pinned, sum of Cs entries): the ranges concatenated, copied there on s
+// A batched request's result per channel: the finished encoding (computed on the device from the
+// KL range as entropy_encoding_from_range / unseen_or_zero do on the host) with the status in the
+// encoding's tail padding, so that a block of them is copied into the caller's encodings as is
+// (status kEntHost: the host search overwrites that channel)
+struct EntropyOut
+{
+    double min, max, delta, offset;
+    int32_t bw;
+    int32_t status;
+};
+static_assert(sizeof(EntropyOut) == sizeof(aimet_tf_encoding) && offsetof(EntropyOut, bw) == offsetof(aimet_tf_encoding, bw),
+              "an encoding with its status in the padding");
+// pinned_dst (optional, host-pinned, sum of Cs entries): the finished encodings concatenated,
+// copied there on s (bw: the request's bitwidth, 8)
 void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, int n, bool sym, bool strict, bool unsign,
-                                hipStream_t s, EntropyRange* pinned_dst = nullptr);
+                                hipStream_t s, EntropyOut* pinned_dst = nullptr, int bw = 8);
 
 }   // namespace aimet_amd

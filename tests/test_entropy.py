@@ -329,6 +329,11 @@ def test_entropy_device_kl_search_per_channel_many():
     ws = [(rng.standard_normal(s) * rng.uniform(0.01, 0.2, (s[0], 1))).astype(np.float32) for s in shapes]
     ws[1][5] = 0                                      # an all-zero channel
     ws[2][:, ::3] = np.abs(ws[2][:, ::3])             # skewed channels
+    # degenerate histograms (equal divergences: near-ties the host search finishes) among channels
+    # the device finishes, so that one quantizer mixes both (its flagged rows read back alone)
+    ws[0][3] = 0.5
+    ws[0][10] = np.where(np.arange(27) % 2 == 0, 0.25, -0.25).astype(np.float32)
+    ws[1][17] = np.float32(1e-3)
     qs = [AimetTensorQuantizer(QuantizationMode.QUANTIZATION_ENTROPY, num_channels=s[0]) for s in shapes]
     AimetTensorQuantizer.updateStatsPerChannelMany(qs, [torch.from_numpy(w).cuda() for w in ws])
     torch.cuda.synchronize()
@@ -336,7 +341,7 @@ def test_entropy_device_kl_search_per_channel_many():
         res = AimetTensorQuantizer.getEncodings(qs, 8, *(bool(v) for v in fl))
         for w, (encs, valid) in zip(ws, res):
             assert valid
-            for c in range(0, w.shape[0], 7):
+            for c in sorted(set(range(0, w.shape[0], 7)) | {3, 5, 10, 17}):
                 a = O.Analyzer(ENTROPY)
                 a.update(w[c])
                 assert _enc_tuple(encs[c]) == a.compute(8, *fl).as_tuple(), (w.shape, c, fl)
