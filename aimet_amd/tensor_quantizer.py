@@ -730,6 +730,32 @@ class PendingEncodings:
                              int(bool(strict)), int(bool(unsign)), torch.cuda.current_stream(dev).cuda_stream,
                              ctypes.byref(req))
             self.req = req
+        self._views = self._encoding_views() if self.live and self.req is not None else None
+
+    def _encoding_views(self):
+        """The result block and its per-quantizer TfEncoding objects, built while the searches run
+        on the device: ctypes array items (and slices) are views into the array's buffer, so
+        aimet_tq_get_encodings_finish filling the block fills them (about 1.3 ms of Python for
+        ResNet-50's 27,560 weight channels, hidden behind the device's ~5 ms)."""
+        total = sum(q._num_channels for q in self.live)
+        out = TfEncoding.array(total)
+        valid = (ctypes.c_int * len(self.live))()
+        views = []
+        # tens of thousands of small objects: keep the cyclic GC from firing mid-list
+        gc_was_enabled = gc.isenabled()
+        gc.disable()
+        try:
+            # ctypes array slicing builds the element objects in one C-level pass (about 2x faster
+            # than list(out) + list slicing)
+            off = 0
+            for q in self.live:
+                C = q._num_channels
+                views.append(out[off] if C == 1 else out[off:off + C])
+                off += C
+        finally:
+            if gc_was_enabled:
+                gc.enable()
+        return out, valid, views
 
     def result(self):
         results = {}
@@ -740,25 +766,12 @@ class PendingEncodings:
         if self.live:
             if self.req is None:
                 raise RuntimeError("PendingEncodings.result() called twice")
-            total = sum(q._num_channels for q in self.live)
-            out = TfEncoding.array(total)
-            valid = (ctypes.c_int * len(self.live))()
+            out, valid, views = self._views
+            self._views = None
             req, self.req = self.req, None
             _native.call("aimet_tq_get_encodings_finish", req, out, valid)
-            # tens of thousands of small objects: keep the cyclic GC from firing mid-list
-            gc_was_enabled = gc.isenabled()
-            gc.disable()
-            try:
-                # ctypes array slicing builds the element objects in one C-level pass (about 2x
-                # faster than list(out) + list slicing)
-                off = 0
-                for i, q in enumerate(self.live):
-                    C = q._num_channels
-                    results[id(q)] = (out[off] if C == 1 else out[off:off + C], bool(valid[i]))
-                    off += C
-            finally:
-                if gc_was_enabled:
-                    gc.enable()
+            for i, q in enumerate(self.live):
+                results[id(q)] = (views[i], bool(valid[i]))
         res = []
         for q in self.quantizers:
             if id(q) in results:
