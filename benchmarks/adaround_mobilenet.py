@@ -147,7 +147,7 @@ def main():
         "ms_per_iteration": round(t_opt / iters * 1e3, 4), "activation_caching_s": round(t_cache, 3),
         "loop": "eager" if args.eager else "hipgraph (one captured iteration replayed per iteration)",
         "miopen_find": bool(args.miopen_find),
-        "rounding_loss_pow": "exact (torch's CPU pow, bit for bit)" if args.exact_pow else "f64 (within 1 ulp of torch's)",
+        "rounding_loss_pow": "exact (torch's CPU pow, bit for bit)" if args.exact_pow else "table-driven f32 (within 1 ulp of torch's)",
         "weights_elems": sum(int(torch.Size(p[1]).numel()) for p in per_layer),
         "kernel_split": "per-kernel time of the loop: rocprofv3 --kernel-trace + tools/studies/ada_trace_summary.py "
                         "(profiles/r02/adaround_loop_kernels_*.csv)",
