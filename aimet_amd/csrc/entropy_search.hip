@@ -351,6 +351,44 @@ __device__ void window_segment(const double* hist, int a, int b, int q0, int q1,
     }
 }
 
+// the job holding global channel g (the last one with start <= g)
+__device__ __forceinline__ int find_job(const EntJob* __restrict__ jobs, int njobs, int64_t g)
+{
+    int lo_j = 0, hi_j = njobs - 1;
+    while (lo_j < hi_j)
+    {
+        const int mid = (lo_j + hi_j + 1) >> 1;
+        if (jobs[mid].start <= g)
+            lo_j = mid;
+        else
+            hi_j = mid - 1;
+    }
+    return lo_j;
+}
+
+// The asymmetric (not strict) window list of every channel, one lane per channel: entropy::windows
+// on the channel's histogram where it lies (an asymmetric search runs on the histogram as
+// accumulated, unrescaled). The walk is 129 dependent steps; inside the search kernel one lane
+// took them while its workgroup's other 191 lanes waited (~0.8 ms for ResNet-50's 27,560
+// channels, profiles/r06/entropy_step_shares.txt); here 64 channels walk side by side per wave.
+// walks[g][0][n] / walks[g][1][n]: window n's first / last bin (every walk has kWindows windows:
+// each step narrows the window by two bins, from 512 to 256).
+__global__ __launch_bounds__(64) void entropy_walk_kernel(const EntJob* __restrict__ jobs, int njobs, int64_t total,
+                                                          short* __restrict__ walks)
+{
+    const int64_t g = (int64_t) blockIdx.x * 64 + threadIdx.x;
+    if (g >= total)
+        return;
+    const EntJob& j = jobs[find_job(jobs, njobs, g)];
+    const int64_t c    = g - j.start;
+    const double tmin = j.acc[2 * c], tmax = j.acc[2 * c + 1];
+    if (!j.pdf_init[c] || !__builtin_isfinite(tmin) || !__builtin_isfinite(tmax))
+        return;   // the search decides these channels without a window list
+    short* w = walks + g * 2 * entropy::kWindows;
+    entropy::windows(j.hist + c * entropy::kBins, tmin, (tmax - tmin) / (double) entropy::kBins, false, w,
+                     w + entropy::kWindows);
+}
+
 // A channel's finished encoding: entropy_encoding_from_range of the KL range (kEntFinal) or
 // unseen_or_zero's all-zero encoding (kEntNoHist; encodings.cpp), the same double operations
 // (mse::computed_encoding is the host's own getComputedEncodings); kEntHost: left to the host
@@ -383,7 +421,7 @@ __device__ __noinline__ EntropyOut entropy_out(float kl_lo, float kl_hi, int sta
 // weights (profiles/r06/entropy_waves_ab.txt): entropy_out stays a call (one lane per channel)
 __global__ __launch_bounds__(kEntBlock) __attribute__((amdgpu_waves_per_eu(4))) void entropy_search_kernel(const EntJob* __restrict__ jobs, int njobs,
                                                                    int64_t total, int sym, int strict, int unsign,
-                                                                   int bw)
+                                                                   int bw, const short* __restrict__ walks)
 {
     // step 1's source histogram and integer accumulators share their LDS with step 3's sums
     __shared__ double scratch[2 * kItems];
@@ -406,16 +444,7 @@ __global__ __launch_bounds__(kEntBlock) __attribute__((amdgpu_waves_per_eu(4))) 
     const int lane = t & 63;
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
     {
-        int lo_j = 0, hi_j = njobs - 1;   // last job with start <= g
-        while (lo_j < hi_j)
-        {
-            int mid = (lo_j + hi_j + 1) >> 1;
-            if (jobs[mid].start <= g)
-                lo_j = mid;
-            else
-                hi_j = mid - 1;
-        }
-        const EntJob& j = jobs[lo_j];
+        const EntJob& j = jobs[find_job(jobs, njobs, g)];
         const int64_t c = g - j.start;
         const double tmin = j.acc[2 * c], tmax = j.acc[2 * c + 1];
         if (!j.pdf_init[c] || !__builtin_isfinite(tmin) || !__builtin_isfinite(tmax))
@@ -539,11 +568,20 @@ __global__ __launch_bounds__(kEntBlock) __attribute__((amdgpu_waves_per_eu(4))) 
                     wb[n] = (short) (entropy::kBins - 1 - n);
                 }
             }
+            else if (walks)   // the walk of this histogram (no rescale here: hist is the source)
+            {
+                const short* w = walks + g * 2 * entropy::kWindows;
+                for (int n = t; n < entropy::kWindows; n += kEntBlock)
+                {
+                    wa[n] = w[n];
+                    wb[n] = w[entropy::kWindows + n];
+                }
+            }
             if (t == 0)
             {
                 s_lo   = dlo;
                 s_hi   = dhi;
-                s_n    = (sym || strict) ? entropy::kWindows
+                s_n    = (sym || strict || walks) ? entropy::kWindows
                                          : entropy::windows(hist, dlo, (dhi - dlo) / (double) entropy::kBins, false, wa, wb);
                 s_rule = 1;   // integral bins: 0 or >= 1
             }
@@ -723,9 +761,19 @@ void launch_entropy_search_many(const TqDevice* const* ds, const int64_t* Cs, in
     }
     auto* dj       = static_cast<EntJob*>(upload_async(jobs.data(), sizeof(EntJob) * (size_t) n, s));
     const int grid = (int) (total < 65536 ? total : 65536);
+    // asymmetric, not strict: every channel's window list first, 64 channels per wave
+    short* walks = nullptr;
+    if (!sym && !strict)
+    {
+        walks = static_cast<short*>(scratch_alloc(sizeof(short) * 2 * entropy::kWindows * (size_t) total, s));
+        entropy_walk_kernel<<<(int) ((total + 63) / 64), 64, 0, s>>>(dj, n, total, walks);
+        AIMET_LAUNCH_CHECK();
+    }
     entropy_search_kernel<<<grid, kEntBlock, 0, s>>>(dj, n, total, sym ? 1 : 0, strict ? 1 : 0, unsign ? 1 : 0,
-                                                               bw);
+                                                               bw, walks);
     AIMET_LAUNCH_CHECK();
+    if (walks)
+        scratch_free(walks, s);
     scratch_free(dj, s);
     if (flat)
     {
