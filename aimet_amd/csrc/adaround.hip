@@ -284,10 +284,13 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
 #pragma unroll
             for (int k = 0; k < E; ++k)
             {
-                // |x| outside (0, 1): 0, 1 or NaN (pow01_fast_l's exact cases and its NaN -> inf)
+                // |x| outside (0, 1) is 0, 1 or NaN (x = 2h - 1, h clamped to [0, 1]): pow01_fast_l's
+                // exact cases give 0, 1 and, for NaN, inf -- |x| itself, or inf for NaN. ln01 and
+                // exp_ln run on those too (every step stays in range: table indices are masked, a
+                // NaN converts to n = 0) and their value is dropped
                 const bool inside = ax[k] > 0.0f && ax[k] < 1.0f;
-                const LnSplit l   = ln01(inside ? ax[k] : 0.5f);
-                const float fixed = ax[k] == 0.0f ? 0.0f : (ax[k] == 1.0f ? 1.0f : __builtin_inff());
+                const LnSplit l   = ln01(ax[k]);
+                const float fixed = ax[k] != ax[k] ? __builtin_inff() : ax[k];
                 pbm1[k]           = inside ? exp_ln(l, p.beta_m1) : fixed;
                 pb[k]             = p.want_loss ? (inside ? exp_ln(l, p.beta) : fixed) : 0.0f;
             }
