@@ -107,13 +107,18 @@ __device__ __forceinline__ float sigmoidf(float a)
 // floor(w / d) exactly as the IEEE division gives it, from q = w * rcp (rcp = v_rcp_f32(d), within
 // 1 ulp): |q - RN(w/d)| <= 3.5 ulp(q) < 2^-21 (|q| + 1), so when q lies farther than that from
 // every integer both floors agree; otherwise (and for non-finite q) the division decides.
+// The distances to floor(q) and floor(q) + 1 as fr = v_fract_f32(q) and 1 - fr: each within 2^-24
+// of the exact distance (fr < 1 after its rounding, clamped to 1 - 2^-24 where it would round to
+// 1), and the threshold exceeds the quotient's 3.5 ulp by at least 2^-21, so a margin above it
+// still proves the floors equal. Either branch returns floor(w / d): the guard only picks how.
 __device__ __forceinline__ float floor_div(float w, float d, float rcp)
 {
     const float q   = w * rcp;
     const float f   = __builtin_floorf(q);
+    const float fr  = __builtin_amdgcn_fractf(q);
     // (|q| + 1) 2^-21 in one instruction: scaling by a power of two commutes with the rounding
     const float thr = __builtin_fmaf(__builtin_fabsf(q), 4.76837158203125e-7f, 4.76837158203125e-7f);
-    if (q - f > thr && (f + 1.0f) - q > thr)
+    if (fr > thr && 1.0f - fr > thr)
         return f;
     return __builtin_floorf(w / d);
 }
@@ -158,7 +163,7 @@ __device__ __forceinline__ float ada_bwd_base(float w, float a, float g, float d
     // sigmoid_backward: (grad * (1 - s)) * s
     in_h     = pre >= 0.0f && pre <= 1.0f;
     float gh = (u >= 0.0f && u <= p.qmax) ? g * d : 0.0f;
-    x        = 2.0f * h + -1.0f;
+    x        = __builtin_fmaf(2.0f, h, -1.0f);   // 2h is exact: one rounding, as 2.0f * h + -1.0f
     return ((in_h ? gh : 0.0f) * kZmG * (1.0f - sg)) * sg;
 }
 
