@@ -95,7 +95,10 @@ __device__ __forceinline__ float clamp_torch(float x, float lo, float hi)
 // of e + 1 here below 2^126 (tools/studies/sigmoid_fast_check.hip, exhaustive); beyond, the division.
 __device__ __forceinline__ float sigmoidf(float a)
 {
-    const float y = sigmoid_expf(0.0f - a) + 1.0f;
+    // -a for 0 - a: they differ only at a = +0 (-0 against +0), and sigmoid_expf(+-0) is 1 either
+    // way (every use of its argument is a product, a sum with a signed-zero-insensitive result or a
+    // comparison); the negation folds into the first instructions' source modifiers
+    const float y = sigmoid_expf(-a) + 1.0f;
     if (y < 0x1p126f)
     {
         const float r = __builtin_amdgcn_rcpf(y);
@@ -156,12 +159,16 @@ __device__ __forceinline__ float ada_bwd_base(float w, float a, float g, float d
     float t   = floor_div(w, d, rcp);
     sg        = sigmoidf(a);
     float pre = sg * kZmG + kGamma;
-    float h   = clamp_torch(pre, 0.0f, 1.0f);
+    // clamp_torch(pre, 0, 1) as v_max / v_min, NaN restored after (they return the other operand):
+    // pre is never -0 (a sum with -0.1f is -0 only for -0 operands), so the two forms agree
+    float h   = __builtin_fminf(__builtin_fmaxf(pre, 0.0f), 1.0f);
+    h         = pre != pre ? pre : h;
     float u   = t + h - o;
     // autograd of apply_adaround, op by op: d wq / d tq = g * delta; clamp_backward passes it where
     // min <= x <= max; the adds pass it on; h's clamp likewise; mul by (zeta - gamma) -> * 1.2f;
-    // sigmoid_backward: (grad * (1 - s)) * s
-    in_h     = pre >= 0.0f && pre <= 1.0f;
+    // sigmoid_backward: (grad * (1 - s)) * s. pre lies in [0, 1] exactly where the clamp returns it
+    // (a NaN pre compares unequal)
+    in_h     = h == pre;
     float gh = (u >= 0.0f && u <= p.qmax) ? g * d : 0.0f;
     x        = __builtin_fmaf(2.0f, h, -1.0f);   // 2h is exact: one rounding, as 2.0f * h + -1.0f
     return ((in_h ? gh : 0.0f) * kZmG * (1.0f - sg)) * sg;
