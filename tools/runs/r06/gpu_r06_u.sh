@@ -13,3 +13,5 @@ rm -rf $OUT/trace $OUT/pmc_fetch $OUT/pmc_write
 run enc_trace 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d $OUT/enc_trace -o run -- python3 bench.py --steps 3 --warmup 1 --no-secondary --no-cpu-baseline --no-dropin
 python3 tools/studies/enc_timeline.py $OUT/enc_trace > $OUT/enc_timeline.txt 2>&1
 rm -rf $OUT/enc_trace
+# the AdaRound backward's instruction counts at the final tree (its own --pmc run)
+run ada_pmc 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_SALU --kernel-trace --output-format csv -d gpurun_out/ada_pmc_final -o run -- python3 tools/studies/ada_bwd_tune.py --scales 1 --reps 1 --tag pmc_final
