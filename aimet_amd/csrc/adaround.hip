@@ -273,14 +273,23 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
     const uint32_t lane = threadIdx.x & 63;
     bool need[E], tail[E];
     uint64_t ballot[E];   // the lane masks themselves (__ballot would round-trip each flag through a VGPR)
+    auto find_need = [&]() {
+#pragma unroll
+        for (int k = 0; k < E; ++k)
+        {
+            need[k]   = use[k] && !(ax[k] == 0.0f || ax[k] == 1.0f);
+            ballot[k] = __builtin_amdgcn_ballot_w64(need[k]);
+        }
+    };
+    // the dense test counts the elements with |x| < 1 (inside h's clamp, give or take the rare
+    // |x| = 0 or an h clamped exactly at 0 or 1): it only picks between forms with the same values,
+    // and the ballot of one comparison is that comparison's lane mask (no VGPR round trip)
     uint32_t total = 0;
 #pragma unroll
     for (int k = 0; k < E; ++k)
     {
-        tail[k]   = TAIL && tail_in[k];
-        need[k]   = use[k] && !(ax[k] == 0.0f || ax[k] == 1.0f);
-        ballot[k] = __builtin_amdgcn_ballot_w64(need[k]);
-        total += (uint32_t) __popcll(ballot[k]);
+        tail[k] = TAIL && tail_in[k];
+        total += (uint32_t) __popcll(__builtin_amdgcn_ballot_w64(ax[k] < 1.0f));
     }
     if (!EXACT && 4 * total >= 3 * 64 * E)
     {
@@ -308,6 +317,7 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
             }
             return;
         }
+        find_need();
 #pragma unroll
         for (int k = 0; k < E; ++k)
         {
@@ -325,6 +335,7 @@ __device__ __forceinline__ void ada_round_pows(const float (&ax)[E], const bool 
         }
         return;
     }
+    find_need();
     if (EXACT && 4 * total >= 3 * 64 * E)
     {
         // a dense wave (few saturated alphas): each lane evaluates its own elements in place, the
