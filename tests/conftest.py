@@ -22,10 +22,10 @@ def gpu_available():
         return False
 
 
-@pytest.fixture(params=[True, False], ids=["exact_pow", "f64_pow"])
+@pytest.fixture(params=[True, False], ids=["exact_pow", "fast_pow"])
 def exact_pow(request):
     """Both forms of the AdaRound rounding loss's pow (aimet_amd.adaround.set_exact_pow): the
-    bit-exact emulation of torch's CPU pow and the default f64 pow."""
+    bit-exact emulation of torch's CPU pow and the default table-driven f32 pow (within 1 ulp)."""
     from aimet_amd.adaround import set_exact_pow
     prev = set_exact_pow(request.param)
     yield request.param

@@ -225,3 +225,66 @@ def test_ste_16bit_autograd_bounds_vs_reference():
         xc = x.cpu()
         want = up.cpu() * (emin <= xc).logical_and(xc <= emax)
         assert torch.equal(a.grad.cpu().view(torch.int16), want.view(torch.int16)), dt
+
+
+def _same_bits_or_nan(got, want):
+    got, want = np.asarray(got, np.float32).ravel(), np.asarray(want, np.float32).ravel()
+    nan = np.isnan(want)
+    return np.array_equal(np.isnan(got), nan) and np.array_equal(got[~nan].view(np.int32), want[~nan].view(np.int32))
+
+
+def test_adaround_special_values_vs_torch_cpu():
+    """Inputs the golden vectors do not hold, against torch's CPU ops on the reference's expressions
+    (oracle/torch_ref.py: apply_adaround, compute_round_loss; autograd for dL/dalpha): alpha NaN,
+    +-inf, +-0, at and beside the sigmoid's range clamps (+-100, -104, 88.7) and +-1e30; weights
+    NaN, +-inf, +-0, tiny negatives (the floor guard's fract near 1) and multiples of delta one ulp
+    off. With the exact pow Wq and dL/dalpha (rounding loss included) are bit-exact, NaN for NaN;
+    with the default pow Wq and the reconstruction gradient are. n = 1024: no scalar pow tail."""
+    from aimet_amd.adaround import AdaroundFunction, set_exact_pow
+    from oracle import torch_ref as T
+    f32 = np.float32
+    alphas = f32([np.nan, np.inf, -np.inf, 0.0, -0.0, 100.0, 100.5, 99.99, -100.0, -103.9, -104.0, -104.5, 88.7,
+                  87.3, -88.7, 1e30, -1e30, 3e38, -3e38, 1e-30, -1e-30, 2.3, -2.3, 0.125])
+    rng = np.random.default_rng(21)
+    C, K = 4, 256
+    a = rng.standard_normal(C * K).astype(f32) * f32(3)
+    a[:alphas.size] = alphas
+    a[512:512 + alphas.size] = alphas[::-1]
+    delta = f32([0.01, 0.0037, 0.25, 1e-3])
+    k = rng.integers(-140, 140, (C, K)).astype(f32)
+    w = (k * delta[:, None]).astype(f32)
+    w[:, 1::3] = np.nextafter(w[:, 1::3], f32(np.inf))
+    w[:, 2::3] = np.nextafter(w[:, 2::3], f32(-np.inf))
+    wspecial = f32([np.nan, np.inf, -np.inf, 0.0, -0.0, -1e-40, -1e-30, 1e-40, -1e-8, -0.0049999])
+    w[0, 100:100 + wspecial.size] = wspecial
+    w[3, 7:7 + wspecial.size] = wspecial
+    a = a.reshape(C, K)
+    off = f32([-128.0, -100.0, -3.0, 0.0])
+    g = rng.standard_normal((C, K)).astype(f32)
+    reg, beta, bw = 0.01, 7.5, 8
+    # torch CPU: the reference's expressions, autograd for dL/dalpha
+    at = torch.from_numpy(a.copy()).requires_grad_(True)
+    dt, ot = torch.from_numpy(delta).view(C, 1), torch.from_numpy(off).view(C, 1)
+    wq_ref = T.adaround_forward(torch.from_numpy(w), at, dt, ot, bw)
+    (wq_ref * torch.from_numpy(g)).sum().backward()
+    ga_recon = at.grad.numpy().copy()
+    at.grad = None
+    wq_ref2 = T.adaround_forward(torch.from_numpy(w), at, dt, ot, bw)
+    ((wq_ref2 * torch.from_numpy(g)).sum() + T.adaround_round_loss(at, reg, beta)).backward()
+    ga_total = at.grad.numpy().copy()
+    wq_ref = wq_ref.detach().numpy()
+    wd, dd, od, gd = (torch.from_numpy(v).to(DEV) for v in (w, delta, off, g))
+    for exact in (True, False):
+        prev = set_exact_pow(exact)
+        try:
+            ad = torch.from_numpy(a).to(DEV).requires_grad_(True)
+            wq = AdaroundFunction.apply(wd, ad, dd, od, bw, 0)
+            (wq * gd).sum().backward()
+            assert _same_bits_or_nan(wq.detach().cpu().numpy(), wq_ref), exact
+            assert _same_bits_or_nan(ad.grad.cpu().numpy(), ga_recon), exact
+            if exact:
+                ad = torch.from_numpy(a).to(DEV).requires_grad_(True)
+                (AdaroundFunction.apply(wd, ad, dd, od, bw, 0, True, reg, beta, None) * gd).sum().backward()
+                assert _same_bits_or_nan(ad.grad.cpu().numpy(), ga_total)
+        finally:
+            set_exact_pow(prev)
