@@ -185,10 +185,20 @@ __device__ __forceinline__ bool ada_needs_log(float ax, bool tail)
 // autograd does: round_loss = reg * sum(1 - |2h - 1|^beta); grad -reg at the pow; pow_backward:
 // grad * (beta * x^(beta - 1)) (= pbm1 here); abs: * sgn(x); 2*h: * 2. Lanes outside h's clamp add
 // the selected +0 term as the full expression does.
+// SIGN_FAST (the caller checks reg > 0, beta > 0 and beta - 1 > 0, uniformly): then dpw <= 0, and
+// on lanes inside h's clamp (the only ones whose dh is used) x = 2h - 1 is finite and never -0, and
+// at x = +0 the pow is 0 so dpw = -0; (dpw * sgn(x)) * 2 is then -copysign(2 dpw, x) exactly
+template <bool SIGN_FAST = false>
 __device__ __forceinline__ float ada_bwd_round(float ga, float sg, float x, bool in_h, float pbm1, const AdaParams& p)
 {
-    float dpw = (-p.reg) * (p.beta * pbm1);
-    float dh  = (dpw * (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f))) * 2.0f;
+    float dh;
+    if constexpr (SIGN_FAST)   // -(reg (beta p)) is (-reg) (beta p) exactly: the negations go last
+        dh = -__builtin_copysignf((p.reg * (p.beta * pbm1)) * 2.0f, x);
+    else
+    {
+        float dpw = (-p.reg) * (p.beta * pbm1);
+        dh        = (dpw * (x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f))) * 2.0f;
+    }
     return ga + ((in_h ? dh : 0.0f) * kZmG * (1.0f - sg)) * sg;
 }
 
@@ -641,10 +651,19 @@ __global__ __launch_bounds__(kBlock) void adaround_bwd_vec_kernel(const f4* __re
             ada_round_pows<E, TAIL, EXACT>(ax, tail, p.want_loss ? valid : in_h, p, wl, pbm1, pb);
 #pragma unroll
             for (int k = 0; k < E; ++k)
-            {
                 if (p.want_loss && valid[k])
                     loss += 1.0f - pb[k];
-                r[k] = ada_bwd_round(r[k], sg[k], x[k], in_h[k], pbm1[k], p);
+            if (p.reg > 0.0f && p.beta > 0.0f && p.beta_m1 > 0.0f)   // uniform: every schedule's case
+            {
+#pragma unroll
+                for (int k = 0; k < E; ++k)
+                    r[k] = ada_bwd_round<true>(r[k], sg[k], x[k], in_h[k], pbm1[k], p);
+            }
+            else
+            {
+#pragma unroll
+                for (int k = 0; k < E; ++k)
+                    r[k] = ada_bwd_round(r[k], sg[k], x[k], in_h[k], pbm1[k], p);
             }
         }
 #pragma unroll
