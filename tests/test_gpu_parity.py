@@ -1985,3 +1985,34 @@ def test_learned_grid_past_2_31_elements(dtype):
     _, gmin, gmax = T.lg_gradients(x.detach().float(), grad.float(), emin.detach(), emax.detach(), 8)
     torch.testing.assert_close(emin.grad, gmin, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(emax.grad, gmax, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("scheme", ["TF_ENHANCED", "MSE", "ENTROPY", "TF"])
+def test_get_encodings_results_independent_across_calls(scheme):
+    """getEncodings' per-channel TfEncoding objects are views into the call's own result block,
+    built while the searches run (tensor_quantizer.PendingEncodings): a later call, on other
+    statistics, leaves an earlier call's objects as they were; every channel equals its own
+    getEncoding."""
+    mode = getattr(QuantizationMode, "QUANTIZATION_" + scheme)
+    g = torch.Generator(device=DEV).manual_seed(31)
+    shapes = [(16, 40), (1, 300), (7, 9)]
+    qs = [AimetTensorQuantizer(mode, num_channels=s[0]) for s in shapes]
+    ws = [torch.randn(s, device=DEV, generator=g) * 0.1 for s in shapes]
+    AimetTensorQuantizer.updateStatsPerChannelMany(qs, ws)
+    first = AimetTensorQuantizer.getEncodings(qs, 8, True, False, False)
+    snap = [[(e.min, e.max, e.delta, e.offset, e.bw) for e in (encs if isinstance(encs, list) else [encs])]
+            for encs, _ in first]
+    # other statistics, a second batched call
+    qs2 = [AimetTensorQuantizer(mode, num_channels=s[0]) for s in shapes]
+    AimetTensorQuantizer.updateStatsPerChannelMany(qs2, [w * 3 + 0.05 for w in ws])
+    second = AimetTensorQuantizer.getEncodings(qs2, 8, False, False, False)
+    again = [[(e.min, e.max, e.delta, e.offset, e.bw) for e in (encs if isinstance(encs, list) else [encs])]
+             for encs, _ in first]
+    assert again == snap
+    for q, (encs, valid) in zip(qs2, second):
+        assert valid
+        one, _ = q.getEncoding(8, False, False, False)
+        encs = encs if isinstance(encs, list) else [encs]
+        one = one if isinstance(one, list) else [one]
+        assert [(e.min, e.max, e.delta, e.offset, e.bw) for e in encs] == \
+            [(e.min, e.max, e.delta, e.offset, e.bw) for e in one]
