@@ -20,7 +20,12 @@
 //     lanes, the segments' sums added per window; a window's empty bins all have the same term,
 //     evaluated once and counted; without the filter (non-integral bins) every window is one;
 //  4. the first strict minimum among the candidates and the near-tie test by wave reductions
-//     (a window ruled out by the filter exceeds the minimum by more than the tolerance).
+//     (a window ruled out by the filter exceeds the minimum by more than the tolerance);
+//  5. for a batched request, the channel's finished encoding (entropy_out: the host's
+//     entropy_encoding_from_range on the chosen range), so the host only re-runs flagged channels.
+// The asymmetric (not strict) window lists are walked before the search by entropy_walk_kernel,
+// one lane per channel (the walk is 129 dependent steps; inside the search one lane had taken
+// them while its workgroup waited).
 //
 // Bit parity: every operation of 1, 2 and the window choice equals the host's. The divergence
 // differs from the host's (log_kl, relative error < 2^-49, for glibc's log; p and q as multiplies
