@@ -67,9 +67,31 @@ struct Setup
     long long total;   // nmins * nmaxs - 1 (the trailing {0, 0} pair is not a candidate)
 };
 
+// the mass of the bin that holds centre c (setup's second loop, one centre)
+AIMET_HD inline float centre_mass(const tfe::Hist& h, float c)
+{
+    const float start = (float) h.xl(0);
+    const float step  = (float) (h.xl(1) - h.xl(0));
+    int idx           = (int) floor((c - start) / step);
+    idx               = tfe::smin(tfe::smax(0, idx), tfe::kBins - 1);
+    return (float) h.pdf[idx];
+}
+
+// setup without the centres' masses: the edges and the centres, whose float sums are sequential
+// (the device fills the masses in parallel after it, mse_search.hip)
+AIMET_HD inline Setup setup_centres(const tfe::Hist& h, int first, int last, float* mins, float* maxs, float* cv);
+
 // mins/maxs: >= kMaxEdges + 1 floats; cv/cw (centre value / mass): >= kMaxEdges floats.
 // first/last: first and last (i > 0) non-empty bins, -1 for none (as tfe::observed_range).
 AIMET_HD inline Setup setup(const tfe::Hist& h, int first, int last, float* mins, float* maxs, float* cv, float* cw)
+{
+    const Setup s = setup_centres(h, first, last, mins, maxs, cv);
+    for (int i = 0; i < s.nc; ++i)
+        cw[i] = centre_mass(h, cv[i]);
+    return s;
+}
+
+AIMET_HD inline Setup setup_centres(const tfe::Hist& h, int first, int last, float* mins, float* maxs, float* cv)
 {
     Setup s {};
     const float width = (float) (h.xl(1) - h.xl(0));
@@ -104,15 +126,8 @@ AIMET_HD inline Setup setup(const tfe::Hist& h, int first, int last, float* mins
     s.nmaxs = nx;
     s.nc    = ne - 1 > 0 ? ne - 1 : 0;
     s.total = (long long) nm * nx - 1;
-    const float start = (float) h.xl(0);
-    const float step  = (float) (h.xl(1) - h.xl(0));
     for (int i = 0; i < s.nc; ++i)
-    {
-        cv[i]   = (i == 0) ? s.lo + width / 2 : cv[i - 1] + width;
-        int idx = (int) floor((cv[i] - start) / step);
-        idx     = tfe::smin(tfe::smax(0, idx), tfe::kBins - 1);
-        cw[i]   = (float) h.pdf[idx];
-    }
+        cv[i] = (i == 0) ? s.lo + width / 2 : cv[i - 1] + width;
     return s;
 }
 

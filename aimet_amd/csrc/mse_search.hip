@@ -165,11 +165,15 @@ __device__ void search_slice(const TqDevice& d, int64_t c, int y, int splits, in
             }
         }
         __syncthreads();
+        // mse::setup in two parts: the edges and the bin centres (sequential float sums) on one
+        // lane, then the centres' masses (a division each) over the workgroup -- the one-lane
+        // setup had been ~1.1 ms of the 5-ms ResNet-50 search (profiles/r06/mse_preamble.txt)
+        const tfe::Hist h {d.hist_min[c], d.bucket_size[c], pdf};
         if (threadIdx.x == 0)
-        {
-            tfe::Hist h {d.hist_min[c], d.bucket_size[c], pdf};
-            st = mse::setup(h, first, last, mins, maxs, cv, cw);
-        }
+            st = mse::setup_centres(h, first, last, mins, maxs, cv);
+        __syncthreads();
+        for (int i = threadIdx.x; i < st.nc; i += kBlock)
+            cw[i] = mse::centre_mass(h, cv[i]);
         __syncthreads();
         bool finite;
         const int nz = compact_bins(st, cv, cw, zv, zw, zvd, zwd, finite);
