@@ -114,6 +114,128 @@ __device__ int compact_bins(const mse::Setup& st, const float* cv, const float* 
     return count;
 }
 
+// exclusive prefix sum over the workgroup's kBlock threads (and the total), in thread order
+__device__ __forceinline__ int block_exscan(int v, int& total)
+{
+    __shared__ int wsum[kBlock / 64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int x = v;
+    for (int o = 1; o < 64; o <<= 1)
+    {
+        const int y = __shfl_up(x, o, 64);
+        if (lane >= o)
+            x += y;
+    }
+    if (lane == 63)
+        wsum[wave] = x;
+    __syncthreads();
+    int before = 0;
+    total      = 0;
+    for (int w = 0; w < kBlock / 64; ++w)
+    {
+        before += w < wave ? wsum[w] : 0;
+        total += wsum[w];
+    }
+    __syncthreads();   // wsum is reused by the next call
+    return before + x - v;
+}
+
+// mse::setup_centres on the device, the same values: the edge walk e += width and the centres'
+// chain cv[i] = cv[i - 1] + width are sequential float sums, each a tight loop on one lane (two
+// lanes of different waves, side by side); which edges are taken (in [lo, hi], the first
+// kMaxEdges - 1 of them) and where they go (mins / maxs, in order) is decided over the workgroup
+// by prefix sums. E: >= 4 kBins floats of scratch. Every thread calls it; the result in `st`.
+__device__ void setup_centres_device(const tfe::Hist& h, int first, int last, float* mins, float* maxs, float* cv,
+                                     float* E, mse::Setup& st)
+{
+    __shared__ int s_nE;
+    constexpr int kIters = 4 * tfe::kBins;
+    constexpr int kPer   = kIters / kBlock;   // consecutive edges per thread in the classification
+    static_assert(kIters % kBlock == 0, "edges split evenly");
+    const float width = (float) (h.xl(1) - h.xl(0));
+    float olo, ohi;
+    tfe::observed_range(h, first, last, olo, ohi);
+    const float lo = olo, hi = ohi + width;
+    if (threadIdx.x == 0)
+    {
+        const float hMin = (float) h.xl(0);
+        const float hMax = (float) h.xl(tfe::kBins - 1) + width;
+        int k   = 0;
+        float e = hMin;
+        for (; e <= hMax && k < kIters; e += width, ++k)
+            E[k] = e;
+        s_nE = k;
+    }
+    else if (threadIdx.x == 64)
+    {
+        // the centres for the longest possible list (kMaxEdges - 1); the caller uses st.nc of them
+        float c = lo + width / 2;
+        for (int i = 0; i < mse::kMaxEdges - 1; ++i)
+        {
+            cv[i] = c;
+            c     = c + width;
+        }
+    }
+    __syncthreads();
+    const int nE = s_nE;
+    // lo itself is taken first (ne = 1); then an edge in [lo, hi] while ne < kMaxEdges
+    const int nm0 = lo < 0 ? 1 : 0, nx0 = lo > 0 ? 1 : 0;
+    int q = 0;
+    bool inr[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u)
+    {
+        const int k = threadIdx.x * kPer + u;
+        inr[u]      = k < nE && E[k] >= lo && E[k] <= hi;
+        q += inr[u] ? 1 : 0;
+    }
+    int nq;
+    int rank = block_exscan(q, nq);
+    int neg = 0, pos = 0;
+    bool take[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u)
+    {
+        const int k = threadIdx.x * kPer + u;
+        take[u]     = inr[u] && rank < mse::kMaxEdges - 1;
+        rank += inr[u] ? 1 : 0;
+        neg += take[u] && E[k] < 0 ? 1 : 0;
+        pos += take[u] && E[k] > 0 ? 1 : 0;
+    }
+    int nneg, npos;
+    int in = block_exscan(neg, nneg) + nm0;
+    int ix = block_exscan(pos, npos) + nx0;
+#pragma unroll
+    for (int u = 0; u < kPer; ++u)
+    {
+        const int k = threadIdx.x * kPer + u;
+        if (take[u] && E[k] < 0)
+            mins[in++] = E[k];
+        else if (take[u] && E[k] > 0)
+            maxs[ix++] = E[k];
+    }
+    if (threadIdx.x == 0)
+    {
+        if (lo < 0)
+            mins[0] = lo;
+        else if (lo > 0)
+            maxs[0] = lo;
+        const int nm = nm0 + nneg, nx = nx0 + npos;
+        const int ne = 1 + (nq < mse::kMaxEdges - 1 ? nq : mse::kMaxEdges - 1);
+        mins[nm] = 0;
+        maxs[nx] = 0;
+        mse::Setup r {};
+        r.lo    = lo;
+        r.hi    = hi;
+        r.nmins = nm + 1;
+        r.nmaxs = nx + 1;
+        r.nc    = ne - 1 > 0 ? ne - 1 : 0;
+        r.total = (long long) r.nmins * r.nmaxs - 1;
+        st      = r;
+    }
+    __syncthreads();
+}
+
 __device__ __forceinline__ bool better(float e, long long t, float be, long long bt)
 {
     if (t < 0)
@@ -130,7 +252,11 @@ __device__ void search_slice(const TqDevice& d, int64_t c, int y, int splits, in
     __shared__ double pdf[tfe::kBins];
     __shared__ float mins[mse::kMaxEdges + 1], maxs[mse::kMaxEdges + 1], cv[mse::kMaxEdges], cw[mse::kMaxEdges];
     __shared__ float zv[mse::kMaxEdges], zw[mse::kMaxEdges];
-    __shared__ double zvd[mse::kMaxEdges], zwd[mse::kMaxEdges];
+    // zvd / zwd (after the setup) share their 8 KiB with the setup's edge scratch (before it)
+    __shared__ double zbuf[2 * mse::kMaxEdges];
+    static_assert(2 * mse::kMaxEdges * sizeof(double) >= 4 * tfe::kBins * sizeof(float), "edge scratch fits");
+    double* zvd = zbuf;
+    double* zwd = zbuf + mse::kMaxEdges;
     __shared__ float wg_best, wmin[kBlock / 64];
     __shared__ mse::Setup st;
     __shared__ int first, last;
@@ -165,13 +291,12 @@ __device__ void search_slice(const TqDevice& d, int64_t c, int y, int splits, in
             }
         }
         __syncthreads();
-        // mse::setup in two parts: the edges and the bin centres (sequential float sums) on one
-        // lane, then the centres' masses (a division each) over the workgroup -- the one-lane
-        // setup had been ~1.1 ms of the 5-ms ResNet-50 search (profiles/r06/mse_preamble.txt)
+        // mse::setup over the workgroup: the edges and the bin centres (sequential float sums) as
+        // tight one-lane loops, their classification and the centres' masses (a division each) in
+        // parallel -- the one-lane setup had been ~1.1 ms of the 5-ms ResNet-50 search
+        // (profiles/r06/mse_preamble.txt)
         const tfe::Hist h {d.hist_min[c], d.bucket_size[c], pdf};
-        if (threadIdx.x == 0)
-            st = mse::setup_centres(h, first, last, mins, maxs, cv);
-        __syncthreads();
+        setup_centres_device(h, first, last, mins, maxs, cv, reinterpret_cast<float*>(zbuf), st);
         for (int i = threadIdx.x; i < st.nc; i += kBlock)
             cw[i] = mse::centre_mass(h, cv[i]);
         __syncthreads();
