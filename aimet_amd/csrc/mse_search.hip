@@ -394,9 +394,10 @@ __device__ void search_slice(const TqDevice& d, int64_t c, int y, int splits, in
     }
 }
 
-// 5 waves per SIMD (<= 96 VGPRs, no spills): the setup's classification arrays had raised the
-// kernel to 106 VGPRs, 4 waves per SIMD
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void mse_search_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
+// 6 waves per SIMD, the most the kernel's 24.9 KB of LDS allows (80 VGPRs, a few spills): 3.80 ms
+// against 4.08 at 5 waves (96 VGPRs, no spills) and 4.69 at 4 (106 VGPRs) on ResNet-50's weights
+// (profiles/r06/mse_preamble.txt)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void mse_search_kernel(TqDevice d, int64_t C, int splits, int bw, int sym,
                                                             int strict, int unsign)
 {
     for (int64_t c = blockIdx.x; c < C; c += gridDim.x)
@@ -428,7 +429,7 @@ __device__ __forceinline__ int job_of(const MseJob* jobs, int njobs, int64_t g, 
     return lo;
 }
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void mse_search_many_kernel(const MseJob* __restrict__ jobs, int njobs,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(6))) void mse_search_many_kernel(const MseJob* __restrict__ jobs, int njobs,
                                                                  int64_t total, int bw, int sym, int strict, int unsign)
 {
     for (int64_t g = blockIdx.x; g < total; g += gridDim.x)
