@@ -49,7 +49,6 @@ namespace
 constexpr int kEntBlock = 192;   // >= kWindows (129): one window per lane in step 2
 static_assert(kEntBlock >= entropy::kWindows, "one window per lane");
 constexpr int kSegs   = 4;                              // step 3: segments of 64 levels per window
-constexpr int kItems  = entropy::kWindows * kSegs;      // 516 (window, segment) items
 constexpr int kSegLev = (entropy::kLevels + kSegs - 1) / kSegs;
 
 struct EntJob
@@ -421,24 +420,27 @@ __device__ __noinline__ EntropyOut entropy_out(float kl_lo, float kl_hi, int sta
     return o;
 }
 
-// 4 waves per SIMD (<= 128 VGPRs): with the kernel's 29.8 KB of LDS, 5 workgroups per CU; at 137
-// VGPRs (entropy_out inlined) 4 fit, and the kernel took 6.0 ms instead of 5.15 on ResNet-50's
-// weights (profiles/r06/entropy_waves_ab.txt): entropy_out stays a call (one lane per channel)
-__global__ __launch_bounds__(kEntBlock) __attribute__((amdgpu_waves_per_eu(4))) void entropy_search_kernel(const EntJob* __restrict__ jobs, int njobs,
+// 5 waves per SIMD (<= 96 VGPRs, a few spills): with the kernel's 23.6 KB of LDS (step 1's scratch
+// in `left` / `ws`, step 3's segments added by shuffles), 6 workgroups of 3 waves per CU, where
+// 29.8 KB had allowed 5. At 137 VGPRs (entropy_out inlined) 4 had fit, and the kernel took 6.0 ms
+// instead of 5.15 on ResNet-50's weights (profiles/r06/entropy_waves_ab.txt): entropy_out stays a
+// call (one lane per channel)
+__global__ __launch_bounds__(kEntBlock) __attribute__((amdgpu_waves_per_eu(5))) void entropy_search_kernel(const EntJob* __restrict__ jobs, int njobs,
                                                                    int64_t total, int sym, int strict, int unsign,
                                                                    int bw, const short* __restrict__ walks)
 {
     // step 1's source histogram and integer accumulators share their LDS with step 3's sums
-    __shared__ double scratch[2 * kItems];
-    double* tpp                 = scratch;
-    unsigned long long* acc_u   = reinterpret_cast<unsigned long long*>(scratch + entropy::kBins);
-    double* part_dv             = scratch;
-    double* part_mag            = scratch + kItems;
-    static_assert(2 * kItems >= 2 * entropy::kBins, "step 1 fits the scratch");
     __shared__ double hist[entropy::kBins];
     __shared__ short wa[entropy::kWindows], wb[entropy::kWindows];
     __shared__ WinState ws[entropy::kWindows];
     __shared__ double left[entropy::kBins];
+    // step 1's source histogram and integer accumulators in the LDS of `left` and `ws`, which
+    // step 1 writes only after it is done with them (the prefix tables) or not at all (ws: step 2)
+    double* tpp               = left;
+    unsigned long long* acc_u = reinterpret_cast<unsigned long long*>(ws);
+    static_assert(sizeof(WinState) * entropy::kWindows >= sizeof(unsigned long long) * entropy::kBins,
+                  "step 1's accumulators fit the window states");
+    __shared__ double s_vt[entropy::kWindows], s_mt[entropy::kWindows];   // step 3's sums per candidate
     __shared__ int zeros[entropy::kBins + 1];
     __shared__ double s_lo, s_hi;
     __shared__ int s_n, s_rule, s_integral;
@@ -665,14 +667,24 @@ __global__ __launch_bounds__(kEntBlock) __attribute__((amdgpu_waves_per_eu(4))) 
                                                            __builtin_amdgcn_mbcnt_lo((uint32_t) cand_mask, 0u))] = (short) t;
         __syncthreads();
         // ---- 3b. the candidates' divergences, (window, segment) items over every lane ------------
+        // a candidate's kSegs segments sit on 4 adjacent lanes of one wave (kEntBlock and 64 are
+        // multiples of kSegs, and every lane of such a group runs the same iterations): the first
+        // adds them, in segment order
+        static_assert(kSegs == 4 && kEntBlock % kSegs == 0, "a candidate's segments on 4 adjacent lanes");
         for (int it = t; it < ncand * kSegs; it += kEntBlock)
         {
             const int w = s_cand[it / kSegs], sgm = it % kSegs;
             const int q0 = sgm * kSegLev, q1 = q0 + kSegLev < entropy::kLevels ? q0 + kSegLev : entropy::kLevels;
             double dv = 0, mag = 0;
             window_segment(hist, wa[w], wb[w], q0, q1, ws[w], pre, integral, dv, mag);
-            part_dv[w * kSegs + sgm]  = dv;
-            part_mag[w * kSegs + sgm] = mag;
+            const double d1 = __shfl(dv, lane + 1, 64), d2 = __shfl(dv, lane + 2, 64), d3 = __shfl(dv, lane + 3, 64);
+            const double m1 = __shfl(mag, lane + 1, 64), m2 = __shfl(mag, lane + 2, 64),
+                         m3 = __shfl(mag, lane + 3, 64);
+            if (sgm == 0)
+            {
+                s_vt[w] = (((0.0 + dv) + d1) + d2) + d3;
+                s_mt[w] = (((0.0 + mag) + m1) + m2) + m3;
+            }
         }
         __syncthreads();
         // ---- 4. the first strict minimum among the candidates (wave reductions), near-tie test ---
@@ -681,12 +693,8 @@ __global__ __launch_bounds__(kEntBlock) __attribute__((amdgpu_waves_per_eu(4))) 
         double v = __builtin_inf(), m = 0.0;
         if (cand)
         {
-            v = 0.0;
-            for (int sgm = 0; sgm < kSegs; ++sgm)   // the segments' sums in segment order
-            {
-                v += part_dv[t * kSegs + sgm];
-                m += part_mag[t * kSegs + sgm];
-            }
+            v = s_vt[t];
+            m = s_mt[t];
         }
         // (value, index) argmin: the smallest value below +inf, the first index among equals
         double bv = (t < nv && v < __builtin_inf()) ? v : __builtin_inf();
